@@ -1,0 +1,220 @@
+"""bench.py — forwarded RTP packets/s of the MI355X forwarding engine.
+
+Workload: BASELINE.json configs[1] = 100 rooms x 10 participants, VP8 3-layer
+simulcast + Opus per participant, each subscribing to the other 9 (18,000
+DownTracks), 2% loss, 1% reorder, target-layer switches every 2 s per
+DownTrack, subscriber mutes.  Synthetic (seeded splitmix64).  One step = one
+batch = 1 s of media time of all 100 rooms through the full per-packet path
+(Forwarder/RTPMunger/VP8 munger/sequencer + wire-packet emission), inputs
+resident in HBM.  Multi-GPU: one process per GPU, each rank forwards its own
+100 rooms (room sharding, no data-path collective) -> weak scaling.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import ctypes as C
+import importlib
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(trace, batches, fwd, out_bytes, active_dts):
+    """sum_in (64 + in_payload) + sum_fwd (out_len + 32) + sum_active_DT 256 per batch."""
+    import numpy as np
+    abi = importlib.import_module("livekit-server_amd.abi")
+    b_in = 0
+    for b in batches:
+        pk, n, _, _ = trace.batch(b)
+        arr = np.ctypeslib.as_array(C.cast(pk, C.POINTER(C.c_uint8)), shape=(n * 64,)).view(
+            np.dtype([("x", "V38"), ("payload_len", "<u2"), ("y", "V24")]))
+        b_in += 64 * n + int(arr["payload_len"].astype(np.int64).sum())
+    return b_in + out_bytes + 32 * fwd + 256 * active_dts * len(batches), b_in
+
+
+def cpu_baseline(threads, sample_rooms=10, sample_batches=2):
+    """CPU oracle (C++ restatement of the Go path, -O3 -march=native) on a bounded
+    sample of the same workload, rooms sharded over `threads` workers."""
+    from tests.oracle_lib import load as load_oracle
+    wl = importlib.import_module("livekit-server_amd.workload")
+    abi = importlib.import_module("livekit-server_amd.abi")
+    o = load_oracle()
+    per = max(1, sample_rooms // threads)
+    shards = []
+    for t in range(threads):
+        tr = wl.Trace(2, duration_s=float(sample_batches), batch_s=1.0, rooms=per, room_base=t * per)
+        h = o.create(500)
+        wl.load_topology(o.api, h, tr)
+        shards.append((tr, h))
+    fwd = [0] * threads
+
+    def work(i):
+        tr, h = shards[i]
+        for b in range(sample_batches):
+            wl.queue_events(o.api, h, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(h, pk, n, ar, alen)
+            st = abi.lkf_stats()
+            o.api["get_stats"](h, C.byref(st))
+            fwd[i] += st.forwarded
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    for tr, h in shards:
+        o.destroy(h)
+        tr.close()
+    return sum(fwd) / dt, dt, per * threads
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rooms", type=int, default=100)
+    ap.add_argument("--batch-s", type=float, default=1.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", ""))
+    args = ap.parse_args()
+
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    pkg = importlib.import_module("livekit-server_amd")
+    wl = importlib.import_module("livekit-server_amd.workload")
+
+    nb = args.warmup + args.steps
+    trace = wl.Trace(2, duration_s=nb * args.batch_s, batch_s=args.batch_s, rooms=args.rooms,
+                     room_base=rank * args.rooms)
+    eng = pkg.Engine.for_trace(trace, device=local)
+    wl.load_topology(eng.api, eng.h, trace)
+
+    # inputs resident in HBM before the timed region
+    dpk, dar, meta = [], [], []
+    for b in range(nb):
+        pk, n, ar, alen = trace.batch(b)
+        tp = torch.frombuffer(bytearray(C.string_at(pk, n * 64)), dtype=torch.uint8).to(dev)
+        ta = torch.zeros(alen + 64, dtype=torch.uint8, device=dev)
+        if alen:
+            ta[:alen].copy_(torch.frombuffer(bytearray(C.string_at(ar, alen)), dtype=torch.uint8))
+        dpk.append(tp)
+        dar.append(ta)
+        meta.append((n, alen))
+    stream = torch.cuda.current_stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+
+    def step(b):
+        wl.queue_events(eng.api, eng.h, trace, b)
+        n, alen = meta[b]
+        eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
+        eng.run(sp)
+
+    for b in range(args.warmup):
+        step(b)
+    torch.cuda.synchronize(dev)
+    eng.sync()
+    eng.cumulative(reset=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for b in range(args.warmup, nb):
+        step(b)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    eng.sync()
+    elapsed = t1 - t0
+    cum = eng.cumulative()
+    dec_ms, emit_ms, tot_ms = eng.timing_window(args.steps)
+
+    fwd = cum["forwarded"]
+    algo, b_in = algorithmic_bytes(trace, range(args.warmup, nb), fwd, cum["out_bytes"], trace.ndts)
+    # emit kernel's own algorithmic bytes: wire bytes + 40-B records written, input payload read once
+    emit_bytes = cum["out_bytes"] + 40 * fwd + (b_in - 64 * sum(meta[b][0] for b in range(args.warmup, nb)))
+    if dist:
+        t = torch.tensor([elapsed, float(fwd), float(algo), tot_ms, emit_ms], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        fwd_all = float(t[1])
+    else:
+        fwd_all = float(fwd)
+
+    if rank == 0:
+        emit_avg_s = emit_ms / 1e3 / args.steps
+        achieved = emit_bytes / args.steps / emit_avg_s / 1e9 if emit_avg_s > 0 else 0.0
+        traffic = None
+        if args.pmc_csv and os.path.exists(args.pmc_csv):
+            try:
+                traffic = json.load(open(args.pmc_csv)).get("emit_hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            v, secs, rooms = cpu_baseline(thr)
+            cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": thr, "kind": "port",
+                   "sample": "configs[1] shape: %d rooms x 10 participants, 2 s of media, rooms sharded over %d "
+                             "threads (%.1f s wall)" % (rooms, thr, secs)}
+        line = {
+            "metric": "forwarded RTP pkts/sec per GPU & node (bit-exact) + % HBM roofline",
+            "value": round(fwd_all / elapsed, 1),
+            "unit": "forwarded RTP pkts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": "configs[1]: %d rooms x 10 participants per GPU, VP8 3-layer simulcast + Opus, "
+                                   "18,000 DownTracks, 2%% loss, 1%% reorder, layer switching" % args.rooms,
+                       "batch": "%.3g s of media per step" % args.batch_s,
+                       "parallelism": "room-sharded x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
+                         "kernel": "k_emit", "emit_ms_avg": round(emit_ms / args.steps, 4),
+                         "decide_ms_avg": round(dec_ms / args.steps, 4),
+                         "gpu_ms_per_step": round(tot_ms / args.steps, 4),
+                         "pipeline_algorithmic_GBps": round(algo / (tot_ms / 1e3), 1) if tot_ms else None},
+            "cpu_baseline": cpu,
+            "tuples_per_step": cum["tuples"] // args.steps,
+            "forwarded_per_step": fwd // args.steps,
+        }
+        print(json.dumps(line))
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

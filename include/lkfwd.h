@@ -1,0 +1,271 @@
+/*
+ * lkfwd.h — C-ABI of the MI355X batched RTP forwarding engine (liblkfwd.so).
+ *
+ * This is the drop-in boundary for livekit-server's per-packet SFU path
+ * (reference: /root/reference = suryatmodulus/livekit-server v1.5.2, Go).
+ * Each entry point names the reference interface it replaces; the cgo
+ * binding a maintainer adds on the Go side is in INTEGRATION.md.
+ *
+ * Plain C types only: pointers, sizes, fixed-width integers.  No torch types.
+ * Return codes: 0 = ok, < 0 = errno-like (LKF_E*).  One engine per GPU,
+ * driven by one host thread (the reference's per-Forwarder mutex becomes
+ * "one lane per DownTrack, packets of a track processed in order").
+ */
+#ifndef LKFWD_H_
+#define LKFWD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------- */
+#define LKF_OK 0
+#define LKF_EINVAL (-22)
+#define LKF_ENOMEM (-12)
+#define LKF_ENOSPC (-28)
+#define LKF_ENODEV (-19)
+#define LKF_EHIP (-5)
+#define LKF_EORDER (-34) /* batch not grouped by track */
+
+/* ---- enums ------------------------------------------------------------- */
+enum lkf_kind { LKF_KIND_AUDIO = 0, LKF_KIND_VIDEO = 1 };
+/* mime of webrtc.RTPCodecCapability (forwarder.go:269-338) */
+enum lkf_codec { LKF_CODEC_NONE = 0, LKF_CODEC_OPUS = 1, LKF_CODEC_VP8 = 2, LKF_CODEC_H264 = 3 };
+
+/* Control ops, applied to one DownTrack immediately before the first packet
+ * of its track whose batch index >= at_pkt (or at batch end).  Each op is the
+ * Forwarder/DownTrack method named beside it (pkg/sfu/forwarder.go). */
+enum lkf_ctl_op {
+  LKF_CTL_MUTE = 1,              /* Mute(a0 muted, a1 isSubscribeMutable)  :377  */
+  LKF_CTL_PUBMUTE = 2,           /* PubMute(a0)                            :422  */
+  LKF_CTL_SET_MAX_SPATIAL = 3,   /* SetMaxSpatialLayer(a0)                 :454  */
+  LKF_CTL_SET_MAX_TEMPORAL = 4,  /* SetMaxTemporalLayer(a0)                :472  */
+  LKF_CTL_SET_MAX_SEEN_SPATIAL = 5,  /* SetMaxPublishedLayer(a0)           :241  */
+  LKF_CTL_SET_MAX_SEEN_TEMPORAL = 6, /* SetMaxTemporalLayerSeen(a0)        :255  */
+  LKF_CTL_SET_ALLOCATION = 7,    /* updateAllocation: a0 target spatial, a1 target temporal,
+                                    a2 request spatial, a3 isDeficient   :1353 */
+  LKF_CTL_RESYNC = 8,            /* Resync()                               :1384 */
+  LKF_CTL_SET_TARGET = 9,        /* vls.SetTarget(a0,a1) (test hook, no resync) */
+  LKF_CTL_PLAYOUT_ACKED = 10     /* DownTrack.playoudDelayAcked = a0       downtrack.go:719 */
+};
+
+/* Drop reasons (TranslationParams.shouldDrop causes), counted per batch. */
+enum lkf_drop {
+  LKF_DROP_MUTED = 0,        /* muted || pubMuted                       forwarder.go:1440 */
+  LKF_DROP_PAUSED = 1,       /* target layer invalid                    :1687 */
+  LKF_DROP_NOT_SELECTED = 2, /* vls.Select !IsSelected                  :1694 */
+  LKF_DROP_DOWNGRADE = 3,    /* pause-on-downgrade                      :1709 */
+  LKF_DROP_SWITCH = 4,       /* processSourceSwitch error               :1652 */
+  LKF_DROP_PADDING = 5,      /* ErrPaddingOnlyPacket                    rtpmunger.go:264 */
+  LKF_DROP_DUPLICATE = 6,    /* ErrDuplicatePacket                      rtpmunger.go:270 */
+  LKF_DROP_OOO_MISS = 7,     /* ErrOutOfOrderSequenceNumberCacheMiss    rtpmunger.go:226 */
+  LKF_DROP_TEMPORAL = 8,     /* ErrFilteredVP8TemporalLayer             vp8.go:266 */
+  LKF_DROP_PICID_MISS = 9,   /* ErrOutOfOrderVP8PictureIdCacheMiss      vp8.go:173 */
+  LKF_DROP_OTHER = 10,
+  LKF_DROP_NREASONS = 11
+};
+
+/* ---- engine configuration ---------------------------------------------- */
+typedef struct lkf_cfg {
+  uint32_t max_tracks;      /* capacity of the track table */
+  uint32_t max_downtracks;  /* capacity of the DownTrack table */
+  uint32_t max_batch_pkts;  /* max ExtPackets per batch */
+  uint32_t seq_size;        /* sequencer ring = PacketBufferSize (config.go:326, default 500) */
+  uint64_t max_batch_arena; /* max input arena bytes per batch */
+  uint64_t max_out_bytes;   /* output arena capacity per batch */
+  uint64_t max_out_pkts;    /* output record capacity per batch */
+  uint64_t max_batch_tuples; /* (packet x DownTrack) evaluations per batch (decide slots) */
+} lkf_cfg;
+
+/* One published track (a MediaTrack/WebRTCReceiver, receiver.go:195). */
+typedef struct lkf_track_params {
+  uint64_t track_id;
+  uint32_t room;        /* room index (speaker ranking, room sharding) */
+  uint32_t publisher;   /* publisher participant index within the room */
+  uint8_t kind;         /* lkf_kind */
+  uint8_t codec;        /* lkf_codec */
+  uint8_t has_ref_ts;   /* 1: getReferenceLayerRTPTimestamp wired to layer_offsets
+                           (streamtrackermanager.go:660-679); 0: nil callback */
+  uint8_t is_mic;       /* TrackSource_MICROPHONE (uptrackmanager.go:425) */
+  uint32_t clock_rate;
+  uint32_t layer_offsets[3][3]; /* layerOffsets[ref][layer]; 0 = unavailable */
+} lkf_track_params;
+
+/* One subscriber DownTrack (NewDownTrack downtrack.go:286 + Bind :362). */
+typedef struct lkf_downtrack_params {
+  int32_t track;        /* handle from lkf_add_track */
+  uint32_t subscriber;  /* subscriber participant index within the room */
+  uint32_t ssrc;        /* d.ssrc */
+  uint8_t payload_type; /* d.payloadType */
+  uint8_t ext_dd;       /* dependencyDescriptorExtID (0 = none) */
+  uint8_t ext_playout;  /* playoutDelayExtID */
+  uint8_t ext_abs_send_time; /* absSendTimeExtID: 3 placeholder bytes, stamped by the sender */
+  uint8_t playout_delay[3];  /* PlayOutDelay.Marshal() bytes (rtpextension/playoutdelay.go:40) */
+  uint8_t has_expected_ts;   /* 1: getExpectedRTPTimestamp wired (downtrack.go:1765); 0: nil */
+  int64_t bind_time_ns;      /* sequencer startTime (sequencer.go:100) on the virtual clock */
+} lkf_downtrack_params;
+
+/* ExtPacket descriptor (buffer.ExtPacket, buffer.go:54-64), 64 bytes.
+ * A batch is an array of these, grouped by track (each track's packets
+ * contiguous, in arrival order), plus one input arena of raw RTP packets. */
+typedef struct lkf_pkt {
+  uint64_t ext_sn;       /* ExtSequenceNumber (after ingress padding-exclusion adjust) */
+  uint64_t ext_ts;       /* ExtTimestamp */
+  int64_t arrival_ns;    /* Arrival, virtual clock */
+  uint32_t arena_off;    /* offset of the raw RTP packet in the batch arena */
+  uint32_t track;        /* track handle */
+  uint32_t ssrc;         /* Packet.SSRC */
+  uint16_t payload_off;  /* offset of the RTP payload within the raw packet */
+  uint16_t payload_len;  /* len(Packet.Payload) (padding excluded) */
+  uint8_t hdr0;          /* raw RTP byte 0: V(2) P(1) X(1) CC(4) */
+  uint8_t hdr1;          /* raw RTP byte 1: M(1) PT(7) */
+  int8_t spatial;        /* VideoLayer.Spatial */
+  int8_t temporal;       /* VideoLayer.Temporal */
+  uint8_t flags;         /* LKF_PKT_* */
+  uint8_t vp8_first;     /* VP8.FirstByte */
+  uint8_t vp8_bits;      /* LKF_VP8_* */
+  uint8_t vp8_hdr_size;  /* VP8.HeaderSize */
+  uint16_t vp8_picture_id;
+  uint8_t vp8_tl0picidx;
+  uint8_t vp8_tid;
+  uint8_t vp8_keyidx;
+  int8_t layer;          /* the `layer` argument of TrackSender.WriteRTP (downtrack.go:680) */
+  uint8_t audio_level;   /* RFC 6464 level (ingress only) */
+  uint8_t reserved[9];
+} lkf_pkt;
+
+#define LKF_PKT_KEYFRAME 0x01
+#define LKF_PKT_VP8 0x02        /* Payload is buffer.VP8 */
+#define LKF_PKT_HAS_LEVEL 0x04  /* audio_level valid */
+
+#define LKF_VP8_S 0x01
+#define LKF_VP8_I 0x02
+#define LKF_VP8_M 0x04
+#define LKF_VP8_L 0x08
+#define LKF_VP8_T 0x10
+#define LKF_VP8_Y 0x20
+#define LKF_VP8_K 0x40
+
+/* One forwarded (packet x DownTrack) tuple = one wire packet handed to the
+ * pacer (pacer.Packet, pacer/pacer.go:25-39), 40 bytes.  Records are
+ * DownTrack-major (a DownTrack's packets contiguous, in send order). */
+typedef struct lkf_out {
+  uint64_t ext_sn;      /* tp.rtp.extSequenceNumber (munged) */
+  uint64_t ext_ts;      /* tp.rtp.extTimestamp (munged) */
+  uint64_t out_off;     /* offset of the wire packet in the output arena */
+  uint32_t dt;          /* DownTrack handle */
+  uint32_t pkt;         /* index of the incoming packet in the batch */
+  uint16_t out_len;     /* wire packet length (RTP header + payload) */
+  uint8_t flags;        /* LKF_OUT_* */
+  int8_t layer;
+  uint32_t reserved;
+} lkf_out;
+
+#define LKF_OUT_SWITCHING 0x01 /* tp.isSwitching */
+#define LKF_OUT_RESUMING 0x02  /* tp.isResuming */
+#define LKF_OUT_KEYFRAME 0x04  /* extPkt.KeyFrame */
+#define LKF_OUT_MARKER 0x08    /* hdr.Marker */
+
+/* Per-batch counters. */
+typedef struct lkf_stats {
+  uint64_t tuples;        /* (packet x DownTrack) evaluations */
+  uint64_t forwarded;     /* tuples that emitted a wire packet */
+  uint64_t out_bytes;     /* sum of out_len */
+  uint64_t arena_bytes;   /* output arena bytes used (16-B aligned packets) */
+  uint64_t drops[LKF_DROP_NREASONS];
+} lkf_stats;
+
+/* Exported Forwarder state: ForwarderState forwarder.go:158-166 with
+ * RTPMungerState rtpmunger.go:53-60 and VP8State codecmunger/vp8.go:35-43. */
+typedef struct lkf_fwd_state {
+  uint8_t started;
+  uint8_t last_marker, second_last_marker;
+  uint8_t has_vp8;
+  int32_t reference_layer_spatial;
+  int64_t pre_start_time_ns;
+  uint64_t ext_first_ts;
+  uint64_t ref_ts_offset;
+  uint64_t ext_last_sn, ext_second_last_sn, ext_last_ts, ext_second_last_ts;
+  int32_t vp8_ext_last_picture_id;
+  uint8_t vp8_picture_id_used, vp8_last_tl0picidx, vp8_tl0picidx_used, vp8_tid_used;
+  uint8_t vp8_last_keyidx, vp8_keyidx_used, pad[2];
+} lkf_fwd_state;
+
+typedef struct lkf_engine lkf_engine;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* Creates an engine bound to HIP device `hip_device`.  NULL on failure. */
+lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg);
+void lkf_destroy(lkf_engine *e);
+const char *lkf_last_error(const lkf_engine *e);
+
+/* ---- topology ----------------------------------------------------------- */
+/* sfu.NewWebRTCReceiver (receiver.go:195) + Forwarder.DetermineCodec. >=0 handle. */
+int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p);
+/* sfu.NewDownTrack + Bind (downtrack.go:286,362) + receiver.AddDownTrack (:410). */
+int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p);
+/* DownTrack.Close / receiver.DeleteDownTrack. */
+int lkf_remove_downtrack(lkf_engine *e, int32_t dt);
+/* Replaces the streamtrackermanager layer offsets (SR data arrived). */
+int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9]);
+
+/* ---- control ------------------------------------------------------------ */
+/* Queues a Forwarder control op for the next lkf_run (lkf_ctl_op). */
+int lkf_ctl(lkf_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64_t a2, int64_t a3,
+            uint32_t at_pkt);
+
+/* ---- data --------------------------------------------------------------- */
+/* Host batch: copies descriptors + arena to HBM (WebRTCReceiver.forwardRTP
+ * receiver.go:635 -> DownTrackSpreader.Broadcast downtrackspreader.go:89). */
+int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len);
+/* Device-resident batch (pointers into HBM, valid until lkf_run returns). */
+int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const uint8_t *d_arena,
+                      uint64_t arena_len);
+/* Runs the batch on `stream` (a hipStream_t, may be NULL): every DownTrack's
+ * TrackSender.WriteRTP (downtrack.go:680-760) for every packet of its track.
+ * Asynchronous; lkf_sync waits. */
+int lkf_run(lkf_engine *e, void *stream);
+int lkf_sync(lkf_engine *e);
+/* Batch results (valid after lkf_sync, until the next lkf_run). */
+int lkf_get_stats(lkf_engine *e, lkf_stats *out);
+/* Copies up to `cap` records and the wire bytes to host memory. */
+int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap, uint64_t *n_out,
+              uint64_t *arena_len);
+/* Device pointers of the output (zero-copy consumer, e.g. an SRTP stage). */
+int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, const uint8_t **d_arena,
+                      uint64_t *arena_len);
+
+/* ---- state (Forwarder.GetState / SeedState forwarder.go:340-375) -------- */
+int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *out);
+int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *in);
+
+/* ---- sequencer (sequencer.getExtPacketMetas sequencer.go:263, for RTX) --- */
+typedef struct lkf_seq_meta {
+  uint64_t ext_sn, ext_ts;
+  uint16_t source_sn, target_sn;
+  uint32_t timestamp;
+  uint32_t last_nack;
+  uint8_t marker, nacked;
+  int8_t layer;
+  uint8_t codec_len;
+  uint8_t codec[8];
+} lkf_seq_meta;
+int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns,
+                   lkf_seq_meta *out, uint32_t *n_out);
+
+/* ---- introspection ------------------------------------------------------ */
+/* Duration of the last batch's decide kernel, emit kernel and whole batch, ms. */
+int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *total_ms);
+/* Sums of the same over the last n runs (n <= 256), from HIP events recorded
+ * on the run stream; synchronises on the newest. */
+int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_ms, float *total_ms);
+/* Counters accumulated on the GPU over all runs since the last reset. */
+int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset);
+const char *lkf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LKFWD_H_ */

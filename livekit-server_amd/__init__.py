@@ -1,0 +1,165 @@
+"""lkfwd — MI355X-native batched RTP forwarding engine (livekit-server SFU hot path).
+
+The product is ``lib/liblkfwd.so`` (gfx950 HIP kernels + C++ host engine,
+C-ABI in ``include/lkfwd.h``).  This module is a thin ctypes loader used by the
+tests and bench: it never computes anything itself and has no CPU fallback —
+if the HIP library is missing or no GPU is present, it raises.
+
+Import with ``importlib.import_module("livekit-server_amd")`` (the directory
+name contains a hyphen).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+LIB_PATH = os.path.join(abi.LIBDIR, "liblkfwd.so")
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library(path=None):
+    """Loads liblkfwd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError("liblkfwd.so not built (%s): run __graft_entry__.build()" % p)
+    lib = C.CDLL(p)
+    v = C.c_void_p
+    lib.lkf_create.restype = v
+    lib.lkf_create.argtypes = [C.c_int, C.POINTER(abi.lkf_cfg)]
+    lib.lkf_destroy.restype = None
+    lib.lkf_destroy.argtypes = [v]
+    lib.lkf_last_error.restype = C.c_char_p
+    lib.lkf_last_error.argtypes = [v]
+    lib.lkf_version.restype = C.c_char_p
+    lib.lkf_version.argtypes = []
+    lib.lkf_submit.restype = C.c_int
+    lib.lkf_submit.argtypes = [v, v, C.c_uint32, v, C.c_uint64]
+    lib.lkf_submit_device.restype = C.c_int
+    lib.lkf_submit_device.argtypes = [v, v, C.c_uint32, v, C.c_uint64]
+    lib.lkf_run.restype = C.c_int
+    lib.lkf_run.argtypes = [v, v]
+    lib.lkf_sync.restype = C.c_int
+    lib.lkf_sync.argtypes = [v]
+    lib.lkf_output_device.restype = C.c_int
+    lib.lkf_output_device.argtypes = [v, C.POINTER(v), C.POINTER(C.c_uint64), C.POINTER(v), C.POINTER(C.c_uint64)]
+    lib.lkf_last_timings.restype = C.c_int
+    lib.lkf_last_timings.argtypes = [v, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    lib.lkf_timing_window.restype = C.c_int
+    lib.lkf_timing_window.argtypes = [v, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                      C.POINTER(C.c_float)]
+    lib.lkf_get_cumulative.restype = C.c_int
+    lib.lkf_get_cumulative.argtypes = [v, C.POINTER(abi.lkf_stats), C.c_int]
+    lib.api = abi.bind_engine_api(lib, "lkf_")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def drain_arrays(api, h, nmax=None):
+    """Reads the last batch's records + wire bytes into numpy arrays."""
+    n = C.c_uint64()
+    alen = C.c_uint64()
+    rc = api["drain"](h, None, 0, None, 0, C.byref(n), C.byref(alen))
+    if rc not in (0, -28):  # -28: ENOSPC for the size probe
+        raise EngineError("drain probe rc=%d" % rc)
+    recs = np.zeros(n.value, dtype=abi.OUT_DTYPE)
+    arena = np.zeros(alen.value, dtype=np.uint8)
+    rc = api["drain"](h, recs.ctypes.data, n.value, arena.ctypes.data, alen.value, C.byref(n), C.byref(alen))
+    if rc != 0:
+        raise EngineError("drain rc=%d" % rc)
+    return recs, arena
+
+
+class Engine:
+    """One lkf_engine on one HIP device (one process per GPU)."""
+
+    def __init__(self, device=0, max_tracks=1024, max_downtracks=16384, max_batch_pkts=1 << 16,
+                 max_batch_arena=64 << 20, max_out_pkts=1 << 20, max_out_bytes=256 << 20,
+                 max_batch_tuples=1 << 21, seq_size=500, lib_path=None):
+        self.lib = load_library(lib_path)
+        self.api = self.lib.api
+        cfg = abi.lkf_cfg(max_tracks=max_tracks, max_downtracks=max_downtracks, max_batch_pkts=max_batch_pkts,
+                          seq_size=seq_size, max_batch_arena=max_batch_arena, max_out_bytes=max_out_bytes,
+                          max_out_pkts=max_out_pkts, max_batch_tuples=max_batch_tuples)
+        self.h = self.lib.lkf_create(device, C.byref(cfg))
+        if not self.h:
+            raise EngineError("lkf_create failed on HIP device %d (no GPU or out of memory)" % device)
+
+    @classmethod
+    def for_trace(cls, trace, device=0, headroom=1.25, **kw):
+        """Engine sized for a synthetic `workload.Trace`."""
+        mp = int(trace.max_batch_pkts * headroom) + 64
+        return cls(device=device, max_tracks=trace.ntracks + 8, max_downtracks=trace.ndts + 8,
+                   max_batch_pkts=mp, max_batch_arena=int(trace.max_batch_arena * headroom) + 4096,
+                   max_batch_tuples=int(trace.max_batch_tuples * headroom) + 1024,
+                   max_out_pkts=int(trace.max_batch_tuples * headroom) + 1024,
+                   max_out_bytes=int(trace.max_batch_tuples * headroom) * 1536 + (1 << 20), **kw)
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise EngineError("%s rc=%d: %s" % (what, rc, self.lib.lkf_last_error(self.h).decode()))
+
+    def submit(self, pkts, n, arena, arena_len):
+        self._chk(self.lib.lkf_submit(self.h, C.cast(pkts, C.c_void_p), n, C.cast(arena, C.c_void_p), arena_len),
+                  "submit")
+
+    def submit_device(self, d_pkts, n, d_arena, arena_len):
+        self._chk(self.lib.lkf_submit_device(self.h, d_pkts, n, d_arena, arena_len), "submit_device")
+
+    def run(self, stream=None):
+        self._chk(self.lib.lkf_run(self.h, stream), "run")
+
+    def sync(self):
+        self._chk(self.lib.lkf_sync(self.h), "sync")
+
+    def stats(self):
+        st = abi.lkf_stats()
+        self._chk(self.api["get_stats"](self.h, C.byref(st)), "get_stats")
+        return st.as_dict()
+
+    def drain(self):
+        return drain_arrays(self.api, self.h)
+
+    def output_device(self):
+        d_out = C.c_void_p()
+        d_ar = C.c_void_p()
+        n = C.c_uint64()
+        alen = C.c_uint64()
+        self._chk(self.lib.lkf_output_device(self.h, C.byref(d_out), C.byref(n), C.byref(d_ar), C.byref(alen)),
+                  "output_device")
+        return d_out.value, n.value, d_ar.value, alen.value
+
+    def timings(self):
+        a, b, c = C.c_float(), C.c_float(), C.c_float()
+        self._chk(self.lib.lkf_last_timings(self.h, C.byref(a), C.byref(b), C.byref(c)), "timings")
+        return a.value, b.value, c.value
+
+    def timing_window(self, n):
+        a, b, c = C.c_float(), C.c_float(), C.c_float()
+        self._chk(self.lib.lkf_timing_window(self.h, n, C.byref(a), C.byref(b), C.byref(c)), "timing_window")
+        return a.value, b.value, c.value
+
+    def cumulative(self, reset=False):
+        st = abi.lkf_stats()
+        self._chk(self.lib.lkf_get_cumulative(self.h, C.byref(st), 1 if reset else 0), "cumulative")
+        return st.as_dict()
+
+    def close(self):
+        if self.h:
+            self.lib.lkf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

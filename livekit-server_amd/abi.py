@@ -1,0 +1,252 @@
+"""ctypes mirror of include/lkfwd.h and csrc/synth.h (plain C structs).
+
+The Python layer is host plumbing only: it loads ``liblkfwd.so`` (the HIP
+engine) and ``liblkfsynth.so`` (the synthetic workload generator) and gives the
+tests / bench a typed view of the C-ABI.  There is no compute here and no
+fallback: a missing library raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "lib")
+
+
+class lkf_cfg(C.Structure):
+    _fields_ = [
+        ("max_tracks", C.c_uint32),
+        ("max_downtracks", C.c_uint32),
+        ("max_batch_pkts", C.c_uint32),
+        ("seq_size", C.c_uint32),
+        ("max_batch_arena", C.c_uint64),
+        ("max_out_bytes", C.c_uint64),
+        ("max_out_pkts", C.c_uint64),
+        ("max_batch_tuples", C.c_uint64),
+    ]
+
+
+class lkf_track_params(C.Structure):
+    _fields_ = [
+        ("track_id", C.c_uint64),
+        ("room", C.c_uint32),
+        ("publisher", C.c_uint32),
+        ("kind", C.c_uint8),
+        ("codec", C.c_uint8),
+        ("has_ref_ts", C.c_uint8),
+        ("is_mic", C.c_uint8),
+        ("clock_rate", C.c_uint32),
+        ("layer_offsets", (C.c_uint32 * 3) * 3),
+    ]
+
+
+class lkf_downtrack_params(C.Structure):
+    _fields_ = [
+        ("track", C.c_int32),
+        ("subscriber", C.c_uint32),
+        ("ssrc", C.c_uint32),
+        ("payload_type", C.c_uint8),
+        ("ext_dd", C.c_uint8),
+        ("ext_playout", C.c_uint8),
+        ("ext_abs_send_time", C.c_uint8),
+        ("playout_delay", C.c_uint8 * 3),
+        ("has_expected_ts", C.c_uint8),
+        ("bind_time_ns", C.c_int64),
+    ]
+
+
+class lkf_pkt(C.Structure):
+    _fields_ = [
+        ("ext_sn", C.c_uint64),
+        ("ext_ts", C.c_uint64),
+        ("arrival_ns", C.c_int64),
+        ("arena_off", C.c_uint32),
+        ("track", C.c_uint32),
+        ("ssrc", C.c_uint32),
+        ("payload_off", C.c_uint16),
+        ("payload_len", C.c_uint16),
+        ("hdr0", C.c_uint8),
+        ("hdr1", C.c_uint8),
+        ("spatial", C.c_int8),
+        ("temporal", C.c_int8),
+        ("flags", C.c_uint8),
+        ("vp8_first", C.c_uint8),
+        ("vp8_bits", C.c_uint8),
+        ("vp8_hdr_size", C.c_uint8),
+        ("vp8_picture_id", C.c_uint16),
+        ("vp8_tl0picidx", C.c_uint8),
+        ("vp8_tid", C.c_uint8),
+        ("vp8_keyidx", C.c_uint8),
+        ("layer", C.c_int8),
+        ("audio_level", C.c_uint8),
+        ("reserved", C.c_uint8 * 9),
+    ]
+
+
+class lkf_out(C.Structure):
+    _fields_ = [
+        ("ext_sn", C.c_uint64),
+        ("ext_ts", C.c_uint64),
+        ("out_off", C.c_uint64),
+        ("dt", C.c_uint32),
+        ("pkt", C.c_uint32),
+        ("out_len", C.c_uint16),
+        ("flags", C.c_uint8),
+        ("layer", C.c_int8),
+        ("reserved", C.c_uint32),
+    ]
+
+
+LKF_DROP_NREASONS = 11
+
+
+class lkf_stats(C.Structure):
+    _fields_ = [
+        ("tuples", C.c_uint64),
+        ("forwarded", C.c_uint64),
+        ("out_bytes", C.c_uint64),
+        ("arena_bytes", C.c_uint64),
+        ("drops", C.c_uint64 * LKF_DROP_NREASONS),
+    ]
+
+    def as_dict(self):
+        return {
+            "tuples": self.tuples,
+            "forwarded": self.forwarded,
+            "out_bytes": self.out_bytes,
+            "arena_bytes": self.arena_bytes,
+            "drops": list(self.drops),
+        }
+
+
+class lkf_fwd_state(C.Structure):
+    _fields_ = [
+        ("started", C.c_uint8),
+        ("last_marker", C.c_uint8),
+        ("second_last_marker", C.c_uint8),
+        ("has_vp8", C.c_uint8),
+        ("reference_layer_spatial", C.c_int32),
+        ("pre_start_time_ns", C.c_int64),
+        ("ext_first_ts", C.c_uint64),
+        ("ref_ts_offset", C.c_uint64),
+        ("ext_last_sn", C.c_uint64),
+        ("ext_second_last_sn", C.c_uint64),
+        ("ext_last_ts", C.c_uint64),
+        ("ext_second_last_ts", C.c_uint64),
+        ("vp8_ext_last_picture_id", C.c_int32),
+        ("vp8_picture_id_used", C.c_uint8),
+        ("vp8_last_tl0picidx", C.c_uint8),
+        ("vp8_tl0picidx_used", C.c_uint8),
+        ("vp8_tid_used", C.c_uint8),
+        ("vp8_last_keyidx", C.c_uint8),
+        ("vp8_keyidx_used", C.c_uint8),
+        ("pad", C.c_uint8 * 2),
+    ]
+
+    def as_tuple(self):
+        return tuple(getattr(self, f[0]) for f in self._fields_ if f[0] != "pad")
+
+
+class lkf_seq_meta(C.Structure):
+    _fields_ = [
+        ("ext_sn", C.c_uint64),
+        ("ext_ts", C.c_uint64),
+        ("source_sn", C.c_uint16),
+        ("target_sn", C.c_uint16),
+        ("timestamp", C.c_uint32),
+        ("last_nack", C.c_uint32),
+        ("marker", C.c_uint8),
+        ("nacked", C.c_uint8),
+        ("layer", C.c_int8),
+        ("codec_len", C.c_uint8),
+        ("codec", C.c_uint8 * 8),
+    ]
+
+
+class lkfs_cfg(C.Structure):
+    _fields_ = [
+        ("config", C.c_int32),
+        ("seed", C.c_uint64),
+        ("duration_s", C.c_double),
+        ("batch_s", C.c_double),
+        ("rooms", C.c_uint32),
+        ("participants", C.c_uint32),
+        ("room_base", C.c_uint32),
+        ("loss", C.c_double),
+        ("reorder", C.c_double),
+        ("with_events", C.c_int32),
+        ("has_callbacks", C.c_int32),
+    ]
+
+
+class lkfs_event(C.Structure):
+    _fields_ = [
+        ("dt", C.c_int32),
+        ("op", C.c_int32),
+        ("a", C.c_int64 * 4),
+        ("at_pkt", C.c_uint32),
+        ("pad", C.c_uint32),
+    ]
+
+
+assert C.sizeof(lkf_pkt) == 64, C.sizeof(lkf_pkt)
+assert C.sizeof(lkf_out) == 40, C.sizeof(lkf_out)
+
+OUT_DTYPE = np.dtype(
+    [("ext_sn", "<u8"), ("ext_ts", "<u8"), ("out_off", "<u8"), ("dt", "<u4"), ("pkt", "<u4"),
+     ("out_len", "<u2"), ("flags", "u1"), ("layer", "i1"), ("reserved", "<u4")]
+)
+assert OUT_DTYPE.itemsize == 40
+
+
+def _bind(lib, name, restype, argtypes):
+    fn = getattr(lib, name)
+    fn.restype = restype
+    fn.argtypes = argtypes
+    return fn
+
+
+P = C.POINTER
+
+
+def bind_engine_api(lib, prefix):
+    """Binds the lkf_* (engine) or orc_* (oracle) entry points of `lib`."""
+    e = C.c_void_p
+    api = {}
+    api["add_track"] = _bind(lib, prefix + "add_track", C.c_int32, [e, P(lkf_track_params)])
+    api["add_downtrack"] = _bind(lib, prefix + "add_downtrack", C.c_int32, [e, P(lkf_downtrack_params)])
+    api["remove_downtrack"] = _bind(lib, prefix + "remove_downtrack", C.c_int, [e, C.c_int32])
+    api["set_layer_offsets"] = _bind(lib, prefix + "set_layer_offsets", C.c_int, [e, C.c_int32, P(C.c_uint32)])
+    api["ctl"] = _bind(lib, prefix + "ctl", C.c_int,
+                       [e, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_uint32])
+    api["get_stats"] = _bind(lib, prefix + "get_stats", C.c_int, [e, P(lkf_stats)])
+    api["drain"] = _bind(lib, prefix + "drain", C.c_int,
+                         [e, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, P(C.c_uint64), P(C.c_uint64)])
+    api["get_state"] = _bind(lib, prefix + "get_state", C.c_int, [e, C.c_int32, P(lkf_fwd_state)])
+    api["seed_state"] = _bind(lib, prefix + "seed_state", C.c_int, [e, C.c_int32, P(lkf_fwd_state)])
+    api["seq_lookup"] = _bind(lib, prefix + "seq_lookup", C.c_int,
+                              [e, C.c_int32, P(C.c_uint16), C.c_uint32, C.c_int64, P(lkf_seq_meta), P(C.c_uint32)])
+    return api
+
+
+def load_synth(path=None):
+    path = path or os.path.join(LIBDIR, "liblkfsynth.so")
+    lib = C.CDLL(path)
+    t = C.c_void_p
+    _bind(lib, "lkfs_generate", t, [P(lkfs_cfg)])
+    _bind(lib, "lkfs_free", None, [t])
+    _bind(lib, "lkfs_num_tracks", C.c_uint32, [t])
+    _bind(lib, "lkfs_num_downtracks", C.c_uint32, [t])
+    _bind(lib, "lkfs_tracks", P(lkf_track_params), [t])
+    _bind(lib, "lkfs_downtracks", P(lkf_downtrack_params), [t])
+    _bind(lib, "lkfs_num_batches", C.c_uint32, [t])
+    _bind(lib, "lkfs_batch", C.c_int,
+          [t, C.c_uint32, P(P(lkf_pkt)), P(C.c_uint32), P(P(C.c_uint8)), P(C.c_uint64)])
+    _bind(lib, "lkfs_batch_events", C.c_int, [t, C.c_uint32, P(P(lkfs_event)), P(C.c_uint32)])
+    _bind(lib, "lkfs_total_pkts", C.c_uint64, [t])
+    _bind(lib, "lkfs_total_arena", C.c_uint64, [t])
+    _bind(lib, "lkfs_max_batch_pkts", C.c_uint32, [t])
+    _bind(lib, "lkfs_max_batch_arena", C.c_uint64, [t])
+    _bind(lib, "lkfs_max_batch_tuples", C.c_uint64, [t])
+    return lib

@@ -1,0 +1,681 @@
+// engine.cpp — host side of liblkfwd.so (the C-ABI of include/lkfwd.h).
+//
+// Owns the HBM-resident per-DownTrack state and the per-batch scratch, turns
+// queued control ops into a per-lane event list, and enqueues the batch
+// pipeline (forward_kernels.hip) on a HIP stream.  There is no CPU
+// forwarding path: every per-packet decision runs in the gfx950 kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lkfwd.h"
+#include "fwd_state.h"
+#include "kernels.h"
+
+using namespace lkf;
+
+namespace {
+
+template <typename T>
+hipError_t dalloc(T **p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T));
+}
+
+constexpr int kStatsWords = 4 + LKF_DROP_NREASONS;
+
+}  // namespace
+
+struct lkf_engine {
+  int dev = 0;
+  hipStream_t own = nullptr;
+  hipStream_t cur = nullptr;
+  lkf_cfg cfg{};
+  std::string err;
+
+  // topology (host mirror)
+  std::vector<lkf_track_params> tracks;
+  std::vector<lkf_downtrack_params> dtp;
+  std::vector<uint8_t> active;
+  bool schedDirty = true;
+  std::vector<uint32_t> sched;   // lane -> dt
+  std::vector<int32_t> dtLane;   // dt -> lane (-1 inactive)
+
+  // queued control ops
+  struct Pend {
+    uint32_t dt;
+    DevEvent ev;
+    uint64_t seq;
+  };
+  std::vector<Pend> pending;
+  uint64_t pendSeq = 0;
+  std::vector<DevEvent> hEvents;
+  std::vector<uint32_t> hEvOff;
+
+  // device: persistent state
+  DevTrack *dTracks = nullptr;
+  DTHot *dHot = nullptr;
+  DevDT *dDTs = nullptr;
+  RangeEntry *dRm = nullptr;
+  VP8Cold *dVc = nullptr;
+  SeqMeta *dSeq = nullptr;
+  uint32_t *dSched = nullptr;
+  // device: batch input
+  lkf_pkt *dPktsOwn = nullptr;
+  uint8_t *dArenaOwn = nullptr;
+  const lkf_pkt *curPkts = nullptr;
+  const uint8_t *curArena = nullptr;
+  uint32_t curN = 0;
+  uint64_t curArenaLen = 0;
+  bool haveBatch = false;
+  // device: batch scratch
+  uint32_t *dTBegin = nullptr, *dTEnd = nullptr, *dTRuns = nullptr, *dErr = nullptr;
+  uint64_t *dSlotBase = nullptr, *dPartA = nullptr, *dPartB = nullptr, *dTot = nullptr;
+  Tuple *dTuples = nullptr;
+  uint32_t *dFwdCnt = nullptr;
+  uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
+  lkf_out *dOut = nullptr;
+  uint8_t *dOutArena = nullptr;
+  DevEvent *dEvents = nullptr;
+  uint32_t *dEvOff = nullptr;
+  uint64_t evCap = 0;
+  uint64_t *dStats = nullptr;
+  // seq lookup scratch
+  uint16_t *dSns = nullptr;
+  lkf_seq_meta *dSeqOut = nullptr;
+  uint32_t *dSeqN = nullptr;
+  uint32_t seqScratchCap = 0;
+
+  hipEvent_t evt[4] = {nullptr, nullptr, nullptr, nullptr};
+  static constexpr int kRing = 256;
+  hipEvent_t ring[kRing][4] = {};
+  uint64_t nRuns = 0;
+  uint64_t *dCum = nullptr;
+  bool ran = false;
+  uint32_t emitGrid = 2048;
+};
+
+static int fail(lkf_engine *e, const char *what, hipError_t r) {
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(r));
+  e->err = buf;
+  return LKF_EHIP;
+}
+#define HIPCHK(call, what)                   \
+  do {                                       \
+    hipError_t _r = (call);                  \
+    if (_r != hipSuccess) return fail(e, what, _r); \
+  } while (0)
+
+// NewForwarder + DetermineCodec + NewRTPMunger + videolayerselector.NewBase +
+// newSequencer (forwarder.go:217-338, rtpmunger.go:94, base.go NewBase,
+// sequencer.go:97) as the initial HBM state of one DownTrack.
+static void init_hot(DTHot &h, const lkf_track_params &tp, const lkf_downtrack_params &p) {
+  std::memset(&h, 0, sizeof(h));
+  h.referenceLayerSpatial = -1;
+  h.maxS = h.maxT = h.seenS = h.seenT = -1;
+  h.tgtS = h.tgtT = h.ptgtS = h.ptgtT = -1;
+  h.curS = h.curT = h.prevS = h.prevT = -1;
+  h.reqS = -1;
+  h.rmOpenStart = 0;  // NewRangeMap: initRanges(0, 0)
+  h.rmOpenValue = 0;
+  uint32_t f = F_ACTIVE;
+  if (tp.kind == LKF_KIND_VIDEO) {
+    f |= F_VIDEO;
+    h.maxT = 3;  // vls.SetMaxTemporal(DefaultMaxLayerTemporal) forwarder.go:235-237
+    if (tp.codec == LKF_CODEC_VP8) f |= F_VP8 | F_SIMULCAST | F_TLS_VP8;
+    if (tp.codec == LKF_CODEC_H264) f |= F_SIMULCAST;
+  }
+  if (p.has_expected_ts) f |= F_HAS_EXPECTED;
+  h.flags = f;
+  h.seqStartMs = p.bind_time_ns / 1000000;
+}
+
+static DevTrack to_dev_track(const lkf_track_params &p) {
+  DevTrack t;
+  std::memset(&t, 0, sizeof(t));
+  t.kind = p.kind;
+  t.codec = p.codec;
+  t.hasRefTS = p.has_ref_ts;
+  t.clockRate = p.clock_rate;
+  for (int r = 0; r < 3; r++)
+    for (int l = 0; l < 3; l++) t.layerOffsets[r * 3 + l] = p.layer_offsets[r][l];
+  return t;
+}
+
+extern "C" {
+
+const char *lkf_version(void) { return "lkfwd 0.1 (gfx950)"; }
+
+const char *lkf_last_error(const lkf_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
+  if (!cfg) return nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || hip_device < 0 || hip_device >= ndev) return nullptr;
+  auto *e = new lkf_engine();
+  e->dev = hip_device;
+  e->cfg = *cfg;
+  if (e->cfg.seq_size == 0) e->cfg.seq_size = 500;
+  if (hipSetDevice(hip_device) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  const lkf_cfg &c = e->cfg;
+  bool ok = true;
+  auto A = [&](hipError_t r) { ok = ok && (r == hipSuccess); };
+  A(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
+  e->cur = e->own;
+  A(dalloc(&e->dTracks, c.max_tracks));
+  A(dalloc(&e->dHot, c.max_downtracks));
+  A(dalloc(&e->dDTs, c.max_downtracks));
+  A(dalloc(&e->dRm, size_t(c.max_downtracks) * kRangeCap));
+  A(dalloc(&e->dVc, c.max_downtracks));
+  A(dalloc(&e->dSeq, size_t(c.max_downtracks) * c.seq_size));
+  A(dalloc(&e->dSched, c.max_downtracks));
+  A(dalloc(&e->dPktsOwn, c.max_batch_pkts));
+  A(dalloc(&e->dArenaOwn, c.max_batch_arena + 64));
+  A(dalloc(&e->dTBegin, c.max_tracks));
+  A(dalloc(&e->dTEnd, c.max_tracks));
+  A(dalloc(&e->dTRuns, c.max_tracks));
+  A(dalloc(&e->dErr, 4));
+  const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
+  A(dalloc(&e->dSlotBase, c.max_downtracks));
+  A(dalloc(&e->dPartA, nparts));
+  A(dalloc(&e->dPartB, nparts));
+  A(dalloc(&e->dTot, 4));
+  A(dalloc(&e->dTuples, c.max_batch_tuples));
+  A(dalloc(&e->dFwdCnt, c.max_downtracks));
+  A(dalloc(&e->dFwdBytes, c.max_downtracks));
+  A(dalloc(&e->dRecBase, c.max_downtracks));
+  A(dalloc(&e->dByteBase, c.max_downtracks));
+  A(dalloc(&e->dOut, c.max_out_pkts));
+  A(dalloc(&e->dOutArena, c.max_out_bytes + 64));
+  A(dalloc(&e->dEvOff, size_t(c.max_downtracks) + 1));
+  A(dalloc(&e->dStats, kStatsWords));
+  for (auto &ev : e->evt) A(hipEventCreate(&ev));
+  for (auto &r : e->ring)
+    for (auto &ev : r) A(hipEventCreate(&ev));
+  A(dalloc(&e->dCum, kStatsWords));
+  if (ok) {
+    A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
+    A(hipMemset(e->dArenaOwn, 0, c.max_batch_arena + 64));
+    A(hipMemset(e->dTot, 0, 4 * sizeof(uint64_t)));
+    A(hipMemset(e->dStats, 0, kStatsWords * sizeof(uint64_t)));
+    A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
+  }
+  if (!ok) {
+    lkf_destroy(e);
+    return nullptr;
+  }
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device);
+  e->emitGrid = uint32_t(cus) * 8;
+  return e;
+}
+
+void lkf_destroy(lkf_engine *e) {
+  if (!e) return;
+  (void)hipSetDevice(e->dev);
+  if (e->own) (void)hipStreamSynchronize(e->own);
+  void *ptrs[] = {e->dTracks, e->dHot, e->dDTs, e->dRm, e->dVc, e->dSeq, e->dSched, e->dPktsOwn, e->dArenaOwn,
+                  e->dTBegin, e->dTEnd, e->dTRuns, e->dErr, e->dSlotBase, e->dPartA, e->dPartB, e->dTot,
+                  e->dTuples, e->dFwdCnt, e->dFwdBytes, e->dRecBase, e->dByteBase, e->dOut, e->dOutArena,
+                  e->dEvents, e->dEvOff, e->dStats, e->dSns, e->dSeqOut, e->dSeqN};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  for (auto &ev : e->evt)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto &r : e->ring)
+    for (auto &ev : r)
+      if (ev) (void)hipEventDestroy(ev);
+  if (e->dCum) (void)hipFree(e->dCum);
+  if (e->own) (void)hipStreamDestroy(e->own);
+  delete e;
+}
+
+int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p) {
+  if (!e || !p) return LKF_EINVAL;
+  if (e->tracks.size() >= e->cfg.max_tracks) return LKF_ENOSPC;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  int32_t h = int32_t(e->tracks.size());
+  e->tracks.push_back(*p);
+  DevTrack t = to_dev_track(*p);
+  HIPCHK(hipMemcpyAsync(e->dTracks + h, &t, sizeof(t), hipMemcpyHostToDevice, e->own), "add_track copy");
+  HIPCHK(hipStreamSynchronize(e->own), "add_track sync");
+  return h;
+}
+
+int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9]) {
+  if (!e || track < 0 || track >= int32_t(e->tracks.size())) return LKF_EINVAL;
+  std::memcpy(e->tracks[track].layer_offsets, offsets, 9 * sizeof(uint32_t));
+  DevTrack t = to_dev_track(e->tracks[track]);
+  HIPCHK(hipMemcpyAsync(e->dTracks + track, &t, sizeof(t), hipMemcpyHostToDevice, e->own), "offsets copy");
+  HIPCHK(hipStreamSynchronize(e->own), "offsets sync");
+  return LKF_OK;
+}
+
+int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
+  if (!e || !p) return LKF_EINVAL;
+  if (p->track < 0 || p->track >= int32_t(e->tracks.size())) return LKF_EINVAL;
+  if (e->dtp.size() >= e->cfg.max_downtracks) return LKF_ENOSPC;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  int32_t h = int32_t(e->dtp.size());
+  e->dtp.push_back(*p);
+  e->active.push_back(1);
+  DTHot hot;
+  init_hot(hot, e->tracks[p->track], *p);
+  DevDT d;
+  std::memset(&d, 0, sizeof(d));
+  d.track = uint32_t(p->track);
+  d.ssrc = p->ssrc;
+  d.pt = p->payload_type;
+  d.extPlayout = p->ext_playout;
+  d.extAbs = p->ext_abs_send_time;
+  d.extDD = p->ext_dd;
+  std::memcpy(d.playout, p->playout_delay, 3);
+  d.active = 1;
+  HIPCHK(hipMemcpyAsync(e->dHot + h, &hot, sizeof(hot), hipMemcpyHostToDevice, e->own), "dt hot copy");
+  HIPCHK(hipMemcpyAsync(e->dDTs + h, &d, sizeof(d), hipMemcpyHostToDevice, e->own), "dt copy");
+  HIPCHK(hipStreamSynchronize(e->own), "add_downtrack sync");
+  e->schedDirty = true;
+  return h;
+}
+
+int lkf_remove_downtrack(lkf_engine *e, int32_t dt) {
+  if (!e || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  HIPCHK(hipStreamSynchronize(e->own), "remove sync");
+  e->active[dt] = 0;
+  uint8_t zero = 0;
+  HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(e->dDTs + dt) + offsetof(DevDT, active), &zero, 1,
+                   hipMemcpyHostToDevice),
+         "remove copy");
+  e->schedDirty = true;
+  return LKF_OK;
+}
+
+int lkf_ctl(lkf_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64_t a2, int64_t a3, uint32_t at_pkt) {
+  if (!e || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  if (op < LKF_CTL_MUTE || op > LKF_CTL_PLAYOUT_ACKED) return LKF_EINVAL;
+  lkf_engine::Pend p;
+  p.dt = uint32_t(dt);
+  std::memset(&p.ev, 0, sizeof(p.ev));
+  p.ev.at = at_pkt;
+  p.ev.op = op;
+  p.ev.a[0] = a0;
+  p.ev.a[1] = a1;
+  p.ev.a[2] = a2;
+  p.ev.a[3] = a3;
+  p.seq = e->pendSeq++;
+  e->pending.push_back(p);
+  return LKF_OK;
+}
+
+int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len) {
+  if (!e || (n && !pkts)) return LKF_EINVAL;
+  if (n > e->cfg.max_batch_pkts || arena_len > e->cfg.max_batch_arena) return LKF_ENOSPC;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (n) HIPCHK(hipMemcpyAsync(e->dPktsOwn, pkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyHostToDevice, e->own), "pkts");
+  if (arena_len) HIPCHK(hipMemcpyAsync(e->dArenaOwn, arena, arena_len, hipMemcpyHostToDevice, e->own), "arena");
+  HIPCHK(hipStreamSynchronize(e->own), "submit sync");
+  e->curPkts = e->dPktsOwn;
+  e->curArena = e->dArenaOwn;
+  e->curN = n;
+  e->curArenaLen = arena_len;
+  e->haveBatch = true;
+  return LKF_OK;
+}
+
+int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const uint8_t *d_arena, uint64_t arena_len) {
+  if (!e || (n && !d_pkts)) return LKF_EINVAL;
+  if (n > e->cfg.max_batch_pkts) return LKF_ENOSPC;
+  e->curPkts = d_pkts;
+  e->curArena = d_arena;
+  e->curN = n;
+  e->curArenaLen = arena_len;
+  e->haveBatch = true;
+  return LKF_OK;
+}
+
+static int rebuild_sched(lkf_engine *e) {
+  const uint32_t nd = uint32_t(e->dtp.size());
+  e->sched.clear();
+  for (uint32_t d = 0; d < nd; d++)
+    if (e->active[d]) e->sched.push_back(d);
+  // lanes of a wave share a track (same packet descriptors); video tracks
+  // (longer packet lists) first so waves are trip-count homogeneous.
+  std::stable_sort(e->sched.begin(), e->sched.end(), [&](uint32_t a, uint32_t b) {
+    const auto &ta = e->tracks[e->dtp[a].track], &tb = e->tracks[e->dtp[b].track];
+    if (ta.kind != tb.kind) return ta.kind > tb.kind;
+    return e->dtp[a].track < e->dtp[b].track;
+  });
+  e->dtLane.assign(nd, -1);
+  for (uint32_t l = 0; l < e->sched.size(); l++) e->dtLane[e->sched[l]] = int32_t(l);
+  if (!e->sched.empty())
+    HIPCHK(hipMemcpy(e->dSched, e->sched.data(), e->sched.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
+           "sched copy");
+  e->schedDirty = false;
+  return LKF_OK;
+}
+
+int lkf_run(lkf_engine *e, void *stream) {
+  if (!e) return LKF_EINVAL;
+  if (!e->haveBatch) {  // control-only run: an empty batch applies queued ops
+    e->curPkts = e->dPktsOwn;
+    e->curArena = e->dArenaOwn;
+    e->curN = 0;
+    e->curArenaLen = 0;
+  }
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (e->schedDirty) {
+    int rc = rebuild_sched(e);
+    if (rc) return rc;
+  }
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e->own;
+  e->cur = s;
+  const uint32_t nt = uint32_t(e->tracks.size());
+  const uint32_t nd = uint32_t(e->dtp.size());
+  const uint32_t nl = uint32_t(e->sched.size());
+
+  // per-lane event CSR (stable by queue order, then by at_pkt)
+  std::stable_sort(e->pending.begin(), e->pending.end(),
+                   [&](const lkf_engine::Pend &a, const lkf_engine::Pend &b) {
+                     int la = e->dtLane[a.dt], lb = e->dtLane[b.dt];
+                     if (la != lb) return la < lb;
+                     return a.ev.at < b.ev.at;
+                   });
+  e->hEvOff.assign(size_t(nl) + 1, 0);
+  e->hEvents.clear();
+  for (auto &p : e->pending) {
+    int l = e->dtLane[p.dt];
+    if (l < 0) continue;  // op for a removed DownTrack
+    e->hEvOff[l + 1]++;
+    e->hEvents.push_back(p.ev);
+  }
+  for (uint32_t l = 0; l < nl; l++) e->hEvOff[l + 1] += e->hEvOff[l];
+  e->pending.clear();
+  if (e->hEvents.size() > e->evCap) {
+    if (e->dEvents) HIPCHK(hipFree(e->dEvents), "free events");
+    e->evCap = std::max<uint64_t>(e->hEvents.size(), 1024);
+    HIPCHK(dalloc(&e->dEvents, e->evCap), "alloc events");
+  }
+  if (!e->hEvents.empty())
+    HIPCHK(hipMemcpyAsync(e->dEvents, e->hEvents.data(), e->hEvents.size() * sizeof(DevEvent), hipMemcpyHostToDevice,
+                          s),
+           "events copy");
+  HIPCHK(hipMemcpyAsync(e->dEvOff, e->hEvOff.data(), e->hEvOff.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s),
+         "evoff copy");
+
+  HIPCHK(hipMemsetAsync(e->dTBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dTEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dTRuns, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dErr, 0, 4 * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dStats, 0, kStatsWords * sizeof(uint64_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dFwdCnt, 0, size_t(std::max(nd, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dFwdBytes, 0, size_t(std::max(nd, 1u)) * sizeof(uint64_t), s), "memset");
+
+  hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
+  HIPCHK(hipEventRecord(e->evt[0], s), "event");
+  HIPCHK(hipEventRecord(rg[0], s), "event");
+  HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, nt, e->dTBegin, e->dTEnd, e->dTRuns, e->dErr), "track_ranges");
+  HIPCHK(launch_scan(s, 0, e->dDTs, e->dTBegin, e->dTEnd, nullptr, nullptr, nd, e->dPartA, e->dPartB, e->dSlotBase,
+                     nullptr, e->dTot + 0, nullptr),
+         "slot scan");
+  DecideLaunch d;
+  d.sched = e->dSched;
+  d.nlanes = nl;
+  d.hot = e->dHot;
+  d.dts = e->dDTs;
+  d.tracks = e->dTracks;
+  d.rm = e->dRm;
+  d.vc = e->dVc;
+  d.seq = e->dSeq;
+  d.seqSize = e->cfg.seq_size;
+  d.pkts = e->curPkts;
+  d.tBegin = e->dTBegin;
+  d.tEnd = e->dTEnd;
+  d.slotBase = e->dSlotBase;
+  d.tuples = e->dTuples;
+  d.tupleCap = e->cfg.max_batch_tuples;
+  d.err = e->dErr;
+  d.events = e->dEvents;
+  d.evOff = e->dEvOff;
+  d.fwdCnt = e->dFwdCnt;
+  d.fwdBytes = e->dFwdBytes;
+  d.stats = e->dStats;
+  HIPCHK(launch_decide(s, d), "decide");
+  HIPCHK(hipEventRecord(e->evt[1], s), "event");
+  HIPCHK(hipEventRecord(rg[1], s), "event");
+  HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, e->dFwdCnt, e->dFwdBytes, nd, e->dPartA, e->dPartB, e->dRecBase,
+                     e->dByteBase, e->dTot + 2, e->dTot + 3),
+         "out scan");
+  HIPCHK(hipEventRecord(e->evt[2], s), "event");
+  HIPCHK(hipEventRecord(rg[2], s), "event");
+  EmitLaunch m;
+  m.recBase = e->dRecBase;
+  m.byteBase = e->dByteBase;
+  m.slotBase = e->dSlotBase;
+  m.totals = e->dTot + 2;
+  m.tuples = e->dTuples;
+  m.pkts = e->curPkts;
+  m.arena = e->curArena;
+  m.dts = e->dDTs;
+  m.ndts = nd;
+  m.out = e->dOut;
+  m.outArena = e->dOutArena;
+  m.outCap = e->cfg.max_out_pkts;
+  m.outByteCap = e->cfg.max_out_bytes;
+  m.err = e->dErr;
+  m.grid = e->emitGrid;
+  if (nd) HIPCHK(launch_emit(s, m), "emit");
+  HIPCHK(hipEventRecord(e->evt[3], s), "event");
+  HIPCHK(hipEventRecord(rg[3], s), "event");
+  HIPCHK(launch_accumulate(s, e->dStats, e->dTot, e->dCum), "accumulate");
+  e->nRuns++;
+  e->haveBatch = false;
+  e->ran = true;
+  return LKF_OK;
+}
+
+int lkf_sync(lkf_engine *e) {
+  if (!e) return LKF_EINVAL;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  if (!e->ran) return LKF_OK;
+  uint32_t err[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpy(err, e->dErr, sizeof(err), hipMemcpyDeviceToHost), "err copy");
+  if (err[0] & 3u) {
+    e->err = "batch not grouped by track / bad track handle";
+    return LKF_EORDER;
+  }
+  if (err[0] & 12u) {
+    e->err = "output or tuple capacity exceeded";
+    return LKF_ENOSPC;
+  }
+  return LKF_OK;
+}
+
+int lkf_get_stats(lkf_engine *e, lkf_stats *out) {
+  if (!e || !out) return LKF_EINVAL;
+  int rc = lkf_sync(e);
+  uint64_t st[kStatsWords];
+  uint64_t tot[4];
+  HIPCHK(hipMemcpy(st, e->dStats, sizeof(st), hipMemcpyDeviceToHost), "stats copy");
+  HIPCHK(hipMemcpy(tot, e->dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  out->tuples = st[0];
+  out->forwarded = st[1];
+  out->out_bytes = st[2];
+  out->arena_bytes = tot[3];
+  for (int i = 0; i < LKF_DROP_NREASONS; i++) out->drops[i] = st[4 + i];
+  return rc;
+}
+
+int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, const uint8_t **d_arena,
+                      uint64_t *arena_len) {
+  if (!e) return LKF_EINVAL;
+  int rc = lkf_sync(e);
+  if (rc) return rc;
+  uint64_t tot[4];
+  HIPCHK(hipMemcpy(tot, e->dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  if (d_out) *d_out = e->dOut;
+  if (d_arena) *d_arena = e->dOutArena;
+  if (n_out) *n_out = tot[2];
+  if (arena_len) *arena_len = tot[3];
+  return LKF_OK;
+}
+
+int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap, uint64_t *n_out,
+              uint64_t *arena_len) {
+  const lkf_out *dOut;
+  const uint8_t *dAr;
+  uint64_t n = 0, len = 0;
+  int rc = lkf_output_device(e, &dOut, &n, &dAr, &len);
+  if (rc) return rc;
+  if (n_out) *n_out = n;
+  if (arena_len) *arena_len = len;
+  if (n > cap || len > arena_cap) return LKF_ENOSPC;
+  if (out && n) HIPCHK(hipMemcpy(out, dOut, n * sizeof(lkf_out), hipMemcpyDeviceToHost), "drain recs");
+  if (arena && len) HIPCHK(hipMemcpy(arena, dAr, len, hipMemcpyDeviceToHost), "drain bytes");
+  return LKF_OK;
+}
+
+int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *o) {
+  if (!e || !o || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  DTHot h;
+  HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "state copy");
+  std::memset(o, 0, sizeof(*o));
+  if (!(h.flags & F_STARTED)) return LKF_OK;  // GetState forwarder.go:344-346
+  o->started = 1;
+  o->reference_layer_spatial = h.referenceLayerSpatial;
+  o->pre_start_time_ns = h.preStartTime;
+  o->ext_first_ts = h.extFirstTS;
+  o->ref_ts_offset = h.refTSOffset;
+  o->ext_last_sn = h.extLastSN;
+  o->ext_second_last_sn = h.extSecondLastSN;
+  o->ext_last_ts = h.extLastTS;
+  o->ext_second_last_ts = h.extSecondLastTS;
+  o->last_marker = (h.flags & F_LAST_MARKER) ? 1 : 0;
+  o->second_last_marker = (h.flags & F_SECOND_LAST_MARKER) ? 1 : 0;
+  o->has_vp8 = (h.flags & F_VP8) ? 1 : 0;
+  o->vp8_ext_last_picture_id = h.extLastPictureId;
+  o->vp8_picture_id_used = (h.flags & F_PICID_USED) ? 1 : 0;
+  o->vp8_last_tl0picidx = h.lastTl0;
+  o->vp8_tl0picidx_used = (h.flags & F_TL0_USED) ? 1 : 0;
+  o->vp8_tid_used = (h.flags & F_TID_USED) ? 1 : 0;
+  o->vp8_last_keyidx = h.lastKeyIdx;
+  o->vp8_keyidx_used = (h.flags & F_KEYIDX_USED) ? 1 : 0;
+  return LKF_OK;
+}
+
+int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *i) {
+  if (!e || !i || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  if (!i->started) return LKF_OK;  // SeedState forwarder.go:360-362
+  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  DTHot h;
+  HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "state copy");
+  auto setf = [&](uint32_t f, bool v) { h.flags = v ? (h.flags | f) : (h.flags & ~f); };
+  // RTPMunger.SeedLast rtpmunger.go:126-133
+  h.extLastSN = i->ext_last_sn;
+  h.extSecondLastSN = i->ext_second_last_sn;
+  h.extLastTS = i->ext_last_ts;
+  h.extSecondLastTS = i->ext_second_last_ts;
+  setf(F_LAST_MARKER, i->last_marker);
+  setf(F_SECOND_LAST_MARKER, i->second_last_marker);
+  // codecMunger.SeedState vp8.go:99-109 (only a VP8 munger takes VP8State)
+  if ((h.flags & F_VP8) && i->has_vp8) {
+    h.extLastPictureId = i->vp8_ext_last_picture_id;
+    setf(F_PICID_USED, i->vp8_picture_id_used);
+    h.lastTl0 = i->vp8_last_tl0picidx;
+    setf(F_TL0_USED, i->vp8_tl0picidx_used);
+    setf(F_TID_USED, i->vp8_tid_used);
+    h.lastKeyIdx = i->vp8_last_keyidx;
+    setf(F_KEYIDX_USED, i->vp8_keyidx_used);
+  }
+  setf(F_STARTED, true);
+  h.referenceLayerSpatial = i->reference_layer_spatial;
+  h.preStartTime = i->pre_start_time_ns;
+  h.extFirstTS = i->ext_first_ts;
+  h.refTSOffset = i->ref_ts_offset;
+  HIPCHK(hipMemcpy(e->dHot + dt, &h, sizeof(h), hipMemcpyHostToDevice), "seed copy");
+  return LKF_OK;
+}
+
+int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns, lkf_seq_meta *out,
+                   uint32_t *n_out) {
+  if (!e || dt < 0 || dt >= int32_t(e->dtp.size()) || (n && (!sns || !out))) return LKF_EINVAL;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  if (n > e->seqScratchCap) {
+    if (e->dSns) (void)hipFree(e->dSns);
+    if (e->dSeqOut) (void)hipFree(e->dSeqOut);
+    e->seqScratchCap = std::max<uint32_t>(n, 256);
+    HIPCHK(dalloc(&e->dSns, e->seqScratchCap), "alloc");
+    HIPCHK(dalloc(&e->dSeqOut, e->seqScratchCap), "alloc");
+  }
+  if (!e->dSeqN) HIPCHK(dalloc(&e->dSeqN, 1), "alloc");
+  if (n) HIPCHK(hipMemcpy(e->dSns, sns, n * sizeof(uint16_t), hipMemcpyHostToDevice), "sns copy");
+  HIPCHK(launch_seq_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, uint32_t(dt), e->dSns, n, now_ns / 1000000,
+                           e->dSeqOut, e->dSeqN),
+         "seq lookup");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  uint32_t cnt = 0;
+  HIPCHK(hipMemcpy(&cnt, e->dSeqN, sizeof(cnt), hipMemcpyDeviceToHost), "n copy");
+  if (cnt) HIPCHK(hipMemcpy(out, e->dSeqOut, cnt * sizeof(lkf_seq_meta), hipMemcpyDeviceToHost), "out copy");
+  if (n_out) *n_out = cnt;
+  return LKF_OK;
+}
+
+int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *total_ms) {
+  if (!e || !e->ran) return LKF_EINVAL;
+  HIPCHK(hipEventSynchronize(e->evt[3]), "evsync");
+  float a = 0, b = 0, c = 0;
+  HIPCHK(hipEventElapsedTime(&a, e->evt[0], e->evt[1]), "elapsed");
+  HIPCHK(hipEventElapsedTime(&b, e->evt[2], e->evt[3]), "elapsed");
+  HIPCHK(hipEventElapsedTime(&c, e->evt[0], e->evt[3]), "elapsed");
+  if (decide_ms) *decide_ms = a;
+  if (emit_ms) *emit_ms = b;
+  if (total_ms) *total_ms = c;
+  return LKF_OK;
+}
+
+int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_ms, float *total_ms) {
+  if (!e || n == 0 || n > lkf_engine::kRing || n > e->nRuns) return LKF_EINVAL;
+  float sa = 0, sb = 0, sc = 0;
+  for (uint64_t r = e->nRuns - n; r < e->nRuns; r++) {
+    hipEvent_t *rg = e->ring[r % lkf_engine::kRing];
+    HIPCHK(hipEventSynchronize(rg[3]), "evsync");
+    float a = 0, b = 0, c = 0;
+    HIPCHK(hipEventElapsedTime(&a, rg[0], rg[1]), "elapsed");
+    HIPCHK(hipEventElapsedTime(&b, rg[2], rg[3]), "elapsed");
+    HIPCHK(hipEventElapsedTime(&c, rg[0], rg[3]), "elapsed");
+    sa += a;
+    sb += b;
+    sc += c;
+  }
+  if (decide_ms) *decide_ms = sa;
+  if (emit_ms) *emit_ms = sb;
+  if (total_ms) *total_ms = sc;
+  return LKF_OK;
+}
+
+int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset) {
+  if (!e || !out) return LKF_EINVAL;
+  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  uint64_t st[kStatsWords];
+  HIPCHK(hipMemcpy(st, e->dCum, sizeof(st), hipMemcpyDeviceToHost), "cum copy");
+  out->tuples = st[0];
+  out->forwarded = st[1];
+  out->out_bytes = st[2];
+  out->arena_bytes = st[3];
+  for (int i = 0; i < LKF_DROP_NREASONS; i++) out->drops[i] = st[4 + i];
+  if (reset) HIPCHK(hipMemset(e->dCum, 0, sizeof(st)), "cum reset");
+  return LKF_OK;
+}
+
+}  // extern "C"

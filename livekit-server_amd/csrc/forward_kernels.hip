@@ -1,0 +1,1400 @@
+// forward_kernels.hip — gfx950 kernels of the batched RTP forwarding engine.
+//
+// Per batch (lkf_run):
+//   k_track_ranges  packets grouped by track -> [begin,end) per track
+//   scan (slots)    per DownTrack tuple-slot base = sum of its track's packets
+//   k_decide        one lane per DownTrack, serial over its track's packets:
+//                   the per-packet recurrence of DownTrack.WriteRTP
+//                   (downtrack.go:680-760) = Forwarder.GetTranslationParams
+//                   (forwarder.go:1436-1765) + RTPMunger (rtpmunger.go) +
+//                   Simulcast/VP8-temporal selectors + VP8 munger
+//                   (codecmunger/vp8.go) + sequencer.push (sequencer.go:123)
+//                   -> compact per-DownTrack Tuple records
+//   scan (output)   per DownTrack record base + byte base (16-B aligned wire
+//                   packets, DownTrack-major)
+//   k_emit          flat 16-B chunk sweep over the output arena: RTP header +
+//                   extension block + munged VP8 descriptor from LDS, payload
+//                   copied byte-shifted from the input arena (coalesced
+//                   dwordx4 loads/stores); one lkf_out record per tuple.
+//
+// No MFMA: nothing here is a contraction.  The emit kernel is HBM-bound
+// (writes ~ out bytes, input payload re-reads served from L2/MALL).
+#include <hip/hip_runtime.h>
+
+#include "../../include/lkfwd.h"
+#include "fwd_state.h"
+#include "kernels.h"
+
+namespace lkf {
+
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+using i32 = int32_t;
+using i64 = int64_t;
+
+constexpr u64 HALF64 = 1ull << 63;
+constexpr i32 INVALID = -1;
+
+// ---------------------------------------------------------------------------
+// Packet view (lkf_pkt, 64 B) loaded with 4 x 16-B loads.
+// ---------------------------------------------------------------------------
+struct PktV {
+  u64 esn, ets;
+  i64 arr;
+  u32 arenaOff, ssrc;
+  u16 poff, plen;
+  u8 hdr0, hdr1, flags, vfirst, vbits, vhs, tl0, tid, keyidx;
+  int8_t spatial, temporal, layer;
+  u16 pid;
+};
+
+__device__ __forceinline__ PktV load_pkt(const lkf_pkt *p) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  PktV v;
+  v.esn = (u64(a.y) << 32) | a.x;
+  v.ets = (u64(a.w) << 32) | a.z;
+  v.arr = i64((u64(b.y) << 32) | b.x);
+  v.arenaOff = b.z;
+  // b.w = track
+  v.ssrc = c.x;
+  v.poff = u16(c.y & 0xffff);
+  v.plen = u16(c.y >> 16);
+  v.hdr0 = u8(c.z);
+  v.hdr1 = u8(c.z >> 8);
+  v.spatial = int8_t(c.z >> 16);
+  v.temporal = int8_t(c.z >> 24);
+  v.flags = u8(c.w);
+  v.vfirst = u8(c.w >> 8);
+  v.vbits = u8(c.w >> 16);
+  v.vhs = u8(c.w >> 24);
+  v.pid = u16(d.x & 0xffff);
+  v.tl0 = u8(d.x >> 16);
+  v.tid = u8(d.x >> 24);
+  v.keyidx = u8(d.y);
+  v.layer = int8_t(d.y >> 8);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Lane context: hot state in registers + cold-state pointers.
+// ---------------------------------------------------------------------------
+struct Lane {
+  DTHot h;
+  RangeEntry *rm;
+  VP8Cold *vc;
+  SeqMeta *seq;
+  u32 seqSize;
+  // track
+  u32 kind, codec, hasRefTS, clockRate;
+  const u32 *offs;
+  // static DT
+  u8 extPlayout, extAbs;
+};
+
+__device__ __forceinline__ bool hasf(const Lane &L, u32 f) { return (L.h.flags & f) != 0; }
+__device__ __forceinline__ void setf(Lane &L, u32 f, bool v) {
+  if (v)
+    L.h.flags |= f;
+  else
+    L.h.flags &= ~f;
+}
+
+// ---- utils.RangeMap<u64,u64>(100): open range in registers, closed ring --
+__device__ __forceinline__ RangeEntry rm_at(const Lane &L, int i) {  // i-th closed range (oldest = 0)
+  int idx = (int(L.h.rmHead) + i) % kRangeCap;
+  return L.rm[idx];
+}
+// ClearAndResetValue rangemap.go:66
+__device__ __forceinline__ void rm_reset(Lane &L, u64 start, u64 val) {
+  L.h.rmHead = 0;
+  L.h.rmCount = 0;
+  L.h.rmOpenStart = start;
+  L.h.rmOpenValue = val;
+}
+// ExcludeRange rangemap.go:100-132
+__device__ bool rm_exclude(Lane &L, u64 s, u64 e) {
+  if (e == s || (e - s) > HALF64) return false;
+  if (L.h.rmOpenStart > s) return false;
+  u64 nv = L.h.rmOpenValue + (e - s);
+  if (L.h.rmOpenStart == s) {
+    L.h.rmOpenStart = e;
+    L.h.rmOpenValue = nv;
+    return true;
+  }
+  RangeEntry c;
+  c.start = L.h.rmOpenStart;
+  c.end = s - 1;
+  c.value = L.h.rmOpenValue;
+  if (L.h.rmCount < kRangeCap) {
+    int idx = (int(L.h.rmHead) + int(L.h.rmCount)) % kRangeCap;
+    L.rm[idx] = c;
+    L.h.rmCount++;
+  } else {  // prune rangemap.go:171: keep the newest size+1 (100 closed + open)
+    L.rm[L.h.rmHead] = c;
+    L.h.rmHead = u16((L.h.rmHead + 1) % kRangeCap);
+  }
+  L.h.rmOpenStart = e;
+  L.h.rmOpenValue = nv;
+  return true;
+}
+// GetValue rangemap.go:134-169 -> true on success
+__device__ bool rm_get(const Lane &L, u64 key, u64 &out) {
+  out = 0;
+  if (key >= L.h.rmOpenStart) {
+    out = L.h.rmOpenValue;
+    return true;
+  }
+  const int nc = L.h.rmCount;
+  u64 firstStart = nc > 0 ? rm_at(L, 0).start : L.h.rmOpenStart;
+  if (key < firstStart) return false;
+  // idx = n-1 (open): only the exclusion test against the newest closed range
+  RangeEntry next;  // rv for the exclusion test
+  next.start = L.h.rmOpenStart;
+  for (int idx = nc; idx >= 0; idx--) {
+    if (idx != nc) {
+      RangeEntry rv = next;
+      if ((key - rv.start) < HALF64 && (rv.end - key) < HALF64) {
+        out = rv.value;
+        return true;
+      }
+    }
+    if (idx > 0) {
+      RangeEntry prev = rm_at(L, idx - 1);
+      u64 before = key - prev.end;
+      u64 after = next.start - key;
+      if (before > 0 && before < HALF64 && after > 0 && after < HALF64) return false;
+      next = prev;
+    }
+  }
+  return false;
+}
+
+// ---- RTPMunger (rtpmunger.go) ---------------------------------------------
+__device__ __forceinline__ void mg_updateSnOffset(Lane &L) {  // :352-358
+  u64 v = 0;
+  rm_get(L, L.h.extHighestIncomingSN + 1, v);
+  L.h.snOffset = v;
+}
+__device__ __forceinline__ void mg_setLastSnTs(Lane &L, u64 esn, u64 ets) {  // :135-145
+  L.h.extHighestIncomingSN = esn - 1;
+  L.h.extLastSN = esn;
+  L.h.extSecondLastSN = esn - 1;
+  rm_reset(L, esn, 0);
+  mg_updateSnOffset(L);
+  L.h.extLastTS = ets;
+  L.h.extSecondLastTS = ets;
+}
+__device__ __forceinline__ void mg_updateSnTsOffsets(Lane &L, u64 esn, u64 ets, u64 snAdj, u64 tsAdj) {  // :147
+  L.h.extHighestIncomingSN = esn - 1;
+  rm_reset(L, esn, esn - L.h.extLastSN - snAdj);
+  mg_updateSnOffset(L);
+  L.h.tsOffset = ets - L.h.extLastTS - tsAdj;
+}
+__device__ __forceinline__ void mg_packetDropped(Lane &L, u64 esn) {  // :156-181
+  if (L.h.extHighestIncomingSN != esn) return;
+  rm_exclude(L, L.h.extHighestIncomingSN, L.h.extHighestIncomingSN + 1);
+  L.h.extLastSN = L.h.extSecondLastSN;
+  mg_updateSnOffset(L);
+  L.h.extLastTS = L.h.extSecondLastTS;
+  setf(L, F_LAST_MARKER, hasf(L, F_SECOND_LAST_MARKER));
+}
+enum { ORD_CONTIG = 0, ORD_OOO = 1, ORD_GAP = 2, ORD_DUP = 3 };
+enum { MG_OK = 0, MG_PADDING, MG_DUP, MG_OOO_MISS };
+// UpdateAndGetSnTs :183-271
+__device__ int mg_update(Lane &L, const PktV &p, bool marker, int &ord, u64 &osn, u64 &ots) {
+  i64 diff = i64(p.esn - L.h.extHighestIncomingSN);
+  if ((diff == 1 && p.plen != 0) || diff > 1) {
+    L.h.extHighestIncomingSN = p.esn;
+    ord = diff > 1 ? ORD_GAP : ORD_CONTIG;
+    u64 msn = p.esn - L.h.snOffset;
+    u64 mts = p.ets - L.h.tsOffset;
+    L.h.extSecondLastSN = L.h.extLastSN;
+    L.h.extLastSN = msn;
+    L.h.extSecondLastTS = L.h.extLastTS;
+    L.h.extLastTS = mts;
+    setf(L, F_SECOND_LAST_MARKER, hasf(L, F_LAST_MARKER));
+    setf(L, F_LAST_MARKER, marker);
+    if (p.flags & LKF_PKT_KEYFRAME) {
+      L.h.extRtxGateSn = msn;
+      setf(L, F_RTX_GATE, true);
+    }
+    if (hasf(L, F_RTX_GATE) && (msn - L.h.extRtxGateSn) > 2000) setf(L, F_RTX_GATE, false);
+    osn = msn;
+    ots = mts;
+    return MG_OK;
+  }
+  if (diff < 0) {
+    ord = ORD_OOO;
+    u64 off = 0;
+    if (!rm_get(L, p.esn, off)) return MG_OOO_MISS;
+    u64 esn = p.esn - off;
+    if (esn >= L.h.extLastSN) return MG_OOO_MISS;
+    osn = esn;
+    ots = p.ets - L.h.tsOffset;
+    return MG_OK;
+  }
+  if (diff == 1) {
+    L.h.extHighestIncomingSN = p.esn;
+    rm_exclude(L, L.h.extHighestIncomingSN, L.h.extHighestIncomingSN + 1);
+    mg_updateSnOffset(L);
+    ord = ORD_CONTIG;
+    return MG_PADDING;
+  }
+  ord = ORD_DUP;
+  return MG_DUP;
+}
+
+// ---- VP8 munger rings (elliotchance/orderedmap semantics) ------------------
+__device__ __forceinline__ int miss_find(const Lane &L, i32 key) {
+  for (int i = 0; i < L.h.missCount; i++) {
+    int idx = (L.h.missHead + i) % kMissCap;
+    if (L.vc->missKey[idx] == key) return idx;
+  }
+  return -1;
+}
+__device__ __forceinline__ bool set_has(const i32 *keys, u8 head, u8 count, i32 key) {
+  for (int i = 0; i < count; i++)
+    if (keys[(head + i) % kSetCap] == key) return true;
+  return false;
+}
+// Set(key,true) then trim to `keep` (vp8.go:242-247, :257-262)
+__device__ __forceinline__ void set_add(i32 *keys, u8 &head, u8 &count, i32 key, int keep) {
+  if (set_has(keys, head, count, key)) return;
+  keys[(head + count) % kSetCap] = key;
+  count++;
+  while (count > keep) {
+    head = u8((head + 1) % kSetCap);
+    count--;
+  }
+}
+__device__ __forceinline__ bool dropped_has(const Lane &L, i32 key) {
+  return set_has(L.vc->dropKey, L.h.dropHead, L.h.dropCount, key);
+}
+
+// The missing-picture loop of vp8.go:218-235, exact:
+//   for lost in [prevMax, ext]: if !dropped(lost): missing.Set(lost, off)
+//   trim missing to the newest 50.
+// Equivalent bounded form: existing entries in range are updated in place;
+// of the new keys only the newest 50 can survive the trim, appended in order.
+__device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
+  if (ext < prevMax) return;
+  const int e0 = L.h.missCount;
+  int inE = 0;  // existing (not dropped) keys inside the range
+  for (int i = 0; i < e0; i++) {
+    int idx = (L.h.missHead + i) % kMissCap;
+    i32 k = L.vc->missKey[idx];
+    if (k >= prevMax && k <= ext && !dropped_has(L, k)) {
+      L.vc->missVal[idx] = off;
+      inE++;
+    }
+  }
+  int nDrop = 0;
+  for (int i = 0; i < L.h.dropCount; i++) {
+    i32 k = L.vc->dropKey[(L.h.dropHead + i) % kSetCap];
+    if (k >= prevMax && k <= ext) nDrop++;
+  }
+  i64 nNew = i64(ext) - i64(prevMax) + 1 - nDrop - inE;
+  if (nNew <= 0) return;
+  int want = nNew > kMissKeep ? kMissKeep : int(nNew);
+  // find the start key s: walking down from ext, the want-th new key
+  i32 s = ext;
+  int got = 0;
+  for (i32 k = ext;; k--) {
+    if (!dropped_has(L, k) && miss_find(L, k) < 0) {
+      got++;
+      if (got == want) {
+        s = k;
+        break;
+      }
+    }
+    if (k == prevMax) break;
+  }
+  // append new keys in [s, ext] in order (before trimming, E intact)
+  for (i32 k = s;; k++) {
+    if (!dropped_has(L, k) && miss_find(L, k) < 0) {
+      int idx = (L.h.missHead + L.h.missCount) % kMissCap;
+      L.vc->missKey[idx] = k;
+      L.vc->missVal[idx] = off;
+      L.h.missCount++;
+    }
+    if (k == ext) break;
+  }
+  while (L.h.missCount > kMissKeep) {
+    L.h.missHead = u8((L.h.missHead + 1) % kMissCap);
+    L.h.missCount--;
+  }
+}
+
+// VP8PictureIdWrapHandler.Unwrap vp8.go:400-483
+__device__ __forceinline__ i32 wr_unwrap(Lane &L, u16 pictureId, bool mBit) {
+  i32 mp = L.h.wrMaxPictureId;
+  bool maxM = hasf(L, F_WR_MAX_MBIT);
+  if (mp > 0) mp = maxM ? (L.h.wrMaxPictureId & 0x7fff) : (L.h.wrMaxPictureId & 0x7f);
+  i32 np = mBit ? i32(pictureId & 0x7fff) : i32(pictureId & 0x7f);
+  if (L.h.wrTotalWrap > 0) {
+    if ((L.h.wrMaxPictureId + (L.h.wrLastWrap >> 1)) < (np + L.h.wrTotalWrap))
+      return np + L.h.wrTotalWrap - L.h.wrLastWrap;
+  }
+  i32 wrap = 0;
+  if (maxM) {
+    if (np < mp && (mp - np) > (1 << 14)) wrap = 1 << 15;
+  } else {
+    if (np < mp && (mp - np) > (1 << 6)) wrap = 1 << 7;
+  }
+  L.h.wrTotalWrap += wrap;
+  if (wrap != 0) L.h.wrLastWrap = wrap;
+  return np + L.h.wrTotalWrap;
+}
+__device__ __forceinline__ void wr_init(Lane &L, i32 ext, bool m) {
+  L.h.wrMaxPictureId = ext;
+  setf(L, F_WR_MAX_MBIT, m);
+  L.h.wrTotalWrap = 0;
+  L.h.wrLastWrap = 0;
+}
+
+// buffer.VP8.MarshalTo helpers.go:170-227 into out[0..6); returns HeaderSize
+// written (or -1 if the fields need more than hs bytes: Go would panic).
+__device__ int vp8_marshal(u8 first, bool I, bool M, u16 pid, bool Lb, u8 tl0, bool T, u8 tid, bool Y, bool K,
+                           u8 keyidx, int hs, u8 *out) {
+  if (hs < 1 || hs > 6) return -1;
+  for (int i = 0; i < 6; i++) out[i] = 0;
+  int idx = 0;
+  out[0] = first;
+  if (I || Lb || T || K) {
+    out[0] |= 0x80;
+    idx++;
+    int xpos = idx;
+    u8 xval = 0;
+    idx++;
+    if (I) {
+      xval |= 0x80;
+      if (M) {
+        if (idx + 1 >= hs) return -1;
+        out[idx] = u8(0x80 | ((pid >> 8) & 0x7f));
+        out[idx + 1] = u8(pid & 0xff);
+        idx += 2;
+      } else {
+        if (idx >= hs) return -1;
+        out[idx] = u8(pid);
+        idx++;
+      }
+    }
+    if (Lb) {
+      xval |= 0x40;
+      if (idx >= hs) return -1;
+      out[idx] = tl0;
+      idx++;
+    }
+    if (T || K) {
+      if (idx >= hs) return -1;
+      out[idx] = 0;
+      if (T) {
+        xval |= 0x20;
+        out[idx] = u8(tid << 6);
+        if (Y) out[idx] |= 0x20;
+      }
+      if (K) {
+        xval |= 0x10;
+        out[idx] |= keyidx & 0x1f;
+      }
+      idx++;
+    }
+    if (xpos >= hs) return -1;
+    out[xpos] = xval;
+  } else {
+    out[0] &= u8(~0x80);
+  }
+  return hs;
+}
+
+enum { CM_OK = 0, CM_FILTERED, CM_PICID_MISS, CM_ERR };
+// VP8.UpdateAndGet vp8.go:161-302
+__device__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool gap, i32 maxTL, u8 *cb, int &cbLen) {
+  const bool I = p.vbits & LKF_VP8_I, M = p.vbits & LKF_VP8_M, Lb = p.vbits & LKF_VP8_L;
+  const bool T = p.vbits & LKF_VP8_T, Y = p.vbits & LKF_VP8_Y, K = p.vbits & LKF_VP8_K;
+  i32 ext = wr_unwrap(L, p.pid, M);
+  if (ooo) {
+    int idx = miss_find(L, ext);
+    if (idx < 0) return CM_PICID_MISS;
+    i32 off = L.vc->missVal[idx];
+    u16 mpid = u16((ext - off) & 0x7fff);
+    bool mM = mpid > 127;
+    int hs = int(p.vhs) + (mM == M ? 0 : (mM ? 1 : -1));
+    cbLen = vp8_marshal(p.vfirst, I, mM, mpid, Lb, u8(p.tl0 - L.h.tl0Off), T, p.tid, Y, K,
+                        u8(p.keyidx - L.h.keyIdxOff), hs, cb);
+    return cbLen < 0 ? CM_ERR : CM_OK;
+  }
+  i32 prevMax = L.h.wrMaxPictureId;
+  L.h.wrMaxPictureId = ext;  // UpdateMaxPictureId
+  setf(L, F_WR_MAX_MBIT, M);
+  if (gap) {
+    vp8_record_missing(L, prevMax, ext, L.h.pictureIdOffset);
+    if (T && p.tid > u8(maxTL)) set_add(L.vc->exKey, L.h.exHead, L.h.exCount, ext, kExemptKeep);
+  } else {
+    if (T && p.tid > u8(maxTL)) {
+      if (!set_has(L.vc->exKey, L.h.exHead, L.h.exCount, ext)) {
+        if (I && prevMax != ext) {
+          set_add(L.vc->dropKey, L.h.dropHead, L.h.dropCount, ext, kDropKeep);
+          L.h.pictureIdOffset += 1;
+        }
+        return CM_FILTERED;
+      }
+    }
+  }
+  i32 mext = ext - L.h.pictureIdOffset;
+  u16 mpid = u16(mext & 0x7fff);
+  u8 mtl0 = u8(p.tl0 - L.h.tl0Off);
+  u8 mkey = u8((p.keyidx - L.h.keyIdxOff) & 0x1f);
+  L.h.extLastPictureId = mext;
+  L.h.lastTl0 = mtl0;
+  L.h.lastKeyIdx = mkey;
+  bool mM = mpid > 127;
+  int hs = int(p.vhs) + (mM == M ? 0 : (mM ? 1 : -1));
+  cbLen = vp8_marshal(p.vfirst, I, mM, mpid, Lb, mtl0, T, p.tid, Y, K, mkey, hs, cb);
+  return cbLen < 0 ? CM_ERR : CM_OK;
+}
+// VP8.SetLast vp8.go:111-134
+__device__ void vp8_setLast(Lane &L, const PktV &p) {
+  if (!(p.flags & LKF_PKT_VP8)) return;
+  bool I = p.vbits & LKF_VP8_I;
+  setf(L, F_PICID_USED, I);
+  if (I) {
+    wr_init(L, i32(p.pid) - 1, p.vbits & LKF_VP8_M);
+    L.h.extLastPictureId = i32(p.pid);
+  }
+  bool Lb = p.vbits & LKF_VP8_L;
+  setf(L, F_TL0_USED, Lb);
+  if (Lb) L.h.lastTl0 = p.tl0;
+  setf(L, F_TID_USED, p.vbits & LKF_VP8_T);
+  bool K = p.vbits & LKF_VP8_K;
+  setf(L, F_KEYIDX_USED, K);
+  if (K) L.h.lastKeyIdx = p.keyidx;
+}
+// VP8.UpdateOffsets vp8.go:136-159
+__device__ void vp8_updateOffsets(Lane &L, const PktV &p) {
+  if (!(p.flags & LKF_PKT_VP8)) return;
+  if (hasf(L, F_PICID_USED)) {
+    wr_init(L, i32(p.pid) - 1, p.vbits & LKF_VP8_M);
+    L.h.pictureIdOffset = i32(p.pid) - L.h.extLastPictureId - 1;
+  }
+  if (hasf(L, F_TL0_USED)) L.h.tl0Off = u8(p.tl0 - L.h.lastTl0 - 1);
+  if (hasf(L, F_KEYIDX_USED)) L.h.keyIdxOff = u8((p.keyidx - L.h.lastKeyIdx - 1) & 0x1f);
+  L.h.missHead = L.h.missCount = 0;
+  L.h.dropHead = L.h.dropCount = 0;
+  L.h.exHead = L.h.exCount = 0;
+}
+
+// ---- Forwarder control (forwarder.go) --------------------------------------
+__device__ __forceinline__ void fw_resync(Lane &L) {  // :1391-1397
+  L.h.curS = INVALID;
+  L.h.curT = INVALID;
+  L.h.lastSSRC = 0;
+  if (hasf(L, F_PUBMUTED)) setf(L, F_RESUME_BEHIND, true);
+}
+__device__ void apply_ctl(Lane &L, const DevEvent &ev) {
+  const bool video = hasf(L, F_VIDEO);
+  switch (ev.op) {
+    case LKF_CTL_MUTE: {  // :377-413
+      bool m = ev.a[0] != 0;
+      if (hasf(L, F_MUTED) == m) break;
+      if (m && ev.a[1] == 0) break;
+      setf(L, F_MUTED, m);
+      if (m) fw_resync(L);
+      break;
+    }
+    case LKF_CTL_PUBMUTE: {  // :422-438
+      bool m = ev.a[0] != 0;
+      if (hasf(L, F_PUBMUTED) == m) break;
+      setf(L, F_PUBMUTED, m);
+      if (m) fw_resync(L);
+      break;
+    }
+    case LKF_CTL_SET_MAX_SPATIAL:  // :454-470
+      if (video && i32(ev.a[0]) != L.h.maxS) L.h.maxS = i32(ev.a[0]);
+      break;
+    case LKF_CTL_SET_MAX_TEMPORAL:  // :472-488
+      if (video && i32(ev.a[0]) != L.h.maxT) L.h.maxT = i32(ev.a[0]);
+      break;
+    case LKF_CTL_SET_MAX_SEEN_SPATIAL:  // :241-253
+      if (i32(ev.a[0]) > L.h.seenS) L.h.seenS = i32(ev.a[0]);
+      break;
+    case LKF_CTL_SET_MAX_SEEN_TEMPORAL:  // :255-267
+      if (i32(ev.a[0]) > L.h.seenT) L.h.seenT = i32(ev.a[0]);
+      break;
+    case LKF_CTL_SET_ALLOCATION: {  // updateAllocation :1353-1382
+      if (!video) break;
+      i32 ts = i32(ev.a[0]), tt = i32(ev.a[1]);
+      bool valid = ts != INVALID && tt != INVALID;
+      if (valid && L.codec == LKF_CODEC_H264) tt = 0;
+      setf(L, F_DEFICIENT, ev.a[3] != 0);
+      L.h.ptgtS = ts;
+      L.h.ptgtT = tt;
+      L.h.tgtS = ts;
+      L.h.tgtT = tt;
+      L.h.reqS = valid ? i32(ev.a[2]) : INVALID;
+      if (!valid) fw_resync(L);
+      break;
+    }
+    case LKF_CTL_RESYNC:
+      fw_resync(L);
+      break;
+    case LKF_CTL_SET_TARGET:
+      L.h.ptgtS = L.h.tgtS = i32(ev.a[0]);
+      L.h.ptgtT = L.h.tgtT = i32(ev.a[1]);
+      break;
+    case LKF_CTL_PLAYOUT_ACKED:
+      setf(L, F_PLAYOUT_ACKED, ev.a[0] != 0);
+      break;
+    default:
+      break;
+  }
+}
+
+// processSourceSwitch forwarder.go:1456-1647 on the virtual clock (now = arrival)
+__device__ bool fw_sourceSwitch(Lane &L, const PktV &p, i32 layer) {
+  if (!hasf(L, F_STARTED)) {
+    setf(L, F_STARTED, true);
+    L.h.referenceLayerSpatial = layer;
+    mg_setLastSnTs(L, p.esn, p.ets);
+    if (hasf(L, F_VP8)) vp8_setLast(L, p);
+    return true;
+  } else if (L.h.referenceLayerSpatial == INVALID) {
+    L.h.referenceLayerSpatial = layer;
+  }
+  const u64 extLastTS = L.h.extLastTS;
+  u64 extExpectedTS = extLastTS;
+  u64 extRefTS = extExpectedTS;
+  if (L.hasRefTS) {  // StreamTrackerManager.GetReferenceLayerRTPTimestamp :660-679
+    i32 ref = L.h.referenceLayerSpatial;
+    if (layer < 0 || layer >= 3 || ref < 0 || ref >= 3) return false;
+    u32 off = L.offs[ref * 3 + layer];
+    if (layer != ref && off == 0) return false;
+    u32 ts = u32(p.ets) + off;
+    extRefTS = (extRefTS & 0xFFFFFFFF00000000ull) + u64(ts);
+    u32 e32 = u32(extExpectedTS);
+    if (u32(ts - e32) < (1u << 31) && ts < e32) extRefTS += (1ull << 32);
+    if (u32(e32 - ts) < (1u << 31) && e32 < ts && extRefTS >= (1ull << 32)) extRefTS -= (1ull << 32);
+  }
+  if (hasf(L, F_HAS_EXPECTED)) {  // DownTrack.getExpectedRTPTimestamp downtrack.go:1765
+    if (hasf(L, F_STATS_INIT)) {
+      i64 diff = (p.arr - L.h.statsFirstTime) * i64(L.clockRate) / 1000000000LL;
+      extExpectedTS = L.h.statsExtStartTS + u64(diff);
+    } else if (L.h.preStartTime != 0) {
+      i64 since = p.arr - L.h.preStartTime;
+      u64 rtpDiff = u64(since * i64(L.clockRate) / 1000000000LL);
+      extExpectedTS = L.h.extFirstTS + rtpDiff;
+      if (L.h.refTSOffset == 0) L.h.refTSOffset = extExpectedTS - extRefTS;
+    }
+  }
+  extRefTS += L.h.refTSOffset;
+  u64 extNextTS;
+  const double cr = double(L.clockRate);
+  if (L.h.lastSSRC == 0) {
+    double diffSeconds = double(i64(extExpectedTS - extRefTS)) / cr;
+    if (diffSeconds >= 0.0) {
+      if (hasf(L, F_RESUME_BEHIND) && diffSeconds > 0.2)
+        extNextTS = extExpectedTS;
+      else if (diffSeconds > 2.0)
+        extNextTS = extExpectedTS;
+      else
+        extNextTS = extRefTS;
+    } else {
+      extNextTS = extRefTS;
+    }
+    setf(L, F_RESUME_BEHIND, false);
+  } else {
+    double diffSeconds = double(i64(extRefTS - extLastTS)) / cr;
+    if (diffSeconds < 0.0) {
+      if (fabs(diffSeconds) > 0.05) return false;
+      extNextTS = extLastTS + 1;
+    } else {
+      extNextTS = extRefTS;
+    }
+  }
+  if (i64(extNextTS - extLastTS) <= 0) extNextTS = extLastTS + 1;
+  mg_updateSnTsOffsets(L, p.esn, p.ets, 1, extNextTS - extLastTS);
+  if (hasf(L, F_VP8)) vp8_updateOffsets(L, p);
+  return true;
+}
+
+// getTranslationParamsCommon :1650-1671 -> drop reason or -1 (forward)
+__device__ __forceinline__ int fw_common(Lane &L, const PktV &p, i32 layer, bool marker, int &ord, u64 &osn,
+                                         u64 &ots) {
+  if (L.h.lastSSRC != p.ssrc) {
+    if (!fw_sourceSwitch(L, p, layer)) return LKF_DROP_SWITCH;
+    L.h.lastSSRC = p.ssrc;
+  }
+  int r = mg_update(L, p, marker, ord, osn, ots);
+  if (r == MG_PADDING) return LKF_DROP_PADDING;
+  if (r == MG_DUP) return LKF_DROP_DUPLICATE;
+  if (r == MG_OOO_MISS) return LKF_DROP_OOO_MISS;
+  return -1;
+}
+
+__device__ __forceinline__ void vls_rollback(Lane &L) {  // base.go Rollback
+  L.h.curS = L.h.prevS;
+  L.h.curT = L.h.prevT;
+  L.h.tgtS = L.h.ptgtS;
+  L.h.tgtT = L.h.ptgtT;
+}
+
+struct Fwd {
+  int ord;
+  u64 osn, ots;
+  bool switching, resuming, marker;
+  int cbLen;
+  u8 cb[6];
+};
+
+// Forwarder.GetTranslationParams forwarder.go:1436-1765 for one (packet, DownTrack).
+__device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
+  o.switching = o.resuming = o.marker = false;
+  o.cbLen = 0;
+  const i32 layer = p.layer;
+  if (hasf(L, F_MUTED) || hasf(L, F_PUBMUTED)) return LKF_DROP_MUTED;
+  if (!hasf(L, F_VIDEO)) return fw_common(L, p, layer, false, o.ord, o.osn, o.ots);
+  // ---- video :1679-1765
+  if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) return LKF_DROP_PAUSED;
+  // vls.Select: Simulcast simulcast.go:42-122 (Null selector: never selected)
+  bool isSelected = false, isSwitching = false, isResuming = false;
+  const bool kf = p.flags & LKF_PKT_KEYFRAME;
+  const bool pktMarker = p.hdr1 & 0x80;
+  if (hasf(L, F_SIMULCAST)) {
+    if (L.h.curS != L.h.tgtS) {
+      bool isActive = L.h.curS != INVALID && L.h.curT != INVALID;
+      bool found = false;
+      if (kf) {
+        if (layer > L.h.curS && layer <= L.h.tgtS) found = true;
+        if (layer < L.h.curS && layer >= L.h.tgtS) found = true;
+      }
+      if (found) {
+        L.h.prevS = L.h.curS;
+        L.h.prevT = L.h.curT;
+        L.h.curS = layer;
+        L.h.curT = p.temporal;
+        L.h.ptgtS = L.h.tgtS;
+        L.h.ptgtT = L.h.tgtT;
+        if (L.h.curS >= L.h.maxS || L.h.curS == L.h.seenS) L.h.tgtS = L.h.curS;
+        isSwitching = true;
+        if (!isActive) isResuming = true;
+      }
+    }
+    if (L.h.curS > L.h.maxS && layer <= L.h.maxS && kf) {
+      L.h.prevS = L.h.curS;
+      L.h.prevT = L.h.curT;
+      L.h.curS = layer;
+      L.h.ptgtS = L.h.tgtS;
+      L.h.ptgtT = L.h.tgtT;
+      if (L.h.curS >= L.h.maxS || L.h.curS == L.h.seenS) L.h.tgtS = layer;
+      isSwitching = true;
+    }
+    isSelected = layer == L.h.curS;
+  }
+  if (!isSelected) return LKF_DROP_NOT_SELECTED;  // IsRelevant == false for Simulcast
+  o.resuming = isResuming;
+  o.switching = isSwitching;
+  o.marker = pktMarker;
+  if (hasf(L, F_DEFICIENT) && L.h.tgtS < L.h.curS) {  // FlagPauseOnDowngrade :1709
+    if (isSwitching) vls_rollback(L);
+    return LKF_DROP_DOWNGRADE;
+  }
+  int dr = fw_common(L, p, layer, pktMarker, o.ord, o.osn, o.ots);
+  if (dr >= 0 || p.plen == 0) {
+    if (isSwitching) vls_rollback(L);
+    return dr;
+  }
+  // vls.SelectTemporal base.go:143-168 + temporallayerselector/vp8.go:32-56
+  i32 tl = L.h.curT;
+  bool tSwitch = false;
+  if (hasf(L, F_TLS_VP8)) {
+    i32 cur = L.h.curT, tgt = L.h.tgtT, nxt = cur;
+    if (cur != tgt && (p.flags & LKF_PKT_VP8) && (p.vbits & LKF_VP8_T)) {
+      i32 tid = i32(p.tid);
+      if (cur < tgt) {
+        if (tid > cur && tid <= tgt && (p.vbits & LKF_VP8_S) && (p.vbits & LKF_VP8_Y)) {
+          tl = tid;
+          nxt = tid;
+        }
+      } else if (pktMarker) {
+        nxt = tgt;
+      }
+    }
+    if (nxt != L.h.curT) {
+      tSwitch = true;
+      L.h.prevS = L.h.curS;
+      L.h.prevT = L.h.curT;
+      L.h.curT = nxt;
+    }
+  }
+  if (hasf(L, F_VP8)) {
+    int cr;
+    if (!(p.flags & LKF_PKT_VP8))
+      cr = CM_ERR;  // ErrNotVP8
+    else
+      cr = vp8_update(L, p, o.ord == ORD_OOO, o.ord == ORD_GAP, tl, o.cb, o.cbLen);
+    if (cr != CM_OK) {
+      if (cr == CM_FILTERED) mg_packetDropped(L, p.esn);
+      if (isSwitching || tSwitch) vls_rollback(L);
+      return cr == CM_FILTERED ? LKF_DROP_TEMPORAL : cr == CM_PICID_MISS ? LKF_DROP_PICID_MISS : LKF_DROP_OTHER;
+    }
+  }
+  return -1;
+}
+
+// sequencer.push sequencer.go:123-209 (no padding exclusions on this path: the
+// sequencer's RangeMap stays at value 0, so slot = extModifiedSN % size)
+__device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, const u8 *cb,
+                         int cbLen) {
+  if (!hasf(L, F_SEQ_INIT)) {
+    setf(L, F_SEQ_INIT, true);
+    L.h.seqExtStartSN = esn;
+    L.h.seqExtHighestSN = esn;
+    L.h.seqExtHighestTS = ets;
+  }
+  if (esn < L.h.seqExtStartSN) return;
+  const u64 adjH = L.h.seqExtHighestSN;
+  const u64 adjM = esn;
+  const u64 size = L.seqSize;
+  if (i64(adjM - adjH) <= -i64(size)) return;
+  if (adjM > adjH) {
+    u64 n = 0;
+    for (u64 x = adjH + 1; x != adjM; x++) {
+      SeqMeta z = {};
+      L.seq[x % size] = z;
+      if (++n >= size) break;
+    }
+  }
+  SeqMeta m = {};
+  m.sourceSeqNo = u16(inSN);
+  m.targetSeqNo = u16(esn);
+  m.timestamp = u32(ets);
+  m.lastNack = u32(arrMs - L.h.seqStartMs);
+  m.marker = marker;
+  m.nacked = 0;
+  m.layer = layer;
+  m.codecLen = u8(cbLen);
+  for (int i = 0; i < 6; i++) m.codec[i] = i < cbLen ? cb[i] : 0;
+  L.seq[adjM % size] = m;
+  if (esn > L.h.seqExtHighestSN) L.h.seqExtHighestSN = esn;
+  if (ets > L.h.seqExtHighestTS) L.h.seqExtHighestTS = ets;
+}
+
+__device__ __forceinline__ u64 wave_sum(u64 v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// k_track_ranges: packets grouped by track -> [begin, end) (+ grouping check)
+// ---------------------------------------------------------------------------
+__global__ void k_track_ranges(const lkf_pkt *__restrict__ pkts, u32 n, u32 ntracks, u32 *__restrict__ tBegin,
+                               u32 *__restrict__ tEnd, u32 *__restrict__ tRuns, u32 *__restrict__ err) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  u32 t = pkts[i].track;
+  if (t >= ntracks) {
+    atomicOr(err, 1u);
+    return;
+  }
+  u32 tp = i > 0 ? pkts[i - 1].track : 0xffffffffu;
+  u32 tn = i + 1 < n ? pkts[i + 1].track : 0xffffffffu;
+  if (tp != t) {
+    tBegin[t] = i;
+    if (atomicAdd(&tRuns[t], 1u) != 0) atomicOr(err, 2u);
+  }
+  if (tn != t) tEnd[t] = i + 1;
+}
+
+// ---------------------------------------------------------------------------
+// Scans (3-phase: block reduce -> top scan -> block rescan with offsets).
+// Value = (a, b) u64 pairs; mode selects how the input is formed.
+// ---------------------------------------------------------------------------
+constexpr int SCAN_T = 256;
+constexpr int SCAN_ITEMS = 4;
+constexpr int SCAN_TILE = SCAN_T * SCAN_ITEMS;
+
+struct ScanIn {
+  int mode;  // 0: slots = npkts(track(d)) if active; 1: (fwdCnt, fwdBytes)
+  const DevDT *dts;
+  const u32 *tBegin, *tEnd;
+  const u32 *cnt;
+  const u64 *bytes;
+};
+
+__device__ __forceinline__ void scan_load(const ScanIn &in, u32 d, u64 &a, u64 &b) {
+  if (in.mode == 0) {
+    DevDT dt = in.dts[d];
+    a = dt.active ? u64(in.tEnd[dt.track] - in.tBegin[dt.track]) : 0;
+    b = 0;
+  } else {
+    a = in.cnt[d];
+    b = in.bytes[d];
+  }
+}
+
+__device__ __forceinline__ void block_scan_excl(u64 &a, u64 &b, u64 &ta, u64 &tb) {
+  // inclusive wave scan
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  u64 ia = a, ib = b;
+  for (int o = 1; o < 64; o <<= 1) {
+    u64 xa = __shfl_up(ia, o, 64), xb = __shfl_up(ib, o, 64);
+    if (lane >= o) {
+      ia += xa;
+      ib += xb;
+    }
+  }
+  __shared__ u64 wa[SCAN_T / 64], wb[SCAN_T / 64];
+  if (lane == 63) {
+    wa[wid] = ia;
+    wb[wid] = ib;
+  }
+  __syncthreads();
+  u64 pa = 0, pb = 0;
+  ta = tb = 0;
+  for (int w = 0; w < SCAN_T / 64; w++) {
+    if (w < wid) {
+      pa += wa[w];
+      pb += wb[w];
+    }
+    ta += wa[w];
+    tb += wb[w];
+  }
+  __syncthreads();
+  a = pa + ia - a;
+  b = pb + ib - b;
+}
+
+__global__ void __launch_bounds__(SCAN_T) k_scan_reduce(ScanIn in, u32 n, u64 *__restrict__ partA,
+                                                        u64 *__restrict__ partB) {
+  u64 sa = 0, sb = 0;
+  u32 base = blockIdx.x * SCAN_TILE;
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    u32 d = base + k * SCAN_T + threadIdx.x;
+    if (d < n) {
+      u64 a, b;
+      scan_load(in, d, a, b);
+      sa += a;
+      sb += b;
+    }
+  }
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  __shared__ u64 ra[SCAN_T / 64], rb[SCAN_T / 64];
+  if ((threadIdx.x & 63) == 0) {
+    ra[threadIdx.x >> 6] = sa;
+    rb[threadIdx.x >> 6] = sb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 ta = 0, tb = 0;
+    for (int w = 0; w < SCAN_T / 64; w++) {
+      ta += ra[w];
+      tb += rb[w];
+    }
+    partA[blockIdx.x] = ta;
+    partB[blockIdx.x] = tb;
+  }
+}
+
+// single block: exclusive scan of nparts partial sums (in place), totals
+__global__ void __launch_bounds__(SCAN_T) k_scan_top(u64 *__restrict__ partA, u64 *__restrict__ partB, u32 nparts,
+                                                     u64 *__restrict__ totA, u64 *__restrict__ totB) {
+  u64 carryA = 0, carryB = 0;
+  for (u32 base = 0; base < nparts; base += SCAN_T) {
+    u32 i = base + threadIdx.x;
+    u64 a = i < nparts ? partA[i] : 0, b = i < nparts ? partB[i] : 0;
+    u64 ta, tb;
+    block_scan_excl(a, b, ta, tb);
+    if (i < nparts) {
+      partA[i] = a + carryA;
+      partB[i] = b + carryB;
+    }
+    carryA += ta;
+    carryB += tb;
+  }
+  if (threadIdx.x == 0) {
+    *totA = carryA;
+    if (totB) *totB = carryB;
+  }
+}
+
+__global__ void __launch_bounds__(SCAN_T) k_scan_down(ScanIn in, u32 n, const u64 *__restrict__ partA,
+                                                      const u64 *__restrict__ partB, u64 *__restrict__ outA,
+                                                      u64 *__restrict__ outB) {
+  u32 base = blockIdx.x * SCAN_TILE;
+  u64 carryA = partA[blockIdx.x], carryB = partB[blockIdx.x];
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    u32 d = base + k * SCAN_T + threadIdx.x;
+    u64 a = 0, b = 0;
+    if (d < n) scan_load(in, d, a, b);
+    u64 ta, tb;
+    block_scan_excl(a, b, ta, tb);
+    if (d < n) {
+      outA[d] = a + carryA;
+      if (outB) outB[d] = b + carryB;
+    }
+    carryA += ta;
+    carryB += tb;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_decide: one lane per DownTrack (lanes ordered by track: the lanes of a
+// wave read the same packet descriptors, broadcast from L1/L2).
+// ---------------------------------------------------------------------------
+struct DecideArgs {
+  const u32 *sched;  // lane -> DownTrack
+  u32 nlanes;
+  DTHot *hot;
+  const DevDT *dts;
+  const DevTrack *tracks;
+  RangeEntry *rm;
+  VP8Cold *vc;
+  SeqMeta *seq;
+  u32 seqSize;
+  const lkf_pkt *pkts;
+  const u32 *tBegin, *tEnd;
+  const u64 *slotBase;
+  Tuple *tuples;
+  u64 tupleCap;
+  u32 *err;
+  const DevEvent *events;
+  const u32 *evOff;  // per lane [evOff[l], evOff[l+1])
+  u32 *fwdCnt;
+  u64 *fwdBytes;
+  u64 *stats;  // lkf_stats as u64[15]
+};
+
+__global__ void __launch_bounds__(64) k_decide(DecideArgs A) {
+  const u32 l = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = l < A.nlanes;
+  u64 nTuples = 0, nFwd = 0, nBytes = 0;
+  u64 drops[LKF_DROP_NREASONS];
+  for (int i = 0; i < LKF_DROP_NREASONS; i++) drops[i] = 0;
+  if (live) {
+    const u32 d = A.sched[l];
+    Lane L;
+    L.h = A.hot[d];
+    L.rm = A.rm + size_t(d) * kRangeCap;
+    L.vc = A.vc + d;
+    L.seq = A.seq + size_t(d) * A.seqSize;
+    L.seqSize = A.seqSize;
+    const DevDT dt = A.dts[d];
+    const DevTrack &tk = A.tracks[dt.track];
+    L.kind = tk.kind;
+    L.codec = tk.codec;
+    L.hasRefTS = tk.hasRefTS;
+    L.clockRate = tk.clockRate;
+    L.offs = tk.layerOffsets;
+    L.extPlayout = dt.extPlayout;
+    L.extAbs = dt.extAbs;
+    const u32 pb = A.tBegin[dt.track];
+    u32 pe = A.tEnd[dt.track];
+    if (A.slotBase[d] + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
+      atomicOr(A.err, 8u);
+      pe = pb;
+    }
+    u32 ev = A.evOff[l];
+    const u32 evEnd = A.evOff[l + 1];
+    Tuple *outT = A.tuples + A.slotBase[d];
+    u32 relOff = 0;
+    for (u32 k = pb; k < pe; k++) {
+      while (ev < evEnd && A.events[ev].at <= k) apply_ctl(L, A.events[ev++]);
+      nTuples++;
+      const PktV p = load_pkt(A.pkts + k);
+      Fwd f;
+      int dr = fw_translate(L, p, f);
+      if (dr >= 0) {
+        drops[dr]++;
+        continue;
+      }
+      // ---- DownTrack.WriteRTP output shape (downtrack.go:693-723, pacer/base.go:71-100)
+      const int cc = p.hdr0 & 0xf;
+      const bool playout = L.extPlayout && !hasf(L, F_PLAYOUT_ACKED);
+      int extBytes = (playout ? 4 : 0) + (L.extAbs ? 4 : 0);  // one-byte profile: 1 + 3 each
+      int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
+      int hdrLen = 12 + 4 * cc + extBlock;
+      const bool useCodec = f.cbLen > 0 && (p.flags & LKF_PKT_VP8);
+      int payLen = useCodec ? (f.cbLen + int(p.plen) - int(p.vhs)) : int(p.plen);
+      const bool marker = f.marker || (p.hdr1 & 0x80);
+      Tuple t;
+      t.extSN = f.osn;
+      t.extTS = f.ots;
+      t.pkt = k;
+      t.relOff = relOff;
+      t.outLen = u16(hdrLen + payLen);
+      t.flags = u8((f.switching ? LKF_OUT_SWITCHING : 0) | (f.resuming ? LKF_OUT_RESUMING : 0) |
+                   ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
+                   (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0));
+      t.layer = p.layer;
+      t.codecLen = u8(f.cbLen);
+      for (int i = 0; i < 6; i++) t.codec[i] = i < f.cbLen ? f.cb[i] : 0;
+      t.hdrLen = u8(hdrLen);
+      for (int i = 0; i < 12; i++) t.pad[i] = 0;
+      outT[nFwd] = t;
+      // sequencer.push (downtrack.go:724-735)
+      seq_push(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
+      // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
+      if (!hasf(L, F_STATS_INIT) && payLen > 0) {
+        setf(L, F_STATS_INIT, true);
+        L.h.statsFirstTime = p.arr;
+        L.h.statsExtStartTS = f.ots;
+      }
+      nFwd++;
+      nBytes += u64(hdrLen + payLen);
+      relOff += u32((hdrLen + payLen + 15) & ~15);
+    }
+    while (ev < evEnd) apply_ctl(L, A.events[ev++]);
+    A.hot[d] = L.h;
+    A.fwdCnt[d] = u32(nFwd);
+    A.fwdBytes[d] = relOff;
+  }
+  // per-wave reduction of counters -> one atomic each
+  u64 v = wave_sum(nTuples);
+  if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)v);
+  v = wave_sum(nFwd);
+  if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)v);
+  v = wave_sum(nBytes);
+  if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[2], (unsigned long long)v);
+  for (int i = 0; i < LKF_DROP_NREASONS; i++) {
+    v = wave_sum(drops[i]);
+    if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[4 + i], (unsigned long long)v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_emit: wire bytes.  A block takes EMIT_G consecutive output records
+// (grid-stride over groups), builds their RTP header + extension block +
+// munged VP8 descriptor ("prefix") in LDS, then sweeps the group's output
+// bytes in 16-B chunks: prefix chunks from LDS, payload chunks as byte-
+// shifted copies of the input packet (two dwordx4 loads + v_alignbyte).
+// ---------------------------------------------------------------------------
+constexpr int EMIT_T = 256;
+constexpr int EMIT_G = 64;
+constexpr int PRE_MAX = 128;
+
+struct EmitArgs {
+  const u64 *recBase;   // [ndts] exclusive scan of forwarded counts
+  const u64 *byteBase;  // [ndts] exclusive scan of output bytes
+  const u64 *slotBase;
+  const u64 *totals;    // [0] records, [1] bytes
+  const Tuple *tuples;
+  const lkf_pkt *pkts;
+  const u8 *arena;
+  const DevDT *dts;
+  u32 ndts;
+  lkf_out *out;
+  u8 *outArena;
+  u64 outCap, outByteCap;
+  u32 *err;
+};
+
+__device__ __forceinline__ u32 align_byte(u32 hi, u32 lo, u32 sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+__device__ __forceinline__ u32 keep_mask(int kb) {  // low kb bytes of a dword
+  return kb >= 4 ? 0xffffffffu : kb <= 0 ? 0u : ((1u << (8 * kb)) - 1);
+}
+
+__global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
+  __shared__ __attribute__((aligned(16))) u8 pre[EMIT_G][PRE_MAX];
+  __shared__ u64 sOff[EMIT_G];
+  __shared__ u64 sSrc[EMIT_G];
+  __shared__ u32 sLen[EMIT_G];
+  __shared__ u32 sPre[EMIT_G];
+  const u64 total = A.totals[0];
+  const u64 ngroups = (total + EMIT_G - 1) / EMIT_G;
+  if (total > A.outCap || A.totals[1] > A.outByteCap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(A.err, 4u);
+    return;
+  }
+  for (u64 g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const u64 r0 = g * EMIT_G;
+    const int nrec = int(min(u64(EMIT_G), total - r0));
+    if (threadIdx.x < nrec) {
+      const u64 r = r0 + threadIdx.x;
+      // DownTrack owning record r: last d with recBase[d] <= r
+      u32 lo = 0, hi = A.ndts;
+      while (hi - lo > 1) {
+        u32 mid = (lo + hi) >> 1;
+        if (A.recBase[mid] <= r)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      const u32 d = lo;
+      const u64 j = r - A.recBase[d];
+      const Tuple t = A.tuples[A.slotBase[d] + j];
+      const lkf_pkt *pp = A.pkts + t.pkt;
+      const PktV p = load_pkt(pp);
+      const DevDT dt = A.dts[d];
+      const u64 outOff = A.byteBase[d] + t.relOff;
+      lkf_out o;
+      o.ext_sn = t.extSN;
+      o.ext_ts = t.extTS;
+      o.out_off = outOff;
+      o.dt = d;
+      o.pkt = t.pkt;
+      o.out_len = t.outLen;
+      o.flags = t.flags & 0x0f;
+      o.layer = t.layer;
+      o.reserved = 0;
+      A.out[r] = o;
+      // prefix: RTP header (getTranslatedRTPHeader downtrack.go:1714-1726)
+      u8 *w = pre[threadIdx.x];
+      const int cc = p.hdr0 & 0xf;
+      const bool playout = t.flags & T_PLAYOUT;
+      const bool hasExt = playout || dt.extAbs;
+      w[0] = u8((p.hdr0 & 0xe0) | (hasExt ? 0x10 : 0) | cc);  // V, P copied; X per new extensions
+      w[1] = u8(((t.flags & LKF_OUT_MARKER) ? 0x80 : 0) | (dt.pt & 0x7f));
+      const u16 sn = u16(t.extSN);
+      const u32 ts = u32(t.extTS);
+      w[2] = u8(sn >> 8);
+      w[3] = u8(sn);
+      w[4] = u8(ts >> 24);
+      w[5] = u8(ts >> 16);
+      w[6] = u8(ts >> 8);
+      w[7] = u8(ts);
+      w[8] = u8(dt.ssrc >> 24);
+      w[9] = u8(dt.ssrc >> 16);
+      w[10] = u8(dt.ssrc >> 8);
+      w[11] = u8(dt.ssrc);
+      int n = 12;
+      const u8 *raw = A.arena + p.arenaOff;
+      for (int i = 0; i < 4 * cc; i++) w[n++] = raw[12 + i];
+      if (hasExt) {  // pion Header.MarshalTo one-byte profile (RFC 8285)
+        const int eb = (playout ? 4 : 0) + (dt.extAbs ? 4 : 0);
+        const int words = (eb + 3) >> 2;
+        w[n++] = 0xBE;
+        w[n++] = 0xDE;
+        w[n++] = u8(words >> 8);
+        w[n++] = u8(words);
+        if (playout) {
+          w[n++] = u8((dt.extPlayout << 4) | 2);
+          w[n++] = dt.playout[0];
+          w[n++] = dt.playout[1];
+          w[n++] = dt.playout[2];
+        }
+        if (dt.extAbs) {
+          w[n++] = u8((dt.extAbs << 4) | 2);
+          w[n++] = 0;
+          w[n++] = 0;
+          w[n++] = 0;
+        }
+      }
+      u64 src = u64(p.arenaOff) + p.poff;
+      if (t.flags & T_CODEC) {  // translateVP8PacketTo downtrack.go:1728-1736
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+          if (i < t.codecLen) w[n + i] = t.codec[i];
+        n += t.codecLen;
+        src += p.vhs;
+      }
+      // LDS region = prefix rounded up to 16 B, tail filled from the payload
+      // (so every 16-B chunk is either all-LDS or all-payload)
+      const int R = (n + 15) & ~15;
+      for (int i = n; i < R; i++) w[i] = (i < int(t.outLen)) ? raw[(src - p.arenaOff) + (i - n)] : 0;
+      sOff[threadIdx.x] = outOff;
+      sSrc[threadIdx.x] = src;
+      sLen[threadIdx.x] = t.outLen;
+      sPre[threadIdx.x] = u32(n) | (u32(R) << 16);
+    }
+    __syncthreads();
+    const u64 base = sOff[0];
+    const u64 end = sOff[nrec - 1] + ((u64(sLen[nrec - 1]) + 15) & ~u64(15));
+    const u32 nchunks = u32((end - base) >> 4);
+    for (u32 c = threadIdx.x; c < nchunks; c += EMIT_T) {
+      const u64 a = base + (u64(c) << 4);
+      int lo = 0, hi = nrec;
+      while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (sOff[mid] <= a)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      const u32 o = u32(a - sOff[lo]);
+      const u32 P = sPre[lo] & 0xffff, R = sPre[lo] >> 16, Ln = sLen[lo];
+      uint4 v;
+      if (o < R) {
+        v = *reinterpret_cast<const uint4 *>(&pre[lo][o]);
+      } else {
+        const u64 s = sSrc[lo] + (o - P);
+        const u64 W = s & ~u64(15);
+        const u32 sh = u32(s & 15);
+        const uint4 q0 = *reinterpret_cast<const uint4 *>(A.arena + W);
+        const uint4 q1 = *reinterpret_cast<const uint4 *>(A.arena + W + 16);
+        const u32 q = sh >> 2, rb = sh & 3;
+        // x_i = dword (q + i) of the 32-B window, q in 0..3
+        const u32 x0 = q == 0 ? q0.x : q == 1 ? q0.y : q == 2 ? q0.z : q0.w;
+        const u32 x1 = q == 0 ? q0.y : q == 1 ? q0.z : q == 2 ? q0.w : q1.x;
+        const u32 x2 = q == 0 ? q0.z : q == 1 ? q0.w : q == 2 ? q1.x : q1.y;
+        const u32 x3 = q == 0 ? q0.w : q == 1 ? q1.x : q == 2 ? q1.y : q1.z;
+        const u32 x4 = q == 0 ? q1.x : q == 1 ? q1.y : q == 2 ? q1.z : q1.w;
+        v.x = align_byte(x1, x0, rb);
+        v.y = align_byte(x2, x1, rb);
+        v.z = align_byte(x3, x2, rb);
+        v.w = align_byte(x4, x3, rb);
+        if (o + 16 > Ln) {  // zero the 16-B tail padding
+          const int keep = int(Ln) - int(o);
+          v.x &= keep_mask(keep);
+          v.y &= keep_mask(keep - 4);
+          v.z &= keep_mask(keep - 8);
+          v.w &= keep_mask(keep - 12);
+        }
+      }
+      *reinterpret_cast<uint4 *>(A.outArena + a) = v;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// sequencer.getExtPacketMetas sequencer.go:263-332 for one DownTrack (RTX
+// lookup; one lane, serial over the NACKed sequence numbers).
+// ---------------------------------------------------------------------------
+__global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u32 d, const u16 *sns, u32 n, i64 nowMs,
+                             lkf_seq_meta *out, u32 *nOut) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  DTHot h = hot[d];
+  SeqMeta *seq = seqBase + size_t(d) * seqSize;
+  u32 cnt = 0;
+  if (h.flags & F_SEQ_INIT) {
+    const u32 rtt = 70;  // defaultRtt (setRTT is out of scope)
+    const u32 refTime = u32(nowMs - h.seqStartMs);
+    const u16 highestSN = u16(h.seqExtHighestSN);
+    const u32 highestTS = u32(h.seqExtHighestTS);
+    for (u32 i = 0; i < n; i++) {
+      const u16 sn = sns[i];
+      if (u16(highestSN - sn) > (1 << 15)) continue;
+      u64 extSN = u64(sn) + (h.seqExtHighestSN & 0xFFFFFFFFFFFF0000ull);
+      if (sn > highestSN) extSN -= (1ull << 16);
+      // video sequencers have a RangeMap at value 0 (GetValue fails only for
+      // keys below its start 0 -> never); audio has none.
+      const u64 adj = extSN, adjH = h.seqExtHighestSN;
+      if (adjH - adj >= u64(seqSize)) continue;
+      SeqMeta &m = seq[adj % seqSize];
+      const bool invalid = m.sourceSeqNo == 0 && m.targetSeqNo == 0 && m.lastNack == 0;
+      if (m.targetSeqNo != sn || invalid) continue;
+      const u32 lim = (2 * rtt < 100) ? 2 * rtt : 100;
+      if (m.nacked < 3 && u32(refTime - m.lastNack) > lim) {
+        m.nacked++;
+        m.lastNack = refTime;
+        u64 extTS = u64(m.timestamp) + (h.seqExtHighestTS & 0xFFFFFFFF00000000ull);
+        if (m.timestamp > highestTS) extTS -= (1ull << 32);
+        lkf_seq_meta o = {};
+        o.ext_sn = extSN;
+        o.ext_ts = extTS;
+        o.source_sn = m.sourceSeqNo;
+        o.target_sn = m.targetSeqNo;
+        o.timestamp = m.timestamp;
+        o.last_nack = m.lastNack;
+        o.marker = m.marker;
+        o.nacked = m.nacked;
+        o.layer = m.layer;
+        o.codec_len = m.codecLen;
+        for (int k = 0; k < 8; k++) o.codec[k] = m.codec[k];
+        out[cnt++] = o;
+      }
+    }
+  }
+  *nOut = cnt;
+}
+
+// per-batch counters -> cumulative (stats[3] := arena bytes from the out scan)
+__global__ void k_accumulate(const u64 *stats, const u64 *tot, u64 *cum) {
+  const int i = threadIdx.x;
+  if (i < 4 + LKF_DROP_NREASONS) cum[i] += (i == 3) ? tot[3] : stats[i];
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers (kernels.h)
+// ---------------------------------------------------------------------------
+static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
+
+hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, u32 n, u32 ntracks, u32 *tBegin, u32 *tEnd,
+                               u32 *tRuns, u32 *err) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_track_ranges, dim3(nblk(n, 256)), dim3(256), 0, s, pkts, n, ntracks, tBegin, tEnd, tRuns, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const u32 *tBegin, const u32 *tEnd, const u32 *cnt,
+                       const u64 *bytes, u32 n, u64 *partA, u64 *partB, u64 *outA, u64 *outB, u64 *totA, u64 *totB) {
+  ScanIn in;
+  in.mode = mode;
+  in.dts = dts;
+  in.tBegin = tBegin;
+  in.tEnd = tEnd;
+  in.cnt = cnt;
+  in.bytes = bytes;
+  u32 nb = nblk(n ? n : 1, SCAN_TILE);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_T), 0, s, in, n, partA, partB);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, partA, partB, nb, totA, totB);
+  hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(SCAN_T), 0, s, in, n, partA, partB, outA, outB);
+  return hipGetLastError();
+}
+
+hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
+  if (a.nlanes == 0) return hipSuccess;
+  DecideArgs A;
+  A.sched = a.sched;
+  A.nlanes = a.nlanes;
+  A.hot = a.hot;
+  A.dts = a.dts;
+  A.tracks = a.tracks;
+  A.rm = a.rm;
+  A.vc = a.vc;
+  A.seq = a.seq;
+  A.seqSize = a.seqSize;
+  A.pkts = a.pkts;
+  A.tBegin = a.tBegin;
+  A.tEnd = a.tEnd;
+  A.slotBase = a.slotBase;
+  A.tuples = a.tuples;
+  A.tupleCap = a.tupleCap;
+  A.err = a.err;
+  A.events = a.events;
+  A.evOff = a.evOff;
+  A.fwdCnt = a.fwdCnt;
+  A.fwdBytes = a.fwdBytes;
+  A.stats = a.stats;
+  hipLaunchKernelGGL(k_decide, dim3(nblk(a.nlanes, 64)), dim3(64), 0, s, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
+  EmitArgs A;
+  A.recBase = a.recBase;
+  A.byteBase = a.byteBase;
+  A.slotBase = a.slotBase;
+  A.totals = a.totals;
+  A.tuples = a.tuples;
+  A.pkts = a.pkts;
+  A.arena = a.arena;
+  A.dts = a.dts;
+  A.ndts = a.ndts;
+  A.out = a.out;
+  A.outArena = a.outArena;
+  A.outCap = a.outCap;
+  A.outByteCap = a.outByteCap;
+  A.err = a.err;
+  hipLaunchKernelGGL(k_emit, dim3(a.grid), dim3(EMIT_T), 0, s, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_accumulate(hipStream_t s, const u64 *stats, const u64 *tot, u64 *cum) {
+  hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, s, stats, tot, cum);
+  return hipGetLastError();
+}
+
+hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, u32 seqSize, u32 d, const u16 *sns, u32 n,
+                             i64 nowMs, lkf_seq_meta *out, u32 *nOut) {
+  hipLaunchKernelGGL(k_seq_lookup, dim3(1), dim3(64), 0, s, hot, seq, seqSize, d, sns, n, nowMs, out, nOut);
+  return hipGetLastError();
+}
+
+}  // namespace lkf

@@ -1,0 +1,146 @@
+// fwd_state.h — HBM layout of the MI355X forwarding engine's per-DownTrack
+// state (shared by the host engine and the HIP kernels).
+//
+// Hot state (DTHot, 256 B AoS, one per DownTrack) holds every field the
+// per-packet recurrence touches on the common path: RTPMunger
+// (rtpmunger.go:73-92) incl. the open range of its RangeMap, the Forwarder
+// scalars (forwarder.go:187-215), the VideoLayerSelector layers
+// (videolayerselector/base.go), the VP8 munger scalars (codecmunger/vp8.go:52-70),
+// the sequencer head (sequencer.go:82-95) and the RTPStatsSender start point
+// (rtpstats_sender.go:245-262).  A decide lane loads it once per batch into
+// registers and stores it back once (2 x 256 B per active DownTrack).
+//
+// Cold state (rare paths only): the RTPMunger RangeMap's closed ranges
+// (ring of 100), the VP8 munger's missing/dropped/exempted picture-id maps
+// (rings), and the sequencer packetMeta ring (seq_size x 32 B).
+#pragma once
+#include <stdint.h>
+
+namespace lkf {
+
+constexpr int kRangeCap = 100;      // NewRangeMap(100) rtpmunger.go:97 (closed ranges)
+constexpr int kMissCap = 100;       // 50 kept + 50 staging (exact orderedmap trim semantics)
+constexpr int kMissKeep = 50;       // missingPictureIdsThreshold vp8.go:28
+constexpr int kDropKeep = 20;       // droppedPictureIdsThreshold vp8.go:29
+constexpr int kExemptKeep = 20;     // exemptedPictureIdsThreshold vp8.go:30
+constexpr int kSetCap = 21;         // 20 kept + 1 transient
+
+// DTHot.flags
+enum : uint32_t {
+  F_MUTED = 1u << 0,
+  F_PUBMUTED = 1u << 1,
+  F_STARTED = 1u << 2,
+  F_RESUME_BEHIND = 1u << 3,  // resumeBehindThreshold == 0.2 (else 0.0)
+  F_DEFICIENT = 1u << 4,      // lastAllocation.IsDeficient
+  F_LAST_MARKER = 1u << 5,
+  F_SECOND_LAST_MARKER = 1u << 6,
+  F_RTX_GATE = 1u << 7,
+  F_WR_MAX_MBIT = 1u << 8,
+  F_PICID_USED = 1u << 9,
+  F_TL0_USED = 1u << 10,
+  F_TID_USED = 1u << 11,
+  F_KEYIDX_USED = 1u << 12,
+  F_SEQ_INIT = 1u << 13,
+  F_STATS_INIT = 1u << 14,
+  F_PLAYOUT_ACKED = 1u << 15,
+  F_VIDEO = 1u << 16,
+  F_VP8 = 1u << 17,        // codecmunger.VP8 attached
+  F_SIMULCAST = 1u << 18,  // videolayerselector.Simulcast
+  F_TLS_VP8 = 1u << 19,    // temporallayerselector.VP8
+  F_HAS_EXPECTED = 1u << 20,
+  F_ACTIVE = 1u << 21,
+};
+
+struct alignas(16) DTHot {
+  // ---- 64-bit ------------------------------------------------------------
+  uint64_t extHighestIncomingSN;  // rtpmunger.go:76
+  uint64_t extLastSN, extSecondLastSN, snOffset;
+  uint64_t extLastTS, extSecondLastTS, tsOffset;
+  uint64_t extRtxGateSn;
+  uint64_t rmOpenStart, rmOpenValue;  // RangeMap open range (value of ranges[len-1])
+  uint64_t extFirstTS, refTSOffset;   // forwarder.go:201,204
+  int64_t preStartTime;               // ns, 0 == zero time
+  uint64_t seqExtStartSN, seqExtHighestSN, seqExtHighestTS;
+  int64_t seqStartMs;
+  int64_t statsFirstTime;
+  uint64_t statsExtStartTS;
+  // ---- 32-bit ------------------------------------------------------------
+  uint32_t flags;
+  uint32_t lastSSRC;
+  int32_t referenceLayerSpatial;
+  int32_t maxS, maxT, seenS, seenT, tgtS, tgtT, ptgtS, ptgtT, curS, curT, prevS, prevT, reqS;
+  int32_t wrMaxPictureId, wrTotalWrap, wrLastWrap;  // VP8PictureIdWrapHandler vp8.go:381
+  int32_t extLastPictureId, pictureIdOffset;
+  // ---- small -----------------------------------------------------------
+  uint16_t rmHead, rmCount;
+  uint8_t missHead, missCount, dropHead, dropCount, exHead, exCount;
+  uint8_t lastTl0, tl0Off, lastKeyIdx, keyIdxOff;
+  uint8_t pad[6];
+};
+static_assert(sizeof(DTHot) == 256, "DTHot must be 256 B");
+
+// Static per-DownTrack parameters (Bind-time: downtrack.go:362-432), 16 B.
+struct DevDT {
+  uint32_t track;
+  uint32_t ssrc;
+  uint8_t pt, extPlayout, extAbs, extDD;
+  uint8_t playout[3];
+  uint8_t active;
+};
+static_assert(sizeof(DevDT) == 16, "DevDT must be 16 B");
+
+struct RangeEntry {  // closed range of utils.RangeMap (rangemap.go:43-47)
+  uint64_t start, end, value;
+};
+
+struct VP8Cold {  // ordered maps of codecmunger.VP8 (vp8.go:67-69) as rings
+  int32_t missKey[kMissCap];
+  int32_t missVal[kMissCap];
+  int32_t dropKey[kSetCap];
+  int32_t exKey[kSetCap];
+  int32_t pad[2];
+};
+
+struct alignas(16) SeqMeta {  // packetMeta sequencer.go:44-73 (32 B)
+  uint16_t sourceSeqNo, targetSeqNo;
+  uint32_t timestamp;
+  uint32_t lastNack;
+  uint8_t marker, nacked;
+  int8_t layer;
+  uint8_t codecLen;
+  uint8_t codec[8];
+  uint8_t pad[8];
+};
+static_assert(sizeof(SeqMeta) == 32, "SeqMeta must be 32 B");
+
+// Decide -> emit hand-off record, one per forwarded tuple (48 B), written at
+// slot_base[dt] + j (j = DownTrack's forwarded ordinal in the batch).
+struct alignas(16) Tuple {
+  uint64_t extSN, extTS;
+  uint32_t pkt;
+  uint32_t relOff;    // byte offset in the DownTrack's output region
+  uint16_t outLen;
+  uint8_t flags;      // lkf_out flags | T_PLAYOUT | T_CODEC
+  int8_t layer;
+  uint8_t codecLen;
+  uint8_t codec[6];
+  uint8_t hdrLen;     // RTP header incl. extension block
+  uint8_t pad[12];
+};
+static_assert(sizeof(Tuple) == 48, "Tuple must be 48 B");
+enum : uint8_t { T_PLAYOUT = 0x40, T_CODEC = 0x80 };
+
+struct DevTrack {  // track table (24 x 4 B)
+  uint32_t kind, codec, hasRefTS, clockRate;
+  uint32_t layerOffsets[9];  // [ref*3 + layer]
+  uint32_t pad[3];
+};
+
+struct DevEvent {  // one queued lkf_ctl op (48 B)
+  uint32_t at;
+  int32_t op;
+  int64_t a[4];
+  int64_t pad;
+};
+
+}  // namespace lkf

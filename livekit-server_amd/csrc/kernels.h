@@ -1,0 +1,59 @@
+// kernels.h — launch interface between the host engine (engine.cpp) and the
+// gfx950 kernels (forward_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/lkfwd.h"
+#include "fwd_state.h"
+
+namespace lkf {
+
+struct DecideLaunch {
+  const uint32_t *sched;
+  uint32_t nlanes;
+  DTHot *hot;
+  const DevDT *dts;
+  const DevTrack *tracks;
+  RangeEntry *rm;
+  VP8Cold *vc;
+  SeqMeta *seq;
+  uint32_t seqSize;
+  const lkf_pkt *pkts;
+  const uint32_t *tBegin, *tEnd;
+  const uint64_t *slotBase;
+  Tuple *tuples;
+  uint64_t tupleCap;
+  uint32_t *err;
+  const DevEvent *events;
+  const uint32_t *evOff;
+  uint32_t *fwdCnt;
+  uint64_t *fwdBytes;
+  uint64_t *stats;
+};
+
+struct EmitLaunch {
+  const uint64_t *recBase, *byteBase, *slotBase, *totals;
+  const Tuple *tuples;
+  const lkf_pkt *pkts;
+  const uint8_t *arena;
+  const DevDT *dts;
+  uint32_t ndts;
+  lkf_out *out;
+  uint8_t *outArena;
+  uint64_t outCap, outByteCap;
+  uint32_t *err;
+  uint32_t grid;
+};
+
+hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, uint32_t n, uint32_t ntracks, uint32_t *tBegin,
+                               uint32_t *tEnd, uint32_t *tRuns, uint32_t *err);
+hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t *tBegin, const uint32_t *tEnd,
+                       const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
+                       uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB);
+hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
+hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
+hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum);
+hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint32_t d,
+                             const uint16_t *sns, uint32_t n, int64_t nowMs, lkf_seq_meta *out, uint32_t *nOut);
+
+}  // namespace lkf

@@ -1,0 +1,554 @@
+// synth.cpp — deterministic synthetic RTP workloads.
+//
+// Media model: VP8 3-layer simulcast L1T3 at 30 fps
+// (q: 1 pkt/frame ~600 B, h: 2 pkt/frame ~1000 B, f: 7 pkt/frame ~1100 B),
+// Opus 50 pkt/s 40-160 B.  Raw packets carry a one-byte header-extension
+// block (transport-cc seq for video, RFC 6464 audio level for audio), as a
+// browser publisher sends them.  Control scripts mirror what the reference's
+// control plane drives into the Forwarder (SetMax*, updateAllocation, Mute).
+#include "synth.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+using i64 = int64_t;
+
+struct Rng {
+  u64 s;
+  explicit Rng(u64 seed) : s(seed) {}
+  u64 next() {  // splitmix64
+    u64 z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  double uni() { return double(next() >> 11) * (1.0 / 9007199254740992.0); }
+  u32 below(u32 n) { return u32(uni() * n) % (n ? n : 1); }
+};
+
+constexpr i64 NS = 1000000000LL;
+constexpr i64 MS = 1000000LL;
+constexpr u16 kPayloadOff = 20;  // 12-byte header + 8-byte one-byte-ext block
+
+struct Plan {
+  i64 arrival;
+  u64 ext_sn;
+  u64 ext_ts;
+  u32 ssrc;
+  u16 payload_len;
+  u16 pid;
+  u16 twcc;
+  int8_t layer;
+  u8 tid;
+  u8 tl0;
+  u8 marker;
+  u8 keyframe;  // S && P==0 (first packet of a key frame)
+  u8 s_bit;
+  u8 y_bit;
+  u8 level;
+  u8 pt;
+};
+
+struct TrackGen {
+  lkf_track_params p;
+  int nlayers = 1;
+  std::vector<Plan> plans;  // merged arrival order
+};
+
+struct Ev {
+  int32_t dt;
+  int32_t op;
+  int64_t a[4];
+  i64 t;  // virtual time; < 0 = before the first packet
+};
+
+const int kPktsPerFrame[3] = {1, 2, 7};
+const int kPayloadMean[3] = {600, 1000, 1100};
+
+}  // namespace
+
+struct lkfs_trace {
+  std::vector<lkf_track_params> tracks;
+  std::vector<lkf_downtrack_params> dts;
+  std::vector<u64> batch_pkt_off;    // nb+1
+  std::vector<u64> batch_arena_off;  // nb+1
+  std::vector<lkf_pkt> pkts;
+  std::vector<u8> arena;
+  std::vector<u64> batch_ev_off;
+  std::vector<lkfs_event> events;
+  u32 max_batch_pkts = 0;
+  u64 max_batch_arena = 0;
+  u64 max_batch_tuples = 0;
+};
+
+static void fill_payload(u8 *dst, int n, u64 key) {
+  u64 x = key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    std::memcpy(dst + i, &x, 8);
+  }
+  for (; i < n; i++) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    dst[i] = u8(x);
+  }
+}
+
+extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
+  if (!cfg || cfg->config < 1 || cfg->config > 4) return nullptr;
+  const int C = cfg->config;
+  Rng rng(cfg->seed ? cfg->seed : (0x4C4Bull + u64(C)));
+  const double dur = cfg->duration_s > 0 ? cfg->duration_s : 10.0;
+  const double bs = cfg->batch_s > 0 ? cfg->batch_s : 1.0;
+  const i64 durNs = i64(dur * NS);
+  const i64 batchNs = i64(bs * NS);
+  const bool withEvents = cfg->with_events != 0;
+  const bool cb = cfg->has_callbacks != 0;
+
+  u32 rooms = cfg->rooms, parts = cfg->participants;
+  double loss = cfg->loss, reorder = cfg->reorder;
+  switch (C) {
+    case 1:
+      if (!rooms) rooms = 1;
+      if (!parts) parts = 10;
+      if (loss < 0) loss = 0;
+      if (reorder < 0) reorder = 0;
+      break;
+    case 2:
+      if (!rooms) rooms = 100;
+      if (!parts) parts = 10;
+      if (loss < 0) loss = 0.02;
+      if (reorder < 0) reorder = 0.01;
+      break;
+    case 3:
+      if (!rooms) rooms = 125;
+      if (!parts) parts = 50;
+      if (loss < 0) loss = 0.0;
+      if (reorder < 0) reorder = 0.0;
+      break;
+    case 4:
+      if (!rooms) rooms = 10;
+      if (!parts) parts = 5000;
+      if (loss < 0) loss = 0.0;
+      if (reorder < 0) reorder = 0.0;
+      break;
+  }
+
+  auto *tr = new lkfs_trace();
+  std::vector<TrackGen> tg;
+  std::vector<Ev> evs;
+  const i64 t0 = 1700000000LL * NS;  // virtual epoch
+
+  // ---- topology -------------------------------------------------------
+  struct RoomTracks {
+    std::vector<int> video;  // track handles
+    std::vector<u32> videoPub;
+    std::vector<int> audio;
+    std::vector<u32> audioPub;
+  };
+  for (u32 r = 0; r < rooms; r++) {
+    const u32 room = cfg->room_base + r;
+    RoomTracks rt;
+    u32 npub = (C == 1 || C == 4) ? 1 : parts;
+    for (u32 p = 0; p < npub; p++) {
+      bool hasVideo = (C != 3) || (p < 5);
+      if (hasVideo) {
+        TrackGen g{};
+        g.p.track_id = (u64(room) << 32) | (u64(p) << 8) | 1;
+        g.p.room = room;
+        g.p.publisher = p;
+        g.p.kind = LKF_KIND_VIDEO;
+        g.p.codec = LKF_CODEC_VP8;
+        g.p.has_ref_ts = cb ? 1 : 0;
+        g.p.is_mic = 0;
+        g.p.clock_rate = 90000;
+        g.nlayers = (C == 3) ? 1 : 3;
+        rt.video.push_back((int)tg.size());
+        rt.videoPub.push_back(p);
+        tg.push_back(g);
+      }
+      TrackGen a{};
+      a.p.track_id = (u64(room) << 32) | (u64(p) << 8) | 2;
+      a.p.room = room;
+      a.p.publisher = p;
+      a.p.kind = LKF_KIND_AUDIO;
+      a.p.codec = LKF_CODEC_OPUS;
+      a.p.has_ref_ts = cb ? 1 : 0;
+      a.p.is_mic = 1;
+      a.p.clock_rate = 48000;
+      a.nlayers = 1;
+      rt.audio.push_back((int)tg.size());
+      rt.audioPub.push_back(p);
+      tg.push_back(a);
+    }
+    // subscribers
+    u32 nsub = (C == 1 || C == 4) ? parts : parts;
+    for (u32 s = 0; s < nsub; s++) {
+      u32 subId = (C == 1 || C == 4) ? (1000000 + s) : s;
+      auto addDT = [&](int track, bool video) {
+        lkf_downtrack_params d{};
+        d.track = track;
+        d.subscriber = subId;
+        d.ssrc = u32(rng.next()) | 1u;
+        d.payload_type = video ? 96 : 111;
+        d.ext_dd = 0;
+        d.ext_playout = 0;
+        d.ext_abs_send_time = video ? 3 : 0;
+        d.has_expected_ts = cb ? 1 : 0;
+        d.bind_time_ns = t0 - 50 * MS;
+        int dt = (int)tr->dts.size();
+        tr->dts.push_back(d);
+        if (!video) return;
+        // subscription settings + publisher layer info (control plane)
+        evs.push_back(Ev{dt, LKF_CTL_SET_MAX_SPATIAL, {tg[track].nlayers - 1, 0, 0, 0}, -1});
+        evs.push_back(Ev{dt, LKF_CTL_SET_MAX_TEMPORAL, {2, 0, 0, 0}, -1});
+        evs.push_back(Ev{dt, LKF_CTL_SET_MAX_SEEN_SPATIAL, {tg[track].nlayers - 1, 0, 0, 0}, -1});
+        evs.push_back(Ev{dt, LKF_CTL_SET_MAX_SEEN_TEMPORAL, {2, 0, 0, 0}, -1});
+        int nl = tg[track].nlayers;
+        int ts;
+        if (C == 1)
+          ts = s < 5 ? 2 : (s < 8 ? 1 : 0);
+        else if (C == 4)
+          ts = rng.uni() < 0.8 ? 2 : int(rng.below(2));
+        else
+          ts = int(rng.below(u32(nl)));
+        if (ts > nl - 1) ts = nl - 1;
+        evs.push_back(Ev{dt, LKF_CTL_SET_ALLOCATION, {ts, 2, ts, 0}, -1});
+        if (withEvents && C == 2) {
+          // congestion/subscription script: new target every 2 s per DT
+          i64 phase = i64(rng.uni() * 2.0 * NS);
+          int cur = ts;
+          for (i64 t = phase; t < durNs; t += 2 * NS) {
+            int ns = int(rng.below(u32(nl)));
+            int nt = 1 + int(rng.below(2));
+            bool deficient = ns < cur;
+            evs.push_back(Ev{dt, LKF_CTL_SET_ALLOCATION, {ns, nt, ns, deficient ? 1 : 0}, t0 + t});
+            cur = ns;
+          }
+        }
+      };
+      for (size_t i = 0; i < rt.video.size(); i++)
+        if (C == 1 || C == 4 || rt.videoPub[i] != s) addDT(rt.video[i], true);
+      for (size_t i = 0; i < rt.audio.size(); i++)
+        if (C == 1 || C == 4 || rt.audioPub[i] != s) addDT(rt.audio[i], false);
+    }
+  }
+  // occasional subscriber mute/unmute (exercises resync + resume path)
+  if (withEvents && (C == 2 || C == 3)) {
+    for (int dt = 0; dt < (int)tr->dts.size(); dt++) {
+      if (rng.uni() < 0.05) {
+        i64 t = i64(rng.uni() * (durNs * 0.7));
+        i64 len = i64((0.3 + rng.uni()) * NS);
+        evs.push_back(Ev{dt, LKF_CTL_MUTE, {1, 1, 0, 0}, t0 + t});
+        evs.push_back(Ev{dt, LKF_CTL_MUTE, {0, 1, 0, 0}, t0 + t + len});
+      }
+    }
+  }
+
+  // ---- keyframe schedule (periodic + PLI-triggered, throttled) --------
+  // PLI: every allocation event that changes the target spatial layer asks
+  // for a key frame on that layer 100 ms later; pli_throttle 500 ms/layer.
+  std::vector<std::vector<std::vector<i64>>> kfReq(tg.size());
+  for (size_t t = 0; t < tg.size(); t++) kfReq[t].assign(3, {});
+  for (auto &e : evs) {
+    if (e.op != LKF_CTL_SET_ALLOCATION || e.t < 0) continue;
+    int track = tr->dts[e.dt].track;
+    int l = int(e.a[0]);
+    if (l >= 0 && l < 3) kfReq[track][l].push_back(e.t - t0 + 100 * MS);
+  }
+
+  // ---- per-track packet plans -------------------------------------------
+  for (size_t ti = 0; ti < tg.size(); ti++) {
+    TrackGen &g = tg[ti];
+    std::vector<std::vector<Plan>> streams(g.nlayers);
+    i64 netDelay = 20 * MS + i64(rng.below(10)) * MS;
+    if (g.p.kind == LKF_KIND_VIDEO) {
+      u32 tsBase[3];
+      for (int l = 0; l < g.nlayers; l++) tsBase[l] = u32(rng.next());
+      for (int r = 0; r < 3; r++)
+        for (int l = 0; l < 3; l++)
+          g.p.layer_offsets[r][l] = (r < g.nlayers && l < g.nlayers && r != l) ? u32(tsBase[r] - tsBase[l]) : 0;
+      for (int l = 0; l < g.nlayers; l++) {
+        int lq = g.nlayers == 1 ? 0 : l;
+        u32 ssrc = u32(rng.next()) | 1u;
+        u64 sn = u64(u16(rng.next()));
+        u16 pid0 = u16(rng.next() & 0x7fff);
+        u8 tl00 = u8(rng.next());
+        u16 twcc = u16(rng.next());
+        auto &reqs = kfReq[ti][l];
+        std::sort(reqs.begin(), reqs.end());
+        size_t ri = 0;
+        i64 lastKf = -10 * NS;
+        int nframes = int(dur * 30.0);
+        for (int f = 0; f < nframes; f++) {
+          i64 cap = i64(f) * NS / 30;
+          bool kf = (f % 60) == 0;
+          while (ri < reqs.size() && reqs[ri] <= cap) {
+            if (cap - lastKf >= 500 * MS) kf = true;
+            ri++;
+          }
+          if (kf) lastKf = cap;
+          int tid = (f % 4 == 0) ? 0 : ((f % 4 == 2) ? 1 : 2);
+          bool y = (f % 4 == 1) || (f % 4 == 2);
+          int np = kPktsPerFrame[lq];
+          for (int k = 0; k < np; k++) {
+            Plan pl{};
+            pl.arrival = t0 + cap + netDelay + i64(k) * 150000 + i64(rng.below(2000000));
+            pl.ext_sn = sn++;
+            pl.ext_ts = u64(tsBase[l]) + u64(f) * 3000;
+            pl.ssrc = ssrc;
+            int m = kPayloadMean[lq];
+            pl.payload_len = u16(m - m / 10 + int(rng.below(u32(m / 5))));
+            pl.pid = u16((pid0 + f) & 0x7fff);
+            pl.twcc = twcc++;
+            pl.layer = int8_t(l);
+            pl.tid = u8(tid);
+            pl.tl0 = u8(tl00 + f / 4);
+            pl.marker = k == np - 1;
+            pl.s_bit = k == 0;
+            pl.keyframe = kf && k == 0;
+            pl.y_bit = y;
+            pl.pt = 96;
+            streams[l].push_back(pl);
+          }
+        }
+      }
+    } else {
+      u32 ssrc = u32(rng.next()) | 1u;
+      u64 sn = u64(u16(rng.next()));
+      u32 ts0 = u32(rng.next());
+      int npk = int(dur * 50.0);
+      bool talking = rng.uni() < 0.33;
+      i64 nextFlip = i64((talking ? 2.0 : 4.0) * -std::log(1.0 - rng.uni()) * NS);
+      for (int k = 0; k < npk; k++) {
+        i64 cap = i64(k) * 20 * MS;
+        while (cap >= nextFlip) {
+          talking = !talking;
+          nextFlip += i64((talking ? 2.0 : 4.0) * -std::log(1.0 - rng.uni()) * NS) + 1;
+        }
+        Plan pl{};
+        pl.arrival = t0 + cap + netDelay + i64(rng.below(2000000));
+        pl.ext_sn = sn++;
+        pl.ext_ts = u64(ts0) + u64(k) * 960;
+        pl.ssrc = ssrc;
+        pl.payload_len = u16(40 + rng.below(121));
+        pl.layer = 0;
+        pl.marker = 0;
+        pl.level = talking ? u8(20 + rng.below(21)) : u8(90 + rng.below(38));
+        pl.pt = 111;
+        streams[0].push_back(pl);
+      }
+    }
+    // per-stream reorder (depth <= 3) and loss, then merge by arrival
+    for (auto &st : streams) {
+      // monotonic arrivals in send order
+      for (size_t i = 1; i < st.size(); i++)
+        if (st[i].arrival <= st[i - 1].arrival) st[i].arrival = st[i - 1].arrival + 1000;
+      if (reorder > 0) {
+        for (size_t i = 0; i + 1 < st.size(); i++) {
+          if (rng.uni() < reorder) {
+            size_t j = std::min(st.size() - 1, i + 1 + rng.below(3));
+            std::swap(st[i].arrival, st[j].arrival);
+          }
+        }
+      }
+      std::vector<Plan> kept;
+      kept.reserve(st.size());
+      for (auto &pl : st)
+        if (!(loss > 0 && rng.uni() < loss)) kept.push_back(pl);
+      st.swap(kept);
+      std::stable_sort(st.begin(), st.end(), [](const Plan &a, const Plan &b) { return a.arrival < b.arrival; });
+    }
+    for (auto &st : streams) g.plans.insert(g.plans.end(), st.begin(), st.end());
+    std::stable_sort(g.plans.begin(), g.plans.end(), [](const Plan &a, const Plan &b) {
+      if (a.arrival != b.arrival) return a.arrival < b.arrival;
+      return a.layer < b.layer;
+    });
+  }
+
+  for (auto &g : tg) tr->tracks.push_back(g.p);
+
+  // ---- batches ------------------------------------------------------------
+  const u32 nb = u32((durNs + batchNs - 1) / batchNs + 1);  // +1: network delay tail
+  std::vector<size_t> cursor(tg.size(), 0);
+  // per (batch, track) index range for event mapping
+  std::vector<std::vector<std::pair<u32, u32>>> trackRange(nb, std::vector<std::pair<u32, u32>>(tg.size()));
+  u64 totalArena = 0, totalPkts = 0;
+  for (auto &g : tg)
+    for (auto &pl : g.plans) {
+      totalPkts++;
+      totalArena += (u64(kPayloadOff) + pl.payload_len + 15) & ~u64(15);
+    }
+  tr->pkts.reserve(totalPkts);
+  tr->arena.resize(totalArena);
+  u64 aoff = 0;
+  tr->batch_pkt_off.push_back(0);
+  tr->batch_arena_off.push_back(0);
+  for (u32 b = 0; b < nb; b++) {
+    i64 end = (b + 1 == nb) ? INT64_MAX : t0 + i64(b + 1) * batchNs;
+    u64 batchA0 = aoff;
+    u64 batchP0 = tr->pkts.size();
+    for (size_t ti = 0; ti < tg.size(); ti++) {
+      TrackGen &g = tg[ti];
+      u32 rb = u32(tr->pkts.size() - batchP0);
+      while (cursor[ti] < g.plans.size() && g.plans[cursor[ti]].arrival < end) {
+        const Plan &pl = g.plans[cursor[ti]++];
+        lkf_pkt d{};
+        d.ext_sn = pl.ext_sn;
+        d.ext_ts = pl.ext_ts;
+        d.arrival_ns = pl.arrival;
+        d.arena_off = u32(aoff - batchA0);
+        d.track = u32(ti);
+        d.ssrc = pl.ssrc;
+        d.payload_off = kPayloadOff;
+        d.payload_len = pl.payload_len;
+        d.hdr0 = 0x90;  // V=2, X=1, CC=0
+        d.hdr1 = u8((pl.marker ? 0x80 : 0) | pl.pt);
+        d.layer = pl.layer;
+        u8 *raw = tr->arena.data() + aoff;
+        raw[0] = d.hdr0;
+        raw[1] = d.hdr1;
+        raw[2] = u8(pl.ext_sn >> 8);
+        raw[3] = u8(pl.ext_sn);
+        u32 ts32 = u32(pl.ext_ts);
+        raw[4] = u8(ts32 >> 24);
+        raw[5] = u8(ts32 >> 16);
+        raw[6] = u8(ts32 >> 8);
+        raw[7] = u8(ts32);
+        raw[8] = u8(pl.ssrc >> 24);
+        raw[9] = u8(pl.ssrc >> 16);
+        raw[10] = u8(pl.ssrc >> 8);
+        raw[11] = u8(pl.ssrc);
+        raw[12] = 0xBE;
+        raw[13] = 0xDE;
+        raw[14] = 0x00;
+        raw[15] = 0x01;
+        u8 *pay = raw + kPayloadOff;
+        fill_payload(pay, pl.payload_len, (u64(pl.ssrc) << 32) ^ pl.ext_sn);
+        if (g.p.kind == LKF_KIND_VIDEO) {
+          raw[16] = 0x51;  // id 5 (transport-cc), len 2
+          raw[17] = u8(pl.twcc >> 8);
+          raw[18] = u8(pl.twcc);
+          raw[19] = 0;
+          // VP8 payload descriptor (RFC 7741): X|S, I|L|T, M|PID(15), TL0, TID|Y
+          pay[0] = u8(0x80 | (pl.s_bit ? 0x10 : 0));
+          pay[1] = 0xE0;
+          pay[2] = u8(0x80 | (pl.pid >> 8));
+          pay[3] = u8(pl.pid);
+          pay[4] = pl.tl0;
+          pay[5] = u8((pl.tid << 6) | (pl.y_bit ? 0x20 : 0));
+          pay[6] = u8((pay[6] & 0xFE) | (pl.keyframe ? 0 : 1));  // VP8 P bit
+          d.flags = LKF_PKT_VP8 | (pl.keyframe ? LKF_PKT_KEYFRAME : 0);
+          d.vp8_first = pay[0];
+          d.vp8_bits = u8((pl.s_bit ? LKF_VP8_S : 0) | LKF_VP8_I | LKF_VP8_M | LKF_VP8_L | LKF_VP8_T |
+                          (pl.y_bit ? LKF_VP8_Y : 0));
+          d.vp8_hdr_size = 6;
+          d.vp8_picture_id = pl.pid;
+          d.vp8_tl0picidx = pl.tl0;
+          d.vp8_tid = pl.tid;
+          d.vp8_keyidx = 0;
+          d.spatial = -1;  // VP8 without DD: buffer.go:605-636
+          d.temporal = int8_t(pl.tid);
+        } else {
+          raw[16] = 0x10;  // id 1 (ssrc-audio-level), len 1
+          raw[17] = u8(0x80 | pl.level);
+          raw[18] = 0;
+          raw[19] = 0;
+          d.flags = LKF_PKT_HAS_LEVEL;
+          d.audio_level = pl.level;
+          d.spatial = -1;
+          d.temporal = 0;  // buffer.go:616
+        }
+        aoff += (u64(kPayloadOff) + pl.payload_len + 15) & ~u64(15);
+        tr->pkts.push_back(d);
+      }
+      trackRange[b][ti] = {rb, u32(tr->pkts.size() - batchP0)};
+    }
+    tr->batch_pkt_off.push_back(tr->pkts.size());
+    tr->batch_arena_off.push_back(aoff);
+    tr->max_batch_pkts = std::max(tr->max_batch_pkts, u32(tr->pkts.size() - batchP0));
+    tr->max_batch_arena = std::max(tr->max_batch_arena, aoff - batchA0);
+  }
+
+  {
+    std::vector<u64> dtsPerTrack(tg.size(), 0);
+    for (auto &d : tr->dts) dtsPerTrack[d.track]++;
+    for (u32 b = 0; b < nb; b++) {
+      u64 tup = 0;
+      for (size_t ti = 0; ti < tg.size(); ti++)
+        tup += u64(trackRange[b][ti].second - trackRange[b][ti].first) * dtsPerTrack[ti];
+      tr->max_batch_tuples = std::max(tr->max_batch_tuples, tup);
+    }
+  }
+  // ---- events -> (batch, at_pkt) -------------------------------------
+  std::vector<std::vector<lkfs_event>> bev(nb);
+  std::stable_sort(evs.begin(), evs.end(), [](const Ev &a, const Ev &b) { return a.t < b.t; });
+  for (auto &e : evs) {
+    lkfs_event o{};
+    o.dt = e.dt;
+    o.op = e.op;
+    for (int i = 0; i < 4; i++) o.a[i] = e.a[i];
+    if (e.t < 0) {
+      o.at_pkt = 0;
+      bev[0].push_back(o);
+      continue;
+    }
+    u32 b = u32(std::min<i64>(i64(nb) - 1, (e.t - t0) / batchNs));
+    int track = tr->dts[e.dt].track;
+    auto rg = trackRange[b][track];
+    const lkf_pkt *bp = tr->pkts.data() + tr->batch_pkt_off[b];
+    u32 at = rg.second;
+    for (u32 i = rg.first; i < rg.second; i++)
+      if (bp[i].arrival_ns >= e.t) {
+        at = i;
+        break;
+      }
+    o.at_pkt = at;
+    bev[b].push_back(o);
+  }
+  tr->batch_ev_off.push_back(0);
+  for (u32 b = 0; b < nb; b++) {
+    tr->events.insert(tr->events.end(), bev[b].begin(), bev[b].end());
+    tr->batch_ev_off.push_back(tr->events.size());
+  }
+  return tr;
+}
+
+extern "C" void lkfs_free(lkfs_trace *t) { delete t; }
+extern "C" uint32_t lkfs_num_tracks(const lkfs_trace *t) { return u32(t->tracks.size()); }
+extern "C" uint32_t lkfs_num_downtracks(const lkfs_trace *t) { return u32(t->dts.size()); }
+extern "C" const lkf_track_params *lkfs_tracks(const lkfs_trace *t) { return t->tracks.data(); }
+extern "C" const lkf_downtrack_params *lkfs_downtracks(const lkfs_trace *t) { return t->dts.data(); }
+extern "C" uint32_t lkfs_num_batches(const lkfs_trace *t) { return u32(t->batch_pkt_off.size() - 1); }
+extern "C" int lkfs_batch(const lkfs_trace *t, uint32_t b, const lkf_pkt **pkts, uint32_t *n, const uint8_t **arena,
+                          uint64_t *arena_len) {
+  if (b + 1 >= t->batch_pkt_off.size()) return LKF_EINVAL;
+  *pkts = t->pkts.data() + t->batch_pkt_off[b];
+  *n = u32(t->batch_pkt_off[b + 1] - t->batch_pkt_off[b]);
+  *arena = t->arena.data() + t->batch_arena_off[b];
+  *arena_len = t->batch_arena_off[b + 1] - t->batch_arena_off[b];
+  return LKF_OK;
+}
+extern "C" int lkfs_batch_events(const lkfs_trace *t, uint32_t b, const lkfs_event **ev, uint32_t *n) {
+  if (b + 1 >= t->batch_ev_off.size()) return LKF_EINVAL;
+  *ev = t->events.data() + t->batch_ev_off[b];
+  *n = u32(t->batch_ev_off[b + 1] - t->batch_ev_off[b]);
+  return LKF_OK;
+}
+extern "C" uint64_t lkfs_total_pkts(const lkfs_trace *t) { return t->pkts.size(); }
+extern "C" uint64_t lkfs_total_arena(const lkfs_trace *t) { return t->arena.size(); }
+extern "C" uint32_t lkfs_max_batch_pkts(const lkfs_trace *t) { return t->max_batch_pkts; }
+extern "C" uint64_t lkfs_max_batch_arena(const lkfs_trace *t) { return t->max_batch_arena; }
+extern "C" uint64_t lkfs_max_batch_tuples(const lkfs_trace *t) { return t->max_batch_tuples; }

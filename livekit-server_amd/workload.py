@@ -1,0 +1,81 @@
+"""Synthetic workloads (BASELINE.json configs) through the C generator.
+
+`Trace` wraps csrc/synth.cpp: topology, ExtPacket batches and scripted control
+events, deterministic for a given (config, seed).  `load_topology` and
+`queue_events` push a trace into anything exposing the lkf_* shaped API
+(the MI355X engine, or — in tests only — the oracle), so both receive
+byte-identical inputs.
+"""
+import ctypes as C
+
+from . import abi
+
+
+class Trace:
+    def __init__(self, config, duration_s=10.0, batch_s=1.0, rooms=0, participants=0, room_base=0,
+                 loss=-1.0, reorder=-1.0, with_events=-1, has_callbacks=-1, seed=0, synth_lib=None):
+        self.lib = synth_lib or abi.load_synth()
+        cfg = abi.lkfs_cfg(config=config, seed=seed, duration_s=duration_s, batch_s=batch_s, rooms=rooms,
+                           participants=participants, room_base=room_base, loss=loss, reorder=reorder,
+                           with_events=with_events, has_callbacks=has_callbacks)
+        self.config = config
+        self.h = self.lib.lkfs_generate(C.byref(cfg))
+        if not self.h:
+            raise ValueError("lkfs_generate failed for config %r" % config)
+        self.ntracks = self.lib.lkfs_num_tracks(self.h)
+        self.ndts = self.lib.lkfs_num_downtracks(self.h)
+        self.tracks = self.lib.lkfs_tracks(self.h)
+        self.downtracks = self.lib.lkfs_downtracks(self.h)
+        self.nbatches = self.lib.lkfs_num_batches(self.h)
+        self.total_pkts = self.lib.lkfs_total_pkts(self.h)
+        self.total_arena = self.lib.lkfs_total_arena(self.h)
+        self.max_batch_pkts = self.lib.lkfs_max_batch_pkts(self.h)
+        self.max_batch_arena = self.lib.lkfs_max_batch_arena(self.h)
+        self.max_batch_tuples = self.lib.lkfs_max_batch_tuples(self.h)
+
+    def batch(self, b):
+        pk = C.POINTER(abi.lkf_pkt)()
+        n = C.c_uint32()
+        ar = C.POINTER(C.c_uint8)()
+        alen = C.c_uint64()
+        rc = self.lib.lkfs_batch(self.h, b, C.byref(pk), C.byref(n), C.byref(ar), C.byref(alen))
+        if rc != 0:
+            raise IndexError(b)
+        return pk, n.value, ar, alen.value
+
+    def events(self, b):
+        ev = C.POINTER(abi.lkfs_event)()
+        n = C.c_uint32()
+        rc = self.lib.lkfs_batch_events(self.h, b, C.byref(ev), C.byref(n))
+        if rc != 0:
+            raise IndexError(b)
+        return [ev[i] for i in range(n.value)]
+
+    def close(self):
+        if self.h:
+            self.lib.lkfs_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load_topology(api, eng, trace):
+    for t in range(trace.ntracks):
+        h = api["add_track"](eng, C.byref(trace.tracks[t]))
+        if h != t:
+            raise RuntimeError("add_track returned %d for track %d" % (h, t))
+    for d in range(trace.ndts):
+        h = api["add_downtrack"](eng, C.byref(trace.downtracks[d]))
+        if h != d:
+            raise RuntimeError("add_downtrack returned %d for dt %d" % (h, d))
+
+
+def queue_events(api, eng, trace, b):
+    for ev in trace.events(b):
+        rc = api["ctl"](eng, ev.dt, ev.op, ev.a[0], ev.a[1], ev.a[2], ev.a[3], ev.at_pkt)
+        if rc != 0:
+            raise RuntimeError("ctl failed rc=%d" % rc)

@@ -1,0 +1,42 @@
+import importlib
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
+
+
+def _make(dirpath):
+    subprocess.run(["make", "-s", "-j8", "-C", dirpath], check=True)
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    """The product package (livekit-server_amd), with its C libraries built."""
+    if not os.path.exists(os.path.join(ROOT, "livekit-server_amd", "lib", "liblkfsynth.so")):
+        _make(os.path.join(ROOT, "livekit-server_amd", "csrc"))
+    return importlib.import_module("livekit-server_amd")
+
+
+@pytest.fixture(scope="session")
+def workload(pkg):
+    return importlib.import_module("livekit-server_amd.workload")
+
+
+@pytest.fixture(scope="session")
+def abi(pkg):
+    return importlib.import_module("livekit-server_amd.abi")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from tests import oracle_lib
+    return oracle_lib.load()

@@ -1,0 +1,162 @@
+"""Bit-exact parity: MI355X engine (liblkfwd.so) vs the CPU oracle.
+
+Both receive the same synthetic topology, ExtPacket batches and scripted
+control ops (BASELINE.json configs at oracle-tractable sizes).  Every output
+record (munged SN/TS, flags, layer, offsets, lengths), every wire byte
+(RTP header, extension block, munged VP8 descriptor, payload), every drop
+counter and the exported Forwarder state must be identical.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests.oracle_lib import load as load_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _drain_oracle(o, h):
+    from importlib import import_module
+    pkg = import_module("livekit-server_amd")
+    return pkg.drain_arrays(o.api, h)
+
+
+def _state_tuple(api, h, dt, abi):
+    st = abi.lkf_fwd_state()
+    assert api["get_state"](h, dt, C.byref(st)) == 0
+    return st.as_tuple()
+
+
+def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True):
+    o = load_oracle()
+    eng = pkg.Engine.for_trace(trace)
+    oh = o.create(500)
+    try:
+        workload.load_topology(eng.api, eng.h, trace)
+        workload.load_topology(o.api, oh, trace)
+        totals = {"forwarded": 0, "tuples": 0}
+        for b in range(trace.nbatches):
+            workload.queue_events(eng.api, eng.h, trace, b)
+            workload.queue_events(o.api, oh, trace, b)
+            pk, n, ar, alen = trace.batch(b)
+            eng.submit(pk, n, ar, alen)
+            eng.run()
+            eng.sync()
+            o.run(oh, pk, n, ar, alen)
+            gs = eng.stats()
+            ost = abi.lkf_stats()
+            o.api["get_stats"](oh, C.byref(ost))
+            os_ = ost.as_dict()
+            assert gs == os_, "batch %d stats differ:\n gpu %s\n orc %s" % (b, gs, os_)
+            grec, gar = eng.drain()
+            orec, oar = _drain_oracle(o, oh)
+            assert len(grec) == len(orec), (b, len(grec), len(orec))
+            if len(grec):
+                for f in abi.OUT_DTYPE.names:
+                    if not np.array_equal(grec[f], orec[f]):
+                        bad = np.nonzero(grec[f] != orec[f])[0][:5]
+                        raise AssertionError("batch %d field %s differs at %s: gpu %s orc %s" % (
+                            b, f, bad, grec[bad], orec[bad]))
+            assert gar.shape == oar.shape
+            if not np.array_equal(gar, oar):
+                bad = np.nonzero(gar != oar)[0]
+                r = np.searchsorted(grec["out_off"], bad[0], side="right") - 1
+                raise AssertionError("batch %d wire bytes differ at %d (record %d: %s)" % (b, bad[0], r, grec[r]))
+            totals["forwarded"] += gs["forwarded"]
+            totals["tuples"] += gs["tuples"]
+        if check_state:
+            for dt in range(trace.ndts):
+                assert _state_tuple(eng.api, eng.h, dt, abi) == _state_tuple(o.api, oh, dt, abi), dt
+        if seq_probe:
+            # sequencer.getExtPacketMetas on a few DownTracks (NACK -> RTX lookup)
+            now = 1700000000 * 10**9 + int(trace.nbatches * 1.5e9)
+            for dt in range(0, trace.ndts, max(1, trace.ndts // 7)):
+                grec_meta = (abi.lkf_seq_meta * 64)()
+                orec_meta = (abi.lkf_seq_meta * 64)()
+                gn, on = C.c_uint32(), C.c_uint32()
+                st = abi.lkf_fwd_state()
+                eng.api["get_state"](eng.h, dt, C.byref(st))
+                base = st.ext_last_sn & 0xFFFF
+                sns = (C.c_uint16 * 40)(*[(base - i * 3) & 0xFFFF for i in range(40)])
+                assert eng.api["seq_lookup"](eng.h, dt, sns, 40, now, grec_meta, C.byref(gn)) == 0
+                assert o.api["seq_lookup"](oh, dt, sns, 40, now, orec_meta, C.byref(on)) == 0
+                assert gn.value == on.value, (dt, gn.value, on.value)
+                for i in range(gn.value):
+                    assert bytes(grec_meta[i]) == bytes(orec_meta[i]), (dt, i)
+        return totals
+    finally:
+        eng.close()
+        o.destroy(oh)
+
+
+def test_config1_full(pkg, workload, abi):
+    """configs[0]: 1 room, VP8 3-layer simulcast + Opus, 10 subscribers, 10 s."""
+    tr = workload.Trace(1, duration_s=10.0, batch_s=1.0)
+    t = run_parity(pkg, workload, abi, tr)
+    assert t["forwarded"] > 17000
+
+
+def test_config2_small(pkg, workload, abi):
+    """configs[1] shape (layer switching, 2% loss, 1% reorder, mutes) on 8 rooms."""
+    tr = workload.Trace(2, duration_s=5.0, batch_s=1.0, rooms=8)
+    run_parity(pkg, workload, abi, tr)
+
+
+def test_config2_no_callbacks_small_batches(pkg, workload, abi):
+    """nil reference/expected-TS callbacks (reference unit-test wiring), 100 ms batches."""
+    tr = workload.Trace(2, duration_s=3.0, batch_s=0.1, rooms=3, has_callbacks=0)
+    run_parity(pkg, workload, abi, tr)
+
+
+def test_config2_heavy_loss(pkg, workload, abi):
+    """Loss/reorder far beyond the config: exercises gaps, OOO cache, missing-picture maps."""
+    tr = workload.Trace(2, duration_s=4.0, batch_s=0.5, rooms=3, loss=0.25, reorder=0.2, seed=77)
+    run_parity(pkg, workload, abi, tr)
+
+
+def test_config3_small(pkg, workload, abi):
+    """configs[2] shape: audio-heavy rooms of 50 (2 rooms)."""
+    tr = workload.Trace(3, duration_s=3.0, batch_s=1.0, rooms=2)
+    run_parity(pkg, workload, abi, tr, seq_probe=False)
+
+
+def test_config4_small(pkg, workload, abi):
+    """configs[3] shape: one publisher fanned out to 600 subscribers."""
+    tr = workload.Trace(4, duration_s=2.0, batch_s=1.0, rooms=1, participants=600)
+    run_parity(pkg, workload, abi, tr, check_state=False)
+
+
+def test_empty_and_control_only_batches(pkg, workload, abi):
+    """An empty batch and a control-only run are no-ops that still apply ops."""
+    tr = workload.Trace(1, duration_s=1.0, batch_s=1.0)
+    eng = pkg.Engine.for_trace(tr)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        eng.run()
+        eng.sync()
+        st = eng.stats()
+        assert st["tuples"] == 0 and st["forwarded"] == 0
+        rec, ar = eng.drain()
+        assert len(rec) == 0 and len(ar) == 0
+    finally:
+        eng.close()
+
+
+def test_ungrouped_batch_rejected(pkg, workload, abi):
+    """A batch whose tracks are not contiguous is refused (lkf_submit contract)."""
+    tr = workload.Trace(1, duration_s=1.0, batch_s=1.0)
+    pk, n, ar, alen = tr.batch(0)
+    arr = (abi.lkf_pkt * n)()
+    C.memmove(arr, pk, C.sizeof(abi.lkf_pkt) * n)
+    # interleave: swap first video packet with last audio packet
+    arr[0], arr[n - 1] = abi.lkf_pkt.from_buffer_copy(arr[n - 1]), abi.lkf_pkt.from_buffer_copy(arr[0])
+    eng = pkg.Engine.for_trace(tr)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        eng.submit(arr, n, ar, alen)
+        eng.run()
+        with pytest.raises(pkg.EngineError):
+            eng.sync()
+    finally:
+        eng.close()
