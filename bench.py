@@ -39,7 +39,7 @@ def algorithmic_bytes(trace, batches, fwd, out_bytes, active_dts):
     return b_in + out_bytes + 32 * fwd + 256 * active_dts * len(batches), b_in
 
 
-def cpu_baseline(threads, sample_rooms=10, sample_batches=2):
+def cpu_baseline(threads, sample_rooms=256, sample_batches=4):
     """CPU oracle (C++ restatement of the Go path, -O3 -march=native) on a bounded
     sample of the same workload, rooms sharded over `threads` workers."""
     from tests.oracle_lib import load as load_oracle
@@ -205,7 +205,7 @@ def main():
                          "kernel": "k_emit", "emit_ms_avg": round(emit_ms / args.steps, 4),
                          "decide_ms_avg": round(dec_ms / args.steps, 4),
                          "gpu_ms_per_step": round(tot_ms / args.steps, 4),
-                         "pipeline_algorithmic_GBps": round(algo / (tot_ms / 1e3), 1) if tot_ms else None},
+                         "pipeline_algorithmic_GBps": round(algo / (tot_ms / 1e3) / 1e9, 1) if tot_ms else None},
             "cpu_baseline": cpu,
             "tuples_per_step": cum["tuples"] // args.steps,
             "forwarded_per_step": fwd // args.steps,

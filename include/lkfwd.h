@@ -216,6 +216,16 @@ int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9
 int lkf_ctl(lkf_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64_t a2, int64_t a3,
             uint32_t at_pkt);
 
+/* Bulk form of lkf_ctl (one call per batch of ops; same semantics, in order). */
+typedef struct lkf_ctl_event {
+  int32_t dt;
+  int32_t op;
+  int64_t a[4];
+  uint32_t at_pkt;
+  uint32_t pad;
+} lkf_ctl_event;
+int lkf_ctl_batch(lkf_engine *e, const lkf_ctl_event *evs, uint32_t n);
+
 /* ---- data --------------------------------------------------------------- */
 /* Host batch: copies descriptors + arena to HBM (WebRTCReceiver.forwardRTP
  * receiver.go:635 -> DownTrackSpreader.Broadcast downtrackspreader.go:89). */

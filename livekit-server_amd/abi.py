@@ -220,6 +220,7 @@ def bind_engine_api(lib, prefix):
     api["set_layer_offsets"] = _bind(lib, prefix + "set_layer_offsets", C.c_int, [e, C.c_int32, P(C.c_uint32)])
     api["ctl"] = _bind(lib, prefix + "ctl", C.c_int,
                        [e, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_uint32])
+    api["ctl_batch"] = _bind(lib, prefix + "ctl_batch", C.c_int, [e, C.c_void_p, C.c_uint32])
     api["get_stats"] = _bind(lib, prefix + "get_stats", C.c_int, [e, P(lkf_stats)])
     api["drain"] = _bind(lib, prefix + "drain", C.c_int,
                          [e, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, P(C.c_uint64), P(C.c_uint64)])

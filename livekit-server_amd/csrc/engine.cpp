@@ -54,8 +54,14 @@ struct lkf_engine {
   };
   std::vector<Pend> pending;
   uint64_t pendSeq = 0;
-  std::vector<DevEvent> hEvents;
-  std::vector<uint32_t> hEvOff;
+  // pinned, double-buffered staging of the per-lane event CSR (async H2D)
+  struct Stage {
+    DevEvent *ev = nullptr;
+    uint32_t *off = nullptr;
+    size_t evCap = 0, offCap = 0;
+    hipEvent_t done = nullptr;
+    bool used = false;
+  } stage[2];
 
   // device: persistent state
   DevTrack *dTracks = nullptr;
@@ -65,6 +71,13 @@ struct lkf_engine {
   VP8Cold *dVc = nullptr;
   SeqMeta *dSeq = nullptr;
   uint32_t *dSched = nullptr;
+  uint32_t *dWaveTrack = nullptr;
+  size_t schedCap = 0;
+  std::vector<uint32_t> waveTrack;
+  // topology added since the last flush (uploaded in one copy each)
+  std::vector<DevTrack> pendTracks;
+  std::vector<DTHot> pendHot;
+  std::vector<DevDT> pendDTs;
   // device: batch input
   lkf_pkt *dPktsOwn = nullptr;
   uint8_t *dArenaOwn = nullptr;
@@ -148,6 +161,29 @@ static DevTrack to_dev_track(const lkf_track_params &p) {
   return t;
 }
 
+// Uploads tracks / DownTracks added since the last flush (contiguous tails).
+static int flush_topology(lkf_engine *e) {
+  if (e->pendTracks.empty() && e->pendDTs.empty()) return LKF_OK;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (!e->pendTracks.empty()) {
+    size_t first = e->tracks.size() - e->pendTracks.size();
+    HIPCHK(hipMemcpy(e->dTracks + first, e->pendTracks.data(), e->pendTracks.size() * sizeof(DevTrack),
+                     hipMemcpyHostToDevice),
+           "tracks upload");
+    e->pendTracks.clear();
+  }
+  if (!e->pendDTs.empty()) {
+    size_t first = e->dtp.size() - e->pendDTs.size();
+    HIPCHK(hipMemcpy(e->dHot + first, e->pendHot.data(), e->pendHot.size() * sizeof(DTHot), hipMemcpyHostToDevice),
+           "hot upload");
+    HIPCHK(hipMemcpy(e->dDTs + first, e->pendDTs.data(), e->pendDTs.size() * sizeof(DevDT), hipMemcpyHostToDevice),
+           "dt upload");
+    e->pendHot.clear();
+    e->pendDTs.clear();
+  }
+  return LKF_OK;
+}
+
 extern "C" {
 
 const char *lkf_version(void) { return "lkfwd 0.1 (gfx950)"; }
@@ -177,7 +213,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dRm, size_t(c.max_downtracks) * kRangeCap));
   A(dalloc(&e->dVc, c.max_downtracks));
   A(dalloc(&e->dSeq, size_t(c.max_downtracks) * c.seq_size));
-  A(dalloc(&e->dSched, c.max_downtracks));
   A(dalloc(&e->dPktsOwn, c.max_batch_pkts));
   A(dalloc(&e->dArenaOwn, c.max_batch_arena + 64));
   A(dalloc(&e->dTBegin, c.max_tracks));
@@ -196,7 +231,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dByteBase, c.max_downtracks));
   A(dalloc(&e->dOut, c.max_out_pkts));
   A(dalloc(&e->dOutArena, c.max_out_bytes + 64));
-  A(dalloc(&e->dEvOff, size_t(c.max_downtracks) + 1));
   A(dalloc(&e->dStats, kStatsWords));
   for (auto &ev : e->evt) A(hipEventCreate(&ev));
   for (auto &r : e->ring)
@@ -226,7 +260,7 @@ void lkf_destroy(lkf_engine *e) {
   void *ptrs[] = {e->dTracks, e->dHot, e->dDTs, e->dRm, e->dVc, e->dSeq, e->dSched, e->dPktsOwn, e->dArenaOwn,
                   e->dTBegin, e->dTEnd, e->dTRuns, e->dErr, e->dSlotBase, e->dPartA, e->dPartB, e->dTot,
                   e->dTuples, e->dFwdCnt, e->dFwdBytes, e->dRecBase, e->dByteBase, e->dOut, e->dOutArena,
-                  e->dEvents, e->dEvOff, e->dStats, e->dSns, e->dSeqOut, e->dSeqN};
+                  e->dEvents, e->dEvOff, e->dStats, e->dSns, e->dSeqOut, e->dSeqN, e->dWaveTrack};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &ev : e->evt)
@@ -235,6 +269,11 @@ void lkf_destroy(lkf_engine *e) {
     for (auto &ev : r)
       if (ev) (void)hipEventDestroy(ev);
   if (e->dCum) (void)hipFree(e->dCum);
+  for (auto &sg : e->stage) {
+    if (sg.ev) (void)hipHostFree(sg.ev);
+    if (sg.off) (void)hipHostFree(sg.off);
+    if (sg.done) (void)hipEventDestroy(sg.done);
+  }
   if (e->own) (void)hipStreamDestroy(e->own);
   delete e;
 }
@@ -242,17 +281,16 @@ void lkf_destroy(lkf_engine *e) {
 int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p) {
   if (!e || !p) return LKF_EINVAL;
   if (e->tracks.size() >= e->cfg.max_tracks) return LKF_ENOSPC;
-  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   int32_t h = int32_t(e->tracks.size());
   e->tracks.push_back(*p);
-  DevTrack t = to_dev_track(*p);
-  HIPCHK(hipMemcpyAsync(e->dTracks + h, &t, sizeof(t), hipMemcpyHostToDevice, e->own), "add_track copy");
-  HIPCHK(hipStreamSynchronize(e->own), "add_track sync");
+  e->pendTracks.push_back(to_dev_track(*p));  // uploaded by flush_topology
   return h;
 }
 
 int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9]) {
   if (!e || track < 0 || track >= int32_t(e->tracks.size())) return LKF_EINVAL;
+  int frc = flush_topology(e);
+  if (frc) return frc;
   std::memcpy(e->tracks[track].layer_offsets, offsets, 9 * sizeof(uint32_t));
   DevTrack t = to_dev_track(e->tracks[track]);
   HIPCHK(hipMemcpyAsync(e->dTracks + track, &t, sizeof(t), hipMemcpyHostToDevice, e->own), "offsets copy");
@@ -264,11 +302,11 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
   if (!e || !p) return LKF_EINVAL;
   if (p->track < 0 || p->track >= int32_t(e->tracks.size())) return LKF_EINVAL;
   if (e->dtp.size() >= e->cfg.max_downtracks) return LKF_ENOSPC;
-  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   int32_t h = int32_t(e->dtp.size());
   e->dtp.push_back(*p);
   e->active.push_back(1);
-  DTHot hot;
+  e->pendHot.emplace_back();
+  DTHot &hot = e->pendHot.back();
   init_hot(hot, e->tracks[p->track], *p);
   DevDT d;
   std::memset(&d, 0, sizeof(d));
@@ -280,15 +318,15 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
   d.extDD = p->ext_dd;
   std::memcpy(d.playout, p->playout_delay, 3);
   d.active = 1;
-  HIPCHK(hipMemcpyAsync(e->dHot + h, &hot, sizeof(hot), hipMemcpyHostToDevice, e->own), "dt hot copy");
-  HIPCHK(hipMemcpyAsync(e->dDTs + h, &d, sizeof(d), hipMemcpyHostToDevice, e->own), "dt copy");
-  HIPCHK(hipStreamSynchronize(e->own), "add_downtrack sync");
+  e->pendDTs.push_back(d);  // uploaded by flush_topology (one copy per batch of adds)
   e->schedDirty = true;
   return h;
 }
 
 int lkf_remove_downtrack(lkf_engine *e, int32_t dt) {
   if (!e || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  int frc = flush_topology(e);
+  if (frc) return frc;
   HIPCHK(hipStreamSynchronize(e->own), "remove sync");
   e->active[dt] = 0;
   uint8_t zero = 0;
@@ -313,6 +351,26 @@ int lkf_ctl(lkf_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64
   p.ev.a[3] = a3;
   p.seq = e->pendSeq++;
   e->pending.push_back(p);
+  return LKF_OK;
+}
+
+int lkf_ctl_batch(lkf_engine *e, const lkf_ctl_event *evs, uint32_t n) {
+  if (!e || (n && !evs)) return LKF_EINVAL;
+  const int32_t nd = int32_t(e->dtp.size());
+  for (uint32_t i = 0; i < n; i++)
+    if (evs[i].dt < 0 || evs[i].dt >= nd || evs[i].op < LKF_CTL_MUTE || evs[i].op > LKF_CTL_PLAYOUT_ACKED)
+      return LKF_EINVAL;
+  e->pending.reserve(e->pending.size() + n);
+  for (uint32_t i = 0; i < n; i++) {
+    lkf_engine::Pend p;
+    p.dt = uint32_t(evs[i].dt);
+    std::memset(&p.ev, 0, sizeof(p.ev));
+    p.ev.at = evs[i].at_pkt;
+    p.ev.op = evs[i].op;
+    for (int j = 0; j < 4; j++) p.ev.a[j] = evs[i].a[j];
+    p.seq = e->pendSeq++;
+    e->pending.push_back(p);
+  }
   return LKF_OK;
 }
 
@@ -342,23 +400,46 @@ int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const ui
   return LKF_OK;
 }
 
+// Lane schedule: one wave per (track, up to 64 of its DownTracks), idle lanes
+// padded with 0xffffffff.  Video tracks first (longest packet lists).
 static int rebuild_sched(lkf_engine *e) {
   const uint32_t nd = uint32_t(e->dtp.size());
-  e->sched.clear();
+  const uint32_t nt = uint32_t(e->tracks.size());
+  std::vector<std::vector<uint32_t>> byTrack(nt);
   for (uint32_t d = 0; d < nd; d++)
-    if (e->active[d]) e->sched.push_back(d);
-  // lanes of a wave share a track (same packet descriptors); video tracks
-  // (longer packet lists) first so waves are trip-count homogeneous.
-  std::stable_sort(e->sched.begin(), e->sched.end(), [&](uint32_t a, uint32_t b) {
-    const auto &ta = e->tracks[e->dtp[a].track], &tb = e->tracks[e->dtp[b].track];
-    if (ta.kind != tb.kind) return ta.kind > tb.kind;
-    return e->dtp[a].track < e->dtp[b].track;
-  });
+    if (e->active[d]) byTrack[e->dtp[d].track].push_back(d);
+  std::vector<uint32_t> order(nt);
+  for (uint32_t t = 0; t < nt; t++) order[t] = t;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t b) { return e->tracks[a].kind > e->tracks[b].kind; });
+  e->sched.clear();
+  e->waveTrack.clear();
+  for (uint32_t t : order) {
+    const auto &v = byTrack[t];
+    for (size_t i = 0; i < v.size(); i += 64) {
+      e->waveTrack.push_back(t);
+      for (size_t j = 0; j < 64; j++) e->sched.push_back(i + j < v.size() ? v[i + j] : 0xffffffffu);
+    }
+  }
   e->dtLane.assign(nd, -1);
-  for (uint32_t l = 0; l < e->sched.size(); l++) e->dtLane[e->sched[l]] = int32_t(l);
-  if (!e->sched.empty())
-    HIPCHK(hipMemcpy(e->dSched, e->sched.data(), e->sched.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
-           "sched copy");
+  for (uint32_t l = 0; l < e->sched.size(); l++)
+    if (e->sched[l] != 0xffffffffu) e->dtLane[e->sched[l]] = int32_t(l);
+  const size_t nl = e->sched.size();
+  if (nl + 1 > e->schedCap) {
+    if (e->dSched) HIPCHK(hipFree(e->dSched), "free sched");
+    if (e->dEvOff) HIPCHK(hipFree(e->dEvOff), "free evoff");
+    if (e->dWaveTrack) HIPCHK(hipFree(e->dWaveTrack), "free wavetrack");
+    e->schedCap = nl + 1 + 4096;
+    HIPCHK(dalloc(&e->dSched, e->schedCap), "alloc sched");
+    HIPCHK(dalloc(&e->dEvOff, e->schedCap + 1), "alloc evoff");
+    HIPCHK(dalloc(&e->dWaveTrack, e->schedCap / 64 + 1), "alloc wavetrack");
+  }
+  if (nl) {
+    HIPCHK(hipMemcpy(e->dSched, e->sched.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice), "sched copy");
+    HIPCHK(hipMemcpy(e->dWaveTrack, e->waveTrack.data(), e->waveTrack.size() * sizeof(uint32_t),
+                     hipMemcpyHostToDevice),
+           "wavetrack copy");
+  }
   e->schedDirty = false;
   return LKF_OK;
 }
@@ -372,6 +453,10 @@ int lkf_run(lkf_engine *e, void *stream) {
     e->curArenaLen = 0;
   }
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  {
+    int frc = flush_topology(e);
+    if (frc) return frc;
+  }
   if (e->schedDirty) {
     int rc = rebuild_sched(e);
     if (rc) return rc;
@@ -389,27 +474,42 @@ int lkf_run(lkf_engine *e, void *stream) {
                      if (la != lb) return la < lb;
                      return a.ev.at < b.ev.at;
                    });
-  e->hEvOff.assign(size_t(nl) + 1, 0);
-  e->hEvents.clear();
+  lkf_engine::Stage &sg = e->stage[e->nRuns & 1];
+  if (sg.used) HIPCHK(hipEventSynchronize(sg.done), "stage wait");
+  size_t nev = 0;
+  for (auto &p : e->pending)
+    if (e->dtLane[p.dt] >= 0) nev++;
+  if (nev > sg.evCap) {
+    if (sg.ev) HIPCHK(hipHostFree(sg.ev), "free stage");
+    sg.evCap = std::max<size_t>(nev, 4096);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sg.ev), sg.evCap * sizeof(DevEvent)), "alloc stage");
+  }
+  if (size_t(nl) + 1 > sg.offCap) {
+    if (sg.off) HIPCHK(hipHostFree(sg.off), "free stage");
+    sg.offCap = size_t(nl) + 1;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sg.off), sg.offCap * sizeof(uint32_t)), "alloc stage");
+  }
+  if (!sg.done) HIPCHK(hipEventCreateWithFlags(&sg.done, hipEventDisableTiming), "stage event");
+  std::memset(sg.off, 0, (size_t(nl) + 1) * sizeof(uint32_t));
+  size_t k = 0;
   for (auto &p : e->pending) {
     int l = e->dtLane[p.dt];
     if (l < 0) continue;  // op for a removed DownTrack
-    e->hEvOff[l + 1]++;
-    e->hEvents.push_back(p.ev);
+    sg.off[l + 1]++;
+    sg.ev[k++] = p.ev;
   }
-  for (uint32_t l = 0; l < nl; l++) e->hEvOff[l + 1] += e->hEvOff[l];
+  for (uint32_t l = 0; l < nl; l++) sg.off[l + 1] += sg.off[l];
   e->pending.clear();
-  if (e->hEvents.size() > e->evCap) {
+  if (nev > e->evCap) {
     if (e->dEvents) HIPCHK(hipFree(e->dEvents), "free events");
-    e->evCap = std::max<uint64_t>(e->hEvents.size(), 1024);
+    e->evCap = std::max<uint64_t>(nev, 4096);
     HIPCHK(dalloc(&e->dEvents, e->evCap), "alloc events");
   }
-  if (!e->hEvents.empty())
-    HIPCHK(hipMemcpyAsync(e->dEvents, e->hEvents.data(), e->hEvents.size() * sizeof(DevEvent), hipMemcpyHostToDevice,
-                          s),
-           "events copy");
-  HIPCHK(hipMemcpyAsync(e->dEvOff, e->hEvOff.data(), e->hEvOff.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s),
+  if (nev) HIPCHK(hipMemcpyAsync(e->dEvents, sg.ev, nev * sizeof(DevEvent), hipMemcpyHostToDevice, s), "events copy");
+  HIPCHK(hipMemcpyAsync(e->dEvOff, sg.off, (size_t(nl) + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s),
          "evoff copy");
+  HIPCHK(hipEventRecord(sg.done, s), "stage record");
+  sg.used = true;
 
   HIPCHK(hipMemsetAsync(e->dTBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
   HIPCHK(hipMemsetAsync(e->dTEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
@@ -428,6 +528,7 @@ int lkf_run(lkf_engine *e, void *stream) {
          "slot scan");
   DecideLaunch d;
   d.sched = e->dSched;
+  d.waveTrack = e->dWaveTrack;
   d.nlanes = nl;
   d.hot = e->dHot;
   d.dts = e->dDTs;
@@ -546,6 +647,10 @@ int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_
 
 int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *o) {
   if (!e || !o || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  {
+    int frc = flush_topology(e);
+    if (frc) return frc;
+  }
   HIPCHK(hipStreamSynchronize(e->cur), "sync");
   DTHot h;
   HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "state copy");
@@ -575,6 +680,10 @@ int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *o) {
 
 int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *i) {
   if (!e || !i || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  {
+    int frc = flush_topology(e);
+    if (frc) return frc;
+  }
   if (!i->started) return LKF_OK;  // SeedState forwarder.go:360-362
   HIPCHK(hipStreamSynchronize(e->cur), "sync");
   DTHot h;
@@ -609,6 +718,10 @@ int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *i) {
 int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns, lkf_seq_meta *out,
                    uint32_t *n_out) {
   if (!e || dt < 0 || dt >= int32_t(e->dtp.size()) || (n && (!sns || !out))) return LKF_EINVAL;
+  {
+    int frc = flush_topology(e);
+    if (frc) return frc;
+  }
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   HIPCHK(hipStreamSynchronize(e->cur), "sync");
   if (n > e->seqScratchCap) {

@@ -50,9 +50,7 @@ struct PktV {
   u16 pid;
 };
 
-__device__ __forceinline__ PktV load_pkt(const lkf_pkt *p) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
-  uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+__device__ __forceinline__ PktV decode_pkt(uint4 a, uint4 b, uint4 c, uint4 d) {
   PktV v;
   v.esn = (u64(a.y) << 32) | a.x;
   v.ets = (u64(a.w) << 32) | a.z;
@@ -78,6 +76,19 @@ __device__ __forceinline__ PktV load_pkt(const lkf_pkt *p) {
   return v;
 }
 
+__device__ __forceinline__ PktV load_pkt(const lkf_pkt *p) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  return decode_pkt(q[0], q[1], q[2], q[3]);
+}
+
+__device__ __forceinline__ uint4 rfl(uint4 v) {  // wave-uniform copy (SGPRs)
+  v.x = __builtin_amdgcn_readfirstlane(v.x);
+  v.y = __builtin_amdgcn_readfirstlane(v.y);
+  v.z = __builtin_amdgcn_readfirstlane(v.z);
+  v.w = __builtin_amdgcn_readfirstlane(v.w);
+  return v;
+}
+
 // ---------------------------------------------------------------------------
 // Lane context: hot state in registers + cold-state pointers.
 // ---------------------------------------------------------------------------
@@ -85,6 +96,8 @@ struct Lane {
   DTHot h;
   RangeEntry *rm;
   VP8Cold *vc;
+  i32 *dropKey;  // LDS copy of vc->dropKey (this lane's row)
+  i32 *exKey;    // LDS copy of vc->exKey
   SeqMeta *seq;
   u32 seqSize;
   // track
@@ -271,7 +284,7 @@ __device__ __forceinline__ void set_add(i32 *keys, u8 &head, u8 &count, i32 key,
   }
 }
 __device__ __forceinline__ bool dropped_has(const Lane &L, i32 key) {
-  return set_has(L.vc->dropKey, L.h.dropHead, L.h.dropCount, key);
+  return set_has(L.dropKey, L.h.dropHead, L.h.dropCount, key);
 }
 
 // The missing-picture loop of vp8.go:218-235, exact:
@@ -293,7 +306,7 @@ __device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
   }
   int nDrop = 0;
   for (int i = 0; i < L.h.dropCount; i++) {
-    i32 k = L.vc->dropKey[(L.h.dropHead + i) % kSetCap];
+    i32 k = L.dropKey[(L.h.dropHead + i) % kSetCap];
     if (k >= prevMax && k <= ext) nDrop++;
   }
   i64 nNew = i64(ext) - i64(prevMax) + 1 - nDrop - inE;
@@ -355,64 +368,62 @@ __device__ __forceinline__ void wr_init(Lane &L, i32 ext, bool m) {
   L.h.wrLastWrap = 0;
 }
 
-// buffer.VP8.MarshalTo helpers.go:170-227 into out[0..6); returns HeaderSize
-// written (or -1 if the fields need more than hs bytes: Go would panic).
-__device__ int vp8_marshal(u8 first, bool I, bool M, u16 pid, bool Lb, u8 tl0, bool T, u8 tid, bool Y, bool K,
-                           u8 keyidx, int hs, u8 *out) {
+// buffer.VP8.MarshalTo helpers.go:170-227, bytes packed little-endian into a
+// u64 (byte i = bits 8i..8i+7); returns HeaderSize (or -1 if the fields need
+// more than hs bytes: Go would panic on the index).
+__device__ __forceinline__ int vp8_marshal(u8 first, bool I, bool M, u16 pid, bool Lb, u8 tl0, bool T, u8 tid,
+                                           bool Y, bool K, u8 keyidx, int hs, u64 &out) {
   if (hs < 1 || hs > 6) return -1;
-  for (int i = 0; i < 6; i++) out[i] = 0;
-  int idx = 0;
-  out[0] = first;
+  out = 0;
   if (I || Lb || T || K) {
-    out[0] |= 0x80;
-    idx++;
-    int xpos = idx;
-    u8 xval = 0;
-    idx++;
+    out = u64(u8(first | 0x80));  // X bit
+    u32 xval = 0;
+    int idx = 2;
     if (I) {
       xval |= 0x80;
       if (M) {
         if (idx + 1 >= hs) return -1;
-        out[idx] = u8(0x80 | ((pid >> 8) & 0x7f));
-        out[idx + 1] = u8(pid & 0xff);
+        out |= u64(0x80 | ((pid >> 8) & 0x7f)) << (8 * idx);
+        out |= u64(pid & 0xff) << (8 * (idx + 1));
         idx += 2;
       } else {
         if (idx >= hs) return -1;
-        out[idx] = u8(pid);
+        out |= u64(pid & 0xff) << (8 * idx);
         idx++;
       }
     }
     if (Lb) {
       xval |= 0x40;
       if (idx >= hs) return -1;
-      out[idx] = tl0;
+      out |= u64(tl0) << (8 * idx);
       idx++;
     }
     if (T || K) {
       if (idx >= hs) return -1;
-      out[idx] = 0;
+      u32 b = 0;
       if (T) {
         xval |= 0x20;
-        out[idx] = u8(tid << 6);
-        if (Y) out[idx] |= 0x20;
+        b = u32(tid << 6) & 0xff;
+        if (Y) b |= 0x20;
       }
       if (K) {
         xval |= 0x10;
-        out[idx] |= keyidx & 0x1f;
+        b |= keyidx & 0x1f;
       }
+      out |= u64(b) << (8 * idx);
       idx++;
     }
-    if (xpos >= hs) return -1;
-    out[xpos] = xval;
+    if (hs < 2) return -1;
+    out |= u64(xval) << 8;
   } else {
-    out[0] &= u8(~0x80);
+    out = u64(u8(first & 0x7f));
   }
   return hs;
 }
 
 enum { CM_OK = 0, CM_FILTERED, CM_PICID_MISS, CM_ERR };
 // VP8.UpdateAndGet vp8.go:161-302
-__device__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool gap, i32 maxTL, u8 *cb, int &cbLen) {
+__device__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool gap, i32 maxTL, u64 &cb, int &cbLen) {
   const bool I = p.vbits & LKF_VP8_I, M = p.vbits & LKF_VP8_M, Lb = p.vbits & LKF_VP8_L;
   const bool T = p.vbits & LKF_VP8_T, Y = p.vbits & LKF_VP8_Y, K = p.vbits & LKF_VP8_K;
   i32 ext = wr_unwrap(L, p.pid, M);
@@ -432,12 +443,12 @@ __device__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool gap, i32 maxTL,
   setf(L, F_WR_MAX_MBIT, M);
   if (gap) {
     vp8_record_missing(L, prevMax, ext, L.h.pictureIdOffset);
-    if (T && p.tid > u8(maxTL)) set_add(L.vc->exKey, L.h.exHead, L.h.exCount, ext, kExemptKeep);
+    if (T && p.tid > u8(maxTL)) set_add(L.exKey, L.h.exHead, L.h.exCount, ext, kExemptKeep);
   } else {
     if (T && p.tid > u8(maxTL)) {
-      if (!set_has(L.vc->exKey, L.h.exHead, L.h.exCount, ext)) {
+      if (!set_has(L.exKey, L.h.exHead, L.h.exCount, ext)) {
         if (I && prevMax != ext) {
-          set_add(L.vc->dropKey, L.h.dropHead, L.h.dropCount, ext, kDropKeep);
+          set_add(L.dropKey, L.h.dropHead, L.h.dropCount, ext, kDropKeep);
           L.h.pictureIdOffset += 1;
         }
         return CM_FILTERED;
@@ -646,13 +657,14 @@ struct Fwd {
   u64 osn, ots;
   bool switching, resuming, marker;
   int cbLen;
-  u8 cb[6];
+  u64 cb;  // munged VP8 descriptor bytes, little-endian packed
 };
 
 // Forwarder.GetTranslationParams forwarder.go:1436-1765 for one (packet, DownTrack).
 __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
   o.switching = o.resuming = o.marker = false;
   o.cbLen = 0;
+  o.cb = 0;
   const i32 layer = p.layer;
   if (hasf(L, F_MUTED) || hasf(L, F_PUBMUTED)) return LKF_DROP_MUTED;
   if (!hasf(L, F_VIDEO)) return fw_common(L, p, layer, false, o.ord, o.osn, o.ots);
@@ -746,24 +758,38 @@ __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
 
 // sequencer.push sequencer.go:123-209 (no padding exclusions on this path: the
 // sequencer's RangeMap stays at value 0, so slot = extModifiedSN % size)
-__device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, const u8 *cb,
+__device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, u64 cb,
                          int cbLen) {
+  const u32 size = L.seqSize;
   if (!hasf(L, F_SEQ_INIT)) {
     setf(L, F_SEQ_INIT, true);
     L.h.seqExtStartSN = esn;
     L.h.seqExtHighestSN = esn;
     L.h.seqExtHighestTS = ets;
+    L.h.seqHighSlot = u16(esn % size);  // once per DownTrack lifetime
   }
   if (esn < L.h.seqExtStartSN) return;
   const u64 adjH = L.h.seqExtHighestSN;
   const u64 adjM = esn;
-  const u64 size = L.seqSize;
-  if (i64(adjM - adjH) <= -i64(size)) return;
-  if (adjM > adjH) {
+  const i64 delta = i64(adjM - adjH);
+  if (delta <= -i64(size)) return;
+  // slot of adjM from the highest slot without a 64-bit modulo
+  u32 slot;
+  if (delta >= 0) {
+    u32 dm = delta < i64(size) ? u32(delta) : u32(u64(delta) % size);
+    slot = L.h.seqHighSlot + dm;
+    if (slot >= size) slot -= size;
+  } else {
+    i32 sl = i32(L.h.seqHighSlot) + i32(delta);
+    slot = u32(sl < 0 ? sl + i32(size) : sl);
+  }
+  if (adjM > adjH) {  // invalidate the skipped slots (sequencer.go:179-189)
+    u32 x = L.h.seqHighSlot;
     u64 n = 0;
-    for (u64 x = adjH + 1; x != adjM; x++) {
+    for (u64 e = adjH + 1; e != adjM; e++) {
+      if (++x == size) x = 0;
       SeqMeta z = {};
-      L.seq[x % size] = z;
+      L.seq[x] = z;
       if (++n >= size) break;
     }
   }
@@ -776,9 +802,13 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
   m.nacked = 0;
   m.layer = layer;
   m.codecLen = u8(cbLen);
-  for (int i = 0; i < 6; i++) m.codec[i] = i < cbLen ? cb[i] : 0;
-  L.seq[adjM % size] = m;
-  if (esn > L.h.seqExtHighestSN) L.h.seqExtHighestSN = esn;
+#pragma unroll
+  for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+  L.seq[slot] = m;
+  if (esn > L.h.seqExtHighestSN) {
+    L.h.seqExtHighestSN = esn;
+    L.h.seqHighSlot = u16(slot);
+  }
   if (ets > L.h.seqExtHighestTS) L.h.seqExtHighestTS = ets;
 }
 
@@ -946,7 +976,8 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_down(ScanIn in, u32 n, const u6
 // wave read the same packet descriptors, broadcast from L1/L2).
 // ---------------------------------------------------------------------------
 struct DecideArgs {
-  const u32 *sched;  // lane -> DownTrack
+  const u32 *sched;      // lane -> DownTrack (0xffffffff = idle lane)
+  const u32 *waveTrack;  // wave -> track (every lane of a wave serves one track)
   u32 nlanes;
   DTHot *hot;
   const DevDT *dts;
@@ -968,18 +999,110 @@ struct DecideArgs {
   u64 *stats;  // lkf_stats as u64[15]
 };
 
-__global__ void __launch_bounds__(64) k_decide(DecideArgs A) {
+// One wave per (track, <=64 DownTracks): the packet loop is wave-uniform, so
+// packet descriptors come through the scalar cache and every branch on packet
+// fields is a scalar branch; lanes diverge only on per-DownTrack state.
+// Per (packet, DownTrack) body of DownTrack.WriteRTP (downtrack.go:680-760).
+struct LaneOut {
+  Tuple *outT;
+  u64 nFwd, nBytes, nTuples;
+  u32 relOff;
+  u32 drops[LKF_DROP_NREASONS];
+};
+
+__device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneOut &o) {
+  o.nTuples++;
+  Fwd f;
+  int dr = fw_translate(L, p, f);
+  if (dr >= 0) {
+#pragma unroll
+    for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] += (dr == i) ? 1u : 0u;
+    return;
+  }
+  // ---- output shape (downtrack.go:693-723, pacer/base.go:71-100)
+  const int cc = p.hdr0 & 0xf;
+  const bool playout = L.extPlayout && !hasf(L, F_PLAYOUT_ACKED);
+  int extBytes = (playout ? 4 : 0) + (L.extAbs ? 4 : 0);  // one-byte profile: 1 + 3 each
+  int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
+  int hdrLen = 12 + 4 * cc + extBlock;
+  const bool useCodec = f.cbLen > 0 && (p.flags & LKF_PKT_VP8);
+  int payLen = useCodec ? (f.cbLen + int(p.plen) - int(p.vhs)) : int(p.plen);
+  const bool marker = f.marker || (p.hdr1 & 0x80);
+  Tuple t;
+  t.extSN = f.osn;
+  t.extTS = f.ots;
+  t.pkt = k;
+  t.relOff = o.relOff;
+  t.outLen = u16(hdrLen + payLen);
+  t.flags = u8((f.switching ? LKF_OUT_SWITCHING : 0) | (f.resuming ? LKF_OUT_RESUMING : 0) |
+               ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
+               (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0));
+  t.layer = p.layer;
+  t.codecLen = u8(f.cbLen);
+#pragma unroll
+  for (int i = 0; i < 6; i++) t.codec[i] = u8(f.cb >> (8 * i));
+  t.hdrLen = u8(hdrLen);
+  for (int i = 0; i < 12; i++) t.pad[i] = 0;
+  o.outT[o.nFwd] = t;
+  // sequencer.push (downtrack.go:724-735)
+  seq_push(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
+  // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
+  if (!hasf(L, F_STATS_INIT) && payLen > 0) {
+    setf(L, F_STATS_INIT, true);
+    L.h.statsFirstTime = p.arr;
+    L.h.statsExtStartTS = f.ots;
+  }
+  o.nFwd++;
+  o.nBytes += u64(hdrLen + payLen);
+  o.relOff += u32((hdrLen + payLen + 15) & ~15);
+}
+
+// One wave per (track, <=64 DownTracks).  The packet loop is wave-uniform:
+// descriptors are staged 16 at a time into LDS by one cooperative 1-KiB load
+// (double-buffered: the next chunk is in flight while this one is decided)
+// and broadcast to SGPRs (readfirstlane), so every branch on packet fields is
+// a scalar branch; lanes diverge only on per-DownTrack state.  The VP8
+// dropped/exempted picture-id sets live in LDS for the whole batch.
+constexpr int CHUNK = 16;  // packets per staged chunk (64 x 16 B)
+
+__global__ void __launch_bounds__(64) k_decide(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
+  __shared__ uint4 sPkt[2][CHUNK * 4];
+  __shared__ i32 sDrop[64][kSetCap];
+  __shared__ i32 sEx[64][kSetCap];
   const u32 l = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = l < A.nlanes;
-  u64 nTuples = 0, nFwd = 0, nBytes = 0;
-  u64 drops[LKF_DROP_NREASONS];
-  for (int i = 0; i < LKF_DROP_NREASONS; i++) drops[i] = 0;
+  const u32 d = l < A.nlanes ? A.sched[l] : 0xffffffffu;
+  const bool live = d != 0xffffffffu;
+  const u32 track = A.waveTrack[blockIdx.x];
+  const u32 pb = A.tBegin[track];
+  u32 pe = A.tEnd[track];
+  const bool over = live && (A.slotBase[d] + (pe - pb) > A.tupleCap);
+  if (__any(over)) {  // tuple slots exhausted: skip this wave, flag
+    if (threadIdx.x == 0) atomicOr(A.err, 8u);
+    pe = pb;
+  }
+  LaneOut o;
+  o.nFwd = o.nBytes = o.nTuples = 0;
+  o.relOff = 0;
+  for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
+  Lane L;
+  u32 ev = 0, evEnd = 0, nextAt = 0xffffffffu;
   if (live) {
-    const u32 d = A.sched[l];
-    Lane L;
     L.h = A.hot[d];
     L.rm = A.rm + size_t(d) * kRangeCap;
     L.vc = A.vc + d;
+    L.dropKey = sDrop[threadIdx.x];
+    L.exKey = sEx[threadIdx.x];
+    if (L.h.flags & F_VP8) {
+      const uint4 *gd = reinterpret_cast<const uint4 *>(L.vc->dropKey);
+      const uint4 *ge = reinterpret_cast<const uint4 *>(L.vc->exKey);
+      uint4 *sd = reinterpret_cast<uint4 *>(L.dropKey);
+      uint4 *se = reinterpret_cast<uint4 *>(L.exKey);
+#pragma unroll
+      for (int i = 0; i < kSetCap / 4; i++) {
+        sd[i] = gd[i];
+        se[i] = ge[i];
+      }
+    }
     L.seq = A.seq + size_t(d) * A.seqSize;
     L.seqSize = A.seqSize;
     const DevDT dt = A.dts[d];
@@ -991,67 +1114,57 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs A) {
     L.offs = tk.layerOffsets;
     L.extPlayout = dt.extPlayout;
     L.extAbs = dt.extAbs;
-    const u32 pb = A.tBegin[dt.track];
-    u32 pe = A.tEnd[dt.track];
-    if (A.slotBase[d] + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
-      atomicOr(A.err, 8u);
-      pe = pb;
-    }
-    u32 ev = A.evOff[l];
-    const u32 evEnd = A.evOff[l + 1];
-    Tuple *outT = A.tuples + A.slotBase[d];
-    u32 relOff = 0;
-    for (u32 k = pb; k < pe; k++) {
-      while (ev < evEnd && A.events[ev].at <= k) apply_ctl(L, A.events[ev++]);
-      nTuples++;
-      const PktV p = load_pkt(A.pkts + k);
-      Fwd f;
-      int dr = fw_translate(L, p, f);
-      if (dr >= 0) {
-        drops[dr]++;
-        continue;
+    ev = A.evOff[l];
+    evEnd = A.evOff[l + 1];
+    o.outT = A.tuples + A.slotBase[d];
+    nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
+  }
+  const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
+  // stage chunk 0
+  if (pb < pe && threadIdx.x < min(u32(CHUNK), pe - pb) * 4) sPkt[0][threadIdx.x] = src[u64(pb) * 4 + threadIdx.x];
+  __syncthreads();
+  int cur = 0;
+  for (u32 base = pb; base < pe; base += CHUNK) {
+    const u32 np = min(u32(CHUNK), pe - base);
+    // prefetch the next chunk into registers (lands while this chunk is decided)
+    const u32 nb = base + CHUNK;
+    uint4 nx = make_uint4(0, 0, 0, 0);
+    const bool hasNext = nb < pe && threadIdx.x < min(u32(CHUNK), pe - nb) * 4;
+    if (hasNext) nx = src[u64(nb) * 4 + threadIdx.x];
+    for (u32 j = 0; j < np; j++) {
+      const PktV p = decode_pkt(rfl(sPkt[cur][j * 4 + 0]), rfl(sPkt[cur][j * 4 + 1]), rfl(sPkt[cur][j * 4 + 2]),
+                                rfl(sPkt[cur][j * 4 + 3]));
+      const u32 k = base + j;
+      if (live) {
+        while (nextAt <= k) {
+          apply_ctl(L, A.events[ev++]);
+          nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
+        }
+        decide_step(L, p, k, o);
       }
-      // ---- DownTrack.WriteRTP output shape (downtrack.go:693-723, pacer/base.go:71-100)
-      const int cc = p.hdr0 & 0xf;
-      const bool playout = L.extPlayout && !hasf(L, F_PLAYOUT_ACKED);
-      int extBytes = (playout ? 4 : 0) + (L.extAbs ? 4 : 0);  // one-byte profile: 1 + 3 each
-      int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
-      int hdrLen = 12 + 4 * cc + extBlock;
-      const bool useCodec = f.cbLen > 0 && (p.flags & LKF_PKT_VP8);
-      int payLen = useCodec ? (f.cbLen + int(p.plen) - int(p.vhs)) : int(p.plen);
-      const bool marker = f.marker || (p.hdr1 & 0x80);
-      Tuple t;
-      t.extSN = f.osn;
-      t.extTS = f.ots;
-      t.pkt = k;
-      t.relOff = relOff;
-      t.outLen = u16(hdrLen + payLen);
-      t.flags = u8((f.switching ? LKF_OUT_SWITCHING : 0) | (f.resuming ? LKF_OUT_RESUMING : 0) |
-                   ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
-                   (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0));
-      t.layer = p.layer;
-      t.codecLen = u8(f.cbLen);
-      for (int i = 0; i < 6; i++) t.codec[i] = i < f.cbLen ? f.cb[i] : 0;
-      t.hdrLen = u8(hdrLen);
-      for (int i = 0; i < 12; i++) t.pad[i] = 0;
-      outT[nFwd] = t;
-      // sequencer.push (downtrack.go:724-735)
-      seq_push(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
-      // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
-      if (!hasf(L, F_STATS_INIT) && payLen > 0) {
-        setf(L, F_STATS_INIT, true);
-        L.h.statsFirstTime = p.arr;
-        L.h.statsExtStartTS = f.ots;
-      }
-      nFwd++;
-      nBytes += u64(hdrLen + payLen);
-      relOff += u32((hdrLen + payLen + 15) & ~15);
     }
+    if (hasNext) sPkt[cur ^ 1][threadIdx.x] = nx;
+    cur ^= 1;
+    __syncthreads();
+  }
+  if (live) {
     while (ev < evEnd) apply_ctl(L, A.events[ev++]);
     A.hot[d] = L.h;
-    A.fwdCnt[d] = u32(nFwd);
-    A.fwdBytes[d] = relOff;
+    if (L.h.flags & F_VP8) {
+      uint4 *gd = reinterpret_cast<uint4 *>(L.vc->dropKey);
+      uint4 *ge = reinterpret_cast<uint4 *>(L.vc->exKey);
+      const uint4 *sd = reinterpret_cast<const uint4 *>(L.dropKey);
+      const uint4 *se = reinterpret_cast<const uint4 *>(L.exKey);
+#pragma unroll
+      for (int i = 0; i < kSetCap / 4; i++) {
+        gd[i] = sd[i];
+        ge[i] = se[i];
+      }
+    }
+    A.fwdCnt[d] = u32(o.nFwd);
+    A.fwdBytes[d] = o.relOff;
   }
+  const u64 nTuples = o.nTuples, nFwd = o.nFwd, nBytes = o.nBytes;
   // per-wave reduction of counters -> one atomic each
   u64 v = wave_sum(nTuples);
   if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)v);
@@ -1059,8 +1172,9 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs A) {
   if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)v);
   v = wave_sum(nBytes);
   if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[2], (unsigned long long)v);
+#pragma unroll
   for (int i = 0; i < LKF_DROP_NREASONS; i++) {
-    v = wave_sum(drops[i]);
+    v = wave_sum(u64(o.drops[i]));
     if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[4 + i], (unsigned long long)v);
   }
 }
@@ -1342,6 +1456,7 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   if (a.nlanes == 0) return hipSuccess;
   DecideArgs A;
   A.sched = a.sched;
+  A.waveTrack = a.waveTrack;
   A.nlanes = a.nlanes;
   A.hot = a.hot;
   A.dts = a.dts;
@@ -1362,7 +1477,7 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.fwdCnt = a.fwdCnt;
   A.fwdBytes = a.fwdBytes;
   A.stats = a.stats;
-  hipLaunchKernelGGL(k_decide, dim3(nblk(a.nlanes, 64)), dim3(64), 0, s, A);
+  hipLaunchKernelGGL(k_decide, dim3(nblk(a.nlanes, 64)), dim3(64), 0, s, A, a.pkts);
   return hipGetLastError();
 }
 

@@ -23,7 +23,7 @@ constexpr int kMissCap = 100;       // 50 kept + 50 staging (exact orderedmap tr
 constexpr int kMissKeep = 50;       // missingPictureIdsThreshold vp8.go:28
 constexpr int kDropKeep = 20;       // droppedPictureIdsThreshold vp8.go:29
 constexpr int kExemptKeep = 20;     // exemptedPictureIdsThreshold vp8.go:30
-constexpr int kSetCap = 21;         // 20 kept + 1 transient
+constexpr int kSetCap = 24;         // 20 kept (+ transient), 16-B multiple for wide copies
 
 // DTHot.flags
 enum : uint32_t {
@@ -75,7 +75,8 @@ struct alignas(16) DTHot {
   uint16_t rmHead, rmCount;
   uint8_t missHead, missCount, dropHead, dropCount, exHead, exCount;
   uint8_t lastTl0, tl0Off, lastKeyIdx, keyIdxOff;
-  uint8_t pad[6];
+  uint16_t seqHighSlot;  // seqExtHighestSN % seq_size (valid once F_SEQ_INIT)
+  uint8_t pad[4];
 };
 static_assert(sizeof(DTHot) == 256, "DTHot must be 256 B");
 
@@ -98,8 +99,8 @@ struct VP8Cold {  // ordered maps of codecmunger.VP8 (vp8.go:67-69) as rings
   int32_t missVal[kMissCap];
   int32_t dropKey[kSetCap];
   int32_t exKey[kSetCap];
-  int32_t pad[2];
 };
+static_assert(sizeof(VP8Cold) % 16 == 0, "VP8Cold must be 16-B granular");
 
 struct alignas(16) SeqMeta {  // packetMeta sequencer.go:44-73 (32 B)
   uint16_t sourceSeqNo, targetSeqNo;

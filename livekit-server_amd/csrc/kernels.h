@@ -10,6 +10,7 @@ namespace lkf {
 
 struct DecideLaunch {
   const uint32_t *sched;
+  const uint32_t *waveTrack;
   uint32_t nlanes;
   DTHot *hot;
   const DevDT *dts;

@@ -74,8 +74,18 @@ def load_topology(api, eng, trace):
             raise RuntimeError("add_downtrack returned %d for dt %d" % (h, d))
 
 
+def events_ptr(trace, b):
+    ev = C.POINTER(abi.lkfs_event)()
+    n = C.c_uint32()
+    if trace.lib.lkfs_batch_events(trace.h, b, C.byref(ev), C.byref(n)) != 0:
+        raise IndexError(b)
+    return ev, n.value
+
+
 def queue_events(api, eng, trace, b):
-    for ev in trace.events(b):
-        rc = api["ctl"](eng, ev.dt, ev.op, ev.a[0], ev.a[1], ev.a[2], ev.a[3], ev.at_pkt)
+    """Queues batch b's scripted control ops (lkfs_event == lkf_ctl_event layout)."""
+    ev, n = events_ptr(trace, b)
+    if n:
+        rc = api["ctl_batch"](eng, C.cast(ev, C.c_void_p), n)
         if rc != 0:
-            raise RuntimeError("ctl failed rc=%d" % rc)
+            raise RuntimeError("ctl_batch failed rc=%d" % rc)

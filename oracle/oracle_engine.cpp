@@ -276,6 +276,14 @@ int orc_ctl(orc_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64
   return LKF_OK;
 }
 
+int orc_ctl_batch(orc_engine *e, const lkf_ctl_event *evs, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) {
+    int rc = orc_ctl(e, evs[i].dt, evs[i].op, evs[i].a[0], evs[i].a[1], evs[i].a[2], evs[i].a[3], evs[i].at_pkt);
+    if (rc) return rc;
+  }
+  return LKF_OK;
+}
+
 // Runs one batch; pkts grouped by track (lkf_submit contract).
 int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len) {
   (void)arena_len;
