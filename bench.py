@@ -110,7 +110,7 @@ def main():
     nb = args.warmup + args.steps
     trace = wl.Trace(2, duration_s=nb * args.batch_s, batch_s=args.batch_s, rooms=args.rooms,
                      room_base=rank * args.rooms)
-    eng = pkg.Engine.for_trace(trace, device=local)
+    eng = pkg.Engine.for_trace(trace, device=local, lib_path=os.environ.get("LKF_LIB") or None)
     wl.load_topology(eng.api, eng.h, trace)
 
     # inputs resident in HBM before the timed region

@@ -2,8 +2,17 @@
 //
 // Owns the HBM-resident per-DownTrack state and the per-batch scratch, turns
 // queued control ops into a per-lane event list, and enqueues the batch
-// pipeline (forward_kernels.hip) on a HIP stream.  There is no CPU
-// forwarding path: every per-packet decision runs in the gfx950 kernels.
+// pipeline (forward_kernels.hip).  There is no CPU forwarding path: every
+// per-packet decision runs in the gfx950 kernels.
+//
+// Two-stage pipeline across batches.  Batch n's "decide" stage (track ranges,
+// slot scan, k_decide, output scan) runs on the run stream; its "emit" stage
+// (k_emit, counters) runs on an engine-owned emit stream after an event.  The
+// decide of batch n+1 depends only on decide n (DownTrack state), so it
+// overlaps emit n.  Per-batch scratch and outputs are double-buffered by run
+// parity: batch n's outputs stay valid until run n+2 is enqueued, and a
+// device batch's input buffers must stay valid until its emit stage is done
+// (lkf_sync, or the enqueue of run n+2).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,13 +37,33 @@ hipError_t dalloc(T **p, size_t n) {
 }
 
 constexpr int kStatsWords = 4 + LKF_DROP_NREASONS;
+constexpr uint32_t kIdle = 0xffffffffu;
+
+// Per-batch device scratch, outputs and events (two of them, by run parity).
+struct BatchCtx {
+  uint32_t *dTBegin = nullptr, *dTEnd = nullptr, *dTRuns = nullptr, *dErr = nullptr;
+  uint64_t *dSlotBase = nullptr, *dPartA = nullptr, *dPartB = nullptr, *dTot = nullptr;
+  Tuple *dTuples = nullptr;
+  uint32_t *dFwdCnt = nullptr;
+  uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
+  lkf_out *dOut = nullptr;
+  uint8_t *dOutArena = nullptr;
+  uint64_t *dStats = nullptr;
+  lkf_pkt *dPktsOwn = nullptr;  // lkf_submit copies land here
+  uint8_t *dArenaOwn = nullptr;
+  hipEvent_t decided = nullptr;  // decide stage done (run stream)
+  hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
+  bool used = false;
+  bool checked = false;  // error word already reported by lkf_sync
+};
 
 }  // namespace
 
 struct lkf_engine {
   int dev = 0;
-  hipStream_t own = nullptr;
-  hipStream_t cur = nullptr;
+  hipStream_t own = nullptr;    // default run stream, copies, lookups
+  hipStream_t emitS = nullptr;  // emit stage
+  hipStream_t cur = nullptr;    // run stream of the last lkf_run
   lkf_cfg cfg{};
   std::string err;
 
@@ -43,17 +72,20 @@ struct lkf_engine {
   std::vector<lkf_downtrack_params> dtp;
   std::vector<uint8_t> active;
   bool schedDirty = true;
-  std::vector<uint32_t> sched;   // lane -> dt
+  std::vector<uint32_t> sched;   // lane -> dt (kIdle = padding)
   std::vector<int32_t> dtLane;   // dt -> lane (-1 inactive)
+  std::vector<uint32_t> waveTrack;
+  // topology added since the last flush (uploaded in one copy each)
+  std::vector<DevTrack> pendTracks;
+  std::vector<DTHot> pendHot;
+  std::vector<DevDT> pendDTs;
 
   // queued control ops
   struct Pend {
     uint32_t dt;
     DevEvent ev;
-    uint64_t seq;
   };
   std::vector<Pend> pending;
-  uint64_t pendSeq = 0;
   // pinned, double-buffered staging of the per-lane event CSR (async H2D)
   struct Stage {
     DevEvent *ev = nullptr;
@@ -72,44 +104,33 @@ struct lkf_engine {
   SeqMeta *dSeq = nullptr;
   uint32_t *dSched = nullptr;
   uint32_t *dWaveTrack = nullptr;
+  uint32_t *dEvOff = nullptr;
   size_t schedCap = 0;
-  std::vector<uint32_t> waveTrack;
-  // topology added since the last flush (uploaded in one copy each)
-  std::vector<DevTrack> pendTracks;
-  std::vector<DTHot> pendHot;
-  std::vector<DevDT> pendDTs;
-  // device: batch input
-  lkf_pkt *dPktsOwn = nullptr;
-  uint8_t *dArenaOwn = nullptr;
+  DevEvent *dEvents = nullptr;
+  uint64_t evCap = 0;
+  uint64_t *dCum = nullptr;
+
+  // batch input for the next run
   const lkf_pkt *curPkts = nullptr;
   const uint8_t *curArena = nullptr;
   uint32_t curN = 0;
   uint64_t curArenaLen = 0;
   bool haveBatch = false;
-  // device: batch scratch
-  uint32_t *dTBegin = nullptr, *dTEnd = nullptr, *dTRuns = nullptr, *dErr = nullptr;
-  uint64_t *dSlotBase = nullptr, *dPartA = nullptr, *dPartB = nullptr, *dTot = nullptr;
-  Tuple *dTuples = nullptr;
-  uint32_t *dFwdCnt = nullptr;
-  uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
-  lkf_out *dOut = nullptr;
-  uint8_t *dOutArena = nullptr;
-  DevEvent *dEvents = nullptr;
-  uint32_t *dEvOff = nullptr;
-  uint64_t evCap = 0;
-  uint64_t *dStats = nullptr;
+
+  BatchCtx ctx[2];
+  uint64_t nRuns = 0;
+  int lastCtx = -1;
+
   // seq lookup scratch
   uint16_t *dSns = nullptr;
   lkf_seq_meta *dSeqOut = nullptr;
   uint32_t *dSeqN = nullptr;
   uint32_t seqScratchCap = 0;
 
-  hipEvent_t evt[4] = {nullptr, nullptr, nullptr, nullptr};
+  // timing ring: [0] decide-stage start, [1] k_decide end (run stream),
+  // [2] emit start, [3] emit end (emit stream)
   static constexpr int kRing = 256;
   hipEvent_t ring[kRing][4] = {};
-  uint64_t nRuns = 0;
-  uint64_t *dCum = nullptr;
-  bool ran = false;
   uint32_t emitGrid = 2048;
 };
 
@@ -119,9 +140,9 @@ static int fail(lkf_engine *e, const char *what, hipError_t r) {
   e->err = buf;
   return LKF_EHIP;
 }
-#define HIPCHK(call, what)                   \
-  do {                                       \
-    hipError_t _r = (call);                  \
+#define HIPCHK(call, what)                          \
+  do {                                              \
+    hipError_t _r = (call);                         \
     if (_r != hipSuccess) return fail(e, what, _r); \
   } while (0)
 
@@ -161,10 +182,20 @@ static DevTrack to_dev_track(const lkf_track_params &p) {
   return t;
 }
 
+// Waits for every queued stage (run, own and emit streams).
+static int drain_streams(lkf_engine *e) {
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (e->cur && e->cur != e->own) HIPCHK(hipStreamSynchronize(e->cur), "sync run stream");
+  HIPCHK(hipStreamSynchronize(e->own), "sync own stream");
+  HIPCHK(hipStreamSynchronize(e->emitS), "sync emit stream");
+  return LKF_OK;
+}
+
 // Uploads tracks / DownTracks added since the last flush (contiguous tails).
 static int flush_topology(lkf_engine *e) {
   if (e->pendTracks.empty() && e->pendDTs.empty()) return LKF_OK;
-  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  int rc = drain_streams(e);
+  if (rc) return rc;
   if (!e->pendTracks.empty()) {
     size_t first = e->tracks.size() - e->pendTracks.size();
     HIPCHK(hipMemcpy(e->dTracks + first, e->pendTracks.data(), e->pendTracks.size() * sizeof(DevTrack),
@@ -186,7 +217,7 @@ static int flush_topology(lkf_engine *e) {
 
 extern "C" {
 
-const char *lkf_version(void) { return "lkfwd 0.1 (gfx950)"; }
+const char *lkf_version(void) { return "lkfwd 0.2 (gfx950)"; }
 
 const char *lkf_last_error(const lkf_engine *e) { return e ? e->err.c_str() : "null engine"; }
 
@@ -194,6 +225,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   if (!cfg) return nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || hip_device < 0 || hip_device >= ndev) return nullptr;
+  if (cfg->seq_size > 65535) return nullptr;
   auto *e = new lkf_engine();
   e->dev = hip_device;
   e->cfg = *cfg;
@@ -206,6 +238,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   bool ok = true;
   auto A = [&](hipError_t r) { ok = ok && (r == hipSuccess); };
   A(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
+  A(hipStreamCreateWithFlags(&e->emitS, hipStreamNonBlocking));
   e->cur = e->own;
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
@@ -213,35 +246,41 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dRm, size_t(c.max_downtracks) * kRangeCap));
   A(dalloc(&e->dVc, c.max_downtracks));
   A(dalloc(&e->dSeq, size_t(c.max_downtracks) * c.seq_size));
-  A(dalloc(&e->dPktsOwn, c.max_batch_pkts));
-  A(dalloc(&e->dArenaOwn, c.max_batch_arena + 64));
-  A(dalloc(&e->dTBegin, c.max_tracks));
-  A(dalloc(&e->dTEnd, c.max_tracks));
-  A(dalloc(&e->dTRuns, c.max_tracks));
-  A(dalloc(&e->dErr, 4));
+  A(dalloc(&e->dCum, kStatsWords));
   const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
-  A(dalloc(&e->dSlotBase, c.max_downtracks));
-  A(dalloc(&e->dPartA, nparts));
-  A(dalloc(&e->dPartB, nparts));
-  A(dalloc(&e->dTot, 4));
-  A(dalloc(&e->dTuples, c.max_batch_tuples));
-  A(dalloc(&e->dFwdCnt, c.max_downtracks));
-  A(dalloc(&e->dFwdBytes, c.max_downtracks));
-  A(dalloc(&e->dRecBase, c.max_downtracks));
-  A(dalloc(&e->dByteBase, c.max_downtracks));
-  A(dalloc(&e->dOut, c.max_out_pkts));
-  A(dalloc(&e->dOutArena, c.max_out_bytes + 64));
-  A(dalloc(&e->dStats, kStatsWords));
-  for (auto &ev : e->evt) A(hipEventCreate(&ev));
+  for (auto &x : e->ctx) {
+    A(dalloc(&x.dTBegin, c.max_tracks));
+    A(dalloc(&x.dTEnd, c.max_tracks));
+    A(dalloc(&x.dTRuns, c.max_tracks));
+    A(dalloc(&x.dErr, 4));
+    A(dalloc(&x.dSlotBase, c.max_downtracks));
+    A(dalloc(&x.dPartA, nparts));
+    A(dalloc(&x.dPartB, nparts));
+    A(dalloc(&x.dTot, 4));
+    A(dalloc(&x.dTuples, c.max_batch_tuples));
+    A(dalloc(&x.dFwdCnt, c.max_downtracks));
+    A(dalloc(&x.dFwdBytes, c.max_downtracks));
+    A(dalloc(&x.dRecBase, c.max_downtracks));
+    A(dalloc(&x.dByteBase, c.max_downtracks));
+    A(dalloc(&x.dOut, c.max_out_pkts));
+    A(dalloc(&x.dOutArena, c.max_out_bytes + 64));
+    A(dalloc(&x.dStats, kStatsWords));
+    A(dalloc(&x.dPktsOwn, c.max_batch_pkts));
+    A(dalloc(&x.dArenaOwn, c.max_batch_arena + 64));
+    A(hipEventCreateWithFlags(&x.decided, hipEventDisableTiming));
+    A(hipEventCreateWithFlags(&x.emitted, hipEventDisableTiming));
+  }
   for (auto &r : e->ring)
     for (auto &ev : r) A(hipEventCreate(&ev));
-  A(dalloc(&e->dCum, kStatsWords));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
-    A(hipMemset(e->dArenaOwn, 0, c.max_batch_arena + 64));
-    A(hipMemset(e->dTot, 0, 4 * sizeof(uint64_t)));
-    A(hipMemset(e->dStats, 0, kStatsWords * sizeof(uint64_t)));
     A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
+    for (auto &x : e->ctx) {
+      A(hipMemset(x.dArenaOwn, 0, c.max_batch_arena + 64));
+      A(hipMemset(x.dTot, 0, 4 * sizeof(uint64_t)));
+      A(hipMemset(x.dStats, 0, kStatsWords * sizeof(uint64_t)));
+      A(hipMemset(x.dErr, 0, 4 * sizeof(uint32_t)));
+    }
   }
   if (!ok) {
     lkf_destroy(e);
@@ -256,24 +295,31 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
 void lkf_destroy(lkf_engine *e) {
   if (!e) return;
   (void)hipSetDevice(e->dev);
+  if (e->cur && e->cur != e->own) (void)hipStreamSynchronize(e->cur);
   if (e->own) (void)hipStreamSynchronize(e->own);
-  void *ptrs[] = {e->dTracks, e->dHot, e->dDTs, e->dRm, e->dVc, e->dSeq, e->dSched, e->dPktsOwn, e->dArenaOwn,
-                  e->dTBegin, e->dTEnd, e->dTRuns, e->dErr, e->dSlotBase, e->dPartA, e->dPartB, e->dTot,
-                  e->dTuples, e->dFwdCnt, e->dFwdBytes, e->dRecBase, e->dByteBase, e->dOut, e->dOutArena,
-                  e->dEvents, e->dEvOff, e->dStats, e->dSns, e->dSeqOut, e->dSeqN, e->dWaveTrack};
+  if (e->emitS) (void)hipStreamSynchronize(e->emitS);
+  void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
+                  e->dWaveTrack, e->dEvOff, e->dEvents, e->dCum, e->dSns, e->dSeqOut, e->dSeqN};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
-  for (auto &ev : e->evt)
-    if (ev) (void)hipEventDestroy(ev);
+  for (auto &x : e->ctx) {
+    void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
+                 x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
+                 x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn};
+    for (void *p : q)
+      if (p) (void)hipFree(p);
+    if (x.decided) (void)hipEventDestroy(x.decided);
+    if (x.emitted) (void)hipEventDestroy(x.emitted);
+  }
   for (auto &r : e->ring)
     for (auto &ev : r)
       if (ev) (void)hipEventDestroy(ev);
-  if (e->dCum) (void)hipFree(e->dCum);
   for (auto &sg : e->stage) {
     if (sg.ev) (void)hipHostFree(sg.ev);
     if (sg.off) (void)hipHostFree(sg.off);
     if (sg.done) (void)hipEventDestroy(sg.done);
   }
+  if (e->emitS) (void)hipStreamDestroy(e->emitS);
   if (e->own) (void)hipStreamDestroy(e->own);
   delete e;
 }
@@ -284,17 +330,19 @@ int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p) {
   int32_t h = int32_t(e->tracks.size());
   e->tracks.push_back(*p);
   e->pendTracks.push_back(to_dev_track(*p));  // uploaded by flush_topology
+  e->schedDirty = true;
   return h;
 }
 
 int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9]) {
   if (!e || track < 0 || track >= int32_t(e->tracks.size())) return LKF_EINVAL;
-  int frc = flush_topology(e);
-  if (frc) return frc;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
   std::memcpy(e->tracks[track].layer_offsets, offsets, 9 * sizeof(uint32_t));
   DevTrack t = to_dev_track(e->tracks[track]);
-  HIPCHK(hipMemcpyAsync(e->dTracks + track, &t, sizeof(t), hipMemcpyHostToDevice, e->own), "offsets copy");
-  HIPCHK(hipStreamSynchronize(e->own), "offsets sync");
+  HIPCHK(hipMemcpy(e->dTracks + track, &t, sizeof(t), hipMemcpyHostToDevice), "offsets copy");
   return LKF_OK;
 }
 
@@ -306,8 +354,7 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
   e->dtp.push_back(*p);
   e->active.push_back(1);
   e->pendHot.emplace_back();
-  DTHot &hot = e->pendHot.back();
-  init_hot(hot, e->tracks[p->track], *p);
+  init_hot(e->pendHot.back(), e->tracks[p->track], *p);
   DevDT d;
   std::memset(&d, 0, sizeof(d));
   d.track = uint32_t(p->track);
@@ -325,9 +372,10 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
 
 int lkf_remove_downtrack(lkf_engine *e, int32_t dt) {
   if (!e || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
-  int frc = flush_topology(e);
-  if (frc) return frc;
-  HIPCHK(hipStreamSynchronize(e->own), "remove sync");
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
   e->active[dt] = 0;
   uint8_t zero = 0;
   HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(e->dDTs + dt) + offsetof(DevDT, active), &zero, 1,
@@ -349,7 +397,6 @@ int lkf_ctl(lkf_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64
   p.ev.a[1] = a1;
   p.ev.a[2] = a2;
   p.ev.a[3] = a3;
-  p.seq = e->pendSeq++;
   e->pending.push_back(p);
   return LKF_OK;
 }
@@ -368,7 +415,6 @@ int lkf_ctl_batch(lkf_engine *e, const lkf_ctl_event *evs, uint32_t n) {
     p.ev.at = evs[i].at_pkt;
     p.ev.op = evs[i].op;
     for (int j = 0; j < 4; j++) p.ev.a[j] = evs[i].a[j];
-    p.seq = e->pendSeq++;
     e->pending.push_back(p);
   }
   return LKF_OK;
@@ -378,11 +424,13 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
   if (!e || (n && !pkts)) return LKF_EINVAL;
   if (n > e->cfg.max_batch_pkts || arena_len > e->cfg.max_batch_arena) return LKF_ENOSPC;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  if (n) HIPCHK(hipMemcpyAsync(e->dPktsOwn, pkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyHostToDevice, e->own), "pkts");
-  if (arena_len) HIPCHK(hipMemcpyAsync(e->dArenaOwn, arena, arena_len, hipMemcpyHostToDevice, e->own), "arena");
+  BatchCtx &x = e->ctx[e->nRuns & 1];
+  if (x.used) HIPCHK(hipEventSynchronize(x.emitted), "wait emit");  // batch n-2 still reads these buffers
+  if (n) HIPCHK(hipMemcpyAsync(x.dPktsOwn, pkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyHostToDevice, e->own), "pkts");
+  if (arena_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, arena, arena_len, hipMemcpyHostToDevice, e->own), "arena");
   HIPCHK(hipStreamSynchronize(e->own), "submit sync");
-  e->curPkts = e->dPktsOwn;
-  e->curArena = e->dArenaOwn;
+  e->curPkts = x.dPktsOwn;
+  e->curArena = x.dArenaOwn;
   e->curN = n;
   e->curArenaLen = arena_len;
   e->haveBatch = true;
@@ -401,7 +449,7 @@ int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const ui
 }
 
 // Lane schedule: one wave per (track, up to 64 of its DownTracks), idle lanes
-// padded with 0xffffffff.  Video tracks first (longest packet lists).
+// padded with kIdle.  Video tracks first (longest packet lists).
 static int rebuild_sched(lkf_engine *e) {
   const uint32_t nd = uint32_t(e->dtp.size());
   const uint32_t nt = uint32_t(e->tracks.size());
@@ -418,13 +466,15 @@ static int rebuild_sched(lkf_engine *e) {
     const auto &v = byTrack[t];
     for (size_t i = 0; i < v.size(); i += 64) {
       e->waveTrack.push_back(t);
-      for (size_t j = 0; j < 64; j++) e->sched.push_back(i + j < v.size() ? v[i + j] : 0xffffffffu);
+      for (size_t j = 0; j < 64; j++) e->sched.push_back(i + j < v.size() ? v[i + j] : kIdle);
     }
   }
   e->dtLane.assign(nd, -1);
   for (uint32_t l = 0; l < e->sched.size(); l++)
-    if (e->sched[l] != 0xffffffffu) e->dtLane[e->sched[l]] = int32_t(l);
+    if (e->sched[l] != kIdle) e->dtLane[e->sched[l]] = int32_t(l);
   const size_t nl = e->sched.size();
+  int rc = drain_streams(e);  // queued runs still read the previous schedule
+  if (rc) return rc;
   if (nl + 1 > e->schedCap) {
     if (e->dSched) HIPCHK(hipFree(e->dSched), "free sched");
     if (e->dEvOff) HIPCHK(hipFree(e->dEvOff), "free evoff");
@@ -446,28 +496,37 @@ static int rebuild_sched(lkf_engine *e) {
 
 int lkf_run(lkf_engine *e, void *stream) {
   if (!e) return LKF_EINVAL;
-  if (!e->haveBatch) {  // control-only run: an empty batch applies queued ops
-    e->curPkts = e->dPktsOwn;
-    e->curArena = e->dArenaOwn;
-    e->curN = 0;
-    e->curArenaLen = 0;
-  }
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   {
-    int frc = flush_topology(e);
-    if (frc) return frc;
+    int rc = flush_topology(e);
+    if (rc) return rc;
   }
   if (e->schedDirty) {
     int rc = rebuild_sched(e);
     if (rc) return rc;
   }
+  const int ci = int(e->nRuns & 1);
+  BatchCtx &x = e->ctx[ci];
+  if (!e->haveBatch) {  // control-only run: an empty batch applies queued ops
+    e->curPkts = x.dPktsOwn;
+    e->curArena = x.dArenaOwn;
+    e->curN = 0;
+    e->curArenaLen = 0;
+  }
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e->own;
+  if (s != e->cur && e->nRuns) {
+    // a different run stream: order after everything the previous one queued
+    int rc = drain_streams(e);
+    if (rc) return rc;
+  }
   e->cur = s;
   const uint32_t nt = uint32_t(e->tracks.size());
   const uint32_t nd = uint32_t(e->dtp.size());
   const uint32_t nl = uint32_t(e->sched.size());
+  // this context's previous batch (run n-2) must have finished its emit stage
+  if (x.used) HIPCHK(hipStreamWaitEvent(s, x.emitted, 0), "wait emit");
 
-  // per-lane event CSR (stable by queue order, then by at_pkt)
+  // per-lane event CSR (stable: queue order within a lane, then by at_pkt)
   std::stable_sort(e->pending.begin(), e->pending.end(),
                    [&](const lkf_engine::Pend &a, const lkf_engine::Pend &b) {
                      int la = e->dtLane[a.dt], lb = e->dtLane[b.dt];
@@ -501,7 +560,10 @@ int lkf_run(lkf_engine *e, void *stream) {
   for (uint32_t l = 0; l < nl; l++) sg.off[l + 1] += sg.off[l];
   e->pending.clear();
   if (nev > e->evCap) {
-    if (e->dEvents) HIPCHK(hipFree(e->dEvents), "free events");
+    if (e->dEvents) {
+      HIPCHK(hipStreamSynchronize(s), "sync before events realloc");
+      HIPCHK(hipFree(e->dEvents), "free events");
+    }
     e->evCap = std::max<uint64_t>(nev, 4096);
     HIPCHK(dalloc(&e->dEvents, e->evCap), "alloc events");
   }
@@ -511,20 +573,20 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipEventRecord(sg.done, s), "stage record");
   sg.used = true;
 
-  HIPCHK(hipMemsetAsync(e->dTBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dTEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dTRuns, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dErr, 0, 4 * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dStats, 0, kStatsWords * sizeof(uint64_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dFwdCnt, 0, size_t(std::max(nd, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dFwdBytes, 0, size_t(std::max(nd, 1u)) * sizeof(uint64_t), s), "memset");
+  HIPCHK(hipMemsetAsync(x.dTBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(x.dTEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(x.dTRuns, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(x.dErr, 0, 4 * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(x.dStats, 0, kStatsWords * sizeof(uint64_t), s), "memset");
+  HIPCHK(hipMemsetAsync(x.dFwdCnt, 0, size_t(std::max(nd, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(x.dFwdBytes, 0, size_t(std::max(nd, 1u)) * sizeof(uint64_t), s), "memset");
 
+  // ---- decide stage (run stream)
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
-  HIPCHK(hipEventRecord(e->evt[0], s), "event");
   HIPCHK(hipEventRecord(rg[0], s), "event");
-  HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, nt, e->dTBegin, e->dTEnd, e->dTRuns, e->dErr), "track_ranges");
-  HIPCHK(launch_scan(s, 0, e->dDTs, e->dTBegin, e->dTEnd, nullptr, nullptr, nd, e->dPartA, e->dPartB, e->dSlotBase,
-                     nullptr, e->dTot + 0, nullptr),
+  HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr), "track_ranges");
+  HIPCHK(launch_scan(s, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
+                     x.dTot + 0, nullptr),
          "slot scan");
   DecideLaunch d;
   d.sched = e->dSched;
@@ -538,63 +600,76 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.seq = e->dSeq;
   d.seqSize = e->cfg.seq_size;
   d.pkts = e->curPkts;
-  d.tBegin = e->dTBegin;
-  d.tEnd = e->dTEnd;
-  d.slotBase = e->dSlotBase;
-  d.tuples = e->dTuples;
+  d.tBegin = x.dTBegin;
+  d.tEnd = x.dTEnd;
+  d.slotBase = x.dSlotBase;
+  d.tuples = x.dTuples;
   d.tupleCap = e->cfg.max_batch_tuples;
-  d.err = e->dErr;
+  d.err = x.dErr;
   d.events = e->dEvents;
   d.evOff = e->dEvOff;
-  d.fwdCnt = e->dFwdCnt;
-  d.fwdBytes = e->dFwdBytes;
-  d.stats = e->dStats;
+  d.fwdCnt = x.dFwdCnt;
+  d.fwdBytes = x.dFwdBytes;
+  d.stats = x.dStats;
   HIPCHK(launch_decide(s, d), "decide");
-  HIPCHK(hipEventRecord(e->evt[1], s), "event");
   HIPCHK(hipEventRecord(rg[1], s), "event");
-  HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, e->dFwdCnt, e->dFwdBytes, nd, e->dPartA, e->dPartB, e->dRecBase,
-                     e->dByteBase, e->dTot + 2, e->dTot + 3),
+  HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
+                     x.dByteBase, x.dTot + 2, x.dTot + 3),
          "out scan");
-  HIPCHK(hipEventRecord(e->evt[2], s), "event");
-  HIPCHK(hipEventRecord(rg[2], s), "event");
+  HIPCHK(hipEventRecord(x.decided, s), "event");
+
+  // ---- emit stage (emit stream), overlaps the next batch's decide stage
+  HIPCHK(hipStreamWaitEvent(e->emitS, x.decided, 0), "wait decided");
+  HIPCHK(hipEventRecord(rg[2], e->emitS), "event");
   EmitLaunch m;
-  m.recBase = e->dRecBase;
-  m.byteBase = e->dByteBase;
-  m.slotBase = e->dSlotBase;
-  m.totals = e->dTot + 2;
-  m.tuples = e->dTuples;
+  m.recBase = x.dRecBase;
+  m.byteBase = x.dByteBase;
+  m.slotBase = x.dSlotBase;
+  m.totals = x.dTot + 2;
+  m.tuples = x.dTuples;
   m.pkts = e->curPkts;
   m.arena = e->curArena;
   m.dts = e->dDTs;
   m.ndts = nd;
-  m.out = e->dOut;
-  m.outArena = e->dOutArena;
+  m.out = x.dOut;
+  m.outArena = x.dOutArena;
   m.outCap = e->cfg.max_out_pkts;
   m.outByteCap = e->cfg.max_out_bytes;
-  m.err = e->dErr;
+  m.err = x.dErr;
   m.grid = e->emitGrid;
-  if (nd) HIPCHK(launch_emit(s, m), "emit");
-  HIPCHK(hipEventRecord(e->evt[3], s), "event");
-  HIPCHK(hipEventRecord(rg[3], s), "event");
-  HIPCHK(launch_accumulate(s, e->dStats, e->dTot, e->dCum), "accumulate");
+  if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
+  HIPCHK(hipEventRecord(rg[3], e->emitS), "event");
+  HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum), "accumulate");
+  HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
+  x.used = true;
+  x.checked = false;
+  e->lastCtx = ci;
   e->nRuns++;
   e->haveBatch = false;
-  e->ran = true;
   return LKF_OK;
 }
 
+// Waits for all queued batches; reports the error word of the last batch and
+// of an earlier batch not yet reported.
 int lkf_sync(lkf_engine *e) {
   if (!e) return LKF_EINVAL;
-  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->cur), "sync");
-  if (!e->ran) return LKF_OK;
-  uint32_t err[4] = {0, 0, 0, 0};
-  HIPCHK(hipMemcpy(err, e->dErr, sizeof(err), hipMemcpyDeviceToHost), "err copy");
-  if (err[0] & 3u) {
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  if (e->lastCtx < 0) return LKF_OK;
+  uint32_t acc = 0;
+  for (int i = 0; i < 2; i++) {
+    BatchCtx &x = e->ctx[i];
+    if (!x.used || (x.checked && i != e->lastCtx)) continue;
+    uint32_t err[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpy(err, x.dErr, sizeof(err), hipMemcpyDeviceToHost), "err copy");
+    x.checked = true;
+    acc |= err[0];
+  }
+  if (acc & 3u) {
     e->err = "batch not grouped by track / bad track handle";
     return LKF_EORDER;
   }
-  if (err[0] & 12u) {
+  if (acc & 12u) {
     e->err = "output or tuple capacity exceeded";
     return LKF_ENOSPC;
   }
@@ -603,11 +678,14 @@ int lkf_sync(lkf_engine *e) {
 
 int lkf_get_stats(lkf_engine *e, lkf_stats *out) {
   if (!e || !out) return LKF_EINVAL;
+  std::memset(out, 0, sizeof(*out));
   int rc = lkf_sync(e);
+  if (e->lastCtx < 0) return rc;
+  BatchCtx &x = e->ctx[e->lastCtx];
   uint64_t st[kStatsWords];
   uint64_t tot[4];
-  HIPCHK(hipMemcpy(st, e->dStats, sizeof(st), hipMemcpyDeviceToHost), "stats copy");
-  HIPCHK(hipMemcpy(tot, e->dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  HIPCHK(hipMemcpy(st, x.dStats, sizeof(st), hipMemcpyDeviceToHost), "stats copy");
+  HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
   out->tuples = st[0];
   out->forwarded = st[1];
   out->out_bytes = st[2];
@@ -621,10 +699,18 @@ int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, con
   if (!e) return LKF_EINVAL;
   int rc = lkf_sync(e);
   if (rc) return rc;
+  if (e->lastCtx < 0) {
+    if (d_out) *d_out = e->ctx[0].dOut;
+    if (d_arena) *d_arena = e->ctx[0].dOutArena;
+    if (n_out) *n_out = 0;
+    if (arena_len) *arena_len = 0;
+    return LKF_OK;
+  }
+  BatchCtx &x = e->ctx[e->lastCtx];
   uint64_t tot[4];
-  HIPCHK(hipMemcpy(tot, e->dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
-  if (d_out) *d_out = e->dOut;
-  if (d_arena) *d_arena = e->dOutArena;
+  HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  if (d_out) *d_out = x.dOut;
+  if (d_arena) *d_arena = x.dOutArena;
   if (n_out) *n_out = tot[2];
   if (arena_len) *arena_len = tot[3];
   return LKF_OK;
@@ -632,8 +718,8 @@ int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, con
 
 int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap, uint64_t *n_out,
               uint64_t *arena_len) {
-  const lkf_out *dOut;
-  const uint8_t *dAr;
+  const lkf_out *dOut = nullptr;
+  const uint8_t *dAr = nullptr;
   uint64_t n = 0, len = 0;
   int rc = lkf_output_device(e, &dOut, &n, &dAr, &len);
   if (rc) return rc;
@@ -647,11 +733,10 @@ int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_
 
 int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *o) {
   if (!e || !o || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
-  {
-    int frc = flush_topology(e);
-    if (frc) return frc;
-  }
-  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
   DTHot h;
   HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "state copy");
   std::memset(o, 0, sizeof(*o));
@@ -680,12 +765,11 @@ int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *o) {
 
 int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *i) {
   if (!e || !i || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
-  {
-    int frc = flush_topology(e);
-    if (frc) return frc;
-  }
   if (!i->started) return LKF_OK;  // SeedState forwarder.go:360-362
-  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
   DTHot h;
   HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "state copy");
   auto setf = [&](uint32_t f, bool v) { h.flags = v ? (h.flags | f) : (h.flags & ~f); };
@@ -718,12 +802,10 @@ int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *i) {
 int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns, lkf_seq_meta *out,
                    uint32_t *n_out) {
   if (!e || dt < 0 || dt >= int32_t(e->dtp.size()) || (n && (!sns || !out))) return LKF_EINVAL;
-  {
-    int frc = flush_topology(e);
-    if (frc) return frc;
-  }
-  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
   if (n > e->seqScratchCap) {
     if (e->dSns) (void)hipFree(e->dSns);
     if (e->dSeqOut) (void)hipFree(e->dSeqOut);
@@ -745,41 +827,39 @@ int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, i
 }
 
 int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *total_ms) {
-  if (!e || !e->ran) return LKF_EINVAL;
-  HIPCHK(hipEventSynchronize(e->evt[3]), "evsync");
-  float a = 0, b = 0, c = 0;
-  HIPCHK(hipEventElapsedTime(&a, e->evt[0], e->evt[1]), "elapsed");
-  HIPCHK(hipEventElapsedTime(&b, e->evt[2], e->evt[3]), "elapsed");
-  HIPCHK(hipEventElapsedTime(&c, e->evt[0], e->evt[3]), "elapsed");
-  if (decide_ms) *decide_ms = a;
-  if (emit_ms) *emit_ms = b;
-  if (total_ms) *total_ms = c;
-  return LKF_OK;
+  return lkf_timing_window(e, 1, decide_ms, emit_ms, total_ms);
 }
 
+// decide = sum of the k_decide-stage spans, emit = sum of the k_emit spans,
+// total = GPU span from the first run's start to the last run's emit end
+// (stages overlap across batches, so total < decide + emit).
 int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_ms, float *total_ms) {
-  if (!e || n == 0 || n > lkf_engine::kRing || n > e->nRuns) return LKF_EINVAL;
-  float sa = 0, sb = 0, sc = 0;
-  for (uint64_t r = e->nRuns - n; r < e->nRuns; r++) {
+  if (!e || n == 0 || n > uint32_t(lkf_engine::kRing) || n > e->nRuns) return LKF_EINVAL;
+  float sa = 0, sb = 0;
+  const uint64_t first = e->nRuns - n;
+  for (uint64_t r = first; r < e->nRuns; r++) {
     hipEvent_t *rg = e->ring[r % lkf_engine::kRing];
     HIPCHK(hipEventSynchronize(rg[3]), "evsync");
-    float a = 0, b = 0, c = 0;
+    float a = 0, b = 0;
     HIPCHK(hipEventElapsedTime(&a, rg[0], rg[1]), "elapsed");
     HIPCHK(hipEventElapsedTime(&b, rg[2], rg[3]), "elapsed");
-    HIPCHK(hipEventElapsedTime(&c, rg[0], rg[3]), "elapsed");
     sa += a;
     sb += b;
-    sc += c;
   }
+  float c = 0;
+  HIPCHK(hipEventElapsedTime(&c, e->ring[first % lkf_engine::kRing][0],
+                             e->ring[(e->nRuns - 1) % lkf_engine::kRing][3]),
+         "elapsed");
   if (decide_ms) *decide_ms = sa;
   if (emit_ms) *emit_ms = sb;
-  if (total_ms) *total_ms = sc;
+  if (total_ms) *total_ms = c;
   return LKF_OK;
 }
 
 int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset) {
   if (!e || !out) return LKF_EINVAL;
-  HIPCHK(hipStreamSynchronize(e->cur), "sync");
+  int rc = drain_streams(e);
+  if (rc) return rc;
   uint64_t st[kStatsWords];
   HIPCHK(hipMemcpy(st, e->dCum, sizeof(st), hipMemcpyDeviceToHost), "cum copy");
   out->tuples = st[0];

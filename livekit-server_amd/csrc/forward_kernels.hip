@@ -25,6 +25,10 @@
 #include "fwd_state.h"
 #include "kernels.h"
 
+#ifndef LKF_ABLATE
+#define LKF_ABLATE 0
+#endif
+
 namespace lkf {
 
 using u8 = uint8_t;
@@ -217,6 +221,26 @@ __device__ __forceinline__ void mg_packetDropped(Lane &L, u64 esn) {  // :156-18
 enum { ORD_CONTIG = 0, ORD_OOO = 1, ORD_GAP = 2, ORD_DUP = 3 };
 enum { MG_OK = 0, MG_PADDING, MG_DUP, MG_OOO_MISS };
 // UpdateAndGetSnTs :183-271
+// in-order branch of UpdateAndGetSnTs (rtpmunger.go:186-217), diff >= 1
+__device__ __forceinline__ void mg_inorder(Lane &L, const PktV &p, bool marker, u64 &osn, u64 &ots) {
+  L.h.extHighestIncomingSN = p.esn;
+  u64 msn = p.esn - L.h.snOffset;
+  u64 mts = p.ets - L.h.tsOffset;
+  L.h.extSecondLastSN = L.h.extLastSN;
+  L.h.extLastSN = msn;
+  L.h.extSecondLastTS = L.h.extLastTS;
+  L.h.extLastTS = mts;
+  setf(L, F_SECOND_LAST_MARKER, hasf(L, F_LAST_MARKER));
+  setf(L, F_LAST_MARKER, marker);
+  if (p.flags & LKF_PKT_KEYFRAME) {
+    L.h.extRtxGateSn = msn;
+    setf(L, F_RTX_GATE, true);
+  }
+  if (hasf(L, F_RTX_GATE) && (msn - L.h.extRtxGateSn) > 2000) setf(L, F_RTX_GATE, false);
+  osn = msn;
+  ots = mts;
+}
+
 __device__ int mg_update(Lane &L, const PktV &p, bool marker, int &ord, u64 &osn, u64 &ots) {
   i64 diff = i64(p.esn - L.h.extHighestIncomingSN);
   if ((diff == 1 && p.plen != 0) || diff > 1) {
@@ -423,7 +447,8 @@ __device__ __forceinline__ int vp8_marshal(u8 first, bool I, bool M, u16 pid, bo
 
 enum { CM_OK = 0, CM_FILTERED, CM_PICID_MISS, CM_ERR };
 // VP8.UpdateAndGet vp8.go:161-302
-__device__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool gap, i32 maxTL, u64 &cb, int &cbLen) {
+__device__ __forceinline__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool gap, i32 maxTL, u64 &cb,
+                                           int &cbLen) {
   const bool I = p.vbits & LKF_VP8_I, M = p.vbits & LKF_VP8_M, Lb = p.vbits & LKF_VP8_L;
   const bool T = p.vbits & LKF_VP8_T, Y = p.vbits & LKF_VP8_Y, K = p.vbits & LKF_VP8_K;
   i32 ext = wr_unwrap(L, p.pid, M);
@@ -761,6 +786,25 @@ __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
 __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, u64 cb,
                          int cbLen) {
   const u32 size = L.seqSize;
+  if (hasf(L, F_SEQ_INIT) && esn == L.h.seqExtHighestSN + 1) {  // in-order: next slot, nothing skipped
+    u32 slot = u32(L.h.seqHighSlot) + 1;
+    if (slot == size) slot = 0;
+    SeqMeta m = {};
+    m.sourceSeqNo = u16(inSN);
+    m.targetSeqNo = u16(esn);
+    m.timestamp = u32(ets);
+    m.lastNack = u32(arrMs - L.h.seqStartMs);
+    m.marker = marker;
+    m.layer = layer;
+    m.codecLen = u8(cbLen);
+#pragma unroll
+    for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+    L.seq[slot] = m;
+    L.h.seqExtHighestSN = esn;
+    L.h.seqHighSlot = u16(slot);
+    if (ets > L.h.seqExtHighestTS) L.h.seqExtHighestTS = ets;
+    return;
+  }
   if (!hasf(L, F_SEQ_INIT)) {
     setf(L, F_SEQ_INIT, true);
     L.h.seqExtStartSN = esn;
@@ -1012,8 +1056,108 @@ struct LaneOut {
 
 __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneOut &o) {
   o.nTuples++;
+#if LKF_ABLATE == 3  // diagnostic: empty per-packet body (staging loop only)
+  o.relOff += u32(p.esn) & 1;
+  return;
+#endif
   Fwd f;
-  int dr = fw_translate(L, p, f);
+#if LKF_ABLATE == 2  // diagnostic: translate replaced by a trivial decision
+  f.osn = p.esn;
+  f.ots = p.ets;
+  f.switching = f.resuming = false;
+  f.marker = false;
+  f.cbLen = 0;
+  f.cb = 0;
+  int dr = (p.layer == L.h.tgtS || !hasf(L, F_VIDEO)) ? -1 : LKF_DROP_NOT_SELECTED;
+#else
+  // Fast classification (pre-state + packet only); anything not covered
+  // takes the full restatement fw_translate.  Each fast case is exactly the
+  // path forwarder.go would take for it:
+  //   muted/pubMuted -> drop (:1440); video with invalid target -> drop (:1687);
+  //   no switch possible in Simulcast.Select and layer != current -> drop (:1694);
+  //   pause-on-downgrade -> drop (:1709);
+  //   same SSRC, contiguous SN with payload -> UpdateAndGetSnTs in-order branch,
+  //   then (video) SelectTemporal + VP8 UpdateAndGet without gap/OOO.
+  const u32 fl = L.h.flags;
+  const bool contig = p.ssrc == L.h.lastSSRC && p.plen != 0 && p.esn == L.h.extHighestIncomingSN + 1;
+  int dr;
+  f.switching = f.resuming = false;
+  f.cbLen = 0;
+  f.cb = 0;
+  f.ord = ORD_CONTIG;
+  int cls;  // -1 fast forward, -2 slow, >= 0 drop
+  const i32 layer = p.layer;
+  const bool kf = p.flags & LKF_PKT_KEYFRAME;
+  if (fl & (F_MUTED | F_PUBMUTED)) {
+    cls = LKF_DROP_MUTED;
+  } else if (!(fl & F_VIDEO)) {
+    cls = contig ? -1 : -2;
+  } else if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) {
+    cls = LKF_DROP_PAUSED;
+  } else if (!(fl & F_SIMULCAST)) {
+    cls = LKF_DROP_NOT_SELECTED;
+  } else {
+    const bool willSwitch =
+        kf && ((L.h.curS != L.h.tgtS && ((layer > L.h.curS && layer <= L.h.tgtS) ||
+                                         (layer < L.h.curS && layer >= L.h.tgtS))) ||
+               (L.h.curS > L.h.maxS && layer <= L.h.maxS));
+    if (willSwitch)
+      cls = -2;
+    else if (layer != L.h.curS)
+      cls = LKF_DROP_NOT_SELECTED;
+    else if ((fl & F_DEFICIENT) && L.h.tgtS < L.h.curS)
+      cls = LKF_DROP_DOWNGRADE;
+    else if (contig && (fl & F_VP8) && (p.flags & LKF_PKT_VP8) && (fl & F_TLS_VP8))
+      cls = -1;
+    else
+      cls = -2;
+  }
+  if (cls >= 0) {
+    dr = cls;
+  } else if (cls == -2) {
+    dr = fw_translate(L, p, f);
+  } else if (!(fl & F_VIDEO)) {
+    f.marker = false;
+    mg_inorder(L, p, false, f.osn, f.ots);
+    dr = -1;
+  } else {
+    const bool pktMarker = p.hdr1 & 0x80;
+    f.marker = pktMarker;
+    mg_inorder(L, p, pktMarker, f.osn, f.ots);
+    // SelectTemporal (base.go:143-168, temporallayerselector/vp8.go:32-56)
+    i32 tl = L.h.curT;
+    bool tSwitch = false;
+    {
+      const i32 cur = L.h.curT, tgt = L.h.tgtT;
+      i32 nxt = cur;
+      if (cur != tgt && (p.vbits & LKF_VP8_T)) {
+        const i32 tid = i32(p.tid);
+        if (cur < tgt) {
+          if (tid > cur && tid <= tgt && (p.vbits & LKF_VP8_S) && (p.vbits & LKF_VP8_Y)) {
+            tl = tid;
+            nxt = tid;
+          }
+        } else if (pktMarker) {
+          nxt = tgt;
+        }
+      }
+      if (nxt != L.h.curT) {
+        tSwitch = true;
+        L.h.prevS = L.h.curS;
+        L.h.prevT = L.h.curT;
+        L.h.curT = nxt;
+      }
+    }
+    const int cr = vp8_update(L, p, false, false, tl, f.cb, f.cbLen);
+    if (cr != CM_OK) {
+      if (cr == CM_FILTERED) mg_packetDropped(L, p.esn);
+      if (tSwitch) vls_rollback(L);
+      dr = cr == CM_FILTERED ? LKF_DROP_TEMPORAL : cr == CM_PICID_MISS ? LKF_DROP_PICID_MISS : LKF_DROP_OTHER;
+    } else {
+      dr = -1;
+    }
+  }
+#endif
   if (dr >= 0) {
 #pragma unroll
     for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] += (dr == i) ? 1u : 0u;
@@ -1043,9 +1187,11 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   for (int i = 0; i < 6; i++) t.codec[i] = u8(f.cb >> (8 * i));
   t.hdrLen = u8(hdrLen);
   for (int i = 0; i < 12; i++) t.pad[i] = 0;
+#if LKF_ABLATE != 1  // diagnostic builds only (never shipped): 1 = no tuple/sequencer writes
   o.outT[o.nFwd] = t;
   // sequencer.push (downtrack.go:724-735)
   seq_push(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
+#endif
   // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
   if (!hasf(L, F_STATS_INIT) && payLen > 0) {
     setf(L, F_STATS_INIT, true);
