@@ -154,9 +154,14 @@ def main():
     dec_ms, emit_ms, tot_ms = eng.timing_window(args.steps)
 
     fwd = cum["forwarded"]
+    steps_pkts = sum(meta[b][0] for b in range(args.warmup, nb))
     algo, b_in = algorithmic_bytes(trace, range(args.warmup, nb), fwd, cum["out_bytes"], trace.ndts)
-    # emit kernel's own algorithmic bytes: wire bytes + 40-B records written, input payload read once
-    emit_bytes = cum["out_bytes"] + 40 * fwd + (b_in - 64 * sum(meta[b][0] for b in range(args.warmup, nb)))
+    payload_in = b_in - 64 * steps_pkts
+    # per-kernel algorithmic bytes (the two halves of SURVEY.md §8(d)'s B):
+    #   decide: packet descriptors once + sequencer record per forwarded tuple + DT hot state
+    #   emit:   input payload once + wire bytes + one 40-B output record per forwarded tuple
+    decide_bytes = 64 * steps_pkts + 32 * fwd + 256 * trace.ndts * args.steps
+    emit_bytes = payload_in + cum["out_bytes"] + 40 * fwd
     if dist:
         t = torch.tensor([elapsed, float(fwd), float(algo), tot_ms, emit_ms], dtype=torch.float64, device=dev)
         tmax = t.clone()
@@ -168,14 +173,23 @@ def main():
         fwd_all = float(fwd)
 
     if rank == 0:
-        emit_avg_s = emit_ms / 1e3 / args.steps
-        achieved = emit_bytes / args.steps / emit_avg_s / 1e9 if emit_avg_s > 0 else 0.0
+        def kern(name, nbytes, ms_sum):
+            avg_s = ms_sum / 1e3 / args.steps
+            ach = nbytes / args.steps / avg_s / 1e9 if avg_s > 0 else 0.0
+            return {"kernel": name, "avg_ms": round(ms_sum / args.steps, 4),
+                    "algorithmic_bytes_per_launch": int(nbytes // args.steps),
+                    "achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBPS, 4)}
+
+        kd = kern("k_decide" if os.environ.get("LKF_DECIDE") == "track" else "k_decide_dt", decide_bytes, dec_ms)
+        ke = kern("k_emit", emit_bytes, emit_ms)
+        dom = kd if kd["avg_ms"] >= ke["avg_ms"] else ke
         traffic = None
         if args.pmc_csv and os.path.exists(args.pmc_csv):
             try:
-                traffic = json.load(open(args.pmc_csv)).get("emit_hbm_bytes_per_launch")
+                traffic = json.load(open(args.pmc_csv)).get(dom["kernel"] + "_hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        pipe_ach = algo / (tot_ms / 1e3) / 1e9 if tot_ms else 0.0
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             thr = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -200,12 +214,15 @@ def main():
                                    "18,000 DownTracks, 2%% loss, 1%% reorder, layer switching" % args.rooms,
                        "batch": "%.3g s of media per step" % args.batch_s,
                        "parallelism": "room-sharded x%d" % world},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
-                         "kernel": "k_emit", "emit_ms_avg": round(emit_ms / args.steps, 4),
-                         "decide_ms_avg": round(dec_ms / args.steps, 4),
-                         "gpu_ms_per_step": round(tot_ms / args.steps, 4),
-                         "pipeline_algorithmic_GBps": round(algo / (tot_ms / 1e3) / 1e9, 1) if tot_ms else None},
+            "roofline": {"bound": "hbm", "achieved": dom["achieved"], "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": dom["frac"], "traffic": traffic, "kernel": dom["kernel"],
+                         "avg_ms": dom["avg_ms"],
+                         "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
+                         "kernels": [kd, ke],
+                         "pipeline": {"bytes_per_step": int(algo // args.steps),
+                                      "gpu_ms_per_step": round(tot_ms / args.steps, 4),
+                                      "achieved": round(pipe_ach, 1),
+                                      "frac": round(pipe_ach / PEAK_HBM_GBPS, 4)}},
             "cpu_baseline": cpu,
             "tuples_per_step": cum["tuples"] // args.steps,
             "forwarded_per_step": fwd // args.steps,

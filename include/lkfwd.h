@@ -268,8 +268,10 @@ int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, i
 /* ---- introspection ------------------------------------------------------ */
 /* Duration of the last batch's decide kernel, emit kernel and whole batch, ms. */
 int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *total_ms);
-/* Sums of the same over the last n runs (n <= 256), from HIP events recorded
- * on the run stream; synchronises on the newest. */
+/* Over the last n runs (n <= 256): sums of the decide-kernel and emit-kernel
+ * durations, and the GPU span from the first run's start to the last run's
+ * emit end (stages overlap across runs).  HIP events recorded on the engine's
+ * decide and emit streams; synchronises on the newest. */
 int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_ms, float *total_ms);
 /* Counters accumulated on the GPU over all runs since the last reset. */
 int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset);

@@ -5,11 +5,12 @@
 // pipeline (forward_kernels.hip).  There is no CPU forwarding path: every
 // per-packet decision runs in the gfx950 kernels.
 //
-// Two-stage pipeline across batches.  Batch n's "decide" stage (track ranges,
-// slot scan, k_decide, output scan) runs on the run stream; its "emit" stage
-// (k_emit, counters) runs on an engine-owned emit stream after an event.  The
-// decide of batch n+1 depends only on decide n (DownTrack state), so it
-// overlaps emit n.  Per-batch scratch and outputs are double-buffered by run
+// Two-stage pipeline across batches.  Batch n's "decide" stage (batch init,
+// track ranges, slot scan, k_decide, output scan) runs on the engine's
+// high-priority decide stream after the caller's stream (which orders the
+// batch's inputs); its "emit" stage (k_emit, counters) runs on a low-priority
+// emit stream after an event.  The decide of batch n+1 depends only on decide
+// n (DownTrack state), so it overlaps emit n.  Per-batch scratch and outputs are double-buffered by run
 // parity: batch n's outputs stay valid until run n+2 is enqueued, and a
 // device batch's input buffers must stay valid until its emit stage is done
 // (lkf_sync, or the enqueue of run n+2).
@@ -17,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -51,7 +53,7 @@ struct BatchCtx {
   uint64_t *dStats = nullptr;
   lkf_pkt *dPktsOwn = nullptr;  // lkf_submit copies land here
   uint8_t *dArenaOwn = nullptr;
-  hipEvent_t decided = nullptr;  // decide stage done (run stream)
+  hipEvent_t decided = nullptr;  // decide stage done (decide stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
   bool used = false;
   bool checked = false;  // error word already reported by lkf_sync
@@ -61,9 +63,11 @@ struct BatchCtx {
 
 struct lkf_engine {
   int dev = 0;
-  hipStream_t own = nullptr;    // default run stream, copies, lookups
-  hipStream_t emitS = nullptr;  // emit stage
-  hipStream_t cur = nullptr;    // run stream of the last lkf_run
+  hipStream_t own = nullptr;    // copies, lookups
+  hipStream_t decS = nullptr;   // decide stage (high priority)
+  hipStream_t emitS = nullptr;  // emit stage (low priority)
+  hipStream_t cur = nullptr;    // caller's stream of the last lkf_run
+  hipEvent_t inEv = nullptr;    // caller-stream work before a run
   lkf_cfg cfg{};
   std::string err;
 
@@ -127,11 +131,15 @@ struct lkf_engine {
   uint32_t *dSeqN = nullptr;
   uint32_t seqScratchCap = 0;
 
-  // timing ring: [0] decide-stage start, [1] k_decide end (run stream),
-  // [2] emit start, [3] emit end (emit stream)
+  // timing ring: [0] decide-stage start, [1] decide kernel start, [2] decide
+  // kernel end (decide stream), [3] emit kernel start, [4] emit kernel end
+  // (emit stream)
   static constexpr int kRing = 256;
-  hipEvent_t ring[kRing][4] = {};
+  hipEvent_t ring[kRing][5] = {};
   uint32_t emitGrid = 2048;
+  // 1: k_decide_dt (one wave per DownTrack, lanes = packets; default)
+  // 0: k_decide (one lane per DownTrack, one wave per track)
+  int decideMode = 1;
 };
 
 static int fail(lkf_engine *e, const char *what, hipError_t r) {
@@ -187,6 +195,7 @@ static int drain_streams(lkf_engine *e) {
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (e->cur && e->cur != e->own) HIPCHK(hipStreamSynchronize(e->cur), "sync run stream");
   HIPCHK(hipStreamSynchronize(e->own), "sync own stream");
+  HIPCHK(hipStreamSynchronize(e->decS), "sync decide stream");
   HIPCHK(hipStreamSynchronize(e->emitS), "sync emit stream");
   return LKF_OK;
 }
@@ -237,8 +246,14 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   const lkf_cfg &c = e->cfg;
   bool ok = true;
   auto A = [&](hipError_t r) { ok = ok && (r == hipSuccess); };
+  // decide is the batch-to-batch critical path: its waves should win CU slots
+  // over the emit stage of the previous batch when both are resident.
+  int leastPrio = 0, greatestPrio = 0;
+  A(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
   A(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
-  A(hipStreamCreateWithFlags(&e->emitS, hipStreamNonBlocking));
+  A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
+  A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
+  A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
   e->cur = e->own;
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
@@ -288,7 +303,12 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   }
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device);
-  e->emitGrid = uint32_t(cus) * 8;
+  // emit is grid-stride: 4 workgroups (16 waves) per CU saturate HBM and
+  // leave wave slots for the next batch's decide stage.
+  if (const char *v = getenv("LKF_DECIDE")) e->decideMode = strcmp(v, "track") == 0 ? 0 : 1;
+  int perCU = 4;
+  if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
+  e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   return e;
 }
 
@@ -297,6 +317,7 @@ void lkf_destroy(lkf_engine *e) {
   (void)hipSetDevice(e->dev);
   if (e->cur && e->cur != e->own) (void)hipStreamSynchronize(e->cur);
   if (e->own) (void)hipStreamSynchronize(e->own);
+  if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dEvOff, e->dEvents, e->dCum, e->dSns, e->dSeqOut, e->dSeqN};
@@ -319,7 +340,9 @@ void lkf_destroy(lkf_engine *e) {
     if (sg.off) (void)hipHostFree(sg.off);
     if (sg.done) (void)hipEventDestroy(sg.done);
   }
+  if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
+  if (e->decS) (void)hipStreamDestroy(e->decS);
   if (e->own) (void)hipStreamDestroy(e->own);
   delete e;
 }
@@ -464,6 +487,13 @@ static int rebuild_sched(lkf_engine *e) {
   e->waveTrack.clear();
   for (uint32_t t : order) {
     const auto &v = byTrack[t];
+    if (e->decideMode == 1) {  // one wave per DownTrack
+      for (uint32_t d : v) {
+        e->sched.push_back(d);
+        e->waveTrack.push_back(t);
+      }
+      continue;
+    }
     for (size_t i = 0; i < v.size(); i += 64) {
       e->waveTrack.push_back(t);
       for (size_t j = 0; j < 64; j++) e->sched.push_back(i + j < v.size() ? v[i + j] : kIdle);
@@ -482,7 +512,7 @@ static int rebuild_sched(lkf_engine *e) {
     e->schedCap = nl + 1 + 4096;
     HIPCHK(dalloc(&e->dSched, e->schedCap), "alloc sched");
     HIPCHK(dalloc(&e->dEvOff, e->schedCap + 1), "alloc evoff");
-    HIPCHK(dalloc(&e->dWaveTrack, e->schedCap / 64 + 1), "alloc wavetrack");
+    HIPCHK(dalloc(&e->dWaveTrack, e->schedCap + 1), "alloc wavetrack");
   }
   if (nl) {
     HIPCHK(hipMemcpy(e->dSched, e->sched.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice), "sched copy");
@@ -513,13 +543,13 @@ int lkf_run(lkf_engine *e, void *stream) {
     e->curN = 0;
     e->curArenaLen = 0;
   }
-  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e->own;
-  if (s != e->cur && e->nRuns) {
-    // a different run stream: order after everything the previous one queued
-    int rc = drain_streams(e);
-    if (rc) return rc;
-  }
-  e->cur = s;
+  // The caller's stream orders the batch's inputs; the stages themselves run
+  // on the engine's decide/emit streams (completion: lkf_sync).
+  hipStream_t us = stream ? reinterpret_cast<hipStream_t>(stream) : e->own;
+  e->cur = us;
+  hipStream_t s = e->decS;
+  HIPCHK(hipEventRecord(e->inEv, us), "event");
+  HIPCHK(hipStreamWaitEvent(s, e->inEv, 0), "wait caller stream");
   const uint32_t nt = uint32_t(e->tracks.size());
   const uint32_t nd = uint32_t(e->dtp.size());
   const uint32_t nl = uint32_t(e->sched.size());
@@ -573,22 +603,18 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipEventRecord(sg.done, s), "stage record");
   sg.used = true;
 
-  HIPCHK(hipMemsetAsync(x.dTBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(x.dTEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(x.dTRuns, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(x.dErr, 0, 4 * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(x.dStats, 0, kStatsWords * sizeof(uint64_t), s), "memset");
-  HIPCHK(hipMemsetAsync(x.dFwdCnt, 0, size_t(std::max(nd, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(x.dFwdBytes, 0, size_t(std::max(nd, 1u)) * sizeof(uint64_t), s), "memset");
-
-  // ---- decide stage (run stream)
+  // ---- decide stage (decide stream)
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
   HIPCHK(hipEventRecord(rg[0], s), "event");
+  HIPCHK(launch_batch_init(s, nt, nd, kStatsWords, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dStats, x.dFwdCnt,
+                           x.dFwdBytes),
+         "batch init");
   HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr), "track_ranges");
   HIPCHK(launch_scan(s, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
                      x.dTot + 0, nullptr),
          "slot scan");
   DecideLaunch d;
+  d.mode = e->decideMode;
   d.sched = e->dSched;
   d.waveTrack = e->dWaveTrack;
   d.nlanes = nl;
@@ -611,8 +637,9 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.fwdCnt = x.dFwdCnt;
   d.fwdBytes = x.dFwdBytes;
   d.stats = x.dStats;
-  HIPCHK(launch_decide(s, d), "decide");
   HIPCHK(hipEventRecord(rg[1], s), "event");
+  HIPCHK(launch_decide(s, d), "decide");
+  HIPCHK(hipEventRecord(rg[2], s), "event");
   HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
                      x.dByteBase, x.dTot + 2, x.dTot + 3),
          "out scan");
@@ -620,7 +647,7 @@ int lkf_run(lkf_engine *e, void *stream) {
 
   // ---- emit stage (emit stream), overlaps the next batch's decide stage
   HIPCHK(hipStreamWaitEvent(e->emitS, x.decided, 0), "wait decided");
-  HIPCHK(hipEventRecord(rg[2], e->emitS), "event");
+  HIPCHK(hipEventRecord(rg[3], e->emitS), "event");
   EmitLaunch m;
   m.recBase = x.dRecBase;
   m.byteBase = x.dByteBase;
@@ -638,7 +665,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.err = x.dErr;
   m.grid = e->emitGrid;
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
-  HIPCHK(hipEventRecord(rg[3], e->emitS), "event");
+  HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum), "accumulate");
   HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
   x.used = true;
@@ -830,7 +857,7 @@ int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *tot
   return lkf_timing_window(e, 1, decide_ms, emit_ms, total_ms);
 }
 
-// decide = sum of the k_decide-stage spans, emit = sum of the k_emit spans,
+// decide = sum of the decide-kernel spans, emit = sum of the k_emit spans,
 // total = GPU span from the first run's start to the last run's emit end
 // (stages overlap across batches, so total < decide + emit).
 int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_ms, float *total_ms) {
@@ -839,21 +866,32 @@ int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_m
   const uint64_t first = e->nRuns - n;
   for (uint64_t r = first; r < e->nRuns; r++) {
     hipEvent_t *rg = e->ring[r % lkf_engine::kRing];
-    HIPCHK(hipEventSynchronize(rg[3]), "evsync");
+    HIPCHK(hipEventSynchronize(rg[4]), "evsync");
     float a = 0, b = 0;
-    HIPCHK(hipEventElapsedTime(&a, rg[0], rg[1]), "elapsed");
-    HIPCHK(hipEventElapsedTime(&b, rg[2], rg[3]), "elapsed");
+    HIPCHK(hipEventElapsedTime(&a, rg[1], rg[2]), "elapsed");
+    HIPCHK(hipEventElapsedTime(&b, rg[3], rg[4]), "elapsed");
     sa += a;
     sb += b;
   }
   float c = 0;
   HIPCHK(hipEventElapsedTime(&c, e->ring[first % lkf_engine::kRing][0],
-                             e->ring[(e->nRuns - 1) % lkf_engine::kRing][3]),
+                             e->ring[(e->nRuns - 1) % lkf_engine::kRing][4]),
          "elapsed");
   if (decide_ms) *decide_ms = sa;
   if (emit_ms) *emit_ms = sb;
   if (total_ms) *total_ms = c;
   return LKF_OK;
+}
+
+// Not part of include/lkfwd.h: counters of a diagnostic build (-DLKF_DIAG=1).
+int lkf_debug_counters(lkf_engine *e, uint64_t out[16], int reset) {
+  if (!e || !out) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  unsigned long long v[16];
+  hipError_t r = read_diag(v, reset);
+  for (int i = 0; i < 16; i++) out[i] = v[i];
+  return r == hipSuccess ? LKF_OK : LKF_ENODEV;
 }
 
 int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset) {

@@ -102,6 +102,8 @@ struct Lane {
   VP8Cold *vc;
   i32 *dropKey;  // LDS copy of vc->dropKey (this lane's row)
   i32 *exKey;    // LDS copy of vc->exKey
+  i32 *missKey;  // vc->missKey (k_decide) or its LDS copy (k_decide_dt)
+  i32 *missVal;
   SeqMeta *seq;
   u32 seqSize;
   // track
@@ -288,7 +290,7 @@ __device__ int mg_update(Lane &L, const PktV &p, bool marker, int &ord, u64 &osn
 __device__ __forceinline__ int miss_find(const Lane &L, i32 key) {
   for (int i = 0; i < L.h.missCount; i++) {
     int idx = (L.h.missHead + i) % kMissCap;
-    if (L.vc->missKey[idx] == key) return idx;
+    if (L.missKey[idx] == key) return idx;
   }
   return -1;
 }
@@ -322,9 +324,9 @@ __device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
   int inE = 0;  // existing (not dropped) keys inside the range
   for (int i = 0; i < e0; i++) {
     int idx = (L.h.missHead + i) % kMissCap;
-    i32 k = L.vc->missKey[idx];
+    i32 k = L.missKey[idx];
     if (k >= prevMax && k <= ext && !dropped_has(L, k)) {
-      L.vc->missVal[idx] = off;
+      L.missVal[idx] = off;
       inE++;
     }
   }
@@ -353,8 +355,8 @@ __device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
   for (i32 k = s;; k++) {
     if (!dropped_has(L, k) && miss_find(L, k) < 0) {
       int idx = (L.h.missHead + L.h.missCount) % kMissCap;
-      L.vc->missKey[idx] = k;
-      L.vc->missVal[idx] = off;
+      L.missKey[idx] = k;
+      L.missVal[idx] = off;
       L.h.missCount++;
     }
     if (k == ext) break;
@@ -455,7 +457,7 @@ __device__ __forceinline__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool
   if (ooo) {
     int idx = miss_find(L, ext);
     if (idx < 0) return CM_PICID_MISS;
-    i32 off = L.vc->missVal[idx];
+    i32 off = L.missVal[idx];
     u16 mpid = u16((ext - off) & 0x7fff);
     bool mM = mpid > 127;
     int hs = int(p.vhs) + (mM == M ? 0 : (mM ? 1 : -1));
@@ -862,6 +864,30 @@ __device__ __forceinline__ u64 wave_sum(u64 v) {
 }
 
 // ---------------------------------------------------------------------------
+// k_batch_init: zeroes one batch context's per-track ranges, per-DownTrack
+// forward counters, error word and counters (one launch instead of seven
+// fills ahead of the decide stage).
+// ---------------------------------------------------------------------------
+__global__ void k_batch_init(u32 ntracks, u32 ndts, u32 nstats, u32 *__restrict__ tBegin, u32 *__restrict__ tEnd,
+                             u32 *__restrict__ tRuns, u32 *__restrict__ err, u64 *__restrict__ stats,
+                             u32 *__restrict__ fwdCnt, u64 *__restrict__ fwdBytes) {
+  const u32 stride = gridDim.x * blockDim.x;
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < ntracks || i < ndts || i < nstats || i < 4; i += stride) {
+    if (i < ntracks) {
+      tBegin[i] = 0;
+      tEnd[i] = 0;
+      tRuns[i] = 0;
+    }
+    if (i < ndts) {
+      fwdCnt[i] = 0;
+      fwdBytes[i] = 0;
+    }
+    if (i < nstats) stats[i] = 0;
+    if (i < 4) err[i] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_track_ranges: packets grouped by track -> [begin, end) (+ grouping check)
 // ---------------------------------------------------------------------------
 __global__ void k_track_ranges(const lkf_pkt *__restrict__ pkts, u32 n, u32 ntracks, u32 *__restrict__ tBegin,
@@ -1238,6 +1264,8 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs A, const lkf_pkt *__re
     L.vc = A.vc + d;
     L.dropKey = sDrop[threadIdx.x];
     L.exKey = sEx[threadIdx.x];
+    L.missKey = L.vc->missKey;
+    L.missVal = L.vc->missVal;
     if (L.h.flags & F_VP8) {
       const uint4 *gd = reinterpret_cast<const uint4 *>(L.vc->dropKey);
       const uint4 *ge = reinterpret_cast<const uint4 *>(L.vc->exKey);
@@ -1322,6 +1350,467 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs A, const lkf_pkt *__re
   for (int i = 0; i < LKF_DROP_NREASONS; i++) {
     v = wave_sum(u64(o.drops[i]));
     if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[4 + i], (unsigned long long)v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_decide_dt: one wave per DownTrack, lanes = packets of its track.
+//
+// The per-DownTrack recurrence is serial in the reference (one Forwarder
+// behind a mutex), but almost every packet takes a branch whose effect on
+// the state is a prefix count: packets of other simulcast layers are dropped
+// without touching state (simulcast.go:42-122 with no switch possible), and
+// in-order contiguous packets of the current layer either forward with
+// SN = esn - snOffset (rtpmunger.go:186-217) or are dropped by the VP8
+// temporal filter, which shifts snOffset and pictureIdOffset by one
+// (rtpmunger.go:156-181, vp8.go:266-280).  A chunk of 64 packets is loaded
+// one per lane; every lane classifies its packet against the DownTrack state
+// at the start of the run; the longest prefix of lanes whose packets are
+// covered is decided in parallel (ballot + popcount prefixes give the
+// offsets, output slots and sequencer slots), and the state is advanced once.
+// The first packet that is not covered (gap, reorder, duplicate, layer or
+// temporal switch point, keyframe, SSRC change, picture-id wrap, pending
+// control op) goes through decide_step — the full restatement — executed by
+// the whole wave on the broadcast packet, and the run restarts after it.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u32 rl32(u32 v, u32 l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ u64 rl64(u64 v, u32 l) {
+  return (u64(rl32(u32(v >> 32), l)) << 32) | u64(rl32(u32(v), l));
+}
+__device__ __forceinline__ u32 sh32(u32 v, int src) { return u32(__shfl(int(v), src, 64)); }
+__device__ __forceinline__ u64 sh64(u64 v, int src) {
+  return (u64(sh32(u32(v >> 32), src)) << 32) | u64(sh32(u32(v), src));
+}
+__device__ __forceinline__ int prev_in(u64 m, u64 lt) {  // highest set lane below this one, or -1
+  const u64 pm = m & lt;
+  return pm ? 63 - __clzll(pm) : -1;
+}
+__device__ __forceinline__ u32 excl_scan_u32(u32 v, u32 lane) {
+  u32 x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    u32 y = u32(__shfl_up(int(x), o, 64));
+    if (lane >= u32(o)) x += y;
+  }
+  return x - v;
+}
+__device__ __forceinline__ u32 wave_sum_u32(u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += u32(__shfl_xor(int(v), o, 64));
+  return v;
+}
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    u64 y = sh64(v, int(threadIdx.x) ^ o);
+    v = y > v ? y : v;
+  }
+  return v;
+}
+
+#ifndef LKF_FORCE_SERIAL
+#define LKF_FORCE_SERIAL 0  // diagnostic: every packet through decide_step
+#endif
+#ifndef LKF_DIAG
+#define LKF_DIAG 0  // diagnostic build: per-wave counters into g_diag (lkf_debug_counters)
+#endif
+#if LKF_DIAG
+__device__ unsigned long long g_diag[16];
+#define DIAG(i, v) dg[i] += (v)
+#else
+#define DIAG(i, v)
+#endif
+
+__global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
+  __shared__ i32 sDrop[kSetCap];
+  __shared__ i32 sEx[kSetCap];
+  __shared__ i32 sMissKey[kMissCap];
+  __shared__ i32 sMissVal[kMissCap];
+  const u32 lane = threadIdx.x;
+  const u64 lt = (1ull << lane) - 1;
+  const u32 w = blockIdx.x;
+  const u32 d = A.sched[w];
+  const DevDT dt = A.dts[d];
+  const u32 track = dt.track;
+  const u32 pb = A.tBegin[track];
+  u32 pe = A.tEnd[track];
+  if (A.slotBase[d] + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
+    if (lane == 0) atomicOr(A.err, 8u);
+    pe = pb;
+  }
+  LaneOut o;
+  o.nFwd = o.nBytes = o.nTuples = 0;
+  o.relOff = 0;
+  for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
+  Lane L;
+  L.h = A.hot[d];
+  L.rm = A.rm + size_t(d) * kRangeCap;
+  L.vc = A.vc + d;
+  L.dropKey = sDrop;
+  L.exKey = sEx;
+  L.missKey = sMissKey;
+  L.missVal = sMissVal;
+  if (L.h.flags & F_VP8) {  // VP8 munger maps live in LDS for the batch
+    if (lane < u32(kSetCap)) {
+      sDrop[lane] = L.vc->dropKey[lane];
+      sEx[lane] = L.vc->exKey[lane];
+    }
+    for (u32 i = lane; i < L.h.missCount; i += 64) {
+      const u32 idx = (L.h.missHead + i) % kMissCap;
+      sMissKey[idx] = L.vc->missKey[idx];
+      sMissVal[idx] = L.vc->missVal[idx];
+    }
+  }
+  __syncthreads();
+  L.seq = A.seq + size_t(d) * A.seqSize;
+  L.seqSize = A.seqSize;
+  const DevTrack &tk = A.tracks[track];
+  L.kind = tk.kind;
+  L.codec = tk.codec;
+  L.hasRefTS = tk.hasRefTS;
+  L.clockRate = tk.clockRate;
+  L.offs = tk.layerOffsets;
+  L.extPlayout = dt.extPlayout;
+  L.extAbs = dt.extAbs;
+  u32 ev = A.evOff[w];
+  const u32 evEnd = A.evOff[w + 1];
+  o.outT = A.tuples + A.slotBase[d];
+  u32 nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
+  const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
+#if LKF_DIAG
+  u64 dg[16] = {};
+  u64 tk0 = clock64();
+  dg[0] = 1;
+  dg[15] = pe - pb;
+#endif
+
+  for (u32 k = pb; k < pe; k += 64) {
+    const u32 n = min(64u, pe - k);
+    const bool valid = lane < n;
+    DIAG(1, 1);
+#if LKF_DIAG
+    u64 tc0 = clock64();
+#endif
+    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
+    if (valid) {
+      const u64 q = u64(k + lane) * 4;
+      r0 = src[q];
+      r1 = src[q + 1];
+      r2 = src[q + 2];
+      r3 = src[q + 3];
+    }
+    const PktV p = decode_pkt(r0, r1, r2, r3);
+#if LKF_DIAG
+    dg[11] += u64(__builtin_amdgcn_readfirstlane(u32(r0.x)) + 1u > 0u) * (clock64() - tc0);
+#endif
+    u32 pos = 0;
+    while (pos < n) {
+#if LKF_DIAG
+      u64 tr0 = clock64();
+#endif
+      while (nextAt <= k + pos) {
+        apply_ctl(L, A.events[ev++]);
+        nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
+      }
+      const bool inWin = valid && lane >= pos && (k + lane) < nextAt;
+      // ---- classification against the state at the start of the run
+      const u32 fl = L.h.flags;
+      const bool video = fl & F_VIDEO;
+      const i32 layer = p.layer;
+      const bool kf = p.flags & LKF_PKT_KEYFRAME;
+      const bool pktMarker = p.hdr1 & 0x80;
+      int cls;  // >= 0: drop with no state change; -1: current-layer candidate; -2: serial
+      if (fl & (F_MUTED | F_PUBMUTED)) {
+        cls = LKF_DROP_MUTED;
+      } else if (!video) {
+        cls = kf ? -2 : -1;  // a keyframe moves the RTX gate (rtpmunger.go:205-208)
+      } else if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) {
+        cls = LKF_DROP_PAUSED;
+      } else if (!(fl & F_SIMULCAST)) {
+        cls = LKF_DROP_NOT_SELECTED;
+      } else {
+        const bool willSwitch =
+            kf && ((L.h.curS != L.h.tgtS && ((layer > L.h.curS && layer <= L.h.tgtS) ||
+                                             (layer < L.h.curS && layer >= L.h.tgtS))) ||
+                   (L.h.curS > L.h.maxS && layer <= L.h.maxS));
+        if (willSwitch)
+          cls = -2;
+        else if (layer != L.h.curS)
+          cls = LKF_DROP_NOT_SELECTED;
+        else if ((fl & F_DEFICIENT) && L.h.tgtS < L.h.curS)
+          cls = LKF_DROP_DOWNGRADE;
+        else if ((fl & F_VP8) && (fl & F_TLS_VP8) && (p.flags & LKF_PKT_VP8) && !kf)
+          cls = -1;
+        else
+          cls = -2;
+      }
+#if LKF_FORCE_SERIAL
+      cls = -2;
+#endif
+      const bool cand = inWin && cls == -1;
+      const u64 candM = __ballot(cand);
+      const int pc = prev_in(candM, lt);
+      const int pcs = pc >= 0 ? pc : int(lane);  // cross-lane reads run on every lane
+      const u64 pcEsn = sh64(p.esn, pcs);
+      const u64 prevEsn = pc >= 0 ? pcEsn : L.h.extHighestIncomingSN;
+      bool ok = cand && p.esn == prevEsn + 1 && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+      // VP8 picture id (VP8PictureIdWrapHandler.Unwrap vp8.go:400-483 without a wrap)
+      const bool M = p.vbits & LKF_VP8_M, I = p.vbits & LKF_VP8_I, T = p.vbits & LKF_VP8_T;
+      const i32 np = M ? i32(p.pid & 0x7fff) : i32(p.pid & 0x7f);
+      const i32 ext = np + L.h.wrTotalWrap;
+      const i32 pcExt = i32(sh32(u32(ext), pcs));
+      const bool pcM = sh32(u32(M), pcs) != 0;
+      const i32 prevExt = pc >= 0 ? pcExt : L.h.wrMaxPictureId;
+      const bool prevM = pc >= 0 ? pcM : ((fl & F_WR_MAX_MBIT) != 0);
+      bool dropT = false;
+      if (video) {
+        i32 mp = prevExt;
+        if (mp > 0) mp = prevM ? (prevExt & 0x7fff) : (prevExt & 0x7f);
+        const bool wrapBack = L.h.wrTotalWrap > 0 && (prevExt + (L.h.wrLastWrap >> 1)) < (np + L.h.wrTotalWrap);
+        const bool wraps = np < mp && (mp - np) > (prevM ? (1 << 14) : (1 << 6));
+        // SelectTemporal would switch here (base.go:143-168, temporallayerselector/vp8.go:32-56)
+        const i32 cT = L.h.curT, gT = L.h.tgtT;
+        const bool tsw = cT != gT && T &&
+                         (cT < gT ? (i32(p.tid) > cT && i32(p.tid) <= gT && (p.vbits & LKF_VP8_S) &&
+                                     (p.vbits & LKF_VP8_Y))
+                                  : pktMarker);
+        const bool overT = cand && T && p.tid > u8(cT);
+        dropT = overT;
+        if (__ballot(overT) && L.h.exCount)  // exempted pictures forward (vp8.go:270)
+          dropT = overT && !set_has(L.exKey, L.h.exHead, L.h.exCount, ext);
+        ok = ok && !wrapBack && !wraps && !tsw && (!dropT || L.h.snOffset == L.h.rmOpenValue);
+      }
+      const u64 tdM = __ballot(ok && dropT);
+      const u64 snOff = L.h.snOffset + u64(__popcll(tdM & lt));
+      const u64 osn = p.esn - snOff;
+      const u64 ots = p.ets - L.h.tsOffset;
+      const bool picDrop = ok && dropT && I && ext != prevExt;
+      const i32 picOff = L.h.pictureIdOffset + i32(__popcll(__ballot(picDrop) & lt));
+      // forwarded: munged descriptor (vp8.go:283-301) + output shape
+      bool fwd = ok && !dropT;
+      const i32 mext = ext - picOff;
+      const u16 mpid = u16(mext & 0x7fff);
+      const u8 mtl0 = u8(p.tl0 - L.h.tl0Off);
+      const u8 mkey = u8((p.keyidx - L.h.keyIdxOff) & 0x1f);
+      u64 cb = 0;
+      int cbLen = 0;
+      if (video) {
+        const bool mM = mpid > 127;
+        const int hs = int(p.vhs) + (mM == M ? 0 : (mM ? 1 : -1));
+        cbLen = vp8_marshal(p.vfirst, I, mM, mpid, p.vbits & LKF_VP8_L, mtl0, T, p.tid, p.vbits & LKF_VP8_Y,
+                            p.vbits & LKF_VP8_K, mkey, hs, cb);
+      }
+      const u64 fwC = __ballot(fwd);
+      const int pf = prev_in(fwC, lt);
+      const u64 pfOsn = sh64(osn, pf >= 0 ? pf : int(lane));
+      const u64 prevOsn = pf >= 0 ? pfOsn : L.h.seqExtHighestSN;
+      const u64 pfOts = sh64(ots, pf >= 0 ? pf : int(lane));
+      // sequencer highest TS = max over pushes; runs keep TS non-decreasing so it is the last one
+      const bool tsMono = ots >= (pf >= 0 ? pfOts : L.h.seqExtHighestTS);
+      const bool seqOk = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && osn == prevOsn + 1 && cbLen >= 0 && tsMono;
+      const bool bad = inWin && ((cls == -2) || (cls == -1 && !ok) || (fwd && !seqOk));
+#if LKF_DIAG
+      {
+        const bool okb = cand && p.esn == prevEsn + 1 && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+        u32 cause = 0;
+        if (!bad)
+          cause = 0;
+        else if (cls == -2)
+          cause = 5;
+        else if (cls == -1 && !okb)
+          cause = 6;
+        else if (cls == -1 && !ok)
+          cause = 7;  // wrap / temporal switch / snOffset mismatch
+        else
+          cause = 10;
+        const u64 sm = __ballot(bad || (valid && lane >= pos && !inWin));
+        if (sm) {
+          const u32 xx = u32(__ffsll((long long)sm) - 1);
+          const u32 c = rl32(cause, xx);
+          if (c) dg[c] += 1;
+          else dg[4] += 1;
+        }
+      }
+#endif
+      const u64 stopM = __ballot(bad || (valid && lane >= pos && !inWin));
+      const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+      // ---- decide lanes [pos, x) together
+      DIAG(2, x > pos ? 1 : 0);
+      if (x > pos) {
+        const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
+        const bool inRun = (runM >> lane) & 1;
+        const u64 tdR = tdM & runM;
+        fwd = fwd && inRun;
+        const u64 fwR = __ballot(fwd);
+        const u64 selR = tdR | fwR;
+        o.nTuples += x - pos;
+#pragma unroll
+        for (int r = 0; r < LKF_DROP_NREASONS; r++) o.drops[r] += u32(__popcll(__ballot(inRun && cls == r)));
+        o.drops[LKF_DROP_TEMPORAL] += u32(__popcll(tdR));
+        // output records + sequencer slots of the forwarded lanes
+        const int cc = p.hdr0 & 0xf;
+        const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
+        const int extBytes = (playout ? 4 : 0) + (L.extAbs ? 4 : 0);
+        const int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
+        const int hdrLen = 12 + 4 * cc + extBlock;
+        const bool useCodec = video && cbLen > 0 && (p.flags & LKF_PKT_VP8);
+        const int payLen = useCodec ? (cbLen + int(p.plen) - int(p.vhs)) : int(p.plen);
+        const u32 outLen = fwd ? u32(hdrLen + payLen) : 0u;
+        const u32 aligned = (outLen + 15) & ~15u;
+        const u32 relEx = excl_scan_u32(aligned, lane);
+        const bool marker = pktMarker;  // tp.marker (= hdr.Marker for video, false for audio) || hdr.Marker
+        const u32 j = u32(__popcll(fwR & lt));
+        if (fwd) {
+          Tuple t;
+          t.extSN = osn;
+          t.extTS = ots;
+          t.pkt = k + lane;
+          t.relOff = o.relOff + relEx;
+          t.outLen = u16(outLen);
+          t.flags = u8(((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
+                       (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0));
+          t.layer = p.layer;
+          t.codecLen = u8(video ? cbLen : 0);
+#pragma unroll
+          for (int i = 0; i < 6; i++) t.codec[i] = u8(cb >> (8 * i));
+          t.hdrLen = u8(hdrLen);
+#pragma unroll
+          for (int i = 0; i < 12; i++) t.pad[i] = 0;
+          o.outT[o.nFwd + j] = t;
+          // sequencer.push in-order branch (sequencer.go:123-209): next slot
+          u32 slot = u32(L.h.seqHighSlot) + 1 + j;
+          while (slot >= L.seqSize) slot -= L.seqSize;
+          SeqMeta m = {};
+          m.sourceSeqNo = u16(p.esn);
+          m.targetSeqNo = u16(osn);
+          m.timestamp = u32(ots);
+          m.lastNack = u32(p.arr / 1000000LL - L.h.seqStartMs);
+          m.marker = marker;
+          m.layer = p.layer;
+          m.codecLen = u8(video ? cbLen : 0);
+#pragma unroll
+          for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+          L.seq[slot] = m;
+        }
+        const u32 sumLen = wave_sum_u32(outLen);
+        // ---- advance the DownTrack state past the run (uniform)
+        if (fwR) {
+          const u32 lastF = 63 - __clzll(fwR);
+          const u32 nF = u32(__popcll(fwR));
+          o.nBytes += sumLen;
+          o.nFwd += nF;
+          u32 slot = u32(L.h.seqHighSlot) + nF;
+          while (slot >= L.seqSize) slot -= L.seqSize;
+          L.h.seqHighSlot = u16(slot);
+          L.h.seqExtHighestSN = rl64(osn, lastF);
+          L.h.seqExtHighestTS = rl64(ots, lastF);  // >= every earlier push (tsMono)
+          if (video) {
+            L.h.extLastPictureId = i32(rl32(u32(mext), lastF));
+            L.h.lastTl0 = u8(rl32(mtl0, lastF));
+            L.h.lastKeyIdx = u8(rl32(mkey, lastF));
+          }
+        }
+        if (selR) {
+          const u32 lastSel = 63 - __clzll(selR);
+          const u64 mk = __ballot(video && pktMarker);  // marker passed to UpdateAndGetSnTs
+          L.h.extHighestIncomingSN = rl64(p.esn, lastSel);
+          const bool lastIsF = (fwR >> lastSel) & 1;
+          const u64 pfM = fwR & ((1ull << lastSel) - 1);
+          u64 sSN = L.h.extLastSN, sTS = L.h.extLastTS;
+          bool sMk = fl & F_LAST_MARKER;
+          if (pfM) {
+            const u32 b = 63 - __clzll(pfM);
+            sSN = rl64(osn, b);
+            sTS = rl64(ots, b);
+            sMk = (mk >> b) & 1;
+          }
+          if (lastIsF) {
+            L.h.extSecondLastSN = sSN;
+            L.h.extSecondLastTS = sTS;
+            L.h.extLastSN = rl64(osn, lastSel);
+            L.h.extLastTS = rl64(ots, lastSel);
+            setf(L, F_SECOND_LAST_MARKER, sMk);
+            setf(L, F_LAST_MARKER, (mk >> lastSel) & 1);
+          } else {
+            L.h.extSecondLastSN = L.h.extLastSN = sSN;
+            L.h.extSecondLastTS = L.h.extLastTS = sTS;
+            setf(L, F_SECOND_LAST_MARKER, sMk);
+            setf(L, F_LAST_MARKER, sMk);
+          }
+          if (hasf(L, F_RTX_GATE) && (rl64(osn, lastSel) - L.h.extRtxGateSn) > 2000) setf(L, F_RTX_GATE, false);
+          if (video) {
+            L.h.wrMaxPictureId = i32(rl32(u32(ext), lastSel));
+            setf(L, F_WR_MAX_MBIT, rl32(u32(M), lastSel) != 0);
+            // temporal drops: one exclusion per run of consecutive dropped packets
+            u64 m = tdR;
+            while (m) {
+              const u32 b = u32(__ffsll((long long)m) - 1);
+              const u64 after = fwR & ~((2ull << b) - 1);
+              const u32 nf = after ? u32(__ffsll((long long)after) - 1) : 64u;
+              const u64 runD = tdR & (nf >= 64 ? ~0ull : ((1ull << nf) - 1)) & ~((1ull << b) - 1);
+              const u64 s0 = rl64(p.esn, b);
+              rm_exclude(L, s0, s0 + u64(__popcll(runD)));
+              m &= ~runD;
+            }
+            if (tdR) L.h.snOffset = L.h.rmOpenValue;
+            u64 pd = __ballot(picDrop && inRun);
+            L.h.pictureIdOffset += i32(__popcll(pd));
+            while (pd) {
+              const u32 b = u32(__ffsll((long long)pd) - 1);
+              set_add(L.dropKey, L.h.dropHead, L.h.dropCount, i32(rl32(u32(ext), b)), kDropKeep);
+              pd &= pd - 1;
+            }
+          }
+        }
+        if (fwR) o.relOff += rl32(relEx + aligned, 63 - __clzll(fwR));
+      }
+      pos = x;
+#if LKF_DIAG
+      u64 ts0 = clock64();
+      dg[12] += ts0 - tr0;
+#endif
+      if (x < n && (k + x) < nextAt) {
+        DIAG(3, 1);
+        // the packet at lane x needs the full restatement
+        const uint4 a0 = make_uint4(rl32(r0.x, x), rl32(r0.y, x), rl32(r0.z, x), rl32(r0.w, x));
+        const uint4 a1 = make_uint4(rl32(r1.x, x), rl32(r1.y, x), rl32(r1.z, x), rl32(r1.w, x));
+        const uint4 a2 = make_uint4(rl32(r2.x, x), rl32(r2.y, x), rl32(r2.z, x), rl32(r2.w, x));
+        const uint4 a3 = make_uint4(rl32(r3.x, x), rl32(r3.y, x), rl32(r3.z, x), rl32(r3.w, x));
+        decide_step(L, decode_pkt(a0, a1, a2, a3), k + x, o);
+        pos = x + 1;
+      }
+#if LKF_DIAG
+      dg[13] += clock64() - ts0;
+#endif
+    }
+  }
+  while (ev < evEnd) apply_ctl(L, A.events[ev++]);
+#if LKF_DIAG
+  dg[14] += clock64() - tk0;
+  if (lane == 0)
+    for (int i = 0; i < 16; i++) atomicAdd(&g_diag[i], (unsigned long long)dg[i]);
+#endif
+  if (lane == 0) A.hot[d] = L.h;
+  if (L.h.flags & F_VP8) {
+    if (lane < u32(kSetCap)) {
+      L.vc->dropKey[lane] = sDrop[lane];
+      L.vc->exKey[lane] = sEx[lane];
+    }
+    for (u32 i = lane; i < L.h.missCount; i += 64) {
+      const u32 idx = (L.h.missHead + i) % kMissCap;
+      L.vc->missKey[idx] = sMissKey[idx];
+      L.vc->missVal[idx] = sMissVal[idx];
+    }
+  }
+  if (lane == 0) {
+    A.fwdCnt[d] = u32(o.nFwd);
+    A.fwdBytes[d] = o.relOff;
+    if (o.nTuples) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)o.nTuples);
+    if (o.nFwd) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)o.nFwd);
+    if (o.nBytes) atomicAdd((unsigned long long *)&A.stats[2], (unsigned long long)o.nBytes);
+#pragma unroll
+    for (int i = 0; i < LKF_DROP_NREASONS; i++)
+      if (o.drops[i]) atomicAdd((unsigned long long *)&A.stats[4 + i], (unsigned long long)o.drops[i]);
   }
 }
 
@@ -1575,6 +2064,33 @@ __global__ void k_accumulate(const u64 *stats, const u64 *tot, u64 *cum) {
 // ---------------------------------------------------------------------------
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 
+#if LKF_DIAG
+hipError_t read_diag(unsigned long long out[16], int reset) {
+  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 16);
+  if (r == hipSuccess && reset) {
+    unsigned long long z[16] = {};
+    r = hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
+  }
+  return r;
+}
+#else
+hipError_t read_diag(unsigned long long out[16], int) {
+  for (int i = 0; i < 16; i++) out[i] = 0;
+  return hipErrorNotSupported;
+}
+#endif
+
+hipError_t launch_batch_init(hipStream_t s, u32 ntracks, u32 ndts, u32 nstats, u32 *tBegin, u32 *tEnd, u32 *tRuns,
+                             u32 *err, u64 *stats, u32 *fwdCnt, u64 *fwdBytes) {
+  u32 n = ntracks > ndts ? ntracks : ndts;
+  if (n < nstats) n = nstats;
+  u32 g = nblk(n, 256);
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(k_batch_init, dim3(g), dim3(256), 0, s, ntracks, ndts, nstats, tBegin, tEnd, tRuns, err, stats,
+                     fwdCnt, fwdBytes);
+  return hipGetLastError();
+}
+
 hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, u32 n, u32 ntracks, u32 *tBegin, u32 *tEnd,
                                u32 *tRuns, u32 *err) {
   if (n == 0) return hipSuccess;
@@ -1623,7 +2139,10 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.fwdCnt = a.fwdCnt;
   A.fwdBytes = a.fwdBytes;
   A.stats = a.stats;
-  hipLaunchKernelGGL(k_decide, dim3(nblk(a.nlanes, 64)), dim3(64), 0, s, A, a.pkts);
+  if (a.mode == 1)
+    hipLaunchKernelGGL(k_decide_dt, dim3(a.nlanes), dim3(64), 0, s, A, a.pkts);
+  else
+    hipLaunchKernelGGL(k_decide, dim3(nblk(a.nlanes, 64)), dim3(64), 0, s, A, a.pkts);
   return hipGetLastError();
 }
 

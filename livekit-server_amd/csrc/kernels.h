@@ -9,9 +9,10 @@
 namespace lkf {
 
 struct DecideLaunch {
-  const uint32_t *sched;
+  int mode;                 // 0: k_decide (lanes = DownTracks of a track), 1: k_decide_dt (wave = DownTrack)
+  const uint32_t *sched;    // mode 0: lane -> DownTrack; mode 1: wave -> DownTrack
   const uint32_t *waveTrack;
-  uint32_t nlanes;
+  uint32_t nlanes;          // mode 0: lanes; mode 1: waves
   DTHot *hot;
   const DevDT *dts;
   const DevTrack *tracks;
@@ -46,6 +47,11 @@ struct EmitLaunch {
   uint32_t grid;
 };
 
+// diagnostic builds (-DLKF_DIAG=1): k_decide_dt per-wave counters
+hipError_t read_diag(unsigned long long out[16], int reset);
+hipError_t launch_batch_init(hipStream_t s, uint32_t ntracks, uint32_t ndts, uint32_t nstats, uint32_t *tBegin,
+                             uint32_t *tEnd, uint32_t *tRuns, uint32_t *err, uint64_t *stats, uint32_t *fwdCnt,
+                             uint64_t *fwdBytes);
 hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, uint32_t n, uint32_t ntracks, uint32_t *tBegin,
                                uint32_t *tEnd, uint32_t *tRuns, uint32_t *err);
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t *tBegin, const uint32_t *tEnd,

@@ -109,7 +109,15 @@ static void fill_payload(u8 *dst, int n, u64 key) {
 extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   if (!cfg || cfg->config < 1 || cfg->config > 4) return nullptr;
   const int C = cfg->config;
-  Rng rng(cfg->seed ? cfg->seed : (0x4C4Bull + u64(C)));
+  // Every room and every track draws from its own splitmix64 stream keyed by
+  // its global id, so a shard (room_base, rooms) generates exactly the rooms
+  // the full trace would: room sharding across GPUs changes no packet.
+  const u64 seedBase = cfg->seed ? cfg->seed : (0x4C4Bull + u64(C));
+  auto keyed = [&](u64 key) {
+    Rng k(seedBase ^ (key * 0xD6E8FEB86659FD93ull));
+    k.next();
+    return Rng(k.next());
+  };
   const double dur = cfg->duration_s > 0 ? cfg->duration_s : 10.0;
   const double bs = cfg->batch_s > 0 ? cfg->batch_s : 1.0;
   const i64 durNs = i64(dur * NS);
@@ -160,6 +168,8 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   };
   for (u32 r = 0; r < rooms; r++) {
     const u32 room = cfg->room_base + r;
+    Rng rng = keyed((1ull << 40) + room);
+    const size_t dt0 = tr->dts.size();
     RoomTracks rt;
     u32 npub = (C == 1 || C == 4) ? 1 : parts;
     for (u32 p = 0; p < npub; p++) {
@@ -244,15 +254,15 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       for (size_t i = 0; i < rt.audio.size(); i++)
         if (C == 1 || C == 4 || rt.audioPub[i] != s) addDT(rt.audio[i], false);
     }
-  }
-  // occasional subscriber mute/unmute (exercises resync + resume path)
-  if (withEvents && (C == 2 || C == 3)) {
-    for (int dt = 0; dt < (int)tr->dts.size(); dt++) {
-      if (rng.uni() < 0.05) {
-        i64 t = i64(rng.uni() * (durNs * 0.7));
-        i64 len = i64((0.3 + rng.uni()) * NS);
-        evs.push_back(Ev{dt, LKF_CTL_MUTE, {1, 1, 0, 0}, t0 + t});
-        evs.push_back(Ev{dt, LKF_CTL_MUTE, {0, 1, 0, 0}, t0 + t + len});
+    // occasional subscriber mute/unmute (exercises resync + resume path)
+    if (withEvents && (C == 2 || C == 3)) {
+      for (int dt = int(dt0); dt < (int)tr->dts.size(); dt++) {
+        if (rng.uni() < 0.05) {
+          i64 t = i64(rng.uni() * (durNs * 0.7));
+          i64 len = i64((0.3 + rng.uni()) * NS);
+          evs.push_back(Ev{dt, LKF_CTL_MUTE, {1, 1, 0, 0}, t0 + t});
+          evs.push_back(Ev{dt, LKF_CTL_MUTE, {0, 1, 0, 0}, t0 + t + len});
+        }
       }
     }
   }
@@ -272,6 +282,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   // ---- per-track packet plans -------------------------------------------
   for (size_t ti = 0; ti < tg.size(); ti++) {
     TrackGen &g = tg[ti];
+    Rng rng = keyed(g.p.track_id);
     std::vector<std::vector<Plan>> streams(g.nlayers);
     i64 netDelay = 20 * MS + i64(rng.below(10)) * MS;
     if (g.p.kind == LKF_KIND_VIDEO) {

@@ -1,0 +1,50 @@
+"""Diagnostic: k_decide_dt per-wave counters from a -DLKF_DIAG=1 build.
+
+    make -C livekit-server_amd/csrc diag && python3 scripts/diag_decide.py [rooms] [batches]
+"""
+import ctypes as C
+import importlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = ["waves", "chunks", "runs", "serial", "event_stops", "cause_cls", "cause_contig", "cause_vp8",
+         "", "", "cause_seq", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
+
+
+def main():
+    rooms = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    nb = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    pkg = importlib.import_module("livekit-server_amd")
+    wl = importlib.import_module("livekit-server_amd.workload")
+    tr = wl.Trace(2, duration_s=float(nb), batch_s=1.0, rooms=rooms)
+    lib = os.path.join(ROOT, "livekit-server_amd", "lib", "liblkfwd_diag.so")
+    eng = pkg.Engine.for_trace(tr, lib_path=lib)
+    fn = eng.lib.lkf_debug_counters
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
+    wl.load_topology(eng.api, eng.h, tr)
+    out = (C.c_uint64 * 16)()
+    for b in range(nb):
+        wl.queue_events(eng.api, eng.h, tr, b)
+        pk, n, ar, alen = tr.batch(b)
+        eng.submit(pk, n, ar, alen)
+        if b == 1:
+            fn(eng.h, out, 1)  # reset after the first (warm-up) batch
+        eng.run()
+        eng.sync()
+    rc = fn(eng.h, out, 0)
+    print("rc", rc)
+    v = list(out)
+    for i, nm in enumerate(NAMES):
+        if nm:
+            print("%-14s %14d  per-wave %10.1f" % (nm, v[i], v[i] / max(1, v[0])))
+    st = eng.stats()
+    print("last batch:", st)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+"""Room sharding across ranks on CPU with torch.distributed/gloo.
+
+Each rank generates only its own rooms (room_base = rank * rooms, as bench.py
+does per GPU) and forwards them through the CPU oracle; the per-rank totals,
+all-reduced over gloo, must equal one process forwarding all rooms.  This is
+the property that lets the GPU bench shard rooms with no data-path collective.
+"""
+import ctypes as C
+import importlib
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOMS_PER_RANK = 2
+WORLD = 2
+
+
+def _forward(rooms, room_base):
+    from tests.oracle_lib import load as load_oracle
+    wl = importlib.import_module("livekit-server_amd.workload")
+    abi = importlib.import_module("livekit-server_amd.abi")
+    o = load_oracle()
+    tr = wl.Trace(2, duration_s=2.0, batch_s=1.0, rooms=rooms, room_base=room_base)
+    h = o.create(500)
+    tot = [0] * (4 + 11)
+    try:
+        wl.load_topology(o.api, h, tr)
+        for b in range(tr.nbatches):
+            wl.queue_events(o.api, h, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(h, pk, n, ar, alen)
+            st = abi.lkf_stats()
+            o.api["get_stats"](h, C.byref(st))
+            d = st.as_dict()
+            tot[0] += d["tuples"]
+            tot[1] += d["forwarded"]
+            tot[2] += d["out_bytes"]
+            for i, v in enumerate(d["drops"]):
+                tot[4 + i] += v
+    finally:
+        o.destroy(h)
+        tr.close()
+    return tot
+
+
+def _worker(rank, port, q):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        tot = _forward(ROOMS_PER_RANK, rank * ROOMS_PER_RANK)
+        t = torch.tensor(tot, dtype=torch.int64)
+        dist.all_reduce(t)
+        if rank == 0:
+            q.put(t.tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_room_sharding_gloo_matches_single_process(pkg):
+    from tests import oracle_lib
+    oracle_lib.load()  # build before forking
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    got = q.get(timeout=10)
+    want = _forward(ROOMS_PER_RANK * WORLD, 0)
+    assert got == want
+    assert got[1] > 0
