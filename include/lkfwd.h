@@ -149,8 +149,9 @@ typedef struct lkf_pkt {
 #define LKF_VP8_K 0x40
 
 /* One forwarded (packet x DownTrack) tuple = one wire packet handed to the
- * pacer (pacer.Packet, pacer/pacer.go:25-39), 40 bytes.  Records are
- * DownTrack-major (a DownTrack's packets contiguous, in send order). */
+ * pacer (pacer.Packet, pacer/pacer.go:25-39), 40 bytes.  Records are ordered
+ * by track handle, then DownTrack handle, then packet (a DownTrack's packets
+ * contiguous, in send order; the DownTracks of one track adjacent). */
 typedef struct lkf_out {
   uint64_t ext_sn;      /* tp.rtp.extSequenceNumber (munged) */
   uint64_t ext_ts;      /* tp.rtp.extTimestamp (munged) */

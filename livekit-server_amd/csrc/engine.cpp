@@ -109,6 +109,7 @@ struct lkf_engine {
   uint32_t *dSched = nullptr;
   uint32_t *dWaveTrack = nullptr;
   uint32_t *dEvOff = nullptr;
+  uint32_t *dPerm = nullptr;  // output position -> DownTrack (track-major)
   size_t schedCap = 0;
   DevEvent *dEvents = nullptr;
   uint64_t evCap = 0;
@@ -262,6 +263,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dVc, c.max_downtracks));
   A(dalloc(&e->dSeq, size_t(c.max_downtracks) * c.seq_size));
   A(dalloc(&e->dCum, kStatsWords));
+  A(dalloc(&e->dPerm, c.max_downtracks));
   const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
   for (auto &x : e->ctx) {
     A(dalloc(&x.dTBegin, c.max_tracks));
@@ -320,7 +322,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
-                  e->dWaveTrack, e->dEvOff, e->dEvents, e->dCum, e->dSns, e->dSeqOut, e->dSeqN};
+                  e->dWaveTrack, e->dEvOff, e->dEvents, e->dCum, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &x : e->ctx) {
@@ -487,7 +489,7 @@ static int rebuild_sched(lkf_engine *e) {
   e->waveTrack.clear();
   for (uint32_t t : order) {
     const auto &v = byTrack[t];
-    if (e->decideMode == 1) {  // one wave per DownTrack
+    if (e->decideMode == 1) {  // one wave per DownTrack (interleaved per XCD below)
       for (uint32_t d : v) {
         e->sched.push_back(d);
         e->waveTrack.push_back(t);
@@ -498,6 +500,41 @@ static int rebuild_sched(lkf_engine *e) {
       e->waveTrack.push_back(t);
       for (size_t j = 0; j < 64; j++) e->sched.push_back(i + j < v.size() ? v[i + j] : kIdle);
     }
+  }
+  if (e->decideMode == 1 && !e->sched.empty()) {
+    // Waves are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8).
+    // Give all DownTracks of a track the same XCD, consecutive in its order,
+    // so the 8-9 waves reading one track's packet descriptors share an L2.
+    // Tracks go to the XCD with the fewest waves so far (video first, so the
+    // long waves spread evenly); idle slots pad the shorter XCD lists.
+    constexpr int kX = 8;
+    std::vector<std::vector<uint32_t>> lst(kX), lstT(kX);
+    std::vector<double> load(kX, 0.0);
+    size_t i = 0;
+    while (i < e->sched.size()) {
+      const uint32_t t = e->waveTrack[i];
+      size_t j = i;
+      while (j < e->sched.size() && e->waveTrack[j] == t) j++;
+      int bx = 0;
+      for (int x = 1; x < kX; x++)
+        if (load[x] < load[bx]) bx = x;
+      const double w = e->tracks[t].kind == LKF_KIND_VIDEO ? 7.0 : 1.0;  // ~packets per wave
+      for (size_t q = i; q < j; q++) {
+        lst[bx].push_back(e->sched[q]);
+        lstT[bx].push_back(t);
+        load[bx] += w;
+      }
+      i = j;
+    }
+    size_t mx = 0;
+    for (auto &l : lst) mx = std::max(mx, l.size());
+    e->sched.assign(mx * kX, kIdle);
+    e->waveTrack.assign(mx * kX, 0);
+    for (int x = 0; x < kX; x++)
+      for (size_t q = 0; q < lst[x].size(); q++) {
+        e->sched[q * kX + x] = lst[x][q];
+        e->waveTrack[q * kX + x] = lstT[x][q];
+      }
   }
   e->dtLane.assign(nd, -1);
   for (uint32_t l = 0; l < e->sched.size(); l++)
@@ -513,6 +550,14 @@ static int rebuild_sched(lkf_engine *e) {
     HIPCHK(dalloc(&e->dSched, e->schedCap), "alloc sched");
     HIPCHK(dalloc(&e->dEvOff, e->schedCap + 1), "alloc evoff");
     HIPCHK(dalloc(&e->dWaveTrack, e->schedCap + 1), "alloc wavetrack");
+  }
+  // output order: by track, then DownTrack handle (every DownTrack, active or not)
+  {
+    std::vector<uint32_t> perm(nd);
+    for (uint32_t d = 0; d < nd; d++) perm[d] = d;
+    std::stable_sort(perm.begin(), perm.end(),
+                     [&](uint32_t a, uint32_t b) { return e->dtp[a].track < e->dtp[b].track; });
+    if (nd) HIPCHK(hipMemcpy(e->dPerm, perm.data(), nd * sizeof(uint32_t), hipMemcpyHostToDevice), "perm copy");
   }
   if (nl) {
     HIPCHK(hipMemcpy(e->dSched, e->sched.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice), "sched copy");
@@ -611,7 +656,7 @@ int lkf_run(lkf_engine *e, void *stream) {
          "batch init");
   HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr), "track_ranges");
   HIPCHK(launch_scan(s, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
-                     x.dTot + 0, nullptr),
+                     x.dTot + 0, nullptr, nullptr),
          "slot scan");
   DecideLaunch d;
   d.mode = e->decideMode;
@@ -641,7 +686,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(launch_decide(s, d), "decide");
   HIPCHK(hipEventRecord(rg[2], s), "event");
   HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
-                     x.dByteBase, x.dTot + 2, x.dTot + 3),
+                     x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm),
          "out scan");
   HIPCHK(hipEventRecord(x.decided, s), "event");
 
@@ -649,6 +694,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipStreamWaitEvent(e->emitS, x.decided, 0), "wait decided");
   HIPCHK(hipEventRecord(rg[3], e->emitS), "event");
   EmitLaunch m;
+  m.perm = e->dPerm;
   m.recBase = x.dRecBase;
   m.byteBase = x.dByteBase;
   m.slotBase = x.dSlotBase;

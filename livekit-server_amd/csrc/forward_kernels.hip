@@ -11,7 +11,7 @@
 //                   (codecmunger/vp8.go) + sequencer.push (sequencer.go:123)
 //                   -> compact per-DownTrack Tuple records
 //   scan (output)   per DownTrack record base + byte base (16-B aligned wire
-//                   packets, DownTrack-major)
+//                   packets; order: track, then DownTrack, then packet)
 //   k_emit          flat 16-B chunk sweep over the output arena: RTP header +
 //                   extension block + munged VP8 descriptor from LDS, payload
 //                   copied byte-shifted from the input arena (coalesced
@@ -30,6 +30,24 @@
 #endif
 
 namespace lkf {
+
+#ifndef LKF_DIAG
+#define LKF_DIAG 0  // diagnostic build: per-wave counters into g_diag (lkf_debug_counters)
+#endif
+#if LKF_DIAG
+__device__ unsigned long long g_diag[16];
+struct DiagTimer {  // adds elapsed cycles of a scope to g_diag[slot] (lane 0)
+  int slot;
+  uint64_t t0;
+  __device__ explicit DiagTimer(int s) : slot(s), t0(clock64()) {}
+  __device__ ~DiagTimer() {
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag[slot], (unsigned long long)(clock64() - t0));
+  }
+};
+#define DIAG_SCOPE(slot) DiagTimer diag_timer_(slot)
+#else
+#define DIAG_SCOPE(slot)
+#endif
 
 using u8 = uint8_t;
 using u16 = uint16_t;
@@ -319,6 +337,7 @@ __device__ __forceinline__ bool dropped_has(const Lane &L, i32 key) {
 // Equivalent bounded form: existing entries in range are updated in place;
 // of the new keys only the newest 50 can survive the trim, appended in order.
 __device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
+  DIAG_SCOPE(8);
   if (ext < prevMax) return;
   const int e0 = L.h.missCount;
   int inE = 0;  // existing (not dropped) keys inside the range
@@ -807,6 +826,7 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     if (ets > L.h.seqExtHighestTS) L.h.seqExtHighestTS = ets;
     return;
   }
+  DIAG_SCOPE(9);
   if (!hasf(L, F_SEQ_INIT)) {
     setf(L, F_SEQ_INIT, true);
     L.h.seqExtStartSN = esn;
@@ -918,13 +938,15 @@ constexpr int SCAN_TILE = SCAN_T * SCAN_ITEMS;
 
 struct ScanIn {
   int mode;  // 0: slots = npkts(track(d)) if active; 1: (fwdCnt, fwdBytes)
+  const u32 *perm;  // position -> DownTrack (nullptr: identity)
   const DevDT *dts;
   const u32 *tBegin, *tEnd;
   const u32 *cnt;
   const u64 *bytes;
 };
 
-__device__ __forceinline__ void scan_load(const ScanIn &in, u32 d, u64 &a, u64 &b) {
+__device__ __forceinline__ void scan_load(const ScanIn &in, u32 i, u64 &a, u64 &b) {
+  const u32 d = in.perm ? in.perm[i] : i;
   if (in.mode == 0) {
     DevDT dt = in.dts[d];
     a = dt.active ? u64(in.tEnd[dt.track] - in.tBegin[dt.track]) : 0;
@@ -1411,11 +1433,7 @@ __device__ __forceinline__ u64 wave_max_u64(u64 v) {
 #ifndef LKF_FORCE_SERIAL
 #define LKF_FORCE_SERIAL 0  // diagnostic: every packet through decide_step
 #endif
-#ifndef LKF_DIAG
-#define LKF_DIAG 0  // diagnostic build: per-wave counters into g_diag (lkf_debug_counters)
-#endif
 #if LKF_DIAG
-__device__ unsigned long long g_diag[16];
 #define DIAG(i, v) dg[i] += (v)
 #else
 #define DIAG(i, v)
@@ -1430,6 +1448,7 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
   const u64 lt = (1ull << lane) - 1;
   const u32 w = blockIdx.x;
   const u32 d = A.sched[w];
+  if (d == 0xffffffffu) return;  // padding slot of the per-XCD schedule
   const DevDT dt = A.dts[d];
   const u32 track = dt.track;
   const u32 pb = A.tBegin[track];
@@ -1826,8 +1845,9 @@ constexpr int EMIT_G = 64;
 constexpr int PRE_MAX = 128;
 
 struct EmitArgs {
-  const u64 *recBase;   // [ndts] exclusive scan of forwarded counts
-  const u64 *byteBase;  // [ndts] exclusive scan of output bytes
+  const u32 *perm;      // output position -> DownTrack (track-major order)
+  const u64 *recBase;   // [position] exclusive scan of forwarded counts
+  const u64 *byteBase;  // [position] exclusive scan of output bytes
   const u64 *slotBase;
   const u64 *totals;    // [0] records, [1] bytes
   const Tuple *tuples;
@@ -1860,7 +1880,17 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(A.err, 4u);
     return;
   }
-  for (u64 g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  // XCD-aware partition: workgroups are dispatched round-robin over the 8
+  // XCDs, so blockIdx % 8 names the XCD.  Each XCD walks its own contiguous
+  // eighth of the (track-major) output in order: the records that re-read a
+  // track's payloads (one per subscribing DownTrack) are adjacent, so the
+  // re-reads hit that XCD's 4 MiB L2 instead of going to HBM.  (Falls back to a plain grid-stride when
+  // the grid is not a multiple of 8.)
+  const u32 nx = (gridDim.x % 8 == 0) ? 8u : 1u;
+  const u32 xcd = blockIdx.x % nx, slotInX = blockIdx.x / nx, perX = gridDim.x / nx;
+  const u64 gpx = (ngroups + nx - 1) / nx;
+  const u64 gBeg = u64(xcd) * gpx, gEnd = min(ngroups, gBeg + gpx);
+  for (u64 g = gBeg + slotInX; g < gEnd; g += perX) {
     const u64 r0 = g * EMIT_G;
     const int nrec = int(min(u64(EMIT_G), total - r0));
     if (threadIdx.x < nrec) {
@@ -1874,13 +1904,13 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         else
           hi = mid;
       }
-      const u32 d = lo;
-      const u64 j = r - A.recBase[d];
+      const u32 d = A.perm[lo];
+      const u64 j = r - A.recBase[lo];
       const Tuple t = A.tuples[A.slotBase[d] + j];
       const lkf_pkt *pp = A.pkts + t.pkt;
       const PktV p = load_pkt(pp);
       const DevDT dt = A.dts[d];
-      const u64 outOff = A.byteBase[d] + t.relOff;
+      const u64 outOff = A.byteBase[lo] + t.relOff;
       lkf_out o;
       o.ext_sn = t.extSN;
       o.ext_ts = t.extTS;
@@ -2099,9 +2129,11 @@ hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, u32 n, u32 nt
 }
 
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const u32 *tBegin, const u32 *tEnd, const u32 *cnt,
-                       const u64 *bytes, u32 n, u64 *partA, u64 *partB, u64 *outA, u64 *outB, u64 *totA, u64 *totB) {
+                       const u64 *bytes, u32 n, u64 *partA, u64 *partB, u64 *outA, u64 *outB, u64 *totA, u64 *totB,
+                       const u32 *perm) {
   ScanIn in;
   in.mode = mode;
+  in.perm = perm;
   in.dts = dts;
   in.tBegin = tBegin;
   in.tEnd = tEnd;
@@ -2148,6 +2180,7 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
 
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   EmitArgs A;
+  A.perm = a.perm;
   A.recBase = a.recBase;
   A.byteBase = a.byteBase;
   A.slotBase = a.slotBase;

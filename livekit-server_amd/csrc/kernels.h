@@ -34,7 +34,8 @@ struct DecideLaunch {
 };
 
 struct EmitLaunch {
-  const uint64_t *recBase, *byteBase, *slotBase, *totals;
+  const uint32_t *perm;  // output position -> DownTrack
+  const uint64_t *recBase, *byteBase, *slotBase, *totals;  // recBase/byteBase by position
   const Tuple *tuples;
   const lkf_pkt *pkts;
   const uint8_t *arena;
@@ -56,7 +57,8 @@ hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, uint32_t n, u
                                uint32_t *tEnd, uint32_t *tRuns, uint32_t *err);
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t *tBegin, const uint32_t *tEnd,
                        const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
-                       uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB);
+                       uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB,
+                       const uint32_t *perm);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
 hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum);

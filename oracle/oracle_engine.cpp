@@ -13,7 +13,8 @@
 //        pacer writeRTPHeaderExtensions   pacer/base.go:71-100
 //        sequencer.push                   sequencer.go:123-209
 //        sendingPacket -> RTPStatsSender  downtrack.go:1930, rtpstats_sender.go:229
-//  Output: DownTrack-major lkf_out records + wire bytes (16-B aligned).
+//  Output: lkf_out records ordered by track, DownTrack, packet + wire bytes
+//  (16-B aligned).
 // =============================================================================
 #include <chrono>
 #include <memory>
@@ -312,20 +313,23 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   }
   for (u32 d = 0; d < ndt; d++)
     while (evc[d] < evq[d].size()) applyCtl(e, *e->dts[d], evq[d][evc[d]++]);
-  // DownTrack-major output, 16-B aligned wire packets
+  // Output order: by track, then DownTrack handle, then packet; wire packets
+  // 16-B aligned.  (An engine-defined batch layout: the reference hands each
+  // packet to its DownTrack's pacer directly.)
   e->outRecs.clear();
   e->outArena.clear();
   u64 off = 0;
-  for (u32 d = 0; d < ndt; d++)
-    for (auto &o : e->dts[d]->outs) {
-      lkf_out r = o.rec;
-      r.out_off = off;
-      e->outRecs.push_back(r);
-      e->outArena.insert(e->outArena.end(), o.bytes.begin(), o.bytes.end());
-      u64 al = (o.bytes.size() + 15) & ~u64(15);
-      e->outArena.resize(off + al, 0);
-      off += al;
-    }
+  for (auto &tds : trackDts)
+    for (u32 d : tds)
+      for (auto &o : e->dts[d]->outs) {
+        lkf_out r = o.rec;
+        r.out_off = off;
+        e->outRecs.push_back(r);
+        e->outArena.insert(e->outArena.end(), o.bytes.begin(), o.bytes.end());
+        u64 al = (o.bytes.size() + 15) & ~u64(15);
+        e->outArena.resize(off + al, 0);
+        off += al;
+      }
   e->stats.arena_bytes = off;
   return LKF_OK;
 }

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 NAMES = ["waves", "chunks", "runs", "serial", "event_stops", "cause_cls", "cause_contig", "cause_vp8",
-         "", "", "cause_seq", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
+         "cyc_missing", "cyc_seqpush", "cause_seq", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
 
 
 def main():
