@@ -77,6 +77,8 @@ typedef struct lkf_cfg {
   uint64_t max_out_bytes;   /* output arena capacity per batch */
   uint64_t max_out_pkts;    /* output record capacity per batch */
   uint64_t max_batch_tuples; /* (packet x DownTrack) evaluations per batch (decide slots) */
+  uint32_t max_streams;     /* ingress streams (one per received SSRC); 0 = 3 x max_tracks */
+  uint32_t reserved_cfg;
 } lkf_cfg;
 
 /* One published track (a MediaTrack/WebRTCReceiver, receiver.go:195). */
@@ -194,6 +196,71 @@ typedef struct lkf_fwd_state {
   uint8_t vp8_last_keyidx, vp8_keyidx_used, pad[2];
 } lkf_fwd_state;
 
+/* ---- ingress ------------------------------------------------------------
+ * One received RTP stream = one buffer.Buffer (buffer.go:66-130, bound by
+ * WebRTCReceiver.AddUpTrack receiver.go:320-360): RTPStatsReceiver, the
+ * padding-exclusion RangeMap(100), and (audio) the AudioLevel observer. */
+typedef struct lkf_stream_params {
+  int32_t track;            /* forwarding track handle (lkf_add_track) */
+  int32_t layer;            /* receiver layer of this SSRC (RidToSpatialLayer); 0 for audio */
+  uint32_t ssrc;
+  uint8_t audio_level_ext;  /* negotiated ssrc-audio-level header extension id; 0 = none */
+  /* AudioLevelParams (receiver.go:342-347); all zero -> config.go:380-385
+   * defaults 35 / 40 / 400 ms / 2 */
+  uint8_t active_level;
+  uint8_t min_percentile;
+  uint8_t reserved;
+  uint32_t observe_duration_ms;
+  uint32_t smooth_intervals;
+} lkf_stream_params;
+
+/* One received datagram of a raw batch (24 B).  A raw batch is grouped by
+ * track (every packet of a track's streams contiguous, in arrival order),
+ * like an ExtPacket batch. */
+typedef struct lkf_raw_pkt {
+  int64_t arrival_ns;  /* arrival time, virtual clock */
+  uint32_t stream;     /* lkf_add_stream handle */
+  uint32_t off;        /* offset of the datagram in the raw arena */
+  uint32_t len;        /* datagram length */
+  uint32_t reserved;
+} lkf_raw_pkt;
+
+/* Per-datagram ingress outcome: RTPFlowState (rtpstats_receiver.go:33-45)
+ * plus the Buffer.calc disposition (buffer.go:417-491), 40 B. */
+typedef struct lkf_flow {
+  uint64_t ext_sn;      /* ExtSequenceNumber, after the padding adjustment (buffer.go:464-471) */
+  uint64_t ext_ts;      /* ExtTimestamp */
+  uint64_t loss_start;  /* NACK range [loss_start, loss_end) when LKF_FLOW_HAS_LOSS */
+  uint64_t loss_end;
+  uint32_t pkt;         /* index of the ExtPacket produced in the forwarding batch, or 0xffffffff */
+  uint8_t flags;        /* LKF_FLOW_* */
+  uint8_t reserved[3];
+} lkf_flow;
+#define LKF_FLOW_NOT_HANDLED 0x01  /* flowState.IsNotHandled */
+#define LKF_FLOW_DUPLICATE 0x02    /* flowState.IsDuplicate */
+#define LKF_FLOW_OUT_OF_ORDER 0x04 /* flowState.IsOutOfOrder */
+#define LKF_FLOW_HAS_LOSS 0x08     /* flowState.HasLoss */
+#define LKF_FLOW_PADDING 0x10      /* padding-only packet dropped (buffer.go:439-460) */
+#define LKF_FLOW_FORWARD 0x20      /* an ExtPacket was produced (buffer.go:489) */
+#define LKF_FLOW_BAD 0x40          /* RTP unmarshal / codec parse failed (buffer.go:424, :632) */
+
+/* RTPStatsReceiver counters of one stream (rtpstats_receiver.go:76-241). */
+typedef struct lkf_stream_stats {
+  uint64_t ext_start_sn, ext_highest_sn, ext_start_ts, ext_highest_ts;
+  uint64_t packets_lost, packets_out_of_order, packets_duplicate, packets_padding;
+  uint64_t bytes, header_bytes, bytes_duplicate, bytes_padding, frames;
+  uint8_t initialized;
+  uint8_t reserved[7];
+} lkf_stream_stats;
+
+/* One active speaker (livekit.SpeakerInfo, room.go:254-279), 16 B. */
+typedef struct lkf_speaker {
+  uint32_t room;
+  uint32_t participant;  /* publisher index */
+  float level;           /* quantised: ceil(level * 8) / 8 (room.go:274-276) */
+  uint32_t active;
+} lkf_speaker;
+
 typedef struct lkf_engine lkf_engine;
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -265,6 +332,32 @@ typedef struct lkf_seq_meta {
 } lkf_seq_meta;
 int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns,
                    lkf_seq_meta *out, uint32_t *n_out);
+
+/* ---- ingress ------------------------------------------------------------ */
+/* Adds one received stream (NewBuffer + Bind, buffer.go:124-215). */
+int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p);
+/* Buffer.calc (buffer.go:417-491) for a raw batch: RTP unmarshal, header
+ * extensions (audio level -> AudioLevel.Observe, buffer.go:573-596),
+ * RTPStatsReceiver.Update, NACK loss ranges, padding exclusion, and
+ * getExtPacket (buffer.go:599-671).  The ExtPackets produced become the batch
+ * of the next lkf_run (the raw arena is the forwarding arena; it must stay
+ * valid until that batch's outputs are drained).  Host buffers are copied. */
+int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len);
+/* Same with device-resident inputs (valid until the forwarded batch is synced). */
+int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, const uint8_t *d_raw,
+                      uint64_t raw_len);
+/* Per-datagram outcomes of the last ingest (input order). */
+int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out);
+/* The ExtPacket batch produced by the last ingest (host copy; the RTX bucket
+ * and the host-side stream trackers read it). */
+int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out);
+int lkf_stream_stats_get(lkf_engine *e, int32_t stream, lkf_stream_stats *out);
+/* Room.GetActiveSpeakers (room.go:254-279) for every room at virtual time
+ * now_ns: per participant the loudest active microphone track
+ * (UpTrackManager.GetAudioLevel uptrackmanager.go:422-436, AudioLevel.GetLevel
+ * audiolevel.go:105-112), sorted by level (ties: participant index), grouped
+ * by room in ascending room order. */
+int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, uint32_t *n_out);
 
 /* ---- introspection ------------------------------------------------------ */
 /* Duration of the last batch's decide kernel, emit kernel and whole batch, ms. */

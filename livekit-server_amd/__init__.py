@@ -79,6 +79,41 @@ def drain_arrays(api, h, nmax=None):
     return recs, arena
 
 
+def flows_array(api, h):
+    """Per-datagram outcomes (lkf_flow) of the last ingest as a numpy array."""
+    n = C.c_uint32()
+    rc = api["ingest_flows"](h, None, 0, C.byref(n))
+    if rc not in (0, -28):
+        raise EngineError("ingest_flows probe rc=%d" % rc)
+    out = np.zeros(n.value, dtype=abi.FLOW_DTYPE)
+    rc = api["ingest_flows"](h, out.ctypes.data, n.value, C.byref(n))
+    if rc != 0:
+        raise EngineError("ingest_flows rc=%d" % rc)
+    return out
+
+
+def speakers_array(api, h, now_ns):
+    """Room.GetActiveSpeakers for every room at now_ns as a numpy array."""
+    n = C.c_uint32()
+    cap = 4096
+    while True:
+        out = np.zeros(cap, dtype=abi.SPEAKER_DTYPE)
+        rc = api["speakers"](h, now_ns, out.ctypes.data, cap, C.byref(n))
+        if rc == 0:
+            return out[:n.value]
+        if rc != -28:
+            raise EngineError("speakers rc=%d" % rc)
+        cap = n.value
+
+
+def stream_stats(api, h, sid):
+    st = abi.lkf_stream_stats()
+    rc = api["stream_stats_get"](h, sid, C.byref(st))
+    if rc != 0:
+        raise EngineError("stream_stats_get rc=%d" % rc)
+    return st.as_tuple()
+
+
 class Engine:
     """One lkf_engine on one HIP device (one process per GPU)."""
 
@@ -117,6 +152,21 @@ class Engine:
 
     def run(self, stream=None):
         self._chk(self.lib.lkf_run(self.h, stream), "run")
+
+    def ingest(self, raws, n, raw, raw_len):
+        """Buffer.calc over a raw batch; the ExtPackets become the next run's batch."""
+        rc = self.api["ingest"](self.h, C.cast(raws, C.c_void_p), n, C.cast(raw, C.c_void_p), raw_len)
+        if rc != 0:
+            raise EngineError("lkf_ingest rc=%d: %s" % (rc, self.lib.lkf_last_error(self.h).decode()))
+
+    def flows(self):
+        return flows_array(self.api, self.h)
+
+    def stream_stats(self, sid):
+        return stream_stats(self.api, self.h, sid)
+
+    def speakers(self, now_ns):
+        return speakers_array(self.api, self.h, now_ns)
 
     def sync(self):
         self._chk(self.lib.lkf_sync(self.h), "sync")

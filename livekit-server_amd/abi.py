@@ -24,7 +24,70 @@ class lkf_cfg(C.Structure):
         ("max_out_bytes", C.c_uint64),
         ("max_out_pkts", C.c_uint64),
         ("max_batch_tuples", C.c_uint64),
+        ("max_streams", C.c_uint32),
+        ("reserved_cfg", C.c_uint32),
     ]
+
+
+class lkf_stream_params(C.Structure):
+    _fields_ = [
+        ("track", C.c_int32),
+        ("layer", C.c_int32),
+        ("ssrc", C.c_uint32),
+        ("audio_level_ext", C.c_uint8),
+        ("active_level", C.c_uint8),
+        ("min_percentile", C.c_uint8),
+        ("reserved", C.c_uint8),
+        ("observe_duration_ms", C.c_uint32),
+        ("smooth_intervals", C.c_uint32),
+    ]
+
+
+class lkf_raw_pkt(C.Structure):
+    _fields_ = [
+        ("arrival_ns", C.c_int64),
+        ("stream", C.c_uint32),
+        ("off", C.c_uint32),
+        ("len", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class lkf_flow(C.Structure):
+    _fields_ = [
+        ("ext_sn", C.c_uint64),
+        ("ext_ts", C.c_uint64),
+        ("loss_start", C.c_uint64),
+        ("loss_end", C.c_uint64),
+        ("pkt", C.c_uint32),
+        ("flags", C.c_uint8),
+        ("reserved", C.c_uint8 * 3),
+    ]
+
+
+class lkf_stream_stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "ext_start_sn", "ext_highest_sn", "ext_start_ts", "ext_highest_ts", "packets_lost",
+        "packets_out_of_order", "packets_duplicate", "packets_padding", "bytes", "header_bytes",
+        "bytes_duplicate", "bytes_padding", "frames")] + [("initialized", C.c_uint8), ("reserved", C.c_uint8 * 7)]
+
+    def as_tuple(self):
+        return tuple(getattr(self, n) for n, _ in self._fields_[:-1])
+
+
+class lkf_speaker(C.Structure):
+    _fields_ = [
+        ("room", C.c_uint32),
+        ("participant", C.c_uint32),
+        ("level", C.c_float),
+        ("active", C.c_uint32),
+    ]
+
+
+FLOW_DTYPE = np.dtype([("ext_sn", "<u8"), ("ext_ts", "<u8"), ("loss_start", "<u8"), ("loss_end", "<u8"),
+                       ("pkt", "<u4"), ("flags", "u1"), ("reserved", "V3")])
+assert FLOW_DTYPE.itemsize == 40
+SPEAKER_DTYPE = np.dtype([("room", "<u4"), ("participant", "<u4"), ("level", "<f4"), ("active", "<u4")])
 
 
 class lkf_track_params(C.Structure):
@@ -228,6 +291,12 @@ def bind_engine_api(lib, prefix):
     api["seed_state"] = _bind(lib, prefix + "seed_state", C.c_int, [e, C.c_int32, P(lkf_fwd_state)])
     api["seq_lookup"] = _bind(lib, prefix + "seq_lookup", C.c_int,
                               [e, C.c_int32, P(C.c_uint16), C.c_uint32, C.c_int64, P(lkf_seq_meta), P(C.c_uint32)])
+    api["add_stream"] = _bind(lib, prefix + "add_stream", C.c_int32, [e, P(lkf_stream_params)])
+    api["ingest"] = _bind(lib, prefix + "ingest", C.c_int, [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64])
+    api["ingest_flows"] = _bind(lib, prefix + "ingest_flows", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
+    api["ingested"] = _bind(lib, prefix + "ingested", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
+    api["stream_stats_get"] = _bind(lib, prefix + "stream_stats_get", C.c_int, [e, C.c_int32, P(lkf_stream_stats)])
+    api["speakers"] = _bind(lib, prefix + "speakers", C.c_int, [e, C.c_int64, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     return api
 
 
@@ -250,4 +319,7 @@ def load_synth(path=None):
     _bind(lib, "lkfs_max_batch_pkts", C.c_uint32, [t])
     _bind(lib, "lkfs_max_batch_arena", C.c_uint64, [t])
     _bind(lib, "lkfs_max_batch_tuples", C.c_uint64, [t])
+    _bind(lib, "lkfs_num_streams", C.c_uint32, [t])
+    _bind(lib, "lkfs_streams", P(lkf_stream_params), [t])
+    _bind(lib, "lkfs_batch_raw", C.c_int, [t, C.c_uint32, P(P(lkf_raw_pkt)), P(C.c_uint32)])
     return lib

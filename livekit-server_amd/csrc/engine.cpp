@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -53,6 +54,7 @@ struct BatchCtx {
   uint64_t *dStats = nullptr;
   lkf_pkt *dPktsOwn = nullptr;  // lkf_submit copies land here
   uint8_t *dArenaOwn = nullptr;
+  lkf_raw_pkt *dRawPkts = nullptr;  // lkf_ingest copies land here
   hipEvent_t decided = nullptr;  // decide stage done (decide stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
   bool used = false;
@@ -83,6 +85,10 @@ struct lkf_engine {
   std::vector<DevTrack> pendTracks;
   std::vector<DTHot> pendHot;
   std::vector<DevDT> pendDTs;
+  // ingress streams (host mirror + uploads pending)
+  std::vector<lkf_stream_params> streams;
+  std::vector<DevStream> pendStreams;
+  bool spkDirty = true;
 
   // queued control ops
   struct Pend {
@@ -138,6 +144,24 @@ struct lkf_engine {
   static constexpr int kRing = 256;
   hipEvent_t ring[kRing][5] = {};
   uint32_t emitGrid = 2048;
+  // ingress (one buffer.Buffer per stream) + speakers
+  uint32_t maxStreams = 0;
+  DevStream *dStreams = nullptr;
+  StreamHot *dStreamHot = nullptr;
+  uint64_t *dHist = nullptr;
+  RangeEntry *dStreamRings = nullptr;
+  IngParsed *dParsed = nullptr;
+  lkf_flow *dFlows = nullptr;
+  uint32_t *dFwdFlag = nullptr;
+  uint64_t *dPos = nullptr, *dIPartA = nullptr, *dIPartB = nullptr, *dITotal = nullptr;
+  uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
+  uint32_t lastIngestN = 0;
+  // speaker ranking tables (rebuilt when topology changes)
+  uint32_t nRooms = 0;
+  uint32_t *dRoomPartOff = nullptr, *dPartId = nullptr, *dPartMicOff = nullptr, *dMics = nullptr, *dRoomId = nullptr;
+  lkf_speaker *dSpkSlots = nullptr;
+  uint32_t *dSpkCounts = nullptr;
+  size_t spkCap = 0;
   // 1: k_decide_dt (one wave per DownTrack, lanes = packets; default)
   // 0: k_decide (one lane per DownTrack, one wave per track)
   int decideMode = 1;
@@ -203,7 +227,7 @@ static int drain_streams(lkf_engine *e) {
 
 // Uploads tracks / DownTracks added since the last flush (contiguous tails).
 static int flush_topology(lkf_engine *e) {
-  if (e->pendTracks.empty() && e->pendDTs.empty()) return LKF_OK;
+  if (e->pendTracks.empty() && e->pendDTs.empty() && e->pendStreams.empty()) return LKF_OK;
   int rc = drain_streams(e);
   if (rc) return rc;
   if (!e->pendTracks.empty()) {
@@ -221,6 +245,21 @@ static int flush_topology(lkf_engine *e) {
            "dt upload");
     e->pendHot.clear();
     e->pendDTs.clear();
+  }
+  if (!e->pendStreams.empty()) {
+    const size_t first = e->streams.size() - e->pendStreams.size();
+    const size_t k = e->pendStreams.size();
+    std::vector<StreamHot> hot(k);
+    for (auto &h : hot) {
+      std::memset(&h, 0, sizeof(h));
+      h.loudest = 127;  // silentAudioLevel (audiolevel.go:24)
+    }
+    HIPCHK(hipMemcpy(e->dStreams + first, e->pendStreams.data(), k * sizeof(DevStream), hipMemcpyHostToDevice),
+           "streams upload");
+    HIPCHK(hipMemcpy(e->dStreamHot + first, hot.data(), k * sizeof(StreamHot), hipMemcpyHostToDevice),
+           "stream state upload");
+    HIPCHK(hipMemset(e->dHist + first * kHistWords, 0, k * kHistWords * sizeof(uint64_t)), "history reset");
+    e->pendStreams.clear();
   }
   return LKF_OK;
 }
@@ -284,11 +323,29 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dStats, kStatsWords));
     A(dalloc(&x.dPktsOwn, c.max_batch_pkts));
     A(dalloc(&x.dArenaOwn, c.max_batch_arena + 64));
+    A(dalloc(&x.dRawPkts, c.max_batch_pkts));
     A(hipEventCreateWithFlags(&x.decided, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.emitted, hipEventDisableTiming));
   }
   for (auto &r : e->ring)
     for (auto &ev : r) A(hipEventCreate(&ev));
+  e->maxStreams = c.max_streams ? c.max_streams : 3 * c.max_tracks;
+  A(dalloc(&e->dStreams, e->maxStreams));
+  A(dalloc(&e->dStreamHot, e->maxStreams));
+  A(dalloc(&e->dHist, size_t(e->maxStreams) * kHistWords));
+  A(dalloc(&e->dStreamRings, size_t(e->maxStreams) * kRangeCap));
+  A(dalloc(&e->dParsed, c.max_batch_pkts));
+  A(dalloc(&e->dFlows, c.max_batch_pkts));
+  A(dalloc(&e->dFwdFlag, c.max_batch_pkts));
+  A(dalloc(&e->dPos, c.max_batch_pkts));
+  const size_t ipart = (size_t(c.max_batch_pkts) + 1023) / 1024 + 1;
+  A(dalloc(&e->dIPartA, ipart));
+  A(dalloc(&e->dIPartB, ipart));
+  A(dalloc(&e->dITotal, 2));
+  A(dalloc(&e->dITBegin, c.max_tracks));
+  A(dalloc(&e->dITEnd, c.max_tracks));
+  A(dalloc(&e->dITRuns, c.max_tracks));
+  A(dalloc(&e->dIErr, 4));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
     A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
@@ -322,13 +379,18 @@ void lkf_destroy(lkf_engine *e) {
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
-                  e->dWaveTrack, e->dEvOff, e->dEvents, e->dCum, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm};
+                  e->dWaveTrack, e->dEvOff, e->dEvents, e->dCum, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
+                  e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
+                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr,
+                  e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
+                  e->dSpkCounts};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &x : e->ctx) {
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
-                 x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn};
+                 x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
+                 x.dRawPkts};
     for (void *p : q)
       if (p) (void)hipFree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
@@ -926,6 +988,258 @@ int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_m
   if (decide_ms) *decide_ms = sa;
   if (emit_ms) *emit_ms = sb;
   if (total_ms) *total_ms = c;
+  return LKF_OK;
+}
+
+// ---- ingress ------------------------------------------------------------------
+
+// NewBuffer + Bind (buffer.go:124-215); AudioLevelParams defaults config.go:380-385.
+int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p) {
+  if (!e || !p || p->track < 0 || p->track >= int32_t(e->tracks.size())) return LKF_EINVAL;
+  if (e->streams.size() >= e->maxStreams) return LKF_ENOSPC;
+  const lkf_track_params &tp = e->tracks[p->track];
+  DevStream d;
+  std::memset(&d, 0, sizeof(d));
+  d.track = uint32_t(p->track);
+  d.layer = p->layer;
+  d.ssrc = p->ssrc;
+  d.clockRate = tp.clock_rate;
+  d.codec = tp.codec;
+  d.levelExt = p->audio_level_ext;
+  const bool dflt = !p->active_level && !p->min_percentile && !p->observe_duration_ms && !p->smooth_intervals;
+  d.activeLevel = dflt ? 35 : p->active_level;
+  d.minPercentile = dflt ? 40 : p->min_percentile;
+  d.observeDuration = dflt ? 400 : p->observe_duration_ms;
+  const uint32_t smooth = dflt ? 2 : p->smooth_intervals;
+  d.minActiveDuration = uint32_t(d.minPercentile) * d.observeDuration / 100;  // audiolevel.go:55
+  d.smoothFactor = smooth > 0 ? double(2) / double(smooth + 1) : 1.0;
+  d.activeThreshold = std::pow(10.0, double(d.activeLevel) * (-1.0 / 20));  // ConvertAudioLevel
+  e->streams.push_back(*p);
+  e->pendStreams.push_back(d);
+  e->spkDirty = true;
+  return int32_t(e->streams.size() - 1);
+}
+
+static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, uint32_t n, const uint8_t *dRaw,
+                         uint64_t rawLen) {
+  const uint32_t nt = uint32_t(e->tracks.size());
+  hipStream_t s = e->own;
+  HIPCHK(hipMemsetAsync(e->dITBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dITEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dITRuns, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dIErr, 0, 4 * sizeof(uint32_t), s), "memset");
+  HIPCHK(hipMemsetAsync(e->dITotal, 0, 2 * sizeof(uint64_t), s), "memset");
+  IngestLaunch a;
+  a.raws = dRaws;
+  a.n = n;
+  a.raw = dRaw;
+  a.streams = e->dStreams;
+  a.nstreams = uint32_t(e->streams.size());
+  a.ntracks = nt;
+  a.hot = e->dStreamHot;
+  a.hist = e->dHist;
+  a.rings = e->dStreamRings;
+  a.parsed = e->dParsed;
+  a.tBegin = e->dITBegin;
+  a.tEnd = e->dITEnd;
+  a.tRuns = e->dITRuns;
+  a.err = e->dIErr;
+  a.flows = e->dFlows;
+  a.fwd = e->dFwdFlag;
+  a.pos = e->dPos;
+  a.partA = e->dIPartA;
+  a.partB = e->dIPartB;
+  a.total = e->dITotal;
+  a.out = x.dPktsOwn;
+  HIPCHK(launch_ingest(s, a), "ingest");
+  uint64_t total = 0;
+  uint32_t err = 0;
+  HIPCHK(hipMemcpyAsync(&total, e->dITotal, sizeof(total), hipMemcpyDeviceToHost, s), "total copy");
+  HIPCHK(hipMemcpyAsync(&err, e->dIErr, sizeof(err), hipMemcpyDeviceToHost, s), "err copy");
+  HIPCHK(hipStreamSynchronize(s), "ingest sync");
+  e->lastIngestN = n;
+  if (err & 3u) {
+    e->err = "raw batch not grouped by track / bad stream handle";
+    return LKF_EORDER;
+  }
+  e->curPkts = x.dPktsOwn;
+  e->curN = uint32_t(total);
+  e->curArena = dRaw;
+  e->curArenaLen = rawLen;
+  e->haveBatch = true;
+  return LKF_OK;
+}
+
+int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len) {
+  if (!e || (n && (!pkts || !raw))) return LKF_EINVAL;
+  if (n > e->cfg.max_batch_pkts || raw_len > e->cfg.max_batch_arena) return LKF_ENOSPC;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  BatchCtx &x = e->ctx[e->nRuns & 1];
+  if (x.used) HIPCHK(hipEventSynchronize(x.emitted), "wait emit");  // batch n-2 still reads these buffers
+  if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->own),
+                "raw pkts");
+  if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->own), "raw arena");
+  return ingest_common(e, x, x.dRawPkts, n, x.dArenaOwn, raw_len);
+}
+
+int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, const uint8_t *d_raw, uint64_t raw_len) {
+  if (!e || (n && (!d_pkts || !d_raw))) return LKF_EINVAL;
+  if (n > e->cfg.max_batch_pkts) return LKF_ENOSPC;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  BatchCtx &x = e->ctx[e->nRuns & 1];
+  if (x.used) HIPCHK(hipEventSynchronize(x.emitted), "wait emit");
+  return ingest_common(e, x, d_pkts, n, d_raw, raw_len);
+}
+
+int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !n_out) return LKF_EINVAL;
+  *n_out = e->lastIngestN;
+  if (cap < e->lastIngestN) return LKF_ENOSPC;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  if (e->lastIngestN)
+    HIPCHK(hipMemcpy(out, e->dFlows, size_t(e->lastIngestN) * sizeof(lkf_flow), hipMemcpyDeviceToHost), "flows");
+  return LKF_OK;
+}
+
+int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !n_out) return LKF_EINVAL;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  const uint32_t n = e->haveBatch ? e->curN : 0;
+  *n_out = n;
+  if (cap < n) return LKF_ENOSPC;
+  if (n) HIPCHK(hipMemcpy(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyDeviceToHost), "ingested copy");
+  return LKF_OK;
+}
+
+int lkf_stream_stats_get(lkf_engine *e, int32_t sid, lkf_stream_stats *o) {
+  if (!e || !o || sid < 0 || sid >= int32_t(e->streams.size())) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  StreamHot h;
+  HIPCHK(hipMemcpy(&h, e->dStreamHot + sid, sizeof(h), hipMemcpyDeviceToHost), "stream state copy");
+  std::memset(o, 0, sizeof(*o));
+  o->initialized = (h.flags & S_INIT) ? 1 : 0;
+  o->ext_start_sn = h.snStart;  // WrapAround.GetExtendedStart = ET(start)
+  o->ext_highest_sn = h.snExtHighest;
+  o->ext_start_ts = h.tsStart;
+  o->ext_highest_ts = h.tsExtHighest;
+  o->packets_lost = h.packetsLost;
+  o->packets_out_of_order = h.packetsOutOfOrder;
+  o->packets_duplicate = h.packetsDuplicate;
+  o->packets_padding = h.packetsPadding;
+  o->bytes = h.bytes;
+  o->header_bytes = h.headerBytes;
+  o->bytes_duplicate = h.bytesDuplicate;
+  o->bytes_padding = h.bytesPadding;
+  o->frames = h.frames;
+  return LKF_OK;
+}
+
+// Room -> participant -> microphone-stream tables for k_speakers.
+static int rebuild_speakers(lkf_engine *e) {
+  // primary receiver of a track = its layer-0 stream (first added)
+  std::vector<int> primary(e->tracks.size(), -1);
+  for (size_t sid = 0; sid < e->streams.size(); sid++) {
+    const auto &sp = e->streams[sid];
+    if (sp.layer == 0 && primary[sp.track] < 0) primary[sp.track] = int(sid);
+  }
+  // (room, participant) -> mic streams with an AudioLevel
+  std::vector<std::pair<std::pair<uint32_t, uint32_t>, uint32_t>> rows;
+  for (size_t t = 0; t < e->tracks.size(); t++) {
+    const auto &tp = e->tracks[t];
+    if (!tp.is_mic || primary[t] < 0 || !e->streams[primary[t]].audio_level_ext) continue;
+    rows.push_back({{tp.room, tp.publisher}, uint32_t(primary[t])});
+  }
+  std::stable_sort(rows.begin(), rows.end(),
+                   [](const auto &a, const auto &b) { return a.first < b.first; });
+  std::vector<uint32_t> roomOff, roomId, partId, partMicOff, mics;
+  for (size_t i = 0; i < rows.size();) {
+    const uint32_t room = rows[i].first.first;
+    roomId.push_back(room);
+    roomOff.push_back(uint32_t(partId.size()));
+    while (i < rows.size() && rows[i].first.first == room) {
+      const uint32_t part = rows[i].first.second;
+      partId.push_back(part);
+      partMicOff.push_back(uint32_t(mics.size()));
+      while (i < rows.size() && rows[i].first.first == room && rows[i].first.second == part) mics.push_back(rows[i++].second);
+    }
+    if (partId.size() - roomOff.back() > 64) {
+      e->err = "more than 64 microphone participants in a room";
+      return LKF_ENOSPC;
+    }
+  }
+  roomOff.push_back(uint32_t(partId.size()));
+  partMicOff.push_back(uint32_t(mics.size()));
+  e->nRooms = uint32_t(roomId.size());
+  uint32_t **bufs[] = {&e->dRoomPartOff, &e->dPartId, &e->dPartMicOff, &e->dMics, &e->dRoomId};
+  const std::vector<uint32_t> *src[] = {&roomOff, &partId, &partMicOff, &mics, &roomId};
+  for (int i = 0; i < 5; i++) {
+    if (*bufs[i]) HIPCHK(hipFree(*bufs[i]), "free");
+    HIPCHK(dalloc(bufs[i], std::max<size_t>(src[i]->size(), 1)), "alloc speakers table");
+    if (!src[i]->empty())
+      HIPCHK(hipMemcpy(*bufs[i], src[i]->data(), src[i]->size() * sizeof(uint32_t), hipMemcpyHostToDevice),
+             "speakers table copy");
+  }
+  if (e->spkCap < size_t(e->nRooms) * 64) {
+    if (e->dSpkSlots) HIPCHK(hipFree(e->dSpkSlots), "free");
+    if (e->dSpkCounts) HIPCHK(hipFree(e->dSpkCounts), "free");
+    e->spkCap = std::max<size_t>(size_t(e->nRooms) * 64, 64);
+    HIPCHK(dalloc(&e->dSpkSlots, e->spkCap), "alloc slots");
+    HIPCHK(dalloc(&e->dSpkCounts, e->spkCap / 64 + 1), "alloc counts");
+  }
+  e->spkDirty = false;
+  return LKF_OK;
+}
+
+int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !n_out) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  if (e->spkDirty) {
+    rc = rebuild_speakers(e);
+    if (rc) return rc;
+  }
+  *n_out = 0;
+  if (e->nRooms == 0) return LKF_OK;
+  SpeakersLaunch a;
+  a.nrooms = e->nRooms;
+  a.roomPartOff = e->dRoomPartOff;
+  a.partId = e->dPartId;
+  a.partMicOff = e->dPartMicOff;
+  a.mics = e->dMics;
+  a.roomId = e->dRoomId;
+  a.streams = e->dStreams;
+  a.hot = e->dStreamHot;
+  a.nowNs = now_ns;
+  a.slots = e->dSpkSlots;
+  a.counts = e->dSpkCounts;
+  HIPCHK(launch_speakers(e->own, a), "speakers");
+  std::vector<uint32_t> counts(e->nRooms);
+  std::vector<lkf_speaker> slots(size_t(e->nRooms) * 64);
+  HIPCHK(hipMemcpyAsync(counts.data(), e->dSpkCounts, counts.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        e->own),
+         "counts copy");
+  HIPCHK(hipMemcpyAsync(slots.data(), e->dSpkSlots, slots.size() * sizeof(lkf_speaker), hipMemcpyDeviceToHost,
+                        e->own),
+         "slots copy");
+  HIPCHK(hipStreamSynchronize(e->own), "speakers sync");
+  uint32_t k = 0;
+  for (uint32_t r = 0; r < e->nRooms; r++) k += counts[r];
+  *n_out = k;
+  if (cap < k) return LKF_ENOSPC;
+  k = 0;
+  for (uint32_t r = 0; r < e->nRooms; r++)
+    for (uint32_t j = 0; j < counts[r]; j++) out[k++] = slots[size_t(r) * 64 + j];
   return LKF_OK;
 }
 

@@ -937,7 +937,7 @@ constexpr int SCAN_ITEMS = 4;
 constexpr int SCAN_TILE = SCAN_T * SCAN_ITEMS;
 
 struct ScanIn {
-  int mode;  // 0: slots = npkts(track(d)) if active; 1: (fwdCnt, fwdBytes)
+  int mode;  // 0: slots = npkts(track(d)) if active; 1: (fwdCnt, fwdBytes); 2: u32 flags
   const u32 *perm;  // position -> DownTrack (nullptr: identity)
   const DevDT *dts;
   const u32 *tBegin, *tEnd;
@@ -947,6 +947,11 @@ struct ScanIn {
 
 __device__ __forceinline__ void scan_load(const ScanIn &in, u32 i, u64 &a, u64 &b) {
   const u32 d = in.perm ? in.perm[i] : i;
+  if (in.mode == 2) {  // u32 flags (ingress forward flags)
+    a = in.cnt[i];
+    b = 0;
+    return;
+  }
   if (in.mode == 0) {
     DevDT dt = in.dts[d];
     a = dt.active ? u64(in.tEnd[dt.track] - in.tBegin[dt.track]) : 0;

@@ -137,6 +137,66 @@ struct DevTrack {  // track table (24 x 4 B)
   uint32_t pad[3];
 };
 
+// ---- ingress: one received stream = one buffer.Buffer (buffer.go:66-130) ----
+constexpr int kHistWords = 64;  // cHistorySize 4096 bits (rtpstats_receiver.go:30)
+
+struct DevStream {  // static stream parameters (64 B)
+  uint32_t track;
+  int32_t layer;
+  uint32_t ssrc;
+  uint32_t clockRate;
+  uint8_t codec, levelExt, activeLevel, minPercentile;
+  uint32_t observeDuration;  // ms
+  uint32_t minActiveDuration;
+  uint32_t pad0;
+  double smoothFactor;
+  double activeThreshold;  // ConvertAudioLevel(ActiveLevel)
+  uint32_t pad1[4];
+};
+static_assert(sizeof(DevStream) == 64, "DevStream must be 64 B");
+
+enum : uint32_t {
+  S_INIT = 1u << 0,       // RTPStatsReceiver.initialized
+  S_SN_INIT = 1u << 1,    // WrapAround sequenceNumber initialized
+  S_TS_INIT = 1u << 2,    // WrapAround timestamp initialized
+  S_LVL_TS_INIT = 1u << 3 // latestTSForAudioLevelInitialized
+};
+
+struct alignas(16) StreamHot {  // per-stream ingress state (256 B)
+  // WrapAround<uint16, uint64> / WrapAround<uint32, uint64> (wraparound.go:33-186)
+  uint64_t snCycles, snExtHighest, tsCycles, tsExtHighest;
+  // padding-exclusion RangeMap(100) open range (buffer.go:134)
+  uint64_t rmOpenStart, rmOpenValue;
+  // RTPStatsReceiver counters
+  uint64_t packetsLost, packetsOutOfOrder, packetsDuplicate, packetsPadding;
+  uint64_t bytes, headerBytes, bytesDuplicate, headerBytesDuplicate, bytesPadding, headerBytesPadding, frames;
+  // AudioLevel (audiolevel.go:36-50)
+  double smoothedLevel;
+  int64_t lastObservedNs;
+  uint32_t activeDuration, observedDuration;
+  uint32_t tsStart, tsHighest;
+  uint32_t latestTSForAudioLevel;
+  uint32_t flags;
+  uint16_t snStart, snHighest;
+  uint16_t rmHead, rmCount;
+  uint8_t loudest;
+  uint8_t pad[71];
+};
+static_assert(sizeof(StreamHot) == 256, "StreamHot must be 256 B");
+
+struct alignas(16) IngParsed {  // k_ing_parse -> k_ing_stream / k_ing_out (48 B)
+  uint32_t ts, ssrc;
+  uint16_t sn, hdrSize, payloadLen;
+  uint8_t paddingSize, flags;  // IP_*
+  uint8_t level, b0, b1;
+  uint8_t vfirst, vbits, vhs, tl0, tid, keyidx;
+  uint16_t pid;
+  uint32_t track;
+  uint8_t pad[16];
+};
+static_assert(sizeof(IngParsed) == 48, "IngParsed must be 48 B");
+enum : uint8_t { IP_OK = 1, IP_MARKER = 2, IP_LEVEL = 4, IP_VP8 = 8, IP_KF = 16, IP_VP8_BAD = 32 };
+
 struct DevEvent {  // one queued lkf_ctl op (48 B)
   uint32_t at;
   int32_t op;

@@ -1,0 +1,674 @@
+// ingress_kernels.hip — gfx950 kernels of the ingress path (Buffer.calc) and
+// the active-speaker ranking.
+//
+// Per raw batch (lkf_ingest):
+//   k_ing_parse    thread per datagram: rtp.Packet.Unmarshal (pion/rtp
+//                  v1.8.3, restated), the ssrc-audio-level extension
+//                  (RFC 6464) and the VP8 payload descriptor
+//                  (buffer/helpers.go:76-162)
+//   k_ing_ranges   datagrams grouped by track -> [begin, end) per track
+//   k_ing_stream   one lane per received stream (buffer.Buffer), serial over
+//                  its datagrams: processHeaderExtensions -> AudioLevel.Observe
+//                  (buffer.go:573-596, audiolevel.go:70-102),
+//                  RTPStatsReceiver.Update (rtpstats_receiver.go:76-241) with
+//                  its WrapArounds and 4096-bit history, NACK loss ranges
+//                  (buffer.go:545-567), padding exclusion + SN adjustment
+//                  (buffer.go:439-471)
+//   scan           positions of the ExtPackets produced
+//   k_ing_out      thread per datagram: the ExtPacket (getExtPacket
+//                  buffer.go:599-671) as an lkf_pkt of the forwarding batch
+// Speakers (lkf_speakers):
+//   k_speakers     one wave per room, lane per participant: loudest active
+//                  microphone (AudioLevel.GetLevel audiolevel.go:105-112,
+//                  uptrackmanager.go:422-436), rank, quantise (room.go:254-279)
+#include <hip/hip_runtime.h>
+
+#include "../../include/lkfwd.h"
+#include "fwd_state.h"
+#include "kernels.h"
+
+namespace lkf {
+
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+using i32 = int32_t;
+using i64 = int64_t;
+
+// ---------------------------------------------------------------------------
+// k_ing_parse
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, IngParsed &q, int &levelOff) {
+  levelOff = -1;
+  if (len < 12) return false;
+  q.b0 = buf[0];
+  q.b1 = buf[1];
+  const bool padding = (buf[0] >> 5) & 1, extension = (buf[0] >> 4) & 1;
+  const int cc = buf[0] & 0xf;
+  int n = 12 + 4 * cc;
+  if (len < n) return false;
+  q.sn = u16((u32(buf[2]) << 8) | buf[3]);
+  q.ts = (u32(buf[4]) << 24) | (u32(buf[5]) << 16) | (u32(buf[6]) << 8) | buf[7];
+  q.ssrc = (u32(buf[8]) << 24) | (u32(buf[9]) << 16) | (u32(buf[10]) << 8) | buf[11];
+  if (extension) {
+    if (len < n + 4) return false;
+    const u32 profile = (u32(buf[n]) << 8) | buf[n + 1];
+    n += 2;
+    const int extLen = int((u32(buf[n]) << 8) | buf[n + 1]) * 4;
+    n += 2;
+    const int extEnd = n + extLen;
+    if (len < extEnd) return false;
+    if (profile == 0xBEDE || profile == 0x1000) {
+      bool seen = false;  // Header.GetExtension returns the first element with the id
+      while (n < extEnd) {
+        if (buf[n] == 0x00) {
+          n++;
+          continue;
+        }
+        u8 id;
+        int pl;
+        if (profile == 0xBEDE) {
+          id = buf[n] >> 4;
+          pl = (buf[n] & 0x0f) + 1;
+          n++;
+          if (id == 15) break;
+        } else {
+          id = buf[n];
+          n++;
+          if (len <= n) return false;
+          pl = buf[n];
+          n++;
+        }
+        if (len <= n + pl) return false;
+        if (levelExt && id == levelExt && !seen) {
+          seen = true;
+          if (pl >= 1) levelOff = n;  // AudioLevelExtension.Unmarshal needs 1 byte
+        }
+        n += pl;
+      }
+    } else {  // RFC 3550 extension: a single element with id 0 (never the level id)
+      n = extEnd;
+    }
+  }
+  int end = len;
+  int padSize = 0;
+  if (padding) {
+    if (end <= n) return false;
+    padSize = buf[end - 1];
+    end -= padSize;
+  }
+  if (end < n) return false;
+  q.hdrSize = u16(n);
+  q.payloadLen = u16(end - n);
+  q.paddingSize = u8(padSize);
+  if (buf[1] & 0x80) q.flags |= IP_MARKER;
+  return true;
+}
+
+// buffer.VP8.Unmarshal helpers.go:76-162
+__device__ __forceinline__ bool vp8_parse(const u8 *p, int len, IngParsed &q) {
+  if (len < 1) return false;
+  int idx = 0;
+  q.vfirst = p[0];
+  const bool S = (p[0] & 0x10) != 0;
+  bool I = false, L = false, T = false, K = false, M = false, Y = false;
+  u16 pid = 0;
+  u8 tl0 = 0, tid = 0, keyidx = 0;
+  bool kf;
+  if (p[0] & 0x80) {
+    idx++;
+    if (len < idx + 1) return false;
+    I = (p[idx] & 0x80) != 0;
+    L = (p[idx] & 0x40) != 0;
+    T = (p[idx] & 0x20) != 0;
+    K = (p[idx] & 0x10) != 0;
+    if (L && !T) return false;
+    if (I) {
+      idx++;
+      if (len < idx + 1) return false;
+      const u8 lo7 = p[idx] & 0x7f;
+      M = (p[idx] & 0x80) != 0;
+      if (M) {
+        idx++;
+        if (len < idx + 1) return false;
+        pid = u16((u16(lo7) << 8) | p[idx]);
+      } else {
+        pid = lo7;
+      }
+    }
+    if (L) {
+      idx++;
+      if (len < idx + 1) return false;
+      tl0 = p[idx];
+    }
+    if (T || K) {
+      idx++;
+      if (len < idx + 1) return false;
+      if (T) {
+        tid = (p[idx] & 0xc0) >> 6;
+        Y = (p[idx] & 0x20) != 0;
+      }
+      if (K) keyidx = p[idx] & 0x1f;
+    }
+    idx++;
+    if (len < idx + 1) return false;
+    kf = (p[idx] & 0x01) == 0 && S;
+  } else {
+    idx++;
+    if (len < idx + 1) return false;
+    kf = (p[idx] & 0x01) == 0 && S;
+  }
+  q.vbits = u8((S ? LKF_VP8_S : 0) | (I ? LKF_VP8_I : 0) | (M ? LKF_VP8_M : 0) | (L ? LKF_VP8_L : 0) |
+               (T ? LKF_VP8_T : 0) | (Y ? LKF_VP8_Y : 0) | (K ? LKF_VP8_K : 0));
+  q.vhs = u8(idx);
+  q.pid = pid;
+  q.tl0 = tl0;
+  q.tid = tid;
+  q.keyidx = keyidx;
+  if (kf) q.flags |= IP_KF;
+  return true;
+}
+
+__global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u8 *__restrict__ raw,
+                            const DevStream *__restrict__ streams, u32 nstreams, IngParsed *__restrict__ out,
+                            u32 *__restrict__ err) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const lkf_raw_pkt rp = raws[i];
+  IngParsed q = {};
+  if (rp.stream >= nstreams) {
+    atomicOr(err, 1u);
+    q.track = 0xffffffffu;
+    out[i] = q;
+    return;
+  }
+  const DevStream s = streams[rp.stream];
+  q.track = s.track;
+  const u8 *b = raw + rp.off;
+  int levelOff = -1;
+  if (rtp_parse(b, int(rp.len), s.levelExt, q, levelOff)) {
+    q.flags |= IP_OK;
+    if (levelOff >= 0) {  // AudioLevelExtension.Unmarshal: level = b & 0x7f
+      q.flags |= IP_LEVEL;
+      q.level = b[levelOff] & 0x7f;
+    }
+    if (s.codec == LKF_CODEC_VP8 && q.payloadLen > 0) {
+      if (vp8_parse(b + q.hdrSize, q.payloadLen, q))
+        q.flags |= IP_VP8;
+      else
+        q.flags |= IP_VP8_BAD;
+    }
+  }
+  out[i] = q;
+}
+
+__global__ void k_ing_ranges(const IngParsed *__restrict__ q, u32 n, u32 ntracks, u32 *__restrict__ tBegin,
+                             u32 *__restrict__ tEnd, u32 *__restrict__ tRuns, u32 *__restrict__ err) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32 t = q[i].track;
+  if (t >= ntracks) {
+    atomicOr(err, 1u);
+    return;
+  }
+  const u32 tp = i > 0 ? q[i - 1].track : 0xffffffffu;
+  const u32 tn = i + 1 < n ? q[i + 1].track : 0xffffffffu;
+  if (tp != t) {
+    tBegin[t] = i;
+    if (atomicAdd(&tRuns[t], 1u) != 0) atomicOr(err, 2u);
+  }
+  if (tn != t) tEnd[t] = i + 1;
+}
+
+// ---------------------------------------------------------------------------
+// k_ing_stream helpers: WrapAround (wraparound.go:68-180, restart disallowed),
+// protocol utils.Bitmap (4096 bits), utils.RangeMap(100), AudioLevel.
+// ---------------------------------------------------------------------------
+struct WAResult {
+  bool unhandled;
+  u64 preHighest, extVal;
+};
+
+// WrapAround<uint16,uint64>{IsRestartAllowed: false}.Update
+__device__ __forceinline__ WAResult wa16_update(StreamHot &h, u16 val) {
+  WAResult r = {false, 0, 0};
+  const u64 full = 1ull << 16;
+  if (!(h.flags & S_SN_INIT)) {
+    r.preHighest = u64(val) - 1;
+    r.extVal = u64(val);
+    h.snStart = val;
+    h.snHighest = val;
+    h.snExtHighest = h.snCycles + u64(val);
+    h.flags |= S_SN_INIT;
+    return r;
+  }
+  const u16 gap = u16(val - h.snHighest);
+  if (gap > u16(full >> 1)) {  // maybeAdjustStart
+    u64 cyc = h.snCycles;
+    const u64 total = h.snExtHighest - u64(h.snStart) + 1;
+    const bool wrapBack = u64(h.snHighest) < (full >> 1) && u64(val) >= (full >> 1);
+    if (total > (full >> 1)) {
+      if (wrapBack) cyc -= full;
+      r.preHighest = h.snExtHighest;
+      r.extVal = cyc + u64(val);
+      return r;
+    }
+    if (u16(val - h.snStart) > u16(full >> 1)) {
+      r.unhandled = true;  // restart not allowed
+    } else if (wrapBack) {
+      cyc -= full;
+    }
+    r.preHighest = h.snExtHighest;
+    r.extVal = cyc + u64(val);
+    return r;
+  }
+  r.preHighest = h.snExtHighest;
+  if (val < h.snHighest) h.snCycles += full;
+  h.snHighest = val;
+  h.snExtHighest = h.snCycles + u64(val);
+  r.extVal = h.snExtHighest;
+  return r;
+}
+
+// WrapAround<uint32,uint64>{IsRestartAllowed: false}.Update
+__device__ __forceinline__ WAResult wa32_update(StreamHot &h, u32 val) {
+  WAResult r = {false, 0, 0};
+  const u64 full = 1ull << 32;
+  if (!(h.flags & S_TS_INIT)) {
+    r.preHighest = u64(val) - 1;
+    r.extVal = u64(val);
+    h.tsStart = val;
+    h.tsHighest = val;
+    h.tsExtHighest = h.tsCycles + u64(val);
+    h.flags |= S_TS_INIT;
+    return r;
+  }
+  const u32 gap = val - h.tsHighest;
+  if (gap > u32(full >> 1)) {
+    u64 cyc = h.tsCycles;
+    const u64 total = h.tsExtHighest - u64(h.tsStart) + 1;
+    const bool wrapBack = u64(h.tsHighest) < (full >> 1) && u64(val) >= (full >> 1);
+    if (total > (full >> 1)) {
+      if (wrapBack) cyc -= full;
+      r.preHighest = h.tsExtHighest;
+      r.extVal = cyc + u64(val);
+      return r;
+    }
+    if (u32(val - h.tsStart) > u32(full >> 1)) {
+      r.unhandled = true;
+    } else if (wrapBack) {
+      cyc -= full;
+    }
+    r.preHighest = h.tsExtHighest;
+    r.extVal = cyc + u64(val);
+    return r;
+  }
+  r.preHighest = h.tsExtHighest;
+  if (val < h.tsHighest) h.tsCycles += full;
+  h.tsHighest = val;
+  h.tsExtHighest = h.tsCycles + u64(val);
+  r.extVal = h.tsExtHighest;
+  return r;
+}
+
+__device__ __forceinline__ bool hist_isset(const u64 *hist, u64 v) {
+  return (hist[(v >> 6) & (kHistWords - 1)] >> (v & 63)) & 1;
+}
+__device__ __forceinline__ void hist_set(u64 *hist, u64 v) { hist[(v >> 6) & (kHistWords - 1)] |= 1ull << (v & 63); }
+__device__ void hist_clear_range(u64 *hist, u64 lo, u64 hi) {  // inclusive; lo > hi: no-op
+  if (lo > hi) return;
+  if (hi - lo + 1 >= u64(kHistWords) * 64) {
+    for (int w = 0; w < kHistWords; w++) hist[w] = 0;
+    return;
+  }
+  for (u64 v = lo;; v++) {
+    hist[(v >> 6) & (kHistWords - 1)] &= ~(1ull << (v & 63));
+    if (v == hi) break;
+  }
+}
+
+// utils.RangeMap[uint64,uint64](100): ExcludeRange (rangemap.go:100-132)
+__device__ bool irm_exclude(StreamHot &h, RangeEntry *ring, u64 s, u64 e) {
+  if (e == s || (e - s) > (1ull << 63)) return false;
+  if (h.rmOpenStart > s) return false;
+  const u64 nv = h.rmOpenValue + (e - s);
+  if (h.rmOpenStart == s) {
+    h.rmOpenStart = e;
+    h.rmOpenValue = nv;
+    return true;
+  }
+  RangeEntry c;
+  c.start = h.rmOpenStart;
+  c.end = s - 1;
+  c.value = h.rmOpenValue;
+  if (h.rmCount < kRangeCap) {
+    ring[(h.rmHead + h.rmCount) % kRangeCap] = c;
+    h.rmCount++;
+  } else {
+    ring[h.rmHead] = c;
+    h.rmHead = u16((h.rmHead + 1) % kRangeCap);
+  }
+  h.rmOpenStart = e;
+  h.rmOpenValue = nv;
+  return true;
+}
+// GetValue (rangemap.go:134-169)
+__device__ bool irm_get(const StreamHot &h, const RangeEntry *ring, u64 key, u64 &out) {
+  out = 0;
+  if (key >= h.rmOpenStart) {
+    out = h.rmOpenValue;
+    return true;
+  }
+  const int nc = h.rmCount;
+  const u64 firstStart = nc > 0 ? ring[h.rmHead].start : h.rmOpenStart;
+  if (key < firstStart) return false;
+  RangeEntry next;
+  next.start = h.rmOpenStart;
+  next.end = 0;
+  next.value = h.rmOpenValue;
+  const u64 half = 1ull << 63;
+  for (int idx = nc; idx >= 0; idx--) {
+    if (idx != nc) {
+      const RangeEntry rv = next;
+      if ((key - rv.start) < half && (rv.end - key) < half) {
+        out = rv.value;
+        return true;
+      }
+    }
+    if (idx > 0) {
+      const RangeEntry prev = ring[(h.rmHead + idx - 1) % kRangeCap];
+      const u64 before = key - prev.end, after = next.start - key;
+      if (before > 0 && before < half && after > 0 && after < half) return false;
+      next = prev;
+    }
+  }
+  return false;
+}
+
+// AudioLevel.Observe audiolevel.go:70-102
+__device__ void level_observe(StreamHot &h, const DevStream &s, u8 level, u32 durationMs, i64 arrivalNs) {
+  h.lastObservedNs = arrivalNs;
+  h.observedDuration += durationMs;
+  if (level <= s.activeLevel) {
+    h.activeDuration += durationMs;
+    if (h.loudest > level) h.loudest = level;
+  }
+  if (h.observedDuration >= s.observeDuration) {
+    double smoothed = 0.0;
+    if (h.activeDuration >= s.minActiveDuration) {
+      const double activityWeight = 20.0 * log10(double(h.activeDuration) / double(s.observeDuration));
+      const double adjusted = double(h.loudest) - activityWeight;
+      const double linear = pow(10.0, adjusted * (-1.0 / 20));
+      smoothed = h.smoothedLevel + (linear - h.smoothedLevel) * s.smoothFactor;
+    }
+    h.smoothedLevel = smoothed;
+    h.loudest = 127;
+    h.activeDuration = 0;
+    h.observedDuration = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_ing_stream: one lane per stream, serial over the stream's datagrams.
+// ---------------------------------------------------------------------------
+__global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
+                             const DevStream *__restrict__ streams, u32 nstreams, StreamHot *__restrict__ hot,
+                             u64 *__restrict__ hist, RangeEntry *__restrict__ rings, const u32 *__restrict__ tBegin,
+                             const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows, u32 *__restrict__ fwd) {
+  const u32 sid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sid >= nstreams) return;
+  const DevStream s = streams[sid];
+  const u32 pb = tBegin[s.track], pe = tEnd[s.track];
+  if (pb >= pe) return;
+  StreamHot h = hot[sid];
+  u64 *hs = hist + size_t(sid) * kHistWords;
+  RangeEntry *ring = rings + size_t(sid) * kRangeCap;
+  for (u32 i = pb; i < pe; i++) {
+    if (raws[i].stream != sid) continue;
+    const IngParsed p = q[i];
+    const i64 arrival = raws[i].arrival_ns;
+    lkf_flow f = {};
+    f.pkt = 0xffffffffu;
+    u32 forward = 0;
+    do {
+      if (!(p.flags & IP_OK)) {
+        f.flags = LKF_FLOW_BAD;
+        break;
+      }
+      // processHeaderExtensions (buffer.go:573-596)
+      if (s.levelExt) {
+        if (!(h.flags & S_LVL_TS_INIT)) {
+          h.flags |= S_LVL_TS_INIT;
+          h.latestTSForAudioLevel = p.ts;
+        }
+        if (p.flags & IP_LEVEL) {
+          if (u32(p.ts - h.latestTSForAudioLevel) < (1u << 31)) {
+            const i64 dur = (i64(p.ts) - i64(h.latestTSForAudioLevel)) * 1000 / i64(s.clockRate);
+            if (dur > 0) level_observe(h, s, p.level, u32(dur), arrival);
+            h.latestTSForAudioLevel = p.ts;
+          }
+        }
+      }
+      // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241)
+      const int hdrSize = p.hdrSize, payloadSize = p.payloadLen, paddingSize = p.paddingSize;
+      WAResult rsn, rts;
+      if (!(h.flags & S_INIT)) {
+        if (payloadSize == 0) {
+          f.flags = LKF_FLOW_NOT_HANDLED;
+          break;
+        }
+        h.flags |= S_INIT;
+        rsn = wa16_update(h, p.sn);
+        rts = wa32_update(h, p.ts);
+      } else {
+        rsn = wa16_update(h, p.sn);
+        if (rsn.unhandled) {
+          f.flags = LKF_FLOW_NOT_HANDLED;
+          break;
+        }
+        rts = wa32_update(h, p.ts);
+      }
+      const u64 pktSize = u64(hdrSize + payloadSize + paddingSize);
+      const i64 gapSN = i64(rsn.extVal - rsn.preHighest);
+      bool dup = false, ooo = false;
+      if (gapSN <= 0) {
+        if (gapSN != 0) h.packetsOutOfOrder++;
+        const i64 diff = i64(rsn.preHighest - rsn.extVal);
+        if (diff >= 0 && diff < i64(kHistWords) * 64) {  // isInRange :427-430
+          if (hist_isset(hs, rsn.extVal)) {
+            h.bytesDuplicate += pktSize;
+            h.headerBytesDuplicate += u64(hdrSize);
+            h.packetsDuplicate++;
+            dup = true;
+          } else {
+            h.packetsLost--;
+            hist_set(hs, rsn.extVal);
+          }
+        }
+        ooo = true;
+      } else {
+        hist_clear_range(hs, rsn.preHighest + 1, rsn.extVal - 1);
+        h.packetsLost += u64(gapSN - 1);
+        hist_set(hs, rsn.extVal);
+        if (gapSN > 1) {
+          f.flags |= LKF_FLOW_HAS_LOSS;
+          f.loss_start = rsn.preHighest + 1;
+          f.loss_end = rsn.extVal;
+        }
+      }
+      f.ext_sn = rsn.extVal;
+      f.ext_ts = rts.extVal;
+      if (!dup) {
+        if (payloadSize == 0) {
+          h.packetsPadding++;
+          h.bytesPadding += pktSize;
+          h.headerBytesPadding += u64(hdrSize);
+        } else {
+          h.bytes += pktSize;
+          h.headerBytes += u64(hdrSize);
+          if (p.flags & IP_MARKER) h.frames++;
+        }
+      }
+      if (dup) f.flags |= LKF_FLOW_DUPLICATE;
+      if (ooo) f.flags |= LKF_FLOW_OUT_OF_ORDER;
+      // Buffer.calc (buffer.go:439-489)
+      if (payloadSize == 0 && (!ooo || dup)) {
+        if (!ooo) irm_exclude(h, ring, rsn.extVal, rsn.extVal + 1);
+        f.flags |= LKF_FLOW_PADDING;
+        break;
+      }
+      u64 adj = 0;
+      if (!irm_get(h, ring, rsn.extVal, adj)) {
+        f.flags |= LKF_FLOW_BAD;
+        break;
+      }
+      f.ext_sn = rsn.extVal - adj;
+      if (dup) break;  // the RTX bucket already holds it (ErrRTXPacket)
+      if (p.flags & IP_VP8_BAD) {  // getExtPacket: VP8 unmarshal failed
+        f.flags |= LKF_FLOW_BAD;
+        break;
+      }
+      forward = 1;
+      f.flags |= LKF_FLOW_FORWARD;
+    } while (false);
+    flows[i] = f;
+    fwd[i] = forward;
+  }
+  hot[sid] = h;
+}
+
+// ---------------------------------------------------------------------------
+// k_ing_out: the ExtPacket of every forwarded datagram at its batch position
+// ---------------------------------------------------------------------------
+__global__ void k_ing_out(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
+                          const DevStream *__restrict__ streams, const u32 *__restrict__ fwd,
+                          const u64 *__restrict__ pos, u32 n, lkf_flow *__restrict__ flows,
+                          lkf_pkt *__restrict__ out) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !fwd[i]) return;
+  const u32 k = u32(pos[i]);
+  const IngParsed p = q[i];
+  const lkf_raw_pkt rp = raws[i];
+  const DevStream s = streams[rp.stream];
+  flows[i].pkt = k;
+  lkf_pkt e = {};
+  e.ext_sn = flows[i].ext_sn;
+  e.ext_ts = flows[i].ext_ts;
+  e.arrival_ns = rp.arrival_ns;
+  e.arena_off = rp.off;
+  e.track = s.track;
+  e.ssrc = p.ssrc;
+  e.payload_off = p.hdrSize;
+  e.payload_len = p.payloadLen;
+  e.hdr0 = p.b0;
+  e.hdr1 = p.b1;
+  e.spatial = -1;
+  e.temporal = p.payloadLen > 0 ? 0 : -1;
+  e.layer = int8_t(s.layer);
+  if (p.flags & IP_LEVEL) {
+    e.flags |= LKF_PKT_HAS_LEVEL;
+    e.audio_level = p.level;
+  }
+  if (p.flags & IP_VP8) {
+    e.flags |= LKF_PKT_VP8 | ((p.flags & IP_KF) ? LKF_PKT_KEYFRAME : 0);
+    e.temporal = int8_t(p.tid);
+    e.vp8_first = p.vfirst;
+    e.vp8_bits = p.vbits;
+    e.vp8_hdr_size = p.vhs;
+    e.vp8_picture_id = p.pid;
+    e.vp8_tl0picidx = p.tl0;
+    e.vp8_tid = p.tid;
+    e.vp8_keyidx = p.keyidx;
+  }
+  out[k] = e;
+}
+
+// ---------------------------------------------------------------------------
+// k_speakers: wave per room, lane per participant (<= 64 per room).
+// partMics[partOff[r*64 + j] .. ) lists participant j's microphone streams.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_speakers(const u32 *__restrict__ roomPartOff, const u32 *__restrict__ partId,
+                                                 const u32 *__restrict__ partMicOff, const u32 *__restrict__ mics,
+                                                 const DevStream *__restrict__ streams, StreamHot *__restrict__ hot,
+                                                 i64 nowNs, lkf_speaker *__restrict__ slots, u32 *__restrict__ counts,
+                                                 const u32 *__restrict__ roomId) {
+  const u32 r = blockIdx.x;
+  const u32 lane = threadIdx.x;
+  const u32 p0 = roomPartOff[r], p1 = roomPartOff[r + 1];
+  const u32 np = p1 - p0;  // host guarantees <= 64
+  const bool live = lane < np;
+  double level = 0.0;
+  bool active = false;
+  u32 pid = 0;
+  if (live) {
+    const u32 pi = p0 + lane;
+    pid = partId[pi];
+    for (u32 m = partMicOff[pi]; m < partMicOff[pi + 1]; m++) {
+      const u32 sid = mics[m];
+      const DevStream s = streams[sid];
+      StreamHot &h = hot[sid];
+      // GetLevel -> resetIfStaleLocked (Milliseconds() truncates toward zero)
+      if (!((nowNs - h.lastObservedNs) / 1000000 < i64(2 * s.observeDuration))) {
+        h.smoothedLevel = 0.0;
+        h.loudest = 127;
+        h.activeDuration = 0;
+        h.observedDuration = 0;
+      }
+      const double lv = h.smoothedLevel;
+      if (lv >= s.activeThreshold) {
+        active = true;
+        if (lv > level) level = lv;
+      }
+    }
+  }
+  const float lf = float(level);
+  // rank among the active participants: level descending, participant ascending
+  u32 rank = 0;
+  for (u32 j = 0; j < 64; j++) {
+    const float lj = __shfl(lf, int(j), 64);
+    const int aj = __shfl(int(active), int(j), 64);
+    const u32 pj = u32(__shfl(int(pid), int(j), 64));
+    if (live && active && aj && j < np && j != lane && (lj > lf || (lj == lf && pj < pid))) rank++;
+  }
+  const u64 am = __ballot(live && active);
+  if (live && active) {
+    lkf_speaker o;
+    o.room = roomId[r];
+    o.participant = pid;
+    o.level = float(ceil(double(lf * 8.0f)) * (1.0 / 8));  // room.go:274-276
+    o.active = 1;
+    slots[size_t(r) * 64 + rank] = o;
+  }
+  if (lane == 0) counts[r] = u32(__popcll(am));
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
+
+hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ing_parse, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.n, a.raw, a.streams, a.nstreams,
+                     a.parsed, a.err);
+  hipLaunchKernelGGL(k_ing_ranges, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.parsed, a.n, a.ntracks, a.tBegin, a.tEnd,
+                     a.tRuns, a.err);
+  hipLaunchKernelGGL(k_ing_stream, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a.raws, a.parsed, a.streams,
+                     a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd);
+  hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
+                             a.total, nullptr, nullptr);
+  if (r != hipSuccess) return r;
+  hipLaunchKernelGGL(k_ing_out, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.parsed, a.streams, a.fwd, a.pos,
+                     a.n, a.flows, a.out);
+  return hipGetLastError();
+}
+
+hipError_t launch_speakers(hipStream_t st, const SpeakersLaunch &a) {
+  if (a.nrooms == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_speakers, dim3(a.nrooms), dim3(64), 0, st, a.roomPartOff, a.partId, a.partMicOff, a.mics,
+                     a.streams, a.hot, a.nowNs, a.slots, a.counts, a.roomId);
+  return hipGetLastError();
+}
+
+}  // namespace lkf

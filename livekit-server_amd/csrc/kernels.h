@@ -59,6 +59,35 @@ hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t
                        const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
                        uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB,
                        const uint32_t *perm);
+struct IngestLaunch {
+  const lkf_raw_pkt *raws;
+  uint32_t n;
+  const uint8_t *raw;
+  const DevStream *streams;
+  uint32_t nstreams, ntracks;
+  StreamHot *hot;
+  uint64_t *hist;
+  RangeEntry *rings;
+  IngParsed *parsed;
+  uint32_t *tBegin, *tEnd, *tRuns, *err;
+  lkf_flow *flows;
+  uint32_t *fwd;
+  uint64_t *pos, *partA, *partB, *total;
+  lkf_pkt *out;
+};
+
+struct SpeakersLaunch {
+  uint32_t nrooms;
+  const uint32_t *roomPartOff, *partId, *partMicOff, *mics, *roomId;
+  const DevStream *streams;
+  StreamHot *hot;
+  int64_t nowNs;
+  lkf_speaker *slots;
+  uint32_t *counts;
+};
+
+hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a);
+hipError_t launch_speakers(hipStream_t s, const SpeakersLaunch &a);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
 hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum);

@@ -60,6 +60,7 @@ struct Plan {
 struct TrackGen {
   lkf_track_params p;
   int nlayers = 1;
+  u32 ssrc[3] = {0, 0, 0};  // per received layer (one ingress stream each)
   std::vector<Plan> plans;  // merged arrival order
 };
 
@@ -81,6 +82,8 @@ struct lkfs_trace {
   std::vector<u64> batch_pkt_off;    // nb+1
   std::vector<u64> batch_arena_off;  // nb+1
   std::vector<lkf_pkt> pkts;
+  std::vector<lkf_raw_pkt> raws;  // the same datagrams as raw ingress input
+  std::vector<lkf_stream_params> streams;
   std::vector<u8> arena;
   std::vector<u64> batch_ev_off;
   std::vector<lkfs_event> events;
@@ -294,6 +297,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       for (int l = 0; l < g.nlayers; l++) {
         int lq = g.nlayers == 1 ? 0 : l;
         u32 ssrc = u32(rng.next()) | 1u;
+        g.ssrc[l] = ssrc;
         u64 sn = u64(u16(rng.next()));
         u16 pid0 = u16(rng.next() & 0x7fff);
         u8 tl00 = u8(rng.next());
@@ -338,6 +342,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       }
     } else {
       u32 ssrc = u32(rng.next()) | 1u;
+      g.ssrc[0] = ssrc;
       u64 sn = u64(u16(rng.next()));
       u32 ts0 = u32(rng.next());
       int npk = int(dur * 50.0);
@@ -390,6 +395,19 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   }
 
   for (auto &g : tg) tr->tracks.push_back(g.p);
+  // ingress streams: one per received SSRC (video layer / audio), in track order
+  std::vector<u32> streamBase(tg.size());
+  for (size_t ti = 0; ti < tg.size(); ti++) {
+    streamBase[ti] = u32(tr->streams.size());
+    for (int l = 0; l < tg[ti].nlayers; l++) {
+      lkf_stream_params sp{};
+      sp.track = int32_t(ti);
+      sp.layer = l;
+      sp.ssrc = tg[ti].ssrc[l];
+      sp.audio_level_ext = tg[ti].p.kind == LKF_KIND_AUDIO ? 1 : 0;
+      tr->streams.push_back(sp);
+    }
+  }
 
   // ---- batches ------------------------------------------------------------
   const u32 nb = u32((durNs + batchNs - 1) / batchNs + 1);  // +1: network delay tail
@@ -482,6 +500,12 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
           d.spatial = -1;
           d.temporal = 0;  // buffer.go:616
         }
+        lkf_raw_pkt rp{};
+        rp.arrival_ns = pl.arrival;
+        rp.stream = streamBase[ti] + u32(g.nlayers == 1 ? 0 : pl.layer);
+        rp.off = d.arena_off;
+        rp.len = u32(kPayloadOff) + pl.payload_len;
+        tr->raws.push_back(rp);
         aoff += (u64(kPayloadOff) + pl.payload_len + 15) & ~u64(15);
         tr->pkts.push_back(d);
       }
@@ -551,6 +575,15 @@ extern "C" int lkfs_batch(const lkfs_trace *t, uint32_t b, const lkf_pkt **pkts,
   *arena = t->arena.data() + t->batch_arena_off[b];
   *arena_len = t->batch_arena_off[b + 1] - t->batch_arena_off[b];
   return LKF_OK;
+}
+
+extern "C" uint32_t lkfs_num_streams(const lkfs_trace *t) { return u32(t->streams.size()); }
+extern "C" const lkf_stream_params *lkfs_streams(const lkfs_trace *t) { return t->streams.data(); }
+extern "C" int lkfs_batch_raw(const lkfs_trace *t, uint32_t b, const lkf_raw_pkt **raws, uint32_t *n) {
+  if (b + 1 >= t->batch_pkt_off.size()) return -1;
+  *raws = t->raws.data() + t->batch_pkt_off[b];
+  *n = u32(t->batch_pkt_off[b + 1] - t->batch_pkt_off[b]);
+  return 0;
 }
 extern "C" int lkfs_batch_events(const lkfs_trace *t, uint32_t b, const lkfs_event **ev, uint32_t *n) {
   if (b + 1 >= t->batch_ev_off.size()) return LKF_EINVAL;

@@ -32,6 +32,8 @@ class Trace:
         self.max_batch_pkts = self.lib.lkfs_max_batch_pkts(self.h)
         self.max_batch_arena = self.lib.lkfs_max_batch_arena(self.h)
         self.max_batch_tuples = self.lib.lkfs_max_batch_tuples(self.h)
+        self.nstreams = self.lib.lkfs_num_streams(self.h)
+        self.streams = self.lib.lkfs_streams(self.h)
 
     def batch(self, b):
         pk = C.POINTER(abi.lkf_pkt)()
@@ -42,6 +44,15 @@ class Trace:
         if rc != 0:
             raise IndexError(b)
         return pk, n.value, ar, alen.value
+
+    def batch_raw(self, b):
+        """Batch b as raw datagrams (ingress input): (raw_pkts, n, arena, arena_len)."""
+        rp = C.POINTER(abi.lkf_raw_pkt)()
+        n = C.c_uint32()
+        if self.lib.lkfs_batch_raw(self.h, b, C.byref(rp), C.byref(n)) != 0:
+            raise IndexError(b)
+        _, _, ar, alen = self.batch(b)
+        return rp, n.value, ar, alen
 
     def events(self, b):
         ev = C.POINTER(abi.lkfs_event)()
@@ -72,6 +83,14 @@ def load_topology(api, eng, trace):
         h = api["add_downtrack"](eng, C.byref(trace.downtracks[d]))
         if h != d:
             raise RuntimeError("add_downtrack returned %d for dt %d" % (h, d))
+
+
+def load_streams(api, eng, trace):
+    """Adds the trace's ingress streams (one per received SSRC) in handle order."""
+    for i in range(trace.nstreams):
+        h = api["add_stream"](eng, C.byref(trace.streams[i]))
+        if h != i:
+            raise RuntimeError("add_stream returned %d for stream %d" % (h, i))
 
 
 def events_ptr(trace, b):

@@ -1666,7 +1666,7 @@ struct AudioLevel {
   u8 loudestObservedLevel = 127;
   u32 activeDuration = 0;
   u32 observedDuration = 0;
-  i64 lastObservedAtMs = 0;  // time.Time{} -> 0 is "zero" only for the stale test
+  i64 lastObservedAtNs = 0;  // virtual ns; 0 = time.Time{} (always stale)
 
   explicit AudioLevel(AudioLevelParams p) : params(p) {
     minActiveDuration = u32(p.MinPercentile) * p.ObserveDuration / 100;
@@ -1674,8 +1674,8 @@ struct AudioLevel {
     if (p.SmoothIntervals > 0) smoothFactor = double(2) / double(p.SmoothIntervals + 1);
   }
   // Observe audiolevel.go:70-102
-  void Observe(u8 level, u32 durationMs, i64 arrivalMs) {
-    lastObservedAtMs = arrivalMs;
+  void Observe(u8 level, u32 durationMs, i64 arrivalNs) {
+    lastObservedAtNs = arrivalNs;
     observedDuration += durationMs;
     if (level <= params.ActiveLevel) {
       activeDuration += durationMs;
@@ -1693,12 +1693,13 @@ struct AudioLevel {
     }
   }
   // GetLevel audiolevel.go:105-112
-  std::pair<double, bool> GetLevel(i64 nowMs) {
-    resetIfStaleLocked(nowMs);
+  std::pair<double, bool> GetLevel(i64 nowNs) {
+    resetIfStaleLocked(nowNs);
     return {smoothedLevel, smoothedLevel >= activeThreshold};
   }
-  void resetIfStaleLocked(i64 nowMs) {
-    if ((nowMs - lastObservedAtMs) < i64(2 * params.ObserveDuration)) return;
+  // arrivalTime.Sub(lastObservedAt).Milliseconds() truncates toward zero
+  void resetIfStaleLocked(i64 nowNs) {
+    if ((nowNs - lastObservedAtNs) / 1000000 < i64(2 * params.ObserveDuration)) return;
     resetLocked(0.0);
   }
   void resetLocked(double s) {
@@ -1770,13 +1771,18 @@ struct RTPStatsReceiver {
   WrapAround<u32, u64> timestamp{false};
   HistoryBitmap history;
   u64 packetsOutOfOrder = 0, packetsDuplicate = 0, packetsLost = 0, packetsPadding = 0, frames = 0;
+  u64 bytes = 0, headerBytes = 0, bytesDuplicate = 0, headerBytesDuplicate = 0, bytesPadding = 0,
+      headerBytesPadding = 0;
 
   bool isInRange(u64 esn, u64 ehsn) const {  // rtpstats_receiver.go:427-430
     i64 diff = i64(ehsn - esn);
     return diff >= 0 && diff < i64(cHistorySize);
   }
-  RTPFlowState Update(u16 sn, u32 ts, bool marker, int payloadSize) {
+  RTPFlowState Update(u16 sn, u32 ts, bool marker, int payloadSize) { return Update(sn, ts, marker, 12, payloadSize, 0); }
+  // Update rtpstats_receiver.go:76-241 (jitter / snapshots / report timing out of scope)
+  RTPFlowState Update(u16 sn, u32 ts, bool marker, int hdrSize, int payloadSize, int paddingSize) {
     RTPFlowState fs;
+    const u64 pktSize = u64(hdrSize + payloadSize + paddingSize);
     if (ended) {
       fs.IsNotHandled = true;
       return fs;
@@ -1804,6 +1810,8 @@ struct RTPStatsReceiver {
       if (gapSN != 0) packetsOutOfOrder++;
       if (isInRange(rsn.ExtendedVal, rsn.PreExtendedHighest)) {
         if (history.IsSet(rsn.ExtendedVal)) {
+          bytesDuplicate += pktSize;
+          headerBytesDuplicate += u64(hdrSize);
           packetsDuplicate++;
           fs.IsDuplicate = true;
         } else {
@@ -1827,13 +1835,121 @@ struct RTPStatsReceiver {
       fs.ExtTimestamp = rts.ExtendedVal;
     }
     if (!fs.IsDuplicate) {
-      if (payloadSize == 0)
+      if (payloadSize == 0) {
         packetsPadding++;
-      else if (marker)
-        frames++;
+        bytesPadding += pktSize;
+        headerBytesPadding += u64(hdrSize);
+      } else {
+        bytes += pktSize;
+        headerBytes += u64(hdrSize);
+        if (marker) frames++;
+      }
     }
     return fs;
   }
 };
+
+// -----------------------------------------------------------------------------
+// rtp.Packet.Unmarshal (pion/rtp v1.8.3 packet.go / header.go), restated:
+// fixed header, CSRCs, one-byte (0xBEDE) / two-byte (0x1000) / RFC 3550
+// extension blocks, padding.  PARITY UNPINNED (no reference test).
+// -----------------------------------------------------------------------------
+struct RtpParsed {
+  u8 b0 = 0, b1 = 0;
+  bool padding = false, extension = false, marker = false;
+  int cc = 0;
+  u8 pt = 0;
+  u16 sn = 0;
+  u32 ts = 0, ssrc = 0;
+  int hdrSize = 0;  // n: payload offset
+  int payloadLen = 0;
+  int paddingSize = 0;
+  u16 extProfile = 0;
+  int nExt = 0;
+  u8 extId[16];
+  int extOff[16], extLen[16];
+  // Header.GetExtension(id): first extension with that id (header.go)
+  bool GetExtension(u8 id, int &off, int &len) const {
+    if (!extension) return false;
+    for (int i = 0; i < nExt; i++)
+      if (extId[i] == id) {
+        off = extOff[i];
+        len = extLen[i];
+        return true;
+      }
+    return false;
+  }
+};
+inline bool rtp_unmarshal(const u8 *buf, int len, RtpParsed &h) {
+  h = RtpParsed{};
+  if (len < 12) return false;
+  h.b0 = buf[0];
+  h.b1 = buf[1];
+  h.padding = (buf[0] >> 5) & 1;
+  h.extension = (buf[0] >> 4) & 1;
+  h.cc = buf[0] & 0xf;
+  int n = 12 + 4 * h.cc;
+  if (len < n) return false;
+  h.marker = buf[1] >> 7;
+  h.pt = buf[1] & 0x7f;
+  h.sn = u16((buf[2] << 8) | buf[3]);
+  h.ts = (u32(buf[4]) << 24) | (u32(buf[5]) << 16) | (u32(buf[6]) << 8) | buf[7];
+  h.ssrc = (u32(buf[8]) << 24) | (u32(buf[9]) << 16) | (u32(buf[10]) << 8) | buf[11];
+  if (h.extension) {
+    if (len < n + 4) return false;
+    h.extProfile = u16((buf[n] << 8) | buf[n + 1]);
+    n += 2;
+    const int extLen = ((buf[n] << 8) | buf[n + 1]) * 4;
+    n += 2;
+    const int extEnd = n + extLen;
+    if (len < extEnd) return false;
+    if (h.extProfile == 0xBEDE || h.extProfile == 0x1000) {
+      while (n < extEnd) {
+        if (buf[n] == 0x00) {  // padding
+          n++;
+          continue;
+        }
+        u8 id;
+        int pl;
+        if (h.extProfile == 0xBEDE) {
+          id = buf[n] >> 4;
+          pl = (buf[n] & 0x0f) + 1;
+          n++;
+          if (id == 15) break;  // extensionIDReserved
+        } else {
+          id = buf[n];
+          n++;
+          if (len <= n) return false;
+          pl = buf[n];
+          n++;
+        }
+        if (len <= n + pl) return false;
+        if (h.nExt < 16) {
+          h.extId[h.nExt] = id;
+          h.extOff[h.nExt] = n;
+          h.extLen[h.nExt] = pl;
+          h.nExt++;
+        }
+        n += pl;
+      }
+    } else {  // RFC 3550 extension: one element, id 0
+      h.extId[0] = 0;
+      h.extOff[0] = n;
+      h.extLen[0] = extEnd - n;
+      h.nExt = 1;
+      n = extEnd;
+    }
+  }
+  int end = len;
+  if (h.padding) {
+    if (end <= n) return false;
+    h.paddingSize = buf[end - 1];
+    end -= h.paddingSize;
+  }
+  if (end < n) return false;
+  h.hdrSize = n;
+  h.payloadLen = end - n;
+  return true;
+}
 
 }  // namespace orc

@@ -55,6 +55,18 @@ struct OEv {
   uint32_t at;
 };
 
+// One received stream = one buffer.Buffer (buffer.go:66-130).
+struct OStream {
+  lkf_stream_params p;
+  u32 clockRate = 0;
+  u8 codec = 0;
+  RTPStatsReceiver stats;
+  RangeMap<u64, u64> snRangeMap{100};  // buffer.go:134
+  std::unique_ptr<AudioLevel> level;   // when the audio-level extension is negotiated (buffer.go:203-205)
+  bool latestTSForAudioLevelInitialized = false;
+  u32 latestTSForAudioLevel = 0;
+};
+
 }  // namespace
 
 struct orc_engine {
@@ -65,6 +77,10 @@ struct orc_engine {
   lkf_stats stats{};
   std::vector<lkf_out> outRecs;
   std::vector<u8> outArena;
+  // ingress
+  std::vector<std::unique_ptr<OStream>> streams;
+  std::vector<lkf_flow> flows;
+  std::vector<lkf_pkt> ingested;
 };
 
 static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
@@ -439,6 +455,261 @@ double orc_run_timed(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8
   }
   auto t1 = std::chrono::steady_clock::now();
   return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// ---- ingress ------------------------------------------------------------------
+
+// NewBuffer + Bind (buffer.go:124-215): audio-level params default to
+// config.go:380-385 (35 / 40 / 400 ms / 2).
+int32_t orc_add_stream(orc_engine *e, const lkf_stream_params *p) {
+  if (!p || p->track < 0 || p->track >= int32_t(e->tracks.size())) return LKF_EINVAL;
+  auto s = std::make_unique<OStream>();
+  s->p = *p;
+  s->clockRate = e->tracks[p->track].p.clock_rate;
+  s->codec = e->tracks[p->track].p.codec;
+  if (p->audio_level_ext) {
+    AudioLevelParams ap;
+    const bool dflt = !p->active_level && !p->min_percentile && !p->observe_duration_ms && !p->smooth_intervals;
+    if (!dflt) {
+      ap.ActiveLevel = p->active_level;
+      ap.MinPercentile = p->min_percentile;
+      ap.ObserveDuration = p->observe_duration_ms;
+      ap.SmoothIntervals = p->smooth_intervals;
+    }
+    s->level = std::make_unique<AudioLevel>(ap);
+  }
+  e->streams.push_back(std::move(s));
+  return int32_t(e->streams.size() - 1);
+}
+
+// Buffer.calc (buffer.go:417-491) + processHeaderExtensions (:573-596) +
+// updateStreamState (:545-567) + getExtPacket (:599-671) for one datagram.
+static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 *raw, lkf_pkt &ep, bool &fwd) {
+  lkf_flow f{};
+  f.pkt = 0xffffffffu;
+  fwd = false;
+  const u8 *buf = raw + rp.off;
+  RtpParsed h;
+  if (!rtp_unmarshal(buf, int(rp.len), h)) {  // "could not unmarshal RTP packet"
+    f.flags = LKF_FLOW_BAD;
+    return f;
+  }
+  // processHeaderExtensions: audio level (TWCC is out of scope)
+  bool hasLevel = false;
+  u8 level = 0;
+  if (b.p.audio_level_ext) {
+    if (!b.latestTSForAudioLevelInitialized) {
+      b.latestTSForAudioLevelInitialized = true;
+      b.latestTSForAudioLevel = h.ts;
+    }
+    int off = 0, len = 0;
+    if (h.GetExtension(b.p.audio_level_ext, off, len) && len >= 1) {  // AudioLevelExtension.Unmarshal
+      hasLevel = true;
+      level = buf[off] & 0x7f;
+      if (u32(h.ts - b.latestTSForAudioLevel) < (1u << 31)) {
+        const i64 duration = (i64(h.ts) - i64(b.latestTSForAudioLevel)) * 1000 / i64(b.clockRate);
+        if (duration > 0 && b.level) b.level->Observe(level, u32(duration), rp.arrival_ns);
+        b.latestTSForAudioLevel = h.ts;
+      }
+    }
+  }
+  RTPFlowState fs = b.stats.Update(h.sn, h.ts, h.marker, h.hdrSize, h.payloadLen, h.paddingSize);
+  f.ext_sn = fs.ExtSequenceNumber;
+  f.ext_ts = fs.ExtTimestamp;
+  if (fs.HasLoss) {  // nacker.Push(lost) for lost in [start, end) (buffer.go:557-562)
+    f.flags |= LKF_FLOW_HAS_LOSS;
+    f.loss_start = fs.LossStartInclusive;
+    f.loss_end = fs.LossEndExclusive;
+  }
+  if (fs.IsDuplicate) f.flags |= LKF_FLOW_DUPLICATE;
+  if (fs.IsOutOfOrder) f.flags |= LKF_FLOW_OUT_OF_ORDER;
+  if (fs.IsNotHandled) {
+    f.flags |= LKF_FLOW_NOT_HANDLED;
+    return f;
+  }
+  if (h.payloadLen == 0 && (!fs.IsOutOfOrder || fs.IsDuplicate)) {  // drop padding-only (:439-460)
+    if (!fs.IsOutOfOrder) (void)b.snRangeMap.ExcludeRange(fs.ExtSequenceNumber, fs.ExtSequenceNumber + 1);
+    f.flags |= LKF_FLOW_PADDING;
+    return f;
+  }
+  u64 adj = 0;
+  if (b.snRangeMap.GetValue(fs.ExtSequenceNumber, adj) != OK) {  // :464-468
+    f.flags |= LKF_FLOW_BAD;
+    return f;
+  }
+  f.ext_sn = fs.ExtSequenceNumber - adj;
+  // bucket.AddPacketWithSequenceNumber rejects a packet it already holds
+  // (ErrRTXPacket): a duplicate produces no ExtPacket.  Other bucket
+  // outcomes (size-dependent ErrPacketTooOld) are not modelled.
+  if (fs.IsDuplicate) return f;
+  // getExtPacket
+  std::memset(&ep, 0, sizeof(ep));
+  ep.ext_sn = f.ext_sn;
+  ep.ext_ts = f.ext_ts;
+  ep.arrival_ns = rp.arrival_ns;
+  ep.arena_off = rp.off;
+  ep.track = u32(b.p.track);
+  ep.ssrc = h.ssrc;
+  ep.payload_off = u16(h.hdrSize);
+  ep.payload_len = u16(h.payloadLen);
+  ep.hdr0 = h.b0;
+  ep.hdr1 = h.b1;
+  ep.spatial = -1;
+  ep.temporal = -1;
+  ep.layer = int8_t(b.p.layer);
+  if (hasLevel) {
+    ep.flags |= LKF_PKT_HAS_LEVEL;
+    ep.audio_level = level;
+  }
+  if (h.payloadLen > 0) {
+    ep.temporal = 0;
+    if (b.codec == LKF_CODEC_VP8) {
+      VP8 v;
+      if (v.Unmarshal(buf + h.hdrSize, h.payloadLen) != OK) {  // "could not unmarshal VP8 packet"
+        f.flags |= LKF_FLOW_BAD;
+        return f;
+      }
+      ep.flags |= LKF_PKT_VP8 | (v.IsKeyFrame ? LKF_PKT_KEYFRAME : 0);
+      ep.temporal = int8_t(v.TID);
+      ep.vp8_first = v.FirstByte;
+      ep.vp8_bits = u8((v.S ? LKF_VP8_S : 0) | (v.I ? LKF_VP8_I : 0) | (v.M ? LKF_VP8_M : 0) |
+                       (v.L ? LKF_VP8_L : 0) | (v.T ? LKF_VP8_T : 0) | (v.Y ? LKF_VP8_Y : 0) |
+                       (v.K ? LKF_VP8_K : 0));
+      ep.vp8_hdr_size = u8(v.HeaderSize);
+      ep.vp8_picture_id = v.PictureID;
+      ep.vp8_tl0picidx = v.TL0PICIDX;
+      ep.vp8_tid = v.TID;
+      ep.vp8_keyidx = v.KEYIDX;
+    }
+  }
+  fwd = true;
+  f.flags |= LKF_FLOW_FORWARD;
+  (void)e;
+  return f;
+}
+
+int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len) {
+  (void)raw_len;
+  e->flows.assign(n, lkf_flow{});
+  e->ingested.clear();
+  for (u32 i = 0; i < n; i++) {
+    if (pkts[i].stream >= e->streams.size()) return LKF_EINVAL;
+    lkf_pkt ep;
+    bool fwd = false;
+    e->flows[i] = calc(e, *e->streams[pkts[i].stream], pkts[i], raw, ep, fwd);
+    if (fwd) {
+      e->flows[i].pkt = u32(e->ingested.size());
+      e->ingested.push_back(ep);
+    }
+  }
+  return LKF_OK;
+}
+
+int orc_ingest_flows(orc_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out) {
+  *n_out = u32(e->flows.size());
+  if (cap < e->flows.size()) return LKF_ENOSPC;
+  if (!e->flows.empty()) std::memcpy(out, e->flows.data(), e->flows.size() * sizeof(lkf_flow));
+  return LKF_OK;
+}
+
+// The ExtPacket batch produced by the last orc_ingest (input of orc_run).
+int orc_ingested_ptr(orc_engine *e, const lkf_pkt **pkts, uint32_t *n) {
+  *pkts = e->ingested.data();
+  *n = u32(e->ingested.size());
+  return LKF_OK;
+}
+int orc_ingested(orc_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
+  *n_out = u32(e->ingested.size());
+  if (cap < e->ingested.size()) return LKF_ENOSPC;
+  if (!e->ingested.empty()) std::memcpy(out, e->ingested.data(), e->ingested.size() * sizeof(lkf_pkt));
+  return LKF_OK;
+}
+
+int orc_stream_stats_get(orc_engine *e, int32_t s, lkf_stream_stats *o) {
+  if (s < 0 || s >= int32_t(e->streams.size())) return LKF_EINVAL;
+  const RTPStatsReceiver &r = e->streams[s]->stats;
+  std::memset(o, 0, sizeof(*o));
+  o->initialized = r.initialized;
+  o->ext_start_sn = r.sequenceNumber.GetExtendedStart();
+  o->ext_highest_sn = r.sequenceNumber.GetExtendedHighest();
+  o->ext_start_ts = r.timestamp.GetExtendedStart();
+  o->ext_highest_ts = r.timestamp.GetExtendedHighest();
+  o->packets_lost = r.packetsLost;
+  o->packets_out_of_order = r.packetsOutOfOrder;
+  o->packets_duplicate = r.packetsDuplicate;
+  o->packets_padding = r.packetsPadding;
+  o->bytes = r.bytes;
+  o->header_bytes = r.headerBytes;
+  o->bytes_duplicate = r.bytesDuplicate;
+  o->bytes_padding = r.bytesPadding;
+  o->frames = r.frames;
+  return LKF_OK;
+}
+
+// Room.GetActiveSpeakers (room.go:254-279) for every room, ascending room id.
+// A microphone track's level is its primary receiver's (layer-0 stream's)
+// AudioLevel.GetLevel(now) (mediatrackreceiver.go:755-762, buffer.go:840-849);
+// a participant's level is the loudest active one (uptrackmanager.go:422-436).
+int orc_speakers(orc_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, uint32_t *n_out) {
+  std::vector<int> primary(e->tracks.size(), -1);
+  for (size_t s = 0; s < e->streams.size(); s++)
+    if (e->streams[s]->p.layer == 0 && primary[e->streams[s]->p.track] < 0) primary[e->streams[s]->p.track] = int(s);
+  // room -> participant -> (level, active)
+  std::vector<std::pair<u32, u32>> keys;  // (room, participant) in first-seen order
+  struct Acc {
+    double level = 0;
+    bool active = false;
+  };
+  std::vector<Acc> acc;
+  auto find = [&](u32 room, u32 part) -> size_t {
+    for (size_t i = 0; i < keys.size(); i++)
+      if (keys[i].first == room && keys[i].second == part) return i;
+    keys.emplace_back(room, part);
+    acc.emplace_back();
+    return keys.size() - 1;
+  };
+  for (size_t t = 0; t < e->tracks.size(); t++) {
+    const lkf_track_params &tp = e->tracks[t].p;
+    size_t k = find(tp.room, tp.publisher);
+    if (!tp.is_mic || primary[t] < 0) continue;
+    OStream &s = *e->streams[primary[t]];
+    if (!s.level) continue;
+    auto lv = s.level->GetLevel(now_ns);
+    if (lv.second) {
+      acc[k].active = true;
+      if (lv.first > acc[k].level) acc[k].level = lv.first;
+    }
+  }
+  std::vector<u32> rooms;
+  for (auto &k : keys)
+    if (std::find(rooms.begin(), rooms.end(), k.first) == rooms.end()) rooms.push_back(k.first);
+  std::sort(rooms.begin(), rooms.end());
+  std::vector<lkf_speaker> res;
+  for (u32 room : rooms) {
+    // participants of the room by ascending index (the tie order)
+    std::vector<std::pair<u32, size_t>> ps;
+    for (size_t i = 0; i < keys.size(); i++)
+      if (keys[i].first == room) ps.emplace_back(keys[i].second, i);
+    std::sort(ps.begin(), ps.end());
+    std::vector<std::pair<double, bool>> levels;
+    std::vector<u32> pidx;
+    for (auto &p : ps) {
+      levels.emplace_back(acc[p.second].level, acc[p.second].active);
+      pidx.push_back(p.first);
+    }
+    for (auto &sp : RankSpeakers(levels)) {
+      lkf_speaker o{};
+      o.room = room;
+      o.participant = pidx[sp.participant];
+      o.level = sp.level;
+      o.active = 1;
+      res.push_back(o);
+    }
+  }
+  *n_out = u32(res.size());
+  if (cap < res.size()) return LKF_ENOSPC;
+  if (!res.empty()) std::memcpy(out, res.data(), res.size() * sizeof(lkf_speaker));
+  return LKF_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,108 @@
+"""Ingress (Buffer.calc) and active-speaker ranking on the CPU oracle.
+
+The synthetic generator knows the ExtPacket each datagram should become; with
+no loss or reordering the oracle's Buffer.calc restatement must reproduce the
+generator's ExtPacket batch byte for byte (wrap-around unwrap, padding-free SN
+adjustment, header/extension/VP8 parsing).  With loss and reordering, the flow
+records must account for every datagram.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests.oracle_lib import load as load_oracle
+
+
+def _ingested(o, abi, h):
+    lib = o.lib
+    lib.orc_ingested_ptr.argtypes = [C.c_void_p, C.POINTER(C.POINTER(abi.lkf_pkt)), C.POINTER(C.c_uint32)]
+    lib.orc_ingested_ptr.restype = C.c_int
+    pk = C.POINTER(abi.lkf_pkt)()
+    n = C.c_uint32()
+    lib.orc_ingested_ptr(h, C.byref(pk), C.byref(n))
+    return pk, n.value
+
+
+@pytest.mark.parametrize("kw", [
+    dict(config=1, duration_s=2.0),
+    dict(config=2, duration_s=2.0, rooms=2, loss=0.0, reorder=0.0),
+    dict(config=3, duration_s=2.0, rooms=1),
+])
+def test_oracle_ingest_reproduces_extpackets(kw, pkg, workload, abi):
+    o = load_oracle()
+    tr = workload.Trace(**kw)
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        workload.load_streams(o.api, h, tr)
+        for b in range(tr.nbatches):
+            rp, n, ar, alen = tr.batch_raw(b)
+            assert o.api["ingest"](h, rp, n, ar, alen) == 0
+            pk, m = _ingested(o, abi, h)
+            spk, sn, _, _ = tr.batch(b)
+            assert m == sn == n
+            got = C.string_at(pk, 64 * m) if m else b""
+            want = C.string_at(spk, 64 * sn) if sn else b""
+            assert got == want, "batch %d ExtPackets differ" % b
+            fl = pkg.flows_array(o.api, h)
+            assert len(fl) == n
+            assert np.all(fl["flags"] & 0x20)  # every datagram forwarded
+            assert np.array_equal(fl["pkt"], np.arange(n, dtype=np.uint32))
+    finally:
+        o.destroy(h)
+        tr.close()
+
+
+def test_oracle_ingest_loss_and_reorder_accounting(pkg, workload, abi):
+    o = load_oracle()
+    tr = workload.Trace(2, duration_s=3.0, rooms=2, loss=0.1, reorder=0.05, seed=5)
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        workload.load_streams(o.api, h, tr)
+        nloss = nooo = nfwd = 0
+        for b in range(tr.nbatches):
+            rp, n, ar, alen = tr.batch_raw(b)
+            assert o.api["ingest"](h, rp, n, ar, alen) == 0
+            fl = pkg.flows_array(o.api, h)
+            fwd = (fl["flags"] & 0x20) != 0
+            _, m = _ingested(o, abi, h)
+            assert fwd.sum() == m
+            assert np.array_equal(fl["pkt"][fwd], np.arange(m, dtype=np.uint32))
+            assert np.all(fl["pkt"][~fwd] == 0xFFFFFFFF)
+            loss = (fl["flags"] & 0x08) != 0
+            assert np.all(fl["loss_end"][loss] > fl["loss_start"][loss])
+            nloss += int((fl["loss_end"][loss] - fl["loss_start"][loss]).sum())
+            nooo += int(((fl["flags"] & 0x04) != 0).sum())
+            nfwd += m
+        lost = sum(pkg.stream_stats(o.api, h, s)[4] for s in range(tr.nstreams))
+        assert nloss > 0 and nooo > 0 and nfwd > 0
+        assert lost <= nloss  # OOO arrivals refill reported holes
+    finally:
+        o.destroy(h)
+        tr.close()
+
+
+def test_oracle_speakers_ranked_and_quantised(pkg, workload, abi):
+    o = load_oracle()
+    tr = workload.Trace(3, duration_s=3.0, rooms=2)
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        workload.load_streams(o.api, h, tr)
+        seen = 0
+        for b in range(tr.nbatches):
+            rp, n, ar, alen = tr.batch_raw(b)
+            assert o.api["ingest"](h, rp, n, ar, alen) == 0
+            now = 1700000000 * 10**9 + (b + 1) * 10**9
+            sp = pkg.speakers_array(o.api, h, now)
+            for room in np.unique(sp["room"]):
+                lv = sp["level"][sp["room"] == room]
+                assert np.all(np.diff(lv) <= 0)  # descending
+                assert np.all(np.abs(lv * 8 - np.round(lv * 8)) < 1e-6)  # multiples of 1/8
+            seen += len(sp)
+        assert seen > 0
+    finally:
+        o.destroy(h)
+        tr.close()

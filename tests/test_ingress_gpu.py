@@ -1,0 +1,103 @@
+"""Bit-exact parity of the GPU ingress path and speaker ranking vs the CPU oracle.
+
+Raw datagrams (with loss, reordering, audio-level extensions, VP8 payloads)
+go through lkf_ingest (Buffer.calc on the GPU) and orc_ingest (the oracle's
+restatement); the per-datagram flow records, the ExtPacket batches produced,
+the forwarded output of that batch, every stream's RTPStatsReceiver counters
+and the per-room active-speaker lists must be identical.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests.oracle_lib import load as load_oracle
+
+pytestmark = pytest.mark.gpu
+
+EPOCH = 1700000000 * 10**9
+
+
+def _ingested(api, h, abi):
+    n = C.c_uint32()
+    rc = api["ingested"](h, None, 0, C.byref(n))
+    assert rc in (0, -28)
+    arr = (abi.lkf_pkt * max(1, n.value))()
+    assert api["ingested"](h, arr, n.value, C.byref(n)) == 0
+    return C.string_at(arr, 64 * n.value) if n.value else b""
+
+
+def run_ingress_parity(pkg, workload, abi, trace, speakers=True):
+    o = load_oracle()
+    eng = pkg.Engine.for_trace(trace)
+    oh = o.create(500)
+    try:
+        for api, h in ((eng.api, eng.h), (o.api, oh)):
+            workload.load_topology(api, h, trace)
+            workload.load_streams(api, h, trace)
+        total_fwd = 0
+        for b in range(trace.nbatches):
+            workload.queue_events(eng.api, eng.h, trace, b)
+            workload.queue_events(o.api, oh, trace, b)
+            rp, n, ar, alen = trace.batch_raw(b)
+            eng.ingest(rp, n, ar, alen)
+            assert o.api["ingest"](oh, rp, n, ar, alen) == 0
+            gf = eng.flows()
+            of = pkg.flows_array(o.api, oh)
+            assert len(gf) == len(of) == n
+            for f in ("ext_sn", "ext_ts", "loss_start", "loss_end", "pkt", "flags"):
+                if not np.array_equal(gf[f], of[f]):
+                    bad = np.nonzero(gf[f] != of[f])[0][:5]
+                    raise AssertionError("batch %d flow field %s differs at %s: gpu %s orc %s" % (
+                        b, f, bad, gf[bad], of[bad]))
+            gp = _ingested(eng.api, eng.h, abi)
+            op = _ingested(o.api, oh, abi)
+            assert gp == op, "batch %d ExtPacket batches differ" % b
+            # forward the ingested batch on both sides
+            eng.run()
+            eng.sync()
+            m = len(op) // 64
+            if m:
+                o.run(oh, C.cast(C.c_char_p(op), C.POINTER(abi.lkf_pkt)), m, ar, alen)
+            else:
+                o.run(oh, None, 0, ar, alen)
+            gs = eng.stats()
+            ost = abi.lkf_stats()
+            o.api["get_stats"](oh, C.byref(ost))
+            assert gs == ost.as_dict(), (b, gs, ost.as_dict())
+            grec, gar = eng.drain()
+            orec, oar = pkg.drain_arrays(o.api, oh)
+            assert len(grec) == len(orec)
+            for f in abi.OUT_DTYPE.names:
+                assert np.array_equal(grec[f], orec[f]), (b, f)
+            assert np.array_equal(gar, oar), b
+            total_fwd += gs["forwarded"]
+            if speakers:
+                now = EPOCH + (b + 1) * 10**9
+                gsp = eng.speakers(now)
+                osp = pkg.speakers_array(o.api, oh, now)
+                assert len(gsp) == len(osp), (b, len(gsp), len(osp))
+                for f in ("room", "participant", "level", "active"):
+                    assert np.array_equal(gsp[f], osp[f]), (b, f, gsp, osp)
+        for s in range(trace.nstreams):
+            assert eng.stream_stats(s) == pkg.stream_stats(o.api, oh, s), s
+        return total_fwd
+    finally:
+        eng.close()
+        o.destroy(oh)
+
+
+def test_ingress_config2_loss_reorder(pkg, workload, abi):
+    tr = workload.Trace(2, duration_s=3.0, batch_s=0.5, rooms=3, loss=0.05, reorder=0.03, seed=21)
+    assert run_ingress_parity(pkg, workload, abi, tr) > 0
+
+
+def test_ingress_config1(pkg, workload, abi):
+    tr = workload.Trace(1, duration_s=3.0, batch_s=1.0)
+    assert run_ingress_parity(pkg, workload, abi, tr) > 0
+
+
+def test_ingress_config3_speakers(pkg, workload, abi):
+    """configs[2] shape: 50-participant audio-heavy rooms, speaker ranking every batch (400 ms)."""
+    tr = workload.Trace(3, duration_s=4.0, batch_s=0.4, rooms=2)
+    assert run_ingress_parity(pkg, workload, abi, tr) > 0
