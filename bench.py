@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", ""))
+    ap.add_argument("--ingress", action="store_true",
+                    help="step = Buffer.calc over raw datagrams (lkf_ingest_device) + forwarding")
     args = ap.parse_args()
 
     import torch
@@ -113,11 +115,19 @@ def main():
     eng = pkg.Engine.for_trace(trace, device=local, lib_path=os.environ.get("LKF_LIB") or None)
     wl.load_topology(eng.api, eng.h, trace)
 
+    if args.ingress:
+        wl.load_streams(eng.api, eng.h, trace)
+
     # inputs resident in HBM before the timed region
     dpk, dar, meta = [], [], []
     for b in range(nb):
-        pk, n, ar, alen = trace.batch(b)
-        tp = torch.frombuffer(bytearray(C.string_at(pk, n * 64)), dtype=torch.uint8).to(dev)
+        if args.ingress:
+            pk, n, ar, alen = trace.batch_raw(b)  # raw datagrams: Buffer.calc runs inside the step
+            rsz = C.sizeof(pkg.abi.lkf_raw_pkt)
+        else:
+            pk, n, ar, alen = trace.batch(b)
+            rsz = 64
+        tp = torch.frombuffer(bytearray(C.string_at(pk, max(1, n) * rsz)), dtype=torch.uint8).to(dev)
         ta = torch.zeros(alen + 64, dtype=torch.uint8, device=dev)
         if alen:
             ta[:alen].copy_(torch.frombuffer(bytearray(C.string_at(ar, alen)), dtype=torch.uint8))
@@ -130,7 +140,10 @@ def main():
     def step(b):
         wl.queue_events(eng.api, eng.h, trace, b)
         n, alen = meta[b]
-        eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
+        if args.ingress:
+            eng.ingest_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
+        else:
+            eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
         eng.run(sp)
 
     for b in range(args.warmup):
@@ -213,6 +226,8 @@ def main():
             "config": {"workload": "configs[1]: %d rooms x 10 participants per GPU, VP8 3-layer simulcast + Opus, "
                                    "18,000 DownTracks, 2%% loss, 1%% reorder, layer switching" % args.rooms,
                        "batch": "%.3g s of media per step" % args.batch_s,
+                       "step": ("raw datagrams -> Buffer.calc -> forward (lkf_ingest_device + lkf_run)"
+                                if args.ingress else "ExtPacket batch -> forward (lkf_submit_device + lkf_run)"),
                        "parallelism": "room-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": dom["achieved"], "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": dom["frac"], "traffic": traffic, "kernel": dom["kernel"],

@@ -343,7 +343,11 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p);
  * of the next lkf_run (the raw arena is the forwarding arena; it must stay
  * valid until that batch's outputs are drained).  Host buffers are copied. */
 int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len);
-/* Same with device-resident inputs (valid until the forwarded batch is synced). */
+/* Same with device-resident inputs (valid until the forwarded batch is synced).
+ * Ingest is enqueued on the engine's decide stream without a host sync: the
+ * inputs must be complete when it is called (produced on a synchronized
+ * stream). The ExtPacket count stays on the device and feeds the next
+ * lkf_run directly; lkf_ingest_flows / lkf_ingested synchronize. */
 int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, const uint8_t *d_raw,
                       uint64_t raw_len);
 /* Per-datagram outcomes of the last ingest (input order). */

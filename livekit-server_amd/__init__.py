@@ -159,6 +159,12 @@ class Engine:
         if rc != 0:
             raise EngineError("lkf_ingest rc=%d: %s" % (rc, self.lib.lkf_last_error(self.h).decode()))
 
+    def ingest_device(self, d_raws, n, d_raw, raw_len):
+        """lkf_ingest with HBM-resident raw datagrams (no host sync)."""
+        rc = self.api["ingest_device"](self.h, d_raws, n, d_raw, raw_len)
+        if rc != 0:
+            raise EngineError("lkf_ingest_device rc=%d: %s" % (rc, self.lib.lkf_last_error(self.h).decode()))
+
     def flows(self):
         return flows_array(self.api, self.h)
 

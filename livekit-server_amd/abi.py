@@ -293,6 +293,9 @@ def bind_engine_api(lib, prefix):
                               [e, C.c_int32, P(C.c_uint16), C.c_uint32, C.c_int64, P(lkf_seq_meta), P(C.c_uint32)])
     api["add_stream"] = _bind(lib, prefix + "add_stream", C.c_int32, [e, P(lkf_stream_params)])
     api["ingest"] = _bind(lib, prefix + "ingest", C.c_int, [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64])
+    if hasattr(lib, prefix + "ingest_device"):  # engine only (the oracle is host-side)
+        api["ingest_device"] = _bind(lib, prefix + "ingest_device", C.c_int,
+                                     [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64])
     api["ingest_flows"] = _bind(lib, prefix + "ingest_flows", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["ingested"] = _bind(lib, prefix + "ingested", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["stream_stats_get"] = _bind(lib, prefix + "stream_stats_get", C.c_int, [e, C.c_int32, P(lkf_stream_stats)])

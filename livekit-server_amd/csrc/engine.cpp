@@ -127,6 +127,9 @@ struct lkf_engine {
   uint32_t curN = 0;
   uint64_t curArenaLen = 0;
   bool haveBatch = false;
+  const uint64_t *curNDev = nullptr;  // device-side batch length (ingest-produced batch)
+  bool ingestUnchecked = false;       // ingest error word not yet reported
+  bool ingestStarted = false;         // this run's start event precedes its ingest
 
   BatchCtx ctx[2];
   uint64_t nRuns = 0;
@@ -519,6 +522,8 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
   e->curPkts = x.dPktsOwn;
   e->curArena = x.dArenaOwn;
   e->curN = n;
+  e->curNDev = nullptr;
+  e->ingestStarted = false;
   e->curArenaLen = arena_len;
   e->haveBatch = true;
   return LKF_OK;
@@ -530,6 +535,8 @@ int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const ui
   e->curPkts = d_pkts;
   e->curArena = d_arena;
   e->curN = n;
+  e->curNDev = nullptr;
+  e->ingestStarted = false;
   e->curArenaLen = arena_len;
   e->haveBatch = true;
   return LKF_OK;
@@ -648,6 +655,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     e->curPkts = x.dPktsOwn;
     e->curArena = x.dArenaOwn;
     e->curN = 0;
+    e->curNDev = nullptr;
     e->curArenaLen = 0;
   }
   // The caller's stream orders the batch's inputs; the stages themselves run
@@ -712,11 +720,13 @@ int lkf_run(lkf_engine *e, void *stream) {
 
   // ---- decide stage (decide stream)
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
-  HIPCHK(hipEventRecord(rg[0], s), "event");
+  if (!e->ingestStarted) HIPCHK(hipEventRecord(rg[0], s), "event");  // else: recorded ahead of the ingest
+  e->ingestStarted = false;
   HIPCHK(launch_batch_init(s, nt, nd, kStatsWords, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dStats, x.dFwdCnt,
                            x.dFwdBytes),
          "batch init");
-  HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr), "track_ranges");
+  HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, e->curNDev, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
+         "track_ranges");
   HIPCHK(launch_scan(s, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
                      x.dTot + 0, nullptr, nullptr),
          "slot scan");
@@ -781,6 +791,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   e->lastCtx = ci;
   e->nRuns++;
   e->haveBatch = false;
+  e->curNDev = nullptr;
   return LKF_OK;
 }
 
@@ -790,6 +801,15 @@ int lkf_sync(lkf_engine *e) {
   if (!e) return LKF_EINVAL;
   int rc = drain_streams(e);
   if (rc) return rc;
+  if (e->ingestUnchecked) {
+    uint32_t ierr = 0;
+    HIPCHK(hipMemcpy(&ierr, e->dIErr, sizeof(ierr), hipMemcpyDeviceToHost), "ingest err copy");
+    e->ingestUnchecked = false;
+    if (ierr & 3u) {
+      e->err = "raw batch not grouped by track / bad stream handle";
+      return LKF_EORDER;
+    }
+  }
   if (e->lastCtx < 0) return LKF_OK;
   uint32_t acc = 0;
   for (int i = 0; i < 2; i++) {
@@ -1020,10 +1040,15 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p) {
   return int32_t(e->streams.size() - 1);
 }
 
+// Enqueued on the decide stream ahead of the batch's decide stage (no host
+// sync): the ExtPacket count stays on the device (k_track_ranges reads it).
 static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, uint32_t n, const uint8_t *dRaw,
                          uint64_t rawLen) {
   const uint32_t nt = uint32_t(e->tracks.size());
-  hipStream_t s = e->own;
+  hipStream_t s = e->decS;
+  // the batch's GPU span (lkf_timing_window total) starts before its ingest
+  HIPCHK(hipEventRecord(e->ring[e->nRuns % lkf_engine::kRing][0], s), "event");
+  e->ingestStarted = true;
   HIPCHK(hipMemsetAsync(e->dITBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
   HIPCHK(hipMemsetAsync(e->dITEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
   HIPCHK(hipMemsetAsync(e->dITRuns, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
@@ -1052,18 +1077,11 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.total = e->dITotal;
   a.out = x.dPktsOwn;
   HIPCHK(launch_ingest(s, a), "ingest");
-  uint64_t total = 0;
-  uint32_t err = 0;
-  HIPCHK(hipMemcpyAsync(&total, e->dITotal, sizeof(total), hipMemcpyDeviceToHost, s), "total copy");
-  HIPCHK(hipMemcpyAsync(&err, e->dIErr, sizeof(err), hipMemcpyDeviceToHost, s), "err copy");
-  HIPCHK(hipStreamSynchronize(s), "ingest sync");
   e->lastIngestN = n;
-  if (err & 3u) {
-    e->err = "raw batch not grouped by track / bad stream handle";
-    return LKF_EORDER;
-  }
+  e->ingestUnchecked = true;
   e->curPkts = x.dPktsOwn;
-  e->curN = uint32_t(total);
+  e->curN = n;  // launch bound; the count is e->dITotal
+  e->curNDev = e->dITotal;
   e->curArena = dRaw;
   e->curArenaLen = rawLen;
   e->haveBatch = true;
@@ -1077,10 +1095,10 @@ int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
   if (rc) return rc;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   BatchCtx &x = e->ctx[e->nRuns & 1];
-  if (x.used) HIPCHK(hipEventSynchronize(x.emitted), "wait emit");  // batch n-2 still reads these buffers
-  if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->own),
+  if (x.used) HIPCHK(hipStreamWaitEvent(e->decS, x.emitted, 0), "wait emit");  // batch n-2 reads these buffers
+  if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->decS),
                 "raw pkts");
-  if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->own), "raw arena");
+  if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->decS), "raw arena");
   return ingest_common(e, x, x.dRawPkts, n, x.dArenaOwn, raw_len);
 }
 
@@ -1091,7 +1109,7 @@ int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, cons
   if (rc) return rc;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   BatchCtx &x = e->ctx[e->nRuns & 1];
-  if (x.used) HIPCHK(hipEventSynchronize(x.emitted), "wait emit");
+  if (x.used) HIPCHK(hipStreamWaitEvent(e->decS, x.emitted, 0), "wait emit");
   return ingest_common(e, x, d_pkts, n, d_raw, raw_len);
 }
 
@@ -1100,7 +1118,7 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
   *n_out = e->lastIngestN;
   if (cap < e->lastIngestN) return LKF_ENOSPC;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  HIPCHK(hipStreamSynchronize(e->decS), "sync");
   if (e->lastIngestN)
     HIPCHK(hipMemcpy(out, e->dFlows, size_t(e->lastIngestN) * sizeof(lkf_flow), hipMemcpyDeviceToHost), "flows");
   return LKF_OK;
@@ -1109,8 +1127,16 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
 int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
   if (!e || !n_out) return LKF_EINVAL;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
-  const uint32_t n = e->haveBatch ? e->curN : 0;
+  HIPCHK(hipStreamSynchronize(e->decS), "sync");
+  uint32_t n = 0;
+  if (e->haveBatch) {
+    n = e->curN;
+    if (e->curNDev) {
+      uint64_t t = 0;
+      HIPCHK(hipMemcpy(&t, e->curNDev, sizeof(t), hipMemcpyDeviceToHost), "count copy");
+      n = uint32_t(t);
+    }
+  }
   *n_out = n;
   if (cap < n) return LKF_ENOSPC;
   if (n) HIPCHK(hipMemcpy(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyDeviceToHost), "ingested copy");
@@ -1223,16 +1249,17 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
   a.nowNs = now_ns;
   a.slots = e->dSpkSlots;
   a.counts = e->dSpkCounts;
-  HIPCHK(launch_speakers(e->own, a), "speakers");
+  // decide stream: ordered after the ingest that updated the levels
+  HIPCHK(launch_speakers(e->decS, a), "speakers");
   std::vector<uint32_t> counts(e->nRooms);
   std::vector<lkf_speaker> slots(size_t(e->nRooms) * 64);
   HIPCHK(hipMemcpyAsync(counts.data(), e->dSpkCounts, counts.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        e->own),
+                        e->decS),
          "counts copy");
   HIPCHK(hipMemcpyAsync(slots.data(), e->dSpkSlots, slots.size() * sizeof(lkf_speaker), hipMemcpyDeviceToHost,
-                        e->own),
+                        e->decS),
          "slots copy");
-  HIPCHK(hipStreamSynchronize(e->own), "speakers sync");
+  HIPCHK(hipStreamSynchronize(e->decS), "speakers sync");
   uint32_t k = 0;
   for (uint32_t r = 0; r < e->nRooms; r++) k += counts[r];
   *n_out = k;

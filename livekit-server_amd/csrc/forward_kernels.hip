@@ -910,9 +910,13 @@ __global__ void k_batch_init(u32 ntracks, u32 ndts, u32 nstats, u32 *__restrict_
 // ---------------------------------------------------------------------------
 // k_track_ranges: packets grouped by track -> [begin, end) (+ grouping check)
 // ---------------------------------------------------------------------------
-__global__ void k_track_ranges(const lkf_pkt *__restrict__ pkts, u32 n, u32 ntracks, u32 *__restrict__ tBegin,
-                               u32 *__restrict__ tEnd, u32 *__restrict__ tRuns, u32 *__restrict__ err) {
+// nDev (optional): the batch length lives on the device (an ingest-produced
+// batch); n is then only the launch bound.
+__global__ void k_track_ranges(const lkf_pkt *__restrict__ pkts, u32 n, const u64 *__restrict__ nDev, u32 ntracks,
+                               u32 *__restrict__ tBegin, u32 *__restrict__ tEnd, u32 *__restrict__ tRuns,
+                               u32 *__restrict__ err) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nDev && *nDev < n) n = u32(*nDev);
   if (i >= n) return;
   u32 t = pkts[i].track;
   if (t >= ntracks) {
@@ -2126,10 +2130,11 @@ hipError_t launch_batch_init(hipStream_t s, u32 ntracks, u32 ndts, u32 nstats, u
   return hipGetLastError();
 }
 
-hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, u32 n, u32 ntracks, u32 *tBegin, u32 *tEnd,
-                               u32 *tRuns, u32 *err) {
+hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, u32 n, const u64 *nDev, u32 ntracks, u32 *tBegin,
+                               u32 *tEnd, u32 *tRuns, u32 *err) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_track_ranges, dim3(nblk(n, 256)), dim3(256), 0, s, pkts, n, ntracks, tBegin, tEnd, tRuns, err);
+  hipLaunchKernelGGL(k_track_ranges, dim3(nblk(n, 256)), dim3(256), 0, s, pkts, n, nDev, ntracks, tBegin, tEnd, tRuns,
+                     err);
   return hipGetLastError();
 }
 

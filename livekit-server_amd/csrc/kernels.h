@@ -53,8 +53,8 @@ hipError_t read_diag(unsigned long long out[16], int reset);
 hipError_t launch_batch_init(hipStream_t s, uint32_t ntracks, uint32_t ndts, uint32_t nstats, uint32_t *tBegin,
                              uint32_t *tEnd, uint32_t *tRuns, uint32_t *err, uint64_t *stats, uint32_t *fwdCnt,
                              uint64_t *fwdBytes);
-hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, uint32_t n, uint32_t ntracks, uint32_t *tBegin,
-                               uint32_t *tEnd, uint32_t *tRuns, uint32_t *err);
+hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, uint32_t n, const uint64_t *nDev, uint32_t ntracks,
+                               uint32_t *tBegin, uint32_t *tEnd, uint32_t *tRuns, uint32_t *err);
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t *tBegin, const uint32_t *tEnd,
                        const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
                        uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB,
