@@ -193,7 +193,7 @@ def main():
                     "algorithmic_bytes_per_launch": int(nbytes // args.steps),
                     "achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBPS, 4)}
 
-        kd = kern("k_decide" if os.environ.get("LKF_DECIDE") == "track" else "k_decide_dt", decide_bytes, dec_ms)
+        kd = kern("k_decide_dt", decide_bytes, dec_ms)
         ke = kern("k_emit", emit_bytes, emit_ms)
         dom = kd if kd["avg_ms"] >= ke["avg_ms"] else ke
         traffic = None

@@ -167,7 +167,6 @@ struct lkf_engine {
   size_t spkCap = 0;
   // 1: k_decide_dt (one wave per DownTrack, lanes = packets; default)
   // 0: k_decide (one lane per DownTrack, one wave per track)
-  int decideMode = 1;
 };
 
 static int fail(lkf_engine *e, const char *what, hipError_t r) {
@@ -367,7 +366,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device);
   // emit is grid-stride: 4 workgroups (16 waves) per CU saturate HBM and
   // leave wave slots for the next batch's decide stage.
-  if (const char *v = getenv("LKF_DECIDE")) e->decideMode = strcmp(v, "track") == 0 ? 0 : 1;
   int perCU = 4;
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
@@ -558,19 +556,12 @@ static int rebuild_sched(lkf_engine *e) {
   e->waveTrack.clear();
   for (uint32_t t : order) {
     const auto &v = byTrack[t];
-    if (e->decideMode == 1) {  // one wave per DownTrack (interleaved per XCD below)
-      for (uint32_t d : v) {
-        e->sched.push_back(d);
-        e->waveTrack.push_back(t);
-      }
-      continue;
-    }
-    for (size_t i = 0; i < v.size(); i += 64) {
+    for (uint32_t d : v) {  // one wave per DownTrack (interleaved per XCD below)
+      e->sched.push_back(d);
       e->waveTrack.push_back(t);
-      for (size_t j = 0; j < 64; j++) e->sched.push_back(i + j < v.size() ? v[i + j] : kIdle);
     }
   }
-  if (e->decideMode == 1 && !e->sched.empty()) {
+  if (!e->sched.empty()) {
     // Waves are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8).
     // Give all DownTracks of a track the same XCD, consecutive in its order,
     // so the 8-9 waves reading one track's packet descriptors share an L2.
@@ -731,7 +722,6 @@ int lkf_run(lkf_engine *e, void *stream) {
                      x.dTot + 0, nullptr, nullptr),
          "slot scan");
   DecideLaunch d;
-  d.mode = e->decideMode;
   d.sched = e->dSched;
   d.waveTrack = e->dWaveTrack;
   d.nlanes = nl;

@@ -3,7 +3,7 @@
 // Per batch (lkf_run):
 //   k_track_ranges  packets grouped by track -> [begin,end) per track
 //   scan (slots)    per DownTrack tuple-slot base = sum of its track's packets
-//   k_decide        one lane per DownTrack, serial over its track's packets:
+//   k_decide_dt     one wave per DownTrack, lanes = its track's packets:
 //                   the per-packet recurrence of DownTrack.WriteRTP
 //                   (downtrack.go:680-760) = Forwarder.GetTranslationParams
 //                   (forwarder.go:1436-1765) + RTPMunger (rtpmunger.go) +
@@ -112,15 +112,65 @@ __device__ __forceinline__ uint4 rfl(uint4 v) {  // wave-uniform copy (SGPRs)
 }
 
 // ---------------------------------------------------------------------------
+// Wave primitives.  k_decide_dt runs one wave per DownTrack: the DownTrack
+// state is wave-uniform, so the rare-path helpers below spread their loops
+// over the 64 lanes (every lane calls them with the same arguments).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u32 lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ u32 rl32(u32 v, u32 l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ u64 rl64(u64 v, u32 l) {
+  return (u64(rl32(u32(v >> 32), l)) << 32) | u64(rl32(u32(v), l));
+}
+__device__ __forceinline__ u32 sh32(u32 v, int src) { return u32(__shfl(int(v), src, 64)); }
+__device__ __forceinline__ u64 sh64(u64 v, int src) {
+  return (u64(sh32(u32(v >> 32), src)) << 32) | u64(sh32(u32(v), src));
+}
+__device__ __forceinline__ int prev_in(u64 m, u64 lt) {  // highest set lane below this one, or -1
+  const u64 pm = m & lt;
+  return pm ? 63 - __clzll(pm) : -1;
+}
+__device__ __forceinline__ u32 excl_scan_u32(u32 v, u32 lane) {
+  u32 x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    u32 y = u32(__shfl_up(int(x), o, 64));
+    if (lane >= u32(o)) x += y;
+  }
+  return x - v;
+}
+__device__ __forceinline__ u32 wave_sum_u32(u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += u32(__shfl_xor(int(v), o, 64));
+  return v;
+}
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    u64 y = sh64(v, int(threadIdx.x) ^ o);
+    v = y > v ? y : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ u64 wave_or_u64(u64 v) {  // -> wave-uniform (SGPR) result
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= sh64(v, int(threadIdx.x) ^ o);
+  return rl64(v, 0);
+}
+// LDS written by some lanes is read by others below: order the accesses
+// (the workgroup is one wave, so the barrier costs no waiting).
+__device__ __forceinline__ void wave_lds_sync() { __syncthreads(); }
+
+// ---------------------------------------------------------------------------
 // Lane context: hot state in registers + cold-state pointers.
 // ---------------------------------------------------------------------------
 struct Lane {
   DTHot h;
   RangeEntry *rm;
   VP8Cold *vc;
-  i32 *dropKey;  // LDS copy of vc->dropKey (this lane's row)
+  i32 *dropKey;  // LDS copy of vc->dropKey
   i32 *exKey;    // LDS copy of vc->exKey
-  i32 *missKey;  // vc->missKey (k_decide) or its LDS copy (k_decide_dt)
+  i32 *missKey;  // LDS copy of vc->missKey
   i32 *missVal;
   SeqMeta *seq;
   u32 seqSize;
@@ -177,7 +227,11 @@ __device__ bool rm_exclude(Lane &L, u64 s, u64 e) {
   L.h.rmOpenValue = nv;
   return true;
 }
-// GetValue rangemap.go:134-169 -> true on success
+// GetValue rangemap.go:134-169 -> true on success.  The reference walks the
+// closed ranges from the newest down; at index i it first tests "key inside
+// range i", then "key strictly between range i-1 and range i" (-> miss).  The
+// first hit of that walk is the hit with the largest index (inside before
+// between at equal index), so each lane tests one index and a ballot picks it.
 __device__ bool rm_get(const Lane &L, u64 key, u64 &out) {
   out = 0;
   if (key >= L.h.rmOpenStart) {
@@ -185,28 +239,41 @@ __device__ bool rm_get(const Lane &L, u64 key, u64 &out) {
     return true;
   }
   const int nc = L.h.rmCount;
-  u64 firstStart = nc > 0 ? rm_at(L, 0).start : L.h.rmOpenStart;
-  if (key < firstStart) return false;
-  // idx = n-1 (open): only the exclusion test against the newest closed range
-  RangeEntry next;  // rv for the exclusion test
-  next.start = L.h.rmOpenStart;
-  for (int idx = nc; idx >= 0; idx--) {
-    if (idx != nc) {
-      RangeEntry rv = next;
-      if ((key - rv.start) < HALF64 && (rv.end - key) < HALF64) {
-        out = rv.value;
-        return true;
+  if (nc == 0) return false;  // key < open start = first start
+  if (key < rm_at(L, 0).start) return false;
+  const u32 l = lane_id();
+  int best = -1;
+  bool bestIn = false;
+  u64 bestVal = 0;
+  for (int base = 0; base <= nc; base += 64) {
+    const int i = base + int(l);
+    bool in = false, between = false;
+    u64 val = 0;
+    if (i <= nc) {
+      u64 nextStart = L.h.rmOpenStart;
+      if (i < nc) {
+        const RangeEntry rv = rm_at(L, i);
+        in = (key - rv.start) < HALF64 && (rv.end - key) < HALF64;
+        val = rv.value;
+        nextStart = rv.start;
+      }
+      if (i > 0) {
+        const u64 before = key - rm_at(L, i - 1).end;
+        const u64 after = nextStart - key;
+        between = before > 0 && before < HALF64 && after > 0 && after < HALF64;
       }
     }
-    if (idx > 0) {
-      RangeEntry prev = rm_at(L, idx - 1);
-      u64 before = key - prev.end;
-      u64 after = next.start - key;
-      if (before > 0 && before < HALF64 && after > 0 && after < HALF64) return false;
-      next = prev;
+    const u64 m = __ballot(in || between);
+    if (m) {
+      const u32 j = 63 - __clzll(m);
+      best = base + int(j);
+      bestIn = rl32(u32(in), j) != 0;
+      bestVal = rl64(val, j);
     }
   }
-  return false;
+  if (best < 0 || !bestIn) return false;
+  out = bestVal;
+  return true;
 }
 
 // ---- RTPMunger (rtpmunger.go) ---------------------------------------------
@@ -305,30 +372,38 @@ __device__ int mg_update(Lane &L, const PktV &p, bool marker, int &ord, u64 &osn
 }
 
 // ---- VP8 munger rings (elliotchance/orderedmap semantics) ------------------
+// All keys of a ring are distinct (map semantics), so a membership test is one
+// ballot over the ring positions (wave-uniform key).
 __device__ __forceinline__ int miss_find(const Lane &L, i32 key) {
-  for (int i = 0; i < L.h.missCount; i++) {
-    int idx = (L.h.missHead + i) % kMissCap;
-    if (L.missKey[idx] == key) return idx;
+  const u32 l = lane_id();
+  for (int base = 0; base < int(L.h.missCount); base += 64) {
+    const int i = base + int(l);
+    const int idx = (L.h.missHead + i) % kMissCap;
+    const u64 m = __ballot(i < int(L.h.missCount) && L.missKey[idx] == key);
+    if (m) return (L.h.missHead + base + __ffsll((long long)m) - 1) % kMissCap;
   }
   return -1;
 }
-__device__ __forceinline__ bool set_has(const i32 *keys, u8 head, u8 count, i32 key) {
+__device__ __forceinline__ bool set_has(const i32 *keys, u8 head, u8 count, i32 key) {  // per-lane key
   for (int i = 0; i < count; i++)
     if (keys[(head + i) % kSetCap] == key) return true;
   return false;
 }
-// Set(key,true) then trim to `keep` (vp8.go:242-247, :257-262)
+__device__ __forceinline__ bool set_has_u(const i32 *keys, u8 head, u8 count, i32 key) {  // wave-uniform key
+  const u32 l = lane_id();
+  return __ballot(l < count && keys[(head + l) % kSetCap] == key) != 0;
+}
+// Set(key,true) then trim to `keep` (vp8.go:242-247, :257-262); wave-uniform
 __device__ __forceinline__ void set_add(i32 *keys, u8 &head, u8 &count, i32 key, int keep) {
-  if (set_has(keys, head, count, key)) return;
+  if (set_has_u(keys, head, count, key)) return;
+  wave_lds_sync();
   keys[(head + count) % kSetCap] = key;
   count++;
-  while (count > keep) {
-    head = u8((head + 1) % kSetCap);
-    count--;
+  if (count > keep) {
+    head = u8((head + count - keep) % kSetCap);
+    count = u8(keep);
   }
-}
-__device__ __forceinline__ bool dropped_has(const Lane &L, i32 key) {
-  return set_has(L.dropKey, L.h.dropHead, L.h.dropCount, key);
+  wave_lds_sync();
 }
 
 // The missing-picture loop of vp8.go:218-235, exact:
@@ -336,15 +411,15 @@ __device__ __forceinline__ bool dropped_has(const Lane &L, i32 key) {
 //   trim missing to the newest 50.
 // Equivalent bounded form: existing entries in range are updated in place;
 // of the new keys only the newest 50 can survive the trim, appended in order.
-__device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
-  DIAG_SCOPE(8);
-  if (ext < prevMax) return;
+// Wave form: the range [prevMax, prevMax+63] is a 64-bit mask; dropped and
+// existing keys are OR-reduced into it, the new keys are its remaining bits.
+__device__ void vp8_record_missing_wide(Lane &L, i32 prevMax, i32 ext, i32 off) {  // range > 64 pictures
   const int e0 = L.h.missCount;
   int inE = 0;  // existing (not dropped) keys inside the range
   for (int i = 0; i < e0; i++) {
     int idx = (L.h.missHead + i) % kMissCap;
     i32 k = L.missKey[idx];
-    if (k >= prevMax && k <= ext && !dropped_has(L, k)) {
+    if (k >= prevMax && k <= ext && !set_has_u(L.dropKey, L.h.dropHead, L.h.dropCount, k)) {
       L.missVal[idx] = off;
       inE++;
     }
@@ -357,11 +432,10 @@ __device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
   i64 nNew = i64(ext) - i64(prevMax) + 1 - nDrop - inE;
   if (nNew <= 0) return;
   int want = nNew > kMissKeep ? kMissKeep : int(nNew);
-  // find the start key s: walking down from ext, the want-th new key
   i32 s = ext;
   int got = 0;
-  for (i32 k = ext;; k--) {
-    if (!dropped_has(L, k) && miss_find(L, k) < 0) {
+  for (i32 k = ext;; k--) {  // walking down from ext, the want-th new key
+    if (!set_has_u(L.dropKey, L.h.dropHead, L.h.dropCount, k) && miss_find(L, k) < 0) {
       got++;
       if (got == want) {
         s = k;
@@ -370,19 +444,73 @@ __device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
     }
     if (k == prevMax) break;
   }
-  // append new keys in [s, ext] in order (before trimming, E intact)
-  for (i32 k = s;; k++) {
-    if (!dropped_has(L, k) && miss_find(L, k) < 0) {
+  for (i32 k = s;; k++) {  // append new keys in [s, ext] in order
+    if (!set_has_u(L.dropKey, L.h.dropHead, L.h.dropCount, k) && miss_find(L, k) < 0) {
+      wave_lds_sync();
       int idx = (L.h.missHead + L.h.missCount) % kMissCap;
       L.missKey[idx] = k;
       L.missVal[idx] = off;
       L.h.missCount++;
+      wave_lds_sync();
     }
     if (k == ext) break;
   }
-  while (L.h.missCount > kMissKeep) {
-    L.h.missHead = u8((L.h.missHead + 1) % kMissCap);
-    L.h.missCount--;
+  if (L.h.missCount > kMissKeep) {
+    L.h.missHead = u8((L.h.missHead + L.h.missCount - kMissKeep) % kMissCap);
+    L.h.missCount = u8(kMissKeep);
+  }
+}
+__device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
+
+  if (ext < prevMax) return;
+  const i64 span = i64(ext) - i64(prevMax) + 1;
+  if (span > 64) {
+    vp8_record_missing_wide(L, prevMax, ext, off);
+    return;
+  }
+  const u32 l = lane_id();
+  const u64 rangeM = span == 64 ? ~0ull : ((1ull << span) - 1);
+  u64 dropBits = 0;
+  if (l < L.h.dropCount) {
+    const i32 k = L.dropKey[(L.h.dropHead + l) % kSetCap];
+    if (k >= prevMax && k <= ext) dropBits = 1ull << (k - prevMax);
+  }
+  const u64 dropM = wave_or_u64(dropBits);
+  const int cnt = L.h.missCount;
+  u64 exBits = 0;
+  for (int base = 0; base < cnt; base += 64) {
+    const int i = base + int(l);
+    if (i < cnt) {
+      const int idx = (L.h.missHead + i) % kMissCap;
+      const i32 k = L.missKey[idx];
+      if (k >= prevMax && k <= ext) {
+        const u64 bit = 1ull << (k - prevMax);
+        exBits |= bit;
+        if (!(dropM & bit)) L.missVal[idx] = off;  // Set on an existing key: in place
+      }
+    }
+  }
+  u64 newM = rangeM & ~dropM & ~wave_or_u64(exBits);
+  int nNew = __popcll(newM);
+  if (nNew == 0) return;
+  while (nNew > kMissKeep) {  // older new keys would be trimmed right away
+    newM &= newM - 1;
+    nNew--;
+  }
+  wave_lds_sync();
+  if ((newM >> l) & 1) {
+    const int r = __popcll(newM & ((1ull << l) - 1));
+    const int idx = (L.h.missHead + cnt + r) % kMissCap;
+    L.missKey[idx] = prevMax + i32(l);
+    L.missVal[idx] = off;
+  }
+  wave_lds_sync();
+  const int total = cnt + nNew;
+  if (total > kMissKeep) {
+    L.h.missHead = u8((L.h.missHead + total - kMissKeep) % kMissCap);
+    L.h.missCount = u8(kMissKeep);
+  } else {
+    L.h.missCount = u8(total);
   }
 }
 
@@ -492,7 +620,7 @@ __device__ __forceinline__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool
     if (T && p.tid > u8(maxTL)) set_add(L.exKey, L.h.exHead, L.h.exCount, ext, kExemptKeep);
   } else {
     if (T && p.tid > u8(maxTL)) {
-      if (!set_has(L.exKey, L.h.exHead, L.h.exCount, ext)) {
+      if (!set_has_u(L.exKey, L.h.exHead, L.h.exCount, ext)) {
         if (I && prevMax != ext) {
           set_add(L.dropKey, L.h.dropHead, L.h.dropCount, ext, kDropKeep);
           L.h.pictureIdOffset += 1;
@@ -802,6 +930,15 @@ __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
   return -1;
 }
 
+// invalidateSlot (sequencer.go:351-366) of the n slots after the highest slot
+__device__ __forceinline__ void seq_invalidate(Lane &L, u32 n) {
+  const SeqMeta z = {};
+  for (u32 i = lane_id(); i < n; i += 64) {
+    u32 x = u32(L.h.seqHighSlot) + 1 + i;
+    while (x >= L.seqSize) x -= L.seqSize;
+    L.seq[x] = z;
+  }
+}
 // sequencer.push sequencer.go:123-209 (no padding exclusions on this path: the
 // sequencer's RangeMap stays at value 0, so slot = extModifiedSN % size)
 __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, u64 cb,
@@ -826,7 +963,7 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     if (ets > L.h.seqExtHighestTS) L.h.seqExtHighestTS = ets;
     return;
   }
-  DIAG_SCOPE(9);
+
   if (!hasf(L, F_SEQ_INIT)) {
     setf(L, F_SEQ_INIT, true);
     L.h.seqExtStartSN = esn;
@@ -849,15 +986,9 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     i32 sl = i32(L.h.seqHighSlot) + i32(delta);
     slot = u32(sl < 0 ? sl + i32(size) : sl);
   }
-  if (adjM > adjH) {  // invalidate the skipped slots (sequencer.go:179-189)
-    u32 x = L.h.seqHighSlot;
-    u64 n = 0;
-    for (u64 e = adjH + 1; e != adjM; e++) {
-      if (++x == size) x = 0;
-      SeqMeta z = {};
-      L.seq[x] = z;
-      if (++n >= size) break;
-    }
+  if (adjM > adjH + 1) {  // invalidate the skipped slots (sequencer.go:179-189), one per lane
+    const u64 nInv = (adjM - adjH - 1) < u64(size) ? (adjM - adjH - 1) : u64(size);
+    seq_invalidate(L, u32(nInv));
   }
   SeqMeta m = {};
   m.sourceSeqNo = u16(inSN);
@@ -1073,8 +1204,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_down(ScanIn in, u32 n, const u6
 }
 
 // ---------------------------------------------------------------------------
-// k_decide: one lane per DownTrack (lanes ordered by track: the lanes of a
-// wave read the same packet descriptors, broadcast from L1/L2).
+// k_decide_dt arguments.
 // ---------------------------------------------------------------------------
 struct DecideArgs {
   const u32 *sched;      // lane -> DownTrack (0xffffffff = idle lane)
@@ -1260,130 +1390,6 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   o.relOff += u32((hdrLen + payLen + 15) & ~15);
 }
 
-// One wave per (track, <=64 DownTracks).  The packet loop is wave-uniform:
-// descriptors are staged 16 at a time into LDS by one cooperative 1-KiB load
-// (double-buffered: the next chunk is in flight while this one is decided)
-// and broadcast to SGPRs (readfirstlane), so every branch on packet fields is
-// a scalar branch; lanes diverge only on per-DownTrack state.  The VP8
-// dropped/exempted picture-id sets live in LDS for the whole batch.
-constexpr int CHUNK = 16;  // packets per staged chunk (64 x 16 B)
-
-__global__ void __launch_bounds__(64) k_decide(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
-  __shared__ uint4 sPkt[2][CHUNK * 4];
-  __shared__ i32 sDrop[64][kSetCap];
-  __shared__ i32 sEx[64][kSetCap];
-  const u32 l = blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 d = l < A.nlanes ? A.sched[l] : 0xffffffffu;
-  const bool live = d != 0xffffffffu;
-  const u32 track = A.waveTrack[blockIdx.x];
-  const u32 pb = A.tBegin[track];
-  u32 pe = A.tEnd[track];
-  const bool over = live && (A.slotBase[d] + (pe - pb) > A.tupleCap);
-  if (__any(over)) {  // tuple slots exhausted: skip this wave, flag
-    if (threadIdx.x == 0) atomicOr(A.err, 8u);
-    pe = pb;
-  }
-  LaneOut o;
-  o.nFwd = o.nBytes = o.nTuples = 0;
-  o.relOff = 0;
-  for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
-  Lane L;
-  u32 ev = 0, evEnd = 0, nextAt = 0xffffffffu;
-  if (live) {
-    L.h = A.hot[d];
-    L.rm = A.rm + size_t(d) * kRangeCap;
-    L.vc = A.vc + d;
-    L.dropKey = sDrop[threadIdx.x];
-    L.exKey = sEx[threadIdx.x];
-    L.missKey = L.vc->missKey;
-    L.missVal = L.vc->missVal;
-    if (L.h.flags & F_VP8) {
-      const uint4 *gd = reinterpret_cast<const uint4 *>(L.vc->dropKey);
-      const uint4 *ge = reinterpret_cast<const uint4 *>(L.vc->exKey);
-      uint4 *sd = reinterpret_cast<uint4 *>(L.dropKey);
-      uint4 *se = reinterpret_cast<uint4 *>(L.exKey);
-#pragma unroll
-      for (int i = 0; i < kSetCap / 4; i++) {
-        sd[i] = gd[i];
-        se[i] = ge[i];
-      }
-    }
-    L.seq = A.seq + size_t(d) * A.seqSize;
-    L.seqSize = A.seqSize;
-    const DevDT dt = A.dts[d];
-    const DevTrack &tk = A.tracks[dt.track];
-    L.kind = tk.kind;
-    L.codec = tk.codec;
-    L.hasRefTS = tk.hasRefTS;
-    L.clockRate = tk.clockRate;
-    L.offs = tk.layerOffsets;
-    L.extPlayout = dt.extPlayout;
-    L.extAbs = dt.extAbs;
-    ev = A.evOff[l];
-    evEnd = A.evOff[l + 1];
-    o.outT = A.tuples + A.slotBase[d];
-    nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
-  }
-  const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
-  // stage chunk 0
-  if (pb < pe && threadIdx.x < min(u32(CHUNK), pe - pb) * 4) sPkt[0][threadIdx.x] = src[u64(pb) * 4 + threadIdx.x];
-  __syncthreads();
-  int cur = 0;
-  for (u32 base = pb; base < pe; base += CHUNK) {
-    const u32 np = min(u32(CHUNK), pe - base);
-    // prefetch the next chunk into registers (lands while this chunk is decided)
-    const u32 nb = base + CHUNK;
-    uint4 nx = make_uint4(0, 0, 0, 0);
-    const bool hasNext = nb < pe && threadIdx.x < min(u32(CHUNK), pe - nb) * 4;
-    if (hasNext) nx = src[u64(nb) * 4 + threadIdx.x];
-    for (u32 j = 0; j < np; j++) {
-      const PktV p = decode_pkt(rfl(sPkt[cur][j * 4 + 0]), rfl(sPkt[cur][j * 4 + 1]), rfl(sPkt[cur][j * 4 + 2]),
-                                rfl(sPkt[cur][j * 4 + 3]));
-      const u32 k = base + j;
-      if (live) {
-        while (nextAt <= k) {
-          apply_ctl(L, A.events[ev++]);
-          nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
-        }
-        decide_step(L, p, k, o);
-      }
-    }
-    if (hasNext) sPkt[cur ^ 1][threadIdx.x] = nx;
-    cur ^= 1;
-    __syncthreads();
-  }
-  if (live) {
-    while (ev < evEnd) apply_ctl(L, A.events[ev++]);
-    A.hot[d] = L.h;
-    if (L.h.flags & F_VP8) {
-      uint4 *gd = reinterpret_cast<uint4 *>(L.vc->dropKey);
-      uint4 *ge = reinterpret_cast<uint4 *>(L.vc->exKey);
-      const uint4 *sd = reinterpret_cast<const uint4 *>(L.dropKey);
-      const uint4 *se = reinterpret_cast<const uint4 *>(L.exKey);
-#pragma unroll
-      for (int i = 0; i < kSetCap / 4; i++) {
-        gd[i] = sd[i];
-        ge[i] = se[i];
-      }
-    }
-    A.fwdCnt[d] = u32(o.nFwd);
-    A.fwdBytes[d] = o.relOff;
-  }
-  const u64 nTuples = o.nTuples, nFwd = o.nFwd, nBytes = o.nBytes;
-  // per-wave reduction of counters -> one atomic each
-  u64 v = wave_sum(nTuples);
-  if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)v);
-  v = wave_sum(nFwd);
-  if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)v);
-  v = wave_sum(nBytes);
-  if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[2], (unsigned long long)v);
-#pragma unroll
-  for (int i = 0; i < LKF_DROP_NREASONS; i++) {
-    v = wave_sum(u64(o.drops[i]));
-    if (threadIdx.x == 0 && v) atomicAdd((unsigned long long *)&A.stats[4 + i], (unsigned long long)v);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // k_decide_dt: one wave per DownTrack, lanes = packets of its track.
 //
@@ -1404,55 +1410,50 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs A, const lkf_pkt *__re
 // control op) goes through decide_step — the full restatement — executed by
 // the whole wave on the broadcast packet, and the run restarts after it.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ u32 rl32(u32 v, u32 l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ u64 rl64(u64 v, u32 l) {
-  return (u64(rl32(u32(v >> 32), l)) << 32) | u64(rl32(u32(v), l));
-}
-__device__ __forceinline__ u32 sh32(u32 v, int src) { return u32(__shfl(int(v), src, 64)); }
-__device__ __forceinline__ u64 sh64(u64 v, int src) {
-  return (u64(sh32(u32(v >> 32), src)) << 32) | u64(sh32(u32(v), src));
-}
-__device__ __forceinline__ int prev_in(u64 m, u64 lt) {  // highest set lane below this one, or -1
-  const u64 pm = m & lt;
-  return pm ? 63 - __clzll(pm) : -1;
-}
-__device__ __forceinline__ u32 excl_scan_u32(u32 v, u32 lane) {
-  u32 x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    u32 y = u32(__shfl_up(int(x), o, 64));
-    if (lane >= u32(o)) x += y;
-  }
-  return x - v;
-}
-__device__ __forceinline__ u32 wave_sum_u32(u32 v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += u32(__shfl_xor(int(v), o, 64));
-  return v;
-}
-__device__ __forceinline__ u64 wave_max_u64(u64 v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    u64 y = sh64(v, int(threadIdx.x) ^ o);
-    v = y > v ? y : v;
-  }
-  return v;
-}
-
 #ifndef LKF_FORCE_SERIAL
 #define LKF_FORCE_SERIAL 0  // diagnostic: every packet through decide_step
 #endif
 #if LKF_DIAG
 #define DIAG(i, v) dg[i] += (v)
+#define DIAG_MARK(i)            \
+  do {                          \
+    const u64 tm_ = clock64();  \
+    dg[i] += tm_ - tmark;       \
+    tmark = tm_;                \
+  } while (0)
 #else
 #define DIAG(i, v)
+#define DIAG_MARK(i)
 #endif
 
-__global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
+#ifndef LKF_DECIDE_WAVES
+#define LKF_DECIDE_WAVES 0  // >0: amdgpu_waves_per_eu floor for k_decide_dt (occupancy experiments)
+#endif
+#ifndef LKF_PREFETCH
+#define LKF_PREFETCH 1  // load the next 64 packet descriptors while deciding the current ones
+#endif
+#if LKF_DECIDE_WAVES
+#define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(LKF_DECIDE_WAVES, 8)))
+#else
+#define DECIDE_ATTR
+#endif
+
+// Consume the chunk's descriptor registers here, once.  gfx9 counts stores in
+// vmcnt too: a first use sunk into the run loop would wait there for every
+// tuple/sequencer store issued so far (one HBM write round trip per run).
+__device__ __forceinline__ void pin_loaded(const uint4 &a, const uint4 &b, const uint4 &c, const uint4 &d) {
+  asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
+               "v"(c.y), "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
+}
+
+__global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
   __shared__ i32 sDrop[kSetCap];
   __shared__ i32 sEx[kSetCap];
   __shared__ i32 sMissKey[kMissCap];
   __shared__ i32 sMissVal[kMissCap];
+#if LKF_DIAG
+  const u64 tEntry = clock64();
+#endif
   const u32 lane = threadIdx.x;
   const u64 lt = (1ull << lane) - 1;
   const u32 w = blockIdx.x;
@@ -1508,10 +1509,21 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
 #if LKF_DIAG
   u64 dg[16] = {};
   u64 tk0 = clock64();
+  dg[7] = tk0 - tEntry;
   dg[0] = 1;
   dg[15] = pe - pb;
 #endif
 
+#if LKF_PREFETCH
+  uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0, f2 = f0, f3 = f0;
+  if (pb + lane < pe) {
+    const u64 q = u64(pb + lane) * 4;
+    f0 = src[q];
+    f1 = src[q + 1];
+    f2 = src[q + 2];
+    f3 = src[q + 3];
+  }
+#endif
   for (u32 k = pb; k < pe; k += 64) {
     const u32 n = min(64u, pe - k);
     const bool valid = lane < n;
@@ -1519,6 +1531,17 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
 #if LKF_DIAG
     u64 tc0 = clock64();
 #endif
+#if LKF_PREFETCH
+    const uint4 r0 = f0, r1 = f1, r2 = f2, r3 = f3;
+    pin_loaded(r0, r1, r2, r3);
+    if (k + 64 + lane < pe) {  // next chunk in flight while this one is decided
+      const u64 q = u64(k + 64 + lane) * 4;
+      f0 = src[q];
+      f1 = src[q + 1];
+      f2 = src[q + 2];
+      f3 = src[q + 3];
+    }
+#else
     uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
     if (valid) {
       const u64 q = u64(k + lane) * 4;
@@ -1527,6 +1550,8 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
       r2 = src[q + 2];
       r3 = src[q + 3];
     }
+    pin_loaded(r0, r1, r2, r3);
+#endif
     const PktV p = decode_pkt(r0, r1, r2, r3);
 #if LKF_DIAG
     dg[11] += u64(__builtin_amdgcn_readfirstlane(u32(r0.x)) + 1u > 0u) * (clock64() - tc0);
@@ -1535,6 +1560,7 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
     while (pos < n) {
 #if LKF_DIAG
       u64 tr0 = clock64();
+      u64 tmark = tr0;
 #endif
       while (nextAt <= k + pos) {
         apply_ctl(L, A.events[ev++]);
@@ -1577,11 +1603,23 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
 #endif
       const bool cand = inWin && cls == -1;
       const u64 candM = __ballot(cand);
+      DIAG_MARK(4);
       const int pc = prev_in(candM, lt);
       const int pcs = pc >= 0 ? pc : int(lane);  // cross-lane reads run on every lane
       const u64 pcEsn = sh64(p.esn, pcs);
       const u64 prevEsn = pc >= 0 ? pcEsn : L.h.extHighestIncomingSN;
-      bool ok = cand && p.esn == prevEsn + 1 && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+      // A loss gap (diff > 1, rtpmunger.go:186-190) is taken in the run when it
+      // is the run's first candidate: its side effects (missing/exempted
+      // pictures vp8.go:218-255, skipped sequencer slots sequencer.go:179-189)
+      // are applied before the run, from the state at the run start.
+      const u64 dEsn = p.esn - prevEsn;
+      const bool gapLane = cand && pc < 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
+                           p.ssrc == L.h.lastSSRC;
+      bool ok = cand && (dEsn == 1 || gapLane) && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+      // a gap behind other candidates ends this run and starts the next one
+      const bool gapLater = cand && pc >= 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
+                            p.ssrc == L.h.lastSSRC;
+      DIAG_MARK(8);
       // VP8 picture id (VP8PictureIdWrapHandler.Unwrap vp8.go:400-483 without a wrap)
       const bool M = p.vbits & LKF_VP8_M, I = p.vbits & LKF_VP8_I, T = p.vbits & LKF_VP8_T;
       const i32 np = M ? i32(p.pid & 0x7fff) : i32(p.pid & 0x7f);
@@ -1591,6 +1629,8 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
       const i32 prevExt = pc >= 0 ? pcExt : L.h.wrMaxPictureId;
       const bool prevM = pc >= 0 ? pcM : ((fl & F_WR_MAX_MBIT) != 0);
       bool dropT = false;
+      bool gapExempt = false;
+      i32 gapExt = 0;
       if (video) {
         i32 mp = prevExt;
         if (mp > 0) mp = prevM ? (prevExt & 0x7fff) : (prevExt & 0x7f);
@@ -1603,11 +1643,17 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
                                      (p.vbits & LKF_VP8_Y))
                                   : pktMarker);
         const bool overT = cand && T && p.tid > u8(cT);
-        dropT = overT;
-        if (__ballot(overT) && L.h.exCount)  // exempted pictures forward (vp8.go:270)
-          dropT = overT && !set_has(L.exKey, L.h.exHead, L.h.exCount, ext);
+        // a gap lane forwards whatever its layer and exempts its picture (vp8.go:249-255)
+        const u64 gapM = __ballot(gapLane);
+        const u32 gl = gapM ? u32(__ffsll((long long)gapM) - 1) : 0u;
+        gapExempt = gapM && rl32(u32(overT), gl) != 0;
+        gapExt = i32(rl32(u32(ext), gl));
+        dropT = overT && !gapLane && !(gapExempt && ext == gapExt);
+        if (__ballot(dropT) && L.h.exCount)  // exempted pictures forward (vp8.go:270)
+          dropT = dropT && !set_has(L.exKey, L.h.exHead, L.h.exCount, ext);
         ok = ok && !wrapBack && !wraps && !tsw && (!dropT || L.h.snOffset == L.h.rmOpenValue);
       }
+      DIAG_MARK(9);
       const u64 tdM = __ballot(ok && dropT);
       const u64 snOff = L.h.snOffset + u64(__popcll(tdM & lt));
       const u64 osn = p.esn - snOff;
@@ -1628,6 +1674,7 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
         cbLen = vp8_marshal(p.vfirst, I, mM, mpid, p.vbits & LKF_VP8_L, mtl0, T, p.tid, p.vbits & LKF_VP8_Y,
                             p.vbits & LKF_VP8_K, mkey, hs, cb);
       }
+      DIAG_MARK(10);
       const u64 fwC = __ballot(fwd);
       const int pf = prev_in(fwC, lt);
       const u64 pfOsn = sh64(osn, pf >= 0 ? pf : int(lane));
@@ -1635,35 +1682,19 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
       const u64 pfOts = sh64(ots, pf >= 0 ? pf : int(lane));
       // sequencer highest TS = max over pushes; runs keep TS non-decreasing so it is the last one
       const bool tsMono = ots >= (pf >= 0 ? pfOts : L.h.seqExtHighestTS);
-      const bool seqOk = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && osn == prevOsn + 1 && cbLen >= 0 && tsMono;
+      // the first push of a run may skip slots (a gap lane: osn - highest < size - 64)
+      const bool seqOk = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && cbLen >= 0 && tsMono &&
+                         (osn == prevOsn + 1 || (gapLane && pf < 0 && osn - prevOsn > 1 &&
+                                                 osn - prevOsn < u64(L.seqSize) - 64));
       const bool bad = inWin && ((cls == -2) || (cls == -1 && !ok) || (fwd && !seqOk));
-#if LKF_DIAG
-      {
-        const bool okb = cand && p.esn == prevEsn + 1 && p.plen != 0 && p.ssrc == L.h.lastSSRC;
-        u32 cause = 0;
-        if (!bad)
-          cause = 0;
-        else if (cls == -2)
-          cause = 5;
-        else if (cls == -1 && !okb)
-          cause = 6;
-        else if (cls == -1 && !ok)
-          cause = 7;  // wrap / temporal switch / snOffset mismatch
-        else
-          cause = 10;
-        const u64 sm = __ballot(bad || (valid && lane >= pos && !inWin));
-        if (sm) {
-          const u32 xx = u32(__ffsll((long long)sm) - 1);
-          const u32 c = rl32(cause, xx);
-          if (c) dg[c] += 1;
-          else dg[4] += 1;
-        }
-      }
-#endif
       const u64 stopM = __ballot(bad || (valid && lane >= pos && !inWin));
       const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
       // ---- decide lanes [pos, x) together
       DIAG(2, x > pos ? 1 : 0);
+#if LKF_DIAG
+      const u64 tb0 = clock64();
+      dg[5] += tb0 - tr0;
+#endif
       if (x > pos) {
         const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
         const bool inRun = (runM >> lane) & 1;
@@ -1675,6 +1706,20 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
 #pragma unroll
         for (int r = 0; r < LKF_DROP_NREASONS; r++) o.drops[r] += u32(__popcll(__ballot(inRun && cls == r)));
         o.drops[LKF_DROP_TEMPORAL] += u32(__popcll(tdR));
+        // first push of the run: slot distance from the sequencer's highest
+        u32 gOff = 1;
+        if (fwR) {
+          const u32 firstF = u32(__ffsll((long long)fwR) - 1);
+          gOff = u32(rl64(osn, firstF) - L.h.seqExtHighestSN);
+          const u64 gR = __ballot(gapLane && inRun);
+          if (gR) {  // the run starts after a loss gap (the gap lane is forwarded)
+            if (video) {
+              vp8_record_missing(L, L.h.wrMaxPictureId, gapExt, L.h.pictureIdOffset);
+              if (gapExempt) set_add(L.exKey, L.h.exHead, L.h.exCount, gapExt, kExemptKeep);
+            }
+            if (gOff > 1) seq_invalidate(L, gOff - 1);
+          }
+        }
         // output records + sequencer slots of the forwarded lanes
         const int cc = p.hdr0 & 0xf;
         const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
@@ -1704,9 +1749,11 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
           t.hdrLen = u8(hdrLen);
 #pragma unroll
           for (int i = 0; i < 12; i++) t.pad[i] = 0;
+#if LKF_ABLATE != 1
           o.outT[o.nFwd + j] = t;
+#endif
           // sequencer.push in-order branch (sequencer.go:123-209): next slot
-          u32 slot = u32(L.h.seqHighSlot) + 1 + j;
+          u32 slot = u32(L.h.seqHighSlot) + gOff + j;
           while (slot >= L.seqSize) slot -= L.seqSize;
           SeqMeta m = {};
           m.sourceSeqNo = u16(p.esn);
@@ -1718,7 +1765,9 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
           m.codecLen = u8(video ? cbLen : 0);
 #pragma unroll
           for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+#if LKF_ABLATE != 1
           L.seq[slot] = m;
+#endif
         }
         const u32 sumLen = wave_sum_u32(outLen);
         // ---- advance the DownTrack state past the run (uniform)
@@ -1727,7 +1776,7 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
           const u32 nF = u32(__popcll(fwR));
           o.nBytes += sumLen;
           o.nFwd += nF;
-          u32 slot = u32(L.h.seqHighSlot) + nF;
+          u32 slot = u32(L.h.seqHighSlot) + gOff - 1 + nF;
           while (slot >= L.seqSize) slot -= L.seqSize;
           L.h.seqHighSlot = u16(slot);
           L.h.seqExtHighestSN = rl64(osn, lastF);
@@ -1796,8 +1845,9 @@ __global__ void __launch_bounds__(64) k_decide_dt(DecideArgs A, const lkf_pkt *_
 #if LKF_DIAG
       u64 ts0 = clock64();
       dg[12] += ts0 - tr0;
+      dg[6] += ts0 - tb0;
 #endif
-      if (x < n && (k + x) < nextAt) {
+      if (x < n && (k + x) < nextAt && rl32(u32(gapLater), x) == 0) {
         DIAG(3, 1);
         // the packet at lane x needs the full restatement
         const uint4 a0 = make_uint4(rl32(r0.x, x), rl32(r0.y, x), rl32(r0.z, x), rl32(r0.w, x));
@@ -2181,10 +2231,7 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.fwdCnt = a.fwdCnt;
   A.fwdBytes = a.fwdBytes;
   A.stats = a.stats;
-  if (a.mode == 1)
-    hipLaunchKernelGGL(k_decide_dt, dim3(a.nlanes), dim3(64), 0, s, A, a.pkts);
-  else
-    hipLaunchKernelGGL(k_decide, dim3(nblk(a.nlanes, 64)), dim3(64), 0, s, A, a.pkts);
+  hipLaunchKernelGGL(k_decide_dt, dim3(a.nlanes), dim3(64), 0, s, A, a.pkts);
   return hipGetLastError();
 }
 

@@ -9,10 +9,9 @@
 namespace lkf {
 
 struct DecideLaunch {
-  int mode;                 // 0: k_decide (lanes = DownTracks of a track), 1: k_decide_dt (wave = DownTrack)
-  const uint32_t *sched;    // mode 0: lane -> DownTrack; mode 1: wave -> DownTrack
+  const uint32_t *sched;    // wave -> DownTrack (per-XCD interleaved schedule)
   const uint32_t *waveTrack;
-  uint32_t nlanes;          // mode 0: lanes; mode 1: waves
+  uint32_t nlanes;          // waves
   DTHot *hot;
   const DevDT *dts;
   const DevTrack *tracks;

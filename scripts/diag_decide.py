@@ -10,8 +10,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-NAMES = ["waves", "chunks", "runs", "serial", "event_stops", "cause_cls", "cause_contig", "cause_vp8",
-         "cyc_missing", "cyc_seqpush", "cause_seq", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
+NAMES = ["waves", "chunks", "runs", "serial", "c_cls", "cyc_classify", "cyc_runbody", "cyc_prologue",
+         "c_esn", "c_vp8", "c_marshal", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
 
 
 def main():
@@ -20,7 +20,7 @@ def main():
     pkg = importlib.import_module("livekit-server_amd")
     wl = importlib.import_module("livekit-server_amd.workload")
     tr = wl.Trace(2, duration_s=float(nb), batch_s=1.0, rooms=rooms)
-    lib = os.path.join(ROOT, "livekit-server_amd", "lib", "liblkfwd_diag.so")
+    lib = os.path.join(ROOT, "livekit-server_amd", "lib", os.environ.get("DIAG_LIB", "liblkfwd_diag.so"))
     eng = pkg.Engine.for_trace(tr, lib_path=lib)
     fn = eng.lib.lkf_debug_counters
     fn.restype = C.c_int
