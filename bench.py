@@ -137,14 +137,24 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
 
+    hprof = [0.0, 0.0, 0.0] if os.environ.get("LKF_HOST_PROF") else None
+
     def step(b):
+        ta = time.perf_counter()
         wl.queue_events(eng.api, eng.h, trace, b)
+        tb = time.perf_counter()
         n, alen = meta[b]
         if args.ingress:
             eng.ingest_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
         else:
             eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
+        tc = time.perf_counter()
         eng.run(sp)
+        if hprof is not None:
+            td = time.perf_counter()
+            hprof[0] += tb - ta
+            hprof[1] += tc - tb
+            hprof[2] += td - tc
 
     for b in range(args.warmup):
         step(b)
@@ -157,6 +167,10 @@ def main():
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
+    t_host = time.perf_counter() - t0  # host time to enqueue the K steps (control ops, submit, lkf_run)
+    if hprof is not None:
+        print("host ms/step (incl. warmup): queue_events %.4f submit %.4f run %.4f" %
+              tuple(1e3 * x / nb for x in hprof), file=sys.stderr)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -239,6 +253,7 @@ def main():
                                       "achieved": round(pipe_ach, 1),
                                       "frac": round(pipe_ach / PEAK_HBM_GBPS, 4)}},
             "cpu_baseline": cpu,
+            "host_enqueue_ms_per_step": round(t_host * 1e3 / args.steps, 4),
             "tuples_per_step": cum["tuples"] // args.steps,
             "forwarded_per_step": fwd // args.steps,
         }

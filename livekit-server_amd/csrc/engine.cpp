@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -49,6 +50,7 @@ struct BatchCtx {
   Tuple *dTuples = nullptr;
   uint32_t *dFwdCnt = nullptr;
   uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
+  uint32_t *dGFirst = nullptr;  // emit group g -> output position owning record 64g
   lkf_out *dOut = nullptr;
   uint8_t *dOutArena = nullptr;
   uint64_t *dStats = nullptr;
@@ -65,6 +67,12 @@ struct BatchCtx {
 
 struct lkf_engine {
   int dev = 0;
+  // LKF_HOST_PROF=1: wall time of lkf_run's host sections (printed by lkf_destroy)
+  bool hostProf = false;
+  double hp[7] = {};  // pre, stage wait, csr build, launches, total, runs, staging copies
+  std::vector<uint32_t> fill;  // event CSR fill cursors
+  std::vector<uint32_t> csrOff;
+  std::vector<DevEvent> csrEv;
   hipStream_t own = nullptr;    // copies, lookups
   hipStream_t decS = nullptr;   // decide stage (high priority)
   hipStream_t emitS = nullptr;  // emit stage (low priority)
@@ -320,6 +328,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dFwdBytes, c.max_downtracks));
     A(dalloc(&x.dRecBase, c.max_downtracks));
     A(dalloc(&x.dByteBase, c.max_downtracks));
+    A(dalloc(&x.dGFirst, c.max_out_pkts / 64 + 2));
     A(dalloc(&x.dOut, c.max_out_pkts));
     A(dalloc(&x.dOutArena, c.max_out_bytes + 64));
     A(dalloc(&x.dStats, kStatsWords));
@@ -364,16 +373,22 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   }
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device);
-  // emit is grid-stride: 4 workgroups (16 waves) per CU saturate HBM and
-  // leave wave slots for the next batch's decide stage.
-  int perCU = 4;
+  // emit is grid-stride with one-wave workgroups: 16 waves per CU saturate
+  // HBM and leave wave slots for the next batch's decide stage.
+  int perCU = 16;
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
+  if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   return e;
 }
 
 void lkf_destroy(lkf_engine *e) {
   if (!e) return;
+  if (e->hostProf && e->hp[5] > 0)
+    fprintf(stderr,
+            "lkf host ms/run: pre %.4f stage-wait %.4f csr %.4f copies %.4f launches %.4f total %.4f (%d runs)\n",
+            e->hp[0] / e->hp[5], e->hp[1] / e->hp[5], e->hp[2] / e->hp[5], e->hp[6] / e->hp[5],
+            e->hp[3] / e->hp[5], e->hp[4] / e->hp[5], int(e->hp[5]));
   (void)hipSetDevice(e->dev);
   if (e->cur && e->cur != e->own) (void)hipStreamSynchronize(e->cur);
   if (e->own) (void)hipStreamSynchronize(e->own);
@@ -391,7 +406,7 @@ void lkf_destroy(lkf_engine *e) {
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
-                 x.dRawPkts};
+                 x.dRawPkts, x.dGFirst};
     for (void *p : q)
       if (p) (void)hipFree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
@@ -651,6 +666,9 @@ int lkf_run(lkf_engine *e, void *stream) {
   }
   // The caller's stream orders the batch's inputs; the stages themselves run
   // on the engine's decide/emit streams (completion: lkf_sync).
+  using clk = std::chrono::steady_clock;
+  const auto tp0 = clk::now();
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   hipStream_t us = stream ? reinterpret_cast<hipStream_t>(stream) : e->own;
   e->cur = us;
   hipStream_t s = e->decS;
@@ -662,39 +680,61 @@ int lkf_run(lkf_engine *e, void *stream) {
   // this context's previous batch (run n-2) must have finished its emit stage
   if (x.used) HIPCHK(hipStreamWaitEvent(s, x.emitted, 0), "wait emit");
 
-  // per-lane event CSR (stable: queue order within a lane, then by at_pkt)
-  std::stable_sort(e->pending.begin(), e->pending.end(),
-                   [&](const lkf_engine::Pend &a, const lkf_engine::Pend &b) {
-                     int la = e->dtLane[a.dt], lb = e->dtLane[b.dt];
-                     if (la != lb) return la < lb;
-                     return a.ev.at < b.ev.at;
-                   });
+  // per-lane event CSR (stable: queue order within a lane, then by at_pkt).
+  // Counting sort by lane straight into the pinned staging buffer; a lane
+  // whose ops were queued out of at_pkt order gets a stable insertion sort.
+  const auto tp1 = clk::now();
   lkf_engine::Stage &sg = e->stage[e->nRuns & 1];
   if (sg.used) HIPCHK(hipEventSynchronize(sg.done), "stage wait");
-  size_t nev = 0;
-  for (auto &p : e->pending)
-    if (e->dtLane[p.dt] >= 0) nev++;
-  if (nev > sg.evCap) {
-    if (sg.ev) HIPCHK(hipHostFree(sg.ev), "free stage");
-    sg.evCap = std::max<size_t>(nev, 4096);
-    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sg.ev), sg.evCap * sizeof(DevEvent)), "alloc stage");
-  }
+  const auto tp2 = clk::now();
   if (size_t(nl) + 1 > sg.offCap) {
     if (sg.off) HIPCHK(hipHostFree(sg.off), "free stage");
     sg.offCap = size_t(nl) + 1;
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sg.off), sg.offCap * sizeof(uint32_t)), "alloc stage");
   }
   if (!sg.done) HIPCHK(hipEventCreateWithFlags(&sg.done, hipEventDisableTiming), "stage event");
-  std::memset(sg.off, 0, (size_t(nl) + 1) * sizeof(uint32_t));
-  size_t k = 0;
+  // built in cacheable host memory, then one sequential write into the
+  // pinned (write-combined) staging buffer, pulled by a copy kernel
+  std::vector<uint32_t> &off = e->csrOff;
+  off.assign(size_t(nl) + 1, 0u);
+  size_t nev = 0;
   for (auto &p : e->pending) {
-    int l = e->dtLane[p.dt];
+    const int l = e->dtLane[p.dt];
     if (l < 0) continue;  // op for a removed DownTrack
-    sg.off[l + 1]++;
-    sg.ev[k++] = p.ev;
+    off[l + 1]++;
+    nev++;
   }
-  for (uint32_t l = 0; l < nl; l++) sg.off[l + 1] += sg.off[l];
+  for (uint32_t l = 0; l < nl; l++) off[l + 1] += off[l];
+  std::vector<DevEvent> &evs = e->csrEv;
+  evs.resize(nev);
+  e->fill.assign(off.begin(), off.begin() + nl);
+  for (auto &p : e->pending) {
+    const int l = e->dtLane[p.dt];
+    if (l < 0) continue;
+    evs[e->fill[l]++] = p.ev;
+  }
+  for (uint32_t l = 0; l < nl; l++) {
+    const uint32_t b = off[l], en = off[l + 1];
+    for (uint32_t i = b + 1; i < en; i++) {
+      if (evs[i].at >= evs[i - 1].at) continue;
+      const DevEvent v = evs[i];  // queued out of at_pkt order: stable insertion
+      uint32_t j = i;
+      while (j > b && evs[j - 1].at > v.at) {
+        evs[j] = evs[j - 1];
+        j--;
+      }
+      evs[j] = v;
+    }
+  }
   e->pending.clear();
+  if (nev > sg.evCap) {
+    if (sg.ev) HIPCHK(hipHostFree(sg.ev), "free stage");
+    sg.evCap = std::max<size_t>(nev, 4096);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sg.ev), sg.evCap * sizeof(DevEvent)), "alloc stage");
+  }
+  if (nev) std::memcpy(sg.ev, evs.data(), nev * sizeof(DevEvent));
+  std::memcpy(sg.off, off.data(), (size_t(nl) + 1) * sizeof(uint32_t));
+  const auto tp25 = clk::now();
   if (nev > e->evCap) {
     if (e->dEvents) {
       HIPCHK(hipStreamSynchronize(s), "sync before events realloc");
@@ -703,11 +743,11 @@ int lkf_run(lkf_engine *e, void *stream) {
     e->evCap = std::max<uint64_t>(nev, 4096);
     HIPCHK(dalloc(&e->dEvents, e->evCap), "alloc events");
   }
-  if (nev) HIPCHK(hipMemcpyAsync(e->dEvents, sg.ev, nev * sizeof(DevEvent), hipMemcpyHostToDevice, s), "events copy");
-  HIPCHK(hipMemcpyAsync(e->dEvOff, sg.off, (size_t(nl) + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s),
-         "evoff copy");
+  HIPCHK(launch_h2d(s, e->dEvents, sg.ev, nev * sizeof(DevEvent), e->dEvOff, sg.off, (size_t(nl) + 1) * sizeof(uint32_t)),
+         "event csr pull");
   HIPCHK(hipEventRecord(sg.done, s), "stage record");
   sg.used = true;
+  const auto tp3 = clk::now();
 
   // ---- decide stage (decide stream)
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
@@ -748,7 +788,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(launch_decide(s, d), "decide");
   HIPCHK(hipEventRecord(rg[2], s), "event");
   HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
-                     x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm),
+                     x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm, x.dGFirst, e->cfg.max_out_pkts),
          "out scan");
   HIPCHK(hipEventRecord(x.decided, s), "event");
 
@@ -759,6 +799,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.perm = e->dPerm;
   m.recBase = x.dRecBase;
   m.byteBase = x.dByteBase;
+  m.gFirst = x.dGFirst;
   m.slotBase = x.dSlotBase;
   m.totals = x.dTot + 2;
   m.tuples = x.dTuples;
@@ -776,6 +817,15 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum), "accumulate");
   HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
+  if (e->hostProf) {
+    e->hp[0] += std::chrono::duration<double, std::milli>(tp1 - tp0).count();
+    e->hp[1] += std::chrono::duration<double, std::milli>(tp2 - tp1).count();
+    e->hp[2] += std::chrono::duration<double, std::milli>(tp25 - tp2).count();
+    e->hp[6] += std::chrono::duration<double, std::milli>(tp3 - tp25).count();
+    e->hp[3] += ms_since(tp3);
+    e->hp[4] += ms_since(tp0);
+    e->hp[5] += 1;
+  }
   x.used = true;
   x.checked = false;
   e->lastCtx = ci;

@@ -1078,6 +1078,8 @@ struct ScanIn {
   const u32 *tBegin, *tEnd;
   const u32 *cnt;
   const u64 *bytes;
+  u32 *gFirst;  // mode 1: emit group index (group g -> position owning record g*EMIT_G)
+  u64 gCap;     // output record capacity (groups beyond it are never read)
 };
 
 __device__ __forceinline__ void scan_load(const ScanIn &in, u32 i, u64 &a, u64 &b) {
@@ -1192,11 +1194,17 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_down(ScanIn in, u32 n, const u6
     u32 d = base + k * SCAN_T + threadIdx.x;
     u64 a = 0, b = 0;
     if (d < n) scan_load(in, d, a, b);
+    const u64 cnt = a;
     u64 ta, tb;
     block_scan_excl(a, b, ta, tb);
     if (d < n) {
       outA[d] = a + carryA;
       if (outB) outB[d] = b + carryB;
+      // emit groups of 64 records whose first record belongs to position d
+      if (in.gFirst && cnt) {
+        const u64 r0 = a + carryA, r1 = min(r0 + cnt, in.gCap);
+        for (u64 g = (r0 + 63) >> 6; (g << 6) < r1; g++) in.gFirst[g] = d;
+      }
     }
     carryA += ta;
     carryB += tb;
@@ -1893,20 +1901,34 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 }
 
 // ---------------------------------------------------------------------------
-// k_emit: wire bytes.  A block takes EMIT_G consecutive output records
-// (grid-stride over groups), builds their RTP header + extension block +
-// munged VP8 descriptor ("prefix") in LDS, then sweeps the group's output
-// bytes in 16-B chunks: prefix chunks from LDS, payload chunks as byte-
-// shifted copies of the input packet (two dwordx4 loads + v_alignbyte).
+// k_emit: wire bytes.  One wave per workgroup; waves run independently (no
+// cross-wave barrier), so one wave's prefix phase (dependent loads) hides
+// behind the other waves' copy phase.  A wave takes EMIT_G consecutive output
+// records (grid-stride over groups):
+//   prefix phase  lane = record: owning DownTrack from the group index
+//                 (gFirst, a 1-3 step search), then the RTP header +
+//                 extension block + munged VP8 descriptor ("prefix") in LDS.
+//   copy phase    the group's output bytes as a flat sweep of 16-B chunks,
+//                 two windows of 64 chunks per iteration (both loads in
+//                 flight together).  A chunk's record comes from a
+//                 wave-uniform cursor plus the record starts inside the
+//                 window (readlane loop, no per-lane search).  Prefix chunks
+//                 come from LDS, payload chunks are byte-shifted copies of the
+//                 input packet (two dwordx4 loads + v_alignbyte).
 // ---------------------------------------------------------------------------
-constexpr int EMIT_T = 256;
+constexpr int EMIT_T = 64;
 constexpr int EMIT_G = 64;
-constexpr int PRE_MAX = 128;
+constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 descriptor = 90
+
+#ifndef LKF_EMIT_NT
+#define LKF_EMIT_NT 1  // non-temporal output stores: keep L2 for the payload re-reads
+#endif
 
 struct EmitArgs {
   const u32 *perm;      // output position -> DownTrack (track-major order)
   const u64 *recBase;   // [position] exclusive scan of forwarded counts
   const u64 *byteBase;  // [position] exclusive scan of output bytes
+  const u32 *gFirst;    // [group] position owning record group*EMIT_G
   const u64 *slotBase;
   const u64 *totals;    // [0] records, [1] bytes
   const Tuple *tuples;
@@ -1926,50 +1948,78 @@ __device__ __forceinline__ u32 align_byte(u32 hi, u32 lo, u32 sh) {
 __device__ __forceinline__ u32 keep_mask(int kb) {  // low kb bytes of a dword
   return kb >= 4 ? 0xffffffffu : kb <= 0 ? 0u : ((1u << (8 * kb)) - 1);
 }
+// bytes [s, s+16) of the arena from the two aligned 16-B words covering them
+__device__ __forceinline__ uint4 shift_window(uint4 q0, uint4 q1, u32 sh) {
+  const u32 q = sh >> 2, rb = sh & 3;
+  const u32 x0 = q == 0 ? q0.x : q == 1 ? q0.y : q == 2 ? q0.z : q0.w;
+  const u32 x1 = q == 0 ? q0.y : q == 1 ? q0.z : q == 2 ? q0.w : q1.x;
+  const u32 x2 = q == 0 ? q0.z : q == 1 ? q0.w : q == 2 ? q1.x : q1.y;
+  const u32 x3 = q == 0 ? q0.w : q == 1 ? q1.x : q == 2 ? q1.y : q1.z;
+  const u32 x4 = q == 0 ? q1.x : q == 1 ? q1.y : q == 2 ? q1.z : q1.w;
+  uint4 v;
+  v.x = align_byte(x1, x0, rb);
+  v.y = align_byte(x2, x1, rb);
+  v.z = align_byte(x3, x2, rb);
+  v.w = align_byte(x4, x3, rb);
+  return v;
+}
+__device__ __forceinline__ void store16(u8 *p, uint4 v) {
+#if LKF_EMIT_NT
+  __builtin_nontemporal_store(v.x, reinterpret_cast<u32 *>(p));
+  __builtin_nontemporal_store(v.y, reinterpret_cast<u32 *>(p) + 1);
+  __builtin_nontemporal_store(v.z, reinterpret_cast<u32 *>(p) + 2);
+  __builtin_nontemporal_store(v.w, reinterpret_cast<u32 *>(p) + 3);
+#else
+  *reinterpret_cast<uint4 *>(p) = v;
+#endif
+}
 
 __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
   __shared__ __attribute__((aligned(16))) u8 pre[EMIT_G][PRE_MAX];
-  __shared__ u64 sOff[EMIT_G];
-  __shared__ u64 sSrc[EMIT_G];
+  __shared__ u64 sSrc[EMIT_G];  // arena offset of the record's first payload byte after the prefix
+  __shared__ u32 sCs[EMIT_G];   // first chunk of the record, relative to the group
   __shared__ u32 sLen[EMIT_G];
-  __shared__ u32 sPre[EMIT_G];
+  __shared__ u32 sPre[EMIT_G];  // prefix length | (LDS region length << 16)
+  const u32 lane = threadIdx.x;
   const u64 total = A.totals[0];
   const u64 ngroups = (total + EMIT_G - 1) / EMIT_G;
   if (total > A.outCap || A.totals[1] > A.outByteCap) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(A.err, 4u);
+    if (blockIdx.x == 0 && lane == 0) atomicOr(A.err, 4u);
     return;
   }
   // XCD-aware partition: workgroups are dispatched round-robin over the 8
   // XCDs, so blockIdx % 8 names the XCD.  Each XCD walks its own contiguous
   // eighth of the (track-major) output in order: the records that re-read a
   // track's payloads (one per subscribing DownTrack) are adjacent, so the
-  // re-reads hit that XCD's 4 MiB L2 instead of going to HBM.  (Falls back to a plain grid-stride when
-  // the grid is not a multiple of 8.)
+  // re-reads hit that XCD's 4 MiB L2 instead of going to HBM.  (Falls back to
+  // a plain grid-stride when the grid is not a multiple of 8.)
   const u32 nx = (gridDim.x % 8 == 0) ? 8u : 1u;
   const u32 xcd = blockIdx.x % nx, slotInX = blockIdx.x / nx, perX = gridDim.x / nx;
   const u64 gpx = (ngroups + nx - 1) / nx;
   const u64 gBeg = u64(xcd) * gpx, gEnd = min(ngroups, gBeg + gpx);
   for (u64 g = gBeg + slotInX; g < gEnd; g += perX) {
     const u64 r0 = g * EMIT_G;
-    const int nrec = int(min(u64(EMIT_G), total - r0));
-    if (threadIdx.x < nrec) {
-      const u64 r = r0 + threadIdx.x;
-      // DownTrack owning record r: last d with recBase[d] <= r
-      u32 lo = 0, hi = A.ndts;
+    const u32 nrec = u32(min(u64(EMIT_G), total - r0));
+    // ---- prefix phase: lane = record
+    const u32 pLo = A.gFirst[g];
+    const u32 pHi = (g + 1 < ngroups) ? A.gFirst[g + 1] + 1 : A.ndts;
+    u64 outOff = 0;
+    if (lane < nrec) {
+      const u64 r = r0 + lane;
+      // position owning record r: last p in [pLo, pHi) with recBase[p] <= r
+      u32 lo = pLo, hi = pHi;
       while (hi - lo > 1) {
-        u32 mid = (lo + hi) >> 1;
+        const u32 mid = (lo + hi) >> 1;
         if (A.recBase[mid] <= r)
           lo = mid;
         else
           hi = mid;
       }
       const u32 d = A.perm[lo];
-      const u64 j = r - A.recBase[lo];
-      const Tuple t = A.tuples[A.slotBase[d] + j];
-      const lkf_pkt *pp = A.pkts + t.pkt;
-      const PktV p = load_pkt(pp);
+      const Tuple t = A.tuples[A.slotBase[d] + (r - A.recBase[lo])];
+      const PktV p = load_pkt(A.pkts + t.pkt);
       const DevDT dt = A.dts[d];
-      const u64 outOff = A.byteBase[lo] + t.relOff;
+      outOff = A.byteBase[lo] + t.relOff;
       lkf_out o;
       o.ext_sn = t.extSN;
       o.ext_ts = t.extTS;
@@ -1982,7 +2032,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       o.reserved = 0;
       A.out[r] = o;
       // prefix: RTP header (getTranslatedRTPHeader downtrack.go:1714-1726)
-      u8 *w = pre[threadIdx.x];
+      u8 *w = pre[lane];
       const int cc = p.hdr0 & 0xf;
       const bool playout = t.flags & T_PLAYOUT;
       const bool hasExt = playout || dt.extAbs;
@@ -2031,62 +2081,102 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         n += t.codecLen;
         src += p.vhs;
       }
-      // LDS region = prefix rounded up to 16 B, tail filled from the payload
-      // (so every 16-B chunk is either all-LDS or all-payload)
+      // LDS region = prefix rounded up to 16 B, its tail filled from the
+      // payload (so every 16-B chunk is either all-LDS or all-payload)
       const int R = (n + 15) & ~15;
-      for (int i = n; i < R; i++) w[i] = (i < int(t.outLen)) ? raw[(src - p.arenaOff) + (i - n)] : 0;
-      sOff[threadIdx.x] = outOff;
-      sSrc[threadIdx.x] = src;
-      sLen[threadIdx.x] = t.outLen;
-      sPre[threadIdx.x] = u32(n) | (u32(R) << 16);
-    }
-    __syncthreads();
-    const u64 base = sOff[0];
-    const u64 end = sOff[nrec - 1] + ((u64(sLen[nrec - 1]) + 15) & ~u64(15));
-    const u32 nchunks = u32((end - base) >> 4);
-    for (u32 c = threadIdx.x; c < nchunks; c += EMIT_T) {
-      const u64 a = base + (u64(c) << 4);
-      int lo = 0, hi = nrec;
-      while (hi - lo > 1) {
-        int mid = (lo + hi) >> 1;
-        if (sOff[mid] <= a)
-          lo = mid;
-        else
-          hi = mid;
-      }
-      const u32 o = u32(a - sOff[lo]);
-      const u32 P = sPre[lo] & 0xffff, R = sPre[lo] >> 16, Ln = sLen[lo];
-      uint4 v;
-      if (o < R) {
-        v = *reinterpret_cast<const uint4 *>(&pre[lo][o]);
-      } else {
-        const u64 s = sSrc[lo] + (o - P);
-        const u64 W = s & ~u64(15);
-        const u32 sh = u32(s & 15);
+      if (R > n) {
+        const u64 W = src & ~u64(15);
         const uint4 q0 = *reinterpret_cast<const uint4 *>(A.arena + W);
         const uint4 q1 = *reinterpret_cast<const uint4 *>(A.arena + W + 16);
-        const u32 q = sh >> 2, rb = sh & 3;
-        // x_i = dword (q + i) of the 32-B window, q in 0..3
-        const u32 x0 = q == 0 ? q0.x : q == 1 ? q0.y : q == 2 ? q0.z : q0.w;
-        const u32 x1 = q == 0 ? q0.y : q == 1 ? q0.z : q == 2 ? q0.w : q1.x;
-        const u32 x2 = q == 0 ? q0.z : q == 1 ? q0.w : q == 2 ? q1.x : q1.y;
-        const u32 x3 = q == 0 ? q0.w : q == 1 ? q1.x : q == 2 ? q1.y : q1.z;
-        const u32 x4 = q == 0 ? q1.x : q == 1 ? q1.y : q == 2 ? q1.z : q1.w;
-        v.x = align_byte(x1, x0, rb);
-        v.y = align_byte(x2, x1, rb);
-        v.z = align_byte(x3, x2, rb);
-        v.w = align_byte(x4, x3, rb);
-        if (o + 16 > Ln) {  // zero the 16-B tail padding
-          const int keep = int(Ln) - int(o);
-          v.x &= keep_mask(keep);
-          v.y &= keep_mask(keep - 4);
-          v.z &= keep_mask(keep - 8);
-          v.w &= keep_mask(keep - 12);
+        const uint4 v = shift_window(q0, q1, u32(src & 15));
+        const u32 vw[4] = {v.x, v.y, v.z, v.w};
+        for (int i = n; i < R; i++) {
+          const int b = i - n;
+          w[i] = (i < int(t.outLen)) ? u8(vw[b >> 2] >> (8 * (b & 3))) : 0;
         }
       }
-      *reinterpret_cast<uint4 *>(A.outArena + a) = v;
+      sSrc[lane] = src;
+      sLen[lane] = t.outLen;
+      sPre[lane] = u32(n) | (u32(R) << 16);
     }
-    __syncthreads();
+    // first chunk of each record relative to the group's first output byte
+    const u64 gByte = rl64(outOff, 0);
+    if (lane < nrec) sCs[lane] = u32((outOff - gByte) >> 4);
+    __syncthreads();  // one wave: orders the LDS writes above before the cross-lane reads below
+    // ---- copy phase: flat sweep of the group's 16-B chunks
+    const u32 nchunks = sCs[nrec - 1] + ((sLen[nrec - 1] + 15) >> 4);
+    u8 *const outG = A.outArena + gByte;
+    u32 cur = 0;  // wave-uniform: a record whose first chunk is <= c0
+    for (u32 c0 = 0; c0 < nchunks;) {
+      u32 wEnd = min(c0 + 2 * 64, nchunks);
+      const u32 ji = cur + 1 + lane;
+      const u32 st = ji < nrec ? sCs[ji] : 0xffffffffu;
+      u64 inW = __ballot(st < wEnd);
+      if (inW == ~0ull) {  // more than 63 records start in the window: cut it
+        wEnd = rl32(st, 63);
+        inW = __ballot(st < wEnd);
+      }
+      const u32 k = u32(__popcll(inW));
+      const u32 cA = c0 + lane, cB = c0 + 64 + lane;
+      u32 jA = cur, jB = cur;
+      for (u32 i = 0; i < k; i++) {
+        const u32 s = rl32(st, i);
+        jA += cA >= s ? 1u : 0u;
+        jB += cB >= s ? 1u : 0u;
+      }
+      const bool actA = cA < wEnd, actB = cB < wEnd;
+      // chunk A / B sources
+      const u32 oA = (cA - sCs[jA]) << 4, oB = (cB - sCs[jB]) << 4;
+      const u32 pA = sPre[jA], pB = sPre[jB];
+      const bool ldsA = oA < (pA >> 16), ldsB = oB < (pB >> 16);
+      const u64 sA = sSrc[jA] + (oA - (pA & 0xffff)), sB = sSrc[jB] + (oB - (pB & 0xffff));
+      uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, b0 = a0, b1 = a0;
+      if (actA && !ldsA) {
+        const u8 *q = A.arena + (sA & ~u64(15));
+        a0 = *reinterpret_cast<const uint4 *>(q);
+        a1 = *reinterpret_cast<const uint4 *>(q + 16);
+      }
+      if (actB && !ldsB) {
+        const u8 *q = A.arena + (sB & ~u64(15));
+        b0 = *reinterpret_cast<const uint4 *>(q);
+        b1 = *reinterpret_cast<const uint4 *>(q + 16);
+      }
+      if (actA) {
+        uint4 v;
+        if (ldsA) {
+          v = *reinterpret_cast<const uint4 *>(&pre[jA][oA]);
+        } else {
+          v = shift_window(a0, a1, u32(sA & 15));
+          const int keep = int(sLen[jA]) - int(oA);
+          if (keep < 16) {  // zero the 16-B tail padding
+            v.x &= keep_mask(keep);
+            v.y &= keep_mask(keep - 4);
+            v.z &= keep_mask(keep - 8);
+            v.w &= keep_mask(keep - 12);
+          }
+        }
+        store16(outG + (u64(cA) << 4), v);
+      }
+      if (actB) {
+        uint4 v;
+        if (ldsB) {
+          v = *reinterpret_cast<const uint4 *>(&pre[jB][oB]);
+        } else {
+          v = shift_window(b0, b1, u32(sB & 15));
+          const int keep = int(sLen[jB]) - int(oB);
+          if (keep < 16) {
+            v.x &= keep_mask(keep);
+            v.y &= keep_mask(keep - 4);
+            v.z &= keep_mask(keep - 8);
+            v.w &= keep_mask(keep - 12);
+          }
+        }
+        store16(outG + (u64(cB) << 4), v);
+      }
+      cur += k;
+      c0 = wEnd;
+    }
+    __syncthreads();  // LDS reused by the next group
   }
 }
 
@@ -2190,8 +2280,10 @@ hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, u32 n, const 
 
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const u32 *tBegin, const u32 *tEnd, const u32 *cnt,
                        const u64 *bytes, u32 n, u64 *partA, u64 *partB, u64 *outA, u64 *outB, u64 *totA, u64 *totB,
-                       const u32 *perm) {
+                       const u32 *perm, u32 *gFirst, u64 gCap) {
   ScanIn in;
+  in.gFirst = gFirst;
+  in.gCap = gCap;
   in.mode = mode;
   in.perm = perm;
   in.dts = dts;
@@ -2240,6 +2332,7 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   A.perm = a.perm;
   A.recBase = a.recBase;
   A.byteBase = a.byteBase;
+  A.gFirst = a.gFirst;
   A.slotBase = a.slotBase;
   A.totals = a.totals;
   A.tuples = a.tuples;
@@ -2253,6 +2346,27 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   A.outByteCap = a.outByteCap;
   A.err = a.err;
   hipLaunchKernelGGL(k_emit, dim3(a.grid), dim3(EMIT_T), 0, s, A);
+  return hipGetLastError();
+}
+
+__global__ void k_h2d(u32 *__restrict__ dA, const u32 *__restrict__ sA, u64 nA, u32 *__restrict__ dB,
+                      const u32 *__restrict__ sB, u64 nB) {
+  const u64 stride = u64(gridDim.x) * blockDim.x;
+  for (u64 i = u64(blockIdx.x) * blockDim.x + threadIdx.x; i < nA + nB; i += stride) {
+    if (i < nA)
+      dA[i] = sA[i];
+    else
+      dB[i - nA] = sB[i - nA];
+  }
+}
+
+hipError_t launch_h2d(hipStream_t s, void *dstA, const void *srcA, size_t nA, void *dstB, const void *srcB,
+                      size_t nB) {
+  const u64 words = (nA + nB) / 4;
+  if (!words) return hipSuccess;
+  const u32 grid = u32(std::min<u64>((words + 255) / 256, 1024));
+  hipLaunchKernelGGL(k_h2d, dim3(grid), dim3(256), 0, s, static_cast<u32 *>(dstA), static_cast<const u32 *>(srcA),
+                     u64(nA / 4), static_cast<u32 *>(dstB), static_cast<const u32 *>(srcB), u64(nB / 4));
   return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ struct DecideLaunch {
 struct EmitLaunch {
   const uint32_t *perm;  // output position -> DownTrack
   const uint64_t *recBase, *byteBase, *slotBase, *totals;  // recBase/byteBase by position
+  const uint32_t *gFirst;  // [group] position owning record 64*group (k_scan_down mode 1)
   const Tuple *tuples;
   const lkf_pkt *pkts;
   const uint8_t *arena;
@@ -57,7 +58,7 @@ hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, uint32_t n, c
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t *tBegin, const uint32_t *tEnd,
                        const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
                        uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB,
-                       const uint32_t *perm);
+                       const uint32_t *perm, uint32_t *gFirst = nullptr, uint64_t gCap = 0);
 struct IngestLaunch {
   const lkf_raw_pkt *raws;
   uint32_t n;
@@ -89,6 +90,9 @@ hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a);
 hipError_t launch_speakers(hipStream_t s, const SpeakersLaunch &a);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
+// pulls two pinned host buffers (device-visible) into device memory with one
+// kernel (sizes multiples of 4 B); replaces two hipMemcpyAsync calls per run
+hipError_t launch_h2d(hipStream_t s, void *dstA, const void *srcA, size_t nA, void *dstB, const void *srcB, size_t nB);
 hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum);
 hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint32_t d,
                              const uint16_t *sns, uint32_t n, int64_t nowMs, lkf_seq_meta *out, uint32_t *nOut);
