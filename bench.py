@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", ""))
+    ap.add_argument("--sync-each", action="store_true",
+                    help="diagnostic: wait for each step (no decide/emit overlap; standalone kernel times)")
     ap.add_argument("--ingress", action="store_true",
                     help="step = Buffer.calc over raw datagrams (lkf_ingest_device) + forwarding")
     args = ap.parse_args()
@@ -150,6 +152,8 @@ def main():
             eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
         tc = time.perf_counter()
         eng.run(sp)
+        if args.sync_each:
+            eng.sync()
         if hprof is not None:
             td = time.perf_counter()
             hprof[0] += tb - ta

@@ -1449,6 +1449,22 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 // Consume the chunk's descriptor registers here, once.  gfx9 counts stores in
 // vmcnt too: a first use sunk into the run loop would wait there for every
 // tuple/sequencer store issued so far (one HBM write round trip per run).
+// Waits for this wave's outstanding vector-memory ops (s_waitcnt vmcnt(0);
+// gfx9 encoding: expcnt and lgkmcnt left at their maxima).  Placed at the end
+// of the rare paths that load from global memory (control ops, the full
+// per-packet step), so the waitcnt pass does not see a load that may still be
+// pending at the run-loop head and insert a vmcnt(0) there — which, with
+// stores counted in vmcnt, would stall every run on the previous run's
+// tuple/sequencer stores.
+#ifndef LKF_VM_DRAIN
+#define LKF_VM_DRAIN 1
+#endif
+__device__ __forceinline__ void vm_drain() {
+#if LKF_VM_DRAIN
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
+}
+
 __device__ __forceinline__ void pin_loaded(const uint4 &a, const uint4 &b, const uint4 &c, const uint4 &d) {
   asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
                "v"(c.y), "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
@@ -1465,16 +1481,19 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const u32 lane = threadIdx.x;
   const u64 lt = (1ull << lane) - 1;
   const u32 w = blockIdx.x;
+  // Prologue: two rounds of independent loads.  Round 1 needs only the wave
+  // index (DownTrack, track, control-op range); round 2 everything keyed by
+  // them, including the VP8 munger maps (read whole, whatever their fill, so
+  // the copy does not wait for the hot state).
   const u32 d = A.sched[w];
+  const u32 track = A.waveTrack[w];
+  u32 ev = A.evOff[w];
+  const u32 evEnd = A.evOff[w + 1];
   if (d == 0xffffffffu) return;  // padding slot of the per-XCD schedule
   const DevDT dt = A.dts[d];
-  const u32 track = dt.track;
   const u32 pb = A.tBegin[track];
   u32 pe = A.tEnd[track];
-  if (A.slotBase[d] + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
-    if (lane == 0) atomicOr(A.err, 8u);
-    pe = pb;
-  }
+  const u64 slot0 = A.slotBase[d];
   LaneOut o;
   o.nFwd = o.nBytes = o.nTuples = 0;
   o.relOff = 0;
@@ -1487,16 +1506,20 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.exKey = sEx;
   L.missKey = sMissKey;
   L.missVal = sMissVal;
-  if (L.h.flags & F_VP8) {  // VP8 munger maps live in LDS for the batch
+  const bool vp8Track = A.tracks[track].codec == LKF_CODEC_VP8;
+  if (vp8Track) {  // VP8 munger maps live in LDS for the batch
     if (lane < u32(kSetCap)) {
       sDrop[lane] = L.vc->dropKey[lane];
       sEx[lane] = L.vc->exKey[lane];
     }
-    for (u32 i = lane; i < L.h.missCount; i += 64) {
-      const u32 idx = (L.h.missHead + i) % kMissCap;
-      sMissKey[idx] = L.vc->missKey[idx];
-      sMissVal[idx] = L.vc->missVal[idx];
+    for (u32 i = lane; i < u32(kMissCap); i += 64) {
+      sMissKey[i] = L.vc->missKey[i];
+      sMissVal[i] = L.vc->missVal[i];
     }
+  }
+  if (slot0 + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
+    if (lane == 0) atomicOr(A.err, 8u);
+    pe = pb;
   }
   __syncthreads();
   L.seq = A.seq + size_t(d) * A.seqSize;
@@ -1509,9 +1532,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.offs = tk.layerOffsets;
   L.extPlayout = dt.extPlayout;
   L.extAbs = dt.extAbs;
-  u32 ev = A.evOff[w];
-  const u32 evEnd = A.evOff[w + 1];
-  o.outT = A.tuples + A.slotBase[d];
+  o.outT = A.tuples + slot0;
   u32 nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
 #if LKF_DIAG
@@ -1570,9 +1591,12 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       u64 tr0 = clock64();
       u64 tmark = tr0;
 #endif
-      while (nextAt <= k + pos) {
-        apply_ctl(L, A.events[ev++]);
-        nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
+      if (nextAt <= k + pos) {
+        while (nextAt <= k + pos) {
+          apply_ctl(L, A.events[ev++]);
+          nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
+        }
+        vm_drain();
       }
       const bool inWin = valid && lane >= pos && (k + lane) < nextAt;
       // ---- classification against the state at the start of the run
@@ -1726,6 +1750,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
               if (gapExempt) set_add(L.exKey, L.h.exHead, L.h.exCount, gapExt, kExemptKeep);
             }
             if (gOff > 1) seq_invalidate(L, gOff - 1);
+            vm_drain();
           }
         }
         // output records + sequencer slots of the forwarded lanes
@@ -1863,6 +1888,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const uint4 a2 = make_uint4(rl32(r2.x, x), rl32(r2.y, x), rl32(r2.z, x), rl32(r2.w, x));
         const uint4 a3 = make_uint4(rl32(r3.x, x), rl32(r3.y, x), rl32(r3.z, x), rl32(r3.w, x));
         decide_step(L, decode_pkt(a0, a1, a2, a3), k + x, o);
+        vm_drain();
         pos = x + 1;
       }
 #if LKF_DIAG
