@@ -32,7 +32,13 @@ extern "C" {
 /* ---- enums ------------------------------------------------------------- */
 enum lkf_kind { LKF_KIND_AUDIO = 0, LKF_KIND_VIDEO = 1 };
 /* mime of webrtc.RTPCodecCapability (forwarder.go:269-338) */
-enum lkf_codec { LKF_CODEC_NONE = 0, LKF_CODEC_OPUS = 1, LKF_CODEC_VP8 = 2, LKF_CODEC_H264 = 3 };
+enum lkf_codec {
+  LKF_CODEC_NONE = 0,
+  LKF_CODEC_OPUS = 1,
+  LKF_CODEC_VP8 = 2,  /* Simulcast selector + VP8 temporal selector + VP8 munger  forwarder.go:287-294 */
+  LKF_CODEC_H264 = 3, /* Simulcast selector                                          :295-300 */
+  LKF_CODEC_VP9 = 4   /* SVC: VP9 selector (no dependency-descriptor ext)           :301-316 */
+};
 
 /* Control ops, applied to one DownTrack immediately before the first packet
  * of its track whose batch index >= at_pkt (or at batch end).  Each op is the
@@ -133,14 +139,29 @@ typedef struct lkf_pkt {
   uint8_t vp8_tl0picidx;
   uint8_t vp8_tid;
   uint8_t vp8_keyidx;
-  int8_t layer;          /* the `layer` argument of TrackSender.WriteRTP (downtrack.go:680) */
+  int8_t layer;          /* the `layer` argument of TrackSender.WriteRTP (downtrack.go:680);
+                            for SVC the packet's spatial layer (receiver.go:667-672) */
   uint8_t audio_level;   /* RFC 6464 level (ingress only) */
-  uint8_t reserved[9];
+  uint8_t vp9_bits;      /* LKF_VP9_*: codecs.VP9Packet flags (valid with LKF_PKT_VP9) */
+  uint8_t reserved[8];
 } lkf_pkt;
 
 #define LKF_PKT_KEYFRAME 0x01
 #define LKF_PKT_VP8 0x02        /* Payload is buffer.VP8 */
 #define LKF_PKT_HAS_LEVEL 0x04  /* audio_level valid */
+#define LKF_PKT_VP9 0x08        /* Payload is codecs.VP9Packet (spatial/temporal = SID/TID) */
+
+/* codecs.VP9Packet flags (pion/rtp v1.8.3 codecs/vp9_packet.go); the first
+ * seven are the descriptor's first byte I|P|L|F|B|E|V, U is from the layer
+ * indices byte (TID|U|SID|D). */
+#define LKF_VP9_I 0x80
+#define LKF_VP9_P 0x40
+#define LKF_VP9_L 0x20
+#define LKF_VP9_F 0x10
+#define LKF_VP9_B 0x08
+#define LKF_VP9_E 0x04
+#define LKF_VP9_V 0x02
+#define LKF_VP9_U 0x01
 
 #define LKF_VP8_S 0x01
 #define LKF_VP8_I 0x02

@@ -143,7 +143,8 @@ class lkf_pkt(C.Structure):
         ("vp8_keyidx", C.c_uint8),
         ("layer", C.c_int8),
         ("audio_level", C.c_uint8),
-        ("reserved", C.c_uint8 * 9),
+        ("vp9_bits", C.c_uint8),
+        ("reserved", C.c_uint8 * 8),
     ]
 
 

@@ -207,6 +207,7 @@ static void init_hot(DTHot &h, const lkf_track_params &tp, const lkf_downtrack_p
     h.maxT = 3;  // vls.SetMaxTemporal(DefaultMaxLayerTemporal) forwarder.go:235-237
     if (tp.codec == LKF_CODEC_VP8) f |= F_VP8 | F_SIMULCAST | F_TLS_VP8;
     if (tp.codec == LKF_CODEC_H264) f |= F_SIMULCAST;
+    if (tp.codec == LKF_CODEC_VP9) f |= F_VP9;
   }
   if (p.has_expected_ts) f |= F_HAS_EXPECTED;
   h.flags = f;

@@ -67,7 +67,7 @@ struct PktV {
   i64 arr;
   u32 arenaOff, ssrc;
   u16 poff, plen;
-  u8 hdr0, hdr1, flags, vfirst, vbits, vhs, tl0, tid, keyidx;
+  u8 hdr0, hdr1, flags, vfirst, vbits, vhs, tl0, tid, keyidx, vp9;
   int8_t spatial, temporal, layer;
   u16 pid;
 };
@@ -95,6 +95,7 @@ __device__ __forceinline__ PktV decode_pkt(uint4 a, uint4 b, uint4 c, uint4 d) {
   v.tid = u8(d.x >> 24);
   v.keyidx = u8(d.y);
   v.layer = int8_t(d.y >> 8);
+  v.vp9 = u8(d.y >> 24);
   return v;
 }
 
@@ -755,8 +756,9 @@ __device__ bool fw_sourceSwitch(Lane &L, const PktV &p, i32 layer) {
   if (L.hasRefTS) {  // StreamTrackerManager.GetReferenceLayerRTPTimestamp :660-679
     i32 ref = L.h.referenceLayerSpatial;
     if (layer < 0 || layer >= 3 || ref < 0 || ref >= 3) return false;
-    u32 off = L.offs[ref * 3 + layer];
-    if (layer != ref && off == 0) return false;
+    // isSVC (:667-671): one stream, one timeline -> offset 0
+    const u32 off = L.codec == LKF_CODEC_VP9 ? 0u : L.offs[ref * 3 + layer];
+    if (L.codec != LKF_CODEC_VP9 && layer != ref && off == 0) return false;
     u32 ts = u32(p.ets) + off;
     extRefTS = (extRefTS & 0xFFFFFFFF00000000ull) + u64(ts);
     u32 e32 = u32(extExpectedTS);
@@ -879,15 +881,74 @@ __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
     }
     isSelected = layer == L.h.curS;
   }
+  bool marker = pktMarker;
+  if (hasf(L, F_VP9)) {  // VP9.Select videolayerselector/vp9.go:43-109
+    bool relevant = false;
+    if (p.flags & LKF_PKT_VP9) {
+      const bool U = p.vp9 & LKF_VP9_U, B = p.vp9 & LKF_VP9_B, E = p.vp9 & LKF_VP9_E, P = p.vp9 & LKF_VP9_P;
+      const i32 pS = p.spatial, pT = p.temporal;
+      i32 cS = L.h.curS, cT = L.h.curT;  // the local currentLayer copy (vp9.go:49)
+      bool zero = false;
+      if (L.h.curS != L.h.tgtS || L.h.curT != L.h.tgtT) {
+        i32 uS = L.h.curS, uT = L.h.curT;
+        const bool curValid = L.h.curS != INVALID && L.h.curT != INVALID;
+        if (!curValid) {
+          if (!kf)
+            zero = true;  // zero result: not selected, not relevant (vp9.go:55-57)
+          else {
+            uS = pS;
+            uT = pT;
+          }
+        } else {
+          if (L.h.curT != L.h.tgtT) {
+            if (L.h.curT < L.h.tgtT) {
+              if (pT > L.h.curT && pT <= L.h.tgtT && U && B) cT = uT = pT;
+            } else if (E) {
+              uT = L.h.tgtT;
+            }
+          }
+          if (L.h.curS != L.h.tgtS) {
+            if (L.h.curS < L.h.tgtS) {
+              if (pS > L.h.curS && pS <= L.h.tgtS && !P && B) cS = uS = pS;
+            } else if (E) {
+              uS = L.h.tgtS;
+            }
+          }
+        }
+        if (!zero && (uS != L.h.curS || uT != L.h.curT)) {
+          isSwitching = true;
+          if (!curValid && uS != INVALID && uT != INVALID) isResuming = true;
+          L.h.prevS = L.h.curS;
+          L.h.prevT = L.h.curT;
+          L.h.curS = uS;
+          L.h.curT = uT;
+        }
+      }
+      if (!zero) {
+        if (E && pS == cS && (P || L.h.tgtS <= L.h.curS)) marker = true;
+        isSelected = !(pS > cS || (pS == cS && pT > cT));
+        relevant = true;
+      }
+    }
+    if (!isSelected) {
+      // forwarder.go:1694-1702: a relevant drop still advances the munger
+      if (relevant && hasf(L, F_STARTED)) {
+        int ord;
+        u64 a, b;
+        if (mg_update(L, p, marker, ord, a, b) == MG_OK && ord == ORD_CONTIG) mg_packetDropped(L, p.esn);
+      }
+      return LKF_DROP_NOT_SELECTED;
+    }
+  }
   if (!isSelected) return LKF_DROP_NOT_SELECTED;  // IsRelevant == false for Simulcast
   o.resuming = isResuming;
   o.switching = isSwitching;
-  o.marker = pktMarker;
+  o.marker = marker;
   if (hasf(L, F_DEFICIENT) && L.h.tgtS < L.h.curS) {  // FlagPauseOnDowngrade :1709
     if (isSwitching) vls_rollback(L);
     return LKF_DROP_DOWNGRADE;
   }
-  int dr = fw_common(L, p, layer, pktMarker, o.ord, o.osn, o.ots);
+  int dr = fw_common(L, p, layer, marker, o.ord, o.osn, o.ots);
   if (dr >= 0 || p.plen == 0) {
     if (isSwitching) vls_rollback(L);
     return dr;
@@ -1290,7 +1351,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   } else if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) {
     cls = LKF_DROP_PAUSED;
   } else if (!(fl & F_SIMULCAST)) {
-    cls = LKF_DROP_NOT_SELECTED;
+    cls = (fl & F_VP9) ? -2 : LKF_DROP_NOT_SELECTED;  // VP9: full step (relevant drops move the munger)
   } else {
     const bool willSwitch =
         kf && ((L.h.curS != L.h.tgtS && ((layer > L.h.curS && layer <= L.h.tgtS) ||
@@ -1613,7 +1674,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       } else if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) {
         cls = LKF_DROP_PAUSED;
       } else if (!(fl & F_SIMULCAST)) {
-        cls = LKF_DROP_NOT_SELECTED;
+        cls = (fl & F_VP9) ? -2 : LKF_DROP_NOT_SELECTED;  // VP9: full step
       } else {
         const bool willSwitch =
             kf && ((L.h.curS != L.h.tgtS && ((layer > L.h.curS && layer <= L.h.tgtS) ||

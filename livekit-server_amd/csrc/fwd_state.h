@@ -49,6 +49,7 @@ enum : uint32_t {
   F_TLS_VP8 = 1u << 19,    // temporallayerselector.VP8
   F_HAS_EXPECTED = 1u << 20,
   F_ACTIVE = 1u << 21,
+  F_VP9 = 1u << 22,  // videolayerselector.VP9 (SVC without dependency descriptor)
 };
 
 struct alignas(16) DTHot {

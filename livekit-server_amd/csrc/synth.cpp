@@ -55,11 +55,13 @@ struct Plan {
   u8 y_bit;
   u8 level;
   u8 pt;
+  u8 vp9;  // LKF_VP9_* flags (config 5 SVC packets)
 };
 
 struct TrackGen {
   lkf_track_params p;
   int nlayers = 1;
+  bool svc = false;         // VP9 SVC: all spatial layers in one stream (one SSRC)
   u32 ssrc[3] = {0, 0, 0};  // per received layer (one ingress stream each)
   std::vector<Plan> plans;  // merged arrival order
 };
@@ -110,7 +112,7 @@ static void fill_payload(u8 *dst, int n, u64 key) {
 }
 
 extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
-  if (!cfg || cfg->config < 1 || cfg->config > 4) return nullptr;
+  if (!cfg || cfg->config < 1 || cfg->config > 5) return nullptr;
   const int C = cfg->config;
   // Every room and every track draws from its own splitmix64 stream keyed by
   // its global id, so a shard (room_base, rooms) generates exactly the rooms
@@ -155,6 +157,12 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       if (loss < 0) loss = 0.0;
       if (reorder < 0) reorder = 0.0;
       break;
+    case 5:  // VP9 L3T3 SVC + Opus DTX, congestion-driven layer changes
+      if (!rooms) rooms = 2000;
+      if (!parts) parts = 5;
+      if (loss < 0) loss = 0.01;
+      if (reorder < 0) reorder = 0.005;
+      break;
   }
 
   auto *tr = new lkfs_trace();
@@ -183,7 +191,8 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         g.p.room = room;
         g.p.publisher = p;
         g.p.kind = LKF_KIND_VIDEO;
-        g.p.codec = LKF_CODEC_VP8;
+        g.p.codec = C == 5 ? LKF_CODEC_VP9 : LKF_CODEC_VP8;
+        g.svc = C == 5;
         g.p.has_ref_ts = cb ? 1 : 0;
         g.p.is_mic = 0;
         g.p.clock_rate = 90000;
@@ -239,13 +248,15 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
           ts = int(rng.below(u32(nl)));
         if (ts > nl - 1) ts = nl - 1;
         evs.push_back(Ev{dt, LKF_CTL_SET_ALLOCATION, {ts, 2, ts, 0}, -1});
-        if (withEvents && C == 2) {
-          // congestion/subscription script: new target every 2 s per DT
-          i64 phase = i64(rng.uni() * 2.0 * NS);
+        if (withEvents && (C == 2 || C == 5)) {
+          // congestion/subscription script: new target every 2 s (config 5:
+          // every 1 s, spatial and temporal) per DT; deficient on downgrades
+          const i64 period = C == 5 ? NS : 2 * NS;
+          i64 phase = i64(rng.uni() * double(period));
           int cur = ts;
-          for (i64 t = phase; t < durNs; t += 2 * NS) {
+          for (i64 t = phase; t < durNs; t += period) {
             int ns = int(rng.below(u32(nl)));
-            int nt = 1 + int(rng.below(2));
+            int nt = C == 5 ? int(rng.below(3)) : 1 + int(rng.below(2));
             bool deficient = ns < cur;
             evs.push_back(Ev{dt, LKF_CTL_SET_ALLOCATION, {ns, nt, ns, deficient ? 1 : 0}, t0 + t});
             cur = ns;
@@ -288,7 +299,62 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
     Rng rng = keyed(g.p.track_id);
     std::vector<std::vector<Plan>> streams(g.nlayers);
     i64 netDelay = 20 * MS + i64(rng.below(10)) * MS;
-    if (g.p.kind == LKF_KIND_VIDEO) {
+    if (g.p.kind == LKF_KIND_VIDEO && g.svc) {
+      // VP9 L3T3 SVC, 30 fps: every frame carries spatial layers 0..2 in one
+      // RTP stream (one SSRC, one sequence, one timestamp per superframe).
+      // Temporal pattern T0 T2 T1 T2; U (switching-up point) on T1/T2 frames;
+      // B/E on the first/last packet of a layer frame; P unless the
+      // superframe is a key superframe; marker on the superframe's last packet.
+      static const int kSvcPkts[3] = {1, 2, 3};
+      static const int kSvcPayload[3] = {300, 600, 1000};
+      u32 ssrc = u32(rng.next()) | 1u;
+      g.ssrc[0] = ssrc;
+      u64 sn = u64(u16(rng.next()));
+      u32 tsBase = u32(rng.next());
+      u16 pid0 = u16(rng.next() & 0x7fff);
+      u8 tl00 = u8(rng.next());
+      u16 twcc = u16(rng.next());
+      std::vector<i64> reqs;
+      for (int l = 0; l < 3; l++) reqs.insert(reqs.end(), kfReq[ti][l].begin(), kfReq[ti][l].end());
+      std::sort(reqs.begin(), reqs.end());
+      size_t ri = 0;
+      i64 lastKf = -10 * NS;
+      int nframes = int(dur * 30.0);
+      for (int f = 0; f < nframes; f++) {
+        i64 cap = i64(f) * NS / 30;
+        bool kf = (f % 60) == 0;
+        while (ri < reqs.size() && reqs[ri] <= cap) {
+          if (cap - lastKf >= 500 * MS) kf = true;
+          ri++;
+        }
+        if (kf) lastKf = cap;
+        int tid = (f % 4 == 0) ? 0 : ((f % 4 == 2) ? 1 : 2);
+        int k = 0;
+        for (int sl = 0; sl < 3; sl++) {
+          for (int q = 0; q < kSvcPkts[sl]; q++, k++) {
+            Plan pl{};
+            pl.arrival = t0 + cap + netDelay + i64(k) * 150000 + i64(rng.below(2000000));
+            pl.ext_sn = sn++;
+            pl.ext_ts = u64(tsBase) + u64(f) * 3000;
+            pl.ssrc = ssrc;
+            int m = kSvcPayload[sl];
+            pl.payload_len = u16(m - m / 10 + int(rng.below(u32(m / 5))));
+            pl.pid = u16((pid0 + f) & 0x7fff);
+            pl.twcc = twcc++;
+            pl.layer = int8_t(sl);
+            pl.tid = u8(tid);
+            pl.tl0 = u8(tl00 + f / 4);
+            pl.marker = sl == 2 && q == kSvcPkts[sl] - 1;
+            pl.s_bit = q == 0;
+            pl.keyframe = kf && sl == 0 && q == 0;  // IsVP9KeyFrame (helpers.go:317-336)
+            pl.vp9 = u8(LKF_VP9_I | LKF_VP9_L | (kf ? 0 : LKF_VP9_P) | (q == 0 ? LKF_VP9_B : 0) |
+                        (q == kSvcPkts[sl] - 1 ? LKF_VP9_E : 0) | (tid > 0 ? LKF_VP9_U : 0));
+            pl.pt = 98;
+            streams[0].push_back(pl);
+          }
+        }
+      }
+    } else if (g.p.kind == LKF_KIND_VIDEO) {
       u32 tsBase[3];
       for (int l = 0; l < g.nlayers; l++) tsBase[l] = u32(rng.next());
       for (int r = 0; r < 3; r++)
@@ -354,6 +420,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
           talking = !talking;
           nextFlip += i64((talking ? 2.0 : 4.0) * -std::log(1.0 - rng.uni()) * NS) + 1;
         }
+        if (C == 5 && !talking && (k % 20) != 0) continue;  // Opus DTX: one frame per 400 ms in silence
         Plan pl{};
         pl.arrival = t0 + cap + netDelay + i64(rng.below(2000000));
         pl.ext_sn = sn++;
@@ -399,7 +466,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   std::vector<u32> streamBase(tg.size());
   for (size_t ti = 0; ti < tg.size(); ti++) {
     streamBase[ti] = u32(tr->streams.size());
-    for (int l = 0; l < tg[ti].nlayers; l++) {
+    for (int l = 0; l < (tg[ti].svc ? 1 : tg[ti].nlayers); l++) {
       lkf_stream_params sp{};
       sp.track = int32_t(ti);
       sp.layer = l;
@@ -466,7 +533,26 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         raw[15] = 0x01;
         u8 *pay = raw + kPayloadOff;
         fill_payload(pay, pl.payload_len, (u64(pl.ssrc) << 32) ^ pl.ext_sn);
-        if (g.p.kind == LKF_KIND_VIDEO) {
+        if (g.p.kind == LKF_KIND_VIDEO && g.svc) {
+          raw[16] = 0x51;  // id 5 (transport-cc), len 2
+          raw[17] = u8(pl.twcc >> 8);
+          raw[18] = u8(pl.twcc);
+          raw[19] = 0;
+          // VP9 payload descriptor (non-flexible mode): I|P|L|F|B|E|V|Z,
+          // M|PID(15), TID|U|SID|D, TL0PICIDX; then on B packets the first
+          // byte of the VP9 uncompressed header (frame marker 10, profile 0,
+          // show_existing 0, frame_type 0 = key / 1 = inter, show_frame 1)
+          pay[0] = u8((pl.vp9 & (LKF_VP9_I | LKF_VP9_P | LKF_VP9_L | LKF_VP9_F | LKF_VP9_B | LKF_VP9_E | LKF_VP9_V)));
+          pay[1] = u8(0x80 | (pl.pid >> 8));
+          pay[2] = u8(pl.pid);
+          pay[3] = u8((pl.tid << 5) | ((pl.vp9 & LKF_VP9_U) ? 0x10 : 0) | (u8(pl.layer) << 1));
+          pay[4] = pl.tl0;
+          if (pl.vp9 & LKF_VP9_B) pay[5] = pl.keyframe ? 0x82 : 0x86;
+          d.flags = LKF_PKT_VP9 | (pl.keyframe ? LKF_PKT_KEYFRAME : 0);
+          d.vp9_bits = pl.vp9;
+          d.spatial = pl.layer;  // VideoLayer{SID, TID} (buffer.go:645-655)
+          d.temporal = int8_t(pl.tid);
+        } else if (g.p.kind == LKF_KIND_VIDEO) {
           raw[16] = 0x51;  // id 5 (transport-cc), len 2
           raw[17] = u8(pl.twcc >> 8);
           raw[18] = u8(pl.twcc);
@@ -502,7 +588,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         }
         lkf_raw_pkt rp{};
         rp.arrival_ns = pl.arrival;
-        rp.stream = streamBase[ti] + u32(g.nlayers == 1 ? 0 : pl.layer);
+        rp.stream = streamBase[ti] + u32((g.nlayers == 1 || g.svc) ? 0 : pl.layer);
         rp.off = d.arena_off;
         rp.len = u32(kPayloadOff) + pl.payload_len;
         tr->raws.push_back(rp);

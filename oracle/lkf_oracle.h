@@ -540,7 +540,14 @@ struct RtpHeader {
 // -----------------------------------------------------------------------------
 // buffer.ExtPacket — pkg/sfu/buffer/buffer.go:54-64
 // -----------------------------------------------------------------------------
-enum PayloadKind : u8 { PayloadNone = 0, PayloadVP8 = 1 };
+enum PayloadKind : u8 { PayloadNone = 0, PayloadVP8 = 1, PayloadVP9 = 2 };
+
+// codecs.VP9Packet (pion/rtp v1.8.3 codecs/vp9_packet.go): the flags the
+// VP9 selector reads (videolayerselector/vp9.go:44-108).  SID/TID arrive as
+// ExtPacket.VideoLayer (buffer.go:645-655).
+struct VP9Flags {
+  bool I = false, P = false, L = false, F = false, B = false, E = false, V = false, U = false;
+};
 
 struct ExtPacket {
   VideoLayer layer;  // ExtPacket.VideoLayer
@@ -552,6 +559,7 @@ struct ExtPacket {
   u8 PaddingSize = 0;
   PayloadKind kind = PayloadNone;
   VP8 vp8;  // valid when kind == PayloadVP8
+  VP9Flags vp9;  // valid when kind == PayloadVP9
   bool KeyFrame = false;
 };
 
@@ -1021,7 +1029,7 @@ struct VideoLayerSelectorResult {  // videolayerselector.go:8-15
   bool RTPMarker = false;
 };
 
-enum VLSKind : u8 { VLSNull = 0, VLSSimulcast = 1 };
+enum VLSKind : u8 { VLSNull = 0, VLSSimulcast = 1, VLSVP9 = 2 };
 
 struct VLS {
   VLSKind kind = VLSNull;
@@ -1054,9 +1062,59 @@ struct VLS {
     return {requestSpatial == currentLayer.Spatial, requestSpatial};
   }
 
-  // Select: Base/Null base.go (zero result) or Simulcast simulcast.go:42-122
+  // VP9.Select videolayerselector/vp9.go:43-109 (SVC: every layer in one
+  // stream; a packet is selected unless its layer is above the current one)
+  VideoLayerSelectorResult SelectVP9(const ExtPacket &p) {
+    VideoLayerSelectorResult r;
+    if (p.kind != PayloadVP9) return r;
+    const VP9Flags &v = p.vp9;
+    VideoLayer cur = currentLayer;
+    if (currentLayer != targetLayer) {
+      VideoLayer upd = currentLayer;
+      if (!currentLayer.IsValid()) {
+        if (!p.KeyFrame) return r;
+        upd = p.layer;
+      } else {
+        if (currentLayer.Temporal != targetLayer.Temporal) {
+          if (currentLayer.Temporal < targetLayer.Temporal) {
+            if (p.layer.Temporal > currentLayer.Temporal && p.layer.Temporal <= targetLayer.Temporal && v.U && v.B) {
+              cur.Temporal = p.layer.Temporal;
+              upd.Temporal = p.layer.Temporal;
+            }
+          } else if (v.E) {
+            upd.Temporal = targetLayer.Temporal;
+          }
+        }
+        if (currentLayer.Spatial != targetLayer.Spatial) {
+          if (currentLayer.Spatial < targetLayer.Spatial) {
+            if (p.layer.Spatial > currentLayer.Spatial && p.layer.Spatial <= targetLayer.Spatial && !v.P && v.B) {
+              cur.Spatial = p.layer.Spatial;
+              upd.Spatial = p.layer.Spatial;
+            }
+          } else if (v.E) {
+            upd.Spatial = targetLayer.Spatial;
+          }
+        }
+      }
+      if (upd != currentLayer) {
+        r.IsSwitching = true;
+        if (!currentLayer.IsValid() && upd.IsValid()) r.IsResuming = true;
+        previousLayer = currentLayer;
+        currentLayer = upd;
+      }
+    }
+    r.RTPMarker = p.Header.Marker;
+    if (v.E && p.layer.Spatial == cur.Spatial && (v.P || targetLayer.Spatial <= currentLayer.Spatial))
+      r.RTPMarker = true;
+    r.IsSelected = !p.layer.GreaterThan(cur);
+    r.IsRelevant = true;
+    return r;
+  }
+
+  // Select: Base/Null base.go (zero result), Simulcast simulcast.go:42-122, VP9 vp9.go:43-109
   VideoLayerSelectorResult Select(const ExtPacket &p, i32 layer) {
     VideoLayerSelectorResult r;
+    if (kind == VLSVP9) return SelectVP9(p);
     if (kind != VLSSimulcast) return r;
     if (currentLayer.Spatial != targetLayer.Spatial) {
       VideoLayer cur = currentLayer;
@@ -1199,6 +1257,8 @@ struct Forwarder {
       vls.tlsVP8 = true;
     } else if (m == MimeH264) {
       vls.kind = VLSSimulcast;
+    } else if (m == MimeVP9) {  // no dependency-descriptor extension negotiated: VP9 selector
+      vls.kind = VLSVP9;
     }
   }
   // GetState / SeedState forwarder.go:340-375

@@ -162,6 +162,17 @@ static ExtPacket toExt(const lkf_pkt &d, const u8 *arena) {
     v.KEYIDX = d.vp8_keyidx;
     v.HeaderSize = d.vp8_hdr_size;
     v.IsKeyFrame = p.KeyFrame;
+  } else if (d.flags & LKF_PKT_VP9) {
+    p.kind = PayloadVP9;
+    VP9Flags &v = p.vp9;
+    v.I = d.vp9_bits & LKF_VP9_I;
+    v.P = d.vp9_bits & LKF_VP9_P;
+    v.L = d.vp9_bits & LKF_VP9_L;
+    v.F = d.vp9_bits & LKF_VP9_F;
+    v.B = d.vp9_bits & LKF_VP9_B;
+    v.E = d.vp9_bits & LKF_VP9_E;
+    v.V = d.vp9_bits & LKF_VP9_V;
+    v.U = d.vp9_bits & LKF_VP9_U;
   }
   return p;
 }
@@ -247,7 +258,10 @@ int32_t orc_add_downtrack(orc_engine *e, const lkf_downtrack_params *p) {
   const lkf_track_params &tp = e->tracks[p->track].p;
   Kind k = tp.kind == LKF_KIND_VIDEO ? KindVideo : KindAudio;
   d->f = std::make_unique<Forwarder>(k);
-  Mime m = tp.codec == LKF_CODEC_VP8 ? MimeVP8 : tp.codec == LKF_CODEC_H264 ? MimeH264 : MimeOpus;
+  Mime m = tp.codec == LKF_CODEC_VP8    ? MimeVP8
+           : tp.codec == LKF_CODEC_H264 ? MimeH264
+           : tp.codec == LKF_CODEC_VP9  ? MimeVP9
+                                        : MimeOpus;
   d->f->DetermineCodec(m, tp.clock_rate);
   d->seq = std::make_unique<Sequencer>(int(e->seqSize), k == KindVideo, p->bind_time_ns / 1000000);
   ODT *dp = d.get();
@@ -256,6 +270,10 @@ int32_t orc_add_downtrack(orc_engine *e, const lkf_downtrack_params *p) {
     // StreamTrackerManager.GetReferenceLayerRTPTimestamp streamtrackermanager.go:660-679
     dp->f->getReferenceLayerRTPTimestamp = [e, track](u32 ts, i32 layer, i32 ref, u32 &out) -> Err {
       if (layer < 0 || layer >= 3 || ref < 0 || ref >= 3) return ErrRefLayerUnavailable;
+      if (e->tracks[track].p.codec == LKF_CODEC_VP9) {  // isSVC: one stream, one timeline (:667-671)
+        out = ts;
+        return OK;
+      }
       u32 off = e->tracks[track].p.layer_offsets[ref][layer];
       if (layer != ref && off == 0) return ErrRefLayerUnavailable;
       out = ts + off;

@@ -25,6 +25,7 @@ CASES = [
     ("config2_nocb", dict(config=2, duration_s=2.0, batch_s=0.1, rooms=1, has_callbacks=0)),
     ("config3_1room", dict(config=3, duration_s=2.0, batch_s=1.0, rooms=1)),
     ("config4_64subs", dict(config=4, duration_s=1.0, batch_s=0.5, rooms=1, participants=64)),
+    ("config5_4rooms", dict(config=5, duration_s=3.0, batch_s=0.5, rooms=4)),
 ]
 
 RECORD_FIELDS = ("ext_sn", "ext_ts", "out_off", "dt", "pkt", "out_len", "flags", "layer")

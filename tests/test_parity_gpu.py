@@ -127,6 +127,20 @@ def test_config4_small(pkg, workload, abi):
     run_parity(pkg, workload, abi, tr, check_state=False)
 
 
+def test_config5_vp9_svc(pkg, workload, abi):
+    """configs[4] shape: VP9 L3T3 SVC (VP9 selector, relevant drops, synthesized
+    markers) + Opus DTX, per-DT target changes every 1 s with deficient downgrades."""
+    tr = workload.Trace(5, duration_s=4.0, batch_s=0.5, rooms=12)
+    t = run_parity(pkg, workload, abi, tr)
+    assert t["forwarded"] > 0
+
+
+def test_config5_vp9_heavy_loss(pkg, workload, abi):
+    """VP9 SVC under 20% loss / 15% reorder: OOO and gap paths through the VP9 selector."""
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.25, rooms=4, loss=0.2, reorder=0.15, seed=55)
+    run_parity(pkg, workload, abi, tr)
+
+
 def test_empty_and_control_only_batches(pkg, workload, abi):
     """An empty batch and a control-only run are no-ops that still apply ops."""
     tr = workload.Trace(1, duration_s=1.0, batch_s=1.0)
