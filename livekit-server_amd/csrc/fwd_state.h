@@ -193,10 +193,12 @@ struct alignas(16) IngParsed {  // k_ing_parse -> k_ing_stream / k_ing_out (48 B
   uint8_t vfirst, vbits, vhs, tl0, tid, keyidx;
   uint16_t pid;
   uint32_t track;
-  uint8_t pad[16];
+  uint8_t vp9bits, sid;  // codecs.VP9Packet flags (LKF_VP9_*) and SID
+  uint8_t pad[14];
 };
 static_assert(sizeof(IngParsed) == 48, "IngParsed must be 48 B");
-enum : uint8_t { IP_OK = 1, IP_MARKER = 2, IP_LEVEL = 4, IP_VP8 = 8, IP_KF = 16, IP_VP8_BAD = 32 };
+// IP_VP8_BAD: the codec payload (VP8 or VP9) failed to unmarshal
+enum : uint8_t { IP_OK = 1, IP_MARKER = 2, IP_LEVEL = 4, IP_VP8 = 8, IP_KF = 16, IP_VP8_BAD = 32, IP_VP9 = 64 };
 
 struct DevEvent {  // one queued lkf_ctl op (48 B)
   uint32_t at;

@@ -170,6 +170,89 @@ __device__ __forceinline__ bool vp8_parse(const u8 *p, int len, IngParsed &q) {
   return true;
 }
 
+// codecs.VP9Packet.Unmarshal (pion/rtp v1.8.3 codecs/vp9_packet.go; not in
+// the reference tree: restated from the published descriptor layout, parity
+// unpinned) + buffer.IsVP9KeyFrame helpers.go:317-336.  Layer info, flexible
+// mode reference indices and scalability-structure data are walked for their
+// lengths; the selector reads I/P/L/F/B/E/V, TID/U/SID.
+__device__ __forceinline__ bool vp9_parse(const u8 *p, int len, IngParsed &q) {
+  if (len < 1) return false;
+  const u8 b0 = p[0];
+  const bool I = b0 & 0x80, P = b0 & 0x40, L = b0 & 0x20, F = b0 & 0x10, V = b0 & 0x02;
+  int pos = 1;
+  u8 tid = 0, sid = 0;
+  bool U = false;
+  if (I) {  // parsePictureID
+    if (len <= pos) return false;
+    if (p[pos] & 0x80) {
+      pos++;
+      if (len <= pos) return false;
+    }
+    pos++;
+  }
+  if (L) {  // parseLayerInfo
+    if (len <= pos) return false;
+    tid = p[pos] >> 5;
+    U = (p[pos] & 0x10) != 0;
+    sid = (p[pos] >> 1) & 0x7;
+    if (sid >= 5) return false;  // errTooManySpatialLayers (maxSpatialLayers 5)
+    pos++;
+    if (!F) {  // non-flexible mode: TL0PICIDX
+      if (len <= pos) return false;
+      pos++;
+    }
+  }
+  if (F && P) {  // parseRefIndices (maxVP9RefPics 3)
+    int nref = 0;
+    for (;;) {
+      if (len <= pos) return false;
+      nref++;
+      if ((p[pos] & 0x01) == 0) break;
+      if (nref >= 3) return false;
+      pos++;
+    }
+    pos++;
+  }
+  if (V) {  // parseSSData
+    if (len <= pos) return false;
+    const int ns = (p[pos] >> 5) + 1;
+    const bool Y = p[pos] & 0x10, G = p[pos] & 0x08;
+    pos++;
+    if (Y) {
+      if (len <= pos + ns * 4 - 1) return false;
+      pos += ns * 4;
+    }
+    int ng = 0;
+    if (G) {
+      if (len <= pos) return false;
+      ng = p[pos];
+      pos++;
+    }
+    for (int i = 0; i < ng; i++) {
+      if (len <= pos) return false;
+      const int r = (p[pos] >> 2) & 0x3;
+      pos++;
+      if (len <= pos + r - 1) return false;
+      pos += r;
+    }
+  }
+  q.vp9bits = u8((b0 & (LKF_VP9_I | LKF_VP9_P | LKF_VP9_L | LKF_VP9_F | LKF_VP9_B | LKF_VP9_E | LKF_VP9_V)) |
+                 (U ? LKF_VP9_U : 0));
+  q.sid = sid;
+  q.tid = tid;
+  // IsVP9KeyFrame: B, frame marker 10, profile -> show_existing_frame / frame_type
+  bool kf = false;
+  if ((b0 & 0x08) && len > pos) {
+    const u8 h = p[pos];
+    if ((h & 0xc0) == 0x80) {
+      const u8 profile = (h >> 4) & 0x3;
+      kf = profile != 3 ? (h & 0xC) == 0 : (h & 0x6) == 0;
+    }
+  }
+  if (kf) q.flags |= IP_KF;
+  return true;
+}
+
 __global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u8 *__restrict__ raw,
                             const DevStream *__restrict__ streams, u32 nstreams, IngParsed *__restrict__ out,
                             u32 *__restrict__ err) {
@@ -196,6 +279,11 @@ __global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u
     if (s.codec == LKF_CODEC_VP8 && q.payloadLen > 0) {
       if (vp8_parse(b + q.hdrSize, q.payloadLen, q))
         q.flags |= IP_VP8;
+      else
+        q.flags |= IP_VP8_BAD;
+    } else if (s.codec == LKF_CODEC_VP9 && q.payloadLen > 0) {  // getExtPacket buffer.go:643-656
+      if (vp9_parse(b + q.hdrSize, q.payloadLen, q))
+        q.flags |= IP_VP9;
       else
         q.flags |= IP_VP8_BAD;
     }
@@ -581,6 +669,13 @@ __global__ void k_ing_out(const lkf_raw_pkt *__restrict__ raws, const IngParsed 
     e.vp8_tid = p.tid;
     e.vp8_keyidx = p.keyidx;
   }
+  if (p.flags & IP_VP9) {  // VideoLayer{SID, TID}, Payload = VP9Packet (buffer.go:645-655)
+    e.flags |= LKF_PKT_VP9 | ((p.flags & IP_KF) ? LKF_PKT_KEYFRAME : 0);
+    e.spatial = int8_t(p.sid);
+    e.temporal = int8_t(p.tid);
+    e.vp9_bits = p.vp9bits;
+  }
+  if (e.spatial >= 0) e.layer = e.spatial;  // svc packet: forwardRTP dispatches pkt.Spatial (receiver.go:667-672)
   out[k] = e;
 }
 

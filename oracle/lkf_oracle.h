@@ -538,6 +538,104 @@ struct RtpHeader {
 };
 
 // -----------------------------------------------------------------------------
+// codecs.VP9Packet.Unmarshal — github.com/pion/rtp v1.8.3 codecs/vp9_packet.go
+// (third-party, absent from the reference tree: restated from its published
+// descriptor layout — parity unpinned) and buffer.IsVP9KeyFrame
+// helpers.go:317-336.
+// -----------------------------------------------------------------------------
+struct VP9Packet {
+  bool I = false, P = false, L = false, F = false, B = false, E = false, V = false, Z = false;
+  u16 PictureID = 0;
+  u8 TID = 0, SID = 0, TL0PICIDX = 0;
+  bool U = false, D = false;
+  std::vector<u8> PDiff;
+  size_t PayloadOff = 0;  // Payload = packet[PayloadOff:]
+
+  Err Unmarshal(const u8 *pk, size_t n) {
+    if (n < 1) return ErrShortPacket;
+    I = pk[0] & 0x80;
+    P = pk[0] & 0x40;
+    L = pk[0] & 0x20;
+    F = pk[0] & 0x10;
+    B = pk[0] & 0x08;
+    E = pk[0] & 0x04;
+    V = pk[0] & 0x02;
+    Z = pk[0] & 0x01;
+    size_t pos = 1;
+    if (I) {  // parsePictureID
+      if (n <= pos) return ErrShortPacket;
+      PictureID = u16(pk[pos] & 0x7F);
+      if (pk[pos] & 0x80) {
+        pos++;
+        if (n <= pos) return ErrShortPacket;
+        PictureID = u16((PictureID << 8) | pk[pos]);
+      }
+      pos++;
+    }
+    if (L) {  // parseLayerInfo: common, then non-flexible TL0PICIDX
+      if (n <= pos) return ErrShortPacket;
+      TID = pk[pos] >> 5;
+      U = pk[pos] & 0x10;
+      SID = (pk[pos] >> 1) & 0x7;
+      D = pk[pos] & 0x01;
+      if (SID >= 5) return ErrShortPacket;  // errTooManySpatialLayers
+      pos++;
+      if (!F) {
+        if (n <= pos) return ErrShortPacket;
+        TL0PICIDX = pk[pos];
+        pos++;
+      }
+    }
+    if (F && P) {  // parseRefIndices
+      for (;;) {
+        if (n <= pos) return ErrShortPacket;
+        PDiff.push_back(pk[pos] >> 1);
+        if ((pk[pos] & 0x01) == 0) break;
+        if (PDiff.size() >= 3) return ErrShortPacket;  // errTooManyPDiff
+        pos++;
+      }
+      pos++;
+    }
+    if (V) {  // parseSSData
+      if (n <= pos) return ErrShortPacket;
+      const size_t ns = size_t(pk[pos] >> 5) + 1;
+      const bool Y = pk[pos] & 0x10, G = pk[pos] & 0x08;
+      pos++;
+      if (Y) {
+        if (n <= pos + ns * 4 - 1) return ErrShortPacket;
+        pos += ns * 4;
+      }
+      size_t ng = 0;
+      if (G) {
+        if (n <= pos) return ErrShortPacket;
+        ng = pk[pos];
+        pos++;
+      }
+      for (size_t i = 0; i < ng; i++) {
+        if (n <= pos) return ErrShortPacket;
+        const size_t r = (pk[pos] >> 2) & 0x3;
+        pos++;
+        if (n <= pos + r - 1) return ErrShortPacket;
+        pos += r;
+      }
+    }
+    PayloadOff = pos;
+    return OK;
+  }
+  // IsVP9KeyFrame helpers.go:317-336 (re-parses the same payload)
+  static bool IsKeyFrame(const u8 *pk, size_t n) {
+    VP9Packet v;
+    if (v.Unmarshal(pk, n) != OK || n - v.PayloadOff < 1) return false;
+    if (!v.B) return false;
+    const u8 h = pk[v.PayloadOff];
+    if ((h & 0xc0) != 0x80) return false;
+    const u8 profile = (h >> 4) & 0x3;
+    if (profile != 3) return (h & 0xC) == 0;
+    return (h & 0x6) == 0;
+  }
+};
+
+// -----------------------------------------------------------------------------
 // buffer.ExtPacket — pkg/sfu/buffer/buffer.go:54-64
 // -----------------------------------------------------------------------------
 enum PayloadKind : u8 { PayloadNone = 0, PayloadVP8 = 1, PayloadVP9 = 2 };

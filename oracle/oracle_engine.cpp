@@ -598,8 +598,22 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
       ep.vp8_tl0picidx = v.TL0PICIDX;
       ep.vp8_tid = v.TID;
       ep.vp8_keyidx = v.KEYIDX;
+    } else if (b.codec == LKF_CODEC_VP9) {  // buffer.go:643-656 (no dependency descriptor)
+      VP9Packet v;
+      if (v.Unmarshal(buf + h.hdrSize, h.payloadLen) != OK) {  // "could not unmarshal VP9 packet"
+        f.flags |= LKF_FLOW_BAD;
+        return f;
+      }
+      const bool kf = VP9Packet::IsKeyFrame(buf + h.hdrSize, h.payloadLen);
+      ep.flags |= LKF_PKT_VP9 | (kf ? LKF_PKT_KEYFRAME : 0);
+      ep.spatial = int8_t(v.SID);
+      ep.temporal = int8_t(v.TID);
+      ep.vp9_bits = u8((v.I ? LKF_VP9_I : 0) | (v.P ? LKF_VP9_P : 0) | (v.L ? LKF_VP9_L : 0) |
+                       (v.F ? LKF_VP9_F : 0) | (v.B ? LKF_VP9_B : 0) | (v.E ? LKF_VP9_E : 0) |
+                       (v.V ? LKF_VP9_V : 0) | (v.U ? LKF_VP9_U : 0));
     }
   }
+  if (ep.spatial >= 0) ep.layer = ep.spatial;  // svc: forwardRTP dispatches pkt.Spatial (receiver.go:667-672)
   fwd = true;
   f.flags |= LKF_FLOW_FORWARD;
   (void)e;

@@ -28,6 +28,7 @@ def _ingested(o, abi, h):
     dict(config=1, duration_s=2.0),
     dict(config=2, duration_s=2.0, rooms=2, loss=0.0, reorder=0.0),
     dict(config=3, duration_s=2.0, rooms=1),
+    dict(config=5, duration_s=2.0, rooms=3, loss=0.0, reorder=0.0),  # VP9 descriptor parse, SVC layer dispatch
 ])
 def test_oracle_ingest_reproduces_extpackets(kw, pkg, workload, abi):
     o = load_oracle()
