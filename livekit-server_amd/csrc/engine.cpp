@@ -51,6 +51,7 @@ struct BatchCtx {
   uint32_t *dFwdCnt = nullptr;
   uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
   uint32_t *dGFirst = nullptr;  // emit group g -> output position owning record 64g
+  uint32_t *dLayerList = nullptr, *dLayerBefore = nullptr, *dLayerCnt = nullptr;  // k_layer_index
   lkf_out *dOut = nullptr;
   uint8_t *dOutArena = nullptr;
   uint64_t *dStats = nullptr;
@@ -330,6 +331,9 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dRecBase, c.max_downtracks));
     A(dalloc(&x.dByteBase, c.max_downtracks));
     A(dalloc(&x.dGFirst, c.max_out_pkts / 64 + 2));
+    A(dalloc(&x.dLayerList, 3 * size_t(c.max_batch_pkts) + 64));
+    A(dalloc(&x.dLayerBefore, 3 * size_t(c.max_batch_pkts) + 64));
+    A(dalloc(&x.dLayerCnt, 3 * size_t(c.max_tracks)));
     A(dalloc(&x.dOut, c.max_out_pkts));
     A(dalloc(&x.dOutArena, c.max_out_bytes + 64));
     A(dalloc(&x.dStats, kStatsWords));
@@ -407,7 +411,7 @@ void lkf_destroy(lkf_engine *e) {
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
-                 x.dRawPkts, x.dGFirst};
+                 x.dRawPkts, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt};
     for (void *p : q)
       if (p) (void)hipFree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
@@ -762,7 +766,14 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(launch_scan(s, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
                      x.dTot + 0, nullptr, nullptr),
          "slot scan");
+  HIPCHK(launch_layer_index(s, e->curPkts, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
+                            x.dLayerBefore, x.dLayerCnt),
+         "layer index");
   DecideLaunch d;
+  d.layerList = x.dLayerList;
+  d.layerBefore = x.dLayerBefore;
+  d.layerCnt = x.dLayerCnt;
+  d.pktStride = e->cfg.max_batch_pkts;
   d.sched = e->dSched;
   d.waveTrack = e->dWaveTrack;
   d.nlanes = nl;

@@ -1297,6 +1297,8 @@ struct DecideArgs {
   u32 *fwdCnt;
   u64 *fwdBytes;
   u64 *stats;  // lkf_stats as u64[15]
+  const u32 *layerList, *layerBefore, *layerCnt;  // k_layer_index
+  u32 pktStride;
 };
 
 // One wave per (track, <=64 DownTracks): the packet loop is wave-uniform, so
@@ -1498,9 +1500,6 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 #ifndef LKF_DECIDE_WAVES
 #define LKF_DECIDE_WAVES 0  // >0: amdgpu_waves_per_eu floor for k_decide_dt (occupancy experiments)
 #endif
-#ifndef LKF_PREFETCH
-#define LKF_PREFETCH 1  // load the next 64 packet descriptors while deciding the current ones
-#endif
 #if LKF_DECIDE_WAVES
 #define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(LKF_DECIDE_WAVES, 8)))
 #else
@@ -1529,6 +1528,51 @@ __device__ __forceinline__ void vm_drain() {
 __device__ __forceinline__ void pin_loaded(const uint4 &a, const uint4 &b, const uint4 &c, const uint4 &d) {
   asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
                "v"(c.y), "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
+}
+
+#ifndef LKF_LAYER_SKIP
+#define LKF_LAYER_SKIP 1  // 0: every chunk is the next 64 packets of the track (A/B)
+#endif
+__device__ __forceinline__ bool steady_state(const Lane &L) {
+  const u32 fl = L.h.flags;
+  return LKF_LAYER_SKIP && (fl & F_VIDEO) && (fl & F_SIMULCAST) && !(fl & (F_MUTED | F_PUBMUTED)) &&
+         L.h.tgtS != INVALID && L.h.tgtT != INVALID && L.h.curS == L.h.tgtS && L.h.curS <= L.h.maxS &&
+         L.h.curS >= 0 && L.h.curS < 3;
+}
+
+// Per-track layer lists for the steady-state chunks of k_decide_dt: one wave
+// per track; for each simulcast layer l, list[l][tBegin + j] = the j-th packet
+// of layer l and before[l][i] = the number of layer-l packets of the track
+// before packet i.
+__global__ void __launch_bounds__(64) k_layer_index(const lkf_pkt *__restrict__ pkts, const u32 *__restrict__ tBegin,
+                                                    const u32 *__restrict__ tEnd, u32 stride, u32 *__restrict__ list,
+                                                    u32 *__restrict__ before, u32 *__restrict__ cnt) {
+  const u32 t = blockIdx.x, lane = threadIdx.x;
+  const u64 lt = (1ull << lane) - 1;
+  const u32 b = tBegin[t], e = tEnd[t];
+  u32 c0 = 0, c1 = 0, c2 = 0;
+  for (u32 base = b; base < e; base += 64) {
+    const u32 i = base + lane;
+    const int l = i < e ? int(reinterpret_cast<const int8_t *>(pkts + i)[53]) : -1;  // lkf_pkt.layer
+    const u64 m0 = __ballot(l == 0), m1 = __ballot(l == 1), m2 = __ballot(l == 2);
+    if (i < e) {
+      const u32 r0 = c0 + u32(__popcll(m0 & lt)), r1 = c1 + u32(__popcll(m1 & lt)), r2 = c2 + u32(__popcll(m2 & lt));
+      before[i] = r0;
+      before[stride + i] = r1;
+      before[2 * size_t(stride) + i] = r2;
+      if (l == 0) list[b + r0] = i;
+      if (l == 1) list[stride + b + r1] = i;
+      if (l == 2) list[2 * size_t(stride) + b + r2] = i;
+    }
+    c0 += u32(__popcll(m0));
+    c1 += u32(__popcll(m1));
+    c2 += u32(__popcll(m2));
+  }
+  if (lane == 0) {
+    cnt[t * 3] = c0;
+    cnt[t * 3 + 1] = c1;
+    cnt[t * 3 + 2] = c2;
+  }
 }
 
 __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
@@ -1604,62 +1648,67 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   dg[15] = pe - pb;
 #endif
 
-#if LKF_PREFETCH
-  uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0, f2 = f0, f3 = f0;
-  if (pb + lane < pe) {
-    const u64 q = u64(pb + lane) * 4;
-    f0 = src[q];
-    f1 = src[q + 1];
-    f2 = src[q + 2];
-    f3 = src[q + 3];
-  }
-#endif
-  for (u32 k = pb; k < pe; k += 64) {
-    const u32 n = min(64u, pe - k);
+  u32 kpos = pb;  // first packet of the track not yet decided
+  while (kpos < pe) {
+    if (nextAt <= kpos) {
+      while (nextAt <= kpos) {
+        apply_ctl(L, A.events[ev++]);
+        nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
+      }
+      vm_drain();
+    }
+    // Steady state: a simulcast DownTrack on its target layer with no switch
+    // possible drops every packet of another layer as NOT_SELECTED with no
+    // state change (simulcast.go:42-122: curS == tgtS <= maxS, forwarder.go
+    // :1440/:1687 not taken).  Its chunk is then the next 64 packets of its
+    // own layer (per-track layer lists); the skipped packets are counted.
+    const bool steady = steady_state(L);
+    u32 pi, n, lim;  // lane -> packet index; packets in the chunk; packet index after it
+    if (steady) {
+      const u32 ls = u32(L.h.curS);
+      const u32 j = A.layerBefore[size_t(ls) * A.pktStride + kpos] + lane;
+      pi = j < A.layerCnt[track * 3 + ls] ? A.layerList[size_t(ls) * A.pktStride + pb + j] : 0xffffffffu;
+      const u32 stopAt = min(nextAt, pe);
+      n = u32(__popcll(__ballot(pi < stopAt)));  // list is increasing: a prefix of the lanes
+      lim = n == 64 ? rl32(pi, 63) + 1 : stopAt;
+    } else {
+      n = min(64u, pe - kpos);
+      pi = kpos + lane;
+      lim = kpos + n;
+    }
     const bool valid = lane < n;
     DIAG(1, 1);
 #if LKF_DIAG
     u64 tc0 = clock64();
 #endif
-#if LKF_PREFETCH
-    const uint4 r0 = f0, r1 = f1, r2 = f2, r3 = f3;
-    pin_loaded(r0, r1, r2, r3);
-    if (k + 64 + lane < pe) {  // next chunk in flight while this one is decided
-      const u64 q = u64(k + 64 + lane) * 4;
-      f0 = src[q];
-      f1 = src[q + 1];
-      f2 = src[q + 2];
-      f3 = src[q + 3];
-    }
-#else
     uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
     if (valid) {
-      const u64 q = u64(k + lane) * 4;
+      const u64 q = u64(pi) * 4;
       r0 = src[q];
       r1 = src[q + 1];
       r2 = src[q + 2];
       r3 = src[q + 3];
     }
     pin_loaded(r0, r1, r2, r3);
-#endif
     const PktV p = decode_pkt(r0, r1, r2, r3);
 #if LKF_DIAG
     dg[11] += u64(__builtin_amdgcn_readfirstlane(u32(r0.x)) + 1u > 0u) * (clock64() - tc0);
 #endif
     u32 pos = 0;
+    u32 own = n;  // packets of the chunk decided (steady: the rest of the range is skipped drops)
     while (pos < n) {
 #if LKF_DIAG
       u64 tr0 = clock64();
       u64 tmark = tr0;
 #endif
-      if (nextAt <= k + pos) {
-        while (nextAt <= k + pos) {
+      if (nextAt <= rl32(pi, pos)) {
+        while (nextAt <= rl32(pi, pos)) {
           apply_ctl(L, A.events[ev++]);
           nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
         }
         vm_drain();
       }
-      const bool inWin = valid && lane >= pos && (k + lane) < nextAt;
+      const bool inWin = valid && lane >= pos && pi < nextAt;
       // ---- classification against the state at the start of the run
       const u32 fl = L.h.flags;
       const bool video = fl & F_VIDEO;
@@ -1831,7 +1880,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           Tuple t;
           t.extSN = osn;
           t.extTS = ots;
-          t.pkt = k + lane;
+          t.pkt = pi;
           t.relOff = o.relOff + relEx;
           t.outLen = u16(outLen);
           t.flags = u8(((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
@@ -1941,21 +1990,33 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       dg[12] += ts0 - tr0;
       dg[6] += ts0 - tb0;
 #endif
-      if (x < n && (k + x) < nextAt && rl32(u32(gapLater), x) == 0) {
+      if (x < n && rl32(pi, x) < nextAt && rl32(u32(gapLater), x) == 0) {
         DIAG(3, 1);
         // the packet at lane x needs the full restatement
         const uint4 a0 = make_uint4(rl32(r0.x, x), rl32(r0.y, x), rl32(r0.z, x), rl32(r0.w, x));
         const uint4 a1 = make_uint4(rl32(r1.x, x), rl32(r1.y, x), rl32(r1.z, x), rl32(r1.w, x));
         const uint4 a2 = make_uint4(rl32(r2.x, x), rl32(r2.y, x), rl32(r2.z, x), rl32(r2.w, x));
         const uint4 a3 = make_uint4(rl32(r3.x, x), rl32(r3.y, x), rl32(r3.z, x), rl32(r3.w, x));
-        decide_step(L, decode_pkt(a0, a1, a2, a3), k + x, o);
+        const u32 px = rl32(pi, x);
+        decide_step(L, decode_pkt(a0, a1, a2, a3), px, o);
         vm_drain();
         pos = x + 1;
+        if (steady && !steady_state(L)) {  // left the steady state: the chunk ends after this packet
+          own = x + 1;
+          lim = px + 1;
+          break;
+        }
       }
 #if LKF_DIAG
       dg[13] += clock64() - ts0;
 #endif
     }
+    if (steady) {  // the other layers' packets in [kpos, lim): NOT_SELECTED drops
+      const u32 skipped = (lim - kpos) - own;
+      o.nTuples += skipped;
+      o.drops[LKF_DROP_NOT_SELECTED] += skipped;
+    }
+    kpos = lim;
   }
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
 #if LKF_DIAG
@@ -2408,9 +2469,20 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.events = a.events;
   A.evOff = a.evOff;
   A.fwdCnt = a.fwdCnt;
+  A.layerList = a.layerList;
+  A.layerBefore = a.layerBefore;
+  A.layerCnt = a.layerCnt;
+  A.pktStride = a.pktStride;
   A.fwdBytes = a.fwdBytes;
   A.stats = a.stats;
   hipLaunchKernelGGL(k_decide_dt, dim3(a.nlanes), dim3(64), 0, s, A, a.pkts);
+  return hipGetLastError();
+}
+
+hipError_t launch_layer_index(hipStream_t s, const lkf_pkt *pkts, const u32 *tBegin, const u32 *tEnd, u32 ntracks,
+                              u32 stride, u32 *list, u32 *before, u32 *cnt) {
+  if (!ntracks) return hipSuccess;
+  hipLaunchKernelGGL(k_layer_index, dim3(ntracks), dim3(64), 0, s, pkts, tBegin, tEnd, stride, list, before, cnt);
   return hipGetLastError();
 }
 

@@ -30,6 +30,8 @@ struct DecideLaunch {
   uint32_t *fwdCnt;
   uint64_t *fwdBytes;
   uint64_t *stats;
+  const uint32_t *layerList, *layerBefore, *layerCnt;  // launch_layer_index outputs
+  uint32_t pktStride;                                  // max_batch_pkts
 };
 
 struct EmitLaunch {
@@ -89,6 +91,8 @@ struct SpeakersLaunch {
 hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a);
 hipError_t launch_speakers(hipStream_t s, const SpeakersLaunch &a);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
+hipError_t launch_layer_index(hipStream_t s, const lkf_pkt *pkts, const uint32_t *tBegin, const uint32_t *tEnd,
+                              uint32_t ntracks, uint32_t stride, uint32_t *list, uint32_t *before, uint32_t *cnt);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
 // pulls two pinned host buffers (device-visible) into device memory with one
 // kernel (sizes multiples of 4 B); replaces two hipMemcpyAsync calls per run
