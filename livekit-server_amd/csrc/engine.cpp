@@ -336,7 +336,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dLayerCnt, 3 * size_t(c.max_tracks)));
     A(dalloc(&x.dOut, c.max_out_pkts));
     A(dalloc(&x.dOutArena, c.max_out_bytes + 64));
-    A(dalloc(&x.dStats, kStatsWords));
+    A(dalloc(&x.dStats, size_t(kStatsWords) * (1 + kStatCopies)));
     A(dalloc(&x.dPktsOwn, c.max_batch_pkts));
     A(dalloc(&x.dArenaOwn, c.max_batch_arena + 64));
     A(dalloc(&x.dRawPkts, c.max_batch_pkts));
@@ -368,7 +368,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     for (auto &x : e->ctx) {
       A(hipMemset(x.dArenaOwn, 0, c.max_batch_arena + 64));
       A(hipMemset(x.dTot, 0, 4 * sizeof(uint64_t)));
-      A(hipMemset(x.dStats, 0, kStatsWords * sizeof(uint64_t)));
+      A(hipMemset(x.dStats, 0, size_t(kStatsWords) * (1 + kStatCopies) * sizeof(uint64_t)));
       A(hipMemset(x.dErr, 0, 4 * sizeof(uint32_t)));
     }
   }
@@ -758,7 +758,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
   if (!e->ingestStarted) HIPCHK(hipEventRecord(rg[0], s), "event");  // else: recorded ahead of the ingest
   e->ingestStarted = false;
-  HIPCHK(launch_batch_init(s, nt, nd, kStatsWords, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dStats, x.dFwdCnt,
+  HIPCHK(launch_batch_init(s, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dStats, x.dFwdCnt,
                            x.dFwdBytes),
          "batch init");
   HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, e->curNDev, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
@@ -798,6 +798,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.stats = x.dStats;
   HIPCHK(hipEventRecord(rg[1], s), "event");
   HIPCHK(launch_decide(s, d), "decide");
+  HIPCHK(launch_stats_reduce(s, x.dStats), "stats reduce");
   HIPCHK(hipEventRecord(rg[2], s), "event");
   HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
                      x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm, x.dGFirst, e->cfg.max_out_pkts),

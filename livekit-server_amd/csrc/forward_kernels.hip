@@ -2039,12 +2039,16 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   if (lane == 0) {
     A.fwdCnt[d] = u32(o.nFwd);
     A.fwdBytes[d] = o.relOff;
-    if (o.nTuples) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)o.nTuples);
-    if (o.nFwd) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)o.nFwd);
-    if (o.nBytes) atomicAdd((unsigned long long *)&A.stats[2], (unsigned long long)o.nBytes);
+    // counters: one of kStatCopies partial copies per wave (same-address
+    // atomics from every wave would serialise in one L2 channel); k_stats_reduce
+    // folds the copies after the kernel
+    u64 *st = A.stats + size_t(1 + (w % kStatCopies)) * kStatWords;
+    if (o.nTuples) atomicAdd((unsigned long long *)&st[0], (unsigned long long)o.nTuples);
+    if (o.nFwd) atomicAdd((unsigned long long *)&st[1], (unsigned long long)o.nFwd);
+    if (o.nBytes) atomicAdd((unsigned long long *)&st[2], (unsigned long long)o.nBytes);
 #pragma unroll
     for (int i = 0; i < LKF_DROP_NREASONS; i++)
-      if (o.drops[i]) atomicAdd((unsigned long long *)&A.stats[4 + i], (unsigned long long)o.drops[i]);
+      if (o.drops[i]) atomicAdd((unsigned long long *)&st[4 + i], (unsigned long long)o.drops[i]);
   }
 }
 
@@ -2381,6 +2385,21 @@ __global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u32 d, c
 }
 
 // per-batch counters -> cumulative (stats[3] := arena bytes from the out scan)
+// stats[0..kStatWords) = sum of the kStatCopies partial copies that follow it
+__global__ void __launch_bounds__(256) k_stats_reduce(u64 *stats) {
+  const u32 i = threadIdx.x;
+  if (i < u32(kStatWords)) {
+    u64 v = 0;
+    for (int c = 0; c < kStatCopies; c++) v += stats[size_t(1 + c) * kStatWords + i];
+    stats[i] = v;
+  }
+}
+
+hipError_t launch_stats_reduce(hipStream_t s, u64 *stats) {
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats);
+  return hipGetLastError();
+}
+
 __global__ void k_accumulate(const u64 *stats, const u64 *tot, u64 *cum) {
   const int i = threadIdx.x;
   if (i < 4 + LKF_DROP_NREASONS) cum[i] += (i == 3) ? tot[3] : stats[i];

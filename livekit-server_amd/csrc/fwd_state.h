@@ -81,6 +81,11 @@ struct alignas(16) DTHot {
 };
 static_assert(sizeof(DTHot) == 256, "DTHot must be 256 B");
 
+// per-batch counters (lkf_stats as u64 words) and the partial copies the
+// decide waves add into (stats buffer = (1 + kStatCopies) * kStatWords)
+constexpr int kStatWords = 4 + LKF_DROP_NREASONS;
+constexpr int kStatCopies = 64;
+
 // Static per-DownTrack parameters (Bind-time: downtrack.go:362-432), 16 B.
 struct DevDT {
   uint32_t track;
