@@ -991,13 +991,35 @@ __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
   return -1;
 }
 
+
+// Records go to HBM as whole, aligned dwordx4 stores (the byte-field struct
+// copy compiles to sub-dword and misaligned stores, which the memory pipeline
+// splits into many transactions and which every later vmcnt wait then drains).
+__device__ __forceinline__ u32 pack4(u8 a, u8 b, u8 c, u8 d) {
+  return u32(a) | (u32(b) << 8) | (u32(c) << 16) | (u32(d) << 24);
+}
+__device__ __forceinline__ void store_rec(Tuple *dst, const Tuple &t) {  // 3 x dwordx4 (pad = 0)
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+  d[0] = make_uint4(u32(t.extSN), u32(t.extSN >> 32), u32(t.extTS), u32(t.extTS >> 32));
+  d[1] = make_uint4(t.pkt, t.relOff, u32(t.outLen) | (u32(t.flags) << 16) | (u32(u8(t.layer)) << 24),
+                    pack4(t.codecLen, t.codec[0], t.codec[1], t.codec[2]));
+  d[2] = make_uint4(pack4(t.codec[3], t.codec[4], t.codec[5], t.hdrLen), 0u, 0u, 0u);
+}
+__device__ __forceinline__ void store_rec(SeqMeta *dst, const SeqMeta &m) {  // 2 x dwordx4 (pad = 0)
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+  d[0] = make_uint4(u32(m.sourceSeqNo) | (u32(m.targetSeqNo) << 16), m.timestamp, m.lastNack,
+                    pack4(m.marker, m.nacked, u8(m.layer), m.codecLen));
+  d[1] = make_uint4(pack4(m.codec[0], m.codec[1], m.codec[2], m.codec[3]),
+                    pack4(m.codec[4], m.codec[5], m.codec[6], m.codec[7]), 0u, 0u);
+}
+
 // invalidateSlot (sequencer.go:351-366) of the n slots after the highest slot
 __device__ __forceinline__ void seq_invalidate(Lane &L, u32 n) {
   const SeqMeta z = {};
   for (u32 i = lane_id(); i < n; i += 64) {
     u32 x = u32(L.h.seqHighSlot) + 1 + i;
     while (x >= L.seqSize) x -= L.seqSize;
-    L.seq[x] = z;
+    store_rec(L.seq + x, z);
   }
 }
 // sequencer.push sequencer.go:123-209 (no padding exclusions on this path: the
@@ -1018,7 +1040,7 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     m.codecLen = u8(cbLen);
 #pragma unroll
     for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
-    L.seq[slot] = m;
+    if (lane_id() == 0) store_rec(L.seq + slot, m);  // wave-uniform record: one lane stores it
     L.h.seqExtHighestSN = esn;
     L.h.seqHighSlot = u16(slot);
     if (ets > L.h.seqExtHighestTS) L.h.seqExtHighestTS = ets;
@@ -1446,7 +1468,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   t.hdrLen = u8(hdrLen);
   for (int i = 0; i < 12; i++) t.pad[i] = 0;
 #if LKF_ABLATE != 1  // diagnostic builds only (never shipped): 1 = no tuple/sequencer writes
-  o.outT[o.nFwd] = t;
+  if (lane_id() == 0) store_rec(o.outT + o.nFwd, t);  // wave-uniform record: one lane stores it
   // sequencer.push (downtrack.go:724-735)
   seq_push(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
 #endif
@@ -1745,7 +1767,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #endif
       const bool cand = inWin && cls == -1;
       const u64 candM = __ballot(cand);
-      DIAG_MARK(4);
       const int pc = prev_in(candM, lt);
       const int pcs = pc >= 0 ? pc : int(lane);  // cross-lane reads run on every lane
       const u64 pcEsn = sh64(p.esn, pcs);
@@ -1761,7 +1782,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       // a gap behind other candidates ends this run and starts the next one
       const bool gapLater = cand && pc >= 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
                             p.ssrc == L.h.lastSSRC;
-      DIAG_MARK(8);
+      // (diag: run-body split below)
       // VP8 picture id (VP8PictureIdWrapHandler.Unwrap vp8.go:400-483 without a wrap)
       const bool M = p.vbits & LKF_VP8_M, I = p.vbits & LKF_VP8_I, T = p.vbits & LKF_VP8_T;
       const i32 np = M ? i32(p.pid & 0x7fff) : i32(p.pid & 0x7f);
@@ -1795,7 +1816,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           dropT = dropT && !set_has(L.exKey, L.h.exHead, L.h.exCount, ext);
         ok = ok && !wrapBack && !wraps && !tsw && (!dropT || L.h.snOffset == L.h.rmOpenValue);
       }
-      DIAG_MARK(9);
+      // (diag: run-body split below)
       const u64 tdM = __ballot(ok && dropT);
       const u64 snOff = L.h.snOffset + u64(__popcll(tdM & lt));
       const u64 osn = p.esn - snOff;
@@ -1816,7 +1837,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         cbLen = vp8_marshal(p.vfirst, I, mM, mpid, p.vbits & LKF_VP8_L, mtl0, T, p.tid, p.vbits & LKF_VP8_Y,
                             p.vbits & LKF_VP8_K, mkey, hs, cb);
       }
-      DIAG_MARK(10);
+      // (diag: run-body split below)
       const u64 fwC = __ballot(fwd);
       const int pf = prev_in(fwC, lt);
       const u64 pfOsn = sh64(osn, pf >= 0 ? pf : int(lane));
@@ -1836,6 +1857,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #if LKF_DIAG
       const u64 tb0 = clock64();
       dg[5] += tb0 - tr0;
+      tmark = tb0;
 #endif
       if (x > pos) {
         const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
@@ -1845,8 +1867,11 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const u64 fwR = __ballot(fwd);
         const u64 selR = tdR | fwR;
         o.nTuples += x - pos;
-#pragma unroll
-        for (int r = 0; r < LKF_DROP_NREASONS; r++) o.drops[r] += u32(__popcll(__ballot(inRun && cls == r)));
+        // the run's drops: the classification's no-state-change reasons + temporal filter
+        o.drops[LKF_DROP_MUTED] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_MUTED)));
+        o.drops[LKF_DROP_PAUSED] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_PAUSED)));
+        o.drops[LKF_DROP_NOT_SELECTED] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_NOT_SELECTED)));
+        o.drops[LKF_DROP_DOWNGRADE] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_DOWNGRADE)));
         o.drops[LKF_DROP_TEMPORAL] += u32(__popcll(tdR));
         // first push of the run: slot distance from the sequencer's highest
         u32 gOff = 1;
@@ -1859,10 +1884,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
               vp8_record_missing(L, L.h.wrMaxPictureId, gapExt, L.h.pictureIdOffset);
               if (gapExempt) set_add(L.exKey, L.h.exHead, L.h.exCount, gapExt, kExemptKeep);
             }
-            if (gOff > 1) seq_invalidate(L, gOff - 1);
-            vm_drain();
+            if (gOff > 1) seq_invalidate(L, gOff - 1);  // stores only: no drain needed
           }
         }
+        DIAG_MARK(8);
         // output records + sequencer slots of the forwarded lanes
         const int cc = p.hdr0 & 0xf;
         const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
@@ -1893,7 +1918,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #pragma unroll
           for (int i = 0; i < 12; i++) t.pad[i] = 0;
 #if LKF_ABLATE != 1
-          o.outT[o.nFwd + j] = t;
+          store_rec(o.outT + o.nFwd + j, t);
 #endif
           // sequencer.push in-order branch (sequencer.go:123-209): next slot
           u32 slot = u32(L.h.seqHighSlot) + gOff + j;
@@ -1909,9 +1934,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #pragma unroll
           for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
 #if LKF_ABLATE != 1
-          L.seq[slot] = m;
+          store_rec(L.seq + slot, m);
 #endif
         }
+        DIAG_MARK(9);
         const u32 sumLen = wave_sum_u32(outLen);
         // ---- advance the DownTrack state past the run (uniform)
         if (fwR) {
@@ -1983,6 +2009,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           }
         }
         if (fwR) o.relOff += rl32(relEx + aligned, 63 - __clzll(fwR));
+        DIAG_MARK(10);
       }
       pos = x;
 #if LKF_DIAG
@@ -1999,7 +2026,13 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const uint4 a3 = make_uint4(rl32(r3.x, x), rl32(r3.y, x), rl32(r3.z, x), rl32(r3.w, x));
         const u32 px = rl32(pi, x);
         decide_step(L, decode_pkt(a0, a1, a2, a3), px, o);
+#if LKF_DIAG
+        const u64 tdr0 = clock64();
+#endif
         vm_drain();
+#if LKF_DIAG
+        dg[4] += clock64() - tdr0;  // (diag slot 4: the drain after the full step)
+#endif
         pos = x + 1;
         if (steady && !steady_state(L)) {  // left the steady state: the chunk ends after this packet
           own = x + 1;

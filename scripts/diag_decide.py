@@ -10,8 +10,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-NAMES = ["waves", "chunks", "runs", "serial", "c_cls", "cyc_classify", "cyc_runbody", "cyc_prologue",
-         "c_esn", "c_vp8", "c_marshal", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
+NAMES = ["waves", "chunks", "runs", "serial", "serial_drain", "cyc_classify", "cyc_runbody", "cyc_prologue",
+         "rb_drops_gap", "rb_stores", "rb_advance", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
 
 
 def main():
