@@ -165,9 +165,17 @@ __device__ __forceinline__ void wave_lds_sync() { __syncthreads(); }
 // ---------------------------------------------------------------------------
 // Lane context: hot state in registers + cold-state pointers.
 // ---------------------------------------------------------------------------
+#ifndef LKF_STATE_LDS
+#define LKF_STATE_LDS 1  // DownTrack hot state in LDS (one copy per wave) instead of registers
+#endif
 struct Lane {
+#if LKF_STATE_LDS
+  DTHot &h;  // the wave's DownTrack state, staged in LDS (no SGPR pressure / spill traffic)
+#else
   DTHot h;
-  RangeEntry *rm;
+#endif
+  RangeEntry *rm;  // the closed-range ring, staged in LDS for the batch
+  bool rmDirty;    // a closed range was written (write the ring back)
   VP8Cold *vc;
   i32 *dropKey;  // LDS copy of vc->dropKey
   i32 *exKey;    // LDS copy of vc->exKey
@@ -224,6 +232,7 @@ __device__ bool rm_exclude(Lane &L, u64 s, u64 e) {
     L.rm[L.h.rmHead] = c;
     L.h.rmHead = u16((L.h.rmHead + 1) % kRangeCap);
   }
+  L.rmDirty = true;
   L.h.rmOpenStart = e;
   L.h.rmOpenValue = nv;
   return true;
@@ -810,6 +819,7 @@ __device__ bool fw_sourceSwitch(Lane &L, const PktV &p, i32 layer) {
 // getTranslationParamsCommon :1650-1671 -> drop reason or -1 (forward)
 __device__ __forceinline__ int fw_common(Lane &L, const PktV &p, i32 layer, bool marker, int &ord, u64 &osn,
                                          u64 &ots) {
+  DIAG_SCOPE(9);
   if (L.h.lastSSRC != p.ssrc) {
     if (!fw_sourceSwitch(L, p, layer)) return LKF_DROP_SWITCH;
     L.h.lastSSRC = p.ssrc;
@@ -838,6 +848,7 @@ struct Fwd {
 
 // Forwarder.GetTranslationParams forwarder.go:1436-1765 for one (packet, DownTrack).
 __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
+  DIAG_SCOPE(8);
   o.switching = o.resuming = o.marker = false;
   o.cbLen = 0;
   o.cb = 0;
@@ -1026,6 +1037,7 @@ __device__ __forceinline__ void seq_invalidate(Lane &L, u32 n) {
 // sequencer's RangeMap stays at value 0, so slot = extModifiedSN % size)
 __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, u64 cb,
                          int cbLen) {
+  DIAG_SCOPE(10);
   const u32 size = L.seqSize;
   if (hasf(L, F_SEQ_INIT) && esn == L.h.seqExtHighestSN + 1) {  // in-order: next slot, nothing skipped
     u32 slot = u32(L.h.seqHighSlot) + 1;
@@ -1602,6 +1614,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __shared__ i32 sEx[kSetCap];
   __shared__ i32 sMissKey[kMissCap];
   __shared__ i32 sMissVal[kMissCap];
+  __shared__ RangeEntry sRm[kRangeCap];
 #if LKF_DIAG
   const u64 tEntry = clock64();
 #endif
@@ -1625,9 +1638,18 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   o.nFwd = o.nBytes = o.nTuples = 0;
   o.relOff = 0;
   for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
+#if LKF_STATE_LDS
+  __shared__ __attribute__((aligned(16))) DTHot sHot;
+  Lane L{sHot};
+  reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
+  __syncthreads();
+#else
   Lane L;
   L.h = A.hot[d];
-  L.rm = A.rm + size_t(d) * kRangeCap;
+#endif
+  RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
+  L.rm = sRm;
+  L.rmDirty = false;
   L.vc = A.vc + d;
   L.dropKey = sDrop;
   L.exKey = sEx;
@@ -1643,6 +1665,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       sMissKey[i] = L.vc->missKey[i];
       sMissVal[i] = L.vc->missVal[i];
     }
+  }
+  for (u32 i = lane; i < L.h.rmCount; i += 64) {  // live closed ranges of the RangeMap ring
+    const u32 idx = (L.h.rmHead + i) % kRangeCap;
+    sRm[idx] = rmG[idx];
   }
   if (slot0 + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
     if (lane == 0) atomicOr(A.err, 8u);
@@ -1887,7 +1913,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
             if (gOff > 1) seq_invalidate(L, gOff - 1);  // stores only: no drain needed
           }
         }
-        DIAG_MARK(8);
         // output records + sequencer slots of the forwarded lanes
         const int cc = p.hdr0 & 0xf;
         const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
@@ -1937,7 +1962,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           store_rec(L.seq + slot, m);
 #endif
         }
-        DIAG_MARK(9);
         const u32 sumLen = wave_sum_u32(outLen);
         // ---- advance the DownTrack state past the run (uniform)
         if (fwR) {
@@ -2009,7 +2033,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           }
         }
         if (fwR) o.relOff += rl32(relEx + aligned, 63 - __clzll(fwR));
-        DIAG_MARK(10);
       }
       pos = x;
 #if LKF_DIAG
@@ -2057,7 +2080,19 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   if (lane == 0)
     for (int i = 0; i < 16; i++) atomicAdd(&g_diag[i], (unsigned long long)dg[i]);
 #endif
+#if LKF_STATE_LDS
+  __syncthreads();
+  reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
+#else
   if (lane == 0) A.hot[d] = L.h;
+#endif
+  if (L.rmDirty) {
+    wave_lds_sync();
+    for (u32 i = lane; i < L.h.rmCount; i += 64) {
+      const u32 idx = (L.h.rmHead + i) % kRangeCap;
+      rmG[idx] = sRm[idx];
+    }
+  }
   if (L.h.flags & F_VP8) {
     if (lane < u32(kSetCap)) {
       L.vc->dropKey[lane] = sDrop[lane];

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 NAMES = ["waves", "chunks", "runs", "serial", "serial_drain", "cyc_classify", "cyc_runbody", "cyc_prologue",
-         "rb_drops_gap", "rb_stores", "rb_advance", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
+         "fw_translate", "fw_common", "seq_push", "cyc_load", "cyc_runs", "cyc_serial", "cyc_total", "packets"]
 
 
 def main():
