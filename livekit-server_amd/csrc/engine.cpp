@@ -155,7 +155,8 @@ struct lkf_engine {
   // (emit stream)
   static constexpr int kRing = 256;
   hipEvent_t ring[kRing][5] = {};
-  uint32_t emitGrid = 2048;
+  uint32_t emitGrid = 2048;       // persistent grid-stride launch (LKF_EMIT_PERSISTENT=1)
+  bool emitPersistent = false;
   // ingress (one buffer.Buffer per stream) + speakers
   uint32_t maxStreams = 0;
   DevStream *dStreams = nullptr;
@@ -378,10 +379,11 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   }
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device);
-  // emit is grid-stride with one-wave workgroups: 16 waves per CU saturate
+  // emit is grid-stride with one-wave workgroups: 24 waves per CU saturate
   // HBM and leave wave slots for the next batch's decide stage.
-  int perCU = 16;
+  int perCU = 24;
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
+  if (const char *v = getenv("LKF_EMIT_PERSISTENT")) e->emitPersistent = atoi(v) != 0;
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   return e;
@@ -825,7 +827,12 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.outCap = e->cfg.max_out_pkts;
   m.outByteCap = e->cfg.max_out_bytes;
   m.err = x.dErr;
-  m.grid = e->emitGrid;
+  // One workgroup per 64-record group (grid = the capacity bound; workgroups
+  // past the batch's records exit at once).  Short-lived workgroups free their
+  // slots as they finish, so the next batch's decide stage (higher-priority
+  // stream) interleaves with this emit instead of waiting for a persistent grid.
+  m.grid = e->emitPersistent ? e->emitGrid
+                             : uint32_t(((e->cfg.max_out_pkts + 63) / 64 + 7) / 8 * 8);
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum), "accumulate");
