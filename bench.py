@@ -87,7 +87,9 @@ def main():
     ap.add_argument("--batch-s", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", ""))
+    # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
+    # summary of this same workload (scripts/gpu_pmc.sh -> profiles/)
+    ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")))
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostic: wait for each step (no decide/emit overlap; standalone kernel times)")
     ap.add_argument("--ingress", action="store_true",
@@ -183,6 +185,21 @@ def main():
     elapsed = t1 - t0
     cum = eng.cumulative()
     dec_ms, emit_ms, tot_ms = eng.timing_window(args.steps)
+    coll = None
+    if dist:
+        # the one collective — per-room speaker summaries
+        # (Room.GetActiveSpeakers) all-gathered over RCCL every 400 ms of media;
+        # outside the timed forwarding region (not part of the throughput metric)
+        rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+        now = 1700000000 * 10**9 + int(nb * args.batch_s * 1e9)
+        sp = pkg.speakers_array(eng.api, eng.h, now)
+        torch.cuda.synchronize(dev)
+        tc0 = time.perf_counter()
+        table = rooms_mod.all_gather_speakers(dist, dev, sp, rank * args.rooms, args.rooms)
+        tc1 = time.perf_counter()
+        coll = {"op": "all_gather (RCCL) of per-room speaker records", "bytes_per_rank": int(table[0].nbytes),
+                "ms": round((tc1 - tc0) * 1e3, 3), "rooms_gathered": int(table.shape[0] * table.shape[1]),
+                "rooms_with_speakers": int((table[:, :, 0, 0] >= 0).sum())}
 
     fwd = cum["forwarded"]
     steps_pkts = sum(meta[b][0] for b in range(args.warmup, nb))
@@ -258,6 +275,7 @@ def main():
                                       "frac": round(pipe_ach / PEAK_HBM_GBPS, 4)}},
             "cpu_baseline": cpu,
             "host_enqueue_ms_per_step": round(t_host * 1e3 / args.steps, 4),
+            "collective": coll,
             "tuples_per_step": cum["tuples"] // args.steps,
             "forwarded_per_step": fwd // args.steps,
         }

@@ -85,3 +85,64 @@ def test_room_sharding_gloo_matches_single_process(pkg):
     want = _forward(ROOMS_PER_RANK * WORLD, 0)
     assert got == want
     assert got[1] > 0
+
+
+# ---- §8(e): the one collective — per-room speaker summaries, all-gathered ----
+SPK_ROOMS_PER_RANK = 1
+
+
+def _speakers(rooms, room_base, now):
+    from tests.oracle_lib import load as load_oracle
+    wl = importlib.import_module("livekit-server_amd.workload")
+    pkg = importlib.import_module("livekit-server_amd")
+    o = load_oracle()
+    tr = wl.Trace(3, duration_s=2.0, batch_s=0.4, rooms=rooms, room_base=room_base)
+    h = o.create(500)
+    try:
+        wl.load_topology(o.api, h, tr)
+        wl.load_streams(o.api, h, tr)
+        for b in range(tr.nbatches):
+            rp, n, ar, alen = tr.batch_raw(b)
+            assert o.api["ingest"](h, rp, n, ar, alen) == 0
+        return pkg.speakers_array(o.api, h, now)
+    finally:
+        o.destroy(h)
+        tr.close()
+
+
+def _spk_worker(rank, port, q):
+    import torch
+    rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        now = 1700000000 * 10**9 + int(2.0e9)
+        base = rank * SPK_ROOMS_PER_RANK
+        sp = _speakers(SPK_ROOMS_PER_RANK, base, now)
+        table = rooms_mod.all_gather_speakers(dist, torch.device("cpu"), sp, base, SPK_ROOMS_PER_RANK)
+        if rank == 0:
+            q.put(table)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_speaker_summaries_all_gathered():
+    """Every rank's per-room speaker records, all-gathered, equal one process ranking all rooms."""
+    rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_spk_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    table = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert table.shape == (WORLD, SPK_ROOMS_PER_RANK, rooms_mod.K_MAX, 3)
+    now = 1700000000 * 10**9 + int(2.0e9)
+    full = _speakers(WORLD * SPK_ROOMS_PER_RANK, 0, now)
+    want = rooms_mod.pack_speakers(full, 0, WORLD * SPK_ROOMS_PER_RANK).reshape(table.shape)
+    assert (table == want).all()
+    assert (table[:, :, 0, 0] >= 0).any()  # at least one room has a ranked speaker
