@@ -2140,6 +2140,11 @@ constexpr int EMIT_T = 64;
 constexpr int EMIT_G = 64;
 constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 descriptor = 90
 
+#ifndef LKF_EMIT_U
+#define LKF_EMIT_U 4  // 16-B chunks per lane per copy iteration (loads in flight together)
+#endif
+constexpr int EMIT_U = LKF_EMIT_U;
+
 #ifndef LKF_EMIT_NT
 #define LKF_EMIT_NT 1  // non-temporal output stores: keep L2 for the payload re-reads
 #endif
@@ -2328,7 +2333,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
     u8 *const outG = A.outArena + gByte;
     u32 cur = 0;  // wave-uniform: a record whose first chunk is <= c0
     for (u32 c0 = 0; c0 < nchunks;) {
-      u32 wEnd = min(c0 + 2 * 64, nchunks);
+      u32 wEnd = min(c0 + EMIT_U * 64, nchunks);
       const u32 ji = cur + 1 + lane;
       const u32 st = ji < nrec ? sCs[ji] : 0xffffffffu;
       u64 inW = __ballot(st < wEnd);
@@ -2337,37 +2342,45 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         inW = __ballot(st < wEnd);
       }
       const u32 k = u32(__popcll(inW));
-      const u32 cA = c0 + lane, cB = c0 + 64 + lane;
-      u32 jA = cur, jB = cur;
+      u32 c[EMIT_U], j[EMIT_U];
+#pragma unroll
+      for (int u = 0; u < EMIT_U; u++) {
+        c[u] = c0 + 64u * u + lane;
+        j[u] = cur;
+      }
       for (u32 i = 0; i < k; i++) {
-        const u32 s = rl32(st, i);
-        jA += cA >= s ? 1u : 0u;
-        jB += cB >= s ? 1u : 0u;
+        const u32 sv = rl32(st, i);
+#pragma unroll
+        for (int u = 0; u < EMIT_U; u++) j[u] += c[u] >= sv ? 1u : 0u;
       }
-      const bool actA = cA < wEnd, actB = cB < wEnd;
-      // chunk A / B sources
-      const u32 oA = (cA - sCs[jA]) << 4, oB = (cB - sCs[jB]) << 4;
-      const u32 pA = sPre[jA], pB = sPre[jB];
-      const bool ldsA = oA < (pA >> 16), ldsB = oB < (pB >> 16);
-      const u64 sA = sSrc[jA] + (oA - (pA & 0xffff)), sB = sSrc[jB] + (oB - (pB & 0xffff));
-      uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, b0 = a0, b1 = a0;
-      if (actA && !ldsA) {
-        const u8 *q = A.arena + (sA & ~u64(15));
-        a0 = *reinterpret_cast<const uint4 *>(q);
-        a1 = *reinterpret_cast<const uint4 *>(q + 16);
+      // sources of the lane's chunks, then all their loads in flight together
+      bool act[EMIT_U], lds[EMIT_U];
+      u32 o[EMIT_U];
+      u64 src[EMIT_U];
+      uint4 q0[EMIT_U], q1[EMIT_U];
+#pragma unroll
+      for (int u = 0; u < EMIT_U; u++) {
+        act[u] = c[u] < wEnd;
+        o[u] = (c[u] - sCs[j[u]]) << 4;
+        const u32 pr = sPre[j[u]];
+        lds[u] = o[u] < (pr >> 16);
+        src[u] = sSrc[j[u]] + (o[u] - (pr & 0xffff));
+        q0[u] = q1[u] = make_uint4(0, 0, 0, 0);
+        if (act[u] && !lds[u]) {
+          const u8 *q = A.arena + (src[u] & ~u64(15));
+          q0[u] = *reinterpret_cast<const uint4 *>(q);
+          q1[u] = *reinterpret_cast<const uint4 *>(q + 16);
+        }
       }
-      if (actB && !ldsB) {
-        const u8 *q = A.arena + (sB & ~u64(15));
-        b0 = *reinterpret_cast<const uint4 *>(q);
-        b1 = *reinterpret_cast<const uint4 *>(q + 16);
-      }
-      if (actA) {
+#pragma unroll
+      for (int u = 0; u < EMIT_U; u++) {
+        if (!act[u]) continue;
         uint4 v;
-        if (ldsA) {
-          v = *reinterpret_cast<const uint4 *>(&pre[jA][oA]);
+        if (lds[u]) {
+          v = *reinterpret_cast<const uint4 *>(&pre[j[u]][o[u]]);
         } else {
-          v = shift_window(a0, a1, u32(sA & 15));
-          const int keep = int(sLen[jA]) - int(oA);
+          v = shift_window(q0[u], q1[u], u32(src[u] & 15));
+          const int keep = int(sLen[j[u]]) - int(o[u]);
           if (keep < 16) {  // zero the 16-B tail padding
             v.x &= keep_mask(keep);
             v.y &= keep_mask(keep - 4);
@@ -2375,23 +2388,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
             v.w &= keep_mask(keep - 12);
           }
         }
-        store16(outG + (u64(cA) << 4), v);
-      }
-      if (actB) {
-        uint4 v;
-        if (ldsB) {
-          v = *reinterpret_cast<const uint4 *>(&pre[jB][oB]);
-        } else {
-          v = shift_window(b0, b1, u32(sB & 15));
-          const int keep = int(sLen[jB]) - int(oB);
-          if (keep < 16) {
-            v.x &= keep_mask(keep);
-            v.y &= keep_mask(keep - 4);
-            v.z &= keep_mask(keep - 8);
-            v.w &= keep_mask(keep - 12);
-          }
-        }
-        store16(outG + (u64(cB) << 4), v);
+        store16(outG + (u64(c[u]) << 4), v);
       }
       cur += k;
       c0 = wEnd;
