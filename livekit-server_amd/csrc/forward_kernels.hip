@@ -819,7 +819,6 @@ __device__ bool fw_sourceSwitch(Lane &L, const PktV &p, i32 layer) {
 // getTranslationParamsCommon :1650-1671 -> drop reason or -1 (forward)
 __device__ __forceinline__ int fw_common(Lane &L, const PktV &p, i32 layer, bool marker, int &ord, u64 &osn,
                                          u64 &ots) {
-  DIAG_SCOPE(9);
   if (L.h.lastSSRC != p.ssrc) {
     if (!fw_sourceSwitch(L, p, layer)) return LKF_DROP_SWITCH;
     L.h.lastSSRC = p.ssrc;
@@ -848,7 +847,6 @@ struct Fwd {
 
 // Forwarder.GetTranslationParams forwarder.go:1436-1765 for one (packet, DownTrack).
 __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
-  DIAG_SCOPE(8);
   o.switching = o.resuming = o.marker = false;
   o.cbLen = 0;
   o.cb = 0;
@@ -1037,7 +1035,6 @@ __device__ __forceinline__ void seq_invalidate(Lane &L, u32 n) {
 // sequencer's RangeMap stays at value 0, so slot = extModifiedSN % size)
 __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, u64 cb,
                          int cbLen) {
-  DIAG_SCOPE(10);
   const u32 size = L.seqSize;
   if (hasf(L, F_SEQ_INIT) && esn == L.h.seqExtHighestSN + 1) {  // in-order: next slot, nothing skipped
     u32 slot = u32(L.h.seqHighSlot) + 1;
@@ -1532,7 +1529,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 #endif
 
 #ifndef LKF_DECIDE_WAVES
-#define LKF_DECIDE_WAVES 0  // >0: amdgpu_waves_per_eu floor for k_decide_dt (occupancy experiments)
+#define LKF_DECIDE_WAVES 5  // amdgpu_waves_per_eu floor for k_decide_dt (5: 96 VGPRs, 32 B scratch; +3-4%)
 #endif
 #if LKF_DECIDE_WAVES
 #define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(LKF_DECIDE_WAVES, 8)))
