@@ -322,6 +322,7 @@ KAT(wraparound_uint32) {
 
 // KATs defined in other translation units register themselves the same way.
 #include "kat_sfu.inc"
+#include "kat_dd.inc"
 
 int main(int argc, char **argv) {
   bool list = false;

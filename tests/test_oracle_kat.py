@@ -4,7 +4,9 @@ oracle/kat.cpp + oracle/kat_sfu.inc transcribe the known-answer vectors of
 rangemap_test.go, wraparound_test.go, rtpmunger_test.go, codecmunger/vp8_test.go,
 buffer/helpers_test.go, forwarder_test.go (GetTranslationParams*, padding,
 blank frames, layers, mute), sequencer_test.go, audio/audiolevel_test.go and
-buffer/rtpstats_receiver_test.go.  Each KAT runs as its own test case.
+buffer/rtpstats_receiver_test.go, and (oracle/kat_dd.inc) the dependency-descriptor
+captures of dependencydescriptor/dependencydescriptorextension_test.go plus
+videolayerselector/framenumberwrapper_test.go.  Each KAT runs as its own test case.
 """
 import os
 import subprocess
@@ -27,10 +29,10 @@ NAMES = _kat_names()
 def test_kat_inventory():
     """Every reference test file named in SURVEY.md §8(c) that the oracle covers has KATs."""
     prefixes = ["rangemap", "wraparound", "rtpmunger", "vp8_", "forwarder_", "sequencer", "audiolevel",
-                "rtpstats_receiver"]
+                "rtpstats_receiver", "dd_"]
     for p in prefixes:
         assert any(n.startswith(p) for n in NAMES), p
-    assert len(NAMES) >= 35
+    assert len(NAMES) >= 40
 
 
 @pytest.mark.parametrize("name", NAMES)
