@@ -58,6 +58,10 @@ struct BatchCtx {
   lkf_pkt *dPktsOwn = nullptr;  // lkf_submit copies land here
   uint8_t *dArenaOwn = nullptr;
   lkf_raw_pkt *dRawPkts = nullptr;  // lkf_ingest copies land here
+  DevEvent *dEvents = nullptr;   // this batch's control ops (per-wave CSR)
+  uint32_t *dEvOff = nullptr;
+  uint64_t evCap = 0, evOffCap = 0;
+  hipEvent_t prepped = nullptr;  // prep stage done (prep stream)
   hipEvent_t decided = nullptr;  // decide stage done (decide stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
   bool used = false;
@@ -75,6 +79,7 @@ struct lkf_engine {
   std::vector<uint32_t> csrOff;
   std::vector<DevEvent> csrEv;
   hipStream_t own = nullptr;    // copies, lookups
+  hipStream_t prepS = nullptr;  // ingest + batch preparation (high priority)
   hipStream_t decS = nullptr;   // decide stage (high priority)
   hipStream_t emitS = nullptr;  // emit stage (low priority)
   hipStream_t cur = nullptr;    // caller's stream of the last lkf_run
@@ -140,7 +145,10 @@ struct lkf_engine {
   bool ingestUnchecked = false;       // ingest error word not yet reported
   bool ingestStarted = false;         // this run's start event precedes its ingest
 
-  BatchCtx ctx[2];
+  // three batch contexts: batch n+1 is ingested/prepared while batch n decides
+  // and batch n-1 emits (its buffers are not reused until n+2)
+  static constexpr int kCtx = 3;
+  BatchCtx ctx[kCtx];
   uint64_t nRuns = 0;
   int lastCtx = -1;
 
@@ -233,6 +241,7 @@ static int drain_streams(lkf_engine *e) {
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (e->cur && e->cur != e->own) HIPCHK(hipStreamSynchronize(e->cur), "sync run stream");
   HIPCHK(hipStreamSynchronize(e->own), "sync own stream");
+  HIPCHK(hipStreamSynchronize(e->prepS), "sync prep stream");
   HIPCHK(hipStreamSynchronize(e->decS), "sync decide stream");
   HIPCHK(hipStreamSynchronize(e->emitS), "sync emit stream");
   return LKF_OK;
@@ -305,6 +314,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
   A(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
   A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
+  A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
   A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
   A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
   e->cur = e->own;
@@ -342,6 +352,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dArenaOwn, c.max_batch_arena + 64));
     A(dalloc(&x.dRawPkts, c.max_batch_pkts));
     A(hipEventCreateWithFlags(&x.decided, hipEventDisableTiming));
+    A(hipEventCreateWithFlags(&x.prepped, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.emitted, hipEventDisableTiming));
   }
   for (auto &r : e->ring)
@@ -399,10 +410,11 @@ void lkf_destroy(lkf_engine *e) {
   (void)hipSetDevice(e->dev);
   if (e->cur && e->cur != e->own) (void)hipStreamSynchronize(e->cur);
   if (e->own) (void)hipStreamSynchronize(e->own);
+  if (e->prepS) (void)hipStreamSynchronize(e->prepS);
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
-                  e->dWaveTrack, e->dEvOff, e->dEvents, e->dCum, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
+                  e->dWaveTrack, e->dCum, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
@@ -413,10 +425,11 @@ void lkf_destroy(lkf_engine *e) {
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
-                 x.dRawPkts, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt};
+                 x.dRawPkts, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff};
     for (void *p : q)
       if (p) (void)hipFree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
+    if (x.prepped) (void)hipEventDestroy(x.prepped);
     if (x.emitted) (void)hipEventDestroy(x.emitted);
   }
   for (auto &r : e->ring)
@@ -430,6 +443,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
   if (e->decS) (void)hipStreamDestroy(e->decS);
+  if (e->prepS) (void)hipStreamDestroy(e->prepS);
   if (e->own) (void)hipStreamDestroy(e->own);
   delete e;
 }
@@ -534,7 +548,7 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
   if (!e || (n && !pkts)) return LKF_EINVAL;
   if (n > e->cfg.max_batch_pkts || arena_len > e->cfg.max_batch_arena) return LKF_ENOSPC;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  BatchCtx &x = e->ctx[e->nRuns & 1];
+  BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
   if (x.used) HIPCHK(hipEventSynchronize(x.emitted), "wait emit");  // batch n-2 still reads these buffers
   if (n) HIPCHK(hipMemcpyAsync(x.dPktsOwn, pkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyHostToDevice, e->own), "pkts");
   if (arena_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, arena, arena_len, hipMemcpyHostToDevice, e->own), "arena");
@@ -626,11 +640,9 @@ static int rebuild_sched(lkf_engine *e) {
   if (rc) return rc;
   if (nl + 1 > e->schedCap) {
     if (e->dSched) HIPCHK(hipFree(e->dSched), "free sched");
-    if (e->dEvOff) HIPCHK(hipFree(e->dEvOff), "free evoff");
     if (e->dWaveTrack) HIPCHK(hipFree(e->dWaveTrack), "free wavetrack");
     e->schedCap = nl + 1 + 4096;
     HIPCHK(dalloc(&e->dSched, e->schedCap), "alloc sched");
-    HIPCHK(dalloc(&e->dEvOff, e->schedCap + 1), "alloc evoff");
     HIPCHK(dalloc(&e->dWaveTrack, e->schedCap + 1), "alloc wavetrack");
   }
   // output order: by track, then DownTrack handle (every DownTrack, active or not)
@@ -662,7 +674,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     int rc = rebuild_sched(e);
     if (rc) return rc;
   }
-  const int ci = int(e->nRuns & 1);
+  const int ci = int(e->nRuns % lkf_engine::kCtx);
   BatchCtx &x = e->ctx[ci];
   if (!e->haveBatch) {  // control-only run: an empty batch applies queued ops
     e->curPkts = x.dPktsOwn;
@@ -678,14 +690,19 @@ int lkf_run(lkf_engine *e, void *stream) {
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   hipStream_t us = stream ? reinterpret_cast<hipStream_t>(stream) : e->own;
   e->cur = us;
+  // prep stream: control-op CSR, per-batch init, track ranges, slot scan,
+  // layer index (and, before lkf_run, the ingest).  It runs ahead: batch n+1
+  // is prepared while batch n decides, so decide(n+1) starts as soon as
+  // decide(n) ends.
+  hipStream_t ps = e->prepS;
   hipStream_t s = e->decS;
   HIPCHK(hipEventRecord(e->inEv, us), "event");
-  HIPCHK(hipStreamWaitEvent(s, e->inEv, 0), "wait caller stream");
+  HIPCHK(hipStreamWaitEvent(ps, e->inEv, 0), "wait caller stream");
   const uint32_t nt = uint32_t(e->tracks.size());
   const uint32_t nd = uint32_t(e->dtp.size());
   const uint32_t nl = uint32_t(e->sched.size());
   // this context's previous batch (run n-2) must have finished its emit stage
-  if (x.used) HIPCHK(hipStreamWaitEvent(s, x.emitted, 0), "wait emit");
+  if (x.used) HIPCHK(hipStreamWaitEvent(ps, x.emitted, 0), "wait emit");
 
   // per-lane event CSR (stable: queue order within a lane, then by at_pkt).
   // Counting sort by lane straight into the pinned staging buffer; a lane
@@ -742,35 +759,42 @@ int lkf_run(lkf_engine *e, void *stream) {
   if (nev) std::memcpy(sg.ev, evs.data(), nev * sizeof(DevEvent));
   std::memcpy(sg.off, off.data(), (size_t(nl) + 1) * sizeof(uint32_t));
   const auto tp25 = clk::now();
-  if (nev > e->evCap) {
-    if (e->dEvents) {
-      HIPCHK(hipStreamSynchronize(s), "sync before events realloc");
-      HIPCHK(hipFree(e->dEvents), "free events");
+  if (nev > x.evCap || size_t(nl) + 1 > x.evOffCap) {  // this context's op buffers (run n-2 is done with them)
+    HIPCHK(hipStreamSynchronize(ps), "sync before events realloc");
+    if (nev > x.evCap) {
+      if (x.dEvents) HIPCHK(hipFree(x.dEvents), "free events");
+      x.evCap = std::max<uint64_t>(nev, 4096);
+      HIPCHK(dalloc(&x.dEvents, x.evCap), "alloc events");
     }
-    e->evCap = std::max<uint64_t>(nev, 4096);
-    HIPCHK(dalloc(&e->dEvents, e->evCap), "alloc events");
+    if (size_t(nl) + 1 > x.evOffCap) {
+      if (x.dEvOff) HIPCHK(hipFree(x.dEvOff), "free evoff");
+      x.evOffCap = size_t(nl) + 1 + 4096;
+      HIPCHK(dalloc(&x.dEvOff, x.evOffCap), "alloc evoff");
+    }
   }
-  HIPCHK(launch_h2d(s, e->dEvents, sg.ev, nev * sizeof(DevEvent), e->dEvOff, sg.off, (size_t(nl) + 1) * sizeof(uint32_t)),
+  HIPCHK(launch_h2d(ps, x.dEvents, sg.ev, nev * sizeof(DevEvent), x.dEvOff, sg.off, (size_t(nl) + 1) * sizeof(uint32_t)),
          "event csr pull");
-  HIPCHK(hipEventRecord(sg.done, s), "stage record");
+  HIPCHK(hipEventRecord(sg.done, ps), "stage record");
   sg.used = true;
   const auto tp3 = clk::now();
 
   // ---- decide stage (decide stream)
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
-  if (!e->ingestStarted) HIPCHK(hipEventRecord(rg[0], s), "event");  // else: recorded ahead of the ingest
+  if (!e->ingestStarted) HIPCHK(hipEventRecord(rg[0], ps), "event");  // else: recorded ahead of the ingest
   e->ingestStarted = false;
-  HIPCHK(launch_batch_init(s, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dStats, x.dFwdCnt,
+  HIPCHK(launch_batch_init(ps, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dStats, x.dFwdCnt,
                            x.dFwdBytes),
          "batch init");
-  HIPCHK(launch_track_ranges(s, e->curPkts, e->curN, e->curNDev, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
+  HIPCHK(launch_track_ranges(ps, e->curPkts, e->curN, e->curNDev, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
          "track_ranges");
-  HIPCHK(launch_scan(s, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
+  HIPCHK(launch_scan(ps, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
                      x.dTot + 0, nullptr, nullptr),
          "slot scan");
-  HIPCHK(launch_layer_index(s, e->curPkts, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
+  HIPCHK(launch_layer_index(ps, e->curPkts, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
                             x.dLayerBefore, x.dLayerCnt),
          "layer index");
+  HIPCHK(hipEventRecord(x.prepped, ps), "event");
+  HIPCHK(hipStreamWaitEvent(s, x.prepped, 0), "wait prep");
   DecideLaunch d;
   d.layerList = x.dLayerList;
   d.layerBefore = x.dLayerBefore;
@@ -793,23 +817,25 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.tuples = x.dTuples;
   d.tupleCap = e->cfg.max_batch_tuples;
   d.err = x.dErr;
-  d.events = e->dEvents;
-  d.evOff = e->dEvOff;
+  d.events = x.dEvents;
+  d.evOff = x.dEvOff;
   d.fwdCnt = x.dFwdCnt;
   d.fwdBytes = x.dFwdBytes;
   d.stats = x.dStats;
   HIPCHK(hipEventRecord(rg[1], s), "event");
   HIPCHK(launch_decide(s, d), "decide");
-  HIPCHK(launch_stats_reduce(s, x.dStats), "stats reduce");
   HIPCHK(hipEventRecord(rg[2], s), "event");
-  HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
-                     x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm, x.dGFirst, e->cfg.max_out_pkts),
-         "out scan");
   HIPCHK(hipEventRecord(x.decided, s), "event");
 
-  // ---- emit stage (emit stream), overlaps the next batch's decide stage
-  HIPCHK(hipStreamWaitEvent(e->emitS, x.decided, 0), "wait decided");
-  HIPCHK(hipEventRecord(rg[3], e->emitS), "event");
+  // ---- emit stage (emit stream): counters, output scan, wire bytes.  The
+  // decide stream goes straight on to the next batch's decide.
+  hipStream_t es = e->emitS;
+  HIPCHK(hipStreamWaitEvent(es, x.decided, 0), "wait decided");
+  HIPCHK(launch_stats_reduce(es, x.dStats), "stats reduce");
+  HIPCHK(launch_scan(es, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
+                     x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm, x.dGFirst, e->cfg.max_out_pkts),
+         "out scan");
+  HIPCHK(hipEventRecord(rg[3], es), "event");
   EmitLaunch m;
   m.perm = e->dPerm;
   m.recBase = x.dRecBase;
@@ -872,7 +898,7 @@ int lkf_sync(lkf_engine *e) {
   }
   if (e->lastCtx < 0) return LKF_OK;
   uint32_t acc = 0;
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < lkf_engine::kCtx; i++) {
     BatchCtx &x = e->ctx[i];
     if (!x.used || (x.checked && i != e->lastCtx)) continue;
     uint32_t err[4] = {0, 0, 0, 0};
@@ -1105,7 +1131,7 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p) {
 static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, uint32_t n, const uint8_t *dRaw,
                          uint64_t rawLen) {
   const uint32_t nt = uint32_t(e->tracks.size());
-  hipStream_t s = e->decS;
+  hipStream_t s = e->prepS;
   // the batch's GPU span (lkf_timing_window total) starts before its ingest
   HIPCHK(hipEventRecord(e->ring[e->nRuns % lkf_engine::kRing][0], s), "event");
   e->ingestStarted = true;
@@ -1154,11 +1180,11 @@ int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
   int rc = flush_topology(e);
   if (rc) return rc;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  BatchCtx &x = e->ctx[e->nRuns & 1];
-  if (x.used) HIPCHK(hipStreamWaitEvent(e->decS, x.emitted, 0), "wait emit");  // batch n-2 reads these buffers
-  if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->decS),
+  BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
+  if (x.used) HIPCHK(hipStreamWaitEvent(e->prepS, x.emitted, 0), "wait emit");  // batch n-2 reads these buffers
+  if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->prepS),
                 "raw pkts");
-  if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->decS), "raw arena");
+  if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->prepS), "raw arena");
   return ingest_common(e, x, x.dRawPkts, n, x.dArenaOwn, raw_len);
 }
 
@@ -1168,8 +1194,8 @@ int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, cons
   int rc = flush_topology(e);
   if (rc) return rc;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  BatchCtx &x = e->ctx[e->nRuns & 1];
-  if (x.used) HIPCHK(hipStreamWaitEvent(e->decS, x.emitted, 0), "wait emit");
+  BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
+  if (x.used) HIPCHK(hipStreamWaitEvent(e->prepS, x.emitted, 0), "wait emit");
   return ingest_common(e, x, d_pkts, n, d_raw, raw_len);
 }
 
@@ -1178,7 +1204,7 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
   *n_out = e->lastIngestN;
   if (cap < e->lastIngestN) return LKF_ENOSPC;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->decS), "sync");
+  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
   if (e->lastIngestN)
     HIPCHK(hipMemcpy(out, e->dFlows, size_t(e->lastIngestN) * sizeof(lkf_flow), hipMemcpyDeviceToHost), "flows");
   return LKF_OK;
@@ -1187,7 +1213,7 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
 int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
   if (!e || !n_out) return LKF_EINVAL;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->decS), "sync");
+  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
   uint32_t n = 0;
   if (e->haveBatch) {
     n = e->curN;
@@ -1310,16 +1336,16 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
   a.slots = e->dSpkSlots;
   a.counts = e->dSpkCounts;
   // decide stream: ordered after the ingest that updated the levels
-  HIPCHK(launch_speakers(e->decS, a), "speakers");
+  HIPCHK(launch_speakers(e->prepS, a), "speakers");
   std::vector<uint32_t> counts(e->nRooms);
   std::vector<lkf_speaker> slots(size_t(e->nRooms) * 64);
   HIPCHK(hipMemcpyAsync(counts.data(), e->dSpkCounts, counts.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        e->decS),
+                        e->prepS),
          "counts copy");
   HIPCHK(hipMemcpyAsync(slots.data(), e->dSpkSlots, slots.size() * sizeof(lkf_speaker), hipMemcpyDeviceToHost,
-                        e->decS),
+                        e->prepS),
          "slots copy");
-  HIPCHK(hipStreamSynchronize(e->decS), "speakers sync");
+  HIPCHK(hipStreamSynchronize(e->prepS), "speakers sync");
   uint32_t k = 0;
   for (uint32_t r = 0; r < e->nRooms; r++) k += counts[r];
   *n_out = k;
