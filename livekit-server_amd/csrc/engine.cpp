@@ -76,8 +76,6 @@ struct lkf_engine {
   bool hostProf = false;
   double hp[7] = {};  // pre, stage wait, csr build, launches, total, runs, staging copies
   std::vector<uint32_t> fill;  // event CSR fill cursors
-  std::vector<uint32_t> csrOff;
-  std::vector<DevEvent> csrEv;
   hipStream_t own = nullptr;    // copies, lookups
   hipStream_t prepS = nullptr;  // ingest + batch preparation (high priority)
   hipStream_t decS = nullptr;   // decide stage (high priority)
@@ -111,9 +109,11 @@ struct lkf_engine {
   };
   std::vector<Pend> pending;
   // pinned, double-buffered staging of the per-lane event CSR (async H2D)
+  // Page-locked, CPU-cached staging (malloc + hipHostRegister): the CSR is
+  // built in place and a copy kernel pulls it through the device mapping.
   struct Stage {
-    DevEvent *ev = nullptr;
-    uint32_t *off = nullptr;
+    DevEvent *ev = nullptr, *evDev = nullptr;
+    uint32_t *off = nullptr, *offDev = nullptr;
     size_t evCap = 0, offCap = 0;
     hipEvent_t done = nullptr;
     bool used = false;
@@ -237,6 +237,36 @@ static DevTrack to_dev_track(const lkf_track_params &p) {
 }
 
 // Waits for every queued stage (run, own and emit streams).
+template <typename T>
+static hipError_t stage_alloc(T **host, T **dev, size_t n) {
+  const size_t bytes = (n * sizeof(T) + 4095) & ~size_t(4095);
+  void *p = std::aligned_alloc(4096, bytes);
+  if (!p) return hipErrorOutOfMemory;
+  hipError_t r = hipHostRegister(p, bytes, hipHostRegisterMapped);
+  if (r != hipSuccess) {
+    std::free(p);
+    return r;
+  }
+  void *d = nullptr;
+  r = hipHostGetDevicePointer(&d, p, 0);
+  if (r != hipSuccess) {
+    (void)hipHostUnregister(p);
+    std::free(p);
+    return r;
+  }
+  *host = static_cast<T *>(p);
+  *dev = static_cast<T *>(d);
+  return hipSuccess;
+}
+template <typename T>
+static void stage_free(T **host, T **dev) {
+  if (*host) {
+    (void)hipHostUnregister(*host);
+    std::free(*host);
+  }
+  *host = *dev = nullptr;
+}
+
 static int drain_streams(lkf_engine *e) {
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (e->cur && e->cur != e->own) HIPCHK(hipStreamSynchronize(e->cur), "sync run stream");
@@ -436,8 +466,8 @@ void lkf_destroy(lkf_engine *e) {
     for (auto &ev : r)
       if (ev) (void)hipEventDestroy(ev);
   for (auto &sg : e->stage) {
-    if (sg.ev) (void)hipHostFree(sg.ev);
-    if (sg.off) (void)hipHostFree(sg.off);
+    stage_free(&sg.ev, &sg.evDev);
+    stage_free(&sg.off, &sg.offDev);
     if (sg.done) (void)hipEventDestroy(sg.done);
   }
   if (e->inEv) (void)hipEventDestroy(e->inEv);
@@ -712,15 +742,14 @@ int lkf_run(lkf_engine *e, void *stream) {
   if (sg.used) HIPCHK(hipEventSynchronize(sg.done), "stage wait");
   const auto tp2 = clk::now();
   if (size_t(nl) + 1 > sg.offCap) {
-    if (sg.off) HIPCHK(hipHostFree(sg.off), "free stage");
-    sg.offCap = size_t(nl) + 1;
-    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sg.off), sg.offCap * sizeof(uint32_t)), "alloc stage");
+    stage_free(&sg.off, &sg.offDev);
+    sg.offCap = size_t(nl) + 1 + 4096;
+    HIPCHK(stage_alloc(&sg.off, &sg.offDev, sg.offCap), "alloc stage");
   }
   if (!sg.done) HIPCHK(hipEventCreateWithFlags(&sg.done, hipEventDisableTiming), "stage event");
-  // built in cacheable host memory, then one sequential write into the
-  // pinned (write-combined) staging buffer, pulled by a copy kernel
-  std::vector<uint32_t> &off = e->csrOff;
-  off.assign(size_t(nl) + 1, 0u);
+  // counting sort by lane, in place in the (cached, page-locked) staging buffers
+  uint32_t *off = sg.off;
+  std::memset(off, 0, (size_t(nl) + 1) * sizeof(uint32_t));
   size_t nev = 0;
   for (auto &p : e->pending) {
     const int l = e->dtLane[p.dt];
@@ -729,35 +758,34 @@ int lkf_run(lkf_engine *e, void *stream) {
     nev++;
   }
   for (uint32_t l = 0; l < nl; l++) off[l + 1] += off[l];
-  std::vector<DevEvent> &evs = e->csrEv;
-  evs.resize(nev);
-  e->fill.assign(off.begin(), off.begin() + nl);
-  for (auto &p : e->pending) {
-    const int l = e->dtLane[p.dt];
-    if (l < 0) continue;
-    evs[e->fill[l]++] = p.ev;
+  if (nev > sg.evCap) {
+    stage_free(&sg.ev, &sg.evDev);
+    sg.evCap = std::max<size_t>(nev, 4096);
+    HIPCHK(stage_alloc(&sg.ev, &sg.evDev, sg.evCap), "alloc stage");
   }
-  for (uint32_t l = 0; l < nl; l++) {
-    const uint32_t b = off[l], en = off[l + 1];
-    for (uint32_t i = b + 1; i < en; i++) {
-      if (evs[i].at >= evs[i - 1].at) continue;
-      const DevEvent v = evs[i];  // queued out of at_pkt order: stable insertion
-      uint32_t j = i;
-      while (j > b && evs[j - 1].at > v.at) {
-        evs[j] = evs[j - 1];
-        j--;
+  DevEvent *evs = sg.ev;
+  if (nev) {
+    e->fill.assign(off, off + nl);
+    for (auto &p : e->pending) {
+      const int l = e->dtLane[p.dt];
+      if (l < 0) continue;
+      evs[e->fill[l]++] = p.ev;
+    }
+    for (uint32_t l = 0; l < nl; l++) {
+      const uint32_t b = off[l], en = off[l + 1];
+      for (uint32_t i = b + 1; i < en; i++) {
+        if (evs[i].at >= evs[i - 1].at) continue;
+        const DevEvent v = evs[i];  // queued out of at_pkt order: stable insertion
+        uint32_t j = i;
+        while (j > b && evs[j - 1].at > v.at) {
+          evs[j] = evs[j - 1];
+          j--;
+        }
+        evs[j] = v;
       }
-      evs[j] = v;
     }
   }
   e->pending.clear();
-  if (nev > sg.evCap) {
-    if (sg.ev) HIPCHK(hipHostFree(sg.ev), "free stage");
-    sg.evCap = std::max<size_t>(nev, 4096);
-    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sg.ev), sg.evCap * sizeof(DevEvent)), "alloc stage");
-  }
-  if (nev) std::memcpy(sg.ev, evs.data(), nev * sizeof(DevEvent));
-  std::memcpy(sg.off, off.data(), (size_t(nl) + 1) * sizeof(uint32_t));
   const auto tp25 = clk::now();
   if (nev > x.evCap || size_t(nl) + 1 > x.evOffCap) {  // this context's op buffers (run n-2 is done with them)
     HIPCHK(hipStreamSynchronize(ps), "sync before events realloc");
@@ -772,7 +800,7 @@ int lkf_run(lkf_engine *e, void *stream) {
       HIPCHK(dalloc(&x.dEvOff, x.evOffCap), "alloc evoff");
     }
   }
-  HIPCHK(launch_h2d(ps, x.dEvents, sg.ev, nev * sizeof(DevEvent), x.dEvOff, sg.off, (size_t(nl) + 1) * sizeof(uint32_t)),
+  HIPCHK(launch_h2d(ps, x.dEvents, sg.evDev, nev * sizeof(DevEvent), x.dEvOff, sg.offDev, (size_t(nl) + 1) * sizeof(uint32_t)),
          "event csr pull");
   HIPCHK(hipEventRecord(sg.done, ps), "stage record");
   sg.used = true;
