@@ -311,6 +311,7 @@ static int flush_topology(lkf_engine *e) {
     HIPCHK(hipMemcpy(e->dStreamHot + first, hot.data(), k * sizeof(StreamHot), hipMemcpyHostToDevice),
            "stream state upload");
     HIPCHK(hipMemset(e->dHist + first * kHistWords, 0, k * kHistWords * sizeof(uint64_t)), "history reset");
+    HIPCHK(hipDeviceSynchronize(), "history reset sync");  // null stream vs the engine's non-blocking streams
     e->pendStreams.clear();
   }
   return LKF_OK;
@@ -413,6 +414,10 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
       A(hipMemset(x.dStats, 0, size_t(kStatsWords) * (1 + kStatCopies) * sizeof(uint64_t)));
       A(hipMemset(x.dErr, 0, 4 * sizeof(uint32_t)));
     }
+    // hipMemset runs on the null stream, which the engine's non-blocking
+    // streams do not wait for: finish the initialisation before any batch
+    // (a late zero-fill raced the first batch's arena copy and sequencer writes)
+    A(hipDeviceSynchronize());
   }
   if (!ok) {
     lkf_destroy(e);
@@ -1406,7 +1411,10 @@ int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset) {
   out->out_bytes = st[2];
   out->arena_bytes = st[3];
   for (int i = 0; i < LKF_DROP_NREASONS; i++) out->drops[i] = st[4 + i];
-  if (reset) HIPCHK(hipMemset(e->dCum, 0, sizeof(st)), "cum reset");
+  if (reset) {
+    HIPCHK(hipMemset(e->dCum, 0, sizeof(st)), "cum reset");
+    HIPCHK(hipDeviceSynchronize(), "cum reset sync");  // before the next run's k_accumulate (emit stream)
+  }
   return LKF_OK;
 }
 

@@ -1764,7 +1764,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       if (fl & (F_MUTED | F_PUBMUTED)) {
         cls = LKF_DROP_MUTED;
       } else if (!video) {
-        cls = kf ? -2 : -1;  // a keyframe moves the RTX gate (rtpmunger.go:205-208)
+        cls = -1;  // (a keyframe's RTX-gate move is applied with the run's state advance)
       } else if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) {
         cls = LKF_DROP_PAUSED;
       } else if (!(fl & F_SIMULCAST)) {
@@ -1780,7 +1780,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           cls = LKF_DROP_NOT_SELECTED;
         else if ((fl & F_DEFICIENT) && L.h.tgtS < L.h.curS)
           cls = LKF_DROP_DOWNGRADE;
-        else if ((fl & F_VP8) && (fl & F_TLS_VP8) && (p.flags & LKF_PKT_VP8) && !kf)
+        else if ((fl & F_VP8) && (fl & F_TLS_VP8) && (p.flags & LKF_PKT_VP8))
           cls = -1;
         else
           cls = -2;
@@ -2005,6 +2005,14 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
             setf(L, F_LAST_MARKER, sMk);
           }
           if (hasf(L, F_RTX_GATE) && (rl64(osn, lastSel) - L.h.extRtxGateSn) > 2000) setf(L, F_RTX_GATE, false);
+          // key frames in the run move the RTX gate to their munged SN
+          // (rtpmunger.go:204-208); later lanes are < 64 past it, so the
+          // 2000-packet expiry above cannot undo the last one
+          const u64 kfM = __ballot(((selR >> lane) & 1) && kf);
+          if (kfM) {
+            L.h.extRtxGateSn = rl64(osn, 63 - __clzll(kfM));
+            setf(L, F_RTX_GATE, true);
+          }
           if (video) {
             L.h.wrMaxPictureId = i32(rl32(u32(ext), lastSel));
             setf(L, F_WR_MAX_MBIT, rl32(u32(M), lastSel) != 0);
