@@ -1815,6 +1815,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       const i32 prevExt = pc >= 0 ? pcExt : L.h.wrMaxPictureId;
       const bool prevM = pc >= 0 ? pcM : ((fl & F_WR_MAX_MBIT) != 0);
       bool dropT = false;
+      u64 tswM = 0;  // candidate lanes at a temporal switch point (the first ends the run)
       bool gapExempt = false;
       i32 gapExt = 0;
       if (video) {
@@ -1837,7 +1838,14 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         dropT = overT && !gapLane && !(gapExempt && ext == gapExt);
         if (__ballot(dropT) && L.h.exCount)  // exempted pictures forward (vp8.go:270)
           dropT = dropT && !set_has(L.exKey, L.h.exHead, L.h.exCount, ext);
-        ok = ok && !wrapBack && !wraps && !tsw && (!dropT || L.h.snOffset == L.h.rmOpenValue);
+        // A temporal switch point is decided in the run and ends it: up, the
+        // packet's own TID is the filter limit (thisL = tid, so it forwards);
+        // down (at a marker), thisL is still the current layer and the packet
+        // must forward — a filtered one would roll the selector back (serial).
+        if (tsw && cT < gT) dropT = false;
+        const bool tswOk = tsw && !gapLane && !dropT;
+        ok = ok && !wrapBack && !wraps && (!tsw || tswOk) && (!dropT || L.h.snOffset == L.h.rmOpenValue);
+        tswM = __ballot(inWin && ok && tsw);
       }
       // (diag: run-body split below)
       const u64 tdM = __ballot(ok && dropT);
@@ -1874,7 +1882,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
                                                  osn - prevOsn < u64(L.seqSize) - 64));
       const bool bad = inWin && ((cls == -2) || (cls == -1 && !ok) || (fwd && !seqOk));
       const u64 stopM = __ballot(bad || (valid && lane >= pos && !inWin));
-      const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+      u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+      if (tswM & ~((1ull << pos) - 1)) x = min(x, u32(__ffsll((long long)(tswM & ~((1ull << pos) - 1))) - 1) + 1u);
       // ---- decide lanes [pos, x) together
       DIAG(2, x > pos ? 1 : 0);
 #if LKF_DIAG
@@ -2028,6 +2037,14 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
               m &= ~runD;
             }
             if (tdR) L.h.snOffset = L.h.rmOpenValue;
+            const u64 tswR = tswM & runM;  // the run's last lane switched the temporal layer
+            if (tswR) {
+              const u32 b = 63 - __clzll(tswR);
+              const i32 nxt = L.h.curT < L.h.tgtT ? i32(rl32(u32(p.tid), b)) : L.h.tgtT;
+              L.h.prevS = L.h.curS;
+              L.h.prevT = L.h.curT;
+              L.h.curT = nxt;
+            }
             u64 pd = __ballot(picDrop && inRun);
             L.h.pictureIdOffset += i32(__popcll(pd));
             while (pd) {
