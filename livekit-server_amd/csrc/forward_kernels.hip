@@ -2482,6 +2482,25 @@ __global__ void __launch_bounds__(256) k_stats_reduce(u64 *stats) {
   }
 }
 
+__global__ void k_ev_offsets(const u32 *__restrict__ laneOf, u32 nev, u32 nl, u32 *__restrict__ off) {
+  const u32 l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l > nl) return;
+  u32 lo = 0, hi = nev;  // lower_bound(laneOf, l)
+  while (lo < hi) {
+    const u32 mid = (lo + hi) >> 1;
+    if (laneOf[mid] < l)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  off[l] = lo;
+}
+
+hipError_t launch_ev_offsets(hipStream_t s, const u32 *laneOf, u32 nev, u32 nl, u32 *off) {
+  hipLaunchKernelGGL(k_ev_offsets, dim3((nl + 1 + 255) / 256), dim3(256), 0, s, laneOf, nev, nl, off);
+  return hipGetLastError();
+}
+
 hipError_t launch_stats_reduce(hipStream_t s, u64 *stats) {
   hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats);
   return hipGetLastError();

@@ -7,7 +7,7 @@ from tests.oracle_lib import load as load_oracle
 pkg = importlib.import_module("livekit-server_amd")
 wl = importlib.import_module("livekit-server_amd.workload")
 abi = importlib.import_module("livekit-server_amd.abi")
-for rep in range(2):
+for rep in range(int(os.environ.get("REPS", "2"))):
     tr = wl.Trace(4, duration_s=2.0, batch_s=1.0, rooms=1, participants=600)
     o = load_oracle(); eng = pkg.Engine.for_trace(tr); oh = o.create(500)
     wl.load_topology(eng.api, eng.h, tr); wl.load_topology(o.api, oh, tr)
