@@ -317,15 +317,26 @@ int lkf_ctl_batch(lkf_engine *e, const lkf_ctl_event *evs, uint32_t n);
 
 /* ---- data --------------------------------------------------------------- */
 /* Host batch: copies descriptors + arena to HBM (WebRTCReceiver.forwardRTP
- * receiver.go:635 -> DownTrackSpreader.Broadcast downtrackspreader.go:89). */
+ * receiver.go:635 -> DownTrackSpreader.Broadcast downtrackspreader.go:89).
+ * The host buffers are reusable when lkf_submit returns. */
 int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len);
-/* Device-resident batch (pointers into HBM, valid until lkf_run returns). */
+/* Device-resident batch (pointers into HBM).  The engine reads them
+ * asynchronously on its own streams after lkf_run returns: they must stay
+ * valid and unmodified until lkf_sync returns (or until the enqueue of the
+ * third lkf_run after this one, which waits for this batch's emit stage).
+ * The emit kernel reads payloads as aligned 16-B words: the 32 bytes after
+ * arena_len must be readable device memory (their content is ignored). */
 int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const uint8_t *d_arena,
                       uint64_t arena_len);
 /* Runs the batch on `stream` (a hipStream_t, may be NULL): every DownTrack's
  * TrackSender.WriteRTP (downtrack.go:680-760) for every packet of its track.
  * Asynchronous; lkf_sync waits. */
 int lkf_run(lkf_engine *e, void *stream);
+/* Waits for every queued run and ingest.  Errors are sticky: the first
+ * lkf_sync after any failing batch or ingest (however many runs were queued
+ * in between) returns its code (LKF_EORDER / LKF_ENOSPC) and clears it.  A
+ * DownTrack whose tuple slots overflowed skips that batch (its state does not
+ * advance): a batch reported LKF_ENOSPC is not bit-exact. */
 int lkf_sync(lkf_engine *e);
 /* Batch results (valid after lkf_sync, until the next lkf_run). */
 int lkf_get_stats(lkf_engine *e, lkf_stats *out);
@@ -364,11 +375,13 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p);
  * of the next lkf_run (the raw arena is the forwarding arena; it must stay
  * valid until that batch's outputs are drained).  Host buffers are copied. */
 int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len);
-/* Same with device-resident inputs (valid until the forwarded batch is synced).
- * Ingest is enqueued on the engine's decide stream without a host sync: the
- * inputs must be complete when it is called (produced on a synchronized
- * stream). The ExtPacket count stays on the device and feeds the next
- * lkf_run directly; lkf_ingest_flows / lkf_ingested synchronize. */
+/* Same with device-resident inputs: they must stay valid and unmodified until
+ * lkf_sync returns after the lkf_run that forwards them, and the 32 bytes
+ * after raw_len must be readable (see lkf_submit_device).  Ingest is enqueued
+ * on the engine's prep stream without a host sync: the inputs must be
+ * complete when it is called (produced on a synchronized stream).  The
+ * ExtPacket count stays on the device and feeds the next lkf_run directly;
+ * lkf_ingest_flows / lkf_ingested synchronize. */
 int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, const uint8_t *d_raw,
                       uint64_t raw_len);
 /* Per-datagram outcomes of the last ingest (input order). */

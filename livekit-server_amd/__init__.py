@@ -137,7 +137,7 @@ class Engine:
                    max_batch_pkts=mp, max_batch_arena=int(trace.max_batch_arena * headroom) + 4096,
                    max_batch_tuples=int(trace.max_batch_tuples * headroom) + 1024,
                    max_out_pkts=int(trace.max_batch_tuples * headroom) + 1024,
-                   max_out_bytes=int(trace.max_batch_tuples * headroom) * 1536 + (1 << 20), **kw)
+                   max_out_bytes=int(trace.max_batch_out_bytes * headroom) + (1 << 20), **kw)
 
     def _chk(self, rc, what):
         if rc != 0:

@@ -323,6 +323,7 @@ def load_synth(path=None):
     _bind(lib, "lkfs_max_batch_pkts", C.c_uint32, [t])
     _bind(lib, "lkfs_max_batch_arena", C.c_uint64, [t])
     _bind(lib, "lkfs_max_batch_tuples", C.c_uint64, [t])
+    _bind(lib, "lkfs_max_batch_out_bytes", C.c_uint64, [t])
     _bind(lib, "lkfs_num_streams", C.c_uint32, [t])
     _bind(lib, "lkfs_streams", P(lkf_stream_params), [t])
     _bind(lib, "lkfs_batch_raw", C.c_int, [t, C.c_uint32, P(P(lkf_raw_pkt)), P(C.c_uint32)])

@@ -66,7 +66,6 @@ struct BatchCtx {
   hipEvent_t decided = nullptr;  // decide stage done (decide stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
   bool used = false;
-  bool checked = false;  // error word already reported by lkf_sync
 };
 
 }  // namespace
@@ -136,6 +135,10 @@ struct lkf_engine {
   DevEvent *dEvents = nullptr;
   uint64_t evCap = 0;
   uint64_t *dCum = nullptr;
+  // sticky error word: every batch's decide/emit error bits (bits 0-3) and
+  // every ingest's error bits (<< 4) are OR-ed in on the GPU; lkf_sync reports
+  // and clears it (per-context error words are reused every kCtx runs)
+  uint32_t *dSticky = nullptr;
 
   // batch input for the next run
   const lkf_pkt *curPkts = nullptr;
@@ -144,7 +147,6 @@ struct lkf_engine {
   uint64_t curArenaLen = 0;
   bool haveBatch = false;
   const uint64_t *curNDev = nullptr;  // device-side batch length (ingest-produced batch)
-  bool ingestUnchecked = false;       // ingest error word not yet reported
   bool ingestStarted = false;         // this run's start event precedes its ingest
 
   // three batch contexts: batch n+1 is ingested/prepared while batch n decides
@@ -279,6 +281,15 @@ static int drain_streams(lkf_engine *e) {
   return LKF_OK;
 }
 
+// hipMemcpy from pageable host memory may return before its DMA lands, and
+// the engine's streams are non-blocking (they do not order against the null
+// stream): every host-side upload ends with a device sync before any engine
+// stream can read what it wrote.
+static int upload_done(lkf_engine *e) {
+  HIPCHK(hipDeviceSynchronize(), "upload sync");
+  return LKF_OK;
+}
+
 // Uploads tracks / DownTracks added since the last flush (contiguous tails).
 static int flush_topology(lkf_engine *e) {
   if (e->pendTracks.empty() && e->pendDTs.empty() && e->pendStreams.empty()) return LKF_OK;
@@ -313,10 +324,9 @@ static int flush_topology(lkf_engine *e) {
     HIPCHK(hipMemcpy(e->dStreamHot + first, hot.data(), k * sizeof(StreamHot), hipMemcpyHostToDevice),
            "stream state upload");
     HIPCHK(hipMemset(e->dHist + first * kHistWords, 0, k * kHistWords * sizeof(uint64_t)), "history reset");
-    HIPCHK(hipDeviceSynchronize(), "history reset sync");  // null stream vs the engine's non-blocking streams
     e->pendStreams.clear();
   }
-  return LKF_OK;
+  return upload_done(e);
 }
 
 extern "C" {
@@ -358,6 +368,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dVc, c.max_downtracks));
   A(dalloc(&e->dSeq, size_t(c.max_downtracks) * c.seq_size));
   A(dalloc(&e->dCum, kStatsWords));
+  A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
   const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
   for (auto &x : e->ctx) {
@@ -410,6 +421,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
     A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
+    A(hipMemset(e->dSticky, 0, 4 * sizeof(uint32_t)));
     for (auto &x : e->ctx) {
       A(hipMemset(x.dArenaOwn, 0, c.max_batch_arena + 64));
       A(hipMemset(x.dTot, 0, 4 * sizeof(uint64_t)));
@@ -451,7 +463,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
-                  e->dWaveTrack, e->dCum, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
+                  e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
@@ -504,7 +516,7 @@ int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9
   std::memcpy(e->tracks[track].layer_offsets, offsets, 9 * sizeof(uint32_t));
   DevTrack t = to_dev_track(e->tracks[track]);
   HIPCHK(hipMemcpy(e->dTracks + track, &t, sizeof(t), hipMemcpyHostToDevice), "offsets copy");
-  return LKF_OK;
+  return upload_done(e);
 }
 
 int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
@@ -543,7 +555,7 @@ int lkf_remove_downtrack(lkf_engine *e, int32_t dt) {
                    hipMemcpyHostToDevice),
          "remove copy");
   e->schedDirty = true;
-  return LKF_OK;
+  return upload_done(e);
 }
 
 int lkf_ctl(lkf_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64_t a2, int64_t a3, uint32_t at_pkt) {
@@ -697,7 +709,7 @@ static int rebuild_sched(lkf_engine *e) {
            "wavetrack copy");
   }
   e->schedDirty = false;
-  return LKF_OK;
+  return upload_done(e);
 }
 
 int lkf_run(lkf_engine *e, void *stream) {
@@ -898,7 +910,7 @@ int lkf_run(lkf_engine *e, void *stream) {
                              : uint32_t(((e->cfg.max_out_pkts + 63) / 64 + 7) / 8 * 8);
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
-  HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum), "accumulate");
+  HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum, x.dErr, e->dSticky), "accumulate");
   HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
   if (e->hostProf && e->nRuns >= 3) {  // steady state: skip the first runs (initial control ops, first touch)
     e->hp[0] += std::chrono::duration<double, std::milli>(tp1 - tp0).count();
@@ -910,7 +922,6 @@ int lkf_run(lkf_engine *e, void *stream) {
     e->hp[5] += 1;
   }
   x.used = true;
-  x.checked = false;
   e->lastCtx = ci;
   e->nRuns++;
   e->haveBatch = false;
@@ -918,30 +929,20 @@ int lkf_run(lkf_engine *e, void *stream) {
   return LKF_OK;
 }
 
-// Waits for all queued batches; reports the error word of the last batch and
-// of an earlier batch not yet reported.
+// Waits for all queued batches; reports (and clears) the sticky error word:
+// every error of every batch and ingest since the last lkf_sync.
 int lkf_sync(lkf_engine *e) {
   if (!e) return LKF_EINVAL;
   int rc = drain_streams(e);
   if (rc) return rc;
-  if (e->ingestUnchecked) {
-    uint32_t ierr = 0;
-    HIPCHK(hipMemcpy(&ierr, e->dIErr, sizeof(ierr), hipMemcpyDeviceToHost), "ingest err copy");
-    e->ingestUnchecked = false;
-    if (ierr & 3u) {
-      e->err = "raw batch not grouped by track / bad stream handle";
-      return LKF_EORDER;
-    }
-  }
-  if (e->lastCtx < 0) return LKF_OK;
   uint32_t acc = 0;
-  for (int i = 0; i < lkf_engine::kCtx; i++) {
-    BatchCtx &x = e->ctx[i];
-    if (!x.used || (x.checked && i != e->lastCtx)) continue;
-    uint32_t err[4] = {0, 0, 0, 0};
-    HIPCHK(hipMemcpy(err, x.dErr, sizeof(err), hipMemcpyDeviceToHost), "err copy");
-    x.checked = true;
-    acc |= err[0];
+  HIPCHK(hipMemcpy(&acc, e->dSticky, sizeof(acc), hipMemcpyDeviceToHost), "err copy");
+  if (!acc) return LKF_OK;
+  HIPCHK(hipMemset(e->dSticky, 0, sizeof(uint32_t)), "err reset");
+  HIPCHK(hipDeviceSynchronize(), "err reset sync");  // null-stream memset vs the engine's streams
+  if (acc & (3u << 4)) {
+    e->err = "raw batch not grouped by track / bad stream handle";
+    return LKF_EORDER;
   }
   if (acc & 3u) {
     e->err = "batch not grouped by track / bad track handle";
@@ -1074,7 +1075,7 @@ int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *i) {
   h.extFirstTS = i->ext_first_ts;
   h.refTSOffset = i->ref_ts_offset;
   HIPCHK(hipMemcpy(e->dHot + dt, &h, sizeof(h), hipMemcpyHostToDevice), "seed copy");
-  return LKF_OK;
+  return upload_done(e);
 }
 
 int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns, lkf_seq_meta *out,
@@ -1093,6 +1094,8 @@ int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, i
   }
   if (!e->dSeqN) HIPCHK(dalloc(&e->dSeqN, 1), "alloc");
   if (n) HIPCHK(hipMemcpy(e->dSns, sns, n * sizeof(uint16_t), hipMemcpyHostToDevice), "sns copy");
+  rc = upload_done(e);
+  if (rc) return rc;
   HIPCHK(launch_seq_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, uint32_t(dt), e->dSns, n, now_ns / 1000000,
                            e->dSeqOut, e->dSeqN),
          "seq lookup");
@@ -1200,8 +1203,8 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.total = e->dITotal;
   a.out = x.dPktsOwn;
   HIPCHK(launch_ingest(s, a), "ingest");
+  HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 4), "ingest error fold");
   e->lastIngestN = n;
-  e->ingestUnchecked = true;
   e->curPkts = x.dPktsOwn;
   e->curN = n;  // launch bound; the count is e->dITotal
   e->curNDev = e->dITotal;
@@ -1222,6 +1225,8 @@ int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
   if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->prepS),
                 "raw pkts");
   if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->prepS), "raw arena");
+  // host buffers are reusable when lkf_ingest returns (the header's contract)
+  HIPCHK(hipStreamSynchronize(e->prepS), "ingest copy sync");
   return ingest_common(e, x, x.dRawPkts, n, x.dArenaOwn, raw_len);
 }
 

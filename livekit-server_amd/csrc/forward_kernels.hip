@@ -2506,9 +2506,21 @@ hipError_t launch_stats_reduce(hipStream_t s, u64 *stats) {
   return hipGetLastError();
 }
 
-__global__ void k_accumulate(const u64 *stats, const u64 *tot, u64 *cum) {
+__global__ void k_accumulate(const u64 *stats, const u64 *tot, u64 *cum, const u32 *err, u32 *sticky) {
   const int i = threadIdx.x;
   if (i < 4 + LKF_DROP_NREASONS) cum[i] += (i == 3) ? tot[3] : stats[i];
+  if (i == 0 && err[0]) sticky[0] |= err[0] & 0xfu;  // one lane: no race within the launch
+}
+
+// ORs an error word into the engine's sticky word (shifted), stream-ordered
+// after the kernels that set it
+__global__ void k_err_fold(const u32 *err, u32 *sticky, u32 shift) {
+  if (threadIdx.x == 0 && err[0]) sticky[0] |= (err[0] & 0xfu) << shift;
+}
+
+hipError_t launch_err_fold(hipStream_t s, const u32 *err, u32 *sticky, u32 shift) {
+  hipLaunchKernelGGL(k_err_fold, dim3(1), dim3(64), 0, s, err, sticky, shift);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -2654,8 +2666,8 @@ hipError_t launch_h2d(hipStream_t s, void *dstA, const void *srcA, size_t nA, vo
   return hipGetLastError();
 }
 
-hipError_t launch_accumulate(hipStream_t s, const u64 *stats, const u64 *tot, u64 *cum) {
-  hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, s, stats, tot, cum);
+hipError_t launch_accumulate(hipStream_t s, const u64 *stats, const u64 *tot, u64 *cum, const u32 *err, u32 *sticky) {
+  hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, s, stats, tot, cum, err, sticky);
   return hipGetLastError();
 }
 

@@ -100,7 +100,9 @@ hipError_t launch_h2d(hipStream_t s, void *dstA, const void *srcA, size_t nA, vo
 hipError_t launch_stats_reduce(hipStream_t s, uint64_t *stats);
 // dense per-lane op offsets from the lane-sorted op list: off[l] = first op with lane >= l
 hipError_t launch_ev_offsets(hipStream_t s, const uint32_t *laneOf, uint32_t nev, uint32_t nl, uint32_t *off);
-hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum);
+hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum,
+                             const uint32_t *err, uint32_t *sticky);
+hipError_t launch_err_fold(hipStream_t s, const uint32_t *err, uint32_t *sticky, uint32_t shift);
 hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint32_t d,
                              const uint16_t *sns, uint32_t n, int64_t nowMs, lkf_seq_meta *out, uint32_t *nOut);
 

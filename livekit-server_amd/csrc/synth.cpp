@@ -92,6 +92,7 @@ struct lkfs_trace {
   u32 max_batch_pkts = 0;
   u64 max_batch_arena = 0;
   u64 max_batch_tuples = 0;
+  u64 max_batch_out_bytes = 0;  // bound on one batch's output arena (every tuple forwarded)
 };
 
 static void fill_payload(u8 *dst, int n, u64 key) {
@@ -607,10 +608,16 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
     std::vector<u64> dtsPerTrack(tg.size(), 0);
     for (auto &d : tr->dts) dtsPerTrack[d.track]++;
     for (u32 b = 0; b < nb; b++) {
-      u64 tup = 0;
-      for (size_t ti = 0; ti < tg.size(); ti++)
+      u64 tup = 0, ob = 0;
+      const lkf_pkt *bp = tr->pkts.data() + tr->batch_pkt_off[b];
+      for (size_t ti = 0; ti < tg.size(); ti++) {
         tup += u64(trackRange[b][ti].second - trackRange[b][ti].first) * dtsPerTrack[ti];
+        u64 tb = 0;  // wire packet <= payload + 12-B header + 12-B extension block + 1 (descriptor growth), 16-B aligned
+        for (u32 i = trackRange[b][ti].first; i < trackRange[b][ti].second; i++) tb += (u64(bp[i].payload_len) + 25 + 15) & ~u64(15);
+        ob += tb * dtsPerTrack[ti];
+      }
       tr->max_batch_tuples = std::max(tr->max_batch_tuples, tup);
+      tr->max_batch_out_bytes = std::max(tr->max_batch_out_bytes, ob);
     }
   }
   // ---- events -> (batch, at_pkt) -------------------------------------
@@ -682,3 +689,4 @@ extern "C" uint64_t lkfs_total_arena(const lkfs_trace *t) { return t->arena.size
 extern "C" uint32_t lkfs_max_batch_pkts(const lkfs_trace *t) { return t->max_batch_pkts; }
 extern "C" uint64_t lkfs_max_batch_arena(const lkfs_trace *t) { return t->max_batch_arena; }
 extern "C" uint64_t lkfs_max_batch_tuples(const lkfs_trace *t) { return t->max_batch_tuples; }
+extern "C" uint64_t lkfs_max_batch_out_bytes(const lkfs_trace *t) { return t->max_batch_out_bytes; }

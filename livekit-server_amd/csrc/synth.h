@@ -62,6 +62,8 @@ uint32_t lkfs_max_batch_pkts(const lkfs_trace *t);
 uint64_t lkfs_max_batch_arena(const lkfs_trace *t);
 /* max over batches of sum over DownTracks of their track's packets */
 uint64_t lkfs_max_batch_tuples(const lkfs_trace *t);
+/* max over batches of the output arena if every tuple were forwarded */
+uint64_t lkfs_max_batch_out_bytes(const lkfs_trace *t);
 /* Ingress view: one stream per received SSRC, and batch b as raw datagrams
  * (the same packets as lkfs_batch, offsets into the same arena). */
 uint32_t lkfs_num_streams(const lkfs_trace *t);

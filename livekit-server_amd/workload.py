@@ -32,6 +32,7 @@ class Trace:
         self.max_batch_pkts = self.lib.lkfs_max_batch_pkts(self.h)
         self.max_batch_arena = self.lib.lkfs_max_batch_arena(self.h)
         self.max_batch_tuples = self.lib.lkfs_max_batch_tuples(self.h)
+        self.max_batch_out_bytes = self.lib.lkfs_max_batch_out_bytes(self.h)
         self.nstreams = self.lib.lkfs_num_streams(self.h)
         self.streams = self.lib.lkfs_streams(self.h)
 

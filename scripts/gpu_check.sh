@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 OUT=gpurun_out
 make -s -C oracle clean all > $OUT/build.log 2>&1 || { echo "oracle build failed"; exit 2; }
 make -s -C livekit-server_amd/csrc >> $OUT/build.log 2>&1 || { echo "engine build failed"; exit 2; }
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

@@ -45,6 +45,19 @@ def main():
         c = out[k]
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             out[k.split("::")[-1] + "_hbm_bytes_per_launch"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+    # whole-step traffic: every engine kernel's bytes over all its dispatches,
+    # per batch (one k_decide_dt dispatch per batch)
+    nsteps = out.get("lkf::k_decide_dt", {}).get("_dispatch_samples", 0)
+    if nsteps:
+        tot = 0.0
+        for k, c in out.items():
+            if k.startswith("lkf::") and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                tot += (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 * c["_dispatch_samples"]
+        out["hbm_bytes_per_step"] = int(tot / nsteps)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_sources_sha
+    out["kernel_sources_sha"] = kernel_sources_sha()
+    out["bench_args_rooms"] = int(os.environ.get("PMC_ROOMS", "100"))
     json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
     if "--delete-raw" in sys.argv:

@@ -28,7 +28,7 @@ def _state_tuple(api, h, dt, abi):
     return st.as_tuple()
 
 
-def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True):
+def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True, extra_ops=None):
     o = load_oracle()
     eng = pkg.Engine.for_trace(trace)
     oh = o.create(500)
@@ -39,6 +39,9 @@ def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True):
         for b in range(trace.nbatches):
             workload.queue_events(eng.api, eng.h, trace, b)
             workload.queue_events(o.api, oh, trace, b)
+            for (dt, op, a0, a1, a2, a3, at) in (extra_ops or {}).get(b, ()):
+                assert eng.api["ctl"](eng.h, dt, op, a0, a1, a2, a3, at) == 0
+                assert o.api["ctl"](oh, dt, op, a0, a1, a2, a3, at) == 0
             pk, n, ar, alen = trace.batch(b)
             eng.submit(pk, n, ar, alen)
             eng.run()
@@ -172,5 +175,82 @@ def test_ungrouped_batch_rejected(pkg, workload, abi):
         eng.run()
         with pytest.raises(pkg.EngineError):
             eng.sync()
+    finally:
+        eng.close()
+
+
+def test_ops_out_of_order_and_equal_at(pkg, workload, abi):
+    """Several ops for one DownTrack queued out of at_pkt order and with equal
+    at_pkt: applied in (at_pkt, queue order) like the oracle's stable sort."""
+    tr = workload.Trace(1, duration_s=3.0, batch_s=1.0)
+    MUTE, MAXT, ALLOC = 1, 4, 7
+    ops = {1: [(0, ALLOC, 1, 2, 1, 0, 900), (0, MAXT, 1, 0, 0, 0, 200), (0, MUTE, 1, 1, 0, 0, 900),
+               (0, MUTE, 0, 1, 0, 0, 600), (0, MUTE, 1, 1, 0, 0, 200), (0, MAXT, 2, 0, 0, 0, 1500),
+               (2, ALLOC, 0, 1, 0, 1, 50), (2, ALLOC, 2, 2, 2, 0, 50)],
+           2: [(0, MUTE, 0, 1, 0, 0, 0), (0, ALLOC, 2, 2, 2, 0, 0)]}
+    run_parity(pkg, workload, abi, tr, extra_ops=ops)
+
+
+def test_pipelined_runs_match_oracle(pkg, workload, abi):
+    """The bench's path: every batch queued back-to-back (three batch contexts,
+    staged control ops, decide(n+1) overlapping emit(n)) with one lkf_sync at
+    the end.  Cumulative counters must equal the oracle's summed per-batch
+    counters, and the last batch's records / wire bytes / final state must be
+    identical."""
+    tr = workload.Trace(2, duration_s=4.0, batch_s=0.5, rooms=4)
+    o = load_oracle()
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+        tot = None
+        for b in range(tr.nbatches):
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            eng.submit(pk, n, ar, alen)
+            eng.run()
+            o.run(oh, pk, n, ar, alen)
+            ost = abi.lkf_stats()
+            o.api["get_stats"](oh, C.byref(ost))
+            d = ost.as_dict()
+            if tot is None:
+                tot = d
+            else:
+                for k in ("tuples", "forwarded", "out_bytes", "arena_bytes"):
+                    tot[k] += d[k]
+                tot["drops"] = [x + y for x, y in zip(tot["drops"], d["drops"])]
+        assert tr.nbatches >= 6
+        eng.sync()
+        assert eng.cumulative() == tot
+        grec, gar = eng.drain()
+        orec, oar = _drain_oracle(o, oh)
+        assert np.array_equal(grec, orec) and np.array_equal(gar, oar)
+        for dt in range(tr.ndts):
+            assert _state_tuple(eng.api, eng.h, dt, abi) == _state_tuple(o.api, oh, dt, abi), dt
+    finally:
+        eng.close()
+        o.destroy(oh)
+
+
+def test_overflow_error_is_sticky(pkg, workload, abi):
+    """A tuple-capacity overflow in the first of six queued runs is still
+    reported (LKF_ENOSPC) by the lkf_sync after the sixth, then cleared."""
+    tr = workload.Trace(1, duration_s=1.0, batch_s=1.0)
+    eng = pkg.Engine(max_tracks=tr.ntracks + 8, max_downtracks=tr.ndts + 8,
+                     max_batch_pkts=tr.max_batch_pkts + 64, max_batch_arena=tr.max_batch_arena + 4096,
+                     max_batch_tuples=1000, max_out_pkts=1 << 16, max_out_bytes=64 << 20)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        pk, n, ar, alen = tr.batch(0)
+        assert n * 10 > 1000
+        eng.submit(pk, n, ar, alen)
+        eng.run()
+        for _ in range(5):
+            eng.run()  # control-only runs reuse every batch context
+        rc = eng.lib.lkf_sync(eng.h)
+        assert rc == -28, rc
+        assert eng.lib.lkf_sync(eng.h) == 0
     finally:
         eng.close()
