@@ -278,7 +278,7 @@ def main():
             # the GPU box gives one GPU a 16-CPU share (os.cpu_count() is the whole host)
             thr = args.cpu_threads or min(16, os.cpu_count() or 1)
             v, secs, rooms, nbat = cpu_baseline(thr)
-            v1, secs1, rooms1, _ = cpu_baseline(1, sample_rooms=8)
+            v1, secs1, rooms1, _ = cpu_baseline(1, sample_rooms=32)
             cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": thr, "kind": "port",
                    "sample": "configs[1] shape: %d rooms x 10 participants, 4 s of media (%d batches incl. the "
                              "arrival tail), rooms sharded over %d threads (%.1f s wall); single thread: %d rooms, "

@@ -37,7 +37,8 @@ enum lkf_codec {
   LKF_CODEC_OPUS = 1,
   LKF_CODEC_VP8 = 2,  /* Simulcast selector + VP8 temporal selector + VP8 munger  forwarder.go:287-294 */
   LKF_CODEC_H264 = 3, /* Simulcast selector                                          :295-300 */
-  LKF_CODEC_VP9 = 4   /* SVC: VP9 selector (no dependency-descriptor ext)           :301-316 */
+  LKF_CODEC_VP9 = 4,  /* SVC: VP9 selector, or the DD selector with has_dd            :301-316 */
+  LKF_CODEC_AV1 = 5   /* SVC: DD selector with has_dd, else Simulcast                 :317-334 */
 };
 
 /* Control ops, applied to one DownTrack immediately before the first packet
@@ -99,6 +100,10 @@ typedef struct lkf_track_params {
   uint8_t is_mic;       /* TrackSource_MICROPHONE (uptrackmanager.go:425) */
   uint32_t clock_rate;
   uint32_t layer_offsets[3][3]; /* layerOffsets[ref][layer]; 0 = unavailable */
+  uint8_t has_dd;       /* the receiver negotiated the dependency-descriptor extension
+                           (Forwarder.DetermineCodec ddAvailable forwarder.go:278-285):
+                           VP9 / AV1 then use videolayerselector.DependencyDescriptor */
+  uint8_t reserved_tp[3];
 } lkf_track_params;
 
 /* One subscriber DownTrack (NewDownTrack downtrack.go:286 + Bind :362). */
@@ -150,6 +155,26 @@ typedef struct lkf_pkt {
 #define LKF_PKT_VP8 0x02        /* Payload is buffer.VP8 */
 #define LKF_PKT_HAS_LEVEL 0x04  /* audio_level valid */
 #define LKF_PKT_VP9 0x08        /* Payload is codecs.VP9Packet (spatial/temporal = SID/TID) */
+#define LKF_PKT_DD 0x10         /* ExtPacket.DependencyDescriptor != nil (spatial/temporal from
+                                   the DD; per-packet metadata in the lkf_pkt_dd side array) */
+
+/* buffer.ExtDependencyDescriptor (buffer/dependencydescriptorparser.go:63-73),
+ * 32 B, one per packet of a batch (entries of packets without LKF_PKT_DD are
+ * ignored).  The parsed descriptor itself is not passed: the engine reads the
+ * DD extension payload from the raw packet (dd_off/dd_len) with the track's
+ * current FrameDependencyStructure, as the Go parser did at ingress
+ * (DependencyDescriptorExtension.Unmarshal, dependencydescriptorreader.go). */
+typedef struct lkf_pkt_dd {
+  uint64_t ext_frame_num;      /* ExtFrameNum */
+  uint64_t ext_key_frame_num;  /* ExtKeyFrameNum */
+  uint16_t dd_off;             /* DD extension payload: offset within the raw RTP packet */
+  uint8_t dd_len;              /* and length (1..255) */
+  uint8_t flags;               /* LKF_DD_* */
+  uint32_t reserved[3];
+} lkf_pkt_dd;
+#define LKF_DD_STRUCTURE_UPDATED 0x01  /* StructureUpdated */
+#define LKF_DD_ACTIVE_UPDATED 0x02     /* ActiveDecodeTargetsUpdated */
+#define LKF_DD_INTEGRITY 0x04          /* Integrity (FrameIntegrityChecker) */
 
 /* codecs.VP9Packet flags (pion/rtp v1.8.3 codecs/vp9_packet.go); the first
  * seven are the descriptor's first byte I|P|L|F|B|E|V, U is from the layer
@@ -230,7 +255,8 @@ typedef struct lkf_stream_params {
    * defaults 35 / 40 / 400 ms / 2 */
   uint8_t active_level;
   uint8_t min_percentile;
-  uint8_t reserved;
+  uint8_t dd_ext;           /* negotiated dependency-descriptor extension id (buffer.go:191-201):
+                               the stream's DependencyDescriptorParser; 0 = none */
   uint32_t observe_duration_ms;
   uint32_t smooth_intervals;
 } lkf_stream_params;
@@ -263,7 +289,8 @@ typedef struct lkf_flow {
 #define LKF_FLOW_HAS_LOSS 0x08     /* flowState.HasLoss */
 #define LKF_FLOW_PADDING 0x10      /* padding-only packet dropped (buffer.go:439-460) */
 #define LKF_FLOW_FORWARD 0x20      /* an ExtPacket was produced (buffer.go:489) */
-#define LKF_FLOW_BAD 0x40          /* RTP unmarshal / codec parse failed (buffer.go:424, :632) */
+#define LKF_FLOW_BAD 0x40          /* RTP unmarshal / codec parse / DD parse failed (buffer.go:424,
+                                      :613-616, :632): getExtPacket returned nil */
 
 /* RTPStatsReceiver counters of one stream (rtpstats_receiver.go:76-241). */
 typedef struct lkf_stream_stats {
@@ -328,6 +355,11 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
  * arena_len must be readable device memory (their content is ignored). */
 int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const uint8_t *d_arena,
                       uint64_t arena_len);
+/* The lkf_pkt_dd side array of the batch just submitted (n == its packet
+ * count); required when the batch has LKF_PKT_DD packets.  Host form copies;
+ * device form has the lifetime of lkf_submit_device's buffers. */
+int lkf_submit_dd(lkf_engine *e, const lkf_pkt_dd *dd, uint32_t n);
+int lkf_submit_dd_device(lkf_engine *e, const lkf_pkt_dd *d_dd, uint32_t n);
 /* Runs the batch on `stream` (a hipStream_t, may be NULL): every DownTrack's
  * TrackSender.WriteRTP (downtrack.go:680-760) for every packet of its track.
  * Asynchronous; lkf_sync waits. */
@@ -389,6 +421,8 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
 /* The ExtPacket batch produced by the last ingest (host copy; the RTX bucket
  * and the host-side stream trackers read it). */
 int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out);
+/* Its lkf_pkt_dd side array (same order and count as lkf_ingested). */
+int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_out);
 int lkf_stream_stats_get(lkf_engine *e, int32_t stream, lkf_stream_stats *out);
 /* Room.GetActiveSpeakers (room.go:254-279) for every room at virtual time
  * now_ns: per participant the loudest active microphone track

@@ -37,7 +37,7 @@ class lkf_stream_params(C.Structure):
         ("audio_level_ext", C.c_uint8),
         ("active_level", C.c_uint8),
         ("min_percentile", C.c_uint8),
-        ("reserved", C.c_uint8),
+        ("dd_ext", C.c_uint8),
         ("observe_duration_ms", C.c_uint32),
         ("smooth_intervals", C.c_uint32),
     ]
@@ -101,6 +101,8 @@ class lkf_track_params(C.Structure):
         ("is_mic", C.c_uint8),
         ("clock_rate", C.c_uint32),
         ("layer_offsets", (C.c_uint32 * 3) * 3),
+        ("has_dd", C.c_uint8),
+        ("reserved_tp", C.c_uint8 * 3),
     ]
 
 
@@ -145,6 +147,17 @@ class lkf_pkt(C.Structure):
         ("audio_level", C.c_uint8),
         ("vp9_bits", C.c_uint8),
         ("reserved", C.c_uint8 * 8),
+    ]
+
+
+class lkf_pkt_dd(C.Structure):
+    _fields_ = [
+        ("ext_frame_num", C.c_uint64),
+        ("ext_key_frame_num", C.c_uint64),
+        ("dd_off", C.c_uint16),
+        ("dd_len", C.c_uint8),
+        ("flags", C.c_uint8),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 
@@ -255,6 +268,8 @@ class lkfs_event(C.Structure):
 
 
 assert C.sizeof(lkf_pkt) == 64, C.sizeof(lkf_pkt)
+assert C.sizeof(lkf_pkt_dd) == 32, C.sizeof(lkf_pkt_dd)
+assert C.sizeof(lkf_track_params) == 64, C.sizeof(lkf_track_params)
 assert C.sizeof(lkf_out) == 40, C.sizeof(lkf_out)
 
 OUT_DTYPE = np.dtype(
@@ -299,6 +314,8 @@ def bind_engine_api(lib, prefix):
                                      [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64])
     api["ingest_flows"] = _bind(lib, prefix + "ingest_flows", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["ingested"] = _bind(lib, prefix + "ingested", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
+    api["ingested_dd"] = _bind(lib, prefix + "ingested_dd", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
+    api["submit_dd"] = _bind(lib, prefix + "submit_dd", C.c_int, [e, C.c_void_p, C.c_uint32])
     api["stream_stats_get"] = _bind(lib, prefix + "stream_stats_get", C.c_int, [e, C.c_int32, P(lkf_stream_stats)])
     api["speakers"] = _bind(lib, prefix + "speakers", C.c_int, [e, C.c_int64, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     return api

@@ -1,0 +1,757 @@
+// dd_device.h — gfx950 device code of the dependency-descriptor path
+// (SURVEY.md §8(a) a9 + a16), included by forward_kernels.hip and
+// ingress_kernels.hip.
+//
+//   dd_parse        DependencyDescriptorExtension.Unmarshal
+//                   (dependencydescriptor/dependencydescriptorreader.go) into a
+//                   DDPkt, with the structure ring of the track; an attached
+//                   FrameDependencyStructure is written to a ring slot and its
+//                   decode targets sorted (ProcessFrameDependencyStructure,
+//                   buffer/dependencydescriptorparser.go:178-201)
+//   dd_marshal      DependencyDescriptorExtension.Marshal
+//                   (dependencydescriptor/dependencydescriptorwriter.go:40-515)
+//   dd_select       videolayerselector.DependencyDescriptor.Select
+//                   (videolayerselector/dependencydescriptor.go:65-355) with the
+//                   SelectorDecisionCache (selectordecisioncache.go), FrameChain
+//                   (framechain.go), DecodeTarget (decodetarget.go) and
+//                   FrameNumberWrapper (framenumberwrapper.go) as one DDState.
+//
+// Everything here is wave-uniform scalar code on one descriptor: the decide
+// kernel runs it on the broadcast packet with the DownTrack's DDState staged in
+// LDS (every lane computes the same values; same-value LDS writes).
+//
+// FrameChain callbacks: the reference registers FrameChain.OnExpectFrameChanged
+// in the decision cache for every unknown previous-in-chain frame and appends
+// the frame to the chain's expectFrames.  All registrations of one frame fire
+// together (on its first non-unknown decision, or when it ages out), and a
+// registration whose frame has left expectFrames (cleared on a chain-intact
+// frame) does nothing; a chain that is broken ignores them until a clearing
+// frame.  So each chain keeps the SET of frames it waits on: a decision for a
+// member removes it, and a non-forwarded decision breaks the chain.
+#pragma once
+#include "fwd_state.h"
+
+namespace lkf {
+namespace dd {
+
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+using i32 = int32_t;
+
+enum Err { OK = 0, EOFB, NO_STRUCTURE, TEMPLATE_WITHOUT_STRUCTURE, TOO_MANY, INVALID, LIMIT };
+
+__device__ __forceinline__ int bitwidth(u32 n) { return n ? 32 - __clz(int(n)) : 0; }
+
+// bitstreamreader.go
+struct BitR {
+  const u8 *buf;
+  int len, pos, remaining;
+  __device__ BitR(const u8 *b, int n) : buf(b), len(n), pos(0), remaining(n * 8) {}
+  __device__ int bits(int n, u64 &out) {
+    out = 0;
+    if (n < 0 || n > 64) return INVALID;
+    if (remaining < n) {
+      remaining -= n;
+      return EOFB;
+    }
+    int inFirst = remaining % 8;
+    remaining -= n;
+    if (n < inFirst) {
+      out = u64((buf[pos] >> (inFirst - n)) & ((1u << n) - 1));
+      return OK;
+    }
+    u64 r = 0;
+    if (inFirst > 0) {
+      n -= inFirst;
+      r = u64(buf[pos] & u8((1u << inFirst) - 1)) << n;
+      pos++;
+    }
+    while (n >= 8) {
+      n -= 8;
+      r |= u64(buf[pos]) << n;
+      pos++;
+    }
+    if (n > 0) r |= u64(buf[pos] >> (8 - n));
+    out = r;
+    return OK;
+  }
+  __device__ int flag(bool &b) {
+    u64 v;
+    const int e = bits(1, v);
+    b = v != 0;
+    return e;
+  }
+  __device__ bool ok() const { return remaining >= 0; }
+  __device__ int nonSymmetric(u32 numValues, u32 &out) {  // av1 ns(n)
+    out = 0;
+    if (numValues >= (1u << 31)) return INVALID;
+    const int w = bitwidth(numValues);
+    const u32 numMin = (1u << w) - numValues;
+    u64 v;
+    int e = bits(w - 1, v);
+    if (e) return e;
+    if (v < numMin) {
+      out = u32(v);
+      return OK;
+    }
+    u64 b;
+    e = bits(1, b);
+    if (e) return e;
+    out = u32((v << 1) + b - numMin);
+    return OK;
+  }
+};
+
+__device__ __forceinline__ u32 dti_at(u64 dtis, int i) { return u32(dtis >> (2 * i)) & 3u; }
+
+// ProcessFrameDependencyStructure: decode-target layers = max (S, T) over the
+// templates that are present in the target; sorted high -> low by
+// VideoLayer.GreaterThan (insertion sort: Go's pdqsort below 12 elements)
+__device__ inline void process_structure(DDStruct &s) {
+  for (int t = 0; t < s.numDT; t++) {
+    int ls = 0, lt = 0;
+    for (int k = 0; k < s.numTmpl; k++)
+      if (dti_at(s.t[k].dtis, t) != 0) {
+        if (ls < s.t[k].sid) ls = s.t[k].sid;
+        if (lt < s.t[k].tid) lt = s.t[k].tid;
+      }
+    s.dtTarget[t] = u8(t);
+    s.dtS[t] = u8(ls);
+    s.dtT[t] = u8(lt);
+  }
+  for (int i = 1; i < s.numDT; i++)
+    for (int j = i; j > 0; j--) {
+      const bool gt = s.dtS[j] > s.dtS[j - 1] || (s.dtS[j] == s.dtS[j - 1] && s.dtT[j] > s.dtT[j - 1]);
+      if (!gt) break;
+      u8 a = s.dtTarget[j], b = s.dtS[j], c = s.dtT[j];
+      s.dtTarget[j] = s.dtTarget[j - 1];
+      s.dtS[j] = s.dtS[j - 1];
+      s.dtT[j] = s.dtT[j - 1];
+      s.dtTarget[j - 1] = a;
+      s.dtS[j - 1] = b;
+      s.dtT[j - 1] = c;
+    }
+}
+
+// templateStructure (dependencydescriptorreader.go readTemplateDependencyStructure)
+__device__ inline int read_structure(BitR &b, DDStruct &s) {
+  u64 v;
+  int e;
+  if ((e = b.bits(6, v))) return e;
+  s.structureId = u8(v);
+  if ((e = b.bits(5, v))) return e;
+  s.numDT = u8(v + 1);
+  s.numTmpl = 0;
+  s.numRes = 0;
+  int tid = 0, sid = 0;
+  for (;;) {
+    if (s.numTmpl == 64) return TOO_MANY;
+    DDTmpl &t = s.t[s.numTmpl++];
+    t.sid = u8(sid);
+    t.tid = u8(tid);
+    t.nfd = 0;
+    t.chains = 0;
+    t.dtis = 0;
+    if ((e = b.bits(2, v))) return e;
+    const int idc = int(v);
+    if (idc == 1) {
+      if (++tid >= 8) return TOO_MANY;
+    } else if (idc == 2) {
+      sid++;
+      tid = 0;
+      if (sid >= 4) return TOO_MANY;
+    }
+    if (!(idc != 3 && b.ok())) break;
+  }
+  for (int k = 0; k < s.numTmpl; k++)
+    for (int i = 0; i < s.numDT; i++) {
+      if ((e = b.bits(2, v))) return e;
+      s.t[k].dtis |= v << (2 * i);
+    }
+  for (int k = 0; k < s.numTmpl; k++)
+    for (;;) {
+      bool follow;
+      if ((e = b.flag(follow))) return e;
+      if (!follow) break;
+      if ((e = b.bits(4, v))) return e;
+      if (s.t[k].nfd >= kDDTmplFdiffs) return LIMIT;
+      s.t[k].fd[s.t[k].nfd++] = u8(v + 1);
+    }
+  u32 nc;
+  if ((e = b.nonSymmetric(u32(s.numDT) + 1, nc))) return e;
+  if (nc > u32(kDDChains)) return LIMIT;
+  s.numChains = u8(nc);
+  if (nc) {
+    for (int i = 0; i < s.numDT; i++) {
+      u32 pb;
+      if ((e = b.nonSymmetric(nc, pb))) return e;
+      s.protectedBy[i] = u8(pb);
+    }
+    for (int k = 0; k < s.numTmpl; k++)
+      for (u32 c = 0; c < nc; c++) {
+        if ((e = b.bits(4, v))) return e;
+        s.t[k].chains |= u32(v) << (4 * c);
+      }
+  }
+  bool hasRes;
+  if ((e = b.flag(hasRes))) return e;
+  if (hasRes) {
+    const int layers = s.t[s.numTmpl - 1].sid + 1;
+    for (int i = 0; i < layers; i++) {
+      u64 w, h;
+      if ((e = b.bits(16, w))) return e;
+      if ((e = b.bits(16, h))) return e;
+      s.resW[i] = u16(w + 1);
+      s.resH[i] = u16(h + 1);
+    }
+    s.numRes = u8(layers);
+  }
+  process_structure(s);
+  return OK;
+}
+
+// Parse: buf/len = the DD extension payload; cur = the track's current
+// structure (nullptr before any); att = the ring slot an attached structure is
+// written to.  On success o holds the descriptor and *usedAttached tells
+// whether att became the structure.
+__device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDStruct *att, DDPkt &o,
+                               bool &usedAttached) {
+  usedAttached = false;
+  BitR b(buf, len);
+  u64 v;
+  int e;
+  bool first, last;
+  if ((e = b.flag(first)) || (e = b.flag(last))) return e;
+  if ((e = b.bits(6, v))) return e;
+  const int templateId = int(v);
+  if ((e = b.bits(16, v))) return e;
+  o.frameNumber = u16(v);
+  o.flags = u8((first ? DP_FIRST : 0) | (last ? DP_LAST : 0));
+  bool structPresent = false, activePresent = false, customDtis = false, customFdiffs = false, customChains = false;
+  if (b.len > 3) {
+    if ((e = b.flag(structPresent)) || (e = b.flag(activePresent)) || (e = b.flag(customDtis)) ||
+        (e = b.flag(customFdiffs)) || (e = b.flag(customChains)))
+      return e;
+    if (structPresent) {
+      if ((e = read_structure(b, *att))) return e;
+      usedAttached = true;
+      o.flags |= DP_ATTACHED | DP_ACTIVE;
+      o.activeMask = u32((u64(1) << att->numDT) - 1);
+    }
+  }
+  const DDStruct *s = usedAttached ? att : cur;
+  if (!s) return NO_STRUCTURE;
+  if (activePresent) {
+    if ((e = b.bits(s->numDT, v))) return e;
+    o.flags |= DP_ACTIVE;
+    o.activeMask = u32(v);
+  }
+  // frameDependencyDefinition: the template, then the custom fields
+  const int idx = (templateId + 64 - s->structureId) % 64;
+  if (idx >= s->numTmpl) return INVALID;
+  const DDTmpl &t = s->t[idx];
+  o.sid = t.sid;
+  o.tid = t.tid;
+  o.dtis = t.dtis;
+  o.ndti = s->numDT;
+  if (t.nfd > kDDFdiffs) return LIMIT;
+  o.nfd = t.nfd;
+  for (int i = 0; i < t.nfd; i++) o.fd[i] = t.fd[i];
+  o.nchain = s->numChains;
+  o.chainDiffs = 0;
+  for (int c = 0; c < s->numChains; c++) o.chainDiffs |= u64((t.chains >> (4 * c)) & 0xf) << (8 * c);
+  if (customDtis) {
+    o.dtis = 0;
+    for (int i = 0; i < s->numDT; i++) {
+      if ((e = b.bits(2, v))) return e;
+      o.dtis |= v << (2 * i);
+    }
+  }
+  if (customFdiffs) {
+    o.nfd = 0;
+    for (;;) {
+      if ((e = b.bits(2, v))) return e;
+      if (v == 0) break;
+      u64 f;
+      if ((e = b.bits(int(v) * 4, f))) return e;
+      if (o.nfd >= kDDFdiffs) return LIMIT;
+      o.fd[o.nfd++] = u16(f + 1);
+    }
+  }
+  if (customChains) {
+    o.chainDiffs = 0;
+    for (int c = 0; c < s->numChains; c++) {
+      if ((e = b.bits(8, v))) return e;
+      o.chainDiffs |= v << (8 * c);
+    }
+  }
+  if (s->numRes && o.sid >= s->numRes) return INVALID;
+  return OK;
+}
+
+// ---- writer (dependencydescriptorwriter.go) ------------------------------------
+struct BitW {
+  u8 *buf;  // zero-initialised, cap bytes
+  int cap, bitPos;
+  __device__ BitW(u8 *b, int c) : buf(b), cap(c), bitPos(0) {}
+  __device__ int write(u64 val, int n) {  // MSB first
+    if (bitPos + n > cap * 8) return INVALID;
+    for (int i = n - 1; i >= 0; i--) {
+      if ((val >> i) & 1) buf[bitPos >> 3] |= u8(0x80u >> (bitPos & 7));
+      bitPos++;
+    }
+    return OK;
+  }
+  __device__ int nonSymmetric(u32 val, u32 numValues) {
+    if (!(val < numValues && numValues <= (1u << 31))) return INVALID;
+    if (numValues == 1) return OK;
+    const int w = bitwidth(numValues);
+    const u32 numMin = (1u << w) - numValues;
+    return val < numMin ? write(val, w - 1) : write(u64(val + numMin), w);
+  }
+};
+__device__ __forceinline__ int ns_bits(u32 val, u32 numValues) {
+  const int w = bitwidth(numValues);
+  const u32 numMin = (1u << w) - numValues;
+  return val < numMin ? w - 1 : w;
+}
+
+struct Match {
+  int idx;
+  bool cDtis, cFdiffs, cChains;
+  int extra;
+};
+
+// calculateMatch: frame DTIs / FrameDiffs are never nil after a parse (Clone);
+// a template's FrameDiffs is nil iff it has none (reflect.DeepEqual(nil, []) = false)
+__device__ inline Match dd_match(const DDStruct &s, int idx, const DDPkt &p) {
+  const DDTmpl &t = s.t[idx];
+  Match m;
+  m.idx = idx;
+  bool fdEq = t.nfd != 0 && t.nfd == p.nfd;
+  for (int i = 0; fdEq && i < p.nfd; i++) fdEq = p.fd[i] == t.fd[i];
+  m.cFdiffs = !fdEq;
+  const u64 dm = p.ndti >= 32 ? ~u64(0) : ((u64(1) << (2 * p.ndti)) - 1);
+  m.cDtis = !(p.ndti == s.numDT && (p.dtis & dm) == (t.dtis & dm));
+  m.cChains = false;
+  for (int i = 0; i < s.numChains; i++)
+    if (p.nchain <= i || u32((p.chainDiffs >> (8 * i)) & 0xff) != ((t.chains >> (4 * i)) & 0xf)) {
+      m.cChains = true;
+      break;
+    }
+  m.extra = 0;
+  if (m.cFdiffs) {
+    m.extra = 2 * (1 + p.nfd);
+    for (int i = 0; i < p.nfd; i++) m.extra += p.fd[i] <= 16 ? 4 : p.fd[i] <= 256 ? 8 : 12;
+  }
+  if (m.cDtis) m.extra += 2 * p.ndti;
+  if (m.cChains) m.extra += 8 * s.numChains;
+  return m;
+}
+
+__device__ inline int structure_bits(const DDStruct &s) {
+  int bits = 11;
+  const int nt = s.numTmpl;
+  bits += 2 * nt + 2 * nt * s.numDT + nt;
+  for (int k = 0; k < nt; k++) bits += 5 * s.t[k].nfd;
+  bits += ns_bits(s.numChains, u32(s.numDT) + 1);
+  if (s.numChains > 0) {
+    for (int i = 0; i < s.numDT; i++) bits += ns_bits(s.protectedBy[i], s.numChains);
+    bits += 4 * nt * s.numChains;
+  }
+  bits += 1 + 32 * s.numRes;
+  return bits;
+}
+
+// Marshal (activeChains = all): writes the descriptor to out (zeroed here),
+// returns its length in bytes, or -1 (error: the selector drops the frame).
+__device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive, u32 active,
+                                 u8 *out) {
+  // findBestTemplate
+  int first = -1;
+  for (int i = 0; i < s.numTmpl; i++)
+    if (s.t[i].sid == p.sid && s.t[i].tid == p.tid) {
+      first = i;
+      break;
+    }
+  if (first < 0) return -1;
+  int lastIdx = 0;  // as written: the last index whose layer differs
+  for (int i = first; i < s.numTmpl; i++)
+    if (s.t[i].sid != p.sid || s.t[i].tid != p.tid) lastIdx = i;
+  Match best = dd_match(s, first, p);
+  for (int i = first + 1; i <= lastIdx; i++) {
+    const Match m = dd_match(s, i, p);
+    if (m.extra < best.extra) best = m;
+  }
+  const bool attached = p.flags & DP_ATTACHED;
+  const u64 all = (u64(1) << s.numDT) - 1;
+  const bool writeActive = hasActive && !(attached && u64(active) == all);
+  const bool extended = best.extra > 0 || attached || hasActive;
+  int vbits = 1 + 1 + 6 + 16 + best.extra;
+  if (extended) {
+    vbits += 5;
+    if (attached) vbits += structure_bits(s);
+    if (writeActive) vbits += s.numDT;
+  }
+  const int nbytes = (vbits + 7) / 8;
+  if (nbytes > kDDMaxBytes) return -1;
+  for (int i = 0; i < nbytes; i++) out[i] = 0;
+  BitW w(out, nbytes);
+  int e = 0;
+  e |= w.write(p.flags & DP_FIRST ? 1 : 0, 1);
+  e |= w.write(p.flags & DP_LAST ? 1 : 0, 1);
+  e |= w.write(u64((best.idx + s.structureId) % 64), 6);
+  e |= w.write(frameNumber, 16);
+  if (extended) {
+    e |= w.write(attached ? 1 : 0, 1);
+    e |= w.write(writeActive ? 1 : 0, 1);
+    e |= w.write(best.cDtis ? 1 : 0, 1);
+    e |= w.write(best.cFdiffs ? 1 : 0, 1);
+    e |= w.write(best.cChains ? 1 : 0, 1);
+    if (attached) {
+      if (!(s.structureId < 64 && s.numDT > 0 && s.numDT <= 32)) return -1;
+      e |= w.write(s.structureId, 6);
+      e |= w.write(u64(s.numDT - 1), 5);
+      if (!(s.numTmpl > 0 && s.t[0].sid == 0 && s.t[0].tid == 0)) return -1;
+      for (int i = 1; i < s.numTmpl; i++) {
+        const DDTmpl &a = s.t[i - 1], &n = s.t[i];
+        int idc;
+        if (n.sid == a.sid && n.tid == a.tid)
+          idc = 0;
+        else if (n.sid == a.sid && n.tid == a.tid + 1)
+          idc = 1;
+        else if (n.sid == a.sid + 1 && n.tid == 0)
+          idc = 2;
+        else
+          return -1;
+        e |= w.write(u64(idc), 2);
+      }
+      e |= w.write(3, 2);
+      for (int k = 0; k < s.numTmpl; k++)
+        for (int i = 0; i < s.numDT; i++) e |= w.write(dti_at(s.t[k].dtis, i), 2);
+      for (int k = 0; k < s.numTmpl; k++) {
+        for (int i = 0; i < s.t[k].nfd; i++) e |= w.write((u64(1) << 4) | u64(s.t[k].fd[i] - 1), 5);
+        e |= w.write(0, 1);
+      }
+      e |= w.nonSymmetric(s.numChains, u32(s.numDT) + 1);
+      if (s.numChains) {
+        for (int i = 0; i < s.numDT; i++) e |= w.nonSymmetric(s.protectedBy[i], s.numChains);
+        for (int k = 0; k < s.numTmpl; k++)
+          for (int c = 0; c < s.numChains; c++) e |= w.write((s.t[k].chains >> (4 * c)) & 0xf, 4);
+      }
+      e |= w.write(s.numRes ? 1 : 0, 1);
+      for (int i = 0; i < s.numRes; i++) {
+        e |= w.write(u64(s.resW[i]) - 1, 16);
+        e |= w.write(u64(s.resH[i]) - 1, 16);
+      }
+    }
+    if (writeActive) e |= w.write(active, s.numDT);
+    if (best.cDtis)
+      for (int i = 0; i < p.ndti; i++) e |= w.write(dti_at(p.dtis, i), 2);
+    if (best.cFdiffs) {
+      for (int i = 0; i < p.nfd; i++) {
+        const u64 f = p.fd[i];
+        if (f <= 16)
+          e |= w.write((u64(1) << 4) | (f - 1), 6);
+        else if (f <= 256)
+          e |= w.write((u64(2) << 8) | (f - 1), 10);
+        else
+          e |= w.write((u64(3) << 12) | (f - 1), 14);
+      }
+      e |= w.write(0, 2);
+    }
+    if (best.cChains) {
+      // every chain is active (Marshal = MarshalWithActiveChains(^0)); a frame
+      // with fewer chain diffs than chains would index out of range (a
+      // recovered panic in the reference): the frame is dropped
+      if (p.nchain < s.numChains) return -1;
+      for (int c = 0; c < s.numChains; c++) e |= w.write((p.chainDiffs >> (8 * c)) & 0xff, 8);
+    }
+  }
+  return e ? -1 : nbytes;
+}
+
+// ---- selector ------------------------------------------------------------------
+enum SD : u32 { SD_MISSING = 0, SD_DROPPED = 1, SD_FORWARDED = 2, SD_UNKNOWN = 3 };
+constexpr u64 kEntries = 256, kNack = 80;
+
+__device__ __forceinline__ u32 c_get(const DDState &d, u64 e) {
+  const u64 off = (e - d.cBase) % kEntries;
+  return u32(d.masks[off >> 5] >> ((off & 31) * 2)) & 3u;
+}
+__device__ __forceinline__ void c_put(DDState &d, u64 e, u32 sd) {
+  const u64 off = (e - d.cBase) % kEntries;
+  const int bp = int(off & 31) * 2;
+  d.masks[off >> 5] = (d.masks[off >> 5] & ~(u64(3) << bp)) | (u64(sd & 3) << bp);
+}
+// callbacks of frame e firing with decision sd (see the header comment)
+__device__ inline void c_fire(DDState &d, u64 e, u32 sd) {
+  for (int c = 0; c < d.numChains; c++) {
+    if ((d.chBroken >> c) & 1) continue;
+    bool hit = false;
+    int n = d.expCount[c];
+    for (int i = 0; i < n;) {
+      if (d.exp[c][i] == e) {
+        hit = true;
+        d.exp[c][i] = d.exp[c][n - 1];
+        n--;
+      } else {
+        i++;
+      }
+    }
+    d.expCount[c] = u8(n);
+    if (hit && sd != SD_FORWARDED) d.chBroken |= u8(1u << c);
+  }
+}
+__device__ __forceinline__ void c_set(DDState &d, u64 e, u32 sd) {
+  c_put(d, e, sd);
+  if (sd != SD_UNKNOWN) c_fire(d, e, sd);
+}
+// GetDecision selectordecisioncache.go:78-94
+__device__ inline u32 c_decision(const DDState &d, u64 e, bool &tooOld) {
+  tooOld = false;
+  if (!(d.flags & DS_CACHE_INIT) || e < d.cBase) return SD_MISSING;
+  if (e > d.cLast) return SD_UNKNOWN;
+  if (d.cLast - e >= kEntries) {
+    tooOld = true;
+    return SD_MISSING;
+  }
+  return c_get(d, e);
+}
+// addEntity :112-165
+__device__ inline void c_add(DDState &d, u64 entity, u32 sd) {
+  if (!(d.flags & DS_CACHE_INIT)) {
+    d.flags |= DS_CACHE_INIT;
+    d.cBase = d.cLast = entity;
+    c_set(d, entity, sd);
+    return;
+  }
+  if (entity <= d.cBase) return;
+  if (entity <= d.cLast) {
+    c_set(d, entity, sd);
+    return;
+  }
+  // [last+1, entity) -> unknown (no callbacks); beyond 256 frames the ring is all unknown
+  const u64 gap = entity - d.cLast - 1;
+  if (gap >= kEntries) {
+    for (int i = 0; i < 8; i++) d.masks[i] = ~u64(0);
+  } else {
+    for (u64 e = d.cLast + 1; e != entity; e++) c_put(d, e, SD_UNKNOWN);
+  }
+  u64 ms = d.cLast, me = entity;
+  ms = ms > kNack + d.cBase ? ms - kNack : d.cBase;
+  me = me > kNack + d.cBase ? me - kNack : d.cBase;
+  if (me > ms) {
+    // each ring slot is first visited within the first 256 frames of the
+    // range; a later visit finds it missing already (not unknown)
+    const u64 n = me - ms < kEntries ? me - ms : kEntries;
+    for (u64 k = 0; k < n; k++)
+      if (c_get(d, ms + k) == SD_UNKNOWN) c_set(d, ms + k, SD_MISSING);
+  }
+  c_set(d, entity, sd);
+  d.cLast = entity;
+  // frames waited on that aged out of the window: missing
+  for (int c = 0; c < d.numChains; c++)
+    for (int i = 0; i < d.expCount[c];) {
+      const u64 e = d.exp[c][i];
+      if (e + kEntries < d.cLast) {
+        c_fire(d, e, SD_MISSING);
+        if (i < d.expCount[c] && d.exp[c][i] == e) i++;  // broken chain keeps its set
+      } else {
+        i++;
+      }
+    }
+}
+// ExpectDecision :96-110 + the chain's append
+__device__ inline bool c_expect(DDState &d, int c, u64 e, bool &overflow) {
+  if (!(d.flags & DS_CACHE_INIT) || e < d.cBase) return false;
+  if (e < d.cLast && d.cLast - e >= kEntries) return false;
+  for (int i = 0; i < d.expCount[c]; i++)
+    if (d.exp[c][i] == e) return true;
+  if (d.expCount[c] >= kDDExpect) {
+    overflow = true;
+    return true;
+  }
+  d.exp[c][d.expCount[c]++] = e;
+  return true;
+}
+
+// FrameChain.OnFrame framechain.go:43-92
+__device__ inline void chain_on_frame(DDState &d, int c, u64 efn, const DDPkt &p, bool &overflow) {
+  if (!((d.chActive >> c) & 1)) return;
+  if (p.nchain <= c) return;
+  const u32 diff = u32(p.chainDiffs >> (8 * c)) & 0xff;
+  if (diff == 0) {
+    d.chBroken &= u8(~(1u << c));
+    d.expCount[c] = 0;
+    return;
+  }
+  if ((d.chBroken >> c) & 1) return;
+  const u64 prev = efn - diff;
+  bool tooOld;
+  const u32 sd = c_decision(d, prev, tooOld);
+  bool intact = false;
+  if (sd == SD_FORWARDED)
+    intact = true;
+  else if (sd == SD_UNKNOWN)
+    intact = c_expect(d, c, prev, overflow);
+  if (!intact) d.chBroken |= u8(1u << c);
+}
+
+// updateDependencyStructure :363-392 (chains recreated: inactive, broken)
+__device__ inline void update_structure(DDState &d, const DDStruct &s, u8 slot, u64 efn) {
+  d.slot = slot;
+  d.extKeyFrameNum = efn;
+  d.flags |= DS_KF_VALID;
+  d.numChains = s.numChains;
+  d.chBroken = u8((1u << s.numChains) - 1);
+  d.chActive = 0;
+  d.chUpdating = 0;
+  for (int c = 0; c < kDDChains; c++) d.expCount[c] = 0;
+  d.numTargets = s.numDT;
+  d.dtActive = 0;
+}
+// updateActiveDecodeTargets :394-408 (+ FrameChain.Begin/EndUpdateActive)
+__device__ inline void update_active(DDState &d, const DDStruct &s, u32 mask) {
+  d.chUpdating = 0;
+  d.dtActive = 0;
+  for (int i = 0; i < d.numTargets; i++) {
+    const bool a = (mask >> s.dtTarget[i]) & 1;
+    if (a) d.dtActive |= 1u << i;
+    if (d.numChains > 0 && a) d.chUpdating |= u8(1u << s.protectedBy[s.dtTarget[i]]);
+  }
+  for (int c = 0; c < d.numChains; c++) {
+    const bool a = (d.chUpdating >> c) & 1, was = (d.chActive >> c) & 1;
+    if (a == was) continue;
+    if (!was) d.chBroken |= u8(1u << c);
+    d.chActive = a ? u8(d.chActive | (1u << c)) : u8(d.chActive & ~(1u << c));
+  }
+  d.chUpdating = 0;
+}
+// invalidateKeyFrame :410-416
+__device__ inline void invalidate_keyframe(DDState &d) {
+  d.flags &= ~u32(DS_KF_VALID);
+  d.numChains = 0;
+  d.numTargets = 0;
+}
+// FrameNumberWrapper.UpdateAndGet framenumberwrapper.go
+__device__ inline u64 fn_update(DDState &d, u64 nw, bool updateOffset) {
+  if (!(d.flags & DS_FN_INIT)) {
+    d.fnLast = nw;
+    d.flags |= DS_FN_INIT;
+    return nw;
+  }
+  if (nw <= d.fnLast) return nw + d.fnOffset;
+  if (updateOffset) {
+    const u16 n16 = u16(nw + d.fnOffset), l16 = u16(d.fnLast + d.fnOffset);
+    const u16 diff = u16(n16 - l16);
+    if (diff > 0x8000 || (diff == 0x8000 && n16 <= l16)) d.fnOffset += u64(65535 - diff + 6000);
+  }
+  d.fnLast = nw;
+  return nw + d.fnOffset;
+}
+
+struct SelResult {
+  bool selected, relevant, switching, resuming, marker;
+  int ddLen;  // marshalled bytes in the output buffer (selected only)
+  bool limit;  // an engine limit was hit (kDDExpect)
+};
+
+// Select :65-355.  Layers are the DownTrack's Base layers (DTHot); structs is
+// the track's structure ring; out receives the marshalled descriptor.
+__device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStruct *structs, const DDPkt &p, bool hasDD, bool pktMarker,
+                                      i32 &curS, i32 &curT, i32 &prevS, i32 &prevT, i32 tgtS, i32 tgtT, u8 *out) {
+  SelResult r = {false, false, false, false, false, 0, false};
+  if (curS != -1 && curT != -1) r.relevant = true;
+  if (!hasDD) return r;
+  const u64 efn = p.extFN;
+  const bool attached = p.flags & DP_ATTACHED;
+  if (!(d.flags & DS_KF_VALID) && !attached) return r;
+  bool tooOld;
+  const u32 sd = c_decision(d, efn, tooOld);
+  if (tooOld || sd == SD_DROPPED) return r;
+  if (p.extFlags & LKF_DD_STRUCTURE_UPDATED) update_structure(d, structs[p.slot], p.slot, efn);
+  if (p.extKFN != d.extKeyFrameNum) {
+    c_add(d, efn, SD_DROPPED);
+    invalidate_keyframe(d);
+    return r;
+  }
+  const DDStruct &s = structs[d.slot];
+  if (p.extFlags & LKF_DD_ACTIVE_UPDATED) update_active(d, s, p.activeMask);
+  if (p.nchain != d.numChains) {
+    c_add(d, efn, SD_DROPPED);
+    return r;
+  }
+  for (int c = 0; c < d.numChains; c++) chain_on_frame(d, c, efn, p, r.limit);
+  int hiPos = -1;
+  u32 dti = 0;
+  for (int i = 0; i < d.numTargets; i++) {
+    if (!((d.dtActive >> i) & 1) || i32(s.dtS[i]) > tgtS || i32(s.dtT[i]) > tgtT) continue;
+    const int target = s.dtTarget[i];
+    if (p.ndti <= target) {  // DecodeTarget.OnFrame error
+      c_add(d, efn, SD_DROPPED);
+      return r;
+    }
+    const bool valid = d.numChains == 0 || !((d.chBroken >> s.protectedBy[target]) & 1);
+    if (valid) {
+      hiPos = i;
+      dti = dti_at(p.dtis, target);
+      break;
+    }
+  }
+  if (hiPos < 0 || dti == 0) {
+    c_add(d, efn, SD_DROPPED);
+    return r;
+  }
+  for (int i = 0; i < p.nfd; i++) {
+    if (p.fd[i] == 0) continue;
+    bool old;
+    if (c_decision(d, efn - p.fd[i], old) == SD_DROPPED) {
+      c_add(d, efn, SD_DROPPED);
+      return r;
+    }
+  }
+  const i32 hs = s.dtS[hiPos], ht = s.dtT[hiPos];
+  if (curS != hs || curT != ht) {
+    r.switching = true;
+    if (curS == -1 || curT == -1) r.resuming = true;
+    prevS = curS;
+    prevT = curT;
+    curS = hs;
+    curT = ht;
+    if (d.flags & DS_HAS_MASK)
+      d.flags |= DS_HAS_PREV_MASK;
+    else
+      d.flags &= ~u32(DS_HAS_PREV_MASK);
+    d.prevMask = d.mask;
+    d.flags |= DS_HAS_MASK;
+    u32 m = 0;  // GetActiveDecodeTargetBitmask over ExtDependencyDescriptor.DecodeTargets (the parse-time structure)
+    const DDStruct &ps = structs[p.slot];
+    for (int i = 0; i < ps.numDT; i++)
+      if (i32(ps.dtS[i]) <= curS && i32(ps.dtT[i]) <= curT) m |= 1u << ps.dtTarget[i];
+    d.mask = m;
+    r.relevant = true;
+  }
+  const u16 fn = u16(fn_update(d, efn, p.extFlags & LKF_DD_STRUCTURE_UPDATED));
+  bool hasActive = p.flags & DP_ACTIVE;
+  u32 active = p.activeMask;
+  if (!attached && (d.flags & DS_HAS_MASK)) {
+    hasActive = true;
+    active = d.mask;
+  }
+  const int n = dd_marshal(s, p, fn, hasActive, active, out);
+  if (n < 0) {
+    c_add(d, efn, SD_DROPPED);
+    return r;
+  }
+  r.ddLen = n;
+  if (p.extFlags & LKF_DD_INTEGRITY) c_add(d, efn, SD_FORWARDED);
+  r.marker = pktMarker || ((p.flags & DP_LAST) && curS == i32(p.sid));
+  r.selected = true;
+  return r;
+}
+
+}  // namespace dd
+}  // namespace lkf

@@ -58,6 +58,12 @@ struct BatchCtx {
   lkf_pkt *dPktsOwn = nullptr;  // lkf_submit copies land here
   uint8_t *dArenaOwn = nullptr;
   lkf_raw_pkt *dRawPkts = nullptr;  // lkf_ingest copies land here
+  // dependency descriptor (allocated with the first DD track): lkf_submit_dd
+  // copies, decoded descriptors, marshalled DD bytes + their bump cursor
+  lkf_pkt_dd *dDDIn = nullptr;
+  DDPkt *dDDPkt = nullptr;
+  uint8_t *dDDArena = nullptr;
+  uint64_t *dDDUsed = nullptr;
   DevEvent *dEvents = nullptr;   // this batch's control ops (per-wave CSR)
   uint32_t *dEvOff = nullptr;
   uint32_t *dEvLane = nullptr;   // lane of each op (sorted), for k_ev_offsets
@@ -88,6 +94,7 @@ struct lkf_engine {
 
   // topology (host mirror)
   std::vector<lkf_track_params> tracks;
+  std::vector<uint32_t> trackDD;  // per track: DD table index or 0xffffffff
   std::vector<lkf_downtrack_params> dtp;
   std::vector<uint8_t> active;
   bool schedDirty = true;
@@ -135,12 +142,25 @@ struct lkf_engine {
   DevEvent *dEvents = nullptr;
   uint64_t evCap = 0;
   uint64_t *dCum = nullptr;
-  // sticky error word: every batch's decide/emit error bits (bits 0-3) and
-  // every ingest's error bits (<< 4) are OR-ed in on the GPU; lkf_sync reports
+  // sticky error word: every batch's decide/emit error bits (bits 0-7) and
+  // every ingest's error bits (<< 8) are OR-ed in on the GPU; lkf_sync reports
   // and clears it (per-context error words are reused every kCtx runs)
   uint32_t *dSticky = nullptr;
 
+  // dependency-descriptor selector tables (allocated with the first DD track)
+  uint32_t nDDTracks = 0;
+  bool ddAlloc = false;
+  uint64_t ddArenaCap = 0;
+  DDStruct *dDDStruct = nullptr;  // [ddIdx * kDDSlots + slot]
+  DDTrack *dDDTrack = nullptr;
+  DDState *dDDState = nullptr;    // per DownTrack
+  size_t ddStateInit = 0;         // DownTracks whose DDState is zeroed
+  uint32_t ddTrackInit = 0;
+  std::vector<uint8_t> dtIsDD;    // per DownTrack: scheduled in k_decide_dt<true>
+  uint32_t ddLanes = 0;
+
   // batch input for the next run
+  const lkf_pkt_dd *curDD = nullptr;
   const lkf_pkt *curPkts = nullptr;
   const uint8_t *curArena = nullptr;
   uint32_t curN = 0;
@@ -219,18 +239,26 @@ static void init_hot(DTHot &h, const lkf_track_params &tp, const lkf_downtrack_p
   if (tp.kind == LKF_KIND_VIDEO) {
     f |= F_VIDEO;
     h.maxT = 3;  // vls.SetMaxTemporal(DefaultMaxLayerTemporal) forwarder.go:235-237
+    const bool svc = tp.codec == LKF_CODEC_VP9 || tp.codec == LKF_CODEC_AV1;
     if (tp.codec == LKF_CODEC_VP8) f |= F_VP8 | F_SIMULCAST | F_TLS_VP8;
     if (tp.codec == LKF_CODEC_H264) f |= F_SIMULCAST;
-    if (tp.codec == LKF_CODEC_VP9) f |= F_VP9;
+    if (svc && tp.has_dd) f |= F_DD;                             // DependencyDescriptor :301-334
+    if (tp.codec == LKF_CODEC_VP9 && !tp.has_dd) f |= F_VP9;      // VP9 selector
+    if (tp.codec == LKF_CODEC_AV1 && !tp.has_dd) f |= F_SIMULCAST;  // AV1 without DD: Simulcast
   }
   if (p.has_expected_ts) f |= F_HAS_EXPECTED;
   h.flags = f;
   h.seqStartMs = p.bind_time_ns / 1000000;
 }
 
-static DevTrack to_dev_track(const lkf_track_params &p) {
+static bool track_has_dd(const lkf_track_params &p) {
+  return p.kind == LKF_KIND_VIDEO && p.has_dd && (p.codec == LKF_CODEC_VP9 || p.codec == LKF_CODEC_AV1);
+}
+
+static DevTrack to_dev_track(const lkf_track_params &p, uint32_t ddIdx) {
   DevTrack t;
   std::memset(&t, 0, sizeof(t));
+  t.ddIdx = ddIdx;
   t.kind = p.kind;
   t.codec = p.codec;
   t.hasRefTS = p.has_ref_ts;
@@ -290,11 +318,38 @@ static int upload_done(lkf_engine *e) {
   return LKF_OK;
 }
 
+// The DD selector tables and per-batch DD buffers, allocated when the first
+// track with the dependency-descriptor selector appears (streams drained).
+static int ensure_dd(lkf_engine *e) {
+  if (e->ddAlloc || e->nDDTracks == 0) return LKF_OK;
+  const lkf_cfg &c = e->cfg;
+  HIPCHK(dalloc(&e->dDDStruct, size_t(c.max_tracks) * kDDSlots), "alloc dd structures");
+  HIPCHK(dalloc(&e->dDDTrack, c.max_tracks), "alloc dd tracks");
+  HIPCHK(dalloc(&e->dDDState, c.max_downtracks), "alloc dd state");
+  HIPCHK(hipMemset(e->dDDTrack, 0, size_t(c.max_tracks) * sizeof(DDTrack)), "dd tracks reset");
+  e->ddArenaCap = c.max_out_bytes / 4 + (1u << 20);
+  for (auto &x : e->ctx) {
+    HIPCHK(dalloc(&x.dDDIn, c.max_batch_pkts), "alloc dd in");
+    HIPCHK(dalloc(&x.dDDPkt, c.max_batch_pkts), "alloc dd pkts");
+    HIPCHK(dalloc(&x.dDDArena, e->ddArenaCap), "alloc dd arena");
+    HIPCHK(dalloc(&x.dDDUsed, 1), "alloc dd cursor");
+  }
+  e->ddAlloc = true;
+  return LKF_OK;
+}
+
 // Uploads tracks / DownTracks added since the last flush (contiguous tails).
 static int flush_topology(lkf_engine *e) {
   if (e->pendTracks.empty() && e->pendDTs.empty() && e->pendStreams.empty()) return LKF_OK;
   int rc = drain_streams(e);
   if (rc) return rc;
+  rc = ensure_dd(e);
+  if (rc) return rc;
+  if (e->ddAlloc && e->ddStateInit < e->dtp.size()) {  // NewDependencyDescriptor: zero selector state
+    HIPCHK(hipMemset(e->dDDState + e->ddStateInit, 0, (e->dtp.size() - e->ddStateInit) * sizeof(DDState)),
+           "dd state reset");
+    e->ddStateInit = e->dtp.size();
+  }
   if (!e->pendTracks.empty()) {
     size_t first = e->tracks.size() - e->pendTracks.size();
     HIPCHK(hipMemcpy(e->dTracks + first, e->pendTracks.data(), e->pendTracks.size() * sizeof(DevTrack),
@@ -470,7 +525,13 @@ void lkf_destroy(lkf_engine *e) {
                   e->dSpkCounts};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
+                  static_cast<void *>(e->dDDState)})
+    if (p) (void)hipFree(p);
   for (auto &x : e->ctx) {
+    for (void *p : {static_cast<void *>(x.dDDIn), static_cast<void *>(x.dDDPkt), static_cast<void *>(x.dDDArena),
+                    static_cast<void *>(x.dDDUsed)})
+      if (p) (void)hipFree(p);
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
@@ -502,7 +563,10 @@ int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p) {
   if (e->tracks.size() >= e->cfg.max_tracks) return LKF_ENOSPC;
   int32_t h = int32_t(e->tracks.size());
   e->tracks.push_back(*p);
-  e->pendTracks.push_back(to_dev_track(*p));  // uploaded by flush_topology
+  uint32_t ddIdx = 0xffffffffu;
+  if (track_has_dd(*p)) ddIdx = e->nDDTracks++;
+  e->trackDD.push_back(ddIdx);
+  e->pendTracks.push_back(to_dev_track(*p, ddIdx));  // uploaded by flush_topology
   e->schedDirty = true;
   return h;
 }
@@ -514,7 +578,7 @@ int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9
   rc = drain_streams(e);
   if (rc) return rc;
   std::memcpy(e->tracks[track].layer_offsets, offsets, 9 * sizeof(uint32_t));
-  DevTrack t = to_dev_track(e->tracks[track]);
+  DevTrack t = to_dev_track(e->tracks[track], e->trackDD[track]);
   HIPCHK(hipMemcpy(e->dTracks + track, &t, sizeof(t), hipMemcpyHostToDevice), "offsets copy");
   return upload_done(e);
 }
@@ -526,6 +590,7 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
   int32_t h = int32_t(e->dtp.size());
   e->dtp.push_back(*p);
   e->active.push_back(1);
+  e->dtIsDD.push_back(track_has_dd(e->tracks[p->track]) ? 1 : 0);
   e->pendHot.emplace_back();
   init_hot(e->pendHot.back(), e->tracks[p->track], *p);
   DevDT d;
@@ -606,6 +671,7 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
   e->curArena = x.dArenaOwn;
   e->curN = n;
   e->curNDev = nullptr;
+  e->curDD = nullptr;
   e->ingestStarted = false;
   e->curArenaLen = arena_len;
   e->haveBatch = true;
@@ -619,9 +685,32 @@ int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const ui
   e->curArena = d_arena;
   e->curN = n;
   e->curNDev = nullptr;
+  e->curDD = nullptr;
   e->ingestStarted = false;
   e->curArenaLen = arena_len;
   e->haveBatch = true;
+  return LKF_OK;
+}
+
+int lkf_submit_dd(lkf_engine *e, const lkf_pkt_dd *dd, uint32_t n) {
+  if (!e || (n && !dd)) return LKF_EINVAL;
+  if (!e->haveBatch || n != e->curN) return LKF_EINVAL;  // parallel to the batch just submitted
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  if (!e->ddAlloc) return LKF_OK;  // no DD track: nothing reads it
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
+  if (x.used) HIPCHK(hipEventSynchronize(x.emitted), "wait emit");  // batch n-3 may still read it
+  if (n) HIPCHK(hipMemcpyAsync(x.dDDIn, dd, size_t(n) * sizeof(lkf_pkt_dd), hipMemcpyHostToDevice, e->own), "dd");
+  HIPCHK(hipStreamSynchronize(e->own), "submit dd sync");
+  e->curDD = x.dDDIn;
+  return LKF_OK;
+}
+
+int lkf_submit_dd_device(lkf_engine *e, const lkf_pkt_dd *d_dd, uint32_t n) {
+  if (!e || (n && !d_dd)) return LKF_EINVAL;
+  if (!e->haveBatch || n != e->curN) return LKF_EINVAL;
+  e->curDD = d_dd;
   return LKF_OK;
 }
 
@@ -637,16 +726,21 @@ static int rebuild_sched(lkf_engine *e) {
   for (uint32_t t = 0; t < nt; t++) order[t] = t;
   std::stable_sort(order.begin(), order.end(),
                    [&](uint32_t a, uint32_t b) { return e->tracks[a].kind > e->tracks[b].kind; });
-  e->sched.clear();
-  e->waveTrack.clear();
-  for (uint32_t t : order) {
-    const auto &v = byTrack[t];
-    for (uint32_t d : v) {  // one wave per DownTrack (interleaved per XCD below)
-      e->sched.push_back(d);
-      e->waveTrack.push_back(t);
+  // Two parts: DownTracks of the plain selectors (k_decide_dt<false>), then
+  // those of the dependency-descriptor selector (k_decide_dt<true>), each
+  // interleaved per XCD.
+  std::vector<uint32_t> sched, waveTrack;
+  e->ddLanes = 0;
+  for (int part = 0; part < 2; part++) {
+    std::vector<uint32_t> ps, pt;
+    for (uint32_t t : order) {
+      if ((e->trackDD[t] != 0xffffffffu) != (part == 1)) continue;
+      for (uint32_t d : byTrack[t]) {  // one wave per DownTrack (interleaved per XCD below)
+        ps.push_back(d);
+        pt.push_back(t);
+      }
     }
-  }
-  if (!e->sched.empty()) {
+    if (ps.empty()) continue;
     // Waves are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8).
     // Give all DownTracks of a track the same XCD, consecutive in its order,
     // so the 8-9 waves reading one track's packet descriptors share an L2.
@@ -656,16 +750,16 @@ static int rebuild_sched(lkf_engine *e) {
     std::vector<std::vector<uint32_t>> lst(kX), lstT(kX);
     std::vector<double> load(kX, 0.0);
     size_t i = 0;
-    while (i < e->sched.size()) {
-      const uint32_t t = e->waveTrack[i];
+    while (i < ps.size()) {
+      const uint32_t t = pt[i];
       size_t j = i;
-      while (j < e->sched.size() && e->waveTrack[j] == t) j++;
+      while (j < ps.size() && pt[j] == t) j++;
       int bx = 0;
       for (int x = 1; x < kX; x++)
         if (load[x] < load[bx]) bx = x;
       const double w = e->tracks[t].kind == LKF_KIND_VIDEO ? 7.0 : 1.0;  // ~packets per wave
       for (size_t q = i; q < j; q++) {
-        lst[bx].push_back(e->sched[q]);
+        lst[bx].push_back(ps[q]);
         lstT[bx].push_back(t);
         load[bx] += w;
       }
@@ -673,14 +767,18 @@ static int rebuild_sched(lkf_engine *e) {
     }
     size_t mx = 0;
     for (auto &l : lst) mx = std::max(mx, l.size());
-    e->sched.assign(mx * kX, kIdle);
-    e->waveTrack.assign(mx * kX, 0);
+    const size_t base = sched.size();
+    sched.resize(base + mx * kX, kIdle);
+    waveTrack.resize(base + mx * kX, 0);
     for (int x = 0; x < kX; x++)
       for (size_t q = 0; q < lst[x].size(); q++) {
-        e->sched[q * kX + x] = lst[x][q];
-        e->waveTrack[q * kX + x] = lstT[x][q];
+        sched[base + q * kX + x] = lst[x][q];
+        waveTrack[base + q * kX + x] = lstT[x][q];
       }
+    if (part == 1) e->ddLanes = uint32_t(mx * kX);
   }
+  e->sched.swap(sched);
+  e->waveTrack.swap(waveTrack);
   e->dtLane.assign(nd, -1);
   for (uint32_t l = 0; l < e->sched.size(); l++)
     if (e->sched[l] != kIdle) e->dtLane[e->sched[l]] = int32_t(l);
@@ -842,6 +940,12 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(launch_layer_index(ps, e->curPkts, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
                             x.dLayerBefore, x.dLayerCnt),
          "layer index");
+  if (e->ddAlloc) {  // dependency descriptors of this batch (track structure rings advance in order)
+    HIPCHK(hipMemsetAsync(x.dDDUsed, 0, sizeof(uint64_t), ps), "dd cursor reset");
+    HIPCHK(launch_dd_decode(ps, e->curPkts, e->curDD, e->curArena, x.dTBegin, x.dTEnd, e->dTracks, nt, e->dDDStruct,
+                            e->dDDTrack, x.dDDPkt, x.dErr),
+           "dd decode");
+  }
   HIPCHK(hipEventRecord(x.prepped, ps), "event");
   HIPCHK(hipStreamWaitEvent(s, x.prepped, 0), "wait prep");
   DecideLaunch d;
@@ -871,6 +975,13 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.fwdCnt = x.dFwdCnt;
   d.fwdBytes = x.dFwdBytes;
   d.stats = x.dStats;
+  d.ddLanes = e->ddLanes;
+  d.ddPkts = e->ddAlloc ? x.dDDPkt : nullptr;
+  d.ddStructs = e->dDDStruct;
+  d.ddState = e->ddAlloc ? e->dDDState : nullptr;
+  d.ddArena = x.dDDArena;
+  d.ddUsed = x.dDDUsed;
+  d.ddCap = e->ddArenaCap;
   HIPCHK(hipEventRecord(rg[1], s), "event");
   HIPCHK(launch_decide(s, d), "decide");
   HIPCHK(hipEventRecord(rg[2], s), "event");
@@ -902,6 +1013,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.outCap = e->cfg.max_out_pkts;
   m.outByteCap = e->cfg.max_out_bytes;
   m.err = x.dErr;
+  m.ddArena = e->ddAlloc ? x.dDDArena : nullptr;
   // One workgroup per 64-record group (grid = the capacity bound; workgroups
   // past the batch's records exit at once).  Short-lived workgroups free their
   // slots as they finish, so the next batch's decide stage (higher-priority
@@ -926,6 +1038,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   e->nRuns++;
   e->haveBatch = false;
   e->curNDev = nullptr;
+  e->curDD = nullptr;
   return LKF_OK;
 }
 
@@ -940,9 +1053,13 @@ int lkf_sync(lkf_engine *e) {
   if (!acc) return LKF_OK;
   HIPCHK(hipMemset(e->dSticky, 0, sizeof(uint32_t)), "err reset");
   HIPCHK(hipDeviceSynchronize(), "err reset sync");  // null-stream memset vs the engine's streams
-  if (acc & (3u << 4)) {
+  if (acc & (3u << 8)) {
     e->err = "raw batch not grouped by track / bad stream handle";
     return LKF_EORDER;
+  }
+  if (acc & 16u) {
+    e->err = "dependency descriptor unreadable, missing its lkf_pkt_dd entry, or beyond an engine limit";
+    return LKF_EINVAL;
   }
   if (acc & 3u) {
     e->err = "batch not grouped by track / bad track handle";
@@ -1203,11 +1320,12 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.total = e->dITotal;
   a.out = x.dPktsOwn;
   HIPCHK(launch_ingest(s, a), "ingest");
-  HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 4), "ingest error fold");
+  HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 8), "ingest error fold");
   e->lastIngestN = n;
   e->curPkts = x.dPktsOwn;
   e->curN = n;  // launch bound; the count is e->dITotal
   e->curNDev = e->dITotal;
+  e->curDD = nullptr;
   e->curArena = dRaw;
   e->curArenaLen = rawLen;
   e->haveBatch = true;
@@ -1268,6 +1386,29 @@ int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
   *n_out = n;
   if (cap < n) return LKF_ENOSPC;
   if (n) HIPCHK(hipMemcpy(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyDeviceToHost), "ingested copy");
+  return LKF_OK;
+}
+
+int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !n_out) return LKF_EINVAL;
+  uint32_t n = 0;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
+  if (e->haveBatch) {
+    n = e->curN;
+    if (e->curNDev) {
+      uint64_t t = 0;
+      HIPCHK(hipMemcpy(&t, e->curNDev, sizeof(t), hipMemcpyDeviceToHost), "count copy");
+      n = uint32_t(t);
+    }
+  }
+  *n_out = n;
+  if (cap < n) return LKF_ENOSPC;
+  if (!n) return LKF_OK;
+  if (e->curDD)
+    HIPCHK(hipMemcpy(out, e->curDD, size_t(n) * sizeof(lkf_pkt_dd), hipMemcpyDeviceToHost), "ingested dd copy");
+  else
+    std::memset(out, 0, size_t(n) * sizeof(lkf_pkt_dd));
   return LKF_OK;
 }
 

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/lkfwd.h"
+#include "dd_device.h"
 #include "fwd_state.h"
 #include "kernels.h"
 
@@ -187,7 +188,14 @@ struct Lane {
   u32 kind, codec, hasRefTS, clockRate;
   const u32 *offs;
   // static DT
-  u8 extPlayout, extAbs;
+  u8 extPlayout, extAbs, extDD;
+  // dependency-descriptor selector (F_DD): state staged in LDS, the track's
+  // structure ring, this batch's decoded descriptors, the marshal buffer
+  DDState *dd;
+  const DDStruct *ddRing;
+  const DDPkt *ddPkts;
+  u8 *ddBuf;
+  u32 *err;
 };
 
 __device__ __forceinline__ bool hasf(const Lane &L, u32 f) { return (L.h.flags & f) != 0; }
@@ -766,8 +774,9 @@ __device__ bool fw_sourceSwitch(Lane &L, const PktV &p, i32 layer) {
     i32 ref = L.h.referenceLayerSpatial;
     if (layer < 0 || layer >= 3 || ref < 0 || ref >= 3) return false;
     // isSVC (:667-671): one stream, one timeline -> offset 0
-    const u32 off = L.codec == LKF_CODEC_VP9 ? 0u : L.offs[ref * 3 + layer];
-    if (L.codec != LKF_CODEC_VP9 && layer != ref && off == 0) return false;
+    const bool svc = L.codec == LKF_CODEC_VP9 || L.codec == LKF_CODEC_AV1;  // IsSvcCodec receiver.go:142-150
+    const u32 off = svc ? 0u : L.offs[ref * 3 + layer];
+    if (!svc && layer != ref && off == 0) return false;
     u32 ts = u32(p.ets) + off;
     extRefTS = (extRefTS & 0xFFFFFFFF00000000ull) + u64(ts);
     u32 e32 = u32(extExpectedTS);
@@ -830,7 +839,15 @@ __device__ __forceinline__ int fw_common(Lane &L, const PktV &p, i32 layer, bool
   return -1;
 }
 
+template <bool DDK = false>
 __device__ __forceinline__ void vls_rollback(Lane &L) {  // base.go Rollback
+  if (DDK && hasf(L, F_DD)) {  // DependencyDescriptor.Rollback dependencydescriptor.go:357-361
+    L.dd->mask = L.dd->prevMask;
+    if (L.dd->flags & DS_HAS_PREV_MASK)
+      L.dd->flags |= DS_HAS_MASK;
+    else
+      L.dd->flags &= ~u32(DS_HAS_MASK);
+  }
   L.h.curS = L.h.prevS;
   L.h.curT = L.h.prevT;
   L.h.tgtS = L.h.ptgtS;
@@ -843,13 +860,18 @@ struct Fwd {
   bool switching, resuming, marker;
   int cbLen;
   u64 cb;  // munged VP8 descriptor bytes, little-endian packed
+  int ddLen;  // marshalled dependency descriptor in L.ddBuf (tp.ddBytes)
 };
 
 // Forwarder.GetTranslationParams forwarder.go:1436-1765 for one (packet, DownTrack).
-__device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
+// DDK: the instantiation for DownTracks with the dependency-descriptor
+// selector (k_decide_dt<true>); the others never compile its code.
+template <bool DDK>
+__device__ int fw_translate(Lane &L, const PktV &p, u32 k, Fwd &o) {
   o.switching = o.resuming = o.marker = false;
   o.cbLen = 0;
   o.cb = 0;
+  o.ddLen = 0;
   const i32 layer = p.layer;
   if (hasf(L, F_MUTED) || hasf(L, F_PUBMUTED)) return LKF_DROP_MUTED;
   if (!hasf(L, F_VIDEO)) return fw_common(L, p, layer, false, o.ord, o.osn, o.ots);
@@ -949,17 +971,38 @@ __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
       return LKF_DROP_NOT_SELECTED;
     }
   }
+  if (DDK && hasf(L, F_DD)) {  // DependencyDescriptor.Select videolayerselector/dependencydescriptor.go:65-355
+    DDPkt dp;
+    const bool hasDD = (p.flags & LKF_PKT_DD) && L.ddPkts && (L.ddPkts[k].flags & DP_VALID);
+    if (hasDD) dp = L.ddPkts[k];
+    const dd::SelResult r = dd::dd_select(*L.dd, L.ddRing, dp, hasDD, pktMarker, L.h.curS, L.h.curT, L.h.prevS,
+                                          L.h.prevT, L.h.tgtS, L.h.tgtT, L.ddBuf);
+    if (r.limit && lane_id() == 0) atomicOr(L.err, 16u);
+    if (!r.selected) {
+      if (r.relevant && hasf(L, F_STARTED)) {  // forwarder.go:1694-1702 (RTPMarker false)
+        int ord;
+        u64 a, b;
+        if (mg_update(L, p, false, ord, a, b) == MG_OK && ord == ORD_CONTIG) mg_packetDropped(L, p.esn);
+      }
+      return LKF_DROP_NOT_SELECTED;
+    }
+    isSelected = true;
+    isSwitching = r.switching;
+    isResuming = r.resuming;
+    marker = r.marker;
+    o.ddLen = r.ddLen;
+  }
   if (!isSelected) return LKF_DROP_NOT_SELECTED;  // IsRelevant == false for Simulcast
   o.resuming = isResuming;
   o.switching = isSwitching;
   o.marker = marker;
   if (hasf(L, F_DEFICIENT) && L.h.tgtS < L.h.curS) {  // FlagPauseOnDowngrade :1709
-    if (isSwitching) vls_rollback(L);
+    if (isSwitching) vls_rollback<DDK>(L);
     return LKF_DROP_DOWNGRADE;
   }
   int dr = fw_common(L, p, layer, marker, o.ord, o.osn, o.ots);
   if (dr >= 0 || p.plen == 0) {
-    if (isSwitching) vls_rollback(L);
+    if (isSwitching) vls_rollback<DDK>(L);
     return dr;
   }
   // vls.SelectTemporal base.go:143-168 + temporallayerselector/vp8.go:32-56
@@ -993,7 +1036,7 @@ __device__ int fw_translate(Lane &L, const PktV &p, Fwd &o) {
       cr = vp8_update(L, p, o.ord == ORD_OOO, o.ord == ORD_GAP, tl, o.cb, o.cbLen);
     if (cr != CM_OK) {
       if (cr == CM_FILTERED) mg_packetDropped(L, p.esn);
-      if (isSwitching || tSwitch) vls_rollback(L);
+      if (isSwitching || tSwitch) vls_rollback<DDK>(L);
       return cr == CM_FILTERED ? LKF_DROP_TEMPORAL : cr == CM_PICID_MISS ? LKF_DROP_PICID_MISS : LKF_DROP_OTHER;
     }
   }
@@ -1012,7 +1055,7 @@ __device__ __forceinline__ void store_rec(Tuple *dst, const Tuple &t) {  // 3 x 
   d[0] = make_uint4(u32(t.extSN), u32(t.extSN >> 32), u32(t.extTS), u32(t.extTS >> 32));
   d[1] = make_uint4(t.pkt, t.relOff, u32(t.outLen) | (u32(t.flags) << 16) | (u32(u8(t.layer)) << 24),
                     pack4(t.codecLen, t.codec[0], t.codec[1], t.codec[2]));
-  d[2] = make_uint4(pack4(t.codec[3], t.codec[4], t.codec[5], t.hdrLen), 0u, 0u, 0u);
+  d[2] = make_uint4(pack4(t.codec[3], t.codec[4], t.codec[5], t.ddLen), u32(t.hdrLen), t.ddOff, 0u);
 }
 __device__ __forceinline__ void store_rec(SeqMeta *dst, const SeqMeta &m) {  // 2 x dwordx4 (pad = 0)
   uint4 *d = reinterpret_cast<uint4 *>(dst);
@@ -1330,6 +1373,14 @@ struct DecideArgs {
   u64 *stats;  // lkf_stats as u64[15]
   const u32 *layerList, *layerBefore, *layerCnt;  // k_layer_index
   u32 pktStride;
+  u32 waveBase;  // schedule index of this launch's first wave
+  // dependency descriptor (F_DD DownTracks)
+  const DDPkt *ddPkts;
+  const DDStruct *ddStructs;
+  DDState *ddState;
+  u8 *ddArena;
+  u64 *ddUsed;
+  u64 ddCap;
 };
 
 // One wave per (track, <=64 DownTracks): the packet loop is wave-uniform, so
@@ -1341,8 +1392,12 @@ struct LaneOut {
   u64 nFwd, nBytes, nTuples;
   u32 relOff;
   u32 drops[LKF_DROP_NREASONS];
+  u8 *ddArena;  // this batch's marshalled DD bytes (bump-allocated)
+  u64 *ddUsed;
+  u64 ddCap;
 };
 
+template <bool DDK>
 __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneOut &o) {
   o.nTuples++;
 #if LKF_ABLATE == 3  // diagnostic: empty per-packet body (staging loop only)
@@ -1373,6 +1428,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   f.switching = f.resuming = false;
   f.cbLen = 0;
   f.cb = 0;
+  f.ddLen = 0;
   f.ord = ORD_CONTIG;
   int cls;  // -1 fast forward, -2 slow, >= 0 drop
   const i32 layer = p.layer;
@@ -1384,7 +1440,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   } else if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) {
     cls = LKF_DROP_PAUSED;
   } else if (!(fl & F_SIMULCAST)) {
-    cls = (fl & F_VP9) ? -2 : LKF_DROP_NOT_SELECTED;  // VP9: full step (relevant drops move the munger)
+    cls = (fl & (F_VP9 | F_DD)) ? -2 : LKF_DROP_NOT_SELECTED;  // SVC: full step (relevant drops move the munger)
   } else {
     const bool willSwitch =
         kf && ((L.h.curS != L.h.tgtS && ((layer > L.h.curS && layer <= L.h.tgtS) ||
@@ -1404,7 +1460,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   if (cls >= 0) {
     dr = cls;
   } else if (cls == -2) {
-    dr = fw_translate(L, p, f);
+    dr = fw_translate<DDK>(L, p, k, f);
   } else if (!(fl & F_VIDEO)) {
     f.marker = false;
     mg_inorder(L, p, false, f.osn, f.ots);
@@ -1452,10 +1508,14 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
     for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] += (dr == i) ? 1u : 0u;
     return;
   }
-  // ---- output shape (downtrack.go:693-723, pacer/base.go:71-100)
+  // ---- output shape (downtrack.go:693-723, pacer/base.go:71-100): the DD
+  // element first (pion picks the two-byte profile when it exceeds 16 B),
+  // then playout delay, then abs-send-time
   const int cc = p.hdr0 & 0xf;
   const bool playout = L.extPlayout && !hasf(L, F_PLAYOUT_ACKED);
-  int extBytes = (playout ? 4 : 0) + (L.extAbs ? 4 : 0);  // one-byte profile: 1 + 3 each
+  const bool ddOn = DDK && f.ddLen > 0 && L.extDD;
+  const int eh = (ddOn && f.ddLen > 16) ? 2 : 1;  // element header bytes
+  int extBytes = (ddOn ? eh + f.ddLen : 0) + (playout ? eh + 3 : 0) + (L.extAbs ? eh + 3 : 0);
   int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
   int hdrLen = 12 + 4 * cc + extBlock;
   const bool useCodec = f.cbLen > 0 && (p.flags & LKF_PKT_VP8);
@@ -1469,13 +1529,30 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   t.outLen = u16(hdrLen + payLen);
   t.flags = u8((f.switching ? LKF_OUT_SWITCHING : 0) | (f.resuming ? LKF_OUT_RESUMING : 0) |
                ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
-               (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0));
+               (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0) | (ddOn ? T_DD : 0));
   t.layer = p.layer;
   t.codecLen = u8(f.cbLen);
 #pragma unroll
   for (int i = 0; i < 6; i++) t.codec[i] = u8(f.cb >> (8 * i));
-  t.hdrLen = u8(hdrLen);
-  for (int i = 0; i < 12; i++) t.pad[i] = 0;
+  t.hdrLen = u16(hdrLen);
+  t.pad0 = 0;
+  t.pad1 = 0;
+  t.ddLen = ddOn ? u8(f.ddLen) : 0;
+  t.ddOff = 0;
+  if (DDK && ddOn) {  // the marshalled DD bytes go to the batch's DD arena (read by k_emit)
+    u64 off = 0;
+    if (lane_id() == 0) off = atomicAdd((unsigned long long *)o.ddUsed, (unsigned long long)f.ddLen);
+    off = rl64(off, 0);
+    if (off + u64(f.ddLen) > o.ddCap) {
+      if (lane_id() == 0) atomicOr(L.err, 8u);
+      t.flags &= u8(~T_DD);
+      t.ddLen = 0;
+    } else {
+      wave_lds_sync();
+      for (int i = int(lane_id()); i < f.ddLen; i += 64) o.ddArena[off + u64(i)] = L.ddBuf[i];
+      t.ddOff = u32(off);
+    }
+  }
 #if LKF_ABLATE != 1  // diagnostic builds only (never shipped): 1 = no tuple/sequencer writes
   if (lane_id() == 0) store_rec(o.outT + o.nFwd, t);  // wave-uniform record: one lane stores it
   // sequencer.push (downtrack.go:724-735)
@@ -1606,18 +1683,23 @@ __global__ void __launch_bounds__(64) k_layer_index(const lkf_pkt *__restrict__ 
   }
 }
 
+template <bool DDK>
 __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
   __shared__ i32 sDrop[kSetCap];
   __shared__ i32 sEx[kSetCap];
   __shared__ i32 sMissKey[kMissCap];
   __shared__ i32 sMissVal[kMissCap];
   __shared__ RangeEntry sRm[kRangeCap];
+  // (the plain instantiation keeps a 16-B stub: LDS is allocated per instantiation)
+  __shared__ __attribute__((aligned(16))) u8 sDDRaw[DDK ? sizeof(DDState) + kDDMaxBytes + 1 : 16];
+  DDState *const sDD = reinterpret_cast<DDState *>(sDDRaw);
+  u8 *const sDDBuf = sDDRaw + (DDK ? sizeof(DDState) : 0);
 #if LKF_DIAG
   const u64 tEntry = clock64();
 #endif
   const u32 lane = threadIdx.x;
   const u64 lt = (1ull << lane) - 1;
-  const u32 w = blockIdx.x;
+  const u32 w = A.waveBase + blockIdx.x;
   // Prologue: two rounds of independent loads.  Round 1 needs only the wave
   // index (DownTrack, track, control-op range); round 2 everything keyed by
   // them, including the VP8 munger maps (read whole, whatever their fill, so
@@ -1682,6 +1764,23 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.offs = tk.layerOffsets;
   L.extPlayout = dt.extPlayout;
   L.extAbs = dt.extAbs;
+  L.extDD = dt.extDD;
+  L.err = A.err;
+  L.ddPkts = A.ddPkts;
+  L.ddRing = nullptr;
+  L.dd = sDD;
+  L.ddBuf = sDDBuf;
+  o.ddArena = A.ddArena;
+  o.ddUsed = A.ddUsed;
+  o.ddCap = A.ddCap;
+  const bool ddDT = DDK && (L.h.flags & F_DD) && A.ddState;
+  if (ddDT) {  // the DD selector state lives in LDS for the batch
+    L.ddRing = A.ddStructs + size_t(tk.ddIdx) * kDDSlots;
+    const uint4 *g = reinterpret_cast<const uint4 *>(A.ddState + d);
+    uint4 *l = reinterpret_cast<uint4 *>(sDD);
+    for (u32 i = lane; i < sizeof(DDState) / 16; i += 64) l[i] = g[i];
+    __syncthreads();
+  }
   o.outT = A.tuples + slot0;
   u32 nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
@@ -1768,7 +1867,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       } else if (L.h.tgtS == INVALID || L.h.tgtT == INVALID) {
         cls = LKF_DROP_PAUSED;
       } else if (!(fl & F_SIMULCAST)) {
-        cls = (fl & F_VP9) ? -2 : LKF_DROP_NOT_SELECTED;  // VP9: full step
+        cls = (fl & (F_VP9 | F_DD)) ? -2 : LKF_DROP_NOT_SELECTED;  // SVC: full step
       } else {
         const bool willSwitch =
             kf && ((L.h.curS != L.h.tgtS && ((layer > L.h.curS && layer <= L.h.tgtS) ||
@@ -1945,9 +2044,11 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           t.codecLen = u8(video ? cbLen : 0);
 #pragma unroll
           for (int i = 0; i < 6; i++) t.codec[i] = u8(cb >> (8 * i));
-          t.hdrLen = u8(hdrLen);
-#pragma unroll
-          for (int i = 0; i < 12; i++) t.pad[i] = 0;
+          t.hdrLen = u16(hdrLen);
+          t.ddLen = 0;
+          t.pad0 = 0;
+          t.ddOff = 0;
+          t.pad1 = 0;
 #if LKF_ABLATE != 1
           store_rec(o.outT + o.nFwd + j, t);
 #endif
@@ -2070,7 +2171,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const uint4 a2 = make_uint4(rl32(r2.x, x), rl32(r2.y, x), rl32(r2.z, x), rl32(r2.w, x));
         const uint4 a3 = make_uint4(rl32(r3.x, x), rl32(r3.y, x), rl32(r3.z, x), rl32(r3.w, x));
         const u32 px = rl32(pi, x);
-        decide_step(L, decode_pkt(a0, a1, a2, a3), px, o);
+        decide_step<DDK>(L, decode_pkt(a0, a1, a2, a3), px, o);
 #if LKF_DIAG
         const u64 tdr0 = clock64();
 #endif
@@ -2114,6 +2215,12 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       const u32 idx = (L.h.rmHead + i) % kRangeCap;
       rmG[idx] = sRm[idx];
     }
+  }
+  if (ddDT) {
+    wave_lds_sync();
+    uint4 *g = reinterpret_cast<uint4 *>(A.ddState + d);
+    const uint4 *l = reinterpret_cast<const uint4 *>(sDD);
+    for (u32 i = lane; i < sizeof(DDState) / 16; i += 64) g[i] = l[i];
   }
   if (L.h.flags & F_VP8) {
     if (lane < u32(kSetCap)) {
@@ -2161,6 +2268,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 constexpr int EMIT_T = 64;
 constexpr int EMIT_G = 64;
 constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 descriptor = 90
+// batches with dependency-descriptor tracks: 12 + 60 CSRC + 4 + (2 + 255) DD + 2 x (2 + 3)
+// (two-byte extension profile) = 343
+constexpr int PRE_MAX_DD = 352;
 
 #ifndef LKF_EMIT_U
 #define LKF_EMIT_U 4  // 16-B chunks per lane per copy iteration (loads in flight together)
@@ -2187,6 +2297,7 @@ struct EmitArgs {
   u8 *outArena;
   u64 outCap, outByteCap;
   u32 *err;
+  const u8 *ddArena;  // marshalled DD bytes of T_DD tuples
 };
 
 __device__ __forceinline__ u32 align_byte(u32 hi, u32 lo, u32 sh) {
@@ -2221,8 +2332,9 @@ __device__ __forceinline__ void store16(u8 *p, uint4 v) {
 #endif
 }
 
+template <int PRE>
 __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
-  __shared__ __attribute__((aligned(16))) u8 pre[EMIT_G][PRE_MAX];
+  __shared__ __attribute__((aligned(16))) u8 pre[EMIT_G][PRE];
   __shared__ u64 sSrc[EMIT_G];  // arena offset of the record's first payload byte after the prefix
   __shared__ u32 sCs[EMIT_G];   // first chunk of the record, relative to the group
   __shared__ u32 sLen[EMIT_G];
@@ -2282,7 +2394,8 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       u8 *w = pre[lane];
       const int cc = p.hdr0 & 0xf;
       const bool playout = t.flags & T_PLAYOUT;
-      const bool hasExt = playout || dt.extAbs;
+      const bool ddOn = (PRE == PRE_MAX_DD) && (t.flags & T_DD);
+      const bool hasExt = playout || dt.extAbs || ddOn;
       w[0] = u8((p.hdr0 & 0xe0) | (hasExt ? 0x10 : 0) | cc);  // V, P copied; X per new extensions
       w[1] = u8(((t.flags & LKF_OUT_MARKER) ? 0x80 : 0) | (dt.pt & 0x7f));
       const u16 sn = u16(t.extSN);
@@ -2300,13 +2413,17 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       int n = 12;
       const u8 *raw = A.arena + p.arenaOff;
       for (int i = 0; i < 4 * cc; i++) w[n++] = raw[12 + i];
-      if (hasExt) {  // pion Header.MarshalTo one-byte profile (RFC 8285)
-        const int eb = (playout ? 4 : 0) + (dt.extAbs ? 4 : 0);
+      if (hasExt && !(ddOn && t.ddLen > 16)) {  // pion Header.MarshalTo one-byte profile (RFC 8285)
+        const int eb = (ddOn ? 1 + t.ddLen : 0) + (playout ? 4 : 0) + (dt.extAbs ? 4 : 0);
         const int words = (eb + 3) >> 2;
         w[n++] = 0xBE;
         w[n++] = 0xDE;
         w[n++] = u8(words >> 8);
         w[n++] = u8(words);
+        if (ddOn) {  // the DD element first (pacer/base.go:77-83)
+          w[n++] = u8((dt.extDD << 4) | (t.ddLen - 1));
+          for (int i = 0; i < t.ddLen; i++) w[n++] = A.ddArena[t.ddOff + i];
+        }
         if (playout) {
           w[n++] = u8((dt.extPlayout << 4) | 2);
           w[n++] = dt.playout[0];
@@ -2319,6 +2436,32 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
           w[n++] = 0;
           w[n++] = 0;
         }
+        for (int i = eb; i < 4 * words; i++) w[n++] = 0;
+      } else if (hasExt) {  // two-byte profile 0x1000: a DD element above 16 B
+        const int eb = 2 + t.ddLen + (playout ? 5 : 0) + (dt.extAbs ? 5 : 0);
+        const int words = (eb + 3) >> 2;
+        w[n++] = 0x10;
+        w[n++] = 0x00;
+        w[n++] = u8(words >> 8);
+        w[n++] = u8(words);
+        w[n++] = dt.extDD;
+        w[n++] = t.ddLen;
+        for (int i = 0; i < t.ddLen; i++) w[n++] = A.ddArena[t.ddOff + i];
+        if (playout) {
+          w[n++] = dt.extPlayout;
+          w[n++] = 3;
+          w[n++] = dt.playout[0];
+          w[n++] = dt.playout[1];
+          w[n++] = dt.playout[2];
+        }
+        if (dt.extAbs) {
+          w[n++] = dt.extAbs;
+          w[n++] = 3;
+          w[n++] = 0;
+          w[n++] = 0;
+          w[n++] = 0;
+        }
+        for (int i = eb; i < 4 * words; i++) w[n++] = 0;
       }
       u64 src = u64(p.arenaOff) + p.poff;
       if (t.flags & T_CODEC) {  // translateVP8PacketTo downtrack.go:1728-1736
@@ -2509,17 +2652,85 @@ hipError_t launch_stats_reduce(hipStream_t s, u64 *stats) {
 __global__ void k_accumulate(const u64 *stats, const u64 *tot, u64 *cum, const u32 *err, u32 *sticky) {
   const int i = threadIdx.x;
   if (i < 4 + LKF_DROP_NREASONS) cum[i] += (i == 3) ? tot[3] : stats[i];
-  if (i == 0 && err[0]) sticky[0] |= err[0] & 0xfu;  // one lane: no race within the launch
+  if (i == 0 && err[0]) sticky[0] |= err[0] & 0xffu;  // one lane: no race within the launch
 }
 
 // ORs an error word into the engine's sticky word (shifted), stream-ordered
 // after the kernels that set it
 __global__ void k_err_fold(const u32 *err, u32 *sticky, u32 shift) {
-  if (threadIdx.x == 0 && err[0]) sticky[0] |= (err[0] & 0xfu) << shift;
+  if (threadIdx.x == 0 && err[0]) sticky[0] |= (err[0] & 0xffu) << shift;
 }
 
 hipError_t launch_err_fold(hipStream_t s, const u32 *err, u32 *sticky, u32 shift) {
   hipLaunchKernelGGL(k_err_fold, dim3(1), dim3(64), 0, s, err, sticky, shift);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// k_dd_decode: the dependency descriptor of every LKF_PKT_DD packet, read from
+// its extension bytes with the track's current FrameDependencyStructure (as
+// the Go parser did at ingress, dependencydescriptorparser.go:86-97), into one
+// DDPkt per packet for k_decide_dt.  A structure attached to a packet goes to
+// the next slot of the track's ring and becomes current.  One thread per
+// track (packets of a track in order); runs on the prep stream, so batch n+1's
+// decode follows batch n's.
+// ---------------------------------------------------------------------------
+__global__ void k_dd_decode(const lkf_pkt *__restrict__ pkts, const lkf_pkt_dd *__restrict__ dds,
+                            const u8 *__restrict__ arena, const u32 *__restrict__ tBegin,
+                            const u32 *__restrict__ tEnd, const DevTrack *__restrict__ tracks, u32 ntracks,
+                            DDStruct *structs, DDTrack *ddTracks, DDPkt *__restrict__ out, u32 *err) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntracks) return;
+  const u32 ddIdx = tracks[t].ddIdx;
+  if (ddIdx == 0xffffffffu) return;
+  DDTrack st = ddTracks[ddIdx];
+  DDStruct *ring = structs + size_t(ddIdx) * kDDSlots;
+  u32 updates = 0;
+  bool bad = false;
+  for (u32 i = tBegin[t]; i < tEnd[t]; i++) {
+    if (!(pkts[i].flags & LKF_PKT_DD)) continue;
+    DDPkt o = {};
+    if (!dds) {  // LKF_PKT_DD packets without their lkf_pkt_dd side array
+      bad = true;
+      out[i] = o;
+      continue;
+    }
+    const lkf_pkt_dd r = dds[i];
+    o.extFN = r.ext_frame_num;
+    o.extKFN = r.ext_key_frame_num;
+    o.extFlags = r.flags;
+    const u32 next = st.valid ? (st.cur + 1) % kDDSlots : 0u;
+    bool att = false;
+    const int e = r.dd_len ? dd::dd_parse(arena + pkts[i].arena_off + r.dd_off, r.dd_len,
+                                          st.valid ? ring + st.cur : nullptr, ring + next, o, att)
+                           : int(dd::INVALID);
+    if (e) {
+      bad = true;
+      o.flags = 0;
+    } else {
+      if (att) {
+        st.cur = next;
+        st.valid = 1;
+        updates++;
+      }
+      o.slot = u8(st.cur);
+      o.flags |= DP_VALID;
+    }
+    out[i] = o;
+  }
+  // batch n+1's decode may run while batch n decides: a ring slot is reused
+  // only after kDDSlots structures, so at most half of them per batch
+  if (updates > u32(kDDSlots / 2)) bad = true;
+  if (bad) atomicOr(err, 16u);
+  ddTracks[ddIdx] = st;
+}
+
+hipError_t launch_dd_decode(hipStream_t s, const lkf_pkt *pkts, const lkf_pkt_dd *dds, const uint8_t *arena,
+                            const uint32_t *tBegin, const uint32_t *tEnd, const DevTrack *tracks, uint32_t ntracks,
+                            DDStruct *structs, DDTrack *ddTracks, DDPkt *out, uint32_t *err) {
+  if (!ntracks) return hipSuccess;
+  hipLaunchKernelGGL(k_dd_decode, dim3((ntracks + 63) / 64), dim3(64), 0, s, pkts, dds, arena, tBegin, tEnd, tracks,
+                     ntracks, structs, ddTracks, out, err);
   return hipGetLastError();
 }
 
@@ -2612,7 +2823,19 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.pktStride = a.pktStride;
   A.fwdBytes = a.fwdBytes;
   A.stats = a.stats;
-  hipLaunchKernelGGL(k_decide_dt, dim3(a.nlanes), dim3(64), 0, s, A, a.pkts);
+  A.ddPkts = a.ddPkts;
+  A.ddStructs = a.ddStructs;
+  A.ddState = a.ddState;
+  A.ddArena = a.ddArena;
+  A.ddUsed = a.ddUsed;
+  A.ddCap = a.ddCap;
+  // DownTracks of the dependency-descriptor selector run in their own
+  // instantiation (the last ddLanes waves of the schedule)
+  const u32 nPlain = a.nlanes - a.ddLanes;
+  A.waveBase = 0;
+  if (nPlain) hipLaunchKernelGGL(k_decide_dt<false>, dim3(nPlain), dim3(64), 0, s, A, a.pkts);
+  A.waveBase = nPlain;
+  if (a.ddLanes) hipLaunchKernelGGL(k_decide_dt<true>, dim3(a.ddLanes), dim3(64), 0, s, A, a.pkts);
   return hipGetLastError();
 }
 
@@ -2641,7 +2864,11 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   A.outCap = a.outCap;
   A.outByteCap = a.outByteCap;
   A.err = a.err;
-  hipLaunchKernelGGL(k_emit, dim3(a.grid), dim3(EMIT_T), 0, s, A);
+  A.ddArena = a.ddArena;
+  if (a.ddArena)
+    hipLaunchKernelGGL(k_emit<PRE_MAX_DD>, dim3(a.grid), dim3(EMIT_T), 0, s, A);
+  else
+    hipLaunchKernelGGL(k_emit<PRE_MAX>, dim3(a.grid), dim3(EMIT_T), 0, s, A);
   return hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ enum : uint32_t {
   F_HAS_EXPECTED = 1u << 20,
   F_ACTIVE = 1u << 21,
   F_VP9 = 1u << 22,  // videolayerselector.VP9 (SVC without dependency descriptor)
+  F_DD = 1u << 23,   // videolayerselector.DependencyDescriptor (VP9 / AV1 with the DD extension)
 };
 
 struct alignas(16) DTHot {
@@ -127,20 +128,95 @@ struct alignas(16) Tuple {
   uint32_t pkt;
   uint32_t relOff;    // byte offset in the DownTrack's output region
   uint16_t outLen;
-  uint8_t flags;      // lkf_out flags | T_PLAYOUT | T_CODEC
+  uint8_t flags;      // lkf_out flags | T_DD | T_PLAYOUT | T_CODEC
   int8_t layer;
   uint8_t codecLen;
   uint8_t codec[6];
-  uint8_t hdrLen;     // RTP header incl. extension block
-  uint8_t pad[12];
+  uint8_t ddLen;      // dependency-descriptor extension bytes (T_DD)
+  uint16_t hdrLen;    // RTP header incl. extension block
+  uint16_t pad0;
+  uint32_t ddOff;     // offset of the DD bytes in the batch's DD arena
+  uint32_t pad1;
 };
 static_assert(sizeof(Tuple) == 48, "Tuple must be 48 B");
-enum : uint8_t { T_PLAYOUT = 0x40, T_CODEC = 0x80 };
+enum : uint8_t { T_DD = 0x20, T_PLAYOUT = 0x40, T_CODEC = 0x80 };
+
+// ---- dependency descriptor (AV1 / VP9 SVC, §8(a) a9 + a16) -----------------
+// Engine limits (the reference allows more; a packet beyond them is flagged
+// with error bit 16 -> LKF_EINVAL at lkf_sync, never decided silently):
+constexpr int kDDChains = 8;       // NumChains (L3T3 uses 3)
+constexpr int kDDTmplFdiffs = 16;  // frame diffs of one template
+constexpr int kDDFdiffs = 8;       // frame diffs of one frame (custom fdiffs)
+constexpr int kDDExpect = 16;      // frames one chain may wait on (FrameChain.expectFrames)
+constexpr int kDDSlots = 8;        // structure ring per track
+constexpr int kDDMaxBytes = 255;   // marshalled DD (pion two-byte extension element)
+
+struct DDTmpl {  // dependencydescriptor.FrameDependencyTemplate of a structure (32 B)
+  uint8_t sid, tid, nfd, pad;
+  uint32_t chains;   // 4-bit frame_chain_fdiff per chain
+  uint64_t dtis;     // 2-bit DecodeTargetIndication per decode target
+  uint8_t fd[kDDTmplFdiffs];  // frame diffs (1..16)
+};
+static_assert(sizeof(DDTmpl) == 32, "DDTmpl must be 32 B");
+
+struct alignas(16) DDStruct {  // FrameDependencyStructure + ProcessFrameDependencyStructure
+  uint8_t structureId, numDT, numChains, numTmpl;
+  uint8_t numRes, pad[3];
+  uint8_t protectedBy[32];     // DecodeTargetProtectedByChain
+  uint16_t resW[4], resH[4];   // Resolutions (width, height)
+  uint8_t dtTarget[32], dtS[32], dtT[32];  // decode targets sorted high -> low layer
+  uint8_t pad2[8];
+  DDTmpl t[64];
+};
+static_assert(sizeof(DDStruct) % 16 == 0, "DDStruct must be 16-B granular");
+
+enum : uint8_t { DP_FIRST = 1, DP_LAST = 2, DP_ATTACHED = 4, DP_ACTIVE = 8, DP_VALID = 16 };
+struct alignas(16) DDPkt {  // one packet's parsed descriptor (k_dd_decode -> k_decide_dt), 64 B
+  uint64_t extFN, extKFN;
+  uint64_t dtis;        // FrameDependencies.DecodeTargetIndications (2 bits each)
+  uint64_t chainDiffs;  // FrameDependencies.ChainDiffs (8 bits each)
+  uint16_t fd[kDDFdiffs];  // FrameDependencies.FrameDiffs
+  uint32_t activeMask;  // ActiveDecodeTargetsBitmask (valid with DP_ACTIVE)
+  uint16_t frameNumber;
+  uint8_t sid, tid, nfd, ndti, nchain, flags;  // flags: DP_*
+  uint8_t extFlags;     // LKF_DD_*
+  uint8_t slot;         // structure ring slot the descriptor was read with (attached: written to)
+  uint8_t pad[2];
+};
+static_assert(sizeof(DDPkt) == 64, "DDPkt must be 64 B");
+
+struct DDTrack {  // per-track structure-ring cursor (forwarding side)
+  uint32_t cur;    // slot of the current structure
+  uint32_t valid;  // a structure has been seen
+  uint32_t pad[2];
+};
+
+// Per-DownTrack DependencyDescriptor selector state
+// (videolayerselector/dependencydescriptor.go:27-43, selectordecisioncache.go:49-58,
+// framechain.go:22-31, decodetarget.go:24-28, framenumberwrapper.go)
+enum : uint32_t { DS_KF_VALID = 1, DS_HAS_MASK = 2, DS_HAS_PREV_MASK = 4, DS_FN_INIT = 8, DS_CACHE_INIT = 16 };
+struct alignas(16) DDState {
+  uint64_t cBase, cLast;        // SelectorDecisionCache(256, 80)
+  uint64_t masks[8];            // 2 bits per entity
+  uint64_t extKeyFrameNum;
+  uint64_t fnLast, fnOffset;    // FrameNumberWrapper
+  uint32_t flags;               // DS_*
+  uint32_t mask, prevMask;      // activeDecodeTargetsBitmask / previous
+  uint32_t dtActive;            // DecodeTarget.active, by position in the sorted list
+  uint8_t slot;                 // structure ring slot of d.structure
+  uint8_t numChains, numTargets;  // len(d.chains), len(d.decodeTargets)
+  uint8_t chBroken, chActive, chUpdating;
+  uint8_t expCount[kDDChains];
+  uint8_t pad[2];
+  uint64_t exp[kDDChains][kDDExpect];  // FrameChain.expectFrames (a set: see dd_device.h)
+};
+static_assert(sizeof(DDState) % 16 == 0, "DDState must be 16-B granular");
 
 struct DevTrack {  // track table (24 x 4 B)
   uint32_t kind, codec, hasRefTS, clockRate;
   uint32_t layerOffsets[9];  // [ref*3 + layer]
-  uint32_t pad[3];
+  uint32_t ddIdx;            // index into the DD structure tables (0xffffffff: no DD selector)
+  uint32_t pad[2];
 };
 
 // ---- ingress: one received stream = one buffer.Buffer (buffer.go:66-130) ----

@@ -12,6 +12,7 @@ struct DecideLaunch {
   const uint32_t *sched;    // wave -> DownTrack (per-XCD interleaved schedule)
   const uint32_t *waveTrack;
   uint32_t nlanes;          // waves
+  uint32_t ddLanes;         // the last ddLanes waves: DownTracks of the DD selector (k_decide_dt<true>)
   DTHot *hot;
   const DevDT *dts;
   const DevTrack *tracks;
@@ -32,6 +33,13 @@ struct DecideLaunch {
   uint64_t *stats;
   const uint32_t *layerList, *layerBefore, *layerCnt;  // launch_layer_index outputs
   uint32_t pktStride;                                  // max_batch_pkts
+  // dependency descriptor (nullptr when no track uses the DD selector)
+  const DDPkt *ddPkts;
+  const DDStruct *ddStructs;
+  DDState *ddState;
+  uint8_t *ddArena;
+  uint64_t *ddUsed;
+  uint64_t ddCap;
 };
 
 struct EmitLaunch {
@@ -48,6 +56,7 @@ struct EmitLaunch {
   uint64_t outCap, outByteCap;
   uint32_t *err;
   uint32_t grid;
+  const uint8_t *ddArena;  // non-null: batches with DD tracks (k_emit<PRE_MAX_DD>)
 };
 
 // diagnostic builds (-DLKF_DIAG=1): k_decide_dt per-wave counters
@@ -94,6 +103,9 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_layer_index(hipStream_t s, const lkf_pkt *pkts, const uint32_t *tBegin, const uint32_t *tEnd,
                               uint32_t ntracks, uint32_t stride, uint32_t *list, uint32_t *before, uint32_t *cnt);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
+hipError_t launch_dd_decode(hipStream_t s, const lkf_pkt *pkts, const lkf_pkt_dd *dds, const uint8_t *arena,
+                            const uint32_t *tBegin, const uint32_t *tEnd, const DevTrack *tracks, uint32_t ntracks,
+                            DDStruct *structs, DDTrack *ddTracks, DDPkt *out, uint32_t *err);
 // pulls two pinned host buffers (device-visible) into device memory with one
 // kernel (sizes multiples of 4 B); replaces two hipMemcpyAsync calls per run
 hipError_t launch_h2d(hipStream_t s, void *dstA, const void *srcA, size_t nA, void *dstB, const void *srcB, size_t nB);

@@ -323,6 +323,7 @@ KAT(wraparound_uint32) {
 // KATs defined in other translation units register themselves the same way.
 #include "kat_sfu.inc"
 #include "kat_dd.inc"
+#include "kat_ddsel.inc"
 
 int main(int argc, char **argv) {
   bool list = false;

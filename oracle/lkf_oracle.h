@@ -282,6 +282,10 @@ struct VideoLayer {
 };
 inline VideoLayer InvalidLayer() { return VideoLayer{InvalidLayerSpatial, InvalidLayerTemporal}; }
 
+}  // namespace orc
+#include "dd_select_oracle.h"  // DD selector / parser (namespace orc; needs VideoLayer, WrapAround)
+namespace orc {
+
 // -----------------------------------------------------------------------------
 // buffer.VP8 payload descriptor — pkg/sfu/buffer/helpers.go:49-241
 // -----------------------------------------------------------------------------
@@ -659,6 +663,7 @@ struct ExtPacket {
   VP8 vp8;  // valid when kind == PayloadVP8
   VP9Flags vp9;  // valid when kind == PayloadVP9
   bool KeyFrame = false;
+  std::shared_ptr<ExtDD> dd;  // ExtPacket.DependencyDescriptor (nil: no DD extension)
 };
 
 // -----------------------------------------------------------------------------
@@ -1125,9 +1130,10 @@ struct VideoLayerSelectorResult {  // videolayerselector.go:8-15
   bool IsSwitching = false;
   bool IsResuming = false;
   bool RTPMarker = false;
+  std::vector<u8> DependencyDescriptorExtension;  // nil unless the DD selector marshalled one
 };
 
-enum VLSKind : u8 { VLSNull = 0, VLSSimulcast = 1, VLSVP9 = 2 };
+enum VLSKind : u8 { VLSNull = 0, VLSSimulcast = 1, VLSVP9 = 2, VLSDD = 3 };
 
 struct VLS {
   VLSKind kind = VLSNull;
@@ -1135,6 +1141,7 @@ struct VLS {
   VideoLayer maxLayer, maxSeenLayer, targetLayer, previousTargetLayer;
   i32 requestSpatial = InvalidLayerSpatial;
   VideoLayer currentLayer, previousLayer;
+  std::shared_ptr<DDSelectorState> dd;  // kind == VLSDD (videolayerselector/dependencydescriptor.go)
 
   void SetMax(VideoLayer l) { maxLayer = l; }
   void SetMaxSpatial(i32 l) { maxLayer.Spatial = l; }
@@ -1152,12 +1159,109 @@ struct VLS {
   VideoLayer GetMaxSeen() const { return maxSeenLayer; }
   void SetCurrent(VideoLayer l) { currentLayer = l; }
   VideoLayer GetCurrent() const { return currentLayer; }
-  void Rollback() {  // base.go Rollback
+  void Rollback() {  // base.go Rollback; DependencyDescriptor.Rollback dependencydescriptor.go:357-361
+    if (kind == VLSDD) {
+      dd->hasMask = dd->hasPrevMask;
+      dd->mask = dd->prevMask;
+    }
     currentLayer = previousLayer;
     targetLayer = previousTargetLayer;
   }
   std::pair<bool, i32> CheckSync() const {
+    if (kind == VLSDD) {  // dependencydescriptor.go:418-434
+      const i32 layer = requestSpatial;
+      if (!currentLayer.IsValid() || !dd->keyFrameValid) return {false, layer};
+      for (auto &t : dd->decodeTargets)
+        if (t.Active() && t.dt.Layer.Spatial == layer && t.Valid()) return {true, layer};
+      return {false, layer};
+    }
     return {requestSpatial == currentLayer.Spatial, requestSpatial};
+  }
+
+  // DependencyDescriptor.Select videolayerselector/dependencydescriptor.go:65-355
+  VideoLayerSelectorResult SelectDD(const ExtPacket &p) {
+    VideoLayerSelectorResult r;
+    DDSelectorState &d = *dd;
+    if (currentLayer.IsValid()) r.IsRelevant = true;
+    if (!p.dd) return r;
+    const ExtDD &w = *p.dd;
+    const orc_dd::Descriptor &desc = *w.Descriptor;
+    const u64 efn = w.ExtFrameNum;
+    const orc_dd::Template &fd = desc.FrameDependencies;
+    if (!d.keyFrameValid && !desc.AttachedStructure) return r;
+    bool tooOld = false;
+    const SelectorDecision sd = d.decisions.GetDecision(efn, &tooOld);
+    if (tooOld) return r;
+    if (sd == SDDropped) return r;
+    if (w.StructureUpdated) d.updateDependencyStructure(desc.AttachedStructure, w.DecodeTargets, efn);
+    if (w.ExtKeyFrameNum != d.extKeyFrameNum) {
+      d.decisions.AddDropped(efn);
+      d.invalidateKeyFrame();
+      return r;
+    }
+    if (w.ActiveDecodeTargetsUpdated) d.updateActiveDecodeTargets(desc.ActiveDecodeTargetsBitmask);
+    if (fd.ChainDiffs.size() != d.chains.size()) {
+      d.decisions.AddDropped(efn);
+      return r;
+    }
+    for (auto &c : d.chains) c->OnFrame(efn, fd);
+    DDDecodeTarget hi;
+    hi.Target = -1;
+    int dti = 0;
+    for (auto &t : d.decodeTargets) {
+      if (!t.Active() || t.dt.Layer.Spatial > targetLayer.Spatial || t.dt.Layer.Temporal > targetLayer.Temporal)
+        continue;
+      bool tv = false;
+      int x = 0;
+      if (!t.OnFrame(efn, fd, tv, x)) {
+        d.decisions.AddDropped(efn);
+        return r;
+      }
+      if (tv) {
+        hi = t.dt;
+        dti = x;
+        break;
+      }
+    }
+    if (hi.Target < 0 || dti == 0) {  // no decode target / DecodeTargetNotPresent
+      d.decisions.AddDropped(efn);
+      return r;
+    }
+    for (int fdiff : fd.FrameDiffs) {
+      if (fdiff == 0) continue;
+      if (d.decisions.GetDecision(efn - u64(fdiff)) == SDDropped) {
+        d.decisions.AddDropped(efn);
+        return r;
+      }
+    }
+    if (currentLayer != hi.Layer) {
+      r.IsSwitching = true;
+      if (!currentLayer.IsValid()) r.IsResuming = true;
+      previousLayer = currentLayer;
+      currentLayer = hi.Layer;
+      d.hasPrevMask = d.hasMask;
+      d.prevMask = d.mask;
+      d.hasMask = true;
+      d.mask = GetActiveDecodeTargetBitmask(currentLayer, w.DecodeTargets);
+      r.IsRelevant = true;
+    }
+    orc_dd::Descriptor out = desc;  // the (shallow) clone of :301/:312
+    const u16 unwrapFn = u16(d.fnWrapper.UpdateAndGet(efn, w.StructureUpdated));
+    if (unwrapFn != desc.FrameNumber) out.FrameNumber = unwrapFn;
+    if (!desc.AttachedStructure && d.hasMask) {
+      out.hasActiveMask = true;
+      out.ActiveDecodeTargetsBitmask = d.mask;
+    }
+    std::vector<u8> bytes;
+    if (orc_dd::Marshal(d.structure.get(), out, ~0u, bytes) != orc_dd::DD_OK) {  // error or recovered panic
+      d.decisions.AddDropped(efn);
+      return r;
+    }
+    r.DependencyDescriptorExtension = bytes;
+    if (w.Integrity) d.decisions.AddForwarded(efn);
+    r.RTPMarker = p.Header.Marker || (desc.LastPacketInFrame && currentLayer.Spatial == fd.SpatialId);
+    r.IsSelected = true;
+    return r;
   }
 
   // VP9.Select videolayerselector/vp9.go:43-109 (SVC: every layer in one
@@ -1213,6 +1317,7 @@ struct VLS {
   VideoLayerSelectorResult Select(const ExtPacket &p, i32 layer) {
     VideoLayerSelectorResult r;
     if (kind == VLSVP9) return SelectVP9(p);
+    if (kind == VLSDD) return SelectDD(p);
     if (kind != VLSSimulcast) return r;
     if (currentLayer.Spatial != targetLayer.Spatial) {
       VideoLayer cur = currentLayer;
@@ -1295,11 +1400,13 @@ struct TranslationParams {  // forwarder.go:146-154
   bool hasRTP = false;
   TranslationParamsRTP rtp;
   std::vector<u8> codecBytes;
+  std::vector<u8> ddBytes;  // tp.ddBytes forwarder.go:1706
   bool marker = false;
   int dropReason = -1;  // engine statistic only (lkf_drop); not part of equality
   bool operator==(const TranslationParams &o) const {
     return shouldDrop == o.shouldDrop && isResuming == o.isResuming && isSwitching == o.isSwitching &&
-           hasRTP == o.hasRTP && (!hasRTP || rtp == o.rtp) && codecBytes == o.codecBytes && marker == o.marker;
+           hasRTP == o.hasRTP && (!hasRTP || rtp == o.rtp) && codecBytes == o.codecBytes && ddBytes == o.ddBytes &&
+           marker == o.marker;
   }
 };
 
@@ -1344,11 +1451,21 @@ struct Forwarder {
   explicit Forwarder(Kind k) : kind(k) {
     if (kind == KindVideo) vls.SetMaxTemporal(DefaultMaxLayerTemporal);
   }
-  // DetermineCodec forwarder.go:269-338 (VP8/H264/Opus; SVC codecs later)
-  void DetermineCodec(Mime m, u32 cr) {
+  // DetermineCodec forwarder.go:269-338; hasDD = the dependency-descriptor
+  // extension is among the receiver's header extensions (ddAvailable :278-285)
+  void DetermineCodec(Mime m, u32 cr, bool hasDD = false) {
     if (mime != MimeNone) return;
     mime = m;
     clockRate = cr;
+    if ((m == MimeVP9 || m == MimeAV1) && hasDD) {  // NewDependencyDescriptor(FromNull)
+      vls.kind = VLSDD;
+      vls.dd = std::make_shared<DDSelectorState>();
+      return;
+    }
+    if (m == MimeAV1) {  // AV1 without DD: Simulcast selector
+      vls.kind = VLSSimulcast;
+      return;
+    }
     if (m == MimeVP8) {
       hasVP8Munger = true;  // NewVP8FromNull seeds from Null's (zero) state
       vls.kind = VLSSimulcast;
@@ -1563,6 +1680,7 @@ struct Forwarder {
     }
     tp.isResuming = res.IsResuming;
     tp.isSwitching = res.IsSwitching;
+    tp.ddBytes = res.DependencyDescriptorExtension;
     tp.marker = res.RTPMarker;
     if (FlagPauseOnDowngrade && lastAllocIsDeficient && vls.GetTarget().Spatial < vls.GetCurrent().Spatial) {
       tp.shouldDrop = true;
@@ -2108,6 +2226,102 @@ inline bool rtp_unmarshal(const u8 *buf, int len, RtpParsed &h) {
   h.hdrSize = n;
   h.payloadLen = end - n;
   return true;
+}
+
+// -----------------------------------------------------------------------------
+// buffer.IsH264KeyFrame helpers.go:248-309 / IsAV1KeyFrame :343-420
+// (restated as written, including the AV1 W-field OBU walk)
+// -----------------------------------------------------------------------------
+inline bool IsH264KeyFrame(const u8 *p, int n) {
+  if (n < 1) return false;
+  const int nalu = p[0] & 0x1F;
+  if (nalu == 0) return false;
+  if (nalu <= 23) return nalu == 7;
+  if (nalu == 24 || nalu == 25 || nalu == 26 || nalu == 27) {
+    int i = 1;
+    if (nalu == 25 || nalu == 26 || nalu == 27) i += 2;
+    while (i < n) {
+      if (i + 2 > n) return false;
+      const int length = (int(p[i]) << 8) | int(p[i + 1]);
+      i += 2;
+      if (i + length > n) return false;
+      int offset = 0;
+      if (nalu == 26)
+        offset = 3;
+      else if (nalu == 27)
+        offset = 4;
+      if (offset >= length) return false;
+      const int nn = p[i + offset] & 0x1F;
+      if (nn == 7) return true;
+      i += length;
+    }
+    return false;
+  }
+  if (nalu == 28 || nalu == 29) {
+    if (n < 2) return false;
+    if ((p[1] & 0x80) == 0) return false;
+    return (p[1] & 0x1F) == 7;
+  }
+  return false;
+}
+
+inline bool IsAV1KeyFrame(const u8 *payload, int n) {
+  if (n < 2) return false;
+  if ((payload[0] & 0x88) != 0x08) return false;  // Z=0, N=1
+  const int w = (payload[0] & 0x30) >> 4;
+  // getObu(data, last) -> (obu ptr/len, consumed length, truncated)
+  auto getObu = [](const u8 *data, int dn, bool last, const u8 *&obu, int &olen, int &length, bool &trunc) {
+    trunc = false;
+    if (last) {
+      obu = data;
+      olen = dn;
+      length = dn;
+      return;
+    }
+    int offset = 0, len = 0;
+    for (;;) {
+      if (dn <= offset) {
+        obu = nullptr;
+        olen = 0;
+        length = offset;
+        trunc = offset > 0;
+        return;
+      }
+      const u8 l = data[offset];
+      len |= int(l & 0x7f) << (offset * 7);
+      offset++;
+      if ((l & 0x80) == 0) break;
+    }
+    if (dn < offset + len) {
+      obu = data + offset;
+      olen = dn - offset;
+      length = dn;
+      trunc = true;
+      return;
+    }
+    obu = data + offset;
+    olen = len;
+    length = offset + len;
+  };
+  int offset = 1, i = 0;
+  for (;;) {
+    const u8 *obu;
+    int olen, length;
+    bool truncated;
+    getObu(payload + offset, n - offset, w == i + 1, obu, olen, length, truncated);
+    if (olen < 1) return false;
+    const int tpe = (obu[0] & 0x38) >> 3;
+    if (i == 0) {
+      if (tpe != 1) return false;  // OBU_SEQUENCE_HEADER
+    } else if (tpe == 3 || tpe == 6) {  // OBU_FRAME_HEADER / OBU_FRAME
+      if (olen < 2) return false;
+      if ((obu[1] & 0x80) != 0) return false;  // show_existing_frame
+      return (obu[1] & 0x60) == 0;             // KEY_FRAME
+    }
+    if (truncated || i >= w) return false;
+    offset += length;
+    i++;
+  }
 }
 
 }  // namespace orc

@@ -29,6 +29,11 @@ namespace {
 
 struct OTrack {
   lkf_track_params p;
+  // the structure the DD extension bytes of this track's ExtPackets are read
+  // with (the Go parser's r.structure at ingress; replaced by every packet
+  // that attaches one) and its decode targets (ProcessFrameDependencyStructure)
+  std::shared_ptr<orc_dd::Structure> ddStructure;
+  std::vector<DDDecodeTarget> ddTargets;
 };
 
 struct OOut {
@@ -63,6 +68,7 @@ struct OStream {
   RTPStatsReceiver stats;
   RangeMap<u64, u64> snRangeMap{100};  // buffer.go:134
   std::unique_ptr<AudioLevel> level;   // when the audio-level extension is negotiated (buffer.go:203-205)
+  std::unique_ptr<DependencyDescriptorParser> ddParser;  // when the DD extension is negotiated (buffer.go:193-201)
   bool latestTSForAudioLevelInitialized = false;
   u32 latestTSForAudioLevel = 0;
 };
@@ -81,6 +87,9 @@ struct orc_engine {
   std::vector<std::unique_ptr<OStream>> streams;
   std::vector<lkf_flow> flows;
   std::vector<lkf_pkt> ingested;
+  std::vector<lkf_pkt_dd> ingestedDD;
+  // lkf_pkt_dd side array of the next orc_run (orc_submit_dd)
+  std::vector<lkf_pkt_dd> pendingDD;
 };
 
 static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
@@ -122,7 +131,8 @@ static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
   (void)e;
 }
 
-static ExtPacket toExt(const lkf_pkt &d, const u8 *arena) {
+static ExtPacket toExt(const lkf_pkt &d, const u8 *arena, const lkf_pkt_dd *dd, OTrack &tr, bool &ok) {
+  ok = true;
   ExtPacket p;
   const u8 *raw = arena + d.arena_off;
   p.layer.Spatial = d.spatial;
@@ -174,6 +184,29 @@ static ExtPacket toExt(const lkf_pkt &d, const u8 *arena) {
     v.V = d.vp9_bits & LKF_VP9_V;
     v.U = d.vp9_bits & LKF_VP9_U;
   }
+  if ((d.flags & LKF_PKT_DD) && dd) {
+    // ExtPacket.DependencyDescriptor: the descriptor as the ingress parser read
+    // it (DependencyDescriptorExtension.Unmarshal with the track's structure,
+    // dependencydescriptorparser.go:86-97), plus the parser's metadata
+    auto e = std::make_shared<ExtDD>();
+    e->Descriptor = std::make_shared<orc_dd::Descriptor>();
+    int nread = 0;
+    if (orc_dd::Unmarshal(raw + dd->dd_off, dd->dd_len, tr.ddStructure.get(), *e->Descriptor, nread) != orc_dd::DD_OK) {
+      ok = false;
+      return p;
+    }
+    if (e->Descriptor->AttachedStructure) {
+      tr.ddStructure = e->Descriptor->AttachedStructure;
+      tr.ddTargets = ProcessFrameDependencyStructure(*tr.ddStructure);
+    }
+    e->DecodeTargets = tr.ddTargets;
+    e->StructureUpdated = dd->flags & LKF_DD_STRUCTURE_UPDATED;
+    e->ActiveDecodeTargetsUpdated = dd->flags & LKF_DD_ACTIVE_UPDATED;
+    e->Integrity = dd->flags & LKF_DD_INTEGRITY;
+    e->ExtFrameNum = dd->ext_frame_num;
+    e->ExtKeyFrameNum = dd->ext_key_frame_num;
+    p.dd = e;
+  }
   return p;
 }
 
@@ -201,19 +234,21 @@ static void writeRTP(orc_engine *e, u32 dtIdx, ODT &d, const ExtPacket &ep, u32 
   hdr.SequenceNumber = u16(tp.rtp.extSequenceNumber);
   hdr.SSRC = d.p.ssrc;
   if (tp.marker) hdr.Marker = true;
-  // pacer Base.writeRTPHeaderExtensions pacer/base.go:71-100 (DD bytes are
-  // never produced by the VP8/Opus selectors; abs-send-time is a 3-byte
-  // placeholder the sender stamps — wall clock excluded from parity)
+  // pacer Base.writeRTPHeaderExtensions pacer/base.go:71-100: DD bytes
+  // (downtrack.go:715-718, skipped when the DownTrack has no DD extension id),
+  // playout delay until acked, abs-send-time as a 3-byte placeholder the
+  // sender stamps (wall clock excluded from parity)
   hdr.Extension = false;
   hdr.ExtensionProfile = 0;
   hdr.Extensions.clear();
+  if (d.p.ext_dd && !tp.ddBytes.empty()) hdr.SetExtension(d.p.ext_dd, tp.ddBytes);
   if (d.p.ext_playout && !d.playoutAcked)
     hdr.SetExtension(d.p.ext_playout, std::vector<u8>(d.p.playout_delay, d.p.playout_delay + 3));
   if (d.p.ext_abs_send_time) hdr.SetExtension(d.p.ext_abs_send_time, std::vector<u8>{0, 0, 0});
   // sequencer.push downtrack.go:724-735
   i64 arrivalMs = ep.Arrival / 1000000;
   d.seq->push(arrivalMs, ep.ExtSequenceNumber, tp.rtp.extSequenceNumber, tp.rtp.extTimestamp, hdr.Marker, i8(layer),
-              tp.codecBytes, {});
+              tp.codecBytes, tp.ddBytes);
   // sendingPacket -> RTPStatsSender.Update init (rtpstats_sender.go:245-262)
   if (!d.statsInit && !payload.empty()) {
     d.statsInit = true;
@@ -247,7 +282,9 @@ orc_engine *orc_create(uint32_t seq_size) {
 void orc_destroy(orc_engine *e) { delete e; }
 
 int32_t orc_add_track(orc_engine *e, const lkf_track_params *p) {
-  e->tracks.push_back(OTrack{*p});
+  OTrack t;
+  t.p = *p;
+  e->tracks.push_back(t);
   return int32_t(e->tracks.size() - 1);
 }
 
@@ -261,8 +298,9 @@ int32_t orc_add_downtrack(orc_engine *e, const lkf_downtrack_params *p) {
   Mime m = tp.codec == LKF_CODEC_VP8    ? MimeVP8
            : tp.codec == LKF_CODEC_H264 ? MimeH264
            : tp.codec == LKF_CODEC_VP9  ? MimeVP9
+           : tp.codec == LKF_CODEC_AV1  ? MimeAV1
                                         : MimeOpus;
-  d->f->DetermineCodec(m, tp.clock_rate);
+  d->f->DetermineCodec(m, tp.clock_rate, tp.has_dd != 0);
   d->seq = std::make_unique<Sequencer>(int(e->seqSize), k == KindVideo, p->bind_time_ns / 1000000);
   ODT *dp = d.get();
   int32_t track = p->track;
@@ -270,7 +308,7 @@ int32_t orc_add_downtrack(orc_engine *e, const lkf_downtrack_params *p) {
     // StreamTrackerManager.GetReferenceLayerRTPTimestamp streamtrackermanager.go:660-679
     dp->f->getReferenceLayerRTPTimestamp = [e, track](u32 ts, i32 layer, i32 ref, u32 &out) -> Err {
       if (layer < 0 || layer >= 3 || ref < 0 || ref >= 3) return ErrRefLayerUnavailable;
-      if (e->tracks[track].p.codec == LKF_CODEC_VP9) {  // isSVC: one stream, one timeline (:667-671)
+      if (e->tracks[track].p.codec == LKF_CODEC_VP9 || e->tracks[track].p.codec == LKF_CODEC_AV1) {  // isSVC (:667-671)
         out = ts;
         return OK;
       }
@@ -319,9 +357,17 @@ int orc_ctl_batch(orc_engine *e, const lkf_ctl_event *evs, uint32_t n) {
   return LKF_OK;
 }
 
+// lkf_submit_dd: the side array of the next batch.
+int orc_submit_dd(orc_engine *e, const lkf_pkt_dd *dd, uint32_t n) {
+  e->pendingDD.assign(dd, dd + n);
+  return LKF_OK;
+}
+
 // Runs one batch; pkts grouped by track (lkf_submit contract).
 int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len) {
   (void)arena_len;
+  std::vector<lkf_pkt_dd> dds;
+  dds.swap(e->pendingDD);
   std::memset(&e->stats, 0, sizeof(e->stats));
   const u32 ndt = u32(e->dts.size());
   std::vector<std::vector<OEv>> evq(ndt);
@@ -338,7 +384,9 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   for (u32 i = 0; i < n; i++) {
     const lkf_pkt &pd = pkts[i];
     if (pd.track >= e->tracks.size()) return LKF_EINVAL;
-    ExtPacket ep = toExt(pd, arena);
+    bool ok = true;
+    ExtPacket ep = toExt(pd, arena, i < dds.size() ? &dds[i] : nullptr, e->tracks[pd.track], ok);
+    if (!ok) return LKF_EINVAL;
     for (u32 d : trackDts[pd.track]) {
       ODT &dt = *e->dts[d];
       while (evc[d] < evq[d].size() && evq[d][evc[d]].at <= i) applyCtl(e, dt, evq[d][evc[d]++]);
@@ -496,13 +544,15 @@ int32_t orc_add_stream(orc_engine *e, const lkf_stream_params *p) {
     }
     s->level = std::make_unique<AudioLevel>(ap);
   }
+  if (p->dd_ext) s->ddParser = std::make_unique<DependencyDescriptorParser>();
   e->streams.push_back(std::move(s));
   return int32_t(e->streams.size() - 1);
 }
 
 // Buffer.calc (buffer.go:417-491) + processHeaderExtensions (:573-596) +
 // updateStreamState (:545-567) + getExtPacket (:599-671) for one datagram.
-static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 *raw, lkf_pkt &ep, bool &fwd) {
+static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 *raw, lkf_pkt &ep, lkf_pkt_dd &epd,
+                     bool &fwd) {
   lkf_flow f{};
   f.pkt = 0xffffffffu;
   fwd = false;
@@ -562,6 +612,7 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
   if (fs.IsDuplicate) return f;
   // getExtPacket
   std::memset(&ep, 0, sizeof(ep));
+  std::memset(&epd, 0, sizeof(epd));
   ep.ext_sn = f.ext_sn;
   ep.ext_ts = f.ext_ts;
   ep.arrival_ns = rp.arrival_ns;
@@ -581,14 +632,42 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
   }
   if (h.payloadLen > 0) {
     ep.temporal = 0;
+    const u8 *pay = buf + h.hdrSize;
+    std::shared_ptr<ExtDD> ddv;
+    if (b.ddParser) {  // DependencyDescriptorParser.Parse (buffer.go:613-621), header SN already adjusted
+      int off = 0, len = 0;
+      const u8 *ddBuf = h.GetExtension(b.p.dd_ext, off, len) ? buf + off : nullptr;
+      VideoLayer vl;
+      if (b.ddParser->Parse(ddBuf, len, u16(f.ext_sn), ddv, vl) != DDP_OK) {
+        f.flags |= LKF_FLOW_BAD;
+        return f;
+      }
+      if (ddv) {
+        ep.flags |= LKF_PKT_DD;
+        ep.spatial = int8_t(vl.Spatial);
+        ep.temporal = int8_t(vl.Temporal);
+        epd.ext_frame_num = ddv->ExtFrameNum;
+        epd.ext_key_frame_num = ddv->ExtKeyFrameNum;
+        epd.dd_off = u16(off);  // offset within the packet (buf = raw + rp.off)
+        epd.dd_len = u8(len);
+        epd.flags = u8((ddv->StructureUpdated ? LKF_DD_STRUCTURE_UPDATED : 0) |
+                       (ddv->ActiveDecodeTargetsUpdated ? LKF_DD_ACTIVE_UPDATED : 0) |
+                       (ddv->Integrity ? LKF_DD_INTEGRITY : 0));
+      }
+    }
     if (b.codec == LKF_CODEC_VP8) {
       VP8 v;
-      if (v.Unmarshal(buf + h.hdrSize, h.payloadLen) != OK) {  // "could not unmarshal VP8 packet"
+      if (v.Unmarshal(pay, h.payloadLen) != OK) {  // "could not unmarshal VP8 packet"
         f.flags |= LKF_FLOW_BAD;
         return f;
       }
       ep.flags |= LKF_PKT_VP8 | (v.IsKeyFrame ? LKF_PKT_KEYFRAME : 0);
-      ep.temporal = int8_t(v.TID);
+      if (!ddv) {
+        ep.temporal = int8_t(v.TID);
+      } else {  // VP8 with DD: TID from the descriptor, no spatial scalability (buffer.go:630-635)
+        v.TID = u8(ep.temporal);
+        ep.spatial = -1;
+      }
       ep.vp8_first = v.FirstByte;
       ep.vp8_bits = u8((v.S ? LKF_VP8_S : 0) | (v.I ? LKF_VP8_I : 0) | (v.M ? LKF_VP8_M : 0) |
                        (v.L ? LKF_VP8_L : 0) | (v.T ? LKF_VP8_T : 0) | (v.Y ? LKF_VP8_Y : 0) |
@@ -598,19 +677,25 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
       ep.vp8_tl0picidx = v.TL0PICIDX;
       ep.vp8_tid = v.TID;
       ep.vp8_keyidx = v.KEYIDX;
-    } else if (b.codec == LKF_CODEC_VP9) {  // buffer.go:643-656 (no dependency descriptor)
-      VP9Packet v;
-      if (v.Unmarshal(buf + h.hdrSize, h.payloadLen) != OK) {  // "could not unmarshal VP9 packet"
-        f.flags |= LKF_FLOW_BAD;
-        return f;
+    } else if (b.codec == LKF_CODEC_VP9) {  // buffer.go:643-656
+      if (!ddv) {
+        VP9Packet v;
+        if (v.Unmarshal(pay, h.payloadLen) != OK) {  // "could not unmarshal VP9 packet"
+          f.flags |= LKF_FLOW_BAD;
+          return f;
+        }
+        ep.flags |= LKF_PKT_VP9;
+        ep.spatial = int8_t(v.SID);
+        ep.temporal = int8_t(v.TID);
+        ep.vp9_bits = u8((v.I ? LKF_VP9_I : 0) | (v.P ? LKF_VP9_P : 0) | (v.L ? LKF_VP9_L : 0) |
+                         (v.F ? LKF_VP9_F : 0) | (v.B ? LKF_VP9_B : 0) | (v.E ? LKF_VP9_E : 0) |
+                         (v.V ? LKF_VP9_V : 0) | (v.U ? LKF_VP9_U : 0));
       }
-      const bool kf = VP9Packet::IsKeyFrame(buf + h.hdrSize, h.payloadLen);
-      ep.flags |= LKF_PKT_VP9 | (kf ? LKF_PKT_KEYFRAME : 0);
-      ep.spatial = int8_t(v.SID);
-      ep.temporal = int8_t(v.TID);
-      ep.vp9_bits = u8((v.I ? LKF_VP9_I : 0) | (v.P ? LKF_VP9_P : 0) | (v.L ? LKF_VP9_L : 0) |
-                       (v.F ? LKF_VP9_F : 0) | (v.B ? LKF_VP9_B : 0) | (v.E ? LKF_VP9_E : 0) |
-                       (v.V ? LKF_VP9_V : 0) | (v.U ? LKF_VP9_U : 0));
+      if (VP9Packet::IsKeyFrame(pay, h.payloadLen)) ep.flags |= LKF_PKT_KEYFRAME;
+    } else if (b.codec == LKF_CODEC_H264) {  // buffer.go:657-658
+      if (IsH264KeyFrame(pay, h.payloadLen)) ep.flags |= LKF_PKT_KEYFRAME;
+    } else if (b.codec == LKF_CODEC_AV1) {  // buffer.go:659-660
+      if (IsAV1KeyFrame(pay, h.payloadLen)) ep.flags |= LKF_PKT_KEYFRAME;
     }
   }
   if (ep.spatial >= 0) ep.layer = ep.spatial;  // svc: forwardRTP dispatches pkt.Spatial (receiver.go:667-672)
@@ -624,16 +709,20 @@ int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
   (void)raw_len;
   e->flows.assign(n, lkf_flow{});
   e->ingested.clear();
+  e->ingestedDD.clear();
   for (u32 i = 0; i < n; i++) {
     if (pkts[i].stream >= e->streams.size()) return LKF_EINVAL;
     lkf_pkt ep;
+    lkf_pkt_dd epd;
     bool fwd = false;
-    e->flows[i] = calc(e, *e->streams[pkts[i].stream], pkts[i], raw, ep, fwd);
+    e->flows[i] = calc(e, *e->streams[pkts[i].stream], pkts[i], raw, ep, epd, fwd);
     if (fwd) {
       e->flows[i].pkt = u32(e->ingested.size());
       e->ingested.push_back(ep);
+      e->ingestedDD.push_back(epd);
     }
   }
+  e->pendingDD = e->ingestedDD;  // the ingested batch is the next run's input
   return LKF_OK;
 }
 
@@ -648,6 +737,12 @@ int orc_ingest_flows(orc_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
 int orc_ingested_ptr(orc_engine *e, const lkf_pkt **pkts, uint32_t *n) {
   *pkts = e->ingested.data();
   *n = u32(e->ingested.size());
+  return LKF_OK;
+}
+int orc_ingested_dd(orc_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_out) {
+  *n_out = u32(e->ingestedDD.size());
+  if (cap < e->ingestedDD.size()) return LKF_ENOSPC;
+  if (!e->ingestedDD.empty()) std::memcpy(out, e->ingestedDD.data(), e->ingestedDD.size() * sizeof(lkf_pkt_dd));
   return LKF_OK;
 }
 int orc_ingested(orc_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {

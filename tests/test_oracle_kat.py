@@ -28,7 +28,7 @@ NAMES = _kat_names()
 
 def test_kat_inventory():
     """Every reference test file named in SURVEY.md §8(c) that the oracle covers has KATs."""
-    prefixes = ["rangemap", "wraparound", "rtpmunger", "vp8_", "forwarder_", "sequencer", "audiolevel",
+    prefixes = ["rangemap", "wraparound", "rtpmunger", "vp8_", "forwarder_", "sequencer", "audiolevel", "ddsel_",
                 "rtpstats_receiver", "dd_"]
     for p in prefixes:
         assert any(n.startswith(p) for n in NAMES), p
