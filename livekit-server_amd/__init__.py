@@ -143,9 +143,12 @@ class Engine:
         if rc != 0:
             raise EngineError("%s rc=%d: %s" % (what, rc, self.lib.lkf_last_error(self.h).decode()))
 
-    def submit(self, pkts, n, arena, arena_len):
+    def submit(self, pkts, n, arena, arena_len, dd=None):
+        """lkf_submit (+ lkf_submit_dd with the batch's lkf_pkt_dd side array)."""
         self._chk(self.lib.lkf_submit(self.h, C.cast(pkts, C.c_void_p), n, C.cast(arena, C.c_void_p), arena_len),
                   "submit")
+        if dd is not None:
+            self._chk(self.api["submit_dd"](self.h, C.cast(dd, C.c_void_p), n), "submit_dd")
 
     def submit_device(self, d_pkts, n, d_arena, arena_len):
         self._chk(self.lib.lkf_submit_device(self.h, d_pkts, n, d_arena, arena_len), "submit_device")

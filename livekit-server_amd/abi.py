@@ -254,6 +254,7 @@ class lkfs_cfg(C.Structure):
         ("reorder", C.c_double),
         ("with_events", C.c_int32),
         ("has_callbacks", C.c_int32),
+        ("svc_dd", C.c_int32),
     ]
 
 
@@ -344,4 +345,5 @@ def load_synth(path=None):
     _bind(lib, "lkfs_num_streams", C.c_uint32, [t])
     _bind(lib, "lkfs_streams", P(lkf_stream_params), [t])
     _bind(lib, "lkfs_batch_raw", C.c_int, [t, C.c_uint32, P(P(lkf_raw_pkt)), P(C.c_uint32)])
+    _bind(lib, "lkfs_batch_dd", C.c_int, [t, C.c_uint32, P(P(lkf_pkt_dd)), P(C.c_uint32)])
     return lib

@@ -39,6 +39,13 @@ constexpr i64 MS = 1000000LL;
 constexpr u16 kPayloadOff = 20;  // 12-byte header + 8-byte one-byte-ext block
 
 struct Plan {
+  std::vector<u8> dd;  // dependency-descriptor extension payload (DD tracks)
+  u64 extFn;           // unwrapped frame number (DD tracks)
+  u8 ddAttach;         // structure attached
+  u8 ddActive;         // active decode targets bitmask present
+  u32 ddMask;
+  u8 frameId;          // frame identity within a track for the integrity model: (superframe, spatial)
+  u8 framePkts;
   i64 arrival;
   u64 ext_sn;
   u64 ext_ts;
@@ -62,6 +69,7 @@ struct TrackGen {
   lkf_track_params p;
   int nlayers = 1;
   bool svc = false;         // VP9 SVC: all spatial layers in one stream (one SSRC)
+  bool dd = false;          // dependency descriptor on every packet (AV1, or VP9 with DD)
   u32 ssrc[3] = {0, 0, 0};  // per received layer (one ingress stream each)
   std::vector<Plan> plans;  // merged arrival order
 };
@@ -82,6 +90,7 @@ struct lkfs_trace {
   std::vector<lkf_track_params> tracks;
   std::vector<lkf_downtrack_params> dts;
   std::vector<u64> batch_pkt_off;    // nb+1
+  std::vector<u64> batch_raw_off;    // nb+1 (raw datagrams: a superset of the ExtPackets)
   std::vector<u64> batch_arena_off;  // nb+1
   std::vector<lkf_pkt> pkts;
   std::vector<lkf_raw_pkt> raws;  // the same datagrams as raw ingress input
@@ -89,6 +98,7 @@ struct lkfs_trace {
   std::vector<u8> arena;
   std::vector<u64> batch_ev_off;
   std::vector<lkfs_event> events;
+  std::vector<lkf_pkt_dd> dds;  // parallel to pkts
   u32 max_batch_pkts = 0;
   u64 max_batch_arena = 0;
   u64 max_batch_tuples = 0;
@@ -112,6 +122,120 @@ static void fill_payload(u8 *dst, int n, u64 key) {
   }
 }
 
+// ---- dependency-descriptor encoder (the publisher side of config 5) -----------
+// L3T3 with inter-layer prediction: per spatial layer s four templates (key T0,
+// T0, T1, T2), 9 decode targets (s*3 + t) protected by chain s (chain c = the
+// T0 frames of spatial layer c), resolutions 320x180 / 640x360 / 1280x720.
+// Frames that deviate from their template (chain diffs after a skipped layer,
+// the second reference of odd T2 frames) carry custom fields.
+struct DDTmplGen {
+  int sid, tid;
+  std::vector<int> fd, chains, dtis;
+};
+static std::vector<DDTmplGen> dd_templates() {
+  static const int ch[3][4][3] = {{{0, 0, 0}, {12, 11, 10}, {6, 5, 4}, {3, 2, 1}},
+                                  {{1, 0, 0}, {1, 12, 11}, {7, 6, 5}, {4, 3, 2}},
+                                  {{2, 1, 0}, {2, 1, 12}, {8, 7, 6}, {5, 4, 3}}};
+  std::vector<DDTmplGen> v;
+  for (int sp = 0; sp < 3; sp++)
+    for (int k = 0; k < 4; k++) {
+      DDTmplGen t;
+      t.sid = sp;
+      t.tid = k <= 1 ? 0 : k - 1;
+      static const int base[4] = {0, 12, 6, 3};
+      if (k > 0) t.fd.push_back(base[k]);
+      if (sp > 0) t.fd.push_back(1);
+      t.chains.assign(ch[sp][k], ch[sp][k] + 3);
+      for (int tg = 0; tg < 9; tg++) {
+        const int s2 = tg / 3, t2 = tg % 3;
+        int x = 0;
+        if (s2 >= t.sid && t2 >= t.tid) x = (k == 0) ? 2 : (k == 3 ? 1 : (s2 == t.sid ? 2 : 3));
+        t.dtis.push_back(x);
+      }
+      v.push_back(t);
+    }
+  return v;
+}
+struct BitOut {
+  std::vector<u8> b;
+  int n = 0;
+  void put(u64 v, int bits) {
+    for (int i = bits - 1; i >= 0; i--) {
+      if ((n >> 3) >= int(b.size())) b.push_back(0);
+      if ((v >> i) & 1) b[size_t(n >> 3)] |= u8(0x80u >> (n & 7));
+      n++;
+    }
+  }
+  void ns(u32 v, u32 numValues) {  // av1 ns(n)
+    if (numValues == 1) return;
+    int w = 0;
+    for (u32 x = numValues; x; x >>= 1) w++;
+    const u32 m = (1u << w) - numValues;
+    if (v < m)
+      put(v, w - 1);
+    else
+      put(v + m, w);
+  }
+};
+static std::vector<u8> dd_encode(const std::vector<DDTmplGen> &T, int structureId, bool first, bool last, int tmpl,
+                                 u16 fn, bool attach, bool active, u32 mask, const std::vector<int> &fd,
+                                 const std::vector<int> &chains) {
+  const DDTmplGen &t = T[size_t(tmpl)];
+  const bool cFd = fd != t.fd, cCh = chains != t.chains;
+  BitOut o;
+  o.put(first, 1);
+  o.put(last, 1);
+  o.put(u64((tmpl + structureId) % 64), 6);
+  o.put(fn, 16);
+  if (attach || active || cFd || cCh) {
+    o.put(attach, 1);
+    o.put(active, 1);
+    o.put(0, 1);
+    o.put(cFd, 1);
+    o.put(cCh, 1);
+    if (attach) {
+      o.put(u64(structureId), 6);
+      o.put(9 - 1, 5);
+      for (size_t i = 1; i < T.size(); i++) {
+        const int idc = (T[i].sid == T[i - 1].sid && T[i].tid == T[i - 1].tid) ? 0 : (T[i].sid == T[i - 1].sid) ? 1 : 2;
+        o.put(u64(idc), 2);
+      }
+      o.put(3, 2);
+      for (auto &x : T)
+        for (int d : x.dtis) o.put(u64(d), 2);
+      for (auto &x : T) {
+        for (int f : x.fd) o.put((1u << 4) | u32(f - 1), 5);
+        o.put(0, 1);
+      }
+      o.ns(3, 9 + 1);
+      for (int tg = 0; tg < 9; tg++) o.ns(u32(tg / 3), 3);
+      for (auto &x : T)
+        for (int c : x.chains) o.put(u64(c), 4);
+      o.put(1, 1);
+      static const int W[3] = {320, 640, 1280}, H[3] = {180, 360, 720};
+      for (int i = 0; i < 3; i++) {
+        o.put(u64(W[i] - 1), 16);
+        o.put(u64(H[i] - 1), 16);
+      }
+    }
+    if (active) o.put(mask, 9);
+    if (cFd) {
+      for (int f : fd) {
+        if (f <= 16)
+          o.put((1u << 4) | u32(f - 1), 6);
+        else if (f <= 256)
+          o.put((2u << 8) | u32(f - 1), 10);
+        else
+          o.put((3u << 12) | u32(f - 1), 14);
+      }
+      o.put(0, 2);
+    }
+    if (cCh)
+      for (int c : chains) o.put(u64(c & 0xff), 8);
+  }
+  return o.b;
+}
+
 extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   if (!cfg || cfg->config < 1 || cfg->config > 5) return nullptr;
   const int C = cfg->config;
@@ -130,6 +254,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   const i64 batchNs = i64(bs * NS);
   const bool withEvents = cfg->with_events != 0;
   const bool cb = cfg->has_callbacks != 0;
+  const bool svcDD = cfg->svc_dd != 0;
 
   u32 rooms = cfg->rooms, parts = cfg->participants;
   double loss = cfg->loss, reorder = cfg->reorder;
@@ -194,6 +319,12 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         g.p.kind = LKF_KIND_VIDEO;
         g.p.codec = C == 5 ? LKF_CODEC_VP9 : LKF_CODEC_VP8;
         g.svc = C == 5;
+        // configs[4]: AV1 (DD only) and VP9 with DD beside VP9-descriptor publishers
+        if (C == 5 && svcDD && (p % 4) != 3) {
+          g.dd = true;
+          g.p.has_dd = 1;
+          if ((p % 4) != 2) g.p.codec = LKF_CODEC_AV1;
+        }
         g.p.has_ref_ts = cb ? 1 : 0;
         g.p.is_mic = 0;
         g.p.clock_rate = 90000;
@@ -226,7 +357,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         d.subscriber = subId;
         d.ssrc = u32(rng.next()) | 1u;
         d.payload_type = video ? 96 : 111;
-        d.ext_dd = 0;
+        d.ext_dd = (video && tg[track].dd && (s % 3) != 2) ? 9 : 0;  // some subscribers lack the DD extension
         d.ext_playout = 0;
         d.ext_abs_send_time = video ? 3 : 0;
         d.has_expected_ts = cb ? 1 : 0;
@@ -315,6 +446,18 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       u16 pid0 = u16(rng.next() & 0x7fff);
       u8 tl00 = u8(rng.next());
       u16 twcc = u16(rng.next());
+      // dependency descriptor (DD tracks only: the RNG stream of VP9 tracks is unchanged)
+      static const std::vector<DDTmplGen> ddT = dd_templates();
+      int structureId = 0;
+      u64 fn0 = 0;
+      bool reducedTrack = false;
+      if (g.dd) {
+        structureId = int(rng.below(64));
+        fn0 = u64(ti % 5 == 0 ? u16(65536 - 40 - rng.below(40)) : u16(rng.next()));  // some wrap early
+        reducedTrack = (ti % 2) == 0;  // publisher drops S2 (active targets 0x3F) for 1 s
+      }
+      u64 lastChain[3] = {0, 0, 0};
+      bool wasReduced = false;
       std::vector<i64> reqs;
       for (int l = 0; l < 3; l++) reqs.insert(reqs.end(), kfReq[ti][l].begin(), kfReq[ti][l].end());
       std::sort(reqs.begin(), reqs.end());
@@ -330,8 +473,28 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         }
         if (kf) lastKf = cap;
         int tid = (f % 4 == 0) ? 0 : ((f % 4 == 2) ? 1 : 2);
+        const bool reduced = g.dd && reducedTrack && cap >= 2 * NS && cap < 3 * NS;
+        const bool sendMask = g.dd && (reduced || wasReduced);  // the change and the period
+        wasReduced = reduced;
         int k = 0;
         for (int sl = 0; sl < 3; sl++) {
+          if (reduced && sl == 2) continue;  // S2 not encoded
+          // the layer frame's descriptor (same template/custom fields on each packet)
+          std::vector<int> fdv, chv;
+          int tmpl = 0;
+          const u64 efn = fn0 + u64(f) * 3 + u64(sl);
+          if (g.dd) {
+            const int kk = kf ? 0 : (tid == 0 ? 1 : (tid == 1 ? 2 : 3));
+            tmpl = sl * 4 + kk;
+            fdv = ddT[size_t(tmpl)].fd;
+            if (!kf && tid == 2 && f % 4 == 3) fdv.push_back(9);
+            if (kf) {
+              chv = ddT[size_t(tmpl)].chains;
+            } else {
+              for (int c = 0; c < 3; c++) chv.push_back(int(std::min<u64>(255, efn - lastChain[c])));
+            }
+            if (kf || tid == 0) lastChain[sl] = efn;
+          }
           for (int q = 0; q < kSvcPkts[sl]; q++, k++) {
             Plan pl{};
             pl.arrival = t0 + cap + netDelay + i64(k) * 150000 + i64(rng.below(2000000));
@@ -350,7 +513,20 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
             pl.keyframe = kf && sl == 0 && q == 0;  // IsVP9KeyFrame (helpers.go:317-336)
             pl.vp9 = u8(LKF_VP9_I | LKF_VP9_L | (kf ? 0 : LKF_VP9_P) | (q == 0 ? LKF_VP9_B : 0) |
                         (q == kSvcPkts[sl] - 1 ? LKF_VP9_E : 0) | (tid > 0 ? LKF_VP9_U : 0));
-            pl.pt = 98;
+            pl.pt = g.p.codec == LKF_CODEC_AV1 ? 35 : 98;
+            if (g.dd) {
+              const bool attach = kf && sl == 0 && q == 0;
+              pl.tid = u8(ddT[size_t(tmpl)].tid);  // the descriptor's TemporalId (key superframes: T0)
+              const bool act = q == 0 && sl == 0 && (sendMask || (attach && reduced));
+              pl.extFn = efn;
+              pl.ddAttach = attach;
+              pl.ddActive = act;
+              pl.ddMask = reduced ? 0x3Fu : 0x1FFu;
+              pl.frameId = u8(sl);
+              pl.framePkts = u8(kSvcPkts[sl]);
+              pl.dd = dd_encode(ddT, structureId, q == 0, q == kSvcPkts[sl] - 1, tmpl, u16(efn), attach, act,
+                                pl.ddMask, fdv, chv);
+            }
             streams[0].push_back(pl);
           }
         }
@@ -442,7 +618,11 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         if (st[i].arrival <= st[i - 1].arrival) st[i].arrival = st[i - 1].arrival + 1000;
       if (reorder > 0) {
         for (size_t i = 0; i + 1 < st.size(); i++) {
-          if (rng.uni() < reorder) {
+          // DD streams keep their first packets in order: a packet older than
+          // the stream's first one is not handled at ingress
+          // (rtpstats_receiver.go), and the dependency descriptor of the
+          // opening key frame must reach the parser for the stream to be readable
+          if (rng.uni() < reorder && !(g.dd && i < 8)) {
             size_t j = std::min(st.size() - 1, i + 1 + rng.below(3));
             std::swap(st[i].arrival, st[j].arrival);
           }
@@ -473,6 +653,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       sp.layer = l;
       sp.ssrc = tg[ti].ssrc[l];
       sp.audio_level_ext = tg[ti].p.kind == LKF_KIND_AUDIO ? 1 : 0;
+      sp.dd_ext = tg[ti].dd ? 8 : 0;
       tr->streams.push_back(sp);
     }
   }
@@ -482,16 +663,33 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   std::vector<size_t> cursor(tg.size(), 0);
   // per (batch, track) index range for event mapping
   std::vector<std::vector<std::pair<u32, u32>>> trackRange(nb, std::vector<std::pair<u32, u32>>(tg.size()));
+  // header size of a raw packet: DD tracks carry the DD element before the
+  // transport-cc one (two-byte profile when the DD exceeds 16 bytes)
+  auto hdrSize = [](const TrackGen &g, const Plan &pl) -> u32 {
+    if (!g.dd) return kPayloadOff;
+    const u32 eh = pl.dd.size() > 16 ? 2 : 1;
+    const u32 el = eh + u32(pl.dd.size()) + eh + 2;
+    return 12 + 4 + ((el + 3) & ~3u);
+  };
   u64 totalArena = 0, totalPkts = 0;
   for (auto &g : tg)
     for (auto &pl : g.plans) {
       totalPkts++;
-      totalArena += (u64(kPayloadOff) + pl.payload_len + 15) & ~u64(15);
+      totalArena += (u64(hdrSize(g, pl)) + pl.payload_len + 15) & ~u64(15);
     }
+  // the ingress parser's view of each DD track, in arrival order (persists across batches)
+  struct DDTrackView {
+    bool hasStructure = false;
+    u64 structureFn = 0, activeSeq = 0;
+    u32 mask = 0;
+    std::vector<std::pair<u64, int>> arrived;  // (extFn, packets seen)
+  };
+  std::vector<DDTrackView> ddv(tg.size());
   tr->pkts.reserve(totalPkts);
   tr->arena.resize(totalArena);
   u64 aoff = 0;
   tr->batch_pkt_off.push_back(0);
+  tr->batch_raw_off.push_back(0);
   tr->batch_arena_off.push_back(0);
   for (u32 b = 0; b < nb; b++) {
     i64 end = (b + 1 == nb) ? INT64_MAX : t0 + i64(b + 1) * batchNs;
@@ -503,13 +701,16 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       while (cursor[ti] < g.plans.size() && g.plans[cursor[ti]].arrival < end) {
         const Plan &pl = g.plans[cursor[ti]++];
         lkf_pkt d{};
+        lkf_pkt_dd dd{};
+        bool keep = true;  // an ExtPacket is produced for this datagram
+        const u32 hsz = hdrSize(g, pl);
         d.ext_sn = pl.ext_sn;
         d.ext_ts = pl.ext_ts;
         d.arrival_ns = pl.arrival;
         d.arena_off = u32(aoff - batchA0);
         d.track = u32(ti);
         d.ssrc = pl.ssrc;
-        d.payload_off = kPayloadOff;
+        d.payload_off = u16(hsz);
         d.payload_len = pl.payload_len;
         d.hdr0 = 0x90;  // V=2, X=1, CC=0
         d.hdr1 = u8((pl.marker ? 0x80 : 0) | pl.pt);
@@ -532,9 +733,94 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         raw[13] = 0xDE;
         raw[14] = 0x00;
         raw[15] = 0x01;
-        u8 *pay = raw + kPayloadOff;
+        u8 *pay = raw + hsz;
         fill_payload(pay, pl.payload_len, (u64(pl.ssrc) << 32) ^ pl.ext_sn);
-        if (g.p.kind == LKF_KIND_VIDEO && g.svc) {
+        if (g.dd) {
+          // extension block: DD (id 8) then transport-cc (id 5)
+          const bool two = pl.dd.size() > 16;
+          const u32 words = (hsz - 16) / 4;
+          raw[12] = two ? 0x10 : 0xBE;
+          raw[13] = two ? 0x00 : 0xDE;
+          raw[14] = u8(words >> 8);
+          raw[15] = u8(words);
+          u32 o = 16;
+          if (two) {
+            raw[o++] = 8;
+            raw[o++] = u8(pl.dd.size());
+          } else {
+            raw[o++] = u8((8 << 4) | (pl.dd.size() - 1));
+          }
+          dd.dd_off = u16(o);
+          dd.dd_len = u8(pl.dd.size());
+          for (u8 x : pl.dd) raw[o++] = x;
+          if (two) {
+            raw[o++] = 5;
+            raw[o++] = 2;
+          } else {
+            raw[o++] = 0x51;
+          }
+          raw[o++] = u8(pl.twcc >> 8);
+          raw[o++] = u8(pl.twcc);
+          while (o < hsz) raw[o++] = 0;
+          if (g.p.codec == LKF_CODEC_AV1) {
+            // AV1 aggregation header; the key superframe's first packet holds a
+            // sequence header OBU and a KEY_FRAME OBU_FRAME (IsAV1KeyFrame)
+            if (pl.keyframe && pl.payload_len > 16) {
+              pay[0] = 0x28;  // Z=0 Y=0 W=2 N=1
+              pay[1] = 8;     // OBU_SEQUENCE_HEADER, 8 bytes
+              pay[2] = 0x08;
+              pay[10] = 0x30;  // OBU_FRAME
+              pay[11] = 0x10;  // show_existing_frame 0, KEY_FRAME, show_frame
+            } else {
+              pay[0] = u8((pl.s_bit ? 0x00 : 0x80) | 0x10);  // Z (continuation) W=1 N=0
+            }
+          } else {  // VP9 with DD: the VP9 payload descriptor is still there (IsVP9KeyFrame)
+            pay[0] = u8((pl.vp9 & (LKF_VP9_I | LKF_VP9_P | LKF_VP9_L | LKF_VP9_F | LKF_VP9_B | LKF_VP9_E | LKF_VP9_V)));
+            pay[1] = u8(0x80 | (pl.pid >> 8));
+            pay[2] = u8(pl.pid);
+            pay[3] = u8((pl.tid << 5) | ((pl.vp9 & LKF_VP9_U) ? 0x10 : 0) | (u8(pl.layer) << 1));
+            pay[4] = pl.tl0;
+            if (pl.vp9 & LKF_VP9_B) pay[5] = pl.keyframe ? 0x82 : 0x86;
+          }
+          d.flags = LKF_PKT_DD | (pl.keyframe ? LKF_PKT_KEYFRAME : 0);
+          d.spatial = pl.layer;  // VideoLayer from the DD (dependencydescriptorparser.go:101-103)
+          d.temporal = int8_t(pl.tid);
+          // the ingress parser's metadata, in arrival order (dependencydescriptorparser.go:99-162);
+          // a packet the parser rejects produces no ExtPacket (buffer.go:613-616): no
+          // structure yet, or a frame older than the current structure's
+          DDTrackView &v = ddv[ti];
+          if ((!v.hasStructure && !pl.ddAttach) || (v.hasStructure && pl.extFn < v.structureFn)) keep = false;
+          dd.ext_frame_num = pl.extFn;
+          if (keep && pl.ddAttach) {
+            v.hasStructure = true;
+            v.structureFn = pl.extFn;
+            dd.flags |= LKF_DD_STRUCTURE_UPDATED | LKF_DD_ACTIVE_UPDATED;
+          }
+          const bool maskPresent = keep && (pl.ddAttach || pl.ddActive);
+          const u32 mask = pl.ddActive ? pl.ddMask : 0x1FFu;
+          if (maskPresent && pl.ext_sn > v.activeSeq) {
+            v.activeSeq = pl.ext_sn;
+            if (mask != v.mask) {
+              v.mask = mask;
+              dd.flags |= LKF_DD_ACTIVE_UPDATED;
+            }
+          }
+          dd.ext_key_frame_num = v.structureFn;
+          int seen = 1;
+          bool found = !keep;
+          for (auto &a : v.arrived) {
+            if (found) break;
+            if (a.first == pl.extFn) {
+              seen = ++a.second;
+              found = true;
+            }
+          }
+          if (!found) {
+            v.arrived.push_back({pl.extFn, 1});
+            if (v.arrived.size() > 256) v.arrived.erase(v.arrived.begin());
+          }
+          if (seen == pl.framePkts) dd.flags |= LKF_DD_INTEGRITY;
+        } else if (g.p.kind == LKF_KIND_VIDEO && g.svc) {
           raw[16] = 0x51;  // id 5 (transport-cc), len 2
           raw[17] = u8(pl.twcc >> 8);
           raw[18] = u8(pl.twcc);
@@ -591,16 +877,20 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         rp.arrival_ns = pl.arrival;
         rp.stream = streamBase[ti] + u32((g.nlayers == 1 || g.svc) ? 0 : pl.layer);
         rp.off = d.arena_off;
-        rp.len = u32(kPayloadOff) + pl.payload_len;
+        rp.len = hsz + pl.payload_len;
         tr->raws.push_back(rp);
-        aoff += (u64(kPayloadOff) + pl.payload_len + 15) & ~u64(15);
-        tr->pkts.push_back(d);
+        aoff += (u64(hsz) + pl.payload_len + 15) & ~u64(15);
+        if (keep) {
+          tr->pkts.push_back(d);
+          tr->dds.push_back(dd);
+        }
       }
       trackRange[b][ti] = {rb, u32(tr->pkts.size() - batchP0)};
     }
     tr->batch_pkt_off.push_back(tr->pkts.size());
+    tr->batch_raw_off.push_back(tr->raws.size());
     tr->batch_arena_off.push_back(aoff);
-    tr->max_batch_pkts = std::max(tr->max_batch_pkts, u32(tr->pkts.size() - batchP0));
+    tr->max_batch_pkts = std::max(tr->max_batch_pkts, u32(tr->raws.size() - tr->batch_raw_off[b]));
     tr->max_batch_arena = std::max(tr->max_batch_arena, aoff - batchA0);
   }
 
@@ -613,7 +903,9 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       for (size_t ti = 0; ti < tg.size(); ti++) {
         tup += u64(trackRange[b][ti].second - trackRange[b][ti].first) * dtsPerTrack[ti];
         u64 tb = 0;  // wire packet <= payload + 12-B header + 12-B extension block + 1 (descriptor growth), 16-B aligned
-        for (u32 i = trackRange[b][ti].first; i < trackRange[b][ti].second; i++) tb += (u64(bp[i].payload_len) + 25 + 15) & ~u64(15);
+        const u64 extra = tg[ti].dd ? 25 + 2 + 255 : 25;  // + a DD element up to 255 bytes
+        for (u32 i = trackRange[b][ti].first; i < trackRange[b][ti].second; i++)
+          tb += (u64(bp[i].payload_len) + extra + 15) & ~u64(15);
         ob += tb * dtsPerTrack[ti];
       }
       tr->max_batch_tuples = std::max(tr->max_batch_tuples, tup);
@@ -670,12 +962,18 @@ extern "C" int lkfs_batch(const lkfs_trace *t, uint32_t b, const lkf_pkt **pkts,
   return LKF_OK;
 }
 
+extern "C" int lkfs_batch_dd(const lkfs_trace *t, uint32_t b, const lkf_pkt_dd **dd, uint32_t *n) {
+  if (b + 1 >= t->batch_pkt_off.size()) return LKF_EINVAL;
+  *dd = t->dds.data() + t->batch_pkt_off[b];
+  *n = u32(t->batch_pkt_off[b + 1] - t->batch_pkt_off[b]);
+  return LKF_OK;
+}
 extern "C" uint32_t lkfs_num_streams(const lkfs_trace *t) { return u32(t->streams.size()); }
 extern "C" const lkf_stream_params *lkfs_streams(const lkfs_trace *t) { return t->streams.data(); }
 extern "C" int lkfs_batch_raw(const lkfs_trace *t, uint32_t b, const lkf_raw_pkt **raws, uint32_t *n) {
   if (b + 1 >= t->batch_pkt_off.size()) return -1;
-  *raws = t->raws.data() + t->batch_pkt_off[b];
-  *n = u32(t->batch_pkt_off[b + 1] - t->batch_pkt_off[b]);
+  *raws = t->raws.data() + t->batch_raw_off[b];
+  *n = u32(t->batch_raw_off[b + 1] - t->batch_raw_off[b]);
   return 0;
 }
 extern "C" int lkfs_batch_events(const lkfs_trace *t, uint32_t b, const lkfs_event **ev, uint32_t *n) {

@@ -30,6 +30,8 @@ typedef struct lkfs_cfg {
   double reorder;        /* -1 -> config default */
   int32_t with_events;   /* -1 -> default (1) */
   int32_t has_callbacks; /* -1 -> default (1): has_ref_ts / has_expected_ts */
+  int32_t svc_dd;        /* config 5: -1 -> default (1): AV1 + VP9 publishers with the dependency
+                            descriptor beside VP9-descriptor ones; 0: VP9 descriptor only */
 } lkfs_cfg;
 
 typedef struct lkfs_event {
@@ -55,6 +57,11 @@ uint32_t lkfs_num_batches(const lkfs_trace *t);
 int lkfs_batch(const lkfs_trace *t, uint32_t b, const lkf_pkt **pkts, uint32_t *n, const uint8_t **arena,
                uint64_t *arena_len);
 int lkfs_batch_events(const lkfs_trace *t, uint32_t b, const lkfs_event **ev, uint32_t *n);
+/* Batch b's lkf_pkt_dd side array (parallel to lkfs_batch; meaningful for
+ * LKF_PKT_DD packets): what the ingress DependencyDescriptorParser reports for
+ * the generated stream (extended frame numbers, the structure's frame, updates,
+ * frame integrity in arrival order). */
+int lkfs_batch_dd(const lkfs_trace *t, uint32_t b, const lkf_pkt_dd **dd, uint32_t *n);
 /* Totals over the whole trace. */
 uint64_t lkfs_total_pkts(const lkfs_trace *t);
 uint64_t lkfs_total_arena(const lkfs_trace *t);

@@ -13,11 +13,11 @@ from . import abi
 
 class Trace:
     def __init__(self, config, duration_s=10.0, batch_s=1.0, rooms=0, participants=0, room_base=0,
-                 loss=-1.0, reorder=-1.0, with_events=-1, has_callbacks=-1, seed=0, synth_lib=None):
+                 loss=-1.0, reorder=-1.0, with_events=-1, has_callbacks=-1, seed=0, svc_dd=-1, synth_lib=None):
         self.lib = synth_lib or abi.load_synth()
         cfg = abi.lkfs_cfg(config=config, seed=seed, duration_s=duration_s, batch_s=batch_s, rooms=rooms,
                            participants=participants, room_base=room_base, loss=loss, reorder=reorder,
-                           with_events=with_events, has_callbacks=has_callbacks)
+                           with_events=with_events, has_callbacks=has_callbacks, svc_dd=svc_dd)
         self.config = config
         self.h = self.lib.lkfs_generate(C.byref(cfg))
         if not self.h:
@@ -45,6 +45,17 @@ class Trace:
         if rc != 0:
             raise IndexError(b)
         return pk, n.value, ar, alen.value
+
+    def batch_dd(self, b):
+        """Batch b's lkf_pkt_dd side array (pointer, n) — parallel to batch(b)."""
+        dd = C.POINTER(abi.lkf_pkt_dd)()
+        n = C.c_uint32()
+        if self.lib.lkfs_batch_dd(self.h, b, C.byref(dd), C.byref(n)) != 0:
+            raise IndexError(b)
+        return dd, n.value
+
+    def has_dd(self):
+        return any(self.tracks[t].has_dd for t in range(self.ntracks))
 
     def batch_raw(self, b):
         """Batch b as raw datagrams (ingress input): (raw_pkts, n, arena, arena_len)."""

@@ -17,6 +17,8 @@
 //  (16-B aligned).
 // =============================================================================
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <thread>
 
@@ -638,7 +640,9 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
       int off = 0, len = 0;
       const u8 *ddBuf = h.GetExtension(b.p.dd_ext, off, len) ? buf + off : nullptr;
       VideoLayer vl;
-      if (b.ddParser->Parse(ddBuf, len, u16(f.ext_sn), ddv, vl) != DDP_OK) {
+      const DDParseErr pe = b.ddParser->Parse(ddBuf, len, u16(f.ext_sn), ddv, vl);
+      if (pe != DDP_OK) {
+        if (getenv("ORC_DD_DEBUG")) fprintf(stderr, "dd parse err %d track %d sn %u len %d fn %u hasStruct %d\n", int(pe), b.p.track, unsigned(h.sn), len, ddBuf ? unsigned((ddBuf[1] << 8) | ddBuf[2]) : 0u, b.ddParser->structure ? 1 : 0);
         f.flags |= LKF_FLOW_BAD;
         return f;
       }

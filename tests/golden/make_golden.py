@@ -36,7 +36,7 @@ def main():
             return st.as_dict()
 
         fx = golden_lib.run_case(o.api, h, tr, wl, stats, lambda: pkg.drain_arrays(o.api, h),
-                                 lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi)
+                                 lambda pk, n, ar, alen, dd: o.run(h, pk, n, ar, alen, dd), abi)
         fx["case"] = name
         fx["trace"] = kw
         with open(golden_lib.path(name), "w") as f:

@@ -26,6 +26,8 @@ CASES = [
     ("config3_1room", dict(config=3, duration_s=2.0, batch_s=1.0, rooms=1)),
     ("config4_64subs", dict(config=4, duration_s=1.0, batch_s=0.5, rooms=1, participants=64)),
     ("config5_4rooms", dict(config=5, duration_s=3.0, batch_s=0.5, rooms=4)),
+    ("config5_vp9only", dict(config=5, duration_s=2.0, batch_s=0.5, rooms=3, svc_dd=0)),
+    ("config5_dd_loss", dict(config=5, duration_s=3.0, batch_s=0.25, rooms=2, loss=0.15, reorder=0.1, seed=17)),
 ]
 
 RECORD_FIELDS = ("ext_sn", "ext_ts", "out_off", "dt", "pkt", "out_len", "flags", "layer")
@@ -68,13 +70,16 @@ def load(name):
 
 
 def run_case(api, h, trace, workload, stats_fn, drain_fn, run_fn, abi):
-    """Drives one trace through an lkf_*-shaped engine; returns the fixture dict."""
+    """Drives one trace through an lkf_*-shaped engine; returns the fixture dict.
+    run_fn(pk, n, ar, alen, dd): dd = the lkf_pkt_dd side array pointer of the
+    batch (dependency-descriptor traces) or None."""
     workload.load_topology(api, h, trace)
+    has_dd = trace.has_dd()
     out = {"batches": []}
     for b in range(trace.nbatches):
         workload.queue_events(api, h, trace, b)
         pk, n, ar, alen = trace.batch(b)
-        run_fn(pk, n, ar, alen)
+        run_fn(pk, n, ar, alen, trace.batch_dd(b)[0] if has_dd else None)
         rec, war = drain_fn()
         out["batches"].append(dict(batch_entry(stats_fn(), rec, war), n_pkts=int(n)))
     out["state_sha256"] = state_digest(api, h, trace.ndts, abi)

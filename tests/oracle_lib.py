@@ -41,7 +41,10 @@ class Oracle:
     def destroy(self, h):
         self.lib.orc_destroy(h)
 
-    def run(self, h, pkts, n, arena, alen):
+    def run(self, h, pkts, n, arena, alen, dd=None):
+        """orc_submit_dd (when the batch has a lkf_pkt_dd side array) + orc_run."""
+        if dd is not None:
+            assert self.api["submit_dd"](h, C.cast(dd, C.c_void_p), n) == 0
         rc = self.lib.orc_run(h, C.cast(pkts, C.c_void_p), n, C.cast(arena, C.c_void_p), alen)
         assert rc == 0, rc
 

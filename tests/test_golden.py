@@ -39,7 +39,7 @@ def test_oracle_matches_golden(name, workload, abi, pkg):
             return st.as_dict()
 
         got = golden_lib.run_case(o.api, h, tr, workload, stats, lambda: pkg.drain_arrays(o.api, h),
-                                  lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi)
+                                  lambda pk, n, ar, alen, dd: o.run(h, pk, n, ar, alen, dd), abi)
     finally:
         o.destroy(h)
         tr.close()
@@ -53,8 +53,8 @@ def test_engine_matches_golden(name, workload, abi, pkg):
     tr = workload.Trace(**CASE_KW[name])
     eng = pkg.Engine.for_trace(tr)
     try:
-        def run(pk, n, ar, alen):
-            eng.submit(pk, n, ar, alen)
+        def run(pk, n, ar, alen, dd):
+            eng.submit(pk, n, ar, alen, dd)
             eng.run()
             eng.sync()
 

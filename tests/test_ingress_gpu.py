@@ -94,7 +94,7 @@ def test_ingress_config2_loss_reorder(pkg, workload, abi):
 
 def test_ingress_config5_vp9(pkg, workload, abi):
     """VP9 SVC datagrams: VP9 descriptor parse, key frames, SID dispatch, then forwarding."""
-    tr = workload.Trace(5, duration_s=3.0, batch_s=0.5, rooms=4, loss=0.05, reorder=0.03, seed=31)
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.5, rooms=4, loss=0.05, reorder=0.03, seed=31, svc_dd=0)
     assert run_ingress_parity(pkg, workload, abi, tr) > 0
 
 

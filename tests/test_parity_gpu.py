@@ -43,10 +43,11 @@ def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True, extr
                 assert eng.api["ctl"](eng.h, dt, op, a0, a1, a2, a3, at) == 0
                 assert o.api["ctl"](oh, dt, op, a0, a1, a2, a3, at) == 0
             pk, n, ar, alen = trace.batch(b)
-            eng.submit(pk, n, ar, alen)
+            dd = trace.batch_dd(b)[0] if trace.has_dd() else None
+            eng.submit(pk, n, ar, alen, dd)
             eng.run()
             eng.sync()
-            o.run(oh, pk, n, ar, alen)
+            o.run(oh, pk, n, ar, alen, dd)
             gs = eng.stats()
             ost = abi.lkf_stats()
             o.api["get_stats"](oh, C.byref(ost))
@@ -131,16 +132,36 @@ def test_config4_small(pkg, workload, abi):
 
 
 def test_config5_vp9_svc(pkg, workload, abi):
-    """configs[4] shape: VP9 L3T3 SVC (VP9 selector, relevant drops, synthesized
-    markers) + Opus DTX, per-DT target changes every 1 s with deficient downgrades."""
-    tr = workload.Trace(5, duration_s=4.0, batch_s=0.5, rooms=12)
+    """configs[4] shape, VP9-descriptor publishers only: VP9 L3T3 SVC (VP9 selector,
+    relevant drops, synthesized markers) + Opus DTX, per-DT target changes every
+    1 s with deficient downgrades."""
+    tr = workload.Trace(5, duration_s=4.0, batch_s=0.5, rooms=12, svc_dd=0)
     t = run_parity(pkg, workload, abi, tr)
     assert t["forwarded"] > 0
 
 
 def test_config5_vp9_heavy_loss(pkg, workload, abi):
     """VP9 SVC under 20% loss / 15% reorder: OOO and gap paths through the VP9 selector."""
-    tr = workload.Trace(5, duration_s=3.0, batch_s=0.25, rooms=4, loss=0.2, reorder=0.15, seed=55)
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.25, rooms=4, loss=0.2, reorder=0.15, seed=55, svc_dd=0)
+    run_parity(pkg, workload, abi, tr)
+
+
+def test_config5_av1_vp9_dd(pkg, workload, abi):
+    """configs[4] as specified: AV1 (DD only) and VP9 with the dependency
+    descriptor beside VP9-descriptor publishers.  DD selector (decision cache,
+    chains, decode targets, active-target updates when a publisher drops S2,
+    frame-number wrap), DD re-marshal per tuple (one- and two-byte extension
+    profiles), subscribers with and without the DD extension."""
+    tr = workload.Trace(5, duration_s=5.0, batch_s=0.5, rooms=12)
+    assert tr.has_dd()
+    t = run_parity(pkg, workload, abi, tr)
+    assert t["forwarded"] > 0
+
+
+def test_config5_dd_heavy_loss(pkg, workload, abi):
+    """DD SVC under 20% loss / 15% reorder: unknown / missing decisions, broken and
+    recovered chains, frames that are not decodable."""
+    tr = workload.Trace(5, duration_s=4.0, batch_s=0.25, rooms=6, loss=0.2, reorder=0.15, seed=56)
     run_parity(pkg, workload, abi, tr)
 
 
