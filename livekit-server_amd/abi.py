@@ -255,6 +255,7 @@ class lkfs_cfg(C.Structure):
         ("with_events", C.c_int32),
         ("has_callbacks", C.c_int32),
         ("svc_dd", C.c_int32),
+        ("h264", C.c_int32),
     ]
 
 

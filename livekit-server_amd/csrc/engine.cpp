@@ -158,6 +158,11 @@ struct lkf_engine {
   uint32_t ddTrackInit = 0;
   std::vector<uint8_t> dtIsDD;    // per DownTrack: scheduled in k_decide_dt<true>
   uint32_t ddLanes = 0;
+  // ingress DependencyDescriptorParser per DD stream (allocated with the first)
+  uint32_t nDDStreams = 0, ddStreamInit = 0;
+  DDIngState *dDDIng = nullptr;      // [stream.ddIdx]
+  DDStruct *dDDIngStruct = nullptr;  // [stream.ddIdx * 2 + DI_CUR slot]
+  IngDD *dIngDD = nullptr;           // per datagram of an ingest
 
   // batch input for the next run
   const lkf_pkt_dd *curDD = nullptr;
@@ -321,15 +326,26 @@ static int upload_done(lkf_engine *e) {
 // The DD selector tables and per-batch DD buffers, allocated when the first
 // track with the dependency-descriptor selector appears (streams drained).
 static int ensure_dd(lkf_engine *e) {
-  if (e->ddAlloc || e->nDDTracks == 0) return LKF_OK;
   const lkf_cfg &c = e->cfg;
+  if ((e->nDDTracks || e->nDDStreams) && !e->ctx[0].dDDIn)  // ingest output / lkf_submit_dd input
+    for (auto &x : e->ctx) HIPCHK(dalloc(&x.dDDIn, c.max_batch_pkts), "alloc dd in");
+  if (e->nDDStreams && !e->dDDIng) {
+    HIPCHK(dalloc(&e->dDDIng, e->maxStreams), "alloc dd parsers");
+    HIPCHK(dalloc(&e->dDDIngStruct, size_t(e->maxStreams) * 2), "alloc dd parser structures");
+    HIPCHK(dalloc(&e->dIngDD, c.max_batch_pkts), "alloc ingest dd");
+  }
+  if (e->nDDStreams > e->ddStreamInit) {  // a fresh parser per new DD stream
+    HIPCHK(hipMemset(e->dDDIng + e->ddStreamInit, 0, size_t(e->nDDStreams - e->ddStreamInit) * sizeof(DDIngState)),
+           "dd parser reset");
+    e->ddStreamInit = e->nDDStreams;
+  }
+  if (e->ddAlloc || e->nDDTracks == 0) return LKF_OK;
   HIPCHK(dalloc(&e->dDDStruct, size_t(c.max_tracks) * kDDSlots), "alloc dd structures");
   HIPCHK(dalloc(&e->dDDTrack, c.max_tracks), "alloc dd tracks");
   HIPCHK(dalloc(&e->dDDState, c.max_downtracks), "alloc dd state");
   HIPCHK(hipMemset(e->dDDTrack, 0, size_t(c.max_tracks) * sizeof(DDTrack)), "dd tracks reset");
   e->ddArenaCap = c.max_out_bytes / 4 + (1u << 20);
   for (auto &x : e->ctx) {
-    HIPCHK(dalloc(&x.dDDIn, c.max_batch_pkts), "alloc dd in");
     HIPCHK(dalloc(&x.dDDPkt, c.max_batch_pkts), "alloc dd pkts");
     HIPCHK(dalloc(&x.dDDArena, e->ddArenaCap), "alloc dd arena");
     HIPCHK(dalloc(&x.dDDUsed, 1), "alloc dd cursor");
@@ -526,7 +542,8 @@ void lkf_destroy(lkf_engine *e) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
-                  static_cast<void *>(e->dDDState)})
+                  static_cast<void *>(e->dDDState), static_cast<void *>(e->dDDIng),
+                  static_cast<void *>(e->dDDIngStruct), static_cast<void *>(e->dIngDD)})
     if (p) (void)hipFree(p);
   for (auto &x : e->ctx) {
     for (void *p : {static_cast<void *>(x.dDDIn), static_cast<void *>(x.dDDPkt), static_cast<void *>(x.dDDArena),
@@ -1057,6 +1074,10 @@ int lkf_sync(lkf_engine *e) {
     e->err = "raw batch not grouped by track / bad stream handle";
     return LKF_EORDER;
   }
+  if (acc & (4u << 8)) {
+    e->err = "dependency descriptor beyond an engine limit (templates, frame diffs, chains)";
+    return LKF_ENOSPC;
+  }
   if (acc & 16u) {
     e->err = "dependency descriptor unreadable, missing its lkf_pkt_dd entry, or beyond an engine limit";
     return LKF_EINVAL;
@@ -1269,6 +1290,8 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p) {
   d.clockRate = tp.clock_rate;
   d.codec = tp.codec;
   d.levelExt = p->audio_level_ext;
+  d.ddExt = p->dd_ext;
+  d.ddIdx = p->dd_ext ? e->nDDStreams++ : 0xffffffffu;  // its DependencyDescriptorParser (buffer.go:193-201)
   const bool dflt = !p->active_level && !p->min_percentile && !p->observe_duration_ms && !p->smooth_intervals;
   d.activeLevel = dflt ? 35 : p->active_level;
   d.minPercentile = dflt ? 40 : p->min_percentile;
@@ -1319,13 +1342,18 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.partB = e->dIPartB;
   a.total = e->dITotal;
   a.out = x.dPktsOwn;
+  const bool dd = e->nDDStreams != 0;
+  a.ddStates = dd ? e->dDDIng : nullptr;
+  a.ddStructs = dd ? e->dDDIngStruct : nullptr;
+  a.ingDD = dd ? e->dIngDD : nullptr;
+  a.outDD = dd ? x.dDDIn : nullptr;
   HIPCHK(launch_ingest(s, a), "ingest");
   HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 8), "ingest error fold");
   e->lastIngestN = n;
   e->curPkts = x.dPktsOwn;
   e->curN = n;  // launch bound; the count is e->dITotal
   e->curNDev = e->dITotal;
-  e->curDD = nullptr;
+  e->curDD = a.outDD;  // the ExtPackets' descriptors (nullptr: no DD stream)
   e->curArena = dRaw;
   e->curArenaLen = rawLen;
   e->haveBatch = true;

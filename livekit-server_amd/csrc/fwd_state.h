@@ -230,10 +230,11 @@ struct DevStream {  // static stream parameters (64 B)
   uint8_t codec, levelExt, activeLevel, minPercentile;
   uint32_t observeDuration;  // ms
   uint32_t minActiveDuration;
-  uint32_t pad0;
+  uint32_t ddIdx;          // index of the stream's DependencyDescriptorParser (0xffffffff: none)
   double smoothFactor;
   double activeThreshold;  // ConvertAudioLevel(ActiveLevel)
-  uint32_t pad1[4];
+  uint8_t ddExt;           // dependency-descriptor extension id
+  uint8_t pad1[15];
 };
 static_assert(sizeof(DevStream) == 64, "DevStream must be 64 B");
 
@@ -275,11 +276,41 @@ struct alignas(16) IngParsed {  // k_ing_parse -> k_ing_stream / k_ing_out (48 B
   uint16_t pid;
   uint32_t track;
   uint8_t vp9bits, sid;  // codecs.VP9Packet flags (LKF_VP9_*) and SID
-  uint8_t pad[14];
+  uint16_t ddOff;        // the DD extension payload (Header.GetExtension), ddLen 0: absent
+  uint8_t ddLen;
+  uint8_t pad[11];
 };
 static_assert(sizeof(IngParsed) == 48, "IngParsed must be 48 B");
 // IP_VP8_BAD: the codec payload (VP8 or VP9) failed to unmarshal
 enum : uint8_t { IP_OK = 1, IP_MARKER = 2, IP_LEVEL = 4, IP_VP8 = 8, IP_KF = 16, IP_VP8_BAD = 32, IP_VP9 = 64 };
+// IP_VP8_BAD: the codec payload (VP8, or VP9 without a DD) failed to unmarshal
+
+// One received stream's buffer.DependencyDescriptorParser
+// (dependencydescriptorparser.go:35-61) with its FrameIntegrityChecker(180,
+// 1024) (frameintegrity.go:150-211).  Its structures: two slots (current and
+// the one an attached structure is read into).
+constexpr int kFICFrames = 180, kFICPktWords = 16;
+enum : uint32_t { DI_SEQ_INIT = 1, DI_FN_INIT = 2, DI_HAS_STRUCT = 4, DI_CUR = 8, DI_FC_INIT = 16, DI_PH_INIT = 32 };
+struct alignas(16) DDIngState {
+  uint64_t seqCycles, seqExtHighest, fnCycles, fnExtHighest;  // WrapAround<uint16,uint64> x2
+  uint16_t seqStart, seqHighest, fnStart, fnHighest;
+  uint32_t flags;  // DI_*
+  uint32_t activeMask;
+  uint64_t structureExtFN, activeExtSeq;
+  uint64_t fcBase, fcLast, phBase, phLast;
+  uint64_t phBits[kFICPktWords];
+  uint64_t feStart[kFICFrames], feEnd[kFICFrames];
+  uint8_t feFlags[kFICFrames];  // 1 hasStart, 2 hasEnd, 4 integrity
+  uint8_t pad[12];
+};
+static_assert(sizeof(DDIngState) % 16 == 0, "DDIngState must be 16-B granular");
+struct IngDD {  // k_ing_stream -> k_ing_out: one datagram's ExtDependencyDescriptor (32 B)
+  uint64_t extFN, extKFN;
+  uint16_t ddOff;
+  uint8_t ddLen, flags;  // LKF_DD_*
+  uint8_t present, sid, tid, pad;
+  uint64_t pad2;
+};
 
 struct DevEvent {  // one queued lkf_ctl op (48 B)
   uint32_t at;

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/lkfwd.h"
+#include "dd_device.h"
 #include "fwd_state.h"
 #include "kernels.h"
 
@@ -39,7 +40,8 @@ using i64 = int64_t;
 // ---------------------------------------------------------------------------
 // k_ing_parse
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, IngParsed &q, int &levelOff) {
+__device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, u8 ddExt, IngParsed &q,
+                                          int &levelOff) {
   levelOff = -1;
   if (len < 12) return false;
   q.b0 = buf[0];
@@ -60,7 +62,7 @@ __device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, I
     const int extEnd = n + extLen;
     if (len < extEnd) return false;
     if (profile == 0xBEDE || profile == 0x1000) {
-      bool seen = false;  // Header.GetExtension returns the first element with the id
+      bool seen = false, seenDD = false;  // Header.GetExtension returns the first element with the id
       while (n < extEnd) {
         if (buf[n] == 0x00) {
           n++;
@@ -84,6 +86,11 @@ __device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, I
         if (levelExt && id == levelExt && !seen) {
           seen = true;
           if (pl >= 1) levelOff = n;  // AudioLevelExtension.Unmarshal needs 1 byte
+        }
+        if (ddExt && id == ddExt && !seenDD) {
+          seenDD = true;
+          q.ddOff = u16(n);
+          q.ddLen = u8(pl);
         }
         n += pl;
       }
@@ -168,6 +175,91 @@ __device__ __forceinline__ bool vp8_parse(const u8 *p, int len, IngParsed &q) {
   q.keyidx = keyidx;
   if (kf) q.flags |= IP_KF;
   return true;
+}
+
+// buffer.IsH264KeyFrame helpers.go:248-309
+__device__ inline bool h264_keyframe(const u8 *p, int n) {
+  if (n < 1) return false;
+  const int nalu = p[0] & 0x1F;
+  if (nalu == 0) return false;
+  if (nalu <= 23) return nalu == 7;
+  if (nalu >= 24 && nalu <= 27) {  // STAP-A/B, MTAP16/24
+    int i = 1;
+    if (nalu != 24) i += 2;  // DON
+    while (i < n) {
+      if (i + 2 > n) return false;
+      const int length = (int(p[i]) << 8) | int(p[i + 1]);
+      i += 2;
+      if (i + length > n) return false;
+      const int offset = nalu == 26 ? 3 : nalu == 27 ? 4 : 0;
+      if (offset >= length) return false;
+      if ((p[i + offset] & 0x1F) == 7) return true;
+      i += length;
+    }
+    return false;
+  }
+  if (nalu == 28 || nalu == 29) {  // FU-A/B: starting fragment of an SPS
+    if (n < 2) return false;
+    if ((p[1] & 0x80) == 0) return false;
+    return (p[1] & 0x1F) == 7;
+  }
+  return false;
+}
+
+// buffer.IsAV1KeyFrame helpers.go:343-420: walk the aggregation's OBUs (W
+// field: the last one carries no length) to the first frame header
+__device__ inline bool av1_keyframe(const u8 *payload, int n) {
+  if (n < 2) return false;
+  if ((payload[0] & 0x88) != 0x08) return false;  // Z=0, N=1
+  const int w = (payload[0] & 0x30) >> 4;
+  int offset = 1;
+  for (int i = 0;; i++) {
+    const u8 *data = payload + offset;
+    const int dn = n - offset;
+    const u8 *obu;
+    int olen, length;
+    bool truncated = false;
+    if (w == i + 1) {
+      obu = data;
+      olen = dn;
+      length = dn;
+    } else {
+      int off = 0, len = 0;
+      bool done = false;
+      for (;;) {
+        if (dn <= off) {
+          done = true;
+          break;
+        }
+        const u8 l = data[off];
+        len |= int(l & 0x7f) << (off * 7);
+        off++;
+        if ((l & 0x80) == 0) break;
+      }
+      if (done) return false;  // no OBU
+      if (dn < off + len) {
+        obu = data + off;
+        olen = dn - off;
+        length = dn;
+        truncated = true;
+      } else {
+        obu = data + off;
+        olen = len;
+        length = off + len;
+      }
+    }
+    if (olen < 1) return false;
+    const int tpe = (obu[0] & 0x38) >> 3;
+    if (i == 0) {
+      if (tpe != 1) return false;  // OBU_SEQUENCE_HEADER
+    } else if (tpe == 3 || tpe == 6) {
+      if (olen < 2) return false;
+      if ((obu[1] & 0x80) != 0) return false;  // show_existing_frame
+      return (obu[1] & 0x60) == 0;             // KEY_FRAME
+    }
+    if (truncated || i >= w) return false;
+    offset += length;
+  }
 }
 
 // codecs.VP9Packet.Unmarshal (pion/rtp v1.8.3 codecs/vp9_packet.go; not in
@@ -270,7 +362,7 @@ __global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u
   q.track = s.track;
   const u8 *b = raw + rp.off;
   int levelOff = -1;
-  if (rtp_parse(b, int(rp.len), s.levelExt, q, levelOff)) {
+  if (rtp_parse(b, int(rp.len), s.levelExt, s.ddExt, q, levelOff)) {
     q.flags |= IP_OK;
     if (levelOff >= 0) {  // AudioLevelExtension.Unmarshal: level = b & 0x7f
       q.flags |= IP_LEVEL;
@@ -286,6 +378,10 @@ __global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u
         q.flags |= IP_VP9;
       else
         q.flags |= IP_VP8_BAD;
+    } else if (s.codec == LKF_CODEC_H264 && q.payloadLen > 0) {  // buffer.go:657-658
+      if (h264_keyframe(b + q.hdrSize, q.payloadLen)) q.flags |= IP_KF;
+    } else if (s.codec == LKF_CODEC_AV1 && q.payloadLen > 0) {  // buffer.go:659-660
+      if (av1_keyframe(b + q.hdrSize, q.payloadLen)) q.flags |= IP_KF;
     }
   }
   out[i] = q;
@@ -498,12 +594,179 @@ __device__ void level_observe(StreamHot &h, const DevStream &s, u8 level, u32 du
 }
 
 // ---------------------------------------------------------------------------
+// buffer.DependencyDescriptorParser (dependencydescriptorparser.go:75-163) and
+// its FrameIntegrityChecker (frameintegrity.go), per stream
+// ---------------------------------------------------------------------------
+// WrapAround<uint16,uint64>{IsRestartAllowed: false}.Update -> ExtendedVal
+__device__ inline u64 wa16_ext(u64 &cycles, u64 &extHighest, u16 &start, u16 &highest, u32 &flags, u32 initBit,
+                               u16 val) {
+  const u64 full = 1ull << 16;
+  if (!(flags & initBit)) {
+    start = val;
+    highest = val;
+    extHighest = cycles + u64(val);
+    flags |= initBit;
+    return u64(val);
+  }
+  const u16 gap = u16(val - highest);
+  if (gap > u16(full >> 1)) {
+    u64 cyc = cycles;
+    const u64 total = extHighest - u64(start) + 1;
+    const bool wrapBack = u64(highest) < (full >> 1) && u64(val) >= (full >> 1);
+    if (total > (full >> 1)) {
+      if (wrapBack) cyc -= full;
+      return cyc + u64(val);
+    }
+    if (!(u16(val - start) > u16(full >> 1)) && wrapBack) cyc -= full;
+    return cyc + u64(val);
+  }
+  if (val < highest) cycles += full;
+  highest = val;
+  extHighest = cycles + u64(val);
+  return extHighest;
+}
+
+// PacketHistory frameintegrity.go:46-146
+__device__ inline void ph_set(DDIngState &d, u64 seq, bool r) {
+  const u64 i = (seq - d.phBase) % u64(kFICPktWords * 64);
+  if (r)
+    d.phBits[i >> 6] |= 1ull << (i & 63);
+  else
+    d.phBits[i >> 6] &= ~(1ull << (i & 63));
+}
+__device__ inline void ph_add(DDIngState &d, u64 seq) {
+  if (!(d.flags & DI_PH_INIT)) {
+    d.flags |= DI_PH_INIT;
+    d.phBase = seq > 100 ? seq - 100 : 0;
+    d.phLast = seq;
+    ph_set(d, seq, true);
+    return;
+  }
+  if (seq <= d.phBase) return;
+  if (seq <= d.phLast) {
+    if (d.phLast - seq < u64(kFICPktWords * 64)) ph_set(d, seq, true);
+    return;
+  }
+  if (seq - d.phLast - 1 >= u64(kFICPktWords * 64)) {  // the clearing loop wraps the whole ring
+    for (int w = 0; w < kFICPktWords; w++) d.phBits[w] = 0;
+  } else {
+    for (u64 i = d.phLast + 1; i < seq; i++) ph_set(d, i, false);
+  }
+  ph_set(d, seq, true);
+  d.phLast = seq;
+}
+__device__ inline bool ph_consecutive(const DDIngState &d, u64 start, u64 end) {
+  const u64 pc = u64(kFICPktWords * 64);
+  if (start > end || end - start >= pc) return false;
+  const u64 si = (start - d.phBase) % pc, ei = (end - d.phBase) % pc;
+  const int sIdx = int(si >> 6), sOff = int(si & 63), eIdx = int(ei >> 6), eOff = int(ei & 63);
+  if (sIdx == eIdx && end - start <= 64) {
+    const int w = eOff - sOff + 1;
+    const u64 tb = (w >= 64 ? ~0ull : ((1ull << w) - 1)) << sOff;
+    return (d.phBits[sIdx] & tb) == tb;
+  }
+  const u64 lhs = (d.phBits[sIdx] >> sOff) + 1;
+  const u64 rhs = (64 - sOff) >= 64 ? 0 : (1ull << (64 - sOff));
+  if (lhs != rhs) return false;
+  for (int i = sIdx + 1; i != eIdx; i++) {
+    if (i == kFICPktWords) {
+      i = 0;
+      if (i == eIdx) break;
+    }
+    if (d.phBits[i] + 1 != 0) return false;
+  }
+  const u64 tb = eOff + 1 >= 64 ? ~0ull : ((1ull << (eOff + 1)) - 1);
+  return (d.phBits[eIdx] & tb) == tb;
+}
+// FrameIntegrityChecker.AddPacket / FrameIntegrity
+__device__ inline void fe_add(DDIngState &d, int slot, u64 seq, bool first, bool last) {
+  u8 f = d.feFlags[slot];
+  if (f & 4) return;
+  if (!(f & 1) && first) {
+    f |= 1;
+    d.feStart[slot] = seq;
+  }
+  if (!(f & 2) && last) {
+    f |= 2;
+    d.feEnd[slot] = seq;
+  }
+  if ((f & 3) == 3 && ph_consecutive(d, d.feStart[slot], d.feEnd[slot])) f |= 4;
+  d.feFlags[slot] = f;
+}
+__device__ inline void fc_add(DDIngState &d, u64 seq, u64 fn, bool first, bool last) {
+  ph_add(d, seq);
+  if (!(d.flags & DI_FC_INIT)) {
+    d.flags |= DI_FC_INIT;
+    d.fcBase = d.fcLast = fn;
+  }
+  if (fn < d.fcBase) return;
+  if (fn <= d.fcLast) {
+    if (d.fcLast - fn >= u64(kFICFrames)) return;
+    fe_add(d, int((fn - d.fcBase) % u64(kFICFrames)), seq, first, last);
+    return;
+  }
+  if (fn - d.fcLast >= u64(kFICFrames)) {  // the reset loop covers every slot
+    for (int i = 0; i < kFICFrames; i++) d.feFlags[i] = 0;
+  } else {
+    for (u64 i = d.fcLast + 1; i <= fn; i++) d.feFlags[int((i - d.fcBase) % u64(kFICFrames))] = 0;
+  }
+  fe_add(d, int((fn - d.fcBase) % u64(kFICFrames)), seq, first, last);
+  d.fcLast = fn;
+}
+__device__ inline bool fc_integrity(const DDIngState &d, u64 fn) {
+  if (fn < d.fcBase || fn > d.fcLast || d.fcLast - fn >= u64(kFICFrames)) return false;
+  return (d.feFlags[int((fn - d.fcBase) % u64(kFICFrames))] & 4) != 0;
+}
+
+// Parse: false -> the packet produces no ExtPacket (a parse error); *limit
+// when an engine limit (not the reference) refused it
+__device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u8 *buf, int len, u16 sn, IngDD &out, bool &limit) {
+  limit = false;
+  const u32 cur = (d.flags & DI_CUR) ? 1u : 0u;
+  DDPkt o = {};
+  bool att = false;
+  const int e = dd::dd_parse(buf, len, (d.flags & DI_HAS_STRUCT) ? structs + cur : nullptr, structs + (cur ^ 1u), o,
+                             att);
+  if (e) {
+    limit = e == dd::LIMIT;
+    return false;
+  }
+  const u64 extSeq = wa16_ext(d.seqCycles, d.seqExtHighest, d.seqStart, d.seqHighest, d.flags, DI_SEQ_INIT, sn);
+  const u64 extFN = wa16_ext(d.fnCycles, d.fnExtHighest, d.fnStart, d.fnHighest, d.flags, DI_FN_INIT, o.frameNumber);
+  if (extFN < d.structureExtFN) return false;  // ErrFrameEarlierThanKeyFrame
+  fc_add(d, extSeq, extFN, o.flags & DP_FIRST, o.flags & DP_LAST);
+  out.extFN = extFN;
+  out.flags = fc_integrity(d, extFN) ? LKF_DD_INTEGRITY : 0;
+  if (att) {
+    if (!(o.flags & DP_FIRST)) return false;  // ErrDDStructureAttachedToNonFirstPacket
+    d.flags ^= DI_CUR;
+    d.flags |= DI_HAS_STRUCT;
+    d.structureExtFN = extFN;
+    out.flags |= LKF_DD_STRUCTURE_UPDATED | LKF_DD_ACTIVE_UPDATED;
+  }
+  if ((o.flags & DP_ACTIVE) && extSeq > d.activeExtSeq) {
+    d.activeExtSeq = extSeq;
+    if (o.activeMask != d.activeMask) {
+      d.activeMask = o.activeMask;
+      out.flags |= LKF_DD_ACTIVE_UPDATED;
+    }
+  }
+  out.extKFN = d.structureExtFN;
+  out.present = 1;
+  out.sid = o.sid;
+  out.tid = o.tid;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
 // k_ing_stream: one lane per stream, serial over the stream's datagrams.
 // ---------------------------------------------------------------------------
 __global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
                              const DevStream *__restrict__ streams, u32 nstreams, StreamHot *__restrict__ hot,
                              u64 *__restrict__ hist, RangeEntry *__restrict__ rings, const u32 *__restrict__ tBegin,
-                             const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows, u32 *__restrict__ fwd) {
+                             const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows, u32 *__restrict__ fwd,
+                             const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
+                             IngDD *__restrict__ ingDD, u32 *err) {
   const u32 sid = blockIdx.x * blockDim.x + threadIdx.x;
   if (sid >= nstreams) return;
   const DevStream s = streams[sid];
@@ -519,6 +782,7 @@ __global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngPars
     lkf_flow f = {};
     f.pkt = 0xffffffffu;
     u32 forward = 0;
+    IngDD dv = {};
     do {
       if (!(p.flags & IP_OK)) {
         f.flags = LKF_FLOW_BAD;
@@ -613,7 +877,20 @@ __global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngPars
       }
       f.ext_sn = rsn.extVal - adj;
       if (dup) break;  // the RTX bucket already holds it (ErrRTXPacket)
-      if (p.flags & IP_VP8_BAD) {  // getExtPacket: VP8 unmarshal failed
+      // getExtPacket (buffer.go:599-671): the dependency descriptor first
+      if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
+        bool limit = false;
+        if (!dd_ingest(ddStates[s.ddIdx], ddStructs + size_t(s.ddIdx) * 2, raw + raws[i].off + p.ddOff, p.ddLen,
+                       u16(f.ext_sn), dv, limit)) {
+          if (limit) atomicOr(err, 4u);
+          f.flags |= LKF_FLOW_BAD;
+          break;
+        }
+        dv.ddOff = p.ddOff;
+        dv.ddLen = p.ddLen;
+      }
+      // VP8 unmarshal failed, or VP9 without a descriptor that failed
+      if ((p.flags & IP_VP8_BAD) && !(s.codec == LKF_CODEC_VP9 && dv.present)) {
         f.flags |= LKF_FLOW_BAD;
         break;
       }
@@ -622,6 +899,7 @@ __global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngPars
     } while (false);
     flows[i] = f;
     fwd[i] = forward;
+    if (ingDD) ingDD[i] = dv;
   }
   hot[sid] = h;
 }
@@ -632,7 +910,7 @@ __global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngPars
 __global__ void k_ing_out(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
                           const DevStream *__restrict__ streams, const u32 *__restrict__ fwd,
                           const u64 *__restrict__ pos, u32 n, lkf_flow *__restrict__ flows,
-                          lkf_pkt *__restrict__ out) {
+                          lkf_pkt *__restrict__ out, const IngDD *__restrict__ ingDD, lkf_pkt_dd *__restrict__ outDD) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !fwd[i]) return;
   const u32 k = u32(pos[i]);
@@ -669,14 +947,40 @@ __global__ void k_ing_out(const lkf_raw_pkt *__restrict__ raws, const IngParsed 
     e.vp8_tid = p.tid;
     e.vp8_keyidx = p.keyidx;
   }
-  if (p.flags & IP_VP9) {  // VideoLayer{SID, TID}, Payload = VP9Packet (buffer.go:645-655)
-    e.flags |= LKF_PKT_VP9 | ((p.flags & IP_KF) ? LKF_PKT_KEYFRAME : 0);
-    e.spatial = int8_t(p.sid);
-    e.temporal = int8_t(p.tid);
-    e.vp9_bits = p.vp9bits;
+  const IngDD dv = ingDD ? ingDD[i] : IngDD{};
+  if (dv.present) {  // ExtPacket.DependencyDescriptor + VideoLayer (buffer.go:613-621)
+    e.flags |= LKF_PKT_DD;
+    e.spatial = int8_t(dv.sid);
+    e.temporal = int8_t(dv.tid);
+    if (p.flags & IP_VP8) {  // VP8 with DD: TID from the descriptor, no spatial (buffer.go:630-635)
+      e.temporal = int8_t(dv.tid);
+      e.vp8_tid = dv.tid;
+      e.spatial = -1;
+    }
   }
+  if (p.flags & IP_VP9) {
+    if (!dv.present) {  // VideoLayer{SID, TID}, Payload = VP9Packet (buffer.go:645-655)
+      e.flags |= LKF_PKT_VP9;
+      e.spatial = int8_t(p.sid);
+      e.temporal = int8_t(p.tid);
+      e.vp9_bits = p.vp9bits;
+    }
+  }
+  if ((s.codec == LKF_CODEC_VP9 || s.codec == LKF_CODEC_H264 || s.codec == LKF_CODEC_AV1) && (p.flags & IP_KF))
+    e.flags |= LKF_PKT_KEYFRAME;  // IsVP9KeyFrame / IsH264KeyFrame / IsAV1KeyFrame (buffer.go:656-660)
   if (e.spatial >= 0) e.layer = e.spatial;  // svc packet: forwardRTP dispatches pkt.Spatial (receiver.go:667-672)
   out[k] = e;
+  if (outDD) {
+    lkf_pkt_dd d = {};
+    if (dv.present) {
+      d.ext_frame_num = dv.extFN;
+      d.ext_key_frame_num = dv.extKFN;
+      d.dd_off = dv.ddOff;
+      d.dd_len = dv.ddLen;
+      d.flags = dv.flags;
+    }
+    outDD[k] = d;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -750,12 +1054,13 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
   hipLaunchKernelGGL(k_ing_ranges, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.parsed, a.n, a.ntracks, a.tBegin, a.tEnd,
                      a.tRuns, a.err);
   hipLaunchKernelGGL(k_ing_stream, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a.raws, a.parsed, a.streams,
-                     a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd);
+                     a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates,
+                     a.ddStructs, a.ingDD, a.err);
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
   if (r != hipSuccess) return r;
   hipLaunchKernelGGL(k_ing_out, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.parsed, a.streams, a.fwd, a.pos,
-                     a.n, a.flows, a.out);
+                     a.n, a.flows, a.out, a.ingDD, a.outDD);
   return hipGetLastError();
 }
 

@@ -85,6 +85,11 @@ struct IngestLaunch {
   uint32_t *fwd;
   uint64_t *pos, *partA, *partB, *total;
   lkf_pkt *out;
+  // dependency descriptor (nullptr: no stream negotiated the DD extension)
+  DDIngState *ddStates;
+  DDStruct *ddStructs;  // two per DD stream
+  IngDD *ingDD;         // per datagram
+  lkf_pkt_dd *outDD;    // the batch's side array
 };
 
 struct SpeakersLaunch {

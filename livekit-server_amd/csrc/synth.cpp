@@ -255,6 +255,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   const bool withEvents = cfg->with_events != 0;
   const bool cb = cfg->has_callbacks != 0;
   const bool svcDD = cfg->svc_dd != 0;
+  const bool h264 = cfg->h264 > 0;
 
   u32 rooms = cfg->rooms, parts = cfg->participants;
   double loss = cfg->loss, reorder = cfg->reorder;
@@ -319,6 +320,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         g.p.kind = LKF_KIND_VIDEO;
         g.p.codec = C == 5 ? LKF_CODEC_VP9 : LKF_CODEC_VP8;
         g.svc = C == 5;
+        if (h264 && C <= 3 && (p % 3) == (C == 1 ? 0u : 1u)) g.p.codec = LKF_CODEC_H264;
         // configs[4]: AV1 (DD only) and VP9 with DD beside VP9-descriptor publishers
         if (C == 5 && svcDD && (p % 4) != 3) {
           g.dd = true;
@@ -839,6 +841,60 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
           d.vp9_bits = pl.vp9;
           d.spatial = pl.layer;  // VideoLayer{SID, TID} (buffer.go:645-655)
           d.temporal = int8_t(pl.tid);
+        } else if (g.p.kind == LKF_KIND_VIDEO && g.p.codec == LKF_CODEC_H264) {
+          raw[16] = 0x51;  // id 5 (transport-cc), len 2
+          raw[17] = u8(pl.twcc >> 8);
+          raw[18] = u8(pl.twcc);
+          raw[19] = 0;
+          // RFC 6184 packetization; a key frame's first packet carries the SPS
+          // (IsH264KeyFrame), in one of the four aggregation forms by picture id
+          const u32 n = pl.payload_len;
+          bool sps = false;
+          if (pl.keyframe && pl.s_bit) {
+            const u32 form = n >= 16 ? pl.pid % 4 : 0;
+            if (form == 0) {
+              pay[0] = 0x67;  // single NALU, type 7
+            } else if (form == 1) {
+              pay[0] = 0x78;  // STAP-A: [len 10][SPS ...][len ...][PPS ...]
+              pay[1] = 0;
+              pay[2] = 10;
+              pay[3] = 0x67;
+              pay[13] = 0;
+              pay[14] = u8(n - 15);
+              pay[15] = 0x68;
+            } else if (form == 2) {
+              pay[0] = 0x7C;  // FU-A start fragment of an SPS
+              pay[1] = 0x87;
+            } else {
+              pay[0] = 0x79;  // STAP-B: DON, then [len 4][AUD][len ..][SPS]
+              pay[1] = 0;
+              pay[2] = 1;
+              pay[3] = 0;
+              pay[4] = 4;
+              pay[5] = 0x09;
+              pay[9] = 0;
+              pay[10] = u8(n - 11);
+              pay[11] = 0x67;
+            }
+            sps = true;
+          } else if (pl.s_bit) {
+            if (pl.pid % 7 == 3 && n >= 4) {
+              pay[0] = 0x78;  // truncated STAP-A (length beyond the payload)
+              pay[1] = 0xFF;
+              pay[2] = 0xFF;
+            } else if (pl.pid % 2) {
+              pay[0] = 0x41;  // single NALU, non-IDR slice
+            } else {
+              pay[0] = 0x7C;  // FU-A start, non-IDR slice
+              pay[1] = 0x81;
+            }
+          } else {
+            pay[0] = 0x7C;  // FU-A continuation
+            pay[1] = pl.keyframe ? 0x05 : 0x01;
+          }
+          d.flags = sps ? LKF_PKT_KEYFRAME : 0;
+          d.spatial = -1;
+          d.temporal = 0;  // buffer.go:616: no temporal layers without a descriptor
         } else if (g.p.kind == LKF_KIND_VIDEO) {
           raw[16] = 0x51;  // id 5 (transport-cc), len 2
           raw[17] = u8(pl.twcc >> 8);

@@ -28,12 +28,16 @@ def _ingested(o, abi, h):
     dict(config=1, duration_s=2.0),
     dict(config=2, duration_s=2.0, rooms=2, loss=0.0, reorder=0.0),
     dict(config=3, duration_s=2.0, rooms=1),
-    dict(config=5, duration_s=2.0, rooms=3, loss=0.0, reorder=0.0),  # VP9 descriptor parse, SVC layer dispatch
+    dict(config=5, duration_s=2.0, rooms=3, loss=0.0, reorder=0.0, svc_dd=0),  # VP9 descriptor, SVC dispatch
+    dict(config=5, duration_s=2.0, rooms=3, loss=0.0, reorder=0.0),  # + AV1 / VP9 dependency descriptors
+    dict(config=1, duration_s=2.0, h264=1),  # H.264 key frames (IsH264KeyFrame forms)
+    dict(config=2, duration_s=2.0, rooms=2, loss=0.0, reorder=0.0, h264=1),
 ])
 def test_oracle_ingest_reproduces_extpackets(kw, pkg, workload, abi):
     o = load_oracle()
     tr = workload.Trace(**kw)
     h = o.create(500)
+    keys = 0
     try:
         workload.load_topology(o.api, h, tr)
         workload.load_streams(o.api, h, tr)
@@ -46,10 +50,20 @@ def test_oracle_ingest_reproduces_extpackets(kw, pkg, workload, abi):
             got = C.string_at(pk, 64 * m) if m else b""
             want = C.string_at(spk, 64 * sn) if sn else b""
             assert got == want, "batch %d ExtPackets differ" % b
+            if tr.has_dd():  # the DependencyDescriptorParser's view, per ExtPacket
+                dsz = C.sizeof(abi.lkf_pkt_dd)
+                buf = C.create_string_buffer(max(1, m) * dsz)
+                k = C.c_uint32()
+                assert o.api["ingested_dd"](h, buf, m, C.byref(k)) == 0 and k.value == m
+                assert buf.raw[: m * dsz] == C.string_at(tr.batch_dd(b)[0], m * dsz), "batch %d DD differs" % b
+            if kw.get("h264"):
+                keys += int(np.sum(np.frombuffer(got, np.uint8).reshape(-1, 64)[:, abi.lkf_pkt.flags.offset] & 0x1 != 0)) if m else 0
             fl = pkg.flows_array(o.api, h)
             assert len(fl) == n
             assert np.all(fl["flags"] & 0x20)  # every datagram forwarded
             assert np.array_equal(fl["pkt"], np.arange(n, dtype=np.uint32))
+        if kw.get("h264"):
+            assert keys > 0
     finally:
         o.destroy(h)
         tr.close()

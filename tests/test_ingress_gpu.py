@@ -27,6 +27,16 @@ def _ingested(api, h, abi):
     return C.string_at(arr, 64 * n.value) if n.value else b""
 
 
+def _ingested_dd(api, h, abi):
+    n = C.c_uint32()
+    rc = api["ingested_dd"](h, None, 0, C.byref(n))
+    assert rc in (0, -28)
+    sz = C.sizeof(abi.lkf_pkt_dd)
+    buf = C.create_string_buffer(max(1, n.value) * sz)
+    assert api["ingested_dd"](h, buf, n.value, C.byref(n)) == 0
+    return buf.raw[: sz * n.value]
+
+
 def run_ingress_parity(pkg, workload, abi, trace, speakers=True):
     o = load_oracle()
     eng = pkg.Engine.for_trace(trace)
@@ -52,7 +62,15 @@ def run_ingress_parity(pkg, workload, abi, trace, speakers=True):
                         b, f, bad, gf[bad], of[bad]))
             gp = _ingested(eng.api, eng.h, abi)
             op = _ingested(o.api, oh, abi)
-            assert gp == op, "batch %d ExtPacket batches differ" % b
+            if gp != op:
+                g = np.frombuffer(gp, np.uint8).reshape(-1, 64)
+                o_ = np.frombuffer(op, np.uint8).reshape(-1, 64)
+                bad = np.nonzero((g != o_).any(1))[0] if len(g) == len(o_) else []
+                raise AssertionError("batch %d ExtPacket batches differ (%d vs %d) first rows %s" % (
+                    b, len(g), len(o_), list(bad[:5])))
+            gd = _ingested_dd(eng.api, eng.h, abi)
+            od = _ingested_dd(o.api, oh, abi)
+            assert gd == od, "batch %d ExtPacket dependency descriptors differ" % b
             # forward the ingested batch on both sides
             eng.run()
             eng.sync()
@@ -95,6 +113,27 @@ def test_ingress_config2_loss_reorder(pkg, workload, abi):
 def test_ingress_config5_vp9(pkg, workload, abi):
     """VP9 SVC datagrams: VP9 descriptor parse, key frames, SID dispatch, then forwarding."""
     tr = workload.Trace(5, duration_s=3.0, batch_s=0.5, rooms=4, loss=0.05, reorder=0.03, seed=31, svc_dd=0)
+    assert run_ingress_parity(pkg, workload, abi, tr) > 0
+
+
+def test_ingress_config5_dd(pkg, workload, abi):
+    """AV1 and VP9 publishers with dependency descriptors: the per-stream
+    DependencyDescriptorParser (structures, frame-number wrap, frame integrity,
+    active decode targets) on the GPU, then the DD selector on its output."""
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.5, rooms=4, seed=41)
+    assert tr.has_dd()
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
+
+
+def test_ingress_config5_dd_loss_reorder(pkg, workload, abi):
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.25, rooms=3, loss=0.06, reorder=0.04, seed=43)
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
+
+
+def test_ingress_h264_keyframes(pkg, workload, abi):
+    """H.264 simulcast publishers: IsH264KeyFrame over single NALU / STAP-A /
+    STAP-B / FU-A SPS packets (and truncated aggregates) on the GPU."""
+    tr = workload.Trace(2, duration_s=3.0, batch_s=0.5, rooms=3, loss=0.04, reorder=0.03, seed=47, h264=1)
     assert run_ingress_parity(pkg, workload, abi, tr) > 0
 
 
