@@ -140,8 +140,12 @@ def main():
     wl = importlib.import_module("livekit-server_amd.workload")
 
     nb = args.warmup + args.steps
-    trace = wl.Trace(2, duration_s=nb * args.batch_s, batch_s=args.batch_s, rooms=args.rooms,
-                     room_base=rank * args.rooms)
+    # rooms -> ranks: LPT bin packing by expected tuples per batch (SURVEY.md
+    # §8(e)); configs[1]'s rooms are all the same shape, so every rank gets
+    # args.rooms of them
+    rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+    plan = rooms_mod.plan_room_shards([1.0] * (world * args.rooms), world)
+    trace = wl.Trace(2, duration_s=nb * args.batch_s, batch_s=args.batch_s, room_ids=plan[rank])
     eng = pkg.Engine.for_trace(trace, device=local, lib_path=os.environ.get("LKF_LIB") or None)
     wl.load_topology(eng.api, eng.h, trace)
 
@@ -216,16 +220,22 @@ def main():
         # the one collective — per-room speaker summaries
         # (Room.GetActiveSpeakers) all-gathered over RCCL every 400 ms of media;
         # outside the timed forwarding region (not part of the throughput metric)
-        rooms_mod = importlib.import_module("livekit-server_amd.rooms")
         now = 1700000000 * 10**9 + int(nb * args.batch_s * 1e9)
         sp = pkg.speakers_array(eng.api, eng.h, now)
+        width = max(len(p) for p in plan)
+        bwe = rooms_mod.fold_summaries(pkg.downtrack_summaries(eng.api, eng.h), plan[rank], rows=width)
         torch.cuda.synchronize(dev)
         tc0 = time.perf_counter()
-        table = rooms_mod.all_gather_speakers(dist, dev, sp, rank * args.rooms, args.rooms)
+        table = rooms_mod.all_gather_speakers(dist, dev, sp, plan[rank])
+        btab = rooms_mod.all_gather_records(dist, dev, bwe)
         tc1 = time.perf_counter()
-        coll = {"op": "all_gather (RCCL) of per-room speaker records", "bytes_per_rank": int(table[0].nbytes),
+        coll = {"op": "all_gather (RCCL) of per-room speaker records + per-subscriber bandwidth records",
+                "bytes_per_rank": int(table[0].nbytes + btab[0].nbytes),
                 "ms": round((tc1 - tc0) * 1e3, 3), "rooms_gathered": int(table.shape[0] * table.shape[1]),
-                "rooms_with_speakers": int((table[:, :, 0, 0] >= 0).sum())}
+                "rooms_with_speakers": int((table[:, :, 0, 0] >= 0).sum()),
+                "subscribers_gathered": int((btab[:, :, :, 0] >= 0).sum()),
+                "subscribers_deficient": int((btab[:, :, :, 3] > 0).sum()),
+                "room_plan": "LPT bin packing by expected tuples (rooms.plan_room_shards)"}
 
     fwd = cum["forwarded"]
     steps_pkts = sum(meta[b][0] for b in range(args.warmup, nb))

@@ -383,6 +383,25 @@ int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, con
 int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *out);
 int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *in);
 
+/* ---- per-subscriber summaries ------------------------ */
+/* Per DownTrack since it was added: DownTrack.sendingPacket's counters
+ * (downtrack.go:1930-1941: bytesSent += header + payload of every forwarded
+ * packet; one RTPStatsSender packet each) and lastAllocation.IsDeficient as
+ * of the last lkf_run (LKF_CTL_SET_ALLOCATION a3) — the per-subscriber
+ * bandwidth records a node gathers per room.  One entry per DownTrack handle,
+ * removed ones included (without LKF_DTS_ACTIVE).  Drains the engine. */
+typedef struct lkf_dt_summary {
+  int32_t dt;           /* DownTrack handle */
+  uint32_t subscriber;  /* lkf_downtrack_params.subscriber */
+  uint32_t room;        /* the track's room */
+  uint32_t flags;       /* LKF_DTS_* */
+  uint64_t packets_sent;
+  uint64_t bytes_sent;
+} lkf_dt_summary;
+#define LKF_DTS_ACTIVE 0x1
+#define LKF_DTS_DEFICIENT 0x2
+int lkf_downtrack_summaries(lkf_engine *e, lkf_dt_summary *out, uint32_t cap, uint32_t *n_out);
+
 /* ---- sequencer (sequencer.getExtPacketMetas sequencer.go:263, for RTX) --- */
 typedef struct lkf_seq_meta {
   uint64_t ext_sn, ext_ts;

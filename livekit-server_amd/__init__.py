@@ -106,6 +106,19 @@ def speakers_array(api, h, now_ns):
         cap = n.value
 
 
+def downtrack_summaries(api, h):
+    """lkf_downtrack_summaries: one DT_SUMMARY_DTYPE row per DownTrack handle."""
+    n = C.c_uint32()
+    rc = api["downtrack_summaries"](h, None, 0, C.byref(n))
+    if rc not in (0, -28):
+        raise EngineError("downtrack_summaries rc=%d" % rc)
+    out = np.zeros(max(1, n.value), dtype=abi.DT_SUMMARY_DTYPE)
+    rc = api["downtrack_summaries"](h, out.ctypes.data, n.value, C.byref(n))
+    if rc != 0:
+        raise EngineError("downtrack_summaries rc=%d" % rc)
+    return out[:n.value]
+
+
 def stream_stats(api, h, sid):
     st = abi.lkf_stream_stats()
     rc = api["stream_stats_get"](h, sid, C.byref(st))

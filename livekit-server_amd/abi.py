@@ -88,6 +88,12 @@ FLOW_DTYPE = np.dtype([("ext_sn", "<u8"), ("ext_ts", "<u8"), ("loss_start", "<u8
                        ("pkt", "<u4"), ("flags", "u1"), ("reserved", "V3")])
 assert FLOW_DTYPE.itemsize == 40
 SPEAKER_DTYPE = np.dtype([("room", "<u4"), ("participant", "<u4"), ("level", "<f4"), ("active", "<u4")])
+# lkf_dt_summary (per-DownTrack sendingPacket totals + lastAllocation.IsDeficient)
+DT_SUMMARY_DTYPE = np.dtype([("dt", "<i4"), ("subscriber", "<u4"), ("room", "<u4"), ("flags", "<u4"),
+                             ("packets_sent", "<u8"), ("bytes_sent", "<u8")])
+assert DT_SUMMARY_DTYPE.itemsize == 32
+DTS_ACTIVE = 0x1
+DTS_DEFICIENT = 0x2
 
 
 class lkf_track_params(C.Structure):
@@ -256,6 +262,8 @@ class lkfs_cfg(C.Structure):
         ("has_callbacks", C.c_int32),
         ("svc_dd", C.c_int32),
         ("h264", C.c_int32),
+        ("pad0", C.c_int32),
+        ("room_ids", C.POINTER(C.c_uint32)),
     ]
 
 
@@ -320,6 +328,8 @@ def bind_engine_api(lib, prefix):
     api["submit_dd"] = _bind(lib, prefix + "submit_dd", C.c_int, [e, C.c_void_p, C.c_uint32])
     api["stream_stats_get"] = _bind(lib, prefix + "stream_stats_get", C.c_int, [e, C.c_int32, P(lkf_stream_stats)])
     api["speakers"] = _bind(lib, prefix + "speakers", C.c_int, [e, C.c_int64, C.c_void_p, C.c_uint32, P(C.c_uint32)])
+    api["downtrack_summaries"] = _bind(lib, prefix + "downtrack_summaries", C.c_int,
+                                       [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     return api
 
 

@@ -130,6 +130,7 @@ struct lkf_engine {
   // device: persistent state
   DevTrack *dTracks = nullptr;
   DTHot *dHot = nullptr;
+  DTCum *dDTCum = nullptr;  // per DownTrack sendingPacket totals (lkf_downtrack_summaries)
   DevDT *dDTs = nullptr;
   RangeEntry *dRm = nullptr;
   VP8Cold *dVc = nullptr;
@@ -379,6 +380,7 @@ static int flush_topology(lkf_engine *e) {
            "hot upload");
     HIPCHK(hipMemcpy(e->dDTs + first, e->pendDTs.data(), e->pendDTs.size() * sizeof(DevDT), hipMemcpyHostToDevice),
            "dt upload");
+    HIPCHK(hipMemset(e->dDTCum + first, 0, e->pendDTs.size() * sizeof(DTCum)), "dt totals reset");
     e->pendHot.clear();
     e->pendDTs.clear();
   }
@@ -434,6 +436,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   e->cur = e->own;
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
+  A(dalloc(&e->dDTCum, c.max_downtracks));
   A(dalloc(&e->dDTs, c.max_downtracks));
   A(dalloc(&e->dRm, size_t(c.max_downtracks) * kRangeCap));
   A(dalloc(&e->dVc, c.max_downtracks));
@@ -533,7 +536,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->prepS) (void)hipStreamSynchronize(e->prepS);
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
-  void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
+  void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr,
@@ -991,6 +994,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.evOff = x.dEvOff;
   d.fwdCnt = x.dFwdCnt;
   d.fwdBytes = x.dFwdBytes;
+  d.dtCum = e->dDTCum;
   d.stats = x.dStats;
   d.ddLanes = e->ddLanes;
   d.ddPkts = e->ddAlloc ? x.dDDPkt : nullptr;
@@ -1568,14 +1572,49 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
 }
 
 // Not part of include/lkfwd.h: counters of a diagnostic build (-DLKF_DIAG=1).
-int lkf_debug_counters(lkf_engine *e, uint64_t out[16], int reset) {
+// out[0..15]: per-wave cycle/event counters; out[16..31]: serial-step triggers.
+int lkf_debug_counters(lkf_engine *e, uint64_t out[32], int reset) {
   if (!e || !out) return LKF_EINVAL;
   int rc = drain_streams(e);
   if (rc) return rc;
-  unsigned long long v[16];
+  unsigned long long v[32];
   hipError_t r = read_diag(v, reset);
-  for (int i = 0; i < 16; i++) out[i] = v[i];
+  for (int i = 0; i < 32; i++) out[i] = v[i];
   return r == hipSuccess ? LKF_OK : LKF_ENODEV;
+}
+
+// Not part of include/lkfwd.h: per-wave stamps of the last k_decide_dt
+// (-DLKF_WTIME=1 builds): 8 words per wave slot.
+int lkf_debug_wtime(lkf_engine *e, uint32_t *out, uint32_t nwaves) {
+  if (!e || !out) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  return read_wtime(out, nwaves) == hipSuccess ? LKF_OK : LKF_ENODEV;
+}
+
+int lkf_downtrack_summaries(lkf_engine *e, lkf_dt_summary *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !n_out) return LKF_EINVAL;
+  const uint32_t nd = uint32_t(e->dtp.size());
+  *n_out = nd;
+  if (cap < nd) return LKF_ENOSPC;
+  if (!nd) return LKF_OK;
+  if (!out) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  std::vector<DTCum> c(nd);
+  HIPCHK(hipMemcpy(c.data(), e->dDTCum, nd * sizeof(DTCum), hipMemcpyDeviceToHost), "dt totals copy");
+  for (uint32_t d = 0; d < nd; d++) {
+    lkf_dt_summary &s = out[d];
+    s.dt = int32_t(d);
+    s.subscriber = e->dtp[d].subscriber;
+    s.room = e->tracks[e->dtp[d].track].room;
+    s.flags = (e->active[d] ? LKF_DTS_ACTIVE : 0u) | ((c[d].flags & F_DEFICIENT) ? LKF_DTS_DEFICIENT : 0u);
+    s.packets_sent = c[d].packets;
+    s.bytes_sent = c[d].bytes;
+  }
+  return LKF_OK;
 }
 
 int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset) {

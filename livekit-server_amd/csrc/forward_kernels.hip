@@ -35,8 +35,16 @@ namespace lkf {
 #ifndef LKF_DIAG
 #define LKF_DIAG 0  // diagnostic build: per-wave counters into g_diag (lkf_debug_counters)
 #endif
+#ifndef LKF_WTIME
+#define LKF_WTIME 0  // diagnostic build: per-wave start/end realtime stamps (lkf_debug_wtime)
+#endif
+#if LKF_WTIME
+constexpr uint32_t kWTimeWaves = 1u << 16;
+__device__ uint32_t g_wtime[kWTimeWaves * 16];  // start, end (100 MHz ticks), packets, serial steps | chunks << 16,
+                                               // cycles: prologue, serial steps, drains after them, total
+#endif
 #if LKF_DIAG
-__device__ unsigned long long g_diag[16];
+__device__ unsigned long long g_diag[32];  // [16..31]: serial-step triggers
 struct DiagTimer {  // adds elapsed cycles of a scope to g_diag[slot] (lane 0)
   int slot;
   uint64_t t0;
@@ -1370,6 +1378,7 @@ struct DecideArgs {
   const u32 *evOff;  // per lane [evOff[l], evOff[l+1])
   u32 *fwdCnt;
   u64 *fwdBytes;
+  DTCum *dtCum;  // per DownTrack totals (sendingPacket counters)
   u64 *stats;  // lkf_stats as u64[15]
   const u32 *layerList, *layerBefore, *layerCnt;  // k_layer_index
   u32 pktStride;
@@ -1638,6 +1647,9 @@ __device__ __forceinline__ void pin_loaded(const uint4 &a, const uint4 &b, const
                "v"(c.y), "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
 }
 
+#ifndef LKF_OOO_RUN
+#define LKF_OOO_RUN 1  // 0: out-of-order packets take the serial step (A/B)
+#endif
 #ifndef LKF_LAYER_SKIP
 #define LKF_LAYER_SKIP 1  // 0: every chunk is the next 64 packets of the track (A/B)
 #endif
@@ -1709,6 +1721,16 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   u32 ev = A.evOff[w];
   const u32 evEnd = A.evOff[w + 1];
   if (d == 0xffffffffu) return;  // padding slot of the per-XCD schedule
+#if LKF_WTIME
+  const u64 wt0 = __builtin_amdgcn_s_memrealtime();
+  const u64 wc0 = __builtin_amdgcn_s_memtime();
+  u32 wtSerial = 0, wtChunks = 0;
+  u64 wcStep = 0, wcDrain = 0, wcPro = 0;
+  u32 wtWhy[4] = {}, wtRuns = 0;
+#endif
+#if LKF_DIAG
+  const u64 tP1 = clock64() + u64(__builtin_amdgcn_readfirstlane(d) & 0);  // after round 1
+#endif
   const DevDT dt = A.dts[d];
   const u32 pb = A.tBegin[track];
   u32 pe = A.tEnd[track];
@@ -1722,6 +1744,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   Lane L{sHot};
   reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
   __syncthreads();
+#if LKF_DIAG
+  const u64 tP2 = clock64() + u64(sHot.flags & 0);  // hot state in LDS
+#endif
 #else
   Lane L;
   L.h = A.hot[d];
@@ -1749,6 +1774,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     const u32 idx = (L.h.rmHead + i) % kRangeCap;
     sRm[idx] = rmG[idx];
   }
+#if LKF_DIAG
+  const u64 tP3 = clock64() + u64(u32(sRm[0].start) & 0 & sMissKey[lane & 63] & sDrop[0]);  // maps + ranges issued
+#endif
   if (slot0 + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
     if (lane == 0) atomicOr(A.err, 8u);
     pe = pb;
@@ -1786,12 +1814,19 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
 #if LKF_DIAG
   u64 dg[16] = {};
+  u32 dg2[16] = {};
   u64 tk0 = clock64();
+  dg2[12] = u32(tP1 - tEntry);
+  dg2[13] = u32(tP2 - tP1);
+  dg2[14] = u32(tP3 - tP2);
   dg[7] = tk0 - tEntry;
   dg[0] = 1;
   dg[15] = pe - pb;
 #endif
 
+#if LKF_WTIME
+  wcPro = __builtin_amdgcn_s_memtime() - wc0;
+#endif
   u32 kpos = pb;  // first packet of the track not yet decided
   while (kpos < pe) {
     if (nextAt <= kpos) {
@@ -1822,6 +1857,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     }
     const bool valid = lane < n;
     DIAG(1, 1);
+#if LKF_WTIME
+    wtChunks++;
+#endif
 #if LKF_DIAG
     u64 tc0 = clock64();
 #endif
@@ -1860,6 +1898,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       const bool kf = p.flags & LKF_PKT_KEYFRAME;
       const bool pktMarker = p.hdr1 & 0x80;
       int cls;  // >= 0: drop with no state change; -1: current-layer candidate; -2: serial
+#if LKF_DIAG || LKF_WTIME
+      int whyKf = 0;
+#endif
       if (fl & (F_MUTED | F_PUBMUTED)) {
         cls = LKF_DROP_MUTED;
       } else if (!video) {
@@ -1883,12 +1924,22 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           cls = -1;
         else
           cls = -2;
+#if LKF_DIAG || LKF_WTIME
+        if (willSwitch) whyKf = 1;
+#endif
       }
 #if LKF_FORCE_SERIAL
       cls = -2;
 #endif
       const bool cand = inWin && cls == -1;
-      const u64 candM = __ballot(cand);
+      // An out-of-order packet — older than the highest SN at the run start
+      // (UpdateAndGetSnTs diff < 0, rtpmunger.go:219-236) — is decided in the
+      // run: its translation reads the RangeMap and the VP8 missing-picture map
+      // and changes no state but the sequencer slot it fills.  The in-order
+      // recurrences (previous candidate, previous forward) skip it.
+      const bool oooL = LKF_OOO_RUN && cand && i64(p.esn - L.h.extHighestIncomingSN) < 0 && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+      const bool candIn = cand && !oooL;
+      const u64 candM = __ballot(candIn);
       const int pc = prev_in(candM, lt);
       const int pcs = pc >= 0 ? pc : int(lane);  // cross-lane reads run on every lane
       const u64 pcEsn = sh64(p.esn, pcs);
@@ -1898,11 +1949,12 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       // pictures vp8.go:218-255, skipped sequencer slots sequencer.go:179-189)
       // are applied before the run, from the state at the run start.
       const u64 dEsn = p.esn - prevEsn;
-      const bool gapLane = cand && pc < 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
+      const bool gapLane = candIn && pc < 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
                            p.ssrc == L.h.lastSSRC;
-      bool ok = cand && (dEsn == 1 || gapLane) && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+      bool ok = candIn && (dEsn == 1 || gapLane) && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+      bool okO = LKF_OOO_RUN && oooL;  // out-of-order lane decided in the run (refined below)
       // a gap behind other candidates ends this run and starts the next one
-      const bool gapLater = cand && pc >= 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
+      const bool gapLater = candIn && pc >= 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
                             p.ssrc == L.h.lastSSRC;
       // (diag: run-body split below)
       // VP8 picture id (VP8PictureIdWrapHandler.Unwrap vp8.go:400-483 without a wrap)
@@ -1914,6 +1966,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       const i32 prevExt = pc >= 0 ? pcExt : L.h.wrMaxPictureId;
       const bool prevM = pc >= 0 ? pcM : ((fl & F_WR_MAX_MBIT) != 0);
       bool dropT = false;
+#if LKF_DIAG || LKF_WTIME
+      int whyVid = 0;
+#endif
       u64 tswM = 0;  // candidate lanes at a temporal switch point (the first ends the run)
       bool gapExempt = false;
       i32 gapExt = 0;
@@ -1928,7 +1983,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
                          (cT < gT ? (i32(p.tid) > cT && i32(p.tid) <= gT && (p.vbits & LKF_VP8_S) &&
                                      (p.vbits & LKF_VP8_Y))
                                   : pktMarker);
-        const bool overT = cand && T && p.tid > u8(cT);
+        const bool overT = candIn && T && p.tid > u8(cT);
+        // VP8PictureIdWrapHandler.Unwrap and SelectTemporal run on an
+        // out-of-order packet too: a wrap or a temporal switch there is serial
+        okO = okO && !wrapBack && !wraps && !tsw;
         // a gap lane forwards whatever its layer and exempts its picture (vp8.go:249-255)
         const u64 gapM = __ballot(gapLane);
         const u32 gl = gapM ? u32(__ffsll((long long)gapM) - 1) : 0u;
@@ -1943,18 +2001,21 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         // must forward — a filtered one would roll the selector back (serial).
         if (tsw && cT < gT) dropT = false;
         const bool tswOk = tsw && !gapLane && !dropT;
+#if LKF_DIAG || LKF_WTIME
+        whyVid = (wrapBack || wraps) ? 1 : ((tsw && !tswOk) ? 2 : ((dropT && L.h.snOffset != L.h.rmOpenValue) ? 3 : 0));
+#endif
         ok = ok && !wrapBack && !wraps && (!tsw || tswOk) && (!dropT || L.h.snOffset == L.h.rmOpenValue);
         tswM = __ballot(inWin && ok && tsw);
       }
       // (diag: run-body split below)
       const u64 tdM = __ballot(ok && dropT);
       const u64 snOff = L.h.snOffset + u64(__popcll(tdM & lt));
-      const u64 osn = p.esn - snOff;
+      u64 osn = p.esn - snOff;  // (an out-of-order lane's is set from the RangeMap below)
       const u64 ots = p.ets - L.h.tsOffset;
       const bool picDrop = ok && dropT && I && ext != prevExt;
       const i32 picOff = L.h.pictureIdOffset + i32(__popcll(__ballot(picDrop) & lt));
       // forwarded: munged descriptor (vp8.go:283-301) + output shape
-      bool fwd = ok && !dropT;
+      const bool fwdIn = ok && !dropT;
       const i32 mext = ext - picOff;
       const u16 mpid = u16(mext & 0x7fff);
       const u8 mtl0 = u8(p.tl0 - L.h.tl0Off);
@@ -1968,23 +2029,90 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
                             p.vbits & LKF_VP8_K, mkey, hs, cb);
       }
       // (diag: run-body split below)
-      const u64 fwC = __ballot(fwd);
+      // the munger's / sequencer's highest before each lane: the previous in-order push
+      const u64 fwC = __ballot(fwdIn);
       const int pf = prev_in(fwC, lt);
-      const u64 pfOsn = sh64(osn, pf >= 0 ? pf : int(lane));
+      const int pfs = pf >= 0 ? pf : int(lane);
+      const u64 pfOsn = sh64(osn, pfs);
       const u64 prevOsn = pf >= 0 ? pfOsn : L.h.seqExtHighestSN;
-      const u64 pfOts = sh64(ots, pf >= 0 ? pf : int(lane));
+      const u64 pfOts = sh64(ots, pfs);
+      const u64 hiTS = pf >= 0 ? pfOts : L.h.seqExtHighestTS;  // the sequencer's highest TS
+      // Out-of-order lanes, one at a time (wave-uniform lookups): the RangeMap
+      // offset (GetValue), "esn - offset < extLastSN", the missing picture's
+      // offset (vp8.go:168-181) and its munged descriptor; a miss takes the
+      // serial step.  Exclusions the run adds lie above the run-start highest
+      // SN, so they do not move an older key's range unless the ring prunes
+      // the range it sits in.
+#if LKF_OOO_RUN
+      if (u64 oM = __ballot(okO)) {
+        const u64 mgLast = pf >= 0 ? pfOsn : L.h.extLastSN;
+        i32 po = 0;
+        do {
+          const u32 b = u32(__ffsll((long long)oM) - 1);
+          const u64 key = rl64(p.esn, b);
+          const int prunes = int(L.h.rmCount) + __popcll(tdM & ((1ull << b) - 1)) - kRangeCap;
+          bool good = !(prunes > 0 && key < L.h.rmOpenStart &&
+                        (prunes >= int(L.h.rmCount) || key < rm_at(L, prunes).start));
+          u64 off = 0;
+          if (good) good = rm_get(L, key, off) && (key - off) < rl64(mgLast, b);
+          i32 pb = 0;
+          if (good && video) {
+            const int mi = miss_find(L, i32(rl32(u32(ext), b)));
+            good = mi >= 0;
+            if (good) pb = L.missVal[mi];
+          }
+          if (lane == b) {
+            okO = good;
+            osn = key - off;
+            po = pb;
+          }
+          oM &= oM - 1;
+        } while (oM);
+        if (video && okO) {
+          const u16 opid = u16((ext - po) & 0x7fff);
+          const bool mM = opid > 127;
+          const int hs = int(p.vhs) + (mM == M ? 0 : (mM ? 1 : -1));
+          cbLen = vp8_marshal(p.vfirst, I, mM, opid, p.vbits & LKF_VP8_L, mtl0, T, p.tid, p.vbits & LKF_VP8_Y,
+                              p.vbits & LKF_VP8_K, mkey, hs, cb);
+        }
+      }
+#endif
+      bool fwd = fwdIn || okO;
       // sequencer highest TS = max over pushes; runs keep TS non-decreasing so it is the last one
-      const bool tsMono = ots >= (pf >= 0 ? pfOts : L.h.seqExtHighestTS);
+      const bool tsMono = ots >= hiTS;
       // the first push of a run may skip slots (a gap lane: osn - highest < size - 64)
       const bool seqOk = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && cbLen >= 0 && tsMono &&
                          (osn == prevOsn + 1 || (gapLane && pf < 0 && osn - prevOsn > 1 &&
                                                  osn - prevOsn < u64(L.seqSize) - 64));
-      const bool bad = inWin && ((cls == -2) || (cls == -1 && !ok) || (fwd && !seqOk));
+      // an out-of-order push fills a past slot and moves neither highest SN nor TS
+      const bool seqOkO = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && cbLen >= 0 && ots <= hiTS &&
+                          i64(osn - prevOsn) < 0;
+      const bool bad =
+          inWin && ((cls == -2) || (cls == -1 && !ok && !okO) || (fwdIn && !seqOk) || (okO && !seqOkO));
+#if LKF_DIAG || LKF_WTIME
+      // serial-step trigger of this lane (read at the stopping lane below)
+      int why = 0;
+      if (cls == -2)
+        why = whyKf ? 16 : (!(fl & F_SIMULCAST) ? 17 : 18);
+      else if (cls == -1 && !ok && !okO) {
+        if (oooL) why = 21;
+        else if (p.ssrc != L.h.lastSSRC) why = 19;
+        else if (p.plen == 0) why = 20;
+        else if (i64(p.esn - prevEsn) <= 0) why = 21;
+        else if (dEsn > 1 && !gapLane) why = 22;
+        else if (whyVid) why = 22 + whyVid;
+        else why = 26;
+      } else if ((fwdIn && !seqOk) || (okO && !seqOkO))
+        why = 27;
+#endif
       const u64 stopM = __ballot(bad || (valid && lane >= pos && !inWin));
       u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
       if (tswM & ~((1ull << pos) - 1)) x = min(x, u32(__ffsll((long long)(tswM & ~((1ull << pos) - 1))) - 1) + 1u);
       // ---- decide lanes [pos, x) together
       DIAG(2, x > pos ? 1 : 0);
+#if LKF_WTIME
+      wtRuns += x > pos ? 1 : 0;
+#endif
 #if LKF_DIAG
       const u64 tb0 = clock64();
       dg[5] += tb0 - tr0;
@@ -1995,8 +2123,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const bool inRun = (runM >> lane) & 1;
         const u64 tdR = tdM & runM;
         fwd = fwd && inRun;
-        const u64 fwR = __ballot(fwd);
-        const u64 selR = tdR | fwR;
+        const u64 fwR = __ballot(fwd);             // every forwarded lane (output order)
+        const u64 fwInR = __ballot(fwd && !oooL);  // in-order pushes
+        const u64 selR = tdR | fwInR;              // lanes that advance the munger
         o.nTuples += x - pos;
         // the run's drops: the classification's no-state-change reasons + temporal filter
         o.drops[LKF_DROP_MUTED] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_MUTED)));
@@ -2006,8 +2135,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         o.drops[LKF_DROP_TEMPORAL] += u32(__popcll(tdR));
         // first push of the run: slot distance from the sequencer's highest
         u32 gOff = 1;
-        if (fwR) {
-          const u32 firstF = u32(__ffsll((long long)fwR) - 1);
+        if (fwInR) {
+          const u32 firstF = u32(__ffsll((long long)fwInR) - 1);
           gOff = u32(rl64(osn, firstF) - L.h.seqExtHighestSN);
           const u64 gR = __ballot(gapLane && inRun);
           if (gR) {  // the run starts after a loss gap (the gap lane is forwarded)
@@ -2031,6 +2160,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const u32 relEx = excl_scan_u32(aligned, lane);
         const bool marker = pktMarker;  // tp.marker (= hdr.Marker for video, false for audio) || hdr.Marker
         const u32 j = u32(__popcll(fwR & lt));
+        const u32 jIn = u32(__popcll(fwInR & lt));
         if (fwd) {
           Tuple t;
           t.extSN = osn;
@@ -2052,8 +2182,19 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #if LKF_ABLATE != 1
           store_rec(o.outT + o.nFwd + j, t);
 #endif
-          // sequencer.push in-order branch (sequencer.go:123-209): next slot
-          u32 slot = u32(L.h.seqHighSlot) + gOff + j;
+          // sequencer.push (sequencer.go:123-209): in order, the next slot; out of
+          // order, the slot delta behind the highest (skipped when older than
+          // the window or the sequencer's start)
+          u32 slot;
+          bool store = true;
+          if (!oooL) {
+            slot = u32(L.h.seqHighSlot) + gOff + jIn;
+          } else {
+            const u32 hs = jIn ? u32(L.h.seqHighSlot) + gOff - 1 + jIn : u32(L.h.seqHighSlot);
+            const i64 delta = i64(osn - prevOsn);
+            store = delta > -i64(L.seqSize) && osn >= L.h.seqExtStartSN;
+            slot = hs + u32(i64(L.seqSize) + delta);
+          }
           while (slot >= L.seqSize) slot -= L.seqSize;
           SeqMeta m = {};
           m.sourceSeqNo = u16(p.esn);
@@ -2066,16 +2207,18 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #pragma unroll
           for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
 #if LKF_ABLATE != 1
-          store_rec(L.seq + slot, m);
+          if (store) store_rec(L.seq + slot, m);
 #endif
         }
         const u32 sumLen = wave_sum_u32(outLen);
         // ---- advance the DownTrack state past the run (uniform)
         if (fwR) {
-          const u32 lastF = 63 - __clzll(fwR);
-          const u32 nF = u32(__popcll(fwR));
           o.nBytes += sumLen;
-          o.nFwd += nF;
+          o.nFwd += u32(__popcll(fwR));
+        }
+        if (fwInR) {
+          const u32 lastF = 63 - __clzll(fwInR);
+          const u32 nF = u32(__popcll(fwInR));
           u32 slot = u32(L.h.seqHighSlot) + gOff - 1 + nF;
           while (slot >= L.seqSize) slot -= L.seqSize;
           L.h.seqHighSlot = u16(slot);
@@ -2091,8 +2234,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           const u32 lastSel = 63 - __clzll(selR);
           const u64 mk = __ballot(video && pktMarker);  // marker passed to UpdateAndGetSnTs
           L.h.extHighestIncomingSN = rl64(p.esn, lastSel);
-          const bool lastIsF = (fwR >> lastSel) & 1;
-          const u64 pfM = fwR & ((1ull << lastSel) - 1);
+          const bool lastIsF = (fwInR >> lastSel) & 1;
+          const u64 pfM = fwInR & ((1ull << lastSel) - 1);
           u64 sSN = L.h.extLastSN, sTS = L.h.extLastTS;
           bool sMk = fl & F_LAST_MARKER;
           if (pfM) {
@@ -2130,7 +2273,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
             u64 m = tdR;
             while (m) {
               const u32 b = u32(__ffsll((long long)m) - 1);
-              const u64 after = fwR & ~((2ull << b) - 1);
+              const u64 after = fwInR & ~((2ull << b) - 1);
               const u32 nf = after ? u32(__ffsll((long long)after) - 1) : 64u;
               const u64 runD = tdR & (nf >= 64 ? ~0ull : ((1ull << nf) - 1)) & ~((1ull << b) - 1);
               const u64 s0 = rl64(p.esn, b);
@@ -2171,11 +2314,38 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const uint4 a2 = make_uint4(rl32(r2.x, x), rl32(r2.y, x), rl32(r2.z, x), rl32(r2.w, x));
         const uint4 a3 = make_uint4(rl32(r3.x, x), rl32(r3.y, x), rl32(r3.z, x), rl32(r3.w, x));
         const u32 px = rl32(pi, x);
+#if LKF_WTIME
+        wtSerial++;
+        {
+          const int wx = int(rl32(u32(why), x));
+          if (wx == 21) wtWhy[0]++;
+          else if (wx == 16) wtWhy[1]++;
+          else if (wx == 19 || wx == 20) wtWhy[2]++;
+          else wtWhy[3]++;
+        }
+#endif
+#if LKF_DIAG
+        {
+          const int wx = int(rl32(u32(why), x));
+          if (wx) dg2[wx - 16] += 1;
+          dg2[15] += 1;
+        }
+#endif
+#if LKF_WTIME
+        const u64 ws0 = __builtin_amdgcn_s_memtime();
+#endif
         decide_step<DDK>(L, decode_pkt(a0, a1, a2, a3), px, o);
+#if LKF_WTIME
+        const u64 ws1 = __builtin_amdgcn_s_memtime();
+        wcStep += ws1 - ws0;
+#endif
 #if LKF_DIAG
         const u64 tdr0 = clock64();
 #endif
         vm_drain();
+#if LKF_WTIME
+        wcDrain += __builtin_amdgcn_s_memtime() - ws1;
+#endif
 #if LKF_DIAG
         dg[4] += clock64() - tdr0;  // (diag slot 4: the drain after the full step)
 #endif
@@ -2198,10 +2368,32 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     kpos = lim;
   }
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
+#if LKF_WTIME
+  if (lane == 0 && w < kWTimeWaves) {
+    const u64 wt1 = __builtin_amdgcn_s_memrealtime();
+    u32 *g = g_wtime + w * 16;
+    g[0] = u32(wt0);
+    g[1] = u32(wt1);
+    g[2] = pe - pb;
+    g[3] = wtSerial | (wtChunks << 16);
+    g[4] = u32(wcPro);
+    g[5] = u32(wcStep);
+    g[6] = u32(wcDrain);
+    g[7] = u32(__builtin_amdgcn_s_memtime() - wc0);
+    g[8] = wtRuns;
+    for (int i = 0; i < 4; i++) g[9 + i] = wtWhy[i];
+    g[13] = u32(L.h.curS) | (u32(L.h.tgtS) << 8) | (u32(L.h.curT) << 16) | (u32(L.h.tgtT) << 24);
+    g[14] = L.h.flags;
+    g[15] = d;
+  }
+#endif
 #if LKF_DIAG
   dg[14] += clock64() - tk0;
   if (lane == 0)
-    for (int i = 0; i < 16; i++) atomicAdd(&g_diag[i], (unsigned long long)dg[i]);
+    for (int i = 0; i < 16; i++) {
+      atomicAdd(&g_diag[i], (unsigned long long)dg[i]);
+      atomicAdd(&g_diag[16 + i], (unsigned long long)dg2[i]);
+    }
 #endif
 #if LKF_STATE_LDS
   __syncthreads();
@@ -2236,6 +2428,12 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   if (lane == 0) {
     A.fwdCnt[d] = u32(o.nFwd);
     A.fwdBytes[d] = o.relOff;
+    // DownTrack.sendingPacket: bytesSent += header + payload (downtrack.go:1934-1940)
+    DTCum c = A.dtCum[d];
+    c.packets += o.nFwd;
+    c.bytes += o.nBytes;
+    c.flags = L.h.flags;
+    A.dtCum[d] = c;
     // counters: one of kStatCopies partial copies per wave (same-address
     // atomics from every wave would serialise in one L2 channel); k_stats_reduce
     // folds the copies after the kernel
@@ -2740,20 +2938,31 @@ hipError_t launch_dd_decode(hipStream_t s, const lkf_pkt *pkts, const lkf_pkt_dd
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 
 #if LKF_DIAG
-hipError_t read_diag(unsigned long long out[16], int reset) {
-  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 16);
+hipError_t read_diag(unsigned long long out[32], int reset) {
+  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 32);
   if (r == hipSuccess && reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     r = hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
   }
   return r;
 }
 #else
-hipError_t read_diag(unsigned long long out[16], int) {
-  for (int i = 0; i < 16; i++) out[i] = 0;
+hipError_t read_diag(unsigned long long out[32], int) {
+  for (int i = 0; i < 32; i++) out[i] = 0;
   return hipErrorNotSupported;
 }
 #endif
+
+hipError_t read_wtime(u32 *out, u32 nwaves) {
+#if LKF_WTIME
+  if (nwaves > kWTimeWaves) nwaves = kWTimeWaves;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtime), sizeof(u32) * 16 * nwaves);
+#else
+  (void)out;
+  (void)nwaves;
+  return hipErrorNotSupported;
+#endif
+}
 
 hipError_t launch_batch_init(hipStream_t s, u32 ntracks, u32 ndts, u32 nstats, u32 *tBegin, u32 *tEnd, u32 *tRuns,
                              u32 *err, u64 *stats, u32 *fwdCnt, u64 *fwdBytes) {
@@ -2822,6 +3031,7 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.layerCnt = a.layerCnt;
   A.pktStride = a.pktStride;
   A.fwdBytes = a.fwdBytes;
+  A.dtCum = a.dtCum;
   A.stats = a.stats;
   A.ddPkts = a.ddPkts;
   A.ddStructs = a.ddStructs;

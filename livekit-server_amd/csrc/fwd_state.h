@@ -220,6 +220,16 @@ struct DevTrack {  // track table (24 x 4 B)
 };
 
 // ---- ingress: one received stream = one buffer.Buffer (buffer.go:66-130) ----
+// per-DownTrack totals since it was added (lkf_downtrack_summaries): written
+// by the DownTrack's decide wave (no atomics: one wave per DownTrack)
+struct DTCum {
+  uint64_t packets, bytes;
+  uint32_t flags;  // DTHot flags after the last batch (F_DEFICIENT)
+  uint32_t pad;
+  uint64_t pad2;
+};
+static_assert(sizeof(DTCum) == 32, "DTCum is 32 B");
+
 constexpr int kHistWords = 64;  // cHistorySize 4096 bits (rtpstats_receiver.go:30)
 
 struct DevStream {  // static stream parameters (64 B)

@@ -30,6 +30,7 @@ struct DecideLaunch {
   const uint32_t *evOff;
   uint32_t *fwdCnt;
   uint64_t *fwdBytes;
+  DTCum *dtCum;
   uint64_t *stats;
   const uint32_t *layerList, *layerBefore, *layerCnt;  // launch_layer_index outputs
   uint32_t pktStride;                                  // max_batch_pkts
@@ -60,7 +61,8 @@ struct EmitLaunch {
 };
 
 // diagnostic builds (-DLKF_DIAG=1): k_decide_dt per-wave counters
-hipError_t read_diag(unsigned long long out[16], int reset);
+hipError_t read_diag(unsigned long long out[32], int reset);
+hipError_t read_wtime(uint32_t *out, uint32_t nwaves);  // LKF_WTIME builds
 hipError_t launch_batch_init(hipStream_t s, uint32_t ntracks, uint32_t ndts, uint32_t nstats, uint32_t *tBegin,
                              uint32_t *tEnd, uint32_t *tRuns, uint32_t *err, uint64_t *stats, uint32_t *fwdCnt,
                              uint64_t *fwdBytes);

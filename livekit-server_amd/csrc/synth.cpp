@@ -305,7 +305,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
     std::vector<u32> audioPub;
   };
   for (u32 r = 0; r < rooms; r++) {
-    const u32 room = cfg->room_base + r;
+    const u32 room = cfg->room_ids ? cfg->room_ids[r] : cfg->room_base + r;
     Rng rng = keyed((1ull << 40) + room);
     const size_t dt0 = tr->dts.size();
     RoomTracks rt;

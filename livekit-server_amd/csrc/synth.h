@@ -35,6 +35,9 @@ typedef struct lkfs_cfg {
   int32_t h264;          /* configs 1-3: 1 -> H.264 simulcast publishers (config 1: the publisher;
                             else every third) with SPS key frames as single NALU / STAP-A / STAP-B /
                             FU-A; <= 0 -> VP8 only */
+  int32_t pad0;
+  const uint32_t *room_ids; /* non-null: generate rooms room_ids[0..rooms) (a bin-packed shard)
+                               instead of room_base + [0, rooms) */
 } lkfs_cfg;
 
 typedef struct lkfs_event {

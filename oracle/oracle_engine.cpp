@@ -54,6 +54,8 @@ struct ODT {
   u64 extStartTS = 0;
   bool playoutAcked = false;
   std::vector<OOut> outs;
+  // DownTrack.sendingPacket counters (downtrack.go:1930-1941)
+  u64 packetsSent = 0, bytesSent = 0;
 };
 
 struct OEv {
@@ -397,6 +399,11 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   }
   for (u32 d = 0; d < ndt; d++)
     while (evc[d] < evq[d].size()) applyCtl(e, *e->dts[d], evq[d][evc[d]++]);
+  for (u32 d = 0; d < ndt; d++)  // sendingPacket: bytesSent += hdrSize + payloadSize
+    for (auto &o : e->dts[d]->outs) {
+      e->dts[d]->packetsSent++;
+      e->dts[d]->bytesSent += o.bytes.size();
+    }
   // Output order: by track, then DownTrack handle, then packet; wire packets
   // 16-B aligned.  (An engine-defined batch layout: the reference hands each
   // packet to its DownTrack's pacer directly.)
@@ -430,6 +437,23 @@ int orc_drain(orc_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_
   if (e->outRecs.size() > cap || e->outArena.size() > arena_cap) return LKF_ENOSPC;
   if (out && !e->outRecs.empty()) std::memcpy(out, e->outRecs.data(), e->outRecs.size() * sizeof(lkf_out));
   if (arena && !e->outArena.empty()) std::memcpy(arena, e->outArena.data(), e->outArena.size());
+  return LKF_OK;
+}
+
+int orc_downtrack_summaries(orc_engine *e, lkf_dt_summary *out, uint32_t cap, uint32_t *n_out) {
+  const u32 nd = u32(e->dts.size());
+  *n_out = nd;
+  if (cap < nd) return LKF_ENOSPC;
+  for (u32 d = 0; d < nd; d++) {
+    const ODT &t = *e->dts[d];
+    lkf_dt_summary &s = out[d];
+    s.dt = int32_t(d);
+    s.subscriber = t.p.subscriber;
+    s.room = e->tracks[t.p.track].p.room;
+    s.flags = (t.active ? LKF_DTS_ACTIVE : 0u) | (t.f->lastAllocIsDeficient ? LKF_DTS_DEFICIENT : 0u);
+    s.packets_sent = t.packetsSent;
+    s.bytes_sent = t.bytesSent;
+  }
   return LKF_OK;
 }
 

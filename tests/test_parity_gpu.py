@@ -69,6 +69,13 @@ def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True, extr
                 raise AssertionError("batch %d wire bytes differ at %d (record %d: %s)" % (b, bad[0], r, grec[r]))
             totals["forwarded"] += gs["forwarded"]
             totals["tuples"] += gs["tuples"]
+        # §8(e) per-subscriber records: DownTrack.sendingPacket totals + IsDeficient
+        gsum = pkg.downtrack_summaries(eng.api, eng.h)
+        osum = pkg.downtrack_summaries(o.api, oh)
+        assert len(gsum) == len(osum) == trace.ndts
+        for f in abi.DT_SUMMARY_DTYPE.names:
+            assert np.array_equal(gsum[f], osum[f]), ("summary field", f)
+        assert int(gsum["packets_sent"].sum()) == totals["forwarded"]
         if check_state:
             for dt in range(trace.ndts):
                 assert _state_tuple(eng.api, eng.h, dt, abi) == _state_tuple(o.api, oh, dt, abi), dt

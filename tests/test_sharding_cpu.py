@@ -120,7 +120,8 @@ def _spk_worker(rank, port, q):
         now = 1700000000 * 10**9 + int(2.0e9)
         base = rank * SPK_ROOMS_PER_RANK
         sp = _speakers(SPK_ROOMS_PER_RANK, base, now)
-        table = rooms_mod.all_gather_speakers(dist, torch.device("cpu"), sp, base, SPK_ROOMS_PER_RANK)
+        table = rooms_mod.all_gather_speakers(dist, torch.device("cpu"), sp,
+                                              rooms_mod.rank_rooms(base, SPK_ROOMS_PER_RANK))
         if rank == 0:
             q.put(table)
     finally:
@@ -143,6 +144,91 @@ def test_speaker_summaries_all_gathered():
     assert table.shape == (WORLD, SPK_ROOMS_PER_RANK, rooms_mod.K_MAX, 3)
     now = 1700000000 * 10**9 + int(2.0e9)
     full = _speakers(WORLD * SPK_ROOMS_PER_RANK, 0, now)
-    want = rooms_mod.pack_speakers(full, 0, WORLD * SPK_ROOMS_PER_RANK).reshape(table.shape)
+    want = rooms_mod.pack_speakers(full, rooms_mod.rank_rooms(0, WORLD * SPK_ROOMS_PER_RANK)).reshape(table.shape)
     assert (table == want).all()
     assert (table[:, :, 0, 0] >= 0).any()  # at least one room has a ranked speaker
+
+
+# ---- §8(e): per-subscriber bandwidth records over a bin-packed room plan ----
+BWE_ROOMS = 5
+
+
+def _bwe(room_ids, rows=None):
+    """Forward the rooms through the oracle; fold lkf_downtrack_summaries per (room, subscriber)."""
+    from tests.oracle_lib import load as load_oracle
+    wl = importlib.import_module("livekit-server_amd.workload")
+    pkg = importlib.import_module("livekit-server_amd")
+    rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+    o = load_oracle()
+    tr = wl.Trace(2, duration_s=2.0, batch_s=1.0, room_ids=list(room_ids))
+    h = o.create(500)
+    try:
+        wl.load_topology(o.api, h, tr)
+        for b in range(tr.nbatches):
+            wl.queue_events(o.api, h, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(h, pk, n, ar, alen)
+        summ = pkg.downtrack_summaries(o.api, h)
+        # the summaries are the per-DownTrack sums of the drained output
+        return rooms_mod.fold_summaries(summ, sorted(room_ids), rows=rows), summ
+    finally:
+        o.destroy(h)
+        tr.close()
+
+
+def _bwe_worker(rank, port, plan, q):
+    width = max(len(p) for p in plan)
+    import torch
+    rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        rec, _ = _bwe(plan[rank], rows=width)
+        table = rooms_mod.all_gather_records(dist, torch.device("cpu"), rec)
+        if rank == 0:
+            q.put(table)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bwe_records_bin_packed_match_single_process():
+    """Rooms bin-packed onto 2 ranks (unequal room counts); each rank forwards
+    only its rooms and folds its DownTrack summaries; the all-gathered
+    per-(room, subscriber) records equal one process forwarding every room."""
+    rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+    costs = [3.0, 1.0, 1.0, 1.0, 2.0]  # expected tuples per room (heterogeneous on purpose)
+    plan = rooms_mod.plan_room_shards(costs, WORLD)
+    assert sorted(r for p in plan for r in p) == list(range(BWE_ROOMS))
+    assert len(plan[0]) != len(plan[1])
+    # fixed-shape gather: pad the shorter shard's room list to the longest
+    width = max(len(p) for p in plan)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bwe_worker, args=(r, port, plan, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    table = q.get(timeout=10)
+    assert table.shape[0] == WORLD and table.shape[1] == width
+    got = rooms_mod.unpack_bwe(table, plan)
+    full, summ = _bwe(range(BWE_ROOMS))
+    want = rooms_mod.unpack_bwe(full[None], [list(range(BWE_ROOMS))])
+    assert got == want
+    assert sum(v[1] for v in got.values()) == int(summ["bytes_sent"].sum()) > 0
+    assert any(v[2] for v in got.values())  # some subscriber was left deficient by an allocation
+
+
+def test_plan_room_shards_lpt():
+    rooms_mod = importlib.import_module("livekit-server_amd.rooms")
+    import itertools
+    costs = [7, 5, 4, 4, 3, 3, 2, 1]
+    plan = rooms_mod.plan_room_shards(costs, 3)
+    loads = [sum(costs[r] for r in p) for p in plan]
+    best = min(max(sum(costs[r] for r in range(8) if a[r] == w) for w in range(3))
+               for a in itertools.product(range(3), repeat=8))
+    assert max(loads) <= best * 4 / 3 + 1e-9  # Graham's LPT bound
+    assert sorted(r for p in plan for r in p) == list(range(8))
