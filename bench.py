@@ -120,6 +120,9 @@ def main():
                     help="diagnostic: wait for each step (no decide/emit overlap; standalone kernel times)")
     ap.add_argument("--ingress", action="store_true",
                     help="step = Buffer.calc over raw datagrams (lkf_ingest_device) + forwarding")
+    ap.add_argument("--host-io", action="store_true",
+                    help="host-fed deployment shape: lkf_submit from pinned host memory and lkf_drain_run of "
+                         "the previous batch into pinned host memory inside the timed region (PCIe both ways)")
     args = ap.parse_args()
 
     import torch
@@ -152,8 +155,9 @@ def main():
     if args.ingress:
         wl.load_streams(eng.api, eng.h, trace)
 
-    # inputs resident in HBM before the timed region
+    # inputs resident in HBM before the timed region (--host-io: in pinned host memory)
     dpk, dar, meta = [], [], []
+    hdev = torch.device("cpu") if args.host_io else dev
     for b in range(nb):
         if args.ingress:
             pk, n, ar, alen = trace.batch_raw(b)  # raw datagrams: Buffer.calc runs inside the step
@@ -161,8 +165,10 @@ def main():
         else:
             pk, n, ar, alen = trace.batch(b)
             rsz = 64
-        tp = torch.frombuffer(bytearray(C.string_at(pk, max(1, n) * rsz)), dtype=torch.uint8).to(dev)
-        ta = torch.zeros(alen + 64, dtype=torch.uint8, device=dev)
+        tp = torch.frombuffer(bytearray(C.string_at(pk, max(1, n) * rsz)), dtype=torch.uint8).to(hdev)
+        if args.host_io:
+            tp = tp.pin_memory()
+        ta = torch.zeros(alen + 64, dtype=torch.uint8, device=hdev, pin_memory=args.host_io)
         if alen:
             ta[:alen].copy_(torch.frombuffer(bytearray(C.string_at(ar, alen)), dtype=torch.uint8))
         dpk.append(tp)
@@ -172,6 +178,18 @@ def main():
     sp = C.c_void_p(stream.cuda_stream)
 
     hprof = [0.0, 0.0, 0.0] if os.environ.get("LKF_HOST_PROF") else None
+    if args.host_io:  # pinned host output buffers for lkf_drain_run
+        out_cap = int(trace.max_batch_tuples)
+        h_out = torch.empty(out_cap * 40, dtype=torch.uint8, pin_memory=True)
+        ar_cap = int(trace.max_batch_out_bytes) + 16 * out_cap
+        h_ar = torch.empty(ar_cap, dtype=torch.uint8, pin_memory=True)
+    drained = [0, 0]
+
+    def drain_prev(age):
+        nrec, nbytes = eng.drain_run_into(age, C.c_void_p(h_out.data_ptr()), out_cap,
+                                          C.c_void_p(h_ar.data_ptr()), ar_cap)
+        drained[0] += nrec
+        drained[1] += nbytes
 
     def step(b):
         ta = time.perf_counter()
@@ -180,10 +198,14 @@ def main():
         n, alen = meta[b]
         if args.ingress:
             eng.ingest_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
+        elif args.host_io:
+            eng.submit(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
         else:
             eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
         tc = time.perf_counter()
         eng.run(sp)
+        if args.host_io and b > args.warmup:  # batch b-1's output over PCIe while batch b computes
+            drain_prev(1)
         if args.sync_each:
             eng.sync()
         if hprof is not None:
@@ -203,6 +225,8 @@ def main():
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
+    if args.host_io:
+        drain_prev(0)  # the last batch's output reaches host memory inside the timed region
     t_host = time.perf_counter() - t0  # host time to enqueue the K steps (control ops, submit, lkf_run)
     if hprof is not None:
         print("host ms/step (incl. warmup): queue_events %.4f submit %.4f run %.4f" %
@@ -311,7 +335,10 @@ def main():
                                    "%d DownTracks, 2%% loss, 1%% reorder, layer switching" % (args.rooms, trace.ndts),
                        "batch": "%.3g s of media per step" % args.batch_s,
                        "step": ("raw datagrams -> Buffer.calc -> forward (lkf_ingest_device + lkf_run)"
-                                if args.ingress else "ExtPacket batch -> forward (lkf_submit_device + lkf_run)"),
+                                if args.ingress else
+                                "host-fed: pinned host ExtPacket batch -> lkf_submit (H2D) + lkf_run + "
+                                "lkf_drain_run of the previous batch (D2H)" if args.host_io else
+                                "ExtPacket batch -> forward (lkf_submit_device + lkf_run)"),
                        "parallelism": "room-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": round(ach / PEAK_HBM_GBPS, 4), "traffic": traffic,
@@ -328,6 +355,12 @@ def main():
             "tuples_per_step": cum["tuples"] // args.steps,
             "forwarded_per_step": fwd // args.steps,
         }
+        if args.host_io:  # PCIe-inclusive deployment shape (never the headline value)
+            h2d = sum(meta[b][0] * 64 + meta[b][1] for b in range(args.warmup, nb))
+            line["host_io"] = {"h2d_bytes_per_step": h2d // args.steps,
+                               "d2h_bytes_per_step": (drained[0] * 40 + drained[1]) // args.steps,
+                               "drained_records": drained[0], "records_forwarded": fwd,
+                               "pcie_GBps_both_ways": round((h2d + drained[0] * 40 + drained[1]) / elapsed / 1e9, 2)}
         print(json.dumps(line))
     eng.close()
     if dist:

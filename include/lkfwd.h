@@ -375,6 +375,14 @@ int lkf_get_stats(lkf_engine *e, lkf_stats *out);
 /* Copies up to `cap` records and the wire bytes to host memory. */
 int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap, uint64_t *n_out,
               uint64_t *arena_len);
+/* Pipelined host output: copies the records and wire bytes of the run `age`
+ * runs before the last one (0 = the last, at most 2: the engine keeps three
+ * batch contexts) once its emit stage has finished, without waiting for the
+ * runs queued after it — a host loop submit(b); run(b); drain_run(1) moves
+ * batch b-1's output over PCIe while batch b computes.  Does not report the
+ * sticky error word (lkf_sync does).  LKF_EINVAL if that run does not exist. */
+int lkf_drain_run(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap,
+                  uint64_t *n_out, uint64_t *arena_len);
 /* Device pointers of the output (zero-copy consumer, e.g. an SRTP stage). */
 int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, const uint8_t **d_arena,
                       uint64_t *arena_len);

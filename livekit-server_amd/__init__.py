@@ -201,6 +201,17 @@ class Engine:
     def drain(self):
         return drain_arrays(self.api, self.h)
 
+    def drain_run_into(self, age, out_ptr, cap, arena_ptr, arena_cap):
+        """lkf_drain_run into caller buffers (e.g. pinned host memory) -> (records, bytes)."""
+        n = C.c_uint64()
+        alen = C.c_uint64()
+        f = self.lib.lkf_drain_run
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        self._chk(f(self.h, age, out_ptr, cap, arena_ptr, arena_cap, C.byref(n), C.byref(alen)), "drain_run")
+        return n.value, alen.value
+
     def output_device(self):
         d_out = C.c_void_p()
         d_ar = C.c_void_p()
