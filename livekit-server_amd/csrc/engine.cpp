@@ -51,7 +51,6 @@ struct BatchCtx {
   uint32_t *dFwdCnt = nullptr;
   uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
   uint32_t *dGFirst = nullptr;  // emit group g -> output position owning record 64g
-  uint32_t *dOrdPos = nullptr, *dOrdJ = nullptr;  // k_emit_order: packet-major record order
   uint32_t *dLayerList = nullptr, *dLayerBefore = nullptr, *dLayerCnt = nullptr;  // k_layer_index
   lkf_out *dOut = nullptr;
   uint8_t *dOutArena = nullptr;
@@ -140,8 +139,6 @@ struct lkf_engine {
   uint32_t *dWaveTrack = nullptr;
   uint32_t *dEvOff = nullptr;
   uint32_t *dPerm = nullptr;  // output position -> DownTrack (track-major)
-  uint32_t *dTrackPos = nullptr;  // [track] first output position of its DownTracks (max_tracks + 1)
-  uint32_t trackPosN = 0;         // tracks dTrackPos covers (later ones have no DownTrack yet)
   size_t schedCap = 0;
   DevEvent *dEvents = nullptr;
   uint64_t evCap = 0;
@@ -447,7 +444,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dCum, kStatsWords));
   A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
-  A(dalloc(&e->dTrackPos, size_t(c.max_tracks) + 1));
   const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
   for (auto &x : e->ctx) {
     A(dalloc(&x.dTBegin, c.max_tracks));
@@ -464,8 +460,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dRecBase, c.max_downtracks));
     A(dalloc(&x.dByteBase, c.max_downtracks));
     A(dalloc(&x.dGFirst, c.max_out_pkts / 64 + 2));
-    A(dalloc(&x.dOrdPos, c.max_out_pkts));
-    A(dalloc(&x.dOrdJ, c.max_out_pkts));
     A(dalloc(&x.dLayerList, 3 * size_t(c.max_batch_pkts) + 64));
     A(dalloc(&x.dLayerBefore, 3 * size_t(c.max_batch_pkts) + 64));
     A(dalloc(&x.dLayerCnt, 3 * size_t(c.max_tracks)));
@@ -543,7 +537,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
-                  e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm, e->dTrackPos,
+                  e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
@@ -561,7 +555,7 @@ void lkf_destroy(lkf_engine *e) {
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
-                 x.dRawPkts, x.dGFirst, x.dOrdPos, x.dOrdJ, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane};
+                 x.dRawPkts, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane};
     for (void *p : q)
       if (p) (void)hipFree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
@@ -825,11 +819,6 @@ static int rebuild_sched(lkf_engine *e) {
     std::stable_sort(perm.begin(), perm.end(),
                      [&](uint32_t a, uint32_t b) { return e->dtp[a].track < e->dtp[b].track; });
     if (nd) HIPCHK(hipMemcpy(e->dPerm, perm.data(), nd * sizeof(uint32_t), hipMemcpyHostToDevice), "perm copy");
-    std::vector<uint32_t> tpos(nt + 1, 0);  // first position of each track's DownTracks
-    for (uint32_t d = 0; d < nd; d++) tpos[e->dtp[d].track + 1]++;
-    for (uint32_t t = 0; t < nt; t++) tpos[t + 1] += tpos[t];
-    HIPCHK(hipMemcpy(e->dTrackPos, tpos.data(), (nt + 1) * sizeof(uint32_t), hipMemcpyHostToDevice), "track pos copy");
-    e->trackPosN = nt;
   }
   if (nl) {
     HIPCHK(hipMemcpy(e->dSched, e->sched.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice), "sched copy");
@@ -1033,10 +1022,6 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.recBase = x.dRecBase;
   m.byteBase = x.dByteBase;
   m.gFirst = x.dGFirst;
-  m.ordPos = x.dOrdPos;
-  m.ordJ = x.dOrdJ;
-  m.tBegin = x.dTBegin;
-  m.tEnd = x.dTEnd;
   m.slotBase = x.dSlotBase;
   m.totals = x.dTot + 2;
   m.tuples = x.dTuples;
@@ -1056,7 +1041,6 @@ int lkf_run(lkf_engine *e, void *stream) {
   // stream) interleaves with this emit instead of waiting for a persistent grid.
   m.grid = e->emitPersistent ? e->emitGrid
                              : uint32_t(((e->cfg.max_out_pkts + 63) / 64 + 7) / 8 * 8);
-  if (nd) HIPCHK(launch_emit_order(e->emitS, m, e->dTrackPos, e->trackPosN), "emit order");
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum, x.dErr, e->dSticky), "accumulate");

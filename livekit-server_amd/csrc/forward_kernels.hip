@@ -2448,99 +2448,20 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 }
 
 // ---------------------------------------------------------------------------
-// k_emit_order: the order k_emit processes a batch's output records in.  The
-// output is track-major, then DownTrack, then packet; k_emit walks each
-// track's records packet-major instead (a counting sort by packet index, one
-// workgroup per track), so every copy of one input packet — one per
-// subscribing DownTrack that forwards it — is made by the same or adjacent
-// waves while its payload is in L1/L2: the payload leaves HBM once per packet
-// rather than once per copy.  ordPos/ordJ[i] = (output position, index of
-// the record within its DownTrack) of the i-th record processed; the output
-// layout is unchanged.
-// ---------------------------------------------------------------------------
-constexpr int ORD_T = 256;
-constexpr u32 kOrdMax = 4096;  // packets of one track per batch sorted in LDS (more: DownTrack order)
-__global__ void __launch_bounds__(ORD_T) k_emit_order(const u32 *__restrict__ trackPos, u32 ndts,
-                                                      const u32 *__restrict__ perm, const u64 *__restrict__ recBase,
-                                                      const u64 *__restrict__ totals, const u64 *__restrict__ slotBase,
-                                                      const Tuple *__restrict__ tuples, const u32 *__restrict__ tBegin,
-                                                      const u32 *__restrict__ tEnd, u32 *__restrict__ ordPos,
-                                                      u32 *__restrict__ ordJ) {
-  __shared__ u32 hist[kOrdMax];
-  __shared__ u32 part[ORD_T];
-  const u32 t = blockIdx.x, tid = threadIdx.x;
-  const u32 p0 = trackPos[t], p1 = trackPos[t + 1];
-  if (p0 == p1) return;
-  const u64 rb = recBase[p0];
-  const u64 re = p1 < ndts ? recBase[p1] : totals[0];
-  if (rb == re) return;
-  const u32 pb = tBegin[t];
-  const u32 np = tEnd[t] - pb;
-  auto recEnd = [&](u32 p) { return p + 1 < ndts ? recBase[p + 1] : totals[0]; };
-  if (np > kOrdMax) {  // DownTrack order (the output order)
-    for (u32 p = p0; p < p1; p++) {
-      const u64 b = recBase[p], e = recEnd(p);
-      for (u64 j = tid; j < e - b; j += ORD_T) {
-        ordPos[b + j] = p;
-        ordJ[b + j] = u32(j);
-      }
-    }
-    return;
-  }
-  for (u32 i = tid; i < np; i += ORD_T) hist[i] = 0;
-  __syncthreads();
-  for (u32 p = p0; p < p1; p++) {
-    const u64 b = recBase[p], e = recEnd(p);
-    const Tuple *tp = tuples + slotBase[perm[p]];
-    for (u64 j = tid; j < e - b; j += ORD_T) atomicAdd(&hist[tp[j].pkt - pb], 1u);
-  }
-  __syncthreads();
-  // exclusive scan of hist[0, np): a contiguous run per thread, then the runs' sums
-  const u32 per = (np + ORD_T - 1) / ORD_T, i0 = tid * per, i1 = min(np, i0 + per);
-  u32 sum = 0;
-  for (u32 i = i0; i < i1; i++) sum += hist[i];
-  part[tid] = sum;
-  __syncthreads();
-  for (u32 o = 1; o < ORD_T; o <<= 1) {  // Hillis-Steele over the run sums
-    const u32 v = tid >= o ? part[tid - o] : 0u;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  u32 run = part[tid] - sum;
-  for (u32 i = i0; i < i1; i++) {
-    const u32 c = hist[i];
-    hist[i] = run;
-    run += c;
-  }
-  __syncthreads();
-  for (u32 p = p0; p < p1; p++) {
-    const u64 b = recBase[p], e = recEnd(p);
-    const Tuple *tp = tuples + slotBase[perm[p]];
-    for (u64 j = tid; j < e - b; j += ORD_T) {
-      const u64 k = rb + atomicAdd(&hist[tp[j].pkt - pb], 1u);
-      ordPos[k] = p;
-      ordJ[k] = u32(j);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // k_emit: wire bytes.  One wave per workgroup; waves run independently (no
 // cross-wave barrier), so one wave's prefix phase (dependent loads) hides
-// behind the other waves' copy phase.  A wave takes EMIT_G consecutive records
-// of the k_emit_order sequence (grid-stride over groups):
-//   prefix phase  lane = record: its position and index from k_emit_order,
-//                 then the RTP header + extension block + munged VP8
-//                 descriptor ("prefix") in LDS.
-//   copy phase    the group's records as one sweep of 16-B chunks (each
-//                 record's chunks to its own output offset), EMIT_U windows
-//                 of 64 chunks per iteration (all loads in flight together).
-//                 A chunk's record comes from a wave-uniform cursor plus the
-//                 record starts inside the window (readlane loop, no per-lane
-//                 search).  Prefix chunks come from LDS, payload chunks are
-//                 byte-shifted copies of the input packet (two dwordx4 loads +
-//                 v_alignbyte).
+// behind the other waves' copy phase.  A wave takes EMIT_G consecutive output
+// records (grid-stride over groups):
+//   prefix phase  lane = record: owning DownTrack from the group index
+//                 (gFirst, a 1-3 step search), then the RTP header +
+//                 extension block + munged VP8 descriptor ("prefix") in LDS.
+//   copy phase    the group's output bytes as a flat sweep of 16-B chunks,
+//                 two windows of 64 chunks per iteration (both loads in
+//                 flight together).  A chunk's record comes from a
+//                 wave-uniform cursor plus the record starts inside the
+//                 window (readlane loop, no per-lane search).  Prefix chunks
+//                 come from LDS, payload chunks are byte-shifted copies of the
+//                 input packet (two dwordx4 loads + v_alignbyte).
 // ---------------------------------------------------------------------------
 constexpr int EMIT_T = 64;
 constexpr int EMIT_G = 64;
@@ -2559,7 +2480,6 @@ constexpr int EMIT_U = LKF_EMIT_U;
 #endif
 
 struct EmitArgs {
-  const u32 *ordPos, *ordJ;  // k_emit_order: processing index -> (position, record index in the DownTrack)
   const u32 *perm;      // output position -> DownTrack (track-major order)
   const u64 *recBase;   // [position] exclusive scan of forwarded counts
   const u64 *byteBase;  // [position] exclusive scan of output bytes
@@ -2617,7 +2537,6 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
   __shared__ u32 sCs[EMIT_G];   // first chunk of the record, relative to the group
   __shared__ u32 sLen[EMIT_G];
   __shared__ u32 sPre[EMIT_G];  // prefix length | (LDS region length << 16)
-  __shared__ u64 sOut[EMIT_G];  // output arena offset of the record
   const u32 lane = threadIdx.x;
   const u64 total = A.totals[0];
   const u64 ngroups = (total + EMIT_G - 1) / EMIT_G;
@@ -2627,10 +2546,10 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
   }
   // XCD-aware partition: workgroups are dispatched round-robin over the 8
   // XCDs, so blockIdx % 8 names the XCD.  Each XCD walks its own contiguous
-  // eighth of the (track-major, packet-major within a track) sequence in
-  // order: the copies of one packet are adjacent, so its payload is read from
-  // HBM once and hits that XCD's L2 for the other copies.  (Falls back to a
-  // plain grid-stride when the grid is not a multiple of 8.)
+  // eighth of the (track-major) output in order: the records that re-read a
+  // track's payloads (one per subscribing DownTrack) are adjacent, so the
+  // re-reads hit that XCD's 4 MiB L2 instead of going to HBM.  (Falls back to
+  // a plain grid-stride when the grid is not a multiple of 8.)
   const u32 nx = (gridDim.x % 8 == 0) ? 8u : 1u;
   const u32 xcd = blockIdx.x % nx, slotInX = blockIdx.x / nx, perX = gridDim.x / nx;
   const u64 gpx = (ngroups + nx - 1) / nx;
@@ -2639,15 +2558,25 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
     const u64 r0 = g * EMIT_G;
     const u32 nrec = u32(min(u64(EMIT_G), total - r0));
     // ---- prefix phase: lane = record
-    u32 nch = 0;  // the record's 16-B chunks
+    const u32 pLo = A.gFirst[g];
+    const u32 pHi = (g + 1 < ngroups) ? A.gFirst[g + 1] + 1 : A.ndts;
+    u64 outOff = 0;
     if (lane < nrec) {
-      const u32 pos = A.ordPos[r0 + lane], jr = A.ordJ[r0 + lane];
-      const u32 d = A.perm[pos];
-      const u64 r = A.recBase[pos] + jr;  // output record index
-      const Tuple t = A.tuples[A.slotBase[d] + jr];
+      const u64 r = r0 + lane;
+      // position owning record r: last p in [pLo, pHi) with recBase[p] <= r
+      u32 lo = pLo, hi = pHi;
+      while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (A.recBase[mid] <= r)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      const u32 d = A.perm[lo];
+      const Tuple t = A.tuples[A.slotBase[d] + (r - A.recBase[lo])];
       const PktV p = load_pkt(A.pkts + t.pkt);
       const DevDT dt = A.dts[d];
-      const u64 outOff = A.byteBase[pos] + t.relOff;
+      outOff = A.byteBase[lo] + t.relOff;
       lkf_out o;
       o.ext_sn = t.extSN;
       o.ext_ts = t.extTS;
@@ -2757,15 +2686,14 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       sSrc[lane] = src;
       sLen[lane] = t.outLen;
       sPre[lane] = u32(n) | (u32(R) << 16);
-      sOut[lane] = outOff;
-      nch = (u32(t.outLen) + 15) >> 4;
     }
-    // first chunk of each record in the group's sweep
-    const u32 cs = excl_scan_u32(nch, lane);
-    if (lane < nrec) sCs[lane] = cs;
-    const u32 nchunks = rl32(cs + nch, nrec - 1);
+    // first chunk of each record relative to the group's first output byte
+    const u64 gByte = rl64(outOff, 0);
+    if (lane < nrec) sCs[lane] = u32((outOff - gByte) >> 4);
     __syncthreads();  // one wave: orders the LDS writes above before the cross-lane reads below
-    // ---- copy phase: one sweep over the group's 16-B chunks
+    // ---- copy phase: flat sweep of the group's 16-B chunks
+    const u32 nchunks = sCs[nrec - 1] + ((sLen[nrec - 1] + 15) >> 4);
+    u8 *const outG = A.outArena + gByte;
     u32 cur = 0;  // wave-uniform: a record whose first chunk is <= c0
     for (u32 c0 = 0; c0 < nchunks;) {
       u32 wEnd = min(c0 + EMIT_U * 64, nchunks);
@@ -2823,7 +2751,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
             v.w &= keep_mask(keep - 12);
           }
         }
-        store16(A.outArena + sOut[j[u]] + o[u], v);
+        store16(outG + (u64(c[u]) << 4), v);
       }
       cur += k;
       c0 = wEnd;
@@ -3128,17 +3056,8 @@ hipError_t launch_layer_index(hipStream_t s, const lkf_pkt *pkts, const u32 *tBe
   return hipGetLastError();
 }
 
-hipError_t launch_emit_order(hipStream_t s, const EmitLaunch &a, const u32 *trackPos, u32 ntracks) {
-  if (!ntracks) return hipSuccess;
-  hipLaunchKernelGGL(k_emit_order, dim3(ntracks), dim3(ORD_T), 0, s, trackPos, a.ndts, a.perm, a.recBase, a.totals,
-                     a.slotBase, a.tuples, a.tBegin, a.tEnd, const_cast<u32 *>(a.ordPos), const_cast<u32 *>(a.ordJ));
-  return hipGetLastError();
-}
-
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   EmitArgs A;
-  A.ordPos = a.ordPos;
-  A.ordJ = a.ordJ;
   A.perm = a.perm;
   A.recBase = a.recBase;
   A.byteBase = a.byteBase;

@@ -44,8 +44,6 @@ struct DecideLaunch {
 };
 
 struct EmitLaunch {
-  const uint32_t *ordPos, *ordJ;  // k_emit_order output (processing order)
-  const uint32_t *tBegin, *tEnd;  // the batch's per-track packet ranges
   const uint32_t *perm;  // output position -> DownTrack
   const uint64_t *recBase, *byteBase, *slotBase, *totals;  // recBase/byteBase by position
   const uint32_t *gFirst;  // [group] position owning record 64*group (k_scan_down mode 1)
@@ -112,8 +110,6 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_layer_index(hipStream_t s, const lkf_pkt *pkts, const uint32_t *tBegin, const uint32_t *tEnd,
                               uint32_t ntracks, uint32_t stride, uint32_t *list, uint32_t *before, uint32_t *cnt);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
-// packet-major record order per track (trackPos: first output position of each track, ntracks + 1)
-hipError_t launch_emit_order(hipStream_t s, const EmitLaunch &a, const uint32_t *trackPos, uint32_t ntracks);
 hipError_t launch_dd_decode(hipStream_t s, const lkf_pkt *pkts, const lkf_pkt_dd *dds, const uint8_t *arena,
                             const uint32_t *tBegin, const uint32_t *tEnd, const DevTrack *tracks, uint32_t ntracks,
                             DDStruct *structs, DDTrack *ddTracks, DDPkt *out, uint32_t *err);

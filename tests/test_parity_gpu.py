@@ -282,3 +282,4 @@ def test_overflow_error_is_sticky(pkg, workload, abi):
         assert eng.lib.lkf_sync(eng.h) == 0
     finally:
         eng.close()
+
