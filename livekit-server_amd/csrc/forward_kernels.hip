@@ -1647,6 +1647,9 @@ __device__ __forceinline__ void pin_loaded(const uint4 &a, const uint4 &b, const
                "v"(c.y), "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
 }
 
+#ifndef LKF_GAP_RUN
+#define LKF_GAP_RUN 1  // loss gaps anywhere in a run (0: only as the run's first candidate; A/B)
+#endif
 #ifndef LKF_OOO_RUN
 #define LKF_OOO_RUN 0  // 1: out-of-order packets decided in the run (A/B: slower, register pressure)
 #endif
@@ -1726,7 +1729,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const u64 wc0 = __builtin_amdgcn_s_memtime();
   u32 wtSerial = 0, wtChunks = 0;
   u64 wcStep = 0, wcDrain = 0, wcPro = 0;
-  u32 wtWhy[4] = {}, wtRuns = 0;
+  u32 wtWhy[4] = {}, wtRuns = 0, wtRunEnd[5] = {};
 #endif
 #if LKF_DIAG
   const u64 tP1 = clock64() + u64(__builtin_amdgcn_readfirstlane(d) & 0);  // after round 1
@@ -1949,8 +1952,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       // pictures vp8.go:218-255, skipped sequencer slots sequencer.go:179-189)
       // are applied before the run, from the state at the run start.
       const u64 dEsn = p.esn - prevEsn;
-      const bool gapLane = candIn && pc < 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
-                           p.ssrc == L.h.lastSSRC;
+      const bool gapLane = candIn && (LKF_GAP_RUN || pc < 0) && dEsn > 1 && dEsn < u64(L.seqSize) - 64 &&
+                           p.plen != 0 && p.ssrc == L.h.lastSSRC;
       bool ok = candIn && (dEsn == 1 || gapLane) && p.plen != 0 && p.ssrc == L.h.lastSSRC;
       bool okO = LKF_OOO_RUN && oooL;  // out-of-order lane decided in the run (refined below)
       // a gap behind other candidates ends this run and starts the next one
@@ -1970,8 +1973,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       int whyVid = 0;
 #endif
       u64 tswM = 0;  // candidate lanes at a temporal switch point (the first ends the run)
-      bool gapExempt = false;
-      i32 gapExt = 0;
+      bool overT = false;
       if (video) {
         i32 mp = prevExt;
         if (mp > 0) mp = prevM ? (prevExt & 0x7fff) : (prevExt & 0x7f);
@@ -1983,16 +1985,18 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
                          (cT < gT ? (i32(p.tid) > cT && i32(p.tid) <= gT && (p.vbits & LKF_VP8_S) &&
                                      (p.vbits & LKF_VP8_Y))
                                   : pktMarker);
-        const bool overT = candIn && T && p.tid > u8(cT);
+        overT = candIn && T && p.tid > u8(cT);
         // VP8PictureIdWrapHandler.Unwrap and SelectTemporal run on an
         // out-of-order packet too: a wrap or a temporal switch there is serial
         okO = okO && !wrapBack && !wraps && !tsw;
-        // a gap lane forwards whatever its layer and exempts its picture (vp8.go:249-255)
-        const u64 gapM = __ballot(gapLane);
-        const u32 gl = gapM ? u32(__ffsll((long long)gapM) - 1) : 0u;
-        gapExempt = gapM && rl32(u32(overT), gl) != 0;
-        gapExt = i32(rl32(u32(ext), gl));
-        dropT = overT && !gapLane && !(gapExempt && ext == gapExt);
+        // a gap lane forwards whatever its layer and exempts its picture
+        // (vp8.go:249-255): later lanes of that picture forward too
+        bool exIn = false;
+        for (u64 ge = __ballot(gapLane && overT); ge; ge &= ge - 1) {
+          const u32 k = u32(__ffsll((long long)ge) - 1);
+          exIn = exIn || (lane > k && ext == i32(rl32(u32(ext), k)));
+        }
+        dropT = overT && !gapLane && !exIn;
         if (__ballot(dropT) && L.h.exCount)  // exempted pictures forward (vp8.go:270)
           dropT = dropT && !set_has(L.exKey, L.h.exHead, L.h.exCount, ext);
         // A temporal switch point is decided in the run and ends it: up, the
@@ -2081,9 +2085,11 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       // sequencer highest TS = max over pushes; runs keep TS non-decreasing so it is the last one
       const bool tsMono = ots >= hiTS;
       // the first push of a run may skip slots (a gap lane: osn - highest < size - 64)
+      // the sequencer slots of a run lie within size - 64 of its highest at the run start
       const bool seqOk = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && cbLen >= 0 && tsMono &&
-                         (osn == prevOsn + 1 || (gapLane && pf < 0 && osn - prevOsn > 1 &&
-                                                 osn - prevOsn < u64(L.seqSize) - 64));
+                         (osn == prevOsn + 1 || (gapLane && (LKF_GAP_RUN || pf < 0) && osn - prevOsn > 1 &&
+                                                 osn - prevOsn < u64(L.seqSize) - 64)) &&
+                         osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
       // an out-of-order push fills a past slot and moves neither highest SN nor TS
       const bool seqOkO = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && cbLen >= 0 && ots <= hiTS &&
                           i64(osn - prevOsn) < 0;
@@ -2112,6 +2118,15 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       DIAG(2, x > pos ? 1 : 0);
 #if LKF_WTIME
       wtRuns += x > pos ? 1 : 0;
+      {  // what ends this run: chunk end, control op, temporal switch, later gap, full step
+        int re;
+        if (x >= n) re = 0;
+        else if (rl32(pi, x) >= nextAt) re = 1;
+        else if (x > pos && ((tswM >> (x - 1)) & 1)) re = 2;
+        else if (rl32(u32(gapLater), x)) re = 3;
+        else re = 4;
+        wtRunEnd[re]++;
+      }
 #endif
 #if LKF_DIAG
       const u64 tb0 = clock64();
@@ -2133,18 +2148,33 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         o.drops[LKF_DROP_NOT_SELECTED] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_NOT_SELECTED)));
         o.drops[LKF_DROP_DOWNGRADE] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_DOWNGRADE)));
         o.drops[LKF_DROP_TEMPORAL] += u32(__popcll(tdR));
-        // first push of the run: slot distance from the sequencer's highest
-        u32 gOff = 1;
-        if (fwInR) {
-          const u32 firstF = u32(__ffsll((long long)fwInR) - 1);
-          gOff = u32(rl64(osn, firstF) - L.h.seqExtHighestSN);
-          const u64 gR = __ballot(gapLane && inRun);
-          if (gR) {  // the run starts after a loss gap (the gap lane is forwarded)
-            if (video) {
-              vp8_record_missing(L, L.h.wrMaxPictureId, gapExt, L.h.pictureIdOffset);
-              if (gapExempt) set_add(L.exKey, L.h.exHead, L.h.exCount, gapExt, kExemptKeep);
+        // Gap lanes (forwarded after a loss) and picture drops, in lane order:
+        // the missing pictures a gap records skip the pictures dropped so far
+        // (vp8.go:218-247), a gap exempts its own picture (:249-255), and the
+        // sequencer slots it skips are invalidated (sequencer.go:179-189).
+        // Sequencer slots are the run-start highest slot + (osn - highest SN).
+        const u64 pdR = video ? __ballot(picDrop && inRun) : 0ull;
+        const u64 gR = __ballot(gapLane && inRun);
+        if (gR) {
+          for (u64 m = gR | pdR; m; m &= m - 1) {
+            const u32 b = u32(__ffsll((long long)m) - 1);
+            const i32 eb = i32(rl32(u32(ext), b));
+            if ((pdR >> b) & 1) {
+              set_add(L.dropKey, L.h.dropHead, L.h.dropCount, eb, kDropKeep);
+              continue;
             }
-            if (gOff > 1) seq_invalidate(L, gOff - 1);  // stores only: no drain needed
+            if (video) {
+              vp8_record_missing(L, i32(rl32(u32(prevExt), b)), eb, i32(rl32(u32(picOff), b)));
+              if (rl32(u32(overT), b)) set_add(L.exKey, L.h.exHead, L.h.exCount, eb, kExemptKeep);
+            }
+            const u64 from = rl64(prevOsn, b), to = rl64(osn, b);  // slots of (from, to) skipped
+            const u32 n = u32(to - from - 1);
+            u32 base = u32(L.h.seqHighSlot) + u32(from - L.h.seqExtHighestSN) + 1;
+            for (u32 i = lane; i < n; i += 64) {  // stores only: no drain needed
+              u32 x2 = base + i;
+              while (x2 >= L.seqSize) x2 -= L.seqSize;
+              store_rec(L.seq + x2, SeqMeta{});
+            }
           }
         }
         // output records + sequencer slots of the forwarded lanes
@@ -2160,7 +2190,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const u32 relEx = excl_scan_u32(aligned, lane);
         const bool marker = pktMarker;  // tp.marker (= hdr.Marker for video, false for audio) || hdr.Marker
         const u32 j = u32(__popcll(fwR & lt));
-        const u32 jIn = u32(__popcll(fwInR & lt));
         if (fwd) {
           Tuple t;
           t.extSN = osn;
@@ -2188,9 +2217,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           u32 slot;
           bool store = true;
           if (!oooL) {
-            slot = u32(L.h.seqHighSlot) + gOff + jIn;
+            slot = u32(L.h.seqHighSlot) + u32(osn - L.h.seqExtHighestSN);
           } else {
-            const u32 hs = jIn ? u32(L.h.seqHighSlot) + gOff - 1 + jIn : u32(L.h.seqHighSlot);
+            const u32 hs = u32(L.h.seqHighSlot) + u32(prevOsn - L.h.seqExtHighestSN);
             const i64 delta = i64(osn - prevOsn);
             store = delta > -i64(L.seqSize) && osn >= L.h.seqExtStartSN;
             slot = hs + u32(i64(L.seqSize) + delta);
@@ -2218,8 +2247,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         }
         if (fwInR) {
           const u32 lastF = 63 - __clzll(fwInR);
-          const u32 nF = u32(__popcll(fwInR));
-          u32 slot = u32(L.h.seqHighSlot) + gOff - 1 + nF;
+          u32 slot = u32(L.h.seqHighSlot) + u32(rl64(osn, lastF) - L.h.seqExtHighestSN);
           while (slot >= L.seqSize) slot -= L.seqSize;
           L.h.seqHighSlot = u16(slot);
           L.h.seqExtHighestSN = rl64(osn, lastF);
@@ -2289,9 +2317,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
               L.h.prevT = L.h.curT;
               L.h.curT = nxt;
             }
-            u64 pd = __ballot(picDrop && inRun);
+            u64 pd = pdR;
             L.h.pictureIdOffset += i32(__popcll(pd));
-            while (pd) {
+            while (pd && !gR) {  // (with gap lanes the drops went into the set in lane order above)
               const u32 b = u32(__ffsll((long long)pd) - 1);
               set_add(L.dropKey, L.h.dropHead, L.h.dropCount, i32(rl32(u32(ext), b)), kDropKeep);
               pd &= pd - 1;
@@ -2383,8 +2411,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     g[8] = wtRuns;
     for (int i = 0; i < 4; i++) g[9 + i] = wtWhy[i];
     g[13] = u32(L.h.curS) | (u32(L.h.tgtS) << 8) | (u32(L.h.curT) << 16) | (u32(L.h.tgtT) << 24);
-    g[14] = L.h.flags;
-    g[15] = d;
+    g[14] = wtRunEnd[0] | (wtRunEnd[1] << 8) | (wtRunEnd[2] << 16) | (wtRunEnd[3] << 24);
+    g[15] = wtRunEnd[4];
   }
 #endif
 #if LKF_DIAG

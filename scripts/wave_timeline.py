@@ -82,10 +82,14 @@ def main():
     for i in top:
         lay = a[i, 13]
         print("  long wave: life %.1f us pk %d serial %d (reorder %d kf %d ssrc/pad %d other %d) runs %d chunks %d "
-              "pro %d step %d tot %d  S %d->%d T %d->%d flags %x dt %d" % (
+              "pro %d step %d tot %d  S %d->%d T %d->%d" % (
                   life[i] / 1e3, pk[i], ser[i], a[i, 9], a[i, 10], a[i, 11], a[i, 12], a[i, 8], ch[i], pro[i],
                   stp[i], tot[i], np.int8(lay & 255), np.int8((lay >> 8) & 255), np.int8((lay >> 16) & 255),
-                  np.int8((lay >> 24) & 255), a[i, 14], a[i, 15]))
+                  np.int8((lay >> 24) & 255)))
+    re = a[:, 14]
+    ends = [(re & 255).sum(), ((re >> 8) & 255).sum(), ((re >> 16) & 255).sum(), ((re >> 24) & 255).sum(),
+            a[:, 15].sum()]
+    print("run ends: chunk end %d, control op %d, temporal switch %d, later gap %d, full step %d" % tuple(ends))
     print("runs per wave %.2f; serial reasons: reorder %d kf %d ssrc/pad %d other %d" % (
         a[:, 8].mean(), a[:, 9].sum(), a[:, 10].sum(), a[:, 11].sum(), a[:, 12].sum()))
     nonrun = tot - stp - drn - pro
