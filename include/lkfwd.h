@@ -424,6 +424,40 @@ typedef struct lkf_seq_meta {
 int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns,
                    lkf_seq_meta *out, uint32_t *n_out);
 
+/* ---- NACK -> RTX (DownTrack.retransmitPackets downtrack.go:1596-1712) --- */
+typedef struct lkf_nack {
+  int32_t dt;       /* DownTrack handle */
+  uint16_t sn;      /* NACKed (munged, outgoing) sequence number */
+  uint16_t reserved;
+} lkf_nack;
+typedef struct lkf_rtx {
+  lkf_seq_meta meta; /* the sequencer record to retransmit (getExtPacketMetas) */
+  int32_t dt;
+  uint32_t reserved;
+} lkf_rtx;
+/* Every DownTrack's NACK list in one call (nacks grouped by DownTrack, each
+ * list in NACK order; LKF_EORDER otherwise): Forwarder.FilterRTX
+ * (forwarder.go:1406-1434, FlagFilterRTX off / FlagFilterRTXLayers on: a
+ * deficient DownTrack retransmits nothing while its target is below its
+ * current layer, and nothing above its current layer),
+ * sequencer.getExtPacketMetas (sequencer.go:263-332; bumps each record's NACK
+ * count and time), then the disallowed layers are skipped.  The records are
+ * what the host reads from the receiver's bucket (Receiver.ReadRTP(layer,
+ * source_sn)).  Waits for queued runs. */
+int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now_ns, lkf_rtx *out, uint32_t cap,
+                   uint32_t *n_out);
+/* The retransmissions (downtrack.go:1640-1698): src[i] locates record i's
+ * source packet (the bucket's raw RTP bytes) in src_arena (len 0: the read
+ * failed, no packet); the header gets the sequencer's marker/SN/TS and the
+ * DownTrack's SSRC and payload type, a VP8 payload its stored munged
+ * descriptor (translateVP8PacketTo), and the pacer's extension block
+ * (abs-send-time placeholder; the DD element is not kept by this sequencer, so
+ * RTX of a DownTrack with the DD extension carries none).  Output as lkf_out
+ * records (pkt = index of the lkf_rtx) + 16-B aligned wire packets. */
+int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
+                 uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
+                 uint64_t *out_len);
+
 /* ---- ingress ------------------------------------------------------------ */
 /* Adds one received stream (NewBuffer + Bind, buffer.go:124-215). */
 int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p);

@@ -92,6 +92,13 @@ SPEAKER_DTYPE = np.dtype([("room", "<u4"), ("participant", "<u4"), ("level", "<f
 DT_SUMMARY_DTYPE = np.dtype([("dt", "<i4"), ("subscriber", "<u4"), ("room", "<u4"), ("flags", "<u4"),
                              ("packets_sent", "<u8"), ("bytes_sent", "<u8")])
 assert DT_SUMMARY_DTYPE.itemsize == 32
+# NACK -> RTX (lkf_nack / lkf_rtx)
+NACK_DTYPE = np.dtype([("dt", "<i4"), ("sn", "<u2"), ("reserved", "<u2")])
+assert NACK_DTYPE.itemsize == 8
+RTX_DTYPE = np.dtype([("ext_sn", "<u8"), ("ext_ts", "<u8"), ("source_sn", "<u2"), ("target_sn", "<u2"),
+                      ("timestamp", "<u4"), ("last_nack", "<u4"), ("marker", "u1"), ("nacked", "u1"), ("layer", "i1"),
+                      ("codec_len", "u1"), ("codec", "u1", 8), ("dt", "<i4"), ("reserved", "<u4")])
+assert RTX_DTYPE.itemsize == 48
 DTS_ACTIVE = 0x1
 DTS_DEFICIENT = 0x2
 
@@ -330,6 +337,11 @@ def bind_engine_api(lib, prefix):
     api["speakers"] = _bind(lib, prefix + "speakers", C.c_int, [e, C.c_int64, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["downtrack_summaries"] = _bind(lib, prefix + "downtrack_summaries", C.c_int,
                                        [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
+    api["rtx_lookup"] = _bind(lib, prefix + "rtx_lookup", C.c_int,
+                              [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_uint32, P(C.c_uint32)])
+    api["rtx_emit"] = _bind(lib, prefix + "rtx_emit", C.c_int,
+                            [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                             C.c_uint64, P(C.c_uint32), P(C.c_uint64)])
     return api
 
 

@@ -182,6 +182,17 @@ struct lkf_engine {
   uint64_t nRuns = 0;
   int lastCtx = -1;
 
+  // NACK -> RTX scratch (grown on demand)
+  lkf_nack *dNacks = nullptr;
+  uint32_t *dNackG = nullptr, *dNackValid = nullptr;
+  lkf_rtx *dRtx = nullptr;
+  uint32_t rtxCap = 0;
+  lkf_raw_pkt *dRtxSrc = nullptr;
+  uint32_t *dRtxLen = nullptr;
+  uint64_t *dRtxOff = nullptr;
+  uint8_t *dRtxIn = nullptr, *dRtxOut = nullptr;
+  uint64_t rtxInCap = 0, rtxOutCap = 0;
+
   // seq lookup scratch
   uint16_t *dSns = nullptr;
   lkf_seq_meta *dSeqOut = nullptr;
@@ -206,6 +217,7 @@ struct lkf_engine {
   uint32_t *dFwdFlag = nullptr;
   uint64_t *dPos = nullptr, *dIPartA = nullptr, *dIPartB = nullptr, *dITotal = nullptr;
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
+  uint32_t *dIList = nullptr, *dIListCnt = nullptr;  // per-stream datagram lists (k_ing_lists)
   uint32_t lastIngestN = 0;
   // speaker ranking tables (rebuilt when topology changes)
   uint32_t nRooms = 0;
@@ -492,6 +504,8 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dITEnd, c.max_tracks));
   A(dalloc(&e->dITRuns, c.max_tracks));
   A(dalloc(&e->dIErr, 4));
+  A(dalloc(&e->dIList, 3 * size_t(c.max_batch_pkts) + 64));
+  A(dalloc(&e->dIListCnt, 3 * size_t(c.max_tracks)));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
     A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
@@ -536,10 +550,14 @@ void lkf_destroy(lkf_engine *e) {
   if (e->prepS) (void)hipStreamSynchronize(e->prepS);
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
+  for (void *p : {static_cast<void *>(e->dNacks), static_cast<void *>(e->dNackG), static_cast<void *>(e->dNackValid),
+                  static_cast<void *>(e->dRtx), static_cast<void *>(e->dRtxSrc), static_cast<void *>(e->dRtxLen),
+                  static_cast<void *>(e->dRtxOff), static_cast<void *>(e->dRtxIn), static_cast<void *>(e->dRtxOut)})
+    if (p) (void)hipFree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
-                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr,
+                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts};
   for (void *p : ptrs)
@@ -1265,6 +1283,156 @@ int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, i
   return LKF_OK;
 }
 
+static int rtx_reserve(lkf_engine *e, uint32_t n) {
+  if (n <= e->rtxCap) return LKF_OK;
+  for (void *p : {static_cast<void *>(e->dNacks), static_cast<void *>(e->dNackG), static_cast<void *>(e->dNackValid),
+                  static_cast<void *>(e->dRtx), static_cast<void *>(e->dRtxSrc), static_cast<void *>(e->dRtxLen),
+                  static_cast<void *>(e->dRtxOff)})
+    if (p) (void)hipFree(p);
+  e->rtxCap = std::max<uint32_t>(n, 1024);
+  HIPCHK(dalloc(&e->dNacks, e->rtxCap), "alloc nacks");
+  HIPCHK(dalloc(&e->dNackG, e->rtxCap + 1), "alloc nack groups");
+  HIPCHK(dalloc(&e->dNackValid, e->rtxCap), "alloc nack valid");
+  HIPCHK(dalloc(&e->dRtx, e->rtxCap), "alloc rtx");
+  HIPCHK(dalloc(&e->dRtxSrc, e->rtxCap), "alloc rtx src");
+  HIPCHK(dalloc(&e->dRtxLen, e->rtxCap), "alloc rtx len");
+  HIPCHK(dalloc(&e->dRtxOff, e->rtxCap), "alloc rtx off");
+  return LKF_OK;
+}
+
+int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now_ns, lkf_rtx *out, uint32_t cap,
+                   uint32_t *n_out) {
+  if (!e || !n_out || (n && !nacks)) return LKF_EINVAL;
+  *n_out = 0;
+  // groups: one per DownTrack's contiguous NACK list (a DownTrack must not reappear)
+  std::vector<uint32_t> gStart;
+  std::vector<uint8_t> seen(e->dtp.size(), 0);
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t dt = nacks[i].dt;
+    if (dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+    if (i == 0 || nacks[i - 1].dt != dt) {
+      if (seen[dt]) return LKF_EORDER;
+      seen[dt] = 1;
+      if (e->active[dt]) gStart.push_back(i);  // a removed DownTrack answers no NACK
+    }
+  }
+  if (gStart.empty()) return LKF_OK;
+  // group ends: the next group's start or the end of its DownTrack's run
+  std::vector<uint32_t> gb(gStart.size() + 1);
+  std::vector<lkf_nack> packed;
+  packed.reserve(n);
+  for (size_t g = 0; g < gStart.size(); g++) {
+    gb[g] = uint32_t(packed.size());
+    uint32_t i = gStart[g];
+    const int32_t dt = nacks[i].dt;
+    while (i < n && nacks[i].dt == dt) packed.push_back(nacks[i++]);
+  }
+  gb[gStart.size()] = uint32_t(packed.size());
+  const uint32_t m = uint32_t(packed.size());
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  rc = rtx_reserve(e, m);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(e->dNacks, packed.data(), m * sizeof(lkf_nack), hipMemcpyHostToDevice), "nacks copy");
+  HIPCHK(hipMemcpy(e->dNackG, gb.data(), gb.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "groups copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_rtx_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, e->dNacks, e->dNackG,
+                           uint32_t(gStart.size()), now_ns / 1000000, e->dRtx, e->dNackValid),
+         "rtx lookup");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  std::vector<lkf_rtx> r(m);
+  std::vector<uint32_t> v(m);
+  HIPCHK(hipMemcpy(r.data(), e->dRtx, m * sizeof(lkf_rtx), hipMemcpyDeviceToHost), "rtx copy");
+  HIPCHK(hipMemcpy(v.data(), e->dNackValid, m * sizeof(uint32_t), hipMemcpyDeviceToHost), "valid copy");
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < m; i++) k += v[i];
+  *n_out = k;
+  if (cap < k) return LKF_ENOSPC;
+  k = 0;
+  for (uint32_t i = 0; i < m; i++)
+    if (v[i]) out[k++] = r[i];
+  return LKF_OK;
+}
+
+int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
+                 uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
+                 uint64_t *out_len) {
+  if (!e || !n_out || !out_len || (n && (!rtx || !src))) return LKF_EINVAL;
+  *n_out = 0;
+  *out_len = 0;
+  if (!n) return LKF_OK;
+  for (uint32_t i = 0; i < n; i++) {
+    if (rtx[i].dt < 0 || rtx[i].dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+    if (src[i].len && (!src_arena || uint64_t(src[i].off) + src[i].len > src_len)) return LKF_EINVAL;
+  }
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  rc = rtx_reserve(e, n);
+  if (rc) return rc;
+  if (src_len + 64 > e->rtxInCap) {
+    if (e->dRtxIn) (void)hipFree(e->dRtxIn);
+    e->rtxInCap = std::max<uint64_t>(src_len + 64, 1 << 20);
+    HIPCHK(dalloc(&e->dRtxIn, e->rtxInCap), "alloc rtx in");
+  }
+  HIPCHK(hipMemcpy(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice), "rtx copy");
+  HIPCHK(hipMemcpy(e->dRtxSrc, src, n * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice), "src copy");
+  if (src_len) HIPCHK(hipMemcpy(e->dRtxIn, src_arena, src_len, hipMemcpyHostToDevice), "src arena copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_rtx_emit(e->own, false, n, e->dRtx, e->dRtxSrc, e->dRtxIn, e->dDTs, e->dTracks, e->dRtxLen, nullptr,
+                         nullptr),
+         "rtx size");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  std::vector<uint32_t> len(n);
+  HIPCHK(hipMemcpy(len.data(), e->dRtxLen, n * sizeof(uint32_t), hipMemcpyDeviceToHost), "len copy");
+  std::vector<uint64_t> off(n, 0);
+  uint64_t tot = 0;
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    off[i] = tot;
+    if (len[i]) {
+      tot += (uint64_t(len[i]) + 15) & ~uint64_t(15);
+      k++;
+    }
+  }
+  *n_out = k;
+  *out_len = tot;
+  if (tot > out_cap || (k && (!out || !out_arena))) return LKF_ENOSPC;
+  if (tot + 64 > e->rtxOutCap) {
+    if (e->dRtxOut) (void)hipFree(e->dRtxOut);
+    e->rtxOutCap = std::max<uint64_t>(tot + 64, 1 << 20);
+    HIPCHK(dalloc(&e->dRtxOut, e->rtxOutCap), "alloc rtx out");
+  }
+  HIPCHK(hipMemcpy(e->dRtxOff, off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice), "off copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_rtx_emit(e->own, true, n, e->dRtx, e->dRtxSrc, e->dRtxIn, e->dDTs, e->dTracks, e->dRtxLen, e->dRtxOff,
+                         e->dRtxOut),
+         "rtx write");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  if (tot) HIPCHK(hipMemcpy(out_arena, e->dRtxOut, tot, hipMemcpyDeviceToHost), "rtx bytes copy");
+  k = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (!len[i]) continue;
+    lkf_out &o = out[k++];
+    std::memset(&o, 0, sizeof(o));
+    o.ext_sn = rtx[i].meta.ext_sn;
+    o.ext_ts = rtx[i].meta.ext_ts;
+    o.out_off = off[i];
+    o.dt = uint32_t(rtx[i].dt);
+    o.pkt = i;
+    o.out_len = uint16_t(len[i]);
+    o.flags = rtx[i].meta.marker ? LKF_OUT_MARKER : 0;
+    o.layer = rtx[i].meta.layer;
+  }
+  return LKF_OK;
+}
+
 int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *total_ms) {
   return lkf_timing_window(e, 1, decide_ms, emit_ms, total_ms);
 }
@@ -1362,6 +1530,9 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.partB = e->dIPartB;
   a.total = e->dITotal;
   a.out = x.dPktsOwn;
+  a.list = e->dIList;
+  a.listCnt = e->dIListCnt;
+  a.listStride = e->cfg.max_batch_pkts;
   const bool dd = e->nDDStreams != 0;
   a.ddStates = dd ? e->dDDIng : nullptr;
   a.ddStructs = dd ? e->dDDIngStruct : nullptr;

@@ -2840,6 +2840,78 @@ __global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u32 d, c
   *nOut = cnt;
 }
 
+// ---------------------------------------------------------------------------
+// k_rtx_lookup: DownTrack.retransmitPackets up to Receiver.ReadRTP
+// (downtrack.go:1596-1631) for many DownTracks at once — one lane per
+// DownTrack NACK list (serial over it, as getExtPacketMetas mutates the
+// records it returns).  FilterRTX layers (forwarder.go:1424-1432) from the
+// DownTrack's state; out[k]/valid[k] per NACK entry (compacted on the host).
+// ---------------------------------------------------------------------------
+__global__ void k_rtx_lookup(const DTHot *__restrict__ hot, SeqMeta *seqBase, u32 seqSize,
+                             const lkf_nack *__restrict__ nacks, const u32 *__restrict__ gStart, u32 ngroups, i64 nowMs,
+                             lkf_rtx *__restrict__ out, u32 *__restrict__ valid) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  const u32 b = gStart[g], e = gStart[g + 1];
+  const u32 d = u32(nacks[b].dt);
+  const DTHot h = hot[d];
+  SeqMeta *seq = seqBase + size_t(d) * seqSize;
+  // FlagFilterRTXLayers: disallowed while deficient and target < current, or above current
+  const bool def = h.flags & F_DEFICIENT;
+  const i32 curS = h.curS, tgtS = h.tgtS;
+  const u32 rtt = 70;  // defaultRtt (setRTT is out of scope)
+  const u32 refTime = u32(nowMs - h.seqStartMs);
+  const u16 highestSN = u16(h.seqExtHighestSN);
+  const u32 highestTS = u32(h.seqExtHighestTS);
+  for (u32 k = b; k < e; k++) {
+    u32 ok = 0;
+    const u16 sn = nacks[k].sn;
+    if ((h.flags & F_SEQ_INIT) && u16(highestSN - sn) <= (1 << 15)) {
+      u64 extSN = u64(sn) + (h.seqExtHighestSN & 0xFFFFFFFFFFFF0000ull);
+      if (sn > highestSN) extSN -= (1ull << 16);
+      if (h.seqExtHighestSN - extSN < u64(seqSize)) {
+        SeqMeta &m = seq[extSN % seqSize];
+        const bool invalid = m.sourceSeqNo == 0 && m.targetSeqNo == 0 && m.lastNack == 0;
+        const u32 lim = (2 * rtt < 100) ? 2 * rtt : 100;
+        if (m.targetSeqNo == sn && !invalid && m.nacked < 3 && u32(refTime - m.lastNack) > lim) {
+          m.nacked++;
+          m.lastNack = refTime;
+          const i32 l = m.layer;
+          const bool dis = def && (tgtS < curS || l > curS) && l >= 0 && l <= 2;
+          if (!dis) {
+            u64 extTS = u64(m.timestamp) + (h.seqExtHighestTS & 0xFFFFFFFF00000000ull);
+            if (m.timestamp > highestTS) extTS -= (1ull << 32);
+            lkf_rtx r = {};
+            r.meta.ext_sn = extSN;
+            r.meta.ext_ts = extTS;
+            r.meta.source_sn = m.sourceSeqNo;
+            r.meta.target_sn = m.targetSeqNo;
+            r.meta.timestamp = m.timestamp;
+            r.meta.last_nack = m.lastNack;
+            r.meta.marker = m.marker;
+            r.meta.nacked = m.nacked;
+            r.meta.layer = m.layer;
+            r.meta.codec_len = m.codecLen;
+            for (int q = 0; q < 8; q++) r.meta.codec[q] = m.codec[q];
+            r.dt = int32_t(d);
+            out[k] = r;
+            ok = 1;
+          }
+        }
+      }
+    }
+    valid[k] = ok;
+  }
+}
+
+hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, u32 seqSize, const lkf_nack *nacks,
+                             const u32 *gStart, u32 ngroups, i64 nowMs, lkf_rtx *out, u32 *valid) {
+  if (!ngroups) return hipSuccess;
+  hipLaunchKernelGGL(k_rtx_lookup, dim3((ngroups + 63) / 64), dim3(64), 0, s, hot, seq, seqSize, nacks, gStart, ngroups,
+                     nowMs, out, valid);
+  return hipGetLastError();
+}
+
 // per-batch counters -> cumulative (stats[3] := arena bytes from the out scan)
 // stats[0..kStatWords) = sum of the kStatCopies partial copies that follow it
 __global__ void __launch_bounds__(256) k_stats_reduce(u64 *stats) {

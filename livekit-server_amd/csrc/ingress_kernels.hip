@@ -496,19 +496,30 @@ __device__ __forceinline__ WAResult wa32_update(StreamHot &h, u32 val) {
   return r;
 }
 
-__device__ __forceinline__ bool hist_isset(const u64 *hist, u64 v) {
-  return (hist[(v >> 6) & (kHistWords - 1)] >> (v & 63)) & 1;
+#ifndef LKF_ING_HOT_LDS
+#define LKF_ING_HOT_LDS 0
+#endif
+// RTPStatsReceiver history (cHistorySize 4096 bits, rtpstats_receiver.go:30),
+// staged in LDS for the ingest: word w of a lane's history at h[w * kHL]
+// (word-major, lane-minor)
+constexpr int kHL = 64;
+__device__ __forceinline__ bool hist_isset(const u64 *h, u64 v) {
+  return (h[((v >> 6) & (kHistWords - 1)) * kHL] >> (v & 63)) & 1;
 }
-__device__ __forceinline__ void hist_set(u64 *hist, u64 v) { hist[(v >> 6) & (kHistWords - 1)] |= 1ull << (v & 63); }
-__device__ void hist_clear_range(u64 *hist, u64 lo, u64 hi) {  // inclusive; lo > hi: no-op
+__device__ __forceinline__ void hist_set(u64 *h, u64 v) { h[((v >> 6) & (kHistWords - 1)) * kHL] |= 1ull << (v & 63); }
+__device__ void hist_clear_range(u64 *h, u64 lo, u64 hi) {  // inclusive; lo > hi: no-op
   if (lo > hi) return;
   if (hi - lo + 1 >= u64(kHistWords) * 64) {
-    for (int w = 0; w < kHistWords; w++) hist[w] = 0;
+    for (int w = 0; w < kHistWords; w++) h[w * kHL] = 0;
     return;
   }
-  for (u64 v = lo;; v++) {
-    hist[(v >> 6) & (kHistWords - 1)] &= ~(1ull << (v & 63));
-    if (v == hi) break;
+  for (u64 v = lo;;) {  // a word at a time
+    const u32 b = u32(v & 63);
+    const u64 nb = min(u64(64 - b), hi - v + 1);
+    const u64 m = (nb == 64 ? ~0ull : ((1ull << nb) - 1)) << b;
+    h[((v >> 6) & (kHistWords - 1)) * kHL] &= ~m;
+    if (hi - v + 1 == nb) break;
+    v += nb;
   }
 }
 
@@ -591,6 +602,38 @@ __device__ void level_observe(StreamHot &h, const DevStream &s, u8 level, u32 du
     h.activeDuration = 0;
     h.observedDuration = 0;
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_ing_lists: per track, the datagrams of each of its streams (simulcast
+// layer slot 0-2) in arrival order — the lane of a stream walks its own list
+// instead of scanning the whole track's datagrams.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_ing_lists(const lkf_raw_pkt *__restrict__ raws,
+                                                  const DevStream *__restrict__ streams, u32 nstreams,
+                                                  const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd,
+                                                  u32 stride, u32 *__restrict__ list, u32 *__restrict__ cnt) {
+  const u32 t = blockIdx.x, lane = threadIdx.x;
+  const u64 lt = (1ull << lane) - 1;
+  const u32 b = tBegin[t], e = tEnd[t];
+  u32 c[3] = {0, 0, 0};
+  for (u32 base = b; base < e; base += 64) {
+    const u32 i = base + lane;
+    int l = -1;
+    if (i < e) {
+      const u32 sid = raws[i].stream;
+      if (sid < nstreams) l = int(streams[sid].layer);
+      if (l > 2) l = -1;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const u64 m = __ballot(l == k);
+      if (l == k) list[size_t(k) * stride + b + c[k] + u32(__popcll(m & lt))] = i;
+      c[k] += u32(__popcll(m));
+    }
+  }
+  if (lane == 0)
+    for (int k = 0; k < 3; k++) cnt[t * 3 + k] = c[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -761,24 +804,52 @@ __device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u
 // ---------------------------------------------------------------------------
 // k_ing_stream: one lane per stream, serial over the stream's datagrams.
 // ---------------------------------------------------------------------------
-__global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
+__global__ void __launch_bounds__(64) k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
                              const DevStream *__restrict__ streams, u32 nstreams, StreamHot *__restrict__ hot,
                              u64 *__restrict__ hist, RangeEntry *__restrict__ rings, const u32 *__restrict__ tBegin,
                              const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows, u32 *__restrict__ fwd,
                              const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
-                             IngDD *__restrict__ ingDD, u32 *err) {
+                             IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list,
+                             const u32 *__restrict__ cnt, u32 stride) {
+  __shared__ u64 sHist[kHistWords * kHL];
+#if LKF_ING_HOT_LDS
+  __shared__ StreamHot sHot[kHL];  // the receiver state in LDS
+#endif
   const u32 sid = blockIdx.x * blockDim.x + threadIdx.x;
   if (sid >= nstreams) return;
   const DevStream s = streams[sid];
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;
-  StreamHot h = hot[sid];
-  u64 *hs = hist + size_t(sid) * kHistWords;
+#if LKF_ING_HOT_LDS
+  StreamHot &h = sHot[threadIdx.x];
+  h = hot[sid];
+#else
+  StreamHot h = hot[sid];  // registers (one wave per 64 streams: occupancy is not the limit)
+#endif
+  u64 *const hg = hist + size_t(sid) * kHistWords;
+  u64 *const hs = sHist + threadIdx.x;  // this lane's history in LDS (lanes never share words)
+  for (int w = 0; w < kHistWords; w++) hs[w * kHL] = hg[w];
   RangeEntry *ring = rings + size_t(sid) * kRangeCap;
-  for (u32 i = pb; i < pe; i++) {
-    if (raws[i].stream != sid) continue;
-    const IngParsed p = q[i];
-    const i64 arrival = raws[i].arrival_ns;
+  // this stream's datagrams: its k_ing_lists list (layer slot), else a scan of the track
+  const bool useList = s.layer < 3;
+  const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
+  const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
+  auto idxAt = [&](u32 j) { return useList ? lst[j] : pb + j; };
+  // software pipeline: the next datagram's descriptor loads while this one is decided
+  u32 i = nIdx ? idxAt(0) : 0;
+  IngParsed pn = nIdx ? q[i] : IngParsed{};
+  lkf_raw_pkt rn = nIdx ? raws[i] : lkf_raw_pkt{};
+  for (u32 j = 0; j < nIdx; j++) {
+    const IngParsed p = pn;
+    const lkf_raw_pkt rp = rn;
+    const u32 ic = i;
+    if (j + 1 < nIdx) {
+      i = idxAt(j + 1);
+      pn = q[i];
+      rn = raws[i];
+    }
+    if (rp.stream != sid) continue;
+    const i64 arrival = rp.arrival_ns;
     lkf_flow f = {};
     f.pkt = 0xffffffffu;
     u32 forward = 0;
@@ -880,7 +951,7 @@ __global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngPars
       // getExtPacket (buffer.go:599-671): the dependency descriptor first
       if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
         bool limit = false;
-        if (!dd_ingest(ddStates[s.ddIdx], ddStructs + size_t(s.ddIdx) * 2, raw + raws[i].off + p.ddOff, p.ddLen,
+        if (!dd_ingest(ddStates[s.ddIdx], ddStructs + size_t(s.ddIdx) * 2, raw + rp.off + p.ddOff, p.ddLen,
                        u16(f.ext_sn), dv, limit)) {
           if (limit) atomicOr(err, 4u);
           f.flags |= LKF_FLOW_BAD;
@@ -897,11 +968,12 @@ __global__ void k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngPars
       forward = 1;
       f.flags |= LKF_FLOW_FORWARD;
     } while (false);
-    flows[i] = f;
-    fwd[i] = forward;
-    if (ingDD) ingDD[i] = dv;
+    flows[ic] = f;
+    fwd[ic] = forward;
+    if (ingDD) ingDD[ic] = dv;
   }
   hot[sid] = h;
+  for (int w = 0; w < kHistWords; w++) hg[w] = hs[w * kHL];
 }
 
 // ---------------------------------------------------------------------------
@@ -984,6 +1056,90 @@ __global__ void k_ing_out(const lkf_raw_pkt *__restrict__ raws, const IngParsed 
 }
 
 // ---------------------------------------------------------------------------
+// k_rtx: the retransmission of one NACKed record (downtrack.go:1640-1698), one
+// workgroup per record.  Lane 0 reads the source packet's layout (pion
+// Packet.Unmarshal; VP8 descriptor for the re-munge) and the RTX header
+// (marker/SN/TS from the sequencer, DownTrack SSRC/PT, source CSRCs, the
+// pacer's extension block: abs-send-time placeholder) into LDS; SIZE pass:
+// lens[i] (0 = skipped); WRITE pass: all lanes write the bytes at offs[i].
+// ---------------------------------------------------------------------------
+template <bool WRITE>
+__global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, const lkf_raw_pkt *__restrict__ src,
+                                            const u8 *__restrict__ arena, const DevDT *__restrict__ dts,
+                                            const DevTrack *__restrict__ tracks, u32 *__restrict__ lens,
+                                            const u64 *__restrict__ offs, u8 *__restrict__ out) {
+  __shared__ u8 pre[12 + 60 + 8 + 8];
+  __shared__ u32 sPre, sLen, sPay, sPayLen;
+  const u32 i = blockIdx.x, lane = threadIdx.x;
+  if (lane == 0) {
+    u32 total = 0;
+    const lkf_raw_pkt rp = src[i];
+    const lkf_rtx x = rtx[i];
+    const DevDT dt = dts[x.dt];
+    IngParsed q = {};
+    int lo = -1;
+    const u8 *b = arena + rp.off;
+    if (rp.len && rtp_parse(b, int(rp.len), 0, 0, q, lo)) {
+      u32 pay = q.hdrSize, payLen = q.payloadLen;
+      bool ok = true;
+      int n = 0;
+      const int cc = q.b0 & 0xf;
+      pre[n++] = u8((q.b0 & 0xe0) | (dt.extAbs ? 0x10 : 0) | cc);
+      pre[n++] = u8((x.meta.marker ? 0x80 : 0) | (dt.pt & 0x7f));
+      pre[n++] = u8(x.meta.target_sn >> 8);
+      pre[n++] = u8(x.meta.target_sn);
+      for (int k = 3; k >= 0; k--) pre[n++] = u8(x.meta.timestamp >> (8 * k));
+      for (int k = 3; k >= 0; k--) pre[n++] = u8(dt.ssrc >> (8 * k));
+      for (int k = 0; k < 4 * cc; k++) pre[n++] = b[12 + k];
+      if (dt.extAbs) {  // pion one-byte profile, one 3-byte element
+        pre[n++] = 0xBE;
+        pre[n++] = 0xDE;
+        pre[n++] = 0;
+        pre[n++] = 1;
+        pre[n++] = u8((dt.extAbs << 4) | 2);
+        pre[n++] = 0;
+        pre[n++] = 0;
+        pre[n++] = 0;
+      }
+      if (tracks[dt.track].codec == LKF_CODEC_VP8 && payLen > 0 && x.meta.codec_len) {
+        IngParsed v = {};
+        if (vp8_parse(b + pay, int(payLen), v)) {  // translateVP8PacketTo downtrack.go:1728-1736
+          for (int k = 0; k < x.meta.codec_len; k++) pre[n++] = x.meta.codec[k];
+          pay += v.vhs;
+          payLen -= v.vhs;
+        } else {
+          ok = false;  // "could not unmarshal VP8 packet": skipped
+        }
+      }
+      if (ok) {
+        total = u32(n) + payLen;
+        sPre = u32(n);
+        sPay = rp.off + pay;
+        sPayLen = payLen;
+      }
+    }
+    sLen = total;
+    if (!WRITE) lens[i] = total;
+  }
+  __syncthreads();
+  if (!WRITE || !sLen) return;
+  u8 *o = out + offs[i];
+  const u32 np = sPre, len = sLen, padded = (len + 15) & ~15u;
+  for (u32 k = lane; k < padded; k += 64) o[k] = k < np ? pre[k] : k < len ? arena[sPay + (k - np)] : 0;
+}
+
+hipError_t launch_rtx_emit(hipStream_t s, bool write, u32 n, const lkf_rtx *rtx, const lkf_raw_pkt *src,
+                           const u8 *arena, const DevDT *dts, const DevTrack *tracks, u32 *lens, const u64 *offs,
+                           u8 *out) {
+  if (!n) return hipSuccess;
+  if (write)
+    hipLaunchKernelGGL(k_rtx<true>, dim3(n), dim3(64), 0, s, rtx, src, arena, dts, tracks, lens, offs, out);
+  else
+    hipLaunchKernelGGL(k_rtx<false>, dim3(n), dim3(64), 0, s, rtx, src, arena, dts, tracks, lens, offs, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // k_speakers: wave per room, lane per participant (<= 64 per room).
 // partMics[partOff[r*64 + j] .. ) lists participant j's microphone streams.
 // ---------------------------------------------------------------------------
@@ -1053,9 +1209,11 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
                      a.parsed, a.err);
   hipLaunchKernelGGL(k_ing_ranges, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.parsed, a.n, a.ntracks, a.tBegin, a.tEnd,
                      a.tRuns, a.err);
+  hipLaunchKernelGGL(k_ing_lists, dim3(a.ntracks), dim3(64), 0, st, a.raws, a.streams, a.nstreams, a.tBegin,
+                     a.tEnd, a.listStride, a.list, a.listCnt);
   hipLaunchKernelGGL(k_ing_stream, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a.raws, a.parsed, a.streams,
                      a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates,
-                     a.ddStructs, a.ingDD, a.err);
+                     a.ddStructs, a.ingDD, a.err, a.list, a.listCnt, a.listStride);
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
   if (r != hipSuccess) return r;

@@ -92,6 +92,9 @@ struct IngestLaunch {
   DDStruct *ddStructs;  // two per DD stream
   IngDD *ingDD;         // per datagram
   lkf_pkt_dd *outDD;    // the batch's side array
+  // per-stream datagram lists (k_ing_lists): [layer slot * listStride + tBegin + j], counts [track * 3 + slot]
+  uint32_t *list, *listCnt;
+  uint32_t listStride;
 };
 
 struct SpeakersLaunch {
@@ -122,6 +125,11 @@ hipError_t launch_ev_offsets(hipStream_t s, const uint32_t *laneOf, uint32_t nev
 hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum,
                              const uint32_t *err, uint32_t *sticky);
 hipError_t launch_err_fold(hipStream_t s, const uint32_t *err, uint32_t *sticky, uint32_t shift);
+hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, uint32_t seqSize, const lkf_nack *nacks,
+                             const uint32_t *gStart, uint32_t ngroups, int64_t nowMs, lkf_rtx *out, uint32_t *valid);
+hipError_t launch_rtx_emit(hipStream_t s, bool write, uint32_t n, const lkf_rtx *rtx, const lkf_raw_pkt *src,
+                           const uint8_t *arena, const DevDT *dts, const DevTrack *tracks, uint32_t *lens,
+                           const uint64_t *offs, uint8_t *out);
 hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint32_t d,
                              const uint16_t *sns, uint32_t n, int64_t nowMs, lkf_seq_meta *out, uint32_t *nOut);
 

@@ -509,6 +509,138 @@ int orc_seed_state(orc_engine *e, int32_t dt, const lkf_fwd_state *i) {
   return LKF_OK;
 }
 
+static void epm_to_meta(const ExtPacketMeta &r, lkf_seq_meta &m) {
+  std::memset(&m, 0, sizeof(m));
+  m.ext_sn = r.extSequenceNumber;
+  m.ext_ts = r.extTimestamp;
+  m.source_sn = r.meta.sourceSeqNo;
+  m.target_sn = r.meta.targetSeqNo;
+  m.timestamp = r.meta.timestamp;
+  m.last_nack = r.meta.lastNack;
+  m.marker = r.meta.marker;
+  m.nacked = r.meta.nacked;
+  m.layer = r.meta.layer;
+  m.codec_len = u8(std::min<size_t>(8, r.meta.codecBytes.size()));
+  std::memcpy(m.codec, r.meta.codecBytes.data(), m.codec_len);
+}
+
+// DownTrack.retransmitPackets (downtrack.go:1596-1631) up to Receiver.ReadRTP,
+// for every DownTrack's NACK list (nacks grouped by DownTrack):
+// Forwarder.FilterRTX (forwarder.go:1406-1434: FlagFilterRTX off, so the SN
+// list passes; FlagFilterRTXLayers on: every layer is disallowed while the
+// last allocation is deficient and the target is below the current layer, and
+// layers above the current one are), then sequencer.getExtPacketMetas
+// (sequencer.go:263-332), then the disallowed layers are skipped.
+int orc_rtx_lookup(orc_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now_ns, lkf_rtx *out, uint32_t cap,
+                   uint32_t *n_out) {
+  *n_out = 0;
+  std::vector<lkf_rtx> res;
+  for (u32 i = 0; i < n;) {
+    const int32_t dt = nacks[i].dt;
+    u32 j = i;
+    while (j < n && nacks[j].dt == dt) j++;
+    if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
+    for (u32 k = j; k < n; k++)
+      if (nacks[k].dt == dt) return LKF_EORDER;  // a DownTrack's NACKs must be contiguous
+    ODT &d = *e->dts[dt];
+    if (d.active) {
+      bool disallowed[DefaultMaxLayerSpatial + 1] = {};
+      const VideoLayer cur = d.f->vls.GetCurrent(), tgt = d.f->vls.GetTarget();
+      for (int l = 0; l <= DefaultMaxLayerSpatial; l++)
+        if (d.f->lastAllocIsDeficient && (tgt.Spatial < cur.Spatial || l > cur.Spatial)) disallowed[l] = true;
+      std::vector<u16> sns;
+      std::vector<u32> idx;
+      for (u32 k = i; k < j; k++) sns.push_back(nacks[k].sn);
+      auto r = d.seq->getExtPacketMetas(sns, now_ns / 1000000);
+      for (auto &epm : r) {
+        if (epm.meta.layer >= 0 && epm.meta.layer <= DefaultMaxLayerSpatial && disallowed[epm.meta.layer]) continue;
+        lkf_rtx x;
+        std::memset(&x, 0, sizeof(x));
+        epm_to_meta(epm, x.meta);
+        x.dt = dt;
+        res.push_back(x);
+      }
+    }
+    i = j;
+  }
+  *n_out = u32(res.size());
+  if (cap < res.size()) return LKF_ENOSPC;
+  if (!res.empty()) std::memcpy(out, res.data(), res.size() * sizeof(lkf_rtx));
+  return LKF_OK;
+}
+
+// The retransmission itself (downtrack.go:1640-1698): the source packet as the
+// receiver's bucket returned it (src[i], len 0: ReadRTP failed, skipped) with
+// marker/SN/TS from the sequencer, the DownTrack's SSRC and payload type; VP8
+// re-munged with the stored descriptor bytes (translateVP8PacketTo); the
+// pacer's extension block (pacer/base.go:71-100: extensions cleared, the DD
+// element for a DownTrack with the DD extension — not kept by this engine's
+// sequencer, see lkfwd.h — and abs-send-time as a 3-byte placeholder).
+int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
+                 uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
+                 uint64_t *out_len) {
+  (void)src_len;
+  std::vector<lkf_out> recs;
+  std::vector<u8> arena;
+  for (u32 i = 0; i < n; i++) {
+    const lkf_rtx &x = rtx[i];
+    if (x.dt < 0 || x.dt >= (int)e->dts.size()) return LKF_EINVAL;
+    const ODT &d = *e->dts[x.dt];
+    if (!src[i].len) continue;  // ReadRTP miss
+    const u8 *buf = src_arena + src[i].off;
+    RtpParsed h;
+    if (!rtp_unmarshal(buf, int(src[i].len), h)) continue;  // "could not unmarshal rtp packet in retransmit"
+    RtpHeader hdr;
+    hdr.Version = h.b0 >> 6;
+    hdr.Padding = h.padding;
+    for (int c = 0; c < h.cc; c++) {
+      const u8 *q = buf + 12 + 4 * c;
+      hdr.CSRC.push_back((u32(q[0]) << 24) | (u32(q[1]) << 16) | (u32(q[2]) << 8) | u32(q[3]));
+    }
+    hdr.Marker = x.meta.marker;
+    hdr.SequenceNumber = x.meta.target_sn;
+    hdr.Timestamp = x.meta.timestamp;
+    hdr.SSRC = d.p.ssrc;
+    hdr.PayloadType = d.p.payload_type;
+    const u8 *pay = buf + h.hdrSize;
+    std::vector<u8> payload;
+    if (e->tracks[d.p.track].p.codec == LKF_CODEC_VP8 && h.payloadLen > 0 && x.meta.codec_len) {
+      VP8 v;
+      if (v.Unmarshal(pay, h.payloadLen) != OK) continue;  // "could not unmarshal VP8 packet"
+      payload.assign(x.meta.codec, x.meta.codec + x.meta.codec_len);
+      payload.insert(payload.end(), pay + v.HeaderSize, pay + h.payloadLen);
+    } else {
+      payload.assign(pay, pay + h.payloadLen);
+    }
+    hdr.Extension = false;
+    hdr.ExtensionProfile = 0;
+    hdr.Extensions.clear();
+    if (d.p.ext_abs_send_time) hdr.SetExtension(d.p.ext_abs_send_time, std::vector<u8>{0, 0, 0});
+    std::vector<u8> bytes;
+    hdr.Marshal(bytes);
+    bytes.insert(bytes.end(), payload.begin(), payload.end());
+    lkf_out o;
+    std::memset(&o, 0, sizeof(o));
+    o.ext_sn = x.meta.ext_sn;
+    o.ext_ts = x.meta.ext_ts;
+    o.out_off = arena.size();
+    o.dt = u32(x.dt);
+    o.pkt = i;
+    o.out_len = u16(bytes.size());
+    o.flags = u8(x.meta.marker ? LKF_OUT_MARKER : 0);
+    o.layer = x.meta.layer;
+    recs.push_back(o);
+    arena.insert(arena.end(), bytes.begin(), bytes.end());
+    arena.resize((arena.size() + 15) & ~size_t(15), 0);
+  }
+  *n_out = u32(recs.size());
+  *out_len = arena.size();
+  if (recs.size() > n || arena.size() > out_cap) return LKF_ENOSPC;
+  if (!recs.empty()) std::memcpy(out, recs.data(), recs.size() * sizeof(lkf_out));
+  if (!arena.empty()) std::memcpy(out_arena, arena.data(), arena.size());
+  return LKF_OK;
+}
+
 int orc_seq_lookup(orc_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns, lkf_seq_meta *out,
                    uint32_t *n_out) {
   if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
