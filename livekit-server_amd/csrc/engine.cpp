@@ -218,6 +218,7 @@ struct lkf_engine {
   uint64_t *dPos = nullptr, *dIPartA = nullptr, *dIPartB = nullptr, *dITotal = nullptr;
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
   uint32_t *dIList = nullptr, *dIListCnt = nullptr;  // per-stream datagram lists (k_ing_lists)
+  uint32_t *dILanePerm = nullptr;                     // k_ing_stream lane -> stream, by (kind, layer)
   uint32_t lastIngestN = 0;
   // speaker ranking tables (rebuilt when topology changes)
   uint32_t nRooms = 0;
@@ -410,6 +411,17 @@ static int flush_topology(lkf_engine *e) {
            "stream state upload");
     HIPCHK(hipMemset(e->dHist + first * kHistWords, 0, k * kHistWords * sizeof(uint64_t)), "history reset");
     e->pendStreams.clear();
+    // k_ing_stream lanes: streams grouped by (kind, layer), so a wave's lanes
+    // have similar datagram counts and take the same branches
+    const uint32_t ns = uint32_t(e->streams.size());
+    std::vector<uint32_t> perm(ns);
+    for (uint32_t i = 0; i < ns; i++) perm[i] = i;
+    auto key = [&](uint32_t i) {
+      const lkf_track_params &tp = e->tracks[e->streams[i].track];
+      return std::make_pair(int(tp.kind), int(e->streams[i].layer));
+    };
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+    HIPCHK(hipMemcpy(e->dILanePerm, perm.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice), "lane perm copy");
   }
   return upload_done(e);
 }
@@ -506,6 +518,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dIErr, 4));
   A(dalloc(&e->dIList, 3 * size_t(c.max_batch_pkts) + 64));
   A(dalloc(&e->dIListCnt, 3 * size_t(c.max_tracks)));
+  A(dalloc(&e->dILanePerm, e->maxStreams));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
     A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
@@ -557,7 +570,7 @@ void lkf_destroy(lkf_engine *e) {
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
-                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt,
+                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts};
   for (void *p : ptrs)
@@ -1533,6 +1546,7 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.list = e->dIList;
   a.listCnt = e->dIListCnt;
   a.listStride = e->cfg.max_batch_pkts;
+  a.lanePerm = e->dILanePerm;
   const bool dd = e->nDDStreams != 0;
   a.ddStates = dd ? e->dDDIng : nullptr;
   a.ddStructs = dd ? e->dDDIngStruct : nullptr;

@@ -524,7 +524,7 @@ __device__ void hist_clear_range(u64 *h, u64 lo, u64 hi) {  // inclusive; lo > h
 }
 
 // utils.RangeMap[uint64,uint64](100): ExcludeRange (rangemap.go:100-132)
-__device__ bool irm_exclude(StreamHot &h, RangeEntry *ring, u64 s, u64 e) {
+__device__ __forceinline__ bool irm_exclude(StreamHot &h, RangeEntry *ring, u64 s, u64 e) {
   if (e == s || (e - s) > (1ull << 63)) return false;
   if (h.rmOpenStart > s) return false;
   const u64 nv = h.rmOpenValue + (e - s);
@@ -549,7 +549,7 @@ __device__ bool irm_exclude(StreamHot &h, RangeEntry *ring, u64 s, u64 e) {
   return true;
 }
 // GetValue (rangemap.go:134-169)
-__device__ bool irm_get(const StreamHot &h, const RangeEntry *ring, u64 key, u64 &out) {
+__device__ __forceinline__ bool irm_get(const StreamHot &h, const RangeEntry *ring, u64 key, u64 &out) {
   out = 0;
   if (key >= h.rmOpenStart) {
     out = h.rmOpenValue;
@@ -582,7 +582,7 @@ __device__ bool irm_get(const StreamHot &h, const RangeEntry *ring, u64 key, u64
 }
 
 // AudioLevel.Observe audiolevel.go:70-102
-__device__ void level_observe(StreamHot &h, const DevStream &s, u8 level, u32 durationMs, i64 arrivalNs) {
+__device__ __forceinline__ void level_observe(StreamHot &h, const DevStream &s, u8 level, u32 durationMs, i64 arrivalNs) {
   h.lastObservedNs = arrivalNs;
   h.observedDuration += durationMs;
   if (level <= s.activeLevel) {
@@ -810,13 +810,16 @@ __global__ void __launch_bounds__(64) k_ing_stream(const lkf_raw_pkt *__restrict
                              const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows, u32 *__restrict__ fwd,
                              const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
                              IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list,
-                             const u32 *__restrict__ cnt, u32 stride) {
+                             const u32 *__restrict__ cnt, u32 stride, const u32 *__restrict__ lanePerm) {
   __shared__ u64 sHist[kHistWords * kHL];
 #if LKF_ING_HOT_LDS
   __shared__ StreamHot sHot[kHL];  // the receiver state in LDS
 #endif
-  const u32 sid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sid >= nstreams) return;
+  // lanes take streams in the engine's (kind, layer) order: a wave's lanes
+  // walk lists of similar length through the same branches
+  const u32 slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= nstreams) return;
+  const u32 sid = lanePerm ? lanePerm[slot] : slot;
   const DevStream s = streams[sid];
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;
@@ -835,19 +838,26 @@ __global__ void __launch_bounds__(64) k_ing_stream(const lkf_raw_pkt *__restrict
   const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
   const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
   auto idxAt = [&](u32 j) { return useList ? lst[j] : pb + j; };
-  // software pipeline: the next datagram's descriptor loads while this one is decided
-  u32 i = nIdx ? idxAt(0) : 0;
-  IngParsed pn = nIdx ? q[i] : IngParsed{};
-  lkf_raw_pkt rn = nIdx ? raws[i] : lkf_raw_pkt{};
+  // software pipeline: descriptors two datagrams ahead, list indices three
+  // ahead, so no iteration waits on a dependent load (gfx9 counts stores in
+  // vmcnt: a load issued right before its use would also wait for the
+  // previous iteration's flow stores)
+  u32 ia = nIdx > 0 ? idxAt(0) : 0, ib = nIdx > 1 ? idxAt(1) : 0, i3 = nIdx > 2 ? idxAt(2) : 0;
+  IngParsed pa = nIdx > 0 ? q[ia] : IngParsed{}, pb2 = nIdx > 1 ? q[ib] : IngParsed{};
+  lkf_raw_pkt ra = nIdx > 0 ? raws[ia] : lkf_raw_pkt{}, rb = nIdx > 1 ? raws[ib] : lkf_raw_pkt{};
   for (u32 j = 0; j < nIdx; j++) {
-    const IngParsed p = pn;
-    const lkf_raw_pkt rp = rn;
-    const u32 ic = i;
-    if (j + 1 < nIdx) {
-      i = idxAt(j + 1);
-      pn = q[i];
-      rn = raws[i];
+    const IngParsed p = pa;
+    const lkf_raw_pkt rp = ra;
+    const u32 ic = ia;
+    ia = ib;
+    pa = pb2;
+    ra = rb;
+    ib = i3;
+    if (j + 2 < nIdx) {
+      pb2 = q[ib];
+      rb = raws[ib];
     }
+    if (j + 3 < nIdx) i3 = idxAt(j + 3);
     if (rp.stream != sid) continue;
     const i64 arrival = rp.arrival_ns;
     lkf_flow f = {};
@@ -1213,7 +1223,7 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
                      a.tEnd, a.listStride, a.list, a.listCnt);
   hipLaunchKernelGGL(k_ing_stream, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a.raws, a.parsed, a.streams,
                      a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates,
-                     a.ddStructs, a.ingDD, a.err, a.list, a.listCnt, a.listStride);
+                     a.ddStructs, a.ingDD, a.err, a.list, a.listCnt, a.listStride, a.lanePerm);
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
   if (r != hipSuccess) return r;

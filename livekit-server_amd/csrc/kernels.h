@@ -95,6 +95,7 @@ struct IngestLaunch {
   // per-stream datagram lists (k_ing_lists): [layer slot * listStride + tBegin + j], counts [track * 3 + slot]
   uint32_t *list, *listCnt;
   uint32_t listStride;
+  const uint32_t *lanePerm;  // k_ing_stream lane -> stream (nullptr: identity)
 };
 
 struct SpeakersLaunch {
