@@ -453,9 +453,26 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   int leastPrio = 0, greatestPrio = 0;
   A(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
   A(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
-  A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
-  A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
-  A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
+  // LKF_CU_SPLIT=D (A/B): of every 32 CUs, D run the prep/decide streams and the
+  // rest the emit stream (hipExtStreamCreateWithCUMask), so the latency-bound
+  // decide and the HBM-bound emit of consecutive batches stop competing for
+  // the same CUs; 0 (default): all CUs, decide at high priority
+  int cuSplit = 0;
+  if (const char *v = getenv("LKF_CU_SPLIT")) cuSplit = atoi(v);
+  if (cuSplit > 0 && cuSplit < 32) {
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device);
+    const uint32_t words = uint32_t((ncu + 31) / 32);
+    std::vector<uint32_t> mA(words, 0), mB(words, 0);
+    for (int i = 0; i < ncu; i++) ((i % 32) < cuSplit ? mA : mB)[size_t(i / 32)] |= 1u << (i % 32);
+    A(hipExtStreamCreateWithCUMask(&e->decS, words, mA.data()));
+    A(hipExtStreamCreateWithCUMask(&e->prepS, words, mA.data()));
+    A(hipExtStreamCreateWithCUMask(&e->emitS, words, mB.data()));
+  } else {
+    A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
+    A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
+    A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
+  }
   A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
   e->cur = e->own;
   A(dalloc(&e->dTracks, c.max_tracks));
