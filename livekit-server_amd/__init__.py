@@ -75,7 +75,8 @@ def drain_arrays(api, h, nmax=None):
     arena = np.zeros(alen.value, dtype=np.uint8)
     rc = api["drain"](h, recs.ctypes.data, n.value, arena.ctypes.data, alen.value, C.byref(n), C.byref(alen))
     if rc != 0:
-        raise EngineError("drain rc=%d" % rc)
+        msg = api["last_error"](h).decode() if "last_error" in api else ""
+        raise EngineError("drain rc=%d (%d records, %d bytes): %s" % (rc, n.value, alen.value, msg))
     return recs, arena
 
 

@@ -318,6 +318,8 @@ def bind_engine_api(lib, prefix):
                        [e, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_uint32])
     api["ctl_batch"] = _bind(lib, prefix + "ctl_batch", C.c_int, [e, C.c_void_p, C.c_uint32])
     api["get_stats"] = _bind(lib, prefix + "get_stats", C.c_int, [e, P(lkf_stats)])
+    if hasattr(lib, prefix + "last_error"):
+        api["last_error"] = _bind(lib, prefix + "last_error", C.c_char_p, [e])
     api["drain"] = _bind(lib, prefix + "drain", C.c_int,
                          [e, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, P(C.c_uint64), P(C.c_uint64)])
     api["get_state"] = _bind(lib, prefix + "get_state", C.c_int, [e, C.c_int32, P(lkf_fwd_state)])
