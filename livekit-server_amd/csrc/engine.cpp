@@ -206,6 +206,7 @@ struct lkf_engine {
   hipEvent_t ring[kRing][5] = {};
   uint32_t emitGrid = 2048;       // persistent grid-stride launch (LKF_EMIT_PERSISTENT=1)
   bool emitPersistent = false;
+  uint32_t decideK = 0;  // DownTracks per decide wave (0: from the batch's packets per track)
   // ingress (one buffer.Buffer per stream) + speakers
   uint32_t maxStreams = 0;
   DevStream *dStreams = nullptr;
@@ -562,6 +563,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   int perCU = 24;
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
   if (const char *v = getenv("LKF_EMIT_PERSISTENT")) e->emitPersistent = atoi(v) != 0;
+  if (const char *v = getenv("LKF_DECIDE_K")) e->decideK = uint32_t(std::min(64, std::max(0, atoi(v))));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   return e;
@@ -1045,6 +1047,15 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.dtCum = e->dDTCum;
   d.stats = x.dStats;
   d.ddLanes = e->ddLanes;
+  // Several DownTracks per decide wave when the batch is short (a 10-20 ms
+  // tick has a few packets per track): the per-DownTrack prologue then
+  // dominates and one workgroup per DownTrack is dispatch-rate bound.
+  if (e->decideK) {
+    d.perWave = e->decideK;
+  } else {
+    const uint64_t per = uint64_t(e->curN) / std::max<uint32_t>(1, nt);  // (ingest: the datagram count bound)
+    d.perWave = per >= 48 ? 1 : per >= 12 ? 2 : 4;
+  }
   d.ddPkts = e->ddAlloc ? x.dDDPkt : nullptr;
   d.ddStructs = e->dDDStruct;
   d.ddState = e->ddAlloc ? e->dDDState : nullptr;

@@ -1383,6 +1383,8 @@ struct DecideArgs {
   const u32 *layerList, *layerBefore, *layerCnt;  // k_layer_index
   u32 pktStride;
   u32 waveBase;  // schedule index of this launch's first wave
+  u32 waveEnd;   // schedule index after this launch's last wave
+  u32 perWave;   // DownTracks (schedule slots) per wave: 1 for long batches, more for short ticks
   // dependency descriptor (F_DD DownTracks)
   const DDPkt *ddPkts;
   const DDStruct *ddStructs;
@@ -1712,18 +1714,58 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #if LKF_DIAG
   const u64 tEntry = clock64();
 #endif
-  const u32 lane = threadIdx.x;
+  // A wave serves perWave schedule slots of its XCD's list (slot index = q * 8
+  // + XCD, q consecutive), one DownTrack after the other.  Short ticks have a
+  // few packets per DownTrack, and one workgroup per DownTrack would leave the
+  // kernel bound by the workgroup dispatch rate (≈30 waves/µs per XCD).
+  // Round 1: lane j fetches slot j's DownTrack, track and control-op range and
+  // then the track's packet range, so the whole wave's list costs two
+  // dependent loads.  A DownTrack with neither packets nor control ops in the
+  // batch is skipped: its state does not change and k_batch_init zeroed its
+  // counters.
+  // The list is kept in LDS (not registers) across the DownTrack loop.
+  __shared__ uint4 sSlot[2 * 64];
+  u64 todo;
+  {
+    const u32 K = A.perWave, lane = threadIdx.x;
+    const u32 wj = A.waveBase + ((blockIdx.x >> 3) * K + lane) * 8 + (blockIdx.x & 7);
+    u32 dj = 0xffffffffu, tj = 0, ej = 0, eej = 0, pbj = 0, pej = 0;
+    if (lane < K && wj < A.waveEnd) {
+      dj = A.sched[wj];
+      tj = A.waveTrack[wj];
+      ej = A.evOff[wj];
+      eej = A.evOff[wj + 1];
+    }
+    if (dj != 0xffffffffu) {  // (0xffffffff: padding slot of the per-XCD schedule)
+      pbj = A.tBegin[tj];
+      pej = A.tEnd[tj];
+    }
+    todo = __ballot(dj != 0xffffffffu && (pbj < pej || ej < eej));
+    if (lane < K) {
+      sSlot[2 * lane] = make_uint4(wj, dj, tj, ej);
+      sSlot[2 * lane + 1] = make_uint4(eej, pbj, pej, 0);
+    }
+    wave_lds_sync();
+  }
+  while (todo) {
+  const u32 jw = u32(__ffsll(static_cast<long long>(todo))) - 1;
+  todo &= todo - 1;
+  // The lane index again, opaque to the compiler, so lane-derived values are
+  // recomputed per DownTrack rather than hoisted out of the loop and held in
+  // registers across the whole body.
+  u32 laneR;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(laneR) : "v"(threadIdx.x));
+  const u32 lane = laneR;
   const u64 lt = (1ull << lane) - 1;
-  const u32 w = A.waveBase + blockIdx.x;
-  // Prologue: two rounds of independent loads.  Round 1 needs only the wave
-  // index (DownTrack, track, control-op range); round 2 everything keyed by
-  // them, including the VP8 munger maps (read whole, whatever their fill, so
-  // the copy does not wait for the hot state).
-  const u32 d = A.sched[w];
-  const u32 track = A.waveTrack[w];
-  u32 ev = A.evOff[w];
-  const u32 evEnd = A.evOff[w + 1];
-  if (d == 0xffffffffu) return;  // padding slot of the per-XCD schedule
+  // Round 2: everything keyed by the DownTrack, including the VP8 munger maps
+  // (read whole, whatever their fill, so the copy does not wait for the hot
+  // state).
+  const uint4 sa = sSlot[2 * jw], sb = sSlot[2 * jw + 1];
+  const u32 w = __builtin_amdgcn_readfirstlane(sa.x);
+  const u32 d = __builtin_amdgcn_readfirstlane(sa.y);
+  const u32 track = __builtin_amdgcn_readfirstlane(sa.z);
+  u32 ev = __builtin_amdgcn_readfirstlane(sa.w);
+  const u32 evEnd = __builtin_amdgcn_readfirstlane(sb.x);
 #if LKF_WTIME
   const u64 wt0 = __builtin_amdgcn_s_memrealtime();
   const u64 wc0 = __builtin_amdgcn_s_memtime();
@@ -1735,8 +1777,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const u64 tP1 = clock64() + u64(__builtin_amdgcn_readfirstlane(d) & 0);  // after round 1
 #endif
   const DevDT dt = A.dts[d];
-  const u32 pb = A.tBegin[track];
-  u32 pe = A.tEnd[track];
+  const u32 pb = __builtin_amdgcn_readfirstlane(sb.y);
+  u32 pe = __builtin_amdgcn_readfirstlane(sb.z);
   const u64 slot0 = A.slotBase[d];
   LaneOut o;
   o.nFwd = o.nBytes = o.nTuples = 0;
@@ -1844,7 +1886,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     // state change (simulcast.go:42-122: curS == tgtS <= maxS, forwarder.go
     // :1440/:1687 not taken).  Its chunk is then the next 64 packets of its
     // own layer (per-track layer lists); the skipped packets are counted.
-    const bool steady = steady_state(L);
+    // (A track with at most 64 packets in the batch is one chunk either way:
+    // read it directly instead of through the layer list, two dependent
+    // loads fewer for the short ticks.)
+    const bool steady = pe - pb > 64 && steady_state(L);
     u32 pi, n, lim;  // lane -> packet index; packets in the chunk; packet index after it
     if (steady) {
       const u32 ls = u32(L.h.curS);
@@ -2457,11 +2502,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     A.fwdCnt[d] = u32(o.nFwd);
     A.fwdBytes[d] = o.relOff;
     // DownTrack.sendingPacket: bytesSent += header + payload (downtrack.go:1934-1940)
-    DTCum c = A.dtCum[d];
-    c.packets += o.nFwd;
-    c.bytes += o.nBytes;
-    c.flags = L.h.flags;
-    A.dtCum[d] = c;
+    // (atomics without return: the wave does not wait for a read of the old totals)
+    if (o.nFwd) atomicAdd((unsigned long long *)&A.dtCum[d].packets, (unsigned long long)o.nFwd);
+    if (o.nBytes) atomicAdd((unsigned long long *)&A.dtCum[d].bytes, (unsigned long long)o.nBytes);
+    A.dtCum[d].flags = L.h.flags;
     // counters: one of kStatCopies partial copies per wave (same-address
     // atomics from every wave would serialise in one L2 channel); k_stats_reduce
     // folds the copies after the kernel
@@ -2473,6 +2517,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     for (int i = 0; i < LKF_DROP_NREASONS; i++)
       if (o.drops[i]) atomicAdd((unsigned long long *)&st[4 + i], (unsigned long long)o.drops[i]);
   }
+  }  // next DownTrack of this wave
 }
 
 // ---------------------------------------------------------------------------
@@ -3141,11 +3186,18 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.ddCap = a.ddCap;
   // DownTracks of the dependency-descriptor selector run in their own
   // instantiation (the last ddLanes waves of the schedule)
+  // Each part is a multiple of 8 slots (per-XCD lists of equal length);
+  // a workgroup takes perWave consecutive slots of one XCD's list.
   const u32 nPlain = a.nlanes - a.ddLanes;
+  const u32 K = a.perWave ? a.perWave : 1;
+  A.perWave = K;
+  auto blocks = [K](u32 lanes) { return (lanes / 8 + K - 1) / K * 8; };
   A.waveBase = 0;
-  if (nPlain) hipLaunchKernelGGL(k_decide_dt<false>, dim3(nPlain), dim3(64), 0, s, A, a.pkts);
+  A.waveEnd = nPlain;
+  if (nPlain) hipLaunchKernelGGL(k_decide_dt<false>, dim3(blocks(nPlain)), dim3(64), 0, s, A, a.pkts);
   A.waveBase = nPlain;
-  if (a.ddLanes) hipLaunchKernelGGL(k_decide_dt<true>, dim3(a.ddLanes), dim3(64), 0, s, A, a.pkts);
+  A.waveEnd = a.nlanes;
+  if (a.ddLanes) hipLaunchKernelGGL(k_decide_dt<true>, dim3(blocks(a.ddLanes)), dim3(64), 0, s, A, a.pkts);
   return hipGetLastError();
 }
 

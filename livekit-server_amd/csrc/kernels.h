@@ -13,6 +13,7 @@ struct DecideLaunch {
   const uint32_t *waveTrack;
   uint32_t nlanes;          // waves
   uint32_t ddLanes;         // the last ddLanes waves: DownTracks of the DD selector (k_decide_dt<true>)
+  uint32_t perWave;         // DownTracks per wave (1..64; 0 = 1)
   DTHot *hot;
   const DevDT *dts;
   const DevTrack *tracks;

@@ -1,8 +1,8 @@
 """Diagnostic: k_decide_dt per-wave lifetimes from a -DLKF_WTIME=1 build.
 
-    make -C livekit-server_amd/csrc wtime && python3 scripts/wave_timeline.py [rooms] [batches]
+    make -C livekit-server_amd/csrc wtime && python3 scripts/wave_timeline.py [rooms] [batches] [batch_s]
 
-Runs configs[1] batches (1 s each) through liblkfwd_wtime.so, then reads the
+Runs configs[1] batches (1 s each by default) through liblkfwd_wtime.so, then reads the
 last decide launch's per-wave stamps (s_memrealtime, 100 MHz): the occupancy
 curve (waves alive over time), wave lifetime vs packets / serial steps.
 """
@@ -22,7 +22,8 @@ def main():
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     pkg = importlib.import_module("livekit-server_amd")
     wl = importlib.import_module("livekit-server_amd.workload")
-    tr = wl.Trace(2, duration_s=float(nb), batch_s=1.0, rooms=rooms)
+    bs = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
+    tr = wl.Trace(2, duration_s=nb * bs, batch_s=bs, rooms=rooms)
     lib = os.path.join(ROOT, "livekit-server_amd", "lib", os.environ.get("WTIME_LIB", "liblkfwd_wtime.so"))
     eng = pkg.Engine.for_trace(tr, lib_path=lib)
     fn = eng.lib.lkf_debug_wtime
