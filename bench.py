@@ -20,6 +20,8 @@ import sys
 import threading
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -123,6 +125,9 @@ def main():
     ap.add_argument("--host-io", action="store_true",
                     help="host-fed deployment shape: lkf_submit from pinned host memory and lkf_drain_run of "
                          "the previous batch into pinned host memory inside the timed region (PCIe both ways)")
+    ap.add_argument("--srtp", action="store_true",
+                    help="step = forward + SRTP protect (lkf_protect: abs-send-time + AES_CM_128_HMAC_SHA1_80 "
+                         "per subscriber transport, every DownTrack bound)")
     args = ap.parse_args()
 
     import torch
@@ -154,6 +159,16 @@ def main():
 
     if args.ingress:
         wl.load_streams(eng.api, eng.h, trace)
+    if args.srtp:  # one transport per (room, subscriber), seeded master keys
+        rng = np.random.default_rng(1234)
+        tps = {}
+        for d in range(trace.ndts):
+            k = (int(trace.tracks[trace.downtracks[d].track].room), int(trace.downtracks[d].subscriber))
+            if k not in tps:
+                tps[k] = eng.api["add_transport"](eng.h, C.byref(pkg.transport_params(
+                    rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 14, dtype=np.uint8).tobytes())))
+                assert tps[k] >= 0
+            assert eng.api["set_downtrack_transport"](eng.h, d, tps[k]) == 0
 
     # inputs resident in HBM before the timed region (--host-io: in pinned host memory)
     dpk, dar, meta = [], [], []
@@ -204,6 +219,8 @@ def main():
             eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
         tc = time.perf_counter()
         eng.run(sp)
+        if args.srtp:
+            assert eng.api["protect"](eng.h, 1700000000 * 10**9 + int(b * args.batch_s * 1e9)) == 0
         if args.host_io and b > args.warmup:  # batch b-1's output over PCIe while batch b computes
             drain_prev(1)
         if args.sync_each:
@@ -242,6 +259,11 @@ def main():
     # time the last `win` steps and scale the sums to all K steps (steady state)
     win = min(args.steps, 250)
     dec_ms, emit_ms, tot_ms = (v * args.steps / win for v in eng.timing_window(win))
+    prot_ms = 0.0
+    if args.srtp:
+        pm = C.c_float()
+        assert eng.lib.lkf_protect_timing_window(C.c_void_p(eng.h), win, C.byref(pm)) == 0
+        prot_ms = pm.value * args.steps / win
     coll = None
     if dist:
         # the one collective — per-room speaker summaries
@@ -341,6 +363,8 @@ def main():
                                 if args.ingress else
                                 "host-fed: pinned host ExtPacket batch -> lkf_submit (H2D) + lkf_run + "
                                 "lkf_drain_run of the previous batch (D2H)" if args.host_io else
+                                "ExtPacket batch -> forward (lkf_submit_device + lkf_run) + SRTP protect (lkf_protect)"
+                                if args.srtp else
                                 "ExtPacket batch -> forward (lkf_submit_device + lkf_run)"),
                        "parallelism": "room-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
@@ -364,6 +388,14 @@ def main():
                                "d2h_bytes_per_step": (drained[0] * 40 + drained[1]) // args.steps,
                                "drained_records": drained[0], "records_forwarded": fwd,
                                "pcie_GBps_both_ways": round((h2d + drained[0] * 40 + drained[1]) / elapsed / 1e9, 2)}
+        if args.srtp:  # the protect stage: VALU/LDS-bound crypto, reported against HBM for the record
+            prot_bytes = cum["out_bytes"] * 2 + 10 * fwd + 40 * fwd
+            pa = prot_bytes / args.steps / (prot_ms / 1e3 / args.steps) / 1e9 if prot_ms else 0.0
+            line["srtp"] = {"profile": "SRTP_AES128_CM_HMAC_SHA1_80", "protected_per_step": fwd // args.steps,
+                            "protect_ms_per_step": round(prot_ms / args.steps, 4),
+                            "protected_pkts_per_s_kernel": round(fwd / (prot_ms / 1e3), 1) if prot_ms else None,
+                            "algorithmic_bytes_per_launch": int(prot_bytes // args.steps),
+                            "achieved": round(pa, 1), "frac_hbm": round(pa / PEAK_HBM_GBPS, 4)}
         print(json.dumps(line))
     eng.close()
     if dist:

@@ -458,6 +458,36 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
                  uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
                  uint64_t *out_len);
 
+/* ---- SRTP protect ----------------------------------- *
+ * The step after the pacer: writeRTPHeaderExtensions sets abs-send-time
+ * (pacer/base.go:71-100), then WriteStream.WriteRTP (base.go:59) protects the
+ * packet with the subscriber transport's SRTP context: pion/srtp/v2 v2.0.18
+ * (go.mod:87) Context.EncryptRTP, profile SRTP_AES128_CM_HMAC_SHA1_80
+ * (RFC 3711: AES-CM keystream, HMAC-SHA1 80-bit tag over header || payload ||
+ * ROC, sender rollover counter per SSRC).  A transport is one subscriber
+ * PeerConnection's DTLS-SRTP context (its exported master key and salt); its
+ * DownTracks are its SSRCs. */
+#define LKF_SRTP_AES128_CM_HMAC_SHA1_80 1
+typedef struct lkf_transport_params {
+  uint8_t master_key[16];
+  uint8_t master_salt[14];
+  uint16_t profile; /* LKF_SRTP_* */
+} lkf_transport_params;
+/* Adds a transport (session keys derived on the GPU: RFC 3711 §4.3.1). */
+int32_t lkf_add_transport(lkf_engine *e, const lkf_transport_params *p);
+/* Binds a DownTrack's packets to a transport (-1: none, its packets are
+ * copied unprotected).  Binding starts a fresh rollover state for its SSRC. */
+int lkf_set_downtrack_transport(lkf_engine *e, int32_t dt, int32_t transport);
+/* Protects the last lkf_run's output (asynchronously, after its emit stage):
+ * every packet gets the abs-send-time of `send_time_ns` (unix ns, pion/rtp
+ * NewAbsSendTimeExtension) in its abs-send-time element, and the packets of a
+ * bound DownTrack are SRTP-protected.  Record i's packet is at
+ * out_off + 16 * i of the protected arena, out_len (+ 10 with a transport)
+ * bytes long.  Valid until the run after next is enqueued, like the output. */
+int lkf_protect(lkf_engine *e, int64_t send_time_ns);
+int lkf_output_protected_device(lkf_engine *e, const uint8_t **d_arena, uint64_t *arena_len);
+int lkf_drain_protected(lkf_engine *e, uint8_t *arena, uint64_t cap, uint64_t *arena_len);
+
 /* ---- ingress ------------------------------------------------------------ */
 /* Adds one received stream (NewBuffer + Bind, buffer.go:124-215). */
 int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p);
@@ -500,6 +530,9 @@ int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *tot
  * emit end (stages overlap across runs).  HIP events recorded on the engine's
  * decide and emit streams; synchronises on the newest. */
 int lkf_timing_window(lkf_engine *e, uint32_t n, float *decide_ms, float *emit_ms, float *total_ms);
+/* Over the last n runs, all protected (n <= 256): the sum of the SRTP
+ * protect stage spans (k_srtp_roc + k_srtp_protect), ms. */
+int lkf_protect_timing_window(lkf_engine *e, uint32_t n, float *protect_ms);
 /* Counters accumulated on the GPU over all runs since the last reset. */
 int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset);
 const char *lkf_version(void);

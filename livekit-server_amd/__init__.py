@@ -80,6 +80,28 @@ def drain_arrays(api, h, nmax=None):
     return recs, arena
 
 
+def transport_params(master_key, master_salt, profile=abi.LKF_SRTP_AES128_CM_HMAC_SHA1_80):
+    """lkf_transport_params from 16 + 14 key bytes (a DTLS-SRTP export)."""
+    t = abi.lkf_transport_params()
+    C.memmove(t.master_key, bytes(master_key), 16)
+    C.memmove(t.master_salt, bytes(master_salt), 14)
+    t.profile = profile
+    return t
+
+
+def drain_protected(api, h):
+    """The last protected run's arena (record i's packet at out_off + 16 * i)."""
+    n = C.c_uint64()
+    rc = api["drain_protected"](h, None, 0, C.byref(n))
+    if rc not in (0, -28):
+        raise EngineError("drain_protected probe rc=%d" % rc)
+    arena = np.zeros(n.value, dtype=np.uint8)
+    rc = api["drain_protected"](h, arena.ctypes.data, n.value, C.byref(n))
+    if rc != 0:
+        raise EngineError("drain_protected rc=%d" % rc)
+    return arena
+
+
 def flows_array(api, h):
     """Per-datagram outcomes (lkf_flow) of the last ingest as a numpy array."""
     n = C.c_uint32()

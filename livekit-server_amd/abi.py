@@ -238,6 +238,18 @@ class lkf_fwd_state(C.Structure):
         return tuple(getattr(self, f[0]) for f in self._fields_ if f[0] != "pad")
 
 
+class lkf_transport_params(C.Structure):
+    _fields_ = [
+        ("master_key", C.c_uint8 * 16),
+        ("master_salt", C.c_uint8 * 14),
+        ("profile", C.c_uint16),
+    ]
+
+
+LKF_SRTP_AES128_CM_HMAC_SHA1_80 = 1
+SRTP_TAG_LEN = 10
+
+
 class lkf_seq_meta(C.Structure):
     _fields_ = [
         ("ext_sn", C.c_uint64),
@@ -344,6 +356,10 @@ def bind_engine_api(lib, prefix):
     api["rtx_emit"] = _bind(lib, prefix + "rtx_emit", C.c_int,
                             [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                              C.c_uint64, P(C.c_uint32), P(C.c_uint64)])
+    api["add_transport"] = _bind(lib, prefix + "add_transport", C.c_int32, [e, P(lkf_transport_params)])
+    api["set_downtrack_transport"] = _bind(lib, prefix + "set_downtrack_transport", C.c_int, [e, C.c_int32, C.c_int32])
+    api["protect"] = _bind(lib, prefix + "protect", C.c_int, [e, C.c_int64])
+    api["drain_protected"] = _bind(lib, prefix + "drain_protected", C.c_int, [e, C.c_void_p, C.c_uint64, P(C.c_uint64)])
     return api
 
 

@@ -72,6 +72,9 @@ struct BatchCtx {
   hipEvent_t decided = nullptr;  // decide stage done (decide stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
   bool used = false;
+  // SRTP-protected copy of the output (lkf_protect; allocated on first use)
+  uint8_t *dProt = nullptr;
+  bool protectedRun = false;
 };
 
 }  // namespace
@@ -207,6 +210,15 @@ struct lkf_engine {
   uint32_t emitGrid = 2048;       // persistent grid-stride launch (LKF_EMIT_PERSISTENT=1)
   bool emitPersistent = false;
   uint32_t decideK = 0;  // DownTracks per decide wave (0: from the batch's packets per track)
+  // SRTP protect (tables allocated with the first transport or lkf_protect)
+  std::vector<lkf_transport_params> transports;
+  lkf_transport_params *dTransports = nullptr;
+  SrtpKeys *dSrtpKeys = nullptr;
+  uint32_t transportCap = 0;
+  uint32_t *dAesTab = nullptr;
+  SrtpDT *dSrtpDT = nullptr;
+  hipEvent_t protRing[256][2] = {};  // k_srtp_roc start / k_srtp_protect end per run (timing)
+  std::vector<uint8_t> protRun;      // per ring slot: that run was protected
   // ingress (one buffer.Buffer per stream) + speakers
   uint32_t maxStreams = 0;
   DevStream *dStreams = nullptr;
@@ -598,7 +610,14 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->dDDState), static_cast<void *>(e->dDDIng),
                   static_cast<void *>(e->dDDIngStruct), static_cast<void *>(e->dIngDD)})
     if (p) (void)hipFree(p);
+  for (auto &r : e->protRing)
+    for (auto &ev : r)
+      if (ev) (void)hipEventDestroy(ev);
+  for (void *p : {static_cast<void *>(e->dTransports), static_cast<void *>(e->dSrtpKeys),
+                  static_cast<void *>(e->dAesTab), static_cast<void *>(e->dSrtpDT)})
+    if (p) (void)hipFree(p);
   for (auto &x : e->ctx) {
+    if (x.dProt) (void)hipFree(x.dProt);
     for (void *p : {static_cast<void *>(x.dDDIn), static_cast<void *>(x.dDDPkt), static_cast<void *>(x.dDDArena),
                     static_cast<void *>(x.dDDUsed)})
       if (p) (void)hipFree(p);
@@ -1114,6 +1133,8 @@ int lkf_run(lkf_engine *e, void *stream) {
     e->hp[5] += 1;
   }
   x.used = true;
+  x.protectedRun = false;
+  if (!e->protRun.empty()) e->protRun[e->nRuns % 256] = 0;
   e->lastCtx = ci;
   e->nRuns++;
   e->haveBatch = false;
@@ -1224,6 +1245,143 @@ int lkf_drain_run(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8
   if (tot[2] > cap || tot[3] > arena_cap) return LKF_ENOSPC;
   if (out && tot[2]) HIPCHK(hipMemcpy(out, x.dOut, tot[2] * sizeof(lkf_out), hipMemcpyDeviceToHost), "drain recs");
   if (arena && tot[3]) HIPCHK(hipMemcpy(arena, x.dOutArena, tot[3], hipMemcpyDeviceToHost), "drain bytes");
+  return LKF_OK;
+}
+
+// ---- SRTP protect ---------------------------------------------------------
+static int srtp_init(lkf_engine *e) {
+  if (e->dAesTab) return LKF_OK;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(dalloc(&e->dAesTab, 256 + 64), "alloc aes tables");
+  HIPCHK(dalloc(&e->dSrtpDT, e->cfg.max_downtracks), "alloc srtp dt");
+  HIPCHK(hipMemsetAsync(e->dSrtpDT, 0, sizeof(SrtpDT) * e->cfg.max_downtracks, e->own), "srtp dt init");
+  HIPCHK(launch_aes_tables(e->own, e->dAesTab), "aes tables");
+  HIPCHK(hipStreamSynchronize(e->own), "srtp init sync");
+  for (auto &r : e->protRing)
+    for (auto &ev : r) HIPCHK(hipEventCreate(&ev), "protect event");
+  e->protRun.assign(256, 0);
+  return LKF_OK;
+}
+
+int32_t lkf_add_transport(lkf_engine *e, const lkf_transport_params *p) {
+  if (!e || !p || p->profile != LKF_SRTP_AES128_CM_HMAC_SHA1_80) return LKF_EINVAL;
+  int rc = srtp_init(e);
+  if (rc) return rc;
+  const uint32_t t = uint32_t(e->transports.size());
+  if (t + 1 > e->transportCap) {  // grow; queued protect stages read the keys
+    rc = drain_streams(e);
+    if (rc) return rc;
+    const uint32_t cap = std::max<uint32_t>(64, 2 * e->transportCap);
+    lkf_transport_params *np = nullptr;
+    SrtpKeys *nk = nullptr;
+    HIPCHK(dalloc(&np, cap), "alloc transports");
+    HIPCHK(dalloc(&nk, cap), "alloc srtp keys");
+    if (t) {
+      HIPCHK(hipMemcpy(np, e->dTransports, t * sizeof(*np), hipMemcpyDeviceToDevice), "copy transports");
+      HIPCHK(hipMemcpy(nk, e->dSrtpKeys, t * sizeof(*nk), hipMemcpyDeviceToDevice), "copy keys");
+    }
+    if (e->dTransports) HIPCHK(hipFree(e->dTransports), "free transports");
+    if (e->dSrtpKeys) HIPCHK(hipFree(e->dSrtpKeys), "free keys");
+    e->dTransports = np;
+    e->dSrtpKeys = nk;
+    e->transportCap = cap;
+  }
+  e->transports.push_back(*p);
+  HIPCHK(hipMemcpyAsync(e->dTransports + t, &e->transports.back(), sizeof(*p), hipMemcpyHostToDevice, e->own),
+         "transport copy");
+  HIPCHK(launch_srtp_keys(e->own, e->dTransports + t, t, 1, e->dAesTab, e->dSrtpKeys), "srtp keys");
+  HIPCHK(hipStreamSynchronize(e->own), "srtp keys sync");
+  return int32_t(t);
+}
+
+int lkf_set_downtrack_transport(lkf_engine *e, int32_t dt, int32_t t) {
+  if (!e || dt < 0 || dt >= int32_t(e->dtp.size()) || t < -1 || t >= int32_t(e->transports.size()))
+    return LKF_EINVAL;
+  int rc = srtp_init(e);
+  if (rc) return rc;
+  rc = drain_streams(e);  // queued protect stages read the binding
+  if (rc) return rc;
+  SrtpDT v{uint32_t(t + 1), 0, 0};
+  HIPCHK(hipMemcpy(e->dSrtpDT + dt, &v, sizeof(v), hipMemcpyHostToDevice), "srtp bind");
+  return upload_done(e);
+}
+
+// pion/rtp NewAbsSendTimeExtension(t).Marshal(): NTP time >> 14, 24 bits
+static uint32_t abs_send_time(int64_t unixNs) {
+  const uint64_t u = uint64_t(unixNs);
+  const uint64_t sec = u / 1000000000ull + 0x83AA7E80ull;
+  const uint64_t frac = ((u % 1000000000ull) << 32) / 1000000000ull;
+  return uint32_t((((sec << 32) | frac) >> 14) & 0xFFFFFF);
+}
+
+int lkf_protect(lkf_engine *e, int64_t send_time_ns) {
+  if (!e || e->lastCtx < 0) return LKF_EINVAL;
+  int rc = srtp_init(e);
+  if (rc) return rc;
+  BatchCtx &x = e->ctx[e->lastCtx];
+  if (!x.dProt)
+    HIPCHK(dalloc(&x.dProt, e->cfg.max_out_bytes + 16 * uint64_t(e->cfg.max_out_pkts)), "alloc protected arena");
+  SrtpProtectArgs a;
+  a.tab = e->dAesTab;
+  a.totals = x.dTot + 2;
+  a.out = x.dOut;
+  a.arena = x.dOutArena;
+  a.prot = x.dProt;
+  a.dts = e->dDTs;
+  a.sd = e->dSrtpDT;
+  a.keys = e->dSrtpKeys;
+  a.cap = e->cfg.max_out_pkts;
+  a.absVal = abs_send_time(send_time_ns);
+  // after the run's emit stage on the emit stream; the context's "emitted"
+  // event (what its next reuse waits for) moves behind the protect stage
+  const size_t slot = (e->nRuns - 1) % 256;
+  HIPCHK(hipEventRecord(e->protRing[slot][0], e->emitS), "event");
+  HIPCHK(launch_srtp_protect(e->emitS, a, uint32_t(e->dtp.size()), e->dPerm, x.dRecBase, x.dFwdCnt), "protect");
+  HIPCHK(hipEventRecord(e->protRing[slot][1], e->emitS), "event");
+  HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
+  e->protRun[slot] = 1;
+  x.protectedRun = true;
+  return LKF_OK;
+}
+
+int lkf_output_protected_device(lkf_engine *e, const uint8_t **d_arena, uint64_t *arena_len) {
+  if (!e || e->lastCtx < 0) return LKF_EINVAL;
+  int rc = lkf_sync(e);
+  if (rc) return rc;
+  BatchCtx &x = e->ctx[e->lastCtx];
+  if (!x.protectedRun) {
+    e->err = "the last run was not protected (lkf_protect)";
+    return LKF_EINVAL;
+  }
+  uint64_t tot[4];
+  HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  if (d_arena) *d_arena = x.dProt;
+  if (arena_len) *arena_len = tot[3] + 16 * tot[2];
+  return LKF_OK;
+}
+
+int lkf_protect_timing_window(lkf_engine *e, uint32_t n, float *protect_ms) {
+  if (!e || !e->dAesTab || n == 0 || n > 256 || n > e->nRuns) return LKF_EINVAL;
+  float sum = 0;
+  for (uint64_t r = e->nRuns - n; r < e->nRuns; r++) {
+    if (!e->protRun[r % 256]) return LKF_EINVAL;
+    HIPCHK(hipEventSynchronize(e->protRing[r % 256][1]), "evsync");
+    float a = 0;
+    HIPCHK(hipEventElapsedTime(&a, e->protRing[r % 256][0], e->protRing[r % 256][1]), "elapsed");
+    sum += a;
+  }
+  if (protect_ms) *protect_ms = sum;
+  return LKF_OK;
+}
+
+int lkf_drain_protected(lkf_engine *e, uint8_t *arena, uint64_t cap, uint64_t *arena_len) {
+  const uint8_t *d = nullptr;
+  uint64_t len = 0;
+  int rc = lkf_output_protected_device(e, &d, &len);
+  if (rc) return rc;
+  if (arena_len) *arena_len = len;
+  if (len > cap) return LKF_ENOSPC;
+  if (arena && len) HIPCHK(hipMemcpy(arena, d, len, hipMemcpyDeviceToHost), "drain protected");
   return LKF_OK;
 }
 

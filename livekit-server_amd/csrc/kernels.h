@@ -132,6 +132,39 @@ hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, uint
 hipError_t launch_rtx_emit(hipStream_t s, bool write, uint32_t n, const lkf_rtx *rtx, const lkf_raw_pkt *src,
                            const uint8_t *arena, const DevDT *dts, const DevTrack *tracks, uint32_t *lens,
                            const uint64_t *offs, uint8_t *out);
+// ---- SRTP protect (srtp_kernels.hip) ----
+struct SrtpKeys {  // one transport's session (RFC 3711 AES_CM_128_HMAC_SHA1_80)
+  uint32_t rk[44];   // AES-128 schedule of the session key (big-endian words)
+  uint32_t ih[5];    // SHA-1 state after the HMAC ipad block
+  uint32_t oh[5];    // ... after the opad block
+  uint32_t salt[4];  // 14-byte session salt, big-endian words, low 16 bits zero
+  uint32_t profile;
+  uint32_t pad[5];
+};
+static_assert(sizeof(SrtpKeys) == 256, "SrtpKeys is 256 B");
+struct SrtpDT {       // per DownTrack (SSRC)
+  uint32_t tp1;       // transport + 1 (0: none)
+  uint32_t init;      // rollover base fixed
+  uint64_t rocBase;   // (ext SN of the first protected packet) >> 16
+};
+struct SrtpProtectArgs {
+  const uint32_t *tab;  // AES te[256] + S-box
+  const uint64_t *totals;  // [0] = records of the batch
+  const lkf_out *out;
+  const uint8_t *arena;
+  uint8_t *prot;
+  const DevDT *dts;
+  SrtpDT *sd;  // (k_srtp_roc fixes rollover bases; k_srtp_protect reads)
+  const SrtpKeys *keys;
+  uint64_t cap;      // record capacity (grid bound)
+  uint32_t absVal;   // abs-send-time, 24 bits
+};
+hipError_t launch_aes_tables(hipStream_t s, uint32_t *tab);
+hipError_t launch_srtp_keys(hipStream_t s, const lkf_transport_params *in, uint32_t first, uint32_t n,
+                            const uint32_t *tab, SrtpKeys *keys);
+hipError_t launch_srtp_protect(hipStream_t s, const SrtpProtectArgs &a, uint32_t ndts, const uint32_t *perm,
+                               const uint64_t *recBase, const uint32_t *fwdCnt);
+
 hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint32_t d,
                              const uint16_t *sns, uint32_t n, int64_t nowMs, lkf_seq_meta *out, uint32_t *nOut);
 

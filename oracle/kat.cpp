@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "lkf_oracle.h"
+#include "srtp_oracle.h"
 
 using namespace orc;
 
@@ -324,6 +325,7 @@ KAT(wraparound_uint32) {
 #include "kat_sfu.inc"
 #include "kat_dd.inc"
 #include "kat_ddsel.inc"
+#include "kat_srtp.inc"
 
 int main(int argc, char **argv) {
   bool list = false;

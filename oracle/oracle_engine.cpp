@@ -24,6 +24,7 @@
 
 #include "../include/lkfwd.h"
 #include "lkf_oracle.h"
+#include "srtp_oracle.h"
 
 using namespace orc;
 
@@ -56,6 +57,9 @@ struct ODT {
   std::vector<OOut> outs;
   // DownTrack.sendingPacket counters (downtrack.go:1930-1941)
   u64 packetsSent = 0, bytesSent = 0;
+  // SRTP: the subscriber transport and this SSRC's rollover state
+  int32_t transport = -1;
+  orc_srtp::SSRCState srtp;
 };
 
 struct OEv {
@@ -94,6 +98,9 @@ struct orc_engine {
   std::vector<lkf_pkt_dd> ingestedDD;
   // lkf_pkt_dd side array of the next orc_run (orc_submit_dd)
   std::vector<lkf_pkt_dd> pendingDD;
+  // SRTP sessions (one per transport) and the last protected output
+  std::vector<orc_srtp::Session> transports;
+  std::vector<u8> protArena;
 };
 
 static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
@@ -437,6 +444,43 @@ int orc_drain(orc_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_
   if (e->outRecs.size() > cap || e->outArena.size() > arena_cap) return LKF_ENOSPC;
   if (out && !e->outRecs.empty()) std::memcpy(out, e->outRecs.data(), e->outRecs.size() * sizeof(lkf_out));
   if (arena && !e->outArena.empty()) std::memcpy(arena, e->outArena.data(), e->outArena.size());
+  return LKF_OK;
+}
+
+// ---- SRTP protect: pacer writeRTPHeaderExtensions (abs-send-time,
+// pacer/base.go:71-100) then WriteStream.WriteRTP -> pion/srtp EncryptRTP
+int32_t orc_add_transport(orc_engine *e, const lkf_transport_params *p) {
+  if (!p || p->profile != LKF_SRTP_AES128_CM_HMAC_SHA1_80) return LKF_EINVAL;
+  e->transports.emplace_back(p->master_key, p->master_salt);
+  return int32_t(e->transports.size() - 1);
+}
+
+int orc_set_downtrack_transport(orc_engine *e, int32_t dt, int32_t t) {
+  if (dt < 0 || dt >= int32_t(e->dts.size()) || t < -1 || t >= int32_t(e->transports.size())) return LKF_EINVAL;
+  e->dts[size_t(dt)]->transport = t;
+  e->dts[size_t(dt)]->srtp = orc_srtp::SSRCState();
+  return LKF_OK;
+}
+
+int orc_protect(orc_engine *e, int64_t send_time_ns) {
+  const u32 abs = orc_srtp::abs_send_time(send_time_ns);
+  const size_t n = e->outRecs.size();
+  e->protArena.assign(e->outArena.size() + 16 * n, 0);
+  for (size_t i = 0; i < n; i++) {  // records in send order (a DownTrack's packets in order)
+    const lkf_out &r = e->outRecs[i];
+    ODT &d = *e->dts[r.dt];
+    std::vector<u8> pkt(e->outArena.begin() + long(r.out_off), e->outArena.begin() + long(r.out_off + r.out_len));
+    orc_srtp::set_abs_send_time(pkt, d.p.ext_abs_send_time, abs);
+    if (d.transport >= 0) pkt = orc_srtp::protect(e->transports[size_t(d.transport)], d.srtp, pkt);
+    std::memcpy(e->protArena.data() + r.out_off + 16 * i, pkt.data(), pkt.size());
+  }
+  return LKF_OK;
+}
+
+int orc_drain_protected(orc_engine *e, uint8_t *arena, uint64_t cap, uint64_t *arena_len) {
+  *arena_len = e->protArena.size();
+  if (e->protArena.size() > cap) return LKF_ENOSPC;
+  if (arena && !e->protArena.empty()) std::memcpy(arena, e->protArena.data(), e->protArena.size());
   return LKF_OK;
 }
 

@@ -1,6 +1,6 @@
 """Diagnostic: k_decide_dt per-wave counters from a -DLKF_DIAG=1 build.
 
-    make -C livekit-server_amd/csrc diag && python3 scripts/diag_decide.py [rooms] [batches]
+    make -C livekit-server_amd/csrc diag && python3 scripts/diag_decide.py [rooms] [batches] [config] [batch_s]
 """
 import ctypes as C
 import importlib
@@ -23,7 +23,8 @@ def main():
     cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     pkg = importlib.import_module("livekit-server_amd")
     wl = importlib.import_module("livekit-server_amd.workload")
-    tr = wl.Trace(cfg, duration_s=float(nb), batch_s=1.0, rooms=rooms)
+    bs = float(sys.argv[4]) if len(sys.argv) > 4 else 1.0
+    tr = wl.Trace(cfg, duration_s=nb * bs, batch_s=bs, rooms=rooms)
     lib = os.path.join(ROOT, "livekit-server_amd", "lib", os.environ.get("DIAG_LIB", "liblkfwd_diag.so"))
     eng = pkg.Engine.for_trace(tr, lib_path=lib)
     fn = eng.lib.lkf_debug_counters

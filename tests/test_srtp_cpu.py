@@ -1,0 +1,60 @@
+"""SRTP protect on the CPU oracle (oracle/srtp_oracle.h), checked against an
+independent RFC 3711 composition of OpenSSL's AES-128 and Python's HMAC-SHA1
+(tests/srtp_lib.py): every forwarded packet of a configs[1] trace, with one
+transport per (room, subscriber), some DownTracks unbound, over several
+batches (rollover state carried across batches)."""
+import importlib
+
+import numpy as np
+import pytest
+
+from tests import srtp_lib
+from tests.oracle_lib import load as load_oracle
+
+EPOCH = 1700000000 * 10**9
+
+
+def _run(o, workload, tr, nb, check):
+    pkg = importlib.import_module("livekit-server_amd")
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        tmap = srtp_lib.bind_transports(pkg, o.api, h, tr, seed=5)
+        ck = srtp_lib.Checker(tr, tmap)
+        n_prot = n_plain = 0
+        for b in range(nb):
+            workload.queue_events(o.api, h, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(h, pk, n, ar, alen)
+            send = EPOCH + b * 10**9 + 123456789
+            assert o.api["protect"](h, send) == 0
+            rec, arena = pkg.drain_arrays(o.api, h)
+            prot = pkg.drain_protected(o.api, h)
+            assert len(prot) == len(arena) + 16 * len(rec)
+            for i in range(len(rec)) if check == "all" else range(0, len(rec), check):
+                r = rec[i]
+                plain = bytes(arena[r["out_off"]:r["out_off"] + r["out_len"]])
+                exp = ck.expect(r, plain, send)
+                off = int(r["out_off"]) + 16 * i
+                got = bytes(prot[off:off + len(exp)])
+                assert got == exp, (b, i, int(r["dt"]), int(r["ext_sn"]))
+                if int(r["dt"]) in tmap:
+                    n_prot += 1
+                else:
+                    n_plain += 1
+        return n_prot, n_plain, ck.n_roc
+    finally:
+        o.destroy(h)
+
+
+def test_oracle_srtp_matches_openssl(workload):
+    # seed 5: some DownTracks' munged sequence numbers wrap (rollover counter 1)
+    tr = workload.Trace(2, duration_s=4.0, batch_s=1.0, rooms=2, seed=5)
+    n_prot, n_plain, n_roc = _run(load_oracle(), workload, tr, tr.nbatches, check=3)
+    assert n_prot > 1000 and n_plain > 100 and n_roc > 50
+
+
+def test_oracle_srtp_small_batches(workload):
+    tr = workload.Trace(1, duration_s=1.0, batch_s=0.05, rooms=1, seed=4)
+    n_prot, n_plain, _ = _run(load_oracle(), workload, tr, tr.nbatches, check="all")
+    assert n_prot > 100
