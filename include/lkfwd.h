@@ -458,6 +458,46 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
                  uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
                  uint64_t *out_len);
 
+/* ---- padding and blank frames ---------------------- *
+ * One request per DownTrack per call (distinct DownTracks; LKF_EINVAL
+ * otherwise).  Both wait for queued runs and change the DownTrack's
+ * Forwarder/sequencer state, so the next lkf_run continues from it.  The
+ * facts the engine does not track come with the request (LKF_PAD_*), and so
+ * does Forwarder.maybeStart's random start (forwarder.go:1774-1775: SN in
+ * [2^15, 2^15 + 2^14), TS in [2^31, 2^31 + 2^30)), used only by a Forwarder
+ * that has not started.  Output as lkf_out records (pkt = request index,
+ * layer -1) + 16-B aligned wire packets, request order; the pacer's
+ * abs-send-time element is a placeholder (TWCC is the sender's). */
+typedef struct lkf_pad_req {
+  int32_t dt;
+  uint32_t bytes_to_send; /* WritePaddingRTP bytesToSend (ignored by lkf_blank_frames) */
+  uint32_t flags;         /* LKF_PAD_* */
+  uint32_t start_sn;      /* maybeStart's random sequence number (16 bits) */
+  uint32_t start_ts;      /* maybeStart's random timestamp */
+  uint32_t reserved;
+} lkf_pad_req;
+#define LKF_PAD_ON_MUTE 0x1      /* WritePaddingRTP paddingOnMute */
+#define LKF_PAD_FORCE_MARKER 0x2 /* WritePaddingRTP forceMarker */
+#define LKF_PAD_WRITABLE 0x4     /* d.writable (bound and not closed) */
+#define LKF_PAD_RR_SEEN 0x8      /* rtpStats.LastReceiverReportTime() is set (an RTCP RR arrived) */
+/* DownTrack.WritePaddingRTP (downtrack.go:764-859): video only, the
+ * mute/RR/active gates, ceil(bytes / 275) padding-only packets of 255 bytes
+ * (Forwarder.GetSnTsForPadding forwarder.go:1798-1813 ->
+ * RTPMunger.UpdateAndGetPaddingSnTs rtpmunger.go:288-346), registered with
+ * sequencer.pushPadding (sequencer.go:211-261) so NACKs for them are
+ * dropped.  bytes_sent[i] = request i's return value (0: nothing sent). */
+int lkf_padding(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
+                uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len, uint32_t *bytes_sent);
+/* One tick of DownTrack.writeBlankFrameRTP (downtrack.go:1307-1401) per
+ * request: Forwarder.GetSnTsForBlankFrames(frameRate, 1) (forwarder.go:
+ * 1815-1839; 30 fps video, 50 audio; one more packet to end an open frame)
+ * and the codec's blank frame — Opus silence, VP8 padding descriptor
+ * (GetPadding :1841, VP8.UpdateAndGetPadding vp8.go:304-363) + 8x8 key frame,
+ * H.264 STAP-A 2x2 key frame; other codecs send nothing.  Counted by
+ * sendingPacket (lkf_downtrack_summaries).  No E2EE trailer. */
+int lkf_blank_frames(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
+                     uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len);
+
 /* ---- SRTP protect ----------------------------------- *
  * The step after the pacer: writeRTPHeaderExtensions sets abs-send-time
  * (pacer/base.go:71-100), then WriteStream.WriteRTP (base.go:59) protects the

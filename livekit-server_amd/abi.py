@@ -101,6 +101,14 @@ RTX_DTYPE = np.dtype([("ext_sn", "<u8"), ("ext_ts", "<u8"), ("source_sn", "<u2")
 assert RTX_DTYPE.itemsize == 48
 DTS_ACTIVE = 0x1
 DTS_DEFICIENT = 0x2
+# padding / blank frames (lkf_pad_req)
+PAD_REQ_DTYPE = np.dtype([("dt", "<i4"), ("bytes_to_send", "<u4"), ("flags", "<u4"), ("start_sn", "<u4"),
+                          ("start_ts", "<u4"), ("reserved", "<u4")])
+assert PAD_REQ_DTYPE.itemsize == 24
+PAD_ON_MUTE = 0x1
+PAD_FORCE_MARKER = 0x2
+PAD_WRITABLE = 0x4
+PAD_RR_SEEN = 0x8
 
 
 class lkf_track_params(C.Structure):
@@ -356,6 +364,12 @@ def bind_engine_api(lib, prefix):
     api["rtx_emit"] = _bind(lib, prefix + "rtx_emit", C.c_int,
                             [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                              C.c_uint64, P(C.c_uint32), P(C.c_uint64)])
+    api["padding"] = _bind(lib, prefix + "padding", C.c_int,
+                           [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                            P(C.c_uint32), P(C.c_uint64), C.c_void_p])
+    api["blank_frames"] = _bind(lib, prefix + "blank_frames", C.c_int,
+                                [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                 P(C.c_uint32), P(C.c_uint64)])
     api["add_transport"] = _bind(lib, prefix + "add_transport", C.c_int32, [e, P(lkf_transport_params)])
     api["set_downtrack_transport"] = _bind(lib, prefix + "set_downtrack_transport", C.c_int, [e, C.c_int32, C.c_int32])
     api["protect"] = _bind(lib, prefix + "protect", C.c_int, [e, C.c_int64])

@@ -196,6 +196,19 @@ struct lkf_engine {
   uint8_t *dRtxIn = nullptr, *dRtxOut = nullptr;
   uint64_t rtxInCap = 0, rtxOutCap = 0;
 
+  // the sequencers' padding RangeMaps (SeqRM regions) and padding scratch
+  uint8_t *dSrm = nullptr;
+  uint64_t srmStride = 0;
+  uint32_t srmCap = 0;
+  lkf_pad_req *dPadReq = nullptr;
+  uint64_t *dPadOff = nullptr;  // [2 * cap]: record bases, then arena bases
+  uint32_t *dPadCnt = nullptr;  // [2 * cap]: packets, then bytes
+  uint32_t padCap = 0;
+  lkf_out *dPadOut = nullptr;
+  uint64_t padOutCap = 0;
+  uint8_t *dPadArena = nullptr;
+  uint64_t padArenaCap = 0;
+
   // seq lookup scratch
   uint16_t *dSns = nullptr;
   lkf_seq_meta *dSeqOut = nullptr;
@@ -495,6 +508,9 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dRm, size_t(c.max_downtracks) * kRangeCap));
   A(dalloc(&e->dVc, c.max_downtracks));
   A(dalloc(&e->dSeq, size_t(c.max_downtracks) * c.seq_size));
+  e->srmCap = seqrm_cap(c.seq_size);
+  e->srmStride = seqrm_stride(e->srmCap);
+  A(dalloc(&e->dSrm, size_t(c.max_downtracks) * e->srmStride));
   A(dalloc(&e->dCum, kStatsWords));
   A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
@@ -596,7 +612,9 @@ void lkf_destroy(lkf_engine *e) {
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   for (void *p : {static_cast<void *>(e->dNacks), static_cast<void *>(e->dNackG), static_cast<void *>(e->dNackValid),
                   static_cast<void *>(e->dRtx), static_cast<void *>(e->dRtxSrc), static_cast<void *>(e->dRtxLen),
-                  static_cast<void *>(e->dRtxOff), static_cast<void *>(e->dRtxIn), static_cast<void *>(e->dRtxOut)})
+                  static_cast<void *>(e->dRtxOff), static_cast<void *>(e->dRtxIn), static_cast<void *>(e->dRtxOut),
+                  static_cast<void *>(e->dSrm), static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff),
+                  static_cast<void *>(e->dPadCnt), static_cast<void *>(e->dPadOut), static_cast<void *>(e->dPadArena)})
     if (p) (void)hipFree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
@@ -1052,6 +1070,9 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.vc = e->dVc;
   d.seq = e->dSeq;
   d.seqSize = e->cfg.seq_size;
+  d.srm = e->dSrm;
+  d.srmStride = e->srmStride;
+  d.srmCap = e->srmCap;
   d.pkts = e->curPkts;
   d.tBegin = x.dTBegin;
   d.tEnd = x.dTEnd;
@@ -1471,7 +1492,8 @@ int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, i
   if (n) HIPCHK(hipMemcpy(e->dSns, sns, n * sizeof(uint16_t), hipMemcpyHostToDevice), "sns copy");
   rc = upload_done(e);
   if (rc) return rc;
-  HIPCHK(launch_seq_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, uint32_t(dt), e->dSns, n, now_ns / 1000000,
+  HIPCHK(launch_seq_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, e->dSrm, e->srmStride, e->srmCap, uint32_t(dt),
+                           e->dSns, n, now_ns / 1000000,
                            e->dSeqOut, e->dSeqN),
          "seq lookup");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
@@ -1538,7 +1560,8 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
   HIPCHK(hipMemcpy(e->dNackG, gb.data(), gb.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "groups copy");
   rc = upload_done(e);
   if (rc) return rc;
-  HIPCHK(launch_rtx_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, e->dNacks, e->dNackG,
+  HIPCHK(launch_rtx_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, e->dSrm, e->srmStride, e->srmCap, e->dNacks,
+                           e->dNackG,
                            uint32_t(gStart.size()), now_ns / 1000000, e->dRtx, e->dNackValid),
          "rtx lookup");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
@@ -1630,6 +1653,138 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
     o.layer = rtx[i].meta.layer;
   }
   return LKF_OK;
+}
+
+// ---- padding / blank frames (downtrack.go:764-859, :1307-1401) -------------
+// Worst-case space per request is reserved (padding: ceil(bytes / 275)
+// packets of at most 12 + 8 + 255 bytes; blank: two packets of at most
+// 12 + 8 + 80), the kernel fills what it sends, the host packs it.
+static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out,
+                      uint8_t *arena, uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len,
+                      uint32_t *bytes_sent) {
+  if (!e || !n_out || !arena_len || (n && !reqs)) return LKF_EINVAL;
+  *n_out = 0;
+  *arena_len = 0;
+  if (!n) return LKF_OK;
+  std::vector<uint8_t> seen(e->dtp.size(), 0);
+  std::vector<uint64_t> off(2 * size_t(n));
+  uint64_t recs = 0, bytes = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t dt = reqs[i].dt;
+    if (dt < 0 || dt >= int32_t(e->dtp.size()) || seen[dt]) return LKF_EINVAL;
+    seen[dt] = 1;
+    const uint64_t np = !e->active[dt] ? 0 : blank ? 2 : (uint64_t(reqs[i].bytes_to_send) + 274) / 275;
+    off[i] = recs;
+    off[n + i] = bytes;
+    recs += np;
+    bytes += np * (blank ? 112 : 288);
+  }
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  if (n > e->padCap) {
+    for (void *p : {static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff), static_cast<void *>(e->dPadCnt)})
+      if (p) (void)hipFree(p);
+    e->padCap = std::max<uint32_t>(n, 1024);
+    HIPCHK(dalloc(&e->dPadReq, e->padCap), "alloc pad reqs");
+    HIPCHK(dalloc(&e->dPadOff, 2 * size_t(e->padCap)), "alloc pad offsets");
+    HIPCHK(dalloc(&e->dPadCnt, 2 * size_t(e->padCap)), "alloc pad counts");
+  }
+  if (recs > e->padOutCap) {
+    if (e->dPadOut) (void)hipFree(e->dPadOut);
+    e->padOutCap = std::max<uint64_t>(recs, 4096);
+    HIPCHK(dalloc(&e->dPadOut, e->padOutCap), "alloc pad out");
+  }
+  if (bytes > e->padArenaCap) {
+    if (e->dPadArena) (void)hipFree(e->dPadArena);
+    e->padArenaCap = std::max<uint64_t>(bytes, 1 << 20);
+    HIPCHK(dalloc(&e->dPadArena, e->padArenaCap), "alloc pad arena");
+  }
+  // a removed DownTrack sends nothing: its request is dropped before the kernel
+  std::vector<lkf_pad_req> q(reqs, reqs + n);
+  std::vector<uint32_t> live;
+  for (uint32_t i = 0; i < n; i++)
+    if (e->active[q[i].dt]) live.push_back(i);
+  std::vector<lkf_pad_req> lq(live.size());
+  std::vector<uint64_t> loff(2 * live.size());
+  for (size_t j = 0; j < live.size(); j++) {
+    lq[j] = q[live[j]];
+    loff[j] = off[live[j]];
+    loff[live.size() + j] = off[n + live[j]];
+  }
+  const uint32_t m = uint32_t(live.size());
+  std::vector<uint32_t> cnt(2 * size_t(m), 0);
+  if (m) {
+    HIPCHK(hipMemcpy(e->dPadReq, lq.data(), m * sizeof(lkf_pad_req), hipMemcpyHostToDevice), "pad req copy");
+    HIPCHK(hipMemcpy(e->dPadOff, loff.data(), 2 * size_t(m) * sizeof(uint64_t), hipMemcpyHostToDevice), "pad off copy");
+    rc = upload_done(e);
+    if (rc) return rc;
+    PadLaunch a;
+    a.blank = blank;
+    a.n = m;
+    a.reqs = e->dPadReq;
+    a.nowNs = now_ns;
+    a.hot = e->dHot;
+    a.dts = e->dDTs;
+    a.tracks = e->dTracks;
+    a.rm = e->dRm;
+    a.seq = e->dSeq;
+    a.seqSize = e->cfg.seq_size;
+    a.srm = e->dSrm;
+    a.srmStride = e->srmStride;
+    a.srmCap = e->srmCap;
+    a.dtCum = e->dDTCum;
+    a.recOff = e->dPadOff;
+    a.byteOff = e->dPadOff + m;
+    a.out = e->dPadOut;
+    a.arena = e->dPadArena;
+    a.cnt = e->dPadCnt;
+    a.bytes = e->dPadCnt + m;
+    HIPCHK(launch_pad(e->own, a), "pad");
+    HIPCHK(hipStreamSynchronize(e->own), "sync");
+    HIPCHK(hipMemcpy(cnt.data(), e->dPadCnt, 2 * size_t(m) * sizeof(uint32_t), hipMemcpyDeviceToHost), "pad cnt copy");
+  }
+  if (bytes_sent)
+    for (uint32_t i = 0; i < n; i++) bytes_sent[i] = 0;
+  uint64_t k = 0, tot = 0;
+  for (uint32_t j = 0; j < m; j++) {
+    k += cnt[j];
+    if (bytes_sent) bytes_sent[live[j]] = cnt[m + j];
+  }
+  std::vector<lkf_out> recv(recs ? recs : 1);
+  std::vector<uint8_t> arv(bytes ? bytes : 1);
+  if (k) {
+    HIPCHK(hipMemcpy(recv.data(), e->dPadOut, recs * sizeof(lkf_out), hipMemcpyDeviceToHost), "pad out copy");
+    HIPCHK(hipMemcpy(arv.data(), e->dPadArena, bytes, hipMemcpyDeviceToHost), "pad arena copy");
+  }
+  for (uint32_t j = 0; j < m; j++)
+    for (uint32_t c = 0; c < cnt[j]; c++) tot += (uint64_t(recv[loff[j] + c].out_len) + 15) & ~uint64_t(15);
+  *n_out = uint32_t(k);
+  *arena_len = tot;
+  if (k > out_cap || tot > arena_cap || (k && (!out || !arena))) return LKF_ENOSPC;
+  uint64_t w = 0, pos = 0;
+  for (uint32_t j = 0; j < m; j++)
+    for (uint32_t c = 0; c < cnt[j]; c++) {
+      lkf_out o = recv[loff[j] + c];
+      const uint64_t al = (uint64_t(o.out_len) + 15) & ~uint64_t(15);
+      std::memcpy(arena + pos, arv.data() + o.out_off, al);
+      o.out_off = pos;
+      o.pkt = live[j];
+      out[w++] = o;
+      pos += al;
+    }
+  return LKF_OK;
+}
+
+int lkf_padding(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
+                uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len, uint32_t *bytes_sent) {
+  return pad_common(e, 0, reqs, n, now_ns, out, arena, out_cap, arena_cap, n_out, arena_len, bytes_sent);
+}
+
+int lkf_blank_frames(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
+                     uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len) {
+  return pad_common(e, 1, reqs, n, now_ns, out, arena, out_cap, arena_cap, n_out, arena_len, nullptr);
 }
 
 int lkf_last_timings(lkf_engine *e, float *decide_ms, float *emit_ms, float *total_ms) {

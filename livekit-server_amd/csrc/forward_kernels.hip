@@ -192,6 +192,8 @@ struct Lane {
   i32 *missVal;
   SeqMeta *seq;
   u32 seqSize;
+  SeqRM *srm;  // the sequencer's RangeMap region (read only with F_SEQ_RM)
+  u32 srmCap;
   // track
   u32 kind, codec, hasRefTS, clockRate;
   const u32 *offs;
@@ -705,7 +707,7 @@ __device__ __forceinline__ void fw_resync(Lane &L) {  // :1391-1397
   L.h.lastSSRC = 0;
   if (hasf(L, F_PUBMUTED)) setf(L, F_RESUME_BEHIND, true);
 }
-__device__ void apply_ctl(Lane &L, const DevEvent &ev) {
+__device__ __forceinline__ void apply_ctl(Lane &L, const DevEvent &ev) {
   const bool video = hasf(L, F_VIDEO);
   switch (ev.op) {
     case LKF_CTL_MUTE: {  // :377-413
@@ -1082,8 +1084,94 @@ __device__ __forceinline__ void seq_invalidate(Lane &L, u32 n) {
     store_rec(L.seq + x, z);
   }
 }
-// sequencer.push sequencer.go:123-209 (no padding exclusions on this path: the
-// sequencer's RangeMap stays at value 0, so slot = extModifiedSN % size)
+// ---- the sequencer's RangeMap (SeqRM): serial forms, one thread or every
+// lane of a wave with the same arguments.  Written only by pushPadding.
+__device__ __forceinline__ RangeEntry *srm_ring(SeqRM *h) { return reinterpret_cast<RangeEntry *>(h + 1); }
+// GetValue rangemap.go:134-169
+__device__ bool srm_get(SeqRM *h, u32 cap, u64 key, u64 &out) {
+  out = 0;
+  if (key >= h->openStart) {
+    out = h->openValue;
+    return true;
+  }
+  const u32 nc = h->count;
+  const RangeEntry *ring = srm_ring(h);
+  if (nc == 0 || key < ring[h->head].start) return false;  // too old
+  for (i32 idx = i32(nc); idx >= 0; idx--) {
+    u64 start = h->openStart;
+    if (idx != i32(nc)) {
+      const RangeEntry rv = ring[(h->head + u32(idx)) % cap];
+      if ((key - rv.start) < HALF64 && (rv.end - key) < HALF64) {
+        out = rv.value;
+        return true;
+      }
+      start = rv.start;
+    }
+    if (idx > 0) {
+      const RangeEntry pv = ring[(h->head + u32(idx) - 1) % cap];
+      const u64 before = key - pv.end, after = start - key;
+      if (before > 0 && before < HALF64 && after > 0 && after < HALF64) return false;  // excluded
+    }
+  }
+  return false;
+}
+// ExcludeRange rangemap.go:100-132 (prune :171: the newest cap closed ranges)
+__device__ bool srm_exclude(SeqRM *h, u32 cap, u64 s, u64 e, bool store) {
+  if (e == s || (e - s) > HALF64) return false;
+  if (h->openStart > s) return false;
+  const u64 nv = h->openValue + (e - s);
+  if (h->openStart == s) {
+    if (store) {
+      h->openStart = e;
+      h->openValue = nv;
+    }
+    return true;
+  }
+  if (store) {
+    RangeEntry c;
+    c.start = h->openStart;
+    c.end = s - 1;
+    c.value = h->openValue;
+    RangeEntry *ring = srm_ring(h);
+    if (h->count < cap) {
+      ring[(h->head + h->count) % cap] = c;
+      h->count++;
+    } else {
+      ring[h->head] = c;
+      h->head = (h->head + 1) % cap;
+    }
+    h->openStart = e;
+    h->openValue = nv;
+  }
+  return true;
+}
+// sequencer.push with padding exclusions (F_SEQ_RM, rare: out of line so the
+// decide kernel keeps its registers): on the first push the sequencer's
+// snOffset (updateSNOffset sequencer.go:136) and the adjusted slot of esn;
+// then extModifiedSNAdjusted / extHighestSNAdjusted (sequencer.go:160-176).
+// false = the push is dropped (an excluded or too-old SN).
+__device__ __noinline__ bool srm_push_adjust(SeqRM *h, u32 cap, u32 size, bool init, u64 esn, u64 highest, u64 &adjM,
+                                             u64 &adjH, u32 &initSlot) {
+  u64 snOff = h->snOffset;
+  if (init) {
+    u64 off = 0;
+    if (srm_get(h, cap, esn + 1, off)) snOff = off;
+    if (lane_id() == 0) h->snOffset = snOff;
+    initSlot = u32((esn - snOff) % size);
+  }
+  adjH = highest - snOff;
+  adjM = esn - snOff;
+  if (esn < highest) {
+    u64 off = 0;
+    if (!srm_get(h, cap, esn, off)) return false;
+    adjM = esn - off;
+  }
+  return true;
+}
+
+// sequencer.push sequencer.go:123-209.  Without padding exclusions (F_SEQ_RM
+// clear) the sequencer's RangeMap maps everything to 0: slot = extModifiedSN
+// % size, kept as seqHighSlot + the distance to the highest SN.
 __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, u64 cb,
                          int cbLen) {
   const u32 size = L.seqSize;
@@ -1107,7 +1195,8 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     return;
   }
 
-  if (!hasf(L, F_SEQ_INIT)) {
+  const bool init = !hasf(L, F_SEQ_INIT);
+  if (init) {
     setf(L, F_SEQ_INIT, true);
     L.h.seqExtStartSN = esn;
     L.h.seqExtHighestSN = esn;
@@ -1115,8 +1204,13 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     L.h.seqHighSlot = u16(esn % size);  // once per DownTrack lifetime
   }
   if (esn < L.h.seqExtStartSN) return;
-  const u64 adjH = L.h.seqExtHighestSN;
-  const u64 adjM = esn;
+  u64 adjH = L.h.seqExtHighestSN;
+  u64 adjM = esn;
+  if (hasf(L, F_SEQ_RM)) {  // padding was sent on this DownTrack
+    u32 initSlot = 0;
+    if (!srm_push_adjust(L.srm, L.srmCap, size, init, esn, L.h.seqExtHighestSN, adjM, adjH, initSlot)) return;
+    if (init) L.h.seqHighSlot = u16(initSlot);
+  }
   const i64 delta = i64(adjM - adjH);
   if (delta <= -i64(size)) return;
   // slot of adjM from the highest slot without a 64-bit modulo
@@ -1368,6 +1462,9 @@ struct DecideArgs {
   VP8Cold *vc;
   SeqMeta *seq;
   u32 seqSize;
+  u8 *srm;  // SeqRM regions (stride srmStride), read with F_SEQ_RM
+  u64 srmStride;
+  u32 srmCap;
   const lkf_pkt *pkts;
   const u32 *tBegin, *tEnd;
   const u64 *slotBase;
@@ -1829,6 +1926,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __syncthreads();
   L.seq = A.seq + size_t(d) * A.seqSize;
   L.seqSize = A.seqSize;
+  L.srm = reinterpret_cast<SeqRM *>(A.srm + size_t(d) * A.srmStride);
+  L.srmCap = A.srmCap;
   const DevTrack &tk = A.tracks[track];
   L.kind = tk.kind;
   L.codec = tk.codec;
@@ -2833,12 +2932,31 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
   }
 }
 
+// getExtPacketMetas sequencer.go:277-300: the ring slot of NACKed sn, or -1
+// (out of order from the head, an excluded padding SN, or too old).  Without
+// padding exclusions slot = extSN % size = seqHighSlot - (highest - extSN).
+__device__ int seq_find(const DTHot &h, SeqRM *srm, u32 cap, u32 size, u16 sn, u64 &extSN) {
+  const u16 highestSN = u16(h.seqExtHighestSN);
+  if (u16(highestSN - sn) > (1 << 15)) return -1;
+  extSN = u64(sn) + (h.seqExtHighestSN & 0xFFFFFFFFFFFF0000ull);
+  if (sn > highestSN) extSN -= (1ull << 16);
+  u64 off = 0, snOff = 0;
+  if (h.flags & F_SEQ_RM) {
+    if (!srm_get(srm, cap, extSN, off)) return -1;
+    snOff = srm->snOffset;
+  }
+  const u64 dist = (h.seqExtHighestSN - snOff) - (extSN - off);
+  if (dist >= u64(size)) return -1;
+  const i32 sl = i32(h.seqHighSlot) - i32(dist);
+  return sl < 0 ? sl + i32(size) : sl;
+}
+
 // ---------------------------------------------------------------------------
 // sequencer.getExtPacketMetas sequencer.go:263-332 for one DownTrack (RTX
 // lookup; one lane, serial over the NACKed sequence numbers).
 // ---------------------------------------------------------------------------
-__global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u32 d, const u16 *sns, u32 n, i64 nowMs,
-                             lkf_seq_meta *out, u32 *nOut) {
+__global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u8 *srmBase, u64 srmStride, u32 srmCap, u32 d,
+                             const u16 *sns, u32 n, i64 nowMs, lkf_seq_meta *out, u32 *nOut) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   DTHot h = hot[d];
   SeqMeta *seq = seqBase + size_t(d) * seqSize;
@@ -2846,18 +2964,14 @@ __global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u32 d, c
   if (h.flags & F_SEQ_INIT) {
     const u32 rtt = 70;  // defaultRtt (setRTT is out of scope)
     const u32 refTime = u32(nowMs - h.seqStartMs);
-    const u16 highestSN = u16(h.seqExtHighestSN);
     const u32 highestTS = u32(h.seqExtHighestTS);
+    SeqRM *srm = reinterpret_cast<SeqRM *>(srmBase + size_t(d) * srmStride);
     for (u32 i = 0; i < n; i++) {
       const u16 sn = sns[i];
-      if (u16(highestSN - sn) > (1 << 15)) continue;
-      u64 extSN = u64(sn) + (h.seqExtHighestSN & 0xFFFFFFFFFFFF0000ull);
-      if (sn > highestSN) extSN -= (1ull << 16);
-      // video sequencers have a RangeMap at value 0 (GetValue fails only for
-      // keys below its start 0 -> never); audio has none.
-      const u64 adj = extSN, adjH = h.seqExtHighestSN;
-      if (adjH - adj >= u64(seqSize)) continue;
-      SeqMeta &m = seq[adj % seqSize];
+      u64 extSN = 0;
+      const int slot = seq_find(h, srm, srmCap, seqSize, sn, extSN);
+      if (slot < 0) continue;
+      SeqMeta &m = seq[slot];
       const bool invalid = m.sourceSeqNo == 0 && m.targetSeqNo == 0 && m.lastNack == 0;
       if (m.targetSeqNo != sn || invalid) continue;
       const u32 lim = (2 * rtt < 100) ? 2 * rtt : 100;
@@ -2892,8 +3006,8 @@ __global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u32 d, c
 // records it returns).  FilterRTX layers (forwarder.go:1424-1432) from the
 // DownTrack's state; out[k]/valid[k] per NACK entry (compacted on the host).
 // ---------------------------------------------------------------------------
-__global__ void k_rtx_lookup(const DTHot *__restrict__ hot, SeqMeta *seqBase, u32 seqSize,
-                             const lkf_nack *__restrict__ nacks, const u32 *__restrict__ gStart, u32 ngroups, i64 nowMs,
+__global__ void k_rtx_lookup(const DTHot *__restrict__ hot, SeqMeta *seqBase, u32 seqSize, u8 *srmBase,
+                             u64 srmStride, u32 srmCap, const lkf_nack *__restrict__ nacks, const u32 *__restrict__ gStart, u32 ngroups, i64 nowMs,
                              lkf_rtx *__restrict__ out, u32 *__restrict__ valid) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngroups) return;
@@ -2906,16 +3020,16 @@ __global__ void k_rtx_lookup(const DTHot *__restrict__ hot, SeqMeta *seqBase, u3
   const i32 curS = h.curS, tgtS = h.tgtS;
   const u32 rtt = 70;  // defaultRtt (setRTT is out of scope)
   const u32 refTime = u32(nowMs - h.seqStartMs);
-  const u16 highestSN = u16(h.seqExtHighestSN);
   const u32 highestTS = u32(h.seqExtHighestTS);
+  SeqRM *srm = reinterpret_cast<SeqRM *>(srmBase + size_t(d) * srmStride);
   for (u32 k = b; k < e; k++) {
     u32 ok = 0;
     const u16 sn = nacks[k].sn;
-    if ((h.flags & F_SEQ_INIT) && u16(highestSN - sn) <= (1 << 15)) {
-      u64 extSN = u64(sn) + (h.seqExtHighestSN & 0xFFFFFFFFFFFF0000ull);
-      if (sn > highestSN) extSN -= (1ull << 16);
-      if (h.seqExtHighestSN - extSN < u64(seqSize)) {
-        SeqMeta &m = seq[extSN % seqSize];
+    u64 extSN = 0;
+    const int slot = (h.flags & F_SEQ_INIT) ? seq_find(h, srm, srmCap, seqSize, sn, extSN) : -1;
+    if (slot >= 0) {
+      {
+        SeqMeta &m = seq[slot];
         const bool invalid = m.sourceSeqNo == 0 && m.targetSeqNo == 0 && m.lastNack == 0;
         const u32 lim = (2 * rtt < 100) ? 2 * rtt : 100;
         if (m.targetSeqNo == sn && !invalid && m.nacked < 3 && u32(refTime - m.lastNack) > lim) {
@@ -2949,11 +3063,373 @@ __global__ void k_rtx_lookup(const DTHot *__restrict__ hot, SeqMeta *seqBase, u3
   }
 }
 
-hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, u32 seqSize, const lkf_nack *nacks,
-                             const u32 *gStart, u32 ngroups, i64 nowMs, lkf_rtx *out, u32 *valid) {
+hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, u32 seqSize, u8 *srm, u64 srmStride,
+                             u32 srmCap, const lkf_nack *nacks, const u32 *gStart, u32 ngroups, i64 nowMs, lkf_rtx *out,
+                             u32 *valid) {
   if (!ngroups) return hipSuccess;
-  hipLaunchKernelGGL(k_rtx_lookup, dim3((ngroups + 63) / 64), dim3(64), 0, s, hot, seq, seqSize, nacks, gStart, ngroups,
-                     nowMs, out, valid);
+  hipLaunchKernelGGL(k_rtx_lookup, dim3((ngroups + 63) / 64), dim3(64), 0, s, hot, seq, seqSize, srm, srmStride, srmCap,
+                     nacks, gStart, ngroups, nowMs, out, valid);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Padding and blank frames: DownTrack.WritePaddingRTP
+// (downtrack.go:764-859) and one tick of writeBlankFrameRTP (:1307-1401) for
+// many DownTracks at once, one wave per request (distinct DownTracks).  The
+// DownTrack's state is staged in LDS like a decide wave's; the munger's
+// RangeMap ring is used in place (a control-rate path).
+// ---------------------------------------------------------------------------
+__constant__ u8 kVP8KeyFrame8x8[31] = {0x10, 0x02, 0x00, 0x9d, 0x01, 0x2a, 0x08, 0x00, 0x08, 0x00, 0x00,
+                                        0x47, 0x08, 0x85, 0x85, 0x88, 0x85, 0x84, 0x88, 0x02, 0x02, 0x00,
+                                        0x0c, 0x0d, 0x60, 0x00, 0xfe, 0xff, 0xab, 0x50, 0x80};  // downtrack.go:91-96
+// STAP-A of H264KeyFrame2x2 SPS, PPS, IDR (downtrack.go:98-110, getH264BlankFrame :1456-1472)
+__constant__ u8 kH264Blank[47] = {0x18, 0x00, 0x18, 0x67, 0x42, 0xc0, 0x1f, 0x0f, 0xd9, 0x1f, 0x88, 0x88, 0x84,
+                                  0x00, 0x00, 0x03, 0x00, 0x04, 0x00, 0x00, 0x03, 0x00, 0xc8, 0x3c, 0x60, 0xc9,
+                                  0x20, 0x00, 0x06, 0x68, 0x87, 0xcb, 0x83, 0xcb, 0x20, 0x00, 0x0a, 0x65, 0x88,
+                                  0x84, 0x0a, 0xf2, 0x62, 0x80, 0x00, 0xa7, 0xbe};
+constexpr int kOpusSilenceLen = 80;  // OpusSilenceFrame downtrack.go:112-123: f8 ff fe, then zeros
+constexpr u32 kPadPayload = 255;     // RTPPaddingMaxPayloadSize downtrack.go:63
+constexpr u32 kPadEstHdr = 20;       // RTPPaddingEstimatedHeaderSize downtrack.go:64
+
+// RangeMap.DecValue rangemap.go:70-88 (munger ring, prune as rm_exclude)
+__device__ void rm_dec(Lane &L, u64 end, u64 dec) {
+  if (L.h.rmOpenStart > end) {
+    L.h.rmOpenValue -= dec;
+    return;
+  }
+  RangeEntry c;
+  c.start = L.h.rmOpenStart;
+  c.end = end;
+  c.value = L.h.rmOpenValue;
+  if (L.h.rmCount < kRangeCap) {
+    const int idx = (int(L.h.rmHead) + int(L.h.rmCount)) % kRangeCap;
+    if (lane_id() == 0) L.rm[idx] = c;
+    L.h.rmCount++;
+  } else {
+    if (lane_id() == 0) L.rm[L.h.rmHead] = c;
+    L.h.rmHead = u16((L.h.rmHead + 1) % kRangeCap);
+  }
+  L.h.rmOpenStart = end + 1;
+  L.h.rmOpenValue = c.value - dec;
+}
+// RTPMunger.UpdateAndGetPaddingSnTs rtpmunger.go:288-346.  ts[0..1]: the
+// timestamps of the first two packets (frameRate != 0 only with num <= 2);
+// every timestamp is extLastTS for frameRate 0.  false: not on a frame boundary.
+__device__ bool mg_padding(Lane &L, u32 num, u32 clockRate, u32 frameRate, bool forceMarker, u64 extRtpTS,
+                           u64 ts[2]) {
+  if (num == 0) return true;
+  bool useLast = false;
+  u32 tsOff = 0;
+  if (!hasf(L, F_LAST_MARKER)) {
+    if (!forceMarker) return false;
+    useLast = true;
+    tsOff = 1;
+  }
+  const u64 lastTS = L.h.extLastTS;
+  u64 eLastTS = lastTS;
+  ts[0] = ts[1] = lastTS;
+  if (frameRate != 0) {
+    for (u32 i = 0; i < num && i < 2; i++) {
+      if (useLast && i == 0) {
+        ts[i] = lastTS;
+      } else {
+        u64 ets = extRtpTS + u64((u32(u32(i + 1 - tsOff) * clockRate) + frameRate - 1) / frameRate);
+        if (i64(ets - eLastTS) <= 0) ets = eLastTS + 1;
+        eLastTS = ets;
+        ts[i] = ets;
+      }
+    }
+  }
+  const u64 eLastSN = L.h.extLastSN + num;
+  L.h.extSecondLastSN = eLastSN - 1;
+  L.h.extLastSN = eLastSN;
+  rm_dec(L, L.h.extHighestIncomingSN, num);
+  mg_updateSnOffset(L);
+  L.h.extSecondLastTS = (num == 1 || frameRate == 0) ? lastTS : ts[num - 2];  // (frameRate 0: all lastTS)
+  L.h.tsOffset -= eLastTS - lastTS;
+  L.h.extLastTS = eLastTS;
+  if (forceMarker) setf(L, F_LAST_MARKER, true);
+  return true;
+}
+// Forwarder.maybeStart forwarder.go:1766-1796 (the random start comes with the request)
+__device__ void fw_maybeStart(Lane &L, i64 now, u64 startSN, u64 startTS) {
+  if (hasf(L, F_STARTED)) return;
+  setf(L, F_STARTED, true);
+  L.h.preStartTime = now;
+  mg_setLastSnTs(L, startSN, startTS);
+  L.h.extFirstTS = startTS;
+}
+// sequencer.pushPadding sequencer.go:211-261 (video DownTracks: the sequencer
+// has its RangeMap).  One thread; the caller syncs the wave after it.
+__device__ void seq_push_padding(Lane &L, u64 s, u64 e) {
+  const u32 size = L.seqSize;
+  const bool rmOn = hasf(L, F_SEQ_RM);
+  const u64 snOff = rmOn ? L.srm->snOffset : 0;
+  const u64 hi = L.h.seqExtHighestSN;
+  if (s <= hi) {  // before what is already sequenced: invalidate those slots
+    for (u64 sn = s; sn != e + 1; sn++) {
+      const i64 diff = i64(sn - hi);
+      if (diff >= 0 || diff < -i64(size)) continue;
+      u64 off = 0;
+      if (rmOn && !srm_get(L.srm, L.srmCap, sn, off)) continue;
+      const u64 dist = (hi - snOff) - (sn - off);
+      if (dist >= u64(size)) continue;
+      i32 sl = i32(L.h.seqHighSlot) - i32(dist);
+      if (sl < 0) sl += i32(size);
+      L.seq[sl] = SeqMeta{};
+    }
+    return;
+  }
+  if (!rmOn) {  // first exclusion: the identity map (NewRangeMap: open range [0, inf) -> 0)
+    L.srm->openStart = 0;
+    L.srm->openValue = 0;
+    L.srm->snOffset = 0;
+    L.srm->head = L.srm->count = 0;
+  }
+  if (!srm_exclude(L.srm, L.srmCap, s, e + 1, true)) return;
+  u64 nOff = snOff;
+  if (srm_get(L.srm, L.srmCap, e + 1, nOff)) L.srm->snOffset = nOff;  // updateSNOffset
+  nOff = L.srm->snOffset;
+  if (hasf(L, F_SEQ_INIT)) {  // the slot of the (adjusted) highest SN moves with it
+    const u64 mv = u64((e - nOff) - (hi - snOff)) % size;
+    L.h.seqHighSlot = u16((u64(L.h.seqHighSlot) + mv) % size);
+  }
+  L.h.seqExtHighestSN = e;
+  setf(L, F_SEQ_RM, true);
+}
+// codecmunger.VP8.UpdateAndGetPadding vp8.go:304-363 -> marshalled descriptor
+__device__ int vp8_padding(Lane &L, bool newPicture, u64 &out) {
+  const i32 offset = newPicture ? 1 : 0;
+  const bool picUsed = hasf(L, F_PICID_USED), tl0Used = hasf(L, F_TL0_USED), tidUsed = hasf(L, F_TID_USED),
+             keyUsed = hasf(L, F_KEYIDX_USED);
+  int hs = 1;
+  if (picUsed || tl0Used || tidUsed || keyUsed) hs += 1;
+  i32 ext = L.h.extLastPictureId;
+  if (picUsed) {
+    ext = L.h.extLastPictureId + offset;
+    L.h.extLastPictureId = ext;
+    L.h.pictureIdOffset -= offset;
+    hs += ((ext & 0x7fff) > 127) ? 2 : 1;
+  }
+  const u16 pid = u16(ext & 0x7fff);
+  u8 tl0 = 0;
+  if (tl0Used) {
+    tl0 = u8(L.h.lastTl0 + offset);
+    L.h.lastTl0 = tl0;
+    L.h.tl0Off = u8(L.h.tl0Off - offset);
+    hs += 1;
+  }
+  if (tidUsed || keyUsed) hs += 1;
+  u8 key = 0;
+  if (keyUsed) {
+    key = u8((L.h.lastKeyIdx + offset) & 0x1f);
+    L.h.lastKeyIdx = key;
+    L.h.keyIdxOff = u8(L.h.keyIdxOff - offset);
+  }
+  return vp8_marshal(0x10, picUsed, pid > 127, pid, tl0Used, tl0, tidUsed, 0, true, keyUsed, key, hs, out);
+}
+
+struct PadArgs {
+  int blank;
+  u32 n;
+  const lkf_pad_req *reqs;
+  i64 nowNs;
+  DTHot *hot;
+  const DevDT *dts;
+  const DevTrack *tracks;
+  RangeEntry *rm;
+  SeqMeta *seq;
+  u32 seqSize;
+  u8 *srm;
+  u64 srmStride;
+  u32 srmCap;
+  DTCum *dtCum;
+  const u64 *recOff, *byteOff;
+  lkf_out *out;
+  u8 *arena;
+  u32 *cnt, *bytes;
+};
+
+// RTP header of a padding / blank packet (pion Header.MarshalTo; pacer
+// writeRTPHeaderExtensions pacer/base.go:71-100: abs-send-time placeholder)
+__device__ int pad_header(u8 *w, bool padding, bool marker, const DevDT &dt, u64 sn, u64 ts) {
+  w[0] = u8(0x80 | (padding ? 0x20 : 0) | (dt.extAbs ? 0x10 : 0));
+  w[1] = u8((marker ? 0x80 : 0) | (dt.pt & 0x7f));
+  w[2] = u8(sn >> 8);
+  w[3] = u8(sn);
+  w[4] = u8(ts >> 24);
+  w[5] = u8(ts >> 16);
+  w[6] = u8(ts >> 8);
+  w[7] = u8(ts);
+  w[8] = u8(dt.ssrc >> 24);
+  w[9] = u8(dt.ssrc >> 16);
+  w[10] = u8(dt.ssrc >> 8);
+  w[11] = u8(dt.ssrc);
+  if (!dt.extAbs) return 12;
+  w[12] = 0xBE;
+  w[13] = 0xDE;
+  w[14] = 0;
+  w[15] = 1;
+  w[16] = u8((dt.extAbs << 4) | 2);
+  w[17] = w[18] = w[19] = 0;
+  return 20;
+}
+__device__ void pad_record(const PadArgs &A, u32 r, u32 k, u32 d, u64 off, u32 len, u64 sn, u64 ts, bool marker) {
+  lkf_out o;
+  o.ext_sn = sn;
+  o.ext_ts = ts;
+  o.out_off = off;
+  o.dt = d;
+  o.pkt = r;
+  o.out_len = u16(len);
+  o.flags = marker ? LKF_OUT_MARKER : 0;
+  o.layer = -1;
+  o.reserved = 0;
+  A.out[A.recOff[r] + k] = o;
+}
+
+#if !LKF_STATE_LDS
+#error "k_pad stages the DownTrack state in LDS (LKF_STATE_LDS=1)"
+#endif
+__global__ void __launch_bounds__(64) k_pad(PadArgs A) {
+  __shared__ __attribute__((aligned(16))) DTHot sHot;
+  const u32 r = blockIdx.x, lane = threadIdx.x;
+  if (r >= A.n) return;
+  const lkf_pad_req q = A.reqs[r];
+  const u32 d = u32(q.dt);
+  reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];
+  __syncthreads();
+  Lane L{sHot};
+  L.rm = A.rm + size_t(d) * kRangeCap;
+  L.rmDirty = false;
+  L.seq = A.seq + size_t(d) * A.seqSize;
+  L.seqSize = A.seqSize;
+  L.srm = reinterpret_cast<SeqRM *>(A.srm + size_t(d) * A.srmStride);
+  L.srmCap = A.srmCap;
+  const DevDT dt = A.dts[d];
+  const DevTrack &tk = A.tracks[dt.track];
+  L.kind = tk.kind;
+  L.codec = tk.codec;
+  L.clockRate = tk.clockRate;
+  const bool onMute = q.flags & LKF_PAD_ON_MUTE;
+  const bool active = hasf(L, F_STATS_INIT);  // rtpStats.IsActive (rtpstats_base.go:308)
+  u32 nPk = 0, nBytes = 0;
+  const u64 ob = A.byteOff[r];
+  if (!A.blank) {
+    bool ok = (q.flags & LKF_PAD_WRITABLE) != 0;
+    if (!active && !onMute) ok = false;
+    if (L.kind == LKF_KIND_AUDIO) ok = false;
+    if (hasf(L, F_MUTED) && !onMute) ok = false;
+    if (!(q.flags & LKF_PAD_RR_SEEN) && !onMute) ok = false;
+    const u32 num = (q.bytes_to_send + kPadPayload + kPadEstHdr - 1) / (kPadPayload + kPadEstHdr);
+    if (num == 0) ok = false;
+    if (ok) {
+      fw_maybeStart(L, A.nowNs, u16(q.start_sn), q.start_ts);  // GetSnTsForPadding forwarder.go:1798-1813
+      const bool force = (q.flags & LKF_PAD_FORCE_MARKER) || L.h.tgtS == INVALID || L.h.tgtT == INVALID;
+      const u64 first = L.h.extLastSN + 1;
+      u64 ts[2];
+      if (mg_padding(L, num, 0, 0, force, 0, ts)) {
+        __syncthreads();
+        if (lane == 0) seq_push_padding(L, first, first + num - 1);
+        __syncthreads();
+        const u32 len = (dt.extAbs ? 20 : 12) + kPadPayload;
+        const u32 stride = (len + 15) & ~15u;
+        for (u32 k = lane; k < num; k += 64) {
+          u8 *w = A.arena + ob + u64(k) * stride;
+          const int h = pad_header(w, true, false, dt, first + k, ts[0]);
+          for (u32 i = 0; i < kPadPayload - 1; i++) w[h + i] = 0;
+          w[h + kPadPayload - 1] = u8(kPadPayload);  // the padding size, that byte included
+          for (u32 i = len; i < stride; i++) w[i] = 0;
+          pad_record(A, r, k, d, ob + u64(k) * stride, len, first + k, ts[0], false);
+        }
+        nPk = num;
+        nBytes = num * (12 + kPadPayload);  // hdr.MarshalSize() + len(payload) (downtrack.go:854)
+      }
+    }
+  } else {
+    const u32 codec = L.codec;
+    bool ok = (q.flags & LKF_PAD_WRITABLE) && active &&
+              (codec == LKF_CODEC_OPUS || codec == LKF_CODEC_VP8 || codec == LKF_CODEC_H264);
+    if (ok) {
+      const u32 frameRate = codec == LKF_CODEC_OPUS ? 50 : 30;
+      fw_maybeStart(L, A.nowNs, u16(q.start_sn), q.start_ts);  // GetSnTsForBlankFrames forwarder.go:1815-1839
+      const bool fen = !hasf(L, F_LAST_MARKER);
+      const u32 num = fen ? 2 : 1;
+      const u64 lastTS = L.h.extLastTS;
+      u64 expTS = lastTS;
+      if (hasf(L, F_HAS_EXPECTED) && active) {  // getExpectedRTPTimestamp downtrack.go:1765
+        const i64 diff = (A.nowNs - L.h.statsFirstTime) * i64(L.clockRate) / 1000000000LL;
+        expTS = L.h.statsExtStartTS + u64(diff);
+      }
+      if (i64(expTS - lastTS) <= 0) expTS = lastTS + 1;
+      const u64 first = L.h.extLastSN + 1;
+      u64 ts[2];
+      mg_padding(L, num, L.clockRate, frameRate, fen, expTS, ts);  // forceMarker = frameEndNeeded: no error
+      u64 off = ob;
+      for (u32 k = 0; k < num; k++) {
+        u64 vd = 0;
+        int vl = 0;
+        if (codec == LKF_CODEC_VP8 && hasf(L, F_VP8)) vl = vp8_padding(L, !(k == 0 && fen), vd);
+        const u32 pl = codec == LKF_CODEC_OPUS ? u32(kOpusSilenceLen) : codec == LKF_CODEC_H264 ? 47u : u32(vl) + 31u;
+        const u32 len = (dt.extAbs ? 20 : 12) + pl;
+        if (lane == 0) {
+          u8 *w = A.arena + off;
+          const int h = pad_header(w, false, true, dt, first + k, ts[k]);
+          for (u32 i = 0; i < pl; i++) {
+            u8 b;
+            if (codec == LKF_CODEC_OPUS)
+              b = i == 0 ? 0xf8 : i == 1 ? 0xff : i == 2 ? 0xfe : 0;
+            else if (codec == LKF_CODEC_H264)
+              b = kH264Blank[i];
+            else
+              b = i < u32(vl) ? u8(vd >> (8 * i)) : kVP8KeyFrame8x8[i - u32(vl)];
+            w[h + i] = b;
+          }
+          for (u32 i = len; i < ((len + 15) & ~15u); i++) w[i] = 0;
+          pad_record(A, r, k, d, off, len, first + k, ts[k], true);
+        }
+        off += (len + 15) & ~15u;
+        nBytes += 12 + pl;  // sendingPacket: hdr.MarshalSize() + len(payload) (downtrack.go:1931-1939)
+      }
+      nPk = num;
+      if (lane == 0) {
+        A.dtCum[d].packets += num;
+        A.dtCum[d].bytes += nBytes;
+      }
+    }
+  }
+  __syncthreads();
+  reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
+  if (lane == 0) {
+    A.cnt[r] = nPk;
+    A.bytes[r] = nBytes;
+  }
+}
+
+hipError_t launch_pad(hipStream_t s, const PadLaunch &a) {
+  if (!a.n) return hipSuccess;
+  PadArgs A;
+  A.blank = a.blank;
+  A.n = a.n;
+  A.reqs = a.reqs;
+  A.nowNs = a.nowNs;
+  A.hot = a.hot;
+  A.dts = a.dts;
+  A.tracks = a.tracks;
+  A.rm = a.rm;
+  A.seq = a.seq;
+  A.seqSize = a.seqSize;
+  A.srm = a.srm;
+  A.srmStride = a.srmStride;
+  A.srmCap = a.srmCap;
+  A.dtCum = a.dtCum;
+  A.recOff = a.recOff;
+  A.byteOff = a.byteOff;
+  A.out = a.out;
+  A.arena = a.arena;
+  A.cnt = a.cnt;
+  A.bytes = a.bytes;
+  hipLaunchKernelGGL(k_pad, dim3(a.n), dim3(64), 0, s, A);
   return hipGetLastError();
 }
 
@@ -3161,6 +3637,9 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.vc = a.vc;
   A.seq = a.seq;
   A.seqSize = a.seqSize;
+  A.srm = a.srm;
+  A.srmStride = a.srmStride;
+  A.srmCap = a.srmCap;
   A.pkts = a.pkts;
   A.tBegin = a.tBegin;
   A.tEnd = a.tEnd;
@@ -3260,9 +3739,10 @@ hipError_t launch_accumulate(hipStream_t s, const u64 *stats, const u64 *tot, u6
   return hipGetLastError();
 }
 
-hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, u32 seqSize, u32 d, const u16 *sns, u32 n,
-                             i64 nowMs, lkf_seq_meta *out, u32 *nOut) {
-  hipLaunchKernelGGL(k_seq_lookup, dim3(1), dim3(64), 0, s, hot, seq, seqSize, d, sns, n, nowMs, out, nOut);
+hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, u32 seqSize, u8 *srm, u64 srmStride, u32 srmCap,
+                             u32 d, const u16 *sns, u32 n, i64 nowMs, lkf_seq_meta *out, u32 *nOut) {
+  hipLaunchKernelGGL(k_seq_lookup, dim3(1), dim3(64), 0, s, hot, seq, seqSize, srm, srmStride, srmCap, d, sns, n, nowMs,
+                     out, nOut);
   return hipGetLastError();
 }
 

@@ -51,7 +51,20 @@ enum : uint32_t {
   F_ACTIVE = 1u << 21,
   F_VP9 = 1u << 22,  // videolayerselector.VP9 (SVC without dependency descriptor)
   F_DD = 1u << 23,   // videolayerselector.DependencyDescriptor (VP9 / AV1 with the DD extension)
+  F_SEQ_RM = 1u << 24,  // the sequencer's RangeMap holds padding exclusions (SeqRM, sequencer.go:211-261)
 };
+
+// The video sequencer's RangeMap((size + 1) / 2) (sequencer.go:97-110).  Only
+// pushPadding (WritePaddingRTP, downtrack.go:814-816) changes it; until then
+// it maps every sequence number to 0 and no kernel reads it (F_SEQ_RM clear).
+// One region per DownTrack: this header, then `cap` closed ranges (a ring,
+// oldest at head), region stride = seqrm_stride(cap).
+struct alignas(16) SeqRM {
+  uint64_t openStart, openValue;  // the open range
+  uint64_t snOffset;              // sequencer.snOffset (updateSNOffset sequencer.go:334-345)
+  uint32_t head, count;
+};
+static_assert(sizeof(SeqRM) == 32, "SeqRM header is 32 B");
 
 struct alignas(16) DTHot {
   // ---- 64-bit ------------------------------------------------------------
@@ -100,6 +113,8 @@ static_assert(sizeof(DevDT) == 16, "DevDT must be 16 B");
 struct RangeEntry {  // closed range of utils.RangeMap (rangemap.go:43-47)
   uint64_t start, end, value;
 };
+inline uint32_t seqrm_cap(uint32_t seqSize) { return (seqSize + 1) / 2 > 1 ? (seqSize + 1) / 2 : 1; }  // minRanges 1
+inline uint64_t seqrm_stride(uint32_t cap) { return (sizeof(SeqRM) + uint64_t(cap) * sizeof(RangeEntry) + 15) & ~15ull; }
 
 struct VP8Cold {  // ordered maps of codecmunger.VP8 (vp8.go:67-69) as rings
   int32_t missKey[kMissCap];

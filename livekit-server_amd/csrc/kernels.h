@@ -21,6 +21,9 @@ struct DecideLaunch {
   VP8Cold *vc;
   SeqMeta *seq;
   uint32_t seqSize;
+  uint8_t *srm;  // SeqRM regions (the sequencer RangeMaps of padding exclusions)
+  uint64_t srmStride;
+  uint32_t srmCap;
   const lkf_pkt *pkts;
   const uint32_t *tBegin, *tEnd;
   const uint64_t *slotBase;
@@ -127,7 +130,8 @@ hipError_t launch_ev_offsets(hipStream_t s, const uint32_t *laneOf, uint32_t nev
 hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum,
                              const uint32_t *err, uint32_t *sticky);
 hipError_t launch_err_fold(hipStream_t s, const uint32_t *err, uint32_t *sticky, uint32_t shift);
-hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, uint32_t seqSize, const lkf_nack *nacks,
+hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint8_t *srm,
+                             uint64_t srmStride, uint32_t srmCap, const lkf_nack *nacks,
                              const uint32_t *gStart, uint32_t ngroups, int64_t nowMs, lkf_rtx *out, uint32_t *valid);
 hipError_t launch_rtx_emit(hipStream_t s, bool write, uint32_t n, const lkf_rtx *rtx, const lkf_raw_pkt *src,
                            const uint8_t *arena, const DevDT *dts, const DevTrack *tracks, uint32_t *lens,
@@ -165,7 +169,32 @@ hipError_t launch_srtp_keys(hipStream_t s, const lkf_transport_params *in, uint3
 hipError_t launch_srtp_protect(hipStream_t s, const SrtpProtectArgs &a, uint32_t ndts, const uint32_t *perm,
                                const uint64_t *recBase, const uint32_t *fwdCnt);
 
-hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint32_t d,
+hipError_t launch_seq_lookup(hipStream_t s, DTHot *hot, SeqMeta *seq, uint32_t seqSize, uint8_t *srm,
+                             uint64_t srmStride, uint32_t srmCap, uint32_t d,
                              const uint16_t *sns, uint32_t n, int64_t nowMs, lkf_seq_meta *out, uint32_t *nOut);
+
+// ---- padding / blank frames (WritePaddingRTP, writeBlankFrameRTP) ----
+struct PadLaunch {
+  int blank;  // 0: WritePaddingRTP requests, 1: one writeBlankFrameRTP tick per request
+  uint32_t n;
+  const lkf_pad_req *reqs;
+  int64_t nowNs;
+  DTHot *hot;
+  const DevDT *dts;
+  const DevTrack *tracks;
+  RangeEntry *rm;
+  SeqMeta *seq;
+  uint32_t seqSize;
+  uint8_t *srm;
+  uint64_t srmStride;
+  uint32_t srmCap;
+  DTCum *dtCum;
+  const uint64_t *recOff, *byteOff;  // per request: first reserved record / arena byte
+  lkf_out *out;
+  uint8_t *arena;
+  uint32_t *cnt;    // per request: packets written
+  uint32_t *bytes;  // per request: WritePaddingRTP's return value (blank: bytes counted by sendingPacket)
+};
+hipError_t launch_pad(hipStream_t s, const PadLaunch &a);
 
 }  // namespace lkf

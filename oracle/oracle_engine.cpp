@@ -685,6 +685,155 @@ int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   return LKF_OK;
 }
 
+// ---- padding / blank frames (lkf_padding / lkf_blank_frames) ---------------
+static const u8 kVP8KeyFrame8x8[31] = {0x10, 0x02, 0x00, 0x9d, 0x01, 0x2a, 0x08, 0x00, 0x08, 0x00, 0x00,
+                                       0x47, 0x08, 0x85, 0x85, 0x88, 0x85, 0x84, 0x88, 0x02, 0x02, 0x00,
+                                       0x0c, 0x0d, 0x60, 0x00, 0xfe, 0xff, 0xab, 0x50, 0x80};  // downtrack.go:91-96
+static const u8 kH264SPS[24] = {0x67, 0x42, 0xc0, 0x1f, 0x0f, 0xd9, 0x1f, 0x88, 0x88, 0x84, 0x00, 0x00,
+                                0x03, 0x00, 0x04, 0x00, 0x00, 0x03, 0x00, 0xc8, 0x3c, 0x60, 0xc9, 0x20};
+static const u8 kH264PPS[6] = {0x68, 0x87, 0xcb, 0x83, 0xcb, 0x20};
+static const u8 kH264IDR[10] = {0x65, 0x88, 0x84, 0x0a, 0xf2, 0x62, 0x80, 0x00, 0xa7, 0xbe};
+
+// pacer.Packet -> wire: writeRTPHeaderExtensions (pacer/base.go:71-100) with
+// the abs-send-time placeholder, then header || payload
+static void padPacket(orc_engine *e, ODT &d, u32 dtIdx, u32 reqIdx, RtpHeader hdr, const std::vector<u8> &payload,
+                      u64 esn, u64 ets) {
+  hdr.Extension = false;
+  hdr.ExtensionProfile = 0;
+  hdr.Extensions.clear();
+  if (d.p.ext_abs_send_time) hdr.SetExtension(d.p.ext_abs_send_time, std::vector<u8>{0, 0, 0});
+  OOut o;
+  hdr.Marshal(o.bytes);
+  o.bytes.insert(o.bytes.end(), payload.begin(), payload.end());
+  std::memset(&o.rec, 0, sizeof(o.rec));
+  o.rec.ext_sn = esn;
+  o.rec.ext_ts = ets;
+  o.rec.dt = dtIdx;
+  o.rec.pkt = reqIdx;
+  o.rec.out_len = u16(o.bytes.size());
+  o.rec.flags = hdr.Marker ? LKF_OUT_MARKER : 0;
+  o.rec.layer = -1;
+  e->outRecs.push_back(o.rec);
+  e->outRecs.back().out_off = e->outArena.size();
+  e->outArena.insert(e->outArena.end(), o.bytes.begin(), o.bytes.end());
+  e->outArena.resize((e->outArena.size() + 15) & ~size_t(15), 0);
+}
+
+// DownTrack.WritePaddingRTP downtrack.go:764-859 (virtual clock)
+static u32 writePadding(orc_engine *e, u32 dtIdx, u32 reqIdx, const lkf_pad_req &q, i64 now) {
+  ODT &d = *e->dts[dtIdx];
+  Forwarder &f = *d.f;
+  const bool onMute = q.flags & LKF_PAD_ON_MUTE;
+  if (!(q.flags & LKF_PAD_WRITABLE)) return 0;
+  if (!d.statsInit && !onMute) return 0;  // rtpStats.IsActive
+  if (f.kind == KindAudio) return 0;
+  if (f.muted && !onMute) return 0;  // Forwarder.IsMuted forwarder.go:415-420
+  if (!(q.flags & LKF_PAD_RR_SEEN) && !onMute) return 0;
+  const int num = int((u64(q.bytes_to_send) + 255 + 20 - 1) / (255 + 20));
+  if (num == 0) return 0;
+  std::vector<SnTs> snts;
+  if (f.GetSnTsForPadding(num, (q.flags & LKF_PAD_FORCE_MARKER) != 0, now, u16(q.start_sn), q.start_ts, snts) != OK)
+    return 0;
+  d.seq->pushPadding(snts.front().extSequenceNumber, snts.back().extSequenceNumber);
+  u32 sent = 0;
+  for (auto &v : snts) {
+    RtpHeader hdr;
+    hdr.Padding = true;
+    hdr.PayloadType = d.p.payload_type;
+    hdr.SequenceNumber = u16(v.extSequenceNumber);
+    hdr.Timestamp = u32(v.extTimestamp);
+    hdr.SSRC = d.p.ssrc;
+    std::vector<u8> payload(255, 0);
+    payload[254] = 255;  // the padding size, that byte included
+    // sendingPacket: shouldDisableCounter, padding (no bytesSent; RTPStatsSender
+    // does not start on a padding-only packet rtpstats_sender.go:246-249)
+    padPacket(e, d, dtIdx, reqIdx, hdr, payload, v.extSequenceNumber, v.extTimestamp);
+    sent += 12 + 255;  // hdr.MarshalSize() + len(payload)
+  }
+  return sent;
+}
+
+// one tick of DownTrack.writeBlankFrameRTP downtrack.go:1307-1401
+static void writeBlank(orc_engine *e, u32 dtIdx, u32 reqIdx, const lkf_pad_req &q, i64 now) {
+  ODT &d = *e->dts[dtIdx];
+  Forwarder &f = *d.f;
+  if (!(q.flags & LKF_PAD_WRITABLE) || !d.statsInit) return;
+  const u8 codec = e->tracks[d.p.track].p.codec;
+  if (codec != LKF_CODEC_OPUS && codec != LKF_CODEC_VP8 && codec != LKF_CODEC_H264) return;
+  const u32 frameRate = codec == LKF_CODEC_OPUS ? 50 : 30;
+  std::vector<SnTs> snts;
+  bool frameEndNeeded = false;
+  if (f.GetSnTsForBlankFrames(frameRate, 1, now, u16(q.start_sn), q.start_ts, snts, frameEndNeeded) != OK) return;
+  for (auto &v : snts) {
+    RtpHeader hdr;
+    hdr.Marker = true;
+    hdr.PayloadType = d.p.payload_type;
+    hdr.SequenceNumber = u16(v.extSequenceNumber);
+    hdr.Timestamp = u32(v.extTimestamp);
+    hdr.SSRC = d.p.ssrc;
+    std::vector<u8> payload;
+    if (codec == LKF_CODEC_OPUS) {  // getOpusBlankFrame :1413-1422 (OpusSilenceFrame, no trailer)
+      payload.assign(80, 0);
+      payload[0] = 0xf8;
+      payload[1] = 0xff;
+      payload[2] = 0xfe;
+    } else if (codec == LKF_CODEC_VP8) {  // getVP8BlankFrame :1439-1454
+      f.GetPadding(frameEndNeeded, payload);
+      payload.insert(payload.end(), kVP8KeyFrame8x8, kVP8KeyFrame8x8 + 31);
+    } else {  // getH264BlankFrame :1456-1472 (STAP-A)
+      payload.push_back(0x18);
+      for (auto nal : {std::make_pair(kH264SPS, 24), std::make_pair(kH264PPS, 6), std::make_pair(kH264IDR, 10)}) {
+        payload.push_back(0);
+        payload.push_back(u8(nal.second));
+        payload.insert(payload.end(), nal.first, nal.first + nal.second);
+      }
+    }
+    d.packetsSent++;  // sendingPacket: hdr.MarshalSize() + len(payload)
+    d.bytesSent += 12 + payload.size();
+    padPacket(e, d, dtIdx, reqIdx, hdr, payload, v.extSequenceNumber, v.extTimestamp);
+    frameEndNeeded = false;  // only the first packet closes the open frame
+  }
+}
+
+static int padCommon(orc_engine *e, int blank, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out,
+                     uint8_t *arena, uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len,
+                     uint32_t *bytes_sent) {
+  if (!n_out || !arena_len || (n && !reqs)) return LKF_EINVAL;
+  std::vector<u8> seen(e->dts.size(), 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (reqs[i].dt < 0 || reqs[i].dt >= (int)e->dts.size() || seen[reqs[i].dt]) return LKF_EINVAL;
+    seen[reqs[i].dt] = 1;
+  }
+  e->outRecs.clear();
+  e->outArena.clear();
+  for (uint32_t i = 0; i < n; i++) {
+    const u32 dt = u32(reqs[i].dt);
+    u32 sent = 0;
+    if (e->dts[dt]->active) {
+      if (blank)
+        writeBlank(e, dt, i, reqs[i], now_ns);
+      else
+        sent = writePadding(e, dt, i, reqs[i], now_ns);
+    }
+    if (bytes_sent) bytes_sent[i] = sent;
+  }
+  *n_out = uint32_t(e->outRecs.size());
+  *arena_len = e->outArena.size();
+  if (e->outRecs.size() > out_cap || e->outArena.size() > arena_cap || (*n_out && (!out || !arena))) return LKF_ENOSPC;
+  if (*n_out) std::memcpy(out, e->outRecs.data(), e->outRecs.size() * sizeof(lkf_out));
+  if (*arena_len) std::memcpy(arena, e->outArena.data(), e->outArena.size());
+  return LKF_OK;
+}
+
+int orc_padding(orc_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
+                uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len, uint32_t *bytes_sent) {
+  return padCommon(e, 0, reqs, n, now_ns, out, arena, out_cap, arena_cap, n_out, arena_len, bytes_sent);
+}
+int orc_blank_frames(orc_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
+                     uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len) {
+  return padCommon(e, 1, reqs, n, now_ns, out, arena, out_cap, arena_cap, n_out, arena_len, nullptr);
+}
+
 int orc_seq_lookup(orc_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, int64_t now_ns, lkf_seq_meta *out,
                    uint32_t *n_out) {
   if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
