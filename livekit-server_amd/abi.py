@@ -364,16 +364,18 @@ def bind_engine_api(lib, prefix):
     api["rtx_emit"] = _bind(lib, prefix + "rtx_emit", C.c_int,
                             [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                              C.c_uint64, P(C.c_uint32), P(C.c_uint64)])
+    api["add_transport"] = _bind(lib, prefix + "add_transport", C.c_int32, [e, P(lkf_transport_params)])
+    api["set_downtrack_transport"] = _bind(lib, prefix + "set_downtrack_transport", C.c_int, [e, C.c_int32, C.c_int32])
+    api["protect"] = _bind(lib, prefix + "protect", C.c_int, [e, C.c_int64])
+    api["drain_protected"] = _bind(lib, prefix + "drain_protected", C.c_int, [e, C.c_void_p, C.c_uint64, P(C.c_uint64)])
+    if not hasattr(lib, prefix + "padding"):  # (an older build, e.g. an A/B baseline library)
+        return api
     api["padding"] = _bind(lib, prefix + "padding", C.c_int,
                            [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                             P(C.c_uint32), P(C.c_uint64), C.c_void_p])
     api["blank_frames"] = _bind(lib, prefix + "blank_frames", C.c_int,
                                 [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                  P(C.c_uint32), P(C.c_uint64)])
-    api["add_transport"] = _bind(lib, prefix + "add_transport", C.c_int32, [e, P(lkf_transport_params)])
-    api["set_downtrack_transport"] = _bind(lib, prefix + "set_downtrack_transport", C.c_int, [e, C.c_int32, C.c_int32])
-    api["protect"] = _bind(lib, prefix + "protect", C.c_int, [e, C.c_int64])
-    api["drain_protected"] = _bind(lib, prefix + "drain_protected", C.c_int, [e, C.c_void_p, C.c_uint64, P(C.c_uint64)])
     return api
 
 

@@ -100,6 +100,9 @@ struct lkf_engine {
   std::vector<uint32_t> trackDD;  // per track: DD table index or 0xffffffff
   std::vector<lkf_downtrack_params> dtp;
   std::vector<uint8_t> active;
+  // the DownTrack's sequencer may hold padding exclusions (lkf_padding sent
+  // packets): it is decided by k_decide_dt<true>, which carries that path
+  std::vector<uint8_t> seqRM;
   bool schedDirty = true;
   std::vector<uint32_t> sched;   // lane -> dt (kIdle = padding)
   std::vector<int32_t> dtLane;   // dt -> lane (-1 inactive)
@@ -697,6 +700,7 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
   int32_t h = int32_t(e->dtp.size());
   e->dtp.push_back(*p);
   e->active.push_back(1);
+  e->seqRM.push_back(0);
   e->dtIsDD.push_back(track_has_dd(e->tracks[p->track]) ? 1 : 0);
   e->pendHot.emplace_back();
   init_hot(e->pendHot.back(), e->tracks[p->track], *p);
@@ -841,8 +845,8 @@ static int rebuild_sched(lkf_engine *e) {
   for (int part = 0; part < 2; part++) {
     std::vector<uint32_t> ps, pt;
     for (uint32_t t : order) {
-      if ((e->trackDD[t] != 0xffffffffu) != (part == 1)) continue;
       for (uint32_t d : byTrack[t]) {  // one wave per DownTrack (interleaved per XCD below)
+        if ((e->trackDD[t] != 0xffffffffu || e->seqRM[d]) != (part == 1)) continue;
         ps.push_back(d);
         pt.push_back(t);
       }
@@ -1182,6 +1186,10 @@ int lkf_sync(lkf_engine *e) {
   if (acc & (4u << 8)) {
     e->err = "dependency descriptor beyond an engine limit (templates, frame diffs, chains)";
     return LKF_ENOSPC;
+  }
+  if (acc & 32u) {
+    e->err = "internal: a DownTrack with padding exclusions was decided by the plain kernel";
+    return LKF_EINVAL;
   }
   if (acc & 16u) {
     e->err = "dependency descriptor unreadable, missing its lkf_pkt_dd entry, or beyond an engine limit";
@@ -1751,6 +1759,10 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   for (uint32_t j = 0; j < m; j++) {
     k += cnt[j];
     if (bytes_sent) bytes_sent[live[j]] = cnt[m + j];
+    if (!blank && cnt[j] && !e->seqRM[lq[j].dt]) {  // pushPadding ran: reschedule (rebuild_sched)
+      e->seqRM[lq[j].dt] = 1;
+      e->schedDirty = true;
+    }
   }
   std::vector<lkf_out> recv(recs ? recs : 1);
   std::vector<uint8_t> arv(bytes ? bytes : 1);

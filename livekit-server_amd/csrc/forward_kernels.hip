@@ -1145,33 +1145,58 @@ __device__ bool srm_exclude(SeqRM *h, u32 cap, u64 s, u64 e, bool store) {
   }
   return true;
 }
-// sequencer.push with padding exclusions (F_SEQ_RM, rare: out of line so the
-// decide kernel keeps its registers): on the first push the sequencer's
-// snOffset (updateSNOffset sequencer.go:136) and the adjusted slot of esn;
-// then extModifiedSNAdjusted / extHighestSNAdjusted (sequencer.go:160-176).
-// false = the push is dropped (an excluded or too-old SN).
-__device__ __noinline__ bool srm_push_adjust(SeqRM *h, u32 cap, u32 size, bool init, u64 esn, u64 highest, u64 &adjM,
-                                             u64 &adjH, u32 &initSlot) {
-  u64 snOff = h->snOffset;
+// sequencer.push sequencer.go:123-209 for a DownTrack whose sequencer has
+// padding exclusions (F_SEQ_RM) and a push that needs them: the first push
+// (updateSNOffset :136) or one below the highest SN (the RangeMap lookup
+// :160-170).  Rare, and out of line with plain pointer arguments so the
+// decide kernel's register allocation does not see it.
+__device__ __noinline__ void seq_push_rm(DTHot *h, SeqMeta *seq, u32 size, SeqRM *srm, u32 cap, u64 esn,
+                                         const SeqMeta *rec, u64 ets) {
+  const bool init = !(h->flags & F_SEQ_INIT);
+  u64 snOff = srm->snOffset;
   if (init) {
+    h->flags |= F_SEQ_INIT;
+    h->seqExtStartSN = esn;
+    h->seqExtHighestSN = esn;
+    h->seqExtHighestTS = ets;
     u64 off = 0;
-    if (srm_get(h, cap, esn + 1, off)) snOff = off;
-    if (lane_id() == 0) h->snOffset = snOff;
-    initSlot = u32((esn - snOff) % size);
+    if (srm_get(srm, cap, esn + 1, off)) snOff = off;
+    if (lane_id() == 0) srm->snOffset = snOff;
+    h->seqHighSlot = u16((esn - snOff) % size);
   }
-  adjH = highest - snOff;
-  adjM = esn - snOff;
-  if (esn < highest) {
+  if (esn < h->seqExtStartSN) return;
+  const u64 adjH = h->seqExtHighestSN - snOff;
+  u64 adjM = esn - snOff;
+  if (esn < h->seqExtHighestSN) {
     u64 off = 0;
-    if (!srm_get(h, cap, esn, off)) return false;
+    if (!srm_get(srm, cap, esn, off)) return;
     adjM = esn - off;
   }
-  return true;
+  const i64 delta = i64(adjM - adjH);
+  if (delta <= -i64(size)) return;
+  u32 slot;
+  if (delta >= 0) {
+    slot = u32((u64(h->seqHighSlot) + u64(delta) % size) % size);
+  } else {
+    const i32 sl = i32(h->seqHighSlot) + i32(delta);
+    slot = u32(sl < 0 ? sl + i32(size) : sl);
+  }
+  if (adjM > adjH + 1) {  // invalidate the skipped slots (sequencer.go:179-189)
+    const u64 nInv = (adjM - adjH - 1) < u64(size) ? (adjM - adjH - 1) : u64(size);
+    for (u32 i = lane_id(); i < u32(nInv); i += 64) seq[(u32(h->seqHighSlot) + 1 + i) % size] = SeqMeta{};
+  }
+  if (lane_id() == 0) seq[slot] = *rec;
+  if (esn > h->seqExtHighestSN) {
+    h->seqExtHighestSN = esn;
+    h->seqHighSlot = u16(slot);
+  }
+  if (ets > h->seqExtHighestTS) h->seqExtHighestTS = ets;
 }
 
 // sequencer.push sequencer.go:123-209.  Without padding exclusions (F_SEQ_RM
 // clear) the sequencer's RangeMap maps everything to 0: slot = extModifiedSN
 // % size, kept as seqHighSlot + the distance to the highest SN.
+template <bool RM>
 __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool marker, int8_t layer, u64 cb,
                          int cbLen) {
   const u32 size = L.seqSize;
@@ -1195,8 +1220,29 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     return;
   }
 
-  const bool init = !hasf(L, F_SEQ_INIT);
-  if (init) {
+  if (hasf(L, F_SEQ_RM) && (!hasf(L, F_SEQ_INIT) || esn < L.h.seqExtHighestSN)) {  // padding was sent
+    if (!RM) {  // the host schedules such DownTracks in k_decide_dt<true>: never reached
+      if (lane_id() == 0) atomicOr(L.err, 32u);
+      return;
+    }
+    SeqMeta m = {};
+    m.sourceSeqNo = u16(inSN);
+    m.targetSeqNo = u16(esn);
+    m.timestamp = u32(ets);
+    m.lastNack = u32(arrMs - L.h.seqStartMs);
+    m.marker = marker;
+    m.layer = layer;
+    m.codecLen = u8(cbLen);
+#pragma unroll
+    for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+    __shared__ SeqMeta sRec;
+    if (lane_id() == 0) sRec = m;
+    __syncthreads();
+    seq_push_rm(&L.h, L.seq, size, L.srm, L.srmCap, esn, &sRec, ets);
+    __syncthreads();
+    return;
+  }
+  if (!hasf(L, F_SEQ_INIT)) {
     setf(L, F_SEQ_INIT, true);
     L.h.seqExtStartSN = esn;
     L.h.seqExtHighestSN = esn;
@@ -1204,13 +1250,8 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     L.h.seqHighSlot = u16(esn % size);  // once per DownTrack lifetime
   }
   if (esn < L.h.seqExtStartSN) return;
-  u64 adjH = L.h.seqExtHighestSN;
-  u64 adjM = esn;
-  if (hasf(L, F_SEQ_RM)) {  // padding was sent on this DownTrack
-    u32 initSlot = 0;
-    if (!srm_push_adjust(L.srm, L.srmCap, size, init, esn, L.h.seqExtHighestSN, adjM, adjH, initSlot)) return;
-    if (init) L.h.seqHighSlot = u16(initSlot);
-  }
+  const u64 adjH = L.h.seqExtHighestSN;
+  const u64 adjM = esn;
   const i64 delta = i64(adjM - adjH);
   if (delta <= -i64(size)) return;
   // slot of adjM from the highest slot without a 64-bit modulo
@@ -1664,7 +1705,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 #if LKF_ABLATE != 1  // diagnostic builds only (never shipped): 1 = no tuple/sequencer writes
   if (lane_id() == 0) store_rec(o.outT + o.nFwd, t);  // wave-uniform record: one lane stores it
   // sequencer.push (downtrack.go:724-735)
-  seq_push(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
+  seq_push<DDK>(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
 #endif
   // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
   if (!hasf(L, F_STATS_INIT) && payLen > 0) {
@@ -1926,7 +1967,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __syncthreads();
   L.seq = A.seq + size_t(d) * A.seqSize;
   L.seqSize = A.seqSize;
-  L.srm = reinterpret_cast<SeqRM *>(A.srm + size_t(d) * A.srmStride);
+  L.srm = DDK ? reinterpret_cast<SeqRM *>(A.srm + size_t(d) * A.srmStride) : nullptr;  // (only <true> reads it)
   L.srmCap = A.srmCap;
   const DevTrack &tk = A.tracks[track];
   L.kind = tk.kind;
