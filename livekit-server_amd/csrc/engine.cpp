@@ -1109,16 +1109,19 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipEventRecord(rg[1], s), "event");
   HIPCHK(launch_decide(s, d), "decide");
   HIPCHK(hipEventRecord(rg[2], s), "event");
-  HIPCHK(hipEventRecord(x.decided, s), "event");
-
-  // ---- emit stage (emit stream): counters, output scan, wire bytes.  The
-  // decide stream goes straight on to the next batch's decide.
-  hipStream_t es = e->emitS;
-  HIPCHK(hipStreamWaitEvent(es, x.decided, 0), "wait decided");
-  HIPCHK(launch_stats_reduce(es, x.dStats), "stats reduce");
-  HIPCHK(launch_scan(es, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
+  // counters and the output scan stay on the (high-priority) decide stream:
+  // on the low-priority emit stream these small kernels queued behind the
+  // next batch's decide waves and were on the emit chain's critical path
+  HIPCHK(launch_stats_reduce(s, x.dStats), "stats reduce");
+  HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
                      x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm, x.dGFirst, e->cfg.max_out_pkts),
          "out scan");
+  HIPCHK(hipEventRecord(x.decided, s), "event");
+
+  // ---- emit stage (emit stream): wire bytes.  The decide stream goes
+  // straight on to the next batch's decide.
+  hipStream_t es = e->emitS;
+  HIPCHK(hipStreamWaitEvent(es, x.decided, 0), "wait decided");
   HIPCHK(hipEventRecord(rg[3], es), "event");
   EmitLaunch m;
   m.perm = e->dPerm;
