@@ -498,6 +498,34 @@ int lkf_padding(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_
 int lkf_blank_frames(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
                      uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len);
 
+/* ---- stream allocation ------------------------------ */
+typedef struct lkf_alloc_req {
+  int32_t dt;
+  uint32_t available_layers;  /* bit s = spatial layer s is available (StreamTrackerManager availableLayers) */
+  int64_t bitrates[3][4];     /* Bitrates[spatial][temporal], bps (0: not measured / not available) */
+  uint8_t allow_overshoot;
+  uint8_t reserved[7];
+} lkf_alloc_req;
+/* VideoAllocation (forwarder.go:82-93) without its Bitrates (the request's). */
+typedef struct lkf_allocation {
+  int32_t dt;
+  int32_t pause_reason; /* VideoPauseReason: 0 none, 1 muted, 2 pub muted, 3 feed dry, 4 bandwidth */
+  int64_t bandwidth_requested, bandwidth_delta, bandwidth_needed;
+  int32_t target_spatial, target_temporal, request_spatial, max_spatial, max_temporal;
+  uint8_t is_deficient;
+  uint8_t reserved[3];
+  double distance_to_desired;
+} lkf_allocation;
+/* Forwarder.AllocateOptimal (forwarder.go:591-725) for many DownTracks (one
+ * request each, distinct; LKF_EINVAL otherwise), each applied as
+ * updateAllocation (:1353-1373: target layer, request spatial, resync when
+ * paused, lastAllocation for the next BandwidthDelta) to the state the next
+ * lkf_run continues from.  Waits for queued runs.  An audio DownTrack answers
+ * VideoAllocationDefault (:111-116).  (LKF_CTL_SET_ALLOCATION, the host-side
+ * allocator's result, does not carry bandwidth: it leaves
+ * lastAllocation.BandwidthRequested as this call last set it.) */
+int lkf_allocate_optimal(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out);
+
 /* ---- SRTP protect ----------------------------------- *
  * The step after the pacer: writeRTPHeaderExtensions sets abs-send-time
  * (pacer/base.go:71-100), then WriteStream.WriteRTP (base.go:59) protects the

@@ -105,6 +105,15 @@ DTS_DEFICIENT = 0x2
 PAD_REQ_DTYPE = np.dtype([("dt", "<i4"), ("bytes_to_send", "<u4"), ("flags", "<u4"), ("start_sn", "<u4"),
                           ("start_ts", "<u4"), ("reserved", "<u4")])
 assert PAD_REQ_DTYPE.itemsize == 24
+ALLOC_REQ_DTYPE = np.dtype([("dt", "<i4"), ("available_layers", "<u4"), ("bitrates", "<i8", (3, 4)),
+                            ("allow_overshoot", "u1"), ("reserved", "u1", 7)])
+assert ALLOC_REQ_DTYPE.itemsize == 112
+ALLOCATION_DTYPE = np.dtype([("dt", "<i4"), ("pause_reason", "<i4"), ("bandwidth_requested", "<i8"),
+                             ("bandwidth_delta", "<i8"), ("bandwidth_needed", "<i8"), ("target_spatial", "<i4"),
+                             ("target_temporal", "<i4"), ("request_spatial", "<i4"), ("max_spatial", "<i4"),
+                             ("max_temporal", "<i4"), ("is_deficient", "u1"), ("reserved", "u1", 3),
+                             ("distance_to_desired", "<f8")])
+assert ALLOCATION_DTYPE.itemsize == 64
 PAD_ON_MUTE = 0x1
 PAD_FORCE_MARKER = 0x2
 PAD_WRITABLE = 0x4
@@ -373,6 +382,9 @@ def bind_engine_api(lib, prefix):
     api["padding"] = _bind(lib, prefix + "padding", C.c_int,
                            [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                             P(C.c_uint32), P(C.c_uint64), C.c_void_p])
+    if hasattr(lib, prefix + "allocate_optimal"):
+        api["allocate_optimal"] = _bind(lib, prefix + "allocate_optimal", C.c_int,
+                                        [e, C.c_void_p, C.c_uint32, C.c_void_p])
     api["blank_frames"] = _bind(lib, prefix + "blank_frames", C.c_int,
                                 [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                  P(C.c_uint32), P(C.c_uint64)])

@@ -199,6 +199,11 @@ struct lkf_engine {
   uint8_t *dRtxIn = nullptr, *dRtxOut = nullptr;
   uint64_t rtxInCap = 0, rtxOutCap = 0;
 
+  // lastAllocation.BandwidthRequested per DownTrack (lkf_allocate_optimal)
+  int64_t *dAllocBw = nullptr;
+  lkf_alloc_req *dAllocReq = nullptr;
+  lkf_allocation *dAllocOut = nullptr;
+  uint32_t allocCap = 0;
   // the sequencers' padding RangeMaps (SeqRM regions) and padding scratch
   uint8_t *dSrm = nullptr;
   uint64_t srmStride = 0;
@@ -514,6 +519,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   e->srmCap = seqrm_cap(c.seq_size);
   e->srmStride = seqrm_stride(e->srmCap);
   A(dalloc(&e->dSrm, size_t(c.max_downtracks) * e->srmStride));
+  A(dalloc(&e->dAllocBw, c.max_downtracks));
   A(dalloc(&e->dCum, kStatsWords));
   A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
@@ -570,6 +576,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dILanePerm, e->maxStreams));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
+    A(hipMemset(e->dAllocBw, 0, size_t(c.max_downtracks) * sizeof(int64_t)));
     A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
     A(hipMemset(e->dSticky, 0, 4 * sizeof(uint32_t)));
     for (auto &x : e->ctx) {
@@ -617,7 +624,9 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->dRtx), static_cast<void *>(e->dRtxSrc), static_cast<void *>(e->dRtxLen),
                   static_cast<void *>(e->dRtxOff), static_cast<void *>(e->dRtxIn), static_cast<void *>(e->dRtxOut),
                   static_cast<void *>(e->dSrm), static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff),
-                  static_cast<void *>(e->dPadCnt), static_cast<void *>(e->dPadOut), static_cast<void *>(e->dPadArena)})
+                  static_cast<void *>(e->dPadCnt), static_cast<void *>(e->dPadOut), static_cast<void *>(e->dPadArena),
+                  static_cast<void *>(e->dAllocBw), static_cast<void *>(e->dAllocReq),
+                  static_cast<void *>(e->dAllocOut)})
     if (p) (void)hipFree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
@@ -1789,6 +1798,37 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
       out[w++] = o;
       pos += al;
     }
+  return LKF_OK;
+}
+
+// ---- Forwarder.AllocateOptimal (forwarder.go:591-725) ----------------------
+int lkf_allocate_optimal(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
+  if (!e || (n && (!reqs || !out))) return LKF_EINVAL;
+  if (!n) return LKF_OK;
+  std::vector<uint8_t> seen(e->dtp.size(), 0);
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t dt = reqs[i].dt;
+    if (dt < 0 || dt >= int32_t(e->dtp.size()) || seen[dt]) return LKF_EINVAL;
+    seen[dt] = 1;
+  }
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  if (n > e->allocCap) {
+    if (e->dAllocReq) (void)hipFree(e->dAllocReq);
+    if (e->dAllocOut) (void)hipFree(e->dAllocOut);
+    e->allocCap = std::max<uint32_t>(n, 1024);
+    HIPCHK(dalloc(&e->dAllocReq, e->allocCap), "alloc alloc reqs");
+    HIPCHK(dalloc(&e->dAllocOut, e->allocCap), "alloc alloc out");
+  }
+  HIPCHK(hipMemcpy(e->dAllocReq, reqs, n * sizeof(lkf_alloc_req), hipMemcpyHostToDevice), "alloc req copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_allocate_optimal(e->own, e->dAllocReq, n, e->dHot, e->dDTs, e->dTracks, e->dAllocBw, e->dAllocOut),
+         "allocate optimal");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  HIPCHK(hipMemcpy(out, e->dAllocOut, n * sizeof(lkf_allocation), hipMemcpyDeviceToHost), "alloc out copy");
   return LKF_OK;
 }
 

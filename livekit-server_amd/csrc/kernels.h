@@ -196,5 +196,7 @@ struct PadLaunch {
   uint32_t *bytes;  // per request: WritePaddingRTP's return value (blank: bytes counted by sendingPacket)
 };
 hipError_t launch_pad(hipStream_t s, const PadLaunch &a);
+hipError_t launch_allocate_optimal(hipStream_t s, const lkf_alloc_req *reqs, uint32_t n, DTHot *hot, const DevDT *dts,
+                                   const DevTrack *tracks, int64_t *lastBw, lkf_allocation *out);
 
 }  // namespace lkf

@@ -31,6 +31,7 @@
 #include <cstring>
 #include <functional>
 #include <utility>
+#include <array>
 #include <vector>
 
 namespace orc {
@@ -1421,6 +1422,77 @@ struct ForwarderState {  // forwarder.go:158-166
   VP8State Codec;
 };
 
+// VideoAllocation forwarder.go:82-93 (Bitrates [spatial][temporal], bps)
+using Bitrates = std::array<std::array<i64, 4>, 3>;
+enum VideoPauseReason : i32 { PauseNone = 0, PauseMuted, PausePubMuted, PauseFeedDry, PauseBandwidth };
+struct VideoAllocation {
+  i32 PauseReason = PauseNone;
+  bool IsDeficient = false;
+  i64 BandwidthRequested = 0, BandwidthDelta = 0, BandwidthNeeded = 0;
+  Bitrates Brs{};
+  VideoLayer TargetLayer{0, 0};
+  i32 RequestLayerSpatial = 0;
+  VideoLayer MaxLayer{0, 0};
+  double DistanceToDesired = 0;
+};
+inline VideoAllocation VideoAllocationDefault() {  // forwarder.go:111-116
+  VideoAllocation a;
+  a.PauseReason = PauseFeedDry;
+  a.TargetLayer = InvalidLayer();
+  a.RequestLayerSpatial = InvalidLayerSpatial;
+  a.MaxLayer = InvalidLayer();
+  return a;
+}
+// getOptimalBandwidthNeeded forwarder.go:1857-1878
+inline i64 getOptimalBandwidthNeeded(bool muted, bool pubMuted, i32 maxPublishedLayer, const Bitrates &brs,
+                                     VideoLayer maxLayer) {
+  if (muted || pubMuted || maxPublishedLayer == InvalidLayerSpatial) return 0;
+  for (i32 i = maxLayer.Spatial; i >= 0; i--)
+    for (i32 j = maxLayer.Temporal; j >= 0; j--)
+      if (brs[i][j] != 0) return brs[i][j];
+  return 0;
+}
+// getBandwidthNeeded forwarder.go:1880-1886
+inline i64 getBandwidthNeeded(const Bitrates &brs, VideoLayer layer, i64 fallback) {
+  if (layer.IsValid() && brs[layer.Spatial][layer.Temporal] > 0) return brs[layer.Spatial][layer.Temporal];
+  return fallback;
+}
+// getDistanceToDesired forwarder.go:1888-1973
+inline double getDistanceToDesired(bool muted, bool pubMuted, VideoLayer maxSeenLayer,
+                                   const std::vector<i32> &availableLayers, const Bitrates &brs,
+                                   VideoLayer targetLayer, VideoLayer maxLayer) {
+  if (muted || pubMuted || !maxSeenLayer.IsValid() || !maxLayer.IsValid()) return 0.0;
+  VideoLayer adj = maxLayer;
+  i32 maxAvailS = InvalidLayerSpatial, maxAvailT = InvalidLayerTemporal;
+  for (i32 s = 2; s >= 0 && maxAvailS == InvalidLayerSpatial; s--)
+    for (i32 t = 3; t >= 0; t--)
+      if (brs[s][t] != 0) {
+        maxAvailS = s;
+        break;
+      }
+  for (i32 l : availableLayers)
+    if (l > maxAvailS) {
+      maxAvailS = l;
+      maxAvailT = maxSeenLayer.Temporal;
+    }
+  if (maxAvailS < adj.Spatial) adj.Spatial = maxAvailS;
+  if (maxSeenLayer.Spatial < adj.Spatial) adj.Spatial = maxSeenLayer.Spatial;
+  if (adj.Spatial != InvalidLayerSpatial)
+    for (i32 t = 3; t >= 0; t--)
+      if (brs[adj.Spatial][t] != 0) {
+        maxAvailT = t;
+        break;
+      }
+  if (maxAvailT < adj.Temporal) adj.Temporal = maxAvailT;
+  if (maxSeenLayer.Temporal < adj.Temporal) adj.Temporal = maxSeenLayer.Temporal;
+  if (!adj.IsValid()) adj = VideoLayer{0, 0};
+  VideoLayer adjT = targetLayer;
+  if (!targetLayer.IsValid()) adjT = VideoLayer{0, 0};
+  i32 distance = ((adj.Spatial - adjT.Spatial) * (maxSeenLayer.Temporal + 1)) + (adj.Temporal - adjT.Temporal);
+  if (!targetLayer.IsValid()) distance += (maxSeenLayer.Temporal + 1);
+  return double(distance) / double(maxSeenLayer.Temporal + 1);
+}
+
 struct Forwarder {
   Kind kind;
   Mime mime = MimeNone;
@@ -1442,6 +1514,7 @@ struct Forwarder {
   i32 referenceLayerSpatial = InvalidLayerSpatial;
   u64 refTSOffset = 0;
   bool lastAllocIsDeficient = false;  // lastAllocation.IsDeficient
+  VideoAllocation lastAllocation = VideoAllocationDefault();  // (AllocateOptimal; IsDeficient above)
   RTPMunger rtpMunger;
   VLS vls;
   bool hasVP8Munger = false;
@@ -1547,6 +1620,73 @@ struct Forwarder {
     vls.SetTarget(target);
     vls.SetRequestSpatial(target.IsValid() ? requestSpatial : InvalidLayerSpatial);
     if (!vls.GetTarget().IsValid()) resyncLocked();
+  }
+  // VideoLayerSelector.IsOvershootOkay: Simulcast true (simulcast.go:38), the
+  // base / VP9 / dependency-descriptor selectors false
+  bool IsOvershootOkay() const { return vls.kind == VLSSimulcast; }
+  // AllocateOptimal forwarder.go:591-725 (+ updateAllocation :1353-1373)
+  VideoAllocation AllocateOptimal(const std::vector<i32> &availableLayers, const Bitrates &brs, bool allowOvershoot) {
+    if (kind == KindAudio) return lastAllocation;
+    const VideoLayer maxLayer = vls.GetMax(), maxSeenLayer = vls.GetMaxSeen(), currentLayer = vls.GetCurrent();
+    const i32 requestSpatial = vls.requestSpatial;
+    VideoAllocation alloc;
+    alloc.PauseReason = PauseNone;
+    alloc.Brs = brs;
+    alloc.TargetLayer = InvalidLayer();
+    alloc.RequestLayerSpatial = requestSpatial;
+    alloc.MaxLayer = maxLayer;
+    const i64 optimal = getOptimalBandwidthNeeded(muted, pubMuted, maxSeenLayer.Spatial, brs, maxLayer);
+    if (optimal == 0) alloc.PauseReason = PauseFeedDry;
+    alloc.BandwidthNeeded = optimal;
+    auto getMaxTemporal = [&]() {
+      i32 mt = maxLayer.Temporal;
+      if (maxSeenLayer.Temporal != InvalidLayerTemporal && maxSeenLayer.Temporal < mt) mt = maxSeenLayer.Temporal;
+      return mt;
+    };
+    if (!maxLayer.IsValid() || maxSeenLayer.Spatial == InvalidLayerSpatial) {
+    } else if (muted) {
+      alloc.PauseReason = PauseMuted;
+    } else if (pubMuted) {
+      alloc.PauseReason = PausePubMuted;
+    } else {
+      const i32 limit = std::min(maxLayer.Spatial, maxSeenLayer.Spatial);
+      i32 highest = InvalidLayerSpatial, request = InvalidLayerSpatial;
+      for (i32 al : availableLayers) {
+        if (al > request && al <= limit) request = al;
+        if (al > highest) highest = al;
+      }
+      if (request == InvalidLayerSpatial && highest != InvalidLayerSpatial && allowOvershoot && IsOvershootOkay())
+        request = highest;
+      if (currentLayer.IsValid()) {
+        if ((request == requestSpatial && currentLayer.Spatial == requestSpatial) || request == InvalidLayerSpatial)
+          alloc.TargetLayer = VideoLayer{currentLayer.Spatial, getMaxTemporal()};
+        else
+          alloc.TargetLayer = VideoLayer{request, getMaxTemporal()};
+        alloc.RequestLayerSpatial = alloc.TargetLayer.Spatial;
+      } else {  // opportunistic
+        i32 maxSpatial = maxLayer.Spatial;
+        if (allowOvershoot && IsOvershootOkay() && maxSeenLayer.Spatial > maxSpatial) maxSpatial = maxSeenLayer.Spatial;
+        alloc.TargetLayer = VideoLayer{std::min(maxSeenLayer.Spatial, maxSpatial), getMaxTemporal()};
+        alloc.RequestLayerSpatial = request == InvalidLayerSpatial ? limit : request;
+      }
+    }
+    if (!alloc.TargetLayer.IsValid()) {
+      alloc.TargetLayer = InvalidLayer();
+      alloc.RequestLayerSpatial = InvalidLayerSpatial;
+    }
+    if (alloc.TargetLayer.IsValid()) alloc.BandwidthRequested = optimal;
+    alloc.BandwidthDelta =
+        alloc.BandwidthRequested - getBandwidthNeeded(brs, vls.GetTarget(), lastAllocation.BandwidthRequested);
+    alloc.DistanceToDesired = getDistanceToDesired(muted, pubMuted, vls.GetMaxSeen(), availableLayers, brs,
+                                                   alloc.TargetLayer, vls.GetMax());
+    // updateAllocation
+    if (alloc.TargetLayer.IsValid() && mime == MimeH264) alloc.TargetLayer.Temporal = 0;
+    lastAllocation = alloc;
+    lastAllocIsDeficient = alloc.IsDeficient;
+    vls.SetTarget(alloc.TargetLayer);
+    vls.SetRequestSpatial(alloc.TargetLayer.IsValid() ? alloc.RequestLayerSpatial : InvalidLayerSpatial);
+    if (!vls.GetTarget().IsValid()) resyncLocked();
+    return lastAllocation;
   }
   // Resync / resyncLocked forwarder.go:1384-1397
   void Resync() { resyncLocked(); }

@@ -825,6 +825,41 @@ static int padCommon(orc_engine *e, int blank, const lkf_pad_req *reqs, uint32_t
   return LKF_OK;
 }
 
+// Forwarder.AllocateOptimal for each request (lkf_allocate_optimal)
+int orc_allocate_optimal(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
+  if (n && (!reqs || !out)) return LKF_EINVAL;
+  std::vector<u8> seen(e->dts.size(), 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (reqs[i].dt < 0 || reqs[i].dt >= (int)e->dts.size() || seen[reqs[i].dt]) return LKF_EINVAL;
+    seen[reqs[i].dt] = 1;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    const lkf_alloc_req &q = reqs[i];
+    std::vector<i32> avail;
+    for (i32 l = 0; l < 32; l++)
+      if (q.available_layers & (1u << l)) avail.push_back(l);
+    Bitrates brs;
+    for (int s = 0; s < 3; s++)
+      for (int t = 0; t < 4; t++) brs[s][t] = q.bitrates[s][t];
+    const VideoAllocation a = e->dts[q.dt]->f->AllocateOptimal(avail, brs, q.allow_overshoot != 0);
+    lkf_allocation &o = out[i];
+    std::memset(&o, 0, sizeof(o));
+    o.dt = q.dt;
+    o.pause_reason = a.PauseReason;
+    o.bandwidth_requested = a.BandwidthRequested;
+    o.bandwidth_delta = a.BandwidthDelta;
+    o.bandwidth_needed = a.BandwidthNeeded;
+    o.target_spatial = a.TargetLayer.Spatial;
+    o.target_temporal = a.TargetLayer.Temporal;
+    o.request_spatial = a.RequestLayerSpatial;
+    o.max_spatial = a.MaxLayer.Spatial;
+    o.max_temporal = a.MaxLayer.Temporal;
+    o.is_deficient = a.IsDeficient;
+    o.distance_to_desired = a.DistanceToDesired;
+  }
+  return LKF_OK;
+}
+
 int orc_padding(orc_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
                 uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len, uint32_t *bytes_sent) {
   return padCommon(e, 0, reqs, n, now_ns, out, arena, out_cap, arena_cap, n_out, arena_len, bytes_sent);

@@ -1,0 +1,88 @@
+"""Forwarder.AllocateOptimal (forwarder.go:591-725), engine vs oracle.
+
+The oracle's restatement is pinned by TestForwarderAllocateOptimal
+(oracle/kat_sfu.inc).  Here every DownTrack of a trace gets an allocation with
+random available layers, bitrate tables (zeros included: feed dry, measurement
+pending) and overshoot permission, between forwarded batches and twice in a row
+(BandwidthDelta against the previous allocation): the allocations, the batches
+forwarded after them (new targets, resyncs when paused) and the Forwarder state
+must be identical."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests.oracle_lib import load as load_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def make_alloc_reqs(abi, ndts, seed):
+    rng = np.random.default_rng(seed)
+    r = np.zeros(ndts, dtype=abi.ALLOC_REQ_DTYPE)
+    r["dt"] = rng.permutation(ndts)
+    r["available_layers"] = rng.integers(0, 8, ndts)
+    brs = rng.integers(100_000, 3_000_000, (ndts, 3, 4))
+    brs[rng.random((ndts, 3, 4)) < 0.3] = 0
+    brs[rng.random(ndts) < 0.1] = 0  # feed dry
+    r["bitrates"] = brs
+    r["allow_overshoot"] = rng.integers(0, 2, ndts)
+    return r
+
+
+def allocate(api, h, reqs, abi):
+    out = np.zeros(len(reqs), dtype=abi.ALLOCATION_DTYPE)
+    assert api["allocate_optimal"](h, reqs.ctypes.data, len(reqs), out.ctypes.data) == 0
+    return out
+
+
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=3, seed=5), dict(config=5, rooms=6, svc_dd=1),
+                                 dict(config=5, rooms=6, svc_dd=0), dict(config=2, rooms=2, h264=1, seed=3)])
+def test_allocate_optimal_matches_oracle(pkg, workload, cfg):
+    o = load_oracle()
+    abi = pkg.abi
+    kw = dict(cfg)
+    tr = workload.Trace(kw.pop("config"), duration_s=4.0, batch_s=1.0, **kw)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+        moved = 0
+        for b in range(tr.nbatches):
+            if b in (1, 3):
+                for k in range(2):
+                    reqs = make_alloc_reqs(abi, tr.ndts, seed=10 * b + k)
+                    g = allocate(eng.api, eng.h, reqs, abi)
+                    r = allocate(o.api, oh, reqs, abi)
+                    for f in abi.ALLOCATION_DTYPE.names:
+                        if f != "reserved":
+                            assert np.array_equal(g[f], r[f]), (b, k, f)
+                    moved += int((r["bandwidth_delta"] != 0).sum())
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            dd = tr.batch_dd(b)[0] if tr.has_dd() else None
+            eng.submit(pk, n, ar, alen, dd)
+            eng.run()
+            eng.sync()
+            o.run(oh, pk, n, ar, alen, dd)
+            grec, gar = eng.drain()
+            orec, oar = pkg.drain_arrays(o.api, oh)
+            assert len(grec) == len(orec), b
+            for f in abi.OUT_DTYPE.names:
+                assert np.array_equal(grec[f], orec[f]), (b, f)
+            assert np.array_equal(gar, oar), b
+        assert moved > 0
+        for dt in range(tr.ndts):
+            gs, os_ = abi.lkf_fwd_state(), abi.lkf_fwd_state()
+            eng.api["get_state"](eng.h, dt, C.byref(gs))
+            o.api["get_state"](oh, dt, C.byref(os_))
+            assert gs.as_tuple() == os_.as_tuple(), dt
+        gsum, osum = pkg.downtrack_summaries(eng.api, eng.h), pkg.downtrack_summaries(o.api, oh)
+        for f in abi.DT_SUMMARY_DTYPE.names:
+            assert np.array_equal(gsum[f], osum[f]), f
+    finally:
+        eng.close()
+        o.destroy(oh)
+        tr.close()
