@@ -498,6 +498,29 @@ int lkf_padding(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_
 int lkf_blank_frames(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
                      uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len);
 
+/* ---- RED for Opus ---------------------------------- *
+ * Both take an ExtPacket batch (grouped by track, as lkf_submit) and a map
+ * from track handle to the handle of the track the output belongs to (-1:
+ * the track's packets are not converted), and return a new ExtPacket batch
+ * (in input order, hence grouped by destination track) whose raw packets are
+ * the source RTP header followed by the new payload, 16-B aligned in
+ * out_arena — ready for lkf_submit on the destination tracks' DownTracks.
+ * Per-track state persists across calls.  Waits for queued runs.
+ *   lkf_red_encode  RedReceiver (redreceiver.go:58-207): each Opus primary
+ *                   becomes a RED packet carrying up to two earlier payloads
+ *                   of its track (RFC 2198, block PT 111);
+ *   lkf_red_decode  RedPrimaryReceiver (redprimaryreceiver.go:60-269): each
+ *                   RED packet yields the packets its blocks recover (lost
+ *                   per the 8-packet receive history; SN/TS/PT patched) and
+ *                   then its primary (which keeps the RED packet's header, as
+ *                   the reference does).  Malformed RED yields nothing. */
+int lkf_red_encode(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len,
+                   const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap, uint8_t *out_arena,
+                   uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len);
+int lkf_red_decode(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len,
+                   const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap, uint8_t *out_arena,
+                   uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len);
+
 /* ---- stream allocation ------------------------------ */
 typedef struct lkf_alloc_req {
   int32_t dt;

@@ -382,6 +382,11 @@ def bind_engine_api(lib, prefix):
     api["padding"] = _bind(lib, prefix + "padding", C.c_int,
                            [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                             P(C.c_uint32), P(C.c_uint64), C.c_void_p])
+    if hasattr(lib, prefix + "red_encode"):
+        for nm in ("red_encode", "red_decode"):
+            api[nm] = _bind(lib, prefix + nm, C.c_int,
+                            [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p,
+                             C.c_uint32, C.c_void_p, C.c_uint64, P(C.c_uint32), P(C.c_uint64)])
     if hasattr(lib, prefix + "allocate_optimal"):
         api["allocate_optimal"] = _bind(lib, prefix + "allocate_optimal", C.c_int,
                                         [e, C.c_void_p, C.c_uint32, C.c_void_p])

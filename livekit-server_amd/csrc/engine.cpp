@@ -40,6 +40,14 @@ hipError_t dalloc(T **p, size_t n) {
   return hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T));
 }
 
+template <typename T>
+static hipError_t grow(T **p, uint64_t &cap, uint64_t need) {
+  if (need <= cap) return hipSuccess;
+  if (*p) (void)hipFree(*p);
+  cap = std::max<uint64_t>(need, 1024);
+  return dalloc(p, cap);
+}
+
 constexpr int kStatsWords = 4 + LKF_DROP_NREASONS;
 constexpr uint32_t kIdle = 0xffffffffu;
 
@@ -199,6 +207,17 @@ struct lkf_engine {
   uint8_t *dRtxIn = nullptr, *dRtxOut = nullptr;
   uint64_t rtxInCap = 0, rtxOutCap = 0;
 
+  // RED per-track state (lkf_red_encode / lkf_red_decode), allocated at first use
+  RedEncState *dRedEnc = nullptr;
+  RedDecState *dRedDec = nullptr;
+  struct RedScratch {
+    lkf_pkt *in = nullptr, *out = nullptr;
+    uint8_t *inArena = nullptr, *outArena = nullptr;
+    uint32_t *g = nullptr, *cnt = nullptr;
+    int32_t *map = nullptr;
+    uint64_t *off = nullptr;
+    uint64_t inCap = 0, outCap = 0, inArenaCap = 0, outArenaCap = 0, gCap = 0, cntCap = 0, mapCap = 0, offCap = 0;
+  } red;
   // lastAllocation.BandwidthRequested per DownTrack (lkf_allocate_optimal)
   int64_t *dAllocBw = nullptr;
   lkf_alloc_req *dAllocReq = nullptr;
@@ -626,6 +645,10 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->dSrm), static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff),
                   static_cast<void *>(e->dPadCnt), static_cast<void *>(e->dPadOut), static_cast<void *>(e->dPadArena),
                   static_cast<void *>(e->dAllocBw), static_cast<void *>(e->dAllocReq),
+                  static_cast<void *>(e->dRedEnc), static_cast<void *>(e->dRedDec),
+                  static_cast<void *>(e->red.in), static_cast<void *>(e->red.out), static_cast<void *>(e->red.inArena),
+                  static_cast<void *>(e->red.outArena), static_cast<void *>(e->red.g), static_cast<void *>(e->red.cnt),
+                  static_cast<void *>(e->red.map), static_cast<void *>(e->red.off),
                   static_cast<void *>(e->dAllocOut)})
     if (p) (void)hipFree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
@@ -1799,6 +1822,140 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
       pos += al;
     }
   return LKF_OK;
+}
+
+// ---- RED for Opus (redreceiver.go, redprimaryreceiver.go) -------------------
+static int red_common(lkf_engine *e, bool decode, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena,
+                      uint64_t arena_len, const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap,
+                      uint8_t *out_arena, uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len) {
+  if (!e || !n_out || !out_arena_len || (n && (!pkts || !arena)) || (map_len && !map)) return LKF_EINVAL;
+  *n_out = 0;
+  *out_arena_len = 0;
+  const uint32_t nt = uint32_t(e->tracks.size());
+  if (map_len > nt) return LKF_EINVAL;
+  for (uint32_t t = 0; t < map_len; t++)
+    if (map[t] >= int32_t(nt) || map[t] < -1) return LKF_EINVAL;
+  // groups: the mapped tracks' contiguous packet runs (each track once)
+  std::vector<uint32_t> gb, ge;
+  std::vector<uint8_t> seen(nt, 0);
+  std::vector<uint64_t> off(2 * size_t(n) + 1, 0);
+  uint64_t recs = 0, bytes = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t t = pkts[i].track;
+    if (t >= nt || uint64_t(pkts[i].arena_off) + pkts[i].payload_off + pkts[i].payload_len > arena_len)
+      return LKF_EINVAL;
+    if (i == 0 || pkts[i - 1].track != t) {
+      if (seen[t]) return LKF_EORDER;
+      seen[t] = 1;
+      if (t < map_len && map[t] >= 0) {
+        gb.push_back(i);
+        ge.push_back(i);
+      }
+    }
+    const bool mapped = t < map_len && map[t] >= 0;
+    if (mapped) ge.back() = i + 1;
+    off[i] = recs;
+    off[n + i] = bytes;
+    if (mapped) {
+      const uint64_t hdr = pkts[i].payload_off, pl = pkts[i].payload_len;
+      recs += decode ? 3 : 1;
+      bytes += decode ? 3 * ((hdr + pl + 15) & ~15ull) : ((hdr + std::max<uint64_t>(1500, pl + 1) + 15) & ~15ull);
+    }
+  }
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  if (!gb.empty()) {
+    auto &r = e->red;
+    if (decode && !e->dRedDec) {
+      HIPCHK(dalloc(&e->dRedDec, e->cfg.max_tracks), "alloc red dec");
+      HIPCHK(hipMemset(e->dRedDec, 0, size_t(e->cfg.max_tracks) * sizeof(RedDecState)), "red dec reset");
+    }
+    if (!decode && !e->dRedEnc) {
+      HIPCHK(dalloc(&e->dRedEnc, e->cfg.max_tracks), "alloc red enc");
+      HIPCHK(hipMemset(e->dRedEnc, 0, size_t(e->cfg.max_tracks) * sizeof(RedEncState)), "red enc reset");
+    }
+    HIPCHK(grow(&r.in, r.inCap, n), "alloc red in");
+    HIPCHK(grow(&r.inArena, r.inArenaCap, arena_len + 64), "alloc red in arena");
+    HIPCHK(grow(&r.out, r.outCap, recs), "alloc red out");
+    HIPCHK(grow(&r.outArena, r.outArenaCap, bytes), "alloc red out arena");
+    HIPCHK(grow(&r.g, r.gCap, 2 * gb.size()), "alloc red groups");
+    HIPCHK(grow(&r.cnt, r.cntCap, n), "alloc red counts");
+    HIPCHK(grow(&r.map, r.mapCap, nt), "alloc red map");
+    HIPCHK(grow(&r.off, r.offCap, 2 * uint64_t(n) + 1), "alloc red offsets");
+    std::vector<int32_t> mp(nt, -1);
+    for (uint32_t t = 0; t < map_len; t++) mp[t] = map[t];
+    std::vector<uint32_t> g(gb);
+    g.insert(g.end(), ge.begin(), ge.end());
+    HIPCHK(hipMemcpy(r.in, pkts, n * sizeof(lkf_pkt), hipMemcpyHostToDevice), "red in copy");
+    HIPCHK(hipMemcpy(r.inArena, arena, arena_len, hipMemcpyHostToDevice), "red arena copy");
+    HIPCHK(hipMemcpy(r.g, g.data(), g.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "red groups copy");
+    HIPCHK(hipMemcpy(r.map, mp.data(), nt * sizeof(int32_t), hipMemcpyHostToDevice), "red map copy");
+    HIPCHK(hipMemcpy(r.off, off.data(), 2 * size_t(n) * sizeof(uint64_t), hipMemcpyHostToDevice), "red off copy");
+    HIPCHK(hipMemset(r.cnt, 0, n * sizeof(uint32_t)), "red counts reset");
+    rc = upload_done(e);
+    if (rc) return rc;
+    RedLaunch a;
+    a.in = r.in;
+    a.inArena = r.inArena;
+    a.gBegin = r.g;
+    a.gEnd = r.g + gb.size();
+    a.ngroups = uint32_t(gb.size());
+    a.map = r.map;
+    a.enc = e->dRedEnc;
+    a.dec = e->dRedDec;
+    a.recOff = r.off;
+    a.byteOff = r.off + n;
+    a.out = r.out;
+    a.outArena = r.outArena;
+    a.cnt = r.cnt;
+    HIPCHK(launch_red(e->own, decode, a), "red");
+    HIPCHK(hipStreamSynchronize(e->own), "sync");
+  }
+  std::vector<uint32_t> cnt(n, 0);
+  std::vector<lkf_pkt> rec(recs ? recs : 1);
+  std::vector<uint8_t> ar(bytes ? bytes : 1);
+  if (!gb.empty()) {
+    HIPCHK(hipMemcpy(cnt.data(), e->red.cnt, n * sizeof(uint32_t), hipMemcpyDeviceToHost), "red cnt copy");
+    if (recs) HIPCHK(hipMemcpy(rec.data(), e->red.out, recs * sizeof(lkf_pkt), hipMemcpyDeviceToHost), "red out copy");
+    if (bytes) HIPCHK(hipMemcpy(ar.data(), e->red.outArena, bytes, hipMemcpyDeviceToHost), "red arena copy");
+  }
+  uint64_t k = 0, tot = 0;
+  for (uint32_t i = 0; i < n; i++)
+    for (uint32_t c = 0; c < cnt[i]; c++) {
+      const lkf_pkt &o = rec[off[i] + c];
+      tot += (uint64_t(o.payload_off) + o.payload_len + 15) & ~15ull;
+      k++;
+    }
+  *n_out = uint32_t(k);
+  *out_arena_len = tot;
+  if (k > out_cap || tot > out_arena_cap || (k && (!out || !out_arena))) return LKF_ENOSPC;
+  uint64_t w = 0, pos = 0;
+  for (uint32_t i = 0; i < n; i++)
+    for (uint32_t c = 0; c < cnt[i]; c++) {
+      lkf_pkt o = rec[off[i] + c];
+      const uint64_t len = uint64_t(o.payload_off) + o.payload_len, al = (len + 15) & ~15ull;
+      std::memcpy(out_arena + pos, ar.data() + o.arena_off, len);
+      std::memset(out_arena + pos + len, 0, al - len);
+      o.arena_off = uint32_t(pos);
+      out[w++] = o;
+      pos += al;
+    }
+  return LKF_OK;
+}
+
+int lkf_red_encode(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len,
+                   const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap, uint8_t *out_arena,
+                   uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len) {
+  return red_common(e, false, pkts, n, arena, arena_len, map, map_len, out, out_cap, out_arena, out_arena_cap, n_out,
+                    out_arena_len);
+}
+int lkf_red_decode(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len,
+                   const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap, uint8_t *out_arena,
+                   uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len) {
+  return red_common(e, true, pkts, n, arena, arena_len, map, map_len, out, out_cap, out_arena, out_arena_cap, n_out,
+                    out_arena_len);
 }
 
 // ---- Forwarder.AllocateOptimal (forwarder.go:591-725) ----------------------

@@ -199,4 +199,31 @@ hipError_t launch_pad(hipStream_t s, const PadLaunch &a);
 hipError_t launch_allocate_optimal(hipStream_t s, const lkf_alloc_req *reqs, uint32_t n, DTHot *hot, const DevDT *dts,
                                    const DevTrack *tracks, int64_t *lastBw, lkf_allocation *out);
 
+// ---- RED for Opus (red_kernels.hip) ----
+struct RedEncState {  // RedReceiver.pktBuff (redreceiver.go:45): the last two primaries of a track
+  uint8_t has[2];
+  uint16_t sn[2];
+  uint32_t ts[2];
+  uint16_t len[2];
+  uint8_t pay[2][1500];
+};
+struct RedDecState {  // RedPrimaryReceiver (redprimaryreceiver.go:37-48)
+  uint8_t first, hist;
+  uint16_t lastSeq;
+};
+struct RedLaunch {
+  const lkf_pkt *in;
+  const uint8_t *inArena;
+  const uint32_t *gBegin, *gEnd;  // per mapped track of the batch: its packet range
+  uint32_t ngroups;
+  const int32_t *map;             // source track -> destination track
+  RedEncState *enc;
+  RedDecState *dec;
+  const uint64_t *recOff, *byteOff;  // per input packet: reserved output records / arena bytes
+  lkf_pkt *out;
+  uint8_t *outArena;
+  uint32_t *cnt;  // per input packet: packets written
+};
+hipError_t launch_red(hipStream_t s, bool decode, const RedLaunch &a);
+
 }  // namespace lkf

@@ -326,6 +326,7 @@ KAT(wraparound_uint32) {
 #include "kat_dd.inc"
 #include "kat_ddsel.inc"
 #include "kat_srtp.inc"
+#include "kat_red.inc"
 
 int main(int argc, char **argv) {
   bool list = false;

@@ -25,6 +25,8 @@
 #include "../include/lkfwd.h"
 #include "lkf_oracle.h"
 #include "srtp_oracle.h"
+#include "red_oracle.h"
+#include <map>
 
 using namespace orc;
 
@@ -101,6 +103,9 @@ struct orc_engine {
   // SRTP sessions (one per transport) and the last protected output
   std::vector<orc_srtp::Session> transports;
   std::vector<u8> protArena;
+  // RED: per source track (lkf_red_encode / lkf_red_decode)
+  std::map<u32, orc_red::RedEncoder> redEnc;
+  std::map<u32, orc_red::RedDecoder> redDec;
 };
 
 static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
@@ -823,6 +828,81 @@ static int padCommon(orc_engine *e, int blank, const lkf_pad_req *reqs, uint32_t
   if (*n_out) std::memcpy(out, e->outRecs.data(), e->outRecs.size() * sizeof(lkf_out));
   if (*arena_len) std::memcpy(arena, e->outArena.data(), e->outArena.size());
   return LKF_OK;
+}
+
+// RedReceiver / RedPrimaryReceiver over a batch (lkf_red_encode / lkf_red_decode)
+static int redCommon(orc_engine *e, bool decode, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena,
+                     uint64_t arena_len, const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap,
+                     uint8_t *out_arena, uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len) {
+  if (!n_out || !out_arena_len || (n && (!pkts || !arena)) || (map_len && !map)) return LKF_EINVAL;
+  const u32 nt = u32(e->tracks.size());
+  if (map_len > nt) return LKF_EINVAL;
+  std::vector<u8> seen(nt, 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (pkts[i].track >= nt || u64(pkts[i].arena_off) + pkts[i].payload_off + pkts[i].payload_len > arena_len)
+      return LKF_EINVAL;
+    if (i == 0 || pkts[i - 1].track != pkts[i].track) {
+      if (seen[pkts[i].track]) return LKF_EORDER;
+      seen[pkts[i].track] = 1;
+    }
+  }
+  std::vector<lkf_pkt> recs;
+  std::vector<u8> ar;
+  for (uint32_t i = 0; i < n; i++) {
+    const lkf_pkt &p = pkts[i];
+    if (p.track >= map_len || map[p.track] < 0) continue;
+    const u8 *raw = arena + p.arena_off;
+    orc_red::Pkt in;
+    in.sn = u16(p.ext_sn);
+    in.ts = u32(p.ext_ts);
+    in.pt = p.hdr1 & 0x7f;
+    in.payload.assign(raw + p.payload_off, raw + p.payload_off + p.payload_len);
+    auto emit = [&](const lkf_pkt &o, const std::vector<u8> &payload) {
+      lkf_pkt r = o;
+      r.track = u32(map[p.track]);
+      r.arena_off = u32(ar.size());
+      r.payload_len = u16(payload.size());
+      ar.insert(ar.end(), raw, raw + p.payload_off);  // the source header
+      ar.insert(ar.end(), payload.begin(), payload.end());
+      ar.resize((ar.size() + 15) & ~size_t(15), 0);
+      recs.push_back(r);
+    };
+    if (!decode) {
+      std::vector<u8> red;
+      if (e->redEnc[p.track].Encode(in, red) != orc_red::OK) continue;  // logged and dropped (redreceiver.go:64)
+      emit(p, red);
+    } else {
+      std::vector<orc_red::Pkt> outp;
+      if (e->redDec[p.track].Decode(in, outp) != orc_red::OK) continue;  // redprimaryreceiver.go:67-70
+      for (size_t k = 0; k < outp.size(); k++) {
+        lkf_pkt o = p;
+        if (k + 1 != outp.size()) {  // recovered: ExtSequenceNumber / ExtTimestamp patched (:76-80)
+          o.ext_sn -= u64(u16(outp.back().sn - outp[k].sn));
+          o.ext_ts -= u64(u32(outp.back().ts - outp[k].ts));
+          o.hdr1 = u8((p.hdr1 & 0x80) | outp[k].pt);
+        }
+        emit(o, outp[k].payload);
+      }
+    }
+  }
+  *n_out = u32(recs.size());
+  *out_arena_len = ar.size();
+  if (recs.size() > out_cap || ar.size() > out_arena_cap || (*n_out && (!out || !out_arena))) return LKF_ENOSPC;
+  if (*n_out) std::memcpy(out, recs.data(), recs.size() * sizeof(lkf_pkt));
+  if (*out_arena_len) std::memcpy(out_arena, ar.data(), ar.size());
+  return LKF_OK;
+}
+int orc_red_encode(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len,
+                   const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap, uint8_t *out_arena,
+                   uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len) {
+  return redCommon(e, false, pkts, n, arena, arena_len, map, map_len, out, out_cap, out_arena, out_arena_cap, n_out,
+                   out_arena_len);
+}
+int orc_red_decode(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len,
+                   const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap, uint8_t *out_arena,
+                   uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len) {
+  return redCommon(e, true, pkts, n, arena, arena_len, map, map_len, out, out_cap, out_arena, out_arena_cap, n_out,
+                   out_arena_len);
 }
 
 // Forwarder.AllocateOptimal for each request (lkf_allocate_optimal)
