@@ -1539,6 +1539,7 @@ struct DecideArgs {
 struct LaneOut {
   Tuple *outT;
   u64 nFwd, nBytes, nTuples;
+  i32 sentDiff;  // sendingPacket's bytesSent - sum of out_len: incoming minus outgoing header bytes
   u32 relOff;
   u32 drops[LKF_DROP_NREASONS];
   u8 *ddArena;  // this batch's marshalled DD bytes (bump-allocated)
@@ -1715,6 +1716,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   }
   o.nFwd++;
   o.nBytes += u64(hdrLen + payLen);
+  o.sentDiff += i32(p.poff) - hdrLen;  // getTranslatedRTPHeader keeps the incoming extensions (downtrack.go:1714-1726)
   o.relOff += u32((hdrLen + payLen + 15) & ~15);
 }
 
@@ -1920,6 +1922,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const u64 slot0 = A.slotBase[d];
   LaneOut o;
   o.nFwd = o.nBytes = o.nTuples = 0;
+  o.sentDiff = 0;
+  i32 sentAcc = 0;  // per lane: run-path forwarded packets' incoming minus outgoing header bytes
   o.relOff = 0;
   for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
 #if LKF_STATE_LDS
@@ -2425,6 +2429,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #endif
         }
         const u32 sumLen = wave_sum_u32(outLen);
+        sentAcc += fwd ? i32(p.poff) - hdrLen : 0;  // (reduced once per DownTrack)
         // ---- advance the DownTrack state past the run (uniform)
         if (fwR) {
           o.nBytes += sumLen;
@@ -2638,13 +2643,15 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       L.vc->missVal[idx] = sMissVal[idx];
     }
   }
+  const i32 sentRun = i32(wave_sum_u32(u32(sentAcc)));  // (every lane: a cross-lane reduction)
   if (lane == 0) {
     A.fwdCnt[d] = u32(o.nFwd);
     A.fwdBytes[d] = o.relOff;
     // DownTrack.sendingPacket: bytesSent += header + payload (downtrack.go:1934-1940)
     // (atomics without return: the wave does not wait for a read of the old totals)
     if (o.nFwd) atomicAdd((unsigned long long *)&A.dtCum[d].packets, (unsigned long long)o.nFwd);
-    if (o.nBytes) atomicAdd((unsigned long long *)&A.dtCum[d].bytes, (unsigned long long)o.nBytes);
+    const u64 nSent = o.nBytes + u64(i64(sentRun) + o.sentDiff);
+    if (nSent) atomicAdd((unsigned long long *)&A.dtCum[d].bytes, (unsigned long long)nSent);
     A.dtCum[d].flags = L.h.flags;
     // counters: one of kStatCopies partial copies per wave (same-address
     // atomics from every wave would serialise in one L2 channel); k_stats_reduce

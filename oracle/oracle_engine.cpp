@@ -44,6 +44,7 @@ struct OTrack {
 struct OOut {
   lkf_out rec;
   std::vector<u8> bytes;
+  u64 sent = 0;  // sendingPacket: hdr.MarshalSize() + len(payload) (downtrack.go:1931-1939)
 };
 
 struct ODT {
@@ -227,7 +228,8 @@ static ExtPacket toExt(const lkf_pkt &d, const u8 *arena, const lkf_pkt_dd *dd, 
 }
 
 // DownTrack.WriteRTP downtrack.go:680-760 on the virtual clock.
-static void writeRTP(orc_engine *e, u32 dtIdx, ODT &d, const ExtPacket &ep, u32 pktIdx, int8_t layer) {
+static void writeRTP(orc_engine *e, u32 dtIdx, ODT &d, const ExtPacket &ep, u32 pktIdx, int8_t layer,
+                     u32 pd_payload_off) {
   e->stats.tuples++;
   TranslationParams tp;
   Err err = d.f->GetTranslationParams(ep, layer, ep.Arrival, tp);
@@ -272,6 +274,9 @@ static void writeRTP(orc_engine *e, u32 dtIdx, ODT &d, const ExtPacket &ep, u32 
     d.extStartTS = tp.rtp.extTimestamp;
   }
   OOut o;
+  // getTranslatedRTPHeader keeps the incoming header's extensions: the
+  // counted header is the incoming one (the raw header, payload_off bytes)
+  o.sent = u64(pd_payload_off) + payload.size();
   hdr.Marshal(o.bytes);
   o.bytes.insert(o.bytes.end(), payload.begin(), payload.end());
   std::memset(&o.rec, 0, sizeof(o.rec));
@@ -406,7 +411,7 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
     for (u32 d : trackDts[pd.track]) {
       ODT &dt = *e->dts[d];
       while (evc[d] < evq[d].size() && evq[d][evc[d]].at <= i) applyCtl(e, dt, evq[d][evc[d]++]);
-      writeRTP(e, d, dt, ep, i, pd.layer);
+      writeRTP(e, d, dt, ep, i, pd.layer, pd.payload_off);
     }
   }
   for (u32 d = 0; d < ndt; d++)
@@ -414,7 +419,7 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   for (u32 d = 0; d < ndt; d++)  // sendingPacket: bytesSent += hdrSize + payloadSize
     for (auto &o : e->dts[d]->outs) {
       e->dts[d]->packetsSent++;
-      e->dts[d]->bytesSent += o.bytes.size();
+      e->dts[d]->bytesSent += o.sent;
     }
   // Output order: by track, then DownTrack handle, then packet; wire packets
   // 16-B aligned.  (An engine-defined batch layout: the reference hands each
