@@ -521,6 +521,38 @@ int lkf_red_decode(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t
                    const int32_t *map, uint32_t map_len, lkf_pkt *out, uint32_t out_cap, uint8_t *out_arena,
                    uint64_t out_arena_cap, uint32_t *n_out, uint64_t *out_arena_len);
 
+/* ---- stream trackers -------------------------------- *
+ * StreamTrackerManager's per-spatial-layer packet trackers (streamtracker.go,
+ * streamtracker_packet.go), fed by every lkf_run batch as forwardRTP does
+ * (receiver.go:686-695: packets of the tracker's layer with a payload; the
+ * packet size is header + payload, a padded packet's padding not counted).
+ * The worker goroutine's tickers are host-driven: lkf_stream_trackers_tick
+ * with check = 1 at each CycleDuration (CheckStatus) and bitrate_elapsed_ns >
+ * 0 at each BitrateReportInterval (the bitrate report over that interval).
+ * A tracker's worker runs from its first observed packet after a reset until
+ * LKF_TRACKER_RESET / PAUSE / STOP; ticks without a live worker change
+ * nothing.  The statuses and bitrates feed lkf_allocate_optimal's
+ * available_layers and bitrates. */
+typedef struct lkf_tracker_status {
+  int32_t tracker;
+  uint8_t status;          /* StreamStatus: 0 stopped, 1 active */
+  uint8_t bitrate_changed; /* onBitrateAvailable fired by this tick's report */
+  uint8_t reserved[2];
+  uint32_t notifications;  /* onStatusChanged calls since the tracker was added */
+  uint32_t reserved2;
+  int64_t bitrate[4];      /* per temporal layer, bps (the last report) */
+  int64_t cumulative[4];   /* BitrateTemporalCumulative */
+} lkf_tracker_status;
+#define LKF_TRACKER_RESET 1 /* StreamTracker.Reset */
+#define LKF_TRACKER_PAUSE 2 /* StreamTracker.SetPaused(arg) */
+#define LKF_TRACKER_STOP 3  /* StreamTracker.Stop */
+/* A StreamTrackerPacket(samples_required, cycles_required) for (track, spatial layer). >= 0 handle. */
+int32_t lkf_add_stream_tracker(lkf_engine *e, int32_t track, int32_t layer, uint32_t samples_required,
+                               uint32_t cycles_required);
+int lkf_stream_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t arg);
+int lkf_stream_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n, int check, int64_t bitrate_elapsed_ns,
+                             lkf_tracker_status *out);
+
 /* ---- stream allocation ------------------------------ */
 typedef struct lkf_alloc_req {
   int32_t dt;

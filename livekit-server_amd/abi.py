@@ -114,6 +114,11 @@ ALLOCATION_DTYPE = np.dtype([("dt", "<i4"), ("pause_reason", "<i4"), ("bandwidth
                              ("max_temporal", "<i4"), ("is_deficient", "u1"), ("reserved", "u1", 3),
                              ("distance_to_desired", "<f8")])
 assert ALLOCATION_DTYPE.itemsize == 64
+TRACKER_STATUS_DTYPE = np.dtype([("tracker", "<i4"), ("status", "u1"), ("bitrate_changed", "u1"), ("reserved", "u1", 2),
+                                 ("notifications", "<u4"), ("reserved2", "<u4"), ("bitrate", "<i8", 4),
+                                 ("cumulative", "<i8", 4)])
+assert TRACKER_STATUS_DTYPE.itemsize == 80
+TRACKER_RESET, TRACKER_PAUSE, TRACKER_STOP = 1, 2, 3
 PAD_ON_MUTE = 0x1
 PAD_FORCE_MARKER = 0x2
 PAD_WRITABLE = 0x4
@@ -382,6 +387,12 @@ def bind_engine_api(lib, prefix):
     api["padding"] = _bind(lib, prefix + "padding", C.c_int,
                            [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                             P(C.c_uint32), P(C.c_uint64), C.c_void_p])
+    if hasattr(lib, prefix + "add_stream_tracker"):
+        api["add_stream_tracker"] = _bind(lib, prefix + "add_stream_tracker", C.c_int32,
+                                          [e, C.c_int32, C.c_int32, C.c_uint32, C.c_uint32])
+        api["stream_tracker_ctl"] = _bind(lib, prefix + "stream_tracker_ctl", C.c_int, [e, C.c_int32, C.c_int32, C.c_int32])
+        api["stream_trackers_tick"] = _bind(lib, prefix + "stream_trackers_tick", C.c_int,
+                                            [e, C.c_void_p, C.c_uint32, C.c_int, C.c_int64, C.c_void_p])
     if hasattr(lib, prefix + "red_encode"):
         for nm in ("red_encode", "red_decode"):
             api[nm] = _bind(lib, prefix + nm, C.c_int,

@@ -207,6 +207,12 @@ struct lkf_engine {
   uint8_t *dRtxIn = nullptr, *dRtxOut = nullptr;
   uint64_t rtxInCap = 0, rtxOutCap = 0;
 
+  // stream trackers (lkf_add_stream_tracker): device state, tick scratch
+  TrackerState *dTrk = nullptr;
+  uint32_t nTrk = 0, trkCap = 0;
+  int32_t *dTrkIds = nullptr;
+  lkf_tracker_status *dTrkOut = nullptr;
+  uint64_t trkIdsCap = 0, trkOutCap = 0;
   // RED per-track state (lkf_red_encode / lkf_red_decode), allocated at first use
   RedEncState *dRedEnc = nullptr;
   RedDecState *dRedDec = nullptr;
@@ -645,7 +651,8 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->dSrm), static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff),
                   static_cast<void *>(e->dPadCnt), static_cast<void *>(e->dPadOut), static_cast<void *>(e->dPadArena),
                   static_cast<void *>(e->dAllocBw), static_cast<void *>(e->dAllocReq),
-                  static_cast<void *>(e->dRedEnc), static_cast<void *>(e->dRedDec),
+                  static_cast<void *>(e->dRedEnc), static_cast<void *>(e->dRedDec), static_cast<void *>(e->dTrk),
+                  static_cast<void *>(e->dTrkIds), static_cast<void *>(e->dTrkOut),
                   static_cast<void *>(e->red.in), static_cast<void *>(e->red.out), static_cast<void *>(e->red.inArena),
                   static_cast<void *>(e->red.outArena), static_cast<void *>(e->red.g), static_cast<void *>(e->red.cnt),
                   static_cast<void *>(e->red.map), static_cast<void *>(e->red.off),
@@ -1083,6 +1090,8 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(launch_layer_index(ps, e->curPkts, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
                             x.dLayerBefore, x.dLayerCnt),
          "layer index");
+  if (e->nTrk)  // StreamTracker.Observe of every (track, spatial layer) tracker (receiver.go:686-695)
+    HIPCHK(launch_tracker_observe(ps, e->dTrk, e->nTrk, e->curPkts, x.dTBegin, x.dTEnd), "tracker observe");
   if (e->ddAlloc) {  // dependency descriptors of this batch (track structure rings advance in order)
     HIPCHK(hipMemsetAsync(x.dDDUsed, 0, sizeof(uint64_t), ps), "dd cursor reset");
     HIPCHK(launch_dd_decode(ps, e->curPkts, e->curDD, e->curArena, x.dTBegin, x.dTEnd, e->dTracks, nt, e->dDDStruct,
@@ -1821,6 +1830,102 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
       out[w++] = o;
       pos += al;
     }
+  return LKF_OK;
+}
+
+// ---- stream trackers (streamtracker.go, streamtracker_packet.go) ------------
+int32_t lkf_add_stream_tracker(lkf_engine *e, int32_t track, int32_t layer, uint32_t samples_required,
+                               uint32_t cycles_required) {
+  if (!e || track < 0 || track >= int32_t(e->tracks.size()) || layer < 0) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  if (e->nTrk + 1 > e->trkCap) {
+    const uint32_t cap = std::max<uint32_t>(2 * e->trkCap, 1024);
+    TrackerState *n = nullptr;
+    HIPCHK(dalloc(&n, cap), "alloc trackers");
+    if (e->nTrk) HIPCHK(hipMemcpy(n, e->dTrk, e->nTrk * sizeof(TrackerState), hipMemcpyDeviceToDevice), "trackers move");
+    if (e->dTrk) HIPCHK(hipFree(e->dTrk), "free trackers");
+    e->dTrk = n;
+    e->trkCap = cap;
+  }
+  TrackerState t = {};
+  t.track = uint32_t(track);
+  t.layer = layer;
+  t.samples = samples_required;
+  t.cycles = cycles_required;
+  HIPCHK(hipMemcpy(e->dTrk + e->nTrk, &t, sizeof(t), hipMemcpyHostToDevice), "tracker init");
+  rc = upload_done(e);
+  if (rc) return rc;
+  return int32_t(e->nTrk++);
+}
+
+// Reset / SetPaused / Stop (streamtracker.go:127-185) on the host copy of the state
+int lkf_stream_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t arg) {
+  if (!e || tracker < 0 || uint32_t(tracker) >= e->nTrk) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  TrackerState t;
+  HIPCHK(hipMemcpy(&t, e->dTrk + tracker, sizeof(t), hipMemcpyDeviceToHost), "tracker read");
+  auto resetLocked = [&]() {
+    t.workerLive = 0;  // generation bump: the worker exits
+    t.status = 0;
+    for (int i = 0; i < 4; i++) t.bytes[i] = t.bitrate[i] = 0;
+    t.countSinceLast = t.cycleCount = 0;
+    t.initialized = 0;
+  };
+  auto notify = [&]() {
+    if (t.status != t.lastNotified) {
+      t.lastNotified = t.status;
+      t.notifications++;
+    }
+  };
+  switch (op) {
+    case LKF_TRACKER_RESET:
+      if (t.stopped) return LKF_OK;
+      resetLocked();
+      notify();
+      break;
+    case LKF_TRACKER_PAUSE:
+      t.paused = arg != 0;
+      if (!t.paused) {
+        resetLocked();
+      } else {
+        t.workerLive = 0;
+        t.status = 0;
+      }
+      notify();
+      break;
+    case LKF_TRACKER_STOP:
+      if (t.stopped) return LKF_OK;
+      t.stopped = 1;
+      t.workerLive = 0;
+      break;
+    default:
+      return LKF_EINVAL;
+  }
+  HIPCHK(hipMemcpy(e->dTrk + tracker, &t, sizeof(t), hipMemcpyHostToDevice), "tracker write");
+  return upload_done(e);
+}
+
+int lkf_stream_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n, int check, int64_t bitrate_elapsed_ns,
+                             lkf_tracker_status *out) {
+  if (!e || (n && (!trackers || !out))) return LKF_EINVAL;
+  if (!n) return LKF_OK;
+  std::vector<uint8_t> seen(e->nTrk, 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (trackers[i] < 0 || uint32_t(trackers[i]) >= e->nTrk || seen[trackers[i]]) return LKF_EINVAL;
+    seen[trackers[i]] = 1;
+  }
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  HIPCHK(grow(&e->dTrkIds, e->trkIdsCap, n), "alloc tracker ids");
+  HIPCHK(grow(&e->dTrkOut, e->trkOutCap, n), "alloc tracker out");
+  HIPCHK(hipMemcpy(e->dTrkIds, trackers, n * sizeof(int32_t), hipMemcpyHostToDevice), "tracker ids copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_tracker_tick(e->own, e->dTrk, e->dTrkIds, n, check, bitrate_elapsed_ns, e->dTrkOut), "tracker tick");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  HIPCHK(hipMemcpy(out, e->dTrkOut, n * sizeof(lkf_tracker_status), hipMemcpyDeviceToHost), "tracker out copy");
   return LKF_OK;
 }
 

@@ -226,4 +226,19 @@ struct RedLaunch {
 };
 hipError_t launch_red(hipStream_t s, bool decode, const RedLaunch &a);
 
+// ---- stream trackers (tracker_kernels.hip) ----
+struct TrackerState {  // StreamTracker + StreamTrackerPacket of one (track, spatial layer)
+  uint32_t track;
+  int32_t layer;
+  uint32_t samples, cycles;  // SamplesRequired, CyclesRequired
+  uint32_t countSinceLast, cycleCount, notifications;
+  uint8_t initialized, paused, stopped, workerLive, status, lastNotified, bitrateChanged, pad;
+  int64_t bytes[4];    // bytesForBitrate
+  int64_t bitrate[4];
+};
+hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const lkf_pkt *pkts,
+                                  const uint32_t *tBegin, const uint32_t *tEnd);
+hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
+                               int64_t elapsedNs, lkf_tracker_status *out);
+
 }  // namespace lkf

@@ -1,0 +1,125 @@
+// tracker_kernels.hip — the packet stream tracker of every (track, spatial
+// layer) on the GPU (StreamTracker.Observe from
+// WebRTCReceiver.forwardRTP receiver.go:686-695; streamtracker.go:57-320,
+// streamtracker_packet.go:29-97).
+//   k_tracker_observe  per batch: one wave per tracker counts its layer's
+//                      packets (payload > 0) and bytes per temporal layer —
+//                      order-free sums, except the first packet after a reset,
+//                      which activates the tracker (and starts its worker)
+//   k_tracker_tick     the worker's tickers, driven by the host: CheckStatus
+//                      (cycle counting) and the bitrate report, one thread each
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace lkf {
+namespace {
+using u32 = uint32_t;
+using i64 = int64_t;
+using u64 = uint64_t;
+
+__device__ __forceinline__ u64 wsum(u64 v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ void notify(TrackerState &s) {  // maybeNotifyStatus streamtracker.go:104-118
+  if (s.status != s.lastNotified) {
+    s.lastNotified = s.status;
+    s.notifications++;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_tracker_observe(TrackerState *st, u32 n, const lkf_pkt *__restrict__ pkts,
+                                                        const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd) {
+  const u32 k = blockIdx.x;
+  if (k >= n) return;
+  TrackerState s = st[k];  // (wave-uniform)
+  if (s.stopped || s.paused) return;
+  const u32 b = tBegin[s.track], e = tEnd[s.track];
+  u64 cnt = 0, bytes[4] = {0, 0, 0, 0};
+  for (u32 i = b + threadIdx.x; i < e; i += 64) {
+    const lkf_pkt &p = pkts[i];
+    if (p.layer != s.layer || p.payload_len == 0) continue;
+    cnt++;
+    // len(pkt.RawPacket): header + payload (the padding of a padded packet is not in lkf_pkt)
+    const int t = p.temporal;
+    if (t >= 0 && t < 4) bytes[t] += u64(p.payload_off) + p.payload_len;
+  }
+  cnt = wsum(cnt);
+  for (int t = 0; t < 4; t++) bytes[t] = wsum(bytes[t]);
+  if (threadIdx.x != 0 || cnt == 0) return;
+  if (!s.initialized) {  // StreamTrackerPacket.Observe: the first packet activates
+    s.initialized = 1;
+    s.countSinceLast = u32(cnt);
+    s.status = 1;
+    s.workerLive = 1;  // go s.worker(generation)
+    notify(s);
+  } else {
+    s.countSinceLast += u32(cnt);
+  }
+  for (int t = 0; t < 4; t++) s.bytes[t] += i64(bytes[t]);
+  st[k] = s;
+}
+
+__global__ void k_tracker_tick(TrackerState *st, const int32_t *__restrict__ ids, u32 n, int check, i64 elapsedNs,
+                               lkf_tracker_status *out) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  TrackerState s = st[ids[i]];
+  s.bitrateChanged = 0;
+  if (s.workerLive) {
+    if (check && s.initialized) {  // updateStatus -> StreamTrackerPacket.CheckStatus
+      if (s.countSinceLast >= s.samples)
+        s.cycleCount++;
+      else
+        s.cycleCount = 0;
+      if (s.cycleCount == 0)
+        s.status = 0;
+      else if (s.cycleCount >= s.cycles)
+        s.status = 1;
+      s.countSinceLast = 0;
+    }
+    if (check) notify(s);
+    if (elapsedNs > 0) {  // bitrateReport
+      const double secs = double(elapsedNs) / 1e9;
+      for (int t = 0; t < 4; t++) {
+        const i64 br = i64(double(s.bytes[t] * 8) / secs);
+        if ((s.bitrate[t] == 0 && br > 0) || (s.bitrate[t] > 0 && br == 0)) s.bitrateChanged = 1;
+        s.bitrate[t] = br;
+        s.bytes[t] = 0;
+      }
+    }
+  }
+  st[ids[i]] = s;
+  lkf_tracker_status o = {};
+  o.tracker = ids[i];
+  o.status = s.status;
+  o.bitrate_changed = s.bitrateChanged;
+  o.notifications = s.notifications;
+  i64 c[4];
+  for (int t = 0; t < 4; t++) o.bitrate[t] = c[t] = s.bitrate[t];
+  for (int t = 3; t >= 1; t--)  // BitrateTemporalCumulative streamtracker.go:221-247
+    if (c[t] != 0)
+      for (int j = t - 1; j >= 0; j--) c[t] += c[j];
+  for (int t = 0; t < 4; t++)
+    if (c[t] == 0)
+      for (int j = t + 1; j < 4; j++) c[j] = 0;
+  for (int t = 0; t < 4; t++) o.cumulative[t] = c[t];
+  out[i] = o;
+}
+}  // namespace
+
+hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const lkf_pkt *pkts,
+                                  const uint32_t *tBegin, const uint32_t *tEnd) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_tracker_observe, dim3(n), dim3(64), 0, s, st, n, pkts, tBegin, tEnd);
+  return hipGetLastError();
+}
+hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
+                               int64_t elapsedNs, lkf_tracker_status *out) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_tracker_tick, dim3((n + 63) / 64), dim3(64), 0, s, st, ids, n, check, elapsedNs, out);
+  return hipGetLastError();
+}
+
+}  // namespace lkf

@@ -327,6 +327,7 @@ KAT(wraparound_uint32) {
 #include "kat_ddsel.inc"
 #include "kat_srtp.inc"
 #include "kat_red.inc"
+#include "kat_tracker.inc"
 
 int main(int argc, char **argv) {
   bool list = false;

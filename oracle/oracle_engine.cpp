@@ -26,6 +26,7 @@
 #include "lkf_oracle.h"
 #include "srtp_oracle.h"
 #include "red_oracle.h"
+#include "tracker_oracle.h"
 #include <map>
 
 using namespace orc;
@@ -107,6 +108,9 @@ struct orc_engine {
   // RED: per source track (lkf_red_encode / lkf_red_decode)
   std::map<u32, orc_red::RedEncoder> redEnc;
   std::map<u32, orc_red::RedDecoder> redDec;
+  // stream trackers: (track, spatial layer) and the tracker
+  std::vector<std::pair<u32, i32>> trkKey;
+  std::vector<orc_st::Tracker> trk;
 };
 
 static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
@@ -416,6 +420,13 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   }
   for (u32 d = 0; d < ndt; d++)
     while (evc[d] < evq[d].size()) applyCtl(e, *e->dts[d], evq[d][evc[d]++]);
+  // spatialTracker.Observe after each packet's fan-out (receiver.go:686-695);
+  // len(RawPacket) = header + payload (padding not counted, as the engine)
+  if (!e->trk.empty())
+    for (u32 i = 0; i < n; i++)
+      for (size_t k = 0; k < e->trk.size(); k++)
+        if (e->trkKey[k].first == pkts[i].track && e->trkKey[k].second == pkts[i].layer)
+          e->trk[k].Observe(pkts[i].temporal, int(pkts[i].payload_off) + pkts[i].payload_len, pkts[i].payload_len);
   for (u32 d = 0; d < ndt; d++)  // sendingPacket: bytesSent += hdrSize + payloadSize
     for (auto &o : e->dts[d]->outs) {
       e->dts[d]->packetsSent++;
@@ -832,6 +843,49 @@ static int padCommon(orc_engine *e, int blank, const lkf_pad_req *reqs, uint32_t
   if (e->outRecs.size() > out_cap || e->outArena.size() > arena_cap || (*n_out && (!out || !arena))) return LKF_ENOSPC;
   if (*n_out) std::memcpy(out, e->outRecs.data(), e->outRecs.size() * sizeof(lkf_out));
   if (*arena_len) std::memcpy(arena, e->outArena.data(), e->outArena.size());
+  return LKF_OK;
+}
+
+// stream trackers (lkf_add_stream_tracker / _ctl / _tick)
+int32_t orc_add_stream_tracker(orc_engine *e, int32_t track, int32_t layer, uint32_t samples, uint32_t cycles) {
+  if (track < 0 || track >= (int)e->tracks.size() || layer < 0) return LKF_EINVAL;
+  e->trkKey.push_back({u32(track), layer});
+  e->trk.emplace_back(samples, cycles);
+  return int32_t(e->trk.size() - 1);
+}
+int orc_stream_tracker_ctl(orc_engine *e, int32_t tracker, int32_t op, int32_t arg) {
+  if (tracker < 0 || tracker >= (int)e->trk.size()) return LKF_EINVAL;
+  orc_st::Tracker &t = e->trk[tracker];
+  if (op == LKF_TRACKER_RESET)
+    t.Reset();
+  else if (op == LKF_TRACKER_PAUSE)
+    t.SetPaused(arg != 0);
+  else if (op == LKF_TRACKER_STOP)
+    t.Stop();
+  else
+    return LKF_EINVAL;
+  return LKF_OK;
+}
+int orc_stream_trackers_tick(orc_engine *e, const int32_t *ids, uint32_t n, int check, int64_t elapsed,
+                             lkf_tracker_status *out) {
+  if (n && (!ids || !out)) return LKF_EINVAL;
+  std::vector<u8> seen(e->trk.size(), 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (ids[i] < 0 || ids[i] >= (int)e->trk.size() || seen[ids[i]]) return LKF_EINVAL;
+    seen[ids[i]] = 1;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    orc_st::Tracker &t = e->trk[ids[i]];
+    t.Tick(check != 0, elapsed);
+    lkf_tracker_status &o = out[i];
+    std::memset(&o, 0, sizeof(o));
+    o.tracker = ids[i];
+    o.status = u8(t.status);
+    o.bitrate_changed = t.bitrateChanged;
+    o.notifications = u32(t.notifications);
+    for (int k = 0; k < 4; k++) o.bitrate[k] = t.bitrate[k];
+    t.Cumulative(o.cumulative);
+  }
   return LKF_OK;
 }
 

@@ -1,0 +1,61 @@
+"""Packet stream trackers (StreamTracker + StreamTrackerPacket,
+streamtracker.go / streamtracker_packet.go; Observe from forwardRTP
+receiver.go:686-695), engine vs oracle.
+
+Every (video track, spatial layer) of a trace gets a tracker with random
+SamplesRequired / CyclesRequired; 100-ms batches are forwarded, CheckStatus
+ticks come every 500 ms and bitrate reports every second, and trackers are
+reset, paused, resumed and stopped along the way: statuses, notification
+counts, bitrates and cumulative bitrates must match at every tick."""
+import numpy as np
+import pytest
+
+from tests import tracker_lib
+from tests.oracle_lib import load as load_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=3, seed=7), dict(config=1, seed=3)])
+def test_stream_trackers_match_oracle(pkg, workload, cfg):
+    o = load_oracle()
+    abi = pkg.abi
+    kw = dict(cfg)
+    tr = workload.Trace(kw.pop("config"), duration_s=6.0, batch_s=0.1, **kw)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    rng = np.random.default_rng(2)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+        ids = tracker_lib.add_trackers(eng.api, eng.h, tr, seed=5)
+        assert np.array_equal(ids, tracker_lib.add_trackers(o.api, oh, tr, seed=5))
+        changes = 0
+        for b in range(tr.nbatches):
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            eng.submit(pk, n, ar, alen)
+            eng.run()
+            eng.sync()
+            o.run(oh, pk, n, ar, alen)
+            eng.drain()
+            if b % 5 == 4 or b % 10 == 9:
+                check, el = b % 5 == 4, (10**9 if b % 10 == 9 else 0)
+                g = tracker_lib.tick(eng.api, eng.h, ids, check, el)
+                r = tracker_lib.tick(o.api, oh, ids, check, el)
+                for f in ("tracker", "status", "bitrate_changed", "notifications", "bitrate", "cumulative"):
+                    assert np.array_equal(g[f], r[f]), (b, f)
+                changes += int(r["bitrate_changed"].sum())
+            if b % 10 == 3:  # reset / pause / resume / stop a few trackers
+                for k in rng.choice(ids, size=min(4, len(ids)), replace=False):
+                    op = int(rng.integers(1, 4))
+                    arg = int(rng.integers(0, 2))
+                    assert eng.api["stream_tracker_ctl"](eng.h, int(k), op, arg) == 0
+                    assert o.api["stream_tracker_ctl"](oh, int(k), op, arg) == 0
+        final = tracker_lib.tick(o.api, oh, ids, True, 0)
+        assert (final["status"] == 1).any() and changes > 0
+    finally:
+        eng.close()
+        o.destroy(oh)
+        tr.close()

@@ -1,0 +1,29 @@
+"""Stream-tracker helpers shared by the CPU (oracle) and GPU (engine vs oracle)
+tests: one packet tracker per (video track, spatial layer) of a trace, driven
+batch by batch with host ticks at CycleDuration / BitrateReportInterval."""
+import ctypes as C
+import importlib
+
+import numpy as np
+
+abi = importlib.import_module("livekit-server_amd.abi")
+
+
+def add_trackers(api, h, trace, seed):
+    rng = np.random.default_rng(seed)
+    ids = []
+    for t in range(trace.ntracks):
+        if trace.tracks[t].kind != 1:
+            continue
+        for layer in range(3):
+            samples, cycles = int(rng.integers(1, 9)), int(rng.integers(1, 7))
+            k = api["add_stream_tracker"](h, t, layer, samples, cycles)
+            assert k >= 0
+            ids.append(k)
+    return np.array(ids, dtype=np.int32)
+
+
+def tick(api, h, ids, check, elapsed_ns):
+    out = np.zeros(len(ids), dtype=abi.TRACKER_STATUS_DTYPE)
+    assert api["stream_trackers_tick"](h, ids.ctypes.data, len(ids), int(check), int(elapsed_ns), out.ctypes.data) == 0
+    return out
