@@ -20,12 +20,30 @@ from tests import golden_lib  # noqa: E402
 from tests.oracle_lib import load as load_oracle  # noqa: E402
 
 
+def main_control(o, abi, wl, pkg):
+    for name, kw in golden_lib.CONTROL_CASES:
+        tr = wl.Trace(**kw)
+        h = o.create(500)
+        fx = golden_lib.run_control_case(o.api, h, tr, wl, lambda: pkg.drain_arrays(o.api, h),
+                                         lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi)
+        fx["case"] = name
+        fx["trace"] = kw
+        with open(golden_lib.path(name), "w") as f:
+            json.dump(fx, f, indent=1, sort_keys=True)
+        o.destroy(h)
+        tr.close()
+        print("wrote", golden_lib.path(name), "steps", len(fx["steps"]))
+
+
 def main():
     abi = importlib.import_module("livekit-server_amd.abi")
     wl = importlib.import_module("livekit-server_amd.workload")
     pkg = importlib.import_module("livekit-server_amd")
     o = load_oracle()
     os.makedirs(golden_lib.GOLDEN_DIR, exist_ok=True)
+    main_control(o, abi, wl, pkg)
+    if "--control-only" in sys.argv:
+        return
     for name, kw in golden_lib.CASES:
         tr = wl.Trace(**kw)
         h = o.create(500)

@@ -85,3 +85,63 @@ def run_case(api, h, trace, workload, stats_fn, drain_fn, run_fn, abi):
     out["state_sha256"] = state_digest(api, h, trace.ndts, abi)
     out["ndts"] = int(trace.ndts)
     return out
+
+
+# ---- control paths between batches (padding, blank frames, AllocateOptimal,
+# RED, stream trackers, NACK lookups) on one trace: one digest per step ----
+CONTROL_CASES = [
+    ("control_config2", dict(config=2, duration_s=3.0, batch_s=0.25, rooms=2, seed=23)),
+]
+
+
+def _sha(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def run_control_case(api, h, trace, workload, drain_fn, run_fn, abi):
+    """Drives `trace` with control calls between its batches; returns the fixture dict."""
+    from tests import pad_lib, red_lib, rtx_lib, tracker_lib
+    from tests.test_alloc_gpu import make_alloc_reqs
+    workload.load_topology(api, h, trace)
+    ids = tracker_lib.add_trackers(api, h, trace, seed=11)
+    m = red_lib.opus_map(trace)
+    out = {"steps": []}
+    epoch = 1700000000 * 10**9
+    for b in range(trace.nbatches):
+        now = epoch + int(b * 0.25e9)
+        if b % 4 == 1:  # padding probe
+            reqs = pad_lib.make_reqs(trace.ndts, seed=b, frac=0.5)
+            rec, war, sent = pad_lib.pad(api, h, reqs, now)
+            out["steps"].append(["padding", b, int(len(rec)), _sha(rec, war, sent)])
+        if b % 4 == 2:  # allocation
+            reqs = make_alloc_reqs(abi, trace.ndts, seed=b)
+            a = np.zeros(len(reqs), dtype=abi.ALLOCATION_DTYPE)
+            assert api["allocate_optimal"](h, reqs.ctypes.data, len(reqs), a.ctypes.data) == 0
+            out["steps"].append(["allocate", b, int(len(a)), _sha(a)])
+        if b % 4 == 3:  # blank frames
+            reqs = pad_lib.make_reqs(trace.ndts, seed=100 + b, frac=0.3)
+            rec, war, _ = pad_lib.pad(api, h, reqs, now, blank=True)
+            out["steps"].append(["blank", b, int(len(rec)), _sha(rec, war)])
+        workload.queue_events(api, h, trace, b)
+        pk, n, ar, alen = trace.batch(b)
+        run_fn(pk, n, ar, alen)
+        rec, war = drain_fn()
+        out["steps"].append(["batch", b, int(len(rec)), _sha(records_digest(rec) if len(rec) else "", war)])
+        pkts, n2, arena, alen2 = red_lib.batch_arrays(trace, b)
+        rp, k, rar = red_lib.red(api, h, "red_encode", pkts, n2, arena, alen2, m)
+        keep = np.arange(k) % 4 != 2
+        lp, lk = red_lib.drop(rp, k, keep)
+        dp, dk, dar = red_lib.red(api, h, "red_decode", lp, lk, rar, len(rar), m)
+        out["steps"].append(["red", b, int(k), int(dk), _sha(rp, rar, dp, dar)])
+        if b % 2 == 1:
+            t = tracker_lib.tick(api, h, ids, True, 500_000_000 if b % 4 == 3 else 0)
+            t = t[["tracker", "status", "bitrate_changed", "notifications", "bitrate", "cumulative"]]
+            out["steps"].append(["trackers", b, int(len(t)), _sha(t.tobytes())])
+    nacks = rtx_lib.make_nacks(api, h, trace, seed=3)
+    r = rtx_lib.rtx_lookup(api, h, nacks, epoch + int(trace.nbatches * 0.25e9) + 10**8)
+    out["steps"].append(["rtx", trace.nbatches, int(len(r)), _sha(r)])
+    out["state_sha256"] = state_digest(api, h, trace.ndts, abi)
+    return out

@@ -63,3 +63,50 @@ def test_engine_matches_golden(name, workload, abi, pkg):
         eng.close()
         tr.close()
     _compare(got, want)
+
+
+CONTROL_NAMES = [c[0] for c in golden_lib.CONTROL_CASES]
+CONTROL_KW = dict(golden_lib.CONTROL_CASES)
+
+
+def _compare_control(got, want):
+    assert len(got["steps"]) == len(want["steps"])
+    for g, w in zip(got["steps"], want["steps"]):
+        assert g == w, "step %s: got %s want %s" % (w[:2], g, w)
+    assert got["state_sha256"] == want["state_sha256"]
+
+
+@pytest.mark.parametrize("name", CONTROL_NAMES)
+def test_oracle_matches_control_golden(name, workload, abi, pkg):
+    """padding, blank frames, AllocateOptimal, RED, stream trackers, NACK lookups between batches"""
+    want = golden_lib.load(name)
+    assert want["trace"] == CONTROL_KW[name]
+    o = load_oracle()
+    tr = workload.Trace(**CONTROL_KW[name])
+    h = o.create(500)
+    try:
+        got = golden_lib.run_control_case(o.api, h, tr, workload, lambda: pkg.drain_arrays(o.api, h),
+                                          lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi)
+    finally:
+        o.destroy(h)
+        tr.close()
+    _compare_control(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CONTROL_NAMES)
+def test_engine_matches_control_golden(name, workload, abi, pkg):
+    want = golden_lib.load(name)
+    tr = workload.Trace(**CONTROL_KW[name])
+    eng = pkg.Engine.for_trace(tr, headroom=3.5)
+    try:
+        def run(pk, n, ar, alen):
+            eng.submit(pk, n, ar, alen)
+            eng.run()
+            eng.sync()
+
+        got = golden_lib.run_control_case(eng.api, eng.h, tr, workload, eng.drain, run, abi)
+    finally:
+        eng.close()
+        tr.close()
+    _compare_control(got, want)
