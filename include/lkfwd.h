@@ -568,7 +568,8 @@ typedef struct lkf_allocation {
   int64_t bandwidth_requested, bandwidth_delta, bandwidth_needed;
   int32_t target_spatial, target_temporal, request_spatial, max_spatial, max_temporal;
   uint8_t is_deficient;
-  uint8_t reserved[3];
+  uint8_t boosted; /* lkf_allocate_next_higher: a higher layer was allocated */
+  uint8_t reserved[2];
   double distance_to_desired;
 } lkf_allocation;
 /* Forwarder.AllocateOptimal (forwarder.go:591-725) for many DownTracks (one
@@ -580,6 +581,33 @@ typedef struct lkf_allocation {
  * allocator's result, does not carry bandwidth: it leaves
  * lastAllocation.BandwidthRequested as this call last set it.) */
 int lkf_allocate_optimal(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out);
+/* Forwarder.AllocateNextHigher (forwarder.go:1107-1217): for each deficient
+ * DownTrack whose target layer has been reached, the next higher layer with a
+ * bitrate (temporal up, then spatial up, then above the max layer with
+ * allow_overshoot on a simulcast selector) if it fits capacity[i] (the
+ * availableChannelCapacity) or overshoot is allowed; applied as
+ * updateAllocation with boosted = 1.  Otherwise the DownTrack's
+ * lastAllocation with boosted = 0.  The lastAllocation returned and kept is
+ * the last lkf_allocate_* result, with is_deficient as the last allocation or
+ * LKF_CTL_SET_ALLOCATION left it. */
+int lkf_allocate_next_higher(lkf_engine *e, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
+                             lkf_allocation *out);
+/* VideoTransition (forwarder.go:134-138) */
+typedef struct lkf_video_transition {
+  int32_t dt;
+  int32_t from_spatial, from_temporal, to_spatial, to_temporal;
+  uint8_t available; /* GetNextHigherTransition's second result */
+  uint8_t reserved[3];
+  int64_t bandwidth_delta;
+} lkf_video_transition;
+/* Forwarder.GetNextHigherTransition (forwarder.go:1219-1306): the probe
+ * goal's next layer (streamallocator.go:1350) for each DownTrack; changes no
+ * state.  Waits for queued runs. */
+int lkf_next_higher_transition(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_video_transition *out);
+/* Forwarder.Pause (forwarder.go:1308-1351): invalid target, pause reason
+ * muted / pub muted / feed dry / bandwidth (deficient), applied as
+ * updateAllocation. */
+int lkf_pause(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out);
 
 /* ---- SRTP protect ----------------------------------- *
  * The step after the pacer: writeRTPHeaderExtensions sets abs-send-time

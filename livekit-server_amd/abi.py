@@ -111,9 +111,14 @@ assert ALLOC_REQ_DTYPE.itemsize == 112
 ALLOCATION_DTYPE = np.dtype([("dt", "<i4"), ("pause_reason", "<i4"), ("bandwidth_requested", "<i8"),
                              ("bandwidth_delta", "<i8"), ("bandwidth_needed", "<i8"), ("target_spatial", "<i4"),
                              ("target_temporal", "<i4"), ("request_spatial", "<i4"), ("max_spatial", "<i4"),
-                             ("max_temporal", "<i4"), ("is_deficient", "u1"), ("reserved", "u1", 3),
+                             ("max_temporal", "<i4"), ("is_deficient", "u1"), ("boosted", "u1"),
+                             ("reserved", "u1", 2),
                              ("distance_to_desired", "<f8")])
 assert ALLOCATION_DTYPE.itemsize == 64
+VIDEO_TRANSITION_DTYPE = np.dtype([("dt", "<i4"), ("from_spatial", "<i4"), ("from_temporal", "<i4"),
+                                   ("to_spatial", "<i4"), ("to_temporal", "<i4"), ("available", "u1"),
+                                   ("reserved", "u1", 3), ("bandwidth_delta", "<i8")])
+assert VIDEO_TRANSITION_DTYPE.itemsize == 32
 TRACKER_STATUS_DTYPE = np.dtype([("tracker", "<i4"), ("status", "u1"), ("bitrate_changed", "u1"), ("reserved", "u1", 2),
                                  ("notifications", "<u4"), ("reserved2", "<u4"), ("bitrate", "<i8", 4),
                                  ("cumulative", "<i8", 4)])
@@ -401,6 +406,12 @@ def bind_engine_api(lib, prefix):
     if hasattr(lib, prefix + "allocate_optimal"):
         api["allocate_optimal"] = _bind(lib, prefix + "allocate_optimal", C.c_int,
                                         [e, C.c_void_p, C.c_uint32, C.c_void_p])
+    if hasattr(lib, prefix + "pause"):
+        api["allocate_next_higher"] = _bind(lib, prefix + "allocate_next_higher", C.c_int,
+                                            [e, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p])
+        api["next_higher_transition"] = _bind(lib, prefix + "next_higher_transition", C.c_int,
+                                              [e, C.c_void_p, C.c_uint32, C.c_void_p])
+        api["pause"] = _bind(lib, prefix + "pause", C.c_int, [e, C.c_void_p, C.c_uint32, C.c_void_p])
     api["blank_frames"] = _bind(lib, prefix + "blank_frames", C.c_int,
                                 [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                  P(C.c_uint32), P(C.c_uint64)])

@@ -225,8 +225,9 @@ struct lkf_engine {
     uint64_t inCap = 0, outCap = 0, inArenaCap = 0, outArenaCap = 0, gCap = 0, cntCap = 0, mapCap = 0, offCap = 0;
   } red;
   // lastAllocation.BandwidthRequested per DownTrack (lkf_allocate_optimal)
-  int64_t *dAllocBw = nullptr;
+  lkf_allocation *dLastAlloc = nullptr;  // lastAllocation per DownTrack
   lkf_alloc_req *dAllocReq = nullptr;
+  int64_t *dAllocCapacity = nullptr;
   lkf_allocation *dAllocOut = nullptr;
   uint32_t allocCap = 0;
   // the sequencers' padding RangeMaps (SeqRM regions) and padding scratch
@@ -544,7 +545,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   e->srmCap = seqrm_cap(c.seq_size);
   e->srmStride = seqrm_stride(e->srmCap);
   A(dalloc(&e->dSrm, size_t(c.max_downtracks) * e->srmStride));
-  A(dalloc(&e->dAllocBw, c.max_downtracks));
+  A(dalloc(&e->dLastAlloc, c.max_downtracks));
   A(dalloc(&e->dCum, kStatsWords));
   A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
@@ -601,7 +602,13 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dILanePerm, e->maxStreams));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
-    A(hipMemset(e->dAllocBw, 0, size_t(c.max_downtracks) * sizeof(int64_t)));
+    {  // VideoAllocationDefault (forwarder.go:111-116)
+      lkf_allocation d = {};
+      d.pause_reason = 3;
+      d.target_spatial = d.target_temporal = d.request_spatial = d.max_spatial = d.max_temporal = -1;
+      std::vector<lkf_allocation> v(c.max_downtracks, d);
+      A(hipMemcpy(e->dLastAlloc, v.data(), v.size() * sizeof(lkf_allocation), hipMemcpyHostToDevice));
+    }
     A(hipMemset(e->dCum, 0, kStatsWords * sizeof(uint64_t)));
     A(hipMemset(e->dSticky, 0, 4 * sizeof(uint32_t)));
     for (auto &x : e->ctx) {
@@ -650,7 +657,7 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->dRtxOff), static_cast<void *>(e->dRtxIn), static_cast<void *>(e->dRtxOut),
                   static_cast<void *>(e->dSrm), static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff),
                   static_cast<void *>(e->dPadCnt), static_cast<void *>(e->dPadOut), static_cast<void *>(e->dPadArena),
-                  static_cast<void *>(e->dAllocBw), static_cast<void *>(e->dAllocReq),
+                  static_cast<void *>(e->dLastAlloc), static_cast<void *>(e->dAllocReq), static_cast<void *>(e->dAllocCapacity),
                   static_cast<void *>(e->dRedEnc), static_cast<void *>(e->dRedDec), static_cast<void *>(e->dTrk),
                   static_cast<void *>(e->dTrkIds), static_cast<void *>(e->dTrkOut),
                   static_cast<void *>(e->red.in), static_cast<void *>(e->red.out), static_cast<void *>(e->red.inArena),
@@ -2063,9 +2070,12 @@ int lkf_red_decode(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t
                     out_arena_len);
 }
 
-// ---- Forwarder.AllocateOptimal (forwarder.go:591-725) ----------------------
-int lkf_allocate_optimal(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
-  if (!e || (n && (!reqs || !out))) return LKF_EINVAL;
+// ---- Forwarder allocation: AllocateOptimal (forwarder.go:591-725),
+// AllocateNextHigher (:1107-1217), GetNextHigherTransition (:1219-1306),
+// Pause (:1308-1351) ------------------------------------------------------
+static int alloc_common(lkf_engine *e, int mode, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
+                        void *out, size_t outSize) {
+  if (!e || (n && (!reqs || !out || (mode == ALLOC_NEXT_HIGHER && !capacity)))) return LKF_EINVAL;
   if (!n) return LKF_OK;
   std::vector<uint8_t> seen(e->dtp.size(), 0);
   for (uint32_t i = 0; i < n; i++) {
@@ -2080,18 +2090,37 @@ int lkf_allocate_optimal(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, l
   if (n > e->allocCap) {
     if (e->dAllocReq) (void)hipFree(e->dAllocReq);
     if (e->dAllocOut) (void)hipFree(e->dAllocOut);
+    if (e->dAllocCapacity) (void)hipFree(e->dAllocCapacity);
     e->allocCap = std::max<uint32_t>(n, 1024);
     HIPCHK(dalloc(&e->dAllocReq, e->allocCap), "alloc alloc reqs");
     HIPCHK(dalloc(&e->dAllocOut, e->allocCap), "alloc alloc out");
+    HIPCHK(dalloc(&e->dAllocCapacity, e->allocCap), "alloc alloc capacity");
   }
+  static_assert(sizeof(lkf_video_transition) <= sizeof(lkf_allocation), "transition fits the out buffer");
   HIPCHK(hipMemcpy(e->dAllocReq, reqs, n * sizeof(lkf_alloc_req), hipMemcpyHostToDevice), "alloc req copy");
+  if (mode == ALLOC_NEXT_HIGHER)
+    HIPCHK(hipMemcpy(e->dAllocCapacity, capacity, n * sizeof(int64_t), hipMemcpyHostToDevice), "capacity copy");
   rc = upload_done(e);
   if (rc) return rc;
-  HIPCHK(launch_allocate_optimal(e->own, e->dAllocReq, n, e->dHot, e->dDTs, e->dTracks, e->dAllocBw, e->dAllocOut),
-         "allocate optimal");
+  HIPCHK(launch_allocate(e->own, mode, e->dAllocReq, e->dAllocCapacity, n, e->dHot, e->dDTs, e->dTracks,
+                         e->dLastAlloc, e->dAllocOut),
+         "allocate");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
-  HIPCHK(hipMemcpy(out, e->dAllocOut, n * sizeof(lkf_allocation), hipMemcpyDeviceToHost), "alloc out copy");
+  HIPCHK(hipMemcpy(out, e->dAllocOut, n * outSize, hipMemcpyDeviceToHost), "alloc out copy");
   return LKF_OK;
+}
+int lkf_allocate_optimal(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
+  return alloc_common(e, ALLOC_OPTIMAL, reqs, nullptr, n, out, sizeof(lkf_allocation));
+}
+int lkf_allocate_next_higher(lkf_engine *e, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
+                             lkf_allocation *out) {
+  return alloc_common(e, ALLOC_NEXT_HIGHER, reqs, capacity, n, out, sizeof(lkf_allocation));
+}
+int lkf_next_higher_transition(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_video_transition *out) {
+  return alloc_common(e, ALLOC_TRANSITION, reqs, nullptr, n, out, sizeof(lkf_video_transition));
+}
+int lkf_pause(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
+  return alloc_common(e, ALLOC_PAUSE, reqs, nullptr, n, out, sizeof(lkf_allocation));
 }
 
 int lkf_padding(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,

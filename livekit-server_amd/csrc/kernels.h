@@ -196,8 +196,12 @@ struct PadLaunch {
   uint32_t *bytes;  // per request: WritePaddingRTP's return value (blank: bytes counted by sendingPacket)
 };
 hipError_t launch_pad(hipStream_t s, const PadLaunch &a);
-hipError_t launch_allocate_optimal(hipStream_t s, const lkf_alloc_req *reqs, uint32_t n, DTHot *hot, const DevDT *dts,
-                                   const DevTrack *tracks, int64_t *lastBw, lkf_allocation *out);
+// allocation control kernels (alloc_kernels.hip); `last` is the stored
+// lastAllocation per DownTrack; `out` is lkf_allocation[n] or, for
+// ALLOC_TRANSITION, lkf_video_transition[n]; `capacity` only for NEXT_HIGHER
+enum AllocMode { ALLOC_OPTIMAL = 0, ALLOC_NEXT_HIGHER = 1, ALLOC_TRANSITION = 2, ALLOC_PAUSE = 3 };
+hipError_t launch_allocate(hipStream_t s, int mode, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
+                           DTHot *hot, const DevDT *dts, const DevTrack *tracks, lkf_allocation *last, void *out);
 
 // ---- RED for Opus (red_kernels.hip) ----
 struct RedEncState {  // RedReceiver.pktBuff (redreceiver.go:45): the last two primaries of a track

@@ -1626,7 +1626,7 @@ struct Forwarder {
   bool IsOvershootOkay() const { return vls.kind == VLSSimulcast; }
   // AllocateOptimal forwarder.go:591-725 (+ updateAllocation :1353-1373)
   VideoAllocation AllocateOptimal(const std::vector<i32> &availableLayers, const Bitrates &brs, bool allowOvershoot) {
-    if (kind == KindAudio) return lastAllocation;
+    if (kind == KindAudio) return LastAllocation();
     const VideoLayer maxLayer = vls.GetMax(), maxSeenLayer = vls.GetMaxSeen(), currentLayer = vls.GetCurrent();
     const i32 requestSpatial = vls.requestSpatial;
     VideoAllocation alloc;
@@ -1679,7 +1679,10 @@ struct Forwarder {
         alloc.BandwidthRequested - getBandwidthNeeded(brs, vls.GetTarget(), lastAllocation.BandwidthRequested);
     alloc.DistanceToDesired = getDistanceToDesired(muted, pubMuted, vls.GetMaxSeen(), availableLayers, brs,
                                                    alloc.TargetLayer, vls.GetMax());
-    // updateAllocation
+    return updateAllocation(alloc);
+  }
+  // updateAllocation forwarder.go:1353-1373 (+ setTargetLayer :1375-1382)
+  VideoAllocation updateAllocation(VideoAllocation alloc) {
     if (alloc.TargetLayer.IsValid() && mime == MimeH264) alloc.TargetLayer.Temporal = 0;
     lastAllocation = alloc;
     lastAllocIsDeficient = alloc.IsDeficient;
@@ -1687,6 +1690,120 @@ struct Forwarder {
     vls.SetRequestSpatial(alloc.TargetLayer.IsValid() ? alloc.RequestLayerSpatial : InvalidLayerSpatial);
     if (!vls.GetTarget().IsValid()) resyncLocked();
     return lastAllocation;
+  }
+  // f.lastAllocation as the reference returns it: the last allocation call's
+  // result with IsDeficient as SetAllocation (LKF_CTL_SET_ALLOCATION) last set it
+  VideoAllocation LastAllocation() const {
+    VideoAllocation a = lastAllocation;
+    a.IsDeficient = lastAllocIsDeficient;
+    return a;
+  }
+  // AllocateNextHigher forwarder.go:1107-1217; returns (allocation, boosted)
+  std::pair<VideoAllocation, bool> AllocateNextHigher(i64 availableChannelCapacity,
+                                                      const std::vector<i32> &availableLayers, const Bitrates &brs,
+                                                      bool allowOvershoot) {
+    if (kind == KindAudio || !lastAllocIsDeficient) return {LastAllocation(), false};
+    const VideoLayer targetLayer = vls.GetTarget();
+    if (targetLayer.IsValid() && !(targetLayer == vls.GetCurrent())) return {LastAllocation(), false};
+    const VideoLayer maxLayer = vls.GetMax(), maxSeenLayer = vls.GetMaxSeen();
+    const i64 optimal = getOptimalBandwidthNeeded(muted, pubMuted, maxSeenLayer.Spatial, brs, maxLayer);
+    const i64 already = targetLayer.IsValid() ? brs[targetLayer.Spatial][targetLayer.Temporal] : 0;
+    const bool overshoot = allowOvershoot && IsOvershootOkay();
+    // doAllocation: 0 = not done, 1 = done (no fit), 2 = done (boosted)
+    VideoAllocation result;
+    auto doAllocation = [&](i32 minS, i32 maxS, i32 minT, i32 maxT) -> int {
+      for (i32 s = minS; s <= maxS; s++)
+        for (i32 t = minT; t <= maxT; t++) {
+          const i64 bwr = brs[s][t];
+          if (bwr == 0) continue;
+          if (!overshoot && bwr - already > availableChannelCapacity) {
+            result = LastAllocation();
+            return 1;
+          }
+          const VideoLayer nt{s, t};
+          VideoAllocation a;
+          a.IsDeficient = true;
+          a.BandwidthRequested = bwr;
+          a.BandwidthDelta = bwr - already;
+          a.BandwidthNeeded = optimal;
+          a.Brs = brs;
+          a.TargetLayer = nt;
+          a.RequestLayerSpatial = nt.Spatial;
+          a.MaxLayer = maxLayer;
+          a.DistanceToDesired = getDistanceToDesired(muted, pubMuted, maxSeenLayer, availableLayers, brs, nt, maxLayer);
+          if (nt.GreaterThan(maxLayer) || bwr >= optimal) a.IsDeficient = false;
+          result = updateAllocation(a);
+          return 2;
+        }
+      return 0;
+    };
+    int done = 0;
+    if (targetLayer.IsValid())
+      done = doAllocation(targetLayer.Spatial, targetLayer.Spatial, targetLayer.Temporal + 1, maxLayer.Temporal);
+    if (!done) done = doAllocation(targetLayer.Spatial + 1, maxLayer.Spatial, 0, maxLayer.Temporal);
+    if (!done && overshoot && maxLayer.IsValid())
+      done = doAllocation(maxLayer.Spatial + 1, DefaultMaxLayerSpatial, 0, DefaultMaxLayerTemporal);
+    if (!done) return {LastAllocation(), false};
+    return {result, done == 2};
+  }
+  // GetNextHigherTransition forwarder.go:1219-1306 (read-only)
+  struct VideoTransition {
+    VideoLayer From{0, 0}, To{0, 0};
+    i64 BandwidthDelta = 0;
+  };
+  std::pair<VideoTransition, bool> GetNextHigherTransition(const Bitrates &brs, bool allowOvershoot) const {
+    if (kind == KindAudio || !lastAllocIsDeficient) return {VideoTransition{}, false};
+    const VideoLayer targetLayer = vls.GetTarget();
+    if (targetLayer.IsValid() && !(targetLayer == vls.GetCurrent())) return {VideoTransition{}, false};
+    const i64 already = targetLayer.IsValid() ? brs[targetLayer.Spatial][targetLayer.Temporal] : 0;
+    VideoTransition tr;
+    auto findNextHigher = [&](i32 minS, i32 maxS, i32 minT, i32 maxT) -> bool {
+      for (i32 s = minS; s <= maxS; s++)
+        for (i32 t = minT; t <= maxT; t++) {
+          const i64 bwr = brs[s][t];
+          if (bwr == 0 || bwr < already) continue;
+          tr.From = targetLayer;
+          tr.To = VideoLayer{s, t};
+          tr.BandwidthDelta = bwr - already;
+          return true;
+        }
+      return false;
+    };
+    const VideoLayer maxLayer = vls.GetMax();
+    if (targetLayer.IsValid() && findNextHigher(targetLayer.Spatial, targetLayer.Spatial, targetLayer.Temporal + 1,
+                                                maxLayer.Temporal))
+      return {tr, true};
+    if (findNextHigher(targetLayer.Spatial + 1, maxLayer.Spatial, 0, maxLayer.Temporal)) return {tr, true};
+    if (allowOvershoot && IsOvershootOkay() && maxLayer.IsValid() &&
+        findNextHigher(maxLayer.Spatial + 1, DefaultMaxLayerSpatial, 0, DefaultMaxLayerTemporal))
+      return {tr, true};
+    return {VideoTransition{}, false};
+  }
+  // Pause forwarder.go:1308-1351
+  VideoAllocation Pause(const std::vector<i32> &availableLayers, const Bitrates &brs) {
+    const VideoLayer maxLayer = vls.GetMax(), maxSeenLayer = vls.GetMaxSeen();
+    const i64 optimal = getOptimalBandwidthNeeded(muted, pubMuted, maxSeenLayer.Spatial, brs, maxLayer);
+    VideoAllocation a;
+    a.BandwidthRequested = 0;
+    a.BandwidthDelta = 0 - getBandwidthNeeded(brs, vls.GetTarget(), lastAllocation.BandwidthRequested);
+    a.Brs = brs;
+    a.BandwidthNeeded = optimal;
+    a.TargetLayer = InvalidLayer();
+    a.RequestLayerSpatial = InvalidLayerSpatial;
+    a.MaxLayer = maxLayer;
+    a.DistanceToDesired =
+        getDistanceToDesired(muted, pubMuted, maxSeenLayer, availableLayers, brs, InvalidLayer(), maxLayer);
+    if (muted)
+      a.PauseReason = PauseMuted;
+    else if (pubMuted)
+      a.PauseReason = PausePubMuted;
+    else if (optimal == 0)
+      a.PauseReason = PauseFeedDry;
+    else {
+      a.IsDeficient = true;
+      a.PauseReason = PauseBandwidth;
+    }
+    return updateAllocation(a);
   }
   // Resync / resyncLocked forwarder.go:1384-1397
   void Resync() { resyncLocked(); }

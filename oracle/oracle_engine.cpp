@@ -964,9 +964,27 @@ int orc_red_decode(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t
                    out_arena_len);
 }
 
-// Forwarder.AllocateOptimal for each request (lkf_allocate_optimal)
-int orc_allocate_optimal(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
-  if (n && (!reqs || !out)) return LKF_EINVAL;
+// Forwarder allocation calls for each request (lkf_allocate_optimal /
+// _next_higher / lkf_next_higher_transition / lkf_pause)
+static void toAllocation(const VideoAllocation &a, int32_t dt, bool boosted, lkf_allocation &o) {
+  std::memset(&o, 0, sizeof(o));
+  o.dt = dt;
+  o.pause_reason = a.PauseReason;
+  o.bandwidth_requested = a.BandwidthRequested;
+  o.bandwidth_delta = a.BandwidthDelta;
+  o.bandwidth_needed = a.BandwidthNeeded;
+  o.target_spatial = a.TargetLayer.Spatial;
+  o.target_temporal = a.TargetLayer.Temporal;
+  o.request_spatial = a.RequestLayerSpatial;
+  o.max_spatial = a.MaxLayer.Spatial;
+  o.max_temporal = a.MaxLayer.Temporal;
+  o.is_deficient = a.IsDeficient;
+  o.boosted = boosted;
+  o.distance_to_desired = a.DistanceToDesired;
+}
+static int allocCommon(orc_engine *e, int mode, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
+                       void *out) {
+  if (n && (!reqs || !out || (mode == 1 && !capacity))) return LKF_EINVAL;
   std::vector<u8> seen(e->dts.size(), 0);
   for (uint32_t i = 0; i < n; i++) {
     if (reqs[i].dt < 0 || reqs[i].dt >= (int)e->dts.size() || seen[reqs[i].dt]) return LKF_EINVAL;
@@ -980,23 +998,48 @@ int orc_allocate_optimal(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n, l
     Bitrates brs;
     for (int s = 0; s < 3; s++)
       for (int t = 0; t < 4; t++) brs[s][t] = q.bitrates[s][t];
-    const VideoAllocation a = e->dts[q.dt]->f->AllocateOptimal(avail, brs, q.allow_overshoot != 0);
-    lkf_allocation &o = out[i];
-    std::memset(&o, 0, sizeof(o));
-    o.dt = q.dt;
-    o.pause_reason = a.PauseReason;
-    o.bandwidth_requested = a.BandwidthRequested;
-    o.bandwidth_delta = a.BandwidthDelta;
-    o.bandwidth_needed = a.BandwidthNeeded;
-    o.target_spatial = a.TargetLayer.Spatial;
-    o.target_temporal = a.TargetLayer.Temporal;
-    o.request_spatial = a.RequestLayerSpatial;
-    o.max_spatial = a.MaxLayer.Spatial;
-    o.max_temporal = a.MaxLayer.Temporal;
-    o.is_deficient = a.IsDeficient;
-    o.distance_to_desired = a.DistanceToDesired;
+    Forwarder &f = *e->dts[q.dt]->f;
+    const bool over = q.allow_overshoot != 0;
+    switch (mode) {
+      case 0:
+        toAllocation(f.AllocateOptimal(avail, brs, over), q.dt, false, static_cast<lkf_allocation *>(out)[i]);
+        break;
+      case 1: {
+        const auto r = f.AllocateNextHigher(capacity[i], avail, brs, over);
+        toAllocation(r.first, q.dt, r.second, static_cast<lkf_allocation *>(out)[i]);
+        break;
+      }
+      case 2: {
+        const auto r = f.GetNextHigherTransition(brs, over);
+        lkf_video_transition &o = static_cast<lkf_video_transition *>(out)[i];
+        std::memset(&o, 0, sizeof(o));
+        o.dt = q.dt;
+        o.from_spatial = r.first.From.Spatial;
+        o.from_temporal = r.first.From.Temporal;
+        o.to_spatial = r.first.To.Spatial;
+        o.to_temporal = r.first.To.Temporal;
+        o.bandwidth_delta = r.first.BandwidthDelta;
+        o.available = r.second;
+        break;
+      }
+      default:
+        toAllocation(f.Pause(avail, brs), q.dt, false, static_cast<lkf_allocation *>(out)[i]);
+    }
   }
   return LKF_OK;
+}
+int orc_allocate_optimal(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
+  return allocCommon(e, 0, reqs, nullptr, n, out);
+}
+int orc_allocate_next_higher(orc_engine *e, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
+                             lkf_allocation *out) {
+  return allocCommon(e, 1, reqs, capacity, n, out);
+}
+int orc_next_higher_transition(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_video_transition *out) {
+  return allocCommon(e, 2, reqs, nullptr, n, out);
+}
+int orc_pause(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
+  return allocCommon(e, 3, reqs, nullptr, n, out);
 }
 
 int orc_padding(orc_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,

@@ -9,7 +9,7 @@ the previous allocation (getBandwidthNeeded forwarder.go:1880-1886)."""
 import numpy as np
 
 from tests.oracle_lib import load as load_oracle
-from tests.test_alloc_gpu import allocate, make_alloc_reqs
+from tests.test_alloc_gpu import allocate, make_alloc_reqs, run_step, stream_allocator_steps
 
 
 def test_orc_allocate_optimal_invariants(pkg, workload):
@@ -38,6 +38,47 @@ def test_orc_allocate_optimal_invariants(pkg, workload):
             if x["target_spatial"] >= 0 and q["bitrates"][x["target_spatial"], x["target_temporal"]] > 0:
                 prev = q["bitrates"][x["target_spatial"], x["target_temporal"]]
             assert y["bandwidth_delta"] == y["bandwidth_requested"] - prev
+    finally:
+        o.destroy(oh)
+        tr.close()
+
+
+def test_orc_pause_next_higher_invariants(pkg, workload):
+    """Pause / GetNextHigherTransition / AllocateNextHigher through the oracle's
+    C entry points on a forwarded trace (the sequence the GPU parity test
+    replays): Pause leaves no target and marks only the bandwidth reason
+    deficient; a boost is a deficient DownTrack's move to a layer with a
+    bitrate, its BandwidthDelta against the previous target's bitrate; a
+    transition, when available, never goes down in bitrate."""
+    o = load_oracle()
+    abi = pkg.abi
+    tr = workload.Trace(2, duration_s=5.0, batch_s=1.0, rooms=2, seed=6)
+    oh = o.create(500)
+    try:
+        workload.load_topology(o.api, oh, tr)
+        boosted = avail = 0
+        for b in range(tr.nbatches):
+            for step in stream_allocator_steps(abi, tr.ndts, b):
+                r = run_step(o.api, oh, abi, step)
+                kind, reqs, caps = step
+                if kind == "pause":
+                    assert (r["target_spatial"] == -1).all() and (r["request_spatial"] == -1).all()
+                    assert (r["bandwidth_requested"] == 0).all()
+                    assert ((r["pause_reason"] == 4) == (r["is_deficient"] == 1)).all()
+                elif kind == "transition":
+                    a = r[r["available"] == 1]
+                    assert (a["bandwidth_delta"] >= 0).all()
+                    avail += len(a)
+                elif kind == "next_higher":
+                    x = r[r["boosted"] == 1]
+                    boosted += len(x)
+                    q = reqs[r["boosted"] == 1]
+                    got = q["bitrates"][np.arange(len(x)), x["target_spatial"], x["target_temporal"]]
+                    assert (got == x["bandwidth_requested"]).all() and (got > 0).all()
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(oh, pk, n, ar, alen)
+        assert boosted > 0 and avail > 0
     finally:
         o.destroy(oh)
         tr.close()

@@ -1,4 +1,6 @@
-"""Forwarder.AllocateOptimal (forwarder.go:591-725), engine vs oracle.
+"""Forwarder.AllocateOptimal (forwarder.go:591-725), AllocateNextHigher
+(:1107-1217), GetNextHigherTransition (:1219-1306) and Pause (:1308-1351),
+engine vs oracle.
 
 The oracle's restatement is pinned by TestForwarderAllocateOptimal
 (oracle/kat_sfu.inc).  Here every DownTrack of a trace gets an allocation with
@@ -34,6 +36,57 @@ def allocate(api, h, reqs, abi):
     out = np.zeros(len(reqs), dtype=abi.ALLOCATION_DTYPE)
     assert api["allocate_optimal"](h, reqs.ctypes.data, len(reqs), out.ctypes.data) == 0
     return out
+
+
+def pause(api, h, reqs, abi):
+    out = np.zeros(len(reqs), dtype=abi.ALLOCATION_DTYPE)
+    assert api["pause"](h, reqs.ctypes.data, len(reqs), out.ctypes.data) == 0
+    return out
+
+
+def next_higher(api, h, reqs, caps, abi):
+    out = np.zeros(len(reqs), dtype=abi.ALLOCATION_DTYPE)
+    caps = np.ascontiguousarray(caps, dtype=np.int64)
+    assert api["allocate_next_higher"](h, reqs.ctypes.data, caps.ctypes.data, len(reqs), out.ctypes.data) == 0
+    return out
+
+
+def transition(api, h, reqs, abi):
+    out = np.zeros(len(reqs), dtype=abi.VIDEO_TRANSITION_DTYPE)
+    assert api["next_higher_transition"](h, reqs.ctypes.data, len(reqs), out.ctypes.data) == 0
+    return out
+
+
+def stream_allocator_steps(abi, ndts, b):
+    """The allocation calls the stream allocator makes between batch b-1 and b
+    (streamallocator.go: allocateAllTracks -> AllocateOptimal / Pause, then
+    probing -> GetNextHigherTransition / AllocateNextHigher): a list of
+    (call, reqs, capacities)."""
+    rng = np.random.default_rng(1000 + b)
+    steps = []
+    if b == 1:
+        steps.append(("optimal", make_alloc_reqs(abi, ndts, seed=70), None))
+        r = make_alloc_reqs(abi, ndts, seed=71)
+        steps.append(("pause", r[rng.random(ndts) < 0.6], None))
+    elif b >= 2:
+        r = make_alloc_reqs(abi, ndts, seed=80 + b)
+        r["bitrates"] = np.sort(r["bitrates"].reshape(ndts, -1), axis=1).reshape(ndts, 3, 4)  # layered: rising
+        steps.append(("transition", r, None))
+        caps = rng.choice(np.array([0, 50_000, 500_000, 5_000_000, 1 << 40]), ndts)
+        steps.append(("next_higher", r, caps))
+        steps.append(("transition", r, None))
+    return steps
+
+
+def run_step(api, h, abi, step):
+    kind, reqs, caps = step
+    if kind == "optimal":
+        return allocate(api, h, reqs, abi)
+    if kind == "pause":
+        return pause(api, h, reqs, abi)
+    if kind == "transition":
+        return transition(api, h, reqs, abi)
+    return next_higher(api, h, reqs, caps, abi)
 
 
 @pytest.mark.parametrize("cfg", [dict(config=2, rooms=3, seed=5), dict(config=5, rooms=6, svc_dd=1),
@@ -74,6 +127,62 @@ def test_allocate_optimal_matches_oracle(pkg, workload, cfg):
                 assert np.array_equal(grec[f], orec[f]), (b, f)
             assert np.array_equal(gar, oar), b
         assert moved > 0
+        for dt in range(tr.ndts):
+            gs, os_ = abi.lkf_fwd_state(), abi.lkf_fwd_state()
+            eng.api["get_state"](eng.h, dt, C.byref(gs))
+            o.api["get_state"](oh, dt, C.byref(os_))
+            assert gs.as_tuple() == os_.as_tuple(), dt
+        gsum, osum = pkg.downtrack_summaries(eng.api, eng.h), pkg.downtrack_summaries(o.api, oh)
+        for f in abi.DT_SUMMARY_DTYPE.names:
+            assert np.array_equal(gsum[f], osum[f]), f
+    finally:
+        eng.close()
+        o.destroy(oh)
+        tr.close()
+
+
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=3, seed=6), dict(config=5, rooms=6, svc_dd=1),
+                                 dict(config=2, rooms=2, h264=1, seed=4)])
+def test_pause_and_next_higher_match_oracle(pkg, workload, cfg):
+    """Pause, then per batch GetNextHigherTransition / AllocateNextHigher with
+    random channel capacities (zero to unlimited): the results (boosted flag
+    included), the batches forwarded after them and the Forwarder state."""
+    o = load_oracle()
+    abi = pkg.abi
+    kw = dict(cfg)
+    tr = workload.Trace(kw.pop("config"), duration_s=6.0, batch_s=1.0, **kw)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+        boosted = avail = 0
+        for b in range(tr.nbatches):
+            for step in stream_allocator_steps(abi, tr.ndts, b):
+                g = run_step(eng.api, eng.h, abi, step)
+                r = run_step(o.api, oh, abi, step)
+                for f in g.dtype.names:
+                    if f != "reserved":
+                        assert np.array_equal(g[f], r[f]), (b, step[0], f)
+                if step[0] == "next_higher":
+                    boosted += int(r["boosted"].sum())
+                if step[0] == "transition":
+                    avail += int(r["available"].sum())
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            dd = tr.batch_dd(b)[0] if tr.has_dd() else None
+            eng.submit(pk, n, ar, alen, dd)
+            eng.run()
+            eng.sync()
+            o.run(oh, pk, n, ar, alen, dd)
+            grec, gar = eng.drain()
+            orec, oar = pkg.drain_arrays(o.api, oh)
+            assert len(grec) == len(orec), b
+            for f in abi.OUT_DTYPE.names:
+                assert np.array_equal(grec[f], orec[f]), (b, f)
+            assert np.array_equal(gar, oar), b
+        assert boosted > 0 and avail > 0
         for dt in range(tr.ndts):
             gs, os_ = abi.lkf_fwd_state(), abi.lkf_fwd_state()
             eng.api["get_state"](eng.h, dt, C.byref(gs))
