@@ -279,6 +279,7 @@ struct lkf_engine {
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
   uint32_t *dIList = nullptr, *dIListCnt = nullptr;  // per-stream datagram lists (k_ing_lists)
   uint32_t *dILanePerm = nullptr;                     // k_ing_stream lane -> stream, by (kind, layer)
+  bool ingLane = false;                               // LKF_ING_LANE=1: lane-per-stream ingress (A/B)
   uint32_t lastIngestN = 0;
   // speaker ranking tables (rebuilt when topology changes)
   uint32_t nRooms = 0;
@@ -636,6 +637,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   if (const char *v = getenv("LKF_DECIDE_K")) e->decideK = uint32_t(std::min(64, std::max(0, atoi(v))));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
+  if (const char *v = getenv("LKF_ING_LANE")) e->ingLane = atoi(v) != 0;
   return e;
 }
 
@@ -2234,6 +2236,7 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.listCnt = e->dIListCnt;
   a.listStride = e->cfg.max_batch_pkts;
   a.lanePerm = e->dILanePerm;
+  a.laneStreams = e->ingLane;
   const bool dd = e->nDDStreams != 0;
   a.ddStates = dd ? e->dDDIng : nullptr;
   a.ddStructs = dd ? e->dDDIngStruct : nullptr;

@@ -502,22 +502,27 @@ __device__ __forceinline__ WAResult wa32_update(StreamHot &h, u32 val) {
 // RTPStatsReceiver history (cHistorySize 4096 bits, rtpstats_receiver.go:30),
 // staged in LDS for the ingest: word w of a lane's history at h[w * kHL]
 // (word-major, lane-minor)
+// (HS: the word stride — kHL for the lane-per-stream kernel, 1 for the
+// wave-per-stream kernel's single history)
 constexpr int kHL = 64;
+template <int HS = kHL>
 __device__ __forceinline__ bool hist_isset(const u64 *h, u64 v) {
-  return (h[((v >> 6) & (kHistWords - 1)) * kHL] >> (v & 63)) & 1;
+  return (h[((v >> 6) & (kHistWords - 1)) * HS] >> (v & 63)) & 1;
 }
-__device__ __forceinline__ void hist_set(u64 *h, u64 v) { h[((v >> 6) & (kHistWords - 1)) * kHL] |= 1ull << (v & 63); }
+template <int HS = kHL>
+__device__ __forceinline__ void hist_set(u64 *h, u64 v) { h[((v >> 6) & (kHistWords - 1)) * HS] |= 1ull << (v & 63); }
+template <int HS = kHL>
 __device__ void hist_clear_range(u64 *h, u64 lo, u64 hi) {  // inclusive; lo > hi: no-op
   if (lo > hi) return;
   if (hi - lo + 1 >= u64(kHistWords) * 64) {
-    for (int w = 0; w < kHistWords; w++) h[w * kHL] = 0;
+    for (int w = 0; w < kHistWords; w++) h[w * HS] = 0;
     return;
   }
   for (u64 v = lo;;) {  // a word at a time
     const u32 b = u32(v & 63);
     const u64 nb = min(u64(64 - b), hi - v + 1);
     const u64 m = (nb == 64 ? ~0ull : ((1ull << nb) - 1)) << b;
-    h[((v >> 6) & (kHistWords - 1)) * kHL] &= ~m;
+    h[((v >> 6) & (kHistWords - 1)) * HS] &= ~m;
     if (hi - v + 1 == nb) break;
     v += nb;
   }
@@ -801,6 +806,138 @@ __device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u
   return true;
 }
 
+// One datagram through Buffer.calc (buffer.go:407-489): processHeaderExtensions,
+// RTPStatsReceiver.Update (rtpstats_receiver.go:76-241), the padding
+// RangeMap, the dependency descriptor; its flow, forward flag and DD record.
+template <int HS>
+__device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream &s,
+                                         const IngParsed &p, const lkf_raw_pkt &rp, u32 ic, lkf_flow *flows,
+                                         u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *ddStates,
+                                         DDStruct *ddStructs, u32 *err) {
+  const i64 arrival = rp.arrival_ns;
+  lkf_flow f = {};
+  f.pkt = 0xffffffffu;
+  u32 forward = 0;
+  IngDD dv = {};
+  do {
+    if (!(p.flags & IP_OK)) {
+      f.flags = LKF_FLOW_BAD;
+      break;
+    }
+    // processHeaderExtensions (buffer.go:573-596)
+    if (s.levelExt) {
+      if (!(h.flags & S_LVL_TS_INIT)) {
+        h.flags |= S_LVL_TS_INIT;
+        h.latestTSForAudioLevel = p.ts;
+      }
+      if (p.flags & IP_LEVEL) {
+        if (u32(p.ts - h.latestTSForAudioLevel) < (1u << 31)) {
+          const i64 dur = (i64(p.ts) - i64(h.latestTSForAudioLevel)) * 1000 / i64(s.clockRate);
+          if (dur > 0) level_observe(h, s, p.level, u32(dur), arrival);
+          h.latestTSForAudioLevel = p.ts;
+        }
+      }
+    }
+    // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241)
+    const int hdrSize = p.hdrSize, payloadSize = p.payloadLen, paddingSize = p.paddingSize;
+    WAResult rsn, rts;
+    if (!(h.flags & S_INIT)) {
+      if (payloadSize == 0) {
+        f.flags = LKF_FLOW_NOT_HANDLED;
+        break;
+      }
+      h.flags |= S_INIT;
+      rsn = wa16_update(h, p.sn);
+      rts = wa32_update(h, p.ts);
+    } else {
+      rsn = wa16_update(h, p.sn);
+      if (rsn.unhandled) {
+        f.flags = LKF_FLOW_NOT_HANDLED;
+        break;
+      }
+      rts = wa32_update(h, p.ts);
+    }
+    const u64 pktSize = u64(hdrSize + payloadSize + paddingSize);
+    const i64 gapSN = i64(rsn.extVal - rsn.preHighest);
+    bool dup = false, ooo = false;
+    if (gapSN <= 0) {
+      if (gapSN != 0) h.packetsOutOfOrder++;
+      const i64 diff = i64(rsn.preHighest - rsn.extVal);
+      if (diff >= 0 && diff < i64(kHistWords) * 64) {  // isInRange :427-430
+        if (hist_isset<HS>(hs, rsn.extVal)) {
+          h.bytesDuplicate += pktSize;
+          h.headerBytesDuplicate += u64(hdrSize);
+          h.packetsDuplicate++;
+          dup = true;
+        } else {
+          h.packetsLost--;
+          hist_set<HS>(hs, rsn.extVal);
+        }
+      }
+      ooo = true;
+    } else {
+      hist_clear_range<HS>(hs, rsn.preHighest + 1, rsn.extVal - 1);
+      h.packetsLost += u64(gapSN - 1);
+      hist_set<HS>(hs, rsn.extVal);
+      if (gapSN > 1) {
+        f.flags |= LKF_FLOW_HAS_LOSS;
+        f.loss_start = rsn.preHighest + 1;
+        f.loss_end = rsn.extVal;
+      }
+    }
+    f.ext_sn = rsn.extVal;
+    f.ext_ts = rts.extVal;
+    if (!dup) {
+      if (payloadSize == 0) {
+        h.packetsPadding++;
+        h.bytesPadding += pktSize;
+        h.headerBytesPadding += u64(hdrSize);
+      } else {
+        h.bytes += pktSize;
+        h.headerBytes += u64(hdrSize);
+        if (p.flags & IP_MARKER) h.frames++;
+      }
+    }
+    if (dup) f.flags |= LKF_FLOW_DUPLICATE;
+    if (ooo) f.flags |= LKF_FLOW_OUT_OF_ORDER;
+    // Buffer.calc (buffer.go:439-489)
+    if (payloadSize == 0 && (!ooo || dup)) {
+      if (!ooo) irm_exclude(h, ring, rsn.extVal, rsn.extVal + 1);
+      f.flags |= LKF_FLOW_PADDING;
+      break;
+    }
+    u64 adj = 0;
+    if (!irm_get(h, ring, rsn.extVal, adj)) {
+      f.flags |= LKF_FLOW_BAD;
+      break;
+    }
+    f.ext_sn = rsn.extVal - adj;
+    if (dup) break;  // the RTX bucket already holds it (ErrRTXPacket)
+    // getExtPacket (buffer.go:599-671): the dependency descriptor first
+    if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
+      bool limit = false;
+      if (!dd_ingest(ddStates[s.ddIdx], ddStructs + size_t(s.ddIdx) * 2, raw + rp.off + p.ddOff, p.ddLen,
+                     u16(f.ext_sn), dv, limit)) {
+        if (limit) atomicOr(err, 4u);
+        f.flags |= LKF_FLOW_BAD;
+        break;
+      }
+      dv.ddOff = p.ddOff;
+      dv.ddLen = p.ddLen;
+    }
+    // VP8 unmarshal failed, or VP9 without a descriptor that failed
+    if ((p.flags & IP_VP8_BAD) && !(s.codec == LKF_CODEC_VP9 && dv.present)) {
+      f.flags |= LKF_FLOW_BAD;
+      break;
+    }
+    forward = 1;
+    f.flags |= LKF_FLOW_FORWARD;
+  } while (false);
+  flows[ic] = f;
+  fwd[ic] = forward;
+  if (ingDD) ingDD[ic] = dv;
+}
+
 // ---------------------------------------------------------------------------
 // k_ing_stream: one lane per stream, serial over the stream's datagrams.
 // ---------------------------------------------------------------------------
@@ -859,131 +996,151 @@ __global__ void __launch_bounds__(64) k_ing_stream(const lkf_raw_pkt *__restrict
     }
     if (j + 3 < nIdx) i3 = idxAt(j + 3);
     if (rp.stream != sid) continue;
-    const i64 arrival = rp.arrival_ns;
-    lkf_flow f = {};
-    f.pkt = 0xffffffffu;
-    u32 forward = 0;
-    IngDD dv = {};
-    do {
-      if (!(p.flags & IP_OK)) {
-        f.flags = LKF_FLOW_BAD;
-        break;
-      }
-      // processHeaderExtensions (buffer.go:573-596)
-      if (s.levelExt) {
-        if (!(h.flags & S_LVL_TS_INIT)) {
-          h.flags |= S_LVL_TS_INIT;
-          h.latestTSForAudioLevel = p.ts;
-        }
-        if (p.flags & IP_LEVEL) {
-          if (u32(p.ts - h.latestTSForAudioLevel) < (1u << 31)) {
-            const i64 dur = (i64(p.ts) - i64(h.latestTSForAudioLevel)) * 1000 / i64(s.clockRate);
-            if (dur > 0) level_observe(h, s, p.level, u32(dur), arrival);
-            h.latestTSForAudioLevel = p.ts;
-          }
-        }
-      }
-      // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241)
-      const int hdrSize = p.hdrSize, payloadSize = p.payloadLen, paddingSize = p.paddingSize;
-      WAResult rsn, rts;
-      if (!(h.flags & S_INIT)) {
-        if (payloadSize == 0) {
-          f.flags = LKF_FLOW_NOT_HANDLED;
-          break;
-        }
-        h.flags |= S_INIT;
-        rsn = wa16_update(h, p.sn);
-        rts = wa32_update(h, p.ts);
-      } else {
-        rsn = wa16_update(h, p.sn);
-        if (rsn.unhandled) {
-          f.flags = LKF_FLOW_NOT_HANDLED;
-          break;
-        }
-        rts = wa32_update(h, p.ts);
-      }
-      const u64 pktSize = u64(hdrSize + payloadSize + paddingSize);
-      const i64 gapSN = i64(rsn.extVal - rsn.preHighest);
-      bool dup = false, ooo = false;
-      if (gapSN <= 0) {
-        if (gapSN != 0) h.packetsOutOfOrder++;
-        const i64 diff = i64(rsn.preHighest - rsn.extVal);
-        if (diff >= 0 && diff < i64(kHistWords) * 64) {  // isInRange :427-430
-          if (hist_isset(hs, rsn.extVal)) {
-            h.bytesDuplicate += pktSize;
-            h.headerBytesDuplicate += u64(hdrSize);
-            h.packetsDuplicate++;
-            dup = true;
-          } else {
-            h.packetsLost--;
-            hist_set(hs, rsn.extVal);
-          }
-        }
-        ooo = true;
-      } else {
-        hist_clear_range(hs, rsn.preHighest + 1, rsn.extVal - 1);
-        h.packetsLost += u64(gapSN - 1);
-        hist_set(hs, rsn.extVal);
-        if (gapSN > 1) {
-          f.flags |= LKF_FLOW_HAS_LOSS;
-          f.loss_start = rsn.preHighest + 1;
-          f.loss_end = rsn.extVal;
-        }
-      }
-      f.ext_sn = rsn.extVal;
-      f.ext_ts = rts.extVal;
-      if (!dup) {
-        if (payloadSize == 0) {
-          h.packetsPadding++;
-          h.bytesPadding += pktSize;
-          h.headerBytesPadding += u64(hdrSize);
-        } else {
-          h.bytes += pktSize;
-          h.headerBytes += u64(hdrSize);
-          if (p.flags & IP_MARKER) h.frames++;
-        }
-      }
-      if (dup) f.flags |= LKF_FLOW_DUPLICATE;
-      if (ooo) f.flags |= LKF_FLOW_OUT_OF_ORDER;
-      // Buffer.calc (buffer.go:439-489)
-      if (payloadSize == 0 && (!ooo || dup)) {
-        if (!ooo) irm_exclude(h, ring, rsn.extVal, rsn.extVal + 1);
-        f.flags |= LKF_FLOW_PADDING;
-        break;
-      }
-      u64 adj = 0;
-      if (!irm_get(h, ring, rsn.extVal, adj)) {
-        f.flags |= LKF_FLOW_BAD;
-        break;
-      }
-      f.ext_sn = rsn.extVal - adj;
-      if (dup) break;  // the RTX bucket already holds it (ErrRTXPacket)
-      // getExtPacket (buffer.go:599-671): the dependency descriptor first
-      if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
-        bool limit = false;
-        if (!dd_ingest(ddStates[s.ddIdx], ddStructs + size_t(s.ddIdx) * 2, raw + rp.off + p.ddOff, p.ddLen,
-                       u16(f.ext_sn), dv, limit)) {
-          if (limit) atomicOr(err, 4u);
-          f.flags |= LKF_FLOW_BAD;
-          break;
-        }
-        dv.ddOff = p.ddOff;
-        dv.ddLen = p.ddLen;
-      }
-      // VP8 unmarshal failed, or VP9 without a descriptor that failed
-      if ((p.flags & IP_VP8_BAD) && !(s.codec == LKF_CODEC_VP9 && dv.present)) {
-        f.flags |= LKF_FLOW_BAD;
-        break;
-      }
-      forward = 1;
-      f.flags |= LKF_FLOW_FORWARD;
-    } while (false);
-    flows[ic] = f;
-    fwd[ic] = forward;
-    if (ingDD) ingDD[ic] = dv;
+    ing_step<kHL>(h, hs, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err);
   }
   hot[sid] = h;
   for (int w = 0; w < kHistWords; w++) hg[w] = hs[w * kHL];
+}
+
+// ---------------------------------------------------------------------------
+// k_ing_stream_wave: one wave per stream, lanes over its datagrams.  The
+// receiver recurrence is serial, but a run of in-order datagrams (SN gap 1 to
+// 2^15, TS gap up to 2^31, a payload, no audio level or DD to observe, the
+// padding RangeMap's open range covering them) only accumulates: the extended
+// SN and TS are prefix sums of the gaps, the counters are sums, the history
+// is one range clear plus one bit per datagram.  A chunk's leading run is
+// taken in one step; the datagram that ends it (reorder, duplicate, padding,
+// DD, first packet, audio) goes through ing_step on lane 0, as the
+// lane-per-stream kernel does for every datagram.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u64 wave_incl_scan_u64(u64 v, u32 lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u64 o = __shfl_up(v, d, 64);
+    if (lane >= u32(d)) v += o;
+  }
+  return v;
+}
+__device__ __forceinline__ u64 wave_sum_u64(u64 v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(64) k_ing_stream_wave(
+    const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q, const DevStream *__restrict__ streams,
+    StreamHot *__restrict__ hot, u64 *__restrict__ hist, RangeEntry *__restrict__ rings,
+    const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows,
+    u32 *__restrict__ fwd, const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
+    IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list, const u32 *__restrict__ cnt, u32 stride) {
+  static_assert(kHistWords == 64, "one history word per lane");
+  static_assert(sizeof(StreamHot) == 64 * sizeof(u32), "one StreamHot dword per lane");
+  __shared__ u64 sHist[kHistWords];
+  __shared__ StreamHot sh;
+  const u32 sid = blockIdx.x, lane = threadIdx.x;
+  const DevStream s = streams[sid];
+  const u32 pb = tBegin[s.track], pe = tEnd[s.track];
+  if (pb >= pe) return;
+  u64 *const hg = hist + size_t(sid) * kHistWords;
+  sHist[lane] = hg[lane];
+  reinterpret_cast<u32 *>(&sh)[lane] = reinterpret_cast<const u32 *>(hot + sid)[lane];
+  __syncthreads();
+  RangeEntry *ring = rings + size_t(sid) * kRangeCap;
+  const bool useList = s.layer < 3;
+  const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
+  const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
+  // datagrams a run may take without looking at them twice (the state part
+  // is checked per chunk)
+  const bool runStream = !s.levelExt;
+  const bool hasDD = s.ddIdx != 0xffffffffu;
+  if (!runStream) {  // audio level observation: every datagram on lane 0
+    if (lane == 0)
+      for (u32 j = 0; j < nIdx; j++) {
+        const u32 ic = useList ? lst[j] : pb + j;
+        const lkf_raw_pkt rp = raws[ic];
+        if (rp.stream != sid) continue;
+        const IngParsed p = q[ic];
+        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err);
+      }
+    __syncthreads();
+  }
+  for (u32 j = 0; runStream && j < nIdx;) {
+    const u32 k = j + lane;
+    const bool in = k < nIdx;
+    u32 ic = 0;
+    IngParsed p = {};
+    lkf_raw_pkt rp = {};
+    if (in) {
+      ic = useList ? lst[k] : pb + k;
+      p = q[ic];
+      rp = raws[ic];
+    }
+    const u32 need = S_INIT | S_SN_INIT | S_TS_INIT;
+    const bool stateOk = runStream && (sh.flags & need) == need && sh.rmOpenStart <= sh.snExtHighest + 1;
+    const u16 prevSn = u16(__shfl_up(u32(p.sn), 1, 64));
+    const u32 prevTs = u32(__shfl_up(p.ts, 1, 64));
+    const u16 gs = u16(p.sn - (lane == 0 ? sh.snHighest : prevSn));
+    const u32 gt = p.ts - (lane == 0 ? sh.tsHighest : prevTs);
+    const bool ok = stateOk && in && rp.stream == sid && (p.flags & IP_OK) && p.payloadLen > 0 &&
+                    !(p.flags & IP_VP8_BAD) && !(hasDD && p.ddLen) && gs >= 1 && gs <= 0x8000u && gt <= 0x80000000u;
+    const u64 snScan = wave_incl_scan_u64(ok ? u64(gs) : 0, lane);  // only read below the run end
+    u64 bad = ~__ballot(ok);
+    // the history update below is exact while the run spans < 4096 SNs
+    bad |= __ballot(snScan >= u64(kHistWords) * 64);
+    const u32 L = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;
+    if (L == 0) {
+      if (lane == 0 && rp.stream == sid)
+        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err);
+      __syncthreads();
+      j++;
+      continue;
+    }
+    const bool run = lane < L;
+    const u64 tsScan = wave_incl_scan_u64(run ? u64(gt) : 0, lane);
+    const u64 ext = sh.snExtHighest + snScan, extTs = sh.tsExtHighest + tsScan;
+    const u64 pktSize = u64(p.hdrSize + p.payloadLen + p.paddingSize);
+    const u64 bytesRun = wave_sum_u64(run ? pktSize : 0), hdrRun = wave_sum_u64(run ? u64(p.hdrSize) : 0);
+    const u32 framesRun = u32(__popcll(__ballot(run && (p.flags & IP_MARKER))));
+    const u64 extLast = __shfl(ext, int(L - 1), 64), extTsLast = __shfl(extTs, int(L - 1), 64);
+    const u16 snLast = u16(__shfl(u32(p.sn), int(L - 1), 64));
+    const u32 tsLast = u32(__shfl(p.ts, int(L - 1), 64));
+    if (run) {
+      lkf_flow f = {};
+      f.pkt = 0xffffffffu;
+      f.ext_sn = ext - sh.rmOpenValue;
+      f.ext_ts = extTs;
+      f.flags = LKF_FLOW_FORWARD;
+      if (gs > 1) {
+        f.flags |= LKF_FLOW_HAS_LOSS;
+        f.loss_start = ext - gs + 1;
+        f.loss_end = ext;
+      }
+      flows[ic] = f;
+      fwd[ic] = 1;
+      if (ingDD) ingDD[ic] = IngDD{};
+    }
+    const u64 pre0 = sh.snExtHighest;
+    __syncthreads();
+    if (lane == 0) {  // the run's gaps cleared, then its SNs set
+      hist_clear_range<1>(sHist, pre0 + 1, extLast);
+      sh.packetsLost += extLast - pre0 - L;
+      sh.bytes += bytesRun;
+      sh.headerBytes += hdrRun;
+      sh.frames += framesRun;
+      sh.snHighest = snLast;
+      sh.snExtHighest = extLast;
+      sh.snCycles = extLast - snLast;
+      sh.tsHighest = tsLast;
+      sh.tsExtHighest = extTsLast;
+      sh.tsCycles = extTsLast - tsLast;
+    }
+    __syncthreads();
+    if (run) atomicOr(reinterpret_cast<unsigned long long *>(&sHist[(ext >> 6) & (kHistWords - 1)]), 1ull << (ext & 63));
+    __syncthreads();
+    j += L;
+  }
+  hg[lane] = sHist[lane];
+  reinterpret_cast<u32 *>(hot + sid)[lane] = reinterpret_cast<const u32 *>(&sh)[lane];
 }
 
 // ---------------------------------------------------------------------------
@@ -1221,9 +1378,14 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
                      a.tRuns, a.err);
   hipLaunchKernelGGL(k_ing_lists, dim3(a.ntracks), dim3(64), 0, st, a.raws, a.streams, a.nstreams, a.tBegin,
                      a.tEnd, a.listStride, a.list, a.listCnt);
-  hipLaunchKernelGGL(k_ing_stream, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a.raws, a.parsed, a.streams,
-                     a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates,
-                     a.ddStructs, a.ingDD, a.err, a.list, a.listCnt, a.listStride, a.lanePerm);
+  if (a.laneStreams)
+    hipLaunchKernelGGL(k_ing_stream, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a.raws, a.parsed, a.streams,
+                       a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates,
+                       a.ddStructs, a.ingDD, a.err, a.list, a.listCnt, a.listStride, a.lanePerm);
+  else if (a.nstreams)
+    hipLaunchKernelGGL(k_ing_stream_wave, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams, a.hot,
+                       a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs, a.ingDD,
+                       a.err, a.list, a.listCnt, a.listStride);
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
   if (r != hipSuccess) return r;

@@ -100,6 +100,7 @@ struct IngestLaunch {
   uint32_t *list, *listCnt;
   uint32_t listStride;
   const uint32_t *lanePerm;  // k_ing_stream lane -> stream (nullptr: identity)
+  bool laneStreams;          // the lane-per-stream k_ing_stream (LKF_ING_LANE=1) instead of k_ing_stream_wave
 };
 
 struct SpeakersLaunch {
