@@ -1027,7 +1027,7 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
   return v;
 }
 
-__global__ void __launch_bounds__(64) k_ing_stream_wave(
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_ing_stream_wave(
     const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q, const DevStream *__restrict__ streams,
     StreamHot *__restrict__ hot, u64 *__restrict__ hist, RangeEntry *__restrict__ rings,
     const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows,
@@ -1053,16 +1053,28 @@ __global__ void __launch_bounds__(64) k_ing_stream_wave(
   // is checked per chunk)
   const bool runStream = !s.levelExt;
   const bool hasDD = s.ddIdx != 0xffffffffu;
-  if (!runStream) {  // audio level observation: every datagram on lane 0
-    if (lane == 0)
-      for (u32 j = 0; j < nIdx; j++) {
-        const u32 ic = useList ? lst[j] : pb + j;
-        const lkf_raw_pkt rp = raws[ic];
-        if (rp.stream != sid) continue;
-        const IngParsed p = q[ic];
-        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err);
+  if (!runStream) {  // audio level observation: every datagram on lane 0,
+    // its descriptors staged in LDS 64 at a time by the whole wave
+    __shared__ IngParsed sP[64];
+    __shared__ lkf_raw_pkt sR[64];
+    __shared__ u32 sI[64];
+    for (u32 base = 0; base < nIdx; base += 64) {
+      const u32 k = base + lane;
+      if (k < nIdx) {
+        const u32 ic = useList ? lst[k] : pb + k;
+        sI[lane] = ic;
+        sP[lane] = q[ic];
+        sR[lane] = raws[ic];
       }
-    __syncthreads();
+      __syncthreads();
+      if (lane == 0) {
+        const u32 m = min(64u, nIdx - base);
+        for (u32 x = 0; x < m; x++)
+          if (sR[x].stream == sid)
+            ing_step<1>(sh, sHist, ring, s, sP[x], sR[x], sI[x], flows, fwd, ingDD, raw, ddStates, ddStructs, err);
+      }
+      __syncthreads();
+    }
   }
   for (u32 j = 0; runStream && j < nIdx;) {
     const u32 k = j + lane;
