@@ -552,6 +552,17 @@ int32_t lkf_add_stream_tracker(lkf_engine *e, int32_t track, int32_t layer, uint
 int lkf_stream_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t arg);
 int lkf_stream_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n, int check, int64_t bitrate_elapsed_ns,
                              lkf_tracker_status *out);
+/* A StreamTrackerFrame (streamtracker_frame.go:39-211) for (track, spatial
+ * layer): its layer's marker packets give the frame rate, estimated at each
+ * CheckStatus over an interval of max(500 ms, 1 / estimated fps, 1 / min_fps)
+ * (StreamTrackerFrameConfig.MinFPS, config.go:413-458: 5 for camera, 0.5 for
+ * screen share); status stopped when no two frames arrived in it.  Its
+ * time.Now() is the virtual clock: the activating packet's arrival, and the
+ * now_ns of lkf_stream_trackers_tick_at (the plain tick passes 0).  Same
+ * _ctl and tick calls as the packet trackers.  >= 0 handle. */
+int32_t lkf_add_stream_tracker_frame(lkf_engine *e, int32_t track, int32_t layer, uint32_t clock_rate, double min_fps);
+int lkf_stream_trackers_tick_at(lkf_engine *e, const int32_t *trackers, uint32_t n, int check,
+                                int64_t bitrate_elapsed_ns, int64_t now_ns, lkf_tracker_status *out);
 
 /* ---- stream allocation ------------------------------ */
 typedef struct lkf_alloc_req {

@@ -398,6 +398,11 @@ def bind_engine_api(lib, prefix):
         api["stream_tracker_ctl"] = _bind(lib, prefix + "stream_tracker_ctl", C.c_int, [e, C.c_int32, C.c_int32, C.c_int32])
         api["stream_trackers_tick"] = _bind(lib, prefix + "stream_trackers_tick", C.c_int,
                                             [e, C.c_void_p, C.c_uint32, C.c_int, C.c_int64, C.c_void_p])
+    if hasattr(lib, prefix + "add_stream_tracker_frame"):
+        api["add_stream_tracker_frame"] = _bind(lib, prefix + "add_stream_tracker_frame", C.c_int32,
+                                                [e, C.c_int32, C.c_int32, C.c_uint32, C.c_double])
+        api["stream_trackers_tick_at"] = _bind(lib, prefix + "stream_trackers_tick_at", C.c_int,
+                                               [e, C.c_void_p, C.c_uint32, C.c_int, C.c_int64, C.c_int64, C.c_void_p])
     if hasattr(lib, prefix + "red_encode"):
         for nm in ("red_encode", "red_decode"):
             api[nm] = _bind(lib, prefix + nm, C.c_int,

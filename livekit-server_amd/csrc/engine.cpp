@@ -1868,6 +1868,24 @@ int32_t lkf_add_stream_tracker(lkf_engine *e, int32_t track, int32_t layer, uint
   return int32_t(e->nTrk++);
 }
 
+// a StreamTrackerFrame (streamtracker_frame.go:39-211) with the source's
+// StreamTrackerFrameConfig.MinFPS (config.go:413-458)
+int32_t lkf_add_stream_tracker_frame(lkf_engine *e, int32_t track, int32_t layer, uint32_t clock_rate,
+                                     double min_fps) {
+  if (!e || track < 0 || track >= int32_t(e->tracks.size()) || layer < 0 || clock_rate == 0) return LKF_EINVAL;
+  const int32_t id = lkf_add_stream_tracker(e, track, layer, 0, 0);
+  if (id < 0) return id;
+  TrackerState t;
+  HIPCHK(hipMemcpy(&t, e->dTrk + id, sizeof(t), hipMemcpyDeviceToHost), "tracker read");
+  t.frame = 1;
+  t.clockRate = clock_rate;
+  t.minFPS = min_fps;
+  tracker_frame_reset_fps(t);
+  HIPCHK(hipMemcpy(e->dTrk + id, &t, sizeof(t), hipMemcpyHostToDevice), "tracker write");
+  const int rc = upload_done(e);
+  return rc ? rc : id;
+}
+
 // Reset / SetPaused / Stop (streamtracker.go:127-185) on the host copy of the state
 int lkf_stream_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t arg) {
   if (!e || tracker < 0 || uint32_t(tracker) >= e->nTrk) return LKF_EINVAL;
@@ -1881,6 +1899,11 @@ int lkf_stream_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t a
     for (int i = 0; i < 4; i++) t.bytes[i] = t.bitrate[i] = 0;
     t.countSinceLast = t.cycleCount = 0;
     t.initialized = 0;
+    if (t.frame) {  // StreamTrackerFrame.Reset
+      tracker_frame_reset_fps(t);
+      t.lastCheckSet = 0;
+      t.lastCheckNs = 0;
+    }
   };
   auto notify = [&]() {
     if (t.status != t.lastNotified) {
@@ -1918,6 +1941,10 @@ int lkf_stream_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t a
 
 int lkf_stream_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n, int check, int64_t bitrate_elapsed_ns,
                              lkf_tracker_status *out) {
+  return lkf_stream_trackers_tick_at(e, trackers, n, check, bitrate_elapsed_ns, 0, out);
+}
+int lkf_stream_trackers_tick_at(lkf_engine *e, const int32_t *trackers, uint32_t n, int check,
+                                int64_t bitrate_elapsed_ns, int64_t now_ns, lkf_tracker_status *out) {
   if (!e || (n && (!trackers || !out))) return LKF_EINVAL;
   if (!n) return LKF_OK;
   std::vector<uint8_t> seen(e->nTrk, 0);
@@ -1932,7 +1959,7 @@ int lkf_stream_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n,
   HIPCHK(hipMemcpy(e->dTrkIds, trackers, n * sizeof(int32_t), hipMemcpyHostToDevice), "tracker ids copy");
   rc = upload_done(e);
   if (rc) return rc;
-  HIPCHK(launch_tracker_tick(e->own, e->dTrk, e->dTrkIds, n, check, bitrate_elapsed_ns, e->dTrkOut), "tracker tick");
+  HIPCHK(launch_tracker_tick(e->own, e->dTrk, e->dTrkIds, n, check, bitrate_elapsed_ns, now_ns, e->dTrkOut), "tracker tick");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
   HIPCHK(hipMemcpy(out, e->dTrkOut, n * sizeof(lkf_tracker_status), hipMemcpyDeviceToHost), "tracker out copy");
   return LKF_OK;

@@ -240,10 +240,35 @@ struct TrackerState {  // StreamTracker + StreamTrackerPacket of one (track, spa
   uint8_t initialized, paused, stopped, workerLive, status, lastNotified, bitrateChanged, pad;
   int64_t bytes[4];    // bytesForBitrate
   int64_t bitrate[4];
+  // StreamTrackerFrame (streamtracker_frame.go:39-211) when `frame`
+  uint8_t frame, tsInit, lastCheckSet, pad2;
+  uint32_t clockRate, oldestTS, newestTS;
+  int32_t numFrames, pad3;
+  double minFPS, estFps;
+  int64_t evalIntervalNs, lastCheckNs;  // virtual clock
 };
+// StreamTrackerFrame.resetFPSCalculator + updateEvalInterval (host and device)
+__host__ __device__ inline void tracker_frame_eval_interval(TrackerState &t) {
+  t.evalIntervalNs = 500000000;  // checkInterval
+  if (t.estFps > 0.0) {
+    const int64_t iv = int64_t(1e9 / t.estFps);
+    if (iv > t.evalIntervalNs) t.evalIntervalNs = iv;
+  }
+  if (t.minFPS > 0.0) {
+    const int64_t iv = int64_t(1e9 / t.minFPS);
+    if (iv > t.evalIntervalNs) t.evalIntervalNs = iv;
+  }
+}
+__host__ __device__ inline void tracker_frame_reset_fps(TrackerState &t) {
+  t.tsInit = 0;
+  t.oldestTS = t.newestTS = 0;
+  t.numFrames = 0;
+  t.estFps = 0.0;
+  tracker_frame_eval_interval(t);
+}
 hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const lkf_pkt *pkts,
                                   const uint32_t *tBegin, const uint32_t *tEnd);
 hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
-                               int64_t elapsedNs, lkf_tracker_status *out);
+                               int64_t elapsedNs, int64_t nowNs, lkf_tracker_status *out);
 
 }  // namespace lkf

@@ -8,6 +8,10 @@
 //                      which activates the tracker (and starts its worker)
 //   k_tracker_tick     the worker's tickers, driven by the host: CheckStatus
 //                      (cycle counting) and the bitrate report, one thread each
+// A frame tracker (streamtracker_frame.go:39-211) observes its layer's marker
+// packets in batch order (oldest / newest timestamp, frame count: lane-uniform
+// updates over the ballot of markers) and estimates the frame rate at
+// CheckStatus on the virtual clock.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -37,19 +41,54 @@ __global__ void __launch_bounds__(64) k_tracker_observe(TrackerState *st, u32 n,
   if (s.stopped || s.paused) return;
   const u32 b = tBegin[s.track], e = tEnd[s.track];
   u64 cnt = 0, bytes[4] = {0, 0, 0, 0};
-  for (u32 i = b + threadIdx.x; i < e; i += 64) {
-    const lkf_pkt &p = pkts[i];
-    if (p.layer != s.layer || p.payload_len == 0) continue;
-    cnt++;
-    // len(pkt.RawPacket): header + payload (the padding of a padded packet is not in lkf_pkt)
-    const int t = p.temporal;
-    if (t >= 0 && t < 4) bytes[t] += u64(p.payload_off) + p.payload_len;
+  bool gotFirst = false;
+  i64 firstArrival = 0;
+  for (u32 base = b; base < e; base += 64) {  // (uniform trip count)
+    const u32 i = base + threadIdx.x;
+    bool q = false, mk = false;
+    u32 ts = 0;
+    i64 arr = 0;
+    if (i < e) {
+      const lkf_pkt &p = pkts[i];
+      q = p.layer == s.layer && p.payload_len > 0;
+      if (q) {
+        cnt++;
+        // len(pkt.RawPacket): header + payload (the padding of a padded packet is not in lkf_pkt)
+        const int t = p.temporal;
+        if (t >= 0 && t < 4) bytes[t] += u64(p.payload_off) + p.payload_len;
+        mk = (p.hdr1 & 0x80) != 0;
+        ts = u32(p.ext_ts);
+        arr = p.arrival_ns;
+      }
+    }
+    if (!s.frame) continue;
+    const u64 qm = __ballot(q);
+    if (!gotFirst && qm) {
+      gotFirst = true;
+      firstArrival = __shfl(arr, __ffsll(static_cast<long long>(qm)) - 1, 64);
+    }
+    for (u64 mm = __ballot(mk); mm; mm &= mm - 1) {  // StreamTrackerFrame.Observe, marker packets in order
+      const u32 t = u32(__shfl(int(ts), __ffsll(static_cast<long long>(mm)) - 1, 64));
+      if (!s.tsInit) {
+        s.tsInit = 1;
+        s.oldestTS = s.newestTS = t;
+        s.numFrames = 1;
+      } else {
+        if (u32(t - s.oldestTS) > (1u << 31)) s.oldestTS = t;
+        if (u32(t - s.newestTS) < (1u << 31)) s.newestTS = t;
+        s.numFrames++;
+      }
+    }
   }
   cnt = wsum(cnt);
   for (int t = 0; t < 4; t++) bytes[t] = wsum(bytes[t]);
   if (threadIdx.x != 0 || cnt == 0) return;
-  if (!s.initialized) {  // StreamTrackerPacket.Observe: the first packet activates
+  if (!s.initialized) {  // StreamTrackerPacket / Frame.Observe: the first packet activates
     s.initialized = 1;
+    if (s.frame) {  // lastStatusCheckAt = time.Now()
+      s.lastCheckSet = 1;
+      s.lastCheckNs = firstArrival;
+    }
     s.countSinceLast = u32(cnt);
     s.status = 1;
     s.workerLive = 1;  // go s.worker(generation)
@@ -61,14 +100,55 @@ __global__ void __launch_bounds__(64) k_tracker_observe(TrackerState *st, u32 n,
   st[k] = s;
 }
 
+__device__ __forceinline__ double round_fps(double fr) { return round(fr / 0.01) * 0.01; }  // roundFrameRate
+
+// StreamTrackerFrame.CheckStatus streamtracker_frame.go:124-186: 0 none, 1 stopped, 2 active
+__device__ int frame_check(TrackerState &s, i64 nowNs) {
+  if (!s.lastCheckSet) {
+    s.lastCheckSet = 1;
+    s.lastCheckNs = nowNs;
+  }
+  if (nowNs - s.lastCheckNs < i64(0.98 * double(s.evalIntervalNs))) return 0;
+  s.lastCheckNs = nowNs;
+  const u32 diff = s.newestTS - s.oldestTS;
+  double frameRate = 0.0;
+  if (diff != 0 && s.numFrames >= 2) {  // updateEstimatedFrameRate
+    frameRate = round_fps(double(s.clockRate) / double(diff) * double(s.numFrames - 1));
+    s.oldestTS = s.newestTS;
+    s.numFrames = 1;
+    double factor = 1.0;
+    if (s.estFps < frameRate)
+      factor = 0.6;
+    else if (s.estFps > frameRate)
+      factor = 0.9;
+    // unfused, as the reference computes it
+    const double est = round_fps(__dadd_rn(__dmul_rn(frameRate, factor), __dmul_rn(s.estFps, __dadd_rn(1.0, -factor))));
+    if (s.estFps != est) {
+      s.estFps = est;
+      tracker_frame_eval_interval(s);
+    }
+  }
+  if (frameRate == 0.0) {
+    tracker_frame_reset_fps(s);
+    return 1;
+  }
+  return 2;
+}
+
 __global__ void k_tracker_tick(TrackerState *st, const int32_t *__restrict__ ids, u32 n, int check, i64 elapsedNs,
-                               lkf_tracker_status *out) {
+                               i64 nowNs, lkf_tracker_status *out) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   TrackerState s = st[ids[i]];
   s.bitrateChanged = 0;
   if (s.workerLive) {
-    if (check && s.initialized) {  // updateStatus -> StreamTrackerPacket.CheckStatus
+    if (check && s.initialized && s.frame) {
+      const int c = frame_check(s, nowNs);
+      if (c == 1)
+        s.status = 0;
+      else if (c == 2)
+        s.status = 1;
+    } else if (check && s.initialized) {  // updateStatus -> StreamTrackerPacket.CheckStatus
       if (s.countSinceLast >= s.samples)
         s.cycleCount++;
       else
@@ -116,9 +196,9 @@ hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, c
   return hipGetLastError();
 }
 hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
-                               int64_t elapsedNs, lkf_tracker_status *out) {
+                               int64_t elapsedNs, int64_t nowNs, lkf_tracker_status *out) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_tracker_tick, dim3((n + 63) / 64), dim3(64), 0, s, st, ids, n, check, elapsedNs, out);
+  hipLaunchKernelGGL(k_tracker_tick, dim3((n + 63) / 64), dim3(64), 0, s, st, ids, n, check, elapsedNs, nowNs, out);
   return hipGetLastError();
 }
 

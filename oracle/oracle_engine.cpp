@@ -426,7 +426,8 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
     for (u32 i = 0; i < n; i++)
       for (size_t k = 0; k < e->trk.size(); k++)
         if (e->trkKey[k].first == pkts[i].track && e->trkKey[k].second == pkts[i].layer)
-          e->trk[k].Observe(pkts[i].temporal, int(pkts[i].payload_off) + pkts[i].payload_len, pkts[i].payload_len);
+          e->trk[k].Observe(pkts[i].temporal, int(pkts[i].payload_off) + pkts[i].payload_len, pkts[i].payload_len,
+                            (pkts[i].hdr1 & 0x80) != 0, u32(pkts[i].ext_ts), pkts[i].arrival_ns);
   for (u32 d = 0; d < ndt; d++)  // sendingPacket: bytesSent += hdrSize + payloadSize
     for (auto &o : e->dts[d]->outs) {
       e->dts[d]->packetsSent++;
@@ -853,6 +854,12 @@ int32_t orc_add_stream_tracker(orc_engine *e, int32_t track, int32_t layer, uint
   e->trk.emplace_back(samples, cycles);
   return int32_t(e->trk.size() - 1);
 }
+int32_t orc_add_stream_tracker_frame(orc_engine *e, int32_t track, int32_t layer, uint32_t clock_rate, double min_fps) {
+  if (track < 0 || track >= (int)e->tracks.size() || layer < 0 || clock_rate == 0) return LKF_EINVAL;
+  e->trkKey.push_back({u32(track), layer});
+  e->trk.push_back(orc_st::Tracker::Frame(clock_rate, min_fps));
+  return int32_t(e->trk.size() - 1);
+}
 int orc_stream_tracker_ctl(orc_engine *e, int32_t tracker, int32_t op, int32_t arg) {
   if (tracker < 0 || tracker >= (int)e->trk.size()) return LKF_EINVAL;
   orc_st::Tracker &t = e->trk[tracker];
@@ -866,8 +873,14 @@ int orc_stream_tracker_ctl(orc_engine *e, int32_t tracker, int32_t op, int32_t a
     return LKF_EINVAL;
   return LKF_OK;
 }
+int orc_stream_trackers_tick_at(orc_engine *e, const int32_t *ids, uint32_t n, int check, int64_t elapsed,
+                                int64_t now_ns, lkf_tracker_status *out);
 int orc_stream_trackers_tick(orc_engine *e, const int32_t *ids, uint32_t n, int check, int64_t elapsed,
                              lkf_tracker_status *out) {
+  return orc_stream_trackers_tick_at(e, ids, n, check, elapsed, 0, out);
+}
+int orc_stream_trackers_tick_at(orc_engine *e, const int32_t *ids, uint32_t n, int check, int64_t elapsed,
+                                int64_t now_ns, lkf_tracker_status *out) {
   if (n && (!ids || !out)) return LKF_EINVAL;
   std::vector<u8> seen(e->trk.size(), 0);
   for (uint32_t i = 0; i < n; i++) {
@@ -876,7 +889,7 @@ int orc_stream_trackers_tick(orc_engine *e, const int32_t *ids, uint32_t n, int 
   }
   for (uint32_t i = 0; i < n; i++) {
     orc_st::Tracker &t = e->trk[ids[i]];
-    t.Tick(check != 0, elapsed);
+    t.Tick(check != 0, elapsed, now_ns);
     lkf_tracker_status &o = out[i];
     std::memset(&o, 0, sizeof(o));
     o.tracker = ids[i];

@@ -12,6 +12,7 @@
 //  worker do nothing.  Pinned by streamtracker_packet_test.go (kat_tracker.inc).
 // =============================================================================
 #pragma once
+#include <cmath>
 #include <cstdint>
 
 namespace orc_st {
@@ -56,8 +57,100 @@ struct PacketTracker {  // StreamTrackerPacket
   }
 };
 
-struct Tracker {  // StreamTracker over a PacketTracker
+// StreamTrackerFrame streamtracker_frame.go:39-211
+struct FrameTracker {
+  u32 clockRate = 0;
+  double minFPS = 0;
+  bool initialized = false, tsInitialized = false;
+  u32 oldestTS = 0, newestTS = 0;
+  int numFrames = 0;
+  double estimatedFrameRate = 0;
+  i64 evalIntervalNs = 0;
+  bool lastCheckSet = false;  // !lastStatusCheckAt.IsZero()
+  i64 lastCheckNs = 0;
+  static double roundFrameRate(double fr) { return std::round(fr / 0.01) * 0.01; }
+  void updateEvalInterval() {
+    evalIntervalNs = 500000000;  // checkInterval
+    if (estimatedFrameRate > 0.0) {
+      const i64 iv = i64(1e9 / estimatedFrameRate);
+      if (iv > evalIntervalNs) evalIntervalNs = iv;
+    }
+    if (minFPS > 0.0) {
+      const i64 iv = i64(1e9 / minFPS);
+      if (iv > evalIntervalNs) evalIntervalNs = iv;
+    }
+  }
+  void resetFPSCalculator() {
+    tsInitialized = false;
+    oldestTS = newestTS = 0;
+    numFrames = 0;
+    estimatedFrameRate = 0.0;
+    updateEvalInterval();
+  }
+  void Reset() {
+    initialized = false;
+    resetFPSCalculator();
+    lastCheckSet = false;
+    lastCheckNs = 0;
+  }
+  Change Observe(bool hasMarker, u32 ts, i64 nowNs) {
+    if (hasMarker) {
+      if (!tsInitialized) {
+        tsInitialized = true;
+        oldestTS = newestTS = ts;
+        numFrames = 1;
+      } else {
+        if (u32(ts - oldestTS) > (1u << 31)) oldestTS = ts;
+        if (u32(ts - newestTS) < (1u << 31)) newestTS = ts;
+        numFrames++;
+      }
+    }
+    if (!initialized) {
+      initialized = true;
+      lastCheckSet = true;
+      lastCheckNs = nowNs;
+      return ChangeActive;
+    }
+    return ChangeNone;
+  }
+  double updateEstimatedFrameRate() {
+    const u32 diff = newestTS - oldestTS;
+    if (diff == 0 || numFrames < 2) return 0.0;
+    const double frameRate = roundFrameRate(double(clockRate) / double(diff) * double(numFrames - 1));
+    oldestTS = newestTS;
+    numFrames = 1;
+    double factor = 1.0;
+    if (estimatedFrameRate < frameRate)
+      factor = 0.6;  // frameRateIncreaseFactor
+    else if (estimatedFrameRate > frameRate)
+      factor = 0.9;  // frameRateDecreaseFactor
+    const double est = roundFrameRate(frameRate * factor + estimatedFrameRate * (1.0 - factor));
+    if (estimatedFrameRate != est) {
+      estimatedFrameRate = est;
+      updateEvalInterval();
+    }
+    return frameRate;
+  }
+  Change CheckStatus(i64 nowNs) {
+    if (!initialized) return ChangeNone;
+    if (!lastCheckSet) {
+      lastCheckSet = true;
+      lastCheckNs = nowNs;
+    }
+    if (nowNs - lastCheckNs < i64(0.98 * double(evalIntervalNs))) return ChangeNone;  // statusCheckTolerance
+    lastCheckNs = nowNs;
+    if (updateEstimatedFrameRate() == 0.0) {
+      resetFPSCalculator();
+      return ChangeStopped;
+    }
+    return ChangeActive;
+  }
+};
+
+struct Tracker {  // StreamTracker over a PacketTracker (or a FrameTracker when frame)
   PacketTracker impl;
+  bool frame = false;
+  FrameTracker fimpl;
   bool paused = false, stopped = false, workerLive = false;
   Status status = Stopped, lastNotified = Stopped;
   int notifications = 0;         // onStatusChanged calls
@@ -66,6 +159,14 @@ struct Tracker {  // StreamTracker over a PacketTracker
   i64 bitrate[4] = {0, 0, 0, 0};
 
   Tracker(u32 samples, u32 cycles) { impl.samplesRequired = samples, impl.cyclesRequired = cycles; }
+  static Tracker Frame(u32 clockRate, double minFPS) {
+    Tracker t(0, 0);
+    t.frame = true;
+    t.fimpl.clockRate = clockRate;
+    t.fimpl.minFPS = minFPS;
+    t.fimpl.Reset();
+    return t;
+  }
   void maybeNotify() {
     if (status != lastNotified) {
       lastNotified = status;
@@ -77,6 +178,7 @@ struct Tracker {  // StreamTracker over a PacketTracker
     status = Stopped;
     for (int i = 0; i < 4; i++) bytesForBitrate[i] = bitrate[i] = 0;
     impl.Reset();
+    if (frame) fimpl.Reset();
   }
   void Reset() {
     if (stopped) return;
@@ -99,9 +201,9 @@ struct Tracker {  // StreamTracker over a PacketTracker
     workerLive = false;
   }
   // Observe streamtracker.go:187-219
-  void Observe(int temporalLayer, int pktSize, int payloadSize) {
+  void Observe(int temporalLayer, int pktSize, int payloadSize, bool hasMarker = false, u32 ts = 0, i64 nowNs = 0) {
     if (stopped || paused || payloadSize == 0) return;
-    const Change c = impl.Observe();
+    const Change c = frame ? fimpl.Observe(hasMarker, ts, nowNs) : impl.Observe();
     if (c == ChangeActive) {
       status = Active;
       workerLive = true;  // go s.worker(generation)
@@ -110,8 +212,8 @@ struct Tracker {  // StreamTracker over a PacketTracker
     if (c != ChangeNone) maybeNotify();
   }
   // updateStatus streamtracker.go:273-284
-  void updateStatus() {
-    switch (impl.CheckStatus()) {
+  void updateStatus(i64 nowNs = 0) {
+    switch (frame ? fimpl.CheckStatus(nowNs) : impl.CheckStatus()) {
       case ChangeStopped:
         status = Stopped;
         break;
@@ -135,10 +237,10 @@ struct Tracker {  // StreamTracker over a PacketTracker
     }
   }
   // the worker's tick(s): check = the status ticker, elapsedNs > 0 = the bitrate ticker
-  void Tick(bool check, i64 elapsedNs) {
+  void Tick(bool check, i64 elapsedNs, i64 nowNs = 0) {
     bitrateChanged = false;
     if (!workerLive) return;
-    if (check) updateStatus();
+    if (check) updateStatus(nowNs);
     if (elapsedNs > 0) bitrateReport(elapsedNs);
   }
   // BitrateTemporalCumulative streamtracker.go:221-247

@@ -38,3 +38,32 @@ def test_trackers_activate_and_report(workload):
     finally:
         o.destroy(oh)
         tr.close()
+
+
+def test_frame_trackers_active_then_stopped(workload):
+    """StreamTrackerFrame on the oracle: every streaming layer's tracker turns
+    active on its first packet and stays active while frames arrive (checks
+    every 500 ms of virtual time); once the feed ends, the next checks find no
+    two frames in the interval and report stopped (streamtracker_frame.go:124-142)."""
+    o = load_oracle()
+    tr = workload.Trace(1, duration_s=3.0, batch_s=0.1, seed=2)
+    oh = o.create(500)
+    try:
+        workload.load_topology(o.api, oh, tr)
+        ids = tracker_lib.add_frame_trackers(o.api, oh, tr, seed=1)
+        for b in range(tr.nbatches):
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(oh, pk, n, ar, alen)
+            now = tracker_lib.EPOCH + int((b + 1) * 0.1e9)
+            r = tracker_lib.tick_at(o.api, oh, ids, b % 5 == 4, 0, now)
+            if b >= 10:
+                assert (r["status"] == 1).all(), b
+        end = tracker_lib.EPOCH + int(tr.nbatches * 0.1e9)
+        for k in range(1, 8):  # no packets any more: 2 s covers the 0.5 fps eval interval
+            r = tracker_lib.tick_at(o.api, oh, ids, True, 0, end + k * 500_000_000)
+        assert (r["status"] == 0).all()
+        assert (r["notifications"] == 2).all()
+    finally:
+        o.destroy(oh)
+        tr.close()

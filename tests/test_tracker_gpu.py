@@ -59,3 +59,54 @@ def test_stream_trackers_match_oracle(pkg, workload, cfg):
         eng.close()
         o.destroy(oh)
         tr.close()
+
+
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=3, seed=8), dict(config=1, seed=4)])
+def test_frame_trackers_match_oracle(pkg, workload, cfg):
+    """StreamTrackerFrame (streamtracker_frame.go:39-211; no reference test:
+    parity unpinned beyond this engine-vs-oracle check): marker packets per
+    batch, CheckStatus ticks every 100-300 ms of virtual time (the frame
+    tracker's own eval interval decides which ones count), bitrate reports
+    every second, resets / pauses / stops along the way."""
+    o = load_oracle()
+    abi = pkg.abi
+    kw = dict(cfg)
+    tr = workload.Trace(kw.pop("config"), duration_s=8.0, batch_s=0.1, **kw)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    rng = np.random.default_rng(3)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+        ids = tracker_lib.add_frame_trackers(eng.api, eng.h, tr, seed=6)
+        assert np.array_equal(ids, tracker_lib.add_frame_trackers(o.api, oh, tr, seed=6))
+        stops = actives = 0
+        for b in range(tr.nbatches):
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            eng.submit(pk, n, ar, alen)
+            eng.run()
+            eng.sync()
+            o.run(oh, pk, n, ar, alen)
+            eng.drain()
+            now = tracker_lib.EPOCH + int((b + 1) * 0.1e9)
+            check = b % int(rng.integers(1, 4)) == 0
+            el = 10**9 if b % 10 == 9 else 0
+            g = tracker_lib.tick_at(eng.api, eng.h, ids, check, el, now)
+            r = tracker_lib.tick_at(o.api, oh, ids, check, el, now)
+            for f in ("tracker", "status", "bitrate_changed", "notifications", "bitrate", "cumulative"):
+                assert np.array_equal(g[f], r[f]), (b, f)
+            actives += int((r["status"] == 1).sum())
+            stops += int((r["status"] == 0).sum())
+            if b % 15 == 7:
+                for k in rng.choice(ids, size=min(4, len(ids)), replace=False):
+                    op = int(rng.integers(1, 4))
+                    arg = int(rng.integers(0, 2))
+                    assert eng.api["stream_tracker_ctl"](eng.h, int(k), op, arg) == 0
+                    assert o.api["stream_tracker_ctl"](oh, int(k), op, arg) == 0
+        assert actives > 0 and stops > 0
+    finally:
+        eng.close()
+        o.destroy(oh)
+        tr.close()

@@ -27,3 +27,29 @@ def tick(api, h, ids, check, elapsed_ns):
     out = np.zeros(len(ids), dtype=abi.TRACKER_STATUS_DTYPE)
     assert api["stream_trackers_tick"](h, ids.ctypes.data, len(ids), int(check), int(elapsed_ns), out.ctypes.data) == 0
     return out
+
+
+EPOCH = 1700000000 * 10**9  # the synthetic workload's virtual epoch (synth.cpp)
+
+
+def add_frame_trackers(api, h, trace, seed):
+    """A StreamTrackerFrame per (video track, spatial layer), MinFPS from the
+    camera / screen-share defaults (config.go:413-458) or none."""
+    rng = np.random.default_rng(seed)
+    ids = []
+    for t in range(trace.ntracks):
+        if trace.tracks[t].kind != 1:
+            continue
+        for layer in range(3):
+            min_fps = float(rng.choice([0.0, 0.5, 5.0]))
+            k = api["add_stream_tracker_frame"](h, t, layer, 90000, min_fps)
+            assert k >= 0
+            ids.append(k)
+    return np.array(ids, dtype=np.int32)
+
+
+def tick_at(api, h, ids, check, elapsed_ns, now_ns):
+    out = np.zeros(len(ids), dtype=abi.TRACKER_STATUS_DTYPE)
+    assert api["stream_trackers_tick_at"](h, ids.ctypes.data, len(ids), int(check), int(elapsed_ns), int(now_ns),
+                                          out.ctypes.data) == 0
+    return out
