@@ -25,7 +25,7 @@ def main_control(o, abi, wl, pkg):
         tr = wl.Trace(**kw)
         h = o.create(500)
         fx = golden_lib.run_control_case(o.api, h, tr, wl, lambda: pkg.drain_arrays(o.api, h),
-                                         lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi)
+                                         lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi, name)
         fx["case"] = name
         fx["trace"] = kw
         with open(golden_lib.path(name), "w") as f:

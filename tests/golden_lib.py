@@ -91,6 +91,8 @@ def run_case(api, h, trace, workload, stats_fn, drain_fn, run_fn, abi):
 # RED, stream trackers, NACK lookups) on one trace: one digest per step ----
 CONTROL_CASES = [
     ("control_config2", dict(config=2, duration_s=3.0, batch_s=0.25, rooms=2, seed=23)),
+    # + Pause / GetNextHigherTransition / AllocateNextHigher and frame trackers
+    ("control_config2_alloc", dict(config=2, duration_s=3.0, batch_s=0.25, rooms=2, seed=29)),
 ]
 
 
@@ -101,12 +103,14 @@ def _sha(*arrays):
     return h.hexdigest()
 
 
-def run_control_case(api, h, trace, workload, drain_fn, run_fn, abi):
+def run_control_case(api, h, trace, workload, drain_fn, run_fn, abi, name="control_config2"):
     """Drives `trace` with control calls between its batches; returns the fixture dict."""
     from tests import pad_lib, red_lib, rtx_lib, tracker_lib
-    from tests.test_alloc_gpu import make_alloc_reqs
+    from tests.test_alloc_gpu import make_alloc_reqs, stream_allocator_steps, run_step
+    ext = name.endswith("_alloc")
     workload.load_topology(api, h, trace)
     ids = tracker_lib.add_trackers(api, h, trace, seed=11)
+    fids = tracker_lib.add_frame_trackers(api, h, trace, seed=12) if ext else None
     m = red_lib.opus_map(trace)
     out = {"steps": []}
     epoch = 1700000000 * 10**9
@@ -121,6 +125,10 @@ def run_control_case(api, h, trace, workload, drain_fn, run_fn, abi):
             a = np.zeros(len(reqs), dtype=abi.ALLOCATION_DTYPE)
             assert api["allocate_optimal"](h, reqs.ctypes.data, len(reqs), a.ctypes.data) == 0
             out["steps"].append(["allocate", b, int(len(a)), _sha(a)])
+        if ext and b >= 1:  # the stream allocator's pause / probe calls
+            for k, step in enumerate(stream_allocator_steps(abi, trace.ndts, min(b, 9))):
+                r = run_step(api, h, abi, step)
+                out["steps"].append([step[0], b, int(len(r)), _sha(r)])
         if b % 4 == 3:  # blank frames
             reqs = pad_lib.make_reqs(trace.ndts, seed=100 + b, frac=0.3)
             rec, war, _ = pad_lib.pad(api, h, reqs, now, blank=True)
@@ -140,6 +148,10 @@ def run_control_case(api, h, trace, workload, drain_fn, run_fn, abi):
             t = tracker_lib.tick(api, h, ids, True, 500_000_000 if b % 4 == 3 else 0)
             t = t[["tracker", "status", "bitrate_changed", "notifications", "bitrate", "cumulative"]]
             out["steps"].append(["trackers", b, int(len(t)), _sha(t.tobytes())])
+        if ext:
+            t = tracker_lib.tick_at(api, h, fids, b % 2 == 0, 10**9 if b % 4 == 0 else 0, now + int(0.25e9))
+            t = t[["tracker", "status", "bitrate_changed", "notifications", "bitrate", "cumulative"]]
+            out["steps"].append(["frame_trackers", b, int(len(t)), _sha(t.tobytes())])
     nacks = rtx_lib.make_nacks(api, h, trace, seed=3)
     r = rtx_lib.rtx_lookup(api, h, nacks, epoch + int(trace.nbatches * 0.25e9) + 10**8)
     out["steps"].append(["rtx", trace.nbatches, int(len(r)), _sha(r)])

@@ -86,7 +86,7 @@ def test_oracle_matches_control_golden(name, workload, abi, pkg):
     h = o.create(500)
     try:
         got = golden_lib.run_control_case(o.api, h, tr, workload, lambda: pkg.drain_arrays(o.api, h),
-                                          lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi)
+                                          lambda pk, n, ar, alen: o.run(h, pk, n, ar, alen), abi, name)
     finally:
         o.destroy(h)
         tr.close()
@@ -105,7 +105,7 @@ def test_engine_matches_control_golden(name, workload, abi, pkg):
             eng.run()
             eng.sync()
 
-        got = golden_lib.run_control_case(eng.api, eng.h, tr, workload, eng.drain, run, abi)
+        got = golden_lib.run_control_case(eng.api, eng.h, tr, workload, eng.drain, run, abi, name)
     finally:
         eng.close()
         tr.close()
