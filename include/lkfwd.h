@@ -259,6 +259,12 @@ typedef struct lkf_stream_params {
                                the stream's DependencyDescriptorParser; 0 = none */
   uint32_t observe_duration_ms;
   uint32_t smooth_intervals;
+  /* NACK feedback negotiated for the codec (buffer.go:248-256): the Buffer
+   * gets mediatransportutil's NackQueue (NackQueueParamsDefault); 0 = none
+   * (audio/red, or no "nack" RTCP feedback) */
+  uint8_t nack;
+  uint8_t reserved[3];
+  uint32_t rtt_ms;          /* initial NackQueue RTT (Buffer.SetRTT); 0 = the queue's default 70 ms */
 } lkf_stream_params;
 
 /* One received datagram of a raw batch (24 B).  A raw batch is grouped by
@@ -297,9 +303,28 @@ typedef struct lkf_stream_stats {
   uint64_t ext_start_sn, ext_highest_sn, ext_start_ts, ext_highest_ts;
   uint64_t packets_lost, packets_out_of_order, packets_duplicate, packets_padding;
   uint64_t bytes, header_bytes, bytes_duplicate, bytes_padding, frames;
+  uint64_t nacks;  /* sequence numbers NACKed (rtpStats.UpdateNack(numSeqNumsNacked), buffer.go:682-684) */
   uint8_t initialized;
   uint8_t reserved[7];
 } lkf_stream_stats;
+
+/* One RTCP TransportLayerNack a Buffer sent from its deferred doNACKs
+ * (buffer.go:417-421, :673-710): NackQueue.Pairs() at the arrival time of
+ * the datagram whose calc emitted it (24 B).  Its pairs are n_pairs
+ * consecutive lkf_nack_pair entries from pair_off. */
+typedef struct lkf_rtcp_nack {
+  uint32_t datagram;    /* index in the ingested raw batch */
+  uint32_t stream;      /* lkf_add_stream handle */
+  uint32_t media_ssrc;  /* SenderSSRC = MediaSSRC = the Buffer's mediaSSRC */
+  uint32_t pair_off;
+  uint16_t n_pairs;
+  uint16_t num_nacked;  /* numSeqNumsNacked */
+  uint32_t reserved;
+} lkf_rtcp_nack;
+typedef struct lkf_nack_pair { /* rtcp.NackPair */
+  uint16_t packet_id;
+  uint16_t lost_packets; /* bit i: packet_id + i + 1 is lost too */
+} lkf_nack_pair;
 
 /* One active speaker (livekit.SpeakerInfo, room.go:254-279), 16 B. */
 typedef struct lkf_speaker {
@@ -677,6 +702,16 @@ int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out);
 /* Its lkf_pkt_dd side array (same order and count as lkf_ingested). */
 int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_out);
 int lkf_stream_stats_get(lkf_engine *e, int32_t stream, lkf_stream_stats *out);
+/* The RTCP NACKs the last ingest's Buffer.calc calls emitted, in datagram
+ * order (at most one per datagram), and their pairs in the same order.
+ * n_out / n_pairs_out are set even when a capacity is too small (LKF_ENOSPC).
+ * Replaces the onRtcpFeedback(TransportLayerNack) calls of Buffer.doNACKs
+ * (buffer.go:673-686). */
+int lkf_ingest_nacks(lkf_engine *e, lkf_rtcp_nack *out, uint32_t cap, lkf_nack_pair *pairs, uint32_t pair_cap,
+                     uint32_t *n_out, uint32_t *n_pairs_out);
+/* Buffer.SetRTT (buffer.go:400-414): the NackQueue RTT of a stream from the
+ * next ingest on (0 is ignored, as in the reference). */
+int lkf_stream_set_rtt(lkf_engine *e, int32_t stream, uint32_t rtt_ms);
 /* Room.GetActiveSpeakers (room.go:254-279) for every room at virtual time
  * now_ns: per participant the loudest active microphone track
  * (UpTrackManager.GetAudioLevel uptrackmanager.go:422-436, AudioLevel.GetLevel

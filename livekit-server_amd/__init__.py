@@ -15,7 +15,9 @@ import numpy as np
 
 from . import abi
 
-LIB_PATH = os.path.join(abi.LIBDIR, "liblkfwd.so")
+# LKF_LIB names another build of the engine in lib/ (liblkfwd_checked.so: the
+# bounds-checked kernels of `make` target liblkfwd_checked.so)
+LIB_PATH = os.path.join(abi.LIBDIR, os.environ.get("LKF_LIB", "liblkfwd.so"))
 _lib = None
 
 
@@ -58,10 +60,25 @@ def load_library(path=None):
                                       C.POINTER(C.c_float)]
     lib.lkf_get_cumulative.restype = C.c_int
     lib.lkf_get_cumulative.argtypes = [v, C.POINTER(abi.lkf_stats), C.c_int]
+    if hasattr(lib, "lkf_debug_check"):
+        lib.lkf_debug_check.restype = C.c_int
+        lib.lkf_debug_check.argtypes = [v, C.POINTER(C.c_uint64), C.c_int]
     lib.api = abi.bind_engine_api(lib, "lkf_")
     if path is None:
         _lib = lib
     return lib
+
+
+def debug_check(reset=True):
+    """Bounds-check record of a checked build (LKF_LIB=liblkfwd_checked.so):
+    (violations, first site, its index, its capacity), or None for a product
+    build."""
+    lib = load_library()
+    out = (C.c_uint64 * 4)()
+    rc = lib.lkf_debug_check(None, out, 1 if reset else 0)
+    if rc != 0:
+        return None
+    return tuple(int(x) for x in out)
 
 
 def drain_arrays(api, h, nmax=None):
@@ -113,6 +130,23 @@ def flows_array(api, h):
     if rc != 0:
         raise EngineError("ingest_flows rc=%d" % rc)
     return out
+
+
+def nacks_arrays(api, h):
+    """lkf_ingest_nacks: the last ingest's RTCP NACKs (RTCP_NACK_DTYPE) and
+    their pairs (NACK_PAIR_DTYPE)."""
+    n = C.c_uint32()
+    npairs = C.c_uint32()
+    rc = api["ingest_nacks"](h, None, 0, None, 0, C.byref(n), C.byref(npairs))
+    if rc not in (0, -28):
+        raise EngineError("ingest_nacks probe rc=%d" % rc)
+    recs = np.zeros(n.value, dtype=abi.RTCP_NACK_DTYPE)
+    pairs = np.zeros(npairs.value, dtype=abi.NACK_PAIR_DTYPE)
+    rc = api["ingest_nacks"](h, recs.ctypes.data, n.value, pairs.ctypes.data, npairs.value, C.byref(n),
+                             C.byref(npairs))
+    if rc != 0:
+        raise EngineError("ingest_nacks rc=%d" % rc)
+    return recs, pairs
 
 
 def speakers_array(api, h, now_ns):

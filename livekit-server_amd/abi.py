@@ -40,6 +40,9 @@ class lkf_stream_params(C.Structure):
         ("dd_ext", C.c_uint8),
         ("observe_duration_ms", C.c_uint32),
         ("smooth_intervals", C.c_uint32),
+        ("nack", C.c_uint8),
+        ("reserved", C.c_uint8 * 3),
+        ("rtt_ms", C.c_uint32),
     ]
 
 
@@ -69,7 +72,8 @@ class lkf_stream_stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "ext_start_sn", "ext_highest_sn", "ext_start_ts", "ext_highest_ts", "packets_lost",
         "packets_out_of_order", "packets_duplicate", "packets_padding", "bytes", "header_bytes",
-        "bytes_duplicate", "bytes_padding", "frames")] + [("initialized", C.c_uint8), ("reserved", C.c_uint8 * 7)]
+        "bytes_duplicate", "bytes_padding", "frames", "nacks")] + [("initialized", C.c_uint8),
+                                                                   ("reserved", C.c_uint8 * 7)]
 
     def as_tuple(self):
         return tuple(getattr(self, n) for n, _ in self._fields_[:-1])
@@ -84,6 +88,10 @@ class lkf_speaker(C.Structure):
     ]
 
 
+RTCP_NACK_DTYPE = np.dtype([("datagram", "<u4"), ("stream", "<u4"), ("media_ssrc", "<u4"), ("pair_off", "<u4"),
+                            ("n_pairs", "<u2"), ("num_nacked", "<u2"), ("reserved", "<u4")])
+assert RTCP_NACK_DTYPE.itemsize == 24
+NACK_PAIR_DTYPE = np.dtype([("packet_id", "<u2"), ("lost_packets", "<u2")])
 FLOW_DTYPE = np.dtype([("ext_sn", "<u8"), ("ext_ts", "<u8"), ("loss_start", "<u8"), ("loss_end", "<u8"),
                        ("pkt", "<u4"), ("flags", "u1"), ("reserved", "V3")])
 assert FLOW_DTYPE.itemsize == 40
@@ -375,6 +383,9 @@ def bind_engine_api(lib, prefix):
     api["ingested_dd"] = _bind(lib, prefix + "ingested_dd", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["submit_dd"] = _bind(lib, prefix + "submit_dd", C.c_int, [e, C.c_void_p, C.c_uint32])
     api["stream_stats_get"] = _bind(lib, prefix + "stream_stats_get", C.c_int, [e, C.c_int32, P(lkf_stream_stats)])
+    api["ingest_nacks"] = _bind(lib, prefix + "ingest_nacks", C.c_int,
+                                [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32)])
+    api["stream_set_rtt"] = _bind(lib, prefix + "stream_set_rtt", C.c_int, [e, C.c_int32, C.c_uint32])
     api["speakers"] = _bind(lib, prefix + "speakers", C.c_int, [e, C.c_int64, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["downtrack_summaries"] = _bind(lib, prefix + "downtrack_summaries", C.c_int,
                                        [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])

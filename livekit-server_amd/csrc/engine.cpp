@@ -279,8 +279,18 @@ struct lkf_engine {
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
   uint32_t *dIList = nullptr, *dIListCnt = nullptr;  // per-stream datagram lists (k_ing_lists)
   uint32_t *dILanePerm = nullptr;                     // k_ing_stream lane -> stream, by (kind, layer)
+  // NACK queues (allocated with the first stream that has one) and the last
+  // ingest's RTCP NACKs (per datagram result + bump-allocated pairs)
+  NackState *dNack = nullptr;
+  uint32_t *dNackInfo = nullptr, *dNackPairOff = nullptr, *dNackPairCnt = nullptr;
+  lkf_nack_pair *dNackPairs = nullptr;
+  uint32_t nackPairCap = 0;
+  uint64_t *dNackRecPos = nullptr, *dNackPairPos = nullptr, *dNackTot = nullptr;
+  lkf_rtcp_nack *dNackOut = nullptr;
+  lkf_nack_pair *dNackPairsOut = nullptr;
   bool ingLane = false;                               // LKF_ING_LANE=1: lane-per-stream ingress (A/B)
   uint32_t lastIngestN = 0;
+  const lkf_raw_pkt *ingRaws = nullptr;  // the last ingest's datagram descriptors (device)
   // speaker ranking tables (rebuilt when topology changes)
   uint32_t nRooms = 0;
   uint32_t *dRoomPartOff = nullptr, *dPartId = nullptr, *dPartMicOff = nullptr, *dMics = nullptr, *dRoomId = nullptr;
@@ -407,6 +417,7 @@ static int ensure_dd(lkf_engine *e) {
   if (e->nDDStreams && !e->dDDIng) {
     HIPCHK(dalloc(&e->dDDIng, e->maxStreams), "alloc dd parsers");
     HIPCHK(dalloc(&e->dDDIngStruct, size_t(e->maxStreams) * 2), "alloc dd parser structures");
+    HIPCHK(hipMemset(e->dDDIngStruct, 0, size_t(e->maxStreams) * 2 * sizeof(DDStruct)), "dd parser structures reset");
     HIPCHK(dalloc(&e->dIngDD, c.max_batch_pkts), "alloc ingest dd");
   }
   if (e->nDDStreams > e->ddStreamInit) {  // a fresh parser per new DD stream
@@ -419,6 +430,7 @@ static int ensure_dd(lkf_engine *e) {
   HIPCHK(dalloc(&e->dDDTrack, c.max_tracks), "alloc dd tracks");
   HIPCHK(dalloc(&e->dDDState, c.max_downtracks), "alloc dd state");
   HIPCHK(hipMemset(e->dDDTrack, 0, size_t(c.max_tracks) * sizeof(DDTrack)), "dd tracks reset");
+  HIPCHK(hipMemset(e->dDDStruct, 0, size_t(c.max_tracks) * kDDSlots * sizeof(DDStruct)), "dd structures reset");
   e->ddArenaCap = c.max_out_bytes / 4 + (1u << 20);
   for (auto &x : e->ctx) {
     HIPCHK(dalloc(&x.dDDPkt, c.max_batch_pkts), "alloc dd pkts");
@@ -461,6 +473,31 @@ static int flush_topology(lkf_engine *e) {
   if (!e->pendStreams.empty()) {
     const size_t first = e->streams.size() - e->pendStreams.size();
     const size_t k = e->pendStreams.size();
+    bool anyNack = false;
+    for (const auto &d : e->pendStreams) anyNack = anyNack || d.nack;
+    if (anyNack && !e->dNack) {  // nack.NewNACKQueue for the first Buffer with NACK feedback
+      const lkf_cfg &c = e->cfg;
+      HIPCHK(dalloc(&e->dNack, e->maxStreams), "alloc nack queues");
+      HIPCHK(hipMemset(e->dNack, 0, size_t(e->maxStreams) * sizeof(NackState)), "nack queues reset");
+      HIPCHK(dalloc(&e->dNackInfo, c.max_batch_pkts), "alloc nack info");
+      HIPCHK(dalloc(&e->dNackPairOff, c.max_batch_pkts), "alloc nack pair offsets");
+      HIPCHK(dalloc(&e->dNackPairCnt, 1), "alloc nack pair count");
+      e->nackPairCap = uint32_t(std::min<uint64_t>(uint64_t(c.max_batch_pkts) * 8 + 4096, 1u << 30));
+      HIPCHK(dalloc(&e->dNackPairs, e->nackPairCap), "alloc nack pairs");
+      HIPCHK(dalloc(&e->dNackRecPos, c.max_batch_pkts), "alloc nack positions");
+      HIPCHK(dalloc(&e->dNackPairPos, c.max_batch_pkts), "alloc nack pair positions");
+      HIPCHK(dalloc(&e->dNackTot, 2), "alloc nack totals");
+      HIPCHK(dalloc(&e->dNackOut, c.max_batch_pkts), "alloc nack records");
+      HIPCHK(dalloc(&e->dNackPairsOut, e->nackPairCap), "alloc nack pairs out");
+      HIPCHK(hipMemset(e->dNackInfo, 0, size_t(c.max_batch_pkts) * sizeof(uint32_t)), "nack info reset");
+      HIPCHK(hipMemset(e->dNackPairCnt, 0, sizeof(uint32_t)), "nack count reset");
+    }
+    if (e->dNack) {  // each new queue: empty, the stream's initial RTT (0: defaultRtt)
+      for (size_t i = 0; i < k; i++) {
+        const uint32_t rtt = e->streams[first + i].rtt_ms ? e->streams[first + i].rtt_ms : kNackDefaultRtt;
+        HIPCHK(hipMemcpy(&e->dNack[first + i].rtt, &rtt, sizeof(rtt), hipMemcpyHostToDevice), "nack rtt");
+      }
+    }
     std::vector<StreamHot> hot(k);
     for (auto &h : hot) {
       std::memset(&h, 0, sizeof(h));
@@ -603,6 +640,20 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dILanePerm, e->maxStreams));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
+    // Every persistent table starts zeroed: hipMalloc hands back memory an
+    // earlier engine of the process wrote, and no kernel may ever see those
+    // bytes (the rings are read only below their counts, but a zero start
+    // makes every batch's inputs the same from one process to the next).
+    A(hipMemset(e->dRm, 0, size_t(c.max_downtracks) * kRangeCap * sizeof(RangeEntry)));
+    A(hipMemset(e->dVc, 0, size_t(c.max_downtracks) * sizeof(VP8Cold)));
+    A(hipMemset(e->dSrm, 0, size_t(c.max_downtracks) * e->srmStride));
+    A(hipMemset(e->dHot, 0, size_t(c.max_downtracks) * sizeof(DTHot)));
+    A(hipMemset(e->dDTs, 0, size_t(c.max_downtracks) * sizeof(DevDT)));
+    A(hipMemset(e->dDTCum, 0, size_t(c.max_downtracks) * sizeof(DTCum)));
+    A(hipMemset(e->dTracks, 0, size_t(c.max_tracks) * sizeof(DevTrack)));
+    A(hipMemset(e->dStreamHot, 0, size_t(e->maxStreams) * sizeof(StreamHot)));
+    A(hipMemset(e->dStreamRings, 0, size_t(e->maxStreams) * kRangeCap * sizeof(RangeEntry)));
+    A(hipMemset(e->dHist, 0, size_t(e->maxStreams) * kHistWords * sizeof(uint64_t)));
     {  // VideoAllocationDefault (forwarder.go:111-116)
       lkf_allocation d = {};
       d.pause_reason = 3;
@@ -672,7 +723,8 @@ void lkf_destroy(lkf_engine *e) {
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
-                  e->dSpkCounts};
+                  e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
+                  e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
@@ -1059,7 +1111,11 @@ int lkf_run(lkf_engine *e, void *stream) {
   }
   e->pending.clear();
   const auto tp25 = clk::now();
-  if (nev > x.evCap || size_t(nl) + 1 > x.evOffCap) {  // this context's op buffers (run n-2 is done with them)
+  if (nev > x.evCap || size_t(nl) + 1 > x.evOffCap || nev > x.evLaneCap) {
+    // this context's op buffers: its previous run (n-3) must be done with them.
+    // ps waits on that run's "emitted" event above, so draining ps covers its
+    // prep, decide and emit stages (the lane list is read by k_ev_offsets on ps,
+    // the ops and offsets by the decide stage).
     HIPCHK(hipStreamSynchronize(ps), "sync before events realloc");
     if (nev > x.evCap) {
       if (x.dEvents) HIPCHK(hipFree(x.dEvents), "free events");
@@ -1071,11 +1127,11 @@ int lkf_run(lkf_engine *e, void *stream) {
       x.evOffCap = size_t(nl) + 1 + 4096;
       HIPCHK(dalloc(&x.dEvOff, x.evOffCap), "alloc evoff");
     }
-  }
-  if (nev > x.evLaneCap) {
-    if (x.dEvLane) HIPCHK(hipFree(x.dEvLane), "free evlane");
-    x.evLaneCap = std::max<uint64_t>(nev, 4096);
-    HIPCHK(dalloc(&x.dEvLane, x.evLaneCap), "alloc evlane");
+    if (nev > x.evLaneCap) {
+      if (x.dEvLane) HIPCHK(hipFree(x.dEvLane), "free evlane");
+      x.evLaneCap = std::max<uint64_t>(nev, 4096);
+      HIPCHK(dalloc(&x.dEvLane, x.evLaneCap), "alloc evlane");
+    }
   }
   HIPCHK(launch_h2d(ps, x.dEvents, sg.evDev, nev * sizeof(DevEvent), x.dEvLane, sg.laneDev, nev * sizeof(uint32_t)),
          "event pull");
@@ -1156,6 +1212,10 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.ddArena = x.dDDArena;
   d.ddUsed = x.dDDUsed;
   d.ddCap = e->ddArenaCap;
+  d.maxDts = e->cfg.max_downtracks;
+  d.maxTracks = e->cfg.max_tracks;
+  d.npkts = e->curN;  // (an ingest-produced batch: the launch bound)
+  d.nev = uint32_t(nev);
   HIPCHK(hipEventRecord(rg[1], s), "event");
   HIPCHK(launch_decide(s, d), "decide");
   HIPCHK(hipEventRecord(rg[2], s), "event");
@@ -1191,6 +1251,12 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.outByteCap = e->cfg.max_out_bytes;
   m.err = x.dErr;
   m.ddArena = e->ddAlloc ? x.dDDArena : nullptr;
+  m.maxDts = e->cfg.max_downtracks;
+  m.npkts = e->curN;
+  m.tupleCap = e->cfg.max_batch_tuples;
+  m.arenaLen = e->curArenaLen;
+  m.ddCap = e->ddArenaCap;
+  m.gCap = e->cfg.max_out_pkts / 64 + 2;
   // One workgroup per 64-record group (grid = the capacity bound; workgroups
   // past the batch's records exit at once).  Short-lived workgroups free their
   // slots as they finish, so the next batch's decide stage (higher-priority
@@ -1238,6 +1304,10 @@ int lkf_sync(lkf_engine *e) {
   }
   if (acc & (4u << 8)) {
     e->err = "dependency descriptor beyond an engine limit (templates, frame diffs, chains)";
+    return LKF_ENOSPC;
+  }
+  if (acc & (8u << 8)) {
+    e->err = "RTCP NACK pair capacity of an ingest exceeded";
     return LKF_ENOSPC;
   }
   if (acc & 32u) {
@@ -1292,6 +1362,13 @@ int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, con
   BatchCtx &x = e->ctx[e->lastCtx];
   uint64_t tot[4];
   HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  // a batch whose output exceeded the engine's capacity wrote nothing (k_emit
+  // flags it; lkf_sync reported it once): never hand out a range beyond the
+  // output buffers, whatever the caller did with that report
+  if (tot[2] > e->cfg.max_out_pkts || tot[3] > e->cfg.max_out_bytes) {
+    e->err = "output or tuple capacity exceeded";
+    return LKF_ENOSPC;
+  }
   if (d_out) *d_out = x.dOut;
   if (d_arena) *d_arena = x.dOutArena;
   if (n_out) *n_out = tot[2];
@@ -1324,6 +1401,10 @@ int lkf_drain_run(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8
   HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
   if (n_out) *n_out = tot[2];
   if (arena_len) *arena_len = tot[3];
+  if (tot[2] > e->cfg.max_out_pkts || tot[3] > e->cfg.max_out_bytes) {  // (see lkf_output_device)
+    e->err = "output or tuple capacity exceeded";
+    return LKF_ENOSPC;
+  }
   if (tot[2] > cap || tot[3] > arena_cap) return LKF_ENOSPC;
   if (out && tot[2]) HIPCHK(hipMemcpy(out, x.dOut, tot[2] * sizeof(lkf_out), hipMemcpyDeviceToHost), "drain recs");
   if (arena && tot[3]) HIPCHK(hipMemcpy(arena, x.dOutArena, tot[3], hipMemcpyDeviceToHost), "drain bytes");
@@ -2209,6 +2290,7 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p) {
   d.levelExt = p->audio_level_ext;
   d.ddExt = p->dd_ext;
   d.ddIdx = p->dd_ext ? e->nDDStreams++ : 0xffffffffu;  // its DependencyDescriptorParser (buffer.go:193-201)
+  d.nack = p->nack ? 1 : 0;  // its NackQueue (buffer.go:248-256)
   const bool dflt = !p->active_level && !p->min_percentile && !p->observe_duration_ms && !p->smooth_intervals;
   d.activeLevel = dflt ? 35 : p->active_level;
   d.minPercentile = dflt ? 40 : p->min_percentile;
@@ -2264,6 +2346,16 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.listStride = e->cfg.max_batch_pkts;
   a.lanePerm = e->dILanePerm;
   a.laneStreams = e->ingLane;
+  a.nack = e->dNack;
+  a.nackInfo = e->dNackInfo;
+  a.nackPairOff = e->dNackPairOff;
+  a.nackPairCnt = e->dNackPairCnt;
+  a.nackPairs = e->dNackPairs;
+  a.nackPairCap = e->nackPairCap;
+  if (e->dNack && n) {  // this ingest's RTCP NACKs start empty
+    HIPCHK(hipMemsetAsync(e->dNackInfo, 0, size_t(n) * sizeof(uint32_t), s), "memset");
+    HIPCHK(hipMemsetAsync(e->dNackPairCnt, 0, sizeof(uint32_t), s), "memset");
+  }
   const bool dd = e->nDDStreams != 0;
   a.ddStates = dd ? e->dDDIng : nullptr;
   a.ddStructs = dd ? e->dDDIngStruct : nullptr;
@@ -2272,6 +2364,7 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   HIPCHK(launch_ingest(s, a), "ingest");
   HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 8), "ingest error fold");
   e->lastIngestN = n;
+  e->ingRaws = dRaws;
   e->curPkts = x.dPktsOwn;
   e->curN = n;  // launch bound; the count is e->dITotal
   e->curNDev = e->dITotal;
@@ -2385,7 +2478,46 @@ int lkf_stream_stats_get(lkf_engine *e, int32_t sid, lkf_stream_stats *o) {
   o->bytes_duplicate = h.bytesDuplicate;
   o->bytes_padding = h.bytesPadding;
   o->frames = h.frames;
+  o->nacks = h.nacks;
   return LKF_OK;
+}
+
+int lkf_ingest_nacks(lkf_engine *e, lkf_rtcp_nack *out, uint32_t cap, lkf_nack_pair *pairs, uint32_t pair_cap,
+                     uint32_t *n_out, uint32_t *n_pairs_out) {
+  if (!e || !n_out || !n_pairs_out) return LKF_EINVAL;
+  *n_out = *n_pairs_out = 0;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (!e->dNack || !e->lastIngestN) return LKF_OK;
+  const uint32_t n = e->lastIngestN;
+  hipStream_t ps = e->prepS;  // after the ingest that produced them
+  HIPCHK(launch_nack_compact(ps, n, e->ingRaws, e->dStreams, e->dNackInfo, e->dNackPairOff, e->dNackPairs, e->dIPartA,
+                             e->dIPartB, e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut),
+         "nack compact");
+  uint64_t tot[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->dNackTot, sizeof(tot), hipMemcpyDeviceToHost, ps), "nack totals");
+  HIPCHK(hipStreamSynchronize(ps), "nack sync");
+  *n_out = uint32_t(tot[0]);
+  *n_pairs_out = uint32_t(tot[1]);
+  if (tot[0] > cap || tot[1] > pair_cap) return LKF_ENOSPC;
+  if (tot[0] && !out) return LKF_EINVAL;
+  if (tot[1] && !pairs) return LKF_EINVAL;
+  if (tot[0]) HIPCHK(hipMemcpy(out, e->dNackOut, tot[0] * sizeof(lkf_rtcp_nack), hipMemcpyDeviceToHost), "nack records");
+  if (tot[1])
+    HIPCHK(hipMemcpy(pairs, e->dNackPairsOut, tot[1] * sizeof(lkf_nack_pair), hipMemcpyDeviceToHost), "nack pairs");
+  return LKF_OK;
+}
+
+int lkf_stream_set_rtt(lkf_engine *e, int32_t sid, uint32_t rtt_ms) {
+  if (!e || sid < 0 || sid >= int32_t(e->streams.size())) return LKF_EINVAL;
+  if (rtt_ms == 0) return LKF_OK;  // Buffer.SetRTT ignores 0
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  if (!e->streams[sid].nack || !e->dNack) return LKF_OK;  // no NackQueue (the rtpStats RTT is out of scope)
+  rc = drain_streams(e);  // a queued ingest reads the RTT
+  if (rc) return rc;
+  e->streams[sid].rtt_ms = rtt_ms;
+  HIPCHK(hipMemcpy(&e->dNack[sid].rtt, &rtt_ms, sizeof(rtt_ms), hipMemcpyHostToDevice), "nack rtt");
+  return upload_done(e);
 }
 
 // Room -> participant -> microphone-stream tables for k_speakers.
@@ -2498,6 +2630,23 @@ int lkf_debug_counters(lkf_engine *e, uint64_t out[32], int reset) {
   unsigned long long v[32];
   hipError_t r = read_diag(v, reset);
   for (int i = 0; i < 32; i++) out[i] = v[i];
+  return r == hipSuccess ? LKF_OK : LKF_ENODEV;
+}
+
+// Not part of include/lkfwd.h: the bounds-check record of a checked build
+// (-DLKF_CHECKED=1, liblkfwd_checked.so): {violations, first site, index,
+// capacity}; LKF_ENODEV from a product build.
+int lkf_debug_check(lkf_engine *e, uint64_t out[4], int reset) {
+  if (!out) return LKF_EINVAL;
+  if (e) {
+    int rc = drain_streams(e);
+    if (rc) return rc;
+  } else if (hipDeviceSynchronize() != hipSuccess) {  // no engine: the whole device
+    return LKF_EHIP;
+  }
+  unsigned long long v[4];
+  hipError_t r = read_check(v, reset);
+  for (int i = 0; i < 4; i++) out[i] = v[i];
   return r == hipSuccess ? LKF_OK : LKF_ENODEV;
 }
 

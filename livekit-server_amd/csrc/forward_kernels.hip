@@ -69,6 +69,57 @@ constexpr u64 HALF64 = 1ull << 63;
 constexpr i32 INVALID = -1;
 
 // ---------------------------------------------------------------------------
+// Checked builds (-DLKF_CHECKED=1, liblkfwd_checked.so): every global access
+// whose index is computed on the device is tested against the capacity of
+// its allocation; the first violation (site, index, capacity) and the count
+// go to g_chk (lkf_debug_check).  The access itself still happens, so a
+// checked run behaves like the product build, but an out-of-bounds index is
+// reported even when it lands in mapped memory (the usual case, which a
+// product run never notices).
+// ---------------------------------------------------------------------------
+#ifndef LKF_CHECKED
+#define LKF_CHECKED 0
+#endif
+#if LKF_CHECKED
+__device__ unsigned long long g_chk[4];
+__device__ __noinline__ void chk_fail(u32 site, u64 idx, u64 cap) {
+  if (atomicAdd(&g_chk[0], 1ull) == 0) {
+    g_chk[1] = site;
+    g_chk[2] = idx;
+    g_chk[3] = cap;
+  }
+}
+#define CHK(cond, site, idx, cap)                   \
+  do {                                              \
+    if (!(cond)) chk_fail(site, u64(idx), u64(cap)); \
+  } while (0)
+#else
+#define CHK(cond, site, idx, cap) \
+  do {                            \
+  } while (0)
+#endif
+enum ChkSite : u32 {
+  CK_DEC_DT = 1,      // decide: DownTrack handle < max_downtracks
+  CK_DEC_TRACK,       // decide: track < max_tracks
+  CK_DEC_PKT,         // decide: packet index < batch packets
+  CK_DEC_TUPLE,       // decide: tuple slot < max_batch_tuples
+  CK_DEC_SEQ,         // decide: sequencer slot < seq_size
+  CK_DEC_LAYER,       // decide: layer-list index < 3 * max_batch_pkts
+  CK_DEC_EVENT,       // decide: control-op index < ops of the batch
+  CK_EMIT_POS,        // emit: output position < DownTracks
+  CK_EMIT_DT,         // emit: DownTrack handle < max_downtracks
+  CK_EMIT_TUPLE,      // emit: tuple slot < max_batch_tuples
+  CK_EMIT_PKT,        // emit: packet index < batch packets
+  CK_EMIT_ARENA,      // emit: payload read end <= arena length + 64
+  CK_EMIT_OUT,        // emit: record < max_out_pkts
+  CK_EMIT_BYTES,      // emit: wire byte end <= max_out_bytes + 64
+  CK_EMIT_DD,         // emit: DD arena read end <= its capacity
+  CK_EMIT_GROUP,      // emit: group index entry < its capacity
+  CK_PAD_DT,          // padding: DownTrack handle < max_downtracks
+  CK_PAD_SEQ,         // padding: sequencer slot < seq_size
+};
+
+// ---------------------------------------------------------------------------
 // Packet view (lkf_pkt, 64 B) loaded with 4 x 16-B loads.
 // ---------------------------------------------------------------------------
 struct PktV {
@@ -1213,6 +1264,7 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
     m.codecLen = u8(cbLen);
 #pragma unroll
     for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+    CHK(slot < size, CK_DEC_SEQ, slot, size);
     if (lane_id() == 0) store_rec(L.seq + slot, m);  // wave-uniform record: one lane stores it
     L.h.seqExtHighestSN = esn;
     L.h.seqHighSlot = u16(slot);
@@ -1279,6 +1331,7 @@ __device__ void seq_push(Lane &L, i64 arrMs, u64 inSN, u64 esn, u64 ets, bool ma
   m.codecLen = u8(cbLen);
 #pragma unroll
   for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+  CHK(slot < size, CK_DEC_SEQ, slot, size);
   L.seq[slot] = m;
   if (esn > L.h.seqExtHighestSN) {
     L.h.seqExtHighestSN = esn;
@@ -1350,7 +1403,8 @@ constexpr int SCAN_ITEMS = 4;
 constexpr int SCAN_TILE = SCAN_T * SCAN_ITEMS;
 
 struct ScanIn {
-  int mode;  // 0: slots = npkts(track(d)) if active; 1: (fwdCnt, fwdBytes); 2: u32 flags
+  int mode;  // 0: slots = npkts(track(d)) if active; 1: (fwdCnt, fwdBytes); 2: u32 flags;
+             // 3: (word != 0, low 16 bits) of u32 words (RTCP NACKs and their pairs)
   const u32 *perm;  // position -> DownTrack (nullptr: identity)
   const DevDT *dts;
   const u32 *tBegin, *tEnd;
@@ -1362,6 +1416,11 @@ struct ScanIn {
 
 __device__ __forceinline__ void scan_load(const ScanIn &in, u32 i, u64 &a, u64 &b) {
   const u32 d = in.perm ? in.perm[i] : i;
+  if (in.mode == 3) {
+    a = in.cnt[i] != 0 ? 1 : 0;
+    b = in.cnt[i] & 0xffffu;
+    return;
+  }
   if (in.mode == 2) {  // u32 flags (ingress forward flags)
     a = in.cnt[i];
     b = 0;
@@ -1530,6 +1589,8 @@ struct DecideArgs {
   u8 *ddArena;
   u64 *ddUsed;
   u64 ddCap;
+  // capacities (checked builds test device-computed indices against them)
+  u32 maxDts, maxTracks, npkts, nev;
 };
 
 // One wave per (track, <=64 DownTracks): the packet loop is wave-uniform, so
@@ -1545,6 +1606,9 @@ struct LaneOut {
   u8 *ddArena;  // this batch's marshalled DD bytes (bump-allocated)
   u64 *ddUsed;
   u64 ddCap;
+#if LKF_CHECKED
+  u64 tupBase, tupCap;  // this DownTrack's first tuple slot, the batch's capacity
+#endif
 };
 
 template <bool DDK>
@@ -1704,6 +1768,9 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
     }
   }
 #if LKF_ABLATE != 1  // diagnostic builds only (never shipped): 1 = no tuple/sequencer writes
+#if LKF_CHECKED
+  CHK(o.tupBase + o.nFwd < o.tupCap, CK_DEC_TUPLE, o.tupBase + o.nFwd, o.tupCap);
+#endif
   if (lane_id() == 0) store_rec(o.outT + o.nFwd, t);  // wave-uniform record: one lane stores it
   // sequencer.push (downtrack.go:724-735)
   seq_push<DDK>(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
@@ -1916,6 +1983,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #if LKF_DIAG
   const u64 tP1 = clock64() + u64(__builtin_amdgcn_readfirstlane(d) & 0);  // after round 1
 #endif
+  CHK(d < A.maxDts, CK_DEC_DT, d, A.maxDts);
+  CHK(track < A.maxTracks, CK_DEC_TRACK, track, A.maxTracks);
+  CHK(evEnd <= A.nev, CK_DEC_EVENT, evEnd, A.nev);
   const DevDT dt = A.dts[d];
   const u32 pb = __builtin_amdgcn_readfirstlane(sb.y);
   u32 pe = __builtin_amdgcn_readfirstlane(sb.z);
@@ -1990,6 +2060,11 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   o.ddArena = A.ddArena;
   o.ddUsed = A.ddUsed;
   o.ddCap = A.ddCap;
+#if LKF_CHECKED
+  o.tupBase = slot0;
+  o.tupCap = A.tupleCap;
+  CHK(pe <= A.npkts, CK_DEC_PKT, pe, A.npkts);
+#endif
   const bool ddDT = DDK && (L.h.flags & F_DD) && A.ddState;
   if (ddDT) {  // the DD selector state lives in LDS for the batch
     L.ddRing = A.ddStructs + size_t(tk.ddIdx) * kDDSlots;
@@ -2037,6 +2112,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     u32 pi, n, lim;  // lane -> packet index; packets in the chunk; packet index after it
     if (steady) {
       const u32 ls = u32(L.h.curS);
+      CHK(size_t(ls) * A.pktStride + kpos < 3 * size_t(A.pktStride), CK_DEC_LAYER, size_t(ls) * A.pktStride + kpos,
+          3 * size_t(A.pktStride));
       const u32 j = A.layerBefore[size_t(ls) * A.pktStride + kpos] + lane;
       pi = j < A.layerCnt[track * 3 + ls] ? A.layerList[size_t(ls) * A.pktStride + pb + j] : 0xffffffffu;
       const u32 stopAt = min(nextAt, pe);
@@ -2057,6 +2134,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #endif
     uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
     if (valid) {
+      CHK(pi < A.npkts, CK_DEC_PKT, pi, A.npkts);
       const u64 q = u64(pi) * 4;
       r0 = src[q];
       r1 = src[q + 1];
@@ -2397,6 +2475,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           t.pad0 = 0;
           t.ddOff = 0;
           t.pad1 = 0;
+#if LKF_CHECKED
+          CHK(slot0 + o.nFwd + j < A.tupleCap, CK_DEC_TUPLE, slot0 + o.nFwd + j, A.tupleCap);
+#endif
 #if LKF_ABLATE != 1
           store_rec(o.outT + o.nFwd + j, t);
 #endif
@@ -2424,6 +2505,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           m.codecLen = u8(video ? cbLen : 0);
 #pragma unroll
           for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
+          CHK(slot < L.seqSize, CK_DEC_SEQ, slot, L.seqSize);
 #if LKF_ABLATE != 1
           if (store) store_rec(L.seq + slot, m);
 #endif
@@ -2716,6 +2798,9 @@ struct EmitArgs {
   u64 outCap, outByteCap;
   u32 *err;
   const u8 *ddArena;  // marshalled DD bytes of T_DD tuples
+  // capacities (checked builds test device-computed indices against them)
+  u32 maxDts, npkts;
+  u64 tupleCap, arenaLen, ddCap, gCap;
 };
 
 __device__ __forceinline__ u32 align_byte(u32 hi, u32 lo, u32 sh) {
@@ -2778,6 +2863,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
     const u64 r0 = g * EMIT_G;
     const u32 nrec = u32(min(u64(EMIT_G), total - r0));
     // ---- prefix phase: lane = record
+    CHK(g + 1 < A.gCap, CK_EMIT_GROUP, g + 1, A.gCap);
     const u32 pLo = A.gFirst[g];
     const u32 pHi = (g + 1 < ngroups) ? A.gFirst[g + 1] + 1 : A.ndts;
     u64 outOff = 0;
@@ -2792,11 +2878,21 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         else
           hi = mid;
       }
+      CHK(lo < A.ndts, CK_EMIT_POS, lo, A.ndts);
       const u32 d = A.perm[lo];
+      CHK(d < A.maxDts, CK_EMIT_DT, d, A.maxDts);
+      CHK(A.slotBase[d] + (r - A.recBase[lo]) < A.tupleCap, CK_EMIT_TUPLE, A.slotBase[d] + (r - A.recBase[lo]),
+          A.tupleCap);
       const Tuple t = A.tuples[A.slotBase[d] + (r - A.recBase[lo])];
+      CHK(t.pkt < A.npkts, CK_EMIT_PKT, t.pkt, A.npkts);
       const PktV p = load_pkt(A.pkts + t.pkt);
       const DevDT dt = A.dts[d];
       outOff = A.byteBase[lo] + t.relOff;
+      CHK(r < A.outCap, CK_EMIT_OUT, r, A.outCap);
+      CHK(outOff + t.outLen <= A.outByteCap, CK_EMIT_BYTES, outOff + t.outLen, A.outByteCap);
+      CHK(u64(p.arenaOff) + p.poff + p.plen <= A.arenaLen, CK_EMIT_ARENA, u64(p.arenaOff) + p.poff + p.plen,
+          A.arenaLen);
+      CHK(!(t.flags & T_DD) || u64(t.ddOff) + t.ddLen <= A.ddCap, CK_EMIT_DD, u64(t.ddOff) + t.ddLen, A.ddCap);
       lkf_out o;
       o.ext_sn = t.extSN;
       o.ext_ts = t.extTS;
@@ -2950,6 +3046,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         src[u] = sSrc[j[u]] + (o[u] - (pr & 0xffff));
         q0[u] = q1[u] = make_uint4(0, 0, 0, 0);
         if (act[u] && !lds[u]) {
+          CHK((src[u] & ~u64(15)) + 32 <= A.arenaLen + 64, CK_EMIT_ARENA, (src[u] & ~u64(15)) + 32, A.arenaLen + 64);
           const u8 *q = A.arena + (src[u] & ~u64(15));
           q0[u] = *reinterpret_cast<const uint4 *>(q);
           q1[u] = *reinterpret_cast<const uint4 *>(q + 16);
@@ -2971,6 +3068,8 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
             v.w &= keep_mask(keep - 12);
           }
         }
+        CHK(gByte + (u64(c[u]) << 4) + 16 <= A.outByteCap + 64, CK_EMIT_BYTES, gByte + (u64(c[u]) << 4) + 16,
+            A.outByteCap + 64);
         store16(outG + (u64(c[u]) << 4), v);
       }
       cur += k;
@@ -3622,6 +3721,21 @@ hipError_t read_diag(unsigned long long out[32], int) {
 }
 #endif
 
+hipError_t read_check(unsigned long long out[4], int reset) {
+#if LKF_CHECKED
+  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chk), sizeof(unsigned long long) * 4);
+  if (r == hipSuccess && reset) {
+    unsigned long long z[4] = {};
+    r = hipMemcpyToSymbol(HIP_SYMBOL(g_chk), z, sizeof(z));
+  }
+  return r;
+#else
+  (void)reset;
+  for (int i = 0; i < 4; i++) out[i] = 0;
+  return hipErrorNotSupported;
+#endif
+}
+
 hipError_t read_wtime(u32 *out, u32 nwaves) {
 #if LKF_WTIME
   if (nwaves > kWTimeWaves) nwaves = kWTimeWaves;
@@ -3711,6 +3825,10 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.ddArena = a.ddArena;
   A.ddUsed = a.ddUsed;
   A.ddCap = a.ddCap;
+  A.maxDts = a.maxDts;
+  A.maxTracks = a.maxTracks;
+  A.npkts = a.npkts;
+  A.nev = a.nev;
   // DownTracks of the dependency-descriptor selector run in their own
   // instantiation (the last ddLanes waves of the schedule)
   // Each part is a multiple of 8 slots (per-XCD lists of equal length);
@@ -3754,6 +3872,12 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   A.outByteCap = a.outByteCap;
   A.err = a.err;
   A.ddArena = a.ddArena;
+  A.maxDts = a.maxDts;
+  A.npkts = a.npkts;
+  A.tupleCap = a.tupleCap;
+  A.arenaLen = a.arenaLen;
+  A.ddCap = a.ddCap;
+  A.gCap = a.gCap;
   if (a.ddArena)
     hipLaunchKernelGGL(k_emit<PRE_MAX_DD>, dim3(a.grid), dim3(EMIT_T), 0, s, A);
   else

@@ -259,7 +259,8 @@ struct DevStream {  // static stream parameters (64 B)
   double smoothFactor;
   double activeThreshold;  // ConvertAudioLevel(ActiveLevel)
   uint8_t ddExt;           // dependency-descriptor extension id
-  uint8_t pad1[15];
+  uint8_t nack;            // the Buffer has a NackQueue (NACK feedback negotiated)
+  uint8_t pad1[14];
 };
 static_assert(sizeof(DevStream) == 64, "DevStream must be 64 B");
 
@@ -278,6 +279,7 @@ struct alignas(16) StreamHot {  // per-stream ingress state (256 B)
   // RTPStatsReceiver counters
   uint64_t packetsLost, packetsOutOfOrder, packetsDuplicate, packetsPadding;
   uint64_t bytes, headerBytes, bytesDuplicate, headerBytesDuplicate, bytesPadding, headerBytesPadding, frames;
+  uint64_t nacks;  // rtpStats.nacks: sequence numbers NACKed (UpdateNack, rtpstats_base.go:315-324)
   // AudioLevel (audiolevel.go:36-50)
   double smoothedLevel;
   int64_t lastObservedNs;
@@ -288,9 +290,28 @@ struct alignas(16) StreamHot {  // per-stream ingress state (256 B)
   uint16_t snStart, snHighest;
   uint16_t rmHead, rmCount;
   uint8_t loudest;
-  uint8_t pad[71];
+  uint8_t pad[63];
 };
 static_assert(sizeof(StreamHot) == 256, "StreamHot must be 256 B");
+
+// One stream's NACK queue: mediatransportutil nack.NackQueue with
+// NackQueueParamsDefault (MaxTries 5, CacheSize 100, MinInterval 20 ms,
+// MaxInterval 400 ms, BackoffFactor 1.25) as buffer.Buffer drives it
+// (buffer.go:545-567, :673-710).  Entries in queue order (oldest first),
+// structure of arrays so a wave holds two entries per lane.
+constexpr int kNackCap = 100;  // NackQueueParamsDefault.CacheSize
+constexpr int kNackSlots = 128;
+constexpr uint32_t kNackMaxTries = 5;
+constexpr uint32_t kNackDefaultRtt = 70;  // nack.go defaultRtt (ms)
+struct alignas(16) NackState {
+  int64_t last[kNackSlots];   // lastNackedAt, ns (virtual clock)
+  uint16_t sn[kNackSlots];    // seqNum
+  uint8_t tries[kNackSlots];
+  uint32_t count;             // entries
+  uint32_t rtt;               // ms (SetRTT)
+  uint8_t pad[8];
+};
+static_assert(sizeof(NackState) % 16 == 0, "NackState must be 16-B granular");
 
 struct alignas(16) IngParsed {  // k_ing_parse -> k_ing_stream / k_ing_out (48 B)
   uint32_t ts, ssrc;

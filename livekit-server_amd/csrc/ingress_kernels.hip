@@ -1156,6 +1156,270 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
 }
 
 // ---------------------------------------------------------------------------
+// k_ing_nack: the receive-side NACK queue (mediatransportutil nack.NackQueue,
+// NackQueueParamsDefault) of every stream that has one, as buffer.Buffer
+// drives it per datagram (buffer.go:417-421, :545-567, :673-710):
+//   updateStreamState: Remove(header SN), then Push(uint16(lost)) for every
+//                      lost SN of the flow's range  (the RTP header parsed)
+//   deferred doNACKs:  Pairs() at now = the arrival time (every datagram)
+// One wave per stream, serial over its datagrams (the queue is one
+// recurrence); the queue lives in LDS with two entries per lane, so Remove,
+// Push and the per-entry getNack decisions are ballots and a shifted copy.
+// The pair packing of the sent entries (a chain over the sent SNs) runs on
+// lane 0.  A datagram's result: info = n_pairs | num_nacked << 16 (0: no
+// RTCP NACK) and the offset of its pairs in the batch's pair buffer.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__ raws,
+                                                 const IngParsed *__restrict__ q, const lkf_flow *__restrict__ flows,
+                                                 const DevStream *__restrict__ streams, NackState *__restrict__ states,
+                                                 StreamHot *__restrict__ hot, const u32 *__restrict__ tBegin,
+                                                 const u32 *__restrict__ tEnd, const u32 *__restrict__ list,
+                                                 const u32 *__restrict__ cnt, u32 stride, u32 *__restrict__ info,
+                                                 u32 *__restrict__ pairOff, u32 *pairCnt,
+                                                 lkf_nack_pair *__restrict__ pairs, u32 pairCap, u32 *err) {
+  __shared__ i64 sLast[kNackSlots];
+  __shared__ u32 sSn[kNackSlots];
+  __shared__ u32 sTries[kNackSlots];
+  __shared__ u32 sPurge[kNackSlots];
+  __shared__ lkf_nack_pair sPairs[kNackCap];
+  const u32 sid = blockIdx.x, lane = threadIdx.x;
+  const DevStream s = streams[sid];
+  if (!s.nack) return;
+  const u32 pb = tBegin[s.track], pe = tEnd[s.track];
+  if (pb >= pe) return;  // no datagram of its track: no calc, no doNACKs
+  NackState *const g = states + sid;
+  for (u32 i = lane; i < u32(kNackSlots); i += 64) {
+    sLast[i] = g->last[i];
+    sSn[i] = g->sn[i];
+    sTries[i] = g->tries[i];
+  }
+  u32 count = g->count;
+  const u32 rtt = g->rtt;
+  __syncthreads();
+  // getNack's required interval per tries value (tries < MaxTries):
+  // tries 0: MinInterval; else min(MaxInterval, floor(rtt * 1.25^(tries-1)) ms),
+  // at least MinInterval (rtt * 1.25^k is exact in float64 for k <= 3)
+  static_assert(kNackMaxTries == 5, "one required interval per tries value 0..4");
+  auto backoff = [&](u64 num, u64 den) {
+    i64 r = i64(num / den) * 1000000;
+    if (r > 400000000) r = 400000000;
+    return r < 20000000 ? i64(20000000) : r;
+  };
+  const i64 req0 = 20000000, req1 = backoff(rtt, 1), req2 = backoff(u64(rtt) * 5, 4),
+            req3 = backoff(u64(rtt) * 25, 16), req4 = backoff(u64(rtt) * 125, 64);
+  // entry idx < count moves down one slot from index k on (NackQueue.Remove)
+  auto removeAt = [&](u32 k) {
+    i64 l[2];
+    u32 sn[2], tr[2];
+    bool mv[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const u32 idx = lane + 64u * u32(h);
+      mv[h] = idx >= k && idx + 1 < count;
+      if (mv[h]) {
+        l[h] = sLast[idx + 1];
+        sn[h] = sSn[idx + 1];
+        tr[h] = sTries[idx + 1];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const u32 idx = lane + 64u * u32(h);
+      if (mv[h]) {
+        sLast[idx] = l[h];
+        sSn[idx] = sn[h];
+        sTries[idx] = tr[h];
+      }
+    }
+    __syncthreads();
+    count--;
+  };
+  auto removeSn = [&](u32 sn16) {  // the first entry with that SN
+    const u64 m0 = __ballot(lane < count && sSn[lane] == sn16);
+    const u64 m1 = __ballot(lane + 64 < count && sSn[lane + 64] == sn16);
+    if (m0 | m1) removeAt(m0 ? u32(__ffsll((long long)m0) - 1) : 64u + u32(__ffsll((long long)m1) - 1));
+  };
+  const bool useList = s.layer < 3;
+  const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
+  const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
+  u64 nacked = 0;
+  for (u32 base = 0; base < nIdx; base += 64) {
+    const u32 k = base + lane;
+    u32 ic = 0, stm = 0xffffffffu, ipf = 0, sn = 0, ff = 0;
+    i64 arr = 0;
+    u64 ls = 0, le = 0;
+    if (k < nIdx) {
+      ic = useList ? lst[k] : pb + k;
+      const lkf_raw_pkt rp = raws[ic];
+      stm = rp.stream;
+      arr = rp.arrival_ns;
+      ipf = q[ic].flags;
+      sn = q[ic].sn;
+      const lkf_flow f = flows[ic];
+      ff = f.flags;
+      ls = f.loss_start;
+      le = f.loss_end;
+    }
+    const u32 m = min(64u, nIdx - base);
+    for (u32 x = 0; x < m; x++) {
+      if (__builtin_amdgcn_readlane(stm, x) != sid) continue;
+      const i64 now = i64((u64(__builtin_amdgcn_readlane(u32(u64(arr) >> 32), x)) << 32) |
+                          u64(__builtin_amdgcn_readlane(u32(u64(arr)), x)));
+      const u32 icx = __builtin_amdgcn_readlane(ic, x);
+      if (__builtin_amdgcn_readlane(ipf, x) & IP_OK) {  // updateStreamState ran
+        removeSn(__builtin_amdgcn_readlane(sn, x));
+        if (__builtin_amdgcn_readlane(ff, x) & LKF_FLOW_HAS_LOSS) {
+          const u64 s0 = (u64(__builtin_amdgcn_readlane(u32(ls >> 32), x)) << 32) | __builtin_amdgcn_readlane(u32(ls), x);
+          const u64 e0 = (u64(__builtin_amdgcn_readlane(u32(le >> 32), x)) << 32) | __builtin_amdgcn_readlane(u32(le), x);
+          // Push each lost SN: the queue keeps the newest CacheSize entries of
+          // (queue, lost SNs in order); every new one has tries 0, lastNackedAt now
+          const u64 L = e0 - s0;
+          const u64 total = u64(count) + L;
+          const u32 drop = total > u64(kNackCap) ? u32(min(total - u64(kNackCap), u64(count))) : 0u;
+          const u32 newCount = total > u64(kNackCap) ? u32(kNackCap) : u32(total);
+          const u64 first = L > u64(kNackCap) ? e0 - u64(kNackCap) : s0;  // first new SN kept
+          const u32 keptOld = count - drop;
+          i64 l[2];
+          u32 sv[2], tv[2];
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const u32 idx = lane + 64u * u32(h);
+            if (idx < newCount) {
+              if (idx < keptOld) {
+                l[h] = sLast[idx + drop];
+                sv[h] = sSn[idx + drop];
+                tv[h] = sTries[idx + drop];
+              } else {
+                l[h] = now;
+                sv[h] = u32(u16(first + (idx - keptOld)));
+                tv[h] = 0;
+              }
+            }
+          }
+          __syncthreads();
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const u32 idx = lane + 64u * u32(h);
+            if (idx < newCount) {
+              sLast[idx] = l[h];
+              sSn[idx] = sv[h];
+              sTries[idx] = tv[h];
+            }
+          }
+          __syncthreads();
+          count = newCount;
+        }
+      }
+      if (count == 0) continue;
+      // ---- Pairs(now): getNack of every entry, in parallel
+      bool rem[2], snd[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const u32 idx = lane + 64u * u32(h);
+        rem[h] = snd[h] = false;
+        if (idx < count) {
+          const u32 t = sTries[idx];
+          rem[h] = t >= kNackMaxTries;
+          const i64 rq = t == 0 ? req0 : t == 1 ? req1 : t == 2 ? req2 : t == 3 ? req3 : req4;
+          snd[h] = !rem[h] && now - sLast[idx] >= rq;
+        }
+      }
+      const u64 r0 = __ballot(rem[0]), r1 = __ballot(rem[1]);
+      const u64 s0m = __ballot(snd[0]), s1m = __ballot(snd[1]);
+      if (!(r0 | r1 | s0m | s1m)) continue;
+      const u32 base16 = u32(u16(sSn[0] - 17u));  // set far back to open the first pair
+      // purge list (queue order), before any entry moves
+      const u32 nr0 = u32(__popcll(r0));
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const u64 mm = h ? r1 : r0;
+        if (rem[h]) sPurge[(h ? nr0 : 0u) + u32(__popcll(mm & ((1ull << lane) - 1)))] = sSn[lane + 64u * u32(h)];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        if (snd[h]) {
+          const u32 idx = lane + 64u * u32(h);
+          sTries[idx] = sTries[idx] + 1;
+          sLast[idx] = now;
+        }
+      __syncthreads();
+      const u32 numNacked = u32(__popcll(s0m) + __popcll(s1m));
+      u32 np = 0;
+      if (lane == 0 && numNacked) {  // pair packing (NackQueue.Pairs), in queue order
+        u32 baseSN = base16;
+        bool active = false;
+        lkf_nack_pair cur = {0, 0};
+        for (int h = 0; h < 2; h++)
+          for (u64 mm = h ? s1m : s0m; mm; mm &= mm - 1) {
+            const u32 sn16 = sSn[u32(__ffsll((long long)mm) - 1) + 64u * u32(h)];
+            const u32 d = u32(u16(sn16 - baseSN));
+            if (d > 16) {
+              if (active) sPairs[np++] = cur;
+              baseSN = sn16;
+              cur.packet_id = u16(sn16);
+              cur.lost_packets = 0;
+              active = true;
+            } else {
+              const u32 sh = u32(u16(d - 1));
+              if (sh < 16) cur.lost_packets = u16(cur.lost_packets | (1u << sh));
+            }
+          }
+        if (active) sPairs[np++] = cur;
+        u32 off = 0;
+        if (np) {
+          off = atomicAdd(pairCnt, np);
+          if (off + np > pairCap) {
+            atomicOr(err, 8u);  // pair buffer capacity: the RTCP NACK is not recorded
+            np = 0;
+          } else {
+            for (u32 i = 0; i < np; i++) pairs[off + i] = sPairs[i];
+          }
+        }
+        if (np) {
+          info[icx] = np | (numNacked << 16);
+          pairOff[icx] = off;
+        }
+      }
+      if (numNacked && __builtin_amdgcn_readfirstlane(np)) nacked += numNacked;  // UpdateNack only with a packet
+      // purge (NackQueue.Remove of every entry at MaxTries, in order)
+      const u32 nPurge = nr0 + u32(__popcll(r1));
+      for (u32 i = 0; i < nPurge; i++) removeSn(sPurge[i]);
+    }
+  }
+  for (u32 i = lane; i < u32(kNackSlots); i += 64) {
+    g->last[i] = sLast[i];
+    g->sn[i] = u16(sSn[i]);
+    g->tries[i] = u8(sTries[i]);
+  }
+  if (lane == 0) {
+    g->count = count;
+    if (nacked) hot[sid].nacks += nacked;
+  }
+}
+
+// lkf_ingest_nacks: records at their compacted positions, pairs gathered in
+// record order
+__global__ void k_nack_compact(u32 n, const lkf_raw_pkt *__restrict__ raws, const DevStream *__restrict__ streams,
+                               const u32 *__restrict__ info, const u32 *__restrict__ pairOff,
+                               const lkf_nack_pair *__restrict__ pairs, const u64 *__restrict__ recPos,
+                               const u64 *__restrict__ pairPos, lkf_rtcp_nack *__restrict__ outRecs,
+                               lkf_nack_pair *__restrict__ outPairs) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !info[i]) return;
+  const u32 np = info[i] & 0xffffu;
+  lkf_rtcp_nack r = {};
+  r.datagram = i;
+  r.stream = raws[i].stream;
+  r.media_ssrc = streams[r.stream].ssrc;
+  r.pair_off = u32(pairPos[i]);
+  r.n_pairs = u16(np);
+  r.num_nacked = u16(info[i] >> 16);
+  outRecs[recPos[i]] = r;
+  for (u32 k = 0; k < np; k++) outPairs[pairPos[i] + k] = pairs[pairOff[i] + k];
+}
+
+// ---------------------------------------------------------------------------
 // k_ing_out: the ExtPacket of every forwarded datagram at its batch position
 // ---------------------------------------------------------------------------
 __global__ void k_ing_out(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
@@ -1398,11 +1662,28 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
     hipLaunchKernelGGL(k_ing_stream_wave, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams, a.hot,
                        a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs, a.ingDD,
                        a.err, a.list, a.listCnt, a.listStride);
+  if (a.nack && a.nstreams)  // after the flows: the loss ranges it pushes
+    hipLaunchKernelGGL(k_ing_nack, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.flows, a.streams, a.nack,
+                       a.hot, a.tBegin, a.tEnd, a.list, a.listCnt, a.listStride, a.nackInfo, a.nackPairOff,
+                       a.nackPairCnt, a.nackPairs, a.nackPairCap, a.err);
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
   if (r != hipSuccess) return r;
   hipLaunchKernelGGL(k_ing_out, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.parsed, a.streams, a.fwd, a.pos,
                      a.n, a.flows, a.out, a.ingDD, a.outDD);
+  return hipGetLastError();
+}
+
+hipError_t launch_nack_compact(hipStream_t st, u32 n, const lkf_raw_pkt *raws, const DevStream *streams,
+                               const u32 *info, const u32 *pairOff, const lkf_nack_pair *pairs, u64 *partA,
+                               u64 *partB, u64 *recPos, u64 *pairPos, u64 *totals, lkf_rtcp_nack *outRecs,
+                               lkf_nack_pair *outPairs) {
+  if (n == 0) return hipSuccess;
+  hipError_t r = launch_scan(st, 3, nullptr, nullptr, nullptr, info, nullptr, n, partA, partB, recPos, pairPos,
+                             totals, totals + 1, nullptr);
+  if (r != hipSuccess) return r;
+  hipLaunchKernelGGL(k_nack_compact, dim3(nblk(n, 256)), dim3(256), 0, st, n, raws, streams, info, pairOff, pairs,
+                     recPos, pairPos, outRecs, outPairs);
   return hipGetLastError();
 }
 

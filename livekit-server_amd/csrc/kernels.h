@@ -45,6 +45,8 @@ struct DecideLaunch {
   uint8_t *ddArena;
   uint64_t *ddUsed;
   uint64_t ddCap;
+  // capacities (tested in -DLKF_CHECKED=1 builds)
+  uint32_t maxDts, maxTracks, npkts, nev;
 };
 
 struct EmitLaunch {
@@ -62,7 +64,12 @@ struct EmitLaunch {
   uint32_t *err;
   uint32_t grid;
   const uint8_t *ddArena;  // non-null: batches with DD tracks (k_emit<PRE_MAX_DD>)
+  // capacities (tested in -DLKF_CHECKED=1 builds)
+  uint32_t maxDts, npkts;
+  uint64_t tupleCap, arenaLen, ddCap, gCap;
 };
+// -DLKF_CHECKED=1 builds: {violations, first site, its index, its capacity}
+hipError_t read_check(unsigned long long out[4], int reset);
 
 // diagnostic builds (-DLKF_DIAG=1): k_decide_dt per-wave counters
 hipError_t read_diag(unsigned long long out[32], int reset);
@@ -101,7 +108,19 @@ struct IngestLaunch {
   uint32_t listStride;
   const uint32_t *lanePerm;  // k_ing_stream lane -> stream (nullptr: identity)
   bool laneStreams;          // the lane-per-stream k_ing_stream (LKF_ING_LANE=1) instead of k_ing_stream_wave
+  // NACK queues (nullptr: no stream has one): per stream state, per datagram
+  // result (n_pairs | num_nacked << 16, 0: no RTCP NACK) and pair offset in
+  // the bump-allocated pair buffer
+  NackState *nack;
+  uint32_t *nackInfo, *nackPairOff, *nackPairCnt;
+  lkf_nack_pair *nackPairs;
+  uint32_t nackPairCap;
 };
+// lkf_ingest_nacks: the last ingest's RTCP NACKs compacted in datagram order
+hipError_t launch_nack_compact(hipStream_t s, uint32_t n, const lkf_raw_pkt *raws, const DevStream *streams,
+                               const uint32_t *info, const uint32_t *pairOff, const lkf_nack_pair *pairs,
+                               uint64_t *partA, uint64_t *partB, uint64_t *recPos, uint64_t *pairPos, uint64_t *totals,
+                               lkf_rtcp_nack *outRecs, lkf_nack_pair *outPairs);
 
 struct SpeakersLaunch {
   uint32_t nrooms;

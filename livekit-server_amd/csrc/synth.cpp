@@ -656,6 +656,11 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       sp.ssrc = tg[ti].ssrc[l];
       sp.audio_level_ext = tg[ti].p.kind == LKF_KIND_AUDIO ? 1 : 0;
       sp.dd_ext = tg[ti].dd ? 8 : 0;
+      // publishers negotiate NACK feedback for Opus and every video codec
+      // (pkg/rtc/config.go:92-101): each Buffer gets a NackQueue; RTTs vary
+      // (a quarter keep the queue's default)
+      sp.nack = 1;
+      sp.rtt_ms = (ti % 4 == 0) ? 0u : u32(20 + (ti * 37 + u32(l) * 11) % 130);
       tr->streams.push_back(sp);
     }
   }

@@ -328,6 +328,7 @@ KAT(wraparound_uint32) {
 #include "kat_srtp.inc"
 #include "kat_red.inc"
 #include "kat_tracker.inc"
+#include "kat_nack.inc"
 
 int main(int argc, char **argv) {
   bool list = false;

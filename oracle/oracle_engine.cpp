@@ -27,6 +27,7 @@
 #include "srtp_oracle.h"
 #include "red_oracle.h"
 #include "tracker_oracle.h"
+#include "nack_oracle.h"
 #include <map>
 
 using namespace orc;
@@ -83,6 +84,8 @@ struct OStream {
   std::unique_ptr<DependencyDescriptorParser> ddParser;  // when the DD extension is negotiated (buffer.go:193-201)
   bool latestTSForAudioLevelInitialized = false;
   u32 latestTSForAudioLevel = 0;
+  std::unique_ptr<NackQueue> nacker;  // codecs with NACK feedback (buffer.go:248-256)
+  u64 nacks = 0;                      // rtpStats.nacks (UpdateNack, rtpstats_base.go:315-324)
 };
 
 }  // namespace
@@ -98,6 +101,8 @@ struct orc_engine {
   // ingress
   std::vector<std::unique_ptr<OStream>> streams;
   std::vector<lkf_flow> flows;
+  std::vector<lkf_rtcp_nack> nackRecs;  // the last ingest's RTCP NACKs
+  std::vector<lkf_nack_pair> nackPairs;
   std::vector<lkf_pkt> ingested;
   std::vector<lkf_pkt_dd> ingestedDD;
   // lkf_pkt_dd side array of the next orc_run (orc_submit_dd)
@@ -1126,6 +1131,10 @@ int32_t orc_add_stream(orc_engine *e, const lkf_stream_params *p) {
     s->level = std::make_unique<AudioLevel>(ap);
   }
   if (p->dd_ext) s->ddParser = std::make_unique<DependencyDescriptorParser>();
+  if (p->nack) {  // nack.NewNACKQueue(nack.NackQueueParamsDefault), then Buffer.SetRTT
+    s->nacker = std::make_unique<NackQueue>();
+    if (p->rtt_ms) s->nacker->SetRTT(p->rtt_ms);
+  }
   e->streams.push_back(std::move(s));
   return int32_t(e->streams.size() - 1);
 }
@@ -1163,6 +1172,11 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
     }
   }
   RTPFlowState fs = b.stats.Update(h.sn, h.ts, h.marker, h.hdrSize, h.payloadLen, h.paddingSize);
+  if (b.nacker) {  // updateStreamState buffer.go:556-564
+    b.nacker->Remove(h.sn);
+    if (fs.HasLoss)
+      for (u64 lost = fs.LossStartInclusive; lost != fs.LossEndExclusive; lost++) b.nacker->Push(u16(lost), rp.arrival_ns);
+  }
   f.ext_sn = fs.ExtSequenceNumber;
   f.ext_ts = fs.ExtTimestamp;
   if (fs.HasLoss) {  // nacker.Push(lost) for lost in [start, end) (buffer.go:557-562)
@@ -1291,6 +1305,8 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
 int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len) {
   (void)raw_len;
   e->flows.assign(n, lkf_flow{});
+  e->nackRecs.clear();
+  e->nackPairs.clear();
   e->ingested.clear();
   e->ingestedDD.clear();
   for (u32 i = 0; i < n; i++) {
@@ -1298,7 +1314,24 @@ int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
     lkf_pkt ep;
     lkf_pkt_dd epd;
     bool fwd = false;
-    e->flows[i] = calc(e, *e->streams[pkts[i].stream], pkts[i], raw, ep, epd, fwd);
+    OStream &b = *e->streams[pkts[i].stream];
+    e->flows[i] = calc(e, b, pkts[i], raw, ep, epd, fwd);
+    if (b.nacker) {  // calc's deferred doNACKs (buffer.go:417-421, :673-710), now = the arrival time
+      int nn = 0;
+      const auto pairs = b.nacker->Pairs(pkts[i].arrival_ns, nn);
+      if (!pairs.empty()) {
+        lkf_rtcp_nack r{};
+        r.datagram = i;
+        r.stream = pkts[i].stream;
+        r.media_ssrc = b.p.ssrc;
+        r.pair_off = u32(e->nackPairs.size());
+        r.n_pairs = u16(pairs.size());
+        r.num_nacked = u16(nn);
+        e->nackRecs.push_back(r);
+        for (const auto &q : pairs) e->nackPairs.push_back(lkf_nack_pair{q.PacketID, q.LostPackets});
+        b.nacks += u64(nn);
+      }
+    }
     if (fwd) {
       e->flows[i].pkt = u32(e->ingested.size());
       e->ingested.push_back(ep);
@@ -1353,6 +1386,24 @@ int orc_stream_stats_get(orc_engine *e, int32_t s, lkf_stream_stats *o) {
   o->bytes_duplicate = r.bytesDuplicate;
   o->bytes_padding = r.bytesPadding;
   o->frames = r.frames;
+  o->nacks = e->streams[s]->nacks;
+  return LKF_OK;
+}
+
+int orc_ingest_nacks(orc_engine *e, lkf_rtcp_nack *out, uint32_t cap, lkf_nack_pair *pairs, uint32_t pair_cap,
+                     uint32_t *n_out, uint32_t *n_pairs_out) {
+  *n_out = u32(e->nackRecs.size());
+  *n_pairs_out = u32(e->nackPairs.size());
+  if (cap < e->nackRecs.size() || pair_cap < e->nackPairs.size()) return LKF_ENOSPC;
+  if (!e->nackRecs.empty()) std::memcpy(out, e->nackRecs.data(), e->nackRecs.size() * sizeof(lkf_rtcp_nack));
+  if (!e->nackPairs.empty()) std::memcpy(pairs, e->nackPairs.data(), e->nackPairs.size() * sizeof(lkf_nack_pair));
+  return LKF_OK;
+}
+
+int orc_stream_set_rtt(orc_engine *e, int32_t s, uint32_t rtt_ms) {  // Buffer.SetRTT buffer.go:400-414
+  if (s < 0 || s >= int32_t(e->streams.size())) return LKF_EINVAL;
+  if (rtt_ms == 0) return LKF_OK;
+  if (e->streams[s]->nacker) e->streams[s]->nacker->SetRTT(rtt_ms);
   return LKF_OK;
 }
 

@@ -40,3 +40,19 @@ def abi(pkg):
 def oracle():
     from tests import oracle_lib
     return oracle_lib.load()
+
+
+@pytest.fixture(autouse=True)
+def _bounds_checked(request):
+    """With LKF_LIB=liblkfwd_checked.so every GPU test ends with the checked
+    kernels' violation record read and required empty (site, index and
+    capacity of the first out-of-bounds index otherwise)."""
+    checked = "checked" in os.environ.get("LKF_LIB", "") and request.node.get_closest_marker("gpu")
+    if checked:
+        p = importlib.import_module("livekit-server_amd")
+        p.debug_check(reset=True)
+    yield
+    if checked:
+        rec = p.debug_check(reset=True)
+        assert rec is not None, "LKF_LIB is not a checked build"
+        assert rec[0] == 0, "out-of-bounds index: %d violations, first at site %d index %d capacity %d" % rec

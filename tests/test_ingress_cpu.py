@@ -121,3 +121,32 @@ def test_oracle_speakers_ranked_and_quantised(pkg, workload, abi):
     finally:
         o.destroy(h)
         tr.close()
+
+
+def test_oracle_nack_rtcp_consistent(pkg, workload, oracle):
+    """The oracle's RTCP NACKs (NackQueue.Pairs per datagram): one per datagram
+    at most, in datagram order, pairs in range, and the streams' UpdateNack
+    totals equal the NACKed sequence numbers of the packets sent."""
+    o = oracle
+    oh = o.create(500)
+    tr = workload.Trace(2, duration_s=2.0, batch_s=0.1, rooms=4, loss=0.08, reorder=0.03, seed=9)
+    try:
+        workload.load_topology(o.api, oh, tr)
+        workload.load_streams(o.api, oh, tr)
+        nacked = 0
+        pkts = 0
+        for b in range(tr.nbatches):
+            rp, n, ar, alen = tr.batch_raw(b)
+            assert o.api["ingest"](oh, rp, n, ar, alen) == 0
+            r, p = pkg.nacks_arrays(o.api, oh)
+            if len(r):
+                assert (np.diff(r["datagram"].astype(np.int64)) > 0).all()
+                assert (r["n_pairs"] > 0).all() and (r["num_nacked"] > 0).all()
+                assert r["pair_off"][-1] + r["n_pairs"][-1] == len(p)
+            nacked += int(r["num_nacked"].sum())
+            pkts += len(r)
+        assert pkts > 50
+        stats = sum(pkg.stream_stats(o.api, oh, s)[13] for s in range(tr.nstreams))
+        assert stats == nacked
+    finally:
+        o.destroy(oh)

@@ -37,7 +37,26 @@ def _ingested_dd(api, h, abi):
     return buf.raw[: sz * n.value]
 
 
-def run_ingress_parity(pkg, workload, abi, trace, speakers=True):
+def check_nacks(pkg, eng, o, oh, b):
+    """The batch's RTCP NACKs (Buffer.doNACKs per datagram) must be identical."""
+    gr, gp = pkg.nacks_arrays(eng.api, eng.h)
+    orr, op = pkg.nacks_arrays(o.api, oh)
+    assert len(gr) == len(orr), (b, len(gr), len(orr))
+    for f in abi_fields(gr):
+        if not np.array_equal(gr[f], orr[f]):
+            bad = np.nonzero(gr[f] != orr[f])[0][:5]
+            raise AssertionError("batch %d NACK field %s differs at %s: gpu %s orc %s" % (b, f, bad, gr[bad], orr[bad]))
+    assert np.array_equal(gp, op), b
+    return len(gr), int(gr["num_nacked"].sum()) if len(gr) else 0
+
+
+def abi_fields(a):
+    return [f for f in a.dtype.names if f != "reserved"]
+
+
+def run_ingress_parity(pkg, workload, abi, trace, speakers=True, rtt_changes=None):
+    """rtt_changes: {batch: [(stream, rtt_ms), ...]} applied (Buffer.SetRTT)
+    before that batch's ingest on both sides."""
     o = load_oracle()
     eng = pkg.Engine.for_trace(trace)
     oh = o.create(500)
@@ -46,12 +65,17 @@ def run_ingress_parity(pkg, workload, abi, trace, speakers=True):
             workload.load_topology(api, h, trace)
             workload.load_streams(api, h, trace)
         total_fwd = 0
+        nack_pkts = 0
         for b in range(trace.nbatches):
+            for sid, rtt in (rtt_changes or {}).get(b, []):
+                assert eng.api["stream_set_rtt"](eng.h, sid, rtt) == 0
+                assert o.api["stream_set_rtt"](oh, sid, rtt) == 0
             workload.queue_events(eng.api, eng.h, trace, b)
             workload.queue_events(o.api, oh, trace, b)
             rp, n, ar, alen = trace.batch_raw(b)
             eng.ingest(rp, n, ar, alen)
             assert o.api["ingest"](oh, rp, n, ar, alen) == 0
+            nack_pkts += check_nacks(pkg, eng, o, oh, b)[0]
             gf = eng.flows()
             of = pkg.flows_array(o.api, oh)
             assert len(gf) == len(of) == n
@@ -99,6 +123,7 @@ def run_ingress_parity(pkg, workload, abi, trace, speakers=True):
                     assert np.array_equal(gsp[f], osp[f]), (b, f, gsp, osp)
         for s in range(trace.nstreams):
             assert eng.stream_stats(s) == pkg.stream_stats(o.api, oh, s), s
+        run_ingress_parity.nack_pkts = nack_pkts
         return total_fwd
     finally:
         eng.close()
@@ -146,3 +171,24 @@ def test_ingress_config3_speakers(pkg, workload, abi):
     """configs[2] shape: 50-participant audio-heavy rooms, speaker ranking every batch (400 ms)."""
     tr = workload.Trace(3, duration_s=4.0, batch_s=0.4, rooms=2)
     assert run_ingress_parity(pkg, workload, abi, tr) > 0
+
+
+def test_ingress_nack_config2_full(pkg, workload, abi):
+    """configs[1] at its benched size (100 rooms x 10 participants, 2 % loss,
+    1 % reorder) through 100-ms ingest ticks: every Buffer's NackQueue
+    (Remove on arrival, Push of loss ranges, Pairs with the RTT backoff and
+    five tries) on the GPU, the RTCP NACK of every datagram and its pairs
+    identical to the oracle's; RTTs change mid-trace (Buffer.SetRTT)."""
+    tr = workload.Trace(2, duration_s=2.0, batch_s=0.1, rooms=100)
+    rtt = {5: [(s, 20 + (7 * s) % 200) for s in range(0, tr.nstreams, 3)],
+           12: [(s, 0) for s in range(0, tr.nstreams, 5)] + [(1, 400)]}
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False, rtt_changes=rtt) > 0
+    assert run_ingress_parity.nack_pkts > 1000
+
+
+def test_ingress_nack_heavy_loss(pkg, workload, abi):
+    """Loss bursts and deep reordering: queues at CacheSize, purges after the
+    fifth try, removals of NACKed SNs that arrive late."""
+    tr = workload.Trace(2, duration_s=3.0, batch_s=0.05, rooms=4, loss=0.25, reorder=0.1, seed=77)
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
+    assert run_ingress_parity.nack_pkts > 100
