@@ -99,9 +99,12 @@ def kernel_sources_sha():
     the build it was measured on."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("forward_kernels.hip", "ingress_kernels.hip", "engine.cpp", "fwd_state.h", "synth.cpp"):
-        p = os.path.join(ROOT, "livekit-server_amd", "csrc", f)
+    csrc = os.path.join(ROOT, "livekit-server_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")) or f == "Makefile")
+    for f in files + ["../../include/lkfwd.h"]:  # every file compiled into liblkfwd.so / the workload
+        p = os.path.join(csrc, f)
         if os.path.exists(p):
+            h.update(f.encode())
             h.update(open(p, "rb").read())
     return h.hexdigest()[:16]
 

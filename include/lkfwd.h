@@ -712,6 +712,15 @@ int lkf_ingest_nacks(lkf_engine *e, lkf_rtcp_nack *out, uint32_t cap, lkf_nack_p
 /* Buffer.SetRTT (buffer.go:400-414): the NackQueue RTT of a stream from the
  * next ingest on (0 is ignored, as in the reference). */
 int lkf_stream_set_rtt(lkf_engine *e, int32_t stream, uint32_t rtt_ms);
+/* Removes a published track: WebRTCReceiver.closeTracks (receiver.go:700-716)
+ * closes its DownTracks (as lkf_remove_downtrack each) and the Buffers of its
+ * streams (Buffer.Close buffer.go:337-352: Write then returns io.EOF, so a
+ * datagram of a closed stream is not processed — its flow is
+ * LKF_FLOW_NOT_HANDLED and no state changes), and it leaves the speaker
+ * ranking (UpTrackManager.RemovePublishedTrack uptrackmanager.go:272).
+ * Handles are not reused; the track's packets in later ExtPacket batches
+ * reach no DownTrack. */
+int lkf_remove_track(lkf_engine *e, int32_t track);
 /* Room.GetActiveSpeakers (room.go:254-279) for every room at virtual time
  * now_ns: per participant the loudest active microphone track
  * (UpTrackManager.GetAudioLevel uptrackmanager.go:422-436, AudioLevel.GetLevel

@@ -200,10 +200,11 @@ class Engine:
             raise EngineError("lkf_create failed on HIP device %d (no GPU or out of memory)" % device)
 
     @classmethod
-    def for_trace(cls, trace, device=0, headroom=1.25, **kw):
-        """Engine sized for a synthetic `workload.Trace`."""
+    def for_trace(cls, trace, device=0, headroom=1.25, extra_dts=0, **kw):
+        """Engine sized for a synthetic `workload.Trace` (extra_dts: DownTracks
+        added beyond the trace's, e.g. re-subscriptions)."""
         mp = int(trace.max_batch_pkts * headroom) + 64
-        return cls(device=device, max_tracks=trace.ntracks + 8, max_downtracks=trace.ndts + 8,
+        return cls(device=device, max_tracks=trace.ntracks + 8, max_downtracks=trace.ndts + 8 + extra_dts,
                    max_batch_pkts=mp, max_batch_arena=int(trace.max_batch_arena * headroom) + 4096,
                    max_batch_tuples=int(trace.max_batch_tuples * headroom) + 1024,
                    max_out_pkts=int(trace.max_batch_tuples * headroom) + 1024,

@@ -224,6 +224,10 @@ class lkf_out(C.Structure):
 
 
 LKF_DROP_NREASONS = 11
+LKF_KIND_AUDIO, LKF_KIND_VIDEO = 0, 1  # enum lkf_kind
+LKF_CTL_MUTE, LKF_CTL_PUBMUTE, LKF_CTL_SET_MAX_SPATIAL, LKF_CTL_SET_MAX_TEMPORAL = 1, 2, 3, 4
+LKF_CTL_SET_MAX_SEEN_SPATIAL, LKF_CTL_SET_MAX_SEEN_TEMPORAL, LKF_CTL_SET_ALLOCATION = 5, 6, 7
+LKF_CTL_RESYNC, LKF_CTL_SET_TARGET, LKF_CTL_PLAYOUT_ACKED = 8, 9, 10
 
 
 class lkf_stats(C.Structure):
@@ -360,6 +364,7 @@ def bind_engine_api(lib, prefix):
     api["add_track"] = _bind(lib, prefix + "add_track", C.c_int32, [e, P(lkf_track_params)])
     api["add_downtrack"] = _bind(lib, prefix + "add_downtrack", C.c_int32, [e, P(lkf_downtrack_params)])
     api["remove_downtrack"] = _bind(lib, prefix + "remove_downtrack", C.c_int, [e, C.c_int32])
+    api["remove_track"] = _bind(lib, prefix + "remove_track", C.c_int, [e, C.c_int32])
     api["set_layer_offsets"] = _bind(lib, prefix + "set_layer_offsets", C.c_int, [e, C.c_int32, P(C.c_uint32)])
     api["ctl"] = _bind(lib, prefix + "ctl", C.c_int,
                        [e, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_uint32])

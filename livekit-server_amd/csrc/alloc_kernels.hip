@@ -294,6 +294,10 @@ __global__ void k_pause(const lkf_alloc_req *__restrict__ reqs, u32 n, DTHot *ho
   const lkf_alloc_req q = reqs[i];
   const u32 d = u32(q.dt);
   DTHot h = hot[d];
+  if (!(h.flags & F_VIDEO)) {  // audio: lastAllocation, no state change (as AllocateOptimal; the
+    out[i] = last_allocation(last, d, h);  // reference's Pause needs the video layer selector)
+    return;
+  }
   const int64_t(*brs)[4] = q.bitrates;
   const bool muted = h.flags & F_MUTED, pubMuted = h.flags & F_PUBMUTED;
   const Layer max{h.maxS, h.maxT}, seen{h.seenS, h.seenT}, target{h.tgtS, h.tgtT};

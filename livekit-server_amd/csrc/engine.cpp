@@ -106,6 +106,7 @@ struct lkf_engine {
   // topology (host mirror)
   std::vector<lkf_track_params> tracks;
   std::vector<uint32_t> trackDD;  // per track: DD table index or 0xffffffff
+  std::vector<uint8_t> trackActive;  // 0 after lkf_remove_track
   std::vector<lkf_downtrack_params> dtp;
   std::vector<uint8_t> active;
   // the DownTrack's sequencer may hold padding exclusions (lkf_padding sent
@@ -776,6 +777,7 @@ int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p) {
   uint32_t ddIdx = 0xffffffffu;
   if (track_has_dd(*p)) ddIdx = e->nDDTracks++;
   e->trackDD.push_back(ddIdx);
+  e->trackActive.push_back(1);
   e->pendTracks.push_back(to_dev_track(*p, ddIdx));  // uploaded by flush_topology
   e->schedDirty = true;
   return h;
@@ -831,6 +833,32 @@ int lkf_remove_downtrack(lkf_engine *e, int32_t dt) {
                    hipMemcpyHostToDevice),
          "remove copy");
   e->schedDirty = true;
+  return upload_done(e);
+}
+
+int lkf_remove_track(lkf_engine *e, int32_t track) {
+  if (!e || track < 0 || track >= int32_t(e->tracks.size())) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  if (!e->trackActive[track]) return LKF_OK;
+  e->trackActive[track] = 0;
+  const uint8_t zero = 0, one = 1;
+  for (size_t d = 0; d < e->dtp.size(); d++)  // closeTracks: every DownTrack of the receiver
+    if (e->dtp[d].track == track && e->active[d]) {
+      e->active[d] = 0;
+      HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(e->dDTs + d) + offsetof(DevDT, active), &zero, 1,
+                       hipMemcpyHostToDevice),
+             "remove copy");
+    }
+  for (size_t sid = 0; sid < e->streams.size(); sid++)  // Buffer.Close of its streams
+    if (e->streams[sid].track == track)
+      HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(e->dStreams + sid) + offsetof(DevStream, closed), &one, 1,
+                       hipMemcpyHostToDevice),
+             "close copy");
+  e->schedDirty = true;
+  e->spkDirty = true;
   return upload_done(e);
 }
 
@@ -2191,6 +2219,10 @@ static int alloc_common(lkf_engine *e, int mode, const lkf_alloc_req *reqs, cons
   for (uint32_t i = 0; i < n; i++) {
     const int32_t dt = reqs[i].dt;
     if (dt < 0 || dt >= int32_t(e->dtp.size()) || seen[dt]) return LKF_EINVAL;
+    if (!e->active[dt]) {  // a removed DownTrack has no allocation (its state stays as it was)
+      e->err = "allocation request for a removed DownTrack";
+      return LKF_EINVAL;
+    }
     seen[dt] = 1;
   }
   int rc = flush_topology(e);
@@ -2532,7 +2564,7 @@ static int rebuild_speakers(lkf_engine *e) {
   std::vector<std::pair<std::pair<uint32_t, uint32_t>, uint32_t>> rows;
   for (size_t t = 0; t < e->tracks.size(); t++) {
     const auto &tp = e->tracks[t];
-    if (!tp.is_mic || primary[t] < 0 || !e->streams[primary[t]].audio_level_ext) continue;
+    if (!tp.is_mic || !e->trackActive[t] || primary[t] < 0 || !e->streams[primary[t]].audio_level_ext) continue;
     rows.push_back({{tp.room, tp.publisher}, uint32_t(primary[t])});
   }
   std::stable_sort(rows.begin(), rows.end(),

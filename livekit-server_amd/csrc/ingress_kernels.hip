@@ -938,6 +938,26 @@ __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring
   if (ingDD) ingDD[ic] = dv;
 }
 
+// The datagrams of a closed stream (lkf_remove_track): not handled, no state
+// change, no ExtPacket (lanes first, first + step, ...)
+__device__ void closed_flows(const DevStream &s, u32 sid, u32 pb, u32 pe, const lkf_raw_pkt *raws, lkf_flow *flows,
+                             u32 *fwd, IngDD *ingDD, const u32 *list, const u32 *cnt, u32 stride, u32 first,
+                             u32 step) {
+  const bool useList = s.layer < 3;
+  const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
+  const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
+  for (u32 k = first; k < nIdx; k += step) {
+    const u32 ic = useList ? lst[k] : pb + k;
+    if (raws[ic].stream != sid) continue;
+    lkf_flow f = {};
+    f.pkt = 0xffffffffu;
+    f.flags = LKF_FLOW_NOT_HANDLED;
+    flows[ic] = f;
+    fwd[ic] = 0;
+    if (ingDD) ingDD[ic] = IngDD{};
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_ing_stream: one lane per stream, serial over the stream's datagrams.
 // ---------------------------------------------------------------------------
@@ -960,6 +980,10 @@ __global__ void __launch_bounds__(64) k_ing_stream(const lkf_raw_pkt *__restrict
   const DevStream s = streams[sid];
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;
+  if (s.closed) {  // Buffer.Close: Write returns io.EOF, nothing is processed
+    closed_flows(s, sid, pb, pe, raws, flows, fwd, ingDD, list, cnt, stride, 0, 1);
+    return;
+  }
 #if LKF_ING_HOT_LDS
   StreamHot &h = sHot[threadIdx.x];
   h = hot[sid];
@@ -1041,6 +1065,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   const DevStream s = streams[sid];
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;
+  if (s.closed) {  // Buffer.Close: Write returns io.EOF, nothing is processed
+    closed_flows(s, sid, pb, pe, raws, flows, fwd, ingDD, list, cnt, stride, lane, 64);
+    return;
+  }
   u64 *const hg = hist + size_t(sid) * kHistWords;
   sHist[lane] = hg[lane];
   reinterpret_cast<u32 *>(&sh)[lane] = reinterpret_cast<const u32 *>(hot + sid)[lane];
@@ -1184,7 +1212,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   __shared__ lkf_nack_pair sPairs[kNackCap];
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
-  if (!s.nack) return;
+  if (!s.nack || s.closed) return;
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;  // no datagram of its track: no calc, no doNACKs
   NackState *const g = states + sid;

@@ -1781,6 +1781,10 @@ struct Forwarder {
   }
   // Pause forwarder.go:1308-1351
   VideoAllocation Pause(const std::vector<i32> &availableLayers, const Bitrates &brs) {
+    // the reference dereferences f.vls (nil for audio): the stream allocator
+    // pauses only video; an audio request answers lastAllocation unchanged,
+    // as AllocateOptimal does (:598-600)
+    if (kind == KindAudio) return LastAllocation();
     const VideoLayer maxLayer = vls.GetMax(), maxSeenLayer = vls.GetMaxSeen();
     const i64 optimal = getOptimalBandwidthNeeded(muted, pubMuted, maxSeenLayer.Spatial, brs, maxLayer);
     VideoAllocation a;

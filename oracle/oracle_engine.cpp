@@ -36,6 +36,7 @@ namespace {
 
 struct OTrack {
   lkf_track_params p;
+  bool removed = false;  // orc_remove_track
   // the structure the DD extension bytes of this track's ExtPackets are read
   // with (the Go parser's r.structure at ingress; replaced by every packet
   // that attaches one) and its decode targets (ProcessFrameDependencyStructure)
@@ -85,6 +86,7 @@ struct OStream {
   bool latestTSForAudioLevelInitialized = false;
   u32 latestTSForAudioLevel = 0;
   std::unique_ptr<NackQueue> nacker;  // codecs with NACK feedback (buffer.go:248-256)
+  bool closed = false;                // Buffer.Close (buffer.go:337-352)
   u64 nacks = 0;                      // rtpStats.nacks (UpdateNack, rtpstats_base.go:315-324)
 };
 
@@ -364,6 +366,18 @@ int32_t orc_add_downtrack(orc_engine *e, const lkf_downtrack_params *p) {
 int orc_remove_downtrack(orc_engine *e, int32_t dt) {
   if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
   e->dts[dt]->active = false;
+  return LKF_OK;
+}
+
+// WebRTCReceiver.closeTracks (receiver.go:700-716): the DownTracks close, the
+// Buffers close (Write -> io.EOF), the track leaves the speaker ranking
+int orc_remove_track(orc_engine *e, int32_t track) {
+  if (track < 0 || track >= (int)e->tracks.size()) return LKF_EINVAL;
+  e->tracks[track].removed = true;
+  for (auto &d : e->dts)
+    if (d->p.track == track) d->active = false;
+  for (auto &s : e->streams)
+    if (s->p.track == track) s->closed = true;
   return LKF_OK;
 }
 
@@ -1006,6 +1020,7 @@ static int allocCommon(orc_engine *e, int mode, const lkf_alloc_req *reqs, const
   std::vector<u8> seen(e->dts.size(), 0);
   for (uint32_t i = 0; i < n; i++) {
     if (reqs[i].dt < 0 || reqs[i].dt >= (int)e->dts.size() || seen[reqs[i].dt]) return LKF_EINVAL;
+    if (!e->dts[reqs[i].dt]->active) return LKF_EINVAL;  // a removed DownTrack has no allocation
     seen[reqs[i].dt] = 1;
   }
   for (uint32_t i = 0; i < n; i++) {
@@ -1315,6 +1330,11 @@ int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
     lkf_pkt_dd epd;
     bool fwd = false;
     OStream &b = *e->streams[pkts[i].stream];
+    if (b.closed) {  // Buffer.Write returns io.EOF: no calc, no doNACKs
+      e->flows[i].pkt = 0xffffffffu;
+      e->flows[i].flags = LKF_FLOW_NOT_HANDLED;
+      continue;
+    }
     e->flows[i] = calc(e, b, pkts[i], raw, ep, epd, fwd);
     if (b.nacker) {  // calc's deferred doNACKs (buffer.go:417-421, :673-710), now = the arrival time
       int nn = 0;
@@ -1432,7 +1452,7 @@ int orc_speakers(orc_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
   for (size_t t = 0; t < e->tracks.size(); t++) {
     const lkf_track_params &tp = e->tracks[t].p;
     size_t k = find(tp.room, tp.publisher);
-    if (!tp.is_mic || primary[t] < 0) continue;
+    if (!tp.is_mic || e->tracks[t].removed || primary[t] < 0) continue;
     OStream &s = *e->streams[primary[t]];
     if (!s.level) continue;
     auto lv = s.level->GetLevel(now_ns);

@@ -106,7 +106,7 @@ def _sha(*arrays):
 def run_control_case(api, h, trace, workload, drain_fn, run_fn, abi, name="control_config2"):
     """Drives `trace` with control calls between its batches; returns the fixture dict."""
     from tests import pad_lib, red_lib, rtx_lib, tracker_lib
-    from tests.test_alloc_gpu import make_alloc_reqs, stream_allocator_steps, run_step
+    from tests.test_alloc_gpu import make_alloc_reqs, run_step, stream_allocator_steps, video_mask
     ext = name.endswith("_alloc")
     workload.load_topology(api, h, trace)
     ids = tracker_lib.add_trackers(api, h, trace, seed=11)
@@ -126,7 +126,7 @@ def run_control_case(api, h, trace, workload, drain_fn, run_fn, abi, name="contr
             assert api["allocate_optimal"](h, reqs.ctypes.data, len(reqs), a.ctypes.data) == 0
             out["steps"].append(["allocate", b, int(len(a)), _sha(a)])
         if ext and b >= 1:  # the stream allocator's pause / probe calls
-            for k, step in enumerate(stream_allocator_steps(abi, trace.ndts, min(b, 9))):
+            for k, step in enumerate(stream_allocator_steps(abi, trace.ndts, min(b, 9), video_mask(abi, trace))):
                 r = run_step(api, h, abi, step)
                 out["steps"].append([step[0], b, int(len(r)), _sha(r)])
         if b % 4 == 3:  # blank frames

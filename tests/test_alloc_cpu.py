@@ -9,7 +9,7 @@ the previous allocation (getBandwidthNeeded forwarder.go:1880-1886)."""
 import numpy as np
 
 from tests.oracle_lib import load as load_oracle
-from tests.test_alloc_gpu import allocate, make_alloc_reqs, run_step, stream_allocator_steps
+from tests.test_alloc_gpu import allocate, make_alloc_reqs, run_step, stream_allocator_steps, video_mask
 
 
 def test_orc_allocate_optimal_invariants(pkg, workload):
@@ -58,7 +58,7 @@ def test_orc_pause_next_higher_invariants(pkg, workload):
         workload.load_topology(o.api, oh, tr)
         boosted = avail = 0
         for b in range(tr.nbatches):
-            for step in stream_allocator_steps(abi, tr.ndts, b):
+            for step in stream_allocator_steps(abi, tr.ndts, b, video_mask(abi, tr)):
                 r = run_step(o.api, oh, abi, step)
                 kind, reqs, caps = step
                 if kind == "pause":

@@ -57,17 +57,25 @@ def transition(api, h, reqs, abi):
     return out
 
 
-def stream_allocator_steps(abi, ndts, b):
+def video_mask(abi, trace):
+    """Per DownTrack: its track is video (the stream allocator manages only those)."""
+    return np.array([trace.tracks[trace.downtracks[d].track].kind == abi.LKF_KIND_VIDEO for d in range(trace.ndts)])
+
+
+def stream_allocator_steps(abi, ndts, b, video):
     """The allocation calls the stream allocator makes between batch b-1 and b
     (streamallocator.go: allocateAllTracks -> AllocateOptimal / Pause, then
     probing -> GetNextHigherTransition / AllocateNextHigher): a list of
-    (call, reqs, capacities)."""
+    (call, reqs, capacities).  Pause goes to video DownTracks only: the
+    allocator tracks only video (Forwarder.Pause dereferences the video layer
+    selector); `video` is the per-DownTrack mask."""
     rng = np.random.default_rng(1000 + b)
     steps = []
     if b == 1:
         steps.append(("optimal", make_alloc_reqs(abi, ndts, seed=70), None))
         r = make_alloc_reqs(abi, ndts, seed=71)
-        steps.append(("pause", r[rng.random(ndts) < 0.6], None))
+        pick = rng.random(ndts) < 0.6
+        steps.append(("pause", r[pick & video[r["dt"]]], None))
     elif b >= 2:
         r = make_alloc_reqs(abi, ndts, seed=80 + b)
         r["bitrates"] = np.sort(r["bitrates"].reshape(ndts, -1), axis=1).reshape(ndts, 3, 4)  # layered: rising
@@ -158,7 +166,7 @@ def test_pause_and_next_higher_match_oracle(pkg, workload, cfg):
         workload.load_topology(o.api, oh, tr)
         boosted = avail = 0
         for b in range(tr.nbatches):
-            for step in stream_allocator_steps(abi, tr.ndts, b):
+            for step in stream_allocator_steps(abi, tr.ndts, b, video_mask(abi, tr)):
                 g = run_step(eng.api, eng.h, abi, step)
                 r = run_step(o.api, oh, abi, step)
                 for f in g.dtype.names:
