@@ -1,13 +1,23 @@
 """bench.py — forwarded RTP packets/s of the MI355X forwarding engine.
 
-Workload: BASELINE.json configs[1] = 100 rooms x 10 participants, VP8 3-layer
-simulcast + Opus per participant, each subscribing to the other 9 (18,000
-DownTracks), 2% loss, 1% reorder, target-layer switches every 2 s per
-DownTrack, subscriber mutes.  Synthetic (seeded splitmix64).  One step = one
-batch = 1 s of media time of all 100 rooms through the full per-packet path
-(Forwarder/RTPMunger/VP8 munger/sequencer + wire-packet emission), inputs
-resident in HBM.  Multi-GPU: one process per GPU, each rank forwards its own
-100 rooms (room sharding, no data-path collective) -> weak scaling.
+Default workload (the headline): BASELINE.json configs[1] = 100 rooms x 10
+participants, VP8 3-layer simulcast + Opus per participant, each subscribing
+to the other 9 (18,000 DownTracks), 2% loss, 1% reorder, target-layer switches
+every 2 s per DownTrack, subscriber mutes.  Synthetic (seeded splitmix64).
+One step = one batch = 1 s of media time of all 100 rooms through the full
+per-packet path (Forwarder/RTPMunger/VP8 munger/sequencer + wire-packet
+emission), inputs resident in HBM.  Multi-GPU: one process per GPU, each rank
+forwards its own 100 rooms (room sharding, no data-path collective) -> weak
+scaling.
+
+--config N times BASELINE.json configs[N-1] instead (per GPU):
+  1  1 room x 10 participants (the reference's CPU-runnable case)
+  3  125 rooms x 50 participants, audio-heavy (1,000 rooms over 8 GPUs):
+     raw datagrams -> Buffer.calc (audio levels, NACK queues) -> forward,
+     plus the speaker ranking tick every step (lkf_speakers_enqueue)
+  4  10 rooms x 1 publisher x 5,000 subscribers (payload-copy bound)
+  5  2,000 rooms x 5 participants, VP9/AV1 SVC with dependency descriptors
+     + Opus DTX, congestion-driven layer drops (the serial SVC decide path)
 
 Prints ONE JSON line (rank 0).
 """
@@ -52,19 +62,45 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(threads, sample_rooms=256, sample_batches=4):
+# per config: default rooms per GPU, CPU-baseline sample rooms (about 10-30 s
+# of oracle work on 16 host threads), one-thread sample rooms
+CONFIGS = {
+    1: dict(rooms=1, sample=1, sample1=1),
+    2: dict(rooms=100, sample=256, sample1=32),
+    3: dict(rooms=125, sample=64, sample1=8),
+    4: dict(rooms=10, sample=2, sample1=1),
+    5: dict(rooms=2000, sample=2048, sample1=256),
+}
+
+
+def workload_name(config, rooms, ndts):
+    return {
+        1: "configs[0]: 1 room x 10 participants, VP8 3-layer simulcast + Opus, %d DownTracks, no loss" % ndts,
+        2: "configs[1]: %d rooms x 10 participants per GPU, VP8 3-layer simulcast + Opus, %d DownTracks, 2%% loss, "
+           "1%% reorder, layer switching" % (rooms, ndts),
+        3: "configs[2]: %d rooms x 50 participants per GPU (1,000 rooms over 8 GPUs), Opus + 5 VP8 publishers per "
+           "room, %d DownTracks, speaker ranking every step" % (rooms, ndts),
+        4: "configs[3]: %d rooms x 1 publisher x 5,000 subscribers per GPU (webinar), %d DownTracks" % (rooms, ndts),
+        5: "configs[4]: %d rooms x 5 participants per GPU, VP9/AV1 L3T3 SVC with dependency descriptors + Opus "
+           "DTX, %d DownTracks, congestion-driven layer drops" % (rooms, ndts),
+    }[config]
+
+
+def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2):
     """CPU oracle (C++ restatement of the Go path, -O3) on a bounded sample of
-    the same workload: `sample_rooms` rooms of configs[1] shape, `sample_batches`
-    one-second batches, rooms sharded over `threads` workers (one oracle engine
-    per worker).  Returns (forwarded/s, wall s, rooms, batches)."""
+    the same workload: `sample_rooms` rooms of the config's shape,
+    `sample_batches` one-second batches, rooms sharded over `threads` workers
+    (one oracle engine per worker).  Returns (forwarded/s, wall s, rooms,
+    batches)."""
     from tests.oracle_lib import load as load_oracle
     wl = importlib.import_module("livekit-server_amd.workload")
     abi = importlib.import_module("livekit-server_amd.abi")
     o = load_oracle()
+    threads = max(1, min(threads, sample_rooms))
     per = max(1, sample_rooms // threads)
     shards = []
     for t in range(threads):
-        tr = wl.Trace(2, duration_s=float(sample_batches), batch_s=1.0, rooms=per, room_base=t * per)
+        tr = wl.Trace(config, duration_s=float(sample_batches), batch_s=1.0, rooms=per, room_base=t * per)
         h = o.create(500)
         wl.load_topology(o.api, h, tr)
         shards.append((tr, h))
@@ -72,10 +108,11 @@ def cpu_baseline(threads, sample_rooms=256, sample_batches=4):
 
     def work(i):
         tr, h = shards[i]
+        dd = tr.has_dd()
         for b in range(tr.nbatches):
             wl.queue_events(o.api, h, tr, b)
             pk, n, ar, alen = tr.batch(b)
-            o.run(h, pk, n, ar, alen)
+            o.run(h, pk, n, ar, alen, tr.batch_dd(b)[0] if dd else None)
             st = abi.lkf_stats()
             o.api["get_stats"](h, C.byref(st))
             fwd[i] += st.forwarded
@@ -114,7 +151,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rooms", type=int, default=100)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[N-1] (2 = configs[1], the headline)")
+    ap.add_argument("--rooms", type=int, default=0, help="rooms per GPU (0: the config's)")
     ap.add_argument("--batch-s", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -132,6 +171,11 @@ def main():
                     help="step = forward + SRTP protect (lkf_protect: abs-send-time + AES_CM_128_HMAC_SHA1_80 "
                          "per subscriber transport, every DownTrack bound)")
     args = ap.parse_args()
+    if not args.rooms:
+        args.rooms = CONFIGS[args.config]["rooms"]
+    speakers = args.config == 3
+    if args.config == 3:  # audio levels come from the ingress path
+        args.ingress = True
 
     import torch
 
@@ -156,7 +200,8 @@ def main():
     # args.rooms of them
     rooms_mod = importlib.import_module("livekit-server_amd.rooms")
     plan = rooms_mod.plan_room_shards([1.0] * (world * args.rooms), world)
-    trace = wl.Trace(2, duration_s=nb * args.batch_s, batch_s=args.batch_s, room_ids=plan[rank])
+    trace = wl.Trace(args.config, duration_s=nb * args.batch_s, batch_s=args.batch_s, room_ids=plan[rank])
+    has_dd = trace.has_dd() and not args.ingress  # (ingest produces the DD side array on the GPU)
     eng = pkg.Engine.for_trace(trace, device=local, lib_path=os.environ.get("LKF_LIB") or None)
     wl.load_topology(eng.api, eng.h, trace)
 
@@ -174,7 +219,7 @@ def main():
             assert eng.api["set_downtrack_transport"](eng.h, d, tps[k]) == 0
 
     # inputs resident in HBM before the timed region (--host-io: in pinned host memory)
-    dpk, dar, meta = [], [], []
+    dpk, dar, meta, ddd = [], [], [], []
     hdev = torch.device("cpu") if args.host_io else dev
     for b in range(nb):
         if args.ingress:
@@ -192,6 +237,10 @@ def main():
         dpk.append(tp)
         dar.append(ta)
         meta.append((n, alen))
+        if has_dd:  # the batch's lkf_pkt_dd side array, resident like the packets
+            dptr, dn = trace.batch_dd(b)
+            dsz = C.sizeof(pkg.abi.lkf_pkt_dd)
+            ddd.append(torch.frombuffer(bytearray(C.string_at(dptr, max(1, dn) * dsz)), dtype=torch.uint8).to(hdev))
     stream = torch.cuda.current_stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
 
@@ -220,8 +269,12 @@ def main():
             eng.submit(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
         else:
             eng.submit_device(C.c_void_p(dpk[b].data_ptr()), n, C.c_void_p(dar[b].data_ptr()), alen)
+            if has_dd:
+                assert eng.api["submit_dd_device"](eng.h, C.c_void_p(ddd[b].data_ptr()), n) == 0
         tc = time.perf_counter()
         eng.run(sp)
+        if speakers:  # Room.audioUpdateWorker's tick (ranking stays in HBM for the all-gather)
+            assert eng.api["speakers_enqueue"](eng.h, 1700000000 * 10**9 + int((b + 1) * args.batch_s * 1e9)) == 0
         if args.srtp:
             assert eng.api["protect"](eng.h, 1700000000 * 10**9 + int(b * args.batch_s * 1e9)) == 0
         if args.host_io and b > args.warmup:  # batch b-1's output over PCIe while batch b computes
@@ -329,7 +382,8 @@ def main():
         if args.pmc_csv and os.path.exists(args.pmc_csv):
             try:
                 pmc = json.load(open(args.pmc_csv))
-                if pmc.get("kernel_sources_sha") == kernel_sources_sha() and pmc.get("bench_args_rooms") == args.rooms:
+                if (pmc.get("kernel_sources_sha") == kernel_sources_sha() and pmc.get("bench_args_rooms") == args.rooms
+                        and pmc.get("bench_args_config", 2) == args.config and not args.ingress):
                     traffic = pmc.get("hbm_bytes_per_step")
                     traffic_src = os.path.relpath(args.pmc_csv, ROOT)
             except Exception:
@@ -339,12 +393,13 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             # the GPU box gives one GPU a 16-CPU share (os.cpu_count() is the whole host)
             thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            v, secs, rooms, nbat = cpu_baseline(thr)
-            v1, secs1, rooms1, _ = cpu_baseline(1, sample_rooms=32)
-            cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": thr, "kind": "port",
-                   "sample": "configs[1] shape: %d rooms x 10 participants, 4 s of media (%d batches incl. the "
-                             "arrival tail), rooms sharded over %d threads (%.1f s wall); single thread: %d rooms, "
-                             "%.1f s wall" % (rooms, nbat, thr, secs, rooms1, secs1),
+            cc = CONFIGS[args.config]
+            v, secs, rooms, nbat = cpu_baseline(thr, sample_rooms=cc["sample"], config=args.config)
+            v1, secs1, rooms1, _ = cpu_baseline(1, sample_rooms=cc["sample1"], config=args.config)
+            cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": min(thr, rooms), "kind": "port",
+                   "sample": "configs[%d] shape: %d rooms, 4 s of media (%d batches incl. the arrival tail), rooms "
+                             "sharded over %d threads (%.1f s wall); single thread: %d rooms, %.1f s wall" % (
+                                 args.config - 1, rooms, nbat, min(thr, rooms), secs, rooms1, secs1),
                    "single_thread_value": round(v1, 1), "host_nproc": os.cpu_count(), "cpu_model": cpu_model()}
         line = {
             "metric": "forwarded RTP pkts/sec per GPU & node (bit-exact) + % HBM roofline",
@@ -359,8 +414,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": "configs[1]: %d rooms x 10 participants per GPU, VP8 3-layer simulcast + Opus, "
-                                   "%d DownTracks, 2%% loss, 1%% reorder, layer switching" % (args.rooms, trace.ndts),
+            "config": {"workload": workload_name(args.config, args.rooms, trace.ndts),
                        "batch": "%.3g s of media per step" % args.batch_s,
                        "step": ("raw datagrams -> Buffer.calc -> forward (lkf_ingest_device + lkf_run)"
                                 if args.ingress else

@@ -727,6 +727,10 @@ int lkf_remove_track(lkf_engine *e, int32_t track);
  * audiolevel.go:105-112), sorted by level (ties: participant index), grouped
  * by room in ascending room order. */
 int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, uint32_t *n_out);
+/* The same ranking enqueued without a host wait (Room.audioUpdateWorker's
+ * tick inside a pipelined loop): it runs after the last enqueued ingest and
+ * stays in HBM for the summary all-gather. */
+int lkf_speakers_enqueue(lkf_engine *e, int64_t now_ns);
 
 /* ---- introspection ------------------------------------------------------ */
 /* Duration of the last batch's decide kernel, emit kernel and whole batch, ms. */

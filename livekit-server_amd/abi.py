@@ -387,6 +387,10 @@ def bind_engine_api(lib, prefix):
     api["ingested"] = _bind(lib, prefix + "ingested", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["ingested_dd"] = _bind(lib, prefix + "ingested_dd", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["submit_dd"] = _bind(lib, prefix + "submit_dd", C.c_int, [e, C.c_void_p, C.c_uint32])
+    if hasattr(lib, prefix + "submit_dd_device"):  # engine only
+        api["submit_dd_device"] = _bind(lib, prefix + "submit_dd_device", C.c_int, [e, C.c_void_p, C.c_uint32])
+    if hasattr(lib, prefix + "speakers_enqueue"):
+        api["speakers_enqueue"] = _bind(lib, prefix + "speakers_enqueue", C.c_int, [e, C.c_int64])
     api["stream_stats_get"] = _bind(lib, prefix + "stream_stats_get", C.c_int, [e, C.c_int32, P(lkf_stream_stats)])
     api["ingest_nacks"] = _bind(lib, prefix + "ingest_nacks", C.c_int,
                                 [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32)])

@@ -2608,6 +2608,37 @@ static int rebuild_speakers(lkf_engine *e) {
   return LKF_OK;
 }
 
+// The speaker tick without a host wait: the ranking of every room at now_ns
+// is enqueued on the prep stream (after the ingest that updated the levels)
+// and stays in HBM (the per-room slots an all-gather reads); lkf_speakers
+// reads a ranking back.
+int lkf_speakers_enqueue(lkf_engine *e, int64_t now_ns) {
+  if (!e) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  if (e->spkDirty) {
+    rc = drain_streams(e);
+    if (rc) return rc;
+    rc = rebuild_speakers(e);
+    if (rc) return rc;
+  }
+  if (e->nRooms == 0) return LKF_OK;
+  SpeakersLaunch a;
+  a.nrooms = e->nRooms;
+  a.roomPartOff = e->dRoomPartOff;
+  a.partId = e->dPartId;
+  a.partMicOff = e->dPartMicOff;
+  a.mics = e->dMics;
+  a.roomId = e->dRoomId;
+  a.streams = e->dStreams;
+  a.hot = e->dStreamHot;
+  a.nowNs = now_ns;
+  a.slots = e->dSpkSlots;
+  a.counts = e->dSpkCounts;
+  HIPCHK(launch_speakers(e->prepS, a), "speakers");
+  return LKF_OK;
+}
+
 int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, uint32_t *n_out) {
   if (!e || !n_out) return LKF_EINVAL;
   int rc = flush_topology(e);

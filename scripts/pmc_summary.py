@@ -71,6 +71,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import kernel_sources_sha
     out["kernel_sources_sha"] = kernel_sources_sha()
+    out["bench_args_config"] = int(os.environ.get("PMC_CONFIG", "2"))
     out["bench_args_rooms"] = int(os.environ.get("PMC_ROOMS", "100"))
     json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
