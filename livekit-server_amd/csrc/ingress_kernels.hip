@@ -1197,6 +1197,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
 // lane 0.  A datagram's result: info = n_pairs | num_nacked << 16 (0: no
 // RTCP NACK) and the offset of its pairs in the batch's pair buffer.
 // ---------------------------------------------------------------------------
+// a 64-bit value of lane x (readlane returns int: the low word must not sign-extend)
+__device__ __forceinline__ u64 rl_u64(u64 v, u32 x) {
+  return (u64(u32(__builtin_amdgcn_readlane(int(u32(v >> 32)), x))) << 32) |
+         u64(u32(__builtin_amdgcn_readlane(int(u32(v)), x)));
+}
+
 __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__ raws,
                                                  const IngParsed *__restrict__ q, const lkf_flow *__restrict__ flows,
                                                  const DevStream *__restrict__ streams, NackState *__restrict__ states,
@@ -1292,14 +1298,12 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
     const u32 m = min(64u, nIdx - base);
     for (u32 x = 0; x < m; x++) {
       if (__builtin_amdgcn_readlane(stm, x) != sid) continue;
-      const i64 now = i64((u64(__builtin_amdgcn_readlane(u32(u64(arr) >> 32), x)) << 32) |
-                          u64(__builtin_amdgcn_readlane(u32(u64(arr)), x)));
+      const i64 now = i64(rl_u64(u64(arr), x));
       const u32 icx = __builtin_amdgcn_readlane(ic, x);
       if (__builtin_amdgcn_readlane(ipf, x) & IP_OK) {  // updateStreamState ran
         removeSn(__builtin_amdgcn_readlane(sn, x));
         if (__builtin_amdgcn_readlane(ff, x) & LKF_FLOW_HAS_LOSS) {
-          const u64 s0 = (u64(__builtin_amdgcn_readlane(u32(ls >> 32), x)) << 32) | __builtin_amdgcn_readlane(u32(ls), x);
-          const u64 e0 = (u64(__builtin_amdgcn_readlane(u32(le >> 32), x)) << 32) | __builtin_amdgcn_readlane(u32(le), x);
+          const u64 s0 = rl_u64(ls, x), e0 = rl_u64(le, x);
           // Push each lost SN: the queue keeps the newest CacheSize entries of
           // (queue, lost SNs in order); every new one has tries 0, lastNackedAt now
           const u64 L = e0 - s0;

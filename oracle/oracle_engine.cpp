@@ -415,7 +415,8 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   std::memset(&e->stats, 0, sizeof(e->stats));
   const u32 ndt = u32(e->dts.size());
   std::vector<std::vector<OEv>> evq(ndt);
-  for (auto &ev : e->pending) evq[ev.dt].push_back(ev);
+  for (auto &ev : e->pending)  // ops for removed DownTracks are dropped (they get no more control calls)
+    if (e->dts[ev.dt]->active) evq[ev.dt].push_back(ev);
   e->pending.clear();
   for (auto &q : evq)
     std::stable_sort(q.begin(), q.end(), [](const OEv &a, const OEv &b) { return a.at < b.at; });

@@ -48,20 +48,22 @@ def _states(abi, api, h, ndts):
     return out
 
 
-def _reuse(abi, trace, api, h, dts, n0):
+def _reuse(abi, trace, api, h, dts, n0, orig):
     """Transceiver reuse of each DownTrack in dts: export, remove, add a new
-    DownTrack with the same parameters (handle n0 + i), seed it, give the video
-    ones an allocation at the batch start.  Returns the exported states."""
+    DownTrack with the same parameters (handle n0 + i; orig maps a handle to
+    its trace DownTrack), seed it, give the video ones an allocation at the
+    batch start.  Returns the exported states."""
     states = []
     for i, d in enumerate(dts):
         s = abi.lkf_fwd_state()
         assert api["get_state"](h, d, C.byref(s)) == 0
         states.append(s.as_tuple())
         assert api["remove_downtrack"](h, d) == 0
-        nh = api["add_downtrack"](h, C.byref(trace.downtracks[d]))
+        p = trace.downtracks[orig[d]]
+        nh = api["add_downtrack"](h, C.byref(p))
         assert nh == n0 + i, (nh, n0 + i)
         assert api["seed_state"](h, nh, C.byref(s)) == 0
-        if trace.tracks[trace.downtracks[d].track].kind == abi.LKF_KIND_VIDEO:
+        if trace.tracks[p.track].kind == abi.LKF_KIND_VIDEO:
             assert api["ctl"](h, nh, abi.LKF_CTL_SET_ALLOCATION, 2, 2, 2, 0, 0) == 0
     return states
 
@@ -78,14 +80,17 @@ def test_state_roundtrip_transceiver_reuse(pkg, workload, abi, cfg):
         workload.load_topology(eng.api, eng.h, tr)
         workload.load_topology(o.api, oh, tr)
         n = tr.ndts
+        orig = {d: d for d in range(n)}
         reused = list(range(1, n, 5))
         seeded = 0
         for b in range(tr.nbatches):
             if b in (2, 4):  # between batches, on both sides
-                gst = _reuse(abi, tr, eng.api, eng.h, reused, n)
-                ost = _reuse(abi, tr, o.api, oh, reused, n)
+                gst = _reuse(abi, tr, eng.api, eng.h, reused, n, orig)
+                ost = _reuse(abi, tr, o.api, oh, reused, n, orig)
                 assert gst == ost, b  # the exported states agree (bit-exact)
                 seeded += sum(1 for s in gst if s[0])
+                for i, d in enumerate(reused):
+                    orig[n + i] = orig[d]
                 reused = list(range(n, n + len(reused)))  # the next reuse takes the new DownTracks
                 n += len(gst)
             workload.queue_events(eng.api, eng.h, tr, b)
