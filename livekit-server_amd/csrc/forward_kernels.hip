@@ -236,6 +236,7 @@ struct Lane {
 #endif
   RangeEntry *rm;  // the closed-range ring, staged in LDS for the batch
   bool rmDirty;    // a closed range was written (write the ring back)
+  bool vcDirty;    // a VP8 munger map changed (write the maps back)
   VP8Cold *vc;
   i32 *dropKey;  // LDS copy of vc->dropKey
   i32 *exKey;    // LDS copy of vc->exKey
@@ -540,7 +541,7 @@ __device__ void vp8_record_missing_wide(Lane &L, i32 prevMax, i32 ext, i32 off) 
   }
 }
 __device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
-
+  L.vcDirty = true;
   if (ext < prevMax) return;
   const i64 span = i64(ext) - i64(prevMax) + 1;
   if (span > 64) {
@@ -696,11 +697,15 @@ __device__ __forceinline__ int vp8_update(Lane &L, const PktV &p, bool ooo, bool
   setf(L, F_WR_MAX_MBIT, M);
   if (gap) {
     vp8_record_missing(L, prevMax, ext, L.h.pictureIdOffset);
-    if (T && p.tid > u8(maxTL)) set_add(L.exKey, L.h.exHead, L.h.exCount, ext, kExemptKeep);
+    if (T && p.tid > u8(maxTL)) {
+      L.vcDirty = true;
+      set_add(L.exKey, L.h.exHead, L.h.exCount, ext, kExemptKeep);
+    }
   } else {
     if (T && p.tid > u8(maxTL)) {
       if (!set_has_u(L.exKey, L.h.exHead, L.h.exCount, ext)) {
         if (I && prevMax != ext) {
+          L.vcDirty = true;
           set_add(L.dropKey, L.h.dropHead, L.h.dropCount, ext, kDropKeep);
           L.h.pictureIdOffset += 1;
         }
@@ -2011,6 +2016,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
   L.rm = sRm;
   L.rmDirty = false;
+  L.vcDirty = false;
   L.vc = A.vc + d;
   L.dropKey = sDrop;
   L.exKey = sEx;
@@ -2427,12 +2433,16 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
             const u32 b = u32(__ffsll((long long)m) - 1);
             const i32 eb = i32(rl32(u32(ext), b));
             if ((pdR >> b) & 1) {
+              L.vcDirty = true;
               set_add(L.dropKey, L.h.dropHead, L.h.dropCount, eb, kDropKeep);
               continue;
             }
             if (video) {
               vp8_record_missing(L, i32(rl32(u32(prevExt), b)), eb, i32(rl32(u32(picOff), b)));
-              if (rl32(u32(overT), b)) set_add(L.exKey, L.h.exHead, L.h.exCount, eb, kExemptKeep);
+              if (rl32(u32(overT), b)) {
+                L.vcDirty = true;
+                set_add(L.exKey, L.h.exHead, L.h.exCount, eb, kExemptKeep);
+              }
             }
             const u64 from = rl64(prevOsn, b), to = rl64(osn, b);  // slots of (from, to) skipped
             const u32 n = u32(to - from - 1);
@@ -2593,6 +2603,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
             L.h.pictureIdOffset += i32(__popcll(pd));
             while (pd && !gR) {  // (with gap lanes the drops went into the set in lane order above)
               const u32 b = u32(__ffsll((long long)pd) - 1);
+              L.vcDirty = true;
               set_add(L.dropKey, L.h.dropHead, L.h.dropCount, i32(rl32(u32(ext), b)), kDropKeep);
               pd &= pd - 1;
             }
@@ -2714,7 +2725,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     const uint4 *l = reinterpret_cast<const uint4 *>(sDD);
     for (u32 i = lane; i < sizeof(DDState) / 16; i += 64) g[i] = l[i];
   }
-  if (L.h.flags & F_VP8) {
+  if ((L.h.flags & F_VP8) && L.vcDirty) {  // the maps go back only when a batch changed them
     if (lane < u32(kSetCap)) {
       L.vc->dropKey[lane] = sDrop[lane];
       L.vc->exKey[lane] = sEx[lane];
@@ -3449,6 +3460,7 @@ __global__ void __launch_bounds__(64) k_pad(PadArgs A) {
   Lane L{sHot};
   L.rm = A.rm + size_t(d) * kRangeCap;
   L.rmDirty = false;
+  L.vcDirty = false;
   L.seq = A.seq + size_t(d) * A.seqSize;
   L.seqSize = A.seqSize;
   L.srm = reinterpret_cast<SeqRM *>(A.srm + size_t(d) * A.srmStride);

@@ -25,4 +25,16 @@ rc=$?; echo "rocprof alloc rc=$rc"; tail -2 $O/trace_alloc.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 $O/bench.log
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+# FETCH_SIZE / WRITE_SIZE calibration on known byte counts (emit's access patterns)
+if [ "${CALIB:-1}" = "1" ]; then
+  timeout -k 10 120 ./scripts/micro/fetch_calib 1024 > $O/calib_time.log 2>&1
+  rc=$?; echo "calib rc=$rc"; cat $O/calib_time.log
+  [ $rc -eq 0 ] || exit $rc
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/calib_$c -o run -- ./scripts/micro/fetch_calib 1024 > $O/calib_$c.log 2>&1
+    rc=$?; echo "calib pmc $c rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+fi
+exit 0
