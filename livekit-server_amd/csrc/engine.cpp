@@ -83,6 +83,17 @@ struct BatchCtx {
   // SRTP-protected copy of the output (lkf_protect; allocated on first use)
   uint8_t *dProt = nullptr;
   bool protectedRun = false;
+  // the run's descriptor (device; k_h2d pulls it from the staging buffer)
+  RunDesc *dDesc = nullptr;
+  // page-locked, CPU-cached staging of the run's RunDesc + control-op CSR
+  // (malloc + hipHostRegister; k_h2d reads it through the device mapping)
+  uint8_t *stage = nullptr, *stageDev = nullptr;
+  uint32_t stageCap = 0;  // ops
+  // the prep stage (k_h2d ... layer index) and the decide stage's tail
+  // (counters, output scan) as HIP graphs, captured for the engine's topology
+  // epoch; replayed every run (one launch each instead of ~11)
+  hipGraphExec_t gPrep = nullptr, gScan = nullptr;
+  uint64_t gPrepEpoch = 0, gScanEpoch = 0;
 };
 
 }  // namespace
@@ -131,16 +142,11 @@ struct lkf_engine {
     DevEvent ev;
   };
   std::vector<Pend> pending;
-  // pinned, double-buffered staging of the per-lane event CSR (async H2D)
-  // Page-locked, CPU-cached staging (malloc + hipHostRegister): the CSR is
-  // built in place and a copy kernel pulls it through the device mapping.
-  struct Stage {
-    DevEvent *ev = nullptr, *evDev = nullptr;
-    uint32_t *lane = nullptr, *laneDev = nullptr;  // lane of each staged op (sorted)
-    size_t evCap = 0;
-    hipEvent_t done = nullptr;
-    bool used = false;
-  } stage[2];
+  // topology epoch: bumped by every change the captured stage graphs depend
+  // on (tables, schedule, DD / tracker allocations); a context re-captures
+  // its graphs when its epoch is older
+  uint64_t epoch = 1;
+  bool useGraph = true;  // LKF_GRAPH=0: the stages as direct launches (A/B)
 
   // device: persistent state
   DevTrack *dTracks = nullptr;
@@ -445,6 +451,7 @@ static int ensure_dd(lkf_engine *e) {
 // Uploads tracks / DownTracks added since the last flush (contiguous tails).
 static int flush_topology(lkf_engine *e) {
   if (e->pendTracks.empty() && e->pendDTs.empty() && e->pendStreams.empty()) return LKF_OK;
+  e->epoch++;  // the stage graphs read the topology's sizes
   int rc = drain_streams(e);
   if (rc) return rc;
   rc = ensure_dd(e);
@@ -613,6 +620,10 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dPktsOwn, c.max_batch_pkts));
     A(dalloc(&x.dArenaOwn, c.max_batch_arena + 64));
     A(dalloc(&x.dRawPkts, c.max_batch_pkts));
+    A(dalloc(&x.dDesc, 1));
+    A(dalloc(&x.dEvents, 4096));
+    A(dalloc(&x.dEvLane, 4096));
+    x.evCap = x.evLaneCap = 4096;
     A(hipEventCreateWithFlags(&x.decided, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.prepped, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.emitted, hipEventDisableTiming));
@@ -690,6 +701,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   if (const char *v = getenv("LKF_ING_LANE")) e->ingLane = atoi(v) != 0;
+  if (const char *v = getenv("LKF_GRAPH")) e->useGraph = atoi(v) != 0;
   return e;
 }
 
@@ -756,10 +768,11 @@ void lkf_destroy(lkf_engine *e) {
   for (auto &r : e->ring)
     for (auto &ev : r)
       if (ev) (void)hipEventDestroy(ev);
-  for (auto &sg : e->stage) {
-    stage_free(&sg.ev, &sg.evDev);
-    stage_free(&sg.lane, &sg.laneDev);
-    if (sg.done) (void)hipEventDestroy(sg.done);
+  for (auto &x : e->ctx) {
+    stage_free(&x.stage, &x.stageDev);
+    if (x.gPrep) (void)hipGraphExecDestroy(x.gPrep);
+    if (x.gScan) (void)hipGraphExecDestroy(x.gScan);
+    if (x.dDesc) (void)hipFree(x.dDesc);
   }
   if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
@@ -1046,6 +1059,7 @@ static int rebuild_sched(lkf_engine *e) {
            "wavetrack copy");
   }
   e->schedDirty = false;
+  e->epoch++;
   return upload_done(e);
 }
 
@@ -1093,14 +1107,13 @@ int lkf_run(lkf_engine *e, void *stream) {
   // Per-lane control-op CSR (stable: queue order within a lane, then by
   // at_pkt).  The host sorts only the ops: an LSD radix sort on the lane
   // (8-bit digits, stable), then a stable insertion by at_pkt inside a lane
-  // with several ops; it stages the sorted ops and their lanes in page-locked
-  // cached memory.  The copy kernel pulls them and k_ev_offsets derives the
-  // dense per-lane offsets on the GPU (no host pass over all lanes).
+  // with several ops; it stages the run's RunDesc, the sorted ops and their
+  // lanes in this context's page-locked cached buffer.  The prep stage's
+  // first kernel pulls them and k_ev_offsets derives the dense per-lane
+  // offsets on the GPU (no host pass over all lanes).
   const auto tp1 = clk::now();
-  lkf_engine::Stage &sg = e->stage[e->nRuns & 1];
-  if (sg.used) HIPCHK(hipEventSynchronize(sg.done), "stage wait");
+  if (x.used) HIPCHK(hipEventSynchronize(x.prepped), "stage wait");  // run n-3's pull of this staging is done
   const auto tp2 = clk::now();
-  if (!sg.done) HIPCHK(hipEventCreateWithFlags(&sg.done, hipEventDisableTiming), "stage event");
   auto &ka = e->sortA, &kb = e->sortB;  // (lane, pending index)
   ka.clear();
   for (uint32_t i = 0; i < uint32_t(e->pending.size()); i++) {
@@ -1116,21 +1129,22 @@ int lkf_run(lkf_engine *e, void *stream) {
     for (auto &k : ka) kb[cnt[(k.first >> shift) & 0xff]++] = k;
     ka.swap(kb);
   }
-  if (nev > sg.evCap) {
-    stage_free(&sg.ev, &sg.evDev);
-    stage_free(&sg.lane, &sg.laneDev);
-    sg.evCap = std::max<size_t>(nev, 4096);
-    HIPCHK(stage_alloc(&sg.ev, &sg.evDev, sg.evCap), "alloc stage");
-    HIPCHK(stage_alloc(&sg.lane, &sg.laneDev, sg.evCap), "alloc stage");
+  if (nev > x.stageCap) {  // (graphs captured with the old staging are re-captured)
+    stage_free(&x.stage, &x.stageDev);
+    x.stageCap = uint32_t(std::max<size_t>(2 * nev, 4096));
+    HIPCHK(stage_alloc(&x.stage, &x.stageDev, sizeof(RunDesc) + size_t(x.stageCap) * (sizeof(DevEvent) + 4)),
+           "alloc stage");
+    x.gPrepEpoch = 0;
   }
-  DevEvent *evs = sg.ev;
+  DevEvent *evs = reinterpret_cast<DevEvent *>(x.stage + sizeof(RunDesc));
+  uint32_t *lanes = reinterpret_cast<uint32_t *>(x.stage + sizeof(RunDesc) + size_t(x.stageCap) * sizeof(DevEvent));
   for (size_t i = 0; i < nev; i++) {
     evs[i] = e->pending[ka[i].second].ev;
-    sg.lane[i] = ka[i].first;
+    lanes[i] = ka[i].first;
     if (i && ka[i - 1].first == ka[i].first && evs[i].at < evs[i - 1].at) {
       const DevEvent v = evs[i];  // queued out of at_pkt order: stable insertion within the lane
       size_t j = i;
-      while (j > 0 && sg.lane[j - 1] == ka[i].first && evs[j - 1].at > v.at) {
+      while (j > 0 && lanes[j - 1] == ka[i].first && evs[j - 1].at > v.at) {
         evs[j] = evs[j - 1];
         j--;
       }
@@ -1138,6 +1152,17 @@ int lkf_run(lkf_engine *e, void *stream) {
     }
   }
   e->pending.clear();
+  {
+    RunDesc &h = *reinterpret_cast<RunDesc *>(x.stage);
+    std::memset(&h, 0, sizeof(h));
+    h.pkts = reinterpret_cast<uint64_t>(e->curPkts);
+    h.arena = reinterpret_cast<uint64_t>(e->curArena);
+    h.dd = reinterpret_cast<uint64_t>(e->curDD);
+    h.nDev = reinterpret_cast<uint64_t>(e->curNDev);
+    h.n = e->curN;
+    h.nev = uint32_t(nev);
+    h.evCap = x.stageCap;
+  }
   const auto tp25 = clk::now();
   if (nev > x.evCap || size_t(nl) + 1 > x.evOffCap || nev > x.evLaneCap) {
     // this context's op buffers: its previous run (n-3) must be done with them.
@@ -1147,7 +1172,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     HIPCHK(hipStreamSynchronize(ps), "sync before events realloc");
     if (nev > x.evCap) {
       if (x.dEvents) HIPCHK(hipFree(x.dEvents), "free events");
-      x.evCap = std::max<uint64_t>(nev, 4096);
+      x.evCap = std::max<uint64_t>(2 * nev, 4096);
       HIPCHK(dalloc(&x.dEvents, x.evCap), "alloc events");
     }
     if (size_t(nl) + 1 > x.evOffCap) {
@@ -1157,39 +1182,78 @@ int lkf_run(lkf_engine *e, void *stream) {
     }
     if (nev > x.evLaneCap) {
       if (x.dEvLane) HIPCHK(hipFree(x.dEvLane), "free evlane");
-      x.evLaneCap = std::max<uint64_t>(nev, 4096);
+      x.evLaneCap = std::max<uint64_t>(2 * nev, 4096);
       HIPCHK(dalloc(&x.dEvLane, x.evLaneCap), "alloc evlane");
     }
+    x.gPrepEpoch = 0;
   }
-  HIPCHK(launch_h2d(ps, x.dEvents, sg.evDev, nev * sizeof(DevEvent), x.dEvLane, sg.laneDev, nev * sizeof(uint32_t)),
-         "event pull");
-  HIPCHK(launch_ev_offsets(ps, x.dEvLane, uint32_t(nev), nl, x.dEvOff), "event offsets");
-  HIPCHK(hipEventRecord(sg.done, ps), "stage record");
-  sg.used = true;
   const auto tp3 = clk::now();
 
-  // ---- decide stage (decide stream)
+  // ---- prep stage (prep stream): the pull, per-batch init, track ranges,
+  // slot scan, layer index, tracker observe, DD decode
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
   if (!e->ingestStarted) HIPCHK(hipEventRecord(rg[0], ps), "event");  // else: recorded ahead of the ingest
   e->ingestStarted = false;
-  HIPCHK(launch_batch_init(ps, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dStats, x.dFwdCnt,
-                           x.dFwdBytes),
-         "batch init");
-  HIPCHK(launch_track_ranges(ps, e->curPkts, e->curN, e->curNDev, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
-         "track_ranges");
-  HIPCHK(launch_scan(ps, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase, nullptr,
-                     x.dTot + 0, nullptr, nullptr),
-         "slot scan");
-  HIPCHK(launch_layer_index(ps, e->curPkts, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
-                            x.dLayerBefore, x.dLayerCnt),
-         "layer index");
-  if (e->nTrk)  // StreamTracker.Observe of every (track, spatial layer) tracker (receiver.go:686-695)
-    HIPCHK(launch_tracker_observe(ps, e->dTrk, e->nTrk, e->curPkts, x.dTBegin, x.dTEnd), "tracker observe");
-  if (e->ddAlloc) {  // dependency descriptors of this batch (track structure rings advance in order)
-    HIPCHK(hipMemsetAsync(x.dDDUsed, 0, sizeof(uint64_t), ps), "dd cursor reset");
-    HIPCHK(launch_dd_decode(ps, e->curPkts, e->curDD, e->curArena, x.dTBegin, x.dTEnd, e->dTracks, nt, e->dDDStruct,
-                            e->dDDTrack, x.dDDPkt, x.dErr),
-           "dd decode");
+  auto prep = [&]() -> int {
+    HIPCHK(launch_h2d(ps, x.stageDev, x.dDesc, x.dEvents, x.dEvLane), "event pull");
+    HIPCHK(launch_ev_offsets(ps, x.dEvLane, x.dDesc, nl, x.dEvOff), "event offsets");
+    HIPCHK(launch_batch_init(ps, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr,
+                             x.dStats, x.dFwdCnt, x.dFwdBytes),
+           "batch init");
+    HIPCHK(launch_track_ranges(ps, x.dDesc, e->cfg.max_batch_pkts, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
+           "track_ranges");
+    HIPCHK(launch_scan(ps, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase,
+                       nullptr, x.dTot + 0, nullptr, nullptr),
+           "slot scan");
+    HIPCHK(launch_layer_index(ps, x.dDesc, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
+                              x.dLayerBefore, x.dLayerCnt),
+           "layer index");
+    if (e->nTrk)  // StreamTracker.Observe of every (track, spatial layer) tracker (receiver.go:686-695)
+      HIPCHK(launch_tracker_observe(ps, e->dTrk, e->nTrk, x.dDesc, x.dTBegin, x.dTEnd), "tracker observe");
+    if (e->ddAlloc) {  // dependency descriptors of this batch (track structure rings advance in order)
+      HIPCHK(hipMemsetAsync(x.dDDUsed, 0, sizeof(uint64_t), ps), "dd cursor reset");
+      HIPCHK(launch_dd_decode(ps, x.dDesc, x.dTBegin, x.dTEnd, e->dTracks, nt, e->dDDStruct, e->dDDTrack, x.dDDPkt,
+                              x.dErr),
+             "dd decode");
+    }
+    return LKF_OK;
+  };
+  auto scanTail = [&](hipStream_t st) -> int {
+    // counters and the output scan stay on the (high-priority) decide stream:
+    // on the low-priority emit stream these small kernels queued behind the
+    // next batch's decide waves and were on the emit chain's critical path
+    HIPCHK(launch_stats_reduce(st, x.dStats), "stats reduce");
+    HIPCHK(launch_scan(st, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
+                       x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm, x.dGFirst, e->cfg.max_out_pkts),
+           "out scan");
+    return LKF_OK;
+  };
+  // (re)captures a stage as a graph on stream st: the captured launches are the
+  // same as the direct ones
+  auto capture = [&](hipStream_t st, hipGraphExec_t &g, auto body) -> int {
+    if (g) HIPCHK(hipGraphExecDestroy(g), "graph destroy");
+    g = nullptr;
+    HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "begin capture");
+    const int rc = body();
+    hipGraph_t graph = nullptr;
+    const hipError_t r = hipStreamEndCapture(st, &graph);
+    if (rc) return rc;
+    HIPCHK(r, "end capture");
+    const hipError_t ri = hipGraphInstantiate(&g, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIPCHK(ri, "graph instantiate");
+    return LKF_OK;
+  };
+  if (e->useGraph) {
+    if (x.gPrepEpoch != e->epoch || !x.gPrep) {
+      const int rc = capture(ps, x.gPrep, prep);
+      if (rc) return rc;
+      x.gPrepEpoch = e->epoch;
+    }
+    HIPCHK(hipGraphLaunch(x.gPrep, ps), "prep graph");
+  } else {
+    const int rc = prep();
+    if (rc) return rc;
   }
   HIPCHK(hipEventRecord(x.prepped, ps), "event");
   HIPCHK(hipStreamWaitEvent(s, x.prepped, 0), "wait prep");
@@ -1247,13 +1311,17 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipEventRecord(rg[1], s), "event");
   HIPCHK(launch_decide(s, d), "decide");
   HIPCHK(hipEventRecord(rg[2], s), "event");
-  // counters and the output scan stay on the (high-priority) decide stream:
-  // on the low-priority emit stream these small kernels queued behind the
-  // next batch's decide waves and were on the emit chain's critical path
-  HIPCHK(launch_stats_reduce(s, x.dStats), "stats reduce");
-  HIPCHK(launch_scan(s, 1, e->dDTs, nullptr, nullptr, x.dFwdCnt, x.dFwdBytes, nd, x.dPartA, x.dPartB, x.dRecBase,
-                     x.dByteBase, x.dTot + 2, x.dTot + 3, e->dPerm, x.dGFirst, e->cfg.max_out_pkts),
-         "out scan");
+  if (e->useGraph) {
+    if (x.gScanEpoch != e->epoch || !x.gScan) {
+      const int rc = capture(s, x.gScan, [&]() { return scanTail(s); });
+      if (rc) return rc;
+      x.gScanEpoch = e->epoch;
+    }
+    HIPCHK(hipGraphLaunch(x.gScan, s), "scan graph");
+  } else {
+    const int rc = scanTail(s);
+    if (rc) return rc;
+  }
   HIPCHK(hipEventRecord(x.decided, s), "event");
 
   // ---- emit stage (emit stream): wire bytes.  The decide stream goes
@@ -1966,6 +2034,7 @@ int32_t lkf_add_stream_tracker(lkf_engine *e, int32_t track, int32_t layer, uint
     e->dTrk = n;
     e->trkCap = cap;
   }
+  e->epoch++;  // the prep graph observes every tracker
   TrackerState t = {};
   t.track = uint32_t(track);
   t.layer = layer;

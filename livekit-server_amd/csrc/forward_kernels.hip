@@ -1379,9 +1379,11 @@ __global__ void k_batch_init(u32 ntracks, u32 ndts, u32 nstats, u32 *__restrict_
 // ---------------------------------------------------------------------------
 // nDev (optional): the batch length lives on the device (an ingest-produced
 // batch); n is then only the launch bound.
-__global__ void k_track_ranges(const lkf_pkt *__restrict__ pkts, u32 n, const u64 *__restrict__ nDev, u32 ntracks,
-                               u32 *__restrict__ tBegin, u32 *__restrict__ tEnd, u32 *__restrict__ tRuns,
-                               u32 *__restrict__ err) {
+__global__ void k_track_ranges(const RunDesc *__restrict__ desc, u32 ntracks, u32 *__restrict__ tBegin,
+                               u32 *__restrict__ tEnd, u32 *__restrict__ tRuns, u32 *__restrict__ err) {
+  const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
+  u32 n = desc->n;
+  const u64 *nDev = reinterpret_cast<const u64 *>(desc->nDev);
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (nDev && *nDev < n) n = u32(*nDev);
   if (i >= n) return;
@@ -1881,9 +1883,10 @@ __device__ __forceinline__ bool steady_state(const Lane &L) {
 // per track; for each simulcast layer l, list[l][tBegin + j] = the j-th packet
 // of layer l and before[l][i] = the number of layer-l packets of the track
 // before packet i.
-__global__ void __launch_bounds__(64) k_layer_index(const lkf_pkt *__restrict__ pkts, const u32 *__restrict__ tBegin,
+__global__ void __launch_bounds__(64) k_layer_index(const RunDesc *__restrict__ desc, const u32 *__restrict__ tBegin,
                                                     const u32 *__restrict__ tEnd, u32 stride, u32 *__restrict__ list,
                                                     u32 *__restrict__ before, u32 *__restrict__ cnt) {
+  const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
   const u32 t = blockIdx.x, lane = threadIdx.x;
   const u64 lt = (1ull << lane) - 1;
   const u32 b = tBegin[t], e = tEnd[t];
@@ -3603,9 +3606,11 @@ __global__ void __launch_bounds__(256) k_stats_reduce(u64 *stats) {
   }
 }
 
-__global__ void k_ev_offsets(const u32 *__restrict__ laneOf, u32 nev, u32 nl, u32 *__restrict__ off) {
+__global__ void k_ev_offsets(const u32 *__restrict__ laneOf, const RunDesc *__restrict__ desc, u32 nl,
+                             u32 *__restrict__ off) {
   const u32 l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l > nl) return;
+  const u32 nev = desc->nev;
   u32 lo = 0, hi = nev;  // lower_bound(laneOf, l)
   while (lo < hi) {
     const u32 mid = (lo + hi) >> 1;
@@ -3617,8 +3622,8 @@ __global__ void k_ev_offsets(const u32 *__restrict__ laneOf, u32 nev, u32 nl, u3
   off[l] = lo;
 }
 
-hipError_t launch_ev_offsets(hipStream_t s, const u32 *laneOf, u32 nev, u32 nl, u32 *off) {
-  hipLaunchKernelGGL(k_ev_offsets, dim3((nl + 1 + 255) / 256), dim3(256), 0, s, laneOf, nev, nl, off);
+hipError_t launch_ev_offsets(hipStream_t s, const u32 *laneOf, const RunDesc *desc, u32 nl, u32 *off) {
+  hipLaunchKernelGGL(k_ev_offsets, dim3((nl + 1 + 255) / 256), dim3(256), 0, s, laneOf, desc, nl, off);
   return hipGetLastError();
 }
 
@@ -3653,10 +3658,12 @@ hipError_t launch_err_fold(hipStream_t s, const u32 *err, u32 *sticky, u32 shift
 // track (packets of a track in order); runs on the prep stream, so batch n+1's
 // decode follows batch n's.
 // ---------------------------------------------------------------------------
-__global__ void k_dd_decode(const lkf_pkt *__restrict__ pkts, const lkf_pkt_dd *__restrict__ dds,
-                            const u8 *__restrict__ arena, const u32 *__restrict__ tBegin,
+__global__ void k_dd_decode(const RunDesc *__restrict__ desc, const u32 *__restrict__ tBegin,
                             const u32 *__restrict__ tEnd, const DevTrack *__restrict__ tracks, u32 ntracks,
                             DDStruct *structs, DDTrack *ddTracks, DDPkt *__restrict__ out, u32 *err) {
+  const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
+  const lkf_pkt_dd *__restrict__ dds = reinterpret_cast<const lkf_pkt_dd *>(desc->dd);
+  const u8 *__restrict__ arena = reinterpret_cast<const u8 *>(desc->arena);
   const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntracks) return;
   const u32 ddIdx = tracks[t].ddIdx;
@@ -3703,12 +3710,12 @@ __global__ void k_dd_decode(const lkf_pkt *__restrict__ pkts, const lkf_pkt_dd *
   ddTracks[ddIdx] = st;
 }
 
-hipError_t launch_dd_decode(hipStream_t s, const lkf_pkt *pkts, const lkf_pkt_dd *dds, const uint8_t *arena,
-                            const uint32_t *tBegin, const uint32_t *tEnd, const DevTrack *tracks, uint32_t ntracks,
-                            DDStruct *structs, DDTrack *ddTracks, DDPkt *out, uint32_t *err) {
+hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
+                            const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,
+                            uint32_t *err) {
   if (!ntracks) return hipSuccess;
-  hipLaunchKernelGGL(k_dd_decode, dim3((ntracks + 63) / 64), dim3(64), 0, s, pkts, dds, arena, tBegin, tEnd, tracks,
-                     ntracks, structs, ddTracks, out, err);
+  hipLaunchKernelGGL(k_dd_decode, dim3((ntracks + 63) / 64), dim3(64), 0, s, desc, tBegin, tEnd, tracks, ntracks,
+                     structs, ddTracks, out, err);
   return hipGetLastError();
 }
 
@@ -3770,10 +3777,12 @@ hipError_t launch_batch_init(hipStream_t s, u32 ntracks, u32 ndts, u32 nstats, u
   return hipGetLastError();
 }
 
-hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, u32 n, const u64 *nDev, u32 ntracks, u32 *tBegin,
-                               u32 *tEnd, u32 *tRuns, u32 *err) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_track_ranges, dim3(nblk(n, 256)), dim3(256), 0, s, pkts, n, nDev, ntracks, tBegin, tEnd, tRuns,
+hipError_t launch_track_ranges(hipStream_t s, const RunDesc *desc, u32 maxPkts, u32 ntracks, u32 *tBegin, u32 *tEnd,
+                               u32 *tRuns, u32 *err) {
+  // grid for the engine's batch capacity (the same launch every run: the
+  // batch length is in the descriptor)
+  if (maxPkts == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_track_ranges, dim3(nblk(maxPkts, 256)), dim3(256), 0, s, desc, ntracks, tBegin, tEnd, tRuns,
                      err);
   return hipGetLastError();
 }
@@ -3858,10 +3867,10 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   return hipGetLastError();
 }
 
-hipError_t launch_layer_index(hipStream_t s, const lkf_pkt *pkts, const u32 *tBegin, const u32 *tEnd, u32 ntracks,
+hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const u32 *tBegin, const u32 *tEnd, u32 ntracks,
                               u32 stride, u32 *list, u32 *before, u32 *cnt) {
   if (!ntracks) return hipSuccess;
-  hipLaunchKernelGGL(k_layer_index, dim3(ntracks), dim3(64), 0, s, pkts, tBegin, tEnd, stride, list, before, cnt);
+  hipLaunchKernelGGL(k_layer_index, dim3(ntracks), dim3(64), 0, s, desc, tBegin, tEnd, stride, list, before, cnt);
   return hipGetLastError();
 }
 
@@ -3897,24 +3906,31 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   return hipGetLastError();
 }
 
-__global__ void k_h2d(u32 *__restrict__ dA, const u32 *__restrict__ sA, u64 nA, u32 *__restrict__ dB,
-                      const u32 *__restrict__ sB, u64 nB) {
+// The run's first kernel: pulls the page-locked staging buffer (the host's
+// RunDesc, then the control ops and their lanes) into device memory through
+// the device mapping.  Sizes come from the staged descriptor, so the launch
+// is the same every run (grid-stride).
+__global__ void k_h2d(const u8 *__restrict__ stage, RunDesc *__restrict__ dDesc, DevEvent *__restrict__ dEv,
+                      u32 *__restrict__ dLane) {
+  const RunDesc *h = reinterpret_cast<const RunDesc *>(stage);
+  const u32 nev = h->nev, cap = h->evCap;
+  const u64 nA = u64(nev) * (sizeof(DevEvent) / 4), nB = nev;
+  const u32 *sA = reinterpret_cast<const u32 *>(stage + sizeof(RunDesc));
+  const u32 *sB = reinterpret_cast<const u32 *>(stage + sizeof(RunDesc) + u64(cap) * sizeof(DevEvent));
+  u32 *dA = reinterpret_cast<u32 *>(dEv);
   const u64 stride = u64(gridDim.x) * blockDim.x;
-  for (u64 i = u64(blockIdx.x) * blockDim.x + threadIdx.x; i < nA + nB; i += stride) {
+  const u64 t = u64(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t < sizeof(RunDesc) / 4) reinterpret_cast<u32 *>(dDesc)[t] = reinterpret_cast<const u32 *>(h)[t];
+  for (u64 i = t; i < nA + nB; i += stride) {
     if (i < nA)
       dA[i] = sA[i];
     else
-      dB[i - nA] = sB[i - nA];
+      dLane[i - nA] = sB[i - nA];
   }
 }
 
-hipError_t launch_h2d(hipStream_t s, void *dstA, const void *srcA, size_t nA, void *dstB, const void *srcB,
-                      size_t nB) {
-  const u64 words = (nA + nB) / 4;
-  if (!words) return hipSuccess;
-  const u32 grid = u32(std::min<u64>((words + 255) / 256, 1024));
-  hipLaunchKernelGGL(k_h2d, dim3(grid), dim3(256), 0, s, static_cast<u32 *>(dstA), static_cast<const u32 *>(srcA),
-                     u64(nA / 4), static_cast<u32 *>(dstB), static_cast<const u32 *>(srcB), u64(nB / 4));
+hipError_t launch_h2d(hipStream_t s, const uint8_t *stage, RunDesc *dDesc, DevEvent *dEv, uint32_t *dLane) {
+  hipLaunchKernelGGL(k_h2d, dim3(256), dim3(256), 0, s, stage, dDesc, dEv, dLane);
   return hipGetLastError();
 }
 

@@ -359,6 +359,24 @@ struct IngDD {  // k_ing_stream -> k_ing_out: one datagram's ExtDependencyDescri
   uint64_t pad2;
 };
 
+// Per-run batch descriptor: what changes from one lkf_run to the next for
+// the prep-stage kernels (batch pointers, length, control-op count).  The host
+// writes it at the head of the run's page-locked staging buffer; the run's
+// first kernel (k_h2d) pulls it into device memory with the control ops, and
+// the kernels after it read it there — so the prep stage is the same kernel
+// sequence every run and is replayed as one HIP graph.
+struct alignas(16) RunDesc {
+  uint64_t pkts;   // const lkf_pkt *
+  uint64_t arena;  // const uint8_t *
+  uint64_t dd;     // const lkf_pkt_dd * (0: none)
+  uint64_t nDev;   // const uint64_t *: the batch length on the device (an ingest), or 0
+  uint32_t n;      // packets (with nDev: the launch bound)
+  uint32_t nev;    // control ops staged behind the descriptor
+  uint32_t evCap;  // staging capacity (ops): the lane list starts at 64 + 48 * evCap
+  uint32_t pad[5];
+};
+static_assert(sizeof(RunDesc) == 64, "RunDesc is 64 B");
+
 struct DevEvent {  // one queued lkf_ctl op (48 B)
   uint32_t at;
   int32_t op;

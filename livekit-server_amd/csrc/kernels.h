@@ -77,7 +77,7 @@ hipError_t read_wtime(uint32_t *out, uint32_t nwaves);  // LKF_WTIME builds
 hipError_t launch_batch_init(hipStream_t s, uint32_t ntracks, uint32_t ndts, uint32_t nstats, uint32_t *tBegin,
                              uint32_t *tEnd, uint32_t *tRuns, uint32_t *err, uint64_t *stats, uint32_t *fwdCnt,
                              uint64_t *fwdBytes);
-hipError_t launch_track_ranges(hipStream_t s, const lkf_pkt *pkts, uint32_t n, const uint64_t *nDev, uint32_t ntracks,
+hipError_t launch_track_ranges(hipStream_t s, const RunDesc *desc, uint32_t maxPkts, uint32_t ntracks,
                                uint32_t *tBegin, uint32_t *tEnd, uint32_t *tRuns, uint32_t *err);
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t *tBegin, const uint32_t *tEnd,
                        const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
@@ -135,18 +135,16 @@ struct SpeakersLaunch {
 hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a);
 hipError_t launch_speakers(hipStream_t s, const SpeakersLaunch &a);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
-hipError_t launch_layer_index(hipStream_t s, const lkf_pkt *pkts, const uint32_t *tBegin, const uint32_t *tEnd,
+hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                               uint32_t ntracks, uint32_t stride, uint32_t *list, uint32_t *before, uint32_t *cnt);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
-hipError_t launch_dd_decode(hipStream_t s, const lkf_pkt *pkts, const lkf_pkt_dd *dds, const uint8_t *arena,
-                            const uint32_t *tBegin, const uint32_t *tEnd, const DevTrack *tracks, uint32_t ntracks,
-                            DDStruct *structs, DDTrack *ddTracks, DDPkt *out, uint32_t *err);
-// pulls two pinned host buffers (device-visible) into device memory with one
-// kernel (sizes multiples of 4 B); replaces two hipMemcpyAsync calls per run
-hipError_t launch_h2d(hipStream_t s, void *dstA, const void *srcA, size_t nA, void *dstB, const void *srcB, size_t nB);
+hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
+                            const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,
+                            uint32_t *err);
+hipError_t launch_h2d(hipStream_t s, const uint8_t *stage, RunDesc *dDesc, DevEvent *dEv, uint32_t *dLane);
 hipError_t launch_stats_reduce(hipStream_t s, uint64_t *stats);
 // dense per-lane op offsets from the lane-sorted op list: off[l] = first op with lane >= l
-hipError_t launch_ev_offsets(hipStream_t s, const uint32_t *laneOf, uint32_t nev, uint32_t nl, uint32_t *off);
+hipError_t launch_ev_offsets(hipStream_t s, const uint32_t *laneOf, const RunDesc *desc, uint32_t nl, uint32_t *off);
 hipError_t launch_accumulate(hipStream_t s, const uint64_t *stats, const uint64_t *tot, uint64_t *cum,
                              const uint32_t *err, uint32_t *sticky);
 hipError_t launch_err_fold(hipStream_t s, const uint32_t *err, uint32_t *sticky, uint32_t shift);
@@ -285,7 +283,7 @@ __host__ __device__ inline void tracker_frame_reset_fps(TrackerState &t) {
   t.estFps = 0.0;
   tracker_frame_eval_interval(t);
 }
-hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const lkf_pkt *pkts,
+hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const RunDesc *desc,
                                   const uint32_t *tBegin, const uint32_t *tEnd);
 hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
                                int64_t elapsedNs, int64_t nowNs, lkf_tracker_status *out);

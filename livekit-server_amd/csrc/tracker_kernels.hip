@@ -33,8 +33,9 @@ __device__ __forceinline__ void notify(TrackerState &s) {  // maybeNotifyStatus 
   }
 }
 
-__global__ void __launch_bounds__(64) k_tracker_observe(TrackerState *st, u32 n, const lkf_pkt *__restrict__ pkts,
+__global__ void __launch_bounds__(64) k_tracker_observe(TrackerState *st, u32 n, const RunDesc *__restrict__ desc,
                                                         const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd) {
+  const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
   const u32 k = blockIdx.x;
   if (k >= n) return;
   TrackerState s = st[k];  // (wave-uniform)
@@ -189,10 +190,10 @@ __global__ void k_tracker_tick(TrackerState *st, const int32_t *__restrict__ ids
 }
 }  // namespace
 
-hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const lkf_pkt *pkts,
+hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const RunDesc *desc,
                                   const uint32_t *tBegin, const uint32_t *tEnd) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_tracker_observe, dim3(n), dim3(64), 0, s, st, n, pkts, tBegin, tEnd);
+  hipLaunchKernelGGL(k_tracker_observe, dim3(n), dim3(64), 0, s, st, n, desc, tBegin, tEnd);
   return hipGetLastError();
 }
 hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
