@@ -367,8 +367,8 @@ __device__ inline int structure_bits(const DDStruct &s) {
 
 // Marshal (activeChains = all): writes the descriptor to out (zeroed here),
 // returns its length in bytes, or -1 (error: the selector drops the frame).
-__device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive, u32 active,
-                                 u8 *out) {
+__device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
+                                              u32 active, u8 *out, int cap) {
   // findBestTemplate
   int first = -1;
   for (int i = 0; i < s.numTmpl; i++)
@@ -396,7 +396,7 @@ __device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDP
     if (writeActive) vbits += s.numDT;
   }
   const int nbytes = (vbits + 7) / 8;
-  if (nbytes > kDDMaxBytes) return -1;
+  if (nbytes > kDDMaxBytes || nbytes > cap) return -1;  // (cap: the caller's buffer; see svc_run)
   for (int i = 0; i < nbytes; i++) out[i] = 0;
   BitW w(out, nbytes);
   int e = 0;
@@ -471,6 +471,10 @@ __device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDP
     }
   }
   return e ? -1 : nbytes;
+}
+__device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
+                                                   u32 active, u8 *out) {
+  return dd_marshal_inl(s, p, frameNumber, hasActive, active, out, kDDMaxBytes);
 }
 
 // ---- selector ------------------------------------------------------------------

@@ -178,7 +178,7 @@ struct lkf_engine {
   DDState *dDDState = nullptr;    // per DownTrack
   size_t ddStateInit = 0;         // DownTracks whose DDState is zeroed
   uint32_t ddTrackInit = 0;
-  std::vector<uint8_t> dtIsDD;    // per DownTrack: scheduled in k_decide_dt<true>
+  std::vector<uint8_t> dtIsDD;    // per DownTrack: SVC (DD selector or VP9), scheduled in k_decide_dt<true>
   uint32_t ddLanes = 0;
   // ingress DependencyDescriptorParser per DD stream (allocated with the first)
   uint32_t nDDStreams = 0, ddStreamInit = 0;
@@ -816,7 +816,11 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
   e->dtp.push_back(*p);
   e->active.push_back(1);
   e->seqRM.push_back(0);
-  e->dtIsDD.push_back(track_has_dd(e->tracks[p->track]) ? 1 : 0);
+  {  // DD selector and VP9 SVC DownTracks: k_decide_dt<true> (svc_run)
+    const lkf_track_params &tp = e->tracks[p->track];
+    const bool vp9 = tp.kind == LKF_KIND_VIDEO && tp.codec == LKF_CODEC_VP9;
+    e->dtIsDD.push_back((track_has_dd(tp) || vp9) ? 1 : 0);
+  }
   e->pendHot.emplace_back();
   init_hot(e->pendHot.back(), e->tracks[p->track], *p);
   DevDT d;
@@ -979,15 +983,16 @@ static int rebuild_sched(lkf_engine *e) {
   std::stable_sort(order.begin(), order.end(),
                    [&](uint32_t a, uint32_t b) { return e->tracks[a].kind > e->tracks[b].kind; });
   // Two parts: DownTracks of the plain selectors (k_decide_dt<false>), then
-  // those of the dependency-descriptor selector (k_decide_dt<true>), each
-  // interleaved per XCD.
+  // the SVC ones (dependency-descriptor or VP9 selector) and those whose
+  // sequencer holds padding exclusions (k_decide_dt<true>), each interleaved
+  // per XCD.
   std::vector<uint32_t> sched, waveTrack;
   e->ddLanes = 0;
   for (int part = 0; part < 2; part++) {
     std::vector<uint32_t> ps, pt;
     for (uint32_t t : order) {
       for (uint32_t d : byTrack[t]) {  // one wave per DownTrack (interleaved per XCD below)
-        if ((e->trackDD[t] != 0xffffffffu || e->seqRM[d]) != (part == 1)) continue;
+        if ((e->dtIsDD[d] || e->seqRM[d]) != (part == 1)) continue;
         ps.push_back(d);
         pt.push_back(t);
       }
@@ -1129,7 +1134,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     for (auto &k : ka) kb[cnt[(k.first >> shift) & 0xff]++] = k;
     ka.swap(kb);
   }
-  if (nev > x.stageCap) {  // (graphs captured with the old staging are re-captured)
+  if (nev > x.stageCap || !x.stage) {  // (graphs captured with the old staging are re-captured)
     stage_free(&x.stage, &x.stageDev);
     x.stageCap = uint32_t(std::max<size_t>(2 * nev, 4096));
     HIPCHK(stage_alloc(&x.stage, &x.stageDev, sizeof(RunDesc) + size_t(x.stageCap) * (sizeof(DevEvent) + 4)),

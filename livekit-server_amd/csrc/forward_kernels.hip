@@ -1915,6 +1915,347 @@ __global__ void __launch_bounds__(64) k_layer_index(const RunDesc *__restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// SVC runs (F_DD / F_VP9 DownTracks).  One SSRC carries every layer, so each
+// packet is relevant to the layer selector: a packet it does not select still
+// advances the munger at the highest SN (forwarder.go:1694-1702 ->
+// rtpmunger.go:156-181), the prefix-count shape of a VP8 temporal drop.  In
+// the steady state (current layers = the selector's choice, no switch, no
+// chain break, no structure or active-target update, contiguous packets) the
+// selector's decision for a packet is a function of the packet and the state
+// at the run start:
+//   VP9.Select (videolayerselector/vp9.go:43-109, no switch pending): selected
+//   iff the packet is not above the current spatial / temporal layer;
+//   DependencyDescriptor.Select (dependencydescriptor.go:65-355): the decode
+//   target the state selects (uniform over the run) and the frame's DTI for
+//   it; a frame already dropped drops its later packets (GetDecision); the
+//   chains and frame references are verified against the decision cache at
+//   the run start plus the decisions of the run's earlier frames.
+// The longest prefix of lanes meeting these conditions is decided together;
+// the first lane that does not goes through decide_step (the full
+// restatement), as in the simulcast runs.
+// ---------------------------------------------------------------------------
+constexpr int kSvcDDBytes = 48;  // per-lane marshal buffer (a descriptor without a structure fits)
+constexpr int kSvcFrames = 72;   // frame decisions of one run: frame cLast + up to 64 new frames
+
+template <bool DDK>
+__device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 pi, u32 n, u32 pos, u32 nextAt, bool valid,
+                       i32 &sentAcc, u8 *sScr, u8 *sFD) {
+  const u32 lane = lane_id();
+  const u64 lt = (1ull << lane) - 1;
+  const u32 fl = L.h.flags;
+  const bool inWin = valid && lane >= pos && pi < nextAt;
+  const bool dd = DDK && (fl & F_DD);
+  // ---- wave-uniform preconditions
+  bool uni = (fl & F_STARTED) && (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && !(fl & (F_MUTED | F_PUBMUTED)) &&
+             L.h.tgtS != INVALID && L.h.tgtT != INVALID && L.h.curS != INVALID && L.h.curT != INVALID &&
+             !((fl & F_DEFICIENT) && L.h.tgtS < L.h.curS) && L.h.lastSSRC != 0;
+  const DDStruct *s = nullptr;
+  int hiPos = -1, maxTgt = -1;
+  u32 hiTarget = 0;
+  if (DDK && dd) {
+    const DDState &d = *L.dd;
+    uni = uni && (d.flags & DS_KF_VALID) && (d.flags & DS_CACHE_INIT) && (d.flags & DS_FN_INIT);
+    for (int c = 0; c < int(d.numChains); c++) uni = uni && d.expCount[c] == 0;  // (no chain waits: c_fire is a no-op)
+    s = L.ddRing + d.slot;
+    // the decode target Select picks (:133-176): uniform while no chain breaks
+    for (int i = 0; uni && i < int(d.numTargets); i++) {
+      if (!((d.dtActive >> i) & 1) || i32(s->dtS[i]) > L.h.tgtS || i32(s->dtT[i]) > L.h.tgtT) continue;
+      const int target = s->dtTarget[i];
+      maxTgt = max(maxTgt, target);
+      if (d.numChains == 0 || !((d.chBroken >> s->protectedBy[target]) & 1)) {
+        hiPos = i;
+        hiTarget = u32(target);
+        break;
+      }
+    }
+    if (hiPos >= 0) uni = uni && i32(s->dtS[hiPos]) == L.h.curS && i32(s->dtT[hiPos]) == L.h.curT;  // no switch
+  } else {
+    uni = uni && L.h.curS == L.h.tgtS && L.h.curT == L.h.tgtT;  // vp9.go:52: no switch pending
+  }
+  if (!uni) return pos;
+  // ---- per lane: every lane of the run advances the munger, in order
+  const int prevLane = int((lane + 63u) & 63u);
+  const u64 pEsn = sh64(p.esn, prevLane);
+  const u64 prevEsn = lane > pos ? pEsn : L.h.extHighestIncomingSN;
+  bool good = inWin && p.plen != 0 && p.ssrc == L.h.lastSSRC && p.esn == prevEsn + 1;
+  bool fwd = false, mk = false;
+  int ddLen = 0;
+  u64 ddEfn = 0;
+  bool ddNew = false, ddPut = false;
+  if (!dd) {  // VP9.Select with the current layers at the target
+    const bool E = p.vp9 & LKF_VP9_E, P = p.vp9 & LKF_VP9_P;
+    const i32 pS = p.spatial, pT = p.temporal;
+    good = good && (p.flags & LKF_PKT_VP9);
+    fwd = !(pS > L.h.curS || (pS == L.h.curS && pT > L.h.curT));
+    mk = (p.hdr1 & 0x80) || (E && pS == L.h.curS && (P || L.h.tgtS <= L.h.curS));
+  } else if (DDK) {
+    DDState &d = *L.dd;
+    DDPkt dp = {};
+    const bool hasDD = inWin && (p.flags & LKF_PKT_DD) && L.ddPkts;
+    if (hasDD) dp = L.ddPkts[pi];
+    good = good && hasDD && (dp.flags & DP_VALID);
+    const u64 cl0 = d.cLast;
+    const u64 efn = dp.extFN;
+    const u64 pEfnL = sh64(efn, prevLane);
+    const u64 pEfn = lane > pos ? pEfnL : cl0;
+    good = good && (efn == pEfn || efn == pEfn + 1);  // frames in order, none skipped
+    const u64 fi = efn - cl0;                         // the frame's index in the run (0: frame cLast)
+    const bool newF = efn != pEfn;
+    // the tentative decision: the selected decode target's DTI (:160-190)
+    const u32 dti = hiPos >= 0 ? dd::dti_at(dp.dtis, int(hiTarget)) : 0u;
+    const bool t0 = hiPos >= 0 && dti != 0;
+    good = good && (maxTgt < 0 || int(dp.ndti) > maxTgt);  // (DecodeTarget.OnFrame errors: serial)
+    const u64 newM = __ballot(inWin && newF);
+    const u64 upto = newM & (lt | (1ull << lane));
+    const u32 head = (fi == 0 || !upto) ? pos : u32(63 - __clzll(upto));  // the frame's first lane in the run
+    const bool t0Head = sh32(u32(t0), int(head)) != 0;
+    const u32 cache0 = dd::c_get(d, cl0);
+    // GetDecision -> dropped: the packet returns before any state change (:86-95)
+    const bool early = fi == 0 ? (cache0 == dd::SD_DROPPED || (lane != head && !t0Head)) : (lane != head && !t0Head);
+    const bool eval = !early;
+    fwd = eval && t0;
+    good = good && (early || lane == head || t0);  // (a later packet dropping a forwarded frame: serial)
+    good = good && (early || (!(dp.flags & DP_ATTACHED) &&
+                              !(dp.extFlags & (LKF_DD_STRUCTURE_UPDATED | LKF_DD_ACTIVE_UPDATED)) &&
+                              dp.extKFN == d.extKeyFrameNum && int(dp.nchain) == int(d.numChains)));
+    good = good && (!fwd || (dp.extFlags & LKF_DD_INTEGRITY));
+    // decisions of the run's frames (lookups by later lanes)
+    if (inWin && fi < u64(kSvcFrames) && (lane == head || (lane == pos && fi != 0))) {
+      if (lane == pos && fi != 0) sFD[0] = u8(cache0);  // frame cLast keeps its cached decision
+      if (lane == head) sFD[fi] = u8((fi == 0 && cache0 == dd::SD_DROPPED) ? dd::SD_DROPPED
+                                     : (t0 ? dd::SD_FORWARDED : dd::SD_DROPPED));
+    }
+    wave_lds_sync();
+    auto dec = [&](u64 e) -> u32 {  // GetDecision(e) as this packet sees it (e < efn)
+      if (e >= cl0 && e < efn) return sFD[e - cl0];
+      bool old;
+      return dd::c_decision(d, e, old);
+    };
+    if (eval && good) {  // FrameChain.OnFrame (framechain.go:43-92): every active chain stays intact
+      for (int c = 0; c < int(d.numChains); c++) {
+        if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c) continue;
+        const u32 diff = u32(dp.chainDiffs >> (8 * c)) & 0xff;
+        const bool broken = (d.chBroken >> c) & 1;
+        if (diff == 0) {
+          good = good && !broken;  // (a broken chain restarting: serial)
+          continue;
+        }
+        if (!broken && dec(efn - diff) != dd::SD_FORWARDED) good = false;
+      }
+    }
+    if (fwd && good)  // a referenced frame that was dropped drops this one (:192-201): serial
+      for (int j = 0; j < int(dp.nfd) && j < kDDFdiffs; j++)
+        if (dp.fd[j] != 0 && dec(efn - dp.fd[j]) == dd::SD_DROPPED) good = false;
+    if (fwd && good) {
+      // frame number (FrameNumberWrapper without a structure update) and the
+      // descriptor marshalled with the active mask in force (:223-262)
+      const bool hasMask = d.flags & DS_HAS_MASK;
+      const bool hasActive = (dp.flags & DP_ACTIVE) || hasMask;
+      const u32 active = hasMask ? d.mask : dp.activeMask;
+      ddLen = dd::dd_marshal_inl(*s, dp, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
+                             kSvcDDBytes);
+      if (ddLen < 0) good = false;
+      mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
+    }
+    ddEfn = efn;
+    ddNew = newF;
+    ddPut = eval && lane == head;
+  }
+  // ---- munger / sequencer conditions (as in the simulcast runs)
+  const u64 dropM = __ballot(inWin && !fwd);
+  const u64 fwdM = __ballot(inWin && fwd);
+  const u64 snOff = L.h.snOffset + u64(__popcll(dropM & lt));
+  const u64 osn = p.esn - snOff;
+  const u64 ots = p.ets - L.h.tsOffset;
+  const int pf = prev_in(fwdM, lt);
+  const int pfs = pf >= 0 ? pf : int(lane);
+  const u64 pfOsn = sh64(osn, pfs), pfOts = sh64(ots, pfs);
+  const u64 prevOsn = pf >= 0 ? pfOsn : L.h.seqExtHighestSN;
+  const u64 hiTS = pf >= 0 ? pfOts : L.h.seqExtHighestTS;
+  if (fwd) good = good && ots >= hiTS && osn == prevOsn + 1 && osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
+  else good = good && L.h.snOffset == L.h.rmOpenValue;  // (a drop moves the open range: rtpmunger.go:156-181)
+  const u64 stopM = __ballot(inWin ? !good : (valid && lane >= pos));
+  const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+  if (x <= pos) return pos;
+  const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
+  const bool inRun = (runM >> lane) & 1;
+  if (DDK && dd) {
+    // decision cache (selectordecisioncache.go:112-165) for the frames of the
+    // run: each frame's first evaluated packet sets its entry, and a new frame
+    // marks the entry kNack behind the previous last frame missing if it is
+    // still unknown (read at the run-start state: it lies before the run)
+    DDState &d = *L.dd;
+    const bool put = inRun && ddPut && ddEfn > d.cBase;
+    u64 missE = 0;
+    bool miss = false;
+    if (inRun && ddNew) {
+      const u64 ms0 = ddEfn - 1, me0 = ddEfn;
+      const u64 ms = ms0 > dd::kNack + d.cBase ? ms0 - dd::kNack : d.cBase;
+      const u64 me = me0 > dd::kNack + d.cBase ? me0 - dd::kNack : d.cBase;
+      if (me > ms && dd::c_get(d, ms) == dd::SD_UNKNOWN) {
+        miss = true;
+        missE = ms;
+      }
+    }
+    wave_lds_sync();
+    if (put) {
+      const u64 off = (ddEfn - d.cBase) % dd::kEntries;
+      const u32 bp = u32(off & 31) * 2;
+      unsigned long long *w = reinterpret_cast<unsigned long long *>(&d.masks[off >> 5]);
+      atomicAnd(w, ~(3ull << bp));
+      atomicOr(w, u64(fwd ? dd::SD_FORWARDED : dd::SD_DROPPED) << bp);
+    }
+    if (miss) {
+      const u64 off = (missE - d.cBase) % dd::kEntries;
+      const u32 bp = u32(off & 31) * 2;
+      unsigned long long *w = reinterpret_cast<unsigned long long *>(&d.masks[off >> 5]);
+      atomicAnd(w, ~(3ull << bp));
+      atomicOr(w, u64(dd::SD_MISSING) << bp);
+    }
+    wave_lds_sync();
+    const u32 lastL = 63 - __clzll(runM);
+    const u64 eLast = rl64(ddEfn, lastL);  // frames are in order: the run's last is its highest
+    const u64 fM = __ballot(inRun && fwd);
+    const u64 eF = fM ? rl64(ddEfn, 63 - __clzll(fM)) : 0;
+    wave_lds_sync();
+    if (eLast > d.cLast) d.cLast = eLast;
+    if (fM && eF > d.fnLast) d.fnLast = eF;  // FrameNumberWrapper.UpdateAndGet of the forwarded frames
+    wave_lds_sync();
+  }
+  // ---- decide lanes [pos, x)
+  const u64 fwR = fwdM & runM, tdR = dropM & runM;
+  const bool f = inRun && fwd;
+  o.nTuples += x - pos;
+  o.drops[LKF_DROP_NOT_SELECTED] += u32(__popcll(tdR));
+  // output shape (downtrack.go:693-723, pacer/base.go:71-100): DD element first
+  const int cc = p.hdr0 & 0xf;
+  const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
+  const bool ddOn = DDK && f && ddLen > 0 && L.extDD;
+  const int eh = (ddOn && ddLen > 16) ? 2 : 1;
+  const int extBytes = (ddOn ? eh + ddLen : 0) + (playout ? eh + 3 : 0) + (L.extAbs ? eh + 3 : 0);
+  const int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
+  const int hdrLen = 12 + 4 * cc + extBlock;
+  const u32 outLen = f ? u32(hdrLen + int(p.plen)) : 0u;
+  const u32 aligned = (outLen + 15) & ~15u;
+  const u32 relEx = excl_scan_u32(aligned, lane);
+  bool ddKeep = ddOn;
+  u32 ddOff = 0;
+  if (DDK && dd) {  // the run's marshalled descriptors: one bump of the batch's DD arena
+    const u32 dl = ddOn ? u32(ddLen) : 0u;
+    const u32 dEx = excl_scan_u32(dl, lane);
+    const u32 dTot = rl32(dEx + dl, 63);
+    if (dTot) {
+      u64 base = 0;
+      if (lane == 0) base = atomicAdd(reinterpret_cast<unsigned long long *>(o.ddUsed), (unsigned long long)dTot);
+      base = rl64(base, 0);
+      if (base + dTot > o.ddCap) {
+        if (lane == 0) atomicOr(L.err, 8u);
+        ddKeep = false;
+      } else if (ddOn) {
+        for (int i = 0; i < ddLen; i++) o.ddArena[base + dEx + u64(i)] = sScr[lane * kSvcDDBytes + u32(i)];
+        ddOff = u32(base + dEx);
+      }
+    }
+  }
+  const bool kf = p.flags & LKF_PKT_KEYFRAME;
+  const u32 j = u32(__popcll(fwR & lt));
+  if (f) {
+    Tuple t;
+    t.extSN = osn;
+    t.extTS = ots;
+    t.pkt = pi;
+    t.relOff = o.relOff + relEx;
+    t.outLen = u16(outLen);
+    t.flags = u8((kf ? LKF_OUT_KEYFRAME : 0) | (mk ? LKF_OUT_MARKER : 0) | (playout ? T_PLAYOUT : 0) |
+                 (ddKeep ? T_DD : 0));
+    t.layer = p.layer;
+    t.codecLen = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) t.codec[i] = 0;
+    t.hdrLen = u16(hdrLen);
+    t.ddLen = ddKeep ? u8(ddLen) : 0;
+    t.pad0 = 0;
+    t.ddOff = ddKeep ? ddOff : 0;
+    t.pad1 = 0;
+#if LKF_CHECKED
+    CHK(o.tupBase + o.nFwd + j < o.tupCap, CK_DEC_TUPLE, o.tupBase + o.nFwd + j, o.tupCap);
+#endif
+    store_rec(o.outT + o.nFwd + j, t);
+    u32 slot = u32(L.h.seqHighSlot) + u32(osn - L.h.seqExtHighestSN);  // sequencer.push, in order
+    while (slot >= L.seqSize) slot -= L.seqSize;
+    SeqMeta m = {};
+    m.sourceSeqNo = u16(p.esn);
+    m.targetSeqNo = u16(osn);
+    m.timestamp = u32(ots);
+    m.lastNack = u32(p.arr / 1000000LL - L.h.seqStartMs);
+    m.marker = mk;
+    m.layer = p.layer;
+    m.codecLen = 0;
+    CHK(slot < L.seqSize, CK_DEC_SEQ, slot, L.seqSize);
+    store_rec(L.seq + slot, m);
+  }
+  const u32 sumLen = wave_sum_u32(outLen);
+  sentAcc += f ? i32(p.poff) - hdrLen : 0;
+  if (fwR) {
+    o.nBytes += sumLen;
+    o.nFwd += u32(__popcll(fwR));
+    const u32 lastF = 63 - __clzll(fwR);
+    u32 slot = u32(L.h.seqHighSlot) + u32(rl64(osn, lastF) - L.h.seqExtHighestSN);
+    while (slot >= L.seqSize) slot -= L.seqSize;
+    L.h.seqHighSlot = u16(slot);
+    L.h.seqExtHighestSN = rl64(osn, lastF);
+    L.h.seqExtHighestTS = rl64(ots, lastF);
+  }
+  // munger past the run: every lane was an UpdateAndGetSnTs, the drops were
+  // PacketDropped right after theirs
+  const u32 lastSel = 63 - __clzll(runM);
+  const u64 mkM = __ballot(mk);
+  L.h.extHighestIncomingSN = rl64(p.esn, lastSel);
+  const bool lastIsF = (fwR >> lastSel) & 1;
+  const u64 pfM = fwR & ((1ull << lastSel) - 1);
+  u64 sSN = L.h.extLastSN, sTS = L.h.extLastTS;
+  bool sMk = fl & F_LAST_MARKER;
+  if (pfM) {
+    const u32 b = 63 - __clzll(pfM);
+    sSN = rl64(osn, b);
+    sTS = rl64(ots, b);
+    sMk = (mkM >> b) & 1;
+  }
+  if (lastIsF) {
+    L.h.extSecondLastSN = sSN;
+    L.h.extSecondLastTS = sTS;
+    L.h.extLastSN = rl64(osn, lastSel);
+    L.h.extLastTS = rl64(ots, lastSel);
+    setf(L, F_SECOND_LAST_MARKER, sMk);
+    setf(L, F_LAST_MARKER, (mkM >> lastSel) & 1);
+  } else {
+    L.h.extSecondLastSN = L.h.extLastSN = sSN;
+    L.h.extSecondLastTS = L.h.extLastTS = sTS;
+    setf(L, F_SECOND_LAST_MARKER, sMk);
+    setf(L, F_LAST_MARKER, sMk);
+  }
+  if (hasf(L, F_RTX_GATE) && (rl64(osn, lastSel) - L.h.extRtxGateSn) > 2000) setf(L, F_RTX_GATE, false);
+  const u64 kfM = __ballot(inRun && kf);
+  if (kfM) {
+    L.h.extRtxGateSn = rl64(osn, 63 - __clzll(kfM));
+    setf(L, F_RTX_GATE, true);
+  }
+  u64 m = tdR;  // one exclusion per run of consecutive drops
+  while (m) {
+    const u32 b = u32(__ffsll((long long)m) - 1);
+    const u64 after = fwR & ~((2ull << b) - 1);
+    const u32 nf = after ? u32(__ffsll((long long)after) - 1) : 64u;
+    const u64 runD = tdR & (nf >= 64 ? ~0ull : ((1ull << nf) - 1)) & ~((1ull << b) - 1);
+    const u64 s0 = rl64(p.esn, b);
+    rm_exclude(L, s0, s0 + u64(__popcll(runD)));
+    m &= ~runD;
+  }
+  if (tdR) L.h.snOffset = L.h.rmOpenValue;
+  if (fwR) o.relOff += rl32(relEx + aligned, 63 - __clzll(fwR));
+  return x;
+}
+
 template <bool DDK>
 __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
   __shared__ i32 sDrop[kSetCap];
@@ -1924,6 +2265,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __shared__ RangeEntry sRm[kRangeCap];
   // (the plain instantiation keeps a 16-B stub: LDS is allocated per instantiation)
   __shared__ __attribute__((aligned(16))) u8 sDDRaw[DDK ? sizeof(DDState) + kDDMaxBytes + 1 : 16];
+  __shared__ u8 sSvcScr[DDK ? 64 * kSvcDDBytes : 16];  // svc_run: per-lane marshalled descriptors
+  __shared__ u8 sSvcFD[kSvcFrames];                    // svc_run: decisions of the run's frames
   DDState *const sDD = reinterpret_cast<DDState *>(sDDRaw);
   u8 *const sDDBuf = sDDRaw + (DDK ? sizeof(DDState) : 0);
 #if LKF_DIAG
@@ -2083,6 +2426,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     __syncthreads();
   }
   o.outT = A.tuples + slot0;
+  // SVC DownTracks (one SSRC, every packet relevant to the selector): svc_run
+  // (the host schedules them in k_decide_dt<true>)
+  const bool svcDT = DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
+                     ((L.h.flags & F_VP9) || ((L.h.flags & F_DD) && ddDT));
   u32 nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
 #if LKF_DIAG
@@ -2169,6 +2516,14 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         }
         vm_drain();
       }
+      u32 x;
+      bool gapStop = false;  // the stopping lane starts the next run (no full step)
+#if LKF_DIAG || LKF_WTIME
+      int why = 0;
+#endif
+      if (DDK && svcDT) {
+        x = svc_run<DDK>(L, o, p, pi, n, pos, nextAt, valid, sentAcc, sSvcScr, sSvcFD);
+      } else {
       const bool inWin = valid && lane >= pos && pi < nextAt;
       // ---- classification against the state at the start of the run
       const u32 fl = L.h.flags;
@@ -2373,7 +2728,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           inWin && ((cls == -2) || (cls == -1 && !ok && !okO) || (fwdIn && !seqOk) || (okO && !seqOkO));
 #if LKF_DIAG || LKF_WTIME
       // serial-step trigger of this lane (read at the stopping lane below)
-      int why = 0;
+      why = 0;
       if (cls == -2)
         why = whyKf ? 16 : (!(fl & F_SIMULCAST) ? 17 : 18);
       else if (cls == -1 && !ok && !okO) {
@@ -2388,7 +2743,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         why = 27;
 #endif
       const u64 stopM = __ballot(bad || (valid && lane >= pos && !inWin));
-      u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+      x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
       if (tswM & ~((1ull << pos) - 1)) x = min(x, u32(__ffsll((long long)(tswM & ~((1ull << pos) - 1))) - 1) + 1u);
       // ---- decide lanes [pos, x) together
       DIAG(2, x > pos ? 1 : 0);
@@ -2614,13 +2969,15 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         }
         if (fwR) o.relOff += rl32(relEx + aligned, 63 - __clzll(fwR));
       }
+      gapStop = x < n && rl32(u32(gapLater), x) != 0;
+      }  // (simulcast / audio runs)
       pos = x;
 #if LKF_DIAG
       u64 ts0 = clock64();
       dg[12] += ts0 - tr0;
       dg[6] += ts0 - tb0;
 #endif
-      if (x < n && rl32(pi, x) < nextAt && rl32(u32(gapLater), x) == 0) {
+      if (x < n && rl32(pi, x) < nextAt && !gapStop) {
         DIAG(3, 1);
         // the packet at lane x needs the full restatement
         const uint4 a0 = make_uint4(rl32(r0.x, x), rl32(r0.y, x), rl32(r0.z, x), rl32(r0.w, x));
@@ -2838,6 +3195,9 @@ __device__ __forceinline__ uint4 shift_window(uint4 q0, uint4 q1, u32 sh) {
   v.w = align_byte(x4, x3, rb);
   return v;
 }
+#ifndef LKF_EMIT_XCD
+#define LKF_EMIT_XCD 1  // 0: plain grid-stride over the output groups (A/B)
+#endif
 __device__ __forceinline__ void store16(u8 *p, uint4 v) {
 #if LKF_EMIT_NT
   __builtin_nontemporal_store(v.x, reinterpret_cast<u32 *>(p));
@@ -2869,7 +3229,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
   // track's payloads (one per subscribing DownTrack) are adjacent, so the
   // re-reads hit that XCD's 4 MiB L2 instead of going to HBM.  (Falls back to
   // a plain grid-stride when the grid is not a multiple of 8.)
-  const u32 nx = (gridDim.x % 8 == 0) ? 8u : 1u;
+  const u32 nx = (LKF_EMIT_XCD && gridDim.x % 8 == 0) ? 8u : 1u;
   const u32 xcd = blockIdx.x % nx, slotInX = blockIdx.x / nx, perX = gridDim.x / nx;
   const u64 gpx = (ngroups + nx - 1) / nx;
   const u64 gBeg = u64(xcd) * gpx, gEnd = min(ngroups, gBeg + gpx);
