@@ -202,7 +202,10 @@ def main():
     plan = rooms_mod.plan_room_shards([1.0] * (world * args.rooms), world)
     trace = wl.Trace(args.config, duration_s=nb * args.batch_s, batch_s=args.batch_s, room_ids=plan[rank])
     has_dd = trace.has_dd() and not args.ingress  # (ingest produces the DD side array on the GPU)
-    eng = pkg.Engine.for_trace(trace, device=local, lib_path=os.environ.get("LKF_LIB") or None)
+    lib = os.environ.get("LKF_LIB") or None
+    if lib and os.sep not in lib:  # a name: one of the in-tree builds
+        lib = os.path.join(ROOT, "livekit-server_amd", "lib", lib)
+    eng = pkg.Engine.for_trace(trace, device=local, lib_path=lib)
     wl.load_topology(eng.api, eng.h, trace)
 
     if args.ingress:

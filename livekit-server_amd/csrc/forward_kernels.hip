@@ -35,6 +35,9 @@ namespace lkf {
 #ifndef LKF_DIAG
 #define LKF_DIAG 0  // diagnostic build: per-wave counters into g_diag (lkf_debug_counters)
 #endif
+#ifndef LKF_SVC_DIAG
+#define LKF_SVC_DIAG 0  // diagnostic build: svc_run counters into g_diag (lkf_debug_counters)
+#endif
 #ifndef LKF_WTIME
 #define LKF_WTIME 0  // diagnostic build: per-wave start/end realtime stamps (lkf_debug_wtime)
 #endif
@@ -43,8 +46,10 @@ constexpr uint32_t kWTimeWaves = 1u << 16;
 __device__ uint32_t g_wtime[kWTimeWaves * 16];  // start, end (100 MHz ticks), packets, serial steps | chunks << 16,
                                                // cycles: prologue, serial steps, drains after them, total
 #endif
-#if LKF_DIAG
+#if LKF_DIAG || LKF_SVC_DIAG
 __device__ unsigned long long g_diag[32];  // [16..31]: serial-step triggers
+#endif
+#if LKF_DIAG
 struct DiagTimer {  // adds elapsed cycles of a scope to g_diag[slot] (lane 0)
   int slot;
   uint64_t t0;
@@ -1973,12 +1978,25 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   } else {
     uni = uni && L.h.curS == L.h.tgtS && L.h.curT == L.h.tgtT;  // vp9.go:52: no switch pending
   }
+#if LKF_SVC_DIAG
+  if (lane == 0) atomicAdd(&g_diag[0], 1ull);
+  if (!uni) {
+    if (lane == 0) atomicAdd(&g_diag[4], 1ull);
+    return pos;
+  }
+  u32 why = 0;
+#define SVC_WHY(c) \
+  if (!good && why == 0) why = (c)
+#else
   if (!uni) return pos;
+#define SVC_WHY(c)
+#endif
   // ---- per lane: every lane of the run advances the munger, in order
   const int prevLane = int((lane + 63u) & 63u);
   const u64 pEsn = sh64(p.esn, prevLane);
   const u64 prevEsn = lane > pos ? pEsn : L.h.extHighestIncomingSN;
   bool good = inWin && p.plen != 0 && p.ssrc == L.h.lastSSRC && p.esn == prevEsn + 1;
+  SVC_WHY(1);
   bool fwd = false, mk = false;
   int ddLen = 0;
   u64 ddEfn = 0;
@@ -1987,6 +2005,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     const bool E = p.vp9 & LKF_VP9_E, P = p.vp9 & LKF_VP9_P;
     const i32 pS = p.spatial, pT = p.temporal;
     good = good && (p.flags & LKF_PKT_VP9);
+    SVC_WHY(2);
     fwd = !(pS > L.h.curS || (pS == L.h.curS && pT > L.h.curT));
     mk = (p.hdr1 & 0x80) || (E && pS == L.h.curS && (P || L.h.tgtS <= L.h.curS));
   } else if (DDK) {
@@ -1995,38 +2014,59 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     const bool hasDD = inWin && (p.flags & LKF_PKT_DD) && L.ddPkts;
     if (hasDD) dp = L.ddPkts[pi];
     good = good && hasDD && (dp.flags & DP_VALID);
+    SVC_WHY(2);
     const u64 cl0 = d.cLast;
     const u64 efn = dp.extFN;
     const u64 pEfnL = sh64(efn, prevLane);
     const u64 pEfn = lane > pos ? pEfnL : cl0;
     good = good && (efn == pEfn || efn == pEfn + 1);  // frames in order, none skipped
+    SVC_WHY(3);
     const u64 fi = efn - cl0;                         // the frame's index in the run (0: frame cLast)
     const bool newF = efn != pEfn;
     // the tentative decision: the selected decode target's DTI (:160-190)
     const u32 dti = hiPos >= 0 ? dd::dti_at(dp.dtis, int(hiTarget)) : 0u;
     const bool t0 = hiPos >= 0 && dti != 0;
     good = good && (maxTgt < 0 || int(dp.ndti) > maxTgt);  // (DecodeTarget.OnFrame errors: serial)
+    SVC_WHY(4);
     const u64 newM = __ballot(inWin && newF);
     const u64 upto = newM & (lt | (1ull << lane));
     const u32 head = (fi == 0 || !upto) ? pos : u32(63 - __clzll(upto));  // the frame's first lane in the run
+    const u64 after = newM & ~((2ull << lane) - 1);
+    const u32 nextHead = after ? u32(__ffsll((long long)after) - 1) : 64u;  // the next frame's first lane
+    const u64 frameM = (nextHead >= 64 ? ~0ull : ((1ull << nextHead) - 1)) & ~((1ull << head) - 1);
     const bool t0Head = sh32(u32(t0), int(head)) != 0;
     const u32 cache0 = dd::c_get(d, cl0);
-    // GetDecision -> dropped: the packet returns before any state change (:86-95)
-    const bool early = fi == 0 ? (cache0 == dd::SD_DROPPED || (lane != head && !t0Head)) : (lane != head && !t0Head);
+    // The DTI is the frame's, so every packet of a frame gets the head's
+    // tentative decision (one that does not goes serial).  GetDecision ->
+    // dropped returns before any state change (:86-95): the packets after a
+    // frame's first dropped one, and all of frame cLast's if it is cached
+    // dropped.  A dropped frame is added to the cache by its first evaluated
+    // packet, a forwarded one by each packet with frame integrity (:245-247);
+    // forwarded packets without it leave the cache alone.
+    const bool drop0 = fi == 0 && cache0 == dd::SD_DROPPED;
+    const bool early = drop0 || (!t0Head && lane != head);
     const bool eval = !early;
     fwd = eval && t0;
-    good = good && (early || lane == head || t0);  // (a later packet dropping a forwarded frame: serial)
+    good = good && (early || t0 == t0Head);
+    SVC_WHY(5);
     good = good && (early || (!(dp.flags & DP_ATTACHED) &&
                               !(dp.extFlags & (LKF_DD_STRUCTURE_UPDATED | LKF_DD_ACTIVE_UPDATED)) &&
                               dp.extKFN == d.extKeyFrameNum && int(dp.nchain) == int(d.numChains)));
-    good = good && (!fwd || (dp.extFlags & LKF_DD_INTEGRITY));
-    // decisions of the run's frames (lookups by later lanes)
-    if (inWin && fi < u64(kSvcFrames) && (lane == head || (lane == pos && fi != 0))) {
-      if (lane == pos && fi != 0) sFD[0] = u8(cache0);  // frame cLast keeps its cached decision
-      if (lane == head) sFD[fi] = u8((fi == 0 && cache0 == dd::SD_DROPPED) ? dd::SD_DROPPED
-                                     : (t0 ? dd::SD_FORWARDED : dd::SD_DROPPED));
-    }
+    SVC_WHY(6);
+    const bool adds = inWin && eval && (!t0 || (dp.extFlags & LKF_DD_INTEGRITY));
+    const u64 addM = __ballot(adds);
+    const bool firstAdd = adds && !(addM & frameM & lt);
+    // decisions of the run's frames as later frames see them: the frame's
+    // first add, else the cached value (frame cLast) or unknown (beyond cLast)
+    if (inWin && fi < u64(kSvcFrames) && lane == head) sFD[fi] = u8(fi == 0 ? cache0 : dd::SD_UNKNOWN);
+    if (inWin && lane == pos && fi != 0) sFD[0] = u8(cache0);
     wave_lds_sync();
+    if (firstAdd && fi < u64(kSvcFrames)) sFD[fi] = u8(t0 ? dd::SD_FORWARDED : dd::SD_DROPPED);
+    wave_lds_sync();
+    // a new frame is added right after the frame before it (no gap for
+    // addEntity to fill: the serial step takes that)
+    if (firstAdd && fi >= 2 && fi < u64(kSvcFrames) && sFD[fi - 1] == dd::SD_UNKNOWN) good = false;
+    SVC_WHY(7);
     auto dec = [&](u64 e) -> u32 {  // GetDecision(e) as this packet sees it (e < efn)
       if (e >= cl0 && e < efn) return sFD[e - cl0];
       bool old;
@@ -2039,14 +2079,17 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
         const bool broken = (d.chBroken >> c) & 1;
         if (diff == 0) {
           good = good && !broken;  // (a broken chain restarting: serial)
+          SVC_WHY(8);
           continue;
         }
         if (!broken && dec(efn - diff) != dd::SD_FORWARDED) good = false;
+        SVC_WHY(8);
       }
     }
     if (fwd && good)  // a referenced frame that was dropped drops this one (:192-201): serial
       for (int j = 0; j < int(dp.nfd) && j < kDDFdiffs; j++)
         if (dp.fd[j] != 0 && dec(efn - dp.fd[j]) == dd::SD_DROPPED) good = false;
+    SVC_WHY(9);
     if (fwd && good) {
       // frame number (FrameNumberWrapper without a structure update) and the
       // descriptor marshalled with the active mask in force (:223-262)
@@ -2056,11 +2099,12 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       ddLen = dd::dd_marshal_inl(*s, dp, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
                              kSvcDDBytes);
       if (ddLen < 0) good = false;
+      SVC_WHY(10);
       mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
     }
     ddEfn = efn;
-    ddNew = newF;
-    ddPut = eval && lane == head;
+    ddNew = firstAdd && fi != 0;  // the first add of a frame beyond cLast: addEntity's new-entity path
+    ddPut = firstAdd;
   }
   // ---- munger / sequencer conditions (as in the simulcast runs)
   const u64 dropM = __ballot(inWin && !fwd);
@@ -2073,10 +2117,27 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   const u64 pfOsn = sh64(osn, pfs), pfOts = sh64(ots, pfs);
   const u64 prevOsn = pf >= 0 ? pfOsn : L.h.seqExtHighestSN;
   const u64 hiTS = pf >= 0 ? pfOts : L.h.seqExtHighestTS;
-  if (fwd) good = good && ots >= hiTS && osn == prevOsn + 1 && osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
-  else good = good && L.h.snOffset == L.h.rmOpenValue;  // (a drop moves the open range: rtpmunger.go:156-181)
+  if (fwd) {
+    good = good && ots >= hiTS && osn == prevOsn + 1 && osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
+    SVC_WHY(11);
+  } else {
+    good = good && L.h.snOffset == L.h.rmOpenValue;  // (a drop moves the open range: rtpmunger.go:156-181)
+    SVC_WHY(12);
+  }
   const u64 stopM = __ballot(inWin ? !good : (valid && lane >= pos));
   const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+#if LKF_SVC_DIAG
+  if (lane == 0) {
+    atomicAdd(&g_diag[1], x > pos ? 1ull : 0ull);
+    atomicAdd(&g_diag[2], (unsigned long long)(x - pos));
+  }
+  {
+    const u32 wx = x < n ? rl32(why, x) : 0u;
+    const bool winX = x < n && rl32(u32(inWin), x);
+    if (lane == 0) atomicAdd(&g_diag[winX ? (16 + wx) : 13], 1ull);
+  }
+#endif
+#undef SVC_WHY
   if (x <= pos) return pos;
   const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
   const bool inRun = (runM >> lane) & 1;
@@ -2114,8 +2175,8 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       atomicOr(w, u64(dd::SD_MISSING) << bp);
     }
     wave_lds_sync();
-    const u32 lastL = 63 - __clzll(runM);
-    const u64 eLast = rl64(ddEfn, lastL);  // frames are in order: the run's last is its highest
+    const u64 aM = __ballot(inRun && ddPut);
+    const u64 eLast = aM ? rl64(ddEfn, 63 - __clzll(aM)) : 0;  // frames are in order: the last added is the highest
     const u64 fM = __ballot(inRun && fwd);
     const u64 eF = fM ? rl64(ddEfn, 63 - __clzll(fM)) : 0;
     wave_lds_sync();
@@ -2153,7 +2214,17 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
         if (lane == 0) atomicOr(L.err, 8u);
         ddKeep = false;
       } else if (ddOn) {
-        for (int i = 0; i < ddLen; i++) o.ddArena[base + dEx + u64(i)] = sScr[lane * kSvcDDBytes + u32(i)];
+        // (a fixed-trip copy: a loop bounded by the per-lane length made the
+        // register allocator give this instantiation 225 VGPRs)
+        u8 *dst = o.ddArena + base + dEx;
+        const u32 *srcw = reinterpret_cast<const u32 *>(sScr + lane * kSvcDDBytes);
+#pragma unroll
+        for (int w = 0; w < kSvcDDBytes / 4; w++) {
+          const u32 v = srcw[w];
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (4 * w + b < ddLen) dst[4 * w + b] = u8(v >> (8 * b));
+        }
         ddOff = u32(base + dEx);
       }
     }
@@ -2522,7 +2593,18 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       int why = 0;
 #endif
       if (DDK && svcDT) {
+        // SVC DownTrack: a run, then the stopping packet's full step (its
+        // descriptor reloaded wave-uniform, so the chunk's raw registers are
+        // dead on this path)
         x = svc_run<DDK>(L, o, p, pi, n, pos, nextAt, valid, sentAcc, sSvcScr, sSvcFD);
+        pos = x;
+        if (x < n && rl32(pi, x) < nextAt) {
+          const u32 px = rl32(pi, x);
+          decide_step<DDK>(L, load_pkt(pkts + px), px, o);
+          vm_drain();
+          pos = x + 1;
+        }
+        continue;
       } else {
       const bool inWin = valid && lane >= pos && pi < nextAt;
       // ---- classification against the state at the start of the run
@@ -4084,7 +4166,7 @@ hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *
 // ---------------------------------------------------------------------------
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 
-#if LKF_DIAG
+#if LKF_DIAG || LKF_SVC_DIAG
 hipError_t read_diag(unsigned long long out[32], int reset) {
   hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 32);
   if (r == hipSuccess && reset) {
