@@ -2787,6 +2787,32 @@ int lkf_debug_check(lkf_engine *e, uint64_t out[4], int reset) {
   return r == hipSuccess ? LKF_OK : LKF_ENODEV;
 }
 
+// Not part of include/lkfwd.h: a DD DownTrack's selector state for debugging
+// (out[16]: cache init, base, last, masks[8], chain broken bits, chain active
+// bits, sum of chain expectations, frame-number wrapper last, current layers
+// spatial | temporal << 8 (+128 each)).
+int lkf_debug_dd_state(lkf_engine *e, int32_t dt, uint64_t out[16]) {
+  if (!e || !out || dt < 0 || size_t(dt) >= e->dtp.size() || !e->dDDState) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  DDState d;
+  DTHot h;
+  HIPCHK(hipMemcpy(&d, e->dDDState + dt, sizeof(d), hipMemcpyDeviceToHost), "dd state");
+  HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "hot state");
+  out[0] = (d.flags & DS_CACHE_INIT) ? 1 : 0;
+  out[1] = d.cBase;
+  out[2] = d.cLast;
+  for (int i = 0; i < 8; i++) out[3 + i] = d.masks[i];
+  out[11] = d.chBroken & ((1u << d.numChains) - 1);
+  out[12] = d.chActive & ((1u << d.numChains) - 1);
+  uint64_t ex = 0;
+  for (int c = 0; c < d.numChains; c++) ex += d.expCount[c];
+  out[13] = ex;
+  out[14] = (d.flags & DS_FN_INIT) ? d.fnLast : ~0ull;
+  out[15] = uint64_t(uint8_t(h.curS + 128)) | (uint64_t(uint8_t(h.curT + 128)) << 8);
+  return LKF_OK;
+}
+
 // Not part of include/lkfwd.h: per-wave stamps of the last k_decide_dt
 // (-DLKF_WTIME=1 builds): 8 words per wave slot.
 int lkf_debug_wtime(lkf_engine *e, uint32_t *out, uint32_t nwaves) {

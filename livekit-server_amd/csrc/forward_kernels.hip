@@ -35,6 +35,9 @@ namespace lkf {
 #ifndef LKF_DIAG
 #define LKF_DIAG 0  // diagnostic build: per-wave counters into g_diag (lkf_debug_counters)
 #endif
+#ifndef LKF_SVC_AB
+#define LKF_SVC_AB 0  // A/B builds of svc_run (bisection only)
+#endif
 #ifndef LKF_SVC_DIAG
 #define LKF_SVC_DIAG 0  // diagnostic build: svc_run counters into g_diag (lkf_debug_counters)
 #endif
@@ -42,12 +45,25 @@ namespace lkf {
 #define LKF_WTIME 0  // diagnostic build: per-wave start/end realtime stamps (lkf_debug_wtime)
 #endif
 #if LKF_WTIME
-constexpr uint32_t kWTimeWaves = 1u << 16;
+constexpr uint32_t kWTimeWaves = 1u << 17;
 __device__ uint32_t g_wtime[kWTimeWaves * 16];  // start, end (100 MHz ticks), packets, serial steps | chunks << 16,
                                                // cycles: prologue, serial steps, drains after them, total
 #endif
 #if LKF_DIAG || LKF_SVC_DIAG
 __device__ unsigned long long g_diag[32];  // [16..31]: serial-step triggers
+#endif
+#ifdef LKF_SVC_WATCH  // diagnostic: svc_run / full-step log of one DownTrack (read through lkf_debug_wtime)
+__device__ uint32_t g_svclog[4 * 4096];  // [0]: entries; entry i at 4 + 4i: kind, packet, x packet, why
+__device__ __forceinline__ void svclog(uint32_t d, uint32_t kind, uint32_t a, uint32_t b, uint32_t c) {
+  if (d != LKF_SVC_WATCH || (threadIdx.x & 63) != 0) return;
+  const uint32_t i = atomicAdd(&g_svclog[0], 1u);
+  if (4 + 4 * i + 3 < 4 * 4096) {
+    g_svclog[4 + 4 * i] = kind;
+    g_svclog[5 + 4 * i] = a;
+    g_svclog[6 + 4 * i] = b;
+    g_svclog[7 + 4 * i] = c;
+  }
+}
 #endif
 #if LKF_DIAG
 struct DiagTimer {  // adds elapsed cycles of a scope to g_diag[slot] (lane 0)
@@ -263,6 +279,9 @@ struct Lane {
   const DDPkt *ddPkts;
   u8 *ddBuf;
   u32 *err;
+#ifdef LKF_SVC_WATCH
+  u32 watchDt;
+#endif
 };
 
 __device__ __forceinline__ bool hasf(const Lane &L, u32 f) { return (L.h.flags & f) != 0; }
@@ -1921,50 +1940,92 @@ __global__ void __launch_bounds__(64) k_layer_index(const RunDesc *__restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// SVC runs (F_DD / F_VP9 DownTracks).  One SSRC carries every layer, so each
-// packet is relevant to the layer selector: a packet it does not select still
-// advances the munger at the highest SN (forwarder.go:1694-1702 ->
-// rtpmunger.go:156-181), the prefix-count shape of a VP8 temporal drop.  In
-// the steady state (current layers = the selector's choice, no switch, no
-// chain break, no structure or active-target update, contiguous packets) the
-// selector's decision for a packet is a function of the packet and the state
-// at the run start:
-//   VP9.Select (videolayerselector/vp9.go:43-109, no switch pending): selected
-//   iff the packet is not above the current spatial / temporal layer;
+// SVC runs (F_DD / F_VP9 DownTracks).  One SSRC carries every layer, so a
+// packet the layer selector does not select is still relevant to it and
+// advances the munger (forwarder.go:1694-1702): dropped at the highest SN it
+// is excluded (rtpmunger.go:156-181, the prefix-count shape of a VP8 temporal
+// drop); after a loss gap it takes its SN like a forwarded packet.  Per lane
+// the selector's decision is a function of the packet and the state at the run
+// start as long as no switch happens:
+//   VP9.Select (videolayerselector/vp9.go:43-109): with a switch pending, a
+//   packet that is not its switch point is decided against the current layers;
+//   with no current layers, a non-key-frame packet is dropped unselected and
+//   irrelevant;
 //   DependencyDescriptor.Select (dependencydescriptor.go:65-355): the decode
-//   target the state selects (uniform over the run) and the frame's DTI for
-//   it; a frame already dropped drops its later packets (GetDecision); the
+//   target the state selects (uniform while no chain breaks) and the frame's
+//   DTI for it; a frame already dropped drops its later packets (GetDecision);
 //   chains and frame references are verified against the decision cache at
-//   the run start plus the decisions of the run's earlier frames.
-// The longest prefix of lanes meeting these conditions is decided together;
-// the first lane that does not goes through decide_step (the full
-// restatement), as in the simulcast runs.
+//   the run start plus the decisions of the run's earlier frames; frames added
+//   to the cache (a dropped frame's first packet, a forwarded frame's packets
+//   with frame integrity, :245-247) update it as addEntity does, gaps included.
+// Muted / paused DownTracks drop every packet with no state change.  Packets
+// without a descriptor, not selected, dropped by pause-on-downgrade (VP9) or
+// before the Forwarder started drop as the reference does.  The longest
+// prefix of lanes meeting these conditions is decided together; the first lane
+// that does not (a switch point, a chain break, a structure or active-target
+// update, a reorder, padding) goes through decide_step, as in the simulcast
+// runs.
 // ---------------------------------------------------------------------------
 constexpr int kSvcDDBytes = 48;  // per-lane marshal buffer (a descriptor without a structure fits)
-constexpr int kSvcFrames = 72;   // frame decisions of one run: frame cLast + up to 64 new frames
+constexpr int kSvcFrames = 72;   // frame decisions of one run: frame cLast + up to 64 later frames
+enum : u32 { SK_BAD = 0, SK_FWD = 1, SK_MDROP = 2, SK_NDROP = 3 };  // lane kinds of an SVC run
+
+#ifndef LKF_SVC_DIAG
+#define LKF_SVC_DIAG 0
+#endif
+#if LKF_SVC_DIAG
+#define SVC_WHY(c) \
+  if (!good && why == 0) why = (c)
+#else
+#define SVC_WHY(c)
+#endif
 
 template <bool DDK>
-__device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 pi, u32 n, u32 pos, u32 nextAt, bool valid,
-                       i32 &sentAcc, u8 *sScr, u8 *sFD) {
+__device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 pi, u32 n, u32 pos, u32 nextAt,
+                                       bool valid, i32 &sentAcc, u8 *sScr, u8 *sFD) {
   const u32 lane = lane_id();
   const u64 lt = (1ull << lane) - 1;
   const u32 fl = L.h.flags;
   const bool inWin = valid && lane >= pos && pi < nextAt;
+  const u64 winM = __ballot(inWin);
   const bool dd = DDK && (fl & F_DD);
-  // ---- wave-uniform preconditions
-  bool uni = (fl & F_STARTED) && (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && !(fl & (F_MUTED | F_PUBMUTED)) &&
-             L.h.tgtS != INVALID && L.h.tgtT != INVALID && L.h.curS != INVALID && L.h.curT != INVALID &&
-             !((fl & F_DEFICIENT) && L.h.tgtS < L.h.curS) && L.h.lastSSRC != 0;
+#if LKF_SVC_DIAG
+  if (lane == 0) atomicAdd(&g_diag[0], 1ull);
+#endif
+  // ---- muted / paused: every packet of the window drops with no state change
+  // (forwarder.go:1440, :1687)
+  {
+    const int ns = (fl & (F_MUTED | F_PUBMUTED)) ? LKF_DROP_MUTED
+                   : (L.h.tgtS == INVALID || L.h.tgtT == INVALID) ? LKF_DROP_PAUSED
+                                                                  : -1;
+#if LKF_SVC_AB == 4
+    if (ns >= 0) return pos;
+#endif
+    if (ns >= 0) {
+      const u32 k = u32(__popcll(winM));
+      o.nTuples += k;
+      o.drops[ns] += k;
+      return pos + k;
+    }
+  }
+  const bool curValid = L.h.curS != INVALID && L.h.curT != INVALID;
+  const bool started = fl & F_STARTED;
+  const bool relevantDrop = curValid && started;  // a not-selected packet advances the munger
+#if LKF_SVC_AB == 2
+  if (!relevantDrop) return pos;
+#endif
+  // ---- dependency-descriptor selector: the uniform part
+  bool uni = true;
   const DDStruct *s = nullptr;
   int hiPos = -1, maxTgt = -1;
   u32 hiTarget = 0;
+  bool swAll = false;  // a selected packet would switch layers
   if (DDK && dd) {
     const DDState &d = *L.dd;
-    uni = uni && (d.flags & DS_KF_VALID) && (d.flags & DS_CACHE_INIT) && (d.flags & DS_FN_INIT);
+    uni = (d.flags & DS_KF_VALID) && (d.flags & DS_CACHE_INIT);
     for (int c = 0; c < int(d.numChains); c++) uni = uni && d.expCount[c] == 0;  // (no chain waits: c_fire is a no-op)
     s = L.ddRing + d.slot;
-    // the decode target Select picks (:133-176): uniform while no chain breaks
-    for (int i = 0; uni && i < int(d.numTargets); i++) {
+    for (int i = 0; uni && i < int(d.numTargets); i++) {  // the decode target Select picks (:133-176)
       if (!((d.dtActive >> i) & 1) || i32(s->dtS[i]) > L.h.tgtS || i32(s->dtT[i]) > L.h.tgtT) continue;
       const int target = s->dtTarget[i];
       maxTgt = max(maxTgt, target);
@@ -1974,99 +2035,136 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
         break;
       }
     }
-    if (hiPos >= 0) uni = uni && i32(s->dtS[hiPos]) == L.h.curS && i32(s->dtT[hiPos]) == L.h.curT;  // no switch
-  } else {
-    uni = uni && L.h.curS == L.h.tgtS && L.h.curT == L.h.tgtT;  // vp9.go:52: no switch pending
+    swAll = hiPos >= 0 && (i32(s->dtS[hiPos]) != L.h.curS || i32(s->dtT[hiPos]) != L.h.curT);
   }
 #if LKF_SVC_DIAG
-  if (lane == 0) atomicAdd(&g_diag[0], 1ull);
   if (!uni) {
     if (lane == 0) atomicAdd(&g_diag[4], 1ull);
+#ifdef LKF_SVC_WATCH
+    svclog(L.watchDt, 2, rl32(pi, pos), 0, 0);
+#endif
     return pos;
   }
   u32 why = 0;
-#define SVC_WHY(c) \
-  if (!good && why == 0) why = (c)
 #else
   if (!uni) return pos;
-#define SVC_WHY(c)
 #endif
-  // ---- per lane: every lane of the run advances the munger, in order
-  const int prevLane = int((lane + 63u) & 63u);
-  const u64 pEsn = sh64(p.esn, prevLane);
-  const u64 prevEsn = lane > pos ? pEsn : L.h.extHighestIncomingSN;
-  bool good = inWin && p.plen != 0 && p.ssrc == L.h.lastSSRC && p.esn == prevEsn + 1;
-  SVC_WHY(1);
-  bool fwd = false, mk = false;
+  bool good = inWin;
+  u32 kind = SK_BAD;
+  int nsr = LKF_DROP_NOT_SELECTED;  // reason of an SK_NDROP lane
+  bool mk = false;                  // marker passed to UpdateAndGetSnTs
   int ddLen = 0;
   u64 ddEfn = 0;
-  bool ddNew = false, ddPut = false;
-  if (!dd) {  // VP9.Select with the current layers at the target
-    const bool E = p.vp9 & LKF_VP9_E, P = p.vp9 & LKF_VP9_P;
+  bool ddPut = false, ddFwdSel = false;
+  if (!dd) {  // ---- VP9.Select
+    const bool isV = p.flags & LKF_PKT_VP9;
+    const bool U = p.vp9 & LKF_VP9_U, B = p.vp9 & LKF_VP9_B, E = p.vp9 & LKF_VP9_E, P = p.vp9 & LKF_VP9_P;
     const i32 pS = p.spatial, pT = p.temporal;
-    good = good && (p.flags & LKF_PKT_VP9);
+    const bool kf = p.flags & LKF_PKT_KEYFRAME;
+    bool zero = !isV, sw = false;
+    if (isV && (L.h.curS != L.h.tgtS || L.h.curT != L.h.tgtT)) {
+      if (!curValid) {
+        if (kf)
+          sw = true;
+        else
+          zero = true;  // (vp9.go:55-57)
+      } else {
+        i32 uS = L.h.curS, uT = L.h.curT;
+        if (L.h.curT != L.h.tgtT) {
+          if (L.h.curT < L.h.tgtT) {
+            if (pT > L.h.curT && pT <= L.h.tgtT && U && B) uT = pT;
+          } else if (E) {
+            uT = L.h.tgtT;
+          }
+        }
+        if (L.h.curS != L.h.tgtS) {
+          if (L.h.curS < L.h.tgtS) {
+            if (pS > L.h.curS && pS <= L.h.tgtS && !P && B) uS = pS;
+          } else if (E) {
+            uS = L.h.tgtS;
+          }
+        }
+        sw = uS != L.h.curS || uT != L.h.curT;
+      }
+    }
+    good = good && !sw;  // a switch point: full step
     SVC_WHY(2);
-    fwd = !(pS > L.h.curS || (pS == L.h.curS && pT > L.h.curT));
-    mk = (p.hdr1 & 0x80) || (E && pS == L.h.curS && (P || L.h.tgtS <= L.h.curS));
-  } else if (DDK) {
+    const bool sel = !zero && !(pS > L.h.curS || (pS == L.h.curS && pT > L.h.curT));
+    mk = (p.hdr1 & 0x80) || (!zero && E && pS == L.h.curS && (P || L.h.tgtS <= L.h.curS));
+    if (!sel) {
+      kind = (!zero && started) ? SK_MDROP : SK_NDROP;
+    } else if ((fl & F_DEFICIENT) && L.h.tgtS < L.h.curS) {  // FlagPauseOnDowngrade :1709
+      kind = SK_NDROP;
+      nsr = LKF_DROP_DOWNGRADE;
+    } else {
+      kind = SK_FWD;
+    }
+  } else if (DDK) {  // ---- DependencyDescriptor.Select
     DDState &d = *L.dd;
     DDPkt dp = {};
     const bool hasDD = inWin && (p.flags & LKF_PKT_DD) && L.ddPkts;
     if (hasDD) dp = L.ddPkts[pi];
-    good = good && hasDD && (dp.flags & DP_VALID);
-    SVC_WHY(2);
+    const bool ddLane = hasDD && (dp.flags & DP_VALID);  // (no descriptor: not selected, no DD state change)
+#if LKF_SVC_AB == 3
+    good = good && ddLane;
+#endif
     const u64 cl0 = d.cLast;
     const u64 efn = dp.extFN;
-    const u64 pEfnL = sh64(efn, prevLane);
-    const u64 pEfn = lane > pos ? pEfnL : cl0;
-    good = good && (efn == pEfn || efn == pEfn + 1);  // frames in order, none skipped
+    const u64 ddM = __ballot(ddLane);
+    const int pdl = prev_in(ddM, lt);
+    const u64 pEfnL = sh64(efn, pdl >= 0 ? pdl : int(lane));
+    const u64 pEfn = pdl >= 0 && u32(pdl) >= pos ? pEfnL : cl0;  // the previous descriptor's frame
+    const u64 fi = efn - cl0;  // the frame's index in the run (0: frame cLast)
+    if (ddLane) good = good && efn >= pEfn && fi < u64(kSvcFrames) - 8;  // frames in order (a reorder: full step)
+#if LKF_SVC_AB == 1
+    if (ddLane) good = good && efn <= pEfn + 1;
+#endif
     SVC_WHY(3);
-    const u64 fi = efn - cl0;                         // the frame's index in the run (0: frame cLast)
-    const bool newF = efn != pEfn;
-    // the tentative decision: the selected decode target's DTI (:160-190)
+    const bool newF = ddLane && efn != pEfn;
     const u32 dti = hiPos >= 0 ? dd::dti_at(dp.dtis, int(hiTarget)) : 0u;
-    const bool t0 = hiPos >= 0 && dti != 0;
-    good = good && (maxTgt < 0 || int(dp.ndti) > maxTgt);  // (DecodeTarget.OnFrame errors: serial)
+    const bool t0 = hiPos >= 0 && dti != 0;  // the tentative decision (:160-190)
+    if (ddLane) good = good && (maxTgt < 0 || int(dp.ndti) > maxTgt);  // (DecodeTarget.OnFrame errors: serial)
     SVC_WHY(4);
+    // the frame's first descriptor lane in the run, and the next frame's
     const u64 newM = __ballot(inWin && newF);
     const u64 upto = newM & (lt | (1ull << lane));
-    const u32 head = (fi == 0 || !upto) ? pos : u32(63 - __clzll(upto));  // the frame's first lane in the run
+    const u32 head = (fi == 0 || !upto) ? pos : u32(63 - __clzll(upto));
     const u64 after = newM & ~((2ull << lane) - 1);
-    const u32 nextHead = after ? u32(__ffsll((long long)after) - 1) : 64u;  // the next frame's first lane
-    const u64 frameM = (nextHead >= 64 ? ~0ull : ((1ull << nextHead) - 1)) & ~((1ull << head) - 1);
-    const bool t0Head = sh32(u32(t0), int(head)) != 0;
+    const u32 nextHead = after ? u32(__ffsll((long long)after) - 1) : 64u;
+    const u64 frameM = (nextHead >= 64 ? ~0ull : ((1ull << nextHead) - 1)) & ~((1ull << head) - 1) & ddM;
+    const int headL = frameM ? __ffsll((long long)frameM) - 1 : int(lane);
+    const bool t0Head = sh32(u32(t0), headL) != 0;
     const u32 cache0 = dd::c_get(d, cl0);
-    // The DTI is the frame's, so every packet of a frame gets the head's
-    // tentative decision (one that does not goes serial).  GetDecision ->
-    // dropped returns before any state change (:86-95): the packets after a
-    // frame's first dropped one, and all of frame cLast's if it is cached
-    // dropped.  A dropped frame is added to the cache by its first evaluated
-    // packet, a forwarded one by each packet with frame integrity (:245-247);
-    // forwarded packets without it leave the cache alone.
+    // GetDecision -> dropped returns before any state change (:86-95): every
+    // packet after a frame's first dropped one, all of frame cLast's if it is
+    // cached dropped.  The DTI is the frame's, so the frame's packets share the
+    // head's decision (one that does not: full step).
     const bool drop0 = fi == 0 && cache0 == dd::SD_DROPPED;
-    const bool early = drop0 || (!t0Head && lane != head);
-    const bool eval = !early;
-    fwd = eval && t0;
-    good = good && (early || t0 == t0Head);
+    const bool early = ddLane && (drop0 || (!t0Head && int(lane) != headL));
+    const bool eval = ddLane && !early;
+    if (eval) good = good && t0 == t0Head;
     SVC_WHY(5);
-    good = good && (early || (!(dp.flags & DP_ATTACHED) &&
-                              !(dp.extFlags & (LKF_DD_STRUCTURE_UPDATED | LKF_DD_ACTIVE_UPDATED)) &&
-                              dp.extKFN == d.extKeyFrameNum && int(dp.nchain) == int(d.numChains)));
+    if (eval)
+      good = good && !(dp.flags & DP_ATTACHED) && !(dp.extFlags & (LKF_DD_STRUCTURE_UPDATED | LKF_DD_ACTIVE_UPDATED)) &&
+             dp.extKFN == d.extKeyFrameNum && int(dp.nchain) == int(d.numChains);
     SVC_WHY(6);
-    const bool adds = inWin && eval && (!t0 || (dp.extFlags & LKF_DD_INTEGRITY));
+    ddFwdSel = eval && t0;
+    if (ddFwdSel) good = good && !swAll && (d.flags & DS_FN_INIT);  // (a switch, the first frame number: full step)
+    SVC_WHY(7);
+    // frames the packet adds to the cache, and the decisions later frames see
+    // Only the in-order prefix of the window can be decided: a lane past the
+    // first out-of-order frame must not publish its frame's decision (a
+    // reordered earlier frame would otherwise be looked up from the future)
+    const u64 ordBadM = __ballot(ddLane && inWin && !(efn >= pEfn && fi < u64(kSvcFrames) - 8));
+    const u32 ordEnd = ordBadM ? u32(__ffsll((long long)ordBadM) - 1) : 64u;
+    const bool adds = inWin && lane < ordEnd && eval && (!t0 || (dp.extFlags & LKF_DD_INTEGRITY));
     const u64 addM = __ballot(adds);
     const bool firstAdd = adds && !(addM & frameM & lt);
-    // decisions of the run's frames as later frames see them: the frame's
-    // first add, else the cached value (frame cLast) or unknown (beyond cLast)
-    if (inWin && fi < u64(kSvcFrames) && lane == head) sFD[fi] = u8(fi == 0 ? cache0 : dd::SD_UNKNOWN);
-    if (inWin && lane == pos && fi != 0) sFD[0] = u8(cache0);
+    if (lane < u32(kSvcFrames)) sFD[lane] = u8(lane == 0 ? cache0 : dd::SD_UNKNOWN);
+    if (lane + 64 < u32(kSvcFrames)) sFD[lane + 64] = u8(dd::SD_UNKNOWN);
     wave_lds_sync();
-    if (firstAdd && fi < u64(kSvcFrames)) sFD[fi] = u8(t0 ? dd::SD_FORWARDED : dd::SD_DROPPED);
+    if (firstAdd && fi < u64(kSvcFrames)) sFD[fi] = u8(t0 ? dd::SD_FORWARDED : dd::SD_DROPPED);  // (a lane past the run may be out of range)
     wave_lds_sync();
-    // a new frame is added right after the frame before it (no gap for
-    // addEntity to fill: the serial step takes that)
-    if (firstAdd && fi >= 2 && fi < u64(kSvcFrames) && sFD[fi - 1] == dd::SD_UNKNOWN) good = false;
-    SVC_WHY(7);
     auto dec = [&](u64 e) -> u32 {  // GetDecision(e) as this packet sees it (e < efn)
       if (e >= cl0 && e < efn) return sFD[e - cl0];
       bool old;
@@ -2078,54 +2176,68 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
         const u32 diff = u32(dp.chainDiffs >> (8 * c)) & 0xff;
         const bool broken = (d.chBroken >> c) & 1;
         if (diff == 0) {
-          good = good && !broken;  // (a broken chain restarting: serial)
-          SVC_WHY(8);
+          good = good && !broken;  // (a broken chain restarting: full step)
           continue;
         }
         if (!broken && dec(efn - diff) != dd::SD_FORWARDED) good = false;
-        SVC_WHY(8);
       }
     }
-    if (fwd && good)  // a referenced frame that was dropped drops this one (:192-201): serial
+    SVC_WHY(8);
+    if (ddFwdSel && good)  // a referenced frame that was dropped drops this one (:192-201): full step
       for (int j = 0; j < int(dp.nfd) && j < kDDFdiffs; j++)
         if (dp.fd[j] != 0 && dec(efn - dp.fd[j]) == dd::SD_DROPPED) good = false;
     SVC_WHY(9);
-    if (fwd && good) {
+    if (ddFwdSel && good) {
       // frame number (FrameNumberWrapper without a structure update) and the
       // descriptor marshalled with the active mask in force (:223-262)
       const bool hasMask = d.flags & DS_HAS_MASK;
       const bool hasActive = (dp.flags & DP_ACTIVE) || hasMask;
       const u32 active = hasMask ? d.mask : dp.activeMask;
       ddLen = dd::dd_marshal_inl(*s, dp, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
-                             kSvcDDBytes);
+                                 kSvcDDBytes);
       if (ddLen < 0) good = false;
-      SVC_WHY(10);
       mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
     }
+    SVC_WHY(10);
+    kind = ddFwdSel ? SK_FWD : (relevantDrop ? SK_MDROP : SK_NDROP);  // (RTPMarker false for the drops)
     ddEfn = efn;
-    ddNew = firstAdd && fi != 0;  // the first add of a frame beyond cLast: addEntity's new-entity path
     ddPut = firstAdd;
   }
-  // ---- munger / sequencer conditions (as in the simulcast runs)
-  const u64 dropM = __ballot(inWin && !fwd);
-  const u64 fwdM = __ballot(inWin && fwd);
-  const u64 snOff = L.h.snOffset + u64(__popcll(dropM & lt));
+  // ---- munger / sequencer (UpdateAndGetSnTs in order, sequencer.push)
+  const bool adv = kind == SK_FWD || kind == SK_MDROP;
+  if (kind == SK_FWD) good = good && started && (fl & F_SEQ_INIT) && (fl & F_STATS_INIT);  // (start: full step)
+  SVC_WHY(1);
+  const u64 advM = __ballot(inWin && adv);
+  const int pa = prev_in(advM, lt);
+  const u64 paEsn = sh64(p.esn, pa >= 0 ? pa : int(lane));
+  const u64 prevEsn = pa >= 0 && u32(pa) >= pos ? paEsn : L.h.extHighestIncomingSN;
+  const u64 dEsn = p.esn - prevEsn;
+  const bool contig = dEsn == 1;
+  const bool gap = dEsn > 1 && dEsn < u64(L.seqSize) - 64;
+  if (adv) good = good && p.ssrc == L.h.lastSSRC && p.plen != 0 && (contig || gap);  // (reorder, dup, padding: full step)
+  SVC_WHY(11);
+  const bool excl = kind == SK_MDROP && contig;  // PacketDropped at the highest SN
+  if (excl) good = good && L.h.snOffset == L.h.rmOpenValue && L.h.rmOpenStart <= p.esn;
+  SVC_WHY(12);
+  const u64 exM = __ballot(inWin && excl);
+  const u64 fwdM = __ballot(inWin && kind == SK_FWD);
+  const u64 snOff = L.h.snOffset + u64(__popcll(exM & lt));
   const u64 osn = p.esn - snOff;
   const u64 ots = p.ets - L.h.tsOffset;
   const int pf = prev_in(fwdM, lt);
   const int pfs = pf >= 0 ? pf : int(lane);
   const u64 pfOsn = sh64(osn, pfs), pfOts = sh64(ots, pfs);
-  const u64 prevOsn = pf >= 0 ? pfOsn : L.h.seqExtHighestSN;
-  const u64 hiTS = pf >= 0 ? pfOts : L.h.seqExtHighestTS;
-  if (fwd) {
-    good = good && ots >= hiTS && osn == prevOsn + 1 && osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
-    SVC_WHY(11);
-  } else {
-    good = good && L.h.snOffset == L.h.rmOpenValue;  // (a drop moves the open range: rtpmunger.go:156-181)
-    SVC_WHY(12);
-  }
+  const u64 prevOsn = pf >= 0 && u32(pf) >= pos ? pfOsn : L.h.seqExtHighestSN;
+  const u64 hiTS = pf >= 0 && u32(pf) >= pos ? pfOts : L.h.seqExtHighestTS;
+  if (kind == SK_FWD)
+    good = good && ots >= hiTS && osn - prevOsn >= 1 && osn - prevOsn < u64(L.seqSize) - 64 &&
+           osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
+  SVC_WHY(13);
   const u64 stopM = __ballot(inWin ? !good : (valid && lane >= pos));
   const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+#if defined(LKF_SVC_WATCH) && LKF_SVC_DIAG
+  svclog(L.watchDt, 1, rl32(pi, pos), x < n ? rl32(pi, x) : 0xffffffffu, x < n ? rl32(why, x) : 0u);
+#endif
 #if LKF_SVC_DIAG
   if (lane == 0) {
     atomicAdd(&g_diag[1], x > pos ? 1ull : 0ull);
@@ -2137,36 +2249,68 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     if (lane == 0) atomicAdd(&g_diag[winX ? (16 + wx) : 13], 1ull);
   }
 #endif
-#undef SVC_WHY
   if (x <= pos) return pos;
   const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
   const bool inRun = (runM >> lane) & 1;
   if (DDK && dd) {
-    // decision cache (selectordecisioncache.go:112-165) for the frames of the
-    // run: each frame's first evaluated packet sets its entry, and a new frame
-    // marks the entry kNack behind the previous last frame missing if it is
-    // still unknown (read at the run-start state: it lies before the run)
+    // ---- decision cache (selectordecisioncache.go:112-165) for the frames the
+    // run added, in lane order: a new frame fills the entries it skipped with
+    // unknown, marks the entries kNack behind the previous last frame missing
+    // if still unknown (they lie before the run: read at the run-start state),
+    // then takes its decision; a frame at or below the last one only sets it
     DDState &d = *L.dd;
+    const u64 pM = __ballot(inRun && ddPut);
+    const int pp = prev_in(pM, lt);
+    const u64 ppE = sh64(ddEfn, pp >= 0 ? pp : int(lane));
+    const u64 cur = pp >= 0 ? ppE : d.cLast;  // cLast when this lane adds
     const bool put = inRun && ddPut && ddEfn > d.cBase;
+    const bool grow = put && ddEfn > cur;  // addEntity's new-entity path
+#if LKF_SVC_AB == 1
+    if (grow && ddEfn != cur + 1 && lane == 0) atomicOr(L.err, 16u);
+#endif
+    const u64 g1M = __ballot(grow && ddEfn == cur + 1);
+    const u64 gNM = __ballot(grow && ddEfn > cur + 1);
+    // one-frame steps: at most one missing mark each, in parallel
     u64 missE = 0;
     bool miss = false;
-    if (inRun && ddNew) {
-      const u64 ms0 = ddEfn - 1, me0 = ddEfn;
-      const u64 ms = ms0 > dd::kNack + d.cBase ? ms0 - dd::kNack : d.cBase;
-      const u64 me = me0 > dd::kNack + d.cBase ? me0 - dd::kNack : d.cBase;
+    if ((g1M >> lane) & 1) {
+      const u64 ms = cur > dd::kNack + d.cBase ? cur - dd::kNack : d.cBase;
+      const u64 me = ddEfn > dd::kNack + d.cBase ? ddEfn - dd::kNack : d.cBase;
       if (me > ms && dd::c_get(d, ms) == dd::SD_UNKNOWN) {
         miss = true;
         missE = ms;
       }
     }
-    wave_lds_sync();
-    if (put) {
-      const u64 off = (ddEfn - d.cBase) % dd::kEntries;
-      const u32 bp = u32(off & 31) * 2;
-      unsigned long long *w = reinterpret_cast<unsigned long long *>(&d.masks[off >> 5]);
-      atomicAnd(w, ~(3ull << bp));
-      atomicOr(w, u64(fwd ? dd::SD_FORWARDED : dd::SD_DROPPED) << bp);
+    // gaps (lost frames): one lane at a time, the wave over the entries
+    for (u64 m = gNM; m; m &= m - 1) {
+      const u32 b = u32(__ffsll((long long)m) - 1);
+      const u64 e = rl64(ddEfn, b), c0 = rl64(cur, b);
+      const u64 ms = c0 > dd::kNack + d.cBase ? c0 - dd::kNack : d.cBase;
+      const u64 me = e > dd::kNack + d.cBase ? e - dd::kNack : d.cBase;
+      u32 st = dd::SD_UNKNOWN + 1;  // (none)
+      u64 ent = 0;
+      if (lane < u32(e - c0 - 1)) {  // [c0 + 1, e) -> unknown (no callbacks)
+        ent = c0 + 1 + lane;
+        st = dd::SD_UNKNOWN;
+      }
+      const u64 mk2 = (me > ms && lane < u32(me - ms)) ? ms + lane : 0;
+      const bool mMiss = me > ms && lane < u32(me - ms) && dd::c_get(d, mk2) == dd::SD_UNKNOWN;
+      wave_lds_sync();
+      if (st == dd::SD_UNKNOWN) {
+        const u64 off = (ent - d.cBase) % dd::kEntries;
+        const u32 bp = u32(off & 31) * 2;
+        atomicOr(reinterpret_cast<unsigned long long *>(&d.masks[off >> 5]), 3ull << bp);
+      }
+      if (mMiss) {
+        const u64 off = (mk2 - d.cBase) % dd::kEntries;
+        const u32 bp = u32(off & 31) * 2;
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(&d.masks[off >> 5]);
+        atomicAnd(w, ~(3ull << bp));
+        atomicOr(w, u64(dd::SD_MISSING) << bp);
+      }
+      wave_lds_sync();
     }
+    wave_lds_sync();
     if (miss) {
       const u64 off = (missE - d.cBase) % dd::kEntries;
       const u32 bp = u32(off & 31) * 2;
@@ -2174,21 +2318,35 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       atomicAnd(w, ~(3ull << bp));
       atomicOr(w, u64(dd::SD_MISSING) << bp);
     }
+    if (put) {
+      const u64 off = (ddEfn - d.cBase) % dd::kEntries;
+      const u32 bp = u32(off & 31) * 2;
+      unsigned long long *w = reinterpret_cast<unsigned long long *>(&d.masks[off >> 5]);
+      atomicAnd(w, ~(3ull << bp));
+      atomicOr(w, u64(kind == SK_FWD ? dd::SD_FORWARDED : dd::SD_DROPPED) << bp);
+    }
     wave_lds_sync();
-    const u64 aM = __ballot(inRun && ddPut);
+    const u64 aM = __ballot(put);
     const u64 eLast = aM ? rl64(ddEfn, 63 - __clzll(aM)) : 0;  // frames are in order: the last added is the highest
-    const u64 fM = __ballot(inRun && fwd);
+    const u64 fM = __ballot(inRun && ddFwdSel);
     const u64 eF = fM ? rl64(ddEfn, 63 - __clzll(fM)) : 0;
     wave_lds_sync();
-    if (eLast > d.cLast) d.cLast = eLast;
-    if (fM && eF > d.fnLast) d.fnLast = eF;  // FrameNumberWrapper.UpdateAndGet of the forwarded frames
+    if (aM && eLast > d.cLast) d.cLast = eLast;
+    if (fM && eF > d.fnLast) d.fnLast = eF;  // FrameNumberWrapper.UpdateAndGet of the selected frames
     wave_lds_sync();
   }
   // ---- decide lanes [pos, x)
-  const u64 fwR = fwdM & runM, tdR = dropM & runM;
-  const bool f = inRun && fwd;
+  const u64 fwR = fwdM & runM, exR = exM & runM;
+  const u64 advR = advM & runM;
+  const u64 setR = advR & ~exR;  // lanes that set the munger's last SN/TS (forwards, drops after a gap)
+  const bool f = inRun && kind == SK_FWD;
   o.nTuples += x - pos;
-  o.drops[LKF_DROP_NOT_SELECTED] += u32(__popcll(tdR));
+  {
+    const bool nd = inRun && kind == SK_NDROP;
+    o.drops[LKF_DROP_NOT_SELECTED] += u32(__popcll(__ballot(inRun && kind == SK_MDROP))) +
+                                      u32(__popcll(__ballot(nd && nsr == LKF_DROP_NOT_SELECTED)));
+    o.drops[LKF_DROP_DOWNGRADE] += u32(__popcll(__ballot(nd && nsr == LKF_DROP_DOWNGRADE)));
+  }
   // output shape (downtrack.go:693-723, pacer/base.go:71-100): DD element first
   const int cc = p.hdr0 & 0xf;
   const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
@@ -2266,6 +2424,18 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     CHK(slot < L.seqSize, CK_DEC_SEQ, slot, L.seqSize);
     store_rec(L.seq + slot, m);
   }
+  // sequencer slots a push skipped (sequencer.go:179-189): invalidated
+  for (u64 gm = __ballot(f && osn - prevOsn > 1); gm; gm &= gm - 1) {
+    const u32 b = u32(__ffsll((long long)gm) - 1);
+    const u64 from = rl64(prevOsn, b), to = rl64(osn, b);
+    const u32 nsk = u32(to - from - 1);
+    const u32 base = u32(L.h.seqHighSlot) + u32(from - L.h.seqExtHighestSN) + 1;
+    for (u32 i = lane; i < nsk; i += 64) {
+      u32 x2 = base + i;
+      while (x2 >= L.seqSize) x2 -= L.seqSize;
+      store_rec(L.seq + x2, SeqMeta{});
+    }
+  }
   const u32 sumLen = wave_sum_u32(outLen);
   sentAcc += f ? i32(p.poff) - hdrLen : 0;
   if (fwR) {
@@ -2277,55 +2447,63 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     L.h.seqHighSlot = u16(slot);
     L.h.seqExtHighestSN = rl64(osn, lastF);
     L.h.seqExtHighestTS = rl64(ots, lastF);
+    o.relOff += rl32(relEx + aligned, lastF);
   }
-  // munger past the run: every lane was an UpdateAndGetSnTs, the drops were
-  // PacketDropped right after theirs
-  const u32 lastSel = 63 - __clzll(runM);
-  const u64 mkM = __ballot(mk);
-  L.h.extHighestIncomingSN = rl64(p.esn, lastSel);
-  const bool lastIsF = (fwR >> lastSel) & 1;
-  const u64 pfM = fwR & ((1ull << lastSel) - 1);
-  u64 sSN = L.h.extLastSN, sTS = L.h.extLastTS;
-  bool sMk = fl & F_LAST_MARKER;
-  if (pfM) {
-    const u32 b = 63 - __clzll(pfM);
-    sSN = rl64(osn, b);
-    sTS = rl64(ots, b);
-    sMk = (mkM >> b) & 1;
+  if (advR) {  // ---- the munger past the run
+    const u64 mkM = __ballot(mk);
+    const u32 lastA = 63 - __clzll(advR);
+    L.h.extHighestIncomingSN = rl64(p.esn, lastA);
+    const bool lastSets = (setR >> lastA) & 1;
+    const u64 psM = setR & ((1ull << lastA) - 1);
+    u64 sSN = L.h.extLastSN, sTS = L.h.extLastTS;
+    bool sMk = fl & F_LAST_MARKER;
+    if (psM) {
+      const u32 b = 63 - __clzll(psM);
+      sSN = rl64(osn, b);
+      sTS = rl64(ots, b);
+      sMk = (mkM >> b) & 1;
+    }
+    if (lastSets) {
+      L.h.extSecondLastSN = sSN;
+      L.h.extSecondLastTS = sTS;
+      L.h.extLastSN = rl64(osn, lastA);
+      L.h.extLastTS = rl64(ots, lastA);
+      setf(L, F_SECOND_LAST_MARKER, sMk);
+      setf(L, F_LAST_MARKER, (mkM >> lastA) & 1);
+    } else {
+      L.h.extSecondLastSN = L.h.extLastSN = sSN;
+      L.h.extSecondLastTS = L.h.extLastTS = sTS;
+      setf(L, F_SECOND_LAST_MARKER, sMk);
+      setf(L, F_LAST_MARKER, sMk);
+    }
+    // RTX gate (rtpmunger.go:204-208): the last key frame sets it, the
+    // 2000-packet expiry is checked against the run's highest munged SN
+    const u64 kfM = __ballot(((advR >> lane) & 1) && kf);
+    if (kfM) {
+      L.h.extRtxGateSn = rl64(osn, 63 - __clzll(kfM));
+      setf(L, F_RTX_GATE, true);
+    }
+    if (hasf(L, F_RTX_GATE) && (rl64(osn, lastA) - L.h.extRtxGateSn) > 2000) setf(L, F_RTX_GATE, false);
+    // exclusions: one per group of drops with consecutive SNs
+    u64 m = exR;
+    while (m) {
+      const u32 b = u32(__ffsll((long long)m) - 1);
+      const u64 s0 = rl64(p.esn, b);
+      u64 e0 = s0 + 1;
+      m &= m - 1;
+      while (m) {
+        const u32 b2 = u32(__ffsll((long long)m) - 1);
+        if (rl64(p.esn, b2) != e0) break;
+        e0++;
+        m &= m - 1;
+      }
+      rm_exclude(L, s0, e0);
+    }
+    if (exR) L.h.snOffset = L.h.rmOpenValue;
   }
-  if (lastIsF) {
-    L.h.extSecondLastSN = sSN;
-    L.h.extSecondLastTS = sTS;
-    L.h.extLastSN = rl64(osn, lastSel);
-    L.h.extLastTS = rl64(ots, lastSel);
-    setf(L, F_SECOND_LAST_MARKER, sMk);
-    setf(L, F_LAST_MARKER, (mkM >> lastSel) & 1);
-  } else {
-    L.h.extSecondLastSN = L.h.extLastSN = sSN;
-    L.h.extSecondLastTS = L.h.extLastTS = sTS;
-    setf(L, F_SECOND_LAST_MARKER, sMk);
-    setf(L, F_LAST_MARKER, sMk);
-  }
-  if (hasf(L, F_RTX_GATE) && (rl64(osn, lastSel) - L.h.extRtxGateSn) > 2000) setf(L, F_RTX_GATE, false);
-  const u64 kfM = __ballot(inRun && kf);
-  if (kfM) {
-    L.h.extRtxGateSn = rl64(osn, 63 - __clzll(kfM));
-    setf(L, F_RTX_GATE, true);
-  }
-  u64 m = tdR;  // one exclusion per run of consecutive drops
-  while (m) {
-    const u32 b = u32(__ffsll((long long)m) - 1);
-    const u64 after = fwR & ~((2ull << b) - 1);
-    const u32 nf = after ? u32(__ffsll((long long)after) - 1) : 64u;
-    const u64 runD = tdR & (nf >= 64 ? ~0ull : ((1ull << nf) - 1)) & ~((1ull << b) - 1);
-    const u64 s0 = rl64(p.esn, b);
-    rm_exclude(L, s0, s0 + u64(__popcll(runD)));
-    m &= ~runD;
-  }
-  if (tdR) L.h.snOffset = L.h.rmOpenValue;
-  if (fwR) o.relOff += rl32(relEx + aligned, 63 - __clzll(fwR));
   return x;
 }
+#undef SVC_WHY
 
 template <bool DDK>
 __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
@@ -2476,6 +2654,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.extAbs = dt.extAbs;
   L.extDD = dt.extDD;
   L.err = A.err;
+#ifdef LKF_SVC_WATCH
+  L.watchDt = d;
+#endif
   L.ddPkts = A.ddPkts;
   L.ddRing = nullptr;
   L.dd = sDD;
@@ -2499,7 +2680,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   o.outT = A.tuples + slot0;
   // SVC DownTracks (one SSRC, every packet relevant to the selector): svc_run
   // (the host schedules them in k_decide_dt<true>)
-  const bool svcDT = DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
+  const bool svcDT = LKF_SVC_AB != 5 && DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
                      ((L.h.flags & F_VP9) || ((L.h.flags & F_DD) && ddDT));
   u32 nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
@@ -2596,12 +2777,29 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         // SVC DownTrack: a run, then the stopping packet's full step (its
         // descriptor reloaded wave-uniform, so the chunk's raw registers are
         // dead on this path)
+#if LKF_WTIME
+        const u64 wr0 = __builtin_amdgcn_s_memtime();
+#endif
         x = svc_run<DDK>(L, o, p, pi, n, pos, nextAt, valid, sentAcc, sSvcScr, sSvcFD);
+#if LKF_WTIME
+        wcDrain += __builtin_amdgcn_s_memtime() - wr0;  // (svc DownTracks: cycles in svc_run)
+        wtRuns += x > pos ? 1 : 0;
+#endif
         pos = x;
         if (x < n && rl32(pi, x) < nextAt) {
           const u32 px = rl32(pi, x);
+#if LKF_WTIME
+          wtSerial++;
+          const u64 ws0 = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef LKF_SVC_WATCH
+          svclog(d, 3, px, L.dd ? u32(L.dd->cLast) : 0u, L.dd ? u32(L.dd->chBroken) | (u32(L.dd->chActive) << 8) : 0u);
+#endif
           decide_step<DDK>(L, load_pkt(pkts + px), px, o);
           vm_drain();
+#if LKF_WTIME
+          wcStep += __builtin_amdgcn_s_memtime() - ws0;
+#endif
           pos = x + 1;
         }
         continue;
@@ -4198,7 +4396,10 @@ hipError_t read_check(unsigned long long out[4], int reset) {
 }
 
 hipError_t read_wtime(u32 *out, u32 nwaves) {
-#if LKF_WTIME
+#ifdef LKF_SVC_WATCH
+  if (nwaves > 4096) nwaves = 4096;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_svclog), sizeof(u32) * 4 * nwaves);
+#elif LKF_WTIME
   if (nwaves > kWTimeWaves) nwaves = kWTimeWaves;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtime), sizeof(u32) * 16 * nwaves);
 #else

@@ -543,6 +543,29 @@ int orc_downtrack_summaries(orc_engine *e, lkf_dt_summary *out, uint32_t cap, ui
   return LKF_OK;
 }
 
+// debugging: the DD selector state in lkf_debug_dd_state's layout
+int orc_debug_dd_state(orc_engine *e, int32_t dt, uint64_t out[16]) {
+  if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
+  const VLS &v = e->dts[dt]->f->vls;
+  for (int i = 0; i < 16; i++) out[i] = 0;
+  out[15] = uint64_t(uint8_t(v.currentLayer.Spatial + 128)) | (uint64_t(uint8_t(v.currentLayer.Temporal + 128)) << 8);
+  if (!v.dd) return LKF_OK;
+  const DDSelectorState &d = *v.dd;
+  out[0] = d.decisions.initialized ? 1 : 0;
+  out[1] = d.decisions.base;
+  out[2] = d.decisions.last;
+  for (int i = 0; i < 8 && i < int(d.decisions.masks.size()); i++) out[3 + i] = d.decisions.masks[i];
+  uint64_t ex = 0;
+  for (size_t c = 0; c < d.chains.size(); c++) {
+    if (d.chains[c]->broken) out[11] |= 1ull << c;
+    if (d.chains[c]->active) out[12] |= 1ull << c;
+    ex += d.chains[c]->expectFrames.size();
+  }
+  out[13] = ex;
+  out[14] = d.fnWrapper.inited ? d.fnWrapper.last : ~0ull;
+  return LKF_OK;
+}
+
 int orc_get_state(orc_engine *e, int32_t dt, lkf_fwd_state *o) {
   if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
   ForwarderState s = e->dts[dt]->f->GetState();

@@ -23,7 +23,8 @@ def main():
     pkg = importlib.import_module("livekit-server_amd")
     wl = importlib.import_module("livekit-server_amd.workload")
     bs = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
-    tr = wl.Trace(2, duration_s=nb * bs, batch_s=bs, rooms=rooms)
+    cfg = int(os.environ.get("WT_CONFIG", "2"))
+    tr = wl.Trace(cfg, duration_s=nb * bs, batch_s=bs, rooms=rooms)
     lib = os.path.join(ROOT, "livekit-server_amd", "lib", os.environ.get("WTIME_LIB", "liblkfwd_wtime.so"))
     eng = pkg.Engine.for_trace(tr, lib_path=lib)
     fn = eng.lib.lkf_debug_wtime
@@ -33,10 +34,10 @@ def main():
     for b in range(nb):
         wl.queue_events(eng.api, eng.h, tr, b)
         pk, n, ar, alen = tr.batch(b)
-        eng.submit(pk, n, ar, alen)
+        eng.submit(pk, n, ar, alen, tr.batch_dd(b)[0] if tr.has_dd() else None)
         eng.run()
         eng.sync()
-    nw = 1 << 16
+    nw = 1 << 17
     buf = (C.c_uint32 * (16 * nw))()
     assert fn(eng.h, buf, nw) == 0
     a = np.frombuffer(buf, dtype=np.uint32).reshape(-1, 16).astype(np.int64)
@@ -78,7 +79,10 @@ def main():
         tot.mean(), pro.mean(), stp.mean(), drn.mean(), 100 * pro.sum() / tot.sum(), 100 * stp.sum() / tot.sum(),
         100 * drn.sum() / tot.sum()))
     ms = ser > 0
-    print("per serial step: %.0f cycles + drain %.0f" % (stp[ms].sum() / ser[ms].sum(), drn[ms].sum() / ser[ms].sum()))
+    print("per serial step: %.0f cycles + drain %.0f (svc DownTracks: 'drain' = cycles in svc_run)" % (
+        stp[ms].sum() / ser[ms].sum(), drn[ms].sum() / ser[ms].sum()))
+    if os.environ.get("WT_PART1"):  # the k_decide_dt<true> waves only (slots past the plain part)
+        pass
     top = np.argsort(-life)[:10]
     for i in top:
         lay = a[i, 13]
