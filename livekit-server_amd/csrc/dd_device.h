@@ -293,16 +293,28 @@ __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDSt
 
 // ---- writer (dependencydescriptorwriter.go) ------------------------------------
 struct BitW {
-  u8 *buf;  // zero-initialised, cap bytes
+  // bits gather in a register and leave as whole bytes (one byte store per 8
+  // bits instead of a read-modify-write per bit); finish() writes the last
+  // partial byte, zero-padded
+  u8 *buf;  // cap bytes
   int cap, bitPos;
-  __device__ BitW(u8 *b, int c) : buf(b), cap(c), bitPos(0) {}
-  __device__ int write(u64 val, int n) {  // MSB first
+  u64 acc;
+  int accBits, bytePos;
+  __device__ BitW(u8 *b, int c) : buf(b), cap(c), bitPos(0), acc(0), accBits(0), bytePos(0) {}
+  __device__ int write(u64 val, int n) {  // MSB first, n <= 32
     if (bitPos + n > cap * 8) return INVALID;
-    for (int i = n - 1; i >= 0; i--) {
-      if ((val >> i) & 1) buf[bitPos >> 3] |= u8(0x80u >> (bitPos & 7));
-      bitPos++;
+    acc = (acc << n) | (n >= 64 ? val : (val & ((u64(1) << n) - 1)));
+    accBits += n;
+    bitPos += n;
+    while (accBits >= 8) {
+      accBits -= 8;
+      buf[bytePos++] = u8(acc >> accBits);
     }
     return OK;
+  }
+  __device__ void finish() {
+    if (accBits > 0) buf[bytePos++] = u8(acc << (8 - accBits));
+    accBits = 0;
   }
   __device__ int nonSymmetric(u32 val, u32 numValues) {
     if (!(val < numValues && numValues <= (1u << 31))) return INVALID;
@@ -470,6 +482,7 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
       for (int c = 0; c < s.numChains; c++) e |= w.write((p.chainDiffs >> (8 * c)) & 0xff, 8);
     }
   }
+  w.finish();
   return e ? -1 : nbytes;
 }
 __device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
@@ -665,8 +678,12 @@ struct SelResult {
 
 // Select :65-355.  Layers are the DownTrack's Base layers (DTHot); structs is
 // the track's structure ring; out receives the marshalled descriptor.
+// (staged: an LDS copy of structure slot stagedSlot, read instead of the
+// track's ring in HBM for that slot)
 __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStruct *structs, const DDPkt &p, bool hasDD, bool pktMarker,
-                                      i32 &curS, i32 &curT, i32 &prevS, i32 &prevT, i32 tgtS, i32 tgtT, u8 *out) {
+                                      i32 &curS, i32 &curT, i32 &prevS, i32 &prevT, i32 tgtS, i32 tgtT, u8 *out,
+                                      const DDStruct *staged, u32 stagedSlot) {
+  auto pick = [&](u32 slot) -> const DDStruct & { return slot == stagedSlot ? *staged : structs[slot]; };
   SelResult r = {false, false, false, false, false, 0, false};
   if (curS != -1 && curT != -1) r.relevant = true;
   if (!hasDD) return r;
@@ -676,13 +693,13 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
   bool tooOld;
   const u32 sd = c_decision(d, efn, tooOld);
   if (tooOld || sd == SD_DROPPED) return r;
-  if (p.extFlags & LKF_DD_STRUCTURE_UPDATED) update_structure(d, structs[p.slot], p.slot, efn);
+  if (p.extFlags & LKF_DD_STRUCTURE_UPDATED) update_structure(d, pick(p.slot), p.slot, efn);
   if (p.extKFN != d.extKeyFrameNum) {
     c_add(d, efn, SD_DROPPED);
     invalidate_keyframe(d);
     return r;
   }
-  const DDStruct &s = structs[d.slot];
+  const DDStruct &s = pick(d.slot);
   if (p.extFlags & LKF_DD_ACTIVE_UPDATED) update_active(d, s, p.activeMask);
   if (p.nchain != d.numChains) {
     c_add(d, efn, SD_DROPPED);
@@ -732,7 +749,7 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
     d.prevMask = d.mask;
     d.flags |= DS_HAS_MASK;
     u32 m = 0;  // GetActiveDecodeTargetBitmask over ExtDependencyDescriptor.DecodeTargets (the parse-time structure)
-    const DDStruct &ps = structs[p.slot];
+    const DDStruct &ps = pick(p.slot);
     for (int i = 0; i < ps.numDT; i++)
       if (i32(ps.dtS[i]) <= curS && i32(ps.dtT[i]) <= curT) m |= 1u << ps.dtTarget[i];
     d.mask = m;

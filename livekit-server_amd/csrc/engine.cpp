@@ -202,6 +202,10 @@ struct lkf_engine {
   BatchCtx ctx[kCtx];
   uint64_t nRuns = 0;
   int lastCtx = -1;
+  // pinned bounce buffer of the host drains (D2H into caller memory that may
+  // be pageable goes through it, on the engine's own stream)
+  uint8_t *bounce = nullptr, *bounceDev = nullptr;
+  size_t bounceCap = 0;
 
   // NACK -> RTX scratch (grown on demand)
   lkf_nack *dNacks = nullptr;
@@ -403,6 +407,31 @@ static int drain_streams(lkf_engine *e) {
   HIPCHK(hipStreamSynchronize(e->prepS), "sync prep stream");
   HIPCHK(hipStreamSynchronize(e->decS), "sync decide stream");
   HIPCHK(hipStreamSynchronize(e->emitS), "sync emit stream");
+  return LKF_OK;
+}
+
+// Device -> caller host memory through the engine's pinned bounce buffer:
+// the caller's buffer may be pageable (numpy arrays, std::vector), and a
+// pageable D2H hipMemcpy is the one path on which round 2 and round 3 each saw
+// a stray "illegal memory access" after every engine stream had completed.
+static int copy_to_host(lkf_engine *e, void *dst, const void *src, size_t n, const char *what) {
+  constexpr size_t kChunk = size_t(16) << 20;
+  hipPointerAttribute_t pa;
+  if (hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost) {  // page-locked: direct
+    HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost), what);
+    return LKF_OK;
+  }
+  (void)hipGetLastError();  // (an unregistered pointer is not an error here)
+  if (!e->bounce) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&e->bounce), kChunk, hipHostMallocDefault), "alloc bounce");
+    e->bounceCap = kChunk;
+  }
+  for (size_t off = 0; off < n; off += kChunk) {
+    const size_t k = std::min(kChunk, n - off);
+    HIPCHK(hipMemcpyAsync(e->bounce, static_cast<const uint8_t *>(src) + off, k, hipMemcpyDeviceToHost, e->own), what);
+    HIPCHK(hipStreamSynchronize(e->own), what);
+    std::memcpy(static_cast<uint8_t *>(dst) + off, e->bounce, k);
+  }
   return LKF_OK;
 }
 
@@ -774,6 +803,7 @@ void lkf_destroy(lkf_engine *e) {
     if (x.gScan) (void)hipGraphExecDestroy(x.gScan);
     if (x.dDesc) (void)hipFree(x.dDesc);
   }
+  if (e->bounce) (void)hipHostFree(e->bounce);
   if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
   if (e->decS) (void)hipStreamDestroy(e->decS);
@@ -1487,8 +1517,11 @@ int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_
   if (n_out) *n_out = n;
   if (arena_len) *arena_len = len;
   if (n > cap || len > arena_cap) return LKF_ENOSPC;
-  if (out && n) HIPCHK(hipMemcpy(out, dOut, n * sizeof(lkf_out), hipMemcpyDeviceToHost), "drain recs");
-  if (arena && len) HIPCHK(hipMemcpy(arena, dAr, len, hipMemcpyDeviceToHost), "drain bytes");
+  if (out && n) {
+    const int r = copy_to_host(e, out, dOut, n * sizeof(lkf_out), "drain recs");
+    if (r) return r;
+  }
+  if (arena && len) return copy_to_host(e, arena, dAr, len, "drain bytes");
   return LKF_OK;
 }
 
@@ -1507,8 +1540,14 @@ int lkf_drain_run(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8
     return LKF_ENOSPC;
   }
   if (tot[2] > cap || tot[3] > arena_cap) return LKF_ENOSPC;
-  if (out && tot[2]) HIPCHK(hipMemcpy(out, x.dOut, tot[2] * sizeof(lkf_out), hipMemcpyDeviceToHost), "drain recs");
-  if (arena && tot[3]) HIPCHK(hipMemcpy(arena, x.dOutArena, tot[3], hipMemcpyDeviceToHost), "drain bytes");
+  if (out && tot[2]) {
+    const int r = copy_to_host(e, out, x.dOut, tot[2] * sizeof(lkf_out), "drain recs");
+    if (r) return r;
+  }
+  if (arena && tot[3]) {
+    const int r = copy_to_host(e, arena, x.dOutArena, tot[3], "drain bytes");
+    if (r) return r;
+  }
   return LKF_OK;
 }
 

@@ -276,6 +276,8 @@ struct Lane {
   // structure ring, this batch's decoded descriptors, the marshal buffer
   DDState *dd;
   const DDStruct *ddRing;
+  const DDStruct *ddS;  // LDS copy of ring slot ddSSlot (the current structure when the batch started)
+  u32 ddSSlot;
   const DDPkt *ddPkts;
   u8 *ddBuf;
   u32 *err;
@@ -1066,7 +1068,7 @@ __device__ int fw_translate(Lane &L, const PktV &p, u32 k, Fwd &o) {
     const bool hasDD = (p.flags & LKF_PKT_DD) && L.ddPkts && (L.ddPkts[k].flags & DP_VALID);
     if (hasDD) dp = L.ddPkts[k];
     const dd::SelResult r = dd::dd_select(*L.dd, L.ddRing, dp, hasDD, pktMarker, L.h.curS, L.h.curT, L.h.prevS,
-                                          L.h.prevT, L.h.tgtS, L.h.tgtT, L.ddBuf);
+                                          L.h.prevT, L.h.tgtS, L.h.tgtT, L.ddBuf, L.ddS, L.ddSSlot);
     if (r.limit && lane_id() == 0) atomicOr(L.err, 16u);
     if (!r.selected) {
       if (r.relevant && hasf(L, F_STARTED)) {  // forwarder.go:1694-1702 (RTPMarker false)
@@ -2023,8 +2025,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   if (DDK && dd) {
     const DDState &d = *L.dd;
     uni = (d.flags & DS_KF_VALID) && (d.flags & DS_CACHE_INIT);
-    for (int c = 0; c < int(d.numChains); c++) uni = uni && d.expCount[c] == 0;  // (no chain waits: c_fire is a no-op)
-    s = L.ddRing + d.slot;
+    s = u32(d.slot) == L.ddSSlot ? L.ddS : L.ddRing + d.slot;
     for (int i = 0; uni && i < int(d.numTargets); i++) {  // the decode target Select picks (:133-176)
       if (!((d.dtActive >> i) & 1) || i32(s->dtS[i]) > L.h.tgtS || i32(s->dtT[i]) > L.h.tgtT) continue;
       const int target = s->dtTarget[i];
@@ -2158,6 +2159,19 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     const u64 ordBadM = __ballot(ddLane && inWin && !(efn >= pEfn && fi < u64(kSvcFrames) - 8));
     const u32 ordEnd = ordBadM ? u32(__ffsll((long long)ordBadM) - 1) : 64u;
     const bool adds = inWin && lane < ordEnd && eval && (!t0 || (dp.extFlags & LKF_DD_INTEGRITY));
+    // Frames an unbroken chain waits on (FrameChain.expectFrames): adding one
+    // fires its callback, and so would marking it missing or aging it out of
+    // the window; a lane whose add could do any of these takes the full step
+    // (bounds: the missing marks of an add lie in [cLast - kNack, efn - kNack))
+    for (int c = 0; c < int(d.numChains); c++) {
+      if ((d.chBroken >> c) & 1) continue;
+      for (int i = 0; i < int(d.expCount[c]); i++) {
+        const u64 e = d.exp[c][i];
+        if (adds && (e == efn || (efn > cl0 && ((e + dd::kNack >= cl0 && e + dd::kNack < efn) || e + dd::kEntries < efn))))
+          good = false;
+      }
+    }
+    SVC_WHY(14);
     const u64 addM = __ballot(adds);
     const bool firstAdd = adds && !(addM & frameM & lt);
     if (lane < u32(kSvcFrames)) sFD[lane] = u8(lane == 0 ? cache0 : dd::SD_UNKNOWN);
@@ -2515,6 +2529,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   // (the plain instantiation keeps a 16-B stub: LDS is allocated per instantiation)
   __shared__ __attribute__((aligned(16))) u8 sDDRaw[DDK ? sizeof(DDState) + kDDMaxBytes + 1 : 16];
   __shared__ u8 sSvcScr[DDK ? 64 * kSvcDDBytes : 16];  // svc_run: per-lane marshalled descriptors
+  __shared__ __attribute__((aligned(16))) u8 sDDSRaw[DDK ? sizeof(DDStruct) : 16];  // the structure in force
   __shared__ u8 sSvcFD[kSvcFrames];                    // svc_run: decisions of the run's frames
   DDState *const sDD = reinterpret_cast<DDState *>(sDDRaw);
   u8 *const sDDBuf = sDDRaw + (DDK ? sizeof(DDState) : 0);
@@ -2659,6 +2674,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #endif
   L.ddPkts = A.ddPkts;
   L.ddRing = nullptr;
+  L.ddS = reinterpret_cast<const DDStruct *>(sDDSRaw);
+  L.ddSSlot = 0xffffffffu;
   L.dd = sDD;
   L.ddBuf = sDDBuf;
   o.ddArena = A.ddArena;
@@ -2676,6 +2693,17 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     uint4 *l = reinterpret_cast<uint4 *>(sDD);
     for (u32 i = lane; i < sizeof(DDState) / 16; i += 64) l[i] = g[i];
     __syncthreads();
+    // the structure in force: its decode targets, chains and templates are
+    // read on every descriptor (selection, marshalling); the ring entries are
+    // fixed while the batch decides (k_dd_decode filled them)
+    const u32 slot = __builtin_amdgcn_readfirstlane(u32(sDD->slot));
+    if (sDD->flags & DS_KF_VALID) {
+      const uint4 *gs = reinterpret_cast<const uint4 *>(L.ddRing + slot);
+      uint4 *ls = reinterpret_cast<uint4 *>(sDDSRaw);
+      for (u32 i = lane; i < sizeof(DDStruct) / 16; i += 64) ls[i] = gs[i];
+      L.ddSSlot = slot;
+      __syncthreads();
+    }
   }
   o.outT = A.tuples + slot0;
   // SVC DownTracks (one SSRC, every packet relevant to the selector): svc_run

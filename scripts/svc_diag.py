@@ -18,7 +18,8 @@ sys.path.insert(0, ROOT)
 WHY = {1: "forward before start / sequencer init", 2: "VP9 switch point", 3: "frame order", 4: "ndti",
        5: "DTI differs within frame", 6: "attached/structure/active update/keyframe num/chains",
        7: "DD switch / first frame number", 8: "chain", 9: "frame reference dropped", 10: "marshal",
-       11: "munger (reorder/dup/padding/ssrc)", 12: "drop with open range moved", 13: "sequencer"}
+       11: "munger (reorder/dup/padding/ssrc)", 12: "drop with open range moved", 13: "sequencer",
+       14: "awaited frame (chain expectation)"}
 
 
 def main():
