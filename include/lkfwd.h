@@ -435,6 +435,37 @@ typedef struct lkf_dt_summary {
 #define LKF_DTS_DEFICIENT 0x2
 int lkf_downtrack_summaries(lkf_engine *e, lkf_dt_summary *out, uint32_t cap, uint32_t *n_out);
 
+/* ---- sender statistics (DownTrack.rtpStats = buffer.RTPStatsSender) ----- *
+ * RTPStatsSender.Update (rtpstats_sender.go:229-432) for every packet
+ * DownTrack.sendingPacket accounts (downtrack.go:1930-1959): forwarded
+ * packets (packet time = ExtPacket.Arrival; header = the incoming header as
+ * getTranslatedRTPHeader keeps it, payload = the forwarded payload), padding
+ * (lkf_padding: 12-B header, padding-only), blank frames (lkf_blank_frames:
+ * counted as padding) and RTX (lkf_rtx_emit: the bucket packet's header and
+ * payload); packet time for the last three = the call's now_ns (lkf_rtx_emit:
+ * that of the last lkf_rtx_lookup), the reference's time.Now().  Key frames
+ * forwarded: UpdateKeyFrame.  Not kept: startTime / endTime / lastKeyFrame
+ * (wall clock) and the RTCP report snapshots.  Waits for queued runs. */
+typedef struct lkf_sender_stats {
+  uint64_t ext_start_sn, ext_highest_sn, ext_start_ts, ext_highest_ts;
+  int64_t first_time_ns, highest_time_ns;
+  uint64_t last_transit, last_jitter_ext_ts;
+  uint64_t bytes, header_bytes, bytes_duplicate, header_bytes_duplicate, bytes_padding, header_bytes_padding;
+  uint64_t packets_duplicate, packets_padding, packets_out_of_order, packets_lost;
+  double jitter, max_jitter;
+  uint32_t frames, key_frames, initialized, clock_rate;
+  uint32_t gap_histogram[101]; /* gapHistogram: [missing - 1], the last bin also counts larger gaps */
+  uint32_t reserved;
+} lkf_sender_stats;
+int lkf_sender_stats_get(lkf_engine *e, int32_t dt, lkf_sender_stats *out);
+/* The snInfo ring entry of extended sequence number esn (pktSize | hdrSize << 16
+ * | flags << 24, rtpstats_sender.go:42-46), as getIntervalStats reads it. */
+int lkf_sender_sninfo(lkf_engine *e, int32_t dt, uint64_t esn, uint32_t *out);
+/* RTPStatsSender.Seed (rtpstats_sender.go:173-201; DownTrack.SeedState
+ * downtrack.go:1051-1055 on transceiver reuse): dt takes from_dt's statistics,
+ * gap histogram and snInfo ring if from_dt's are initialized (clock rate kept). */
+int lkf_sender_stats_seed(lkf_engine *e, int32_t dt, int32_t from_dt);
+
 /* ---- sequencer (sequencer.getExtPacketMetas sequencer.go:263, for RTX) --- */
 typedef struct lkf_seq_meta {
   uint64_t ext_sn, ext_ts;

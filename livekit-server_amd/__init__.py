@@ -176,6 +176,16 @@ def downtrack_summaries(api, h):
     return out[:n.value]
 
 
+def sender_stats(api, h, dts):
+    """lkf_sender_stats_get for each DownTrack handle in `dts`: SENDER_STATS_DTYPE rows."""
+    out = np.zeros(len(dts), dtype=abi.SENDER_STATS_DTYPE)
+    for i, d in enumerate(dts):
+        rc = api["sender_stats_get"](h, int(d), out[i:i + 1].ctypes.data)
+        if rc != 0:
+            raise EngineError("sender_stats_get(%d) rc=%d" % (d, rc))
+    return out
+
+
 def stream_stats(api, h, sid):
     st = abi.lkf_stream_stats()
     rc = api["stream_stats_get"](h, sid, C.byref(st))

@@ -100,6 +100,17 @@ SPEAKER_DTYPE = np.dtype([("room", "<u4"), ("participant", "<u4"), ("level", "<f
 DT_SUMMARY_DTYPE = np.dtype([("dt", "<i4"), ("subscriber", "<u4"), ("room", "<u4"), ("flags", "<u4"),
                              ("packets_sent", "<u8"), ("bytes_sent", "<u8")])
 assert DT_SUMMARY_DTYPE.itemsize == 32
+# lkf_sender_stats (DownTrack.rtpStats = buffer.RTPStatsSender)
+SENDER_STATS_DTYPE = np.dtype(
+    [(f, "<u8") for f in ("ext_start_sn", "ext_highest_sn", "ext_start_ts", "ext_highest_ts")]
+    + [("first_time_ns", "<i8"), ("highest_time_ns", "<i8"), ("last_transit", "<u8"), ("last_jitter_ext_ts", "<u8")]
+    + [(f, "<u8") for f in ("bytes", "header_bytes", "bytes_duplicate", "header_bytes_duplicate", "bytes_padding",
+                            "header_bytes_padding", "packets_duplicate", "packets_padding", "packets_out_of_order",
+                            "packets_lost")]
+    + [("jitter", "<f8"), ("max_jitter", "<f8")]
+    + [(f, "<u4") for f in ("frames", "key_frames", "initialized", "clock_rate")]
+    + [("gap_histogram", "<u4", (101,)), ("reserved", "<u4")])
+assert SENDER_STATS_DTYPE.itemsize == 584
 # NACK -> RTX (lkf_nack / lkf_rtx)
 NACK_DTYPE = np.dtype([("dt", "<i4"), ("sn", "<u2"), ("reserved", "<u2")])
 assert NACK_DTYPE.itemsize == 8
@@ -340,6 +351,7 @@ assert C.sizeof(lkf_pkt_dd) == 32, C.sizeof(lkf_pkt_dd)
 assert C.sizeof(lkf_track_params) == 64, C.sizeof(lkf_track_params)
 assert C.sizeof(lkf_out) == 40, C.sizeof(lkf_out)
 
+LKF_OUT_SWITCHING, LKF_OUT_RESUMING, LKF_OUT_KEYFRAME, LKF_OUT_MARKER = 0x01, 0x02, 0x04, 0x08  # lkf_out.flags
 OUT_DTYPE = np.dtype(
     [("ext_sn", "<u8"), ("ext_ts", "<u8"), ("out_off", "<u8"), ("dt", "<u4"), ("pkt", "<u4"),
      ("out_len", "<u2"), ("flags", "u1"), ("layer", "i1"), ("reserved", "<u4")]
@@ -437,6 +449,10 @@ def bind_engine_api(lib, prefix):
         api["next_higher_transition"] = _bind(lib, prefix + "next_higher_transition", C.c_int,
                                               [e, C.c_void_p, C.c_uint32, C.c_void_p])
         api["pause"] = _bind(lib, prefix + "pause", C.c_int, [e, C.c_void_p, C.c_uint32, C.c_void_p])
+    if hasattr(lib, prefix + "sender_stats_get"):
+        api["sender_stats_get"] = _bind(lib, prefix + "sender_stats_get", C.c_int, [e, C.c_int32, C.c_void_p])
+        api["sender_sninfo"] = _bind(lib, prefix + "sender_sninfo", C.c_int, [e, C.c_int32, C.c_uint64, P(C.c_uint32)])
+        api["sender_stats_seed"] = _bind(lib, prefix + "sender_stats_seed", C.c_int, [e, C.c_int32, C.c_int32])
     api["blank_frames"] = _bind(lib, prefix + "blank_frames", C.c_int,
                                 [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                  P(C.c_uint32), P(C.c_uint64)])

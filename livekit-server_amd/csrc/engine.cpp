@@ -152,6 +152,15 @@ struct lkf_engine {
   DevTrack *dTracks = nullptr;
   DTHot *dHot = nullptr;
   DTCum *dDTCum = nullptr;  // per DownTrack sendingPacket totals (lkf_downtrack_summaries)
+  // per DownTrack RTPStatsSender (sender_kernels.hip): statistics, gap
+  // histogram, snInfo ring; host-listed updates (padding / blank / RTX)
+  SenderStats *dSS = nullptr;
+  uint32_t *dSSGap = nullptr;
+  uint32_t *dSSRing = nullptr;
+  SenderUpd *dSSList = nullptr;
+  uint32_t *dSSGroups = nullptr;
+  uint32_t ssListCap = 0;
+  int64_t rtxNow = 0;  // now_ns of the last lkf_rtx_lookup (the RTX packets' sendingPacket time)
   DevDT *dDTs = nullptr;
   RangeEntry *dRm = nullptr;
   VP8Cold *dVc = nullptr;
@@ -443,6 +452,7 @@ static int upload_done(lkf_engine *e) {
   HIPCHK(hipDeviceSynchronize(), "upload sync");
   return LKF_OK;
 }
+static int sender_list(lkf_engine *e, std::vector<SenderUpd> &list);
 
 // The DD selector tables and per-batch DD buffers, allocated when the first
 // track with the dependency-descriptor selector appears (streams drained).
@@ -504,6 +514,17 @@ static int flush_topology(lkf_engine *e) {
     HIPCHK(hipMemcpy(e->dDTs + first, e->pendDTs.data(), e->pendDTs.size() * sizeof(DevDT), hipMemcpyHostToDevice),
            "dt upload");
     HIPCHK(hipMemset(e->dDTCum + first, 0, e->pendDTs.size() * sizeof(DTCum)), "dt totals reset");
+    {  // NewRTPStatsSender (downtrack.go:315): zero statistics at the track's clock rate
+      std::vector<SenderStats> ss(e->pendDTs.size());
+      std::memset(ss.data(), 0, ss.size() * sizeof(SenderStats));
+      for (size_t i = 0; i < ss.size(); i++) ss[i].clockRate = e->tracks[e->pendDTs[i].track].clock_rate;
+      HIPCHK(hipMemcpy(e->dSS + first, ss.data(), ss.size() * sizeof(SenderStats), hipMemcpyHostToDevice),
+             "sender stats init");
+      HIPCHK(hipMemset(e->dSSGap + first * kGapWords, 0, e->pendDTs.size() * kGapWords * sizeof(uint32_t)),
+             "sender gap reset");
+      HIPCHK(hipMemset(e->dSSRing + first * kSnInfoSize, 0, e->pendDTs.size() * kSnInfoSize * sizeof(uint32_t)),
+             "sender ring reset");
+    }
     e->pendHot.clear();
     e->pendDTs.clear();
   }
@@ -613,6 +634,9 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
   A(dalloc(&e->dDTCum, c.max_downtracks));
+  A(dalloc(&e->dSS, c.max_downtracks));
+  A(dalloc(&e->dSSGap, size_t(c.max_downtracks) * kGapWords));
+  A(dalloc(&e->dSSRing, size_t(c.max_downtracks) * kSnInfoSize));
   A(dalloc(&e->dDTs, c.max_downtracks));
   A(dalloc(&e->dRm, size_t(c.max_downtracks) * kRangeCap));
   A(dalloc(&e->dVc, c.max_downtracks));
@@ -766,7 +790,8 @@ void lkf_destroy(lkf_engine *e) {
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
-                  e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut};
+                  e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut,
+                  e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
@@ -1397,6 +1422,19 @@ int lkf_run(lkf_engine *e, void *stream) {
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum, x.dErr, e->dSticky), "accumulate");
+  {  // sendingPacket -> RTPStatsSender.Update per forwarded tuple (off the
+     // decide path: the next batch's decide runs beside it)
+    SenderLaunch sl;
+    sl.tuples = x.dTuples;
+    sl.slotBase = x.dSlotBase;
+    sl.fwdCnt = x.dFwdCnt;
+    sl.pkts = e->curPkts;
+    sl.ss = e->dSS;
+    sl.ring = e->dSSRing;
+    sl.gap = e->dSSGap;
+    sl.ndts = nd;
+    HIPCHK(launch_sender_stats(e->emitS, sl), "sender stats");
+  }
   HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
   if (e->hostProf && e->nRuns >= 3) {  // steady state: skip the first runs (initial control ops, first touch)
     e->hp[0] += std::chrono::duration<double, std::milli>(tp1 - tp0).count();
@@ -1688,6 +1726,79 @@ int lkf_drain_protected(lkf_engine *e, uint8_t *arena, uint64_t cap, uint64_t *a
   return LKF_OK;
 }
 
+int lkf_sender_stats_get(lkf_engine *e, int32_t dt, lkf_sender_stats *out) {
+  if (!e || !out || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  SenderStats s;
+  HIPCHK(hipMemcpy(&s, e->dSS + dt, sizeof(s), hipMemcpyDeviceToHost), "sender stats copy");
+  std::memset(out, 0, sizeof(*out));
+  out->ext_start_sn = s.extStartSN;
+  out->ext_highest_sn = s.extHighestSN;
+  out->ext_start_ts = s.extStartTS;
+  out->ext_highest_ts = s.extHighestTS;
+  out->first_time_ns = s.firstTime;
+  out->highest_time_ns = s.highestTime;
+  out->last_transit = s.lastTransit;
+  out->last_jitter_ext_ts = s.lastJitterExtTimestamp;
+  out->bytes = s.bytes;
+  out->header_bytes = s.headerBytes;
+  out->bytes_duplicate = s.bytesDuplicate;
+  out->header_bytes_duplicate = s.headerBytesDuplicate;
+  out->bytes_padding = s.bytesPadding;
+  out->header_bytes_padding = s.headerBytesPadding;
+  out->packets_duplicate = s.packetsDuplicate;
+  out->packets_padding = s.packetsPadding;
+  out->packets_out_of_order = s.packetsOutOfOrder;
+  out->packets_lost = s.packetsLost;
+  out->jitter = s.jitter;
+  out->max_jitter = s.maxJitter;
+  out->frames = s.frames;
+  out->key_frames = s.keyFrames;
+  out->initialized = s.initialized;
+  out->clock_rate = s.clockRate;
+  HIPCHK(hipMemcpy(out->gap_histogram, e->dSSGap + size_t(dt) * kGapWords, kGapBins * sizeof(uint32_t),
+                   hipMemcpyDeviceToHost),
+         "sender gap copy");
+  return LKF_OK;
+}
+
+int lkf_sender_sninfo(lkf_engine *e, int32_t dt, uint64_t esn, uint32_t *out) {
+  if (!e || !out || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(out, e->dSSRing + size_t(dt) * kSnInfoSize + (esn & (kSnInfoSize - 1)), sizeof(uint32_t),
+                   hipMemcpyDeviceToHost),
+         "sninfo copy");
+  return LKF_OK;
+}
+
+int lkf_sender_stats_seed(lkf_engine *e, int32_t dt, int32_t from_dt) {
+  if (!e || dt < 0 || dt >= int32_t(e->dtp.size()) || from_dt < 0 || from_dt >= int32_t(e->dtp.size()))
+    return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  SenderStats from, to;
+  HIPCHK(hipMemcpy(&from, e->dSS + from_dt, sizeof(from), hipMemcpyDeviceToHost), "sender stats copy");
+  if (!from.initialized) return LKF_OK;  // rtpStatsBase.seed: from must be initialized
+  HIPCHK(hipMemcpy(&to, e->dSS + dt, sizeof(to), hipMemcpyDeviceToHost), "sender stats copy");
+  from.clockRate = to.clockRate;  // params are not seeded
+  HIPCHK(hipMemcpy(e->dSS + dt, &from, sizeof(from), hipMemcpyHostToDevice), "sender stats seed");
+  HIPCHK(hipMemcpy(e->dSSGap + size_t(dt) * kGapWords, e->dSSGap + size_t(from_dt) * kGapWords,
+                   kGapWords * sizeof(uint32_t), hipMemcpyDeviceToDevice),
+         "sender gap seed");
+  HIPCHK(hipMemcpy(e->dSSRing + size_t(dt) * kSnInfoSize, e->dSSRing + size_t(from_dt) * kSnInfoSize,
+                   kSnInfoSize * sizeof(uint32_t), hipMemcpyDeviceToDevice),
+         "sender ring seed");
+  return upload_done(e);
+}
+
 int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *o) {
   if (!e || !o || dt < 0 || dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
   int rc = flush_topology(e);
@@ -1819,6 +1930,7 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
       if (e->active[dt]) gStart.push_back(i);  // a removed DownTrack answers no NACK
     }
   }
+  e->rtxNow = now_ns;  // retransmitPackets' time.Now() for the RTX sendingPacket (lkf_rtx_emit)
   if (gStart.empty()) return LKF_OK;
   // group ends: the next group's start or the end of its DownTrack's run
   std::vector<uint32_t> gb(gStart.size() + 1);
@@ -1920,6 +2032,30 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
          "rtx write");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
   if (tot) HIPCHK(hipMemcpy(out_arena, e->dRtxOut, tot, hipMemcpyDeviceToHost), "rtx bytes copy");
+  {  // sendingPacket (downtrack.go:1671-1681): the bucket packet's header as
+     // unmarshalled (CSRCs and extensions kept), the forwarded payload
+    std::vector<SenderUpd> ul;
+    for (uint32_t i = 0; i < n; i++) {
+      if (!len[i]) continue;
+      const uint8_t *b = src_arena + src[i].off;
+      const uint32_t cc = b[0] & 0xf;
+      uint32_t h = 12 + 4 * cc;
+      if ((b[0] & 0x10) && h + 4 <= src[i].len) h += 4 + 4 * ((uint32_t(b[h + 2]) << 8) | b[h + 3]);
+      const uint32_t outHdr = 12 + 4 * cc + (e->dtp[rtx[i].dt].ext_abs_send_time ? 8 : 0);
+      SenderUpd u;
+      std::memset(&u, 0, sizeof(u));
+      u.esn = rtx[i].meta.ext_sn;
+      u.ets = rtx[i].meta.ext_ts;
+      u.t = e->rtxNow;
+      u.dt = uint32_t(rtx[i].dt);
+      u.hdr = uint16_t(h);
+      u.pay = uint16_t(len[i] - outHdr);
+      u.marker = rtx[i].meta.marker ? 1 : 0;
+      ul.push_back(u);
+    }
+    rc = sender_list(e, ul);
+    if (rc) return rc;
+  }
   k = 0;
   for (uint32_t i = 0; i < n; i++) {
     if (!len[i]) continue;
@@ -1941,6 +2077,39 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
 // Worst-case space per request is reserved (padding: ceil(bytes / 275)
 // packets of at most 12 + 8 + 255 bytes; blank: two packets of at most
 // 12 + 8 + 80), the kernel fills what it sends, the host packs it.
+// sendingPacket -> RTPStatsSender.Update for host-listed packets (padding,
+// blank frames, RTX): grouped by DownTrack in call order, one thread per
+// DownTrack (k_sender_updates).  Runs on e->own after the producing kernel.
+static int sender_list(lkf_engine *e, std::vector<SenderUpd> &list) {
+  if (list.empty()) return LKF_OK;
+  std::stable_sort(list.begin(), list.end(), [](const SenderUpd &a, const SenderUpd &b) { return a.dt < b.dt; });
+  std::vector<uint32_t> g;
+  for (uint32_t i = 0; i < list.size(); i++)
+    if (i == 0 || list[i].dt != list[i - 1].dt) g.push_back(i);
+  g.push_back(uint32_t(list.size()));
+  if (list.size() > e->ssListCap || g.size() > e->ssListCap + 1) {
+    if (e->dSSList) (void)hipFree(e->dSSList);
+    if (e->dSSGroups) (void)hipFree(e->dSSGroups);
+    e->ssListCap = uint32_t(std::max<size_t>(2 * list.size(), 4096));
+    HIPCHK(dalloc(&e->dSSList, e->ssListCap), "alloc sender list");
+    HIPCHK(dalloc(&e->dSSGroups, e->ssListCap + 1), "alloc sender groups");
+  }
+  HIPCHK(hipMemcpy(e->dSSList, list.data(), list.size() * sizeof(SenderUpd), hipMemcpyHostToDevice), "sender list copy");
+  HIPCHK(hipMemcpy(e->dSSGroups, g.data(), g.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "sender groups copy");
+  int rc = upload_done(e);
+  if (rc) return rc;
+  SenderListLaunch a;
+  a.list = e->dSSList;
+  a.gBegin = e->dSSGroups;
+  a.ngroups = uint32_t(g.size() - 1);
+  a.ss = e->dSS;
+  a.ring = e->dSSRing;
+  a.gap = e->dSSGap;
+  HIPCHK(launch_sender_updates(e->own, a), "sender updates");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  return LKF_OK;
+}
+
 static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out,
                       uint8_t *arena, uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len,
                       uint32_t *bytes_sent) {
@@ -2043,6 +2212,26 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   if (k) {
     HIPCHK(hipMemcpy(recv.data(), e->dPadOut, recs * sizeof(lkf_out), hipMemcpyDeviceToHost), "pad out copy");
     HIPCHK(hipMemcpy(arv.data(), e->dPadArena, bytes, hipMemcpyDeviceToHost), "pad arena copy");
+    // sendingPacket (downtrack.go:835-846, :1377-1386): isPadding, a 12-B
+    // header (the pacer adds the extensions later), the payload as padding
+    std::vector<SenderUpd> ul;
+    for (uint32_t j = 0; j < m; j++)
+      for (uint32_t c = 0; c < cnt[j]; c++) {
+        const lkf_out &o = recv[loff[j] + c];
+        SenderUpd u;
+        std::memset(&u, 0, sizeof(u));
+        u.esn = o.ext_sn;
+        u.ets = o.ext_ts;
+        u.t = now_ns;
+        u.dt = o.dt;
+        u.hdr = 12;
+        u.pay = 0;
+        u.pad = uint16_t(o.out_len - (e->dtp[o.dt].ext_abs_send_time ? 20 : 12));
+        u.marker = (o.flags & LKF_OUT_MARKER) ? 1 : 0;
+        ul.push_back(u);
+      }
+    rc = sender_list(e, ul);
+    if (rc) return rc;
   }
   for (uint32_t j = 0; j < m; j++)
     for (uint32_t c = 0; c < cnt[j]; c++) tot += (uint64_t(recv[loff[j] + c].out_len) + 15) & ~uint64_t(15);

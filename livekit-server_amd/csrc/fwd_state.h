@@ -245,6 +245,25 @@ struct DTCum {
 };
 static_assert(sizeof(DTCum) == 32, "DTCum is 32 B");
 
+// DownTrack.rtpStats: buffer.RTPStatsSender (rtpstats_sender.go:135-171 and
+// the rtpStatsBase counters rtpstats_base.go:133-190 it updates per sent
+// packet).  One per DownTrack, plus its gap histogram and its 4096-entry
+// snInfo ring (u32 per slot: pktSize | hdrSize << 16 | flags << 24).
+constexpr int kSnInfoSize = 4096;  // cSnInfoSize rtpstats_sender.go:30
+constexpr int kGapBins = 101;      // cGapHistogramNumBins rtpstats_base.go:31
+constexpr int kGapWords = 104;     // per-DownTrack histogram stride (16-B multiple)
+struct alignas(16) SenderStats {
+  uint64_t extStartSN, extHighestSN, extStartTS, extHighestTS;
+  int64_t firstTime, highestTime;  // ns, virtual clock (packet arrival / call time)
+  uint64_t lastTransit, lastJitterExtTimestamp;
+  uint64_t bytes, headerBytes, bytesDuplicate, headerBytesDuplicate, bytesPadding, headerBytesPadding;
+  uint64_t packetsDuplicate, packetsPadding, packetsOutOfOrder, packetsLost;
+  double jitter, maxJitter;
+  uint32_t frames, keyFrames, initialized, clockRate;
+  uint32_t pad[4];
+};
+static_assert(sizeof(SenderStats) == 192, "SenderStats is 192 B");
+
 constexpr int kHistWords = 64;  // cHistorySize 4096 bits (rtpstats_receiver.go:30)
 
 struct DevStream {  // static stream parameters (64 B)

@@ -288,4 +288,33 @@ hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, c
 hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
                                int64_t elapsedNs, int64_t nowNs, lkf_tracker_status *out);
 
+// ---- DownTrack sender statistics (sender_kernels.hip) ------------------------
+struct SenderLaunch {  // the forwarded tuples of one batch
+  const Tuple *tuples;
+  const uint64_t *slotBase;
+  const uint32_t *fwdCnt;
+  const lkf_pkt *pkts;
+  SenderStats *ss;
+  uint32_t *ring;  // kSnInfoSize per DownTrack
+  uint32_t *gap;   // kGapWords per DownTrack
+  uint32_t ndts;
+};
+struct SenderUpd {  // one host-listed sendingPacket (padding, blank frame, RTX)
+  uint64_t esn, ets;
+  int64_t t;
+  uint32_t dt;
+  uint16_t hdr, pay, pad;
+  uint8_t marker, rsv;
+};
+struct SenderListLaunch {
+  const SenderUpd *list;   // grouped by DownTrack, call order within a group
+  const uint32_t *gBegin;  // ngroups + 1
+  uint32_t ngroups;
+  SenderStats *ss;
+  uint32_t *ring;
+  uint32_t *gap;
+};
+hipError_t launch_sender_stats(hipStream_t s, const SenderLaunch &a);
+hipError_t launch_sender_updates(hipStream_t s, const SenderListLaunch &a);
+
 }  // namespace lkf

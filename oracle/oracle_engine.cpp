@@ -28,6 +28,7 @@
 #include "red_oracle.h"
 #include "tracker_oracle.h"
 #include "nack_oracle.h"
+#include "sender_oracle.h"
 #include <map>
 
 using namespace orc;
@@ -63,6 +64,8 @@ struct ODT {
   std::vector<OOut> outs;
   // DownTrack.sendingPacket counters (downtrack.go:1930-1941)
   u64 packetsSent = 0, bytesSent = 0;
+  // DownTrack.rtpStats (buffer.NewRTPStatsSender downtrack.go:315)
+  orc_ss::RTPStatsSender ss;
   // SRTP: the subscriber transport and this SSRC's rollover state
   int32_t transport = -1;
   orc_srtp::SSRCState srtp;
@@ -118,6 +121,7 @@ struct orc_engine {
   // stream trackers: (track, spatial layer) and the tracker
   std::vector<std::pair<u32, i32>> trkKey;
   std::vector<orc_st::Tracker> trk;
+  i64 rtxNow = 0;  // now_ns of the last orc_rtx_lookup
 };
 
 static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
@@ -284,6 +288,12 @@ static void writeRTP(orc_engine *e, u32 dtIdx, ODT &d, const ExtPacket &ep, u32 
     d.firstTime = ep.Arrival;
     d.extStartTS = tp.rtp.extTimestamp;
   }
+  // sendingPacket (downtrack.go:737-749, :1930-1959): hdr.MarshalSize() of the
+  // translated header (getTranslatedRTPHeader keeps the incoming extensions:
+  // the raw header, payload_off bytes), len(payload), packet time = Arrival
+  d.ss.Update(ep.Arrival, tp.rtp.extSequenceNumber, tp.rtp.extTimestamp, hdr.Marker, int(pd_payload_off),
+              int(payload.size()), 0);
+  if (ep.KeyFrame) d.ss.UpdateKeyFrame(1);
   OOut o;
   // getTranslatedRTPHeader keeps the incoming header's extensions: the
   // counted header is the incoming one (the raw header, payload_off bytes)
@@ -334,6 +344,7 @@ int32_t orc_add_downtrack(orc_engine *e, const lkf_downtrack_params *p) {
                                         : MimeOpus;
   d->f->DetermineCodec(m, tp.clock_rate, tp.has_dd != 0);
   d->seq = std::make_unique<Sequencer>(int(e->seqSize), k == KindVideo, p->bind_time_ns / 1000000);
+  d->ss.clockRate = tp.clock_rate;
   ODT *dp = d.get();
   int32_t track = p->track;
   if (tp.has_ref_ts) {
@@ -566,6 +577,57 @@ int orc_debug_dd_state(orc_engine *e, int32_t dt, uint64_t out[16]) {
   return LKF_OK;
 }
 
+int orc_sender_stats_get(orc_engine *e, int32_t dt, lkf_sender_stats *o) {
+  if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
+  const orc_ss::RTPStatsSender &s = e->dts[dt]->ss;
+  std::memset(o, 0, sizeof(*o));
+  o->ext_start_sn = s.extStartSN;
+  o->ext_highest_sn = s.extHighestSN;
+  o->ext_start_ts = s.extStartTS;
+  o->ext_highest_ts = s.extHighestTS;
+  o->first_time_ns = s.firstTime;
+  o->highest_time_ns = s.highestTime;
+  o->last_transit = s.lastTransit;
+  o->last_jitter_ext_ts = s.lastJitterExtTimestamp;
+  o->bytes = s.bytes;
+  o->header_bytes = s.headerBytes;
+  o->bytes_duplicate = s.bytesDuplicate;
+  o->header_bytes_duplicate = s.headerBytesDuplicate;
+  o->bytes_padding = s.bytesPadding;
+  o->header_bytes_padding = s.headerBytesPadding;
+  o->packets_duplicate = s.packetsDuplicate;
+  o->packets_padding = s.packetsPadding;
+  o->packets_out_of_order = s.packetsOutOfOrder;
+  o->packets_lost = s.packetsLost;
+  o->jitter = s.jitter;
+  o->max_jitter = s.maxJitter;
+  o->frames = s.frames;
+  o->key_frames = s.keyFrames;
+  o->initialized = s.initialized ? 1 : 0;
+  o->clock_rate = s.clockRate;
+  std::memcpy(o->gap_histogram, s.gapHistogram, sizeof(s.gapHistogram));
+  return LKF_OK;
+}
+
+int orc_sender_sninfo(orc_engine *e, int32_t dt, uint64_t esn, uint32_t *out) {
+  if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
+  const orc_ss::SnInfo &i = e->dts[dt]->ss.snInfos[esn & orc_ss::kSnInfoMask];
+  *out = u32(i.pktSize) | (u32(i.hdrSize) << 16) | (u32(i.flags) << 24);
+  return LKF_OK;
+}
+
+// RTPStatsSender.Seed rtpstats_sender.go:173-201 (rtpStatsBase.seed :206-262)
+int orc_sender_stats_seed(orc_engine *e, int32_t dt, int32_t from) {
+  if (dt < 0 || dt >= (int)e->dts.size() || from < 0 || from >= (int)e->dts.size()) return LKF_EINVAL;
+  const orc_ss::RTPStatsSender &f = e->dts[from]->ss;
+  if (!f.initialized) return LKF_OK;
+  orc_ss::RTPStatsSender &t = e->dts[dt]->ss;
+  const u32 cr = t.clockRate;
+  t = f;
+  t.clockRate = cr;
+  return LKF_OK;
+}
+
 int orc_get_state(orc_engine *e, int32_t dt, lkf_fwd_state *o) {
   if (dt < 0 || dt >= (int)e->dts.size()) return LKF_EINVAL;
   ForwarderState s = e->dts[dt]->f->GetState();
@@ -643,6 +705,7 @@ static void epm_to_meta(const ExtPacketMeta &r, lkf_seq_meta &m) {
 int orc_rtx_lookup(orc_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now_ns, lkf_rtx *out, uint32_t cap,
                    uint32_t *n_out) {
   *n_out = 0;
+  e->rtxNow = now_ns;
   std::vector<lkf_rtx> res;
   for (u32 i = 0; i < n;) {
     const int32_t dt = nacks[i].dt;
@@ -694,7 +757,7 @@ int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   for (u32 i = 0; i < n; i++) {
     const lkf_rtx &x = rtx[i];
     if (x.dt < 0 || x.dt >= (int)e->dts.size()) return LKF_EINVAL;
-    const ODT &d = *e->dts[x.dt];
+    ODT &d = *e->dts[x.dt];
     if (!src[i].len) continue;  // ReadRTP miss
     const u8 *buf = src_arena + src[i].off;
     RtpParsed h;
@@ -728,6 +791,10 @@ int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
     std::vector<u8> bytes;
     hdr.Marshal(bytes);
     bytes.insert(bytes.end(), payload.begin(), payload.end());
+    // sendingPacket (downtrack.go:1671-1681): pkt.Header as unmarshalled from the
+    // bucket (CSRCs, extensions), len(payload), packet time = time.Now() (the
+    // NACK processing time of the last orc_rtx_lookup)
+    d.ss.Update(e->rtxNow, x.meta.ext_sn, x.meta.ext_ts, x.meta.marker != 0, h.hdrSize, int(payload.size()), 0);
     lkf_out o;
     std::memset(&o, 0, sizeof(o));
     o.ext_sn = x.meta.ext_sn;
@@ -813,6 +880,7 @@ static u32 writePadding(orc_engine *e, u32 dtIdx, u32 reqIdx, const lkf_pad_req 
     // sendingPacket: shouldDisableCounter, padding (no bytesSent; RTPStatsSender
     // does not start on a padding-only packet rtpstats_sender.go:246-249)
     padPacket(e, d, dtIdx, reqIdx, hdr, payload, v.extSequenceNumber, v.extTimestamp);
+    d.ss.Update(now, v.extSequenceNumber, v.extTimestamp, hdr.Marker, 12, 0, int(payload.size()));  // isPadding
     sent += 12 + 255;  // hdr.MarshalSize() + len(payload)
   }
   return sent;
@@ -855,6 +923,7 @@ static void writeBlank(orc_engine *e, u32 dtIdx, u32 reqIdx, const lkf_pad_req &
     }
     d.packetsSent++;  // sendingPacket: hdr.MarshalSize() + len(payload)
     d.bytesSent += 12 + payload.size();
+    d.ss.Update(now, v.extSequenceNumber, v.extTimestamp, true, 12, 0, int(payload.size()));  // isPadding (:1383)
     padPacket(e, d, dtIdx, reqIdx, hdr, payload, v.extSequenceNumber, v.extTimestamp);
     frameEndNeeded = false;  // only the first packet closes the open frame
   }

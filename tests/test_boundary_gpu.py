@@ -18,6 +18,7 @@ import numpy as np
 import pytest
 
 from tests.oracle_lib import load as load_oracle
+from tests.test_parity_gpu import check_sender_stats
 from tests.test_ingress_gpu import check_nacks
 
 pytestmark = pytest.mark.gpu
@@ -63,6 +64,7 @@ def _reuse(abi, trace, api, h, dts, n0, orig):
         nh = api["add_downtrack"](h, C.byref(p))
         assert nh == n0 + i, (nh, n0 + i)
         assert api["seed_state"](h, nh, C.byref(s)) == 0
+        assert api["sender_stats_seed"](h, nh, d) == 0  # DownTrack.SeedState: rtpStats.Seed (downtrack.go:1051-1055)
         if trace.tracks[p.track].kind == abi.LKF_KIND_VIDEO:
             assert api["ctl"](h, nh, abi.LKF_CTL_SET_ALLOCATION, 2, 2, 2, 0, 0) == 0
     return states
@@ -107,6 +109,8 @@ def test_state_roundtrip_transceiver_reuse(pkg, workload, abi, cfg):
         gsum, osum = pkg.downtrack_summaries(eng.api, eng.h), pkg.downtrack_summaries(o.api, oh)
         for f in abi.DT_SUMMARY_DTYPE.names:
             assert np.array_equal(gsum[f], osum[f]), f
+        ss = check_sender_stats(pkg, eng.api, eng.h, o.api, oh, range(n))
+        assert int(ss["initialized"][tr.ndts:].sum()) > 0  # seeded statistics carried on
     finally:
         eng.close()
         o.destroy(oh)

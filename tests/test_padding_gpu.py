@@ -14,6 +14,7 @@ import pytest
 
 from tests import pad_lib, rtx_lib
 from tests.oracle_lib import load as load_oracle
+from tests.test_parity_gpu import check_sender_stats
 
 pytestmark = pytest.mark.gpu
 EPOCH = 1700000000 * 10**9
@@ -76,6 +77,9 @@ def test_padding_and_blank_frames_match_oracle(pkg, workload, cfg):
         for dt in range(tr.ndts):
             assert _state(eng.api, eng.h, dt, abi) == _state(o.api, oh, dt, abi), dt
         _same(pkg.downtrack_summaries(eng.api, eng.h), pkg.downtrack_summaries(o.api, oh), "summaries")
+        # RTPStatsSender after forwarded packets, padding and blank frames (sendingPacket isPadding)
+        ss = check_sender_stats(pkg, eng.api, eng.h, o.api, oh, range(tr.ndts))
+        assert int(ss["packets_padding"].sum()) > 0
         nacks = rtx_lib.make_nacks(o.api, oh, tr, seed=7, per_dt=12)
         now = EPOCH + tr.nbatches * 10**9 + 5 * 10**8
         _same(rtx_lib.rtx_lookup(eng.api, eng.h, nacks, now), rtx_lib.rtx_lookup(o.api, oh, nacks, now), "rtx")

@@ -28,6 +28,28 @@ def _state_tuple(api, h, dt, abi):
     return st.as_tuple()
 
 
+def check_sender_stats(pkg, gapi, gh, oapi, oh, dts):
+    """DownTrack.rtpStats (RTPStatsSender) of every listed DownTrack: every field
+    bit-exact (jitter as float64 bits) and the snInfo ring around the highest SN."""
+    dts = list(dts)
+    g = pkg.sender_stats(gapi, gh, dts)
+    o = pkg.sender_stats(oapi, oh, dts)
+    gb, ob = g.view(np.uint8).reshape(len(dts), -1), o.view(np.uint8).reshape(len(dts), -1)
+    if not np.array_equal(gb, ob):
+        i = int(np.nonzero((gb != ob).any(axis=1))[0][0])
+        diff = [f for f in g.dtype.names if not np.array_equal(g[f][i], o[f][i])]
+        raise AssertionError("sender stats of DownTrack %d differ in %s: gpu %s orc %s" % (
+            dts[i], diff, [g[f][i] for f in diff], [o[f][i] for f in diff]))
+    gi, oi = C.c_uint32(), C.c_uint32()
+    for k, d in enumerate(dts[::max(1, len(dts) // 9)]):
+        hi = int(g["ext_highest_sn"][dts.index(d)])
+        for esn in range(hi - 70, hi + 2):
+            assert gapi["sender_sninfo"](gh, d, esn, C.byref(gi)) == 0
+            assert oapi["sender_sninfo"](oh, d, esn, C.byref(oi)) == 0
+            assert gi.value == oi.value, ("snInfo", d, esn, hex(gi.value), hex(oi.value))
+    return g
+
+
 def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True, extra_ops=None):
     o = load_oracle()
     eng = pkg.Engine.for_trace(trace)
@@ -79,6 +101,7 @@ def run_parity(pkg, workload, abi, trace, check_state=True, seq_probe=True, extr
         if check_state:
             for dt in range(trace.ndts):
                 assert _state_tuple(eng.api, eng.h, dt, abi) == _state_tuple(o.api, oh, dt, abi), dt
+            check_sender_stats(pkg, eng.api, eng.h, o.api, oh, range(trace.ndts))
         if seq_probe:
             # sequencer.getExtPacketMetas on a few DownTracks (NACK -> RTX lookup)
             now = 1700000000 * 10**9 + int(trace.nbatches * 1.5e9)

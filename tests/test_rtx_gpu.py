@@ -9,6 +9,7 @@ import pytest
 
 from tests import rtx_lib
 from tests.oracle_lib import load as load_oracle
+from tests.test_parity_gpu import check_sender_stats
 
 pytestmark = pytest.mark.gpu
 EPOCH = 1700000000 * 10**9
@@ -51,6 +52,9 @@ def test_rtx_lookup_and_emit_match_oracle(pkg, workload, cfg):
                 for f in oo.dtype.names:
                     assert np.array_equal(go[f], oo[f]), f
                 assert np.array_equal(gw, ow)
+                # RTPStatsSender.Update of the retransmissions (duplicates / out of order)
+                ss = check_sender_stats(pkg, eng.api, eng.h, o.api, oh, range(tr.ndts))
+                assert int(ss["packets_duplicate"].sum()) > 0
     finally:
         eng.close()
         o.destroy(oh)
