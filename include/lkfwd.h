@@ -506,10 +506,12 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
  * source packet (the bucket's raw RTP bytes) in src_arena (len 0: the read
  * failed, no packet); the header gets the sequencer's marker/SN/TS and the
  * DownTrack's SSRC and payload type, a VP8 payload its stored munged
- * descriptor (translateVP8PacketTo), and the pacer's extension block
- * (abs-send-time placeholder; the DD element is not kept by this sequencer, so
- * RTX of a DownTrack with the DD extension carries none).  Output as lkf_out
- * records (pkt = index of the lkf_rtx) + 16-B aligned wire packets. */
+ * descriptor (translateVP8PacketTo), and the pacer's extension block: the
+ * sequencer slot's ddBytes under the DownTrack's DD extension id
+ * (sequencer.go:198-199, :326; downtrack.go:1684 — lkf_rtx.reserved carries
+ * the slot from lkf_rtx_lookup, read while the slot still holds the record, so
+ * emit before the next lkf_run), then the abs-send-time placeholder.  Output as
+ * lkf_out records (pkt = index of the lkf_rtx) + 16-B aligned wire packets. */
 int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
                  uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
                  uint64_t *out_len);

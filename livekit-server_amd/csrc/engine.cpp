@@ -161,6 +161,15 @@ struct lkf_engine {
   uint32_t *dSSGroups = nullptr;
   uint32_t ssListCap = 0;
   int64_t rtxNow = 0;  // now_ns of the last lkf_rtx_lookup (the RTX packets' sendingPacket time)
+  // sequencer ddBytes (sequencer.go:198-199) of the DownTracks that can forward
+  // a dependency descriptor: [ring index][slot] kSeqDDBytes, grown on demand
+  uint8_t *dSeqDD = nullptr;
+  uint32_t *dSeqDDIdx = nullptr;   // per DownTrack: ring index or 0xffffffff
+  uint32_t *dSeqDDList = nullptr;  // ring index -> DownTrack
+  uint32_t nSeqDD = 0, seqDDCap = 0;
+  std::vector<uint32_t> seqDDList;
+  uint8_t *dRtxDD = nullptr;  // lkf_rtx_emit: per record kSeqDDBytes
+  uint32_t rtxDDCap = 0;
   DevDT *dDTs = nullptr;
   RangeEntry *dRm = nullptr;
   VP8Cold *dVc = nullptr;
@@ -525,6 +534,36 @@ static int flush_topology(lkf_engine *e) {
       HIPCHK(hipMemset(e->dSSRing + first * kSnInfoSize, 0, e->pendDTs.size() * kSnInfoSize * sizeof(uint32_t)),
              "sender ring reset");
     }
+    {  // DownTracks that can forward a DD (its selector and a negotiated extension id): a ddBytes ring
+      std::vector<uint32_t> idx;
+      const uint32_t n0 = e->nSeqDD;
+      for (size_t i = 0; i < e->pendDTs.size(); i++) {
+        const uint32_t d = uint32_t(first + i);
+        const bool dd = track_has_dd(e->tracks[e->dtp[d].track]) && e->dtp[d].ext_dd != 0;
+        idx.push_back(dd ? e->nSeqDD++ : 0xffffffffu);
+        if (dd) e->seqDDList.push_back(d);
+      }
+      if (e->nSeqDD > e->seqDDCap) {  // grow (the streams are drained): copy the rings already filled
+        const uint32_t cap = std::max<uint32_t>(e->nSeqDD, 2 * e->seqDDCap);
+        const size_t per = size_t(e->cfg.seq_size) * kSeqDDBytes;
+        uint8_t *nr = nullptr;
+        HIPCHK(dalloc(&nr, size_t(cap) * per), "alloc sequencer dd");
+        HIPCHK(hipMemset(nr, 0, size_t(cap) * per), "sequencer dd reset");
+        if (e->dSeqDD) {
+          HIPCHK(hipMemcpy(nr, e->dSeqDD, size_t(n0) * per, hipMemcpyDeviceToDevice), "sequencer dd move");
+          HIPCHK(hipFree(e->dSeqDD), "free sequencer dd");
+        }
+        if (e->dSeqDDList) HIPCHK(hipFree(e->dSeqDDList), "free sequencer dd list");
+        HIPCHK(dalloc(&e->dSeqDDList, cap), "alloc sequencer dd list");
+        e->dSeqDD = nr;
+        e->seqDDCap = cap;
+      }
+      HIPCHK(hipMemcpy(e->dSeqDDIdx + first, idx.data(), idx.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
+             "sequencer dd index");
+      if (e->nSeqDD > n0)
+        HIPCHK(hipMemcpy(e->dSeqDDList, e->seqDDList.data(), e->nSeqDD * sizeof(uint32_t), hipMemcpyHostToDevice),
+               "sequencer dd list");
+    }
     e->pendHot.clear();
     e->pendDTs.clear();
   }
@@ -635,6 +674,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dHot, c.max_downtracks));
   A(dalloc(&e->dDTCum, c.max_downtracks));
   A(dalloc(&e->dSS, c.max_downtracks));
+  A(dalloc(&e->dSeqDDIdx, c.max_downtracks));
   A(dalloc(&e->dSSGap, size_t(c.max_downtracks) * kGapWords));
   A(dalloc(&e->dSSRing, size_t(c.max_downtracks) * kSnInfoSize));
   A(dalloc(&e->dDTs, c.max_downtracks));
@@ -715,6 +755,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(hipMemset(e->dHot, 0, size_t(c.max_downtracks) * sizeof(DTHot)));
     A(hipMemset(e->dDTs, 0, size_t(c.max_downtracks) * sizeof(DevDT)));
     A(hipMemset(e->dDTCum, 0, size_t(c.max_downtracks) * sizeof(DTCum)));
+    A(hipMemset(e->dSeqDDIdx, 0xff, size_t(c.max_downtracks) * sizeof(uint32_t)));
     A(hipMemset(e->dTracks, 0, size_t(c.max_tracks) * sizeof(DevTrack)));
     A(hipMemset(e->dStreamHot, 0, size_t(e->maxStreams) * sizeof(StreamHot)));
     A(hipMemset(e->dStreamRings, 0, size_t(e->maxStreams) * kRangeCap * sizeof(RangeEntry)));
@@ -791,7 +832,8 @@ void lkf_destroy(lkf_engine *e) {
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
                   e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut,
-                  e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups};
+                  e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups, e->dSeqDD, e->dSeqDDIdx,
+                  e->dSeqDDList, e->dRtxDD};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
@@ -1383,6 +1425,25 @@ int lkf_run(lkf_engine *e, void *stream) {
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(x.decided, s), "event");
+  if (e->nSeqDD && e->ddAlloc) {  // sequencer ddBytes (decide stream: before the next batch's decide)
+    SeqDDLaunch q;
+    q.list = e->dSeqDDList;
+    q.n = e->nSeqDD;
+    q.hot = e->dHot;
+    q.seq = e->dSeq;
+    q.seqSize = e->cfg.seq_size;
+    q.srm = e->dSrm;
+    q.srmStride = e->srmStride;
+    q.srmCap = e->srmCap;
+    q.ddIdx = e->dSeqDDIdx;
+    q.seqDD = e->dSeqDD;
+    q.tuples = x.dTuples;
+    q.slotBase = x.dSlotBase;
+    q.fwdCnt = x.dFwdCnt;
+    q.pkts = e->curPkts;
+    q.ddArena = x.dDDArena;
+    HIPCHK(launch_seq_dd(s, q), "sequencer dd");
+  }
 
   // ---- emit stage (emit stream): wire bytes.  The decide stream goes
   // straight on to the next batch's decide.
@@ -2000,8 +2061,19 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   if (src_len) HIPCHK(hipMemcpy(e->dRtxIn, src_arena, src_len, hipMemcpyHostToDevice), "src arena copy");
   rc = upload_done(e);
   if (rc) return rc;
+  const uint8_t *rtxDD = nullptr;
+  if (e->nSeqDD) {  // epm.ddBytes of each record (its sequencer slot)
+    if (n > e->rtxDDCap) {
+      if (e->dRtxDD) (void)hipFree(e->dRtxDD);
+      e->rtxDDCap = std::max<uint32_t>(n, 1024);
+      HIPCHK(dalloc(&e->dRtxDD, size_t(e->rtxDDCap) * kSeqDDBytes), "alloc rtx dd");
+    }
+    HIPCHK(launch_rtx_dd(e->own, n, e->dRtx, e->dDTs, e->dSeq, e->cfg.seq_size, e->dSeqDDIdx, e->dSeqDD, e->dRtxDD),
+           "rtx dd");
+    rtxDD = e->dRtxDD;
+  }
   HIPCHK(launch_rtx_emit(e->own, false, n, e->dRtx, e->dRtxSrc, e->dRtxIn, e->dDTs, e->dTracks, e->dRtxLen, nullptr,
-                         nullptr),
+                         nullptr, rtxDD),
          "rtx size");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
   std::vector<uint32_t> len(n);
@@ -2028,7 +2100,7 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   rc = upload_done(e);
   if (rc) return rc;
   HIPCHK(launch_rtx_emit(e->own, true, n, e->dRtx, e->dRtxSrc, e->dRtxIn, e->dDTs, e->dTracks, e->dRtxLen, e->dRtxOff,
-                         e->dRtxOut),
+                         e->dRtxOut, rtxDD),
          "rtx write");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
   if (tot) HIPCHK(hipMemcpy(out_arena, e->dRtxOut, tot, hipMemcpyDeviceToHost), "rtx bytes copy");
@@ -2041,7 +2113,9 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
       const uint32_t cc = b[0] & 0xf;
       uint32_t h = 12 + 4 * cc;
       if ((b[0] & 0x10) && h + 4 <= src[i].len) h += 4 + 4 * ((uint32_t(b[h + 2]) << 8) | b[h + 3]);
-      const uint32_t outHdr = 12 + 4 * cc + (e->dtp[rtx[i].dt].ext_abs_send_time ? 8 : 0);
+      const uint8_t *w = out_arena + off[i];  // the RTX header as written (CSRCs, pacer extension block)
+      uint32_t outHdr = 12 + 4 * uint32_t(w[0] & 0xf);
+      if (w[0] & 0x10) outHdr += 4 + 4 * ((uint32_t(w[outHdr + 2]) << 8) | w[outHdr + 3]);
       SenderUpd u;
       std::memset(&u, 0, sizeof(u));
       u.esn = rtx[i].meta.ext_sn;

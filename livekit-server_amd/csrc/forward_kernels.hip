@@ -3829,6 +3829,57 @@ __global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u8 *srmB
 }
 
 // ---------------------------------------------------------------------------
+// k_seq_dd: the ddBytes of sequencer.push (sequencer.go:198-199) for the
+// DownTracks that can forward a dependency descriptor (one wave each, after
+// the batch's decide, on the decide stream, so the DownTrack's sequencer head
+// is the batch's final one).  A tuple whose record is still in the ring —
+// seq_find of its munged SN gives a slot holding that target and source SN —
+// stores its descriptor bytes (or none) in the slot's 256-B DD entry (length
+// byte + up to 255 bytes); a tuple pushed out later in the batch or never
+// stored (too old) has no slot, as in the reference.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_seq_dd(const u32 *__restrict__ list, u32 n, const DTHot *__restrict__ hot,
+                                               const SeqMeta *__restrict__ seqBase, u32 seqSize, u8 *srmBase,
+                                               u64 srmStride, u32 srmCap, const u32 *__restrict__ ddIdx, u8 *seqDD,
+                                               const Tuple *__restrict__ tuples, const u64 *__restrict__ slotBase,
+                                               const u32 *__restrict__ fwdCnt, const lkf_pkt *__restrict__ pkts,
+                                               const u8 *__restrict__ ddArena) {
+  const u32 w = blockIdx.x, lane = threadIdx.x;
+  if (w >= n) return;
+  const u32 d = list[w];
+  const u32 cnt = fwdCnt[d];
+  if (!cnt) return;
+  const DTHot h = hot[d];
+  if (!(h.flags & F_SEQ_INIT)) return;
+  const SeqMeta *seq = seqBase + size_t(d) * seqSize;
+  SeqRM *srm = reinterpret_cast<SeqRM *>(srmBase + size_t(d) * srmStride);
+  u8 *ring = seqDD + size_t(ddIdx[d]) * seqSize * kSeqDDBytes;
+  const Tuple *tp = tuples + slotBase[d];
+  for (u32 c0 = 0; c0 < cnt; c0 += 64) {
+    const u32 k = c0 + lane;
+    if (k < cnt) {
+      const Tuple t = tp[k];
+      u64 ext = 0;
+      const int slot = seq_find(h, srm, srmCap, seqSize, u16(t.extSN), ext);
+      if (slot >= 0 && ext == t.extSN && seq[slot].targetSeqNo == u16(t.extSN) &&
+          seq[slot].sourceSeqNo == u16(pkts[t.pkt].ext_sn)) {
+        u8 *e = ring + size_t(slot) * kSeqDDBytes;
+        const u32 len = (t.flags & T_DD) ? t.ddLen : 0u;
+        e[0] = u8(len);
+        for (u32 i = 0; i < len; i++) e[1 + i] = ddArena[t.ddOff + i];
+      }
+    }
+  }
+}
+
+hipError_t launch_seq_dd(hipStream_t s, const SeqDDLaunch &a) {
+  if (!a.n) return hipSuccess;
+  hipLaunchKernelGGL(k_seq_dd, dim3(a.n), dim3(64), 0, s, a.list, a.n, a.hot, a.seq, a.seqSize, a.srm, a.srmStride,
+                     a.srmCap, a.ddIdx, a.seqDD, a.tuples, a.slotBase, a.fwdCnt, a.pkts, a.ddArena);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // k_rtx_lookup: DownTrack.retransmitPackets up to Receiver.ReadRTP
 // (downtrack.go:1596-1631) for many DownTracks at once — one lane per
 // DownTrack NACK list (serial over it, as getExtPacketMetas mutates the
@@ -3882,6 +3933,7 @@ __global__ void k_rtx_lookup(const DTHot *__restrict__ hot, SeqMeta *seqBase, u3
             r.meta.codec_len = m.codecLen;
             for (int q = 0; q < 8; q++) r.meta.codec[q] = m.codec[q];
             r.dt = int32_t(d);
+            r.reserved = u32(slot) + 1;  // the sequencer slot: lkf_rtx_emit reads its ddBytes there
             out[k] = r;
             ok = 1;
           }

@@ -165,6 +165,7 @@ constexpr int kDDFdiffs = 8;       // frame diffs of one frame (custom fdiffs)
 constexpr int kDDExpect = 16;      // frames one chain may wait on (FrameChain.expectFrames)
 constexpr int kDDSlots = 8;        // structure ring per track
 constexpr int kDDMaxBytes = 255;   // marshalled DD (pion two-byte extension element)
+constexpr int kSeqDDBytes = 256;   // a sequencer slot's ddBytes entry: length byte + kDDMaxBytes
 
 struct DDTmpl {  // dependencydescriptor.FrameDependencyTemplate of a structure (32 B)
   uint8_t sid, tid, nfd, pad;

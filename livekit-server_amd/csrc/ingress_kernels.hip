@@ -1542,8 +1542,9 @@ template <bool WRITE>
 __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, const lkf_raw_pkt *__restrict__ src,
                                             const u8 *__restrict__ arena, const DevDT *__restrict__ dts,
                                             const DevTrack *__restrict__ tracks, u32 *__restrict__ lens,
-                                            const u64 *__restrict__ offs, u8 *__restrict__ out) {
-  __shared__ u8 pre[12 + 60 + 8 + 8];
+                                            const u64 *__restrict__ offs, u8 *__restrict__ out,
+                                            const u8 *__restrict__ dd) {
+  __shared__ u8 pre[12 + 60 + 4 + 2 + kDDMaxBytes + 5 + 3 + 8 + 4];
   __shared__ u32 sPre, sLen, sPay, sPayLen;
   const u32 i = blockIdx.x, lane = threadIdx.x;
   if (lane == 0) {
@@ -1566,15 +1567,50 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
       for (int k = 3; k >= 0; k--) pre[n++] = u8(x.meta.timestamp >> (8 * k));
       for (int k = 3; k >= 0; k--) pre[n++] = u8(dt.ssrc >> (8 * k));
       for (int k = 0; k < 4 * cc; k++) pre[n++] = b[12 + k];
-      if (dt.extAbs) {  // pion one-byte profile, one 3-byte element
+      // the pacer's extension block (pacer/base.go:71-100): the sequencer's
+      // ddBytes under the DownTrack's DD extension id (downtrack.go:1684; ID 0
+      // or no bytes: skipped), then abs-send-time; pion's one-byte profile, or
+      // the two-byte profile for a DD above 16 B
+      const u32 ddLen = (dd && dt.extDD) ? dd[size_t(i) * kSeqDDBytes] : 0u;
+      const u8 *ddB = ddLen ? dd + size_t(i) * kSeqDDBytes + 1 : nullptr;
+      if (ddLen > 16) {
+        const int eb = 2 + int(ddLen) + (dt.extAbs ? 5 : 0);
+        const int words = (eb + 3) >> 2;
+        pre[0] |= 0x10;
+        pre[n++] = 0x10;
+        pre[n++] = 0x00;
+        pre[n++] = u8(words >> 8);
+        pre[n++] = u8(words);
+        pre[n++] = dt.extDD;
+        pre[n++] = u8(ddLen);
+        for (u32 k = 0; k < ddLen; k++) pre[n++] = ddB[k];
+        if (dt.extAbs) {
+          pre[n++] = dt.extAbs;
+          pre[n++] = 3;
+          pre[n++] = 0;
+          pre[n++] = 0;
+          pre[n++] = 0;
+        }
+        for (int k = eb; k < 4 * words; k++) pre[n++] = 0;
+      } else if (ddLen || dt.extAbs) {
+        const int eb = (ddLen ? 1 + int(ddLen) : 0) + (dt.extAbs ? 4 : 0);
+        const int words = (eb + 3) >> 2;
+        pre[0] |= 0x10;
         pre[n++] = 0xBE;
         pre[n++] = 0xDE;
-        pre[n++] = 0;
-        pre[n++] = 1;
-        pre[n++] = u8((dt.extAbs << 4) | 2);
-        pre[n++] = 0;
-        pre[n++] = 0;
-        pre[n++] = 0;
+        pre[n++] = u8(words >> 8);
+        pre[n++] = u8(words);
+        if (ddLen) {
+          pre[n++] = u8((dt.extDD << 4) | (ddLen - 1));
+          for (u32 k = 0; k < ddLen; k++) pre[n++] = ddB[k];
+        }
+        if (dt.extAbs) {
+          pre[n++] = u8((dt.extAbs << 4) | 2);
+          pre[n++] = 0;
+          pre[n++] = 0;
+          pre[n++] = 0;
+        }
+        for (int k = eb; k < 4 * words; k++) pre[n++] = 0;
       }
       if (tracks[dt.track].codec == LKF_CODEC_VP8 && payLen > 0 && x.meta.codec_len) {
         IngParsed v = {};
@@ -1605,12 +1641,43 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
 
 hipError_t launch_rtx_emit(hipStream_t s, bool write, u32 n, const lkf_rtx *rtx, const lkf_raw_pkt *src,
                            const u8 *arena, const DevDT *dts, const DevTrack *tracks, u32 *lens, const u64 *offs,
-                           u8 *out) {
+                           u8 *out, const u8 *dd) {
   if (!n) return hipSuccess;
   if (write)
-    hipLaunchKernelGGL(k_rtx<true>, dim3(n), dim3(64), 0, s, rtx, src, arena, dts, tracks, lens, offs, out);
+    hipLaunchKernelGGL(k_rtx<true>, dim3(n), dim3(64), 0, s, rtx, src, arena, dts, tracks, lens, offs, out, dd);
   else
-    hipLaunchKernelGGL(k_rtx<false>, dim3(n), dim3(64), 0, s, rtx, src, arena, dts, tracks, lens, offs, out);
+    hipLaunchKernelGGL(k_rtx<false>, dim3(n), dim3(64), 0, s, rtx, src, arena, dts, tracks, lens, offs, out, dd);
+  return hipGetLastError();
+}
+
+// k_rtx_dd: epm.ddBytes of each lkf_rtx record (sequencer.go:326: copied
+// from its slot at getExtPacketMetas) — the slot k_rtx_lookup returned
+// (reserved = slot + 1), if it still holds the record's target SN; one
+// thread per record, 256 B staged per record
+__global__ void k_rtx_dd(u32 n, const lkf_rtx *__restrict__ rtx, const DevDT *__restrict__ dts,
+                         const SeqMeta *__restrict__ seq, u32 seqSize, const u32 *__restrict__ ddIdx,
+                         const u8 *__restrict__ seqDD, u8 *__restrict__ dd) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const lkf_rtx x = rtx[i];
+  u8 *o = dd + size_t(i) * kSeqDDBytes;
+  u32 len = 0;
+  const u32 d = u32(x.dt);
+  if (x.reserved && x.reserved <= seqSize && ddIdx[d] != 0xffffffffu && dts[d].extDD) {
+    const u32 slot = x.reserved - 1;
+    if (seq[size_t(d) * seqSize + slot].targetSeqNo == x.meta.target_sn) {
+      const u8 *e = seqDD + (size_t(ddIdx[d]) * seqSize + slot) * kSeqDDBytes;
+      len = e[0];
+      for (u32 k = 0; k < len; k++) o[1 + k] = e[1 + k];
+    }
+  }
+  o[0] = u8(len);
+}
+
+hipError_t launch_rtx_dd(hipStream_t s, u32 n, const lkf_rtx *rtx, const DevDT *dts, const SeqMeta *seq, u32 seqSize,
+                         const u32 *ddIdx, const u8 *seqDD, u8 *dd) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_rtx_dd, dim3((n + 63) / 64), dim3(64), 0, s, n, rtx, dts, seq, seqSize, ddIdx, seqDD, dd);
   return hipGetLastError();
 }
 

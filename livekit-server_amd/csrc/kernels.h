@@ -153,7 +153,7 @@ hipError_t launch_rtx_lookup(hipStream_t s, const DTHot *hot, SeqMeta *seq, uint
                              const uint32_t *gStart, uint32_t ngroups, int64_t nowMs, lkf_rtx *out, uint32_t *valid);
 hipError_t launch_rtx_emit(hipStream_t s, bool write, uint32_t n, const lkf_rtx *rtx, const lkf_raw_pkt *src,
                            const uint8_t *arena, const DevDT *dts, const DevTrack *tracks, uint32_t *lens,
-                           const uint64_t *offs, uint8_t *out);
+                           const uint64_t *offs, uint8_t *out, const uint8_t *dd);
 // ---- SRTP protect (srtp_kernels.hip) ----
 struct SrtpKeys {  // one transport's session (RFC 3711 AES_CM_128_HMAC_SHA1_80)
   uint32_t rk[44];   // AES-128 schedule of the session key (big-endian words)
@@ -287,6 +287,30 @@ hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, c
                                   const uint32_t *tBegin, const uint32_t *tEnd);
 hipError_t launch_tracker_tick(hipStream_t s, TrackerState *st, const int32_t *ids, uint32_t n, int check,
                                int64_t elapsedNs, int64_t nowNs, lkf_tracker_status *out);
+
+// ---- sequencer ddBytes (forward_kernels.hip k_seq_dd, ingress_kernels.hip k_rtx_dd)
+struct SeqDDLaunch {
+  const uint32_t *list;  // DownTracks with a DD entry ring
+  uint32_t n;
+  const DTHot *hot;
+  const SeqMeta *seq;
+  uint32_t seqSize;
+  uint8_t *srm;
+  uint64_t srmStride;
+  uint32_t srmCap;
+  const uint32_t *ddIdx;  // DownTrack -> ring index
+  uint8_t *seqDD;         // [ring index][slot] kSeqDDBytes
+  const Tuple *tuples;
+  const uint64_t *slotBase;
+  const uint32_t *fwdCnt;
+  const lkf_pkt *pkts;
+  const uint8_t *ddArena;
+};
+hipError_t launch_seq_dd(hipStream_t s, const SeqDDLaunch &a);
+// per lkf_rtx record: the DD bytes of its sequencer slot (still holding its
+// target SN) staged at dd + 256 * i (length byte first); 0 length otherwise
+hipError_t launch_rtx_dd(hipStream_t s, uint32_t n, const lkf_rtx *rtx, const DevDT *dts, const SeqMeta *seq,
+                         uint32_t seqSize, const uint32_t *ddIdx, const uint8_t *seqDD, uint8_t *dd);
 
 // ---- DownTrack sender statistics (sender_kernels.hip) ------------------------
 struct SenderLaunch {  // the forwarded tuples of one batch

@@ -2046,6 +2046,7 @@ struct ExtPacketMeta {
   PacketMeta meta;
   u64 extSequenceNumber = 0;
   u64 extTimestamp = 0;
+  u64 slot = 0;  // the ring slot the record was read from (engine-defined: lkf_rtx.reserved - 1)
 };
 
 struct Sequencer {
@@ -2157,6 +2158,7 @@ struct Sequencer {
         epm.meta = m;
         epm.extSequenceNumber = extSN;
         epm.extTimestamp = extTS;
+        epm.slot = slot;
         res.push_back(epm);
       }
     }

@@ -730,6 +730,7 @@ int orc_rtx_lookup(orc_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
         std::memset(&x, 0, sizeof(x));
         epm_to_meta(epm, x.meta);
         x.dt = dt;
+        x.reserved = u32(epm.slot) + 1;
         res.push_back(x);
       }
     }
@@ -787,6 +788,14 @@ int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
     hdr.Extension = false;
     hdr.ExtensionProfile = 0;
     hdr.Extensions.clear();
+    // pacer Extensions {dependencyDescriptorExtID: epm.ddBytes} (downtrack.go:1684;
+    // pacer/base.go:76-81 skips ID 0 / empty), epm.ddBytes copied from the
+    // record's slot (sequencer.go:326) — read here, at emit, from the slot the
+    // lookup returned while it still holds the record
+    if (d.p.ext_dd && x.reserved && x.reserved <= u32(d.seq->size)) {
+      const PacketMeta &m = d.seq->meta[x.reserved - 1];
+      if (m.targetSeqNo == x.meta.target_sn && !m.ddBytes.empty()) hdr.SetExtension(d.p.ext_dd, m.ddBytes);
+    }
     if (d.p.ext_abs_send_time) hdr.SetExtension(d.p.ext_abs_send_time, std::vector<u8>{0, 0, 0});
     std::vector<u8> bytes;
     hdr.Marshal(bytes);

@@ -65,7 +65,7 @@ def rtx_emit(api, h, trace, rtx, idx):
         blob += bytes((-len(blob)) % 16)
     arena = (C.c_uint8 * max(1, len(blob))).from_buffer_copy(bytes(blob) or b"\0")
     out = np.zeros(max(1, n), dtype=abi.OUT_DTYPE)
-    cap = len(blob) + 64 * n + 64
+    cap = len(blob) + 320 * n + 64  # (+ CSRCs and the pacer's extension block, a DD up to 255 B)
     wire = np.zeros(cap, dtype=np.uint8)
     k = C.c_uint32()
     ol = C.c_uint64()
@@ -73,3 +73,35 @@ def rtx_emit(api, h, trace, rtx, idx):
                          C.byref(k), C.byref(ol))
     assert rc == 0, rc
     return out[:k.value], wire[:ol.value]
+
+
+def count_dd_elements(trace, out, wire):
+    """RTX packets whose extension block carries the DownTrack's DD element."""
+    k = 0
+    for r in out:
+        dd_id = int(trace.downtracks[int(r["dt"])].ext_dd)
+        w = wire[int(r["out_off"]):int(r["out_off"]) + int(r["out_len"])]
+        if not dd_id or not (int(w[0]) & 0x10):
+            continue
+        h = 12 + 4 * (int(w[0]) & 0xF)
+        prof = (int(w[h]) << 8) | int(w[h + 1])
+        words = (int(w[h + 2]) << 8) | int(w[h + 3])
+        q, end = h + 4, h + 4 + 4 * words
+        while q < end:
+            if prof == 0xBEDE:
+                if w[q] == 0:
+                    q += 1
+                    continue
+                eid, ln = int(w[q]) >> 4, (int(w[q]) & 0xF) + 1
+                q += 1
+            else:
+                if w[q] == 0:
+                    q += 1
+                    continue
+                eid, ln = int(w[q]), int(w[q + 1])
+                q += 2
+            if eid == dd_id:
+                k += 1
+                break
+            q += ln
+    return k

@@ -80,3 +80,63 @@ def test_oracle_rtx_matches_forwarded_packets(workload):
     finally:
         o.destroy(h)
         tr.close()
+
+
+def _ext_element(pkt, eid):
+    """The payload of extension element `eid` of an RTP packet (one- or two-byte profile), or None."""
+    if not pkt[0] & 0x10:
+        return None
+    h = 12 + 4 * (pkt[0] & 0xF)
+    prof = (pkt[h] << 8) | pkt[h + 1]
+    q, end = h + 4, h + 4 + 4 * ((pkt[h + 2] << 8) | pkt[h + 3])
+    while q < end:
+        if pkt[q] == 0:
+            q += 1
+            continue
+        if prof == 0xBEDE:
+            i, ln, q = pkt[q] >> 4, (pkt[q] & 0xF) + 1, q + 1
+        else:
+            i, ln, q = pkt[q], pkt[q + 1], q + 2
+        if i == eid:
+            return bytes(pkt[q:q + ln])
+        q += ln
+    return None
+
+
+def test_oracle_rtx_keeps_dependency_descriptor(workload):
+    """RTX of a DD DownTrack: the pacer writes epm.ddBytes (sequencer.go:198-199,
+    :326; downtrack.go:1684) — the same DD element the forwarded packet carried."""
+    o = load_oracle()
+    tr = workload.Trace(5, duration_s=3.0, batch_s=1.0, rooms=4, svc_dd=1, seed=14)
+    nb = 3
+    h = o.create(500)
+    workload.load_topology(o.api, h, tr)
+    pkg = __import__("importlib").import_module("livekit-server_amd")
+    fwd = {}
+    try:
+        for b in range(nb):
+            workload.queue_events(o.api, h, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(h, pk, n, ar, alen, tr.batch_dd(b)[0])
+            rec, arena = pkg.drain_arrays(o.api, h)
+            for r in rec:
+                fwd[(int(r["dt"]), int(r["ext_sn"]) & 0xFFFF)] = bytes(arena[r["out_off"]:r["out_off"] + r["out_len"]])
+        idx = rtx_lib.packet_index(tr, nb)
+        nacks = rtx_lib.make_nacks(o.api, h, tr, seed=4)
+        rtx = rtx_lib.rtx_lookup(o.api, h, nacks, EPOCH + nb * 10**9 + 500 * 10**6)
+        out, wire = rtx_lib.rtx_emit(o.api, h, tr, rtx, idx)
+        with_dd = 0
+        for r in out:
+            d = int(r["dt"])
+            eid = int(tr.downtracks[d].ext_dd)
+            pkt = bytes(wire[r["out_off"]:r["out_off"] + r["out_len"]])
+            orig = fwd.get((d, int(r["ext_sn"]) & 0xFFFF))
+            if not eid or orig is None:
+                continue
+            assert _ext_element(pkt, eid) == _ext_element(orig, eid), d
+            assert _payload(pkt) == _payload(orig)
+            with_dd += _ext_element(pkt, eid) is not None
+        assert with_dd > 20
+    finally:
+        o.destroy(h)
+        tr.close()

@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 EPOCH = 1700000000 * 10**9
 
 
-@pytest.mark.parametrize("cfg", [dict(config=2, rooms=4, seed=9), dict(config=1, seed=4), dict(config=3, rooms=2)])
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=4, seed=9), dict(config=1, seed=4), dict(config=3, rooms=2),
+                                 dict(config=5, rooms=4, svc_dd=1, seed=14)])
 def test_rtx_lookup_and_emit_match_oracle(pkg, workload, cfg):
     o = load_oracle()
     kw = dict(cfg)
@@ -30,10 +31,11 @@ def test_rtx_lookup_and_emit_match_oracle(pkg, workload, cfg):
             workload.queue_events(eng.api, eng.h, tr, b)
             workload.queue_events(o.api, oh, tr, b)
             pk, n, ar, alen = tr.batch(b)
-            eng.submit(pk, n, ar, alen)
+            dd = tr.batch_dd(b)[0] if tr.has_dd() else None
+            eng.submit(pk, n, ar, alen, dd)
             eng.run()
             eng.sync()
-            o.run(oh, pk, n, ar, alen)
+            o.run(oh, pk, n, ar, alen, dd)
         idx = rtx_lib.packet_index(tr, nb)
         nacks = rtx_lib.make_nacks(o.api, oh, tr, seed=5)
         assert len(nacks) > 50
@@ -52,6 +54,8 @@ def test_rtx_lookup_and_emit_match_oracle(pkg, workload, cfg):
                 for f in oo.dtype.names:
                     assert np.array_equal(go[f], oo[f]), f
                 assert np.array_equal(gw, ow)
+                if tr.has_dd():  # RTX of a DD DownTrack carries the sequencer's ddBytes (downtrack.go:1684)
+                    assert rtx_lib.count_dd_elements(tr, oo, ow) > 0
                 # RTPStatsSender.Update of the retransmissions (duplicates / out of order)
                 ss = check_sender_stats(pkg, eng.api, eng.h, o.api, oh, range(tr.ndts))
                 assert int(ss["packets_duplicate"].sum()) > 0
