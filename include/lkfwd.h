@@ -678,6 +678,55 @@ int lkf_next_higher_transition(lkf_engine *e, const lkf_alloc_req *reqs, uint32_
  * updateAllocation. */
 int lkf_pause(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out);
 
+/* ---- the stream allocator's cooperative pass (forwarder.go:727-1105) ---- *
+ * The Forwarder halves the stream allocator drives (streamallocator.go
+ * allocateTrack :880-1010, allocateAllTracks :1092-1178), each for many video
+ * DownTracks per call (distinct DownTracks; an audio or removed DownTrack is
+ * LKF_EINVAL: the reference's selector is nil for audio).  The provisional
+ * state (VideoAllocationProvisional :96-106) lives per DownTrack in HBM
+ * between the calls; Commit applies the result as updateAllocation.  Every
+ * call waits for queued runs. */
+typedef struct lkf_prov_req {
+  int32_t dt;
+  int32_t spatial, temporal; /* ProvisionalAllocate: the layer tried */
+  uint8_t allow_pause, allow_overshoot;
+  uint8_t reserved[2];
+  int64_t capacity;          /* ProvisionalAllocate: availableChannelCapacity */
+} lkf_prov_req;
+typedef struct lkf_prov_result {
+  int32_t dt;
+  uint8_t is_candidate;
+  uint8_t reserved[3];
+  int64_t used;              /* the bitrate the allocation adds (may be negative) */
+} lkf_prov_result;
+/* ProvisionalAllocatePrepare(availableLayers, bitrates) :727-743 */
+int lkf_provisional_prepare(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n);
+/* ProvisionalAllocateReset :745-750 */
+int lkf_provisional_reset(lkf_engine *e, const int32_t *dts, uint32_t n);
+/* ProvisionalAllocate(capacity, layer, allowPause, allowOvershoot) :752-794 */
+int lkf_provisional_allocate(lkf_engine *e, const lkf_prov_req *reqs, uint32_t n, lkf_prov_result *out);
+/* ProvisionalAllocateGetCooperativeTransition(allow_overshoot) :796-929 */
+int lkf_provisional_cooperative(lkf_engine *e, const lkf_prov_req *reqs, uint32_t n, lkf_video_transition *out);
+/* ProvisionalAllocateGetBestWeightedTransition :931-1025 */
+int lkf_provisional_best_weighted(lkf_engine *e, const int32_t *dts, uint32_t n, lkf_video_transition *out);
+/* ProvisionalAllocateCommit :1027-1105 (+ updateAllocation) */
+int lkf_provisional_commit(lkf_engine *e, const int32_t *dts, uint32_t n, lkf_allocation *out);
+/* allocateAllTracks' managed-track pass (streamallocator.go:1147-1172) for
+ * many subscribers at once: per group (one subscriber's stream allocator, its
+ * DownTracks reqs[first .. first + count) in priority order), Prepare each,
+ * then for every layer (0,0) .. (2,3) and every DownTrack in order
+ * ProvisionalAllocate(capacity, layer, allow_pause, allow_overshoot) with
+ * capacity -= used (floored at 0), then Commit each -> out[first + k].  One
+ * thread per subscriber on the GPU (the pass is serial within one). */
+typedef struct lkf_alloc_group {
+  uint32_t first, count;
+  int64_t capacity;          /* availableChannelCapacity after the exempt tracks */
+  uint8_t allow_pause, allow_overshoot;
+  uint8_t reserved[6];
+} lkf_alloc_group;
+int lkf_allocate_all(lkf_engine *e, const lkf_alloc_group *groups, uint32_t ngroups, const lkf_alloc_req *reqs,
+                     uint32_t n, lkf_allocation *out);
+
 /* ---- SRTP protect ----------------------------------- *
  * The step after the pacer: writeRTPHeaderExtensions sets abs-send-time
  * (pacer/base.go:71-100), then WriteStream.WriteRTP (base.go:59) protects the

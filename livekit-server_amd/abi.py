@@ -100,6 +100,15 @@ SPEAKER_DTYPE = np.dtype([("room", "<u4"), ("participant", "<u4"), ("level", "<f
 DT_SUMMARY_DTYPE = np.dtype([("dt", "<i4"), ("subscriber", "<u4"), ("room", "<u4"), ("flags", "<u4"),
                              ("packets_sent", "<u8"), ("bytes_sent", "<u8")])
 assert DT_SUMMARY_DTYPE.itemsize == 32
+# the cooperative allocation pass (lkf_prov_req / lkf_prov_result / lkf_alloc_group)
+PROV_REQ_DTYPE = np.dtype([("dt", "<i4"), ("spatial", "<i4"), ("temporal", "<i4"), ("allow_pause", "u1"),
+                           ("allow_overshoot", "u1"), ("reserved", "u1", 2), ("capacity", "<i8")])
+assert PROV_REQ_DTYPE.itemsize == 24
+PROV_RESULT_DTYPE = np.dtype([("dt", "<i4"), ("is_candidate", "u1"), ("reserved", "u1", 3), ("used", "<i8")])
+assert PROV_RESULT_DTYPE.itemsize == 16
+ALLOC_GROUP_DTYPE = np.dtype([("first", "<u4"), ("count", "<u4"), ("capacity", "<i8"), ("allow_pause", "u1"),
+                              ("allow_overshoot", "u1"), ("reserved", "u1", 6)])
+assert ALLOC_GROUP_DTYPE.itemsize == 24
 # lkf_sender_stats (DownTrack.rtpStats = buffer.RTPStatsSender)
 SENDER_STATS_DTYPE = np.dtype(
     [(f, "<u8") for f in ("ext_start_sn", "ext_highest_sn", "ext_start_ts", "ext_highest_ts")]
@@ -449,6 +458,14 @@ def bind_engine_api(lib, prefix):
         api["next_higher_transition"] = _bind(lib, prefix + "next_higher_transition", C.c_int,
                                               [e, C.c_void_p, C.c_uint32, C.c_void_p])
         api["pause"] = _bind(lib, prefix + "pause", C.c_int, [e, C.c_void_p, C.c_uint32, C.c_void_p])
+    if hasattr(lib, prefix + "provisional_prepare"):
+        api["provisional_prepare"] = _bind(lib, prefix + "provisional_prepare", C.c_int, [e, C.c_void_p, C.c_uint32])
+        api["provisional_reset"] = _bind(lib, prefix + "provisional_reset", C.c_int, [e, C.c_void_p, C.c_uint32])
+        for nm in ("provisional_allocate", "provisional_cooperative", "provisional_best_weighted",
+                   "provisional_commit"):
+            api[nm] = _bind(lib, prefix + nm, C.c_int, [e, C.c_void_p, C.c_uint32, C.c_void_p])
+        api["allocate_all"] = _bind(lib, prefix + "allocate_all", C.c_int,
+                                    [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p])
     if hasattr(lib, prefix + "sender_stats_get"):
         api["sender_stats_get"] = _bind(lib, prefix + "sender_stats_get", C.c_int, [e, C.c_int32, C.c_void_p])
         api["sender_sninfo"] = _bind(lib, prefix + "sender_sninfo", C.c_int, [e, C.c_int32, C.c_uint64, P(C.c_uint32)])

@@ -324,7 +324,279 @@ __global__ void k_pause(const lkf_alloc_req *__restrict__ reqs, u32 n, DTHot *ho
   hot[d] = h;
   out[i] = a;
 }
+
+// ---- the stream allocator's cooperative pass (forwarder.go:727-1105) --------
+__device__ __forceinline__ bool greater(Layer a, Layer b) {  // VideoLayer.GreaterThan
+  return a.s > b.s || (a.s == b.s && a.t > b.t);
+}
+// ProvisionalAllocatePrepare :727-743
+__device__ void prov_prepare(const DTHot &h, ProvState &p, const lkf_alloc_req &q) {
+  for (int s = 0; s < 3; s++)
+    for (int t = 0; t < 4; t++) p.brs[s][t] = q.bitrates[s][t];
+  p.allocS = p.allocT = INV;
+  p.muted = ((h.flags & F_MUTED) ? 1u : 0u) | ((h.flags & F_PUBMUTED) ? 2u : 0u);
+  p.seenS = h.seenS, p.seenT = h.seenT;
+  p.maxS = h.maxS, p.maxT = h.maxT;
+  p.curS = h.curS, p.curT = h.curT;
+  p.avail = q.available_layers;
+}
+// ProvisionalAllocate :752-794
+__device__ bool prov_allocate(const DTHot &h, ProvState &p, i64 cap, Layer layer, bool allowPause, bool allowOvershoot,
+                              i64 &used) {
+  used = 0;
+  const Layer max{p.maxS, p.maxT}, al{p.allocS, p.allocT};
+  const bool ovOk = allowOvershoot && (h.flags & F_SIMULCAST);  // IsOvershootOkay: Simulcast only
+  if (p.muted || p.seenS == INV || !max.valid() || (!ovOk && greater(layer, max))) return false;
+  const i64 required = p.brs[layer.s][layer.t];
+  if (required == 0) return false;
+  const i64 already = al.valid() ? p.brs[al.s][al.t] : 0;
+  if (!greater(layer, max) && required <= cap + already) {
+    p.allocS = layer.s, p.allocT = layer.t;
+    used = required - already;
+    return true;
+  }
+  if (!allowPause && (!al.valid() || !greater(layer, al))) {
+    p.allocS = layer.s, p.allocT = layer.t;
+    used = required - already;
+    return true;
+  }
+  return false;
+}
+__device__ lkf_video_transition transition(i32 dt, Layer from, Layer to, i64 delta) {
+  lkf_video_transition tr = {};
+  tr.dt = dt;
+  tr.from_spatial = from.s, tr.from_temporal = from.t;
+  tr.to_spatial = to.s, tr.to_temporal = to.t;
+  tr.bandwidth_delta = delta;
+  tr.available = 1;
+  return tr;
+}
+// ProvisionalAllocateGetCooperativeTransition :796-929
+__device__ lkf_video_transition prov_cooperative(i32 dt, const DTHot &h, ProvState &p, i64 lastReq, bool allowOvershoot) {
+  const Layer existing{h.tgtS, h.tgtT}, max{p.maxS, p.maxT}, cur{p.curS, p.curT};
+  if (p.muted) {
+    p.allocS = p.allocT = INV;
+    return transition(dt, existing, Layer{INV, INV}, -bw_needed(p.brs, existing, lastReq));
+  }
+  if (existing.valid()) {
+    Layer maximal{INV, INV};
+    i64 maximalBw = 0;
+    for (i32 s = max.s; s >= 0 && maximalBw == 0; s--)
+      for (i32 t = max.t; t >= 0; t--)
+        if (p.brs[s][t] != 0) {
+          maximal = Layer{s, t};
+          maximalBw = p.brs[s][t];
+          break;
+        }
+    if (maximal.valid()) {
+      if (!greater(existing, maximal) && p.brs[existing.s][existing.t] != 0) {
+        p.allocS = existing.s, p.allocT = existing.t;
+        return transition(dt, existing, existing, 0);
+      }
+      if (greater(existing, maximal)) {
+        p.allocS = maximal.s, p.allocT = maximal.t;
+        return transition(dt, existing, maximal, maximalBw - bw_needed(p.brs, existing, lastReq));
+      }
+    }
+  }
+  Layer target{INV, INV};
+  i64 required = 0;
+  auto next = [&](i32 minS, i32 maxS, i32 minT, i32 maxT) {
+    for (i32 s = minS; s <= maxS && required == 0; s++)
+      for (i32 t = minT; t <= maxT; t++)
+        if (p.brs[s][t] != 0) {
+          target = Layer{s, t};
+          required = p.brs[s][t];
+          break;
+        }
+  };
+  if (!existing.valid()) {
+    next(0, max.s, 0, max.t);
+    if (required == 0 && max.valid() && allowOvershoot && (h.flags & F_SIMULCAST)) {
+      target = Layer{INV, INV};
+      next(max.s + 1, 2, 0, 3);
+    }
+  }
+  if (!target.valid()) {
+    target = cur;
+    if (target.valid()) required = p.brs[target.s][target.t];
+  }
+  p.allocS = target.s, p.allocT = target.t;
+  return transition(dt, existing, target, required - bw_needed(p.brs, existing, lastReq));
+}
+// ProvisionalAllocateGetBestWeightedTransition :931-1025
+__device__ lkf_video_transition prov_best_weighted(i32 dt, const DTHot &h, ProvState &p, i64 lastReq) {
+  const Layer target{h.tgtS, h.tgtT}, max{p.maxS, p.maxT};
+  if (p.muted) {
+    p.allocS = p.allocT = INV;
+    return transition(dt, target, Layer{INV, INV}, 0 - bw_needed(p.brs, target, lastReq));
+  }
+  i32 reachT = INV;
+  for (i32 t = max.t; t >= 0 && reachT == INV; t--)
+    for (i32 s = max.s; s >= 0; s--)
+      if (p.brs[s][t] != 0) {
+        reachT = t;
+        break;
+      }
+  if (reachT == INV) {
+    p.allocS = p.curS, p.allocT = p.curT;
+    return transition(dt, target, Layer{p.curS, p.curT}, 0 - bw_needed(p.brs, target, lastReq));
+  }
+  const i64 existingBw = bw_needed(p.brs, target, lastReq);
+  Layer best{INV, INV};
+  i64 bestDelta = 0;
+  float bestValue = 0.0f;
+  for (i32 s = 0; s <= target.s; s++)
+    for (i32 t = 0; t <= target.t; t++) {
+      if (s == target.s && t == target.t) break;
+      const i64 delta = i64(fmax(0.0, double(existingBw - p.brs[s][t])));
+      const i32 transitionCost = target.s != s ? 10 : 0;  // TransitionCostSpatial forwarder.go:43
+      const i32 qualityCost = (reachT + 1) * (target.s - s) + (target.t - t);
+      float value = 0.0f;
+      if (transitionCost + qualityCost != 0) value = float(delta) / float(transitionCost + qualityCost);
+      if (value > bestValue || (value == bestValue && delta > bestDelta)) {
+        bestValue = value;
+        bestDelta = delta;
+        best = Layer{s, t};
+      }
+    }
+  p.allocS = best.s, p.allocT = best.t;
+  return transition(dt, target, best, -bestDelta);
+}
+// ProvisionalAllocateCommit :1027-1105 (+ updateAllocation)
+__device__ lkf_allocation prov_commit(i32 dt, DTHot &h, ProvState &p, bool h264, lkf_allocation *last, u32 d) {
+  const bool muted = p.muted & 1, pubMuted = p.muted & 2;
+  const Layer max{p.maxS, p.maxT}, seen{p.seenS, p.seenT}, cur{p.curS, p.curT}, target{h.tgtS, h.tgtT};
+  const i64 lastReq = last[d].bandwidth_requested;
+  const i64 optimal = optimal_bw(muted, pubMuted, seen.s, p.brs, max);
+  lkf_allocation a = {};
+  a.dt = dt;
+  a.bandwidth_requested = 0;
+  a.bandwidth_delta = 0 - bw_needed(p.brs, target, lastReq);
+  a.bandwidth_needed = optimal;
+  Layer al{p.allocS, p.allocT};
+  a.target_spatial = al.s, a.target_temporal = al.t;
+  a.request_spatial = al.s;
+  a.max_spatial = max.s, a.max_temporal = max.t;
+  a.distance_to_desired = distance(muted, pubMuted, seen, p.avail, p.brs, al, max);
+  if (muted) {
+    a.pause_reason = 1;
+  } else if (pubMuted) {
+    a.pause_reason = 2;
+  } else if (optimal == 0) {
+    if (al.valid()) {  // overshoot
+      a.bandwidth_requested = p.brs[al.s][al.t];
+      a.bandwidth_delta = a.bandwidth_requested - bw_needed(p.brs, target, lastReq);
+    } else {
+      a.pause_reason = 3;
+      if (cur.valid() && cur.s <= max.s) {  // leave target at current for opportunistic forwarding
+        p.allocS = cur.s, p.allocT = cur.t;
+        a.target_spatial = cur.s, a.target_temporal = cur.t;
+        a.request_spatial = cur.s;
+      }
+    }
+  } else {
+    if (al.valid()) a.bandwidth_requested = p.brs[al.s][al.t];
+    a.bandwidth_delta = a.bandwidth_requested - bw_needed(p.brs, target, lastReq);
+    if (greater(al, max) || a.bandwidth_requested >= optimal) {
+      a.is_deficient = 0;
+    } else {
+      a.is_deficient = 1;
+      if (!al.valid()) a.pause_reason = 4;
+    }
+  }
+  update_allocation(a, h, h264, last, d);
+  return a;
+}
+
+__global__ void k_prov(ProvLaunch A) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const i32 dt = A.mode == PROV_PREPARE ? A.alloc[i].dt : A.reqs[i].dt;
+  const u32 d = u32(dt);
+  DTHot h = A.hot[d];
+  ProvState p = A.prov[d];
+  switch (A.mode) {
+    case PROV_PREPARE:
+      prov_prepare(h, p, A.alloc[i]);
+      break;
+    case PROV_RESET:
+      p.allocS = p.allocT = INV;
+      break;
+    case PROV_ALLOCATE: {
+      const lkf_prov_req q = A.reqs[i];
+      lkf_prov_result r = {};
+      r.dt = dt;
+      const bool ok = q.spatial >= 0 && q.spatial <= 2 && q.temporal >= 0 && q.temporal <= 3;
+      r.is_candidate = ok && prov_allocate(h, p, q.capacity, Layer{q.spatial, q.temporal}, q.allow_pause != 0,
+                                           q.allow_overshoot != 0, r.used);
+      static_cast<lkf_prov_result *>(A.out)[i] = r;
+      break;
+    }
+    case PROV_COOPERATIVE:
+      static_cast<lkf_video_transition *>(A.out)[i] =
+          prov_cooperative(dt, h, p, A.last[d].bandwidth_requested, A.reqs[i].allow_overshoot != 0);
+      break;
+    case PROV_BEST_WEIGHTED:
+      static_cast<lkf_video_transition *>(A.out)[i] = prov_best_weighted(dt, h, p, A.last[d].bandwidth_requested);
+      break;
+    case PROV_COMMIT:
+      static_cast<lkf_allocation *>(A.out)[i] = prov_commit(dt, h, p, is_h264(A.dts, A.tracks, d), A.last, d);
+      A.hot[d] = h;
+      break;
+  }
+  A.prov[d] = p;
+}
+
+// allocateAllTracks' managed pass (streamallocator.go:1147-1172): one thread
+// per subscriber group, serial over its layers and DownTracks
+__global__ void k_allocate_all(const lkf_alloc_group *__restrict__ groups, u32 ngroups,
+                               const lkf_alloc_req *__restrict__ reqs, DTHot *hot, const DevDT *dts,
+                               const DevTrack *tracks, lkf_allocation *last, ProvState *prov, lkf_allocation *out) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  const lkf_alloc_group G = groups[g];
+  for (u32 k = 0; k < G.count; k++) {
+    const u32 d = u32(reqs[G.first + k].dt);
+    ProvState p;
+    prov_prepare(hot[d], p, reqs[G.first + k]);
+    prov[d] = p;
+  }
+  i64 cap = G.capacity;
+  for (i32 s = 0; s <= 2; s++)
+    for (i32 t = 0; t <= 3; t++)
+      for (u32 k = 0; k < G.count; k++) {
+        const u32 d = u32(reqs[G.first + k].dt);
+        i64 used = 0;
+        prov_allocate(hot[d], prov[d], cap, Layer{s, t}, G.allow_pause != 0, G.allow_overshoot != 0, used);
+        cap -= used;
+        if (cap < 0) cap = 0;
+      }
+  for (u32 k = 0; k < G.count; k++) {
+    const u32 d = u32(reqs[G.first + k].dt);
+    DTHot h = hot[d];
+    ProvState p = prov[d];
+    out[G.first + k] = prov_commit(i32(d), h, p, is_h264(dts, tracks, d), last, d);
+    hot[d] = h;
+    prov[d] = p;
+  }
+}
 }  // namespace
+
+hipError_t launch_prov(hipStream_t s, const ProvLaunch &a) {
+  if (!a.n) return hipSuccess;
+  hipLaunchKernelGGL(k_prov, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_allocate_all(hipStream_t s, const lkf_alloc_group *groups, uint32_t ngroups, const lkf_alloc_req *reqs,
+                               DTHot *hot, const DevDT *dts, const DevTrack *tracks, lkf_allocation *last,
+                               ProvState *prov, lkf_allocation *out) {
+  if (!ngroups) return hipSuccess;
+  hipLaunchKernelGGL(k_allocate_all, dim3((ngroups + 63) / 64), dim3(64), 0, s, groups, ngroups, reqs, hot, dts, tracks,
+                     last, prov, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_allocate(hipStream_t s, int mode, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
                            DTHot *hot, const DevDT *dts, const DevTrack *tracks, lkf_allocation *last, void *out) {

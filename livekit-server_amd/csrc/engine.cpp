@@ -169,6 +169,12 @@ struct lkf_engine {
   uint32_t nSeqDD = 0, seqDDCap = 0;
   std::vector<uint32_t> seqDDList;
   uint8_t *dRtxDD = nullptr;  // lkf_rtx_emit: per record kSeqDDBytes
+  // the cooperative allocation pass: per DownTrack provisional state + call buffers
+  ProvState *dProv = nullptr;
+  lkf_prov_req *dProvReq = nullptr;
+  lkf_alloc_group *dProvGroups = nullptr;
+  uint8_t *dProvOut = nullptr;
+  uint32_t provCap = 0, provGroupCap = 0;
   uint32_t rtxDDCap = 0;
   DevDT *dDTs = nullptr;
   RangeEntry *dRm = nullptr;
@@ -833,7 +839,7 @@ void lkf_destroy(lkf_engine *e) {
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
                   e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut,
                   e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups, e->dSeqDD, e->dSeqDDIdx,
-                  e->dSeqDDList, e->dRtxDD};
+                  e->dSeqDDList, e->dRtxDD, e->dProv, e->dProvReq, e->dProvGroups, e->dProvOut};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
@@ -2639,6 +2645,140 @@ int lkf_next_higher_transition(lkf_engine *e, const lkf_alloc_req *reqs, uint32_
 }
 int lkf_pause(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
   return alloc_common(e, ALLOC_PAUSE, reqs, nullptr, n, out, sizeof(lkf_allocation));
+}
+
+// ---- the cooperative allocation pass (Provisional*, allocateAllTracks) ------
+// distinct, active, video DownTracks (the reference's selector is nil for audio)
+static int prov_check(lkf_engine *e, const int32_t *dts, uint32_t n, size_t stride) {
+  std::vector<uint8_t> seen(e->dtp.size(), 0);
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t dt = *reinterpret_cast<const int32_t *>(reinterpret_cast<const uint8_t *>(dts) + i * stride);
+    if (dt < 0 || dt >= int32_t(e->dtp.size()) || seen[dt] || !e->active[dt] ||
+        e->tracks[e->dtp[dt].track].kind != LKF_KIND_VIDEO) {
+      e->err = "provisional allocation: DownTracks must be distinct, active and video";
+      return LKF_EINVAL;
+    }
+    seen[dt] = 1;
+  }
+  return LKF_OK;
+}
+static int prov_reserve(lkf_engine *e, uint32_t n, uint32_t ngroups) {
+  const lkf_cfg &c = e->cfg;
+  if (!e->dProv) {
+    HIPCHK(dalloc(&e->dProv, c.max_downtracks), "alloc provisional");
+    HIPCHK(hipMemset(e->dProv, 0, size_t(c.max_downtracks) * sizeof(ProvState)), "provisional reset");
+  }
+  if (n > e->provCap) {
+    if (e->dProvReq) (void)hipFree(e->dProvReq);
+    if (e->dProvOut) (void)hipFree(e->dProvOut);
+    if (e->dAllocReq) (void)hipFree(e->dAllocReq);
+    if (e->dAllocOut) (void)hipFree(e->dAllocOut);
+    if (e->dAllocCapacity) (void)hipFree(e->dAllocCapacity);
+    e->provCap = std::max<uint32_t>(n, 1024);
+    e->allocCap = std::max<uint32_t>(e->allocCap, e->provCap);
+    HIPCHK(dalloc(&e->dProvReq, e->provCap), "alloc prov reqs");
+    HIPCHK(dalloc(&e->dProvOut, size_t(e->provCap) * sizeof(lkf_allocation)), "alloc prov out");
+    HIPCHK(dalloc(&e->dAllocReq, e->allocCap), "alloc alloc reqs");
+    HIPCHK(dalloc(&e->dAllocOut, e->allocCap), "alloc alloc out");
+    HIPCHK(dalloc(&e->dAllocCapacity, e->allocCap), "alloc alloc capacity");
+  }
+  if (ngroups > e->provGroupCap) {
+    if (e->dProvGroups) (void)hipFree(e->dProvGroups);
+    e->provGroupCap = std::max<uint32_t>(ngroups, 256);
+    HIPCHK(dalloc(&e->dProvGroups, e->provGroupCap), "alloc prov groups");
+  }
+  return LKF_OK;
+}
+static int prov_common(lkf_engine *e, int mode, const lkf_prov_req *reqs, const lkf_alloc_req *alloc, uint32_t n,
+                       void *out, size_t outSize) {
+  if (!e || (n && !reqs && !alloc) || (n && outSize && !out)) return LKF_EINVAL;
+  if (!n) return LKF_OK;
+  int rc = alloc ? prov_check(e, &alloc[0].dt, n, sizeof(lkf_alloc_req)) : prov_check(e, &reqs[0].dt, n, sizeof(lkf_prov_req));
+  if (rc) return rc;
+  rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  rc = prov_reserve(e, n, 0);
+  if (rc) return rc;
+  if (alloc)
+    HIPCHK(hipMemcpy(e->dAllocReq, alloc, n * sizeof(lkf_alloc_req), hipMemcpyHostToDevice), "prov req copy");
+  else
+    HIPCHK(hipMemcpy(e->dProvReq, reqs, n * sizeof(lkf_prov_req), hipMemcpyHostToDevice), "prov req copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  ProvLaunch a;
+  a.mode = mode;
+  a.n = n;
+  a.reqs = e->dProvReq;
+  a.alloc = e->dAllocReq;
+  a.hot = e->dHot;
+  a.dts = e->dDTs;
+  a.tracks = e->dTracks;
+  a.last = e->dLastAlloc;
+  a.prov = e->dProv;
+  a.out = e->dProvOut;
+  HIPCHK(launch_prov(e->own, a), "provisional");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  if (outSize) HIPCHK(hipMemcpy(out, e->dProvOut, n * outSize, hipMemcpyDeviceToHost), "prov out copy");
+  return LKF_OK;
+}
+static int prov_dts(lkf_engine *e, int mode, const int32_t *dts, uint32_t n, void *out, size_t outSize) {
+  if (n && !dts) return LKF_EINVAL;
+  std::vector<lkf_prov_req> r(n);
+  for (uint32_t i = 0; i < n; i++) {
+    std::memset(&r[i], 0, sizeof(r[i]));
+    r[i].dt = dts[i];
+  }
+  return prov_common(e, mode, r.data(), nullptr, n, out, outSize);
+}
+int lkf_provisional_prepare(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n) {
+  return prov_common(e, PROV_PREPARE, nullptr, reqs, n, nullptr, 0);
+}
+int lkf_provisional_reset(lkf_engine *e, const int32_t *dts, uint32_t n) {
+  return prov_dts(e, PROV_RESET, dts, n, nullptr, 0);
+}
+int lkf_provisional_allocate(lkf_engine *e, const lkf_prov_req *reqs, uint32_t n, lkf_prov_result *out) {
+  return prov_common(e, PROV_ALLOCATE, reqs, nullptr, n, out, sizeof(lkf_prov_result));
+}
+int lkf_provisional_cooperative(lkf_engine *e, const lkf_prov_req *reqs, uint32_t n, lkf_video_transition *out) {
+  return prov_common(e, PROV_COOPERATIVE, reqs, nullptr, n, out, sizeof(lkf_video_transition));
+}
+int lkf_provisional_best_weighted(lkf_engine *e, const int32_t *dts, uint32_t n, lkf_video_transition *out) {
+  return prov_dts(e, PROV_BEST_WEIGHTED, dts, n, out, sizeof(lkf_video_transition));
+}
+int lkf_provisional_commit(lkf_engine *e, const int32_t *dts, uint32_t n, lkf_allocation *out) {
+  return prov_dts(e, PROV_COMMIT, dts, n, out, sizeof(lkf_allocation));
+}
+int lkf_allocate_all(lkf_engine *e, const lkf_alloc_group *groups, uint32_t ngroups, const lkf_alloc_req *reqs,
+                     uint32_t n, lkf_allocation *out) {
+  if (!e || (ngroups && !groups) || (n && (!reqs || !out))) return LKF_EINVAL;
+  std::vector<uint8_t> cover(n, 0);  // groups are disjoint ranges of reqs
+  for (uint32_t g = 0; g < ngroups; g++) {
+    if (uint64_t(groups[g].first) + groups[g].count > n) return LKF_EINVAL;
+    for (uint32_t k = 0; k < groups[g].count; k++)
+      if (cover[groups[g].first + k]++) return LKF_EINVAL;
+  }
+  if (!ngroups || !n) return LKF_OK;
+  int rc = prov_check(e, &reqs[0].dt, n, sizeof(lkf_alloc_req));
+  if (rc) return rc;
+  rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  rc = prov_reserve(e, n, ngroups);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(e->dAllocReq, reqs, n * sizeof(lkf_alloc_req), hipMemcpyHostToDevice), "alloc req copy");
+  HIPCHK(hipMemcpy(e->dProvGroups, groups, ngroups * sizeof(lkf_alloc_group), hipMemcpyHostToDevice), "groups copy");
+  HIPCHK(hipMemset(e->dProvOut, 0, n * sizeof(lkf_allocation)), "alloc out reset");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_allocate_all(e->own, e->dProvGroups, ngroups, e->dAllocReq, e->dHot, e->dDTs, e->dTracks,
+                             e->dLastAlloc, e->dProv, reinterpret_cast<lkf_allocation *>(e->dProvOut)),
+         "allocate all");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  HIPCHK(hipMemcpy(out, e->dProvOut, n * sizeof(lkf_allocation), hipMemcpyDeviceToHost), "alloc out copy");
+  return LKF_OK;
 }
 
 int lkf_padding(lkf_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,

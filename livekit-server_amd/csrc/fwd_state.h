@@ -265,6 +265,18 @@ struct alignas(16) SenderStats {
 };
 static_assert(sizeof(SenderStats) == 192, "SenderStats is 192 B");
 
+// Forwarder.provisional: VideoAllocationProvisional (forwarder.go:96-106),
+// one per DownTrack, written by lkf_provisional_prepare / lkf_allocate_all
+struct alignas(16) ProvState {
+  int64_t brs[3][4];                       // bitrates
+  int32_t allocS, allocT;                  // allocatedLayer
+  int32_t seenS, seenT, maxS, maxT, curS, curT;  // maxSeenLayer, maxLayer, currentLayer
+  uint32_t avail;                          // availableLayers (bit set)
+  uint32_t muted;                          // 1 muted, 2 pubMuted
+  uint32_t pad[2];
+};
+static_assert(sizeof(ProvState) == 144, "ProvState is 144 B");
+
 constexpr int kHistWords = 64;  // cHistorySize 4096 bits (rtpstats_receiver.go:30)
 
 struct DevStream {  // static stream parameters (64 B)

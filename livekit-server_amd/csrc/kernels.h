@@ -218,6 +218,24 @@ hipError_t launch_pad(hipStream_t s, const PadLaunch &a);
 // lastAllocation per DownTrack; `out` is lkf_allocation[n] or, for
 // ALLOC_TRANSITION, lkf_video_transition[n]; `capacity` only for NEXT_HIGHER
 enum AllocMode { ALLOC_OPTIMAL = 0, ALLOC_NEXT_HIGHER = 1, ALLOC_TRANSITION = 2, ALLOC_PAUSE = 3 };
+// the cooperative pass (alloc_kernels.hip k_prov / k_allocate_all)
+enum ProvMode { PROV_PREPARE = 0, PROV_RESET, PROV_ALLOCATE, PROV_COOPERATIVE, PROV_BEST_WEIGHTED, PROV_COMMIT };
+struct ProvLaunch {
+  int mode;
+  uint32_t n;
+  const lkf_prov_req *reqs;   // (PROV_PREPARE: alloc)
+  const lkf_alloc_req *alloc;
+  DTHot *hot;
+  const DevDT *dts;
+  const DevTrack *tracks;
+  lkf_allocation *last;
+  ProvState *prov;
+  void *out;  // lkf_prov_result / lkf_video_transition / lkf_allocation per request
+};
+hipError_t launch_prov(hipStream_t s, const ProvLaunch &a);
+hipError_t launch_allocate_all(hipStream_t s, const lkf_alloc_group *groups, uint32_t ngroups, const lkf_alloc_req *reqs,
+                               DTHot *hot, const DevDT *dts, const DevTrack *tracks, lkf_allocation *last,
+                               ProvState *prov, lkf_allocation *out);
 hipError_t launch_allocate(hipStream_t s, int mode, const lkf_alloc_req *reqs, const int64_t *capacity, uint32_t n,
                            DTHot *hot, const DevDT *dts, const DevTrack *tracks, lkf_allocation *last, void *out);
 

@@ -1425,6 +1425,7 @@ struct ForwarderState {  // forwarder.go:158-166
 // VideoAllocation forwarder.go:82-93 (Bitrates [spatial][temporal], bps)
 using Bitrates = std::array<std::array<i64, 4>, 3>;
 enum VideoPauseReason : i32 { PauseNone = 0, PauseMuted, PausePubMuted, PauseFeedDry, PauseBandwidth };
+constexpr i32 TransitionCostSpatial = 10;  // forwarder.go:43
 struct VideoAllocation {
   i32 PauseReason = PauseNone;
   bool IsDeficient = false;
@@ -1809,6 +1810,203 @@ struct Forwarder {
     }
     return updateAllocation(a);
   }
+  // ---- the stream allocator's cooperative pass (forwarder.go:727-1105) ----
+  // VideoAllocationProvisional forwarder.go:96-106
+  struct Provisional {
+    VideoLayer allocatedLayer = InvalidLayer();
+    bool muted = false, pubMuted = false;
+    VideoLayer maxSeenLayer = InvalidLayer();
+    Bitrates bitrates{};
+    std::vector<i32> availableLayers;
+    VideoLayer maxLayer = InvalidLayer(), currentLayer = InvalidLayer();
+  } provisional;
+  // ProvisionalAllocatePrepare :727-743
+  void ProvisionalAllocatePrepare(const std::vector<i32> &availableLayers, const Bitrates &bitrates) {
+    provisional = Provisional{};
+    provisional.muted = muted;
+    provisional.pubMuted = pubMuted;
+    provisional.maxSeenLayer = vls.GetMaxSeen();
+    provisional.bitrates = bitrates;
+    provisional.maxLayer = vls.GetMax();
+    provisional.currentLayer = vls.GetCurrent();
+    provisional.availableLayers = availableLayers;
+  }
+  // ProvisionalAllocateReset :745-750
+  void ProvisionalAllocateReset() { provisional.allocatedLayer = InvalidLayer(); }
+  // ProvisionalAllocate :752-794 -> (isCandidate, usedBitrate)
+  std::pair<bool, i64> ProvisionalAllocate(i64 availableChannelCapacity, VideoLayer layer, bool allowPause,
+                                           bool allowOvershoot) {
+    Provisional &p = provisional;
+    if (p.muted || p.pubMuted || p.maxSeenLayer.Spatial == InvalidLayerSpatial || !p.maxLayer.IsValid() ||
+        ((!allowOvershoot || !IsOvershootOkay()) && layer.GreaterThan(p.maxLayer)))
+      return {false, 0};
+    const i64 required = p.bitrates[layer.Spatial][layer.Temporal];
+    if (required == 0) return {false, 0};
+    i64 already = 0;
+    if (p.allocatedLayer.IsValid()) already = p.bitrates[p.allocatedLayer.Spatial][p.allocatedLayer.Temporal];
+    if (!layer.GreaterThan(p.maxLayer) && required <= availableChannelCapacity + already) {
+      p.allocatedLayer = layer;
+      return {true, required - already};
+    }
+    if (!allowPause && (!p.allocatedLayer.IsValid() || !layer.GreaterThan(p.allocatedLayer))) {
+      p.allocatedLayer = layer;
+      return {true, required - already};
+    }
+    return {false, 0};
+  }
+  // ProvisionalAllocateGetCooperativeTransition :796-929
+  VideoTransition ProvisionalAllocateGetCooperativeTransition(bool allowOvershoot) {
+    Provisional &p = provisional;
+    const VideoLayer existing = vls.GetTarget();
+    if (p.muted || p.pubMuted) {
+      p.allocatedLayer = InvalidLayer();
+      return VideoTransition{existing, p.allocatedLayer,
+                             -getBandwidthNeeded(p.bitrates, existing, lastAllocation.BandwidthRequested)};
+    }
+    if (existing.IsValid()) {
+      VideoLayer maximal = InvalidLayer();
+      i64 maximalBw = 0;
+      for (i32 s = p.maxLayer.Spatial; s >= 0; s--) {
+        for (i32 t = p.maxLayer.Temporal; t >= 0; t--)
+          if (p.bitrates[s][t] != 0) {
+            maximal = VideoLayer{s, t};
+            maximalBw = p.bitrates[s][t];
+            break;
+          }
+        if (maximalBw != 0) break;
+      }
+      if (maximal.IsValid()) {
+        if (!existing.GreaterThan(maximal) && p.bitrates[existing.Spatial][existing.Temporal] != 0) {
+          p.allocatedLayer = existing;
+          return VideoTransition{existing, existing, 0};
+        }
+        if (existing.GreaterThan(maximal)) {
+          p.allocatedLayer = maximal;
+          return VideoTransition{existing, maximal,
+                                 maximalBw - getBandwidthNeeded(p.bitrates, existing, lastAllocation.BandwidthRequested)};
+        }
+      }
+    }
+    auto findNextLayer = [&](i32 minS, i32 maxS, i32 minT, i32 maxT, i64 &bw) {
+      VideoLayer l = InvalidLayer();
+      bw = 0;
+      for (i32 s = minS; s <= maxS; s++) {
+        for (i32 t = minT; t <= maxT; t++)
+          if (p.bitrates[s][t] != 0) {
+            l = VideoLayer{s, t};
+            bw = p.bitrates[s][t];
+            break;
+          }
+        if (bw != 0) break;
+      }
+      return l;
+    };
+    VideoLayer target = InvalidLayer();
+    i64 required = 0;
+    if (!existing.IsValid()) {
+      target = findNextLayer(0, p.maxLayer.Spatial, 0, p.maxLayer.Temporal, required);
+      if (required == 0 && p.maxLayer.IsValid() && allowOvershoot && IsOvershootOkay())
+        target = findNextLayer(p.maxLayer.Spatial + 1, DefaultMaxLayerSpatial, 0, DefaultMaxLayerTemporal, required);
+    }
+    if (!target.IsValid()) {
+      target = p.currentLayer;
+      if (target.IsValid()) required = p.bitrates[target.Spatial][target.Temporal];
+    }
+    p.allocatedLayer = target;
+    return VideoTransition{vls.GetTarget(), target,
+                           required - getBandwidthNeeded(p.bitrates, existing, lastAllocation.BandwidthRequested)};
+  }
+  // ProvisionalAllocateGetBestWeightedTransition :931-1025
+  VideoTransition ProvisionalAllocateGetBestWeightedTransition() {
+    Provisional &p = provisional;
+    const VideoLayer target = vls.GetTarget();
+    if (p.muted || p.pubMuted) {
+      p.allocatedLayer = InvalidLayer();
+      return VideoTransition{target, p.allocatedLayer,
+                             0 - getBandwidthNeeded(p.bitrates, target, lastAllocation.BandwidthRequested)};
+    }
+    i32 maxReachT = InvalidLayerTemporal;
+    for (i32 t = p.maxLayer.Temporal; t >= 0; t--) {
+      for (i32 s = p.maxLayer.Spatial; s >= 0; s--)
+        if (p.bitrates[s][t] != 0) {
+          maxReachT = t;
+          break;
+        }
+      if (maxReachT != InvalidLayerTemporal) break;
+    }
+    if (maxReachT == InvalidLayerTemporal) {
+      p.allocatedLayer = p.currentLayer;
+      return VideoTransition{target, p.allocatedLayer,
+                             0 - getBandwidthNeeded(p.bitrates, target, lastAllocation.BandwidthRequested)};
+    }
+    const i64 existingBw = getBandwidthNeeded(p.bitrates, target, lastAllocation.BandwidthRequested);
+    VideoLayer best = InvalidLayer();
+    i64 bestDelta = 0;
+    float bestValue = 0;
+    for (i32 s = 0; s <= target.Spatial; s++) {
+      for (i32 t = 0; t <= target.Temporal; t++) {
+        if (s == target.Spatial && t == target.Temporal) break;
+        // int64(math.Max(float64(0), float64(existing - brs))) (exact below 2^53)
+        const i64 delta = i64(std::max(0.0, double(existingBw - p.bitrates[s][t])));
+        const i32 transitionCost = target.Spatial != s ? TransitionCostSpatial : 0;
+        const i32 qualityCost = (maxReachT + 1) * (target.Spatial - s) + (target.Temporal - t);
+        float value = 0;
+        if (transitionCost + qualityCost != 0) value = float(delta) / float(transitionCost + qualityCost);
+        if (value > bestValue || (value == bestValue && delta > bestDelta)) {
+          bestValue = value;
+          bestDelta = delta;
+          best = VideoLayer{s, t};
+        }
+      }
+    }
+    p.allocatedLayer = best;
+    return VideoTransition{target, best, -bestDelta};
+  }
+  // ProvisionalAllocateCommit :1027-1105
+  VideoAllocation ProvisionalAllocateCommit() {
+    Provisional &p = provisional;
+    const i64 optimal = getOptimalBandwidthNeeded(p.muted, p.pubMuted, p.maxSeenLayer.Spatial, p.bitrates, p.maxLayer);
+    VideoAllocation a;
+    a.BandwidthRequested = 0;
+    a.BandwidthDelta = 0 - getBandwidthNeeded(p.bitrates, vls.GetTarget(), lastAllocation.BandwidthRequested);
+    a.Brs = p.bitrates;
+    a.BandwidthNeeded = optimal;
+    a.TargetLayer = p.allocatedLayer;
+    a.RequestLayerSpatial = p.allocatedLayer.Spatial;
+    a.MaxLayer = p.maxLayer;
+    a.DistanceToDesired = getDistanceToDesired(p.muted, p.pubMuted, p.maxSeenLayer, p.availableLayers, p.bitrates,
+                                               p.allocatedLayer, p.maxLayer);
+    if (p.muted) {
+      a.PauseReason = PauseMuted;
+    } else if (p.pubMuted) {
+      a.PauseReason = PausePubMuted;
+    } else if (optimal == 0) {
+      if (p.allocatedLayer.IsValid()) {  // overshoot
+        a.BandwidthRequested = p.bitrates[p.allocatedLayer.Spatial][p.allocatedLayer.Temporal];
+        a.BandwidthDelta =
+            a.BandwidthRequested - getBandwidthNeeded(p.bitrates, vls.GetTarget(), lastAllocation.BandwidthRequested);
+      } else {
+        a.PauseReason = PauseFeedDry;
+        if (p.currentLayer.IsValid() && p.currentLayer.Spatial <= p.maxLayer.Spatial) {
+          p.allocatedLayer = p.currentLayer;
+          a.TargetLayer = p.allocatedLayer;
+          a.RequestLayerSpatial = a.TargetLayer.Spatial;
+        }
+      }
+    } else {
+      if (p.allocatedLayer.IsValid()) a.BandwidthRequested = p.bitrates[p.allocatedLayer.Spatial][p.allocatedLayer.Temporal];
+      a.BandwidthDelta =
+          a.BandwidthRequested - getBandwidthNeeded(p.bitrates, vls.GetTarget(), lastAllocation.BandwidthRequested);
+      if (p.allocatedLayer.GreaterThan(p.maxLayer) || a.BandwidthRequested >= optimal) {
+        a.IsDeficient = false;
+      } else {
+        a.IsDeficient = true;
+        if (!p.allocatedLayer.IsValid()) a.PauseReason = PauseBandwidth;
+      }
+    }
+    return updateAllocation(a);
+  }
+
   // Resync / resyncLocked forwarder.go:1384-1397
   void Resync() { resyncLocked(); }
   void resyncLocked() {

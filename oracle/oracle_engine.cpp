@@ -1177,6 +1177,118 @@ int orc_pause(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocati
   return allocCommon(e, 3, reqs, nullptr, n, out);
 }
 
+// ---- the cooperative allocation pass (Provisional*, allocateAllTracks) ------
+static bool provCheck(orc_engine *e, const int32_t *dts, uint32_t n, size_t stride) {
+  std::vector<u8> seen(e->dts.size(), 0);
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t dt = *reinterpret_cast<const int32_t *>(reinterpret_cast<const u8 *>(dts) + i * stride);
+    if (dt < 0 || dt >= (int)e->dts.size() || seen[dt] || !e->dts[dt]->active ||
+        e->tracks[e->dts[dt]->p.track].p.kind != LKF_KIND_VIDEO)
+      return false;
+    seen[dt] = 1;
+  }
+  return true;
+}
+static void reqLayers(const lkf_alloc_req &q, std::vector<i32> &avail, Bitrates &brs) {
+  for (i32 l = 0; l < 32; l++)
+    if (q.available_layers & (1u << l)) avail.push_back(l);
+  for (int s = 0; s < 3; s++)
+    for (int t = 0; t < 4; t++) brs[s][t] = q.bitrates[s][t];
+}
+static void toTransition(const Forwarder::VideoTransition &tr, int32_t dt, lkf_video_transition &o) {
+  std::memset(&o, 0, sizeof(o));
+  o.dt = dt;
+  o.from_spatial = tr.From.Spatial;
+  o.from_temporal = tr.From.Temporal;
+  o.to_spatial = tr.To.Spatial;
+  o.to_temporal = tr.To.Temporal;
+  o.bandwidth_delta = tr.BandwidthDelta;
+  o.available = 1;
+}
+int orc_provisional_prepare(orc_engine *e, const lkf_alloc_req *reqs, uint32_t n) {
+  if (n && (!reqs || !provCheck(e, &reqs[0].dt, n, sizeof(lkf_alloc_req)))) return LKF_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    std::vector<i32> avail;
+    Bitrates brs;
+    reqLayers(reqs[i], avail, brs);
+    e->dts[reqs[i].dt]->f->ProvisionalAllocatePrepare(avail, brs);
+  }
+  return LKF_OK;
+}
+int orc_provisional_reset(orc_engine *e, const int32_t *dts, uint32_t n) {
+  if (n && (!dts || !provCheck(e, dts, n, sizeof(int32_t)))) return LKF_EINVAL;
+  for (uint32_t i = 0; i < n; i++) e->dts[dts[i]]->f->ProvisionalAllocateReset();
+  return LKF_OK;
+}
+int orc_provisional_allocate(orc_engine *e, const lkf_prov_req *reqs, uint32_t n, lkf_prov_result *out) {
+  if (n && (!reqs || !out || !provCheck(e, &reqs[0].dt, n, sizeof(lkf_prov_req)))) return LKF_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    const lkf_prov_req &q = reqs[i];
+    std::memset(&out[i], 0, sizeof(out[i]));
+    out[i].dt = q.dt;
+    if (q.spatial < 0 || q.spatial > 2 || q.temporal < 0 || q.temporal > 3) continue;
+    const auto r = e->dts[q.dt]->f->ProvisionalAllocate(q.capacity, VideoLayer{q.spatial, q.temporal}, q.allow_pause != 0,
+                                                          q.allow_overshoot != 0);
+    out[i].is_candidate = r.first ? 1 : 0;
+    out[i].used = r.second;
+  }
+  return LKF_OK;
+}
+int orc_provisional_cooperative(orc_engine *e, const lkf_prov_req *reqs, uint32_t n, lkf_video_transition *out) {
+  if (n && (!reqs || !out || !provCheck(e, &reqs[0].dt, n, sizeof(lkf_prov_req)))) return LKF_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    toTransition(e->dts[reqs[i].dt]->f->ProvisionalAllocateGetCooperativeTransition(reqs[i].allow_overshoot != 0),
+                 reqs[i].dt, out[i]);
+  return LKF_OK;
+}
+int orc_provisional_best_weighted(orc_engine *e, const int32_t *dts, uint32_t n, lkf_video_transition *out) {
+  if (n && (!dts || !out || !provCheck(e, dts, n, sizeof(int32_t)))) return LKF_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    toTransition(e->dts[dts[i]]->f->ProvisionalAllocateGetBestWeightedTransition(), dts[i], out[i]);
+  return LKF_OK;
+}
+int orc_provisional_commit(orc_engine *e, const int32_t *dts, uint32_t n, lkf_allocation *out) {
+  if (n && (!dts || !out || !provCheck(e, dts, n, sizeof(int32_t)))) return LKF_EINVAL;
+  for (uint32_t i = 0; i < n; i++) toAllocation(e->dts[dts[i]]->f->ProvisionalAllocateCommit(), dts[i], false, out[i]);
+  return LKF_OK;
+}
+// StreamAllocator.allocateAllTracks managed pass streamallocator.go:1147-1172
+int orc_allocate_all(orc_engine *e, const lkf_alloc_group *groups, uint32_t ngroups, const lkf_alloc_req *reqs,
+                     uint32_t n, lkf_allocation *out) {
+  std::vector<u8> cover(n, 0);
+  for (uint32_t g = 0; g < ngroups; g++) {
+    if (u64(groups[g].first) + groups[g].count > n) return LKF_EINVAL;
+    for (uint32_t k = 0; k < groups[g].count; k++)
+      if (cover[groups[g].first + k]++) return LKF_EINVAL;
+  }
+  if (!ngroups || !n) return LKF_OK;
+  if (!provCheck(e, &reqs[0].dt, n, sizeof(lkf_alloc_req))) return LKF_EINVAL;
+  std::memset(out, 0, n * sizeof(lkf_allocation));
+  for (uint32_t g = 0; g < ngroups; g++) {
+    const lkf_alloc_group &G = groups[g];
+    for (uint32_t k = 0; k < G.count; k++) {
+      std::vector<i32> avail;
+      Bitrates brs;
+      reqLayers(reqs[G.first + k], avail, brs);
+      e->dts[reqs[G.first + k].dt]->f->ProvisionalAllocatePrepare(avail, brs);
+    }
+    i64 cap = G.capacity;
+    for (i32 s = 0; s <= DefaultMaxLayerSpatial; s++)
+      for (i32 t = 0; t <= DefaultMaxLayerTemporal; t++)
+        for (uint32_t k = 0; k < G.count; k++) {
+          const auto r = e->dts[reqs[G.first + k].dt]->f->ProvisionalAllocate(cap, VideoLayer{s, t}, G.allow_pause != 0,
+                                                                                G.allow_overshoot != 0);
+          cap -= r.second;
+          if (cap < 0) cap = 0;
+        }
+    for (uint32_t k = 0; k < G.count; k++) {
+      const int32_t dt = reqs[G.first + k].dt;
+      toAllocation(e->dts[dt]->f->ProvisionalAllocateCommit(), dt, false, out[G.first + k]);
+    }
+  }
+  return LKF_OK;
+}
+
 int orc_padding(orc_engine *e, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out, uint8_t *arena,
                 uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len, uint32_t *bytes_sent) {
   return padCommon(e, 0, reqs, n, now_ns, out, arena, out_cap, arena_cap, n_out, arena_len, bytes_sent);

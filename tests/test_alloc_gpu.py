@@ -203,3 +203,59 @@ def test_pause_and_next_higher_match_oracle(pkg, workload, cfg):
         eng.close()
         o.destroy(oh)
         tr.close()
+
+
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=3, seed=41), dict(config=5, rooms=6, svc_dd=1, seed=42),
+                                 dict(config=5, rooms=6, svc_dd=0, seed=43), dict(config=2, rooms=2, h264=1, seed=44)])
+def test_provisional_pass_matches_oracle(pkg, workload, cfg):
+    """The stream allocator's cooperative pass (Forwarder.Provisional*,
+    forwarder.go:727-1105, and allocateAllTracks' greedy per subscriber) between
+    batches: every result, the batches forwarded on the committed targets and
+    the Forwarder state must be identical."""
+    from tests import prov_lib
+    o = load_oracle()
+    abi = pkg.abi
+    kw = dict(cfg)
+    tr = workload.Trace(kw.pop("config"), duration_s=4.0, batch_s=1.0, **kw)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+        committed = 0
+        for b in range(tr.nbatches):
+            if b in (1, 2, 3):
+                for i, step in enumerate(prov_lib.steps(tr, seed=100 * b + cfg.get("seed", 0))):
+                    g = prov_lib.run(eng.api, eng.h, step)
+                    r = prov_lib.run(o.api, oh, step)
+                    if r is None:
+                        continue
+                    for f in r.dtype.names:
+                        if f != "reserved":
+                            assert np.array_equal(g[f], r[f]), (b, i, step[0], f)
+                    if step[0] in ("commit", "allocate_all"):
+                        committed += len(r)
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            dd = tr.batch_dd(b)[0] if tr.has_dd() else None
+            eng.submit(pk, n, ar, alen, dd)
+            eng.run()
+            eng.sync()
+            o.run(oh, pk, n, ar, alen, dd)
+            grec, gar = eng.drain()
+            orec, oar = pkg.drain_arrays(o.api, oh)
+            assert len(grec) == len(orec), b
+            for f in abi.OUT_DTYPE.names:
+                assert np.array_equal(grec[f], orec[f]), (b, f)
+            assert np.array_equal(gar, oar), b
+        assert committed > 0
+        for dt in range(tr.ndts):
+            gs, os_ = abi.lkf_fwd_state(), abi.lkf_fwd_state()
+            eng.api["get_state"](eng.h, dt, C.byref(gs))
+            o.api["get_state"](oh, dt, C.byref(os_))
+            assert gs.as_tuple() == os_.as_tuple(), dt
+    finally:
+        eng.close()
+        o.destroy(oh)
+        tr.close()
