@@ -622,6 +622,33 @@ int32_t lkf_add_stream_tracker_frame(lkf_engine *e, int32_t track, int32_t layer
 int lkf_stream_trackers_tick_at(lkf_engine *e, const int32_t *trackers, uint32_t n, int check,
                                 int64_t bitrate_elapsed_ns, int64_t now_ns, lkf_tracker_status *out);
 
+/* The dependency-descriptor stream tracker (streamtracker_dd.go:27-289) of an
+ * SVC track with the DD extension (StreamTrackerManager.AddDependencyDescriptorTrackers,
+ * streamtrackermanager.go:166-186): observed on the GPU with every lkf_run
+ * batch's descriptors (k_dd_decode: an updated active-decode-target mask sets
+ * the max spatial / temporal layer and notifies the spatial layers that start
+ * or stop; each packet's size is added to the bitrate bytes of every decode
+ * target its frame is present in).  Its worker (started by the first mask or
+ * SetPaused(true)) reports bitrates at host ticks (Duration.Seconds of the
+ * elapsed interval).  Status(layer) = active up to the max spatial layer;
+ * BitrateTemporalCumulative(layer) = that layer's per-temporal bitrates. */
+typedef struct lkf_dd_tracker_status {
+  int32_t tracker;
+  int32_t max_spatial, max_temporal;
+  uint32_t bitrate_changed;   /* bit s: onBitrateAvailable(s) fired by this tick's report */
+  uint32_t notifications[3];  /* onStatusChanged calls per spatial layer */
+  int32_t last_notified[3];   /* the status passed by the last call per layer (-1: none) */
+  uint8_t status[3];          /* Status(layer): 0 stopped, 1 active */
+  uint8_t worker;             /* the bitrate worker runs */
+  uint32_t reserved;
+  int64_t bitrate[3][4];      /* BitrateTemporalCumulative(layer) */
+} lkf_dd_tracker_status;
+/* >= 0 handle; LKF_EINVAL for a track without the DD selector or a second tracker. */
+int32_t lkf_add_stream_tracker_dd(lkf_engine *e, int32_t track);
+int lkf_dd_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t arg); /* LKF_TRACKER_PAUSE / _STOP */
+int lkf_dd_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n, int64_t bitrate_elapsed_ns,
+                         lkf_dd_tracker_status *out);
+
 /* ---- stream allocation ------------------------------ */
 typedef struct lkf_alloc_req {
   int32_t dt;

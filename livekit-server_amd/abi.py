@@ -109,6 +109,12 @@ assert PROV_RESULT_DTYPE.itemsize == 16
 ALLOC_GROUP_DTYPE = np.dtype([("first", "<u4"), ("count", "<u4"), ("capacity", "<i8"), ("allow_pause", "u1"),
                               ("allow_overshoot", "u1"), ("reserved", "u1", 6)])
 assert ALLOC_GROUP_DTYPE.itemsize == 24
+# lkf_dd_tracker_status (StreamTrackerDependencyDescriptor)
+DD_TRACKER_STATUS_DTYPE = np.dtype([("tracker", "<i4"), ("max_spatial", "<i4"), ("max_temporal", "<i4"),
+                                    ("bitrate_changed", "<u4"), ("notifications", "<u4", (3,)),
+                                    ("last_notified", "<i4", (3,)), ("status", "u1", (3,)), ("worker", "u1"),
+                                    ("reserved", "<u4"), ("bitrate", "<i8", (3, 4))])
+assert DD_TRACKER_STATUS_DTYPE.itemsize == 144
 # lkf_sender_stats (DownTrack.rtpStats = buffer.RTPStatsSender)
 SENDER_STATS_DTYPE = np.dtype(
     [(f, "<u8") for f in ("ext_start_sn", "ext_highest_sn", "ext_start_ts", "ext_highest_ts")]
@@ -458,6 +464,11 @@ def bind_engine_api(lib, prefix):
         api["next_higher_transition"] = _bind(lib, prefix + "next_higher_transition", C.c_int,
                                               [e, C.c_void_p, C.c_uint32, C.c_void_p])
         api["pause"] = _bind(lib, prefix + "pause", C.c_int, [e, C.c_void_p, C.c_uint32, C.c_void_p])
+    if hasattr(lib, prefix + "add_stream_tracker_dd"):
+        api["add_stream_tracker_dd"] = _bind(lib, prefix + "add_stream_tracker_dd", C.c_int32, [e, C.c_int32])
+        api["dd_tracker_ctl"] = _bind(lib, prefix + "dd_tracker_ctl", C.c_int, [e, C.c_int32, C.c_int32, C.c_int32])
+        api["dd_trackers_tick"] = _bind(lib, prefix + "dd_trackers_tick", C.c_int,
+                                        [e, C.c_void_p, C.c_uint32, C.c_int64, C.c_void_p])
     if hasattr(lib, prefix + "provisional_prepare"):
         api["provisional_prepare"] = _bind(lib, prefix + "provisional_prepare", C.c_int, [e, C.c_void_p, C.c_uint32])
         api["provisional_reset"] = _bind(lib, prefix + "provisional_reset", C.c_int, [e, C.c_void_p, C.c_uint32])

@@ -175,6 +175,14 @@ struct lkf_engine {
   lkf_alloc_group *dProvGroups = nullptr;
   uint8_t *dProvOut = nullptr;
   uint32_t provCap = 0, provGroupCap = 0;
+  // dependency-descriptor stream trackers (lkf_add_stream_tracker_dd)
+  DDTrkState *dDDTrk = nullptr;
+  uint32_t *dTrackDDTrk = nullptr;  // track -> DD tracker (0xffffffff none), max_tracks
+  std::vector<int32_t> trackDDTrk;
+  uint32_t nDDTrk = 0, ddTrkCap = 0;
+  int32_t *dDDTrkIds = nullptr;
+  lkf_dd_tracker_status *dDDTrkOut = nullptr;
+  uint64_t ddTrkIdsCap = 0, ddTrkOutCap = 0;
   uint32_t rtxDDCap = 0;
   DevDT *dDTs = nullptr;
   RangeEntry *dRm = nullptr;
@@ -839,7 +847,8 @@ void lkf_destroy(lkf_engine *e) {
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
                   e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut,
                   e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups, e->dSeqDD, e->dSeqDDIdx,
-                  e->dSeqDDList, e->dRtxDD, e->dProv, e->dProvReq, e->dProvGroups, e->dProvOut};
+                  e->dSeqDDList, e->dRtxDD, e->dProv, e->dProvReq, e->dProvGroups, e->dProvOut,
+                  e->dDDTrk, e->dTrackDDTrk, e->dDDTrkIds, e->dDDTrkOut};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
@@ -1321,7 +1330,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     if (e->ddAlloc) {  // dependency descriptors of this batch (track structure rings advance in order)
       HIPCHK(hipMemsetAsync(x.dDDUsed, 0, sizeof(uint64_t), ps), "dd cursor reset");
       HIPCHK(launch_dd_decode(ps, x.dDesc, x.dTBegin, x.dTEnd, e->dTracks, nt, e->dDDStruct, e->dDDTrack, x.dDDPkt,
-                              x.dErr),
+                              x.dErr, e->nDDTrk ? e->dTrackDDTrk : nullptr, e->dDDTrk),
              "dd decode");
     }
     return LKF_OK;
@@ -2329,6 +2338,89 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
       out[w++] = o;
       pos += al;
     }
+  return LKF_OK;
+}
+
+// ---- the dependency-descriptor stream tracker (streamtracker_dd.go) --------
+int32_t lkf_add_stream_tracker_dd(lkf_engine *e, int32_t track) {
+  if (!e || track < 0 || track >= int32_t(e->tracks.size()) || !track_has_dd(e->tracks[track])) return LKF_EINVAL;
+  if (e->trackDDTrk.size() < e->tracks.size()) e->trackDDTrk.resize(e->tracks.size(), -1);
+  if (e->trackDDTrk[track] >= 0) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  if (!e->dTrackDDTrk) {
+    HIPCHK(dalloc(&e->dTrackDDTrk, e->cfg.max_tracks), "alloc track dd trackers");
+    HIPCHK(hipMemset(e->dTrackDDTrk, 0xff, size_t(e->cfg.max_tracks) * sizeof(uint32_t)), "track dd trackers reset");
+  }
+  if (e->nDDTrk + 1 > e->ddTrkCap) {
+    const uint32_t cap = std::max<uint32_t>(2 * e->ddTrkCap, 256);
+    DDTrkState *n = nullptr;
+    HIPCHK(dalloc(&n, cap), "alloc dd trackers");
+    if (e->nDDTrk) HIPCHK(hipMemcpy(n, e->dDDTrk, e->nDDTrk * sizeof(DDTrkState), hipMemcpyDeviceToDevice), "dd trackers move");
+    if (e->dDDTrk) HIPCHK(hipFree(e->dDDTrk), "free dd trackers");
+    e->dDDTrk = n;
+    e->ddTrkCap = cap;
+  }
+  DDTrkState t;
+  std::memset(&t, 0, sizeof(t));
+  t.maxS = t.maxT = -1;
+  for (int l = 0; l < 3; l++) t.lastNotified[l] = -1;
+  t.track = uint32_t(track);
+  const uint32_t id = e->nDDTrk++;
+  HIPCHK(hipMemcpy(e->dDDTrk + id, &t, sizeof(t), hipMemcpyHostToDevice), "dd tracker init");
+  HIPCHK(hipMemcpy(e->dTrackDDTrk + track, &id, sizeof(id), hipMemcpyHostToDevice), "track dd tracker");
+  e->trackDDTrk[track] = int32_t(id);
+  e->epoch++;  // the prep graph's k_dd_decode observes the trackers
+  return upload_done(e) ? LKF_EHIP : int32_t(id);
+}
+
+// SetPaused / Stop (streamtracker_dd.go:57-68, :123-137) on the host copy
+int lkf_dd_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t arg) {
+  if (!e || tracker < 0 || uint32_t(tracker) >= e->nDDTrk) return LKF_EINVAL;
+  if (op != LKF_TRACKER_PAUSE && op != LKF_TRACKER_STOP) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  DDTrkState t;
+  HIPCHK(hipMemcpy(&t, e->dDDTrk + tracker, sizeof(t), hipMemcpyDeviceToHost), "dd tracker read");
+  if (op == LKF_TRACKER_STOP) {
+    if (!(t.flags & DT_STOPPED)) t.flags = (t.flags | DT_STOPPED) & ~DT_WORKER;
+  } else {
+    const bool p = arg != 0;
+    if (bool(t.flags & DT_PAUSED) != p) {
+      if (p) {
+        t.flags |= DT_PAUSED | DT_WORKER;  // a worker drains the bitrates while paused
+      } else {  // resetLocked :108-121
+        t.flags &= ~(DT_PAUSED | DT_WORKER);
+        std::memset(t.bytes, 0, sizeof(t.bytes));
+        std::memset(t.bitrate, 0, sizeof(t.bitrate));
+      }
+    }
+  }
+  HIPCHK(hipMemcpy(e->dDDTrk + tracker, &t, sizeof(t), hipMemcpyHostToDevice), "dd tracker write");
+  return upload_done(e);
+}
+
+int lkf_dd_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n, int64_t bitrate_elapsed_ns,
+                         lkf_dd_tracker_status *out) {
+  if (!e || (n && (!trackers || !out))) return LKF_EINVAL;
+  std::vector<uint8_t> seen(e->nDDTrk, 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (trackers[i] < 0 || uint32_t(trackers[i]) >= e->nDDTrk || seen[trackers[i]]) return LKF_EINVAL;
+    seen[trackers[i]] = 1;
+  }
+  if (!n) return LKF_OK;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  HIPCHK(grow(&e->dDDTrkIds, e->ddTrkIdsCap, n), "alloc dd tracker ids");
+  HIPCHK(grow(&e->dDDTrkOut, e->ddTrkOutCap, n), "alloc dd tracker out");
+  HIPCHK(hipMemcpy(e->dDDTrkIds, trackers, n * sizeof(int32_t), hipMemcpyHostToDevice), "dd tracker ids copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_dd_tracker_tick(e->own, e->dDDTrk, e->dDDTrkIds, n, bitrate_elapsed_ns, e->dDDTrkOut), "dd tracker tick");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  HIPCHK(hipMemcpy(out, e->dDDTrkOut, n * sizeof(lkf_dd_tracker_status), hipMemcpyDeviceToHost), "dd tracker out copy");
   return LKF_OK;
 }
 

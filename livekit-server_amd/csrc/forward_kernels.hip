@@ -4378,9 +4378,41 @@ hipError_t launch_err_fold(hipStream_t s, const u32 *err, u32 *sticky, u32 shift
 // track (packets of a track in order); runs on the prep stream, so batch n+1's
 // decode follows batch n's.
 // ---------------------------------------------------------------------------
+// StreamTrackerDependencyDescriptor.Observe (streamtracker_dd.go:133-212) of one
+// packet, serial in the track's lane
+__device__ void dd_tracker_observe(DDTrkState &T, const DDStruct &S, const DDPkt &o, u32 ddFlags, u32 pktSize,
+                                   u32 payload) {
+  if ((T.flags & (DT_PAUSED | DT_STOPPED)) || payload == 0) return;
+  if ((o.flags & DP_ACTIVE) && (ddFlags & LKF_DD_ACTIVE_UPDATED)) {
+    i32 ms = 0, mt = 0;
+    for (u32 k = 0; k < S.numDT; k++)
+      if (o.activeMask & (1u << S.dtTarget[k])) {
+        ms = max(ms, i32(S.dtS[k]));
+        mt = max(mt, i32(S.dtT[k]));
+      }
+    ms = min(ms, 2);
+    mt = min(mt, 3);
+    const i32 old = T.maxS;
+    T.maxS = ms;
+    T.maxT = mt;
+    if (old == -1) T.flags |= DT_WORKER;  // go s.worker(generation)
+    const i32 lo = old > ms ? ms + 1 : old + 1, hi = old > ms ? old : ms;
+    for (i32 l = lo; l <= hi && old != ms; l++) {
+      T.notif[l]++;
+      T.lastNotified[l] = old > ms ? 0 : 1;  // StreamStatusStopped / Active
+    }
+  }
+  for (u32 k = 0; k < S.numDT; k++) {
+    const u32 tg = S.dtTarget[k];
+    if (o.ndti <= tg || ((o.dtis >> (2 * tg)) & 3) == 0) continue;  // DecodeTargetNotPresent
+    T.bytes[S.dtS[k]][S.dtT[k]] += pktSize;
+  }
+}
+
 __global__ void k_dd_decode(const RunDesc *__restrict__ desc, const u32 *__restrict__ tBegin,
                             const u32 *__restrict__ tEnd, const DevTrack *__restrict__ tracks, u32 ntracks,
-                            DDStruct *structs, DDTrack *ddTracks, DDPkt *__restrict__ out, u32 *err) {
+                            DDStruct *structs, DDTrack *ddTracks, DDPkt *__restrict__ out, u32 *err,
+                            const u32 *__restrict__ trackDDTrk, DDTrkState *ddTrk) {
   const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
   const lkf_pkt_dd *__restrict__ dds = reinterpret_cast<const lkf_pkt_dd *>(desc->dd);
   const u8 *__restrict__ arena = reinterpret_cast<const u8 *>(desc->arena);
@@ -4420,6 +4452,9 @@ __global__ void k_dd_decode(const RunDesc *__restrict__ desc, const u32 *__restr
       }
       o.slot = u8(st.cur);
       o.flags |= DP_VALID;
+      if (trackDDTrk && trackDDTrk[t] != 0xffffffffu)  // the track's DD stream tracker (receiver.go:686-695)
+        dd_tracker_observe(ddTrk[trackDDTrk[t]], ring[o.slot], o, r.flags,
+                           u32(pkts[i].payload_off) + pkts[i].payload_len, pkts[i].payload_len);
     }
     out[i] = o;
   }
@@ -4432,10 +4467,10 @@ __global__ void k_dd_decode(const RunDesc *__restrict__ desc, const u32 *__restr
 
 hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                             const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,
-                            uint32_t *err) {
+                            uint32_t *err, const uint32_t *trackDDTrk, DDTrkState *ddTrk) {
   if (!ntracks) return hipSuccess;
   hipLaunchKernelGGL(k_dd_decode, dim3((ntracks + 63) / 64), dim3(64), 0, s, desc, tBegin, tEnd, tracks, ntracks,
-                     structs, ddTracks, out, err);
+                     structs, ddTracks, out, err, trackDDTrk, ddTrk);
   return hipGetLastError();
 }
 

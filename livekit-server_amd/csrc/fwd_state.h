@@ -277,6 +277,20 @@ struct alignas(16) ProvState {
 };
 static_assert(sizeof(ProvState) == 144, "ProvState is 144 B");
 
+// StreamTrackerDependencyDescriptor (streamtracker_dd.go:27-289), one per DD
+// track that has one (lkf_add_stream_tracker_dd)
+enum : uint32_t { DT_PAUSED = 1, DT_STOPPED = 2, DT_WORKER = 4 };
+struct alignas(16) DDTrkState {
+  int64_t bytes[3][4], bitrate[3][4];
+  int32_t maxS, maxT;
+  uint32_t flags;         // DT_*
+  uint32_t changedMask;   // onBitrateAvailable per spatial layer by the last report
+  uint32_t notif[3];      // onStatusChanged calls per spatial layer
+  int32_t lastNotified[3];
+  uint32_t track, pad;
+};
+static_assert(sizeof(DDTrkState) % 16 == 0, "DDTrkState is 16-B granular");
+
 constexpr int kHistWords = 64;  // cHistorySize 4096 bits (rtpstats_receiver.go:30)
 
 struct DevStream {  // static stream parameters (64 B)

@@ -140,7 +140,10 @@ hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const uint32_t
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
 hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                             const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,
-                            uint32_t *err);
+                            uint32_t *err, const uint32_t *trackDDTrk = nullptr, DDTrkState *ddTrk = nullptr);
+// the DD stream trackers' bitrate report (tracker_kernels.hip)
+hipError_t launch_dd_tracker_tick(hipStream_t s, DDTrkState *st, const int32_t *ids, uint32_t n, int64_t elapsedNs,
+                                  lkf_dd_tracker_status *out);
 hipError_t launch_h2d(hipStream_t s, const uint8_t *stage, RunDesc *dDesc, DevEvent *dEv, uint32_t *dLane);
 hipError_t launch_stats_reduce(hipStream_t s, uint64_t *stats);
 // dense per-lane op offsets from the lane-sorted op list: off[l] = first op with lane >= l

@@ -188,7 +188,51 @@ __global__ void k_tracker_tick(TrackerState *st, const int32_t *__restrict__ ids
   for (int t = 0; t < 4; t++) o.cumulative[t] = c[t];
   out[i] = o;
 }
+
+// the DD stream tracker's worker tick: bitrateReport (streamtracker_dd.go:226-259)
+// over the elapsed interval (time.Duration.Seconds), then the status
+__global__ void k_dd_tracker_tick(DDTrkState *st, const int32_t *__restrict__ ids, u32 n, i64 elapsedNs,
+                                  lkf_dd_tracker_status *out) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DDTrkState s = st[ids[i]];
+  s.changedMask = 0;
+  if ((s.flags & DT_WORKER) && elapsedNs > 0) {
+    const double secs = double(elapsedNs / 1000000000LL) + double(elapsedNs % 1000000000LL) / 1e9;
+    for (int l = 0; l < 3; l++) {
+      bool changed = false;
+      for (int t = 0; t < 4; t++) {
+        const i64 br = i64(double(s.bytes[l][t] * 8) / secs);
+        if ((s.bitrate[l][t] == 0 && br > 0) || (s.bitrate[l][t] > 0 && br == 0)) changed = true;
+        s.bitrate[l][t] = br;
+        s.bytes[l][t] = 0;
+      }
+      if (changed) s.changedMask |= 1u << l;
+    }
+  }
+  st[ids[i]] = s;
+  lkf_dd_tracker_status o = {};
+  o.tracker = ids[i];
+  o.max_spatial = s.maxS;
+  o.max_temporal = s.maxT;
+  o.bitrate_changed = s.changedMask;
+  for (int l = 0; l < 3; l++) {
+    o.notifications[l] = s.notif[l];
+    o.last_notified[l] = s.lastNotified[l];
+    o.status[l] = l > s.maxS ? 0 : 1;  // Status(layer) :84-93
+    for (int t = 0; t < 4; t++) o.bitrate[l][t] = l > s.maxS ? 0 : s.bitrate[l][t];  // BitrateTemporalCumulative
+  }
+  o.worker = (s.flags & DT_WORKER) ? 1 : 0;
+  out[i] = o;
+}
 }  // namespace
+
+hipError_t launch_dd_tracker_tick(hipStream_t s, DDTrkState *st, const int32_t *ids, uint32_t n, int64_t elapsedNs,
+                                  lkf_dd_tracker_status *out) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_dd_tracker_tick, dim3((n + 63) / 64), dim3(64), 0, s, st, ids, n, elapsedNs, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_tracker_observe(hipStream_t s, TrackerState *st, uint32_t n, const RunDesc *desc,
                                   const uint32_t *tBegin, const uint32_t *tEnd) {

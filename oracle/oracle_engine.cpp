@@ -122,6 +122,10 @@ struct orc_engine {
   std::vector<std::pair<u32, i32>> trkKey;
   std::vector<orc_st::Tracker> trk;
   i64 rtxNow = 0;  // now_ns of the last orc_rtx_lookup
+  // dependency-descriptor stream trackers: the track and the tracker
+  std::vector<u32> ddTrkTrack;
+  std::vector<orc_st::DDTracker> ddTrk;
+  std::vector<int32_t> trackDDTrk;  // track -> DD tracker (-1 none)
 };
 
 static void applyCtl(orc_engine *e, ODT &d, const OEv &ev) {
@@ -443,6 +447,21 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
     bool ok = true;
     ExtPacket ep = toExt(pd, arena, i < dds.size() ? &dds[i] : nullptr, e->tracks[pd.track], ok);
     if (!ok) return LKF_EINVAL;
+    // the DD stream tracker's Observe (receiver.go:686-695; streamtracker_dd.go:133-212)
+    if (pd.track < e->trackDDTrk.size() && e->trackDDTrk[pd.track] >= 0 && ep.dd && ep.dd->Descriptor) {
+      const ExtDD &x = *ep.dd;
+      orc_st::DDTracker::DT tg[32];
+      int nt = 0;
+      for (const auto &t : x.DecodeTargets)
+        if (nt < 32) tg[nt++] = {t.Target, t.Layer.Spatial, t.Layer.Temporal};
+      uint8_t dtis[32];
+      const auto &di = x.Descriptor->FrameDependencies.DTIs;
+      const int nd = int(std::min<size_t>(di.size(), 32));
+      for (int k = 0; k < nd; k++) dtis[k] = uint8_t(di[k]);
+      e->ddTrk[e->trackDDTrk[pd.track]].Observe(int(pd.payload_off) + pd.payload_len, pd.payload_len, true,
+                                                x.ActiveDecodeTargetsUpdated, x.Descriptor->hasActiveMask,
+                                                x.Descriptor->ActiveDecodeTargetsBitmask, tg, nt, dtis, nd);
+    }
     for (u32 d : trackDts[pd.track]) {
       ODT &dt = *e->dts[d];
       while (evc[d] < evq[d].size() && evq[d][evc[d]].at <= i) applyCtl(e, dt, evq[d][evc[d]++]);
@@ -969,6 +988,51 @@ static int padCommon(orc_engine *e, int blank, const lkf_pad_req *reqs, uint32_t
 }
 
 // stream trackers (lkf_add_stream_tracker / _ctl / _tick)
+// ---- the dependency-descriptor stream tracker (streamtracker_dd.go) --------
+int32_t orc_add_stream_tracker_dd(orc_engine *e, int32_t track) {
+  if (track < 0 || track >= (int)e->tracks.size()) return LKF_EINVAL;
+  const lkf_track_params &p = e->tracks[track].p;
+  if (!p.has_dd || (p.codec != LKF_CODEC_VP9 && p.codec != LKF_CODEC_AV1)) return LKF_EINVAL;
+  if (e->trackDDTrk.size() < e->tracks.size()) e->trackDDTrk.resize(e->tracks.size(), -1);
+  if (e->trackDDTrk[track] >= 0) return LKF_EINVAL;
+  e->trackDDTrk[track] = int32_t(e->ddTrk.size());
+  e->ddTrkTrack.push_back(u32(track));
+  e->ddTrk.emplace_back();
+  return int32_t(e->ddTrk.size() - 1);
+}
+int orc_dd_tracker_ctl(orc_engine *e, int32_t id, int32_t op, int32_t arg) {
+  if (id < 0 || id >= (int)e->ddTrk.size()) return LKF_EINVAL;
+  if (op == LKF_TRACKER_PAUSE)
+    e->ddTrk[id].SetPaused(arg != 0);
+  else if (op == LKF_TRACKER_STOP)
+    e->ddTrk[id].Stop();
+  else
+    return LKF_EINVAL;
+  return LKF_OK;
+}
+int orc_dd_trackers_tick(orc_engine *e, const int32_t *ids, uint32_t n, int64_t elapsed, lkf_dd_tracker_status *out) {
+  for (uint32_t i = 0; i < n; i++)
+    if (ids[i] < 0 || ids[i] >= (int)e->ddTrk.size()) return LKF_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    orc_st::DDTracker &t = e->ddTrk[ids[i]];
+    t.Tick(elapsed);
+    lkf_dd_tracker_status &o = out[i];
+    std::memset(&o, 0, sizeof(o));
+    o.tracker = ids[i];
+    o.max_spatial = t.maxS;
+    o.max_temporal = t.maxT;
+    o.bitrate_changed = t.bitrateChangedMask;
+    for (int l = 0; l < 3; l++) {
+      o.notifications[l] = u32(t.notifications[l]);
+      o.last_notified[l] = t.lastNotified[l];
+      o.status[l] = u8(t.Status(l));
+      t.Cumulative(l, o.bitrate[l]);
+    }
+    o.worker = t.workerLive ? 1 : 0;
+  }
+  return LKF_OK;
+}
+
 int32_t orc_add_stream_tracker(orc_engine *e, int32_t track, int32_t layer, uint32_t samples, uint32_t cycles) {
   if (track < 0 || track >= (int)e->tracks.size() || layer < 0) return LKF_EINVAL;
   e->trkKey.push_back({u32(track), layer});

@@ -255,4 +255,102 @@ struct Tracker {  // StreamTracker over a PacketTracker (or a FrameTracker when 
   }
 };
 
+// StreamTrackerDependencyDescriptor streamtracker_dd.go:27-289 — one per SVC
+// track with the dependency-descriptor extension, shared by its spatial
+// layers (LayeredTracker).  Observe takes the packet's ExtDependencyDescriptor
+// (nullptr-equivalent: hasDD false): the active-decode-target mask when
+// updated, the parser's decode targets and the frame's DTIs.  The worker runs
+// from the first mask (maxSpatial leaving -1) or a SetPaused(true) until
+// Stop / SetPaused(false); host ticks report bitrates over `elapsedNs`.
+// Pinned by streamtracker_dd_test.go (kat_tracker.inc).
+struct DDTracker {
+  struct DT {
+    int target;
+    int s, t;
+  };
+  bool paused = false, stopped = false, workerLive = false;
+  int maxS = -1, maxT = -1;  // InvalidLayerSpatial / InvalidLayerTemporal
+  i64 bytes[3][4] = {}, bitrate[3][4] = {};
+  int notifications[3] = {0, 0, 0};  // onStatusChanged calls per layer
+  int lastNotified[3] = {-1, -1, -1};  // the status of the last call per layer (-1: none)
+  u32 bitrateChangedMask = 0;          // onBitrateAvailable per layer by the last report
+  void notify(int from, int to, int st) {
+    for (int i = from; i <= to; i++) {
+      notifications[i]++;
+      lastNotified[i] = st;
+    }
+  }
+  // Observe :133-212
+  void Observe(int pktSize, int payloadSize, bool hasDD, bool activeUpdated, bool hasMask, u32 mask,
+               const DT *targets, int ntargets, const uint8_t *dtis, int ndtis) {
+    if (stopped || paused || payloadSize == 0 || !hasDD) return;
+    if (hasMask && activeUpdated) {
+      int ms = 0, mt = 0;
+      for (int k = 0; k < ntargets; k++)
+        if ((mask & (1u << targets[k].target)) != 0) {  // != DecodeTargetNotPresent (0)
+          if (ms < targets[k].s) ms = targets[k].s;
+          if (mt < targets[k].t) mt = targets[k].t;
+        }
+      if (ms > 2) ms = 2;
+      if (mt > 3) mt = 3;
+      const int old = maxS;
+      maxS = ms, maxT = mt;
+      if (old == -1) workerLive = true;  // go s.worker(s.generation.Inc())
+      if (old > maxS)
+        notify(maxS + 1, old, Stopped);
+      else if (old < maxS)
+        notify(old + 1, maxS, Active);
+    }
+    for (int k = 0; k < ntargets; k++) {
+      if (ndtis <= targets[k].target) continue;
+      if (dtis[targets[k].target] == 0) continue;  // DecodeTargetNotPresent
+      bytes[targets[k].s][targets[k].t] += pktSize;
+    }
+  }
+  // resetLocked :108-121
+  void resetLocked() {
+    workerLive = false;
+    for (int s = 0; s < 3; s++)
+      for (int t = 0; t < 4; t++) bytes[s][t] = bitrate[s][t] = 0;
+  }
+  // SetPaused :123-137
+  void SetPaused(bool p) {
+    if (paused == p) return;
+    paused = p;
+    if (!p)
+      resetLocked();
+    else
+      workerLive = true;
+  }
+  // Stop :57-68
+  void Stop() {
+    if (stopped) return;
+    stopped = true;
+    workerLive = false;
+  }
+  int Status(int layer) const { return layer > maxS ? Stopped : Active; }  // :84-93
+  void Cumulative(int layer, i64 out[4]) const {                            // :95-106 (not cumulative)
+    for (int t = 0; t < 4; t++) out[t] = layer > maxS ? 0 : bitrate[layer][t];
+  }
+  // bitrateReport :226-259, diff = the elapsed report interval (Duration.Seconds)
+  void bitrateReport(i64 elapsedNs) {
+    const double secs = double(elapsedNs / 1000000000LL) + double(elapsedNs % 1000000000LL) / 1e9;
+    bitrateChangedMask = 0;
+    for (int s = 0; s < 3; s++) {
+      bool changed = false;
+      for (int t = 0; t < 4; t++) {
+        const i64 br = i64(double(bytes[s][t] * 8) / secs);
+        if ((bitrate[s][t] == 0 && br > 0) || (bitrate[s][t] > 0 && br == 0)) changed = true;
+        bitrate[s][t] = br;
+        bytes[s][t] = 0;
+      }
+      if (changed) bitrateChangedMask |= 1u << s;
+    }
+  }
+  void Tick(i64 elapsedNs) {
+    bitrateChangedMask = 0;
+    if (workerLive && elapsedNs > 0) bitrateReport(elapsedNs);
+  }
+};
+
 }  // namespace orc_st

@@ -40,9 +40,9 @@ def test_struct_sizes(abi):
 #include <stdio.h>
 #include <stddef.h>
 #include "include/lkfwd.h"
-int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(lkf_tracker_status), sizeof(lkf_alloc_req), sizeof(lkf_allocation), sizeof(lkf_pad_req), sizeof(lkf_cfg), sizeof(lkf_track_params),
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(lkf_tracker_status), sizeof(lkf_alloc_req), sizeof(lkf_allocation), sizeof(lkf_pad_req), sizeof(lkf_cfg), sizeof(lkf_track_params),
  sizeof(lkf_downtrack_params), sizeof(lkf_pkt), sizeof(lkf_out), sizeof(lkf_fwd_state), sizeof(lkf_seq_meta),
- sizeof(lkf_pkt_dd), sizeof(lkf_stream_params), sizeof(lkf_dt_summary), sizeof(lkf_transport_params), sizeof(lkf_video_transition), sizeof(lkf_sender_stats), sizeof(lkf_prov_req), sizeof(lkf_prov_result), sizeof(lkf_alloc_group));return 0;}
+ sizeof(lkf_pkt_dd), sizeof(lkf_stream_params), sizeof(lkf_dt_summary), sizeof(lkf_transport_params), sizeof(lkf_video_transition), sizeof(lkf_sender_stats), sizeof(lkf_prov_req), sizeof(lkf_prov_result), sizeof(lkf_alloc_group), sizeof(lkf_dd_tracker_status));return 0;}
 '''
     exe = "/tmp/lkf_sizes"
     with open(exe + ".c", "w") as f:
@@ -53,7 +53,8 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %
           C.sizeof(abi.lkf_pkt), C.sizeof(abi.lkf_out), C.sizeof(abi.lkf_fwd_state), C.sizeof(abi.lkf_seq_meta),
           C.sizeof(abi.lkf_pkt_dd), C.sizeof(abi.lkf_stream_params), abi.DT_SUMMARY_DTYPE.itemsize,
           C.sizeof(abi.lkf_transport_params), abi.VIDEO_TRANSITION_DTYPE.itemsize, abi.SENDER_STATS_DTYPE.itemsize,
-          abi.PROV_REQ_DTYPE.itemsize, abi.PROV_RESULT_DTYPE.itemsize, abi.ALLOC_GROUP_DTYPE.itemsize]
+          abi.PROV_REQ_DTYPE.itemsize, abi.PROV_RESULT_DTYPE.itemsize, abi.ALLOC_GROUP_DTYPE.itemsize,
+          abi.DD_TRACKER_STATUS_DTYPE.itemsize]
     assert sizes == py, (sizes, py)
 
 

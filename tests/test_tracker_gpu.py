@@ -110,3 +110,45 @@ def test_frame_trackers_match_oracle(pkg, workload, cfg):
         eng.close()
         o.destroy(oh)
         tr.close()
+
+
+@pytest.mark.parametrize("cfg", [dict(config=5, rooms=4, svc_dd=1, seed=51), dict(config=5, rooms=6, svc_dd=-1, seed=52)])
+def test_dd_tracker_matches_oracle(pkg, workload, cfg):
+    """StreamTrackerDependencyDescriptor (streamtracker_dd.go) observed in
+    k_dd_decode per batch: every tick's max layers, notifications, statuses
+    and bitrates (with a pause, an unpause and a stop on the way) equal the
+    oracle's."""
+    from tests.test_dd_tracker_cpu import run_dd_trackers
+    o = load_oracle()
+    abi = pkg.abi
+    kw = dict(cfg)
+    tr = workload.Trace(kw.pop("config"), duration_s=5.0, batch_s=1.0, **kw)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+
+        def run_eng(b):
+            workload.queue_events(eng.api, eng.h, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            eng.submit(pk, n, ar, alen, tr.batch_dd(b)[0])
+            eng.run()
+            eng.sync()
+
+        def run_orc(b):
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(oh, pk, n, ar, alen, tr.batch_dd(b)[0])
+
+        g = run_dd_trackers(pkg, workload, eng.api, eng.h, tr, run_eng, abi)
+        r = run_dd_trackers(pkg, workload, o.api, oh, tr, run_orc, abi)
+        for b, (x, y) in enumerate(zip(g, r)):
+            for f in abi.DD_TRACKER_STATUS_DTYPE.names:
+                if f != "reserved":
+                    assert np.array_equal(x[f], y[f]), (b, f, x[f], y[f])
+        assert (r[0]["bitrate"][:, 0, 0] > 0).all()
+    finally:
+        eng.close()
+        o.destroy(oh)
+        tr.close()
