@@ -78,6 +78,7 @@ struct BatchCtx {
   uint64_t evCap = 0, evOffCap = 0, evLaneCap = 0;
   hipEvent_t prepped = nullptr;  // prep stage done (prep stream)
   hipEvent_t decided = nullptr;  // decide stage done (decide stream)
+  hipEvent_t sent = nullptr;     // sender statistics done (sender stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
   bool used = false;
   // SRTP-protected copy of the output (lkf_protect; allocated on first use)
@@ -109,6 +110,7 @@ struct lkf_engine {
   hipStream_t prepS = nullptr;  // ingest + batch preparation (high priority)
   hipStream_t decS = nullptr;   // decide stage (high priority)
   hipStream_t emitS = nullptr;  // emit stage (low priority)
+  hipStream_t sendS = nullptr;  // sender statistics of a decided batch (low priority, beside its emit)
   hipStream_t cur = nullptr;    // caller's stream of the last lkf_run
   hipEvent_t inEv = nullptr;    // caller-stream work before a run
   lkf_cfg cfg{};
@@ -439,6 +441,7 @@ static int drain_streams(lkf_engine *e) {
   HIPCHK(hipStreamSynchronize(e->prepS), "sync prep stream");
   HIPCHK(hipStreamSynchronize(e->decS), "sync decide stream");
   HIPCHK(hipStreamSynchronize(e->emitS), "sync emit stream");
+  if (e->sendS) HIPCHK(hipStreamSynchronize(e->sendS), "sync sender stream");
   return LKF_OK;
 }
 
@@ -677,10 +680,12 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(hipExtStreamCreateWithCUMask(&e->decS, words, mA.data()));
     A(hipExtStreamCreateWithCUMask(&e->prepS, words, mA.data()));
     A(hipExtStreamCreateWithCUMask(&e->emitS, words, mB.data()));
+    A(hipExtStreamCreateWithCUMask(&e->sendS, words, mB.data()));
   } else {
     A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
     A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
     A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
+    A(hipStreamCreateWithPriority(&e->sendS, hipStreamNonBlocking, leastPrio));
   }
   A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
   e->cur = e->own;
@@ -734,6 +739,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(hipEventCreateWithFlags(&x.decided, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.prepped, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.emitted, hipEventDisableTiming));
+    A(hipEventCreateWithFlags(&x.sent, hipEventDisableTiming));
   }
   for (auto &r : e->ring)
     for (auto &ev : r) A(hipEventCreate(&ev));
@@ -875,6 +881,7 @@ void lkf_destroy(lkf_engine *e) {
     if (x.decided) (void)hipEventDestroy(x.decided);
     if (x.prepped) (void)hipEventDestroy(x.prepped);
     if (x.emitted) (void)hipEventDestroy(x.emitted);
+    if (x.sent) (void)hipEventDestroy(x.sent);
   }
   for (auto &r : e->ring)
     for (auto &ev : r)
@@ -888,6 +895,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->bounce) (void)hipHostFree(e->bounce);
   if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
+  if (e->sendS) (void)hipStreamDestroy(e->sendS);
   if (e->decS) (void)hipStreamDestroy(e->decS);
   if (e->prepS) (void)hipStreamDestroy(e->prepS);
   if (e->own) (void)hipStreamDestroy(e->own);
@@ -1498,8 +1506,10 @@ int lkf_run(lkf_engine *e, void *stream) {
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum, x.dErr, e->dSticky), "accumulate");
-  {  // sendingPacket -> RTPStatsSender.Update per forwarded tuple (off the
-     // decide path: the next batch's decide runs beside it)
+  {  // sendingPacket -> RTPStatsSender.Update per forwarded tuple: on its own
+     // stream from the decided tuples, beside this batch's emit and the next
+     // decide; the emit stream waits for it before the context counts as done
+    HIPCHK(hipStreamWaitEvent(e->sendS, x.decided, 0), "wait decided (sender)");
     SenderLaunch sl;
     sl.tuples = x.dTuples;
     sl.slotBase = x.dSlotBase;
@@ -1509,7 +1519,9 @@ int lkf_run(lkf_engine *e, void *stream) {
     sl.ring = e->dSSRing;
     sl.gap = e->dSSGap;
     sl.ndts = nd;
-    HIPCHK(launch_sender_stats(e->emitS, sl), "sender stats");
+    HIPCHK(launch_sender_stats(e->sendS, sl), "sender stats");
+    HIPCHK(hipEventRecord(x.sent, e->sendS), "event");
+    HIPCHK(hipStreamWaitEvent(e->emitS, x.sent, 0), "wait sender stats");
   }
   HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
   if (e->hostProf && e->nRuns >= 3) {  // steady state: skip the first runs (initial control ops, first touch)

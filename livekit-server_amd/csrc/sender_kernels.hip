@@ -144,6 +144,10 @@ __device__ __forceinline__ u64 scan_max64(u64 v) {
   }
   return v;
 }
+__device__ __forceinline__ u32 wave_sum32(u32 v) {
+  for (int d = 32; d >= 1; d >>= 1) v += u32(__shfl_xor(int(v), d, 64));
+  return v;
+}
 __device__ __forceinline__ u64 wave_sum64(u64 v) {
   for (int d = 32; d >= 1; d >>= 1) {
     const u32 lo = u32(__shfl_xor(int(u32(v)), d, 64)), hi = u32(__shfl_xor(int(u32(v >> 32)), d, 64));
@@ -210,9 +214,10 @@ __global__ void __launch_bounds__(64) k_sender_stats(SenderLaunch A) {
       // ---- the in-order segment starting at pos
       const bool inSeg = valid && lane >= pos;
       const u64 high0 = sS.extHighestSN;
-      const u64 pm = scan_max64(inSeg ? esn : 0ull);  // max esn over [pos, lane]
-      const u64 pmEx = shfl_up64(pm, 1);             // ... over [pos, lane)
-      const u64 prev = (lane > pos && pmEx > high0) ? pmEx : high0;
+      // in a run where every SN exceeds the one before it, the highest SN
+      // before a lane is its predecessor's; the first lane breaking that ends the run
+      const u64 prevLane = shfl_up64(esn, 1);
+      const u64 prev = lane > pos ? prevLane : high0;
       const u64 g = esn - prev;
       const bool ok = inSeg && sS.initialized && pay > 0 && i64(esn - prev) > 0 && g <= 64 && ets >= sS.extStartTS;
       const u64 badM = __ballot(inSeg && !ok);
@@ -228,14 +233,20 @@ __global__ void __launch_bounds__(64) k_sender_stats(SenderLaunch A) {
           const u64 pk = u64(hdr + pay);
           ring[esn & kSnMask] = u32(u16(pk)) | (u32(u8(hdr)) << 16) | ((marker ? kFlagMarker : 0u) << 24);
         }
-        // highest timestamp: the lanes whose ets exceeds every earlier one
+        // highest timestamp: the lanes whose ets exceeds every earlier one (a
+        // prefix max, unless the run's timestamps never decrease)
         const u64 h0 = sS.extHighestTS;
-        const u64 tm = scan_max64(act ? ets : 0ull);
-        const u64 tmEx = shfl_up64(tm, 1);
-        const u64 before = (lane > pos && tmEx > h0) ? tmEx : h0;
+        const u64 prevEts = shfl_up64(ets, 1);
+        u64 before = lane > pos ? prevEts : h0;
+        if (__ballot(act && lane > pos && ets < prevEts)) {
+          const u64 tm = scan_max64(act ? ets : 0ull);
+          const u64 tmEx = shfl_up64(tm, 1);
+          before = (lane > pos && tmEx > h0) ? tmEx : h0;
+        } else if (lane > pos && h0 > before) {
+          before = h0;
+        }
         const u64 upM = __ballot(act && ets > before);
         // jitter over the segment's new frames (ets differs from the previous packet's)
-        const u64 prevEts = shfl_up64(ets, 1);
         const bool isNew = act && ets != (lane > pos ? prevEts : sS.lastJitterExtTimestamp);
         const u64 newM = __ballot(isNew);
         const i64 since = i64(u64(t) - u64(sS.firstTime));
@@ -253,9 +264,10 @@ __global__ void __launch_bounds__(64) k_sender_stats(SenderLaunch A) {
           sPT[lane] = prevTransit != 0;
           sTr[lane] = transit;
         }
-        const u64 sumB = wave_sum64(act ? u64(hdr + pay) : 0ull), sumH = wave_sum64(act ? u64(hdr) : 0ull);
+        // (a run of <= 64 packets: the byte, header and loss sums fit 32 bits)
+        const u64 sumB = wave_sum32(act ? hdr + pay : 0u), sumH = wave_sum32(act ? hdr : 0u);
         const u32 frames = u32(__popcll(__ballot(act && marker))), kfs = u32(__popcll(__ballot(act && kf)));
-        const u64 lost = wave_sum64((act && g >= 2) ? g - 1 : 0ull);
+        const u64 lost = wave_sum32((act && g >= 2) ? u32(g - 1) : 0u);
         __threadfence_block();
         __syncthreads();
         if (lane == 0) {  // the serial jitter filter over the new frames, then the segment's totals
