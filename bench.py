@@ -170,6 +170,8 @@ def main():
     ap.add_argument("--srtp", action="store_true",
                     help="step = forward + SRTP protect (lkf_protect: abs-send-time + AES_CM_128_HMAC_SHA1_80 "
                          "per subscriber transport, every DownTrack bound)")
+    ap.add_argument("--srtp-profile", choices=["aes_cm", "gcm"], default="aes_cm",
+                    help="with --srtp: SRTP_AES128_CM_HMAC_SHA1_80 or SRTP_AEAD_AES_128_GCM transports")
     args = ap.parse_args()
     if not args.rooms:
         args.rooms = CONFIGS[args.config]["rooms"]
@@ -216,8 +218,11 @@ def main():
         for d in range(trace.ndts):
             k = (int(trace.tracks[trace.downtracks[d].track].room), int(trace.downtracks[d].subscriber))
             if k not in tps:
+                gcm = args.srtp_profile == "gcm"
                 tps[k] = eng.api["add_transport"](eng.h, C.byref(pkg.transport_params(
-                    rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 14, dtype=np.uint8).tobytes())))
+                    rng.integers(0, 256, 16, dtype=np.uint8).tobytes(),
+                    rng.integers(0, 256, 12 if gcm else 14, dtype=np.uint8).tobytes(),
+                    pkg.abi.LKF_SRTP_AEAD_AES_128_GCM if gcm else pkg.abi.LKF_SRTP_AES128_CM_HMAC_SHA1_80)))
                 assert tps[k] >= 0
             assert eng.api["set_downtrack_transport"](eng.h, d, tps[k]) == 0
 
@@ -459,9 +464,10 @@ def main():
                                "drained_records": drained[0], "records_forwarded": fwd,
                                "pcie_GBps_both_ways": round((h2d + drained[0] * 40 + drained[1]) / elapsed / 1e9, 2)}
         if args.srtp:  # the protect stage: VALU/LDS-bound crypto, reported against HBM for the record
-            prot_bytes = cum["out_bytes"] * 2 + 10 * fwd + 40 * fwd
+            tag = 16 if args.srtp_profile == "gcm" else 10
+            prot_bytes = cum["out_bytes"] * 2 + tag * fwd + 40 * fwd
             pa = prot_bytes / args.steps / (prot_ms / 1e3 / args.steps) / 1e9 if prot_ms else 0.0
-            line["srtp"] = {"profile": "SRTP_AES128_CM_HMAC_SHA1_80", "protected_per_step": fwd // args.steps,
+            line["srtp"] = {"profile": "SRTP_AEAD_AES_128_GCM" if tag == 16 else "SRTP_AES128_CM_HMAC_SHA1_80", "protected_per_step": fwd // args.steps,
                             "protect_ms_per_step": round(prot_ms / args.steps, 4),
                             "protected_pkts_per_s_kernel": round(fwd / (prot_ms / 1e3), 1) if prot_ms else None,
                             "algorithmic_bytes_per_launch": int(prot_bytes // args.steps),

@@ -764,6 +764,10 @@ int lkf_allocate_all(lkf_engine *e, const lkf_alloc_group *groups, uint32_t ngro
  * PeerConnection's DTLS-SRTP context (its exported master key and salt); its
  * DownTracks are its SSRCs. */
 #define LKF_SRTP_AES128_CM_HMAC_SHA1_80 1
+/* AEAD_AES_128_GCM (RFC 7714; pion srtp_cipher_aead_aes_gcm.go): 12-byte
+ * master salt (master_salt[0..11]), IV = (0^16 || SSRC || ROC || SEQ) XOR the
+ * session salt, AAD = the RTP header, a 16-byte tag after the ciphertext */
+#define LKF_SRTP_AEAD_AES_128_GCM 2
 typedef struct lkf_transport_params {
   uint8_t master_key[16];
   uint8_t master_salt[14];
@@ -778,8 +782,8 @@ int lkf_set_downtrack_transport(lkf_engine *e, int32_t dt, int32_t transport);
  * every packet gets the abs-send-time of `send_time_ns` (unix ns, pion/rtp
  * NewAbsSendTimeExtension) in its abs-send-time element, and the packets of a
  * bound DownTrack are SRTP-protected.  Record i's packet is at
- * out_off + 16 * i of the protected arena, out_len (+ 10 with a transport)
- * bytes long.  Valid until the run after next is enqueued, like the output. */
+ * out_off + 16 * i of the protected arena, out_len (+ 10 with an AES-CM
+ * transport, + 16 with GCM) bytes long.  Valid until the run after next is enqueued, like the output. */
 int lkf_protect(lkf_engine *e, int64_t send_time_ns);
 int lkf_output_protected_device(lkf_engine *e, const uint8_t **d_arena, uint64_t *arena_len);
 int lkf_drain_protected(lkf_engine *e, uint8_t *arena, uint64_t cap, uint64_t *arena_len);

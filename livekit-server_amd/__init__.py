@@ -98,10 +98,11 @@ def drain_arrays(api, h, nmax=None):
 
 
 def transport_params(master_key, master_salt, profile=abi.LKF_SRTP_AES128_CM_HMAC_SHA1_80):
-    """lkf_transport_params from 16 + 14 key bytes (a DTLS-SRTP export)."""
+    """lkf_transport_params from a DTLS-SRTP export: 16 key bytes and 14 salt
+    bytes (12 for AEAD_AES_128_GCM)."""
     t = abi.lkf_transport_params()
     C.memmove(t.master_key, bytes(master_key), 16)
-    C.memmove(t.master_salt, bytes(master_salt), 14)
+    C.memmove(t.master_salt, bytes(master_salt), len(master_salt))
     t.profile = profile
     return t
 

@@ -312,6 +312,7 @@ class lkf_transport_params(C.Structure):
 
 
 LKF_SRTP_AES128_CM_HMAC_SHA1_80 = 1
+LKF_SRTP_AEAD_AES_128_GCM = 2
 SRTP_TAG_LEN = 10
 
 

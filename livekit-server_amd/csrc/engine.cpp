@@ -1693,7 +1693,8 @@ static int srtp_init(lkf_engine *e) {
 }
 
 int32_t lkf_add_transport(lkf_engine *e, const lkf_transport_params *p) {
-  if (!e || !p || p->profile != LKF_SRTP_AES128_CM_HMAC_SHA1_80) return LKF_EINVAL;
+  if (!e || !p || (p->profile != LKF_SRTP_AES128_CM_HMAC_SHA1_80 && p->profile != LKF_SRTP_AEAD_AES_128_GCM))
+    return LKF_EINVAL;
   int rc = srtp_init(e);
   if (rc) return rc;
   const uint32_t t = uint32_t(e->transports.size());

@@ -176,8 +176,9 @@ __global__ void k_srtp_keys(const lkf_transport_params *__restrict__ in, u32 fir
   aes_expand(t, mk, mrk);
   // PRF input: master salt (14 B) with the label XORed into byte 7, then a
   // 16-bit block counter (pion key_derivation.go aesCmKeyDerivation)
+  const bool gcm = p.profile == LKF_SRTP_AEAD_AES_128_GCM;  // 12-byte master salt
   u8 ms[16] = {0};
-  for (int k = 0; k < 14; k++) ms[k] = p.master_salt[k];
+  for (int k = 0; k < (gcm ? 12 : 14); k++) ms[k] = p.master_salt[k];
   u32 prf[4];
   auto derive = [&](u32 label, u32 ctr, u32 out[4]) {
     for (int k = 0; k < 4; k++) prf[k] = be32(ms + 4 * k);
@@ -202,6 +203,18 @@ __global__ void k_srtp_keys(const lkf_transport_params *__restrict__ in, u32 fir
   K.salt[1] = sl[1];
   K.salt[2] = sl[2];
   K.salt[3] = sl[3] & 0xFFFF0000u;  // 14-byte salt
+  K.profile = p.profile;
+  if (gcm) {  // newSrtpCipherAeadAesGcm: 12-byte session salt, GHASH key H = E(K, 0^128)
+    K.salt[3] = 0;
+    u32 h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    aes_encrypt(t, rk, h0, h1, h2, h3);
+    K.ih[0] = h0;
+    K.ih[1] = h1;
+    K.ih[2] = h2;
+    K.ih[3] = h3;
+    K.ih[4] = 0;
+    return;
+  }
   // HMAC-SHA1 with the 20-byte auth key: midstates after the ipad / opad blocks
   const u32 ak[5] = {a0[0], a0[1], a0[2], a0[3], a1[0]};
   u32 w[16], hi[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
@@ -214,7 +227,6 @@ __global__ void k_srtp_keys(const lkf_transport_params *__restrict__ in, u32 fir
     K.ih[k] = hi[k];
     K.oh[k] = ho[k];
   }
-  K.profile = p.profile;
 }
 
 // ---- rollover bases -----------------------------------------------------------
@@ -252,6 +264,118 @@ struct AesLds {
   __device__ __forceinline__ u32 T3(u32 x) const { return ror32(T0(x), 24); }
   __device__ __forceinline__ u32 S(u32 x) const { return (T0(x) >> 16) & 255; }
 };
+
+// GHASH multiply Y <- Y * H in GF(2^128) (NIST SP 800-38D §6.3: bit 0 = the
+// most significant bit of byte 0; big-endian words), bit-serial
+__device__ __forceinline__ void gf_mul(u32 y[4], const u32 h[4]) {
+  u32 z0 = 0, z1 = 0, z2 = 0, z3 = 0, v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const u32 x = y[w];
+    for (int b = 31; b >= 0; b--) {
+      const u32 m = 0u - ((x >> b) & 1u);
+      z0 ^= v0 & m;
+      z1 ^= v1 & m;
+      z2 ^= v2 & m;
+      z3 ^= v3 & m;
+      const u32 r = 0xE1000000u & (0u - (v3 & 1u));
+      v3 = (v3 >> 1) | (v2 << 31);
+      v2 = (v2 >> 1) | (v1 << 31);
+      v1 = (v1 >> 1) | (v0 << 31);
+      v0 = (v0 >> 1) ^ r;
+    }
+  }
+  y[0] = z0, y[1] = z1, y[2] = z2, y[3] = z3;
+}
+__device__ __forceinline__ void ghash_block(u32 y[4], const u32 h[4], u32 b0, u32 b1, u32 b2, u32 b3) {
+  y[0] ^= b0, y[1] ^= b1, y[2] ^= b2, y[3] ^= b3;
+  gf_mul(y, h);
+}
+
+// AEAD_AES_128_GCM (RFC 7714 §8, pion srtpCipherAeadAesGcm.encryptRTP) of one
+// record: IV = (0^16 || SSRC || ROC || SEQ) XOR salt, counter blocks IV || 2,
+// 3, ..; pass 1 writes the header (abs-send-time stamped) and the ciphertext in
+// whole 16-B chunks (one new keystream block per chunk: the window is offset
+// from the chunk by the header length, a whole number of words); pass 2 runs
+// GHASH over the header (AAD) and the ciphertext read back from the output,
+// then the 16-byte tag E(K, J0) ^ GHASH after the ciphertext.
+template <class Tab>
+__device__ void protect_gcm(const Tab &tb, const SrtpKeys *K, const uint4 *src, uint4 *dst, u32 len, u32 hw,
+                            u32 absPos, u32 absVal, u32 ssrc, u32 seq, u32 roc) {
+  u32 rk[44];
+#pragma unroll
+  for (int k = 0; k < 11; k++) {
+    const uint4 q = reinterpret_cast<const uint4 *>(K->rk)[k];
+    rk[4 * k] = q.x, rk[4 * k + 1] = q.y, rk[4 * k + 2] = q.z, rk[4 * k + 3] = q.w;
+  }
+  const u32 iv0 = (ssrc >> 16) ^ K->salt[0], iv1 = ((ssrc << 16) | (roc >> 16)) ^ K->salt[1],
+            iv2 = ((roc << 16) | seq) ^ K->salt[2];
+  const u32 ch0 = (hw + 3) >> 2, sft = 4 * ch0 - hw;
+  u32 win[8];
+  auto ks = [&](int q, u32 *o) {
+    u32 a0 = iv0, a1 = iv1, a2 = iv2, a3 = u32(2 + q);
+    aes_encrypt(tb, rk, a0, a1, a2, a3);
+    o[0] = a0, o[1] = a1, o[2] = a2, o[3] = a3;
+  };
+  ks(-int(ch0), win);
+  ks(1 - int(ch0), win + 4);
+  const u32 nch = (len + 15) / 16;
+  for (u32 c = 0; c < nch; c++) {
+    if (c) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) win[k] = win[4 + k];
+      ks(int(c) + 1 - int(ch0), win + 4);
+    }
+    uint4 ch = src[c];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      u32 &v = j == 0 ? ch.x : j == 1 ? ch.y : j == 2 ? ch.z : ch.w;
+      const u32 w = 4 * c + u32(j);
+      if (w < hw) {  // header word: abs-send-time stamped
+        for (u32 k = 0; k < 3; k++) {
+          const u32 pos = absPos + k;
+          if (pos / 4 == w) {
+            const u32 sh = 8 * (pos & 3);
+            v = (v & ~(255u << sh)) | (((absVal >> (16 - 8 * k)) & 255) << sh);
+          }
+        }
+      } else {
+        const u32 kw = sft + u32(j);
+        v ^= bswap(kw == 0 ? win[0] : kw == 1 ? win[1] : kw == 2 ? win[2] : kw == 3 ? win[3] : kw == 4 ? win[4]
+                                                                                                 : kw == 5 ? win[5] : win[6]);
+      }
+    }
+    dst[c] = ch;
+  }
+  // GHASH(H, A = header, C)
+  const u32 H[4] = {K->ih[0], K->ih[1], K->ih[2], K->ih[3]};
+  const u32 *ow = reinterpret_cast<const u32 *>(dst);
+  u32 y[4] = {0, 0, 0, 0};
+  for (u32 b = 0; 4 * b < hw; b++) {
+    u32 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) x[j] = (4 * b + j < hw) ? bswap(ow[4 * b + j]) : 0u;
+    ghash_block(y, H, x[0], x[1], x[2], x[3]);
+  }
+  const u32 lc = len - 4 * hw;  // ciphertext bytes
+  for (u32 b = 0; 16 * b < lc; b++) {
+    u32 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int left = int(lc) - int(16 * b + 4 * j);  // bytes of this word inside the ciphertext
+      const u32 v = left > 0 ? bswap(ow[hw + 4 * b + j]) : 0u;
+      x[j] = left >= 4 ? v : left > 0 ? (v & (0xFFFFFFFFu << (8 * (4 - left)))) : 0u;
+    }
+    ghash_block(y, H, x[0], x[1], x[2], x[3]);
+  }
+  ghash_block(y, H, 0u, 32u * hw, 0u, 8u * lc);  // len(A) || len(C) in bits
+  u32 e0 = iv0, e1 = iv1, e2 = iv2, e3 = 1u;     // E(K, J0)
+  aes_encrypt(tb, rk, e0, e1, e2, e3);
+  const u32 t[4] = {e0 ^ y[0], e1 ^ y[1], e2 ^ y[2], e3 ^ y[3]};
+  u8 *tag = reinterpret_cast<u8 *>(dst) + len;
+#pragma unroll
+  for (int k = 0; k < 16; k++) tag[k] = u8(t[k / 4] >> (24 - 8 * (k & 3)));
+}
 
 __global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
   __shared__ u32 sTe[256 * 32];
@@ -313,6 +437,11 @@ __global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
   u32 roc = 0, ctr0 = 0, ctr1 = 0, ctr2 = 0, ctr3 = 0;
   u32 hs[5] = {0, 0, 0, 0, 0};
   const SrtpKeys *K = prot ? A.keys + (s.tp1 - 1) : A.keys;
+  if (prot && K->profile == LKF_SRTP_AEAD_AES_128_GCM) {
+    protect_gcm(tb, K, src, dst, len, hw, absPos, A.absVal, bswap(c0v.z), bswap(w0) & 0xFFFF,
+                u32((r.ext_sn >> 16) - s.rocBase));
+    return;
+  }
   if (prot) {
 #pragma unroll
     for (int k = 0; k < 11; k++) {

@@ -114,6 +114,7 @@ struct orc_engine {
   std::vector<lkf_pkt_dd> pendingDD;
   // SRTP sessions (one per transport) and the last protected output
   std::vector<orc_srtp::Session> transports;
+  std::vector<std::unique_ptr<orc_srtp::SessionGcm>> transportsGcm;  // (null: AES-CM transport)
   std::vector<u8> protArena;
   // RED: per source track (lkf_red_encode / lkf_red_decode)
   std::map<u32, orc_red::RedEncoder> redEnc;
@@ -522,8 +523,12 @@ int orc_drain(orc_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_
 // ---- SRTP protect: pacer writeRTPHeaderExtensions (abs-send-time,
 // pacer/base.go:71-100) then WriteStream.WriteRTP -> pion/srtp EncryptRTP
 int32_t orc_add_transport(orc_engine *e, const lkf_transport_params *p) {
-  if (!p || p->profile != LKF_SRTP_AES128_CM_HMAC_SHA1_80) return LKF_EINVAL;
+  if (!p || (p->profile != LKF_SRTP_AES128_CM_HMAC_SHA1_80 && p->profile != LKF_SRTP_AEAD_AES_128_GCM))
+    return LKF_EINVAL;
   e->transports.emplace_back(p->master_key, p->master_salt);
+  e->transportsGcm.emplace_back(p->profile == LKF_SRTP_AEAD_AES_128_GCM
+                                    ? std::make_unique<orc_srtp::SessionGcm>(p->master_key, p->master_salt)
+                                    : nullptr);
   return int32_t(e->transports.size() - 1);
 }
 
@@ -543,7 +548,10 @@ int orc_protect(orc_engine *e, int64_t send_time_ns) {
     ODT &d = *e->dts[r.dt];
     std::vector<u8> pkt(e->outArena.begin() + long(r.out_off), e->outArena.begin() + long(r.out_off + r.out_len));
     orc_srtp::set_abs_send_time(pkt, d.p.ext_abs_send_time, abs);
-    if (d.transport >= 0) pkt = orc_srtp::protect(e->transports[size_t(d.transport)], d.srtp, pkt);
+    if (d.transport >= 0)
+      pkt = e->transportsGcm[size_t(d.transport)]
+                ? orc_srtp::protect_gcm(*e->transportsGcm[size_t(d.transport)], d.srtp, pkt)
+                : orc_srtp::protect(e->transports[size_t(d.transport)], d.srtp, pkt);
     std::memcpy(e->protArena.data() + r.out_off + 16 * i, pkt.data(), pkt.size());
   }
   return LKF_OK;

@@ -198,11 +198,11 @@ inline std::array<u8, 20> hmac_sha1(const u8 *key, size_t klen, const u8 *msg, s
 // ---- pion/srtp v2.0.18 ------------------------------------------------------
 // key_derivation.go aesCmKeyDerivation (indexOverKdr == 0): PRF input = master
 // salt with the label XORed into byte 7, the last two bytes a block counter.
-inline std::vector<u8> kdf(u8 label, const u8 mk[16], const u8 ms[14], size_t outLen) {
+inline std::vector<u8> kdf(u8 label, const u8 mk[16], const u8 *ms, size_t outLen, size_t saltLen = 14) {
   Aes128 a(mk);
   std::vector<u8> out;
   u8 in[16] = {0};
-  std::memcpy(in, ms, 14);
+  std::memcpy(in, ms, saltLen);
   in[7] ^= label;
   for (u16 i = 0; out.size() < outLen; i++) {
     in[14] = u8(i >> 8);
@@ -308,6 +308,100 @@ inline std::vector<u8> protect(const Session &s, SSRCState &st, const std::vecto
   for (int i = 0; i < 4; i++) m.push_back(u8(roc >> (24 - 8 * i)));
   const auto tag = hmac_sha1(s.auth, 20, m.data(), m.size());
   out.insert(out.end(), tag.begin(), tag.begin() + 10);
+  return out;
+}
+
+// ---- AEAD_AES_128_GCM (RFC 7714; pion srtp_cipher_aead_aes_gcm.go) --------
+// GCM per NIST SP 800-38D: GHASH over GF(2^128) with the bit-reflected
+// convention (bit 0 = the most significant bit of byte 0), R = 11100001 || 0^120
+inline void gf_mul(const u8 X[16], const u8 Y[16], u8 out[16]) {
+  u8 Z[16] = {0}, V[16];
+  std::memcpy(V, Y, 16);
+  for (int i = 0; i < 128; i++) {
+    if (X[i / 8] & (0x80 >> (i % 8)))
+      for (int k = 0; k < 16; k++) Z[k] ^= V[k];
+    const bool lsb = V[15] & 1;
+    for (int k = 15; k > 0; k--) V[k] = u8((V[k] >> 1) | (V[k - 1] << 7));
+    V[0] >>= 1;
+    if (lsb) V[0] ^= 0xE1;
+  }
+  std::memcpy(out, Z, 16);
+}
+inline void ghash_update(const u8 H[16], u8 Y[16], const u8 *data, size_t n) {  // zero-padded 16-B blocks
+  for (size_t off = 0; off < n; off += 16) {
+    u8 b[16] = {0};
+    std::memcpy(b, data + off, std::min<size_t>(16, n - off));
+    for (int k = 0; k < 16; k++) Y[k] ^= b[k];
+    gf_mul(Y, H, Y);
+  }
+}
+// GCM-AE(K, IV (96 bits), P, A) -> C || T (128-bit tag)
+inline std::vector<u8> gcm_seal(const u8 key[16], const u8 iv[12], const u8 *p, size_t np, const u8 *a, size_t na) {
+  Aes128 c(key);
+  u8 H[16] = {0}, J0[16];
+  c.encrypt(H, H);
+  std::memcpy(J0, iv, 12);
+  J0[12] = J0[13] = J0[14] = 0;
+  J0[15] = 1;
+  std::vector<u8> out(np + 16);
+  u8 ctr[16];
+  std::memcpy(ctr, J0, 16);
+  for (size_t off = 0; off < np; off += 16) {
+    for (int i = 15; i >= 12; i--)  // inc32
+      if (++ctr[i] != 0) break;
+    u8 ks[16];
+    c.encrypt(ctr, ks);
+    for (size_t j = 0; j < 16 && off + j < np; j++) out[off + j] = p[off + j] ^ ks[j];
+  }
+  u8 Y[16] = {0};
+  ghash_update(H, Y, a, na);
+  ghash_update(H, Y, out.data(), np);
+  u8 L[16];
+  const u64 la = u64(na) * 8, lc = u64(np) * 8;
+  for (int i = 0; i < 8; i++) {
+    L[i] = u8(la >> (56 - 8 * i));
+    L[8 + i] = u8(lc >> (56 - 8 * i));
+  }
+  ghash_update(H, Y, L, 16);
+  u8 E[16];
+  c.encrypt(J0, E);
+  for (int k = 0; k < 16; k++) out[np + k] = E[k] ^ Y[k];
+  return out;
+}
+// newSrtpCipherAeadAesGcm: session key and 12-byte session salt from the
+// AES-CM PRF over the 12-byte master salt (labels 0 and 2)
+struct SessionGcm {
+  u8 key[16];
+  u8 salt[12];
+  SessionGcm(const u8 mk[16], const u8 ms[12]) {
+    auto k = kdf(0x00, mk, ms, 16, 12), sl = kdf(0x02, mk, ms, 12, 12);
+    std::memcpy(key, k.data(), 16);
+    std::memcpy(salt, sl.data(), 12);
+  }
+};
+// srtpCipherAeadAesGcm.encryptRTP: IV = (0^16 || SSRC || ROC || SEQ) XOR salt
+// (RFC 7714 §8.1), AAD = the RTP header (extensions included), output =
+// header || GCM ciphertext || 16-byte tag; the rollover guess as for AES-CM
+inline std::vector<u8> protect_gcm(const SessionGcm &s, SSRCState &st, const std::vector<u8> &pkt) {
+  const size_t cc = pkt[0] & 0x0f;
+  size_t h = 12 + 4 * cc;
+  if (pkt[0] & 0x10) h += 4 + 4 * ((size_t(pkt[h + 2]) << 8) | pkt[h + 3]);
+  const u16 seq = u16((pkt[2] << 8) | pkt[3]);
+  u32 roc;
+  int32_t diff;
+  st.next(seq, roc, diff);
+  st.update(seq, diff);
+  u8 iv[12] = {0};
+  for (int i = 0; i < 4; i++) {
+    iv[2 + i] = pkt[8 + size_t(i)];
+    iv[6 + i] = u8(roc >> (24 - 8 * i));
+  }
+  iv[10] = u8(seq >> 8);
+  iv[11] = u8(seq);
+  for (int i = 0; i < 12; i++) iv[i] ^= s.salt[i];
+  std::vector<u8> out(pkt.begin(), pkt.begin() + long(h));
+  const auto ct = gcm_seal(s.key, iv, pkt.data() + h, pkt.size() - h, pkt.data(), h);
+  out.insert(out.end(), ct.begin(), ct.end());
   return out;
 }
 

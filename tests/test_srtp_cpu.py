@@ -1,6 +1,7 @@
 """SRTP protect on the CPU oracle (oracle/srtp_oracle.h), checked against an
 independent RFC 3711 composition of OpenSSL's AES-128 and Python's HMAC-SHA1
-(tests/srtp_lib.py): every forwarded packet of a configs[1] trace, with one
+(tests/srtp_lib.py), and its AEAD_AES_128_GCM protect against OpenSSL's
+AES-128-GCM: every forwarded packet of a configs[1] trace, with one
 transport per (room, subscriber), some DownTracks unbound, over several
 batches (rollover state carried across batches)."""
 import importlib
@@ -14,12 +15,12 @@ from tests.oracle_lib import load as load_oracle
 EPOCH = 1700000000 * 10**9
 
 
-def _run(o, workload, tr, nb, check):
+def _run(o, workload, tr, nb, check, gcm_every=0):
     pkg = importlib.import_module("livekit-server_amd")
     h = o.create(500)
     try:
         workload.load_topology(o.api, h, tr)
-        tmap = srtp_lib.bind_transports(pkg, o.api, h, tr, seed=5)
+        tmap = srtp_lib.bind_transports(pkg, o.api, h, tr, seed=5, gcm_every=gcm_every)
         ck = srtp_lib.Checker(tr, tmap)
         n_prot = n_plain = 0
         for b in range(nb):
@@ -58,3 +59,11 @@ def test_oracle_srtp_small_batches(workload):
     tr = workload.Trace(1, duration_s=1.0, batch_s=0.05, rooms=1, seed=4)
     n_prot, n_plain, _ = _run(load_oracle(), workload, tr, tr.nbatches, check="all")
     assert n_prot > 100
+
+
+def test_oracle_srtp_gcm_matches_openssl(workload):
+    """AEAD_AES_128_GCM transports (every second one) beside AES-CM ones,
+    against OpenSSL's AES-128-GCM (rollover counters included)."""
+    tr = workload.Trace(2, duration_s=4.0, batch_s=1.0, rooms=2, seed=5)
+    n_prot, n_plain, n_roc = _run(load_oracle(), workload, tr, tr.nbatches, check=3, gcm_every=2)
+    assert n_prot > 1000 and n_plain > 100 and n_roc > 50

@@ -3,7 +3,8 @@
 The same batches, transports (one per (room, subscriber), every seventh
 DownTrack unbound) and send times on both; every protected packet — header
 with its abs-send-time stamped, AES-CM ciphertext, HMAC-SHA1 tag — must be
-identical, over several batches (rollover bases carried; seed 5 has DownTracks
+identical (AES-CM ciphertext and HMAC-SHA1 tag, or AEAD_AES_128_GCM
+ciphertext and GCM tag for the GCM transports), over several batches (rollover bases carried; seed 5 has DownTracks
 whose munged sequence numbers wrap), with a pipelined variant that protects
 each run before the previous one has been drained."""
 import numpy as np
@@ -30,7 +31,8 @@ def _compare(pkg, eng, o, oh, b, bound):
     for i in range(len(orec)):
         r = orec[i]
         off = int(r["out_off"]) + 16 * i
-        ln = int(r["out_len"]) + (10 if int(r["dt"]) in bound else 0)
+        d = int(r["dt"])
+        ln = int(r["out_len"]) + ((16 if bound[d][3] == srtp_lib.GCM else 10) if d in bound else 0)
         if not np.array_equal(gp[off:off + ln], op[off:off + ln]):
             bad = int(np.nonzero(gp[off:off + ln] != op[off:off + ln])[0][0])
             raise AssertionError("batch %d record %d (dt %d sn %d len %d) differs at byte %d" % (
@@ -39,10 +41,13 @@ def _compare(pkg, eng, o, oh, b, bound):
     return n_prot
 
 
-@pytest.mark.parametrize("cfg", [dict(config=2, rooms=2, seed=5), dict(config=1, seed=4, batch_s=0.05)])
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=2, seed=5), dict(config=1, seed=4, batch_s=0.05),
+                                 dict(config=2, rooms=2, seed=5, gcm_every=2),
+                                 dict(config=1, seed=4, batch_s=0.05, gcm_every=1)])
 def test_protect_matches_oracle(pkg, workload, cfg):
     kw = dict(cfg)
     bs = kw.pop("batch_s", 1.0)
+    ge = kw.pop("gcm_every", 0)
     tr = workload.Trace(kw.pop("config"), duration_s=4.0 if bs == 1.0 else 1.0, batch_s=bs, **kw)
     o = load_oracle()
     eng = pkg.Engine.for_trace(tr)
@@ -50,8 +55,8 @@ def test_protect_matches_oracle(pkg, workload, cfg):
     try:
         workload.load_topology(eng.api, eng.h, tr)
         workload.load_topology(o.api, oh, tr)
-        tg = srtp_lib.bind_transports(pkg, eng.api, eng.h, tr, seed=5)
-        to = srtp_lib.bind_transports(pkg, o.api, oh, tr, seed=5)
+        tg = srtp_lib.bind_transports(pkg, eng.api, eng.h, tr, seed=5, gcm_every=ge)
+        to = srtp_lib.bind_transports(pkg, o.api, oh, tr, seed=5, gcm_every=ge)
         assert sorted(tg) == sorted(to)
         n_prot = 0
         for b in range(tr.nbatches):
