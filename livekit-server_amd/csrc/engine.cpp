@@ -302,6 +302,7 @@ struct lkf_engine {
   uint32_t emitGrid = 2048;       // persistent grid-stride launch (LKF_EMIT_PERSISTENT=1)
   bool emitPersistent = false;
   uint32_t decideK = 0;  // DownTracks per decide wave (0: from the batch's packets per track)
+  uint32_t senderMode = 0;  // sender statistics kernel: 0 by batch shape, 1 thread per DownTrack, 2 wave
   // SRTP protect (tables allocated with the first transport or lkf_protect)
   std::vector<lkf_transport_params> transports;
   lkf_transport_params *dTransports = nullptr;
@@ -812,6 +813,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
   if (const char *v = getenv("LKF_EMIT_PERSISTENT")) e->emitPersistent = atoi(v) != 0;
   if (const char *v = getenv("LKF_DECIDE_K")) e->decideK = uint32_t(std::min(64, std::max(0, atoi(v))));
+  if (const char *v = getenv("LKF_SENDER_MODE")) e->senderMode = uint32_t(std::min(2, std::max(0, atoi(v))));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   if (const char *v = getenv("LKF_ING_LANE")) e->ingLane = atoi(v) != 0;
@@ -1519,6 +1521,9 @@ int lkf_run(lkf_engine *e, void *stream) {
     sl.ring = e->dSSRing;
     sl.gap = e->dSSGap;
     sl.ndts = nd;
+    // a few tuples per DownTrack (the same estimate as decide's DownTracks per wave)
+    sl.perThread = e->senderMode ? uint32_t(e->senderMode == 1)
+                                 : uint32_t(uint64_t(e->curN) / std::max<uint32_t>(1, nt) < 12);
     HIPCHK(launch_sender_stats(e->sendS, sl), "sender stats");
     HIPCHK(hipEventRecord(x.sent, e->sendS), "event");
     HIPCHK(hipStreamWaitEvent(e->emitS, x.sent, 0), "wait sender stats");

@@ -343,6 +343,7 @@ struct SenderLaunch {  // the forwarded tuples of one batch
   uint32_t *ring;  // kSnInfoSize per DownTrack
   uint32_t *gap;   // kGapWords per DownTrack
   uint32_t ndts;
+  uint32_t perThread;  // 1: one thread per DownTrack (short batches), 0: one wave
 };
 struct SenderUpd {  // one host-listed sendingPacket (padding, blank frame, RTX)
   uint64_t esn, ets;

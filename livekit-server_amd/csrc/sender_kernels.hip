@@ -319,6 +319,28 @@ __global__ void __launch_bounds__(64) k_sender_stats(SenderLaunch A) {
   if (lane < kW) reinterpret_cast<uint4 *>(A.ss + d)[lane] = reinterpret_cast<const uint4 *>(&sS)[lane];
 }
 
+// Short batches (a 10-ms tick: one or two tuples per DownTrack): one thread
+// per DownTrack, the scalar Update per tuple in send order — a wave per
+// DownTrack would spend its time loading and storing the state.
+__global__ void __launch_bounds__(64) k_sender_stats_thread(SenderLaunch A) {
+  const u32 d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= A.ndts) return;
+  const u32 n = A.fwdCnt[d];
+  if (n == 0) return;
+  SenderStats S = A.ss[d];
+  u32 *ring = A.ring + size_t(d) * kSnInfoSize;
+  u32 *gap = A.gap + size_t(d) * kGapWords;
+  const Tuple *tp = A.tuples + A.slotBase[d];
+  for (u32 k = 0; k < n; k++) {
+    const Tuple tu = tp[k];
+    const lkf_pkt &p = A.pkts[tu.pkt];
+    ss_update(S, ring, gap, p.arrival_ns, tu.extSN, tu.extTS, (tu.flags & LKF_OUT_MARKER) != 0, p.payload_off,
+              u32(tu.outLen - tu.hdrLen), 0);
+    if (tu.flags & LKF_OUT_KEYFRAME) S.keyFrames++;  // UpdateKeyFrame(1) rtpstats_base.go:429-439
+  }
+  A.ss[d] = S;
+}
+
 __global__ void k_sender_updates(SenderListLaunch A) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.ngroups) return;
@@ -338,7 +360,10 @@ __global__ void k_sender_updates(SenderListLaunch A) {
 
 hipError_t launch_sender_stats(hipStream_t s, const SenderLaunch &a) {
   if (!a.ndts) return hipSuccess;
-  hipLaunchKernelGGL(k_sender_stats, dim3(a.ndts), dim3(64), 0, s, a);
+  if (a.perThread)
+    hipLaunchKernelGGL(k_sender_stats_thread, dim3((a.ndts + 63) / 64), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_sender_stats, dim3(a.ndts), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

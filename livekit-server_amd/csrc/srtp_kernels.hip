@@ -70,8 +70,16 @@ __device__ __forceinline__ void aes_expand(const AesTab &t, const u32 key[4], u3
   }
 }
 
-template <class Tab>
-__device__ __forceinline__ void aes_encrypt(const Tab &t, const u32 rk[44], u32 &s0, u32 &s1, u32 &s2, u32 &s3) {
+// round keys read where they are used (the transport's session in global
+// memory, L1-resident: every lane of a wave mostly shares one) instead of 44
+// registers per lane — the protect kernel's occupancy
+struct RkG {
+  const u32 *p;
+  __device__ __forceinline__ u32 operator[](int i) const { return p[i]; }
+};
+
+template <class Tab, class RK>
+__device__ __forceinline__ void aes_encrypt(const Tab &t, const RK &rk, u32 &s0, u32 &s1, u32 &s2, u32 &s3) {
   s0 ^= rk[0];
   s1 ^= rk[1];
   s2 ^= rk[2];
@@ -265,49 +273,116 @@ struct AesLds {
   __device__ __forceinline__ u32 S(u32 x) const { return (T0(x) >> 16) & 255; }
 };
 
-// GHASH multiply Y <- Y * H in GF(2^128) (NIST SP 800-38D §6.3: bit 0 = the
-// most significant bit of byte 0; big-endian words), bit-serial
-__device__ __forceinline__ void gf_mul(u32 y[4], const u32 h[4]) {
-  u32 z0 = 0, z1 = 0, z2 = 0, z3 = 0, v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
+// ---- AEAD_AES_128_GCM -----------------------------------------------------
+// GHASH (NIST SP 800-38D §6.4; bit 0 = the most significant bit of byte 0, the
+// block as big-endian words) with Shoup's 4-bit tables: M[n] = n * H for the 16
+// nibbles (M[8] = H, M[4] = H*x, M[2] = H*x^2, M[1] = H*x^3, the rest XORs),
+// Y * H one nibble at a time from the last byte, each step shifting Z right by
+// 4 and folding the 4 bits shifted out back in through R = last4[rem] << 112.
+// A wave's GCM lanes are grouped by transport: one 256-B table per wave in LDS
+// (16 entries, one bank row: lanes reading different entries never conflict),
+// rebuilt per distinct transport among the wave's records (records of a
+// DownTrack are contiguous, so a wave sees one or two).
+struct GcmDefer {  // a GCM record's GHASH inputs, carried from the CTR pass
+  uint4 *dst;
+  u32 len, hw, key;
+  u32 ej[4];  // E(K, J0)
+};
+
+__device__ __forceinline__ void gf_mul_tab(u32 y[4], const uint4 *M, const u32 *L4) {
+  u32 z0, z1, z2, z3;
+  {
+    const uint4 m = M[y[3] & 15];
+    z0 = m.x, z1 = m.y, z2 = m.z, z3 = m.w;
+  }
+  auto step = [&](u32 nib) {
+    const u32 rem = z3 & 15;
+    z3 = (z3 >> 4) | (z2 << 28);
+    z2 = (z2 >> 4) | (z1 << 28);
+    z1 = (z1 >> 4) | (z0 << 28);
+    z0 = (z0 >> 4) ^ (L4[rem] << 16);
+    const uint4 m = M[nib];
+    z0 ^= m.x, z1 ^= m.y, z2 ^= m.z, z3 ^= m.w;
+  };
+  step((y[3] >> 4) & 15);
 #pragma unroll
-  for (int w = 0; w < 4; w++) {
-    const u32 x = y[w];
-    for (int b = 31; b >= 0; b--) {
-      const u32 m = 0u - ((x >> b) & 1u);
-      z0 ^= v0 & m;
-      z1 ^= v1 & m;
-      z2 ^= v2 & m;
-      z3 ^= v3 & m;
-      const u32 r = 0xE1000000u & (0u - (v3 & 1u));
-      v3 = (v3 >> 1) | (v2 << 31);
-      v2 = (v2 >> 1) | (v1 << 31);
-      v1 = (v1 >> 1) | (v0 << 31);
-      v0 = (v0 >> 1) ^ r;
-    }
+  for (int i = 14; i >= 0; i--) {
+    const u32 xb = (y[i >> 2] >> (24 - 8 * (i & 3))) & 255;
+    step(xb & 15);
+    step(xb >> 4);
   }
   y[0] = z0, y[1] = z1, y[2] = z2, y[3] = z3;
 }
-__device__ __forceinline__ void ghash_block(u32 y[4], const u32 h[4], u32 b0, u32 b1, u32 b2, u32 b3) {
-  y[0] ^= b0, y[1] ^= b1, y[2] ^= b2, y[3] ^= b3;
-  gf_mul(y, h);
+
+// GHASH(H, A = header, C) for the wave's deferred GCM records, then each tag
+// E(K, J0) ^ S after its ciphertext.  Every lane of the wave calls it (the
+// loop over transports is wave-uniform).
+__device__ void gcm_ghash_wave(const SrtpKeys *keys, const GcmDefer &g, bool on, uint4 *M, const u32 *L4) {
+  const u32 lane = threadIdx.x & 63;
+  u64 pend = __ballot(on);
+  while (pend) {
+    const u32 key = __shfl(g.key, __ffsll((long long)pend) - 1);
+    if (lane < 16) {  // this transport's table: lane n builds M[n]
+      const SrtpKeys &K = keys[key];
+      u32 b[4] = {K.ih[0], K.ih[1], K.ih[2], K.ih[3]};  // H = M[8]
+      u32 m[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int bit = 3; bit >= 0; bit--) {
+        if ((lane >> bit) & 1) m[0] ^= b[0], m[1] ^= b[1], m[2] ^= b[2], m[3] ^= b[3];
+        const u32 r = 0xE1000000u & (0u - (b[3] & 1u));  // * x
+        b[3] = (b[3] >> 1) | (b[2] << 31);
+        b[2] = (b[2] >> 1) | (b[1] << 31);
+        b[1] = (b[1] >> 1) | (b[0] << 31);
+        b[0] = (b[0] >> 1) ^ r;
+      }
+      M[lane] = make_uint4(m[0], m[1], m[2], m[3]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool mine = on && g.key == key;
+    if (mine) {
+      const u32 *ow = reinterpret_cast<const u32 *>(g.dst);
+      const u32 hw = g.hw, lc = g.len - 4 * g.hw;  // ciphertext bytes
+      u32 y[4] = {0, 0, 0, 0};
+      for (u32 blk = 0; 4 * blk < hw; blk++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) y[j] ^= (4 * blk + j < hw) ? bswap(ow[4 * blk + j]) : 0u;
+        gf_mul_tab(y, M, L4);
+      }
+      for (u32 blk = 0; 16 * blk < lc; blk++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int left = int(lc) - int(16 * blk + 4 * j);  // bytes of this word inside the ciphertext
+          const u32 v = left > 0 ? bswap(ow[hw + 4 * blk + j]) : 0u;
+          y[j] ^= left >= 4 ? v : left > 0 ? (v & (0xFFFFFFFFu << (8 * (4 - left)))) : 0u;
+        }
+        gf_mul_tab(y, M, L4);
+      }
+      y[1] ^= 32u * hw;  // len(A) || len(C) in bits
+      y[3] ^= 8u * lc;
+      gf_mul_tab(y, M, L4);
+      u8 *tag = reinterpret_cast<u8 *>(g.dst) + g.len;
+#pragma unroll
+      for (int k = 0; k < 16; k++) tag[k] = u8((g.ej[k / 4] ^ y[k / 4]) >> (24 - 8 * (k & 3)));
+    }
+    pend &= ~__ballot(mine);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // table reads done before the next rebuild
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 // AEAD_AES_128_GCM (RFC 7714 §8, pion srtpCipherAeadAesGcm.encryptRTP) of one
-// record: IV = (0^16 || SSRC || ROC || SEQ) XOR salt, counter blocks IV || 2,
-// 3, ..; pass 1 writes the header (abs-send-time stamped) and the ciphertext in
-// whole 16-B chunks (one new keystream block per chunk: the window is offset
-// from the chunk by the header length, a whole number of words); pass 2 runs
-// GHASH over the header (AAD) and the ciphertext read back from the output,
-// then the 16-byte tag E(K, J0) ^ GHASH after the ciphertext.
+// record, CTR half: IV = (0^16 || SSRC || ROC || SEQ) XOR salt, counter blocks
+// IV || 2, 3, ..; writes the header (abs-send-time stamped) and the ciphertext
+// in whole 16-B chunks (one new keystream block per chunk: the window is offset
+// from the chunk by the header length, a whole number of words), and E(K, J0)
+// for the tag.  GHASH over the header and the ciphertext read back from the
+// output follows in gcm_ghash_wave.
 template <class Tab>
 __device__ void protect_gcm(const Tab &tb, const SrtpKeys *K, const uint4 *src, uint4 *dst, u32 len, u32 hw,
-                            u32 absPos, u32 absVal, u32 ssrc, u32 seq, u32 roc) {
-  u32 rk[44];
-#pragma unroll
-  for (int k = 0; k < 11; k++) {
-    const uint4 q = reinterpret_cast<const uint4 *>(K->rk)[k];
-    rk[4 * k] = q.x, rk[4 * k + 1] = q.y, rk[4 * k + 2] = q.z, rk[4 * k + 3] = q.w;
-  }
+                            u32 absPos, u32 absVal, u32 ssrc, u32 seq, u32 roc, GcmDefer &g) {
+  const RkG rk{K->rk};
   const u32 iv0 = (ssrc >> 16) ^ K->salt[0], iv1 = ((ssrc << 16) | (roc >> 16)) ^ K->salt[1],
             iv2 = ((roc << 16) | seq) ^ K->salt[2];
   const u32 ch0 = (hw + 3) >> 2, sft = 4 * ch0 - hw;
@@ -347,45 +422,16 @@ __device__ void protect_gcm(const Tab &tb, const SrtpKeys *K, const uint4 *src, 
     }
     dst[c] = ch;
   }
-  // GHASH(H, A = header, C)
-  const u32 H[4] = {K->ih[0], K->ih[1], K->ih[2], K->ih[3]};
-  const u32 *ow = reinterpret_cast<const u32 *>(dst);
-  u32 y[4] = {0, 0, 0, 0};
-  for (u32 b = 0; 4 * b < hw; b++) {
-    u32 x[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) x[j] = (4 * b + j < hw) ? bswap(ow[4 * b + j]) : 0u;
-    ghash_block(y, H, x[0], x[1], x[2], x[3]);
-  }
-  const u32 lc = len - 4 * hw;  // ciphertext bytes
-  for (u32 b = 0; 16 * b < lc; b++) {
-    u32 x[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int left = int(lc) - int(16 * b + 4 * j);  // bytes of this word inside the ciphertext
-      const u32 v = left > 0 ? bswap(ow[hw + 4 * b + j]) : 0u;
-      x[j] = left >= 4 ? v : left > 0 ? (v & (0xFFFFFFFFu << (8 * (4 - left)))) : 0u;
-    }
-    ghash_block(y, H, x[0], x[1], x[2], x[3]);
-  }
-  ghash_block(y, H, 0u, 32u * hw, 0u, 8u * lc);  // len(A) || len(C) in bits
-  u32 e0 = iv0, e1 = iv1, e2 = iv2, e3 = 1u;     // E(K, J0)
+  u32 e0 = iv0, e1 = iv1, e2 = iv2, e3 = 1u;  // E(K, J0)
   aes_encrypt(tb, rk, e0, e1, e2, e3);
-  const u32 t[4] = {e0 ^ y[0], e1 ^ y[1], e2 ^ y[2], e3 ^ y[3]};
-  u8 *tag = reinterpret_cast<u8 *>(dst) + len;
-#pragma unroll
-  for (int k = 0; k < 16; k++) tag[k] = u8(t[k / 4] >> (24 - 8 * (k & 3)));
+  g.dst = dst;
+  g.len = len;
+  g.hw = hw;
+  g.ej[0] = e0, g.ej[1] = e1, g.ej[2] = e2, g.ej[3] = e3;
 }
 
-__global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
-  __shared__ u32 sTe[256 * 32];
-  const u32 tid = threadIdx.x;
-  for (u32 k = tid; k < 256 * 32; k += SRTP_T) sTe[k] = A.tab[k >> 5];
-  __syncthreads();
-  const u64 n = A.totals[0];
-  const u64 i = u64(blockIdx.x) * SRTP_T + tid;
-  if (i >= n || i >= A.cap) return;
-  const AesLds tb{sTe, tid & 31};
+// One record; a GCM record's GHASH half is deferred to the wave pass (g, true).
+__device__ bool protect_record(const SrtpProtectArgs &A, const AesLds &tb, u64 i, GcmDefer &g) {
   const lkf_out r = A.out[i];
   const u32 len = r.out_len;
   const uint4 *src = reinterpret_cast<const uint4 *>(A.arena + r.out_off);
@@ -433,24 +479,17 @@ __global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
   const u32 hw = h / 4;
   const SrtpDT s = A.sd[r.dt];
   const bool prot = s.tp1 != 0;
-  u32 rk[44];
   u32 roc = 0, ctr0 = 0, ctr1 = 0, ctr2 = 0, ctr3 = 0;
   u32 hs[5] = {0, 0, 0, 0, 0};
   const SrtpKeys *K = prot ? A.keys + (s.tp1 - 1) : A.keys;
   if (prot && K->profile == LKF_SRTP_AEAD_AES_128_GCM) {
     protect_gcm(tb, K, src, dst, len, hw, absPos, A.absVal, bswap(c0v.z), bswap(w0) & 0xFFFF,
-                u32((r.ext_sn >> 16) - s.rocBase));
-    return;
+                u32((r.ext_sn >> 16) - s.rocBase), g);
+    g.key = s.tp1 - 1;
+    return true;
   }
+  const RkG rk{K->rk};
   if (prot) {
-#pragma unroll
-    for (int k = 0; k < 11; k++) {
-      const uint4 q = reinterpret_cast<const uint4 *>(K->rk)[k];
-      rk[4 * k] = q.x;
-      rk[4 * k + 1] = q.y;
-      rk[4 * k + 2] = q.z;
-      rk[4 * k + 3] = q.w;
-    }
     roc = u32((r.ext_sn >> 16) - s.rocBase);
     const u32 ssrc = bswap(c0v.z);
     const u32 seq = bswap(w0) & 0xFFFF;
@@ -459,9 +498,6 @@ __global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
     ctr2 = K->salt[2] ^ roc;
     ctr3 = K->salt[3] ^ (seq << 16);
     for (int k = 0; k < 5; k++) hs[k] = K->ih[k];
-  } else {
-#pragma unroll
-    for (int k = 0; k < 44; k++) rk[k] = 0;
   }
   const u32 sft = (0u - hw) & 3;  // keystream window offset of message word 0
   int blk0 = -int((hw + 3) >> 2);   // AES block index of window slot 0
@@ -534,7 +570,7 @@ __global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
     for (int k = 0; k < 4; k++) win[k] = win[16 + k];
     blk0 += 4;
   }
-  if (!prot) return;  // no transport: the packet goes out as is (abs-send-time stamped)
+  if (!prot) return false;  // no transport: the packet goes out as is (abs-send-time stamped)
   // outer hash, then the 80-bit tag after the payload
   u32 ho[5] = {K->oh[0], K->oh[1], K->oh[2], K->oh[3], K->oh[4]};
   {
@@ -544,6 +580,25 @@ __global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
   u8 *tag = reinterpret_cast<u8 *>(dst) + len;
 #pragma unroll
   for (int k = 0; k < 10; k++) tag[k] = u8(ho[k / 4] >> (24 - 8 * (k & 3)));
+  return false;
+}
+
+__global__ void __launch_bounds__(SRTP_T) k_srtp_protect(SrtpProtectArgs A) {
+  __shared__ u32 sTe[256 * 32];
+  __shared__ uint4 sGt[SRTP_T / 64][16];  // per-wave GHASH table
+  __shared__ u32 sL4[16];
+  const u32 tid = threadIdx.x;
+  for (u32 k = tid; k < 256 * 32; k += SRTP_T) sTe[k] = A.tab[k >> 5];
+  if (tid < 16)  // last4[r] = r (carry-less) * 0xE1 << 5
+    sL4[tid] = ((tid & 1) ? 0x1C20u : 0u) ^ ((tid & 2) ? 0x3840u : 0u) ^ ((tid & 4) ? 0x7080u : 0u) ^
+               ((tid & 8) ? 0xE100u : 0u);
+  __syncthreads();
+  const u64 n = A.totals[0];
+  const u64 i = u64(blockIdx.x) * SRTP_T + tid;
+  const AesLds tb{sTe, tid & 31};
+  GcmDefer g{};
+  const bool gcm = (i < n && i < A.cap) ? protect_record(A, tb, i, g) : false;
+  gcm_ghash_wave(A.keys, g, gcm, sGt[tid >> 6], sL4);
 }
 
 }  // namespace

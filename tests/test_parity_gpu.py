@@ -149,6 +149,17 @@ def test_config2_heavy_loss(pkg, workload, abi):
     run_parity(pkg, workload, abi, tr)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_sender_stats_kernels(pkg, workload, abi, monkeypatch, mode):
+    """Both sender-statistics kernels on the same heavy-loss/reorder trace
+    (LKF_SENDER_MODE 1: one thread per DownTrack, the short-batch choice; 2:
+    one wave per DownTrack with in-order runs decided in parallel), against
+    the oracle's scalar RTPStatsSender.Update."""
+    monkeypatch.setenv("LKF_SENDER_MODE", str(mode))
+    tr = workload.Trace(2, duration_s=3.0, batch_s=0.5, rooms=2, loss=0.2, reorder=0.2, seed=31)
+    run_parity(pkg, workload, abi, tr)
+
+
 def test_config3_small(pkg, workload, abi):
     """configs[2] shape: audio-heavy rooms of 50 (2 rooms)."""
     tr = workload.Trace(3, duration_s=3.0, batch_s=1.0, rooms=2)
