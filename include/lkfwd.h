@@ -263,7 +263,9 @@ typedef struct lkf_stream_params {
    * gets mediatransportutil's NackQueue (NackQueueParamsDefault); 0 = none
    * (audio/red, or no "nack" RTCP feedback) */
   uint8_t nack;
-  uint8_t reserved[3];
+  uint8_t twcc_ext;         /* negotiated transport-cc extension id (buffer.go:238-245, SetTWCC): the
+                               datagrams' TWCC responder pushes (lkf_ingest_twcc); 0 = none */
+  uint8_t reserved[2];
   uint32_t rtt_ms;          /* initial NackQueue RTT (Buffer.SetRTT); 0 = the queue's default 70 ms */
 } lkf_stream_params;
 
@@ -812,6 +814,21 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
 /* The ExtPacket batch produced by the last ingest (host copy; the RTX bucket
  * and the host-side stream trackers read it). */
 int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out);
+/* The TWCC responder's input of the last ingest (processHeaderExtensions,
+ * buffer.go:569-576): every datagram that unmarshals, on a stream with a
+ * twcc_ext, whose header carries that element (GetExtension: the first
+ * element with the id) is pushed as twcc.Responder.Push(BigEndian SN of the
+ * element's first two bytes, arrival, marker) — padding-only, duplicate and
+ * out-of-order datagrams included, before any stream-state decision.  out[i]
+ * is datagram i's word: LKF_TWCC_PUSH | (marker ? LKF_TWCC_MARKER : 0) | SN,
+ * or 0 (no push; an element shorter than two bytes, which the reference's
+ * ext[0:2] would not survive, is not pushed).  The caller feeds the pushes to
+ * its Responder in datagram order with its own arrival times (the Responder
+ * builds the RTCP TransportLayerCC at control rate: mediatransportutil, out of
+ * the path).  Replaces the per-packet b.twcc.Push call. */
+#define LKF_TWCC_PUSH 0x80000000u
+#define LKF_TWCC_MARKER 0x00010000u
+int lkf_ingest_twcc(lkf_engine *e, uint32_t *out, uint32_t cap, uint32_t *n_out);
 /* Its lkf_pkt_dd side array (same order and count as lkf_ingested). */
 int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_out);
 int lkf_stream_stats_get(lkf_engine *e, int32_t stream, lkf_stream_stats *out);

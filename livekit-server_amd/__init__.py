@@ -120,6 +120,19 @@ def drain_protected(api, h):
     return arena
 
 
+def twcc_words(api, h):
+    """Per-datagram TWCC responder push words (LKF_TWCC_*) of the last ingest."""
+    n = C.c_uint32()
+    rc = api["ingest_twcc"](h, None, 0, C.byref(n))
+    if rc not in (0, -28):
+        raise EngineError("ingest_twcc probe rc=%d" % rc)
+    out = np.zeros(n.value, dtype=np.uint32)
+    rc = api["ingest_twcc"](h, out.ctypes.data, n.value, C.byref(n))
+    if rc != 0:
+        raise EngineError("ingest_twcc rc=%d" % rc)
+    return out
+
+
 def flows_array(api, h):
     """Per-datagram outcomes (lkf_flow) of the last ingest as a numpy array."""
     n = C.c_uint32()

@@ -41,7 +41,8 @@ class lkf_stream_params(C.Structure):
         ("observe_duration_ms", C.c_uint32),
         ("smooth_intervals", C.c_uint32),
         ("nack", C.c_uint8),
-        ("reserved", C.c_uint8 * 3),
+        ("twcc_ext", C.c_uint8),
+        ("reserved", C.c_uint8 * 2),
         ("rtt_ms", C.c_uint32),
     ]
 
@@ -313,6 +314,8 @@ class lkf_transport_params(C.Structure):
 
 LKF_SRTP_AES128_CM_HMAC_SHA1_80 = 1
 LKF_SRTP_AEAD_AES_128_GCM = 2
+LKF_TWCC_PUSH = 0x80000000
+LKF_TWCC_MARKER = 0x00010000
 SRTP_TAG_LEN = 10
 
 
@@ -411,6 +414,7 @@ def bind_engine_api(lib, prefix):
     if hasattr(lib, prefix + "ingest_device"):  # engine only (the oracle is host-side)
         api["ingest_device"] = _bind(lib, prefix + "ingest_device", C.c_int,
                                      [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64])
+    api["ingest_twcc"] = _bind(lib, prefix + "ingest_twcc", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["ingest_flows"] = _bind(lib, prefix + "ingest_flows", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["ingested"] = _bind(lib, prefix + "ingested", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])
     api["ingested_dd"] = _bind(lib, prefix + "ingested_dd", C.c_int, [e, C.c_void_p, C.c_uint32, P(C.c_uint32)])

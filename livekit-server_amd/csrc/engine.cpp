@@ -320,6 +320,7 @@ struct lkf_engine {
   RangeEntry *dStreamRings = nullptr;
   IngParsed *dParsed = nullptr;
   lkf_flow *dFlows = nullptr;
+  uint32_t *dTwcc = nullptr;  // per datagram TWCC push word of the last ingest
   uint32_t *dFwdFlag = nullptr;
   uint64_t *dPos = nullptr, *dIPartA = nullptr, *dIPartB = nullptr, *dITotal = nullptr;
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
@@ -751,6 +752,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dStreamRings, size_t(e->maxStreams) * kRangeCap));
   A(dalloc(&e->dParsed, c.max_batch_pkts));
   A(dalloc(&e->dFlows, c.max_batch_pkts));
+  A(dalloc(&e->dTwcc, c.max_batch_pkts));
   A(dalloc(&e->dFwdFlag, c.max_batch_pkts));
   A(dalloc(&e->dPos, c.max_batch_pkts));
   const size_t ipart = (size_t(c.max_batch_pkts) + 1023) / 1024 + 1;
@@ -850,7 +852,7 @@ void lkf_destroy(lkf_engine *e) {
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
-                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
+                  e->dTwcc, e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
                   e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut,
@@ -2947,6 +2949,7 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p) {
   d.codec = tp.codec;
   d.levelExt = p->audio_level_ext;
   d.ddExt = p->dd_ext;
+  d.twccExt = p->twcc_ext;
   d.ddIdx = p->dd_ext ? e->nDDStreams++ : 0xffffffffu;  // its DependencyDescriptorParser (buffer.go:193-201)
   d.nack = p->nack ? 1 : 0;  // its NackQueue (buffer.go:248-256)
   const bool dflt = !p->active_level && !p->min_percentile && !p->observe_duration_ms && !p->smooth_intervals;
@@ -2994,6 +2997,7 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.err = e->dIErr;
   a.flows = e->dFlows;
   a.fwd = e->dFwdFlag;
+  a.twcc = e->dTwcc;
   a.pos = e->dPos;
   a.partA = e->dIPartA;
   a.partB = e->dIPartB;
@@ -3068,6 +3072,17 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
   HIPCHK(hipStreamSynchronize(e->prepS), "sync");
   if (e->lastIngestN)
     HIPCHK(hipMemcpy(out, e->dFlows, size_t(e->lastIngestN) * sizeof(lkf_flow), hipMemcpyDeviceToHost), "flows");
+  return LKF_OK;
+}
+
+int lkf_ingest_twcc(lkf_engine *e, uint32_t *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !n_out) return LKF_EINVAL;
+  *n_out = e->lastIngestN;
+  if (cap < e->lastIngestN) return LKF_ENOSPC;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
+  if (e->lastIngestN)
+    HIPCHK(hipMemcpy(out, e->dTwcc, size_t(e->lastIngestN) * sizeof(uint32_t), hipMemcpyDeviceToHost), "twcc");
   return LKF_OK;
 }
 

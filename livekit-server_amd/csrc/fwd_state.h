@@ -307,7 +307,8 @@ struct DevStream {  // static stream parameters (64 B)
   uint8_t ddExt;           // dependency-descriptor extension id
   uint8_t nack;            // the Buffer has a NackQueue (NACK feedback negotiated)
   uint8_t closed;          // Buffer.Close (lkf_remove_track): datagrams are not processed
-  uint8_t pad1[13];
+  uint8_t twccExt;         // transport-cc extension id (0: no TWCC responder)
+  uint8_t pad1[12];
 };
 static_assert(sizeof(DevStream) == 64, "DevStream must be 64 B");
 

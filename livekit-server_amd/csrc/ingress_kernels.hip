@@ -41,7 +41,8 @@ using i64 = int64_t;
 // k_ing_parse
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, u8 ddExt, IngParsed &q,
-                                          int &levelOff) {
+                                          int &levelOff, u8 twccExt = 0, int *twccOff = nullptr,
+                                          int *twccLen = nullptr) {
   levelOff = -1;
   if (len < 12) return false;
   q.b0 = buf[0];
@@ -62,7 +63,7 @@ __device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, u
     const int extEnd = n + extLen;
     if (len < extEnd) return false;
     if (profile == 0xBEDE || profile == 0x1000) {
-      bool seen = false, seenDD = false;  // Header.GetExtension returns the first element with the id
+      bool seen = false, seenDD = false, seenTw = false;  // Header.GetExtension: the first element with the id
       while (n < extEnd) {
         if (buf[n] == 0x00) {
           n++;
@@ -91,6 +92,11 @@ __device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, u
           seenDD = true;
           q.ddOff = u16(n);
           q.ddLen = u8(pl);
+        }
+        if (twccExt && id == twccExt && !seenTw) {
+          seenTw = true;
+          *twccOff = n;
+          *twccLen = pl;
         }
         n += pl;
       }
@@ -347,11 +353,12 @@ __device__ __forceinline__ bool vp9_parse(const u8 *p, int len, IngParsed &q) {
 
 __global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u8 *__restrict__ raw,
                             const DevStream *__restrict__ streams, u32 nstreams, IngParsed *__restrict__ out,
-                            u32 *__restrict__ err) {
+                            u32 *__restrict__ twcc, u32 *__restrict__ err) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const lkf_raw_pkt rp = raws[i];
   IngParsed q = {};
+  twcc[i] = 0;
   if (rp.stream >= nstreams) {
     atomicOr(err, 1u);
     q.track = 0xffffffffu;
@@ -361,9 +368,13 @@ __global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u
   const DevStream s = streams[rp.stream];
   q.track = s.track;
   const u8 *b = raw + rp.off;
-  int levelOff = -1;
-  if (rtp_parse(b, int(rp.len), s.levelExt, s.ddExt, q, levelOff)) {
+  int levelOff = -1, twOff = -1, twLen = 0;
+  if (rtp_parse(b, int(rp.len), s.levelExt, s.ddExt, q, levelOff, s.twccExt, &twOff, &twLen)) {
     q.flags |= IP_OK;
+    // processHeaderExtensions (buffer.go:569-576): the TWCC responder sees every
+    // datagram that unmarshals (a closed Buffer takes none: Write returns first)
+    if (twOff >= 0 && twLen >= 2 && !s.closed)
+      twcc[i] = LKF_TWCC_PUSH | ((b[1] & 0x80) ? LKF_TWCC_MARKER : 0u) | (u32(b[twOff]) << 8) | b[twOff + 1];
     if (levelOff >= 0) {  // AudioLevelExtension.Unmarshal: level = b & 0x7f
       q.flags |= IP_LEVEL;
       q.level = b[levelOff] & 0x7f;
@@ -1748,7 +1759,7 @@ static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
   if (a.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ing_parse, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.n, a.raw, a.streams, a.nstreams,
-                     a.parsed, a.err);
+                     a.parsed, a.twcc, a.err);
   hipLaunchKernelGGL(k_ing_ranges, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.parsed, a.n, a.ntracks, a.tBegin, a.tEnd,
                      a.tRuns, a.err);
   hipLaunchKernelGGL(k_ing_lists, dim3(a.ntracks), dim3(64), 0, st, a.raws, a.streams, a.nstreams, a.tBegin,

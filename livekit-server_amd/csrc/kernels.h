@@ -96,6 +96,7 @@ struct IngestLaunch {
   uint32_t *tBegin, *tEnd, *tRuns, *err;
   lkf_flow *flows;
   uint32_t *fwd;
+  uint32_t *twcc;  // per datagram: TWCC responder push word (LKF_TWCC_*)
   uint64_t *pos, *partA, *partB, *total;
   lkf_pkt *out;
   // dependency descriptor (nullptr: no stream negotiated the DD extension)

@@ -656,6 +656,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       sp.ssrc = tg[ti].ssrc[l];
       sp.audio_level_ext = tg[ti].p.kind == LKF_KIND_AUDIO ? 1 : 0;
       sp.dd_ext = tg[ti].dd ? 8 : 0;
+      sp.twcc_ext = 5;  // transport-cc (video datagrams carry it; audio ones do not)
       // publishers negotiate NACK feedback for Opus and every video codec
       // (pkg/rtc/config.go:92-101): each Buffer gets a NackQueue; RTTs vary
       // (a quarter keep the queue's default)

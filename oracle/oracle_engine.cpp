@@ -106,6 +106,7 @@ struct orc_engine {
   // ingress
   std::vector<std::unique_ptr<OStream>> streams;
   std::vector<lkf_flow> flows;
+  std::vector<u32> twcc;  // per datagram TWCC responder push word (LKF_TWCC_*)
   std::vector<lkf_rtcp_nack> nackRecs;  // the last ingest's RTCP NACKs
   std::vector<lkf_nack_pair> nackPairs;
   std::vector<lkf_pkt> ingested;
@@ -1453,7 +1454,7 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
     f.flags = LKF_FLOW_BAD;
     return f;
   }
-  // processHeaderExtensions: audio level (TWCC is out of scope)
+  // processHeaderExtensions: audio level (the TWCC push: orc_ingest)
   bool hasLevel = false;
   u8 level = 0;
   if (b.p.audio_level_ext) {
@@ -1606,6 +1607,7 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
 int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len) {
   (void)raw_len;
   e->flows.assign(n, lkf_flow{});
+  e->twcc.assign(n, 0u);
   e->nackRecs.clear();
   e->nackPairs.clear();
   e->ingested.clear();
@@ -1620,6 +1622,13 @@ int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
       e->flows[i].pkt = 0xffffffffu;
       e->flows[i].flags = LKF_FLOW_NOT_HANDLED;
       continue;
+    }
+    if (b.p.twcc_ext) {  // processHeaderExtensions (buffer.go:569-576): b.twcc.Push before the stream state
+      RtpParsed h;
+      int off = 0, len = 0;
+      const u8 *buf = raw + pkts[i].off;
+      if (rtp_unmarshal(buf, int(pkts[i].len), h) && h.GetExtension(b.p.twcc_ext, off, len) && len >= 2)
+        e->twcc[i] = LKF_TWCC_PUSH | (h.marker ? LKF_TWCC_MARKER : 0u) | (u32(buf[off]) << 8) | buf[off + 1];
     }
     e->flows[i] = calc(e, b, pkts[i], raw, ep, epd, fwd);
     if (b.nacker) {  // calc's deferred doNACKs (buffer.go:417-421, :673-710), now = the arrival time
@@ -1645,6 +1654,13 @@ int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
     }
   }
   e->pendingDD = e->ingestedDD;  // the ingested batch is the next run's input
+  return LKF_OK;
+}
+
+int orc_ingest_twcc(orc_engine *e, uint32_t *out, uint32_t cap, uint32_t *n_out) {
+  *n_out = u32(e->twcc.size());
+  if (cap < e->twcc.size()) return LKF_ENOSPC;
+  if (!e->twcc.empty()) std::memcpy(out, e->twcc.data(), e->twcc.size() * sizeof(u32));
   return LKF_OK;
 }
 

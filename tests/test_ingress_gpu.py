@@ -3,7 +3,8 @@
 Raw datagrams (with loss, reordering, audio-level extensions, VP8 payloads)
 go through lkf_ingest (Buffer.calc on the GPU) and orc_ingest (the oracle's
 restatement); the per-datagram flow records, the ExtPacket batches produced,
-the forwarded output of that batch, every stream's RTPStatsReceiver counters
+the TWCC responder pushes (processHeaderExtensions), the forwarded output of
+that batch, every stream's RTPStatsReceiver counters
 and the per-room active-speaker lists must be identical.
 """
 import ctypes as C
@@ -66,6 +67,7 @@ def run_ingress_parity(pkg, workload, abi, trace, speakers=True, rtt_changes=Non
             workload.load_streams(api, h, trace)
         total_fwd = 0
         nack_pkts = 0
+        twcc_pushes = 0
         for b in range(trace.nbatches):
             for sid, rtt in (rtt_changes or {}).get(b, []):
                 assert eng.api["stream_set_rtt"](eng.h, sid, rtt) == 0
@@ -84,6 +86,12 @@ def run_ingress_parity(pkg, workload, abi, trace, speakers=True, rtt_changes=Non
                     bad = np.nonzero(gf[f] != of[f])[0][:5]
                     raise AssertionError("batch %d flow field %s differs at %s: gpu %s orc %s" % (
                         b, f, bad, gf[bad], of[bad]))
+            gt, ot = pkg.twcc_words(eng.api, eng.h), pkg.twcc_words(o.api, oh)
+            assert len(gt) == len(ot) == n
+            if not np.array_equal(gt, ot):
+                bad = np.nonzero(gt != ot)[0][:5]
+                raise AssertionError("batch %d TWCC pushes differ at %s: gpu %s orc %s" % (b, bad, gt[bad], ot[bad]))
+            twcc_pushes += int(np.count_nonzero(gt & abi.LKF_TWCC_PUSH))
             gp = _ingested(eng.api, eng.h, abi)
             op = _ingested(o.api, oh, abi)
             if gp != op:
@@ -124,6 +132,7 @@ def run_ingress_parity(pkg, workload, abi, trace, speakers=True, rtt_changes=Non
         for s in range(trace.nstreams):
             assert eng.stream_stats(s) == pkg.stream_stats(o.api, oh, s), s
         run_ingress_parity.nack_pkts = nack_pkts
+        run_ingress_parity.twcc_pushes = twcc_pushes
         return total_fwd
     finally:
         eng.close()
@@ -133,6 +142,7 @@ def run_ingress_parity(pkg, workload, abi, trace, speakers=True, rtt_changes=Non
 def test_ingress_config2_loss_reorder(pkg, workload, abi):
     tr = workload.Trace(2, duration_s=3.0, batch_s=0.5, rooms=3, loss=0.05, reorder=0.03, seed=21)
     assert run_ingress_parity(pkg, workload, abi, tr) > 0
+    assert run_ingress_parity.twcc_pushes > 1000  # every video datagram carries transport-cc
 
 
 def test_ingress_config5_vp9(pkg, workload, abi):
