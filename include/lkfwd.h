@@ -299,6 +299,8 @@ typedef struct lkf_flow {
 #define LKF_FLOW_FORWARD 0x20      /* an ExtPacket was produced (buffer.go:489) */
 #define LKF_FLOW_BAD 0x40          /* RTP unmarshal / codec parse / DD parse failed (buffer.go:424,
                                       :613-616, :632): getExtPacket returned nil */
+#define LKF_FLOW_BUCKET 0x80       /* stored in the stream's RTX bucket (buffer.go:471): every packet
+                                      the bucket takes, an ExtPacket or not */
 
 /* RTPStatsReceiver counters of one stream (rtpstats_receiver.go:76-241). */
 typedef struct lkf_stream_stats {
@@ -517,6 +519,17 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
 int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
                  uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
                  uint64_t *out_len);
+/* The same with the source packets read from the receivers' buckets on the GPU
+ * (Receiver.ReadRTP(layer, sourceSeqNo) -> Buffer.GetPacket -> Bucket.GetPacket,
+ * receiver.go:559-566, buffer.go:772-784): lkf_ingest stores every packet the
+ * Buffer's bucket takes (buffer.go:471, mediatransportutil bucket: video
+ * PacketBufferSize = seq_size slots, audio 200, of 1500 bytes) in HBM under
+ * its adjusted SN; the record's track buffer of its layer (an SVC track's
+ * single buffer) is read, a miss (closed buffer, too new, too old, slot
+ * invalid or holding another SN) skips the record.  No host copy of the
+ * packets is needed. */
+int lkf_rtx_emit_bucket(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *out, uint8_t *out_arena,
+                        uint64_t out_cap, uint32_t *n_out, uint64_t *out_len);
 
 /* ---- padding and blank frames ---------------------- *
  * One request per DownTrack per call (distinct DownTracks; LKF_EINVAL

@@ -315,6 +315,7 @@ class lkf_transport_params(C.Structure):
 LKF_SRTP_AES128_CM_HMAC_SHA1_80 = 1
 LKF_SRTP_AEAD_AES_128_GCM = 2
 LKF_TWCC_PUSH = 0x80000000
+LKF_FLOW_BUCKET = 0x80
 LKF_TWCC_MARKER = 0x00010000
 SRTP_TAG_LEN = 10
 
@@ -435,6 +436,9 @@ def bind_engine_api(lib, prefix):
     api["rtx_emit"] = _bind(lib, prefix + "rtx_emit", C.c_int,
                             [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                              C.c_uint64, P(C.c_uint32), P(C.c_uint64)])
+    api["rtx_emit_bucket"] = _bind(lib, prefix + "rtx_emit_bucket", C.c_int,
+                                   [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint32),
+                                    P(C.c_uint64)])
     api["add_transport"] = _bind(lib, prefix + "add_transport", C.c_int32, [e, P(lkf_transport_params)])
     api["set_downtrack_transport"] = _bind(lib, prefix + "set_downtrack_transport", C.c_int, [e, C.c_int32, C.c_int32])
     api["protect"] = _bind(lib, prefix + "protect", C.c_int, [e, C.c_int64])

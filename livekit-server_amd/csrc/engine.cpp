@@ -321,6 +321,15 @@ struct lkf_engine {
   IngParsed *dParsed = nullptr;
   lkf_flow *dFlows = nullptr;
   uint32_t *dTwcc = nullptr;  // per datagram TWCC push word of the last ingest
+  // the receivers' RTX buckets (kernels.h BucketState): per stream state, slot
+  // tags / batch owners / bytes, per datagram slot
+  BucketState *dBkt = nullptr;
+  uint32_t *dBktTag = nullptr, *dBktOwner = nullptr, *dBktSlotOf = nullptr;
+  uint8_t *dBktRing = nullptr;
+  uint64_t bktSlots = 0, bktCap = 0;
+  int32_t *dBktStream = nullptr;
+  uint16_t *dBktSn = nullptr;
+  uint32_t bktReadCap = 0;
   uint32_t *dFwdFlag = nullptr;
   uint64_t *dPos = nullptr, *dIPartA = nullptr, *dIPartB = nullptr, *dITotal = nullptr;
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
@@ -589,6 +598,44 @@ static int flush_topology(lkf_engine *e) {
   if (!e->pendStreams.empty()) {
     const size_t first = e->streams.size() - e->pendStreams.size();
     const size_t k = e->pendStreams.size();
+    {  // RTX buckets (buffer/factory.go:31-44): audio 200 slots, video PacketBufferSize
+      std::vector<BucketState> bs(k);
+      uint64_t need = 0;
+      for (size_t i = 0; i < k; i++) {
+        const bool audio = e->tracks[e->streams[first + i].track].kind == LKF_KIND_AUDIO;
+        std::memset(&bs[i], 0, sizeof(BucketState));
+        bs[i].base = uint32_t(e->bktSlots + need);
+        bs[i].maxSteps = audio ? 200u : e->cfg.seq_size;
+        need += bs[i].maxSteps;
+      }
+      const uint64_t total = e->bktSlots + need;
+      if (total * kBktSlot >= (uint64_t(1) << 32)) return LKF_ENOSPC;  // (32-bit ring offsets)
+      if (!e->dBkt) HIPCHK(dalloc(&e->dBkt, e->maxStreams), "alloc buckets");
+      if (total > e->bktCap) {
+        const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(total, 2 * e->bktCap), ((uint64_t(1) << 32) - 1) / kBktSlot);
+        uint32_t *tag = nullptr, *own = nullptr;
+        uint8_t *ring = nullptr;
+        HIPCHK(dalloc(&tag, cap), "alloc bucket tags");
+        HIPCHK(dalloc(&own, cap), "alloc bucket owners");
+        HIPCHK(dalloc(&ring, cap * kBktSlot), "alloc bucket ring");
+        if (e->bktSlots) {
+          HIPCHK(hipMemcpy(tag, e->dBktTag, e->bktSlots * 4, hipMemcpyDeviceToDevice), "bucket tags copy");
+          HIPCHK(hipMemcpy(ring, e->dBktRing, e->bktSlots * kBktSlot, hipMemcpyDeviceToDevice), "bucket ring copy");
+        }
+        for (void *p : {static_cast<void *>(e->dBktTag), static_cast<void *>(e->dBktOwner),
+                        static_cast<void *>(e->dBktRing)})
+          if (p) HIPCHK(hipFree(p), "free bucket");
+        e->dBktTag = tag;
+        e->dBktOwner = own;
+        e->dBktRing = ring;
+        e->bktCap = cap;
+      }
+      if (!e->dBktSlotOf) HIPCHK(dalloc(&e->dBktSlotOf, e->cfg.max_batch_pkts), "alloc bucket slots");
+      HIPCHK(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(e->dBktTag + e->bktSlots), 0xFFFF0000u, need),
+             "bucket tags init");  // every slot invalid (NewBucket)
+      HIPCHK(hipMemcpy(e->dBkt + first, bs.data(), k * sizeof(BucketState), hipMemcpyHostToDevice), "buckets upload");
+      e->bktSlots = total;
+    }
     bool anyNack = false;
     for (const auto &d : e->pendStreams) anyNack = anyNack || d.nack;
     if (anyNack && !e->dNack) {  // nack.NewNACKQueue for the first Buffer with NACK feedback
@@ -852,7 +899,8 @@ void lkf_destroy(lkf_engine *e) {
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
-                  e->dTwcc, e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
+                  e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktSlotOf, e->dBktRing, e->dBktStream, e->dBktSn,
+                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
                   e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut,
@@ -2069,6 +2117,9 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
   return LKF_OK;
 }
 
+static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const uint8_t *srcArena,
+                           const std::vector<uint16_t> &srcHdr, lkf_out *out, uint8_t *out_arena, uint64_t out_cap,
+                           uint32_t *n_out, uint64_t *out_len);
 int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
                  uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
                  uint64_t *out_len) {
@@ -2096,6 +2147,24 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   if (src_len) HIPCHK(hipMemcpy(e->dRtxIn, src_arena, src_len, hipMemcpyHostToDevice), "src arena copy");
   rc = upload_done(e);
   if (rc) return rc;
+  std::vector<uint16_t> hdr(n, 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (!src[i].len) continue;
+    const uint8_t *b = src_arena + src[i].off;
+    uint32_t h = 12 + 4 * (b[0] & 0xf);
+    if ((b[0] & 0x10) && h + 4 <= src[i].len) h += 4 + 4 * ((uint32_t(b[h + 2]) << 8) | b[h + 3]);
+    hdr[i] = uint16_t(h);
+  }
+  return rtx_emit_common(e, rtx, n, e->dRtxIn, hdr, out, out_arena, out_cap, n_out, out_len);
+}
+
+// The retransmissions from device-side sources (dRtx / dRtxSrc filled; srcArena:
+// the bytes they index): sizes, offsets, wire bytes, then sendingPacket per
+// retransmission (srcHdr[i]: the source header's size).
+static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const uint8_t *srcArena,
+                           const std::vector<uint16_t> &srcHdr, lkf_out *out, uint8_t *out_arena, uint64_t out_cap,
+                           uint32_t *n_out, uint64_t *out_len) {
+  int rc = LKF_OK;
   const uint8_t *rtxDD = nullptr;
   if (e->nSeqDD) {  // epm.ddBytes of each record (its sequencer slot)
     if (n > e->rtxDDCap) {
@@ -2107,7 +2176,7 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
            "rtx dd");
     rtxDD = e->dRtxDD;
   }
-  HIPCHK(launch_rtx_emit(e->own, false, n, e->dRtx, e->dRtxSrc, e->dRtxIn, e->dDTs, e->dTracks, e->dRtxLen, nullptr,
+  HIPCHK(launch_rtx_emit(e->own, false, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen, nullptr,
                          nullptr, rtxDD),
          "rtx size");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
@@ -2134,7 +2203,7 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   HIPCHK(hipMemcpy(e->dRtxOff, off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice), "off copy");
   rc = upload_done(e);
   if (rc) return rc;
-  HIPCHK(launch_rtx_emit(e->own, true, n, e->dRtx, e->dRtxSrc, e->dRtxIn, e->dDTs, e->dTracks, e->dRtxLen, e->dRtxOff,
+  HIPCHK(launch_rtx_emit(e->own, true, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen, e->dRtxOff,
                          e->dRtxOut, rtxDD),
          "rtx write");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
@@ -2144,10 +2213,7 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
     std::vector<SenderUpd> ul;
     for (uint32_t i = 0; i < n; i++) {
       if (!len[i]) continue;
-      const uint8_t *b = src_arena + src[i].off;
-      const uint32_t cc = b[0] & 0xf;
-      uint32_t h = 12 + 4 * cc;
-      if ((b[0] & 0x10) && h + 4 <= src[i].len) h += 4 + 4 * ((uint32_t(b[h + 2]) << 8) | b[h + 3]);
+      const uint32_t h = srcHdr[i];
       const uint8_t *w = out_arena + off[i];  // the RTX header as written (CSRCs, pacer extension block)
       uint32_t outHdr = 12 + 4 * uint32_t(w[0] & 0xf);
       if (w[0] & 0x10) outHdr += 4 + 4 * ((uint32_t(w[outHdr + 2]) << 8) | w[outHdr + 3]);
@@ -2180,6 +2246,66 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
     o.layer = rtx[i].meta.layer;
   }
   return LKF_OK;
+}
+
+// Receiver.ReadRTP(layer, sourceSeqNo) (receiver.go:559-566) from the GPU
+// buckets: the DownTrack's track buffer of the record's layer (an SVC track's
+// single buffer; a closed buffer returns io.EOF), Bucket.GetPacket on the
+// device, then the retransmissions as lkf_rtx_emit.
+int lkf_rtx_emit_bucket(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *out, uint8_t *out_arena,
+                        uint64_t out_cap, uint32_t *n_out, uint64_t *out_len) {
+  if (!e || !n_out || !out_len || (n && !rtx)) return LKF_EINVAL;
+  *n_out = 0;
+  *out_len = 0;
+  if (!n) return LKF_OK;
+  for (uint32_t i = 0; i < n; i++)
+    if (rtx[i].dt < 0 || rtx[i].dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  rc = drain_streams(e);
+  if (rc) return rc;
+  rc = rtx_reserve(e, n);
+  if (rc) return rc;
+  std::vector<int32_t> sid(n, -1);
+  std::vector<uint16_t> sn(n);
+  {
+    std::vector<std::vector<int32_t>> byTrack(e->tracks.size());
+    for (size_t s = 0; s < e->streams.size(); s++) byTrack[size_t(e->streams[s].track)].push_back(int32_t(s));
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t t = e->dtp[size_t(rtx[i].dt)].track;
+      sn[i] = rtx[i].meta.source_sn;
+      if (!e->trackActive[t]) continue;
+      const auto &v = byTrack[t];
+      const int layer = rtx[i].meta.layer < 0 ? 0 : rtx[i].meta.layer;
+      if (v.size() == 1) {
+        sid[i] = v[0];
+      } else {
+        for (int32_t s : v)
+          if (e->streams[size_t(s)].layer == layer) sid[i] = s;
+      }
+    }
+  }
+  if (!e->bktSlots) std::fill(sid.begin(), sid.end(), -1);
+  if (n > e->bktReadCap) {
+    if (e->dBktStream) (void)hipFree(e->dBktStream);
+    if (e->dBktSn) (void)hipFree(e->dBktSn);
+    e->bktReadCap = std::max<uint32_t>(n, 1024);
+    HIPCHK(dalloc(&e->dBktStream, e->bktReadCap), "alloc bucket reads");
+    HIPCHK(dalloc(&e->dBktSn, e->bktReadCap), "alloc bucket read sns");
+  }
+  HIPCHK(hipMemcpy(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice), "rtx copy");
+  HIPCHK(hipMemcpy(e->dBktStream, sid.data(), n * sizeof(int32_t), hipMemcpyHostToDevice), "bucket read copy");
+  HIPCHK(hipMemcpy(e->dBktSn, sn.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice), "bucket sn copy");
+  rc = upload_done(e);
+  if (rc) return rc;
+  HIPCHK(launch_bucket_read(e->own, n, e->dBktStream, e->dBktSn, e->dBkt, e->dBktTag, e->dBktRing, e->dRtxSrc),
+         "bucket read");
+  std::vector<lkf_raw_pkt> src(n);
+  HIPCHK(hipMemcpyAsync(src.data(), e->dRtxSrc, n * sizeof(lkf_raw_pkt), hipMemcpyDeviceToHost, e->own), "src back");
+  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  std::vector<uint16_t> hdr(n, 0);
+  for (uint32_t i = 0; i < n; i++) hdr[i] = uint16_t(src[i].len ? src[i].reserved : 0);
+  return rtx_emit_common(e, rtx, n, e->dBktRing, hdr, out, out_arena, out_cap, n_out, out_len);
 }
 
 // ---- padding / blank frames (downtrack.go:764-859, :1307-1401) -------------
@@ -3017,6 +3143,27 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   if (e->dNack && n) {  // this ingest's RTCP NACKs start empty
     HIPCHK(hipMemsetAsync(e->dNackInfo, 0, size_t(n) * sizeof(uint32_t), s), "memset");
     HIPCHK(hipMemsetAsync(e->dNackPairCnt, 0, sizeof(uint32_t), s), "memset");
+  }
+  BucketLaunch bl;
+  if (e->bktSlots) {
+    bl.raws = dRaws;
+    bl.raw = dRaw;
+    bl.n = n;
+    bl.streams = e->dStreams;
+    bl.nstreams = uint32_t(e->streams.size());
+    bl.tBegin = e->dITBegin;
+    bl.tEnd = e->dITEnd;
+    bl.list = e->dIList;
+    bl.listCnt = e->dIListCnt;
+    bl.listStride = e->cfg.max_batch_pkts;
+    bl.flows = e->dFlows;
+    bl.fwd = e->dFwdFlag;
+    bl.state = e->dBkt;
+    bl.tag = e->dBktTag;
+    bl.owner = e->dBktOwner;
+    bl.slotOf = e->dBktSlotOf;
+    bl.ring = e->dBktRing;
+    a.bucket = &bl;
   }
   const bool dd = e->nDDStreams != 0;
   a.ddStates = dd ? e->dDDIng : nullptr;

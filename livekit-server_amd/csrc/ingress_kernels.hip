@@ -34,6 +34,7 @@ using u8 = uint8_t;
 using u16 = uint16_t;
 using u32 = uint32_t;
 using u64 = uint64_t;
+using i16 = int16_t;
 using i32 = int32_t;
 using i64 = int64_t;
 
@@ -924,6 +925,7 @@ __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring
     }
     f.ext_sn = rsn.extVal - adj;
     if (dup) break;  // the RTX bucket already holds it (ErrRTXPacket)
+    f.flags |= LKF_FLOW_BUCKET;  // AddPacketWithSequenceNumber (k_bkt_add decides, in stream order)
     // getExtPacket (buffer.go:599-671): the dependency descriptor first
     if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
       bool limit = false;
@@ -1160,7 +1162,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
       f.pkt = 0xffffffffu;
       f.ext_sn = ext - sh.rmOpenValue;
       f.ext_ts = extTs;
-      f.flags = LKF_FLOW_FORWARD;
+      f.flags = LKF_FLOW_FORWARD | LKF_FLOW_BUCKET;
       if (gs > 1) {
         f.flags |= LKF_FLOW_HAS_LOSS;
         f.loss_start = ext - gs + 1;
@@ -1772,6 +1774,10 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
     hipLaunchKernelGGL(k_ing_stream_wave, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams, a.hot,
                        a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs, a.ingDD,
                        a.err, a.list, a.listCnt, a.listStride);
+  if (a.bucket) {  // the RTX buckets (before the ExtPackets: a rejected packet produces none)
+    const hipError_t r = launch_bucket_add(st, *a.bucket);
+    if (r != hipSuccess) return r;
+  }
   if (a.nack && a.nstreams)  // after the flows: the loss ranges it pushes
     hipLaunchKernelGGL(k_ing_nack, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.flows, a.streams, a.nack,
                        a.hot, a.tBegin, a.tEnd, a.list, a.listCnt, a.listStride, a.nackInfo, a.nackPairOff,
@@ -1781,6 +1787,145 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
   if (r != hipSuccess) return r;
   hipLaunchKernelGGL(k_ing_out, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.parsed, a.streams, a.fwd, a.pos,
                      a.n, a.flows, a.out, a.ingDD, a.outDD);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The RTX bucket (bucket_oracle.h restates it): k_bkt_add walks each stream's
+// datagrams of the batch in order (one thread per stream: index arithmetic
+// only) and decides AddPacketWithSequenceNumber for those that reached it —
+// push (invalidate the skipped slots, store at the new head) or set (too old:
+// rejected; the slot already holds the SN: ErrRTXPacket) — on the slot tags;
+// a rejected packet produces no ExtPacket.  k_bkt_store then copies each
+// stored datagram whose slot no later datagram of the batch took (one wave
+// per datagram, 4-byte words), its SN field set to the adjusted SN.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
+  const u32 sid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sid >= A.nstreams) return;
+  const DevStream s = A.streams[sid];
+  if (s.closed) return;
+  const u32 pb = A.tBegin[s.track], pe = A.tEnd[s.track];
+  if (pb >= pe) return;
+  BucketState b = A.state[sid];
+  u32 *tag = A.tag + b.base, *owner = A.owner + b.base;
+  const bool useList = s.layer < 3;
+  const u32 nIdx = useList ? A.listCnt[s.track * 3 + s.layer] : pe - pb;
+  const u32 *lst = A.list + size_t(useList ? s.layer : 0) * A.listStride + pb;
+  const int M = int(b.maxSteps);
+  auto wrap = [&](int x) {
+    x %= M;
+    return x < 0 ? x + M : x;
+  };
+  for (u32 k = 0; k < nIdx; k++) {
+    const u32 ic = useList ? lst[k] : pb + k;
+    if (A.raws[ic].stream != sid) continue;
+    const u8 fl = A.flows[ic].flags;
+    if (!(fl & LKF_FLOW_BUCKET)) continue;
+    const u16 sn = u16(A.flows[ic].ext_sn);
+    const u32 len = A.raws[ic].len;
+    int slot = -1;
+    if (len <= 1498) {
+      if (!b.init) {
+        b.head = u16(sn - 1);
+        b.init = 1;
+      }
+      const u16 diff = u16(sn - b.head);
+      if (diff == 0 || diff > (1u << 15)) {  // set
+        const int back = int(u16(b.head - sn));
+        if (back < M) {
+          const int sl = wrap(int(b.step) - back - 1);
+          const u32 t = tag[sl];
+          if (!((t >> 16) != 0xFFFFu && u16(t) == sn)) slot = sl;  // (a duplicate is not overwritten)
+        }
+      } else {  // push
+        const int gap = int(diff) - 1;
+        b.head = sn;
+        for (int i = 0; i < min(gap, M); i++) {
+          const int sl = wrap(int(b.step) + i);
+          tag[sl] = 0xFFFF0000u;
+          owner[sl] = 0xFFFFFFFFu;
+        }
+        slot = wrap(int(b.step) + gap);
+        b.step = u32(wrap(int(b.step) + gap + 1));
+      }
+    }
+    if (slot >= 0) {
+      tag[slot] = (len << 16) | sn;
+      owner[slot] = ic;
+      A.slotOf[ic] = b.base + u32(slot);
+    } else {  // ErrPacketTooOld / ErrRTXPacket: no ExtPacket
+      A.flows[ic].flags = u8(fl & ~(LKF_FLOW_BUCKET | LKF_FLOW_FORWARD));
+      A.fwd[ic] = 0;
+    }
+  }
+  A.state[sid] = b;
+}
+
+__global__ void __launch_bounds__(64) k_bkt_store(BucketLaunch A) {
+  const u32 ic = blockIdx.x, lane = threadIdx.x;
+  if (ic >= A.n) return;
+  if (!(A.flows[ic].flags & LKF_FLOW_BUCKET)) return;
+  const u32 slot = A.slotOf[ic];
+  if (A.owner[slot] != ic) return;  // a later datagram of the batch took the slot
+  const lkf_raw_pkt rp = A.raws[ic];
+  const u16 sn = u16(A.flows[ic].ext_sn);
+  u8 *dst = A.ring + size_t(slot) * kBktSlot + 16;
+  const u8 *src = A.raw + rp.off;
+  const u32 nw = (rp.len + 3) / 4;
+  if ((rp.off & 3) == 0) {
+    for (u32 w = lane; w < nw; w += 64) {
+      u32 v = reinterpret_cast<const u32 *>(src)[w];
+      if (w == 0) v = (v & 0x0000FFFFu) | (u32(sn >> 8) << 16) | (u32(sn & 255) << 24);  // SN field (bytes 2-3)
+      reinterpret_cast<u32 *>(dst)[w] = v;
+    }
+  } else {
+    for (u32 j = lane; j < rp.len; j += 64) dst[j] = j == 2 ? u8(sn >> 8) : j == 3 ? u8(sn) : src[j];
+  }
+}
+
+__global__ void k_bkt_read(u32 n, const int32_t *__restrict__ stream, const u16 *__restrict__ sns,
+                           const BucketState *__restrict__ state, const u32 *__restrict__ tag,
+                           const u8 *__restrict__ ring, lkf_raw_pkt *__restrict__ src) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  lkf_raw_pkt r = {};
+  const int32_t sid = stream[i];
+  if (sid >= 0) {
+    const BucketState b = state[sid];
+    const u16 sn = sns[i];
+    const int diff = int(i16(u16(b.head - sn)));
+    const int M = int(b.maxSteps);
+    if (b.init && diff >= 0 && diff < M) {  // else ErrPacketTooNew / ErrPacketTooOld
+      int sl = (int(b.step) - diff - 1) % M;
+      if (sl < 0) sl += M;
+      const u32 t = tag[b.base + u32(sl)];
+      if ((t >> 16) != 0xFFFFu && u16(t) == sn) {  // else ErrPacketSizeInvalid / ErrPacketMismatch
+        const size_t off = size_t(b.base + u32(sl)) * kBktSlot + 16;
+        const u8 *p = ring + off;
+        const u32 len = t >> 16;
+        u32 h = 12 + 4 * (p[0] & 15);
+        if ((p[0] & 0x10) && h + 4 <= len) h += 4 + 4 * ((u32(p[h + 2]) << 8) | p[h + 3]);
+        r.off = u32(off);
+        r.len = len;
+        r.reserved = h;
+      }
+    }
+  }
+  src[i] = r;
+}
+
+hipError_t launch_bucket_add(hipStream_t st, const BucketLaunch &a) {
+  if (a.n == 0 || a.nstreams == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bkt_add, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(k_bkt_store, dim3(a.n), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_bucket_read(hipStream_t st, u32 n, const int32_t *stream, const u16 *sn, const BucketState *state,
+                              const u32 *tag, const u8 *ring, lkf_raw_pkt *src) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_bkt_read, dim3(nblk(n, 64)), dim3(64), 0, st, n, stream, sn, state, tag, ring, src);
   return hipGetLastError();
 }
 

@@ -83,6 +83,7 @@ hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t
                        const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
                        uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB,
                        const uint32_t *perm, uint32_t *gFirst = nullptr, uint64_t gCap = 0);
+struct BucketLaunch;
 struct IngestLaunch {
   const lkf_raw_pkt *raws;
   uint32_t n;
@@ -116,7 +117,41 @@ struct IngestLaunch {
   uint32_t *nackInfo, *nackPairOff, *nackPairCnt;
   lkf_nack_pair *nackPairs;
   uint32_t nackPairCap;
+  const BucketLaunch *bucket = nullptr;  // the RTX buckets (nullptr: none)
 };
+// The receivers' RTX buckets (mediatransportutil bucket, buffer.go:471; oracle
+// bucket_oracle.h): per stream a ring of maxSteps slots of kBktSlot bytes (the
+// packet at +16), its logical state (size << 16 | stored SN; size 0xFFFF =
+// invalid) in tag, the batch's last writer of a slot in owner.
+constexpr uint32_t kBktSlot = 1536;
+struct BucketState {  // 16 B
+  uint32_t base;      // first slot of the stream's ring
+  uint32_t maxSteps;  // 200 (audio) / PacketBufferSize (video)
+  uint32_t step;
+  uint16_t head;
+  uint8_t init, pad;
+};
+struct BucketLaunch {
+  const lkf_raw_pkt *raws;
+  const uint8_t *raw;
+  uint32_t n;
+  const DevStream *streams;
+  uint32_t nstreams;
+  const uint32_t *tBegin, *tEnd, *list, *listCnt;
+  uint32_t listStride;
+  lkf_flow *flows;
+  uint32_t *fwd;
+  BucketState *state;
+  uint32_t *tag, *owner, *slotOf;  // slotOf: per datagram, the slot it was stored in
+  uint8_t *ring;
+};
+hipError_t launch_bucket_add(hipStream_t s, const BucketLaunch &a);
+// Bucket.GetPacket for RTX records: stream[i] (-1: no buffer / closed) and the
+// source SN; src[i] = (offset of the stored packet in the ring, its length, its
+// header size in reserved) or len 0
+hipError_t launch_bucket_read(hipStream_t s, uint32_t n, const int32_t *stream, const uint16_t *sn,
+                              const BucketState *state, const uint32_t *tag, const uint8_t *ring, lkf_raw_pkt *src);
+
 // lkf_ingest_nacks: the last ingest's RTCP NACKs compacted in datagram order
 hipError_t launch_nack_compact(hipStream_t s, uint32_t n, const lkf_raw_pkt *raws, const DevStream *streams,
                                const uint32_t *info, const uint32_t *pairOff, const lkf_nack_pair *pairs,

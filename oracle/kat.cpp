@@ -329,6 +329,7 @@ KAT(wraparound_uint32) {
 #include "kat_red.inc"
 #include "kat_tracker.inc"
 #include "kat_nack.inc"
+#include "kat_bucket.inc"
 
 int main(int argc, char **argv) {
   bool list = false;

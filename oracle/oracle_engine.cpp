@@ -22,6 +22,7 @@
 #include <memory>
 #include <thread>
 
+#include "bucket_oracle.h"
 #include "../include/lkfwd.h"
 #include "lkf_oracle.h"
 #include "srtp_oracle.h"
@@ -90,6 +91,7 @@ struct OStream {
   u32 latestTSForAudioLevel = 0;
   std::unique_ptr<NackQueue> nacker;  // codecs with NACK feedback (buffer.go:248-256)
   bool closed = false;                // Buffer.Close (buffer.go:337-352)
+  std::unique_ptr<orc_bucket::Bucket> bucket;  // the RTX bucket (video PacketBufferSize slots, audio 200)
   u64 nacks = 0;                      // rtpStats.nacks (UpdateNack, rtpstats_base.go:315-324)
 };
 
@@ -777,6 +779,40 @@ int orc_rtx_lookup(orc_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
 // pacer's extension block (pacer/base.go:71-100: extensions cleared, the DD
 // element for a DownTrack with the DD extension — not kept by this engine's
 // sequencer, see lkfwd.h — and abs-send-time as a 3-byte placeholder).
+// Receiver.ReadRTP(layer, sourceSeqNo) for each record (receiver.go:559-566):
+// the track's buffer of the record's layer (an SVC track's single buffer),
+// Bucket.GetPacket; then the retransmissions as orc_rtx_emit.
+int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
+                 uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
+                 uint64_t *out_len);
+int orc_rtx_emit_bucket(orc_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *out, uint8_t *out_arena,
+                        uint64_t out_cap, uint32_t *n_out, uint64_t *out_len) {
+  std::vector<lkf_raw_pkt> src(n);
+  std::vector<u8> arena;
+  for (u32 i = 0; i < n; i++) {
+    std::memset(&src[i], 0, sizeof(lkf_raw_pkt));
+    if (rtx[i].dt < 0 || rtx[i].dt >= (int)e->dts.size()) return LKF_EINVAL;
+    const u32 track = u32(e->dts[rtx[i].dt]->p.track);
+    int only = -1, match = -1, count = 0;
+    for (size_t s = 0; s < e->streams.size(); s++) {
+      if (u32(e->streams[s]->p.track) != track) continue;
+      count++;
+      only = int(s);
+      if (e->streams[s]->p.layer == (rtx[i].meta.layer < 0 ? 0 : rtx[i].meta.layer)) match = int(s);
+    }
+    const int s = count == 1 ? only : match;
+    if (s < 0 || e->streams[s]->closed) continue;  // ErrBufferNotFound / io.EOF
+    const u8 *p = nullptr;
+    int len = 0;
+    if (e->streams[s]->bucket->Get(rtx[i].meta.source_sn, p, len) != orc_bucket::OK) continue;
+    src[i].off = u32(arena.size());
+    src[i].len = u32(len);
+    arena.insert(arena.end(), p, p + len);
+  }
+  arena.resize(arena.size() + 64);
+  return orc_rtx_emit(e, rtx, n, src.data(), arena.data(), arena.size(), out, out_arena, out_cap, n_out, out_len);
+}
+
 int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
                  uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
                  uint64_t *out_len) {
@@ -1433,6 +1469,8 @@ int32_t orc_add_stream(orc_engine *e, const lkf_stream_params *p) {
     s->level = std::make_unique<AudioLevel>(ap);
   }
   if (p->dd_ext) s->ddParser = std::make_unique<DependencyDescriptorParser>();
+  // buffer/factory.go:31-44: audio buckets 200 packets, video PacketBufferSize
+  s->bucket = std::make_unique<orc_bucket::Bucket>(e->tracks[p->track].p.kind == LKF_KIND_AUDIO ? 200 : int(e->seqSize));
   if (p->nack) {  // nack.NewNACKQueue(nack.NackQueueParamsDefault), then Buffer.SetRTT
     s->nacker = std::make_unique<NackQueue>();
     if (p->rtt_ms) s->nacker->SetRTT(p->rtt_ms);
@@ -1503,10 +1541,13 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
     return f;
   }
   f.ext_sn = fs.ExtSequenceNumber - adj;
-  // bucket.AddPacketWithSequenceNumber rejects a packet it already holds
-  // (ErrRTXPacket): a duplicate produces no ExtPacket.  Other bucket
-  // outcomes (size-dependent ErrPacketTooOld) are not modelled.
+  // bucket.AddPacketWithSequenceNumber (buffer.go:471-481) under the adjusted
+  // SN: a packet the bucket already holds (ErrRTXPacket — every duplicate,
+  // which therefore skips the add) or one older than its window
+  // (ErrPacketTooOld) produces no ExtPacket.
   if (fs.IsDuplicate) return f;
+  if (b.bucket->Add(buf, int(rp.len), u16(f.ext_sn)) != orc_bucket::OK) return f;
+  f.flags |= LKF_FLOW_BUCKET;
   // getExtPacket
   std::memset(&ep, 0, sizeof(ep));
   std::memset(&epd, 0, sizeof(epd));

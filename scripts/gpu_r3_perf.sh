@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${OUT_NAME:-r3_perf}
 mkdir -p $O
 st() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; grep '^{' $O/$name.log | tail -1 > $O/$name.json; tail -1 $O/$name.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc; }
-st micro 120 ./scripts/micro/fetch_calib 1024
+[ "${RUN_MICRO:-0}" = "1" ] && st micro 120 ./scripts/micro/fetch_calib 1024
 st bench_c2 300 python3 bench.py --steps 20 --warmup 5
 st bench_c2_sync 300 python3 bench.py --steps 20 --warmup 5 --sync-each --no-cpu-baseline
 for c in 1 3 4 5; do st bench_c$c 400 python3 bench.py --config $c --steps 10 --warmup 3; done

@@ -15,7 +15,7 @@ from collections import defaultdict
 
 def short_name(name):
     """'void lkf::k_emit<96>(lkf::EmitArgs)' -> 'lkf::k_emit<96>' (template kernels carry a return type)"""
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     return n[5:] if n.startswith("void ") else n
 
 

@@ -75,6 +75,40 @@ def rtx_emit(api, h, trace, rtx, idx):
     return out[:k.value], wire[:ol.value]
 
 
+def rtx_emit_bucket(api, h, rtx, cap_per=1700):
+    """lkf_rtx_emit_bucket: the sources read from the receivers' buckets."""
+    n = len(rtx)
+    out = np.zeros(max(1, n), dtype=abi.OUT_DTYPE)
+    cap = cap_per * n + 64
+    wire = np.zeros(cap, dtype=np.uint8)
+    k = C.c_uint32()
+    ol = C.c_uint64()
+    rc = api["rtx_emit_bucket"](h, rtx.ctypes.data, n, out.ctypes.data, wire.ctypes.data, cap, C.byref(k),
+                                C.byref(ol))
+    assert rc == 0, rc
+    return out[:k.value], wire[:ol.value]
+
+
+def ingest_forward(api, h, trace, workload, nb, run):
+    """Raw datagrams through lkf_ingest (the buckets fill), then the ingested
+    ExtPackets forwarded: run(b, ingested lkf_pkt bytes, count, arena, len)."""
+    for b in range(nb):
+        workload.queue_events(api, h, trace, b)
+        rp, n, ar, alen = trace.batch_raw(b)
+        assert api["ingest"](h, rp, n, ar, alen) == 0
+        k = C.c_uint32()
+        rc = api["ingested"](h, None, 0, C.byref(k))
+        assert rc in (0, -28)
+        arr = (abi.lkf_pkt * max(1, k.value))()
+        assert api["ingested"](h, arr, k.value, C.byref(k)) == 0
+        run(b, arr, k.value, ar, alen)
+
+
+def wire_by_rtx(out, wire):
+    """RTX index (lkf_out.pkt) -> its wire packet."""
+    return {int(r["pkt"]): bytes(wire[int(r["out_off"]):int(r["out_off"]) + int(r["out_len"])]) for r in out}
+
+
 def count_dd_elements(trace, out, wire):
     """RTX packets whose extension block carries the DownTrack's DD element."""
     k = 0

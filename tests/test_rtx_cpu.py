@@ -140,3 +140,32 @@ def test_oracle_rtx_keeps_dependency_descriptor(workload):
     finally:
         o.destroy(h)
         tr.close()
+
+
+def test_oracle_rtx_from_bucket(workload):
+    """The receivers' buckets (bucket_oracle.h) filled by ingest give the same
+    retransmissions as the trace's own packets, wherever the bucket still
+    holds the source (audio buckets keep 200 packets, video 500)."""
+    o = load_oracle()
+    tr = workload.Trace(2, duration_s=3.0, batch_s=1.0, rooms=2, seed=11, loss=0.02, reorder=0.01)
+    nb = 3
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        workload.load_streams(o.api, h, tr)
+        rtx_lib.ingest_forward(o.api, h, tr, workload, nb,
+                               lambda b, pk, n, ar, alen: o.run(h, pk if n else None, n, ar, alen))
+        nacks = rtx_lib.make_nacks(o.api, h, tr, seed=6)
+        r = rtx_lib.rtx_lookup(o.api, h, nacks, EPOCH + nb * 10**9 + 5 * 10**8)
+        assert len(r) > 50
+        idx = rtx_lib.packet_index(tr, nb)
+        io, iw = rtx_lib.rtx_emit(o.api, h, tr, r, idx)
+        bo, bw = rtx_lib.rtx_emit_bucket(o.api, h, r)
+        want, got = rtx_lib.wire_by_rtx(io, iw), rtx_lib.wire_by_rtx(bo, bw)
+        assert set(got) <= set(want)
+        for k, v in got.items():
+            assert v == want[k], k
+        video = [k for k in want if tr.tracks[tr.downtracks[int(r["dt"][k])].track].kind != 0]
+        assert len(got) > 0.6 * len(want) and sum(k in got for k in video) > 0.9 * len(video), (len(got), len(want))
+    finally:
+        o.destroy(h)

@@ -79,3 +79,59 @@ def test_rtx_lookup_rejects_split_lists(pkg, workload):
     finally:
         eng.close()
         tr.close()
+
+
+@pytest.mark.parametrize("cfg", [dict(config=2, rooms=3, seed=11, loss=0.02, reorder=0.01),
+                                 dict(config=5, rooms=3, svc_dd=1, seed=15)])
+def test_rtx_from_bucket_matches_oracle(pkg, workload, abi, cfg):
+    """Raw datagrams ingested on both sides fill the receivers' buckets (the
+    GPU's in HBM: k_bkt_add / k_bkt_store); the retransmissions read from them
+    (lkf_rtx_emit_bucket: k_bkt_read + k_rtx) must equal the oracle's bucket
+    restatement's, records and wire bytes."""
+    import ctypes as C
+    o = load_oracle()
+    kw = dict(cfg)
+    tr = workload.Trace(kw.pop("config"), duration_s=3.0, batch_s=1.0, **kw)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    nb = 3
+    try:
+        for api, h in ((eng.api, eng.h), (o.api, oh)):
+            workload.load_topology(api, h, tr)
+            workload.load_streams(api, h, tr)
+
+        def run_eng(b, pk, n, ar, alen):
+            eng.run()
+            eng.sync()
+
+        def run_orc(b, pk, n, ar, alen):  # (the ingest's DD side array stays with the oracle, as in test_ingress_gpu)
+            o.run(oh, pk if n else None, n, ar, alen)
+
+        for b in range(nb):  # interleaved: the engine's ingest feeds its next run
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            rp, n, ar, alen = tr.batch_raw(b)
+            eng.ingest(rp, n, ar, alen)
+            assert o.api["ingest"](oh, rp, n, ar, alen) == 0
+            assert np.array_equal(eng.flows()["flags"], pkg.flows_array(o.api, oh)["flags"]), b
+            k = C.c_uint32()
+            assert o.api["ingested"](oh, None, 0, C.byref(k)) in (0, -28)
+            arr = (abi.lkf_pkt * max(1, k.value))()
+            assert o.api["ingested"](oh, arr, k.value, C.byref(k)) == 0
+            run_eng(b, None, 0, ar, alen)
+            run_orc(b, arr, k.value, ar, alen)
+        nacks = rtx_lib.make_nacks(o.api, oh, tr, seed=7)
+        now = EPOCH + nb * 10**9 + 5 * 10**8
+        g = rtx_lib.rtx_lookup(eng.api, eng.h, nacks, now)
+        r = rtx_lib.rtx_lookup(o.api, oh, nacks, now)
+        assert len(g) == len(r) > 20
+        go, gw = rtx_lib.rtx_emit_bucket(eng.api, eng.h, g)
+        oo, ow = rtx_lib.rtx_emit_bucket(o.api, oh, r)
+        assert len(go) == len(oo) > 10, (len(go), len(oo))
+        for f in oo.dtype.names:
+            assert np.array_equal(go[f], oo[f]), f
+        assert np.array_equal(gw, ow)
+        check_sender_stats(pkg, eng.api, eng.h, o.api, oh, range(tr.ndts))
+    finally:
+        o.destroy(oh)
+        eng.close()
