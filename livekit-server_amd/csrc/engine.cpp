@@ -609,10 +609,9 @@ static int flush_topology(lkf_engine *e) {
         need += bs[i].maxSteps;
       }
       const uint64_t total = e->bktSlots + need;
-      if (total * kBktSlot >= (uint64_t(1) << 32)) return LKF_ENOSPC;  // (32-bit ring offsets)
       if (!e->dBkt) HIPCHK(dalloc(&e->dBkt, e->maxStreams), "alloc buckets");
       if (total > e->bktCap) {
-        const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(total, 2 * e->bktCap), ((uint64_t(1) << 32) - 1) / kBktSlot);
+        const uint64_t cap = std::max<uint64_t>(total, 2 * e->bktCap);
         uint32_t *tag = nullptr, *own = nullptr;
         uint8_t *ring = nullptr;
         HIPCHK(dalloc(&tag, cap), "alloc bucket tags");
@@ -2298,14 +2297,20 @@ int lkf_rtx_emit_bucket(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *
   HIPCHK(hipMemcpy(e->dBktSn, sn.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice), "bucket sn copy");
   rc = upload_done(e);
   if (rc) return rc;
-  HIPCHK(launch_bucket_read(e->own, n, e->dBktStream, e->dBktSn, e->dBkt, e->dBktTag, e->dBktRing, e->dRtxSrc),
+  if (uint64_t(n) * kBktSlot + 64 > e->rtxInCap) {
+    if (e->dRtxIn) (void)hipFree(e->dRtxIn);
+    e->rtxInCap = std::max<uint64_t>(uint64_t(n) * kBktSlot + 64, 1 << 20);
+    HIPCHK(dalloc(&e->dRtxIn, e->rtxInCap), "alloc rtx in");
+  }
+  HIPCHK(launch_bucket_read(e->own, n, e->dBktStream, e->dBktSn, e->dBkt, e->dBktTag, e->dBktRing, e->dRtxIn,
+                            e->dRtxSrc),
          "bucket read");
   std::vector<lkf_raw_pkt> src(n);
   HIPCHK(hipMemcpyAsync(src.data(), e->dRtxSrc, n * sizeof(lkf_raw_pkt), hipMemcpyDeviceToHost, e->own), "src back");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
   std::vector<uint16_t> hdr(n, 0);
   for (uint32_t i = 0; i < n; i++) hdr[i] = uint16_t(src[i].len ? src[i].reserved : 0);
-  return rtx_emit_common(e, rtx, n, e->dBktRing, hdr, out, out_arena, out_cap, n_out, out_len);
+  return rtx_emit_common(e, rtx, n, e->dRtxIn, hdr, out, out_arena, out_cap, n_out, out_len);
 }
 
 // ---- padding / blank frames (downtrack.go:764-859, :1307-1401) -------------

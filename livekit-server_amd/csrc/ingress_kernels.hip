@@ -1801,7 +1801,11 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
 // per datagram, 4-byte words), its SN field set to the adjusted SN.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
-  const u32 sid = blockIdx.x * blockDim.x + threadIdx.x;
+  // one wave per stream: lanes gather 64 datagrams' inputs at a time (the
+  // stream's candidates compacted into LDS in order), lane 0 steps the
+  // bucket over them — index arithmetic and tag stores only
+  __shared__ u32 sIc[64], sSn[64], sLen[64];
+  const u32 sid = blockIdx.x, lane = threadIdx.x;
   if (sid >= A.nstreams) return;
   const DevStream s = A.streams[sid];
   if (s.closed) return;
@@ -1817,79 +1821,112 @@ __global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
     x %= M;
     return x < 0 ? x + M : x;
   };
-  for (u32 k = 0; k < nIdx; k++) {
-    const u32 ic = useList ? lst[k] : pb + k;
-    if (A.raws[ic].stream != sid) continue;
-    const u8 fl = A.flows[ic].flags;
-    if (!(fl & LKF_FLOW_BUCKET)) continue;
+  for (u32 base = 0; base < nIdx; base += 64) {
+    const u32 k = base + lane;
+    u32 ic = 0;
+    bool cand = false;
+    if (k < nIdx) {
+      ic = useList ? lst[k] : pb + k;
+      cand = A.raws[ic].stream == sid && (A.flows[ic].flags & LKF_FLOW_BUCKET);
+    }
+    const u64 cm = __ballot(cand);
+    if (cand) {
+      const u32 pos = u32(__popcll(cm & ((1ull << lane) - 1)));
+      sIc[pos] = ic;
+      sSn[pos] = u32(u16(A.flows[ic].ext_sn));
+      sLen[pos] = A.raws[ic].len;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const u32 m = u32(__popcll(cm));
+      for (u32 j = 0; j < m; j++) {
+        const u32 icj = sIc[j], len = sLen[j];
+        const u16 sn = u16(sSn[j]);
+        int slot = -1;
+        if (len <= 1498) {
+          if (!b.init) {
+            b.head = u16(sn - 1);
+            b.init = 1;
+          }
+          const u16 diff = u16(sn - b.head);
+          if (diff == 0 || diff > (1u << 15)) {  // set
+            const int back = int(u16(b.head - sn));
+            if (back < M) {
+              const int sl = wrap(int(b.step) - back - 1);
+              const u32 t = tag[sl];
+              if (!((t >> 16) != 0xFFFFu && u16(t) == sn)) slot = sl;  // (a duplicate is not overwritten)
+            }
+          } else {  // push
+            const int gap = int(diff) - 1;
+            b.head = sn;
+            for (int i = 0; i < min(gap, M); i++) {
+              const int sl = wrap(int(b.step) + i);
+              tag[sl] = 0xFFFF0000u;
+              owner[sl] = 0xFFFFFFFFu;
+            }
+            slot = wrap(int(b.step) + gap);
+            b.step = u32(wrap(int(b.step) + gap + 1));
+          }
+        }
+        if (slot >= 0) {
+          tag[slot] = (len << 16) | sn;
+          owner[slot] = icj;
+          A.slotOf[icj] = b.base + u32(slot);
+        } else {  // ErrPacketTooOld / ErrRTXPacket: no ExtPacket
+          A.flows[icj].flags = u8(A.flows[icj].flags & ~(LKF_FLOW_BUCKET | LKF_FLOW_FORWARD));
+          A.fwd[icj] = 0;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (lane == 0) A.state[sid] = b;
+}
+
+// one wave per datagram at a time, grid-stride; 16-B copies when the source is
+// 16-B aligned (the ring slots are)
+__global__ void __launch_bounds__(256) k_bkt_store(BucketLaunch A) {
+  const u32 lane = threadIdx.x & 63;
+  const u32 w0 = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (u32 ic = w0; ic < A.n; ic += nw) {
+    if (!(A.flows[ic].flags & LKF_FLOW_BUCKET)) continue;
+    const u32 slot = A.slotOf[ic];
+    if (A.owner[slot] != ic) continue;  // a later datagram of the batch took the slot
+    const lkf_raw_pkt rp = A.raws[ic];
     const u16 sn = u16(A.flows[ic].ext_sn);
-    const u32 len = A.raws[ic].len;
-    int slot = -1;
-    if (len <= 1498) {
-      if (!b.init) {
-        b.head = u16(sn - 1);
-        b.init = 1;
+    u8 *dst = A.ring + size_t(slot) * kBktSlot + 16;
+    const u8 *src = A.raw + rp.off;
+    const u32 snw = (u32(sn >> 8) << 16) | (u32(sn & 255) << 24);  // SN field (bytes 2-3), little-endian word 0
+    if ((rp.off & 15) == 0) {
+      for (u32 c = lane; c < (rp.len + 15) / 16; c += 64) {
+        uint4 v = reinterpret_cast<const uint4 *>(src)[c];
+        if (c == 0) v.x = (v.x & 0x0000FFFFu) | snw;
+        reinterpret_cast<uint4 *>(dst)[c] = v;
       }
-      const u16 diff = u16(sn - b.head);
-      if (diff == 0 || diff > (1u << 15)) {  // set
-        const int back = int(u16(b.head - sn));
-        if (back < M) {
-          const int sl = wrap(int(b.step) - back - 1);
-          const u32 t = tag[sl];
-          if (!((t >> 16) != 0xFFFFu && u16(t) == sn)) slot = sl;  // (a duplicate is not overwritten)
-        }
-      } else {  // push
-        const int gap = int(diff) - 1;
-        b.head = sn;
-        for (int i = 0; i < min(gap, M); i++) {
-          const int sl = wrap(int(b.step) + i);
-          tag[sl] = 0xFFFF0000u;
-          owner[sl] = 0xFFFFFFFFu;
-        }
-        slot = wrap(int(b.step) + gap);
-        b.step = u32(wrap(int(b.step) + gap + 1));
+    } else if ((rp.off & 3) == 0) {
+      for (u32 w = lane; w < (rp.len + 3) / 4; w += 64) {
+        u32 v = reinterpret_cast<const u32 *>(src)[w];
+        if (w == 0) v = (v & 0x0000FFFFu) | snw;
+        reinterpret_cast<u32 *>(dst)[w] = v;
       }
+    } else {
+      for (u32 j = lane; j < rp.len; j += 64) dst[j] = j == 2 ? u8(sn >> 8) : j == 3 ? u8(sn) : src[j];
     }
-    if (slot >= 0) {
-      tag[slot] = (len << 16) | sn;
-      owner[slot] = ic;
-      A.slotOf[ic] = b.base + u32(slot);
-    } else {  // ErrPacketTooOld / ErrRTXPacket: no ExtPacket
-      A.flows[ic].flags = u8(fl & ~(LKF_FLOW_BUCKET | LKF_FLOW_FORWARD));
-      A.fwd[ic] = 0;
-    }
-  }
-  A.state[sid] = b;
-}
-
-__global__ void __launch_bounds__(64) k_bkt_store(BucketLaunch A) {
-  const u32 ic = blockIdx.x, lane = threadIdx.x;
-  if (ic >= A.n) return;
-  if (!(A.flows[ic].flags & LKF_FLOW_BUCKET)) return;
-  const u32 slot = A.slotOf[ic];
-  if (A.owner[slot] != ic) return;  // a later datagram of the batch took the slot
-  const lkf_raw_pkt rp = A.raws[ic];
-  const u16 sn = u16(A.flows[ic].ext_sn);
-  u8 *dst = A.ring + size_t(slot) * kBktSlot + 16;
-  const u8 *src = A.raw + rp.off;
-  const u32 nw = (rp.len + 3) / 4;
-  if ((rp.off & 3) == 0) {
-    for (u32 w = lane; w < nw; w += 64) {
-      u32 v = reinterpret_cast<const u32 *>(src)[w];
-      if (w == 0) v = (v & 0x0000FFFFu) | (u32(sn >> 8) << 16) | (u32(sn & 255) << 24);  // SN field (bytes 2-3)
-      reinterpret_cast<u32 *>(dst)[w] = v;
-    }
-  } else {
-    for (u32 j = lane; j < rp.len; j += 64) dst[j] = j == 2 ? u8(sn >> 8) : j == 3 ? u8(sn) : src[j];
   }
 }
 
-__global__ void k_bkt_read(u32 n, const int32_t *__restrict__ stream, const u16 *__restrict__ sns,
-                           const BucketState *__restrict__ state, const u32 *__restrict__ tag,
-                           const u8 *__restrict__ ring, lkf_raw_pkt *__restrict__ src) {
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+// Bucket.GetPacket per RTX record, one wave each: the lookup on every lane
+// (uniform), then the stored bytes gathered into the record's kBktSlot-byte
+// slot of the RTX input buffer (the rings are 64-bit addressed; the RTX
+// kernels take 32-bit offsets into that buffer).
+__global__ void __launch_bounds__(64) k_bkt_read(u32 n, const int32_t *__restrict__ stream,
+                                                 const u16 *__restrict__ sns, const BucketState *__restrict__ state,
+                                                 const u32 *__restrict__ tag, const u8 *__restrict__ ring,
+                                                 u8 *__restrict__ out, lkf_raw_pkt *__restrict__ src) {
+  const u32 i = blockIdx.x, lane = threadIdx.x;
   if (i >= n) return;
-  lkf_raw_pkt r = {};
+  u32 len = 0;
+  const u8 *p = nullptr;
   const int32_t sid = stream[i];
   if (sid >= 0) {
     const BucketState b = state[sid];
@@ -1901,31 +1938,37 @@ __global__ void k_bkt_read(u32 n, const int32_t *__restrict__ stream, const u16 
       if (sl < 0) sl += M;
       const u32 t = tag[b.base + u32(sl)];
       if ((t >> 16) != 0xFFFFu && u16(t) == sn) {  // else ErrPacketSizeInvalid / ErrPacketMismatch
-        const size_t off = size_t(b.base + u32(sl)) * kBktSlot + 16;
-        const u8 *p = ring + off;
-        const u32 len = t >> 16;
-        u32 h = 12 + 4 * (p[0] & 15);
-        if ((p[0] & 0x10) && h + 4 <= len) h += 4 + 4 * ((u32(p[h + 2]) << 8) | p[h + 3]);
-        r.off = u32(off);
-        r.len = len;
-        r.reserved = h;
+        p = ring + size_t(b.base + u32(sl)) * kBktSlot + 16;
+        len = t >> 16;
       }
     }
   }
-  src[i] = r;
+  u8 *dst = out + size_t(i) * kBktSlot;
+  for (u32 w = lane; w < (len + 3) / 4; w += 64) reinterpret_cast<u32 *>(dst)[w] = reinterpret_cast<const u32 *>(p)[w];
+  if (lane == 0) {
+    lkf_raw_pkt r = {};
+    if (len) {
+      u32 h = 12 + 4 * (p[0] & 15);
+      if ((p[0] & 0x10) && h + 4 <= len) h += 4 + 4 * ((u32(p[h + 2]) << 8) | p[h + 3]);
+      r.off = i * kBktSlot;
+      r.len = len;
+      r.reserved = h;
+    }
+    src[i] = r;
+  }
 }
 
 hipError_t launch_bucket_add(hipStream_t st, const BucketLaunch &a) {
   if (a.n == 0 || a.nstreams == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bkt_add, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(k_bkt_store, dim3(a.n), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(k_bkt_add, dim3(a.nstreams), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(k_bkt_store, dim3(std::min<u32>(nblk(a.n, 4), 4096)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_bucket_read(hipStream_t st, u32 n, const int32_t *stream, const u16 *sn, const BucketState *state,
-                              const u32 *tag, const u8 *ring, lkf_raw_pkt *src) {
+                              const u32 *tag, const u8 *ring, u8 *out, lkf_raw_pkt *src) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_bkt_read, dim3(nblk(n, 64)), dim3(64), 0, st, n, stream, sn, state, tag, ring, src);
+  hipLaunchKernelGGL(k_bkt_read, dim3(n), dim3(64), 0, st, n, stream, sn, state, tag, ring, out, src);
   return hipGetLastError();
 }
 

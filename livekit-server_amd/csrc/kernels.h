@@ -147,10 +147,11 @@ struct BucketLaunch {
 };
 hipError_t launch_bucket_add(hipStream_t s, const BucketLaunch &a);
 // Bucket.GetPacket for RTX records: stream[i] (-1: no buffer / closed) and the
-// source SN; src[i] = (offset of the stored packet in the ring, its length, its
-// header size in reserved) or len 0
+// source SN; the packet is gathered to out + i * kBktSlot and src[i] = (that
+// offset, its length, its header size in reserved) or len 0
 hipError_t launch_bucket_read(hipStream_t s, uint32_t n, const int32_t *stream, const uint16_t *sn,
-                              const BucketState *state, const uint32_t *tag, const uint8_t *ring, lkf_raw_pkt *src);
+                              const BucketState *state, const uint32_t *tag, const uint8_t *ring, uint8_t *out,
+                              lkf_raw_pkt *src);
 
 // lkf_ingest_nacks: the last ingest's RTCP NACKs compacted in datagram order
 hipError_t launch_nack_compact(hipStream_t s, uint32_t n, const lkf_raw_pkt *raws, const DevStream *streams,
