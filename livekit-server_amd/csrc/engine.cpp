@@ -66,6 +66,7 @@ struct BatchCtx {
   lkf_pkt *dPktsOwn = nullptr;  // lkf_submit copies land here
   uint8_t *dArenaOwn = nullptr;
   lkf_raw_pkt *dRawPkts = nullptr;  // lkf_ingest copies land here
+  uint64_t *dBktStore = nullptr;    // per datagram: what the bucket store copies (kernels.h BucketLaunch)
   // dependency descriptor (allocated with the first DD track): lkf_submit_dd
   // copies, decoded descriptors, marshalled DD bytes + their bump cursor
   lkf_pkt_dd *dDDIn = nullptr;
@@ -113,6 +114,7 @@ struct lkf_engine {
   hipStream_t sendS = nullptr;  // sender statistics of a decided batch (low priority, beside its emit)
   hipStream_t cur = nullptr;    // caller's stream of the last lkf_run
   hipEvent_t inEv = nullptr;    // caller-stream work before a run
+  hipEvent_t bktEv = nullptr;   // an ingest's bucket decisions (the sender stream copies after it)
   lkf_cfg cfg{};
   std::string err;
 
@@ -324,7 +326,9 @@ struct lkf_engine {
   // the receivers' RTX buckets (kernels.h BucketState): per stream state, slot
   // tags / batch owners / bytes, per datagram slot
   BucketState *dBkt = nullptr;
-  uint32_t *dBktTag = nullptr, *dBktOwner = nullptr, *dBktSlotOf = nullptr;
+  uint32_t *dBktTag = nullptr;
+  uint64_t *dBktOwner = nullptr;
+  uint32_t bktEpoch = 0;
   uint8_t *dBktRing = nullptr;
   uint64_t bktSlots = 0, bktCap = 0;
   int32_t *dBktStream = nullptr;
@@ -612,10 +616,12 @@ static int flush_topology(lkf_engine *e) {
       if (!e->dBkt) HIPCHK(dalloc(&e->dBkt, e->maxStreams), "alloc buckets");
       if (total > e->bktCap) {
         const uint64_t cap = std::max<uint64_t>(total, 2 * e->bktCap);
-        uint32_t *tag = nullptr, *own = nullptr;
+        uint32_t *tag = nullptr;
+        uint64_t *own = nullptr;
         uint8_t *ring = nullptr;
         HIPCHK(dalloc(&tag, cap), "alloc bucket tags");
         HIPCHK(dalloc(&own, cap), "alloc bucket owners");
+        HIPCHK(hipMemset(own, 0, cap * sizeof(uint64_t)), "bucket owners init");  // (epochs start at 1)
         HIPCHK(dalloc(&ring, cap * kBktSlot), "alloc bucket ring");
         if (e->bktSlots) {
           HIPCHK(hipMemcpy(tag, e->dBktTag, e->bktSlots * 4, hipMemcpyDeviceToDevice), "bucket tags copy");
@@ -629,7 +635,6 @@ static int flush_topology(lkf_engine *e) {
         e->dBktRing = ring;
         e->bktCap = cap;
       }
-      if (!e->dBktSlotOf) HIPCHK(dalloc(&e->dBktSlotOf, e->cfg.max_batch_pkts), "alloc bucket slots");
       HIPCHK(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(e->dBktTag + e->bktSlots), 0xFFFF0000u, need),
              "bucket tags init");  // every slot invalid (NewBucket)
       HIPCHK(hipMemcpy(e->dBkt + first, bs.data(), k * sizeof(BucketState), hipMemcpyHostToDevice), "buckets upload");
@@ -736,6 +741,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(hipStreamCreateWithPriority(&e->sendS, hipStreamNonBlocking, leastPrio));
   }
   A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
+  A(hipEventCreateWithFlags(&e->bktEv, hipEventDisableTiming));
   e->cur = e->own;
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
@@ -780,6 +786,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dPktsOwn, c.max_batch_pkts));
     A(dalloc(&x.dArenaOwn, c.max_batch_arena + 64));
     A(dalloc(&x.dRawPkts, c.max_batch_pkts));
+    A(dalloc(&x.dBktStore, c.max_batch_pkts));
     A(dalloc(&x.dDesc, 1));
     A(dalloc(&x.dEvents, 4096));
     A(dalloc(&x.dEvLane, 4096));
@@ -898,7 +905,7 @@ void lkf_destroy(lkf_engine *e) {
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
-                  e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktSlotOf, e->dBktRing, e->dBktStream, e->dBktSn,
+                  e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktRing, e->dBktStream, e->dBktSn,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
@@ -926,7 +933,7 @@ void lkf_destroy(lkf_engine *e) {
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
-                 x.dRawPkts, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane};
+                 x.dRawPkts, x.dBktStore, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane};
     for (void *p : q)
       if (p) (void)hipFree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
@@ -945,6 +952,7 @@ void lkf_destroy(lkf_engine *e) {
   }
   if (e->bounce) (void)hipHostFree(e->bounce);
   if (e->inEv) (void)hipEventDestroy(e->inEv);
+  if (e->bktEv) (void)hipEventDestroy(e->bktEv);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
   if (e->sendS) (void)hipStreamDestroy(e->sendS);
   if (e->decS) (void)hipStreamDestroy(e->decS);
@@ -3166,8 +3174,9 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
     bl.state = e->dBkt;
     bl.tag = e->dBktTag;
     bl.owner = e->dBktOwner;
-    bl.slotOf = e->dBktSlotOf;
+    bl.store = x.dBktStore;
     bl.ring = e->dBktRing;
+    bl.epoch = ++e->bktEpoch;
     a.bucket = &bl;
   }
   const bool dd = e->nDDStreams != 0;
@@ -3176,6 +3185,12 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.ingDD = dd ? e->dIngDD : nullptr;
   a.outDD = dd ? x.dDDIn : nullptr;
   HIPCHK(launch_ingest(s, a), "ingest");
+  if (a.bucket && n) {  // the bucket copies, off the forwarding path: the sender stream (the
+                        // batch context counts as done only after it, like the sender statistics)
+    HIPCHK(hipEventRecord(e->bktEv, s), "event");
+    HIPCHK(hipStreamWaitEvent(e->sendS, e->bktEv, 0), "wait ingest (bucket store)");
+    HIPCHK(launch_bucket_store(e->sendS, bl), "bucket store");
+  }
   HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 8), "ingest error fold");
   e->lastIngestN = n;
   e->ingRaws = dRaws;

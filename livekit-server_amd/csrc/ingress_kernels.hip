@@ -1805,6 +1805,8 @@ __global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
   // stream's candidates compacted into LDS in order), lane 0 steps the
   // bucket over them — index arithmetic and tag stores only
   __shared__ u32 sIc[64], sSn[64], sLen[64];
+  constexpr int kLdsSlots = 2048;
+  __shared__ u32 sOwn[kLdsSlots];  // this ingest's writer of each slot (rings up to 2,048 slots)
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   if (sid >= A.nstreams) return;
   const DevStream s = A.streams[sid];
@@ -1812,7 +1814,27 @@ __global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
   const u32 pb = A.tBegin[s.track], pe = A.tEnd[s.track];
   if (pb >= pe) return;
   BucketState b = A.state[sid];
-  u32 *tag = A.tag + b.base, *owner = A.owner + b.base;
+  u32 *tag = A.tag + b.base;
+  u64 *owner = A.owner + b.base;
+  const u64 ep = u64(A.epoch) << 32;
+  const int Mc = int(b.maxSteps);
+  const bool lds = Mc <= kLdsSlots;
+  if (lds)
+    for (int i = int(lane); i < Mc; i += 64) sOwn[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  // a slot taken again in this ingest: the earlier datagram is not stored
+  // (the LDS map, or for larger rings the global owner tagged with the epoch)
+  auto supersede = [&](int sl, u32 ic) {
+    if (lds) {
+      const u32 o = sOwn[sl];
+      if (o != 0xFFFFFFFFu) A.store[o] = 0;
+      sOwn[sl] = ic;
+    } else {
+      const u64 o = owner[sl];
+      if ((o & 0xFFFFFFFF00000000ull) == ep) A.store[u32(o)] = 0;
+      owner[sl] = ic == 0xFFFFFFFFu ? 0 : (ep | ic);
+    }
+  };
   const bool useList = s.layer < 3;
   const u32 nIdx = useList ? A.listCnt[s.track * 3 + s.layer] : pe - pb;
   const u32 *lst = A.list + size_t(useList ? s.layer : 0) * A.listStride + pb;
@@ -1862,7 +1884,7 @@ __global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
             for (int i = 0; i < min(gap, M); i++) {
               const int sl = wrap(int(b.step) + i);
               tag[sl] = 0xFFFF0000u;
-              owner[sl] = 0xFFFFFFFFu;
+              supersede(sl, 0xFFFFFFFFu);
             }
             slot = wrap(int(b.step) + gap);
             b.step = u32(wrap(int(b.step) + gap + 1));
@@ -1870,8 +1892,8 @@ __global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
         }
         if (slot >= 0) {
           tag[slot] = (len << 16) | sn;
-          owner[slot] = icj;
-          A.slotOf[icj] = b.base + u32(slot);
+          supersede(slot, icj);
+          A.store[icj] = (1ull << 63) | (u64(sn) << 32) | u64(b.base + u32(slot));
         } else {  // ErrPacketTooOld / ErrRTXPacket: no ExtPacket
           A.flows[icj].flags = u8(A.flows[icj].flags & ~(LKF_FLOW_BUCKET | LKF_FLOW_FORWARD));
           A.fwd[icj] = 0;
@@ -1889,11 +1911,11 @@ __global__ void __launch_bounds__(256) k_bkt_store(BucketLaunch A) {
   const u32 lane = threadIdx.x & 63;
   const u32 w0 = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   for (u32 ic = w0; ic < A.n; ic += nw) {
-    if (!(A.flows[ic].flags & LKF_FLOW_BUCKET)) continue;
-    const u32 slot = A.slotOf[ic];
-    if (A.owner[slot] != ic) continue;  // a later datagram of the batch took the slot
+    const u64 st = A.store[ic];
+    if (!(st >> 63)) continue;
+    const u32 slot = u32(st);
     const lkf_raw_pkt rp = A.raws[ic];
-    const u16 sn = u16(A.flows[ic].ext_sn);
+    const u16 sn = u16(st >> 32);
     u8 *dst = A.ring + size_t(slot) * kBktSlot + 16;
     const u8 *src = A.raw + rp.off;
     const u32 snw = (u32(sn >> 8) << 16) | (u32(sn & 255) << 24);  // SN field (bytes 2-3), little-endian word 0
@@ -1960,7 +1982,13 @@ __global__ void __launch_bounds__(64) k_bkt_read(u32 n, const int32_t *__restric
 
 hipError_t launch_bucket_add(hipStream_t st, const BucketLaunch &a) {
   if (a.n == 0 || a.nstreams == 0) return hipSuccess;
+  (void)hipMemsetAsync(a.store, 0, size_t(a.n) * sizeof(u64), st);
   hipLaunchKernelGGL(k_bkt_add, dim3(a.nstreams), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_bucket_store(hipStream_t st, const BucketLaunch &a) {
+  if (a.n == 0 || a.nstreams == 0) return hipSuccess;
   hipLaunchKernelGGL(k_bkt_store, dim3(std::min<u32>(nblk(a.n, 4), 4096)), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -122,7 +122,12 @@ struct IngestLaunch {
 // The receivers' RTX buckets (mediatransportutil bucket, buffer.go:471; oracle
 // bucket_oracle.h): per stream a ring of maxSteps slots of kBktSlot bytes (the
 // packet at +16), its logical state (size << 16 | stored SN; size 0xFFFF =
-// invalid) in tag, the batch's last writer of a slot in owner.
+// invalid) in tag, the last writer of a slot in owner (ingest epoch << 32 |
+// datagram), and per datagram of the batch what to store (valid << 63 |
+// adjusted SN << 32 | slot; 0: nothing — not stored, or a later datagram of
+// the batch took the slot).  k_bkt_store reads only that and the datagrams, so
+// it runs off the forwarding path (the sender stream) while the next batches
+// are ingested and decided.
 constexpr uint32_t kBktSlot = 1536;
 struct BucketState {  // 16 B
   uint32_t base;      // first slot of the stream's ring
@@ -142,10 +147,14 @@ struct BucketLaunch {
   lkf_flow *flows;
   uint32_t *fwd;
   BucketState *state;
-  uint32_t *tag, *owner, *slotOf;  // slotOf: per datagram, the slot it was stored in
+  uint32_t *tag;
+  uint64_t *owner;
+  uint64_t *store;  // per datagram of this batch (its context's array)
   uint8_t *ring;
+  uint32_t epoch;   // this ingest's number (from 1)
 };
 hipError_t launch_bucket_add(hipStream_t s, const BucketLaunch &a);
+hipError_t launch_bucket_store(hipStream_t s, const BucketLaunch &a);
 // Bucket.GetPacket for RTX records: stream[i] (-1: no buffer / closed) and the
 // source SN; the packet is gathered to out + i * kBktSlot and src[i] = (that
 // offset, its length, its header size in reserved) or len 0
