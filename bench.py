@@ -159,7 +159,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
     # summary of this same workload (scripts/gpu_pmc.sh -> profiles/)
-    ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")))
+    ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", os.path.join(ROOT, "profiles", "r3_pmc_traffic.json")))
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostic: wait for each step (no decide/emit overlap; standalone kernel times)")
     ap.add_argument("--ingress", action="store_true",
