@@ -315,7 +315,9 @@ class lkf_transport_params(C.Structure):
 LKF_SRTP_AES128_CM_HMAC_SHA1_80 = 1
 LKF_SRTP_AEAD_AES_128_GCM = 2
 LKF_TWCC_PUSH = 0x80000000
-LKF_FLOW_BUCKET = 0x80
+# lkf_flow.flags (LKF_FLOW_*)
+LKF_FLOW_NOT_HANDLED, LKF_FLOW_DUPLICATE, LKF_FLOW_OUT_OF_ORDER, LKF_FLOW_HAS_LOSS = 0x01, 0x02, 0x04, 0x08
+LKF_FLOW_PADDING, LKF_FLOW_FORWARD, LKF_FLOW_BAD, LKF_FLOW_BUCKET = 0x10, 0x20, 0x40, 0x80
 LKF_TWCC_MARKER = 0x00010000
 SRTP_TAG_LEN = 10
 

@@ -169,3 +169,33 @@ def test_oracle_rtx_from_bucket(workload):
         assert len(got) > 0.6 * len(want) and sum(k in got for k in video) > 0.9 * len(video), (len(got), len(want))
     finally:
         o.destroy(h)
+
+
+def test_oracle_bucket_too_old_and_wrap(workload):
+    """A 5-s batch wraps the audio buckets inside the batch and delivers one
+    audio and one video datagram later than their bucket's window: both are
+    rejected (ErrPacketTooOld: no ExtPacket, no LKF_FLOW_BUCKET) although
+    RTPStatsReceiver counts them as out-of-order arrivals, and the RTX reads
+    of the wrapped audio ring return the latest packets."""
+    import importlib
+    from tests import bucket_lib
+    pkg = importlib.import_module("livekit-server_amd")
+    abi = importlib.import_module("livekit-server_amd.abi")
+    o = load_oracle()
+    tr = workload.Trace(2, duration_s=5.0, batch_s=5.0, rooms=1, seed=3, loss=0.0, reorder=0.0)
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        workload.load_streams(o.api, h, tr)
+        arr, n, ar, alen, moved = bucket_lib.late_batch(tr)
+        assert len(moved) == 2
+        assert o.api["ingest"](h, arr, n, ar, alen) == 0
+        f = pkg.flows_array(o.api, h)
+        rej = [i for i in range(n) if (f["flags"][i] & abi.LKF_FLOW_OUT_OF_ORDER)
+               and not (f["flags"][i] & (abi.LKF_FLOW_BUCKET | abi.LKF_FLOW_DUPLICATE | abi.LKF_FLOW_PADDING))]
+        assert len(rej) == 2, rej
+        assert all(not (f["flags"][i] & abi.LKF_FLOW_FORWARD) for i in rej)
+        stored = int(np.count_nonzero(f["flags"] & abi.LKF_FLOW_BUCKET))
+        assert stored == int(np.count_nonzero(f["flags"] & abi.LKF_FLOW_FORWARD)) > 1000
+    finally:
+        o.destroy(h)

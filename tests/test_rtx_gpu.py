@@ -135,3 +135,54 @@ def test_rtx_from_bucket_matches_oracle(pkg, workload, abi, cfg):
     finally:
         o.destroy(oh)
         eng.close()
+
+
+def test_bucket_too_old_and_wrap_match_oracle(pkg, workload, abi):
+    """The bucket edge cases on the GPU (k_bkt_add / k_bkt_store) against the
+    oracle: a 5-s batch wraps the audio rings inside the batch (the earlier
+    writer of a reused slot is not stored), and two datagrams arrive later
+    than their bucket's window (too old: no ExtPacket).  Flows, ExtPackets and
+    the retransmissions read back from the buckets must be identical."""
+    import ctypes as C
+    from tests import bucket_lib
+    o = load_oracle()
+    tr = workload.Trace(2, duration_s=5.0, batch_s=5.0, rooms=2, seed=3, loss=0.0, reorder=0.0)
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    try:
+        for api, h in ((eng.api, eng.h), (o.api, oh)):
+            workload.load_topology(api, h, tr)
+            workload.load_streams(api, h, tr)
+        workload.queue_events(eng.api, eng.h, tr, 0)
+        workload.queue_events(o.api, oh, tr, 0)
+        arr, n, ar, alen, moved = bucket_lib.late_batch(tr)
+        assert len(moved) == 2
+        eng.ingest(arr, n, ar, alen)
+        assert o.api["ingest"](oh, arr, n, ar, alen) == 0
+        gf, of = eng.flows(), pkg.flows_array(o.api, oh)
+        for f in ("ext_sn", "ext_ts", "pkt", "flags"):
+            assert np.array_equal(gf[f], of[f]), f
+        late = (of["flags"] & abi.LKF_FLOW_OUT_OF_ORDER) != 0
+        ok = (of["flags"] & (abi.LKF_FLOW_BUCKET | abi.LKF_FLOW_DUPLICATE | abi.LKF_FLOW_PADDING)) == 0
+        assert int(np.count_nonzero(late & ok)) == 2
+        k = C.c_uint32()
+        assert o.api["ingested"](oh, None, 0, C.byref(k)) in (0, -28)
+        pk = (abi.lkf_pkt * max(1, k.value))()
+        assert o.api["ingested"](oh, pk, k.value, C.byref(k)) == 0
+        eng.run()
+        eng.sync()
+        o.run(oh, pk, k.value, ar, alen)
+        nacks = rtx_lib.make_nacks(o.api, oh, tr, seed=8)
+        now = EPOCH + 6 * 10**9
+        g = rtx_lib.rtx_lookup(eng.api, eng.h, nacks, now)
+        r = rtx_lib.rtx_lookup(o.api, oh, nacks, now)
+        assert len(g) == len(r) > 20
+        go, gw = rtx_lib.rtx_emit_bucket(eng.api, eng.h, g)
+        oo, ow = rtx_lib.rtx_emit_bucket(o.api, oh, r)
+        assert len(go) == len(oo) > 10
+        for f in oo.dtype.names:
+            assert np.array_equal(go[f], oo[f]), f
+        assert np.array_equal(gw, ow)
+    finally:
+        o.destroy(oh)
+        eng.close()
