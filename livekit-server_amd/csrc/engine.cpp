@@ -3171,6 +3171,11 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
     HIPCHK(hipMemsetAsync(e->dNackPairCnt, 0, sizeof(uint32_t), s), "memset");
   }
   BucketLaunch bl;
+  if (e->bktSlots && e->bktStorePending) {  // a second ingest before lkf_run: the first one's copies read this
+                                            // context's store list first
+    HIPCHK(hipEventRecord(e->bktEv, e->sendS), "event");
+    HIPCHK(hipStreamWaitEvent(s, e->bktEv, 0), "wait bucket store");
+  }
   if (e->bktSlots) {
     bl.raws = dRaws;
     bl.raw = dRaw;

@@ -1982,7 +1982,8 @@ __global__ void __launch_bounds__(64) k_bkt_read(u32 n, const int32_t *__restric
 
 hipError_t launch_bucket_add(hipStream_t st, const BucketLaunch &a) {
   if (a.n == 0 || a.nstreams == 0) return hipSuccess;
-  (void)hipMemsetAsync(a.store, 0, size_t(a.n) * sizeof(u64), st);
+  const hipError_t r = hipMemsetAsync(a.store, 0, size_t(a.n) * sizeof(u64), st);
+  if (r != hipSuccess) return r;
   hipLaunchKernelGGL(k_bkt_add, dim3(a.nstreams), dim3(64), 0, st, a);
   return hipGetLastError();
 }
