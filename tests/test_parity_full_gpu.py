@@ -4,7 +4,8 @@ The engine and the CPU oracle take the same full-size traces: configs[1] at the
 benched size (100 rooms x 10 participants, 18,000 DownTracks, 1-s batches),
 configs[3] at its full fan-out (one publisher to 5,000 subscribers) and
 configs[2] at one GPU's full shard (125 rooms x 50 participants, ~337 k
-DownTracks).  Every record, every wire byte, every counter, every exported
+DownTracks) and configs[4] at 2,000 rooms (the SVC / dependency-descriptor
+path).  Every record, every wire byte, every counter, every exported
 Forwarder state and sequencer probes must be identical.
 """
 import pytest
@@ -35,3 +36,12 @@ def test_config3_full_shard(pkg, workload, abi):
     assert tr.ndts > 300000
     t = run_parity(pkg, workload, abi, tr)
     assert t["forwarded"] > 25_000_000
+
+
+def test_config5_full_shard(pkg, workload, abi):
+    """configs[4] at its specified size: 2,000 rooms x 5 participants, VP9 / AV1
+    L3T3 SVC with dependency descriptors (the DD decide path), 1-s batches."""
+    tr = workload.Trace(5, duration_s=1.0, batch_s=1.0, rooms=2000)
+    assert tr.ndts >= 2000 * 5 * 4
+    t = run_parity(pkg, workload, abi, tr, seq_probe=False)
+    assert t["forwarded"] > 1_000_000
