@@ -170,6 +170,9 @@ def main():
     ap.add_argument("--srtp", action="store_true",
                     help="step = forward + SRTP protect (lkf_protect: abs-send-time + AES_CM_128_HMAC_SHA1_80 "
                          "per subscriber transport, every DownTrack bound)")
+    ap.add_argument("--alloc-per-step", type=int, default=0,
+                    help="deployment shape: the stream allocator's AllocateOptimal for this many video DownTracks "
+                         "after every step's run (a control-rate call: it waits for the queued runs)")
     ap.add_argument("--srtp-profile", choices=["aes_cm", "gcm"], default="aes_cm",
                     help="with --srtp: SRTP_AES128_CM_HMAC_SHA1_80 or SRTP_AEAD_AES_128_GCM transports")
     args = ap.parse_args()
@@ -266,6 +269,15 @@ def main():
         drained[0] += nrec
         drained[1] += nbytes
 
+    if args.alloc_per_step:
+        vdts = np.array([d for d in range(trace.ndts)
+                         if trace.tracks[trace.downtracks[d].track].kind == pkg.abi.LKF_KIND_VIDEO], dtype=np.int32)
+        areq = np.zeros(args.alloc_per_step, dtype=pkg.abi.ALLOC_REQ_DTYPE)
+        areq["available_layers"] = 7
+        areq["bitrates"] = np.sort(np.random.default_rng(7).integers(100_000, 3_000_000, (args.alloc_per_step, 12)),
+                                   axis=1).reshape(-1, 3, 4)
+        aout = np.zeros(args.alloc_per_step, dtype=pkg.abi.ALLOCATION_DTYPE)
+
     def step(b):
         ta = time.perf_counter()
         wl.queue_events(eng.api, eng.h, trace, b)
@@ -285,6 +297,11 @@ def main():
             assert eng.api["speakers_enqueue"](eng.h, 1700000000 * 10**9 + int((b + 1) * args.batch_s * 1e9)) == 0
         if args.srtp:
             assert eng.api["protect"](eng.h, 1700000000 * 10**9 + int(b * args.batch_s * 1e9)) == 0
+        if args.alloc_per_step:  # StreamAllocator tick: AllocateOptimal on a rotating set of video DownTracks
+            k = args.alloc_per_step
+            sel = vdts[(b * k + np.arange(k)) % len(vdts)]
+            areq["dt"] = sel
+            assert eng.api["allocate_optimal"](eng.h, areq.ctypes.data, k, aout.ctypes.data) == 0
         if args.host_io and b > args.warmup:  # batch b-1's output over PCIe while batch b computes
             drain_prev(1)
         if args.sync_each:
@@ -472,6 +489,10 @@ def main():
                             "protected_pkts_per_s_kernel": round(fwd / (prot_ms / 1e3), 1) if prot_ms else None,
                             "algorithmic_bytes_per_launch": int(prot_bytes // args.steps),
                             "achieved": round(pa, 1), "frac_hbm": round(pa / PEAK_HBM_GBPS, 4)}
+        if args.alloc_per_step:  # control-rate calls inside the timed loop (each drains the queued runs)
+            line["control"] = {"alloc_optimal_per_step": args.alloc_per_step,
+                               "note": "lkf_allocate_optimal after every run: waits for the queued runs (no overlap "
+                                       "across that step boundary)"}
         print(json.dumps(line))
     eng.close()
     if dist:

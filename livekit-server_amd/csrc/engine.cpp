@@ -2873,9 +2873,15 @@ static int alloc_common(lkf_engine *e, int mode, const lkf_alloc_req *reqs, cons
   }
   int rc = flush_topology(e);
   if (rc) return rc;
-  rc = drain_streams(e);
-  if (rc) return rc;
+  // The allocation reads and writes the DownTracks' hot state and last
+  // allocation, which between runs only the decide stream touches: it is
+  // ordered on that stream after the queued runs' decides, and the host waits
+  // for it alone, not for their emits, sender statistics or protect stages
+  // (those keep overlapping the call).
+  hipStream_t s = e->decS;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (n > e->allocCap) {
+    HIPCHK(hipStreamSynchronize(s), "sync before alloc buffers realloc");
     if (e->dAllocReq) (void)hipFree(e->dAllocReq);
     if (e->dAllocOut) (void)hipFree(e->dAllocOut);
     if (e->dAllocCapacity) (void)hipFree(e->dAllocCapacity);
@@ -2885,16 +2891,18 @@ static int alloc_common(lkf_engine *e, int mode, const lkf_alloc_req *reqs, cons
     HIPCHK(dalloc(&e->dAllocCapacity, e->allocCap), "alloc alloc capacity");
   }
   static_assert(sizeof(lkf_video_transition) <= sizeof(lkf_allocation), "transition fits the out buffer");
-  HIPCHK(hipMemcpy(e->dAllocReq, reqs, n * sizeof(lkf_alloc_req), hipMemcpyHostToDevice), "alloc req copy");
+  // (the engine's own stream: anything an earlier control call left there)
+  HIPCHK(hipEventRecord(e->inEv, e->own), "event");
+  HIPCHK(hipStreamWaitEvent(s, e->inEv, 0), "wait own stream");
+  HIPCHK(hipMemcpyAsync(e->dAllocReq, reqs, n * sizeof(lkf_alloc_req), hipMemcpyHostToDevice, s), "alloc req copy");
   if (mode == ALLOC_NEXT_HIGHER)
-    HIPCHK(hipMemcpy(e->dAllocCapacity, capacity, n * sizeof(int64_t), hipMemcpyHostToDevice), "capacity copy");
-  rc = upload_done(e);
-  if (rc) return rc;
-  HIPCHK(launch_allocate(e->own, mode, e->dAllocReq, e->dAllocCapacity, n, e->dHot, e->dDTs, e->dTracks,
-                         e->dLastAlloc, e->dAllocOut),
+    HIPCHK(hipMemcpyAsync(e->dAllocCapacity, capacity, n * sizeof(int64_t), hipMemcpyHostToDevice, s),
+           "capacity copy");
+  HIPCHK(launch_allocate(s, mode, e->dAllocReq, e->dAllocCapacity, n, e->dHot, e->dDTs, e->dTracks, e->dLastAlloc,
+                         e->dAllocOut),
          "allocate");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
-  HIPCHK(hipMemcpy(out, e->dAllocOut, n * outSize, hipMemcpyDeviceToHost), "alloc out copy");
+  HIPCHK(hipMemcpyAsync(out, e->dAllocOut, n * outSize, hipMemcpyDeviceToHost, s), "alloc out copy");
+  HIPCHK(hipStreamSynchronize(s), "sync");
   return LKF_OK;
 }
 int lkf_allocate_optimal(lkf_engine *e, const lkf_alloc_req *reqs, uint32_t n, lkf_allocation *out) {
