@@ -2110,23 +2110,28 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
   const uint32_t m = uint32_t(packed.size());
   int rc = flush_topology(e);
   if (rc) return rc;
-  rc = drain_streams(e);
-  if (rc) return rc;
+  // The lookup reads and updates the sequencer records and the DownTracks'
+  // hot state, which between runs only the decide stream touches: ordered on
+  // that stream behind the queued decides (their emits keep running), as the
+  // allocation calls.
+  hipStream_t s = e->decS;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (m > e->rtxCap) HIPCHK(hipStreamSynchronize(s), "sync decide stream");  // (rtx_reserve reallocates)
   rc = rtx_reserve(e, m);
   if (rc) return rc;
-  HIPCHK(hipMemcpy(e->dNacks, packed.data(), m * sizeof(lkf_nack), hipMemcpyHostToDevice), "nacks copy");
-  HIPCHK(hipMemcpy(e->dNackG, gb.data(), gb.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "groups copy");
-  rc = upload_done(e);
-  if (rc) return rc;
-  HIPCHK(launch_rtx_lookup(e->own, e->dHot, e->dSeq, e->cfg.seq_size, e->dSrm, e->srmStride, e->srmCap, e->dNacks,
-                           e->dNackG,
-                           uint32_t(gStart.size()), now_ns / 1000000, e->dRtx, e->dNackValid),
+  HIPCHK(hipEventRecord(e->inEv, e->own), "event");
+  HIPCHK(hipStreamWaitEvent(s, e->inEv, 0), "wait own stream");
+  HIPCHK(hipMemcpyAsync(e->dNacks, packed.data(), m * sizeof(lkf_nack), hipMemcpyHostToDevice, s), "nacks copy");
+  HIPCHK(hipMemcpyAsync(e->dNackG, gb.data(), gb.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s),
+         "groups copy");
+  HIPCHK(launch_rtx_lookup(s, e->dHot, e->dSeq, e->cfg.seq_size, e->dSrm, e->srmStride, e->srmCap, e->dNacks,
+                           e->dNackG, uint32_t(gStart.size()), now_ns / 1000000, e->dRtx, e->dNackValid),
          "rtx lookup");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
   std::vector<lkf_rtx> r(m);
   std::vector<uint32_t> v(m);
-  HIPCHK(hipMemcpy(r.data(), e->dRtx, m * sizeof(lkf_rtx), hipMemcpyDeviceToHost), "rtx copy");
-  HIPCHK(hipMemcpy(v.data(), e->dNackValid, m * sizeof(uint32_t), hipMemcpyDeviceToHost), "valid copy");
+  HIPCHK(hipMemcpyAsync(r.data(), e->dRtx, m * sizeof(lkf_rtx), hipMemcpyDeviceToHost, s), "rtx copy");
+  HIPCHK(hipMemcpyAsync(v.data(), e->dNackValid, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "valid copy");
+  HIPCHK(hipStreamSynchronize(s), "sync");
   uint32_t k = 0;
   for (uint32_t i = 0; i < m; i++) k += v[i];
   *n_out = k;
