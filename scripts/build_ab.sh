@@ -8,6 +8,7 @@ make -s
 for v in ${VARIANTS}; do
   name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $flags -c forward_kernels.hip -o ../lib/fk_$name.o
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/liblkfwd_$name.so ../lib/fk_$name.o ../lib/ingress_kernels.o ../lib/srtp_kernels.o ../lib/alloc_kernels.o ../lib/red_kernels.o ../lib/tracker_kernels.o ../lib/engine.o
+  others=$(ls ../lib/*.o | grep -v -e '/forward_kernels.o$' -e '/fk_' -e '/synth')
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/liblkfwd_$name.so ../lib/fk_$name.o $others
   echo "built liblkfwd_$name.so ($flags)"
 done
