@@ -2145,6 +2145,19 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
 static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const uint8_t *srcArena,
                            const std::vector<uint16_t> &srcHdr, lkf_out *out, uint8_t *out_arena, uint64_t out_cap,
                            uint32_t *n_out, uint64_t *out_len);
+// The retransmissions run on the sender stream: after the queued runs'
+// sender statistics (the RTX sendingPacket updates the same RTPStatsSender),
+// their bucket copies, and — through an event — their decides and sequencer
+// DD bytes; the queued emits and protect stages keep running.
+static int rtx_order(lkf_engine *e, uint32_t n) {
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  HIPCHK(hipEventRecord(e->inEv, e->decS), "event");
+  HIPCHK(hipStreamWaitEvent(e->sendS, e->inEv, 0), "wait decide stream");
+  HIPCHK(hipEventRecord(e->inEv, e->own), "event");
+  HIPCHK(hipStreamWaitEvent(e->sendS, e->inEv, 0), "wait own stream");
+  HIPCHK(hipStreamSynchronize(e->sendS), "sync sender stream");  // (buffers below are rewritten from the host)
+  return rtx_reserve(e, n);
+}
 int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
                  uint64_t src_len, lkf_out *out, uint8_t *out_arena, uint64_t out_cap, uint32_t *n_out,
                  uint64_t *out_len) {
@@ -2158,9 +2171,7 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   }
   int rc = flush_topology(e);
   if (rc) return rc;
-  rc = drain_streams(e);
-  if (rc) return rc;
-  rc = rtx_reserve(e, n);
+  rc = rtx_order(e, n);
   if (rc) return rc;
   if (src_len + 64 > e->rtxInCap) {
     if (e->dRtxIn) (void)hipFree(e->dRtxIn);
@@ -2170,8 +2181,6 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   HIPCHK(hipMemcpy(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice), "rtx copy");
   HIPCHK(hipMemcpy(e->dRtxSrc, src, n * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice), "src copy");
   if (src_len) HIPCHK(hipMemcpy(e->dRtxIn, src_arena, src_len, hipMemcpyHostToDevice), "src arena copy");
-  rc = upload_done(e);
-  if (rc) return rc;
   std::vector<uint16_t> hdr(n, 0);
   for (uint32_t i = 0; i < n; i++) {
     if (!src[i].len) continue;
@@ -2197,16 +2206,17 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
       e->rtxDDCap = std::max<uint32_t>(n, 1024);
       HIPCHK(dalloc(&e->dRtxDD, size_t(e->rtxDDCap) * kSeqDDBytes), "alloc rtx dd");
     }
-    HIPCHK(launch_rtx_dd(e->own, n, e->dRtx, e->dDTs, e->dSeq, e->cfg.seq_size, e->dSeqDDIdx, e->dSeqDD, e->dRtxDD),
+    HIPCHK(launch_rtx_dd(e->sendS, n, e->dRtx, e->dDTs, e->dSeq, e->cfg.seq_size, e->dSeqDDIdx, e->dSeqDD,
+                         e->dRtxDD),
            "rtx dd");
     rtxDD = e->dRtxDD;
   }
-  HIPCHK(launch_rtx_emit(e->own, false, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen, nullptr,
-                         nullptr, rtxDD),
+  HIPCHK(launch_rtx_emit(e->sendS, false, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen,
+                         nullptr, nullptr, rtxDD),
          "rtx size");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
   std::vector<uint32_t> len(n);
-  HIPCHK(hipMemcpy(len.data(), e->dRtxLen, n * sizeof(uint32_t), hipMemcpyDeviceToHost), "len copy");
+  HIPCHK(hipMemcpyAsync(len.data(), e->dRtxLen, n * sizeof(uint32_t), hipMemcpyDeviceToHost, e->sendS), "len copy");
+  HIPCHK(hipStreamSynchronize(e->sendS), "sync");
   std::vector<uint64_t> off(n, 0);
   uint64_t tot = 0;
   uint32_t k = 0;
@@ -2225,14 +2235,13 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
     e->rtxOutCap = std::max<uint64_t>(tot + 64, 1 << 20);
     HIPCHK(dalloc(&e->dRtxOut, e->rtxOutCap), "alloc rtx out");
   }
-  HIPCHK(hipMemcpy(e->dRtxOff, off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice), "off copy");
-  rc = upload_done(e);
-  if (rc) return rc;
-  HIPCHK(launch_rtx_emit(e->own, true, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen, e->dRtxOff,
-                         e->dRtxOut, rtxDD),
+  HIPCHK(hipMemcpyAsync(e->dRtxOff, off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, e->sendS), "off copy");
+  HIPCHK(launch_rtx_emit(e->sendS, true, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen,
+                         e->dRtxOff, e->dRtxOut, rtxDD),
          "rtx write");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
-  if (tot) HIPCHK(hipMemcpy(out_arena, e->dRtxOut, tot, hipMemcpyDeviceToHost), "rtx bytes copy");
+  if (tot)
+    HIPCHK(hipMemcpyAsync(out_arena, e->dRtxOut, tot, hipMemcpyDeviceToHost, e->sendS), "rtx bytes copy");
+  HIPCHK(hipStreamSynchronize(e->sendS), "sync");
   {  // sendingPacket (downtrack.go:1671-1681): the bucket packet's header as
      // unmarshalled (CSRCs and extensions kept), the forwarded payload
     std::vector<SenderUpd> ul;
@@ -2287,9 +2296,7 @@ int lkf_rtx_emit_bucket(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *
     if (rtx[i].dt < 0 || rtx[i].dt >= int32_t(e->dtp.size())) return LKF_EINVAL;
   int rc = flush_topology(e);
   if (rc) return rc;
-  rc = drain_streams(e);
-  if (rc) return rc;
-  rc = rtx_reserve(e, n);
+  rc = rtx_order(e, n);
   if (rc) return rc;
   std::vector<int32_t> sid(n, -1);
   std::vector<uint16_t> sn(n);
@@ -2321,19 +2328,18 @@ int lkf_rtx_emit_bucket(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *
   HIPCHK(hipMemcpy(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice), "rtx copy");
   HIPCHK(hipMemcpy(e->dBktStream, sid.data(), n * sizeof(int32_t), hipMemcpyHostToDevice), "bucket read copy");
   HIPCHK(hipMemcpy(e->dBktSn, sn.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice), "bucket sn copy");
-  rc = upload_done(e);
-  if (rc) return rc;
   if (uint64_t(n) * kBktSlot + 64 > e->rtxInCap) {
     if (e->dRtxIn) (void)hipFree(e->dRtxIn);
     e->rtxInCap = std::max<uint64_t>(uint64_t(n) * kBktSlot + 64, 1 << 20);
     HIPCHK(dalloc(&e->dRtxIn, e->rtxInCap), "alloc rtx in");
   }
-  HIPCHK(launch_bucket_read(e->own, n, e->dBktStream, e->dBktSn, e->dBkt, e->dBktTag, e->dBktRing, e->dRtxIn,
+  HIPCHK(launch_bucket_read(e->sendS, n, e->dBktStream, e->dBktSn, e->dBkt, e->dBktTag, e->dBktRing, e->dRtxIn,
                             e->dRtxSrc),
          "bucket read");
   std::vector<lkf_raw_pkt> src(n);
-  HIPCHK(hipMemcpyAsync(src.data(), e->dRtxSrc, n * sizeof(lkf_raw_pkt), hipMemcpyDeviceToHost, e->own), "src back");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  HIPCHK(hipMemcpyAsync(src.data(), e->dRtxSrc, n * sizeof(lkf_raw_pkt), hipMemcpyDeviceToHost, e->sendS),
+         "src back");
+  HIPCHK(hipStreamSynchronize(e->sendS), "sync");
   std::vector<uint16_t> hdr(n, 0);
   for (uint32_t i = 0; i < n; i++) hdr[i] = uint16_t(src[i].len ? src[i].reserved : 0);
   return rtx_emit_common(e, rtx, n, e->dRtxIn, hdr, out, out_arena, out_cap, n_out, out_len);
@@ -2360,10 +2366,13 @@ static int sender_list(lkf_engine *e, std::vector<SenderUpd> &list) {
     HIPCHK(dalloc(&e->dSSList, e->ssListCap), "alloc sender list");
     HIPCHK(dalloc(&e->dSSGroups, e->ssListCap + 1), "alloc sender groups");
   }
-  HIPCHK(hipMemcpy(e->dSSList, list.data(), list.size() * sizeof(SenderUpd), hipMemcpyHostToDevice), "sender list copy");
-  HIPCHK(hipMemcpy(e->dSSGroups, g.data(), g.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "sender groups copy");
-  int rc = upload_done(e);
-  if (rc) return rc;
+  // on the sender stream: after the queued runs' sender statistics, which
+  // update the same DownTracks' RTPStatsSender
+  hipStream_t st = e->sendS;
+  HIPCHK(hipMemcpyAsync(e->dSSList, list.data(), list.size() * sizeof(SenderUpd), hipMemcpyHostToDevice, st),
+         "sender list copy");
+  HIPCHK(hipMemcpyAsync(e->dSSGroups, g.data(), g.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st),
+         "sender groups copy");
   SenderListLaunch a;
   a.list = e->dSSList;
   a.gBegin = e->dSSGroups;
@@ -2371,8 +2380,8 @@ static int sender_list(lkf_engine *e, std::vector<SenderUpd> &list) {
   a.ss = e->dSS;
   a.ring = e->dSSRing;
   a.gap = e->dSSGap;
-  HIPCHK(launch_sender_updates(e->own, a), "sender updates");
-  HIPCHK(hipStreamSynchronize(e->own), "sync");
+  HIPCHK(launch_sender_updates(st, a), "sender updates");
+  HIPCHK(hipStreamSynchronize(st), "sync");
   return LKF_OK;
 }
 
