@@ -2407,8 +2407,12 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   }
   int rc = flush_topology(e);
   if (rc) return rc;
-  rc = drain_streams(e);
-  if (rc) return rc;
+  // k_pad reads and writes the DownTracks' Forwarder / sequencer state, which
+  // between runs only the decide stream touches: it runs there, behind the
+  // queued decides (their emits keep running); its sendingPacket updates go to
+  // the sender stream (sender_list)
+  const hipStream_t ds = e->decS;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (n > e->padCap) {
     for (void *p : {static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff), static_cast<void *>(e->dPadCnt)})
       if (p) (void)hipFree(p);
@@ -2444,8 +2448,8 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   if (m) {
     HIPCHK(hipMemcpy(e->dPadReq, lq.data(), m * sizeof(lkf_pad_req), hipMemcpyHostToDevice), "pad req copy");
     HIPCHK(hipMemcpy(e->dPadOff, loff.data(), 2 * size_t(m) * sizeof(uint64_t), hipMemcpyHostToDevice), "pad off copy");
-    rc = upload_done(e);
-    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->inEv, e->own), "event");
+    HIPCHK(hipStreamWaitEvent(ds, e->inEv, 0), "wait own stream");
     PadLaunch a;
     a.blank = blank;
     a.n = m;
@@ -2467,8 +2471,8 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
     a.arena = e->dPadArena;
     a.cnt = e->dPadCnt;
     a.bytes = e->dPadCnt + m;
-    HIPCHK(launch_pad(e->own, a), "pad");
-    HIPCHK(hipStreamSynchronize(e->own), "sync");
+    HIPCHK(launch_pad(ds, a), "pad");
+    HIPCHK(hipStreamSynchronize(ds), "sync");
     HIPCHK(hipMemcpy(cnt.data(), e->dPadCnt, 2 * size_t(m) * sizeof(uint32_t), hipMemcpyDeviceToHost), "pad cnt copy");
   }
   if (bytes_sent)
