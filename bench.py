@@ -38,17 +38,28 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes(trace, batches, fwd, out_bytes, active_dts):
-    """sum_in (64 + in_payload) + sum_fwd (out_len + 32) + sum_active_DT 256 per batch."""
+def algorithmic_bytes(trace, batches, fwd, out_bytes, active_dts, ingress=False):
+    """sum_in (64 + in_payload) + sum_fwd (out_len + 32) + sum_active_DT 256 per batch.
+    With the ingress stage (Buffer.calc in the step), per raw datagram its
+    24-B descriptor and bytes read once and a 40-B flow record written, plus
+    each stored packet's bytes written into its RTX bucket (counted as the
+    ExtPackets' header + payload: every ExtPacket was stored, padding not
+    counted — a lower bound).  -> (B, forward-stage input bytes, ingress bytes)"""
     import numpy as np
-    abi = importlib.import_module("livekit-server_amd.abi")
-    b_in = 0
+    b_in = b_ing = 0
     for b in batches:
         pk, n, _, _ = trace.batch(b)
         arr = np.ctypeslib.as_array(C.cast(pk, C.POINTER(C.c_uint8)), shape=(n * 64,)).view(
-            np.dtype([("x", "V38"), ("payload_len", "<u2"), ("y", "V24")]))
-        b_in += 64 * n + int(arr["payload_len"].astype(np.int64).sum())
-    return b_in + out_bytes + 32 * fwd + 256 * active_dts * len(batches), b_in
+            np.dtype([("x", "V36"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("y", "V24")]))
+        pl = int(arr["payload_len"].astype(np.int64).sum())
+        b_in += 64 * n + pl
+        if ingress:
+            rp, nraw, _, _ = trace.batch_raw(b)
+            raw = np.ctypeslib.as_array(C.cast(rp, C.POINTER(C.c_uint8)), shape=(nraw * 24,)).view(
+                np.dtype([("t", "<i8"), ("s", "<u4"), ("off", "<u4"), ("len", "<u4"), ("r", "<u4")]))
+            b_ing += (24 + 40) * nraw + int(raw["len"].astype(np.int64).sum())
+            b_ing += pl + int(arr["payload_off"].astype(np.int64).sum())
+    return b_in + b_ing + out_bytes + 32 * fwd + 256 * active_dts * len(batches), b_in, b_ing
 
 
 def cpu_model():
@@ -86,49 +97,64 @@ def workload_name(config, rooms, ndts):
     }[config]
 
 
-def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2):
+class _BenchBatch(C.Structure):  # oracle/cpu_bench.cpp orc_bench_batch
+    _fields_ = [("pkts", C.c_void_p), ("n", C.c_uint32), ("nraw", C.c_uint32), ("arena", C.c_void_p),
+                ("alen", C.c_uint64), ("dd", C.c_void_p), ("raws", C.c_void_p), ("ev", C.c_void_p),
+                ("nev", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class _BenchShard(C.Structure):  # oracle/cpu_bench.cpp orc_bench_shard
+    _fields_ = [("tracks", C.c_void_p), ("dts", C.c_void_p), ("streams", C.c_void_p), ("batches", C.c_void_p),
+                ("ntracks", C.c_uint32), ("ndts", C.c_uint32), ("nstreams", C.c_uint32), ("nbatches", C.c_uint32)]
+
+
+def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2, ingress=False):
     """CPU oracle (C++ restatement of the Go path, -O3) on a bounded sample of
     the same workload: `sample_rooms` rooms of the config's shape,
-    `sample_batches` one-second batches, rooms sharded over `threads` workers
-    (one oracle engine per worker).  Returns (forwarded/s, wall s, rooms,
-    batches)."""
+    `sample_batches` one-second batches, rooms sharded over `threads` C++
+    threads (oracle/cpu_bench.cpp: one oracle engine per thread, no Python in
+    the timed region).  With `ingress` each batch goes through Buffer.calc
+    (orc_ingest) first, as the GPU step does.  Returns (forwarded/s, wall s,
+    rooms, batches, per-thread busy s)."""
     from tests.oracle_lib import load as load_oracle
     wl = importlib.import_module("livekit-server_amd.workload")
-    abi = importlib.import_module("livekit-server_amd.abi")
     o = load_oracle()
     threads = max(1, min(threads, sample_rooms))
     per = max(1, sample_rooms // threads)
-    shards = []
+    traces, shards, keep = [], (_BenchShard * threads)(), []
     for t in range(threads):
         tr = wl.Trace(config, duration_s=float(sample_batches), batch_s=1.0, rooms=per, room_base=t * per)
-        h = o.create(500)
-        wl.load_topology(o.api, h, tr)
-        shards.append((tr, h))
-    fwd = [0] * threads
-
-    def work(i):
-        tr, h = shards[i]
-        dd = tr.has_dd()
+        traces.append(tr)
+        bb = (_BenchBatch * tr.nbatches)()
+        dd = tr.has_dd() and not ingress
         for b in range(tr.nbatches):
-            wl.queue_events(o.api, h, tr, b)
             pk, n, ar, alen = tr.batch(b)
-            o.run(h, pk, n, ar, alen, tr.batch_dd(b)[0] if dd else None)
-            st = abi.lkf_stats()
-            o.api["get_stats"](h, C.byref(st))
-            fwd[i] += st.forwarded
-
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    dt = time.perf_counter() - t0
-    nb = shards[0][0].nbatches
-    for tr, h in shards:
-        o.destroy(h)
+            ev, nev = wl.events_ptr(tr, b)
+            x = bb[b]
+            x.pkts, x.n, x.arena, x.alen = C.cast(pk, C.c_void_p), n, C.cast(ar, C.c_void_p), alen
+            x.ev, x.nev = C.cast(ev, C.c_void_p), nev
+            x.dd = C.cast(tr.batch_dd(b)[0], C.c_void_p) if dd else None
+            if ingress:
+                rp, nraw, _, _ = tr.batch_raw(b)
+                x.raws, x.nraw = C.cast(rp, C.c_void_p), nraw
+        keep.append(bb)
+        s = shards[t]
+        s.tracks, s.dts = C.cast(tr.tracks, C.c_void_p), C.cast(tr.downtracks, C.c_void_p)
+        s.streams = C.cast(tr.streams, C.c_void_p) if ingress else None
+        s.batches = C.cast(bb, C.c_void_p)
+        s.ntracks, s.ndts, s.nstreams, s.nbatches = tr.ntracks, tr.ndts, (tr.nstreams if ingress else 0), tr.nbatches
+    fwd = (C.c_uint64 * threads)()
+    busy = (C.c_double * threads)()
+    wall = C.c_double()
+    o.lib.orc_cpu_bench.restype = C.c_int
+    o.lib.orc_cpu_bench.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    rc = o.lib.orc_cpu_bench(C.cast(shards, C.c_void_p), threads, 1 if ingress else 0, 500, C.cast(fwd, C.c_void_p),
+                             C.cast(busy, C.c_void_p), C.byref(wall))
+    assert rc == 0, rc
+    nb = traces[0].nbatches
+    for tr in traces:
         tr.close()
-    return sum(fwd) / dt, dt, per * threads, nb
+    return sum(fwd) / wall.value, wall.value, per * threads, nb, list(busy)
 
 
 def kernel_sources_sha():
@@ -162,8 +188,11 @@ def main():
     ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", os.path.join(ROOT, "profiles", "r3_pmc_traffic.json")))
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostic: wait for each step (no decide/emit overlap; standalone kernel times)")
-    ap.add_argument("--ingress", action="store_true",
-                    help="step = Buffer.calc over raw datagrams (lkf_ingest_device) + forwarding")
+    ap.add_argument("--extpackets", action="store_true",
+                    help="step = forwarding of pre-built ExtPacket batches (lkf_submit_device + lkf_run) instead of "
+                         "the default raw datagrams -> Buffer.calc (lkf_ingest_device: RTPStatsReceiver, NACK "
+                         "queues, RTX buckets) -> forwarding")
+    ap.add_argument("--ingress", action="store_true", help="(the default step; kept for older command lines)")
     ap.add_argument("--host-io", action="store_true",
                     help="host-fed deployment shape: lkf_submit from pinned host memory and lkf_drain_run of "
                          "the previous batch into pinned host memory inside the timed region (PCIe both ways)")
@@ -179,8 +208,12 @@ def main():
     if not args.rooms:
         args.rooms = CONFIGS[args.config]["rooms"]
     speakers = args.config == 3
-    if args.config == 3:  # audio levels come from the ingress path
-        args.ingress = True
+    # the whole north-star path by default: raw datagrams through Buffer.calc
+    # (pkg/sfu/buffer sequence and NACK tracking) then the forwarding path;
+    # configs[2]'s audio levels come from the ingress path in any case
+    args.ingress = not args.extpackets or args.config == 3
+    if args.host_io and args.config != 3:  # the host-fed shape submits ExtPacket batches from pinned host memory
+        args.ingress = False
 
     import torch
 
@@ -369,7 +402,8 @@ def main():
 
     fwd = cum["forwarded"]
     steps_pkts = sum(meta[b][0] for b in range(args.warmup, nb))
-    algo, b_in = algorithmic_bytes(trace, range(args.warmup, nb), fwd, cum["out_bytes"], trace.ndts)
+    algo, b_in, b_ing = algorithmic_bytes(trace, range(args.warmup, nb), fwd, cum["out_bytes"], trace.ndts,
+                                          ingress=args.ingress)
     payload_in = b_in - 64 * steps_pkts
     # per-kernel algorithmic bytes (the two halves of SURVEY.md §8(d)'s B):
     #   decide: packet descriptors once + sequencer record per forwarded tuple + DT hot state
@@ -408,7 +442,8 @@ def main():
             try:
                 pmc = json.load(open(args.pmc_csv))
                 if (pmc.get("kernel_sources_sha") == kernel_sources_sha() and pmc.get("bench_args_rooms") == args.rooms
-                        and pmc.get("bench_args_config", 2) == args.config and not args.ingress):
+                        and pmc.get("bench_args_config", 2) == args.config
+                        and bool(pmc.get("bench_args_ingress", False)) == bool(args.ingress)):
                     traffic = pmc.get("hbm_bytes_per_step")
                     traffic_src = os.path.relpath(args.pmc_csv, ROOT)
             except Exception:
@@ -419,19 +454,23 @@ def main():
             # the GPU box gives one GPU a 16-CPU share (os.cpu_count() is the whole host)
             thr = args.cpu_threads or min(16, os.cpu_count() or 1)
             cc = CONFIGS[args.config]
-            v, secs, rooms, nbat = cpu_baseline(thr, sample_rooms=cc["sample"], config=args.config)
-            v1, secs1, rooms1, _ = cpu_baseline(1, sample_rooms=cc["sample1"], config=args.config)
-            cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": min(thr, rooms), "kind": "port",
-                   "sample": "configs[%d] shape: %d rooms, 4 s of media (%d batches incl. the arrival tail), rooms "
-                             "sharded over %d threads (%.1f s wall); single thread: %d rooms, %.1f s wall" % (
-                                 args.config - 1, rooms, nbat, min(thr, rooms), secs, rooms1, secs1),
-                   "single_thread_value": round(v1, 1), "host_nproc": os.cpu_count(), "cpu_model": cpu_model()}
-            # one thread per host core: rooms shard with no
-            # shared state, so the oracle scales with threads (the measured
-            # 16-thread / single-thread ratio is the evidence); the GPU box
-            # gives one GPU a 16-CPU share, so the all-core figure is
-            # extrapolated from the 16-thread run, not run
+            v, secs, rooms, nbat, busy = cpu_baseline(thr, sample_rooms=cc["sample"], config=args.config,
+                                                      ingress=args.ingress)
+            v1, secs1, rooms1, _, _ = cpu_baseline(1, sample_rooms=cc["sample1"], config=args.config,
+                                                   ingress=args.ingress)
             used = max(1, min(thr, rooms))
+            cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": used, "kind": "port",
+                   "sample": "configs[%d] shape%s: %d rooms, 4 s of media (%d batches incl. the arrival tail), rooms "
+                             "sharded over %d C++ threads, one oracle engine each (oracle/cpu_bench.cpp; %.1f s "
+                             "wall); single thread: %d rooms, %.1f s wall" % (
+                                 args.config - 1, " through Buffer.calc (orc_ingest)" if args.ingress else "", rooms,
+                                 nbat, used, secs, rooms1, secs1),
+                   "single_thread_value": round(v1, 1), "host_nproc": os.cpu_count(), "cpu_model": cpu_model(),
+                   "thread_busy_s": {"min": round(min(busy), 3), "max": round(max(busy), 3)}}
+            # one thread per core of the box's 16-CPU share per GPU; rooms shard
+            # with no shared state, so the rate scales with threads up to the
+            # memory system (thread_scaling_eff = the 16-thread rate over 16 x
+            # the single-thread rate, both measured)
             cpu["thread_scaling_eff"] = round(v / (v1 * used), 3) if v1 else None
             cpu["all_cores"] = {"value": round(v / used * (os.cpu_count() or used), 1), "cores": os.cpu_count(),
                                 "basis": "extrapolated: %d-thread rate x %d/%d host threads (not run: the box's "

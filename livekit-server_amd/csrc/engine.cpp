@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -33,17 +35,54 @@ using namespace lkf;
 
 namespace {
 
+// Every device buffer the engine allocates, base -> bytes (all engines of the
+// process).  Each device -> host copy of an engine buffer is checked against
+// it (check_dev_range): a source range that does not lie inside one live
+// allocation — a freed or reallocated buffer, or a length past the end — is
+// reported as an error instead of reaching the copy engine.
+struct DevRegistry {
+  std::mutex m;
+  std::map<uintptr_t, size_t> a;
+};
+DevRegistry &dreg() {
+  static DevRegistry r;
+  return r;
+}
+
 template <typename T>
 hipError_t dalloc(T **p, size_t n) {
   *p = nullptr;
   if (n == 0) n = 1;
-  return hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T));
+  const hipError_t r = hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T));
+  if (r == hipSuccess) {
+    std::lock_guard<std::mutex> g(dreg().m);
+    dreg().a[reinterpret_cast<uintptr_t>(*p)] = n * sizeof(T);
+  }
+  return r;
+}
+
+hipError_t dfree(void *p) {
+  if (p) {
+    std::lock_guard<std::mutex> g(dreg().m);
+    dreg().a.erase(reinterpret_cast<uintptr_t>(p));
+  }
+  return hipFree(p);
+}
+
+// [src, src + n) inside one live allocation of this registry
+bool dev_range_ok(const void *src, size_t n) {
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src);
+  std::lock_guard<std::mutex> g(dreg().m);
+  auto it = dreg().a.upper_bound(s);
+  if (it == dreg().a.begin()) return false;
+  --it;
+  return s >= it->first && n <= it->second && s - it->first <= it->second - n;
 }
 
 template <typename T>
 static hipError_t grow(T **p, uint64_t &cap, uint64_t need) {
   if (need <= cap) return hipSuccess;
-  if (*p) (void)hipFree(*p);
+  if (*p) (void)dfree(*p);
   cap = std::max<uint64_t>(need, 1024);
   return dalloc(p, cap);
 }
@@ -78,6 +117,7 @@ struct BatchCtx {
   uint32_t *dEvLane = nullptr;   // lane of each op (sorted), for k_ev_offsets
   uint64_t evCap = 0, evOffCap = 0, evLaneCap = 0;
   hipEvent_t prepped = nullptr;  // prep stage done (prep stream)
+  hipEvent_t pulled = nullptr;   // the control-op pull from the staging buffer done (own stream)
   hipEvent_t decided = nullptr;  // decide stage done (decide stream)
   hipEvent_t sent = nullptr;     // sender statistics done (sender stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
@@ -94,8 +134,8 @@ struct BatchCtx {
   // the prep stage (k_h2d ... layer index) and the decide stage's tail
   // (counters, output scan) as HIP graphs, captured for the engine's topology
   // epoch; replayed every run (one launch each instead of ~11)
-  hipGraphExec_t gPrep = nullptr, gScan = nullptr;
-  uint64_t gPrepEpoch = 0, gScanEpoch = 0;
+  hipGraphExec_t gPrep = nullptr, gScan = nullptr, gCtl = nullptr;
+  uint64_t gPrepEpoch = 0, gScanEpoch = 0, gCtlEpoch = 0;
 };
 
 }  // namespace
@@ -112,6 +152,9 @@ struct lkf_engine {
   hipStream_t decS = nullptr;   // decide stage (high priority)
   hipStream_t emitS = nullptr;  // emit stage (low priority)
   hipStream_t sendS = nullptr;  // sender statistics of a decided batch (low priority, beside its emit)
+  hipStream_t sideS = nullptr;  // an ingest's NACK queues, beside the rest of the ingest and the run
+  hipEvent_t sideFork = nullptr, sideDone = nullptr;
+  bool sidePending = false;     // the next ingest waits for sideDone
   hipStream_t cur = nullptr;    // caller's stream of the last lkf_run
   hipEvent_t inEv = nullptr;    // caller-stream work before a run
   hipEvent_t bktEv = nullptr;   // an ingest's bucket decisions (the sender stream copies after it)
@@ -339,7 +382,6 @@ struct lkf_engine {
   uint64_t *dPos = nullptr, *dIPartA = nullptr, *dIPartB = nullptr, *dITotal = nullptr;
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
   uint32_t *dIList = nullptr, *dIListCnt = nullptr;  // per-stream datagram lists (k_ing_lists)
-  uint32_t *dILanePerm = nullptr;                     // k_ing_stream lane -> stream, by (kind, layer)
   // NACK queues (allocated with the first stream that has one) and the last
   // ingest's RTCP NACKs (per datagram result + bump-allocated pairs)
   NackState *dNack = nullptr;
@@ -347,9 +389,9 @@ struct lkf_engine {
   lkf_nack_pair *dNackPairs = nullptr;
   uint32_t nackPairCap = 0;
   uint64_t *dNackRecPos = nullptr, *dNackPairPos = nullptr, *dNackTot = nullptr;
+  uint64_t *dNackPartA = nullptr, *dNackPartB = nullptr;  // the compaction's scan partials (side stream)
   lkf_rtcp_nack *dNackOut = nullptr;
   lkf_nack_pair *dNackPairsOut = nullptr;
-  bool ingLane = false;                               // LKF_ING_LANE=1: lane-per-stream ingress (A/B)
   uint32_t lastIngestN = 0;
   const lkf_raw_pkt *ingRaws = nullptr;  // the last ingest's datagram descriptors (device)
   // speaker ranking tables (rebuilt when topology changes)
@@ -458,15 +500,43 @@ static int drain_streams(lkf_engine *e) {
   HIPCHK(hipStreamSynchronize(e->decS), "sync decide stream");
   HIPCHK(hipStreamSynchronize(e->emitS), "sync emit stream");
   if (e->sendS) HIPCHK(hipStreamSynchronize(e->sendS), "sync sender stream");
+  if (e->sideS) HIPCHK(hipStreamSynchronize(e->sideS), "sync side stream");
   return LKF_OK;
 }
 
-// Device -> caller host memory through the engine's pinned bounce buffer:
-// the caller's buffer may be pageable (numpy arrays, std::vector), and a
-// pageable D2H hipMemcpy is the one path on which round 2 and round 3 each saw
-// a stray "illegal memory access" after every engine stream had completed.
+// A device -> host copy whose source range is not inside one live engine
+// allocation (a length past a buffer's end, a freed or reallocated buffer):
+// refused with LKF_EHIP and counted (lkf_debug_check folds the count into its
+// violation total).  A pageable D2H copy of such a range is what surfaces as
+// "an illegal memory access" from the copy call itself (the runtime's staging
+// copy reads the bad range) — round 2's recorded fault was exactly that
+// (a drain of tot[3] bytes past the output arena).
+static uint64_t gRangeViolations = 0;
+static int range_fail(lkf_engine *e, const void *src, size_t n, const char *what) {
+  char buf[256];
+  snprintf(buf, sizeof(buf), "internal: %s: device range [%p, +%zu) outside every live engine allocation", what, src,
+           n);
+  e->err = buf;
+  gRangeViolations++;
+  return LKF_EHIP;
+}
+#define CHKRANGE(src, n, what)                                                     \
+  do {                                                                             \
+    if ((n) && !dev_range_ok(src, n)) return range_fail(e, src, n, what);          \
+  } while (0)
+static int copy_to_host(lkf_engine *e, void *dst, const void *src, size_t n, const char *what);
+#define D2H(dst, src, n, what)                                   \
+  do {                                                           \
+    const int _rc = copy_to_host(e, dst, src, n, what);          \
+    if (_rc) return _rc;                                         \
+  } while (0)
+
+// Device -> caller host memory, range-checked (CHKRANGE).  A page-locked
+// destination is copied directly; a pageable one (numpy arrays, std::vector,
+// the stack) through the engine's pinned bounce buffer on its own stream.
 static int copy_to_host(lkf_engine *e, void *dst, const void *src, size_t n, const char *what) {
   constexpr size_t kChunk = size_t(16) << 20;
+  CHKRANGE(src, n, what);
   hipPointerAttribute_t pa;
   if (hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost) {  // page-locked: direct
     HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost), what);
@@ -495,6 +565,20 @@ static int upload_done(lkf_engine *e) {
   return LKF_OK;
 }
 static int sender_list(lkf_engine *e, std::vector<SenderUpd> &list);
+
+// Orders the sender stream after everything queued so far on the decide, emit
+// and own streams.  The per-run sender statistics run on the sender stream
+// (long batches) or on the emit stream right after emit (short batches,
+// k_sender_stats_thread); a control call that updates RTPStatsSender from the
+// sender stream (padding, blank frames, RTX) must come after both, or a
+// queued tick's Update and the call's load/store of the same SenderStats race.
+static int sender_after_queued(lkf_engine *e) {
+  for (hipStream_t s : {e->decS, e->emitS, e->own}) {
+    HIPCHK(hipEventRecord(e->inEv, s), "event");
+    HIPCHK(hipStreamWaitEvent(e->sendS, e->inEv, 0), "wait queued stage");
+  }
+  return LKF_OK;
+}
 
 // The DD selector tables and per-batch DD buffers, allocated when the first
 // track with the dependency-descriptor selector appears (streams drained).
@@ -584,9 +668,9 @@ static int flush_topology(lkf_engine *e) {
         HIPCHK(hipMemset(nr, 0, size_t(cap) * per), "sequencer dd reset");
         if (e->dSeqDD) {
           HIPCHK(hipMemcpy(nr, e->dSeqDD, size_t(n0) * per, hipMemcpyDeviceToDevice), "sequencer dd move");
-          HIPCHK(hipFree(e->dSeqDD), "free sequencer dd");
+          HIPCHK(dfree(e->dSeqDD), "free sequencer dd");
         }
-        if (e->dSeqDDList) HIPCHK(hipFree(e->dSeqDDList), "free sequencer dd list");
+        if (e->dSeqDDList) HIPCHK(dfree(e->dSeqDDList), "free sequencer dd list");
         HIPCHK(dalloc(&e->dSeqDDList, cap), "alloc sequencer dd list");
         e->dSeqDD = nr;
         e->seqDDCap = cap;
@@ -630,7 +714,7 @@ static int flush_topology(lkf_engine *e) {
         }
         for (void *p : {static_cast<void *>(e->dBktTag), static_cast<void *>(e->dBktOwner),
                         static_cast<void *>(e->dBktRing)})
-          if (p) HIPCHK(hipFree(p), "free bucket");
+          if (p) HIPCHK(dfree(p), "free bucket");
         e->dBktTag = tag;
         e->dBktOwner = own;
         e->dBktRing = ring;
@@ -655,6 +739,9 @@ static int flush_topology(lkf_engine *e) {
       HIPCHK(dalloc(&e->dNackRecPos, c.max_batch_pkts), "alloc nack positions");
       HIPCHK(dalloc(&e->dNackPairPos, c.max_batch_pkts), "alloc nack pair positions");
       HIPCHK(dalloc(&e->dNackTot, 2), "alloc nack totals");
+      const size_t npart = (size_t(c.max_batch_pkts) + 1023) / 1024 + 1;  // (as the ingest's scan partials)
+      HIPCHK(dalloc(&e->dNackPartA, npart), "alloc nack scan partials");
+      HIPCHK(dalloc(&e->dNackPartB, npart), "alloc nack scan partials");
       HIPCHK(dalloc(&e->dNackOut, c.max_batch_pkts), "alloc nack records");
       HIPCHK(dalloc(&e->dNackPairsOut, e->nackPairCap), "alloc nack pairs out");
       HIPCHK(hipMemset(e->dNackInfo, 0, size_t(c.max_batch_pkts) * sizeof(uint32_t)), "nack info reset");
@@ -677,17 +764,6 @@ static int flush_topology(lkf_engine *e) {
            "stream state upload");
     HIPCHK(hipMemset(e->dHist + first * kHistWords, 0, k * kHistWords * sizeof(uint64_t)), "history reset");
     e->pendStreams.clear();
-    // k_ing_stream lanes: streams grouped by (kind, layer), so a wave's lanes
-    // have similar datagram counts and take the same branches
-    const uint32_t ns = uint32_t(e->streams.size());
-    std::vector<uint32_t> perm(ns);
-    for (uint32_t i = 0; i < ns; i++) perm[i] = i;
-    auto key = [&](uint32_t i) {
-      const lkf_track_params &tp = e->tracks[e->streams[i].track];
-      return std::make_pair(int(tp.kind), int(e->streams[i].layer));
-    };
-    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
-    HIPCHK(hipMemcpy(e->dILanePerm, perm.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice), "lane perm copy");
   }
   return upload_done(e);
 }
@@ -741,8 +817,11 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
     A(hipStreamCreateWithPriority(&e->sendS, hipStreamNonBlocking, leastPrio));
   }
+  A(hipStreamCreateWithFlags(&e->sideS, hipStreamNonBlocking));
   A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
   A(hipEventCreateWithFlags(&e->bktEv, hipEventDisableTiming));
+  A(hipEventCreateWithFlags(&e->sideFork, hipEventDisableTiming));
+  A(hipEventCreateWithFlags(&e->sideDone, hipEventDisableTiming));
   e->cur = e->own;
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
@@ -794,6 +873,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     x.evCap = x.evLaneCap = 4096;
     A(hipEventCreateWithFlags(&x.decided, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.prepped, hipEventDisableTiming));
+    A(hipEventCreateWithFlags(&x.pulled, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.emitted, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.sent, hipEventDisableTiming));
   }
@@ -819,7 +899,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dIErr, 4));
   A(dalloc(&e->dIList, 3 * size_t(c.max_batch_pkts) + 64));
   A(dalloc(&e->dIListCnt, 3 * size_t(c.max_tracks)));
-  A(dalloc(&e->dILanePerm, e->maxStreams));
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
     // Every persistent table starts zeroed: hipMalloc hands back memory an
@@ -872,7 +951,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   if (const char *v = getenv("LKF_SENDER_MODE")) e->senderMode = uint32_t(std::min(2, std::max(0, atoi(v))));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
-  if (const char *v = getenv("LKF_ING_LANE")) e->ingLane = atoi(v) != 0;
   if (const char *v = getenv("LKF_GRAPH")) e->useGraph = atoi(v) != 0;
   return e;
 }
@@ -902,43 +980,45 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->red.outArena), static_cast<void *>(e->red.g), static_cast<void *>(e->red.cnt),
                   static_cast<void *>(e->red.map), static_cast<void *>(e->red.off),
                   static_cast<void *>(e->dAllocOut)})
-    if (p) (void)hipFree(p);
+    if (p) (void)dfree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
                   e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktRing, e->dBktStream, e->dBktSn,
-                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt, e->dILanePerm,
+                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
                   e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
-                  e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut,
+                  e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut, e->dNackPartA,
+                  e->dNackPartB,
                   e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups, e->dSeqDD, e->dSeqDDIdx,
                   e->dSeqDDList, e->dRtxDD, e->dProv, e->dProvReq, e->dProvGroups, e->dProvOut,
                   e->dDDTrk, e->dTrackDDTrk, e->dDDTrkIds, e->dDDTrkOut};
   for (void *p : ptrs)
-    if (p) (void)hipFree(p);
+    if (p) (void)dfree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
                   static_cast<void *>(e->dDDState), static_cast<void *>(e->dDDIng),
                   static_cast<void *>(e->dDDIngStruct), static_cast<void *>(e->dIngDD)})
-    if (p) (void)hipFree(p);
+    if (p) (void)dfree(p);
   for (auto &r : e->protRing)
     for (auto &ev : r)
       if (ev) (void)hipEventDestroy(ev);
   for (void *p : {static_cast<void *>(e->dTransports), static_cast<void *>(e->dSrtpKeys),
                   static_cast<void *>(e->dAesTab), static_cast<void *>(e->dSrtpDT)})
-    if (p) (void)hipFree(p);
+    if (p) (void)dfree(p);
   for (auto &x : e->ctx) {
-    if (x.dProt) (void)hipFree(x.dProt);
+    if (x.dProt) (void)dfree(x.dProt);
     for (void *p : {static_cast<void *>(x.dDDIn), static_cast<void *>(x.dDDPkt), static_cast<void *>(x.dDDArena),
                     static_cast<void *>(x.dDDUsed)})
-      if (p) (void)hipFree(p);
+      if (p) (void)dfree(p);
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
                  x.dRawPkts, x.dBktStore, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane};
     for (void *p : q)
-      if (p) (void)hipFree(p);
+      if (p) (void)dfree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
     if (x.prepped) (void)hipEventDestroy(x.prepped);
+    if (x.pulled) (void)hipEventDestroy(x.pulled);
     if (x.emitted) (void)hipEventDestroy(x.emitted);
     if (x.sent) (void)hipEventDestroy(x.sent);
   }
@@ -948,12 +1028,16 @@ void lkf_destroy(lkf_engine *e) {
   for (auto &x : e->ctx) {
     stage_free(&x.stage, &x.stageDev);
     if (x.gPrep) (void)hipGraphExecDestroy(x.gPrep);
+    if (x.gCtl) (void)hipGraphExecDestroy(x.gCtl);
     if (x.gScan) (void)hipGraphExecDestroy(x.gScan);
-    if (x.dDesc) (void)hipFree(x.dDesc);
+    if (x.dDesc) (void)dfree(x.dDesc);
   }
   if (e->bounce) (void)hipHostFree(e->bounce);
   if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->bktEv) (void)hipEventDestroy(e->bktEv);
+  if (e->sideFork) (void)hipEventDestroy(e->sideFork);
+  if (e->sideDone) (void)hipEventDestroy(e->sideDone);
+  if (e->sideS) (void)hipStreamDestroy(e->sideS);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
   if (e->sendS) (void)hipStreamDestroy(e->sendS);
   if (e->decS) (void)hipStreamDestroy(e->decS);
@@ -1223,8 +1307,8 @@ static int rebuild_sched(lkf_engine *e) {
   int rc = drain_streams(e);  // queued runs still read the previous schedule
   if (rc) return rc;
   if (nl + 1 > e->schedCap) {
-    if (e->dSched) HIPCHK(hipFree(e->dSched), "free sched");
-    if (e->dWaveTrack) HIPCHK(hipFree(e->dWaveTrack), "free wavetrack");
+    if (e->dSched) HIPCHK(dfree(e->dSched), "free sched");
+    if (e->dWaveTrack) HIPCHK(dfree(e->dWaveTrack), "free wavetrack");
     e->schedCap = nl + 1 + 4096;
     HIPCHK(dalloc(&e->dSched, e->schedCap), "alloc sched");
     HIPCHK(dalloc(&e->dWaveTrack, e->schedCap + 1), "alloc wavetrack");
@@ -1297,7 +1381,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   // first kernel pulls them and k_ev_offsets derives the dense per-lane
   // offsets on the GPU (no host pass over all lanes).
   const auto tp1 = clk::now();
-  if (x.used) HIPCHK(hipEventSynchronize(x.prepped), "stage wait");  // run n-3's pull of this staging is done
+  if (x.used) HIPCHK(hipEventSynchronize(x.pulled), "stage wait");  // run n-3's pull of this staging is done
   const auto tp2 = clk::now();
   auto &ka = e->sortA, &kb = e->sortB;  // (lane, pending index)
   ka.clear();
@@ -1320,6 +1404,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     HIPCHK(stage_alloc(&x.stage, &x.stageDev, sizeof(RunDesc) + size_t(x.stageCap) * (sizeof(DevEvent) + 4)),
            "alloc stage");
     x.gPrepEpoch = 0;
+    x.gCtlEpoch = 0;
   }
   DevEvent *evs = reinterpret_cast<DevEvent *>(x.stage + sizeof(RunDesc));
   uint32_t *lanes = reinterpret_cast<uint32_t *>(x.stage + sizeof(RunDesc) + size_t(x.stageCap) * sizeof(DevEvent));
@@ -1356,21 +1441,22 @@ int lkf_run(lkf_engine *e, void *stream) {
     // the ops and offsets by the decide stage).
     HIPCHK(hipStreamSynchronize(ps), "sync before events realloc");
     if (nev > x.evCap) {
-      if (x.dEvents) HIPCHK(hipFree(x.dEvents), "free events");
+      if (x.dEvents) HIPCHK(dfree(x.dEvents), "free events");
       x.evCap = std::max<uint64_t>(2 * nev, 4096);
       HIPCHK(dalloc(&x.dEvents, x.evCap), "alloc events");
     }
     if (size_t(nl) + 1 > x.evOffCap) {
-      if (x.dEvOff) HIPCHK(hipFree(x.dEvOff), "free evoff");
+      if (x.dEvOff) HIPCHK(dfree(x.dEvOff), "free evoff");
       x.evOffCap = size_t(nl) + 1 + 4096;
       HIPCHK(dalloc(&x.dEvOff, x.evOffCap), "alloc evoff");
     }
     if (nev > x.evLaneCap) {
-      if (x.dEvLane) HIPCHK(hipFree(x.dEvLane), "free evlane");
+      if (x.dEvLane) HIPCHK(dfree(x.dEvLane), "free evlane");
       x.evLaneCap = std::max<uint64_t>(2 * nev, 4096);
       HIPCHK(dalloc(&x.dEvLane, x.evLaneCap), "alloc evlane");
     }
     x.gPrepEpoch = 0;
+    x.gCtlEpoch = 0;
   }
   const auto tp3 = clk::now();
 
@@ -1379,9 +1465,18 @@ int lkf_run(lkf_engine *e, void *stream) {
   hipEvent_t *rg = e->ring[e->nRuns % lkf_engine::kRing];
   if (!e->ingestStarted) HIPCHK(hipEventRecord(rg[0], ps), "event");  // else: recorded ahead of the ingest
   e->ingestStarted = false;
+  // the control-op pull (k_h2d: the run descriptor and the ops from the
+  // pinned staging; k_ev_offsets) on the engine's own stream: it does not
+  // depend on the batch, so it runs beside a preceding ingest instead of after
+  // it on the prep stream
+  hipStream_t cs = e->own;
+  if (x.used) HIPCHK(hipStreamWaitEvent(cs, x.emitted, 0), "wait emit (pull)");
+  auto ctl = [&]() -> int {
+    HIPCHK(launch_h2d(cs, x.stageDev, x.dDesc, x.dEvents, x.dEvLane), "event pull");
+    HIPCHK(launch_ev_offsets(cs, x.dEvLane, x.dDesc, nl, x.dEvOff), "event offsets");
+    return LKF_OK;
+  };
   auto prep = [&]() -> int {
-    HIPCHK(launch_h2d(ps, x.stageDev, x.dDesc, x.dEvents, x.dEvLane), "event pull");
-    HIPCHK(launch_ev_offsets(ps, x.dEvLane, x.dDesc, nl, x.dEvOff), "event offsets");
     HIPCHK(launch_batch_init(ps, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr,
                              x.dStats, x.dFwdCnt, x.dFwdBytes),
            "batch init");
@@ -1429,6 +1524,19 @@ int lkf_run(lkf_engine *e, void *stream) {
     HIPCHK(ri, "graph instantiate");
     return LKF_OK;
   };
+  if (e->useGraph) {
+    if (x.gCtlEpoch != e->epoch || !x.gCtl) {
+      const int rc = capture(cs, x.gCtl, ctl);
+      if (rc) return rc;
+      x.gCtlEpoch = e->epoch;
+    }
+    HIPCHK(hipGraphLaunch(x.gCtl, cs), "pull graph");
+  } else {
+    const int rc = ctl();
+    if (rc) return rc;
+  }
+  HIPCHK(hipEventRecord(x.pulled, cs), "event");
+  HIPCHK(hipStreamWaitEvent(ps, x.pulled, 0), "wait pull");
   if (e->useGraph) {
     if (x.gPrepEpoch != e->epoch || !x.gPrep) {
       const int rc = capture(ps, x.gPrep, prep);
@@ -1626,7 +1734,7 @@ int lkf_sync(lkf_engine *e) {
   int rc = drain_streams(e);
   if (rc) return rc;
   uint32_t acc = 0;
-  HIPCHK(hipMemcpy(&acc, e->dSticky, sizeof(acc), hipMemcpyDeviceToHost), "err copy");
+  D2H(&acc, e->dSticky, sizeof(acc), "err copy");
   if (!acc) return LKF_OK;
   HIPCHK(hipMemset(e->dSticky, 0, sizeof(uint32_t)), "err reset");
   HIPCHK(hipDeviceSynchronize(), "err reset sync");  // null-stream memset vs the engine's streams
@@ -1669,8 +1777,8 @@ int lkf_get_stats(lkf_engine *e, lkf_stats *out) {
   BatchCtx &x = e->ctx[e->lastCtx];
   uint64_t st[kStatsWords];
   uint64_t tot[4];
-  HIPCHK(hipMemcpy(st, x.dStats, sizeof(st), hipMemcpyDeviceToHost), "stats copy");
-  HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  D2H(st, x.dStats, sizeof(st), "stats copy");
+  D2H(tot, x.dTot, sizeof(tot), "tot copy");
   out->tuples = st[0];
   out->forwarded = st[1];
   out->out_bytes = st[2];
@@ -1693,7 +1801,7 @@ int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, con
   }
   BatchCtx &x = e->ctx[e->lastCtx];
   uint64_t tot[4];
-  HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  D2H(tot, x.dTot, sizeof(tot), "tot copy");
   // a batch whose output exceeded the engine's capacity wrote nothing (k_emit
   // flags it; lkf_sync reported it once): never hand out a range beyond the
   // output buffers, whatever the caller did with that report
@@ -1733,7 +1841,7 @@ int lkf_drain_run(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8
   BatchCtx &x = e->ctx[(e->nRuns - 1 - age) % lkf_engine::kCtx];
   HIPCHK(hipEventSynchronize(x.emitted), "wait emitted");
   uint64_t tot[4];
-  HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  D2H(tot, x.dTot, sizeof(tot), "tot copy");
   if (n_out) *n_out = tot[2];
   if (arena_len) *arena_len = tot[3];
   if (tot[2] > e->cfg.max_out_pkts || tot[3] > e->cfg.max_out_bytes) {  // (see lkf_output_device)
@@ -1785,8 +1893,8 @@ int32_t lkf_add_transport(lkf_engine *e, const lkf_transport_params *p) {
       HIPCHK(hipMemcpy(np, e->dTransports, t * sizeof(*np), hipMemcpyDeviceToDevice), "copy transports");
       HIPCHK(hipMemcpy(nk, e->dSrtpKeys, t * sizeof(*nk), hipMemcpyDeviceToDevice), "copy keys");
     }
-    if (e->dTransports) HIPCHK(hipFree(e->dTransports), "free transports");
-    if (e->dSrtpKeys) HIPCHK(hipFree(e->dSrtpKeys), "free keys");
+    if (e->dTransports) HIPCHK(dfree(e->dTransports), "free transports");
+    if (e->dSrtpKeys) HIPCHK(dfree(e->dSrtpKeys), "free keys");
     e->dTransports = np;
     e->dSrtpKeys = nk;
     e->transportCap = cap;
@@ -1859,7 +1967,7 @@ int lkf_output_protected_device(lkf_engine *e, const uint8_t **d_arena, uint64_t
     return LKF_EINVAL;
   }
   uint64_t tot[4];
-  HIPCHK(hipMemcpy(tot, x.dTot, sizeof(tot), hipMemcpyDeviceToHost), "tot copy");
+  D2H(tot, x.dTot, sizeof(tot), "tot copy");
   if (d_arena) *d_arena = x.dProt;
   if (arena_len) *arena_len = tot[3] + 16 * tot[2];
   return LKF_OK;
@@ -1886,7 +1994,7 @@ int lkf_drain_protected(lkf_engine *e, uint8_t *arena, uint64_t cap, uint64_t *a
   if (rc) return rc;
   if (arena_len) *arena_len = len;
   if (len > cap) return LKF_ENOSPC;
-  if (arena && len) HIPCHK(hipMemcpy(arena, d, len, hipMemcpyDeviceToHost), "drain protected");
+  if (arena && len) D2H(arena, d, len, "drain protected");
   return LKF_OK;
 }
 
@@ -1897,7 +2005,7 @@ int lkf_sender_stats_get(lkf_engine *e, int32_t dt, lkf_sender_stats *out) {
   rc = drain_streams(e);
   if (rc) return rc;
   SenderStats s;
-  HIPCHK(hipMemcpy(&s, e->dSS + dt, sizeof(s), hipMemcpyDeviceToHost), "sender stats copy");
+  D2H(&s, e->dSS + dt, sizeof(s), "sender stats copy");
   std::memset(out, 0, sizeof(*out));
   out->ext_start_sn = s.extStartSN;
   out->ext_highest_sn = s.extHighestSN;
@@ -1923,9 +2031,7 @@ int lkf_sender_stats_get(lkf_engine *e, int32_t dt, lkf_sender_stats *out) {
   out->key_frames = s.keyFrames;
   out->initialized = s.initialized;
   out->clock_rate = s.clockRate;
-  HIPCHK(hipMemcpy(out->gap_histogram, e->dSSGap + size_t(dt) * kGapWords, kGapBins * sizeof(uint32_t),
-                   hipMemcpyDeviceToHost),
-         "sender gap copy");
+  D2H(out->gap_histogram, e->dSSGap + size_t(dt) * kGapWords, kGapBins * sizeof(uint32_t), "sender gap copy");
   return LKF_OK;
 }
 
@@ -1935,9 +2041,7 @@ int lkf_sender_sninfo(lkf_engine *e, int32_t dt, uint64_t esn, uint32_t *out) {
   if (rc) return rc;
   rc = drain_streams(e);
   if (rc) return rc;
-  HIPCHK(hipMemcpy(out, e->dSSRing + size_t(dt) * kSnInfoSize + (esn & (kSnInfoSize - 1)), sizeof(uint32_t),
-                   hipMemcpyDeviceToHost),
-         "sninfo copy");
+  D2H(out, e->dSSRing + size_t(dt) * kSnInfoSize + (esn & (kSnInfoSize - 1)), sizeof(uint32_t), "sninfo copy");
   return LKF_OK;
 }
 
@@ -1949,9 +2053,9 @@ int lkf_sender_stats_seed(lkf_engine *e, int32_t dt, int32_t from_dt) {
   rc = drain_streams(e);
   if (rc) return rc;
   SenderStats from, to;
-  HIPCHK(hipMemcpy(&from, e->dSS + from_dt, sizeof(from), hipMemcpyDeviceToHost), "sender stats copy");
+  D2H(&from, e->dSS + from_dt, sizeof(from), "sender stats copy");
   if (!from.initialized) return LKF_OK;  // rtpStatsBase.seed: from must be initialized
-  HIPCHK(hipMemcpy(&to, e->dSS + dt, sizeof(to), hipMemcpyDeviceToHost), "sender stats copy");
+  D2H(&to, e->dSS + dt, sizeof(to), "sender stats copy");
   from.clockRate = to.clockRate;  // params are not seeded
   HIPCHK(hipMemcpy(e->dSS + dt, &from, sizeof(from), hipMemcpyHostToDevice), "sender stats seed");
   HIPCHK(hipMemcpy(e->dSSGap + size_t(dt) * kGapWords, e->dSSGap + size_t(from_dt) * kGapWords,
@@ -1970,7 +2074,7 @@ int lkf_get_state(lkf_engine *e, int32_t dt, lkf_fwd_state *o) {
   rc = drain_streams(e);
   if (rc) return rc;
   DTHot h;
-  HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "state copy");
+  D2H(&h, e->dHot + dt, sizeof(h), "state copy");
   std::memset(o, 0, sizeof(*o));
   if (!(h.flags & F_STARTED)) return LKF_OK;  // GetState forwarder.go:344-346
   o->started = 1;
@@ -2003,7 +2107,7 @@ int lkf_seed_state(lkf_engine *e, int32_t dt, const lkf_fwd_state *i) {
   rc = drain_streams(e);
   if (rc) return rc;
   DTHot h;
-  HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "state copy");
+  D2H(&h, e->dHot + dt, sizeof(h), "state copy");
   auto setf = [&](uint32_t f, bool v) { h.flags = v ? (h.flags | f) : (h.flags & ~f); };
   // RTPMunger.SeedLast rtpmunger.go:126-133
   h.extLastSN = i->ext_last_sn;
@@ -2039,8 +2143,8 @@ int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, i
   rc = drain_streams(e);
   if (rc) return rc;
   if (n > e->seqScratchCap) {
-    if (e->dSns) (void)hipFree(e->dSns);
-    if (e->dSeqOut) (void)hipFree(e->dSeqOut);
+    if (e->dSns) (void)dfree(e->dSns);
+    if (e->dSeqOut) (void)dfree(e->dSeqOut);
     e->seqScratchCap = std::max<uint32_t>(n, 256);
     HIPCHK(dalloc(&e->dSns, e->seqScratchCap), "alloc");
     HIPCHK(dalloc(&e->dSeqOut, e->seqScratchCap), "alloc");
@@ -2055,8 +2159,8 @@ int lkf_seq_lookup(lkf_engine *e, int32_t dt, const uint16_t *sns, uint32_t n, i
          "seq lookup");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
   uint32_t cnt = 0;
-  HIPCHK(hipMemcpy(&cnt, e->dSeqN, sizeof(cnt), hipMemcpyDeviceToHost), "n copy");
-  if (cnt) HIPCHK(hipMemcpy(out, e->dSeqOut, cnt * sizeof(lkf_seq_meta), hipMemcpyDeviceToHost), "out copy");
+  D2H(&cnt, e->dSeqN, sizeof(cnt), "n copy");
+  if (cnt) D2H(out, e->dSeqOut, cnt * sizeof(lkf_seq_meta), "out copy");
   if (n_out) *n_out = cnt;
   return LKF_OK;
 }
@@ -2066,7 +2170,7 @@ static int rtx_reserve(lkf_engine *e, uint32_t n) {
   for (void *p : {static_cast<void *>(e->dNacks), static_cast<void *>(e->dNackG), static_cast<void *>(e->dNackValid),
                   static_cast<void *>(e->dRtx), static_cast<void *>(e->dRtxSrc), static_cast<void *>(e->dRtxLen),
                   static_cast<void *>(e->dRtxOff)})
-    if (p) (void)hipFree(p);
+    if (p) (void)dfree(p);
   e->rtxCap = std::max<uint32_t>(n, 1024);
   HIPCHK(dalloc(&e->dNacks, e->rtxCap), "alloc nacks");
   HIPCHK(dalloc(&e->dNackG, e->rtxCap + 1), "alloc nack groups");
@@ -2129,7 +2233,9 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
          "rtx lookup");
   std::vector<lkf_rtx> r(m);
   std::vector<uint32_t> v(m);
+  CHKRANGE(e->dRtx, m * sizeof(lkf_rtx), "async d2h");
   HIPCHK(hipMemcpyAsync(r.data(), e->dRtx, m * sizeof(lkf_rtx), hipMemcpyDeviceToHost, s), "rtx copy");
+  CHKRANGE(e->dNackValid, m * sizeof(uint32_t), "async d2h");
   HIPCHK(hipMemcpyAsync(v.data(), e->dNackValid, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "valid copy");
   HIPCHK(hipStreamSynchronize(s), "sync");
   uint32_t k = 0;
@@ -2145,17 +2251,17 @@ int lkf_rtx_lookup(lkf_engine *e, const lkf_nack *nacks, uint32_t n, int64_t now
 static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const uint8_t *srcArena,
                            const std::vector<uint16_t> &srcHdr, lkf_out *out, uint8_t *out_arena, uint64_t out_cap,
                            uint32_t *n_out, uint64_t *out_len);
-// The retransmissions run on the sender stream: after the queued runs'
-// sender statistics (the RTX sendingPacket updates the same RTPStatsSender),
-// their bucket copies, and — through an event — their decides and sequencer
-// DD bytes; the queued emits and protect stages keep running.
+// The retransmissions run on the sender stream, after every queued stage that
+// touches what they read or update: the decides and sequencer DD bytes
+// (decide stream), the sender statistics (sender stream for long batches,
+// emit stream for short ones — the RTX sendingPacket updates the same
+// RTPStatsSender) and the bucket copies (sender stream).  The host then waits
+// for that point: the scratch buffers below are rewritten from the host.
 static int rtx_order(lkf_engine *e, uint32_t n) {
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipEventRecord(e->inEv, e->decS), "event");
-  HIPCHK(hipStreamWaitEvent(e->sendS, e->inEv, 0), "wait decide stream");
-  HIPCHK(hipEventRecord(e->inEv, e->own), "event");
-  HIPCHK(hipStreamWaitEvent(e->sendS, e->inEv, 0), "wait own stream");
-  HIPCHK(hipStreamSynchronize(e->sendS), "sync sender stream");  // (buffers below are rewritten from the host)
+  const int rc = sender_after_queued(e);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(e->sendS), "sync sender stream");
   return rtx_reserve(e, n);
 }
 int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pkt *src, const uint8_t *src_arena,
@@ -2174,13 +2280,17 @@ int lkf_rtx_emit(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
   rc = rtx_order(e, n);
   if (rc) return rc;
   if (src_len + 64 > e->rtxInCap) {
-    if (e->dRtxIn) (void)hipFree(e->dRtxIn);
+    if (e->dRtxIn) (void)dfree(e->dRtxIn);
     e->rtxInCap = std::max<uint64_t>(src_len + 64, 1 << 20);
     HIPCHK(dalloc(&e->dRtxIn, e->rtxInCap), "alloc rtx in");
   }
-  HIPCHK(hipMemcpy(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice), "rtx copy");
-  HIPCHK(hipMemcpy(e->dRtxSrc, src, n * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice), "src copy");
-  if (src_len) HIPCHK(hipMemcpy(e->dRtxIn, src_arena, src_len, hipMemcpyHostToDevice), "src arena copy");
+  // uploads ordered on the sender stream ahead of the kernels that read them
+  // (a pageable hipMemcpy may return before its DMA lands, and the engine's
+  // streams do not order against the null stream)
+  HIPCHK(hipMemcpyAsync(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice, e->sendS), "rtx copy");
+  HIPCHK(hipMemcpyAsync(e->dRtxSrc, src, n * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->sendS), "src copy");
+  if (src_len)
+    HIPCHK(hipMemcpyAsync(e->dRtxIn, src_arena, src_len, hipMemcpyHostToDevice, e->sendS), "src arena copy");
   std::vector<uint16_t> hdr(n, 0);
   for (uint32_t i = 0; i < n; i++) {
     if (!src[i].len) continue;
@@ -2202,7 +2312,7 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
   const uint8_t *rtxDD = nullptr;
   if (e->nSeqDD) {  // epm.ddBytes of each record (its sequencer slot)
     if (n > e->rtxDDCap) {
-      if (e->dRtxDD) (void)hipFree(e->dRtxDD);
+      if (e->dRtxDD) (void)dfree(e->dRtxDD);
       e->rtxDDCap = std::max<uint32_t>(n, 1024);
       HIPCHK(dalloc(&e->dRtxDD, size_t(e->rtxDDCap) * kSeqDDBytes), "alloc rtx dd");
     }
@@ -2215,6 +2325,7 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
                          nullptr, nullptr, rtxDD),
          "rtx size");
   std::vector<uint32_t> len(n);
+  CHKRANGE(e->dRtxLen, n * sizeof(uint32_t), "async d2h");
   HIPCHK(hipMemcpyAsync(len.data(), e->dRtxLen, n * sizeof(uint32_t), hipMemcpyDeviceToHost, e->sendS), "len copy");
   HIPCHK(hipStreamSynchronize(e->sendS), "sync");
   std::vector<uint64_t> off(n, 0);
@@ -2231,7 +2342,7 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
   *out_len = tot;
   if (tot > out_cap || (k && (!out || !out_arena))) return LKF_ENOSPC;
   if (tot + 64 > e->rtxOutCap) {
-    if (e->dRtxOut) (void)hipFree(e->dRtxOut);
+    if (e->dRtxOut) (void)dfree(e->dRtxOut);
     e->rtxOutCap = std::max<uint64_t>(tot + 64, 1 << 20);
     HIPCHK(dalloc(&e->dRtxOut, e->rtxOutCap), "alloc rtx out");
   }
@@ -2239,8 +2350,10 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
   HIPCHK(launch_rtx_emit(e->sendS, true, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen,
                          e->dRtxOff, e->dRtxOut, rtxDD),
          "rtx write");
-  if (tot)
+  if (tot) {
+    CHKRANGE(e->dRtxOut, tot, "async d2h");
     HIPCHK(hipMemcpyAsync(out_arena, e->dRtxOut, tot, hipMemcpyDeviceToHost, e->sendS), "rtx bytes copy");
+  }
   HIPCHK(hipStreamSynchronize(e->sendS), "sync");
   {  // sendingPacket (downtrack.go:1671-1681): the bucket packet's header as
      // unmarshalled (CSRCs and extensions kept), the forwarded payload
@@ -2319,17 +2432,20 @@ int lkf_rtx_emit_bucket(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *
   }
   if (!e->bktSlots) std::fill(sid.begin(), sid.end(), -1);
   if (n > e->bktReadCap) {
-    if (e->dBktStream) (void)hipFree(e->dBktStream);
-    if (e->dBktSn) (void)hipFree(e->dBktSn);
+    if (e->dBktStream) (void)dfree(e->dBktStream);
+    if (e->dBktSn) (void)dfree(e->dBktSn);
     e->bktReadCap = std::max<uint32_t>(n, 1024);
     HIPCHK(dalloc(&e->dBktStream, e->bktReadCap), "alloc bucket reads");
     HIPCHK(dalloc(&e->dBktSn, e->bktReadCap), "alloc bucket read sns");
   }
-  HIPCHK(hipMemcpy(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice), "rtx copy");
-  HIPCHK(hipMemcpy(e->dBktStream, sid.data(), n * sizeof(int32_t), hipMemcpyHostToDevice), "bucket read copy");
-  HIPCHK(hipMemcpy(e->dBktSn, sn.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice), "bucket sn copy");
+  // (uploads on the sender stream, ahead of k_bkt_read / k_rtx: see lkf_rtx_emit)
+  HIPCHK(hipMemcpyAsync(e->dRtx, rtx, n * sizeof(lkf_rtx), hipMemcpyHostToDevice, e->sendS), "rtx copy");
+  HIPCHK(hipMemcpyAsync(e->dBktStream, sid.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, e->sendS),
+         "bucket read copy");
+  HIPCHK(hipMemcpyAsync(e->dBktSn, sn.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice, e->sendS),
+         "bucket sn copy");
   if (uint64_t(n) * kBktSlot + 64 > e->rtxInCap) {
-    if (e->dRtxIn) (void)hipFree(e->dRtxIn);
+    if (e->dRtxIn) (void)dfree(e->dRtxIn);
     e->rtxInCap = std::max<uint64_t>(uint64_t(n) * kBktSlot + 64, 1 << 20);
     HIPCHK(dalloc(&e->dRtxIn, e->rtxInCap), "alloc rtx in");
   }
@@ -2337,6 +2453,7 @@ int lkf_rtx_emit_bucket(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, lkf_out *
                             e->dRtxSrc),
          "bucket read");
   std::vector<lkf_raw_pkt> src(n);
+  CHKRANGE(e->dRtxSrc, n * sizeof(lkf_raw_pkt), "async d2h");
   HIPCHK(hipMemcpyAsync(src.data(), e->dRtxSrc, n * sizeof(lkf_raw_pkt), hipMemcpyDeviceToHost, e->sendS),
          "src back");
   HIPCHK(hipStreamSynchronize(e->sendS), "sync");
@@ -2360,15 +2477,19 @@ static int sender_list(lkf_engine *e, std::vector<SenderUpd> &list) {
     if (i == 0 || list[i].dt != list[i - 1].dt) g.push_back(i);
   g.push_back(uint32_t(list.size()));
   if (list.size() > e->ssListCap || g.size() > e->ssListCap + 1) {
-    if (e->dSSList) (void)hipFree(e->dSSList);
-    if (e->dSSGroups) (void)hipFree(e->dSSGroups);
+    if (e->dSSList) (void)dfree(e->dSSList);
+    if (e->dSSGroups) (void)dfree(e->dSSGroups);
     e->ssListCap = uint32_t(std::max<size_t>(2 * list.size(), 4096));
     HIPCHK(dalloc(&e->dSSList, e->ssListCap), "alloc sender list");
     HIPCHK(dalloc(&e->dSSGroups, e->ssListCap + 1), "alloc sender groups");
   }
-  // on the sender stream: after the queued runs' sender statistics, which
-  // update the same DownTracks' RTPStatsSender
+  // on the sender stream, after the queued runs' sender statistics (sender or
+  // emit stream), which update the same DownTracks' RTPStatsSender
   hipStream_t st = e->sendS;
+  {
+    const int rc = sender_after_queued(e);
+    if (rc) return rc;
+  }
   HIPCHK(hipMemcpyAsync(e->dSSList, list.data(), list.size() * sizeof(SenderUpd), hipMemcpyHostToDevice, st),
          "sender list copy");
   HIPCHK(hipMemcpyAsync(e->dSSGroups, g.data(), g.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st),
@@ -2415,19 +2536,19 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (n > e->padCap) {
     for (void *p : {static_cast<void *>(e->dPadReq), static_cast<void *>(e->dPadOff), static_cast<void *>(e->dPadCnt)})
-      if (p) (void)hipFree(p);
+      if (p) (void)dfree(p);
     e->padCap = std::max<uint32_t>(n, 1024);
     HIPCHK(dalloc(&e->dPadReq, e->padCap), "alloc pad reqs");
     HIPCHK(dalloc(&e->dPadOff, 2 * size_t(e->padCap)), "alloc pad offsets");
     HIPCHK(dalloc(&e->dPadCnt, 2 * size_t(e->padCap)), "alloc pad counts");
   }
   if (recs > e->padOutCap) {
-    if (e->dPadOut) (void)hipFree(e->dPadOut);
+    if (e->dPadOut) (void)dfree(e->dPadOut);
     e->padOutCap = std::max<uint64_t>(recs, 4096);
     HIPCHK(dalloc(&e->dPadOut, e->padOutCap), "alloc pad out");
   }
   if (bytes > e->padArenaCap) {
-    if (e->dPadArena) (void)hipFree(e->dPadArena);
+    if (e->dPadArena) (void)dfree(e->dPadArena);
     e->padArenaCap = std::max<uint64_t>(bytes, 1 << 20);
     HIPCHK(dalloc(&e->dPadArena, e->padArenaCap), "alloc pad arena");
   }
@@ -2446,10 +2567,12 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   const uint32_t m = uint32_t(live.size());
   std::vector<uint32_t> cnt(2 * size_t(m), 0);
   if (m) {
-    HIPCHK(hipMemcpy(e->dPadReq, lq.data(), m * sizeof(lkf_pad_req), hipMemcpyHostToDevice), "pad req copy");
-    HIPCHK(hipMemcpy(e->dPadOff, loff.data(), 2 * size_t(m) * sizeof(uint64_t), hipMemcpyHostToDevice), "pad off copy");
     HIPCHK(hipEventRecord(e->inEv, e->own), "event");
     HIPCHK(hipStreamWaitEvent(ds, e->inEv, 0), "wait own stream");
+    // the request uploads on the decide stream, ordered ahead of k_pad (see lkf_rtx_emit)
+    HIPCHK(hipMemcpyAsync(e->dPadReq, lq.data(), m * sizeof(lkf_pad_req), hipMemcpyHostToDevice, ds), "pad req copy");
+    HIPCHK(hipMemcpyAsync(e->dPadOff, loff.data(), 2 * size_t(m) * sizeof(uint64_t), hipMemcpyHostToDevice, ds),
+           "pad off copy");
     PadLaunch a;
     a.blank = blank;
     a.n = m;
@@ -2473,7 +2596,7 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
     a.bytes = e->dPadCnt + m;
     HIPCHK(launch_pad(ds, a), "pad");
     HIPCHK(hipStreamSynchronize(ds), "sync");
-    HIPCHK(hipMemcpy(cnt.data(), e->dPadCnt, 2 * size_t(m) * sizeof(uint32_t), hipMemcpyDeviceToHost), "pad cnt copy");
+    D2H(cnt.data(), e->dPadCnt, 2 * size_t(m) * sizeof(uint32_t), "pad cnt copy");
   }
   if (bytes_sent)
     for (uint32_t i = 0; i < n; i++) bytes_sent[i] = 0;
@@ -2489,8 +2612,8 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   std::vector<lkf_out> recv(recs ? recs : 1);
   std::vector<uint8_t> arv(bytes ? bytes : 1);
   if (k) {
-    HIPCHK(hipMemcpy(recv.data(), e->dPadOut, recs * sizeof(lkf_out), hipMemcpyDeviceToHost), "pad out copy");
-    HIPCHK(hipMemcpy(arv.data(), e->dPadArena, bytes, hipMemcpyDeviceToHost), "pad arena copy");
+    D2H(recv.data(), e->dPadOut, recs * sizeof(lkf_out), "pad out copy");
+    D2H(arv.data(), e->dPadArena, bytes, "pad arena copy");
     // sendingPacket (downtrack.go:835-846, :1377-1386): isPadding, a 12-B
     // header (the pacer adds the extensions later), the payload as padding
     std::vector<SenderUpd> ul;
@@ -2549,7 +2672,7 @@ int32_t lkf_add_stream_tracker_dd(lkf_engine *e, int32_t track) {
     DDTrkState *n = nullptr;
     HIPCHK(dalloc(&n, cap), "alloc dd trackers");
     if (e->nDDTrk) HIPCHK(hipMemcpy(n, e->dDDTrk, e->nDDTrk * sizeof(DDTrkState), hipMemcpyDeviceToDevice), "dd trackers move");
-    if (e->dDDTrk) HIPCHK(hipFree(e->dDDTrk), "free dd trackers");
+    if (e->dDDTrk) HIPCHK(dfree(e->dDDTrk), "free dd trackers");
     e->dDDTrk = n;
     e->ddTrkCap = cap;
   }
@@ -2573,7 +2696,7 @@ int lkf_dd_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t arg) 
   int rc = drain_streams(e);
   if (rc) return rc;
   DDTrkState t;
-  HIPCHK(hipMemcpy(&t, e->dDDTrk + tracker, sizeof(t), hipMemcpyDeviceToHost), "dd tracker read");
+  D2H(&t, e->dDDTrk + tracker, sizeof(t), "dd tracker read");
   if (op == LKF_TRACKER_STOP) {
     if (!(t.flags & DT_STOPPED)) t.flags = (t.flags | DT_STOPPED) & ~DT_WORKER;
   } else {
@@ -2610,7 +2733,7 @@ int lkf_dd_trackers_tick(lkf_engine *e, const int32_t *trackers, uint32_t n, int
   if (rc) return rc;
   HIPCHK(launch_dd_tracker_tick(e->own, e->dDDTrk, e->dDDTrkIds, n, bitrate_elapsed_ns, e->dDDTrkOut), "dd tracker tick");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
-  HIPCHK(hipMemcpy(out, e->dDDTrkOut, n * sizeof(lkf_dd_tracker_status), hipMemcpyDeviceToHost), "dd tracker out copy");
+  D2H(out, e->dDDTrkOut, n * sizeof(lkf_dd_tracker_status), "dd tracker out copy");
   return LKF_OK;
 }
 
@@ -2625,7 +2748,7 @@ int32_t lkf_add_stream_tracker(lkf_engine *e, int32_t track, int32_t layer, uint
     TrackerState *n = nullptr;
     HIPCHK(dalloc(&n, cap), "alloc trackers");
     if (e->nTrk) HIPCHK(hipMemcpy(n, e->dTrk, e->nTrk * sizeof(TrackerState), hipMemcpyDeviceToDevice), "trackers move");
-    if (e->dTrk) HIPCHK(hipFree(e->dTrk), "free trackers");
+    if (e->dTrk) HIPCHK(dfree(e->dTrk), "free trackers");
     e->dTrk = n;
     e->trkCap = cap;
   }
@@ -2649,7 +2772,7 @@ int32_t lkf_add_stream_tracker_frame(lkf_engine *e, int32_t track, int32_t layer
   const int32_t id = lkf_add_stream_tracker(e, track, layer, 0, 0);
   if (id < 0) return id;
   TrackerState t;
-  HIPCHK(hipMemcpy(&t, e->dTrk + id, sizeof(t), hipMemcpyDeviceToHost), "tracker read");
+  D2H(&t, e->dTrk + id, sizeof(t), "tracker read");
   t.frame = 1;
   t.clockRate = clock_rate;
   t.minFPS = min_fps;
@@ -2665,7 +2788,7 @@ int lkf_stream_tracker_ctl(lkf_engine *e, int32_t tracker, int32_t op, int32_t a
   int rc = drain_streams(e);
   if (rc) return rc;
   TrackerState t;
-  HIPCHK(hipMemcpy(&t, e->dTrk + tracker, sizeof(t), hipMemcpyDeviceToHost), "tracker read");
+  D2H(&t, e->dTrk + tracker, sizeof(t), "tracker read");
   auto resetLocked = [&]() {
     t.workerLive = 0;  // generation bump: the worker exits
     t.status = 0;
@@ -2734,7 +2857,7 @@ int lkf_stream_trackers_tick_at(lkf_engine *e, const int32_t *trackers, uint32_t
   if (rc) return rc;
   HIPCHK(launch_tracker_tick(e->own, e->dTrk, e->dTrkIds, n, check, bitrate_elapsed_ns, now_ns, e->dTrkOut), "tracker tick");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
-  HIPCHK(hipMemcpy(out, e->dTrkOut, n * sizeof(lkf_tracker_status), hipMemcpyDeviceToHost), "tracker out copy");
+  D2H(out, e->dTrkOut, n * sizeof(lkf_tracker_status), "tracker out copy");
   return LKF_OK;
 }
 
@@ -2831,9 +2954,9 @@ static int red_common(lkf_engine *e, bool decode, const lkf_pkt *pkts, uint32_t 
   std::vector<lkf_pkt> rec(recs ? recs : 1);
   std::vector<uint8_t> ar(bytes ? bytes : 1);
   if (!gb.empty()) {
-    HIPCHK(hipMemcpy(cnt.data(), e->red.cnt, n * sizeof(uint32_t), hipMemcpyDeviceToHost), "red cnt copy");
-    if (recs) HIPCHK(hipMemcpy(rec.data(), e->red.out, recs * sizeof(lkf_pkt), hipMemcpyDeviceToHost), "red out copy");
-    if (bytes) HIPCHK(hipMemcpy(ar.data(), e->red.outArena, bytes, hipMemcpyDeviceToHost), "red arena copy");
+    D2H(cnt.data(), e->red.cnt, n * sizeof(uint32_t), "red cnt copy");
+    if (recs) D2H(rec.data(), e->red.out, recs * sizeof(lkf_pkt), "red out copy");
+    if (bytes) D2H(ar.data(), e->red.outArena, bytes, "red arena copy");
   }
   uint64_t k = 0, tot = 0;
   for (uint32_t i = 0; i < n; i++)
@@ -2900,9 +3023,9 @@ static int alloc_common(lkf_engine *e, int mode, const lkf_alloc_req *reqs, cons
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (n > e->allocCap) {
     HIPCHK(hipStreamSynchronize(s), "sync before alloc buffers realloc");
-    if (e->dAllocReq) (void)hipFree(e->dAllocReq);
-    if (e->dAllocOut) (void)hipFree(e->dAllocOut);
-    if (e->dAllocCapacity) (void)hipFree(e->dAllocCapacity);
+    if (e->dAllocReq) (void)dfree(e->dAllocReq);
+    if (e->dAllocOut) (void)dfree(e->dAllocOut);
+    if (e->dAllocCapacity) (void)dfree(e->dAllocCapacity);
     e->allocCap = std::max<uint32_t>(n, 1024);
     HIPCHK(dalloc(&e->dAllocReq, e->allocCap), "alloc alloc reqs");
     HIPCHK(dalloc(&e->dAllocOut, e->allocCap), "alloc alloc out");
@@ -2919,6 +3042,7 @@ static int alloc_common(lkf_engine *e, int mode, const lkf_alloc_req *reqs, cons
   HIPCHK(launch_allocate(s, mode, e->dAllocReq, e->dAllocCapacity, n, e->dHot, e->dDTs, e->dTracks, e->dLastAlloc,
                          e->dAllocOut),
          "allocate");
+  CHKRANGE(e->dAllocOut, n * outSize, "async d2h");
   HIPCHK(hipMemcpyAsync(out, e->dAllocOut, n * outSize, hipMemcpyDeviceToHost, s), "alloc out copy");
   HIPCHK(hipStreamSynchronize(s), "sync");
   return LKF_OK;
@@ -2959,11 +3083,11 @@ static int prov_reserve(lkf_engine *e, uint32_t n, uint32_t ngroups) {
     HIPCHK(hipMemset(e->dProv, 0, size_t(c.max_downtracks) * sizeof(ProvState)), "provisional reset");
   }
   if (n > e->provCap) {
-    if (e->dProvReq) (void)hipFree(e->dProvReq);
-    if (e->dProvOut) (void)hipFree(e->dProvOut);
-    if (e->dAllocReq) (void)hipFree(e->dAllocReq);
-    if (e->dAllocOut) (void)hipFree(e->dAllocOut);
-    if (e->dAllocCapacity) (void)hipFree(e->dAllocCapacity);
+    if (e->dProvReq) (void)dfree(e->dProvReq);
+    if (e->dProvOut) (void)dfree(e->dProvOut);
+    if (e->dAllocReq) (void)dfree(e->dAllocReq);
+    if (e->dAllocOut) (void)dfree(e->dAllocOut);
+    if (e->dAllocCapacity) (void)dfree(e->dAllocCapacity);
     e->provCap = std::max<uint32_t>(n, 1024);
     e->allocCap = std::max<uint32_t>(e->allocCap, e->provCap);
     HIPCHK(dalloc(&e->dProvReq, e->provCap), "alloc prov reqs");
@@ -2973,7 +3097,7 @@ static int prov_reserve(lkf_engine *e, uint32_t n, uint32_t ngroups) {
     HIPCHK(dalloc(&e->dAllocCapacity, e->allocCap), "alloc alloc capacity");
   }
   if (ngroups > e->provGroupCap) {
-    if (e->dProvGroups) (void)hipFree(e->dProvGroups);
+    if (e->dProvGroups) (void)dfree(e->dProvGroups);
     e->provGroupCap = std::max<uint32_t>(ngroups, 256);
     HIPCHK(dalloc(&e->dProvGroups, e->provGroupCap), "alloc prov groups");
   }
@@ -3010,7 +3134,7 @@ static int prov_common(lkf_engine *e, int mode, const lkf_prov_req *reqs, const 
   a.out = e->dProvOut;
   HIPCHK(launch_prov(e->own, a), "provisional");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
-  if (outSize) HIPCHK(hipMemcpy(out, e->dProvOut, n * outSize, hipMemcpyDeviceToHost), "prov out copy");
+  if (outSize) D2H(out, e->dProvOut, n * outSize, "prov out copy");
   return LKF_OK;
 }
 static int prov_dts(lkf_engine *e, int mode, const int32_t *dts, uint32_t n, void *out, size_t outSize) {
@@ -3067,7 +3191,7 @@ int lkf_allocate_all(lkf_engine *e, const lkf_alloc_group *groups, uint32_t ngro
                              e->dLastAlloc, e->dProv, reinterpret_cast<lkf_allocation *>(e->dProvOut)),
          "allocate all");
   HIPCHK(hipStreamSynchronize(e->own), "sync");
-  HIPCHK(hipMemcpy(out, e->dProvOut, n * sizeof(lkf_allocation), hipMemcpyDeviceToHost), "alloc out copy");
+  D2H(out, e->dProvOut, n * sizeof(lkf_allocation), "alloc out copy");
   return LKF_OK;
 }
 
@@ -3153,11 +3277,10 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   // the batch's GPU span (lkf_timing_window total) starts before its ingest
   HIPCHK(hipEventRecord(e->ring[e->nRuns % lkf_engine::kRing][0], s), "event");
   e->ingestStarted = true;
-  HIPCHK(hipMemsetAsync(e->dITBegin, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dITEnd, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dITRuns, 0, size_t(std::max(nt, 1u)) * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dIErr, 0, 4 * sizeof(uint32_t), s), "memset");
-  HIPCHK(hipMemsetAsync(e->dITotal, 0, 2 * sizeof(uint64_t), s), "memset");
+  // the previous ingest's NACK queues (side stream) read this ingest's scratch
+  // (parsed datagrams, flows, lists, track ranges) and update the stream state
+  if (e->sidePending) HIPCHK(hipStreamWaitEvent(s, e->sideDone, 0), "wait nack queues");
+  e->sidePending = false;
   IngestLaunch a;
   a.raws = dRaws;
   a.n = n;
@@ -3184,18 +3307,12 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.list = e->dIList;
   a.listCnt = e->dIListCnt;
   a.listStride = e->cfg.max_batch_pkts;
-  a.lanePerm = e->dILanePerm;
-  a.laneStreams = e->ingLane;
   a.nack = e->dNack;
   a.nackInfo = e->dNackInfo;
   a.nackPairOff = e->dNackPairOff;
   a.nackPairCnt = e->dNackPairCnt;
   a.nackPairs = e->dNackPairs;
   a.nackPairCap = e->nackPairCap;
-  if (e->dNack && n) {  // this ingest's RTCP NACKs start empty
-    HIPCHK(hipMemsetAsync(e->dNackInfo, 0, size_t(n) * sizeof(uint32_t), s), "memset");
-    HIPCHK(hipMemsetAsync(e->dNackPairCnt, 0, sizeof(uint32_t), s), "memset");
-  }
   BucketLaunch bl;
   if (e->bktSlots && e->bktStorePending) {  // a second ingest before lkf_run: the first one's copies read this
                                             // context's store list first
@@ -3228,7 +3345,11 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.ddStructs = dd ? e->dDDIngStruct : nullptr;
   a.ingDD = dd ? e->dIngDD : nullptr;
   a.outDD = dd ? x.dDDIn : nullptr;
-  HIPCHK(launch_ingest(s, a), "ingest");
+  {
+    bool side = false;
+    HIPCHK(launch_ingest(s, a, e->sideS, e->sideFork, e->sideDone, &side), "ingest");
+    e->sidePending = side;
+  }
   if (a.bucket && n) {  // the bucket copies, off the forwarding path: the sender stream (the
                         // batch context counts as done only after it, like the sender statistics)
     HIPCHK(hipEventRecord(e->bktEv, s), "event");
@@ -3283,7 +3404,7 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   HIPCHK(hipStreamSynchronize(e->prepS), "sync");
   if (e->lastIngestN)
-    HIPCHK(hipMemcpy(out, e->dFlows, size_t(e->lastIngestN) * sizeof(lkf_flow), hipMemcpyDeviceToHost), "flows");
+    D2H(out, e->dFlows, size_t(e->lastIngestN) * sizeof(lkf_flow), "flows");
   return LKF_OK;
 }
 
@@ -3294,7 +3415,7 @@ int lkf_ingest_twcc(lkf_engine *e, uint32_t *out, uint32_t cap, uint32_t *n_out)
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   HIPCHK(hipStreamSynchronize(e->prepS), "sync");
   if (e->lastIngestN)
-    HIPCHK(hipMemcpy(out, e->dTwcc, size_t(e->lastIngestN) * sizeof(uint32_t), hipMemcpyDeviceToHost), "twcc");
+    D2H(out, e->dTwcc, size_t(e->lastIngestN) * sizeof(uint32_t), "twcc");
   return LKF_OK;
 }
 
@@ -3307,13 +3428,13 @@ int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
     n = e->curN;
     if (e->curNDev) {
       uint64_t t = 0;
-      HIPCHK(hipMemcpy(&t, e->curNDev, sizeof(t), hipMemcpyDeviceToHost), "count copy");
+      D2H(&t, e->curNDev, sizeof(t), "count copy");
       n = uint32_t(t);
     }
   }
   *n_out = n;
   if (cap < n) return LKF_ENOSPC;
-  if (n) HIPCHK(hipMemcpy(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyDeviceToHost), "ingested copy");
+  if (n) D2H(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), "ingested copy");
   return LKF_OK;
 }
 
@@ -3326,7 +3447,7 @@ int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_ou
     n = e->curN;
     if (e->curNDev) {
       uint64_t t = 0;
-      HIPCHK(hipMemcpy(&t, e->curNDev, sizeof(t), hipMemcpyDeviceToHost), "count copy");
+      D2H(&t, e->curNDev, sizeof(t), "count copy");
       n = uint32_t(t);
     }
   }
@@ -3334,7 +3455,7 @@ int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_ou
   if (cap < n) return LKF_ENOSPC;
   if (!n) return LKF_OK;
   if (e->curDD)
-    HIPCHK(hipMemcpy(out, e->curDD, size_t(n) * sizeof(lkf_pkt_dd), hipMemcpyDeviceToHost), "ingested dd copy");
+    D2H(out, e->curDD, size_t(n) * sizeof(lkf_pkt_dd), "ingested dd copy");
   else
     std::memset(out, 0, size_t(n) * sizeof(lkf_pkt_dd));
   return LKF_OK;
@@ -3347,7 +3468,7 @@ int lkf_stream_stats_get(lkf_engine *e, int32_t sid, lkf_stream_stats *o) {
   rc = drain_streams(e);
   if (rc) return rc;
   StreamHot h;
-  HIPCHK(hipMemcpy(&h, e->dStreamHot + sid, sizeof(h), hipMemcpyDeviceToHost), "stream state copy");
+  D2H(&h, e->dStreamHot + sid, sizeof(h), "stream state copy");
   std::memset(o, 0, sizeof(*o));
   o->initialized = (h.flags & S_INIT) ? 1 : 0;
   o->ext_start_sn = h.snStart;  // WrapAround.GetExtendedStart = ET(start)
@@ -3374,11 +3495,12 @@ int lkf_ingest_nacks(lkf_engine *e, lkf_rtcp_nack *out, uint32_t cap, lkf_nack_p
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (!e->dNack || !e->lastIngestN) return LKF_OK;
   const uint32_t n = e->lastIngestN;
-  hipStream_t ps = e->prepS;  // after the ingest that produced them
-  HIPCHK(launch_nack_compact(ps, n, e->ingRaws, e->dStreams, e->dNackInfo, e->dNackPairOff, e->dNackPairs, e->dIPartA,
-                             e->dIPartB, e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut),
+  hipStream_t ps = e->sideS;  // after the NACK queues of the ingest that produced them (same stream)
+  HIPCHK(launch_nack_compact(ps, n, e->ingRaws, e->dStreams, e->dNackInfo, e->dNackPairOff, e->dNackPairs,
+                             e->dNackPartA, e->dNackPartB, e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut),
          "nack compact");
   uint64_t tot[2] = {0, 0};
+  CHKRANGE(e->dNackTot, sizeof(tot), "async d2h");
   HIPCHK(hipMemcpyAsync(tot, e->dNackTot, sizeof(tot), hipMemcpyDeviceToHost, ps), "nack totals");
   HIPCHK(hipStreamSynchronize(ps), "nack sync");
   *n_out = uint32_t(tot[0]);
@@ -3386,9 +3508,9 @@ int lkf_ingest_nacks(lkf_engine *e, lkf_rtcp_nack *out, uint32_t cap, lkf_nack_p
   if (tot[0] > cap || tot[1] > pair_cap) return LKF_ENOSPC;
   if (tot[0] && !out) return LKF_EINVAL;
   if (tot[1] && !pairs) return LKF_EINVAL;
-  if (tot[0]) HIPCHK(hipMemcpy(out, e->dNackOut, tot[0] * sizeof(lkf_rtcp_nack), hipMemcpyDeviceToHost), "nack records");
+  if (tot[0]) D2H(out, e->dNackOut, tot[0] * sizeof(lkf_rtcp_nack), "nack records");
   if (tot[1])
-    HIPCHK(hipMemcpy(pairs, e->dNackPairsOut, tot[1] * sizeof(lkf_nack_pair), hipMemcpyDeviceToHost), "nack pairs");
+    D2H(pairs, e->dNackPairsOut, tot[1] * sizeof(lkf_nack_pair), "nack pairs");
   return LKF_OK;
 }
 
@@ -3444,15 +3566,15 @@ static int rebuild_speakers(lkf_engine *e) {
   uint32_t **bufs[] = {&e->dRoomPartOff, &e->dPartId, &e->dPartMicOff, &e->dMics, &e->dRoomId};
   const std::vector<uint32_t> *src[] = {&roomOff, &partId, &partMicOff, &mics, &roomId};
   for (int i = 0; i < 5; i++) {
-    if (*bufs[i]) HIPCHK(hipFree(*bufs[i]), "free");
+    if (*bufs[i]) HIPCHK(dfree(*bufs[i]), "free");
     HIPCHK(dalloc(bufs[i], std::max<size_t>(src[i]->size(), 1)), "alloc speakers table");
     if (!src[i]->empty())
       HIPCHK(hipMemcpy(*bufs[i], src[i]->data(), src[i]->size() * sizeof(uint32_t), hipMemcpyHostToDevice),
              "speakers table copy");
   }
   if (e->spkCap < size_t(e->nRooms) * 64) {
-    if (e->dSpkSlots) HIPCHK(hipFree(e->dSpkSlots), "free");
-    if (e->dSpkCounts) HIPCHK(hipFree(e->dSpkCounts), "free");
+    if (e->dSpkSlots) HIPCHK(dfree(e->dSpkSlots), "free");
+    if (e->dSpkCounts) HIPCHK(dfree(e->dSpkCounts), "free");
     e->spkCap = std::max<size_t>(size_t(e->nRooms) * 64, 64);
     HIPCHK(dalloc(&e->dSpkSlots, e->spkCap), "alloc slots");
     HIPCHK(dalloc(&e->dSpkCounts, e->spkCap / 64 + 1), "alloc counts");
@@ -3520,9 +3642,11 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
   HIPCHK(launch_speakers(e->prepS, a), "speakers");
   std::vector<uint32_t> counts(e->nRooms);
   std::vector<lkf_speaker> slots(size_t(e->nRooms) * 64);
+  CHKRANGE(e->dSpkCounts, counts.size() * sizeof(uint32_t), "async d2h");
   HIPCHK(hipMemcpyAsync(counts.data(), e->dSpkCounts, counts.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->prepS),
          "counts copy");
+  CHKRANGE(e->dSpkSlots, slots.size() * sizeof(lkf_speaker), "async d2h");
   HIPCHK(hipMemcpyAsync(slots.data(), e->dSpkSlots, slots.size() * sizeof(lkf_speaker), hipMemcpyDeviceToHost,
                         e->prepS),
          "slots copy");
@@ -3563,6 +3687,14 @@ int lkf_debug_check(lkf_engine *e, uint64_t out[4], int reset) {
   unsigned long long v[4];
   hipError_t r = read_check(v, reset);
   for (int i = 0; i < 4; i++) out[i] = v[i];
+  // host-side device -> host range violations (CHKRANGE) count as well, in
+  // every build; site 0xD2H marks one when the device recorded none
+  if (gRangeViolations) {
+    if (!out[0]) out[1] = 0xD2, out[2] = 0, out[3] = 0;
+    out[0] += gRangeViolations;
+    if (reset) gRangeViolations = 0;
+    return LKF_OK;
+  }
   return r == hipSuccess ? LKF_OK : LKF_ENODEV;
 }
 
@@ -3576,8 +3708,8 @@ int lkf_debug_dd_state(lkf_engine *e, int32_t dt, uint64_t out[16]) {
   if (rc) return rc;
   DDState d;
   DTHot h;
-  HIPCHK(hipMemcpy(&d, e->dDDState + dt, sizeof(d), hipMemcpyDeviceToHost), "dd state");
-  HIPCHK(hipMemcpy(&h, e->dHot + dt, sizeof(h), hipMemcpyDeviceToHost), "hot state");
+  D2H(&d, e->dDDState + dt, sizeof(d), "dd state");
+  D2H(&h, e->dHot + dt, sizeof(h), "hot state");
   out[0] = (d.flags & DS_CACHE_INIT) ? 1 : 0;
   out[1] = d.cBase;
   out[2] = d.cLast;
@@ -3613,7 +3745,7 @@ int lkf_downtrack_summaries(lkf_engine *e, lkf_dt_summary *out, uint32_t cap, ui
   rc = drain_streams(e);
   if (rc) return rc;
   std::vector<DTCum> c(nd);
-  HIPCHK(hipMemcpy(c.data(), e->dDTCum, nd * sizeof(DTCum), hipMemcpyDeviceToHost), "dt totals copy");
+  D2H(c.data(), e->dDTCum, nd * sizeof(DTCum), "dt totals copy");
   for (uint32_t d = 0; d < nd; d++) {
     lkf_dt_summary &s = out[d];
     s.dt = int32_t(d);
@@ -3631,7 +3763,7 @@ int lkf_get_cumulative(lkf_engine *e, lkf_stats *out, int reset) {
   int rc = drain_streams(e);
   if (rc) return rc;
   uint64_t st[kStatsWords];
-  HIPCHK(hipMemcpy(st, e->dCum, sizeof(st), hipMemcpyDeviceToHost), "cum copy");
+  D2H(st, e->dCum, sizeof(st), "cum copy");
   out->tuples = st[0];
   out->forwarded = st[1];
   out->out_bytes = st[2];

@@ -7,13 +7,16 @@
 //                  (RFC 6464) and the VP8 payload descriptor
 //                  (buffer/helpers.go:76-162)
 //   k_ing_ranges   datagrams grouped by track -> [begin, end) per track
-//   k_ing_stream   one lane per received stream (buffer.Buffer), serial over
-//                  its datagrams: processHeaderExtensions -> AudioLevel.Observe
-//                  (buffer.go:573-596, audiolevel.go:70-102),
+//   k_ing_stream_wave  one wave per received stream (buffer.Buffer), its
+//                  datagrams in order: processHeaderExtensions ->
+//                  AudioLevel.Observe (buffer.go:573-596, audiolevel.go:70-102),
 //                  RTPStatsReceiver.Update (rtpstats_receiver.go:76-241) with
 //                  its WrapArounds and 4096-bit history, NACK loss ranges
 //                  (buffer.go:545-567), padding exclusion + SN adjustment
-//                  (buffer.go:439-471)
+//                  (buffer.go:439-471), the RTX bucket's
+//                  AddPacketWithSequenceNumber (:471-481), getExtPacket's
+//                  dependency descriptor (:599-671); in-order runs lane-parallel
+//   k_ing_nack     (side stream) the NackQueue per stream
 //   scan           positions of the ExtPackets produced
 //   k_ing_out      thread per datagram: the ExtPacket (getExtPacket
 //                  buffer.go:599-671) as an lkf_pkt of the forwarding batch
@@ -818,6 +821,80 @@ __device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u
   return true;
 }
 
+// The stream's RTX bucket inside the stream kernel (mediatransportutil
+// bucket.AddPacketWithSequenceNumber as buffer.go:471-481 calls it; oracle
+// bucket_oracle.h): the logical state (head, step) in LDS, the slot tags in
+// HBM, and this ingest's writer of each slot (sOwn in LDS for rings of up to
+// kBktLds slots, else the global owner words tagged with the ingest epoch) so
+// a slot taken again later in the batch cancels the earlier datagram's copy.
+constexpr int kBktLds = 2048;
+constexpr u32 kNoOwner = 0xFFFFFFFFu;
+struct BktCtx {
+  BucketState *b;  // LDS
+  u32 *tag;        // the stream's slot tags
+  u64 *owner;      // the stream's global owner words (rings above kBktLds)
+  u64 *store;      // per datagram of the batch
+  u32 *sOwn;       // LDS owner map (rings up to kBktLds)
+  u64 ep;          // ingest epoch << 32
+  bool lds;
+};
+__device__ __forceinline__ int bkt_wrap(int x, int M) {
+  x %= M;
+  return x < 0 ? x + M : x;
+}
+// the slot's previous writer in this ingest is not stored; ic takes it (kNoOwner: invalidated)
+__device__ __forceinline__ void bkt_supersede(const BktCtx &k, int sl, u32 ic) {
+  if (k.lds) {
+    const u32 o = k.sOwn[sl];
+    if (o != kNoOwner) k.store[o] = 0;
+    k.sOwn[sl] = ic;
+  } else {
+    const u64 o = k.owner[sl];
+    if ((o & 0xFFFFFFFF00000000ull) == k.ep) k.store[u32(o)] = 0;
+    k.owner[sl] = ic == kNoOwner ? 0 : (k.ep | ic);
+  }
+}
+// AddPacketWithSequenceNumber for one datagram (one lane): push (the skipped
+// slots invalidated, the packet at the new head) or set (an older SN inside
+// the window, unless the slot already holds it: ErrRTXPacket); too old or too
+// large (> MaxPktSize - 2) is refused.  -> the slot, or -1 (no ExtPacket).
+__device__ int bkt_add_one(const BktCtx &k, u16 sn, u32 len, u32 ic) {
+  BucketState &b = *k.b;
+  const int M = int(b.maxSteps);
+  int slot = -1;
+  if (len <= 1498) {
+    if (!b.init) {
+      b.head = u16(sn - 1);
+      b.init = 1;
+    }
+    const u16 diff = u16(sn - b.head);
+    if (diff == 0 || diff > (1u << 15)) {  // set
+      const int back = int(u16(b.head - sn));
+      if (back < M) {
+        const int sl = bkt_wrap(int(b.step) - back - 1, M);
+        const u32 t = k.tag[sl];
+        if (!((t >> 16) != 0xFFFFu && u16(t) == sn)) slot = sl;  // (a duplicate is not overwritten)
+      }
+    } else {  // push
+      const int gap = int(diff) - 1;
+      b.head = sn;
+      for (int i = 0; i < min(gap, M); i++) {
+        const int sl = bkt_wrap(int(b.step) + i, M);
+        k.tag[sl] = 0xFFFF0000u;
+        bkt_supersede(k, sl, kNoOwner);
+      }
+      slot = bkt_wrap(int(b.step) + gap, M);
+      b.step = u32(bkt_wrap(int(b.step) + gap + 1, M));
+    }
+  }
+  if (slot >= 0) {
+    k.tag[slot] = (len << 16) | sn;
+    bkt_supersede(k, slot, ic);
+    k.store[ic] = (1ull << 63) | (u64(sn) << 32) | u64(b.base + u32(slot));
+  }
+  return slot;
+}
+
 // One datagram through Buffer.calc (buffer.go:407-489): processHeaderExtensions,
 // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241), the padding
 // RangeMap, the dependency descriptor; its flow, forward flag and DD record.
@@ -825,7 +902,7 @@ template <int HS>
 __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream &s,
                                          const IngParsed &p, const lkf_raw_pkt &rp, u32 ic, lkf_flow *flows,
                                          u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *ddStates,
-                                         DDStruct *ddStructs, u32 *err) {
+                                         DDStruct *ddStructs, u32 *err, const BktCtx *bk) {
   const i64 arrival = rp.arrival_ns;
   lkf_flow f = {};
   f.pkt = 0xffffffffu;
@@ -925,7 +1002,10 @@ __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring
     }
     f.ext_sn = rsn.extVal - adj;
     if (dup) break;  // the RTX bucket already holds it (ErrRTXPacket)
-    f.flags |= LKF_FLOW_BUCKET;  // AddPacketWithSequenceNumber (k_bkt_add decides, in stream order)
+    // AddPacketWithSequenceNumber under the adjusted SN (buffer.go:471-481):
+    // too old, too large or already held -> no ExtPacket (before getExtPacket)
+    if (bk && bkt_add_one(*bk, u16(f.ext_sn), rp.len, ic) < 0) break;
+    f.flags |= LKF_FLOW_BUCKET;
     // getExtPacket (buffer.go:599-671): the dependency descriptor first
     if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
       bool limit = false;
@@ -972,74 +1052,6 @@ __device__ void closed_flows(const DevStream &s, u32 sid, u32 pb, u32 pe, const 
 }
 
 // ---------------------------------------------------------------------------
-// k_ing_stream: one lane per stream, serial over the stream's datagrams.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_ing_stream(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
-                             const DevStream *__restrict__ streams, u32 nstreams, StreamHot *__restrict__ hot,
-                             u64 *__restrict__ hist, RangeEntry *__restrict__ rings, const u32 *__restrict__ tBegin,
-                             const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows, u32 *__restrict__ fwd,
-                             const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
-                             IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list,
-                             const u32 *__restrict__ cnt, u32 stride, const u32 *__restrict__ lanePerm) {
-  __shared__ u64 sHist[kHistWords * kHL];
-#if LKF_ING_HOT_LDS
-  __shared__ StreamHot sHot[kHL];  // the receiver state in LDS
-#endif
-  // lanes take streams in the engine's (kind, layer) order: a wave's lanes
-  // walk lists of similar length through the same branches
-  const u32 slot = blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= nstreams) return;
-  const u32 sid = lanePerm ? lanePerm[slot] : slot;
-  const DevStream s = streams[sid];
-  const u32 pb = tBegin[s.track], pe = tEnd[s.track];
-  if (pb >= pe) return;
-  if (s.closed) {  // Buffer.Close: Write returns io.EOF, nothing is processed
-    closed_flows(s, sid, pb, pe, raws, flows, fwd, ingDD, list, cnt, stride, 0, 1);
-    return;
-  }
-#if LKF_ING_HOT_LDS
-  StreamHot &h = sHot[threadIdx.x];
-  h = hot[sid];
-#else
-  StreamHot h = hot[sid];  // registers (one wave per 64 streams: occupancy is not the limit)
-#endif
-  u64 *const hg = hist + size_t(sid) * kHistWords;
-  u64 *const hs = sHist + threadIdx.x;  // this lane's history in LDS (lanes never share words)
-  for (int w = 0; w < kHistWords; w++) hs[w * kHL] = hg[w];
-  RangeEntry *ring = rings + size_t(sid) * kRangeCap;
-  // this stream's datagrams: its k_ing_lists list (layer slot), else a scan of the track
-  const bool useList = s.layer < 3;
-  const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
-  const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
-  auto idxAt = [&](u32 j) { return useList ? lst[j] : pb + j; };
-  // software pipeline: descriptors two datagrams ahead, list indices three
-  // ahead, so no iteration waits on a dependent load (gfx9 counts stores in
-  // vmcnt: a load issued right before its use would also wait for the
-  // previous iteration's flow stores)
-  u32 ia = nIdx > 0 ? idxAt(0) : 0, ib = nIdx > 1 ? idxAt(1) : 0, i3 = nIdx > 2 ? idxAt(2) : 0;
-  IngParsed pa = nIdx > 0 ? q[ia] : IngParsed{}, pb2 = nIdx > 1 ? q[ib] : IngParsed{};
-  lkf_raw_pkt ra = nIdx > 0 ? raws[ia] : lkf_raw_pkt{}, rb = nIdx > 1 ? raws[ib] : lkf_raw_pkt{};
-  for (u32 j = 0; j < nIdx; j++) {
-    const IngParsed p = pa;
-    const lkf_raw_pkt rp = ra;
-    const u32 ic = ia;
-    ia = ib;
-    pa = pb2;
-    ra = rb;
-    ib = i3;
-    if (j + 2 < nIdx) {
-      pb2 = q[ib];
-      rb = raws[ib];
-    }
-    if (j + 3 < nIdx) i3 = idxAt(j + 3);
-    if (rp.stream != sid) continue;
-    ing_step<kHL>(h, hs, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err);
-  }
-  hot[sid] = h;
-  for (int w = 0; w < kHistWords; w++) hg[w] = hs[w * kHL];
-}
-
-// ---------------------------------------------------------------------------
 // k_ing_stream_wave: one wave per stream, lanes over its datagrams.  The
 // receiver recurrence is serial, but a run of in-order datagrams (SN gap 1 to
 // 2^15, TS gap up to 2^31, a payload, no audio level or DD to observe, the
@@ -1069,11 +1081,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     StreamHot *__restrict__ hot, u64 *__restrict__ hist, RangeEntry *__restrict__ rings,
     const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows,
     u32 *__restrict__ fwd, const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
-    IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list, const u32 *__restrict__ cnt, u32 stride) {
+    IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list, const u32 *__restrict__ cnt, u32 stride,
+    BktArgs bka) {
   static_assert(kHistWords == 64, "one history word per lane");
   static_assert(sizeof(StreamHot) == 64 * sizeof(u32), "one StreamHot dword per lane");
   __shared__ u64 sHist[kHistWords];
   __shared__ StreamHot sh;
+  __shared__ BucketState sB;
+  __shared__ u32 sOwn[kBktLds];
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
@@ -1085,6 +1100,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   u64 *const hg = hist + size_t(sid) * kHistWords;
   sHist[lane] = hg[lane];
   reinterpret_cast<u32 *>(&sh)[lane] = reinterpret_cast<const u32 *>(hot + sid)[lane];
+  // the stream's RTX bucket (bka.state nullptr: no buckets)
+  const bool bkOn = bka.state != nullptr;
+  BktCtx bk = {};
+  int M = 1;
+  if (bkOn) {
+    if (lane < 4) reinterpret_cast<u32 *>(&sB)[lane] = reinterpret_cast<const u32 *>(bka.state + sid)[lane];
+    __syncthreads();
+    M = int(sB.maxSteps);
+    bk.b = &sB;
+    bk.tag = bka.tag + sB.base;
+    bk.owner = bka.owner + sB.base;
+    bk.store = bka.store;
+    bk.sOwn = sOwn;
+    bk.ep = u64(bka.epoch) << 32;
+    bk.lds = M <= kBktLds;
+    if (bk.lds)
+      for (int i = int(lane); i < M; i += 64) sOwn[i] = kNoOwner;
+  }
+  const BktCtx *bkp = bkOn ? &bk : nullptr;
   __syncthreads();
   RangeEntry *ring = rings + size_t(sid) * kRangeCap;
   const bool useList = s.layer < 3;
@@ -1112,7 +1146,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         const u32 m = min(64u, nIdx - base);
         for (u32 x = 0; x < m; x++)
           if (sR[x].stream == sid)
-            ing_step<1>(sh, sHist, ring, s, sP[x], sR[x], sI[x], flows, fwd, ingDD, raw, ddStates, ddStructs, err);
+            ing_step<1>(sh, sHist, ring, s, sP[x], sR[x], sI[x], flows, fwd, ingDD, raw, ddStates, ddStructs, err,
+                        bkp);
       }
       __syncthreads();
     }
@@ -1135,15 +1170,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u16 gs = u16(p.sn - (lane == 0 ? sh.snHighest : prevSn));
     const u32 gt = p.ts - (lane == 0 ? sh.tsHighest : prevTs);
     const bool ok = stateOk && in && rp.stream == sid && (p.flags & IP_OK) && p.payloadLen > 0 &&
-                    !(p.flags & IP_VP8_BAD) && !(hasDD && p.ddLen) && gs >= 1 && gs <= 0x8000u && gt <= 0x80000000u;
+                    !(p.flags & IP_VP8_BAD) && !(hasDD && p.ddLen) && gs >= 1 && gs <= 0x8000u &&
+                    gt <= 0x80000000u && (!bkOn || rp.len <= 1498u);
     const u64 snScan = wave_incl_scan_u64(ok ? u64(gs) : 0, lane);  // only read below the run end
     u64 bad = ~__ballot(ok);
     // the history update below is exact while the run spans < 4096 SNs
     bad |= __ballot(snScan >= u64(kHistWords) * 64);
+    // the bucket: every datagram of the run is a push; the first one's step
+    // from the bucket head d0 (its adjusted SN against the head), the others'
+    // their SN gaps; S = the run's pushes so far, slots distinct while S <= M
+    u64 bS = 0;
+    u32 d0 = 0;
+    if (bkOn) {
+      const u32 gs0 = u32(__shfl(u32(gs), 0, 64));
+      d0 = u32(u16(u16(sh.snExtHighest + gs0 - sh.rmOpenValue) - sB.head));
+      if (!sB.init || d0 < 1 || d0 > 0x8000u) bad |= 1ull;
+      bS = snScan - gs0 + d0;
+      bad |= __ballot(bS > u64(M));
+    }
     const u32 L = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;
     if (L == 0) {
       if (lane == 0 && rp.stream == sid)
-        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err);
+        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err, bkp);
       __syncthreads();
       j++;
       continue;
@@ -1157,6 +1205,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u64 extLast = __shfl(ext, int(L - 1), 64), extTsLast = __shfl(extTs, int(L - 1), 64);
     const u16 snLast = u16(__shfl(u32(p.sn), int(L - 1), 64));
     const u32 tsLast = u32(__shfl(p.ts, int(L - 1), 64));
+    const u64 bSLast = __shfl(bS, int(L - 1), 64);
     if (run) {
       lkf_flow f = {};
       f.pkt = 0xffffffffu;
@@ -1171,8 +1220,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
       flows[ic] = f;
       fwd[ic] = 1;
       if (ingDD) ingDD[ic] = IngDD{};
+      if (bkOn) {  // the run's pushes: this lane's skipped slots invalidated, then its own
+        const u32 dk = lane == 0 ? d0 : u32(gs);
+        const int step0 = int(sB.step);
+        const int first = int(bS - dk);  // pushes before this lane's gap
+        for (u32 i = 0; i + 1 < dk; i++) {
+          const int sl = bkt_wrap(step0 + first + int(i), M);
+          bk.tag[sl] = 0xFFFF0000u;
+          bkt_supersede(bk, sl, kNoOwner);
+        }
+        const int slot = bkt_wrap(step0 + int(bS) - 1, M);
+        const u16 sn = u16(f.ext_sn);
+        bk.tag[slot] = (rp.len << 16) | sn;
+        bkt_supersede(bk, slot, ic);
+        bk.store[ic] = (1ull << 63) | (u64(sn) << 32) | u64(sB.base + u32(slot));
+      }
     }
     const u64 pre0 = sh.snExtHighest;
+    const u64 adjLast = extLast - sh.rmOpenValue;
     __syncthreads();
     if (lane == 0) {  // the run's gaps cleared, then its SNs set
       hist_clear_range<1>(sHist, pre0 + 1, extLast);
@@ -1186,6 +1251,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
       sh.tsHighest = tsLast;
       sh.tsExtHighest = extTsLast;
       sh.tsCycles = extTsLast - tsLast;
+      if (bkOn) {
+        sB.head = u16(adjLast);
+        sB.step = u32(bkt_wrap(int(sB.step) + int(bSLast), M));
+      }
     }
     __syncthreads();
     if (run) atomicOr(reinterpret_cast<unsigned long long *>(&sHist[(ext >> 6) & (kHistWords - 1)]), 1ull << (ext & 63));
@@ -1194,6 +1263,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   }
   hg[lane] = sHist[lane];
   reinterpret_cast<u32 *>(hot + sid)[lane] = reinterpret_cast<const u32 *>(&sh)[lane];
+  if (bkOn && lane < 4) reinterpret_cast<u32 *>(bka.state + sid)[lane] = reinterpret_cast<const u32 *>(&sB)[lane];
 }
 
 // ---------------------------------------------------------------------------
@@ -1291,6 +1361,34 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
   const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
   u64 nacked = 0;
+  // The earliest arrival time at which Pairs() can do anything: min over the
+  // entries of lastNackedAt + the interval its tries require (an entry at
+  // MaxTries is purged by the next call: -inf).  Before it, Pairs() sends and
+  // purges nothing, so a datagram that arrives earlier skips it (exactly the
+  // reference's outcome: no entry due, no RTCP NACK).  Pushes lower it; after
+  // a Pairs() that changed entries it is recomputed; removals leave a bound
+  // that is at most early (a skipped call is then only not skipped).
+  auto reqOf = [&](u32 t) { return t == 0 ? req0 : t == 1 ? req1 : t == 2 ? req2 : t == 3 ? req3 : req4; };
+  auto dueMin = [&]() -> i64 {
+    i64 m = INT64_MAX;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const u32 idx = lane + 64u * u32(h);
+      if (idx < count) {
+        const u32 t = sTries[idx];
+        const i64 d = t >= kNackMaxTries ? INT64_MIN : sLast[idx] + reqOf(t);
+        m = d < m ? d : m;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const i64 x = i64((u64(u32(__shfl_xor(int(u32(u64(m) >> 32)), o, 64))) << 32) |
+                        u64(u32(__shfl_xor(int(u32(u64(m))), o, 64))));
+      m = x < m ? x : m;
+    }
+    return i64(rl_u64(u64(m), 0));
+  };
+  i64 nextDue = count ? dueMin() : INT64_MAX;
   for (u32 base = 0; base < nIdx; base += 64) {
     const u32 k = base + lane;
     u32 ic = 0, stm = 0xffffffffu, ipf = 0, sn = 0, ff = 0;
@@ -1354,9 +1452,10 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
           }
           __syncthreads();
           count = newCount;
+          nextDue = now + req0 < nextDue ? now + req0 : nextDue;  // the new entries (tries 0, lastNackedAt now)
         }
       }
-      if (count == 0) continue;
+      if (count == 0 || now < nextDue) continue;
       // ---- Pairs(now): getNack of every entry, in parallel
       bool rem[2], snd[2];
 #pragma unroll
@@ -1372,7 +1471,10 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
       }
       const u64 r0 = __ballot(rem[0]), r1 = __ballot(rem[1]);
       const u64 s0m = __ballot(snd[0]), s1m = __ballot(snd[1]);
-      if (!(r0 | r1 | s0m | s1m)) continue;
+      if (!(r0 | r1 | s0m | s1m)) {
+        nextDue = dueMin();  // (a removal left the bound early)
+        continue;
+      }
       const u32 base16 = u32(u16(sSn[0] - 17u));  // set far back to open the first pair
       // purge list (queue order), before any entry moves
       const u32 nr0 = u32(__popcll(r0));
@@ -1430,6 +1532,8 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
       // purge (NackQueue.Remove of every entry at MaxTries, in order)
       const u32 nPurge = nr0 + u32(__popcll(r1));
       for (u32 i = 0; i < nPurge; i++) removeSn(sPurge[i]);
+      __syncthreads();
+      nextDue = count ? dueMin() : INT64_MAX;
     }
   }
   for (u32 i = lane; i < u32(kNackSlots); i += 64) {
@@ -1758,30 +1862,80 @@ __global__ void __launch_bounds__(64) k_speakers(const u32 *__restrict__ roomPar
 // ---------------------------------------------------------------------------
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 
-hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
+// Zeroes an ingest's per-track ranges, error words, ExtPacket total and (with
+// buckets) the per-datagram store list in one launch (they were five to six
+// memsets on the ingest's critical path).
+__global__ void k_ing_init(u32 ntracks, u32 n, u32 *__restrict__ tBegin, u32 *__restrict__ tEnd,
+                           u32 *__restrict__ tRuns, u32 *__restrict__ err, u64 *__restrict__ total,
+                           u64 *__restrict__ store) {
+  const u32 stride = gridDim.x * blockDim.x;
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < ntracks || i < n || i < 4; i += stride) {
+    if (i < ntracks) {
+      tBegin[i] = 0;
+      tEnd[i] = 0;
+      tRuns[i] = 0;
+    }
+    if (store && i < n) store[i] = 0;
+    if (i < 4) err[i] = 0;
+    if (i < 2) total[i] = 0;
+  }
+}
+
+// An ingest's RTCP NACK results start empty (side stream, before k_ing_nack).
+__global__ void k_nack_init(u32 n, u32 *__restrict__ info, u32 *__restrict__ pairCnt) {
+  const u32 stride = gridDim.x * blockDim.x;
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) info[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *pairCnt = 0;
+}
+
+// The ingest chain on st (the prep stream: the next lkf_run's batch depends on
+// it).  The NACK queues (k_ing_nack) need only the flows: they run on `side`
+// after the stream kernel, beside the bucket decisions, the ExtPacket scan and
+// the run's preparation; `sideDone` is recorded after them (the next ingest
+// waits for it: it rewrites the parsed datagrams, flows and lists they read).
+hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side, hipEvent_t sideFork,
+                         hipEvent_t sideDone, bool *sideUsed) {
+  *sideUsed = false;
   if (a.n == 0) return hipSuccess;
+  {
+    const u32 m = a.ntracks > a.n ? a.ntracks : a.n;
+    u32 g = nblk(m < 4 ? 4 : m, 256);
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_ing_init, dim3(g), dim3(256), 0, st, a.ntracks, a.n, a.tBegin, a.tEnd, a.tRuns, a.err,
+                       a.total, a.bucket ? a.bucket->store : nullptr);
+  }
   hipLaunchKernelGGL(k_ing_parse, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.n, a.raw, a.streams, a.nstreams,
                      a.parsed, a.twcc, a.err);
   hipLaunchKernelGGL(k_ing_ranges, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.parsed, a.n, a.ntracks, a.tBegin, a.tEnd,
                      a.tRuns, a.err);
   hipLaunchKernelGGL(k_ing_lists, dim3(a.ntracks), dim3(64), 0, st, a.raws, a.streams, a.nstreams, a.tBegin,
                      a.tEnd, a.listStride, a.list, a.listCnt);
-  if (a.laneStreams)
-    hipLaunchKernelGGL(k_ing_stream, dim3(nblk(a.nstreams, 64)), dim3(64), 0, st, a.raws, a.parsed, a.streams,
-                       a.nstreams, a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates,
-                       a.ddStructs, a.ingDD, a.err, a.list, a.listCnt, a.listStride, a.lanePerm);
-  else if (a.nstreams)
+  if (a.nstreams) {
+    BktArgs bka = {};
+    if (a.bucket) {  // the buckets decided in stream order inside the stream kernel
+      bka.state = a.bucket->state;
+      bka.tag = a.bucket->tag;
+      bka.owner = a.bucket->owner;
+      bka.store = a.bucket->store;
+      bka.epoch = a.bucket->epoch;
+    }
     hipLaunchKernelGGL(k_ing_stream_wave, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams, a.hot,
                        a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs, a.ingDD,
-                       a.err, a.list, a.listCnt, a.listStride);
-  if (a.bucket) {  // the RTX buckets (before the ExtPackets: a rejected packet produces none)
-    const hipError_t r = launch_bucket_add(st, *a.bucket);
-    if (r != hipSuccess) return r;
+                       a.err, a.list, a.listCnt, a.listStride, bka);
   }
-  if (a.nack && a.nstreams)  // after the flows: the loss ranges it pushes
-    hipLaunchKernelGGL(k_ing_nack, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.flows, a.streams, a.nack,
+  if (a.nack && a.nstreams) {  // after the flows: the loss ranges it pushes
+    hipError_t r = hipEventRecord(sideFork, st);
+    if (r == hipSuccess) r = hipStreamWaitEvent(side, sideFork, 0);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL(k_nack_init, dim3(std::min<u32>(nblk(a.n, 256), 1024)), dim3(256), 0, side, a.n, a.nackInfo,
+                       a.nackPairCnt);
+    hipLaunchKernelGGL(k_ing_nack, dim3(a.nstreams), dim3(64), 0, side, a.raws, a.parsed, a.flows, a.streams, a.nack,
                        a.hot, a.tBegin, a.tEnd, a.list, a.listCnt, a.listStride, a.nackInfo, a.nackPairOff,
                        a.nackPairCnt, a.nackPairs, a.nackPairCap, a.err);
+    r = hipEventRecord(sideDone, side);
+    if (r != hipSuccess) return r;
+    *sideUsed = true;
+  }
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
   if (r != hipSuccess) return r;
@@ -1791,120 +1945,12 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a) {
 }
 
 // ---------------------------------------------------------------------------
-// The RTX bucket (bucket_oracle.h restates it): k_bkt_add walks each stream's
-// datagrams of the batch in order (one thread per stream: index arithmetic
-// only) and decides AddPacketWithSequenceNumber for those that reached it —
-// push (invalidate the skipped slots, store at the new head) or set (too old:
-// rejected; the slot already holds the SN: ErrRTXPacket) — on the slot tags;
-// a rejected packet produces no ExtPacket.  k_bkt_store then copies each
-// stored datagram whose slot no later datagram of the batch took (one wave
-// per datagram, 4-byte words), its SN field set to the adjusted SN.
+// The RTX bucket (bucket_oracle.h restates it): k_ing_stream_wave decides
+// AddPacketWithSequenceNumber per stream in datagram order (bkt_add_one; the
+// in-order runs' pushes lane-parallel) on the slot tags and lists what to
+// store per datagram; k_bkt_store then copies each stored datagram whose slot
+// no later datagram of the batch took, its SN field set to the adjusted SN.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_bkt_add(BucketLaunch A) {
-  // one wave per stream: lanes gather 64 datagrams' inputs at a time (the
-  // stream's candidates compacted into LDS in order), lane 0 steps the
-  // bucket over them — index arithmetic and tag stores only
-  __shared__ u32 sIc[64], sSn[64], sLen[64];
-  constexpr int kLdsSlots = 2048;
-  __shared__ u32 sOwn[kLdsSlots];  // this ingest's writer of each slot (rings up to 2,048 slots)
-  const u32 sid = blockIdx.x, lane = threadIdx.x;
-  if (sid >= A.nstreams) return;
-  const DevStream s = A.streams[sid];
-  if (s.closed) return;
-  const u32 pb = A.tBegin[s.track], pe = A.tEnd[s.track];
-  if (pb >= pe) return;
-  BucketState b = A.state[sid];
-  u32 *tag = A.tag + b.base;
-  u64 *owner = A.owner + b.base;
-  const u64 ep = u64(A.epoch) << 32;
-  const int Mc = int(b.maxSteps);
-  const bool lds = Mc <= kLdsSlots;
-  if (lds)
-    for (int i = int(lane); i < Mc; i += 64) sOwn[i] = 0xFFFFFFFFu;
-  __syncthreads();
-  // a slot taken again in this ingest: the earlier datagram is not stored
-  // (the LDS map, or for larger rings the global owner tagged with the epoch)
-  auto supersede = [&](int sl, u32 ic) {
-    if (lds) {
-      const u32 o = sOwn[sl];
-      if (o != 0xFFFFFFFFu) A.store[o] = 0;
-      sOwn[sl] = ic;
-    } else {
-      const u64 o = owner[sl];
-      if ((o & 0xFFFFFFFF00000000ull) == ep) A.store[u32(o)] = 0;
-      owner[sl] = ic == 0xFFFFFFFFu ? 0 : (ep | ic);
-    }
-  };
-  const bool useList = s.layer < 3;
-  const u32 nIdx = useList ? A.listCnt[s.track * 3 + s.layer] : pe - pb;
-  const u32 *lst = A.list + size_t(useList ? s.layer : 0) * A.listStride + pb;
-  const int M = int(b.maxSteps);
-  auto wrap = [&](int x) {
-    x %= M;
-    return x < 0 ? x + M : x;
-  };
-  for (u32 base = 0; base < nIdx; base += 64) {
-    const u32 k = base + lane;
-    u32 ic = 0;
-    bool cand = false;
-    if (k < nIdx) {
-      ic = useList ? lst[k] : pb + k;
-      cand = A.raws[ic].stream == sid && (A.flows[ic].flags & LKF_FLOW_BUCKET);
-    }
-    const u64 cm = __ballot(cand);
-    if (cand) {
-      const u32 pos = u32(__popcll(cm & ((1ull << lane) - 1)));
-      sIc[pos] = ic;
-      sSn[pos] = u32(u16(A.flows[ic].ext_sn));
-      sLen[pos] = A.raws[ic].len;
-    }
-    __syncthreads();
-    if (lane == 0) {
-      const u32 m = u32(__popcll(cm));
-      for (u32 j = 0; j < m; j++) {
-        const u32 icj = sIc[j], len = sLen[j];
-        const u16 sn = u16(sSn[j]);
-        int slot = -1;
-        if (len <= 1498) {
-          if (!b.init) {
-            b.head = u16(sn - 1);
-            b.init = 1;
-          }
-          const u16 diff = u16(sn - b.head);
-          if (diff == 0 || diff > (1u << 15)) {  // set
-            const int back = int(u16(b.head - sn));
-            if (back < M) {
-              const int sl = wrap(int(b.step) - back - 1);
-              const u32 t = tag[sl];
-              if (!((t >> 16) != 0xFFFFu && u16(t) == sn)) slot = sl;  // (a duplicate is not overwritten)
-            }
-          } else {  // push
-            const int gap = int(diff) - 1;
-            b.head = sn;
-            for (int i = 0; i < min(gap, M); i++) {
-              const int sl = wrap(int(b.step) + i);
-              tag[sl] = 0xFFFF0000u;
-              supersede(sl, 0xFFFFFFFFu);
-            }
-            slot = wrap(int(b.step) + gap);
-            b.step = u32(wrap(int(b.step) + gap + 1));
-          }
-        }
-        if (slot >= 0) {
-          tag[slot] = (len << 16) | sn;
-          supersede(slot, icj);
-          A.store[icj] = (1ull << 63) | (u64(sn) << 32) | u64(b.base + u32(slot));
-        } else {  // ErrPacketTooOld / ErrRTXPacket: no ExtPacket
-          A.flows[icj].flags = u8(A.flows[icj].flags & ~(LKF_FLOW_BUCKET | LKF_FLOW_FORWARD));
-          A.fwd[icj] = 0;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (lane == 0) A.state[sid] = b;
-}
-
 // one wave per datagram at a time, grid-stride; 16-B copies when the source is
 // 16-B aligned (the ring slots are)
 __global__ void __launch_bounds__(256) k_bkt_store(BucketLaunch A) {
@@ -1978,14 +2024,6 @@ __global__ void __launch_bounds__(64) k_bkt_read(u32 n, const int32_t *__restric
     }
     src[i] = r;
   }
-}
-
-hipError_t launch_bucket_add(hipStream_t st, const BucketLaunch &a) {
-  if (a.n == 0 || a.nstreams == 0) return hipSuccess;
-  const hipError_t r = hipMemsetAsync(a.store, 0, size_t(a.n) * sizeof(u64), st);
-  if (r != hipSuccess) return r;
-  hipLaunchKernelGGL(k_bkt_add, dim3(a.nstreams), dim3(64), 0, st, a);
-  return hipGetLastError();
 }
 
 hipError_t launch_bucket_store(hipStream_t st, const BucketLaunch &a) {

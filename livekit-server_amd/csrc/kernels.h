@@ -108,8 +108,6 @@ struct IngestLaunch {
   // per-stream datagram lists (k_ing_lists): [layer slot * listStride + tBegin + j], counts [track * 3 + slot]
   uint32_t *list, *listCnt;
   uint32_t listStride;
-  const uint32_t *lanePerm;  // k_ing_stream lane -> stream (nullptr: identity)
-  bool laneStreams;          // the lane-per-stream k_ing_stream (LKF_ING_LANE=1) instead of k_ing_stream_wave
   // NACK queues (nullptr: no stream has one): per stream state, per datagram
   // result (n_pairs | num_nacked << 16, 0: no RTCP NACK) and pair offset in
   // the bump-allocated pair buffer
@@ -153,7 +151,15 @@ struct BucketLaunch {
   uint8_t *ring;
   uint32_t epoch;   // this ingest's number (from 1)
 };
-hipError_t launch_bucket_add(hipStream_t s, const BucketLaunch &a);
+// the bucket arrays k_ing_stream_wave decides AddPacketWithSequenceNumber on
+// (state nullptr: no buckets)
+struct BktArgs {
+  BucketState *state;
+  uint32_t *tag;
+  uint64_t *owner;
+  uint64_t *store;
+  uint32_t epoch;
+};
 hipError_t launch_bucket_store(hipStream_t s, const BucketLaunch &a);
 // Bucket.GetPacket for RTX records: stream[i] (-1: no buffer / closed) and the
 // source SN; the packet is gathered to out + i * kBktSlot and src[i] = (that
@@ -178,7 +184,10 @@ struct SpeakersLaunch {
   uint32_t *counts;
 };
 
-hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a);
+// the ingest chain on s; with NACK queues k_ing_nack forks onto `side` after the
+// stream kernel (*sideUsed: sideDone was recorded there)
+hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a, hipStream_t side, hipEvent_t sideFork,
+                         hipEvent_t sideDone, bool *sideUsed);
 hipError_t launch_speakers(hipStream_t s, const SpeakersLaunch &a);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,

@@ -1,0 +1,116 @@
+// cpu_bench.cpp — the CPU baseline driver of bench.py (TEST INFRASTRUCTURE:
+// only bench.py's cpu_baseline leg calls it; the product path never does).
+//
+// the reference Go path cannot run here or on the GPU box,
+// so the CPU baseline is the oracle (this directory's scalar C++ restatement
+// of the Go forwarding path) timed on the host cores: one oracle engine per
+// thread, each forwarding its own shard of rooms (no shared state), every
+// thread started by one barrier; the timed region is the batches' control ops
+// (orc_ctl_batch), Buffer.calc (orc_ingest, with `ingress`) and the forwarding
+// (orc_run) — the same step bench.py times on the GPU.  Driving the shards
+// from C++ threads keeps Python (the GIL, ctypes marshalling) out of the
+// measurement.
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <thread>
+#include <vector>
+
+#include "../include/lkfwd.h"
+
+extern "C" {
+struct orc_engine;
+orc_engine *orc_create(uint32_t seq_size);
+void orc_destroy(orc_engine *e);
+int32_t orc_add_track(orc_engine *e, const lkf_track_params *p);
+int32_t orc_add_downtrack(orc_engine *e, const lkf_downtrack_params *p);
+int32_t orc_add_stream(orc_engine *e, const lkf_stream_params *p);
+int orc_ctl_batch(orc_engine *e, const lkf_ctl_event *evs, uint32_t n);
+int orc_submit_dd(orc_engine *e, const lkf_pkt_dd *dd, uint32_t n);
+int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena, uint64_t arena_len);
+int orc_get_stats(orc_engine *e, lkf_stats *out);
+int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len);
+int orc_ingested_ptr(orc_engine *e, const lkf_pkt **pkts, uint32_t *n);
+
+// one batch of a shard (pointers into the synthetic trace)
+typedef struct orc_bench_batch {
+  const lkf_pkt *pkts;
+  uint32_t n;
+  uint32_t nraw;
+  const uint8_t *arena;
+  uint64_t alen;
+  const lkf_pkt_dd *dd;     // nullptr: no DD side array
+  const lkf_raw_pkt *raws;  // the same batch as datagrams (ingress)
+  const lkf_ctl_event *ev;
+  uint32_t nev;
+  uint32_t pad;
+} orc_bench_batch;
+
+typedef struct orc_bench_shard {
+  const lkf_track_params *tracks;
+  const lkf_downtrack_params *dts;
+  const lkf_stream_params *streams;
+  const orc_bench_batch *batches;
+  uint32_t ntracks, ndts, nstreams, nbatches;
+} orc_bench_shard;
+
+// Runs every shard on its own thread (nshards threads); forwarded[i] = shard
+// i's forwarded tuples, *wall_s = seconds from the common start to the last
+// thread's end, busy_s[i] = shard i's own timed seconds (nullptr: not wanted).
+// 0, or the first non-zero return code of an oracle call.
+int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, int ingress, uint32_t seq_size,
+                  uint64_t *forwarded, double *busy_s, double *wall_s) {
+  std::vector<orc_engine *> eng(nshards, nullptr);
+  std::atomic<int> rc{0};
+  std::atomic<uint32_t> ready{0};
+  std::atomic<bool> go{false};
+  using clk = std::chrono::steady_clock;
+  std::vector<std::thread> th;
+  clk::time_point t0;
+  for (uint32_t i = 0; i < nshards; i++)
+    th.emplace_back([&, i]() {
+      const orc_bench_shard &s = shards[i];
+      orc_engine *e = orc_create(seq_size);
+      eng[i] = e;
+      int r = 0;
+      for (uint32_t t = 0; t < s.ntracks && !r; t++) r = orc_add_track(e, &s.tracks[t]) == int32_t(t) ? 0 : -1;
+      for (uint32_t d = 0; d < s.ndts && !r; d++) r = orc_add_downtrack(e, &s.dts[d]) == int32_t(d) ? 0 : -1;
+      if (ingress)
+        for (uint32_t k = 0; k < s.nstreams && !r; k++) r = orc_add_stream(e, &s.streams[k]) == int32_t(k) ? 0 : -1;
+      if (r) rc = r;
+      ready++;
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      const clk::time_point a = clk::now();
+      uint64_t fwd = 0;
+      for (uint32_t b = 0; b < s.nbatches && !r; b++) {
+        const orc_bench_batch &x = s.batches[b];
+        if (x.nev) r = orc_ctl_batch(e, x.ev, x.nev);
+        if (r) break;
+        if (ingress) {
+          r = orc_ingest(e, x.raws, x.nraw, x.arena, x.alen);
+          const lkf_pkt *p = nullptr;
+          uint32_t n = 0;
+          if (!r) r = orc_ingested_ptr(e, &p, &n);
+          if (!r) r = orc_run(e, p, n, x.arena, x.alen);
+        } else {
+          if (x.dd) r = orc_submit_dd(e, x.dd, x.n);
+          if (!r) r = orc_run(e, x.pkts, x.n, x.arena, x.alen);
+        }
+        lkf_stats st{};
+        if (!r) r = orc_get_stats(e, &st);
+        fwd += st.forwarded;
+      }
+      if (busy_s) busy_s[i] = std::chrono::duration<double>(clk::now() - a).count();
+      forwarded[i] = fwd;
+      if (r) rc = r;
+    });
+  while (ready.load() < nshards) std::this_thread::yield();
+  t0 = clk::now();
+  go.store(true, std::memory_order_release);
+  for (auto &t : th) t.join();
+  *wall_s = std::chrono::duration<double>(clk::now() - t0).count();
+  for (orc_engine *e : eng)
+    if (e) orc_destroy(e);
+  return rc.load();
+}
+}
