@@ -117,6 +117,15 @@ typedef struct lkf_downtrack_params {
   uint8_t ext_abs_send_time; /* absSendTimeExtID: 3 placeholder bytes, stamped by the sender */
   uint8_t playout_delay[3];  /* PlayOutDelay.Marshal() bytes (rtpextension/playoutdelay.go:40) */
   uint8_t has_expected_ts;   /* 1: getExpectedRTPTimestamp wired (downtrack.go:1765); 0: nil */
+  /* transport-cc extension id (0 = none): with send-side BWE (config.go:119-121) a video
+   * subscriber negotiates transport-cc instead of abs-send-time, and pion's TWCC
+   * HeaderExtensionInterceptor (transport.go:352-355; pion/interceptor v0.1.25
+   * pkg/twcc/header_extension_interceptor.go) appends a 2-byte transport-wide sequence number
+   * to every RTP packet the subscriber PeerConnection sends, counted per transport in send
+   * order (lkf_set_downtrack_transport binds the DownTrack to its PeerConnection's transport;
+   * an unbound DownTrack counts on its own) */
+  uint8_t ext_transport_cc;
+  uint8_t reserved_dp[3];
   int64_t bind_time_ns;      /* sequencer startTime (sequencer.go:100) on the virtual clock */
 } lkf_downtrack_params;
 
@@ -310,6 +319,15 @@ typedef struct lkf_stream_stats {
   uint64_t nacks;  /* sequence numbers NACKed (rtpStats.UpdateNack(numSeqNumsNacked), buffer.go:682-684) */
   uint8_t initialized;
   uint8_t reserved[7];
+  /* rtpStatsBase timing (rtpstats_receiver.go:106-107, :209-213): the first packet's arrival and the
+   * arrival of the latest in-order packet that started a new timestamp */
+  int64_t first_time_ns, highest_time_ns;
+  /* updateJitter (rtpstats_base.go:775-810, receive jitter in RTP clock units, float64) over the
+   * in-order and out-of-order non-duplicate packets with a payload, first packet of each timestamp */
+  uint64_t last_transit, last_jitter_ext_ts;
+  double jitter, max_jitter;
+  uint32_t gap_histogram[101]; /* updateGapHistogram (:201): [missing - 1] of in-order gaps, last bin also larger */
+  uint32_t reserved2;
 } lkf_stream_stats;
 
 /* One RTCP TransportLayerNack a Buffer sent from its deferred doNACKs

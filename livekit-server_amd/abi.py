@@ -73,11 +73,27 @@ class lkf_stream_stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "ext_start_sn", "ext_highest_sn", "ext_start_ts", "ext_highest_ts", "packets_lost",
         "packets_out_of_order", "packets_duplicate", "packets_padding", "bytes", "header_bytes",
-        "bytes_duplicate", "bytes_padding", "frames", "nacks")] + [("initialized", C.c_uint8),
-                                                                   ("reserved", C.c_uint8 * 7)]
+        "bytes_duplicate", "bytes_padding", "frames", "nacks")] + [
+            ("initialized", C.c_uint8), ("reserved", C.c_uint8 * 7),
+            ("first_time_ns", C.c_int64), ("highest_time_ns", C.c_int64),
+            ("last_transit", C.c_uint64), ("last_jitter_ext_ts", C.c_uint64),
+            ("jitter", C.c_double), ("max_jitter", C.c_double),
+            ("gap_histogram", C.c_uint32 * 101), ("reserved2", C.c_uint32)]
 
     def as_tuple(self):
-        return tuple(getattr(self, n) for n, _ in self._fields_[:-1])
+        """Every field but the reserved ones (jitter as float64 bits: compared exactly)."""
+        import struct
+        out = []
+        for n, _ in self._fields_:
+            if n.startswith("reserved"):
+                continue
+            v = getattr(self, n)
+            if n in ("jitter", "max_jitter"):
+                v = struct.unpack("<Q", struct.pack("<d", v))[0]
+            elif n == "gap_histogram":
+                v = tuple(v)
+            out.append(v)
+        return tuple(out)
 
 
 class lkf_speaker(C.Structure):
@@ -192,6 +208,8 @@ class lkf_downtrack_params(C.Structure):
         ("ext_abs_send_time", C.c_uint8),
         ("playout_delay", C.c_uint8 * 3),
         ("has_expected_ts", C.c_uint8),
+        ("ext_transport_cc", C.c_uint8),
+        ("reserved_dp", C.c_uint8 * 3),
         ("bind_time_ns", C.c_int64),
     ]
 
@@ -353,7 +371,7 @@ class lkfs_cfg(C.Structure):
         ("has_callbacks", C.c_int32),
         ("svc_dd", C.c_int32),
         ("h264", C.c_int32),
-        ("pad0", C.c_int32),
+        ("twcc", C.c_int32),
         ("room_ids", C.POINTER(C.c_uint32)),
     ]
 

@@ -98,6 +98,7 @@ struct BatchCtx {
   uint32_t *dFwdCnt = nullptr;
   uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
   uint32_t *dGFirst = nullptr;  // emit group g -> output position owning record 64g
+  uint32_t *dTwccBase = nullptr;  // per DownTrack: the batch's first transport-wide sequence number
   uint32_t *dLayerList = nullptr, *dLayerBefore = nullptr, *dLayerCnt = nullptr;  // k_layer_index
   lkf_out *dOut = nullptr;
   uint8_t *dOutArena = nullptr;
@@ -152,6 +153,13 @@ struct lkf_engine {
   hipStream_t decS = nullptr;   // decide stage (high priority)
   hipStream_t emitS = nullptr;  // emit stage (low priority)
   hipStream_t sendS = nullptr;  // sender statistics of a decided batch (low priority, beside its emit)
+  // transport-wide sequence numbers (pion TWCC header-extension interceptor,
+  // send-side BWE): a counter per transport (DownTracks bound to it count
+  // together, in record order) or per unbound DownTrack
+  std::vector<int32_t> dtTransport;
+  uint32_t *dTwccCtrD = nullptr, *dTwccCtrT = nullptr, *dTwccTOff = nullptr, *dTwccTList = nullptr;
+  uint32_t twccTCap = 0, twccListCap = 0, nTwccT = 0;
+  bool anyTwcc = false, twccDirty = false;
   hipStream_t sideS = nullptr;  // an ingest's NACK queues, beside the rest of the ingest and the run
   hipEvent_t sideFork = nullptr, sideDone = nullptr;
   bool sidePending = false;     // the next ingest waits for sideDone
@@ -363,6 +371,7 @@ struct lkf_engine {
   DevStream *dStreams = nullptr;
   StreamHot *dStreamHot = nullptr;
   uint64_t *dHist = nullptr;
+  uint32_t *dRxGap = nullptr;  // per stream RTPStatsReceiver gap histogram (kGapWords u32)
   RangeEntry *dStreamRings = nullptr;
   IngParsed *dParsed = nullptr;
   lkf_flow *dFlows = nullptr;
@@ -763,6 +772,7 @@ static int flush_topology(lkf_engine *e) {
     HIPCHK(hipMemcpy(e->dStreamHot + first, hot.data(), k * sizeof(StreamHot), hipMemcpyHostToDevice),
            "stream state upload");
     HIPCHK(hipMemset(e->dHist + first * kHistWords, 0, k * kHistWords * sizeof(uint64_t)), "history reset");
+    HIPCHK(hipMemset(e->dRxGap + first * kGapWords, 0, k * kGapWords * sizeof(uint32_t)), "gap histogram reset");
     e->pendStreams.clear();
   }
   return upload_done(e);
@@ -826,6 +836,8 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
   A(dalloc(&e->dDTCum, c.max_downtracks));
+  A(dalloc(&e->dTwccCtrD, c.max_downtracks));
+  if (ok) A(hipMemset(e->dTwccCtrD, 0, size_t(c.max_downtracks) * sizeof(uint32_t)));
   A(dalloc(&e->dSS, c.max_downtracks));
   A(dalloc(&e->dSeqDDIdx, c.max_downtracks));
   A(dalloc(&e->dSSGap, size_t(c.max_downtracks) * kGapWords));
@@ -857,6 +869,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dRecBase, c.max_downtracks));
     A(dalloc(&x.dByteBase, c.max_downtracks));
     A(dalloc(&x.dGFirst, c.max_out_pkts / 64 + 2));
+    A(dalloc(&x.dTwccBase, c.max_downtracks));
     A(dalloc(&x.dLayerList, 3 * size_t(c.max_batch_pkts) + 64));
     A(dalloc(&x.dLayerBefore, 3 * size_t(c.max_batch_pkts) + 64));
     A(dalloc(&x.dLayerCnt, 3 * size_t(c.max_tracks)));
@@ -883,6 +896,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dStreams, e->maxStreams));
   A(dalloc(&e->dStreamHot, e->maxStreams));
   A(dalloc(&e->dHist, size_t(e->maxStreams) * kHistWords));
+  A(dalloc(&e->dRxGap, size_t(e->maxStreams) * kGapWords));
   A(dalloc(&e->dStreamRings, size_t(e->maxStreams) * kRangeCap));
   A(dalloc(&e->dParsed, c.max_batch_pkts));
   A(dalloc(&e->dFlows, c.max_batch_pkts));
@@ -983,7 +997,7 @@ void lkf_destroy(lkf_engine *e) {
     if (p) (void)dfree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
-                  e->dStreams, e->dStreamHot, e->dHist, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
+                  e->dStreams, e->dStreamHot, e->dHist, e->dRxGap, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
                   e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktRing, e->dBktStream, e->dBktSn,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
@@ -992,7 +1006,8 @@ void lkf_destroy(lkf_engine *e) {
                   e->dNackPartB,
                   e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups, e->dSeqDD, e->dSeqDDIdx,
                   e->dSeqDDList, e->dRtxDD, e->dProv, e->dProvReq, e->dProvGroups, e->dProvOut,
-                  e->dDDTrk, e->dTrackDDTrk, e->dDDTrkIds, e->dDDTrkOut};
+                  e->dDDTrk, e->dTrackDDTrk, e->dDDTrkIds, e->dDDTrkOut, e->dTwccCtrD,
+                  e->dTwccCtrT, e->dTwccTOff, e->dTwccTList};
   for (void *p : ptrs)
     if (p) (void)dfree(p);
   for (void *p : {static_cast<void *>(e->dDDStruct), static_cast<void *>(e->dDDTrack),
@@ -1013,7 +1028,7 @@ void lkf_destroy(lkf_engine *e) {
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
-                 x.dRawPkts, x.dBktStore, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane};
+                 x.dRawPkts, x.dBktStore, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane, x.dTwccBase};
     for (void *p : q)
       if (p) (void)dfree(p);
     if (x.decided) (void)hipEventDestroy(x.decided);
@@ -1095,8 +1110,12 @@ int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
   d.extPlayout = p->ext_playout;
   d.extAbs = p->ext_abs_send_time;
   d.extDD = p->ext_dd;
+  d.extTcc = p->ext_transport_cc;
+  d.twccGroup = uint32_t(h);  // its own counter until bound to a transport
   std::memcpy(d.playout, p->playout_delay, 3);
   d.active = 1;
+  e->dtTransport.push_back(-1);
+  if (p->ext_transport_cc) e->anyTwcc = e->twccDirty = true;
   e->pendDTs.push_back(d);  // uploaded by flush_topology (one copy per batch of adds)
   e->schedDirty = true;
   return h;
@@ -1332,6 +1351,56 @@ static int rebuild_sched(lkf_engine *e) {
   return upload_done(e);
 }
 
+// Per transport, its transport-cc DownTracks in record order (track, then
+// DownTrack handle) for k_twcc_base; the counters of transports added since
+// the last rebuild start at 0 (pion's interceptor starts at 0 per
+// PeerConnection).  Queued runs read the lists: drained first.
+static int rebuild_twcc(lkf_engine *e) {
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  const uint32_t nt = uint32_t(e->transports.size());
+  std::vector<std::vector<uint32_t>> lst(nt);
+  std::vector<uint32_t> order(e->dtp.size());
+  for (uint32_t d = 0; d < order.size(); d++) order[d] = d;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t b) { return e->dtp[a].track < e->dtp[b].track; });
+  for (uint32_t d : order)
+    if (e->dtp[d].ext_transport_cc && e->dtTransport[d] >= 0) lst[size_t(e->dtTransport[d])].push_back(d);
+  std::vector<uint32_t> off(nt + 1, 0), flat;
+  for (uint32_t t = 0; t < nt; t++) {
+    off[t] = uint32_t(flat.size());
+    flat.insert(flat.end(), lst[t].begin(), lst[t].end());
+  }
+  off[nt] = uint32_t(flat.size());
+  if (nt > e->twccTCap) {  // grow the transport counters, keeping the old ones
+    const uint32_t cap = std::max<uint32_t>(nt, 2 * e->twccTCap + 64);
+    uint32_t *c = nullptr, *o = nullptr;
+    HIPCHK(dalloc(&c, cap), "alloc twcc counters");
+    HIPCHK(hipMemset(c, 0, size_t(cap) * sizeof(uint32_t)), "twcc counters reset");
+    if (e->dTwccCtrT) {
+      HIPCHK(hipMemcpy(c, e->dTwccCtrT, size_t(e->twccTCap) * sizeof(uint32_t), hipMemcpyDeviceToDevice),
+             "twcc counters move");
+      HIPCHK(dfree(e->dTwccCtrT), "free twcc counters");
+    }
+    if (e->dTwccTOff) HIPCHK(dfree(e->dTwccTOff), "free twcc offsets");
+    HIPCHK(dalloc(&o, cap + 1), "alloc twcc offsets");
+    e->dTwccCtrT = c;
+    e->dTwccTOff = o;
+    e->twccTCap = cap;
+  }
+  if (flat.size() > e->twccListCap || !e->dTwccTList) {
+    if (e->dTwccTList) HIPCHK(dfree(e->dTwccTList), "free twcc lists");
+    e->twccListCap = uint32_t(std::max<size_t>(flat.size(), 1024));
+    HIPCHK(dalloc(&e->dTwccTList, e->twccListCap), "alloc twcc lists");
+  }
+  HIPCHK(hipMemcpy(e->dTwccTOff, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "twcc offsets");
+  if (!flat.empty())
+    HIPCHK(hipMemcpy(e->dTwccTList, flat.data(), flat.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "twcc lists");
+  e->nTwccT = nt;
+  e->twccDirty = false;
+  return upload_done(e);
+}
+
 int lkf_run(lkf_engine *e, void *stream) {
   if (!e) return LKF_EINVAL;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
@@ -1341,6 +1410,10 @@ int lkf_run(lkf_engine *e, void *stream) {
   }
   if (e->schedDirty) {
     int rc = rebuild_sched(e);
+    if (rc) return rc;
+  }
+  if (e->twccDirty) {
+    int rc = rebuild_twcc(e);
     if (rc) return rc;
   }
   const int ci = int(e->nRuns % lkf_engine::kCtx);
@@ -1615,6 +1688,10 @@ int lkf_run(lkf_engine *e, void *stream) {
     const int rc = scanTail(s);
     if (rc) return rc;
   }
+  if (e->anyTwcc)  // the transports' sequence ranges of this batch (after the forwarded counts)
+    HIPCHK(launch_twcc_base(s, e->dDTs, nd, x.dFwdCnt, e->dTwccCtrD, e->dTwccCtrT, e->dTwccTOff, e->dTwccTList,
+                            e->nTwccT, x.dTwccBase),
+           "twcc base");
   HIPCHK(hipEventRecord(x.decided, s), "event");
   if (e->nSeqDD && e->ddAlloc) {  // sequencer ddBytes (decide stream: before the next batch's decide)
     SeqDDLaunch q;
@@ -1664,6 +1741,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.tupleCap = e->cfg.max_batch_tuples;
   m.arenaLen = e->curArenaLen;
   m.ddCap = e->ddArenaCap;
+  m.twccBase = e->anyTwcc ? x.dTwccBase : nullptr;
   m.gCap = e->cfg.max_out_pkts / 64 + 2;
   // One workgroup per 64-record group (grid = the capacity bound; workgroups
   // past the batch's records exit at once).  Short-lived workgroups free their
@@ -1912,10 +1990,19 @@ int lkf_set_downtrack_transport(lkf_engine *e, int32_t dt, int32_t t) {
     return LKF_EINVAL;
   int rc = srtp_init(e);
   if (rc) return rc;
+  rc = flush_topology(e);  // (the DownTrack's static parameters are on the device)
+  if (rc) return rc;
   rc = drain_streams(e);  // queued protect stages read the binding
   if (rc) return rc;
   SrtpDT v{uint32_t(t + 1), 0, 0};
   HIPCHK(hipMemcpy(e->dSrtpDT + dt, &v, sizeof(v), hipMemcpyHostToDevice), "srtp bind");
+  // its transport-wide sequence numbers: the transport's counter from now on
+  e->dtTransport[size_t(dt)] = t;
+  const uint32_t grp = t >= 0 ? (0x80000000u | uint32_t(t)) : uint32_t(dt);
+  HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(e->dDTs + dt) + offsetof(DevDT, twccGroup), &grp, sizeof(grp),
+                   hipMemcpyHostToDevice),
+         "twcc group");
+  if (e->dtp[size_t(dt)].ext_transport_cc) e->twccDirty = true;
   return upload_done(e);
 }
 
@@ -2350,6 +2437,10 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
   HIPCHK(launch_rtx_emit(e->sendS, true, n, e->dRtx, e->dRtxSrc, srcArena, e->dDTs, e->dTracks, e->dRtxLen,
                          e->dRtxOff, e->dRtxOut, rtxDD),
          "rtx write");
+  if (e->anyTwcc)  // transport-cc numbers in record (send) order
+    HIPCHK(launch_twcc_stamp(e->sendS, e->dDTs, e->dTwccCtrD, e->dTwccCtrT, n, nullptr, nullptr, nullptr, e->dRtx,
+                             e->dRtxOff, e->dRtxLen, e->dRtxOut),
+           "twcc stamp");
   if (tot) {
     CHKRANGE(e->dRtxOut, tot, "async d2h");
     HIPCHK(hipMemcpyAsync(out_arena, e->dRtxOut, tot, hipMemcpyDeviceToHost, e->sendS), "rtx bytes copy");
@@ -2506,6 +2597,13 @@ static int sender_list(lkf_engine *e, std::vector<SenderUpd> &list) {
   return LKF_OK;
 }
 
+// a padding / blank packet's header with the pacer's extension block
+// (abs-send-time) and the TWCC interceptor's element (k_pad pad_hdr_len)
+static uint32_t pad_hdr_bytes(const lkf_downtrack_params &p) {
+  const uint32_t eb = (p.ext_abs_send_time ? 4u : 0u) + (p.ext_transport_cc ? 3u : 0u);
+  return eb ? 16u + ((eb + 3) & ~3u) : 12u;
+}
+
 static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_t n, int64_t now_ns, lkf_out *out,
                       uint8_t *arena, uint64_t out_cap, uint64_t arena_cap, uint32_t *n_out, uint64_t *arena_len,
                       uint32_t *bytes_sent) {
@@ -2595,6 +2693,10 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
     a.cnt = e->dPadCnt;
     a.bytes = e->dPadCnt + m;
     HIPCHK(launch_pad(ds, a), "pad");
+    if (e->anyTwcc)  // transport-cc numbers in request (send) order
+      HIPCHK(launch_twcc_stamp(ds, e->dDTs, e->dTwccCtrD, e->dTwccCtrT, m, e->dPadOut, e->dPadOff, e->dPadCnt, nullptr,
+                               nullptr, nullptr, e->dPadArena),
+             "twcc stamp");
     HIPCHK(hipStreamSynchronize(ds), "sync");
     D2H(cnt.data(), e->dPadCnt, 2 * size_t(m) * sizeof(uint32_t), "pad cnt copy");
   }
@@ -2628,7 +2730,7 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
         u.dt = o.dt;
         u.hdr = 12;
         u.pay = 0;
-        u.pad = uint16_t(o.out_len - (e->dtp[o.dt].ext_abs_send_time ? 20 : 12));
+        u.pad = uint16_t(o.out_len - pad_hdr_bytes(e->dtp[o.dt]));
         u.marker = (o.flags & LKF_OUT_MARKER) ? 1 : 0;
         ul.push_back(u);
       }
@@ -3290,6 +3392,7 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.ntracks = nt;
   a.hot = e->dStreamHot;
   a.hist = e->dHist;
+  a.rxGap = e->dRxGap;
   a.rings = e->dStreamRings;
   a.parsed = e->dParsed;
   a.tBegin = e->dITBegin;
@@ -3485,6 +3588,13 @@ int lkf_stream_stats_get(lkf_engine *e, int32_t sid, lkf_stream_stats *o) {
   o->bytes_padding = h.bytesPadding;
   o->frames = h.frames;
   o->nacks = h.nacks;
+  o->first_time_ns = h.firstTime;
+  o->highest_time_ns = h.highestTime;
+  o->last_transit = h.lastTransit;
+  o->last_jitter_ext_ts = h.lastJitterExtTs;
+  o->jitter = h.jitter;
+  o->max_jitter = h.maxJitter;
+  D2H(o->gap_histogram, e->dRxGap + size_t(sid) * kGapWords, kGapBins * sizeof(uint32_t), "stream gap copy");
   return LKF_OK;
 }
 

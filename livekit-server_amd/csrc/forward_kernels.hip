@@ -271,7 +271,7 @@ struct Lane {
   u32 kind, codec, hasRefTS, clockRate;
   const u32 *offs;
   // static DT
-  u8 extPlayout, extAbs, extDD;
+  u8 extPlayout, extAbs, extDD, extTcc;
   // dependency-descriptor selector (F_DD): state staged in LDS, the track's
   // structure ring, this batch's decoded descriptors, the marshal buffer
   DDState *dd;
@@ -1762,7 +1762,8 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   const bool playout = L.extPlayout && !hasf(L, F_PLAYOUT_ACKED);
   const bool ddOn = DDK && f.ddLen > 0 && L.extDD;
   const int eh = (ddOn && f.ddLen > 16) ? 2 : 1;  // element header bytes
-  int extBytes = (ddOn ? eh + f.ddLen : 0) + (playout ? eh + 3 : 0) + (L.extAbs ? eh + 3 : 0);
+  // (+ the transport-cc element pion's TWCC interceptor appends after the pacer's, 2 bytes)
+  int extBytes = (ddOn ? eh + f.ddLen : 0) + (playout ? eh + 3 : 0) + (L.extAbs ? eh + 3 : 0) + (L.extTcc ? eh + 2 : 0);
   int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
   int hdrLen = 12 + 4 * cc + extBlock;
   const bool useCodec = f.cbLen > 0 && (p.flags & LKF_PKT_VP8);
@@ -2366,7 +2367,8 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
   const bool ddOn = DDK && f && ddLen > 0 && L.extDD;
   const int eh = (ddOn && ddLen > 16) ? 2 : 1;
-  const int extBytes = (ddOn ? eh + ddLen : 0) + (playout ? eh + 3 : 0) + (L.extAbs ? eh + 3 : 0);
+  const int extBytes =
+      (ddOn ? eh + ddLen : 0) + (playout ? eh + 3 : 0) + (L.extAbs ? eh + 3 : 0) + (L.extTcc ? eh + 2 : 0);
   const int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
   const int hdrLen = 12 + 4 * cc + extBlock;
   const u32 outLen = f ? u32(hdrLen + int(p.plen)) : 0u;
@@ -2668,6 +2670,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.extPlayout = dt.extPlayout;
   L.extAbs = dt.extAbs;
   L.extDD = dt.extDD;
+  L.extTcc = dt.extTcc;
   L.err = A.err;
 #ifdef LKF_SVC_WATCH
   L.watchDt = d;
@@ -3123,7 +3126,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         // output records + sequencer slots of the forwarded lanes
         const int cc = p.hdr0 & 0xf;
         const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
-        const int extBytes = (playout ? 4 : 0) + (L.extAbs ? 4 : 0);
+        const int extBytes = (playout ? 4 : 0) + (L.extAbs ? 4 : 0) + (L.extTcc ? 3 : 0);
         const int extBlock = extBytes ? 4 + ((extBytes + 3) & ~3) : 0;
         const int hdrLen = 12 + 4 * cc + extBlock;
         const bool useCodec = video && cbLen > 0 && (p.flags & LKF_PKT_VP8);
@@ -3477,6 +3480,7 @@ struct EmitArgs {
   u64 outCap, outByteCap;
   u32 *err;
   const u8 *ddArena;  // marshalled DD bytes of T_DD tuples
+  const u32 *twccBase;  // per DownTrack: the batch's first transport-wide sequence number (k_twcc_base)
   // capacities (checked builds test device-computed indices against them)
   u32 maxDts, npkts;
   u64 tupleCap, arenaLen, ddCap, gCap;
@@ -3591,7 +3595,11 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       const int cc = p.hdr0 & 0xf;
       const bool playout = t.flags & T_PLAYOUT;
       const bool ddOn = (PRE == PRE_MAX_DD) && (t.flags & T_DD);
-      const bool hasExt = playout || dt.extAbs || ddOn;
+      const bool hasExt = playout || dt.extAbs || ddOn || dt.extTcc;
+      // pion's TWCC HeaderExtensionInterceptor: the transport's next sequence
+      // number in send order (this record's ordinal in its DownTrack's output
+      // after the DownTrack's base)
+      const u16 tcc = dt.extTcc ? u16(A.twccBase[d] + u32(r - A.recBase[lo])) : u16(0);
       w[0] = u8((p.hdr0 & 0xe0) | (hasExt ? 0x10 : 0) | cc);  // V, P copied; X per new extensions
       w[1] = u8(((t.flags & LKF_OUT_MARKER) ? 0x80 : 0) | (dt.pt & 0x7f));
       const u16 sn = u16(t.extSN);
@@ -3610,7 +3618,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       const u8 *raw = A.arena + p.arenaOff;
       for (int i = 0; i < 4 * cc; i++) w[n++] = raw[12 + i];
       if (hasExt && !(ddOn && t.ddLen > 16)) {  // pion Header.MarshalTo one-byte profile (RFC 8285)
-        const int eb = (ddOn ? 1 + t.ddLen : 0) + (playout ? 4 : 0) + (dt.extAbs ? 4 : 0);
+        const int eb = (ddOn ? 1 + t.ddLen : 0) + (playout ? 4 : 0) + (dt.extAbs ? 4 : 0) + (dt.extTcc ? 3 : 0);
         const int words = (eb + 3) >> 2;
         w[n++] = 0xBE;
         w[n++] = 0xDE;
@@ -3632,9 +3640,14 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
           w[n++] = 0;
           w[n++] = 0;
         }
+        if (dt.extTcc) {  // rtp.TransportCCExtension.Marshal: big-endian u16
+          w[n++] = u8((dt.extTcc << 4) | 1);
+          w[n++] = u8(tcc >> 8);
+          w[n++] = u8(tcc);
+        }
         for (int i = eb; i < 4 * words; i++) w[n++] = 0;
       } else if (hasExt) {  // two-byte profile 0x1000: a DD element above 16 B
-        const int eb = 2 + t.ddLen + (playout ? 5 : 0) + (dt.extAbs ? 5 : 0);
+        const int eb = 2 + t.ddLen + (playout ? 5 : 0) + (dt.extAbs ? 5 : 0) + (dt.extTcc ? 4 : 0);
         const int words = (eb + 3) >> 2;
         w[n++] = 0x10;
         w[n++] = 0x00;
@@ -3656,6 +3669,12 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
           w[n++] = 0;
           w[n++] = 0;
           w[n++] = 0;
+        }
+        if (dt.extTcc) {
+          w[n++] = dt.extTcc;
+          w[n++] = 2;
+          w[n++] = u8(tcc >> 8);
+          w[n++] = u8(tcc);
         }
         for (int i = eb; i < 4 * words; i++) w[n++] = 0;
       }
@@ -4133,8 +4152,14 @@ struct PadArgs {
 
 // RTP header of a padding / blank packet (pion Header.MarshalTo; pacer
 // writeRTPHeaderExtensions pacer/base.go:71-100: abs-send-time placeholder)
+__device__ __forceinline__ u32 pad_hdr_len(const DevDT &dt) {
+  const u32 eb = (dt.extAbs ? 4u : 0u) + (dt.extTcc ? 3u : 0u);
+  return eb ? 16u + ((eb + 3) & ~3u) : 12u;
+}
+// (the transport-cc element, when negotiated, is written with 0 and stamped in
+// send order by k_twcc_stamp after the kernel)
 __device__ int pad_header(u8 *w, bool padding, bool marker, const DevDT &dt, u64 sn, u64 ts) {
-  w[0] = u8(0x80 | (padding ? 0x20 : 0) | (dt.extAbs ? 0x10 : 0));
+  w[0] = u8(0x80 | (padding ? 0x20 : 0) | ((dt.extAbs || dt.extTcc) ? 0x10 : 0));
   w[1] = u8((marker ? 0x80 : 0) | (dt.pt & 0x7f));
   w[2] = u8(sn >> 8);
   w[3] = u8(sn);
@@ -4146,14 +4171,26 @@ __device__ int pad_header(u8 *w, bool padding, bool marker, const DevDT &dt, u64
   w[9] = u8(dt.ssrc >> 16);
   w[10] = u8(dt.ssrc >> 8);
   w[11] = u8(dt.ssrc);
-  if (!dt.extAbs) return 12;
+  const int hl = int(pad_hdr_len(dt));
+  if (hl == 12) return 12;
   w[12] = 0xBE;
   w[13] = 0xDE;
   w[14] = 0;
-  w[15] = 1;
-  w[16] = u8((dt.extAbs << 4) | 2);
-  w[17] = w[18] = w[19] = 0;
-  return 20;
+  w[15] = u8((hl - 16) / 4);
+  int n = 16;
+  if (dt.extAbs) {
+    w[n++] = u8((dt.extAbs << 4) | 2);
+    w[n++] = 0;
+    w[n++] = 0;
+    w[n++] = 0;
+  }
+  if (dt.extTcc) {
+    w[n++] = u8((dt.extTcc << 4) | 1);
+    w[n++] = 0;
+    w[n++] = 0;
+  }
+  while (n < hl) w[n++] = 0;
+  return hl;
 }
 __device__ void pad_record(const PadArgs &A, u32 r, u32 k, u32 d, u64 off, u32 len, u64 sn, u64 ts, bool marker) {
   lkf_out o;
@@ -4214,7 +4251,7 @@ __global__ void __launch_bounds__(64) k_pad(PadArgs A) {
         __syncthreads();
         if (lane == 0) seq_push_padding(L, first, first + num - 1);
         __syncthreads();
-        const u32 len = (dt.extAbs ? 20 : 12) + kPadPayload;
+        const u32 len = pad_hdr_len(dt) + kPadPayload;
         const u32 stride = (len + 15) & ~15u;
         for (u32 k = lane; k < num; k += 64) {
           u8 *w = A.arena + ob + u64(k) * stride;
@@ -4253,7 +4290,7 @@ __global__ void __launch_bounds__(64) k_pad(PadArgs A) {
         int vl = 0;
         if (codec == LKF_CODEC_VP8 && hasf(L, F_VP8)) vl = vp8_padding(L, !(k == 0 && fen), vd);
         const u32 pl = codec == LKF_CODEC_OPUS ? u32(kOpusSilenceLen) : codec == LKF_CODEC_H264 ? 47u : u32(vl) + 31u;
-        const u32 len = (dt.extAbs ? 20 : 12) + pl;
+        const u32 len = pad_hdr_len(dt) + pl;
         if (lane == 0) {
           u8 *w = A.arena + off;
           const int h = pad_header(w, false, true, dt, first + k, ts[k]);
@@ -4632,6 +4669,118 @@ hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const u32 *tBe
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Transport-wide sequence numbers (pion/interceptor v0.1.25 pkg/twcc
+// HeaderExtensionInterceptor, added per subscriber PeerConnection with
+// send-side BWE, pkg/rtc/transport.go:352-355): every RTP packet a
+// PeerConnection writes on a stream that negotiated transport-cc gets
+// uint16(n) of the PeerConnection's counter n (atomic.AddUint32 - 1) as a
+// 2-byte extension element, in send order.  A batch's send order is its
+// record order (track, DownTrack, packet): a transport's DownTracks take
+// consecutive ranges in that order (k_twcc_base, after decide), the records
+// their base plus their ordinal (k_emit); padding, blank frames and RTX are
+// stamped in call order (k_twcc_stamp).
+// ---------------------------------------------------------------------------
+__global__ void k_twcc_base(const DevDT *__restrict__ dts, u32 ndts, const u32 *__restrict__ fwdCnt,
+                            u32 *__restrict__ ctrD, u32 *__restrict__ ctrT, const u32 *__restrict__ tOff,
+                            const u32 *__restrict__ tList, u32 ntr, u32 *__restrict__ base) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < ndts) {  // a DownTrack counting on its own (no transport bound)
+    const DevDT dt = dts[i];
+    if (dt.extTcc && !(dt.twccGroup & 0x80000000u)) {
+      base[i] = ctrD[i];
+      ctrD[i] += fwdCnt[i];
+    }
+  } else if (i - ndts < ntr) {  // a transport: its DownTracks in record order
+    const u32 t = i - ndts;
+    u32 c = ctrT[t];
+    for (u32 k = tOff[t]; k < tOff[t + 1]; k++) {
+      const u32 d = tList[k];
+      base[d] = c;
+      c += fwdCnt[d];
+    }
+    ctrT[t] = c;
+  }
+}
+hipError_t launch_twcc_base(hipStream_t s, const DevDT *dts, uint32_t ndts, const uint32_t *fwdCnt, uint32_t *ctrD,
+                            uint32_t *ctrT, const uint32_t *tOff, const uint32_t *tList, uint32_t ntr,
+                            uint32_t *base) {
+  const u32 n = ndts + ntr;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_twcc_base, dim3((n + 255) / 256), dim3(256), 0, s, dts, ndts, fwdCnt, ctrD, ctrT, tOff, tList,
+                     ntr, base);
+  return hipGetLastError();
+}
+
+// the 2-byte element with extension id `id` (RFC 8285 one- or two-byte block) <- seq
+__device__ void twcc_put(u8 *pkt, u32 len, u8 id, u16 seq) {
+  if (len < 12 || !(pkt[0] & 0x10)) return;
+  u32 n = 12 + 4 * (pkt[0] & 15);
+  if (n + 4 > len) return;
+  const u32 prof = (u32(pkt[n]) << 8) | pkt[n + 1];
+  const u32 end = n + 4 + 4 * ((u32(pkt[n + 2]) << 8) | pkt[n + 3]);
+  n += 4;
+  while (n < end && end <= len) {
+    if (pkt[n] == 0) {
+      n++;
+      continue;
+    }
+    u8 eid;
+    u32 el;
+    if (prof == 0xBEDE) {
+      eid = pkt[n] >> 4;
+      el = (pkt[n] & 15) + 1;
+      n++;
+      if (eid == 15) return;
+    } else {
+      eid = pkt[n];
+      el = pkt[n + 1];
+      n += 2;
+    }
+    if (eid == id && el == 2 && n + 2 <= len) {
+      pkt[n] = u8(seq >> 8);
+      pkt[n + 1] = u8(seq);
+      return;
+    }
+    n += el;
+  }
+}
+
+// Control-rate packets in send order (one thread: a few packets per call).
+// pad mode: requests r < n, packets k < cnt[r] at records recOff[r] + k;
+// rtx mode: records r < n with len[r] > 0 at off[r], DownTrack rtx[r].dt.
+__global__ void k_twcc_stamp(const DevDT *__restrict__ dts, u32 *ctrD, u32 *ctrT, u32 n, const lkf_out *recs,
+                             const u64 *recOff, const u32 *cnt, const lkf_rtx *rtx, const u64 *off, const u32 *len,
+                             u8 *arena) {
+  if (threadIdx.x || blockIdx.x) return;
+  auto next = [&](u32 d) -> u16 {
+    const DevDT dt = dts[d];
+    u32 &c = (dt.twccGroup & 0x80000000u) ? ctrT[dt.twccGroup & 0x7fffffffu] : ctrD[d];
+    return u16(c++);
+  };
+  for (u32 r = 0; r < n; r++) {
+    if (recs) {
+      for (u32 k = 0; k < cnt[r]; k++) {
+        const lkf_out &o = recs[recOff[r] + k];
+        const u8 id = dts[o.dt].extTcc;
+        if (id) twcc_put(arena + o.out_off, o.out_len, id, next(o.dt));
+      }
+    } else if (len[r]) {
+      const u32 d = u32(rtx[r].dt);
+      const u8 id = dts[d].extTcc;
+      if (id) twcc_put(arena + off[r], len[r], id, next(d));
+    }
+  }
+}
+hipError_t launch_twcc_stamp(hipStream_t s, const DevDT *dts, uint32_t *ctrD, uint32_t *ctrT, uint32_t n,
+                             const lkf_out *recs, const uint64_t *recOff, const uint32_t *cnt, const lkf_rtx *rtx,
+                             const uint64_t *off, const uint32_t *len, uint8_t *arena) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_twcc_stamp, dim3(1), dim3(64), 0, s, dts, ctrD, ctrT, n, recs, recOff, cnt, rtx, off, len,
+                     arena);
+  return hipGetLastError();
+}
+
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   EmitArgs A;
   A.perm = a.perm;
@@ -4651,6 +4800,7 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   A.outByteCap = a.outByteCap;
   A.err = a.err;
   A.ddArena = a.ddArena;
+  A.twccBase = a.twccBase;
   A.maxDts = a.maxDts;
   A.npkts = a.npkts;
   A.tupleCap = a.tupleCap;

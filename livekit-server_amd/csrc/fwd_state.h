@@ -100,15 +100,19 @@ static_assert(sizeof(DTHot) == 256, "DTHot must be 256 B");
 constexpr int kStatWords = 4 + LKF_DROP_NREASONS;
 constexpr int kStatCopies = 64;
 
-// Static per-DownTrack parameters (Bind-time: downtrack.go:362-432), 16 B.
-struct DevDT {
+// Static per-DownTrack parameters (Bind-time: downtrack.go:362-432), 32 B.
+struct alignas(16) DevDT {
   uint32_t track;
   uint32_t ssrc;
   uint8_t pt, extPlayout, extAbs, extDD;
   uint8_t playout[3];
   uint8_t active;
+  uint8_t extTcc;   // transport-cc extension id (pion TWCC HeaderExtensionInterceptor), 0: none
+  uint8_t pad[3];
+  uint32_t twccGroup;  // transport-wide sequence counter (its transport's, or the DownTrack's own)
+  uint32_t pad2[2];
 };
-static_assert(sizeof(DevDT) == 16, "DevDT must be 16 B");
+static_assert(sizeof(DevDT) == 32, "DevDT must be 32 B");
 
 struct RangeEntry {  // closed range of utils.RangeMap (rangemap.go:43-47)
   uint64_t start, end, value;
@@ -337,8 +341,13 @@ struct alignas(16) StreamHot {  // per-stream ingress state (256 B)
   uint32_t flags;
   uint16_t snStart, snHighest;
   uint16_t rmHead, rmCount;
+  // rtpStatsBase timing and receive jitter (rtpstats_receiver.go:106-107,
+  // :209-213, :237; rtpstats_base.go:775-810): virtual clock = arrival
+  int64_t firstTime, highestTime;
+  uint64_t lastTransit, lastJitterExtTs;
+  double jitter, maxJitter;
   uint8_t loudest;
-  uint8_t pad[63];
+  uint8_t pad[15];
 };
 static_assert(sizeof(StreamHot) == 256, "StreamHot must be 256 B");
 

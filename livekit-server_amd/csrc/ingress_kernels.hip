@@ -895,6 +895,33 @@ __device__ int bkt_add_one(const BktCtx &k, u16 sn, u32 len, u32 ic) {
   return slot;
 }
 
+// rtpStatsBase.updateGapHistogram (rtpstats_base.go:871-882) of the receiver
+__device__ __forceinline__ void rx_gap(u32 *gap, u64 g) {
+  if (g < 2) return;
+  const u64 missing = g - 1;
+  atomicAdd(&gap[missing > u64(kGapBins) ? kGapBins - 1 : u32(missing - 1)], 1u);
+}
+// rtpStatsBase.updateJitter (rtpstats_base.go:775-810) of the receiver (Go's
+// int64 products wrap: formed in u64)
+__device__ __forceinline__ u64 rx_transit(const StreamHot &h, u32 clockRate, u64 ets, i64 t) {
+  const i64 since = i64(u64(t) - u64(h.firstTime));
+  return u64(i64(u64(since) * u64(i64(clockRate))) / 1000000000LL) - ets;
+}
+__device__ __forceinline__ void rx_jitter_fold(StreamHot &h, u64 transit, u64 ets) {
+  if (h.lastTransit != 0) {
+    i64 d = i64(transit - h.lastTransit);
+    if (d < 0) d = i64(0 - u64(d));
+    h.jitter += (double(d) - h.jitter) / 16;
+    if (h.jitter > h.maxJitter) h.maxJitter = h.jitter;
+  }
+  h.lastTransit = transit;
+  h.lastJitterExtTs = ets;
+}
+__device__ __forceinline__ void rx_jitter(StreamHot &h, u32 clockRate, u64 ets, i64 t) {
+  if (h.lastJitterExtTs == ets) return;
+  rx_jitter_fold(h, rx_transit(h, clockRate, ets, t), ets);
+}
+
 // One datagram through Buffer.calc (buffer.go:407-489): processHeaderExtensions,
 // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241), the padding
 // RangeMap, the dependency descriptor; its flow, forward flag and DD record.
@@ -902,7 +929,7 @@ template <int HS>
 __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream &s,
                                          const IngParsed &p, const lkf_raw_pkt &rp, u32 ic, lkf_flow *flows,
                                          u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *ddStates,
-                                         DDStruct *ddStructs, u32 *err, const BktCtx *bk) {
+                                         DDStruct *ddStructs, u32 *err, const BktCtx *bk, u32 *gap) {
   const i64 arrival = rp.arrival_ns;
   lkf_flow f = {};
   f.pkt = 0xffffffffu;
@@ -936,6 +963,8 @@ __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring
         break;
       }
       h.flags |= S_INIT;
+      h.firstTime = arrival;  // rtpstats_receiver.go:106-107
+      h.highestTime = arrival;
       rsn = wa16_update(h, p.sn);
       rts = wa32_update(h, p.ts);
     } else {
@@ -965,9 +994,11 @@ __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring
       }
       ooo = true;
     } else {
+      rx_gap(gap, u64(gapSN));
       hist_clear_range<HS>(hs, rsn.preHighest + 1, rsn.extVal - 1);
       h.packetsLost += u64(gapSN - 1);
       hist_set<HS>(hs, rsn.extVal);
+      if (p.ts != u32(rts.preHighest)) h.highestTime = arrival;  // :209-213
       if (gapSN > 1) {
         f.flags |= LKF_FLOW_HAS_LOSS;
         f.loss_start = rsn.preHighest + 1;
@@ -985,6 +1016,7 @@ __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring
         h.bytes += pktSize;
         h.headerBytes += u64(hdrSize);
         if (p.flags & IP_MARKER) h.frames++;
+        rx_jitter(h, s.clockRate, rts.extVal, arrival);
       }
     }
     if (dup) f.flags |= LKF_FLOW_DUPLICATE;
@@ -1062,6 +1094,11 @@ __device__ void closed_flows(const DevStream &s, u32 sid, u32 pb, u32 pe, const 
 // DD, first packet, audio) goes through ing_step on lane 0, as the
 // lane-per-stream kernel does for every datagram.
 // ---------------------------------------------------------------------------
+// a 64-bit value of lane x (readlane returns int: the low word must not sign-extend)
+__device__ __forceinline__ u64 rl_u64(u64 v, u32 x) {
+  return (u64(u32(__builtin_amdgcn_readlane(int(u32(v >> 32)), x))) << 32) |
+         u64(u32(__builtin_amdgcn_readlane(int(u32(v)), x)));
+}
 __device__ __forceinline__ u64 wave_incl_scan_u64(u64 v, u32 lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -1082,7 +1119,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows,
     u32 *__restrict__ fwd, const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
     IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list, const u32 *__restrict__ cnt, u32 stride,
-    BktArgs bka) {
+    BktArgs bka, u32 *__restrict__ rxGap) {
   static_assert(kHistWords == 64, "one history word per lane");
   static_assert(sizeof(StreamHot) == 64 * sizeof(u32), "one StreamHot dword per lane");
   __shared__ u64 sHist[kHistWords];
@@ -1098,6 +1135,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     return;
   }
   u64 *const hg = hist + size_t(sid) * kHistWords;
+  u32 *const gap = rxGap + size_t(sid) * kGapWords;
   sHist[lane] = hg[lane];
   reinterpret_cast<u32 *>(&sh)[lane] = reinterpret_cast<const u32 *>(hot + sid)[lane];
   // the stream's RTX bucket (bka.state nullptr: no buckets)
@@ -1147,7 +1185,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         for (u32 x = 0; x < m; x++)
           if (sR[x].stream == sid)
             ing_step<1>(sh, sHist, ring, s, sP[x], sR[x], sI[x], flows, fwd, ingDD, raw, ddStates, ddStructs, err,
-                        bkp);
+                        bkp, gap);
       }
       __syncthreads();
     }
@@ -1191,7 +1229,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u32 L = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;
     if (L == 0) {
       if (lane == 0 && rp.stream == sid)
-        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err, bkp);
+        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err, bkp, gap);
       __syncthreads();
       j++;
       continue;
@@ -1206,6 +1244,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u16 snLast = u16(__shfl(u32(p.sn), int(L - 1), 64));
     const u32 tsLast = u32(__shfl(p.ts, int(L - 1), 64));
     const u64 bSLast = __shfl(bS, int(L - 1), 64);
+    // RTPStatsReceiver timing: highestTime from the run's last lane that
+    // starts a timestamp (the TS never decreases inside a run); the jitter
+    // filter over the run's new timestamps, in order (a float64 recurrence:
+    // transits in parallel, the fold serial and wave-uniform)
+    const u64 newTs = __ballot(run && p.ts != (lane == 0 ? sh.tsHighest : prevTs));
+    const u64 prevExtTs = __shfl_up(extTs, 1, 64);
+    const u64 newJ = __ballot(run && extTs != (lane == 0 ? sh.lastJitterExtTs : prevExtTs));
+    const u64 transit = rx_transit(sh, s.clockRate, extTs, rp.arrival_ns);
+    if (run) rx_gap(gap, u64(gs));
     if (run) {
       lkf_flow f = {};
       f.pkt = 0xffffffffu;
@@ -1256,6 +1303,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         sB.step = u32(bkt_wrap(int(sB.step) + int(bSLast), M));
       }
     }
+    if (newTs) {
+      const int kl = 63 - __clzll(static_cast<long long>(newTs));
+      const i64 tl = i64(rl_u64(u64(rp.arrival_ns), u32(kl)));
+      if (lane == 0) sh.highestTime = tl;
+    }
+    if (newJ) {  // (every lane runs the fold on uniform values; lane 0 stores it)
+      StreamHot jh;
+      jh.lastTransit = sh.lastTransit;
+      jh.jitter = sh.jitter;
+      jh.maxJitter = sh.maxJitter;
+      jh.lastJitterExtTs = sh.lastJitterExtTs;
+      for (u64 w = newJ; w; w &= w - 1) {
+        const u32 k = u32(__ffsll(static_cast<long long>(w)) - 1);
+        rx_jitter_fold(jh, rl_u64(transit, k), rl_u64(extTs, k));
+      }
+      if (lane == 0) {
+        sh.lastTransit = jh.lastTransit;
+        sh.jitter = jh.jitter;
+        sh.maxJitter = jh.maxJitter;
+        sh.lastJitterExtTs = jh.lastJitterExtTs;
+      }
+    }
     __syncthreads();
     if (run) atomicOr(reinterpret_cast<unsigned long long *>(&sHist[(ext >> 6) & (kHistWords - 1)]), 1ull << (ext & 63));
     __syncthreads();
@@ -1280,11 +1349,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
 // lane 0.  A datagram's result: info = n_pairs | num_nacked << 16 (0: no
 // RTCP NACK) and the offset of its pairs in the batch's pair buffer.
 // ---------------------------------------------------------------------------
-// a 64-bit value of lane x (readlane returns int: the low word must not sign-extend)
-__device__ __forceinline__ u64 rl_u64(u64 v, u32 x) {
-  return (u64(u32(__builtin_amdgcn_readlane(int(u32(v >> 32)), x))) << 32) |
-         u64(u32(__builtin_amdgcn_readlane(int(u32(v)), x)));
-}
 
 __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__ raws,
                                                  const IngParsed *__restrict__ q, const lkf_flow *__restrict__ flows,
@@ -1677,7 +1741,7 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
       bool ok = true;
       int n = 0;
       const int cc = q.b0 & 0xf;
-      pre[n++] = u8((q.b0 & 0xe0) | (dt.extAbs ? 0x10 : 0) | cc);
+      pre[n++] = u8((q.b0 & 0xe0) | ((dt.extAbs || dt.extTcc) ? 0x10 : 0) | cc);
       pre[n++] = u8((x.meta.marker ? 0x80 : 0) | (dt.pt & 0x7f));
       pre[n++] = u8(x.meta.target_sn >> 8);
       pre[n++] = u8(x.meta.target_sn);
@@ -1686,12 +1750,13 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
       for (int k = 0; k < 4 * cc; k++) pre[n++] = b[12 + k];
       // the pacer's extension block (pacer/base.go:71-100): the sequencer's
       // ddBytes under the DownTrack's DD extension id (downtrack.go:1684; ID 0
-      // or no bytes: skipped), then abs-send-time; pion's one-byte profile, or
-      // the two-byte profile for a DD above 16 B
+      // or no bytes: skipped), then abs-send-time, then the TWCC interceptor's
+      // transport-cc element (0 here, stamped in send order by k_twcc_stamp);
+      // pion's one-byte profile, or the two-byte profile for a DD above 16 B
       const u32 ddLen = (dd && dt.extDD) ? dd[size_t(i) * kSeqDDBytes] : 0u;
       const u8 *ddB = ddLen ? dd + size_t(i) * kSeqDDBytes + 1 : nullptr;
       if (ddLen > 16) {
-        const int eb = 2 + int(ddLen) + (dt.extAbs ? 5 : 0);
+        const int eb = 2 + int(ddLen) + (dt.extAbs ? 5 : 0) + (dt.extTcc ? 4 : 0);
         const int words = (eb + 3) >> 2;
         pre[0] |= 0x10;
         pre[n++] = 0x10;
@@ -1708,9 +1773,15 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
           pre[n++] = 0;
           pre[n++] = 0;
         }
+        if (dt.extTcc) {
+          pre[n++] = dt.extTcc;
+          pre[n++] = 2;
+          pre[n++] = 0;
+          pre[n++] = 0;
+        }
         for (int k = eb; k < 4 * words; k++) pre[n++] = 0;
-      } else if (ddLen || dt.extAbs) {
-        const int eb = (ddLen ? 1 + int(ddLen) : 0) + (dt.extAbs ? 4 : 0);
+      } else if (ddLen || dt.extAbs || dt.extTcc) {
+        const int eb = (ddLen ? 1 + int(ddLen) : 0) + (dt.extAbs ? 4 : 0) + (dt.extTcc ? 3 : 0);
         const int words = (eb + 3) >> 2;
         pre[0] |= 0x10;
         pre[n++] = 0xBE;
@@ -1724,6 +1795,11 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
         if (dt.extAbs) {
           pre[n++] = u8((dt.extAbs << 4) | 2);
           pre[n++] = 0;
+          pre[n++] = 0;
+          pre[n++] = 0;
+        }
+        if (dt.extTcc) {
+          pre[n++] = u8((dt.extTcc << 4) | 1);
           pre[n++] = 0;
           pre[n++] = 0;
         }
@@ -1921,7 +1997,7 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
     }
     hipLaunchKernelGGL(k_ing_stream_wave, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams, a.hot,
                        a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs, a.ingDD,
-                       a.err, a.list, a.listCnt, a.listStride, bka);
+                       a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap);
   }
   if (a.nack && a.nstreams) {  // after the flows: the loss ranges it pushes
     hipError_t r = hipEventRecord(sideFork, st);

@@ -64,10 +64,20 @@ struct EmitLaunch {
   uint32_t *err;
   uint32_t grid;
   const uint8_t *ddArena;  // non-null: batches with DD tracks (k_emit<PRE_MAX_DD>)
+  const uint32_t *twccBase = nullptr;  // per DownTrack transport-cc base of the batch (DownTracks with extTcc)
   // capacities (tested in -DLKF_CHECKED=1 builds)
   uint32_t maxDts, npkts;
   uint64_t tupleCap, arenaLen, ddCap, gCap;
 };
+// transport-wide sequence numbers (pion TWCC header-extension interceptor):
+// the batch's base per DownTrack after decide, and the stamping of control-rate
+// packets (padding / blank: recs + recOff + cnt; RTX: rtx + off + len)
+hipError_t launch_twcc_base(hipStream_t s, const DevDT *dts, uint32_t ndts, const uint32_t *fwdCnt, uint32_t *ctrD,
+                            uint32_t *ctrT, const uint32_t *tOff, const uint32_t *tList, uint32_t ntr,
+                            uint32_t *base);
+hipError_t launch_twcc_stamp(hipStream_t s, const DevDT *dts, uint32_t *ctrD, uint32_t *ctrT, uint32_t n,
+                             const lkf_out *recs, const uint64_t *recOff, const uint32_t *cnt, const lkf_rtx *rtx,
+                             const uint64_t *off, const uint32_t *len, uint8_t *arena);
 // -DLKF_CHECKED=1 builds: {violations, first site, its index, its capacity}
 hipError_t read_check(unsigned long long out[4], int reset);
 
@@ -92,6 +102,7 @@ struct IngestLaunch {
   uint32_t nstreams, ntracks;
   StreamHot *hot;
   uint64_t *hist;
+  uint32_t *rxGap;  // per stream RTPStatsReceiver gap histogram (kGapWords)
   RangeEntry *rings;
   IngParsed *parsed;
   uint32_t *tBegin, *tEnd, *tRuns, *err;

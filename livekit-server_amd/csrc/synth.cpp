@@ -362,6 +362,10 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         d.ext_dd = (video && tg[track].dd && (s % 3) != 2) ? 9 : 0;  // some subscribers lack the DD extension
         d.ext_playout = 0;
         d.ext_abs_send_time = video ? 3 : 0;
+        if (video && (cfg->twcc >= 2 || (cfg->twcc == 1 && (s % 2) == 0))) {  // send-side BWE subscriber
+          d.ext_abs_send_time = 0;
+          d.ext_transport_cc = 5;
+        }
         d.has_expected_ts = cb ? 1 : 0;
         d.bind_time_ns = t0 - 50 * MS;
         int dt = (int)tr->dts.size();

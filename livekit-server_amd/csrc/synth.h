@@ -35,7 +35,8 @@ typedef struct lkfs_cfg {
   int32_t h264;          /* configs 1-3: 1 -> H.264 simulcast publishers (config 1: the publisher;
                             else every third) with SPS key frames as single NALU / STAP-A / STAP-B /
                             FU-A; <= 0 -> VP8 only */
-  int32_t pad0;
+  int32_t twcc;          /* send-side BWE: 1 -> every second subscriber's video DownTracks negotiate
+                            transport-cc (id 5) instead of abs-send-time; 2 -> all of them; 0 -> none */
   const uint32_t *room_ids; /* non-null: generate rooms room_ids[0..rooms) (a bin-packed shard)
                                instead of room_base + [0, rooms) */
 } lkfs_cfg;

@@ -14,11 +14,12 @@ from . import abi
 class Trace:
     def __init__(self, config, duration_s=10.0, batch_s=1.0, rooms=0, participants=0, room_base=0,
                  loss=-1.0, reorder=-1.0, with_events=-1, has_callbacks=-1, seed=0, svc_dd=-1, h264=0, room_ids=None,
-                 synth_lib=None):
+                 synth_lib=None, twcc=0):
         self.lib = synth_lib or abi.load_synth()
         cfg = abi.lkfs_cfg(config=config, seed=seed, duration_s=duration_s, batch_s=batch_s, rooms=rooms,
                            participants=participants, room_base=room_base, loss=loss, reorder=reorder,
-                           with_events=with_events, has_callbacks=has_callbacks, svc_dd=svc_dd, h264=h264)
+                           with_events=with_events, has_callbacks=has_callbacks, svc_dd=svc_dd, h264=h264,
+                           twcc=twcc)
         if room_ids is not None:  # a bin-packed shard (rooms.plan_room_shards)
             self._room_ids = (C.c_uint32 * max(1, len(room_ids)))(*room_ids)
             cfg.room_ids = self._room_ids

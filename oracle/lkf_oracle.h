@@ -2510,14 +2510,49 @@ struct RTPStatsReceiver {
   u64 packetsOutOfOrder = 0, packetsDuplicate = 0, packetsLost = 0, packetsPadding = 0, frames = 0;
   u64 bytes = 0, headerBytes = 0, bytesDuplicate = 0, headerBytesDuplicate = 0, bytesPadding = 0,
       headerBytesPadding = 0;
+  // rtpStatsBase timing and jitter (rtpstats_base.go:133-190): packet times on
+  // the caller's clock (the datagram arrival), clock rate of the stream
+  i64 firstTime = 0, highestTime = 0;
+  u64 lastTransit = 0, lastJitterExtTimestamp = 0;
+  double jitter = 0, maxJitter = 0;
+  u32 clockRate = 0;
+  u32 gapHistogram[101] = {};  // cGapHistogramNumBins rtpstats_base.go:31
 
   bool isInRange(u64 esn, u64 ehsn) const {  // rtpstats_receiver.go:427-430
     i64 diff = i64(ehsn - esn);
     return diff >= 0 && diff < i64(cHistorySize);
   }
-  RTPFlowState Update(u16 sn, u32 ts, bool marker, int payloadSize) { return Update(sn, ts, marker, 12, payloadSize, 0); }
-  // Update rtpstats_receiver.go:76-241 (jitter / snapshots / report timing out of scope)
+  // rtpStatsBase.updateGapHistogram rtpstats_base.go:871-882
+  void updateGapHistogram(i64 gap) {
+    if (gap < 2) return;
+    const i64 missing = gap - 1;
+    if (missing > i64(101))
+      gapHistogram[100]++;
+    else
+      gapHistogram[missing - 1]++;
+  }
+  // rtpStatsBase.updateJitter rtpstats_base.go:775-810 (Go's int64 products wrap:
+  // formed in u64; no snapshots)
+  void updateJitter(u64 ets, i64 packetTime) {
+    if (lastJitterExtTimestamp == ets) return;
+    const i64 since = i64(u64(packetTime) - u64(firstTime));
+    const u64 packetTimeRTP = u64(i64(u64(since) * u64(i64(clockRate))) / 1000000000LL);
+    const u64 transit = packetTimeRTP - ets;
+    if (lastTransit != 0) {
+      i64 d = i64(transit - lastTransit);
+      if (d < 0) d = i64(0 - u64(d));
+      jitter += (double(d) - jitter) / 16;
+      if (jitter > maxJitter) maxJitter = jitter;
+    }
+    lastTransit = transit;
+    lastJitterExtTimestamp = ets;
+  }
+  RTPFlowState Update(u16 sn, u32 ts, bool marker, int payloadSize) { return Update(0, sn, ts, marker, 12, payloadSize, 0); }
   RTPFlowState Update(u16 sn, u32 ts, bool marker, int hdrSize, int payloadSize, int paddingSize) {
+    return Update(0, sn, ts, marker, hdrSize, payloadSize, paddingSize);
+  }
+  // Update rtpstats_receiver.go:76-241 (snapshots / report timing out of scope)
+  RTPFlowState Update(i64 packetTime, u16 sn, u32 ts, bool marker, int hdrSize, int payloadSize, int paddingSize) {
     RTPFlowState fs;
     const u64 pktSize = u64(hdrSize + payloadSize + paddingSize);
     if (ended) {
@@ -2532,6 +2567,8 @@ struct RTPStatsReceiver {
         return fs;
       }
       initialized = true;
+      firstTime = packetTime;
+      highestTime = packetTime;
       rsn = sequenceNumber.Update(sn);
       rts = timestamp.Update(ts);
     } else {
@@ -2560,9 +2597,12 @@ struct RTPStatsReceiver {
       fs.ExtSequenceNumber = rsn.ExtendedVal;
       fs.ExtTimestamp = rts.ExtendedVal;
     } else {
+      updateGapHistogram(gapSN);
       history.ClearRange(rsn.PreExtendedHighest + 1, rsn.ExtendedVal - 1);
       packetsLost += u64(gapSN - 1);
       history.Set(rsn.ExtendedVal);
+      // the first packet of a timestamp (rtpstats_receiver.go:209-213)
+      if (ts != u32(rts.PreExtendedHighest)) highestTime = packetTime;
       if (gapSN > 1) {
         fs.HasLoss = true;
         fs.LossStartInclusive = rsn.PreExtendedHighest + 1;
@@ -2580,6 +2620,7 @@ struct RTPStatsReceiver {
         bytes += pktSize;
         headerBytes += u64(hdrSize);
         if (marker) frames++;
+        updateJitter(rts.ExtendedVal, packetTime);
       }
     }
     return fs;

@@ -69,6 +69,7 @@ struct ODT {
   orc_ss::RTPStatsSender ss;
   // SRTP: the subscriber transport and this SSRC's rollover state
   int32_t transport = -1;
+  u32 ownTwcc = 0;  // transport-wide sequence counter while no transport is bound
   orc_srtp::SSRCState srtp;
 };
 
@@ -117,7 +118,8 @@ struct orc_engine {
   std::vector<lkf_pkt_dd> pendingDD;
   // SRTP sessions (one per transport) and the last protected output
   std::vector<orc_srtp::Session> transports;
-  std::vector<std::unique_ptr<orc_srtp::SessionGcm>> transportsGcm;  // (null: AES-CM transport)
+  std::vector<std::unique_ptr<orc_srtp::SessionGcm>> transportsGcm;
+  std::vector<u32> transportTwcc;  // pion TWCC HeaderExtensionInterceptor.nextSequenceNr per PeerConnection  // (null: AES-CM transport)
   std::vector<u8> protArena;
   // RED: per source track (lkf_red_encode / lkf_red_decode)
   std::map<u32, orc_red::RedEncoder> redEnc;
@@ -250,6 +252,51 @@ static ExtPacket toExt(const lkf_pkt &d, const u8 *arena, const lkf_pkt_dd *dd, 
   return p;
 }
 
+// pion/interceptor v0.1.25 pkg/twcc HeaderExtensionInterceptor.BindLocalStream
+// (added per subscriber PeerConnection with send-side BWE, pkg/rtc/
+// transport.go:352-355): every RTP packet written on a stream that negotiated
+// transport-cc gets SetExtension(id, TransportCCExtension{uint16(n)}.Marshal())
+// with n = atomic.AddUint32(&nextSequenceNr, 1) - 1 of the PeerConnection, in
+// send order.  PARITY UNPINNED (no reference test covers it).
+static u16 twcc_next(orc_engine *e, ODT &d) {
+  u32 &c = d.transport >= 0 ? e->transportTwcc[size_t(d.transport)] : d.ownTwcc;
+  return u16(c++);
+}
+// writes the 2-byte element `id` of a marshalled packet in place (the element
+// was set with a placeholder where the pacer path builds the header)
+static void twcc_put(u8 *pkt, size_t len, u8 id, u16 v) {
+  if (len < 12 || !(pkt[0] & 0x10)) return;
+  size_t x = 12 + 4 * size_t(pkt[0] & 0x0f);
+  if (x + 4 > len) return;
+  const u16 prof = u16((pkt[x] << 8) | pkt[x + 1]);
+  const size_t end = x + 4 + 4 * ((size_t(pkt[x + 2]) << 8) | pkt[x + 3]);
+  size_t p = x + 4;
+  while (p < end && end <= len) {
+    if (pkt[p] == 0) {
+      p++;
+      continue;
+    }
+    u8 eid;
+    size_t l;
+    if (prof == 0xBEDE) {
+      eid = u8(pkt[p] >> 4);
+      l = size_t(pkt[p] & 0x0f) + 1;
+      p++;
+      if (eid == 15) return;
+    } else {
+      eid = pkt[p];
+      l = pkt[p + 1];
+      p += 2;
+    }
+    if (eid == id && l == 2) {
+      pkt[p] = u8(v >> 8);
+      pkt[p + 1] = u8(v);
+      return;
+    }
+    p += l;
+  }
+}
+
 // DownTrack.WriteRTP downtrack.go:680-760 on the virtual clock.
 static void writeRTP(orc_engine *e, u32 dtIdx, ODT &d, const ExtPacket &ep, u32 pktIdx, int8_t layer,
                      u32 pd_payload_off) {
@@ -286,6 +333,8 @@ static void writeRTP(orc_engine *e, u32 dtIdx, ODT &d, const ExtPacket &ep, u32 
   if (d.p.ext_playout && !d.playoutAcked)
     hdr.SetExtension(d.p.ext_playout, std::vector<u8>(d.p.playout_delay, d.p.playout_delay + 3));
   if (d.p.ext_abs_send_time) hdr.SetExtension(d.p.ext_abs_send_time, std::vector<u8>{0, 0, 0});
+  // the TWCC interceptor's element (numbered in send order: orc_run's output pass)
+  if (d.p.ext_transport_cc) hdr.SetExtension(d.p.ext_transport_cc, std::vector<u8>{0, 0});
   // sequencer.push downtrack.go:724-735
   i64 arrivalMs = ep.Arrival / 1000000;
   d.seq->push(arrivalMs, ep.ExtSequenceNumber, tp.rtp.extSequenceNumber, tp.rtp.extTimestamp, hdr.Marker, i8(layer),
@@ -496,6 +545,8 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   for (auto &tds : trackDts)
     for (u32 d : tds)
       for (auto &o : e->dts[d]->outs) {
+        if (e->dts[d]->p.ext_transport_cc)  // send order = output order
+          twcc_put(o.bytes.data(), o.bytes.size(), e->dts[d]->p.ext_transport_cc, twcc_next(e, *e->dts[d]));
         lkf_out r = o.rec;
         r.out_off = off;
         e->outRecs.push_back(r);
@@ -529,6 +580,7 @@ int32_t orc_add_transport(orc_engine *e, const lkf_transport_params *p) {
   if (!p || (p->profile != LKF_SRTP_AES128_CM_HMAC_SHA1_80 && p->profile != LKF_SRTP_AEAD_AES_128_GCM))
     return LKF_EINVAL;
   e->transports.emplace_back(p->master_key, p->master_salt);
+  e->transportTwcc.push_back(0);
   e->transportsGcm.emplace_back(p->profile == LKF_SRTP_AEAD_AES_128_GCM
                                     ? std::make_unique<orc_srtp::SessionGcm>(p->master_key, p->master_salt)
                                     : nullptr);
@@ -861,6 +913,10 @@ int orc_rtx_emit(orc_engine *e, const lkf_rtx *rtx, uint32_t n, const lkf_raw_pk
       if (m.targetSeqNo == x.meta.target_sn && !m.ddBytes.empty()) hdr.SetExtension(d.p.ext_dd, m.ddBytes);
     }
     if (d.p.ext_abs_send_time) hdr.SetExtension(d.p.ext_abs_send_time, std::vector<u8>{0, 0, 0});
+    if (d.p.ext_transport_cc) {  // the TWCC interceptor, in send order
+      const u16 tcc = twcc_next(e, d);
+      hdr.SetExtension(d.p.ext_transport_cc, std::vector<u8>{u8(tcc >> 8), u8(tcc)});
+    }
     std::vector<u8> bytes;
     hdr.Marshal(bytes);
     bytes.insert(bytes.end(), payload.begin(), payload.end());
@@ -907,6 +963,10 @@ static void padPacket(orc_engine *e, ODT &d, u32 dtIdx, u32 reqIdx, RtpHeader hd
   hdr.ExtensionProfile = 0;
   hdr.Extensions.clear();
   if (d.p.ext_abs_send_time) hdr.SetExtension(d.p.ext_abs_send_time, std::vector<u8>{0, 0, 0});
+  if (d.p.ext_transport_cc) {  // the TWCC interceptor, in send order
+    const u16 tcc = twcc_next(e, d);
+    hdr.SetExtension(d.p.ext_transport_cc, std::vector<u8>{u8(tcc >> 8), u8(tcc)});
+  }
   OOut o;
   hdr.Marshal(o.bytes);
   o.bytes.insert(o.bytes.end(), payload.begin(), payload.end());
@@ -1456,6 +1516,7 @@ int32_t orc_add_stream(orc_engine *e, const lkf_stream_params *p) {
   auto s = std::make_unique<OStream>();
   s->p = *p;
   s->clockRate = e->tracks[p->track].p.clock_rate;
+  s->stats.clockRate = s->clockRate;  // RTPStatsParams.ClockRate (buffer.go Bind)
   s->codec = e->tracks[p->track].p.codec;
   if (p->audio_level_ext) {
     AudioLevelParams ap;
@@ -1511,7 +1572,7 @@ static lkf_flow calc(orc_engine *e, OStream &b, const lkf_raw_pkt &rp, const u8 
       }
     }
   }
-  RTPFlowState fs = b.stats.Update(h.sn, h.ts, h.marker, h.hdrSize, h.payloadLen, h.paddingSize);
+  RTPFlowState fs = b.stats.Update(rp.arrival_ns, h.sn, h.ts, h.marker, h.hdrSize, h.payloadLen, h.paddingSize);
   if (b.nacker) {  // updateStreamState buffer.go:556-564
     b.nacker->Remove(h.sn);
     if (fs.HasLoss)
@@ -1750,6 +1811,13 @@ int orc_stream_stats_get(orc_engine *e, int32_t s, lkf_stream_stats *o) {
   o->bytes_padding = r.bytesPadding;
   o->frames = r.frames;
   o->nacks = e->streams[s]->nacks;
+  o->first_time_ns = r.firstTime;
+  o->highest_time_ns = r.highestTime;
+  o->last_transit = r.lastTransit;
+  o->last_jitter_ext_ts = r.lastJitterExtTimestamp;
+  o->jitter = r.jitter;
+  o->max_jitter = r.maxJitter;
+  for (int i = 0; i < 101; i++) o->gap_histogram[i] = r.gapHistogram[i];
   return LKF_OK;
 }
 

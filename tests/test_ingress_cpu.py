@@ -150,3 +150,75 @@ def test_oracle_nack_rtcp_consistent(pkg, workload, oracle):
         assert stats == nacked
     finally:
         o.destroy(oh)
+
+
+def test_oracle_receiver_timing_and_jitter(pkg, workload, abi):
+    """RTPStatsReceiver's firstTime / highestTime, gap histogram and receive
+    jitter (rtpstats_receiver.go:106-107, :201, :209-213, :237; updateJitter
+    rtpstats_base.go:775-810) against an independent Python restatement that
+    walks each stream's datagrams with the oracle's flow classification (no
+    reference test covers these fields: parity unpinned beyond this
+    cross-check and GPU = oracle).  Config 1 has no padding-only datagrams, so
+    every handled datagram carries a payload and its flow SN is unadjusted."""
+    import struct
+    o = load_oracle()
+    tr = workload.Trace(1, duration_s=4.0, batch_s=1.0, loss=0.08, reorder=0.05, seed=12)
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        workload.load_streams(o.api, h, tr)
+        st = {}
+        for b in range(tr.nbatches):
+            rp, n, ar, alen = tr.batch_raw(b)
+            assert o.api["ingest"](h, rp, n, ar, alen) == 0
+            fl = pkg.flows_array(o.api, h)
+            for i in range(n):
+                f = int(fl["flags"][i])
+                if f & (abi.LKF_FLOW_NOT_HANDLED | abi.LKF_FLOW_BAD):
+                    continue
+                s = st.setdefault(int(rp[i].stream), dict(first=None, high=None, hsn=None, hts=None, lt=0,
+                                                          ljt=0, j=0.0, mj=0.0, gap=[0] * 101))
+                t, esn, ets = int(rp[i].arrival_ns), int(fl["ext_sn"][i]), int(fl["ext_ts"][i])
+                clock = tr.tracks[tr.streams[int(rp[i].stream)].track].clock_rate
+                if s["first"] is None:
+                    s["first"] = s["high"] = t
+                    pre_ts = (ets - 1) & 0xFFFFFFFF
+                    s["hsn"] = esn - 1
+                else:
+                    pre_ts = s["hts"] & 0xFFFFFFFF
+                if esn > s["hsn"]:  # in order
+                    g = esn - s["hsn"]
+                    if g >= 2:
+                        s["gap"][100 if g - 1 > 101 else g - 2] += 1
+                    if (ets & 0xFFFFFFFF) != pre_ts:
+                        s["high"] = t
+                    s["hsn"] = esn
+                s["hts"] = ets if s["hts"] is None else max(s["hts"], ets)
+                if not f & abi.LKF_FLOW_DUPLICATE and s["ljt"] != ets:  # updateJitter
+                    since = (t - s["first"]) & (2**64 - 1)
+                    prod = (since * clock) & (2**64 - 1)
+                    prod = prod - 2**64 if prod >= 2**63 else prod
+                    rtp = ((abs(prod) // 10**9) * (1 if prod >= 0 else -1)) & (2**64 - 1)  # Go's truncating /
+                    transit = (rtp - ets) & (2**64 - 1)
+                    if s["lt"] != 0:
+                        d = (transit - s["lt"]) & (2**64 - 1)
+                        d = d - 2**64 if d >= 2**63 else d
+                        s["j"] += (float(abs(d)) - s["j"]) / 16
+                        s["mj"] = max(s["mj"], s["j"])
+                    s["lt"], s["ljt"] = transit, ets
+        assert len(st) == tr.nstreams
+        jit = 0
+        for sid, s in st.items():
+            g = abi.lkf_stream_stats()
+            assert o.api["stream_stats_get"](h, sid, C.byref(g)) == 0
+            assert g.first_time_ns == s["first"] and g.highest_time_ns == s["high"], sid
+            assert list(g.gap_histogram) == s["gap"], sid
+            assert g.last_transit == s["lt"] and g.last_jitter_ext_ts == s["ljt"], sid
+            assert struct.pack("<d", g.jitter) == struct.pack("<d", s["j"]), (sid, g.jitter, s["j"])
+            assert struct.pack("<d", g.max_jitter) == struct.pack("<d", s["mj"]), sid
+            jit += g.jitter > 0
+        assert jit == tr.nstreams
+        assert sum(sum(s["gap"]) for s in st.values()) > 0
+    finally:
+        o.destroy(h)
+        tr.close()

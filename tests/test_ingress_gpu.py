@@ -202,3 +202,14 @@ def test_ingress_nack_heavy_loss(pkg, workload, abi):
     tr = workload.Trace(2, duration_s=3.0, batch_s=0.05, rooms=4, loss=0.25, reorder=0.1, seed=77)
     assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
     assert run_ingress_parity.nack_pkts > 100
+
+
+def test_ingress_config3_bench_size(pkg, workload, abi):
+    """configs[2] at the per-GPU size bench.py runs (125 rooms x 50
+    participants, 6,875 streams, ~16 M tuples per 1-s batch): raw datagrams
+    through Buffer.calc (stream kernel, buckets, NACK queues) and the
+    forwarding, the speaker ranking after every batch, and every stream's
+    RTPStatsReceiver — counters, timing, gap histogram and jitter — equal to
+    the oracle's."""
+    tr = workload.Trace(3, duration_s=2.0, batch_s=1.0, rooms=125)
+    assert run_ingress_parity(pkg, workload, abi, tr) > 0

@@ -75,3 +75,43 @@ def test_oracle_twcc_pushes(kw, pkg, workload, abi):
         assert pushes > 500 and markers > 10
     finally:
         o.destroy(h)
+
+
+def test_oracle_transport_cc_numbering(pkg, workload, abi):
+    """The oracle's TWCC interceptor restatement: per transport, the records of
+    its transport-cc DownTracks carry consecutive sequence numbers in output
+    (send) order across batches; abs-send-time subscribers carry none; an
+    unbound DownTrack counts on its own."""
+    import ctypes as C
+
+    from tests import srtp_lib
+    from tests.oracle_lib import load as load_oracle
+    from tests.test_twcc_send_gpu import _tcc_values
+    o = load_oracle()
+    tr = workload.Trace(2, duration_s=3.0, batch_s=1.0, rooms=2, seed=8, twcc=1)
+    h = o.create(500)
+    try:
+        workload.load_topology(o.api, h, tr)
+        tmap = srtp_lib.bind_transports(pkg, o.api, h, tr, seed=6)
+        nxt = {}
+        seen = 0
+        for b in range(tr.nbatches):
+            workload.queue_events(o.api, h, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            o.run(h, pk, n, ar, alen)
+            rec, arr = pkg.drain_arrays(o.api, h)
+            for d, v in _tcc_values(tr, rec, arr):
+                key = ("t", tmap[d][0]) if d in tmap else ("d", d)
+                assert v == nxt.get(key, 0) & 0xFFFF, (b, d, v, nxt.get(key))
+                nxt[key] = nxt.get(key, 0) + 1
+                seen += 1
+            for r in rec:  # an abs-send-time subscriber's packet keeps its 20-B header (no element added)
+                p = tr.downtracks[int(r["dt"])]
+                if p.ext_abs_send_time and not p.ext_dd:
+                    w = arr[int(r["out_off"]):int(r["out_off"]) + 16]
+                    assert (int(w[14]) << 8 | int(w[15])) == 1, "one-word extension block"
+        assert seen > 1000
+        assert any(k[0] == "d" for k in nxt) and any(k[0] == "t" for k in nxt)
+    finally:
+        o.destroy(h)
+        tr.close()
