@@ -3771,18 +3771,6 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
   return LKF_OK;
 }
 
-// Not part of include/lkfwd.h: counters of a diagnostic build (-DLKF_DIAG=1).
-// out[0..15]: per-wave cycle/event counters; out[16..31]: serial-step triggers.
-int lkf_debug_counters(lkf_engine *e, uint64_t out[32], int reset) {
-  if (!e || !out) return LKF_EINVAL;
-  int rc = drain_streams(e);
-  if (rc) return rc;
-  unsigned long long v[32];
-  hipError_t r = read_diag(v, reset);
-  for (int i = 0; i < 32; i++) out[i] = v[i];
-  return r == hipSuccess ? LKF_OK : LKF_ENODEV;
-}
-
 // Not part of include/lkfwd.h: the bounds-check record of a checked build
 // (-DLKF_CHECKED=1, liblkfwd_checked.so): {violations, first site, index,
 // capacity}; LKF_ENODEV from a product build.
@@ -3832,15 +3820,6 @@ int lkf_debug_dd_state(lkf_engine *e, int32_t dt, uint64_t out[16]) {
   out[14] = (d.flags & DS_FN_INIT) ? d.fnLast : ~0ull;
   out[15] = uint64_t(uint8_t(h.curS + 128)) | (uint64_t(uint8_t(h.curT + 128)) << 8);
   return LKF_OK;
-}
-
-// Not part of include/lkfwd.h: per-wave stamps of the last k_decide_dt
-// (-DLKF_WTIME=1 builds): 8 words per wave slot.
-int lkf_debug_wtime(lkf_engine *e, uint32_t *out, uint32_t nwaves) {
-  if (!e || !out) return LKF_EINVAL;
-  int rc = drain_streams(e);
-  if (rc) return rc;
-  return read_wtime(out, nwaves) == hipSuccess ? LKF_OK : LKF_ENODEV;
 }
 
 int lkf_downtrack_summaries(lkf_engine *e, lkf_dt_summary *out, uint32_t cap, uint32_t *n_out) {

@@ -26,58 +26,7 @@
 #include "fwd_state.h"
 #include "kernels.h"
 
-#ifndef LKF_ABLATE
-#define LKF_ABLATE 0
-#endif
-
 namespace lkf {
-
-#ifndef LKF_DIAG
-#define LKF_DIAG 0  // diagnostic build: per-wave counters into g_diag (lkf_debug_counters)
-#endif
-#ifndef LKF_SVC_AB
-#define LKF_SVC_AB 0  // A/B builds of svc_run (bisection only)
-#endif
-#ifndef LKF_SVC_DIAG
-#define LKF_SVC_DIAG 0  // diagnostic build: svc_run counters into g_diag (lkf_debug_counters)
-#endif
-#ifndef LKF_WTIME
-#define LKF_WTIME 0  // diagnostic build: per-wave start/end realtime stamps (lkf_debug_wtime)
-#endif
-#if LKF_WTIME
-constexpr uint32_t kWTimeWaves = 1u << 17;
-__device__ uint32_t g_wtime[kWTimeWaves * 16];  // start, end (100 MHz ticks), packets, serial steps | chunks << 16,
-                                               // cycles: prologue, serial steps, drains after them, total
-#endif
-#if LKF_DIAG || LKF_SVC_DIAG
-__device__ unsigned long long g_diag[32];  // [16..31]: serial-step triggers
-#endif
-#ifdef LKF_SVC_WATCH  // diagnostic: svc_run / full-step log of one DownTrack (read through lkf_debug_wtime)
-__device__ uint32_t g_svclog[4 * 4096];  // [0]: entries; entry i at 4 + 4i: kind, packet, x packet, why
-__device__ __forceinline__ void svclog(uint32_t d, uint32_t kind, uint32_t a, uint32_t b, uint32_t c) {
-  if (d != LKF_SVC_WATCH || (threadIdx.x & 63) != 0) return;
-  const uint32_t i = atomicAdd(&g_svclog[0], 1u);
-  if (4 + 4 * i + 3 < 4 * 4096) {
-    g_svclog[4 + 4 * i] = kind;
-    g_svclog[5 + 4 * i] = a;
-    g_svclog[6 + 4 * i] = b;
-    g_svclog[7 + 4 * i] = c;
-  }
-}
-#endif
-#if LKF_DIAG
-struct DiagTimer {  // adds elapsed cycles of a scope to g_diag[slot] (lane 0)
-  int slot;
-  uint64_t t0;
-  __device__ explicit DiagTimer(int s) : slot(s), t0(clock64()) {}
-  __device__ ~DiagTimer() {
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag[slot], (unsigned long long)(clock64() - t0));
-  }
-};
-#define DIAG_SCOPE(slot) DiagTimer diag_timer_(slot)
-#else
-#define DIAG_SCOPE(slot)
-#endif
 
 using u8 = uint8_t;
 using u16 = uint16_t;
@@ -88,6 +37,10 @@ using i64 = int64_t;
 
 constexpr u64 HALF64 = 1ull << 63;
 constexpr i32 INVALID = -1;
+// Out-of-order packets decided inside a decide run instead of the serial step
+// (round 2: parity held, but the extra live state spilled and the run bodies
+// slowed down; off — the code paths below compile away)
+constexpr bool kOooRun = false;
 
 // ---------------------------------------------------------------------------
 // Checked builds (-DLKF_CHECKED=1, liblkfwd_checked.so): every global access
@@ -246,15 +199,8 @@ __device__ __forceinline__ void wave_lds_sync() { __syncthreads(); }
 // ---------------------------------------------------------------------------
 // Lane context: hot state in registers + cold-state pointers.
 // ---------------------------------------------------------------------------
-#ifndef LKF_STATE_LDS
-#define LKF_STATE_LDS 1  // DownTrack hot state in LDS (one copy per wave) instead of registers
-#endif
 struct Lane {
-#if LKF_STATE_LDS
   DTHot &h;  // the wave's DownTrack state, staged in LDS (no SGPR pressure / spill traffic)
-#else
-  DTHot h;
-#endif
   RangeEntry *rm;  // the closed-range ring, staged in LDS for the batch
   bool rmDirty;    // a closed range was written (write the ring back)
   bool vcDirty;    // a VP8 munger map changed (write the maps back)
@@ -281,9 +227,6 @@ struct Lane {
   const DDPkt *ddPkts;
   u8 *ddBuf;
   u32 *err;
-#ifdef LKF_SVC_WATCH
-  u32 watchDt;
-#endif
 };
 
 __device__ __forceinline__ bool hasf(const Lane &L, u32 f) { return (L.h.flags & f) != 0; }
@@ -1647,20 +1590,7 @@ struct LaneOut {
 template <bool DDK>
 __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneOut &o) {
   o.nTuples++;
-#if LKF_ABLATE == 3  // diagnostic: empty per-packet body (staging loop only)
-  o.relOff += u32(p.esn) & 1;
-  return;
-#endif
   Fwd f;
-#if LKF_ABLATE == 2  // diagnostic: translate replaced by a trivial decision
-  f.osn = p.esn;
-  f.ots = p.ets;
-  f.switching = f.resuming = false;
-  f.marker = false;
-  f.cbLen = 0;
-  f.cb = 0;
-  int dr = (p.layer == L.h.tgtS || !hasf(L, F_VIDEO)) ? -1 : LKF_DROP_NOT_SELECTED;
-#else
   // Fast classification (pre-state + packet only); anything not covered
   // takes the full restatement fw_translate.  Each fast case is exactly the
   // path forwarder.go would take for it:
@@ -1749,7 +1679,6 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
       dr = -1;
     }
   }
-#endif
   if (dr >= 0) {
 #pragma unroll
     for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] += (dr == i) ? 1u : 0u;
@@ -1801,14 +1730,12 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
       t.ddOff = u32(off);
     }
   }
-#if LKF_ABLATE != 1  // diagnostic builds only (never shipped): 1 = no tuple/sequencer writes
 #if LKF_CHECKED
   CHK(o.tupBase + o.nFwd < o.tupCap, CK_DEC_TUPLE, o.tupBase + o.nFwd, o.tupCap);
 #endif
   if (lane_id() == 0) store_rec(o.outT + o.nFwd, t);  // wave-uniform record: one lane stores it
   // sequencer.push (downtrack.go:724-735)
   seq_push<DDK>(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
-#endif
   // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
   if (!hasf(L, F_STATS_INIT) && payLen > 0) {
     setf(L, F_STATS_INIT, true);
@@ -1841,30 +1768,8 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 // control op) goes through decide_step — the full restatement — executed by
 // the whole wave on the broadcast packet, and the run restarts after it.
 // ---------------------------------------------------------------------------
-#ifndef LKF_FORCE_SERIAL
-#define LKF_FORCE_SERIAL 0  // diagnostic: every packet through decide_step
-#endif
-#if LKF_DIAG
-#define DIAG(i, v) dg[i] += (v)
-#define DIAG_MARK(i)            \
-  do {                          \
-    const u64 tm_ = clock64();  \
-    dg[i] += tm_ - tmark;       \
-    tmark = tm_;                \
-  } while (0)
-#else
-#define DIAG(i, v)
-#define DIAG_MARK(i)
-#endif
 
-#ifndef LKF_DECIDE_WAVES
-#define LKF_DECIDE_WAVES 5  // amdgpu_waves_per_eu floor for k_decide_dt (5: 96 VGPRs, 32 B scratch; +3-4%)
-#endif
-#if LKF_DECIDE_WAVES
-#define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(LKF_DECIDE_WAVES, 8)))
-#else
-#define DECIDE_ATTR
-#endif
+#define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
 
 // Consume the chunk's descriptor registers here, once.  gfx9 counts stores in
 // vmcnt too: a first use sunk into the run loop would wait there for every
@@ -1876,13 +1781,8 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 // pending at the run-loop head and insert a vmcnt(0) there — which, with
 // stores counted in vmcnt, would stall every run on the previous run's
 // tuple/sequencer stores.
-#ifndef LKF_VM_DRAIN
-#define LKF_VM_DRAIN 1
-#endif
 __device__ __forceinline__ void vm_drain() {
-#if LKF_VM_DRAIN
   __builtin_amdgcn_s_waitcnt(0x0F70);
-#endif
 }
 
 __device__ __forceinline__ void pin_loaded(const uint4 &a, const uint4 &b, const uint4 &c, const uint4 &d) {
@@ -1890,18 +1790,9 @@ __device__ __forceinline__ void pin_loaded(const uint4 &a, const uint4 &b, const
                "v"(c.y), "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
 }
 
-#ifndef LKF_GAP_RUN
-#define LKF_GAP_RUN 1  // loss gaps anywhere in a run (0: only as the run's first candidate; A/B)
-#endif
-#ifndef LKF_OOO_RUN
-#define LKF_OOO_RUN 0  // 1: out-of-order packets decided in the run (A/B: slower, register pressure)
-#endif
-#ifndef LKF_LAYER_SKIP
-#define LKF_LAYER_SKIP 1  // 0: every chunk is the next 64 packets of the track (A/B)
-#endif
 __device__ __forceinline__ bool steady_state(const Lane &L) {
   const u32 fl = L.h.flags;
-  return LKF_LAYER_SKIP && (fl & F_VIDEO) && (fl & F_SIMULCAST) && !(fl & (F_MUTED | F_PUBMUTED)) &&
+  return (fl & F_VIDEO) && (fl & F_SIMULCAST) && !(fl & (F_MUTED | F_PUBMUTED)) &&
          L.h.tgtS != INVALID && L.h.tgtT != INVALID && L.h.curS == L.h.tgtS && L.h.curS <= L.h.maxS &&
          L.h.curS >= 0 && L.h.curS < 3;
 }
@@ -1973,15 +1864,7 @@ constexpr int kSvcDDBytes = 48;  // per-lane marshal buffer (a descriptor withou
 constexpr int kSvcFrames = 72;   // frame decisions of one run: frame cLast + up to 64 later frames
 enum : u32 { SK_BAD = 0, SK_FWD = 1, SK_MDROP = 2, SK_NDROP = 3 };  // lane kinds of an SVC run
 
-#ifndef LKF_SVC_DIAG
-#define LKF_SVC_DIAG 0
-#endif
-#if LKF_SVC_DIAG
-#define SVC_WHY(c) \
-  if (!good && why == 0) why = (c)
-#else
 #define SVC_WHY(c)
-#endif
 
 template <bool DDK>
 __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 pi, u32 n, u32 pos, u32 nextAt,
@@ -1992,18 +1875,12 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   const bool inWin = valid && lane >= pos && pi < nextAt;
   const u64 winM = __ballot(inWin);
   const bool dd = DDK && (fl & F_DD);
-#if LKF_SVC_DIAG
-  if (lane == 0) atomicAdd(&g_diag[0], 1ull);
-#endif
   // ---- muted / paused: every packet of the window drops with no state change
   // (forwarder.go:1440, :1687)
   {
     const int ns = (fl & (F_MUTED | F_PUBMUTED)) ? LKF_DROP_MUTED
                    : (L.h.tgtS == INVALID || L.h.tgtT == INVALID) ? LKF_DROP_PAUSED
                                                                   : -1;
-#if LKF_SVC_AB == 4
-    if (ns >= 0) return pos;
-#endif
     if (ns >= 0) {
       const u32 k = u32(__popcll(winM));
       o.nTuples += k;
@@ -2014,9 +1891,6 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   const bool curValid = L.h.curS != INVALID && L.h.curT != INVALID;
   const bool started = fl & F_STARTED;
   const bool relevantDrop = curValid && started;  // a not-selected packet advances the munger
-#if LKF_SVC_AB == 2
-  if (!relevantDrop) return pos;
-#endif
   // ---- dependency-descriptor selector: the uniform part
   bool uni = true;
   const DDStruct *s = nullptr;
@@ -2039,18 +1913,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     }
     swAll = hiPos >= 0 && (i32(s->dtS[hiPos]) != L.h.curS || i32(s->dtT[hiPos]) != L.h.curT);
   }
-#if LKF_SVC_DIAG
-  if (!uni) {
-    if (lane == 0) atomicAdd(&g_diag[4], 1ull);
-#ifdef LKF_SVC_WATCH
-    svclog(L.watchDt, 2, rl32(pi, pos), 0, 0);
-#endif
-    return pos;
-  }
-  u32 why = 0;
-#else
   if (!uni) return pos;
-#endif
   bool good = inWin;
   u32 kind = SK_BAD;
   int nsr = LKF_DROP_NOT_SELECTED;  // reason of an SK_NDROP lane
@@ -2107,9 +1970,6 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     const bool hasDD = inWin && (p.flags & LKF_PKT_DD) && L.ddPkts;
     if (hasDD) dp = L.ddPkts[pi];
     const bool ddLane = hasDD && (dp.flags & DP_VALID);  // (no descriptor: not selected, no DD state change)
-#if LKF_SVC_AB == 3
-    good = good && ddLane;
-#endif
     const u64 cl0 = d.cLast;
     const u64 efn = dp.extFN;
     const u64 ddM = __ballot(ddLane);
@@ -2118,9 +1978,6 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     const u64 pEfn = pdl >= 0 && u32(pdl) >= pos ? pEfnL : cl0;  // the previous descriptor's frame
     const u64 fi = efn - cl0;  // the frame's index in the run (0: frame cLast)
     if (ddLane) good = good && efn >= pEfn && fi < u64(kSvcFrames) - 8;  // frames in order (a reorder: full step)
-#if LKF_SVC_AB == 1
-    if (ddLane) good = good && efn <= pEfn + 1;
-#endif
     SVC_WHY(3);
     const bool newF = ddLane && efn != pEfn;
     const u32 dti = hiPos >= 0 ? dd::dti_at(dp.dtis, int(hiTarget)) : 0u;
@@ -2250,20 +2107,6 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   SVC_WHY(13);
   const u64 stopM = __ballot(inWin ? !good : (valid && lane >= pos));
   const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
-#if defined(LKF_SVC_WATCH) && LKF_SVC_DIAG
-  svclog(L.watchDt, 1, rl32(pi, pos), x < n ? rl32(pi, x) : 0xffffffffu, x < n ? rl32(why, x) : 0u);
-#endif
-#if LKF_SVC_DIAG
-  if (lane == 0) {
-    atomicAdd(&g_diag[1], x > pos ? 1ull : 0ull);
-    atomicAdd(&g_diag[2], (unsigned long long)(x - pos));
-  }
-  {
-    const u32 wx = x < n ? rl32(why, x) : 0u;
-    const bool winX = x < n && rl32(u32(inWin), x);
-    if (lane == 0) atomicAdd(&g_diag[winX ? (16 + wx) : 13], 1ull);
-  }
-#endif
   if (x <= pos) return pos;
   const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
   const bool inRun = (runM >> lane) & 1;
@@ -2280,9 +2123,6 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     const u64 cur = pp >= 0 ? ppE : d.cLast;  // cLast when this lane adds
     const bool put = inRun && ddPut && ddEfn > d.cBase;
     const bool grow = put && ddEfn > cur;  // addEntity's new-entity path
-#if LKF_SVC_AB == 1
-    if (grow && ddEfn != cur + 1 && lane == 0) atomicOr(L.err, 16u);
-#endif
     const u64 g1M = __ballot(grow && ddEfn == cur + 1);
     const u64 gNM = __ballot(grow && ddEfn > cur + 1);
     // one-frame steps: at most one missing mark each, in parallel
@@ -2535,9 +2375,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __shared__ u8 sSvcFD[kSvcFrames];                    // svc_run: decisions of the run's frames
   DDState *const sDD = reinterpret_cast<DDState *>(sDDRaw);
   u8 *const sDDBuf = sDDRaw + (DDK ? sizeof(DDState) : 0);
-#if LKF_DIAG
-  const u64 tEntry = clock64();
-#endif
   // A wave serves perWave schedule slots of its XCD's list (slot index = q * 8
   // + XCD, q consecutive), one DownTrack after the other.  Short ticks have a
   // few packets per DownTrack, and one workgroup per DownTrack would leave the
@@ -2590,16 +2427,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const u32 track = __builtin_amdgcn_readfirstlane(sa.z);
   u32 ev = __builtin_amdgcn_readfirstlane(sa.w);
   const u32 evEnd = __builtin_amdgcn_readfirstlane(sb.x);
-#if LKF_WTIME
-  const u64 wt0 = __builtin_amdgcn_s_memrealtime();
-  const u64 wc0 = __builtin_amdgcn_s_memtime();
-  u32 wtSerial = 0, wtChunks = 0;
-  u64 wcStep = 0, wcDrain = 0, wcPro = 0;
-  u32 wtWhy[4] = {}, wtRuns = 0, wtRunEnd[5] = {};
-#endif
-#if LKF_DIAG
-  const u64 tP1 = clock64() + u64(__builtin_amdgcn_readfirstlane(d) & 0);  // after round 1
-#endif
   CHK(d < A.maxDts, CK_DEC_DT, d, A.maxDts);
   CHK(track < A.maxTracks, CK_DEC_TRACK, track, A.maxTracks);
   CHK(evEnd <= A.nev, CK_DEC_EVENT, evEnd, A.nev);
@@ -2613,18 +2440,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   i32 sentAcc = 0;  // per lane: run-path forwarded packets' incoming minus outgoing header bytes
   o.relOff = 0;
   for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
-#if LKF_STATE_LDS
   __shared__ __attribute__((aligned(16))) DTHot sHot;
   Lane L{sHot};
   reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
   __syncthreads();
-#if LKF_DIAG
-  const u64 tP2 = clock64() + u64(sHot.flags & 0);  // hot state in LDS
-#endif
-#else
-  Lane L;
-  L.h = A.hot[d];
-#endif
   RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
   L.rm = sRm;
   L.rmDirty = false;
@@ -2649,9 +2468,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     const u32 idx = (L.h.rmHead + i) % kRangeCap;
     sRm[idx] = rmG[idx];
   }
-#if LKF_DIAG
-  const u64 tP3 = clock64() + u64(u32(sRm[0].start) & 0 & sMissKey[lane & 63] & sDrop[0]);  // maps + ranges issued
-#endif
   if (slot0 + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
     if (lane == 0) atomicOr(A.err, 8u);
     pe = pb;
@@ -2672,9 +2488,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.extDD = dt.extDD;
   L.extTcc = dt.extTcc;
   L.err = A.err;
-#ifdef LKF_SVC_WATCH
-  L.watchDt = d;
-#endif
   L.ddPkts = A.ddPkts;
   L.ddRing = nullptr;
   L.ddS = reinterpret_cast<const DDStruct *>(sDDSRaw);
@@ -2711,25 +2524,11 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   o.outT = A.tuples + slot0;
   // SVC DownTracks (one SSRC, every packet relevant to the selector): svc_run
   // (the host schedules them in k_decide_dt<true>)
-  const bool svcDT = LKF_SVC_AB != 5 && DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
+  const bool svcDT = 0 != 5 && DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
                      ((L.h.flags & F_VP9) || ((L.h.flags & F_DD) && ddDT));
   u32 nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
-#if LKF_DIAG
-  u64 dg[16] = {};
-  u32 dg2[16] = {};
-  u64 tk0 = clock64();
-  dg2[12] = u32(tP1 - tEntry);
-  dg2[13] = u32(tP2 - tP1);
-  dg2[14] = u32(tP3 - tP2);
-  dg[7] = tk0 - tEntry;
-  dg[0] = 1;
-  dg[15] = pe - pb;
-#endif
 
-#if LKF_WTIME
-  wcPro = __builtin_amdgcn_s_memtime() - wc0;
-#endif
   u32 kpos = pb;  // first packet of the track not yet decided
   while (kpos < pe) {
     if (nextAt <= kpos) {
@@ -2764,13 +2563,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       lim = kpos + n;
     }
     const bool valid = lane < n;
-    DIAG(1, 1);
-#if LKF_WTIME
-    wtChunks++;
-#endif
-#if LKF_DIAG
-    u64 tc0 = clock64();
-#endif
     uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
     if (valid) {
       CHK(pi < A.npkts, CK_DEC_PKT, pi, A.npkts);
@@ -2782,16 +2574,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     }
     pin_loaded(r0, r1, r2, r3);
     const PktV p = decode_pkt(r0, r1, r2, r3);
-#if LKF_DIAG
-    dg[11] += u64(__builtin_amdgcn_readfirstlane(u32(r0.x)) + 1u > 0u) * (clock64() - tc0);
-#endif
     u32 pos = 0;
     u32 own = n;  // packets of the chunk decided (steady: the rest of the range is skipped drops)
     while (pos < n) {
-#if LKF_DIAG
-      u64 tr0 = clock64();
-      u64 tmark = tr0;
-#endif
       if (nextAt <= rl32(pi, pos)) {
         while (nextAt <= rl32(pi, pos)) {
           apply_ctl(L, A.events[ev++]);
@@ -2801,36 +2586,16 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       }
       u32 x;
       bool gapStop = false;  // the stopping lane starts the next run (no full step)
-#if LKF_DIAG || LKF_WTIME
-      int why = 0;
-#endif
       if (DDK && svcDT) {
         // SVC DownTrack: a run, then the stopping packet's full step (its
         // descriptor reloaded wave-uniform, so the chunk's raw registers are
         // dead on this path)
-#if LKF_WTIME
-        const u64 wr0 = __builtin_amdgcn_s_memtime();
-#endif
         x = svc_run<DDK>(L, o, p, pi, n, pos, nextAt, valid, sentAcc, sSvcScr, sSvcFD);
-#if LKF_WTIME
-        wcDrain += __builtin_amdgcn_s_memtime() - wr0;  // (svc DownTracks: cycles in svc_run)
-        wtRuns += x > pos ? 1 : 0;
-#endif
         pos = x;
         if (x < n && rl32(pi, x) < nextAt) {
           const u32 px = rl32(pi, x);
-#if LKF_WTIME
-          wtSerial++;
-          const u64 ws0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef LKF_SVC_WATCH
-          svclog(d, 3, px, L.dd ? u32(L.dd->cLast) : 0u, L.dd ? u32(L.dd->chBroken) | (u32(L.dd->chActive) << 8) : 0u);
-#endif
           decide_step<DDK>(L, load_pkt(pkts + px), px, o);
           vm_drain();
-#if LKF_WTIME
-          wcStep += __builtin_amdgcn_s_memtime() - ws0;
-#endif
           pos = x + 1;
         }
         continue;
@@ -2843,9 +2608,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       const bool kf = p.flags & LKF_PKT_KEYFRAME;
       const bool pktMarker = p.hdr1 & 0x80;
       int cls;  // >= 0: drop with no state change; -1: current-layer candidate; -2: serial
-#if LKF_DIAG || LKF_WTIME
-      int whyKf = 0;
-#endif
       if (fl & (F_MUTED | F_PUBMUTED)) {
         cls = LKF_DROP_MUTED;
       } else if (!video) {
@@ -2869,20 +2631,14 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           cls = -1;
         else
           cls = -2;
-#if LKF_DIAG || LKF_WTIME
-        if (willSwitch) whyKf = 1;
-#endif
       }
-#if LKF_FORCE_SERIAL
-      cls = -2;
-#endif
       const bool cand = inWin && cls == -1;
       // An out-of-order packet — older than the highest SN at the run start
       // (UpdateAndGetSnTs diff < 0, rtpmunger.go:219-236) — is decided in the
       // run: its translation reads the RangeMap and the VP8 missing-picture map
       // and changes no state but the sequencer slot it fills.  The in-order
       // recurrences (previous candidate, previous forward) skip it.
-      const bool oooL = LKF_OOO_RUN && cand && i64(p.esn - L.h.extHighestIncomingSN) < 0 && p.plen != 0 && p.ssrc == L.h.lastSSRC;
+      const bool oooL = kOooRun && cand && i64(p.esn - L.h.extHighestIncomingSN) < 0 && p.plen != 0 && p.ssrc == L.h.lastSSRC;
       const bool candIn = cand && !oooL;
       const u64 candM = __ballot(candIn);
       const int pc = prev_in(candM, lt);
@@ -2894,10 +2650,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       // pictures vp8.go:218-255, skipped sequencer slots sequencer.go:179-189)
       // are applied before the run, from the state at the run start.
       const u64 dEsn = p.esn - prevEsn;
-      const bool gapLane = candIn && (LKF_GAP_RUN || pc < 0) && dEsn > 1 && dEsn < u64(L.seqSize) - 64 &&
+      const bool gapLane = candIn && dEsn > 1 && dEsn < u64(L.seqSize) - 64 &&
                            p.plen != 0 && p.ssrc == L.h.lastSSRC;
       bool ok = candIn && (dEsn == 1 || gapLane) && p.plen != 0 && p.ssrc == L.h.lastSSRC;
-      bool okO = LKF_OOO_RUN && oooL;  // out-of-order lane decided in the run (refined below)
+      bool okO = kOooRun && oooL;  // out-of-order lane decided in the run (refined below)
       // a gap behind other candidates ends this run and starts the next one
       const bool gapLater = candIn && pc >= 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
                             p.ssrc == L.h.lastSSRC;
@@ -2911,9 +2667,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       const i32 prevExt = pc >= 0 ? pcExt : L.h.wrMaxPictureId;
       const bool prevM = pc >= 0 ? pcM : ((fl & F_WR_MAX_MBIT) != 0);
       bool dropT = false;
-#if LKF_DIAG || LKF_WTIME
-      int whyVid = 0;
-#endif
       u64 tswM = 0;  // candidate lanes at a temporal switch point (the first ends the run)
       bool overT = false;
       if (video) {
@@ -2947,9 +2700,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         // must forward — a filtered one would roll the selector back (serial).
         if (tsw && cT < gT) dropT = false;
         const bool tswOk = tsw && !gapLane && !dropT;
-#if LKF_DIAG || LKF_WTIME
-        whyVid = (wrapBack || wraps) ? 1 : ((tsw && !tswOk) ? 2 : ((dropT && L.h.snOffset != L.h.rmOpenValue) ? 3 : 0));
-#endif
         ok = ok && !wrapBack && !wraps && (!tsw || tswOk) && (!dropT || L.h.snOffset == L.h.rmOpenValue);
         tswM = __ballot(inWin && ok && tsw);
       }
@@ -2989,47 +2739,13 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       // serial step.  Exclusions the run adds lie above the run-start highest
       // SN, so they do not move an older key's range unless the ring prunes
       // the range it sits in.
-#if LKF_OOO_RUN
-      if (u64 oM = __ballot(okO)) {
-        const u64 mgLast = pf >= 0 ? pfOsn : L.h.extLastSN;
-        i32 po = 0;
-        do {
-          const u32 b = u32(__ffsll((long long)oM) - 1);
-          const u64 key = rl64(p.esn, b);
-          const int prunes = int(L.h.rmCount) + __popcll(tdM & ((1ull << b) - 1)) - kRangeCap;
-          bool good = !(prunes > 0 && key < L.h.rmOpenStart &&
-                        (prunes >= int(L.h.rmCount) || key < rm_at(L, prunes).start));
-          u64 off = 0;
-          if (good) good = rm_get(L, key, off) && (key - off) < rl64(mgLast, b);
-          i32 pb = 0;
-          if (good && video) {
-            const int mi = miss_find(L, i32(rl32(u32(ext), b)));
-            good = mi >= 0;
-            if (good) pb = L.missVal[mi];
-          }
-          if (lane == b) {
-            okO = good;
-            osn = key - off;
-            po = pb;
-          }
-          oM &= oM - 1;
-        } while (oM);
-        if (video && okO) {
-          const u16 opid = u16((ext - po) & 0x7fff);
-          const bool mM = opid > 127;
-          const int hs = int(p.vhs) + (mM == M ? 0 : (mM ? 1 : -1));
-          cbLen = vp8_marshal(p.vfirst, I, mM, opid, p.vbits & LKF_VP8_L, mtl0, T, p.tid, p.vbits & LKF_VP8_Y,
-                              p.vbits & LKF_VP8_K, mkey, hs, cb);
-        }
-      }
-#endif
       bool fwd = fwdIn || okO;
       // sequencer highest TS = max over pushes; runs keep TS non-decreasing so it is the last one
       const bool tsMono = ots >= hiTS;
       // the first push of a run may skip slots (a gap lane: osn - highest < size - 64)
       // the sequencer slots of a run lie within size - 64 of its highest at the run start
       const bool seqOk = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && cbLen >= 0 && tsMono &&
-                         (osn == prevOsn + 1 || (gapLane && (LKF_GAP_RUN || pf < 0) && osn - prevOsn > 1 &&
+                         (osn == prevOsn + 1 || (gapLane && osn - prevOsn > 1 &&
                                                  osn - prevOsn < u64(L.seqSize) - 64)) &&
                          osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
       // an out-of-order push fills a past slot and moves neither highest SN nor TS
@@ -3037,44 +2753,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
                           i64(osn - prevOsn) < 0;
       const bool bad =
           inWin && ((cls == -2) || (cls == -1 && !ok && !okO) || (fwdIn && !seqOk) || (okO && !seqOkO));
-#if LKF_DIAG || LKF_WTIME
-      // serial-step trigger of this lane (read at the stopping lane below)
-      why = 0;
-      if (cls == -2)
-        why = whyKf ? 16 : (!(fl & F_SIMULCAST) ? 17 : 18);
-      else if (cls == -1 && !ok && !okO) {
-        if (oooL) why = 21;
-        else if (p.ssrc != L.h.lastSSRC) why = 19;
-        else if (p.plen == 0) why = 20;
-        else if (i64(p.esn - prevEsn) <= 0) why = 21;
-        else if (dEsn > 1 && !gapLane) why = 22;
-        else if (whyVid) why = 22 + whyVid;
-        else why = 26;
-      } else if ((fwdIn && !seqOk) || (okO && !seqOkO))
-        why = 27;
-#endif
       const u64 stopM = __ballot(bad || (valid && lane >= pos && !inWin));
       x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
       if (tswM & ~((1ull << pos) - 1)) x = min(x, u32(__ffsll((long long)(tswM & ~((1ull << pos) - 1))) - 1) + 1u);
       // ---- decide lanes [pos, x) together
-      DIAG(2, x > pos ? 1 : 0);
-#if LKF_WTIME
-      wtRuns += x > pos ? 1 : 0;
-      {  // what ends this run: chunk end, control op, temporal switch, later gap, full step
-        int re;
-        if (x >= n) re = 0;
-        else if (rl32(pi, x) >= nextAt) re = 1;
-        else if (x > pos && ((tswM >> (x - 1)) & 1)) re = 2;
-        else if (rl32(u32(gapLater), x)) re = 3;
-        else re = 4;
-        wtRunEnd[re]++;
-      }
-#endif
-#if LKF_DIAG
-      const u64 tb0 = clock64();
-      dg[5] += tb0 - tr0;
-      tmark = tb0;
-#endif
       if (x > pos) {
         const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
         const bool inRun = (runM >> lane) & 1;
@@ -3157,9 +2839,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #if LKF_CHECKED
           CHK(slot0 + o.nFwd + j < A.tupleCap, CK_DEC_TUPLE, slot0 + o.nFwd + j, A.tupleCap);
 #endif
-#if LKF_ABLATE != 1
           store_rec(o.outT + o.nFwd + j, t);
-#endif
           // sequencer.push (sequencer.go:123-209): in order, the next slot; out of
           // order, the slot delta behind the highest (skipped when older than
           // the window or the sequencer's start)
@@ -3185,9 +2865,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #pragma unroll
           for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
           CHK(slot < L.seqSize, CK_DEC_SEQ, slot, L.seqSize);
-#if LKF_ABLATE != 1
           if (store) store_rec(L.seq + slot, m);
-#endif
         }
         const u32 sumLen = wave_sum_u32(outLen);
         sentAcc += fwd ? i32(p.poff) - hdrLen : 0;  // (reduced once per DownTrack)
@@ -3283,54 +2961,15 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       gapStop = x < n && rl32(u32(gapLater), x) != 0;
       }  // (simulcast / audio runs)
       pos = x;
-#if LKF_DIAG
-      u64 ts0 = clock64();
-      dg[12] += ts0 - tr0;
-      dg[6] += ts0 - tb0;
-#endif
       if (x < n && rl32(pi, x) < nextAt && !gapStop) {
-        DIAG(3, 1);
         // the packet at lane x needs the full restatement
         const uint4 a0 = make_uint4(rl32(r0.x, x), rl32(r0.y, x), rl32(r0.z, x), rl32(r0.w, x));
         const uint4 a1 = make_uint4(rl32(r1.x, x), rl32(r1.y, x), rl32(r1.z, x), rl32(r1.w, x));
         const uint4 a2 = make_uint4(rl32(r2.x, x), rl32(r2.y, x), rl32(r2.z, x), rl32(r2.w, x));
         const uint4 a3 = make_uint4(rl32(r3.x, x), rl32(r3.y, x), rl32(r3.z, x), rl32(r3.w, x));
         const u32 px = rl32(pi, x);
-#if LKF_WTIME
-        wtSerial++;
-        {
-          const int wx = int(rl32(u32(why), x));
-          if (wx == 21) wtWhy[0]++;
-          else if (wx == 16) wtWhy[1]++;
-          else if (wx == 19 || wx == 20) wtWhy[2]++;
-          else wtWhy[3]++;
-        }
-#endif
-#if LKF_DIAG
-        {
-          const int wx = int(rl32(u32(why), x));
-          if (wx) dg2[wx - 16] += 1;
-          dg2[15] += 1;
-        }
-#endif
-#if LKF_WTIME
-        const u64 ws0 = __builtin_amdgcn_s_memtime();
-#endif
         decide_step<DDK>(L, decode_pkt(a0, a1, a2, a3), px, o);
-#if LKF_WTIME
-        const u64 ws1 = __builtin_amdgcn_s_memtime();
-        wcStep += ws1 - ws0;
-#endif
-#if LKF_DIAG
-        const u64 tdr0 = clock64();
-#endif
         vm_drain();
-#if LKF_WTIME
-        wcDrain += __builtin_amdgcn_s_memtime() - ws1;
-#endif
-#if LKF_DIAG
-        dg[4] += clock64() - tdr0;  // (diag slot 4: the drain after the full step)
-#endif
         pos = x + 1;
         if (steady && !steady_state(L)) {  // left the steady state: the chunk ends after this packet
           own = x + 1;
@@ -3338,9 +2977,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           break;
         }
       }
-#if LKF_DIAG
-      dg[13] += clock64() - ts0;
-#endif
     }
     if (steady) {  // the other layers' packets in [kpos, lim): NOT_SELECTED drops
       const u32 skipped = (lim - kpos) - own;
@@ -3350,39 +2986,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     kpos = lim;
   }
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
-#if LKF_WTIME
-  if (lane == 0 && w < kWTimeWaves) {
-    const u64 wt1 = __builtin_amdgcn_s_memrealtime();
-    u32 *g = g_wtime + w * 16;
-    g[0] = u32(wt0);
-    g[1] = u32(wt1);
-    g[2] = pe - pb;
-    g[3] = wtSerial | (wtChunks << 16);
-    g[4] = u32(wcPro);
-    g[5] = u32(wcStep);
-    g[6] = u32(wcDrain);
-    g[7] = u32(__builtin_amdgcn_s_memtime() - wc0);
-    g[8] = wtRuns;
-    for (int i = 0; i < 4; i++) g[9 + i] = wtWhy[i];
-    g[13] = u32(L.h.curS) | (u32(L.h.tgtS) << 8) | (u32(L.h.curT) << 16) | (u32(L.h.tgtT) << 24);
-    g[14] = wtRunEnd[0] | (wtRunEnd[1] << 8) | (wtRunEnd[2] << 16) | (wtRunEnd[3] << 24);
-    g[15] = wtRunEnd[4];
-  }
-#endif
-#if LKF_DIAG
-  dg[14] += clock64() - tk0;
-  if (lane == 0)
-    for (int i = 0; i < 16; i++) {
-      atomicAdd(&g_diag[i], (unsigned long long)dg[i]);
-      atomicAdd(&g_diag[16 + i], (unsigned long long)dg2[i]);
-    }
-#endif
-#if LKF_STATE_LDS
   __syncthreads();
   reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
-#else
-  if (lane == 0) A.hot[d] = L.h;
-#endif
   if (L.rmDirty) {
     wave_lds_sync();
     for (u32 i = lane; i < L.h.rmCount; i += 64) {
@@ -3454,14 +3059,8 @@ constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 desc
 // (two-byte extension profile) = 343
 constexpr int PRE_MAX_DD = 352;
 
-#ifndef LKF_EMIT_U
-#define LKF_EMIT_U 4  // 16-B chunks per lane per copy iteration (loads in flight together)
-#endif
-constexpr int EMIT_U = LKF_EMIT_U;
+constexpr int EMIT_U = 4;
 
-#ifndef LKF_EMIT_NT
-#define LKF_EMIT_NT 1  // non-temporal output stores: keep L2 for the payload re-reads
-#endif
 
 struct EmitArgs {
   const u32 *perm;      // output position -> DownTrack (track-major order)
@@ -3507,18 +3106,11 @@ __device__ __forceinline__ uint4 shift_window(uint4 q0, uint4 q1, u32 sh) {
   v.w = align_byte(x4, x3, rb);
   return v;
 }
-#ifndef LKF_EMIT_XCD
-#define LKF_EMIT_XCD 1  // 0: plain grid-stride over the output groups (A/B)
-#endif
 __device__ __forceinline__ void store16(u8 *p, uint4 v) {
-#if LKF_EMIT_NT
   __builtin_nontemporal_store(v.x, reinterpret_cast<u32 *>(p));
   __builtin_nontemporal_store(v.y, reinterpret_cast<u32 *>(p) + 1);
   __builtin_nontemporal_store(v.z, reinterpret_cast<u32 *>(p) + 2);
   __builtin_nontemporal_store(v.w, reinterpret_cast<u32 *>(p) + 3);
-#else
-  *reinterpret_cast<uint4 *>(p) = v;
-#endif
 }
 
 template <int PRE>
@@ -3541,7 +3133,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
   // track's payloads (one per subscribing DownTrack) are adjacent, so the
   // re-reads hit that XCD's 4 MiB L2 instead of going to HBM.  (Falls back to
   // a plain grid-stride when the grid is not a multiple of 8.)
-  const u32 nx = (LKF_EMIT_XCD && gridDim.x % 8 == 0) ? 8u : 1u;
+  const u32 nx = (gridDim.x % 8 == 0) ? 8u : 1u;
   const u32 xcd = blockIdx.x % nx, slotInX = blockIdx.x / nx, perX = gridDim.x / nx;
   const u64 gpx = (ngroups + nx - 1) / nx;
   const u64 gBeg = u64(xcd) * gpx, gEnd = min(ngroups, gBeg + gpx);
@@ -4206,9 +3798,6 @@ __device__ void pad_record(const PadArgs &A, u32 r, u32 k, u32 d, u64 off, u32 l
   A.out[A.recOff[r] + k] = o;
 }
 
-#if !LKF_STATE_LDS
-#error "k_pad stages the DownTrack state in LDS (LKF_STATE_LDS=1)"
-#endif
 __global__ void __launch_bounds__(64) k_pad(PadArgs A) {
   __shared__ __attribute__((aligned(16))) DTHot sHot;
   const u32 r = blockIdx.x, lane = threadIdx.x;
@@ -4516,22 +4105,6 @@ hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *
 // ---------------------------------------------------------------------------
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 
-#if LKF_DIAG || LKF_SVC_DIAG
-hipError_t read_diag(unsigned long long out[32], int reset) {
-  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 32);
-  if (r == hipSuccess && reset) {
-    unsigned long long z[32] = {};
-    r = hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
-  }
-  return r;
-}
-#else
-hipError_t read_diag(unsigned long long out[32], int) {
-  for (int i = 0; i < 32; i++) out[i] = 0;
-  return hipErrorNotSupported;
-}
-#endif
-
 hipError_t read_check(unsigned long long out[4], int reset) {
 #if LKF_CHECKED
   hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chk), sizeof(unsigned long long) * 4);
@@ -4543,20 +4116,6 @@ hipError_t read_check(unsigned long long out[4], int reset) {
 #else
   (void)reset;
   for (int i = 0; i < 4; i++) out[i] = 0;
-  return hipErrorNotSupported;
-#endif
-}
-
-hipError_t read_wtime(u32 *out, u32 nwaves) {
-#ifdef LKF_SVC_WATCH
-  if (nwaves > 4096) nwaves = 4096;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_svclog), sizeof(u32) * 4 * nwaves);
-#elif LKF_WTIME
-  if (nwaves > kWTimeWaves) nwaves = kWTimeWaves;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtime), sizeof(u32) * 16 * nwaves);
-#else
-  (void)out;
-  (void)nwaves;
   return hipErrorNotSupported;
 #endif
 }

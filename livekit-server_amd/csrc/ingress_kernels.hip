@@ -511,22 +511,15 @@ __device__ __forceinline__ WAResult wa32_update(StreamHot &h, u32 val) {
   return r;
 }
 
-#ifndef LKF_ING_HOT_LDS
-#define LKF_ING_HOT_LDS 0
-#endif
 // RTPStatsReceiver history (cHistorySize 4096 bits, rtpstats_receiver.go:30),
-// staged in LDS for the ingest: word w of a lane's history at h[w * kHL]
-// (word-major, lane-minor)
-// (HS: the word stride — kHL for the lane-per-stream kernel, 1 for the
-// wave-per-stream kernel's single history)
-constexpr int kHL = 64;
-template <int HS = kHL>
+// staged in LDS for the ingest (HS: the word stride of the staged copy)
+template <int HS = 1>
 __device__ __forceinline__ bool hist_isset(const u64 *h, u64 v) {
   return (h[((v >> 6) & (kHistWords - 1)) * HS] >> (v & 63)) & 1;
 }
-template <int HS = kHL>
+template <int HS = 1>
 __device__ __forceinline__ void hist_set(u64 *h, u64 v) { h[((v >> 6) & (kHistWords - 1)) * HS] |= 1ull << (v & 63); }
-template <int HS = kHL>
+template <int HS = 1>
 __device__ void hist_clear_range(u64 *h, u64 lo, u64 hi) {  // inclusive; lo > hi: no-op
   if (lo > hi) return;
   if (hi - lo + 1 >= u64(kHistWords) * 64) {

@@ -81,9 +81,6 @@ hipError_t launch_twcc_stamp(hipStream_t s, const DevDT *dts, uint32_t *ctrD, ui
 // -DLKF_CHECKED=1 builds: {violations, first site, its index, its capacity}
 hipError_t read_check(unsigned long long out[4], int reset);
 
-// diagnostic builds (-DLKF_DIAG=1): k_decide_dt per-wave counters
-hipError_t read_diag(unsigned long long out[32], int reset);
-hipError_t read_wtime(uint32_t *out, uint32_t nwaves);  // LKF_WTIME builds
 hipError_t launch_batch_init(hipStream_t s, uint32_t ntracks, uint32_t ndts, uint32_t nstats, uint32_t *tBegin,
                              uint32_t *tEnd, uint32_t *tRuns, uint32_t *err, uint64_t *stats, uint32_t *fwdCnt,
                              uint64_t *fwdBytes);
