@@ -3088,23 +3088,34 @@ struct EmitArgs {
 __device__ __forceinline__ u32 align_byte(u32 hi, u32 lo, u32 sh) {
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
-__device__ __forceinline__ u32 keep_mask(int kb) {  // low kb bytes of a dword
-  return kb >= 4 ? 0xffffffffu : kb <= 0 ? 0u : ((1u << (8 * kb)) - 1);
-}
-// bytes [s, s+16) of the arena from the two aligned 16-B words covering them
-__device__ __forceinline__ uint4 shift_window(uint4 q0, uint4 q1, u32 sh) {
-  const u32 q = sh >> 2, rb = sh & 3;
-  const u32 x0 = q == 0 ? q0.x : q == 1 ? q0.y : q == 2 ? q0.z : q0.w;
-  const u32 x1 = q == 0 ? q0.y : q == 1 ? q0.z : q == 2 ? q0.w : q1.x;
-  const u32 x2 = q == 0 ? q0.z : q == 1 ? q0.w : q == 2 ? q1.x : q1.y;
-  const u32 x3 = q == 0 ? q0.w : q == 1 ? q1.x : q == 2 ? q1.y : q1.z;
-  const u32 x4 = q == 0 ? q1.x : q == 1 ? q1.y : q == 2 ? q1.z : q1.w;
-  uint4 v;
-  v.x = align_byte(x1, x0, rb);
-  v.y = align_byte(x2, x1, rb);
-  v.z = align_byte(x3, x2, rb);
-  v.w = align_byte(x4, x3, rb);
+// the low kb (0..16) bytes of a 16-B chunk kept, the rest zeroed (two 64-bit
+// shifts instead of four per-dword selects)
+__device__ __forceinline__ uint4 keep_bytes(uint4 v, int kb) {
+  const u32 bits = u32(kb < 0 ? 0 : kb > 16 ? 16 : kb) * 8;
+  const u64 lo = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+  const u64 hi = bits <= 64 ? 0ull : bits >= 128 ? ~0ull : ((1ull << (bits - 64)) - 1);
+  v.x &= u32(lo);
+  v.y &= u32(lo >> 32);
+  v.z &= u32(hi);
+  v.w &= u32(hi >> 32);
   return v;
+}
+// bytes [s, s + 16) of the arena: one dword-aligned 16-B load plus the next
+// dword (global loads need only dword alignment), funnel-shifted by s & 3
+struct __attribute__((aligned(4))) U4A {
+  u32 x, y, z, w;
+};
+__device__ __forceinline__ uint4 window_of(const U4A &a, u32 b, u32 rb) {
+  uint4 v;
+  v.x = align_byte(a.y, a.x, rb);
+  v.y = align_byte(a.z, a.y, rb);
+  v.z = align_byte(a.w, a.z, rb);
+  v.w = align_byte(b, a.w, rb);
+  return v;
+}
+__device__ __forceinline__ uint4 load_window(const u8 *arena, u64 s) {
+  const u8 *q = arena + (s & ~u64(3));
+  return window_of(*reinterpret_cast<const U4A *>(q), *reinterpret_cast<const u32 *>(q + 16), u32(s & 3));
 }
 __device__ __forceinline__ void store16(u8 *p, uint4 v) {
   __builtin_nontemporal_store(v.x, reinterpret_cast<u32 *>(p));
@@ -3282,10 +3293,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       // payload (so every 16-B chunk is either all-LDS or all-payload)
       const int R = (n + 15) & ~15;
       if (R > n) {
-        const u64 W = src & ~u64(15);
-        const uint4 q0 = *reinterpret_cast<const uint4 *>(A.arena + W);
-        const uint4 q1 = *reinterpret_cast<const uint4 *>(A.arena + W + 16);
-        const uint4 v = shift_window(q0, q1, u32(src & 15));
+        const uint4 v = load_window(A.arena, src);
         const u32 vw[4] = {v.x, v.y, v.z, v.w};
         for (int i = n; i < R; i++) {
           const int b = i - n;
@@ -3329,7 +3337,9 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       bool act[EMIT_U], lds[EMIT_U];
       u32 o[EMIT_U];
       u64 src[EMIT_U];
-      uint4 q0[EMIT_U], q1[EMIT_U];
+      U4A qa[EMIT_U];
+      u32 qb[EMIT_U];
+      uint4 v[EMIT_U];
 #pragma unroll
       for (int u = 0; u < EMIT_U; u++) {
         act[u] = c[u] < wEnd;
@@ -3337,33 +3347,25 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         const u32 pr = sPre[j[u]];
         lds[u] = o[u] < (pr >> 16);
         src[u] = sSrc[j[u]] + (o[u] - (pr & 0xffff));
-        q0[u] = q1[u] = make_uint4(0, 0, 0, 0);
-        if (act[u] && !lds[u]) {
-          CHK((src[u] & ~u64(15)) + 32 <= A.arenaLen + 64, CK_EMIT_ARENA, (src[u] & ~u64(15)) + 32, A.arenaLen + 64);
-          const u8 *q = A.arena + (src[u] & ~u64(15));
-          q0[u] = *reinterpret_cast<const uint4 *>(q);
-          q1[u] = *reinterpret_cast<const uint4 *>(q + 16);
+        qa[u] = U4A{0, 0, 0, 0};
+        qb[u] = 0;
+        if (act[u] && !lds[u]) {  // (issued together: the loads of all EMIT_U chunks in flight)
+          CHK((src[u] & ~u64(3)) + 20 <= A.arenaLen + 32, CK_EMIT_ARENA, (src[u] & ~u64(3)) + 20, A.arenaLen + 32);
+          const u8 *q = A.arena + (src[u] & ~u64(3));
+          qa[u] = *reinterpret_cast<const U4A *>(q);
+          qb[u] = *reinterpret_cast<const u32 *>(q + 16);
         }
       }
 #pragma unroll
       for (int u = 0; u < EMIT_U; u++) {
         if (!act[u]) continue;
-        uint4 v;
-        if (lds[u]) {
-          v = *reinterpret_cast<const uint4 *>(&pre[j[u]][o[u]]);
-        } else {
-          v = shift_window(q0[u], q1[u], u32(src[u] & 15));
-          const int keep = int(sLen[j[u]]) - int(o[u]);
-          if (keep < 16) {  // zero the 16-B tail padding
-            v.x &= keep_mask(keep);
-            v.y &= keep_mask(keep - 4);
-            v.z &= keep_mask(keep - 8);
-            v.w &= keep_mask(keep - 12);
-          }
-        }
+        if (lds[u])
+          v[u] = *reinterpret_cast<const uint4 *>(&pre[j[u]][o[u]]);
+        else  // the funnel shift, then the 16-B tail padding zeroed
+          v[u] = keep_bytes(window_of(qa[u], qb[u], u32(src[u] & 3)), int(sLen[j[u]]) - int(o[u]));
         CHK(gByte + (u64(c[u]) << 4) + 16 <= A.outByteCap + 64, CK_EMIT_BYTES, gByte + (u64(c[u]) << 4) + 16,
             A.outByteCap + 64);
-        store16(outG + (u64(c[u]) << 4), v);
+        store16(outG + (u64(c[u]) << 4), v[u]);
       }
       cur += k;
       c0 = wEnd;
