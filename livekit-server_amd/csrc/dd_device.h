@@ -680,13 +680,14 @@ struct SelResult {
 // the track's structure ring; out receives the marshalled descriptor.
 // (staged: an LDS copy of structure slot stagedSlot, read instead of the
 // track's ring in HBM for that slot)
-__device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStruct *structs, const DDPkt &p, bool hasDD, bool pktMarker,
+__device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStruct *structs, const DDPkt *pp, bool pktMarker,
                                       i32 &curS, i32 &curT, i32 &prevS, i32 &prevT, i32 tgtS, i32 tgtT, u8 *out,
                                       const DDStruct *staged, u32 stagedSlot) {
   auto pick = [&](u32 slot) -> const DDStruct & { return slot == stagedSlot ? *staged : structs[slot]; };
   SelResult r = {false, false, false, false, false, 0, false};
   if (curS != -1 && curT != -1) r.relevant = true;
-  if (!hasDD) return r;
+  if (!pp) return r;  // (no descriptor)
+  const DDPkt &p = *pp;
   const u64 efn = p.extFN;
   const bool attached = p.flags & DP_ATTACHED;
   if (!(d.flags & DS_KF_VALID) && !attached) return r;

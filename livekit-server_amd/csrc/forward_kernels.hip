@@ -250,7 +250,7 @@ __device__ __forceinline__ void rm_reset(Lane &L, u64 start, u64 val) {
   L.h.rmOpenValue = val;
 }
 // ExcludeRange rangemap.go:100-132
-__device__ bool rm_exclude(Lane &L, u64 s, u64 e) {
+__device__ __forceinline__ bool rm_exclude(Lane &L, u64 s, u64 e) {
   if (e == s || (e - s) > HALF64) return false;
   if (L.h.rmOpenStart > s) return false;
   u64 nv = L.h.rmOpenValue + (e - s);
@@ -509,7 +509,7 @@ __device__ void vp8_record_missing_wide(Lane &L, i32 prevMax, i32 ext, i32 off) 
     L.h.missCount = u8(kMissKeep);
   }
 }
-__device__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
+__device__ __forceinline__ void vp8_record_missing(Lane &L, i32 prevMax, i32 ext, i32 off) {
   L.vcDirty = true;
   if (ext < prevMax) return;
   const i64 span = i64(ext) - i64(prevMax) + 1;
@@ -1007,10 +1007,9 @@ __device__ int fw_translate(Lane &L, const PktV &p, u32 k, Fwd &o) {
     }
   }
   if (DDK && hasf(L, F_DD)) {  // DependencyDescriptor.Select videolayerselector/dependencydescriptor.go:65-355
-    DDPkt dp;
     const bool hasDD = (p.flags & LKF_PKT_DD) && L.ddPkts && (L.ddPkts[k].flags & DP_VALID);
-    if (hasDD) dp = L.ddPkts[k];
-    const dd::SelResult r = dd::dd_select(*L.dd, L.ddRing, dp, hasDD, pktMarker, L.h.curS, L.h.curT, L.h.prevS,
+    // (the descriptor is read where k_dd_decode left it: no private copy)
+    const dd::SelResult r = dd::dd_select(*L.dd, L.ddRing, hasDD ? L.ddPkts + k : nullptr, pktMarker, L.h.curS, L.h.curT, L.h.prevS,
                                           L.h.prevT, L.h.tgtS, L.h.tgtT, L.ddBuf, L.ddS, L.ddSSlot);
     if (r.limit && lane_id() == 0) atomicOr(L.err, 16u);
     if (!r.selected) {
@@ -1884,7 +1883,10 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     if (ns >= 0) {
       const u32 k = u32(__popcll(winM));
       o.nTuples += k;
-      o.drops[ns] += k;
+      if (ns == LKF_DROP_MUTED)
+        o.drops[LKF_DROP_MUTED] += k;
+      else
+        o.drops[LKF_DROP_PAUSED] += k;
       return pos + k;
     }
   }
@@ -1966,9 +1968,10 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     }
   } else if (DDK) {  // ---- DependencyDescriptor.Select
     DDState &d = *L.dd;
-    DDPkt dp = {};
+    DDPkt dp = {};  // (scalar fields only: the frame diffs and the marshal read dpg)
     const bool hasDD = inWin && (p.flags & LKF_PKT_DD) && L.ddPkts;
-    if (hasDD) dp = L.ddPkts[pi];
+    const DDPkt *const dpg = L.ddPkts + (hasDD ? pi : 0u);
+    if (hasDD) dp = *dpg;
     const bool ddLane = hasDD && (dp.flags & DP_VALID);  // (no descriptor: not selected, no DD state change)
     const u64 cl0 = d.cLast;
     const u64 efn = dp.extFN;
@@ -2057,7 +2060,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     SVC_WHY(8);
     if (ddFwdSel && good)  // a referenced frame that was dropped drops this one (:192-201): full step
       for (int j = 0; j < int(dp.nfd) && j < kDDFdiffs; j++)
-        if (dp.fd[j] != 0 && dec(efn - dp.fd[j]) == dd::SD_DROPPED) good = false;
+        if (dpg->fd[j] != 0 && dec(efn - dpg->fd[j]) == dd::SD_DROPPED) good = false;
     SVC_WHY(9);
     if (ddFwdSel && good) {
       // frame number (FrameNumberWrapper without a structure update) and the
@@ -2065,7 +2068,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       const bool hasMask = d.flags & DS_HAS_MASK;
       const bool hasActive = (dp.flags & DP_ACTIVE) || hasMask;
       const u32 active = hasMask ? d.mask : dp.activeMask;
-      ddLen = dd::dd_marshal_inl(*s, dp, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
+      ddLen = dd::dd_marshal_inl(*s, *dpg, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
                                  kSvcDDBytes);
       if (ddLen < 0) good = false;
       mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
