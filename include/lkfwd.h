@@ -809,7 +809,10 @@ typedef struct lkf_transport_params {
 /* Adds a transport (session keys derived on the GPU: RFC 3711 §4.3.1). */
 int32_t lkf_add_transport(lkf_engine *e, const lkf_transport_params *p);
 /* Binds a DownTrack's packets to a transport (-1: none, its packets are
- * copied unprotected).  Binding starts a fresh rollover state for its SSRC. */
+ * copied unprotected).  Binding starts a fresh rollover state for its SSRC.
+ * The transport is also the DownTrack's PeerConnection for send-side TWCC:
+ * the DownTracks bound to one transport share its transport-wide sequence
+ * counter (pkg/rtc/transport.go:352-355). */
 int lkf_set_downtrack_transport(lkf_engine *e, int32_t dt, int32_t transport);
 /* Protects the last lkf_run's output (asynchronously, after its emit stage):
  * every packet gets the abs-send-time of `send_time_ns` (unix ns, pion/rtp

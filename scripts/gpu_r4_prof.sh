@@ -1,7 +1,7 @@
 #!/bin/bash
 # Bench lines + rocprofv3 kernel stats of chosen bench shapes (round 4).
-# PROF_SHAPES: '|'-separated bench argument lists (default: the ExtPacket
-# headline and the raw-datagram ingress step).  OUT_NAME names the output
+# PROF_SHAPES: '|'-separated bench argument lists (default: the ingress-inclusive
+# headline step and the ExtPacket step).  OUT_NAME names the output
 # directory under gpurun_out/.  Each GPU step has its own limit; the script
 # stops at the first failure.
 set -u
@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${OUT_NAME:-r4_prof}
 mkdir -p $O
-SHAPES="${PROF_SHAPES:---steps 20 --warmup 5 --no-cpu-baseline|--ingress --steps 20 --warmup 5 --no-cpu-baseline}"
+SHAPES="${PROF_SHAPES:---steps 20 --warmup 5 --no-cpu-baseline|--extpackets --steps 20 --warmup 5 --no-cpu-baseline}"
 IFS='|' read -ra LIST <<< "$SHAPES"
 if [ "${RUN_TESTS:-0}" = "1" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest.log 2>&1
