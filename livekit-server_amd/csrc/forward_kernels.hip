@@ -44,6 +44,13 @@ constexpr i32 INVALID = -1;
 #define LKF_OOO_RUN 1
 #endif
 constexpr bool kOooRun = LKF_OOO_RUN != 0;
+// Decide reads and writes the munger's closed RangeMap ranges in HBM instead
+// of staging the ring in LDS: the ring is read only for an out-of-order key
+// below the open range, and an exclusion writes one entry.
+#ifndef LKF_RM_LDS
+#define LKF_RM_LDS 0
+#endif
+constexpr bool kRmLds = LKF_RM_LDS != 0;
 
 // ---------------------------------------------------------------------------
 // Checked builds (-DLKF_CHECKED=1, liblkfwd_checked.so): every global access
@@ -2385,7 +2392,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __shared__ i32 sEx[kSetCap];
   __shared__ i32 sMissKey[kMissCap];
   __shared__ i32 sMissVal[kMissCap];
-  __shared__ RangeEntry sRm[kRangeCap];
+  __shared__ RangeEntry sRm[kRmLds ? kRangeCap : 1];
   // (the plain instantiation keeps a 16-B stub: LDS is allocated per instantiation)
   __shared__ __attribute__((aligned(16))) u8 sDDRaw[DDK ? sizeof(DDState) + kDDMaxBytes + 1 : 16];
   __shared__ u8 sSvcScr[DDK ? 64 * kSvcDDBytes : 16];  // svc_run: per-lane marshalled descriptors
@@ -2463,7 +2470,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
   __syncthreads();
   RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
-  L.rm = sRm;
+  L.rm = kRmLds ? sRm : rmG;
   L.rmDirty = false;
   L.vcDirty = false;
   L.vc = A.vc + d;
@@ -2477,12 +2484,13 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       sDrop[lane] = L.vc->dropKey[lane];
       sEx[lane] = L.vc->exKey[lane];
     }
-    for (u32 i = lane; i < u32(kMissCap); i += 64) {
-      sMissKey[i] = L.vc->missKey[i];
-      sMissVal[i] = L.vc->missVal[i];
+    for (u32 i = lane; i < L.h.missCount; i += 64) {  // the live entries of the missing-picture ring
+      const u32 idx = (L.h.missHead + i) % kMissCap;
+      sMissKey[idx] = L.vc->missKey[idx];
+      sMissVal[idx] = L.vc->missVal[idx];
     }
   }
-  for (u32 i = lane; i < L.h.rmCount; i += 64) {  // live closed ranges of the RangeMap ring
+  for (u32 i = lane; kRmLds && i < L.h.rmCount; i += 64) {  // live closed ranges of the RangeMap ring
     const u32 idx = (L.h.rmHead + i) % kRangeCap;
     sRm[idx] = rmG[idx];
   }
@@ -3087,7 +3095,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
   __syncthreads();
   reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
-  if (L.rmDirty) {
+  if (kRmLds && L.rmDirty) {
     wave_lds_sync();
     for (u32 i = lane; i < L.h.rmCount; i += 64) {
       const u32 idx = (L.h.rmHead + i) % kRangeCap;
