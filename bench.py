@@ -24,6 +24,7 @@ Prints ONE JSON line (rank 0).
 import argparse
 import ctypes as C
 import importlib
+import glob
 import json
 import os
 import sys
@@ -185,7 +186,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
     # summary of this same workload (scripts/gpu_pmc.sh -> profiles/)
-    ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", os.path.join(ROOT, "profiles", "r3_pmc_traffic.json")))
+    ap.add_argument("--pmc-csv", default=os.environ.get("LKF_PMC_CSV", ""),
+                    help="PMC summary to quote (default: the profiles/r*_pmc_*.json measured on this build and shape)")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostic: wait for each step (no decide/emit overlap; standalone kernel times)")
     ap.add_argument("--extpackets", action="store_true",
@@ -438,16 +440,21 @@ def main():
         kd = kern("k_decide_dt", decide_bytes, dec_ms)
         ke = kern("k_emit", emit_bytes, emit_ms)
         traffic, traffic_src = None, None
-        if args.pmc_csv and os.path.exists(args.pmc_csv):
+        cands = [args.pmc_csv] if args.pmc_csv else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json")))
+        sha = kernel_sources_sha()
+        for path in cands:  # a summary of this build and this exact shape (scripts/gpu_pmc.sh)
             try:
-                pmc = json.load(open(args.pmc_csv))
-                if (pmc.get("kernel_sources_sha") == kernel_sources_sha() and pmc.get("bench_args_rooms") == args.rooms
-                        and pmc.get("bench_args_config", 2) == args.config
-                        and bool(pmc.get("bench_args_ingress", False)) == bool(args.ingress)):
-                    traffic = pmc.get("hbm_bytes_per_step")
-                    traffic_src = os.path.relpath(args.pmc_csv, ROOT)
+                pmc = json.load(open(path))
             except Exception:
-                traffic = None
+                continue
+            if (pmc.get("kernel_sources_sha") == sha and pmc.get("bench_args_rooms") == args.rooms
+                    and pmc.get("bench_args_config", 2) == args.config
+                    and bool(pmc.get("bench_args_ingress", False)) == bool(args.ingress)
+                    and abs(float(pmc.get("bench_args_batch_s", 1.0)) - args.batch_s) < 1e-9
+                    and bool(pmc.get("bench_args_srtp", False)) == bool(args.srtp)):
+                traffic = pmc.get("hbm_bytes_per_step")
+                traffic_src = os.path.relpath(path, ROOT)
+                break
         pipe_ach = algo / (tot_ms / 1e3) / 1e9 if tot_ms else 0.0
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -472,9 +479,6 @@ def main():
             # memory system (thread_scaling_eff = the 16-thread rate over 16 x
             # the single-thread rate, both measured)
             cpu["thread_scaling_eff"] = round(v / (v1 * used), 3) if v1 else None
-            cpu["all_cores"] = {"value": round(v / used * (os.cpu_count() or used), 1), "cores": os.cpu_count(),
-                                "basis": "extrapolated: %d-thread rate x %d/%d host threads (not run: the box's "
-                                         "CPU share is 16 per GPU)" % (used, os.cpu_count() or used, used)}
         line = {
             "metric": "forwarded RTP pkts/sec per GPU & node (bit-exact) + % HBM roofline",
             "value": round(fwd_all / elapsed, 1),

@@ -36,6 +36,26 @@ def totals(out):
     return out
 
 
+def bench_shape(argstr):
+    """The workload a bench.py command line measures (the keys bench.py matches
+    before quoting this summary's traffic): config, rooms, batch length, and
+    whether the step ingests raw datagrams or protects with SRTP."""
+    import argparse
+    import shlex
+    from bench import CONFIGS
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--rooms", type=int, default=0)
+    ap.add_argument("--batch-s", type=float, default=1.0)
+    ap.add_argument("--extpackets", action="store_true")
+    ap.add_argument("--host-io", action="store_true")
+    ap.add_argument("--srtp", action="store_true")
+    a, _ = ap.parse_known_args(shlex.split(argstr))
+    ingress = (not a.extpackets or a.config == 3) and not (a.host_io and a.config != 3)
+    return {"bench_args": argstr, "bench_args_config": a.config, "bench_args_rooms": a.rooms or CONFIGS[a.config]["rooms"],
+            "bench_args_batch_s": a.batch_s, "bench_args_ingress": ingress, "bench_args_srtp": a.srtp}
+
+
 def main():
     d = sys.argv[1]
     if "--from-summary" in sys.argv:  # re-derive the totals of an existing summary.json (raw CSVs deleted)
@@ -71,8 +91,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import kernel_sources_sha
     out["kernel_sources_sha"] = kernel_sources_sha()
-    out["bench_args_config"] = int(os.environ.get("PMC_CONFIG", "2"))
-    out["bench_args_rooms"] = int(os.environ.get("PMC_ROOMS", "100"))
+    out.update(bench_shape(os.environ.get("BENCH_ARGS", "")))
     json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
     if "--delete-raw" in sys.argv:
