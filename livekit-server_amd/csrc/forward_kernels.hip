@@ -3166,7 +3166,10 @@ constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 desc
 // (two-byte extension profile) = 343
 constexpr int PRE_MAX_DD = 352;
 
-constexpr int EMIT_U = 4;
+#ifndef LKF_EMIT_U
+#define LKF_EMIT_U 4
+#endif
+constexpr int EMIT_U = LKF_EMIT_U;  // 16-B chunks per lane in flight per copy iteration
 
 
 struct EmitArgs {

@@ -1,8 +1,9 @@
 #!/bin/bash
-# A/B timing of the product build (A, liblkfwd.so) against lib/liblkfwd_ab.so
-# (B, `make -C livekit-server_amd/csrc ab ABFLAGS=...`) in one GPU call:
-# every shape in AB_SHAPES ('|'-separated bench argument lists) runs A, B, A, B
-# (AB_REPS rounds).  One line per run: build, shape, ms_per_step, value.
+# A/B timing of in-tree builds in one GPU call (AB_LIBS, default the product
+# liblkfwd.so against lib/liblkfwd_ab.so from `make -C livekit-server_amd/csrc
+# ab ABNAME=ab ABFLAGS=...`): every shape in AB_SHAPES ('|'-separated bench
+# argument lists) runs each build in turn, AB_REPS rounds.  One line per run:
+# build, shape, ms_per_step, value.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -13,7 +14,7 @@ IFS='|' read -ra LIST <<< "$SHAPES"
 i=0
 for a in "${LIST[@]}"; do
   for r in $(seq 1 ${AB_REPS:-2}); do
-    for lib in liblkfwd.so liblkfwd_ab.so; do
+    for lib in ${AB_LIBS:-liblkfwd.so liblkfwd_ab.so}; do
       LKF_LIB=$lib timeout -k 10 300 python3 bench.py $a > $O/s${i}_${lib%.so}_$r.log 2>&1
       rc=$?
       [ $rc -eq 0 ] || { echo "$lib shape$i rc=$rc"; tail -5 $O/s${i}_${lib%.so}_$r.log; exit $rc; }
