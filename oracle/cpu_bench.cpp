@@ -54,57 +54,72 @@ typedef struct orc_bench_shard {
   uint32_t ntracks, ndts, nstreams, nbatches;
 } orc_bench_shard;
 
-// Runs every shard on its own thread (nshards threads); forwarded[i] = shard
-// i's forwarded tuples, *wall_s = seconds from the common start to the last
-// thread's end, busy_s[i] = shard i's own timed seconds (nullptr: not wanted).
-// 0, or the first non-zero return code of an oracle call.
-int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, int ingress, uint32_t seq_size,
-                  uint64_t *forwarded, double *busy_s, double *wall_s) {
+// Runs the shards on `nthreads` threads: every shard's engine is built
+// first (tracks, DownTracks, streams: untimed), then all threads start at one
+// barrier and pull shards from a shared counter, each shard's batches in
+// order on the thread that took it (dynamic balancing: rooms differ in work —
+// mutes, layer switches, loss — so a static split leaves threads idle while
+// the slowest finishes).  forwarded[i] = shard i's forwarded tuples, *wall_s =
+// seconds from the common start to the last thread's end, busy_s[t] = thread
+// t's own timed seconds (nullptr: not wanted).  0, or the first non-zero
+// return code of an oracle call.
+int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthreads, int ingress,
+                  uint32_t seq_size, uint64_t *forwarded, double *busy_s, double *wall_s) {
+  if (nthreads == 0) nthreads = 1;
   std::vector<orc_engine *> eng(nshards, nullptr);
   std::atomic<int> rc{0};
-  std::atomic<uint32_t> ready{0};
+  std::atomic<uint32_t> built{0}, next{0}, ready{0};
   std::atomic<bool> go{false};
   using clk = std::chrono::steady_clock;
   std::vector<std::thread> th;
   clk::time_point t0;
-  for (uint32_t i = 0; i < nshards; i++)
-    th.emplace_back([&, i]() {
-      const orc_bench_shard &s = shards[i];
-      orc_engine *e = orc_create(seq_size);
-      eng[i] = e;
-      int r = 0;
-      for (uint32_t t = 0; t < s.ntracks && !r; t++) r = orc_add_track(e, &s.tracks[t]) == int32_t(t) ? 0 : -1;
-      for (uint32_t d = 0; d < s.ndts && !r; d++) r = orc_add_downtrack(e, &s.dts[d]) == int32_t(d) ? 0 : -1;
-      if (ingress)
-        for (uint32_t k = 0; k < s.nstreams && !r; k++) r = orc_add_stream(e, &s.streams[k]) == int32_t(k) ? 0 : -1;
-      if (r) rc = r;
+  auto build = [&](uint32_t i) {
+    const orc_bench_shard &s = shards[i];
+    orc_engine *e = orc_create(seq_size);
+    eng[i] = e;
+    int r = 0;
+    for (uint32_t t = 0; t < s.ntracks && !r; t++) r = orc_add_track(e, &s.tracks[t]) == int32_t(t) ? 0 : -1;
+    for (uint32_t d = 0; d < s.ndts && !r; d++) r = orc_add_downtrack(e, &s.dts[d]) == int32_t(d) ? 0 : -1;
+    if (ingress)
+      for (uint32_t k = 0; k < s.nstreams && !r; k++) r = orc_add_stream(e, &s.streams[k]) == int32_t(k) ? 0 : -1;
+    if (r) rc = r;
+  };
+  auto forward = [&](uint32_t i) {
+    const orc_bench_shard &s = shards[i];
+    orc_engine *e = eng[i];
+    uint64_t fwd = 0;
+    int r = 0;
+    for (uint32_t b = 0; b < s.nbatches && !r; b++) {
+      const orc_bench_batch &x = s.batches[b];
+      if (x.nev) r = orc_ctl_batch(e, x.ev, x.nev);
+      if (r) break;
+      if (ingress) {
+        r = orc_ingest(e, x.raws, x.nraw, x.arena, x.alen);
+        const lkf_pkt *p = nullptr;
+        uint32_t n = 0;
+        if (!r) r = orc_ingested_ptr(e, &p, &n);
+        if (!r) r = orc_run(e, p, n, x.arena, x.alen);
+      } else {
+        if (x.dd) r = orc_submit_dd(e, x.dd, x.n);
+        if (!r) r = orc_run(e, x.pkts, x.n, x.arena, x.alen);
+      }
+      lkf_stats st{};
+      if (!r) r = orc_get_stats(e, &st);
+      fwd += st.forwarded;
+    }
+    forwarded[i] = fwd;
+    if (r) rc = r;
+  };
+  for (uint32_t t = 0; t < nthreads; t++)
+    th.emplace_back([&, t]() {
+      for (uint32_t i; (i = built.fetch_add(1)) < nshards;) build(i);  // (untimed)
       ready++;
       while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
       const clk::time_point a = clk::now();
-      uint64_t fwd = 0;
-      for (uint32_t b = 0; b < s.nbatches && !r; b++) {
-        const orc_bench_batch &x = s.batches[b];
-        if (x.nev) r = orc_ctl_batch(e, x.ev, x.nev);
-        if (r) break;
-        if (ingress) {
-          r = orc_ingest(e, x.raws, x.nraw, x.arena, x.alen);
-          const lkf_pkt *p = nullptr;
-          uint32_t n = 0;
-          if (!r) r = orc_ingested_ptr(e, &p, &n);
-          if (!r) r = orc_run(e, p, n, x.arena, x.alen);
-        } else {
-          if (x.dd) r = orc_submit_dd(e, x.dd, x.n);
-          if (!r) r = orc_run(e, x.pkts, x.n, x.arena, x.alen);
-        }
-        lkf_stats st{};
-        if (!r) r = orc_get_stats(e, &st);
-        fwd += st.forwarded;
-      }
-      if (busy_s) busy_s[i] = std::chrono::duration<double>(clk::now() - a).count();
-      forwarded[i] = fwd;
-      if (r) rc = r;
+      for (uint32_t i; (i = next.fetch_add(1)) < nshards;) forward(i);
+      if (busy_s) busy_s[t] = std::chrono::duration<double>(clk::now() - a).count();
     });
-  while (ready.load() < nshards) std::this_thread::yield();
+  while (ready.load() < nthreads) std::this_thread::yield();
   t0 = clk::now();
   go.store(true, std::memory_order_release);
   for (auto &t : th) t.join();
