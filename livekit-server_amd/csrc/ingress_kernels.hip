@@ -44,7 +44,19 @@ using i64 = int64_t;
 // ---------------------------------------------------------------------------
 // k_ing_parse
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, u8 ddExt, IngParsed &q,
+// A datagram's bytes for the parsers: the first n staged in LDS, the rest read
+// from HBM (the parsers walk the header, extensions and codec descriptor byte
+// by byte; from LDS those dependent reads cost LDS latency, not HBM latency).
+struct StagedBytes {
+  const u8 *lds;
+  const u8 *g;
+  int n;
+  __device__ __forceinline__ u8 operator[](int i) const { return i < n ? lds[i] : g[i]; }
+  __device__ __forceinline__ StagedBytes operator+(int k) const { return StagedBytes{lds + k, g + k, n - k}; }
+};
+
+template <typename BP>
+__device__ __forceinline__ bool rtp_parse(BP buf, int len, u8 levelExt, u8 ddExt, IngParsed &q,
                                           int &levelOff, u8 twccExt = 0, int *twccOff = nullptr,
                                           int *twccLen = nullptr) {
   levelOff = -1;
@@ -124,7 +136,8 @@ __device__ __forceinline__ bool rtp_parse(const u8 *buf, int len, u8 levelExt, u
 }
 
 // buffer.VP8.Unmarshal helpers.go:76-162
-__device__ __forceinline__ bool vp8_parse(const u8 *p, int len, IngParsed &q) {
+template <typename BP>
+__device__ __forceinline__ bool vp8_parse(BP p, int len, IngParsed &q) {
   if (len < 1) return false;
   int idx = 0;
   q.vfirst = p[0];
@@ -188,7 +201,8 @@ __device__ __forceinline__ bool vp8_parse(const u8 *p, int len, IngParsed &q) {
 }
 
 // buffer.IsH264KeyFrame helpers.go:248-309
-__device__ inline bool h264_keyframe(const u8 *p, int n) {
+template <typename BP>
+__device__ inline bool h264_keyframe(BP p, int n) {
   if (n < 1) return false;
   const int nalu = p[0] & 0x1F;
   if (nalu == 0) return false;
@@ -218,15 +232,16 @@ __device__ inline bool h264_keyframe(const u8 *p, int n) {
 
 // buffer.IsAV1KeyFrame helpers.go:343-420: walk the aggregation's OBUs (W
 // field: the last one carries no length) to the first frame header
-__device__ inline bool av1_keyframe(const u8 *payload, int n) {
+template <typename BP>
+__device__ inline bool av1_keyframe(BP payload, int n) {
   if (n < 2) return false;
   if ((payload[0] & 0x88) != 0x08) return false;  // Z=0, N=1
   const int w = (payload[0] & 0x30) >> 4;
   int offset = 1;
   for (int i = 0;; i++) {
-    const u8 *data = payload + offset;
+    const BP data = payload + offset;
     const int dn = n - offset;
-    const u8 *obu;
+    BP obu = data;
     int olen, length;
     bool truncated = false;
     if (w == i + 1) {
@@ -277,7 +292,8 @@ __device__ inline bool av1_keyframe(const u8 *payload, int n) {
 // unpinned) + buffer.IsVP9KeyFrame helpers.go:317-336.  Layer info, flexible
 // mode reference indices and scalability-structure data are walked for their
 // lengths; the selector reads I/P/L/F/B/E/V, TID/U/SID.
-__device__ __forceinline__ bool vp9_parse(const u8 *p, int len, IngParsed &q) {
+template <typename BP>
+__device__ __forceinline__ bool vp9_parse(BP p, int len, IngParsed &q) {
   if (len < 1) return false;
   const u8 b0 = p[0];
   const bool I = b0 & 0x80, P = b0 & 0x40, L = b0 & 0x20, F = b0 & 0x10, V = b0 & 0x02;
@@ -355,12 +371,31 @@ __device__ __forceinline__ bool vp9_parse(const u8 *p, int len, IngParsed &q) {
   return true;
 }
 
-__global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u8 *__restrict__ raw,
-                            const DevStream *__restrict__ streams, u32 nstreams, IngParsed *__restrict__ out,
-                            u32 *__restrict__ twcc, u32 *__restrict__ err) {
+constexpr int kParseT = 256;      // k_ing_parse block
+constexpr int kParseStage = 128;  // bytes of each datagram staged in LDS
+constexpr int kStageW = kParseStage / 4 + 1;  // dwords per thread: a dword-aligned window (odd stride: no bank conflicts)
+__global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n,
+                                                      const u8 *__restrict__ raw, const DevStream *__restrict__ streams,
+                                                      u32 nstreams, IngParsed *__restrict__ out, u32 *__restrict__ twcc,
+                                                      u32 *__restrict__ err) {
+  __shared__ u32 sStage[kParseT * kStageW];
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const lkf_raw_pkt rp = raws[i];
+  // the datagram's first bytes into LDS: dword loads of the dword-aligned
+  // window (global loads need only dword alignment; a dword holding a byte of
+  // the datagram lies in that byte's page), all in flight together
+  u32 *const st = sStage + threadIdx.x * kStageW;
+  const int sl = int(rp.len) < kParseStage ? int(rp.len) : kParseStage;
+  {
+    const u32 *g = reinterpret_cast<const u32 *>(raw + (rp.off & ~u64(3)));
+    const int nw = (sl + int(rp.off & 3) + 3) >> 2;
+    u32 w[kStageW];
+#pragma unroll
+    for (int k = 0; k < kStageW; k++) w[k] = k < nw ? g[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < kStageW; k++) st[k] = w[k];
+  }
   IngParsed q = {};
   twcc[i] = 0;
   if (rp.stream >= nstreams) {
@@ -371,7 +406,8 @@ __global__ void k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n, const u
   }
   const DevStream s = streams[rp.stream];
   q.track = s.track;
-  const u8 *b = raw + rp.off;
+  // (each thread reads only its own staged window: no barrier needed)
+  const StagedBytes b{reinterpret_cast<const u8 *>(st) + (rp.off & 3), raw + rp.off, sl};
   int levelOff = -1, twOff = -1, twLen = 0;
   if (rtp_parse(b, int(rp.len), s.levelExt, s.ddExt, q, levelOff, s.twccExt, &twOff, &twLen)) {
     q.flags |= IP_OK;
@@ -1719,7 +1755,7 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
                                             const u64 *__restrict__ offs, u8 *__restrict__ out,
                                             const u8 *__restrict__ dd) {
   __shared__ u8 pre[12 + 60 + 4 + 2 + kDDMaxBytes + 5 + 3 + 8 + 4];
-  __shared__ u32 sPre, sLen, sPay, sPayLen;
+  __shared__ u32 sPre, sLen, sPay;
   const u32 i = blockIdx.x, lane = threadIdx.x;
   if (lane == 0) {
     u32 total = 0;
@@ -1812,7 +1848,6 @@ __global__ void __launch_bounds__(64) k_rtx(const lkf_rtx *__restrict__ rtx, con
         total = u32(n) + payLen;
         sPre = u32(n);
         sPay = rp.off + pay;
-        sPayLen = payLen;
       }
     }
     sLen = total;
@@ -1973,7 +2008,7 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
     hipLaunchKernelGGL(k_ing_init, dim3(g), dim3(256), 0, st, a.ntracks, a.n, a.tBegin, a.tEnd, a.tRuns, a.err,
                        a.total, a.bucket ? a.bucket->store : nullptr);
   }
-  hipLaunchKernelGGL(k_ing_parse, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.n, a.raw, a.streams, a.nstreams,
+  hipLaunchKernelGGL(k_ing_parse, dim3(nblk(a.n, kParseT)), dim3(kParseT), 0, st, a.raws, a.n, a.raw, a.streams, a.nstreams,
                      a.parsed, a.twcc, a.err);
   hipLaunchKernelGGL(k_ing_ranges, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.parsed, a.n, a.ntracks, a.tBegin, a.tEnd,
                      a.tRuns, a.err);
