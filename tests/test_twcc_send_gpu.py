@@ -8,7 +8,7 @@ traces mix abs-send-time and transport-cc subscribers (Trace(twcc=1): every
 second subscriber), DownTracks are bound to one transport per (room,
 subscriber) with every seventh left unbound (its own counter); forwarded
 batches, padding, blank frames and RTX interleave, and the protected output
-(SRTP over headers that carry the element) is compared too.  Every record
+(SRTP over headers that carry the element, packet by packet) is compared too.  Every record
 and wire byte must equal the oracle's.  No reference test covers the
 interceptor: parity unpinned beyond the oracle restatement."""
 import numpy as np
@@ -84,7 +84,12 @@ def test_transport_cc_matches_oracle(pkg, workload, abi, cfg):
             for f in abi.OUT_DTYPE.names:
                 assert np.array_equal(grec[f], orec[f]), (b, f)
             assert np.array_equal(gar, oar), b
-            assert np.array_equal(pkg.drain_protected(eng.api, eng.h), pkg.drain_protected(o.api, oh)), b
+            gp, op = pkg.drain_protected(eng.api, eng.h), pkg.drain_protected(o.api, oh)
+            assert len(gp) == len(op)
+            for i in range(len(orec)):  # every protected packet (the gaps between them are unspecified)
+                off = int(orec["out_off"][i]) + 16 * i
+                ln = int(orec["out_len"][i]) + (10 if int(orec["dt"][i]) in tg else 0)
+                assert np.array_equal(gp[off:off + ln], op[off:off + ln]), (b, i)
             tv = _tcc_values(tr, orec, oar)
             stamped += len(tv)
             now = EPOCH + (b + 1) * 10**9
