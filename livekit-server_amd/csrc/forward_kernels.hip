@@ -44,13 +44,7 @@ constexpr i32 INVALID = -1;
 #define LKF_OOO_RUN 1
 #endif
 constexpr bool kOooRun = LKF_OOO_RUN != 0;
-// Decide reads and writes the munger's closed RangeMap ranges in HBM instead
-// of staging the ring in LDS: the ring is read only for an out-of-order key
-// below the open range, and an exclusion writes one entry.
-#ifndef LKF_RM_LDS
-#define LKF_RM_LDS 0
-#endif
-constexpr bool kRmLds = LKF_RM_LDS != 0;
+
 
 // ---------------------------------------------------------------------------
 // Checked builds (-DLKF_CHECKED=1, liblkfwd_checked.so): every global access
@@ -2392,7 +2386,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __shared__ i32 sEx[kSetCap];
   __shared__ i32 sMissKey[kMissCap];
   __shared__ i32 sMissVal[kMissCap];
-  __shared__ RangeEntry sRm[kRmLds ? kRangeCap : 1];
+  __shared__ RangeEntry sRm[kRangeCap];
   // (the plain instantiation keeps a 16-B stub: LDS is allocated per instantiation)
   __shared__ __attribute__((aligned(16))) u8 sDDRaw[DDK ? sizeof(DDState) + kDDMaxBytes + 1 : 16];
   __shared__ u8 sSvcScr[DDK ? 64 * kSvcDDBytes : 16];  // svc_run: per-lane marshalled descriptors
@@ -2470,7 +2464,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
   __syncthreads();
   RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
-  L.rm = kRmLds ? sRm : rmG;
+  L.rm = sRm;
   L.rmDirty = false;
   L.vcDirty = false;
   L.vc = A.vc + d;
@@ -2490,7 +2484,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       sMissVal[idx] = L.vc->missVal[idx];
     }
   }
-  for (u32 i = lane; kRmLds && i < L.h.rmCount; i += 64) {  // live closed ranges of the RangeMap ring
+  for (u32 i = lane; i < L.h.rmCount; i += 64) {  // live closed ranges of the RangeMap ring
     const u32 idx = (L.h.rmHead + i) % kRangeCap;
     sRm[idx] = rmG[idx];
   }
@@ -2668,9 +2662,16 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       // in-order recurrences (previous candidate, previous forward) skip it.
       bool oooL = false;
       if (kOooRun) {
-        u64 hi = excl_max_u64(cand ? p.esn : 0ull, lane);
-        if (hi < L.h.extHighestIncomingSN) hi = L.h.extHighestIncomingSN;
-        oooL = cand && i64(p.esn - hi) < 0;
+        // (the scan only when the window has one: a candidate not above the
+        // previous candidate, or the first one not above the state's highest)
+        const u64 cM = __ballot(cand);
+        const int pcA = prev_in(cM, lt);
+        const u64 pcAEsn = sh64(p.esn, pcA >= 0 ? pcA : int(lane));
+        if (__ballot(cand && i64(p.esn - (pcA >= 0 ? pcAEsn : L.h.extHighestIncomingSN)) <= 0)) {
+          u64 hi = excl_max_u64(cand ? p.esn : 0ull, lane);
+          if (hi < L.h.extHighestIncomingSN) hi = L.h.extHighestIncomingSN;
+          oooL = cand && i64(p.esn - hi) < 0;
+        }
       }
       const bool candIn = cand && !oooL;
       const u64 candM = __ballot(candIn);
@@ -3095,7 +3096,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
   __syncthreads();
   reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
-  if (kRmLds && L.rmDirty) {
+  if (L.rmDirty) {
     wave_lds_sync();
     for (u32 i = lane; i < L.h.rmCount; i += 64) {
       const u32 idx = (L.h.rmHead + i) % kRangeCap;

@@ -47,11 +47,19 @@ using i64 = int64_t;
 // A datagram's bytes for the parsers: the first n staged in LDS, the rest read
 // from HBM (the parsers walk the header, extensions and codec descriptor byte
 // by byte; from LDS those dependent reads cost LDS latency, not HBM latency).
+typedef const __attribute__((address_space(3))) u8 *LdsBytes;  // (ds_read, not a flat load)
 struct StagedBytes {
-  const u8 *lds;
+  LdsBytes lds;
   const u8 *g;
   int n;
-  __device__ __forceinline__ u8 operator[](int i) const { return i < n ? lds[i] : g[i]; }
+  __device__ __forceinline__ u8 operator[](int i) const {
+    u8 v;
+    if (i < n)
+      v = lds[i];
+    else
+      v = g[i];
+    return v;
+  }
   __device__ __forceinline__ StagedBytes operator+(int k) const { return StagedBytes{lds + k, g + k, n - k}; }
 };
 
@@ -407,7 +415,7 @@ __global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__rest
   const DevStream s = streams[rp.stream];
   q.track = s.track;
   // (each thread reads only its own staged window: no barrier needed)
-  const StagedBytes b{reinterpret_cast<const u8 *>(st) + (rp.off & 3), raw + rp.off, sl};
+  const StagedBytes b{(LdsBytes)(reinterpret_cast<const u8 *>(st)) + (rp.off & 3), raw + rp.off, sl};
   int levelOff = -1, twOff = -1, twLen = 0;
   if (rtp_parse(b, int(rp.len), s.levelExt, s.ddExt, q, levelOff, s.twccExt, &twOff, &twLen)) {
     q.flags |= IP_OK;
@@ -853,19 +861,17 @@ __device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u
 // The stream's RTX bucket inside the stream kernel (mediatransportutil
 // bucket.AddPacketWithSequenceNumber as buffer.go:471-481 calls it; oracle
 // bucket_oracle.h): the logical state (head, step) in LDS, the slot tags in
-// HBM, and this ingest's writer of each slot (sOwn in LDS for rings of up to
-// kBktLds slots, else the global owner words tagged with the ingest epoch) so
-// a slot taken again later in the batch cancels the earlier datagram's copy.
-constexpr int kBktLds = 2048;
+// HBM, and this ingest's writer of each slot (owner words in HBM tagged with
+// the ingest epoch) so a slot taken again later in the batch cancels the
+// earlier datagram's copy.  (An LDS owner map cost 8 KB per stream wave and
+// with it the occupancy that puts every stream of a batch in flight at once.)
 constexpr u32 kNoOwner = 0xFFFFFFFFu;
 struct BktCtx {
   BucketState *b;  // LDS
   u32 *tag;        // the stream's slot tags
-  u64 *owner;      // the stream's global owner words (rings above kBktLds)
+  u64 *owner;      // the stream's owner words
   u64 *store;      // per datagram of the batch
-  u32 *sOwn;       // LDS owner map (rings up to kBktLds)
   u64 ep;          // ingest epoch << 32
-  bool lds;
 };
 __device__ __forceinline__ int bkt_wrap(int x, int M) {
   x %= M;
@@ -873,15 +879,9 @@ __device__ __forceinline__ int bkt_wrap(int x, int M) {
 }
 // the slot's previous writer in this ingest is not stored; ic takes it (kNoOwner: invalidated)
 __device__ __forceinline__ void bkt_supersede(const BktCtx &k, int sl, u32 ic) {
-  if (k.lds) {
-    const u32 o = k.sOwn[sl];
-    if (o != kNoOwner) k.store[o] = 0;
-    k.sOwn[sl] = ic;
-  } else {
-    const u64 o = k.owner[sl];
-    if ((o & 0xFFFFFFFF00000000ull) == k.ep) k.store[u32(o)] = 0;
-    k.owner[sl] = ic == kNoOwner ? 0 : (k.ep | ic);
-  }
+  const u64 o = k.owner[sl];
+  if ((o & 0xFFFFFFFF00000000ull) == k.ep) k.store[u32(o)] = 0;
+  k.owner[sl] = ic == kNoOwner ? 0 : (k.ep | ic);
 }
 // AddPacketWithSequenceNumber for one datagram (one lane): push (the skipped
 // slots invalidated, the packet at the new head) or set (an older SN inside
@@ -955,10 +955,10 @@ __device__ __forceinline__ void rx_jitter(StreamHot &h, u32 clockRate, u64 ets, 
 // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241), the padding
 // RangeMap, the dependency descriptor; its flow, forward flag and DD record.
 template <int HS>
-__device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream &s,
+__device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream &s,
                                          const IngParsed &p, const lkf_raw_pkt &rp, u32 ic, lkf_flow *flows,
                                          u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *ddStates,
-                                         DDStruct *ddStructs, u32 *err, const BktCtx *bk, u32 *gap) {
+                                         DDStruct *ddStructs, u32 *err, const BktCtx &bk, bool bkOn, u32 *gap) {
   const i64 arrival = rp.arrival_ns;
   lkf_flow f = {};
   f.pkt = 0xffffffffu;
@@ -1065,7 +1065,7 @@ __device__ __forceinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring
     if (dup) break;  // the RTX bucket already holds it (ErrRTXPacket)
     // AddPacketWithSequenceNumber under the adjusted SN (buffer.go:471-481):
     // too old, too large or already held -> no ExtPacket (before getExtPacket)
-    if (bk && bkt_add_one(*bk, u16(f.ext_sn), rp.len, ic) < 0) break;
+    if (bkOn && bkt_add_one(bk, u16(f.ext_sn), rp.len, ic) < 0) break;
     f.flags |= LKF_FLOW_BUCKET;
     // getExtPacket (buffer.go:599-671): the dependency descriptor first
     if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
@@ -1154,7 +1154,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   __shared__ u64 sHist[kHistWords];
   __shared__ StreamHot sh;
   __shared__ BucketState sB;
-  __shared__ u32 sOwn[kBktLds];
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
@@ -1179,13 +1178,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     bk.tag = bka.tag + sB.base;
     bk.owner = bka.owner + sB.base;
     bk.store = bka.store;
-    bk.sOwn = sOwn;
     bk.ep = u64(bka.epoch) << 32;
-    bk.lds = M <= kBktLds;
-    if (bk.lds)
-      for (int i = int(lane); i < M; i += 64) sOwn[i] = kNoOwner;
   }
-  const BktCtx *bkp = bkOn ? &bk : nullptr;
   __syncthreads();
   RangeEntry *ring = rings + size_t(sid) * kRangeCap;
   const bool useList = s.layer < 3;
@@ -1214,7 +1208,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         for (u32 x = 0; x < m; x++)
           if (sR[x].stream == sid)
             ing_step<1>(sh, sHist, ring, s, sP[x], sR[x], sI[x], flows, fwd, ingDD, raw, ddStates, ddStructs, err,
-                        bkp, gap);
+                        bk, bkOn, gap);
       }
       __syncthreads();
     }
@@ -1258,7 +1252,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u32 L = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;
     if (L == 0) {
       if (lane == 0 && rp.stream == sid)
-        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err, bkp, gap);
+        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err, bk, bkOn, gap);
       __syncthreads();
       j++;
       continue;
