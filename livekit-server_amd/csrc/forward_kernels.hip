@@ -37,13 +37,6 @@ using i64 = int64_t;
 
 constexpr u64 HALF64 = 1ull << 63;
 constexpr i32 INVALID = -1;
-// Out-of-order packets decided inside a decide run instead of the serial step:
-// classified by a prefix max, resolved after the run's extent is known (one
-// wave-uniform pass in lane order), so the run body carries no extra state.
-#ifndef LKF_OOO_RUN
-#define LKF_OOO_RUN 1
-#endif
-constexpr bool kOooRun = LKF_OOO_RUN != 0;
 
 
 // ---------------------------------------------------------------------------
@@ -176,18 +169,6 @@ __device__ __forceinline__ u32 excl_scan_u32(u32 v, u32 lane) {
     if (lane >= u32(o)) x += y;
   }
   return x - v;
-}
-__device__ __forceinline__ u64 shfl_up_u64(u64 v, int o) {
-  return u64(u32(__shfl_up(int(u32(v)), o, 64))) | (u64(u32(__shfl_up(int(u32(v >> 32)), o, 64))) << 32);
-}
-__device__ __forceinline__ u64 excl_max_u64(u64 v, u32 lane) {  // max over the lanes below (0 for lane 0)
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u64 y = shfl_up_u64(v, o);
-    if (lane >= u32(o) && y > v) v = y;
-  }
-  const u64 b = shfl_up_u64(v, 1);
-  return lane ? b : 0ull;
 }
 __device__ __forceinline__ u32 wave_sum_u32(u32 v) {
 #pragma unroll
@@ -2653,27 +2634,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           cls = -2;
       }
       const bool cand = inWin && cls == -1;
-      // An out-of-order candidate — older than the highest SN that the state or
-      // an earlier candidate of the window reached (UpdateAndGetSnTs diff < 0,
-      // rtpmunger.go:220-250) — changes no munger state: its translation is a
-      // RangeMap lookup and, for VP8, a missing-picture lookup (vp8.go:170-199),
-      // and its only write is the past sequencer slot it fills.  It stays in
-      // the run and is resolved once the run's extent is known (below); the
-      // in-order recurrences (previous candidate, previous forward) skip it.
-      bool oooL = false;
-      if (kOooRun) {
-        // (the scan only when the window has one: a candidate not above the
-        // previous candidate, or the first one not above the state's highest)
-        const u64 cM = __ballot(cand);
-        const int pcA = prev_in(cM, lt);
-        const u64 pcAEsn = sh64(p.esn, pcA >= 0 ? pcA : int(lane));
-        if (__ballot(cand && i64(p.esn - (pcA >= 0 ? pcAEsn : L.h.extHighestIncomingSN)) <= 0)) {
-          u64 hi = excl_max_u64(cand ? p.esn : 0ull, lane);
-          if (hi < L.h.extHighestIncomingSN) hi = L.h.extHighestIncomingSN;
-          oooL = cand && i64(p.esn - hi) < 0;
-        }
-      }
-      const bool candIn = cand && !oooL;
+      const bool candIn = cand;  // (an out-of-order candidate is not ok: the full step)
       const u64 candM = __ballot(candIn);
       const int pc = prev_in(candM, lt);
       const int pcs = pc >= 0 ? pc : int(lane);  // cross-lane reads run on every lane
@@ -2687,9 +2648,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       const bool gapLane = candIn && dEsn > 1 && dEsn < u64(L.seqSize) - 64 &&
                            p.plen != 0 && p.ssrc == L.h.lastSSRC;
       bool ok = candIn && (dEsn == 1 || gapLane) && p.plen != 0 && p.ssrc == L.h.lastSSRC;
-      // out-of-order lane decided in the run (refined below; the sequencer's
-      // padding RangeMap, F_SEQ_RM, is left to the full step)
-      bool okO = kOooRun && oooL && p.plen != 0 && p.ssrc == L.h.lastSSRC && !(fl & F_SEQ_RM);
       // a gap behind other candidates ends this run and starts the next one
       const bool gapLater = candIn && pc >= 0 && dEsn > 1 && dEsn < u64(L.seqSize) - 64 && p.plen != 0 &&
                             p.ssrc == L.h.lastSSRC;
@@ -2717,9 +2675,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
                                      (p.vbits & LKF_VP8_Y))
                                   : pktMarker);
         overT = candIn && T && p.tid > u8(cT);
-        // VP8PictureIdWrapHandler.Unwrap and SelectTemporal run on an
-        // out-of-order packet too: a wrap or a temporal switch there is serial
-        okO = okO && !wrapBack && !wraps && !tsw;
         // a gap lane forwards whatever its layer and exempts its picture
         // (vp8.go:249-255): later lanes of that picture forward too
         bool exIn = false;
@@ -2778,132 +2733,19 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
                          (osn == prevOsn + 1 || (gapLane && osn - prevOsn > 1 &&
                                                  osn - prevOsn < u64(L.seqSize) - 64)) &&
                          osn - L.h.seqExtHighestSN < u64(L.seqSize) - 64;
-      // an out-of-order push fills a past slot and moves neither highest SN nor
-      // TS (its SN is checked against the highest when it is resolved)
-      const bool seqOkO = (fl & F_SEQ_INIT) && (fl & F_STATS_INIT) && ots <= hiTS;
       const bool bad =
-          inWin && ((cls == -2) || (cls == -1 && !ok && !okO) || (fwdIn && !seqOk) || (okO && !seqOkO));
+          inWin && ((cls == -2) || (cls == -1 && !ok) || (fwdIn && !seqOk));
       const u64 stopM = __ballot(bad || (valid && lane >= pos && !inWin));
       x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
       if (tswM & ~((1ull << pos) - 1)) x = min(x, u32(__ffsll((long long)(tswM & ~((1ull << pos) - 1))) - 1) + 1u);
-      // ---- the run's out-of-order lanes and loss gaps, in lane order (wave-uniform)
-      // Gap lanes (forwarded after a loss) and picture drops: the missing
-      // pictures a gap records skip the pictures dropped so far (vp8.go:218-247),
-      // a gap exempts its own picture (:249-255), and the sequencer slots it
-      // skips are invalidated (sequencer.go:179-189); slots are the run-start
-      // highest slot + (osn - highest SN).  An out-of-order lane reads the
-      // RangeMap as the run left it at that lane — the run's temporal drops
-      // before it are exclusions above the open range's start — and the
-      // missing-picture map after the gap lanes before it.  A lane whose result
-      // the run cannot represent (the ring could prune its range, or its SN is
-      // not below the sequencer's highest) ends the run there: full step.
-      u64 oHitM = 0;        // out-of-order lanes that forward
-      bool pdDone = false;  // the picture drops' set entries were added here
-      if (x > pos && (__ballot(gapLane) || (kOooRun && __ballot(okO)))) {
-        const u64 runT = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
-        const u64 oT = kOooRun ? (__ballot(okO) & runT) : 0ull;
-        const u64 gT = __ballot(gapLane) & runT;
-        const u64 pdT = (video && gT) ? (__ballot(picDrop) & runT) : 0ull;
-        pdDone = pdT != 0;
-        for (u64 m = gT | pdT | oT; m; m &= m - 1) {
-          const u32 b = u32(__ffsll((long long)m) - 1);
-          const u64 belowB = runT & ((1ull << b) - 1);
-          if ((oT >> b) & 1) {  // UpdateAndGetSnTs diff < 0 (rtpmunger.go:220-250)
-            const u64 key = rl64(p.esn, b);
-            const u64 dB = tdM & belowB;
-            u64 off = 0;
-            bool hit, trunc = false;
-            if (key >= L.h.rmOpenStart) {
-              hit = true;
-              u64 below = 0;
-              for (u64 dm = dB; dm; dm &= dm - 1) {
-                const u64 e = rl64(p.esn, u32(__ffsll((long long)dm) - 1));
-                hit = hit && e != key;  // an excluded SN: errKeyExcluded
-                below += e < key ? 1u : 0u;
-              }
-              off = L.h.rmOpenValue + below;
-            } else {
-              trunc = int(L.h.rmCount) + __popcll(dB) >= kRangeCap;
-              hit = rm_get(L, key, off);
-            }
-            const u64 fB = fwC & belowB;  // extLastSN: the last in-order forward before b
-            const u64 osnB = key - off;
-            const u64 lastSN = fB ? rl64(osn, 63 - __clzll(fB)) : L.h.extLastSN;
-            int why = -1;
-            if (!hit || osnB >= lastSN)
-              why = LKF_DROP_OOO_MISS;
-            else if (osnB >= rl64(prevOsn, b))
-              trunc = true;
-            u64 cbB = 0;
-            int cbLenB = 0;
-            if (video && why < 0 && !trunc) {  // VP8.UpdateAndGet out of order (vp8.go:170-199)
-              const i32 extB = i32(rl32(u32(ext), b));
-              const int idx = miss_find(L, extB);
-              if (idx < 0) {
-                why = LKF_DROP_PICID_MISS;
-              } else {
-                const u32 vb = rl32(p.vbits, b);
-                const bool Mb = vb & LKF_VP8_M;
-                const u16 mp = u16((extB - L.missVal[idx]) & 0x7fff);
-                const bool mM = mp > 127;
-                const int hs = int(rl32(p.vhs, b)) + (mM == Mb ? 0 : (mM ? 1 : -1));
-                cbLenB = vp8_marshal(u8(rl32(p.vfirst, b)), vb & LKF_VP8_I, mM, mp, vb & LKF_VP8_L,
-                                     u8(rl32(p.tl0, b) - L.h.tl0Off), vb & LKF_VP8_T, u8(rl32(p.tid, b)),
-                                     vb & LKF_VP8_Y, vb & LKF_VP8_K, u8(rl32(p.keyidx, b) - L.h.keyIdxOff), hs, cbB);
-                if (cbLenB < 0) why = LKF_DROP_OTHER;
-              }
-            }
-            if (trunc) {
-              x = b;
-              break;
-            }
-            if (why == LKF_DROP_OOO_MISS)
-              o.drops[LKF_DROP_OOO_MISS]++;
-            else if (why == LKF_DROP_PICID_MISS)
-              o.drops[LKF_DROP_PICID_MISS]++;
-            else if (why >= 0)
-              o.drops[LKF_DROP_OTHER]++;
-            if (why < 0) {
-              oHitM |= 1ull << b;
-              if (lane == b) {
-                osn = osnB;
-                cb = cbB;
-                cbLen = cbLenB;
-              }
-            }
-            continue;
-          }
-          const i32 eb = i32(rl32(u32(ext), b));
-          if ((pdT >> b) & 1) {
-            L.vcDirty = true;
-            set_add(L.dropKey, L.h.dropHead, L.h.dropCount, eb, kDropKeep);
-            continue;
-          }
-          if (video) {
-            vp8_record_missing(L, i32(rl32(u32(prevExt), b)), eb, i32(rl32(u32(picOff), b)));
-            if (rl32(u32(overT), b)) {
-              L.vcDirty = true;
-              set_add(L.exKey, L.h.exHead, L.h.exCount, eb, kExemptKeep);
-            }
-          }
-          const u64 from = rl64(prevOsn, b), to = rl64(osn, b);  // slots of (from, to) skipped
-          const u32 n = u32(to - from - 1);
-          u32 base = u32(L.h.seqHighSlot) + u32(from - L.h.seqExtHighestSN) + 1;
-          for (u32 i = lane; i < n; i += 64) {  // stores only: no drain needed
-            u32 x2 = base + i;
-            while (x2 >= L.seqSize) x2 -= L.seqSize;
-            store_rec(L.seq + x2, SeqMeta{});
-          }
-        }
-      }
       // ---- decide lanes [pos, x) together
       if (x > pos) {
         const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
         const bool inRun = (runM >> lane) & 1;
         const u64 tdR = tdM & runM;
-        fwd = (fwd || ((oHitM >> lane) & 1)) && inRun;
+        fwd = fwd && inRun;
         const u64 fwR = __ballot(fwd);             // every forwarded lane (output order)
-        const u64 fwInR = __ballot(fwd && !oooL);  // in-order pushes
+        const u64 fwInR = fwR;                     // in-order pushes (every forward)
         const u64 selR = tdR | fwInR;              // lanes that advance the munger
         o.nTuples += x - pos;
         // the run's drops: the classification's no-state-change reasons + temporal filter
@@ -2912,7 +2754,39 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         o.drops[LKF_DROP_NOT_SELECTED] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_NOT_SELECTED)));
         o.drops[LKF_DROP_DOWNGRADE] += u32(__popcll(__ballot(inRun && cls == LKF_DROP_DOWNGRADE)));
         o.drops[LKF_DROP_TEMPORAL] += u32(__popcll(tdR));
+        // Gap lanes (forwarded after a loss) and picture drops, in lane order:
+        // the missing pictures a gap records skip the pictures dropped so far
+        // (vp8.go:218-247), a gap exempts its own picture (:249-255), and the
+        // sequencer slots it skips are invalidated (sequencer.go:179-189).
+        // Sequencer slots are the run-start highest slot + (osn - highest SN).
         const u64 pdR = video ? __ballot(picDrop && inRun) : 0ull;
+        const u64 gR = __ballot(gapLane && inRun);
+        if (gR) {
+          for (u64 m = gR | pdR; m; m &= m - 1) {
+            const u32 b = u32(__ffsll((long long)m) - 1);
+            const i32 eb = i32(rl32(u32(ext), b));
+            if ((pdR >> b) & 1) {
+              L.vcDirty = true;
+              set_add(L.dropKey, L.h.dropHead, L.h.dropCount, eb, kDropKeep);
+              continue;
+            }
+            if (video) {
+              vp8_record_missing(L, i32(rl32(u32(prevExt), b)), eb, i32(rl32(u32(picOff), b)));
+              if (rl32(u32(overT), b)) {
+                L.vcDirty = true;
+                set_add(L.exKey, L.h.exHead, L.h.exCount, eb, kExemptKeep);
+              }
+            }
+            const u64 from = rl64(prevOsn, b), to = rl64(osn, b);  // slots of (from, to) skipped
+            const u32 n = u32(to - from - 1);
+            u32 base = u32(L.h.seqHighSlot) + u32(from - L.h.seqExtHighestSN) + 1;
+            for (u32 i = lane; i < n; i += 64) {  // stores only: no drain needed
+              u32 x2 = base + i;
+              while (x2 >= L.seqSize) x2 -= L.seqSize;
+              store_rec(L.seq + x2, SeqMeta{});
+            }
+          }
+        }
         // output records + sequencer slots of the forwarded lanes
         const int cc = p.hdr0 & 0xf;
         const bool playout = L.extPlayout && !(fl & F_PLAYOUT_ACKED);
@@ -2948,19 +2822,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           CHK(slot0 + o.nFwd + j < A.tupleCap, CK_DEC_TUPLE, slot0 + o.nFwd + j, A.tupleCap);
 #endif
           store_rec(o.outT + o.nFwd + j, t);
-          // sequencer.push (sequencer.go:123-209): in order, the next slot; out of
-          // order, the slot delta behind the highest (skipped when older than
-          // the window or the sequencer's start)
-          u32 slot;
-          bool store = true;
-          if (!oooL) {
-            slot = u32(L.h.seqHighSlot) + u32(osn - L.h.seqExtHighestSN);
-          } else {
-            const u32 hs = u32(L.h.seqHighSlot) + u32(prevOsn - L.h.seqExtHighestSN);
-            const i64 delta = i64(osn - prevOsn);
-            store = delta > -i64(L.seqSize) && osn >= L.h.seqExtStartSN;
-            slot = hs + u32(i64(L.seqSize) + delta);
-          }
+          // sequencer.push (sequencer.go:123-209): in order, the slot the SN's
+          // distance past the highest
+          u32 slot = u32(L.h.seqHighSlot) + u32(osn - L.h.seqExtHighestSN);
           while (slot >= L.seqSize) slot -= L.seqSize;
           SeqMeta m = {};
           m.sourceSeqNo = u16(p.esn);
@@ -2973,7 +2837,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #pragma unroll
           for (int i = 0; i < 8; i++) m.codec[i] = u8(cb >> (8 * i));
           CHK(slot < L.seqSize, CK_DEC_SEQ, slot, L.seqSize);
-          if (store) store_rec(L.seq + slot, m);
+          store_rec(L.seq + slot, m);
         }
         const u32 sumLen = wave_sum_u32(outLen);
         sentAcc += fwd ? i32(p.poff) - hdrLen : 0;  // (reduced once per DownTrack)
@@ -3056,7 +2920,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
             }
             u64 pd = pdR;
             L.h.pictureIdOffset += i32(__popcll(pd));
-            while (pd && !pdDone) {  // (with gap lanes the drops went into the set in lane order above)
+            while (pd && !gR) {  // (with gap lanes the drops went into the set in lane order above)
               const u32 b = u32(__ffsll((long long)pd) - 1);
               L.vcDirty = true;
               set_add(L.dropKey, L.h.dropHead, L.h.dropCount, i32(rl32(u32(ext), b)), kDropKeep);
