@@ -638,6 +638,14 @@ __device__ __forceinline__ bool irm_get(const StreamHot &h, const RangeEntry *ri
   return false;
 }
 
+// the window's smoothed level (audiolevel.go:88-96; once per observe window: out of line)
+__device__ __noinline__ double level_smooth(double prev, u32 activeDuration, u8 loudest, u32 observeDuration,
+                                            double smoothFactor) {
+  const double activityWeight = 20.0 * log10(double(activeDuration) / double(observeDuration));
+  const double adjusted = double(loudest) - activityWeight;
+  const double linear = pow(10.0, adjusted * (-1.0 / 20));
+  return prev + (linear - prev) * smoothFactor;
+}
 // AudioLevel.Observe audiolevel.go:70-102
 __device__ __forceinline__ void level_observe(StreamHot &h, const DevStream &s, u8 level, u32 durationMs, i64 arrivalNs) {
   h.lastObservedNs = arrivalNs;
@@ -647,17 +655,28 @@ __device__ __forceinline__ void level_observe(StreamHot &h, const DevStream &s, 
     if (h.loudest > level) h.loudest = level;
   }
   if (h.observedDuration >= s.observeDuration) {
-    double smoothed = 0.0;
-    if (h.activeDuration >= s.minActiveDuration) {
-      const double activityWeight = 20.0 * log10(double(h.activeDuration) / double(s.observeDuration));
-      const double adjusted = double(h.loudest) - activityWeight;
-      const double linear = pow(10.0, adjusted * (-1.0 / 20));
-      smoothed = h.smoothedLevel + (linear - h.smoothedLevel) * s.smoothFactor;
-    }
-    h.smoothedLevel = smoothed;
+    h.smoothedLevel = h.activeDuration >= s.minActiveDuration
+                          ? level_smooth(h.smoothedLevel, h.activeDuration, h.loudest, s.observeDuration, s.smoothFactor)
+                          : 0.0;
     h.loudest = 127;
     h.activeDuration = 0;
     h.observedDuration = 0;
+  }
+}
+
+// processHeaderExtensions' audio level (buffer.go:573-596) for one datagram
+__device__ __forceinline__ void level_step(StreamHot &h, const DevStream &s, u32 pflags, u32 ts, u8 level,
+                                           i64 arrival) {
+  if (!(h.flags & S_LVL_TS_INIT)) {
+    h.flags |= S_LVL_TS_INIT;
+    h.latestTSForAudioLevel = ts;
+  }
+  if (pflags & IP_LEVEL) {
+    if (u32(ts - h.latestTSForAudioLevel) < (1u << 31)) {
+      const i64 dur = (i64(ts) - i64(h.latestTSForAudioLevel)) * 1000 / i64(s.clockRate);
+      if (dur > 0) level_observe(h, s, level, u32(dur), arrival);
+      h.latestTSForAudioLevel = ts;
+    }
   }
 }
 
@@ -970,19 +989,7 @@ __device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, c
       break;
     }
     // processHeaderExtensions (buffer.go:573-596)
-    if (s.levelExt) {
-      if (!(h.flags & S_LVL_TS_INIT)) {
-        h.flags |= S_LVL_TS_INIT;
-        h.latestTSForAudioLevel = p.ts;
-      }
-      if (p.flags & IP_LEVEL) {
-        if (u32(p.ts - h.latestTSForAudioLevel) < (1u << 31)) {
-          const i64 dur = (i64(p.ts) - i64(h.latestTSForAudioLevel)) * 1000 / i64(s.clockRate);
-          if (dur > 0) level_observe(h, s, p.level, u32(dur), arrival);
-          h.latestTSForAudioLevel = p.ts;
-        }
-      }
-    }
+    if (s.levelExt) level_step(h, s, p.flags, p.ts, p.level, arrival);
     // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241)
     const int hdrSize = p.hdrSize, payloadSize = p.payloadLen, paddingSize = p.paddingSize;
     WAResult rsn, rts;
@@ -1187,32 +1194,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
   // datagrams a run may take without looking at them twice (the state part
   // is checked per chunk)
-  const bool runStream = !s.levelExt;
+  // (audio streams run too: the audio level's own recurrence is folded over
+  // each run's datagrams in order, below)
+  const bool runStream = true;
   const bool hasDD = s.ddIdx != 0xffffffffu;
-  if (!runStream) {  // audio level observation: every datagram on lane 0,
-    // its descriptors staged in LDS 64 at a time by the whole wave
-    __shared__ IngParsed sP[64];
-    __shared__ lkf_raw_pkt sR[64];
-    __shared__ u32 sI[64];
-    for (u32 base = 0; base < nIdx; base += 64) {
-      const u32 k = base + lane;
-      if (k < nIdx) {
-        const u32 ic = useList ? lst[k] : pb + k;
-        sI[lane] = ic;
-        sP[lane] = q[ic];
-        sR[lane] = raws[ic];
-      }
-      __syncthreads();
-      if (lane == 0) {
-        const u32 m = min(64u, nIdx - base);
-        for (u32 x = 0; x < m; x++)
-          if (sR[x].stream == sid)
-            ing_step<1>(sh, sHist, ring, s, sP[x], sR[x], sI[x], flows, fwd, ingDD, raw, ddStates, ddStructs, err,
-                        bk, bkOn, gap);
-      }
-      __syncthreads();
-    }
-  }
   for (u32 j = 0; runStream && j < nIdx;) {
     const u32 k = j + lane;
     const bool in = k < nIdx;
@@ -1308,6 +1293,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     }
     const u64 pre0 = sh.snExtHighest;
     const u64 adjLast = extLast - sh.rmOpenValue;
+    if (s.levelExt) {  // AudioLevel.Observe over the run's datagrams, in order (wave-uniform; lane 0 stores it)
+      StreamHot lh;
+      lh.flags = sh.flags;
+      lh.latestTSForAudioLevel = sh.latestTSForAudioLevel;
+      lh.lastObservedNs = sh.lastObservedNs;
+      lh.observedDuration = sh.observedDuration;
+      lh.activeDuration = sh.activeDuration;
+      lh.loudest = sh.loudest;
+      lh.smoothedLevel = sh.smoothedLevel;
+      for (u32 x = 0; x < L; x++)
+        level_step(lh, s, __builtin_amdgcn_readlane(u32(p.flags), x), __builtin_amdgcn_readlane(p.ts, x),
+                   u8(__builtin_amdgcn_readlane(u32(p.level), x)), i64(rl_u64(u64(rp.arrival_ns), x)));
+      __syncthreads();
+      if (lane == 0) {
+        sh.flags |= lh.flags & S_LVL_TS_INIT;
+        sh.latestTSForAudioLevel = lh.latestTSForAudioLevel;
+        sh.lastObservedNs = lh.lastObservedNs;
+        sh.observedDuration = lh.observedDuration;
+        sh.activeDuration = lh.activeDuration;
+        sh.loudest = lh.loudest;
+        sh.smoothedLevel = lh.smoothedLevel;
+      }
+    }
     __syncthreads();
     if (lane == 0) {  // the run's gaps cleared, then its SNs set
       hist_clear_range<1>(sHist, pre0 + 1, extLast);
@@ -1493,9 +1501,32 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
       ls = f.loss_start;
       le = f.loss_end;
     }
-    const u32 m = min(64u, nIdx - base);
-    for (u32 x = 0; x < m; x++) {
-      if (__builtin_amdgcn_readlane(stm, x) != sid) continue;
+    // Only some datagrams can act on the queue: one whose SN may be in it
+    // (the chunk-start entries, or a range an earlier datagram of the chunk
+    // pushes — Remove), one with a loss range (Push), and the first one at or
+    // past nextDue (Pairs).  The others are skipped: Remove finds nothing and
+    // Pairs sends and purges nothing, as in the reference.
+    const bool mine = k < nIdx && stm == sid;
+    const bool upd = mine && (ipf & IP_OK);
+    const bool lossL = upd && (ff & LKF_FLOW_HAS_LOSS);
+    bool hit = false;
+    if (upd) {
+      for (u32 i = 0; i < count; i++) hit = hit || sSn[i] == u32(u16(sn));
+    }
+    for (u64 lm = __ballot(lossL); lm; lm &= lm - 1) {  // SNs the chunk's earlier datagrams push
+      const u32 a = u32(__ffsll((long long)lm) - 1);
+      const u64 s0 = rl_u64(ls, a), e0 = rl_u64(le, a);
+      hit = hit || (lane > a && u64(u16(u16(sn) - u16(s0))) < e0 - s0);
+    }
+    const u64 evM = __ballot(upd && (hit || lossL));
+    const u64 mineM = __ballot(mine);
+    for (u32 pos = 0; pos < 64;) {
+      const u64 after = ~((1ull << pos) - 1);
+      const u64 dueM = count ? (__ballot(mine && arr >= nextDue) & mineM) : 0ull;
+      const u64 nx = (evM | dueM) & after;
+      if (!nx) break;
+      const u32 x = u32(__ffsll((long long)nx) - 1);
+      pos = x + 1;
       const i64 now = i64(rl_u64(u64(arr), x));
       const u32 icx = __builtin_amdgcn_readlane(ic, x);
       if (__builtin_amdgcn_readlane(ipf, x) & IP_OK) {  // updateStreamState ran
