@@ -1393,7 +1393,12 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   __shared__ u32 sSn[kNackSlots];
   __shared__ u32 sTries[kNackSlots];
   __shared__ u32 sPurge[kNackSlots];
-  __shared__ lkf_nack_pair sPairs[kNackCap];
+  // the stream's RTCP NACKs of this ingest, staged and written in blocks: one
+  // reservation in the batch's pair buffer per block instead of one atomic per
+  // NACK (every stream's NACKs on one counter serialised the kernel)
+  constexpr u32 kPairStage = 512, kRecStage = 64;
+  __shared__ lkf_nack_pair sStage[kPairStage];
+  __shared__ u32 sRecIc[kRecStage], sRecInfo[kRecStage], sRecOff[kRecStage];
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
   if (!s.nack || s.closed) return;
@@ -1484,6 +1489,26 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
     return i64(rl_u64(u64(m), 0));
   };
   i64 nextDue = count ? dueMin() : INT64_MAX;
+  u32 stageN = 0, recN = 0;  // wave-uniform
+  auto flush = [&]() {
+    __syncthreads();  // (lane 0's staged pairs and records)
+    if (stageN) {
+      u32 off = 0;
+      if (lane == 0) off = atomicAdd(pairCnt, stageN);
+      off = __builtin_amdgcn_readfirstlane(off);
+      if (off + stageN > pairCap) {
+        if (lane == 0) atomicOr(err, 8u);  // pair buffer capacity: these RTCP NACKs are not recorded
+      } else {
+        for (u32 i = lane; i < stageN; i += 64) pairs[off + i] = sStage[i];
+        if (lane < recN) {
+          info[sRecIc[lane]] = sRecInfo[lane];
+          pairOff[sRecIc[lane]] = off + sRecOff[lane];
+        }
+      }
+    }
+    __syncthreads();
+    stageN = recN = 0;
+  };
   for (u32 base = 0; base < nIdx; base += 64) {
     const u32 k = base + lane;
     u32 ic = 0, stm = 0xffffffffu, ipf = 0, sn = 0, ff = 0;
@@ -1610,6 +1635,8 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
         }
       __syncthreads();
       const u32 numNacked = u32(__popcll(s0m) + __popcll(s1m));
+      if (numNacked && (stageN + u32(kNackCap) > kPairStage || recN == kRecStage)) flush();
+      lkf_nack_pair *const sPairs = sStage + stageN;
       u32 np = 0;
       if (lane == 0 && numNacked) {  // pair packing (NackQueue.Pairs), in queue order
         u32 baseSN = base16;
@@ -1631,22 +1658,18 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
             }
           }
         if (active) sPairs[np++] = cur;
-        u32 off = 0;
         if (np) {
-          off = atomicAdd(pairCnt, np);
-          if (off + np > pairCap) {
-            atomicOr(err, 8u);  // pair buffer capacity: the RTCP NACK is not recorded
-            np = 0;
-          } else {
-            for (u32 i = 0; i < np; i++) pairs[off + i] = sPairs[i];
-          }
-        }
-        if (np) {
-          info[icx] = np | (numNacked << 16);
-          pairOff[icx] = off;
+          sRecIc[recN] = icx;
+          sRecInfo[recN] = np | (numNacked << 16);
+          sRecOff[recN] = stageN;
         }
       }
-      if (numNacked && __builtin_amdgcn_readfirstlane(np)) nacked += numNacked;  // UpdateNack only with a packet
+      np = __builtin_amdgcn_readfirstlane(np);
+      if (np) {
+        stageN += np;
+        recN++;
+      }
+      if (numNacked && np) nacked += numNacked;  // UpdateNack only with a packet
       // purge (NackQueue.Remove of every entry at MaxTries, in order)
       const u32 nPurge = nr0 + u32(__popcll(r1));
       for (u32 i = 0; i < nPurge; i++) removeSn(sPurge[i]);
@@ -1654,6 +1677,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
       nextDue = count ? dueMin() : INT64_MAX;
     }
   }
+  flush();
   for (u32 i = lane; i < u32(kNackSlots); i += 64) {
     g->last[i] = sLast[i];
     g->sn[i] = u16(sSn[i]);

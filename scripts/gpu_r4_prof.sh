@@ -25,7 +25,8 @@ for a in "${LIST[@]}"; do
     rc=$?; echo "prof$i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/prof$i.log; exit $rc; }
     f=$(find $O/prof$i -name '*kernel_stats.csv' | head -1)
     [ -n "$f" ] && cp "$f" $O/kernel_stats$i.csv && head -20 $O/kernel_stats$i.csv | cut -d, -f1-5
-    find $O/prof$i -name '*kernel_trace.csv' -size +20M -delete
+    f=$(find $O/prof$i -name "*kernel_trace.csv" -size -20M | head -1); [ -n "$f" ] && cp "$f" $O/kernel_trace$i.csv
+    find $O/prof$i -name "*kernel_trace.csv" -delete
   fi
   i=$((i+1))
 done
