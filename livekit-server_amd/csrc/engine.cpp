@@ -161,8 +161,10 @@ struct lkf_engine {
   uint32_t twccTCap = 0, twccListCap = 0, nTwccT = 0;
   bool anyTwcc = false, twccDirty = false;
   hipStream_t sideS = nullptr;  // an ingest's NACK queues, beside the rest of the ingest and the run
-  hipEvent_t sideFork = nullptr, sideDone = nullptr;
-  bool sidePending = false;     // the next ingest waits for sideDone
+  hipEvent_t sideFork = nullptr, sideDone[2] = {nullptr, nullptr};
+  bool sidePending[2] = {false, false};  // an ingest waits for the NACK queues of the one two back
+  hipEvent_t bktDone[2] = {nullptr, nullptr};
+  bool bktPending[2] = {false, false};   // ... and for its bucket copies
   hipStream_t cur = nullptr;    // caller's stream of the last lkf_run
   hipEvent_t inEv = nullptr;    // caller-stream work before a run
   hipEvent_t bktEv = nullptr;   // an ingest's bucket decisions (the sender stream copies after it)
@@ -391,6 +393,18 @@ struct lkf_engine {
   uint64_t *dPos = nullptr, *dIPartA = nullptr, *dIPartB = nullptr, *dITotal = nullptr;
   uint32_t *dITBegin = nullptr, *dITEnd = nullptr, *dITRuns = nullptr, *dIErr = nullptr;
   uint32_t *dIList = nullptr, *dIListCnt = nullptr;  // per-stream datagram lists (k_ing_lists)
+  // The ingest scratch the NACK queues (side stream) and the bucket copies
+  // (sender stream) read after the ingest chain has moved on: two sets,
+  // alternating per ingest, so an ingest waits only for the side work of the
+  // ingest two back.  The d* pointers above and below name the last ingest's set.
+  struct IngSet {
+    IngParsed *parsed = nullptr;
+    lkf_flow *flows = nullptr;
+    uint32_t *fwd = nullptr, *tBegin = nullptr, *tEnd = nullptr, *list = nullptr, *listCnt = nullptr;
+    uint32_t *nackInfo = nullptr, *nackPairOff = nullptr, *nackPairCnt = nullptr;
+    lkf_nack_pair *nackPairs = nullptr;
+  } ing[2];
+  int ingPar = 0;
   // NACK queues (allocated with the first stream that has one) and the last
   // ingest's RTCP NACKs (per datagram result + bump-allocated pairs)
   NackState *dNack = nullptr;
@@ -740,11 +754,19 @@ static int flush_topology(lkf_engine *e) {
       const lkf_cfg &c = e->cfg;
       HIPCHK(dalloc(&e->dNack, e->maxStreams), "alloc nack queues");
       HIPCHK(hipMemset(e->dNack, 0, size_t(e->maxStreams) * sizeof(NackState)), "nack queues reset");
-      HIPCHK(dalloc(&e->dNackInfo, c.max_batch_pkts), "alloc nack info");
-      HIPCHK(dalloc(&e->dNackPairOff, c.max_batch_pkts), "alloc nack pair offsets");
-      HIPCHK(dalloc(&e->dNackPairCnt, 1), "alloc nack pair count");
       e->nackPairCap = uint32_t(std::min<uint64_t>(uint64_t(c.max_batch_pkts) * 8 + 4096, 1u << 30));
-      HIPCHK(dalloc(&e->dNackPairs, e->nackPairCap), "alloc nack pairs");
+      for (auto &g : e->ing) {
+        HIPCHK(dalloc(&g.nackInfo, c.max_batch_pkts), "alloc nack info");
+        HIPCHK(dalloc(&g.nackPairOff, c.max_batch_pkts), "alloc nack pair offsets");
+        HIPCHK(dalloc(&g.nackPairCnt, 1), "alloc nack pair count");
+        HIPCHK(dalloc(&g.nackPairs, e->nackPairCap), "alloc nack pairs");
+        HIPCHK(hipMemset(g.nackInfo, 0, size_t(c.max_batch_pkts) * sizeof(uint32_t)), "nack info reset");
+        HIPCHK(hipMemset(g.nackPairCnt, 0, sizeof(uint32_t)), "nack count reset");
+      }
+      e->dNackInfo = e->ing[e->ingPar].nackInfo;
+      e->dNackPairOff = e->ing[e->ingPar].nackPairOff;
+      e->dNackPairCnt = e->ing[e->ingPar].nackPairCnt;
+      e->dNackPairs = e->ing[e->ingPar].nackPairs;
       HIPCHK(dalloc(&e->dNackRecPos, c.max_batch_pkts), "alloc nack positions");
       HIPCHK(dalloc(&e->dNackPairPos, c.max_batch_pkts), "alloc nack pair positions");
       HIPCHK(dalloc(&e->dNackTot, 2), "alloc nack totals");
@@ -753,8 +775,6 @@ static int flush_topology(lkf_engine *e) {
       HIPCHK(dalloc(&e->dNackPartB, npart), "alloc nack scan partials");
       HIPCHK(dalloc(&e->dNackOut, c.max_batch_pkts), "alloc nack records");
       HIPCHK(dalloc(&e->dNackPairsOut, e->nackPairCap), "alloc nack pairs out");
-      HIPCHK(hipMemset(e->dNackInfo, 0, size_t(c.max_batch_pkts) * sizeof(uint32_t)), "nack info reset");
-      HIPCHK(hipMemset(e->dNackPairCnt, 0, sizeof(uint32_t)), "nack count reset");
     }
     if (e->dNack) {  // each new queue: empty, the stream's initial RTT (0: defaultRtt)
       for (size_t i = 0; i < k; i++) {
@@ -831,7 +851,10 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
   A(hipEventCreateWithFlags(&e->bktEv, hipEventDisableTiming));
   A(hipEventCreateWithFlags(&e->sideFork, hipEventDisableTiming));
-  A(hipEventCreateWithFlags(&e->sideDone, hipEventDisableTiming));
+  for (int i = 0; i < 2; i++) {
+    A(hipEventCreateWithFlags(&e->sideDone[i], hipEventDisableTiming));
+    A(hipEventCreateWithFlags(&e->bktDone[i], hipEventDisableTiming));
+  }
   e->cur = e->own;
   A(dalloc(&e->dTracks, c.max_tracks));
   A(dalloc(&e->dHot, c.max_downtracks));
@@ -898,21 +921,30 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dHist, size_t(e->maxStreams) * kHistWords));
   A(dalloc(&e->dRxGap, size_t(e->maxStreams) * kGapWords));
   A(dalloc(&e->dStreamRings, size_t(e->maxStreams) * kRangeCap));
-  A(dalloc(&e->dParsed, c.max_batch_pkts));
-  A(dalloc(&e->dFlows, c.max_batch_pkts));
+  for (auto &g : e->ing) {
+    A(dalloc(&g.parsed, c.max_batch_pkts));
+    A(dalloc(&g.flows, c.max_batch_pkts));
+    A(dalloc(&g.fwd, c.max_batch_pkts));
+    A(dalloc(&g.tBegin, c.max_tracks));
+    A(dalloc(&g.tEnd, c.max_tracks));
+    A(dalloc(&g.list, 3 * size_t(c.max_batch_pkts) + 64));
+    A(dalloc(&g.listCnt, 3 * size_t(c.max_tracks)));
+  }
+  e->dParsed = e->ing[0].parsed;
+  e->dFlows = e->ing[0].flows;
   A(dalloc(&e->dTwcc, c.max_batch_pkts));
-  A(dalloc(&e->dFwdFlag, c.max_batch_pkts));
+  e->dFwdFlag = e->ing[0].fwd;
   A(dalloc(&e->dPos, c.max_batch_pkts));
   const size_t ipart = (size_t(c.max_batch_pkts) + 1023) / 1024 + 1;
   A(dalloc(&e->dIPartA, ipart));
   A(dalloc(&e->dIPartB, ipart));
   A(dalloc(&e->dITotal, 2));
-  A(dalloc(&e->dITBegin, c.max_tracks));
-  A(dalloc(&e->dITEnd, c.max_tracks));
+  e->dITBegin = e->ing[0].tBegin;
+  e->dITEnd = e->ing[0].tEnd;
   A(dalloc(&e->dITRuns, c.max_tracks));
   A(dalloc(&e->dIErr, 4));
-  A(dalloc(&e->dIList, 3 * size_t(c.max_batch_pkts) + 64));
-  A(dalloc(&e->dIListCnt, 3 * size_t(c.max_tracks)));
+  e->dIList = e->ing[0].list;
+  e->dIListCnt = e->ing[0].listCnt;
   if (ok) {
     A(hipMemset(e->dSeq, 0, size_t(c.max_downtracks) * c.seq_size * sizeof(SeqMeta)));
     // Every persistent table starts zeroed: hipMalloc hands back memory an
@@ -997,11 +1029,11 @@ void lkf_destroy(lkf_engine *e) {
     if (p) (void)dfree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
                   e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
-                  e->dStreams, e->dStreamHot, e->dHist, e->dRxGap, e->dStreamRings, e->dParsed, e->dFlows, e->dFwdFlag,
+                  e->dStreams, e->dStreamHot, e->dHist, e->dRxGap, e->dStreamRings,
                   e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktRing, e->dBktStream, e->dBktSn,
-                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITBegin, e->dITEnd, e->dITRuns, e->dIErr, e->dIList, e->dIListCnt,
+                  e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITRuns, e->dIErr,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
-                  e->dSpkCounts, e->dNack, e->dNackInfo, e->dNackPairOff, e->dNackPairCnt, e->dNackPairs,
+                  e->dSpkCounts, e->dNack,
                   e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut, e->dNackPartA,
                   e->dNackPartB,
                   e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups, e->dSeqDD, e->dSeqDDIdx,
@@ -1051,7 +1083,16 @@ void lkf_destroy(lkf_engine *e) {
   if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->bktEv) (void)hipEventDestroy(e->bktEv);
   if (e->sideFork) (void)hipEventDestroy(e->sideFork);
-  if (e->sideDone) (void)hipEventDestroy(e->sideDone);
+  for (int i = 0; i < 2; i++) {
+    if (e->sideDone[i]) (void)hipEventDestroy(e->sideDone[i]);
+    if (e->bktDone[i]) (void)hipEventDestroy(e->bktDone[i]);
+  }
+  for (auto &g : e->ing)
+    for (void *p : {static_cast<void *>(g.parsed), static_cast<void *>(g.flows), static_cast<void *>(g.fwd),
+                    static_cast<void *>(g.tBegin), static_cast<void *>(g.tEnd), static_cast<void *>(g.list),
+                    static_cast<void *>(g.listCnt), static_cast<void *>(g.nackInfo), static_cast<void *>(g.nackPairOff),
+                    static_cast<void *>(g.nackPairCnt), static_cast<void *>(g.nackPairs)})
+      if (p) (void)dfree(p);
   if (e->sideS) (void)hipStreamDestroy(e->sideS);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
   if (e->sendS) (void)hipStreamDestroy(e->sendS);
@@ -3372,6 +3413,23 @@ int32_t lkf_add_stream(lkf_engine *e, const lkf_stream_params *p) {
 
 // Enqueued on the decide stream ahead of the batch's decide stage (no host
 // sync): the ExtPacket count stays on the device (k_track_ranges reads it).
+// the d* names of the ingest scratch point at set `par` (the last ingest's)
+static void IngSetSelect(lkf_engine *e, int par) {
+  const lkf_engine::IngSet &g = e->ing[par];
+  e->ingPar = par;
+  e->dParsed = g.parsed;
+  e->dFlows = g.flows;
+  e->dFwdFlag = g.fwd;
+  e->dITBegin = g.tBegin;
+  e->dITEnd = g.tEnd;
+  e->dIList = g.list;
+  e->dIListCnt = g.listCnt;
+  e->dNackInfo = g.nackInfo;
+  e->dNackPairOff = g.nackPairOff;
+  e->dNackPairCnt = g.nackPairCnt;
+  e->dNackPairs = g.nackPairs;
+}
+
 static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, uint32_t n, const uint8_t *dRaw,
                          uint64_t rawLen) {
   const uint32_t nt = uint32_t(e->tracks.size());
@@ -3379,10 +3437,14 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   // the batch's GPU span (lkf_timing_window total) starts before its ingest
   HIPCHK(hipEventRecord(e->ring[e->nRuns % lkf_engine::kRing][0], s), "event");
   e->ingestStarted = true;
-  // the previous ingest's NACK queues (side stream) read this ingest's scratch
-  // (parsed datagrams, flows, lists, track ranges) and update the stream state
-  if (e->sidePending) HIPCHK(hipStreamWaitEvent(s, e->sideDone, 0), "wait nack queues");
-  e->sidePending = false;
+  // this ingest's scratch set: the ingest two back used it, and its NACK
+  // queues (side stream) and bucket copies (sender stream) read it
+  const int par = e->ingPar ^ 1;
+  IngSetSelect(e, par);
+  if (e->sidePending[par]) HIPCHK(hipStreamWaitEvent(s, e->sideDone[par], 0), "wait nack queues");
+  e->sidePending[par] = false;
+  if (e->bktPending[par]) HIPCHK(hipStreamWaitEvent(s, e->bktDone[par], 0), "wait bucket copies");
+  e->bktPending[par] = false;
   IngestLaunch a;
   a.raws = dRaws;
   a.n = n;
@@ -3450,14 +3512,16 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.outDD = dd ? x.dDDIn : nullptr;
   {
     bool side = false;
-    HIPCHK(launch_ingest(s, a, e->sideS, e->sideFork, e->sideDone, &side), "ingest");
-    e->sidePending = side;
+    HIPCHK(launch_ingest(s, a, e->sideS, e->sideFork, e->sideDone[par], &side), "ingest");
+    e->sidePending[par] = side;
   }
   if (a.bucket && n) {  // the bucket copies, off the forwarding path: the sender stream (the
                         // batch context counts as done only after it, like the sender statistics)
     HIPCHK(hipEventRecord(e->bktEv, s), "event");
     HIPCHK(hipStreamWaitEvent(e->sendS, e->bktEv, 0), "wait ingest (bucket store)");
     HIPCHK(launch_bucket_store(e->sendS, bl), "bucket store");
+    HIPCHK(hipEventRecord(e->bktDone[par], e->sendS), "event");
+    e->bktPending[par] = true;
     e->bktStorePending = true;
   }
   HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 8), "ingest error fold");
@@ -3588,6 +3652,11 @@ int lkf_stream_stats_get(lkf_engine *e, int32_t sid, lkf_stream_stats *o) {
   o->bytes_padding = h.bytesPadding;
   o->frames = h.frames;
   o->nacks = h.nacks;
+  if (e->dNack) {  // (the NACK queues keep the count: see NackState)
+    uint64_t nq = 0;
+    D2H(&nq, &e->dNack[sid].nacks, sizeof(nq), "stream nacks");
+    o->nacks += nq;
+  }
   o->first_time_ns = h.firstTime;
   o->highest_time_ns = h.highestTime;
   o->last_transit = h.lastTransit;

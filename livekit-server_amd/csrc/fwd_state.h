@@ -366,7 +366,8 @@ struct alignas(16) NackState {
   uint8_t tries[kNackSlots];
   uint32_t count;             // entries
   uint32_t rtt;               // ms (SetRTT)
-  uint8_t pad[8];
+  uint64_t nacks;             // rtpStats.nacks (UpdateNack): kept here, not in StreamHot, because the
+                              // queues run beside the next ingest's stream kernel, which rewrites StreamHot
 };
 static_assert(sizeof(NackState) % 16 == 0, "NackState must be 16-B granular");
 

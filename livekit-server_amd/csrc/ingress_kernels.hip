@@ -1685,7 +1685,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   }
   if (lane == 0) {
     g->count = count;
-    if (nacked) hot[sid].nacks += nacked;
+    if (nacked) g->nacks += nacked;
   }
 }
 
