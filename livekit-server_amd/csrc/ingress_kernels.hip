@@ -379,7 +379,7 @@ __device__ __forceinline__ bool vp9_parse(BP p, int len, IngParsed &q) {
   return true;
 }
 
-constexpr int kParseT = 256;      // k_ing_parse block
+constexpr int kParseT = 64;       // k_ing_parse block (8 KB of LDS: fits beside the decide waves)
 constexpr int kParseStage = 128;  // bytes of each datagram staged in LDS
 constexpr int kStageW = kParseStage / 4 + 1;  // dwords per thread: a dword-aligned window (odd stride: no bank conflicts)
 __global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n,
