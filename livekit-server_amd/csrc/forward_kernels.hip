@@ -3031,10 +3031,7 @@ constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 desc
 // (two-byte extension profile) = 343
 constexpr int PRE_MAX_DD = 352;
 
-#ifndef LKF_EMIT_U
-#define LKF_EMIT_U 4
-#endif
-constexpr int EMIT_U = LKF_EMIT_U;  // 16-B chunks per lane in flight per copy iteration
+constexpr int EMIT_U = 4;  // 16-B chunks per lane in flight per copy iteration (6 and 8 measured no faster, r4_ab_runs.txt)
 
 
 struct EmitArgs {
