@@ -880,17 +880,19 @@ __device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u
 // The stream's RTX bucket inside the stream kernel (mediatransportutil
 // bucket.AddPacketWithSequenceNumber as buffer.go:471-481 calls it; oracle
 // bucket_oracle.h): the logical state (head, step) in LDS, the slot tags in
-// HBM, and this ingest's writer of each slot (owner words in HBM tagged with
-// the ingest epoch) so a slot taken again later in the batch cancels the
-// earlier datagram's copy.  (An LDS owner map cost 8 KB per stream wave and
-// with it the occupancy that puts every stream of a batch in flight at once.)
+// HBM, and this ingest's writer of each slot (sOwn in LDS for rings of up to
+// kBktLds slots, else the global owner words tagged with the ingest epoch) so
+// a slot taken again later in the batch cancels the earlier datagram's copy.
+constexpr int kBktLds = 2048;
 constexpr u32 kNoOwner = 0xFFFFFFFFu;
 struct BktCtx {
   BucketState *b;  // LDS
   u32 *tag;        // the stream's slot tags
-  u64 *owner;      // the stream's owner words
+  u64 *owner;      // the stream's owner words (rings above kBktLds)
   u64 *store;      // per datagram of the batch
+  u32 *sOwn;       // LDS owner map (rings up to kBktLds)
   u64 ep;          // ingest epoch << 32
+  bool lds;
 };
 __device__ __forceinline__ int bkt_wrap(int x, int M) {
   x %= M;
@@ -898,9 +900,15 @@ __device__ __forceinline__ int bkt_wrap(int x, int M) {
 }
 // the slot's previous writer in this ingest is not stored; ic takes it (kNoOwner: invalidated)
 __device__ __forceinline__ void bkt_supersede(const BktCtx &k, int sl, u32 ic) {
-  const u64 o = k.owner[sl];
-  if ((o & 0xFFFFFFFF00000000ull) == k.ep) k.store[u32(o)] = 0;
-  k.owner[sl] = ic == kNoOwner ? 0 : (k.ep | ic);
+  if (k.lds) {
+    const u32 o = k.sOwn[sl];
+    if (o != kNoOwner) k.store[o] = 0;
+    k.sOwn[sl] = ic;
+  } else {
+    const u64 o = k.owner[sl];
+    if ((o & 0xFFFFFFFF00000000ull) == k.ep) k.store[u32(o)] = 0;
+    k.owner[sl] = ic == kNoOwner ? 0 : (k.ep | ic);
+  }
 }
 // AddPacketWithSequenceNumber for one datagram (one lane): push (the skipped
 // slots invalidated, the packet at the new head) or set (an older SN inside
@@ -1161,6 +1169,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   __shared__ u64 sHist[kHistWords];
   __shared__ StreamHot sh;
   __shared__ BucketState sB;
+  __shared__ u32 sOwn[kBktLds];  // (LDS is otherwise small: 4 waves per SIMD either way)
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
@@ -1185,7 +1194,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     bk.tag = bka.tag + sB.base;
     bk.owner = bka.owner + sB.base;
     bk.store = bka.store;
+    bk.sOwn = sOwn;
     bk.ep = u64(bka.epoch) << 32;
+    bk.lds = M <= kBktLds;
+    if (bk.lds)
+      for (int i = int(lane); i < M; i += 64) sOwn[i] = kNoOwner;
   }
   __syncthreads();
   RangeEntry *ring = rings + size_t(sid) * kRangeCap;
@@ -1198,7 +1211,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   // each run's datagrams in order, below)
   const bool runStream = true;
   const bool hasDD = s.ddIdx != 0xffffffffu;
-  for (u32 j = 0; runStream && j < nIdx;) {
+  for (u32 j = 0; runStream && j < nIdx; j += 64) {
+    // a chunk of 64 datagrams stays in registers while runs and serial steps
+    // take its lanes in order from `pos`
     const u32 k = j + lane;
     const bool in = k < nIdx;
     u32 ic = 0;
@@ -1209,56 +1224,59 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
       p = q[ic];
       rp = raws[ic];
     }
+    const u32 m = min(64u, nIdx - j);
+    for (u32 pos = 0; pos < m;) {
     const u32 need = S_INIT | S_SN_INIT | S_TS_INIT;
     const bool stateOk = runStream && (sh.flags & need) == need && sh.rmOpenStart <= sh.snExtHighest + 1;
     const u16 prevSn = u16(__shfl_up(u32(p.sn), 1, 64));
     const u32 prevTs = u32(__shfl_up(p.ts, 1, 64));
-    const u16 gs = u16(p.sn - (lane == 0 ? sh.snHighest : prevSn));
-    const u32 gt = p.ts - (lane == 0 ? sh.tsHighest : prevTs);
-    const bool ok = stateOk && in && rp.stream == sid && (p.flags & IP_OK) && p.payloadLen > 0 &&
+    const u16 gs = u16(p.sn - (lane == pos ? sh.snHighest : prevSn));
+    const u32 gt = p.ts - (lane == pos ? sh.tsHighest : prevTs);
+    const bool ok = lane >= pos && stateOk && in && rp.stream == sid && (p.flags & IP_OK) && p.payloadLen > 0 &&
                     !(p.flags & IP_VP8_BAD) && !(hasDD && p.ddLen) && gs >= 1 && gs <= 0x8000u &&
                     gt <= 0x80000000u && (!bkOn || rp.len <= 1498u);
     const u64 snScan = wave_incl_scan_u64(ok ? u64(gs) : 0, lane);  // only read below the run end
-    u64 bad = ~__ballot(ok);
+    u64 bad = ~__ballot(ok) & ~((1ull << pos) - 1);
     // the history update below is exact while the run spans < 4096 SNs
-    bad |= __ballot(snScan >= u64(kHistWords) * 64);
+    bad |= __ballot(lane >= pos && snScan >= u64(kHistWords) * 64);
     // the bucket: every datagram of the run is a push; the first one's step
     // from the bucket head d0 (its adjusted SN against the head), the others'
     // their SN gaps; S = the run's pushes so far, slots distinct while S <= M
     u64 bS = 0;
     u32 d0 = 0;
     if (bkOn) {
-      const u32 gs0 = u32(__shfl(u32(gs), 0, 64));
+      const u32 gs0 = __builtin_amdgcn_readlane(u32(gs), pos);
       d0 = u32(u16(u16(sh.snExtHighest + gs0 - sh.rmOpenValue) - sB.head));
-      if (!sB.init || d0 < 1 || d0 > 0x8000u) bad |= 1ull;
+      if (!sB.init || d0 < 1 || d0 > 0x8000u) bad |= 1ull << pos;
       bS = snScan - gs0 + d0;
-      bad |= __ballot(bS > u64(M));
+      bad |= __ballot(lane >= pos && bS > u64(M));
     }
-    const u32 L = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;
-    if (L == 0) {
-      if (lane == 0 && rp.stream == sid)
+    const u32 end = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;  // the run is [pos, end)
+    if (end == pos) {  // the datagram at pos through the serial Buffer.calc step
+      if (lane == pos && rp.stream == sid)
         ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err, bk, bkOn, gap);
       __syncthreads();
-      j++;
+      pos++;
       continue;
     }
-    const bool run = lane < L;
+    const u32 L = end - pos;
+    const bool run = lane >= pos && lane < end;
     const u64 tsScan = wave_incl_scan_u64(run ? u64(gt) : 0, lane);
     const u64 ext = sh.snExtHighest + snScan, extTs = sh.tsExtHighest + tsScan;
     const u64 pktSize = u64(p.hdrSize + p.payloadLen + p.paddingSize);
     const u64 bytesRun = wave_sum_u64(run ? pktSize : 0), hdrRun = wave_sum_u64(run ? u64(p.hdrSize) : 0);
     const u32 framesRun = u32(__popcll(__ballot(run && (p.flags & IP_MARKER))));
-    const u64 extLast = __shfl(ext, int(L - 1), 64), extTsLast = __shfl(extTs, int(L - 1), 64);
-    const u16 snLast = u16(__shfl(u32(p.sn), int(L - 1), 64));
-    const u32 tsLast = u32(__shfl(p.ts, int(L - 1), 64));
-    const u64 bSLast = __shfl(bS, int(L - 1), 64);
+    const u64 extLast = __shfl(ext, int(end - 1), 64), extTsLast = __shfl(extTs, int(end - 1), 64);
+    const u16 snLast = u16(__shfl(u32(p.sn), int(end - 1), 64));
+    const u32 tsLast = u32(__shfl(p.ts, int(end - 1), 64));
+    const u64 bSLast = __shfl(bS, int(end - 1), 64);
     // RTPStatsReceiver timing: highestTime from the run's last lane that
     // starts a timestamp (the TS never decreases inside a run); the jitter
     // filter over the run's new timestamps, in order (a float64 recurrence:
     // transits in parallel, the fold serial and wave-uniform)
-    const u64 newTs = __ballot(run && p.ts != (lane == 0 ? sh.tsHighest : prevTs));
+    const u64 newTs = __ballot(run && p.ts != (lane == pos ? sh.tsHighest : prevTs));
     const u64 prevExtTs = __shfl_up(extTs, 1, 64);
-    const u64 newJ = __ballot(run && extTs != (lane == 0 ? sh.lastJitterExtTs : prevExtTs));
+    const u64 newJ = __ballot(run && extTs != (lane == pos ? sh.lastJitterExtTs : prevExtTs));
     const u64 transit = rx_transit(sh, s.clockRate, extTs, rp.arrival_ns);
     if (run) rx_gap(gap, u64(gs));
     if (run) {
@@ -1276,7 +1294,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
       fwd[ic] = 1;
       if (ingDD) ingDD[ic] = IngDD{};
       if (bkOn) {  // the run's pushes: this lane's skipped slots invalidated, then its own
-        const u32 dk = lane == 0 ? d0 : u32(gs);
+        const u32 dk = lane == pos ? d0 : u32(gs);
         const int step0 = int(sB.step);
         const int first = int(bS - dk);  // pushes before this lane's gap
         for (u32 i = 0; i + 1 < dk; i++) {
@@ -1302,7 +1320,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
       lh.activeDuration = sh.activeDuration;
       lh.loudest = sh.loudest;
       lh.smoothedLevel = sh.smoothedLevel;
-      for (u32 x = 0; x < L; x++)
+      for (u32 x = pos; x < end; x++)
         level_step(lh, s, __builtin_amdgcn_readlane(u32(p.flags), x), __builtin_amdgcn_readlane(p.ts, x),
                    u8(__builtin_amdgcn_readlane(u32(p.level), x)), i64(rl_u64(u64(rp.arrival_ns), x)));
       __syncthreads();
@@ -1359,7 +1377,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     __syncthreads();
     if (run) atomicOr(reinterpret_cast<unsigned long long *>(&sHist[(ext >> 6) & (kHistWords - 1)]), 1ull << (ext & 63));
     __syncthreads();
-    j += L;
+    pos = end;
+    }
   }
   hg[lane] = sHist[lane];
   reinterpret_cast<u32 *>(hot + sid)[lane] = reinterpret_cast<const u32 *>(&sh)[lane];
