@@ -819,6 +819,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || hip_device < 0 || hip_device >= ndev) return nullptr;
   if (cfg->seq_size > 65535) return nullptr;
+  if (cfg->max_out_bytes >= (uint64_t(1) << 32)) return nullptr;  // (packet-major offsets are 32-bit)
   auto *e = new lkf_engine();
   e->dev = hip_device;
   e->cfg = *cfg;

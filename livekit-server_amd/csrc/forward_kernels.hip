@@ -3137,7 +3137,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       CHK(t.pkt < A.npkts, CK_EMIT_PKT, t.pkt, A.npkts);
       const PktV p = load_pkt(A.pkts + t.pkt);
       const DevDT dt = A.dts[d];
-      outOff = u64(t.relOff) | (u64(t.pad1) << 32);  // (absolute: the packet-major layout)
+      outOff = t.relOff;  // (absolute: the packet-major layout)
       CHK(r < A.outCap, CK_EMIT_OUT, r, A.outCap);
       CHK(outOff + t.outLen <= A.outByteCap, CK_EMIT_BYTES, outOff + t.outLen, A.outByteCap);
       CHK(u64(p.arenaOff) + p.poff + p.plen <= A.arenaLen, CK_EMIT_ARENA, u64(p.arenaOff) + p.poff + p.plen,
@@ -4341,9 +4341,7 @@ __global__ void __launch_bounds__(64) k_pm_group(PmLaunch A) {
         const u32 al = (u32(t->outLen) + 15u) & ~15u;
         const uint2 v = acc[p];
         if (ASSIGN) {
-          const u64 off = A.pktByteBase[p] + v.x;
-          t->relOff = u32(off);  // (low and high halves of the arena offset)
-          t->pad1 = u32(off >> 32);
+          t->relOff = u32(A.pktByteBase[p] + v.x);
           const u64 pos = A.pktPos[p] + v.y;
           if (pos < A.outCap) A.pmMap[pos] = make_uint4(u32(base + j), u32(rec0 + j), d, 0u);
         }

@@ -145,8 +145,7 @@ static_assert(sizeof(SeqMeta) == 32, "SeqMeta must be 32 B");
 struct alignas(16) Tuple {
   uint64_t extSN, extTS;
   uint32_t pkt;
-  uint32_t relOff;    // byte offset in the DownTrack's output region (decide); after the packet-major
-                      // layout pass, the low half of the arena offset (high half in pad1)
+  uint32_t relOff;    // byte offset in the DownTrack's output region
   uint16_t outLen;
   uint8_t flags;      // lkf_out flags | T_DD | T_PLAYOUT | T_CODEC
   int8_t layer;
