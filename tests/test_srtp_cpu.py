@@ -31,7 +31,7 @@ def _run(o, workload, tr, nb, check, gcm_every=0):
             assert o.api["protect"](h, send) == 0
             rec, arena = pkg.drain_arrays(o.api, h)
             prot = pkg.drain_protected(o.api, h)
-            assert len(prot) == 2 * len(arena)
+            assert len(prot) == len(arena) + 16 * len(rec)
             for i in range(len(rec)) if check == "all" else range(0, len(rec), check):
                 r = rec[i]
                 plain = bytes(arena[r["out_off"]:r["out_off"] + r["out_len"]])
