@@ -212,10 +212,7 @@ typedef struct lkf_pkt_dd {
 typedef struct lkf_out {
   uint64_t ext_sn;      /* tp.rtp.extSequenceNumber (munged) */
   uint64_t ext_ts;      /* tp.rtp.extTimestamp (munged) */
-  uint64_t out_off;     /* offset of the wire packet in the output arena.  The arena is laid out
-                         * packet-major: by input packet (batch order), one packet's copies for its
-                         * DownTracks contiguous in record order, each 16-B aligned; records
-                         * themselves are in send order (track, DownTrack handle, packet) */
+  uint64_t out_off;     /* offset of the wire packet in the output arena */
   uint32_t dt;          /* DownTrack handle */
   uint32_t pkt;         /* index of the incoming packet in the batch */
   uint16_t out_len;     /* wire packet length (RTP header + payload) */
@@ -820,9 +817,9 @@ int lkf_set_downtrack_transport(lkf_engine *e, int32_t dt, int32_t transport);
 /* Protects the last lkf_run's output (asynchronously, after its emit stage):
  * every packet gets the abs-send-time of `send_time_ns` (unix ns, pion/rtp
  * NewAbsSendTimeExtension) in its abs-send-time element, and the packets of a
- * bound DownTrack are SRTP-protected.  A record's packet is at 2 * out_off
- * of the protected arena (twice the output arena), out_len (+ 10 with an
- * AES-CM transport, + 16 with GCM) bytes long.  Valid until the run after next is enqueued, like the output. */
+ * bound DownTrack are SRTP-protected.  Record i's packet is at
+ * out_off + 16 * i of the protected arena, out_len (+ 10 with an AES-CM
+ * transport, + 16 with GCM) bytes long.  Valid until the run after next is enqueued, like the output. */
 int lkf_protect(lkf_engine *e, int64_t send_time_ns);
 int lkf_output_protected_device(lkf_engine *e, const uint8_t **d_arena, uint64_t *arena_len);
 int lkf_drain_protected(lkf_engine *e, uint8_t *arena, uint64_t cap, uint64_t *arena_len);

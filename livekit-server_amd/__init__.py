@@ -108,7 +108,7 @@ def transport_params(master_key, master_salt, profile=abi.LKF_SRTP_AES128_CM_HMA
 
 
 def drain_protected(api, h):
-    """The last protected run's arena (a record's packet at 2 * out_off)."""
+    """The last protected run's arena (record i's packet at out_off + 16 * i)."""
     n = C.c_uint64()
     rc = api["drain_protected"](h, None, 0, C.byref(n))
     if rc not in (0, -28):

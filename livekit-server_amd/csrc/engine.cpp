@@ -250,16 +250,6 @@ struct lkf_engine {
   uint32_t *dWaveTrack = nullptr;
   uint32_t *dEvOff = nullptr;
   uint32_t *dPerm = nullptr;  // output position -> DownTrack (track-major)
-  // packet-major output layout (kernels.h PmLaunch): position groups, per-track
-  // group counts, the per (group, packet) accumulators and per-packet bases
-  uint4 *dPmGroups = nullptr;
-  uint32_t nPmGroups = 0, pmGroupsCap = 0, pmMaxG = 0;
-  uint32_t *dTrackGroups = nullptr;
-  uint2 *dPmAcc = nullptr;
-  uint32_t *dPktCnt = nullptr;
-  uint64_t *dPktBytes = nullptr, *dPktPos = nullptr, *dPktByteBase = nullptr, *dPmPartA = nullptr,
-           *dPmPartB = nullptr, *dPmTot = nullptr;
-  uint4 *dPmMap = nullptr;
   size_t schedCap = 0;
   DevEvent *dEvents = nullptr;
   uint64_t evCap = 0;
@@ -819,7 +809,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || hip_device < 0 || hip_device >= ndev) return nullptr;
   if (cfg->seq_size > 65535) return nullptr;
-  if (cfg->max_out_bytes >= (uint64_t(1) << 32)) return nullptr;  // (packet-major offsets are 32-bit)
   auto *e = new lkf_engine();
   e->dev = hip_device;
   e->cfg = *cfg;
@@ -887,15 +876,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dCum, kStatsWords));
   A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
-  A(dalloc(&e->dTrackGroups, c.max_tracks));
-  A(dalloc(&e->dPktCnt, c.max_batch_pkts));
-  A(dalloc(&e->dPktBytes, c.max_batch_pkts));
-  A(dalloc(&e->dPktPos, c.max_batch_pkts));
-  A(dalloc(&e->dPktByteBase, c.max_batch_pkts));
-  A(dalloc(&e->dPmPartA, size_t(c.max_batch_pkts) / 1024 + 2));
-  A(dalloc(&e->dPmPartB, size_t(c.max_batch_pkts) / 1024 + 2));
-  A(dalloc(&e->dPmTot, 2));
-  A(dalloc(&e->dPmMap, c.max_out_pkts + 64));
   const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
   for (auto &x : e->ctx) {
     A(dalloc(&x.dTBegin, c.max_tracks));
@@ -1048,8 +1028,7 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->dAllocOut)})
     if (p) (void)dfree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
-                  e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm, e->dTrackGroups, e->dPktCnt, e->dPktBytes,
-                  e->dPktPos, e->dPktByteBase, e->dPmPartA, e->dPmPartB, e->dPmTot, e->dPmMap, e->dPmGroups, e->dPmAcc,
+                  e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
                   e->dStreams, e->dStreamHot, e->dHist, e->dRxGap, e->dStreamRings,
                   e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktRing, e->dBktStream, e->dBktSn,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITRuns, e->dIErr,
@@ -1401,34 +1380,6 @@ static int rebuild_sched(lkf_engine *e) {
     std::stable_sort(perm.begin(), perm.end(),
                      [&](uint32_t a, uint32_t b) { return e->dtp[a].track < e->dtp[b].track; });
     if (nd) HIPCHK(hipMemcpy(e->dPerm, perm.data(), nd * sizeof(uint32_t), hipMemcpyHostToDevice), "perm copy");
-    // packet-major layout groups: up to 64 consecutive positions of one track
-    std::vector<uint4> groups;
-    std::vector<uint32_t> tg(e->cfg.max_tracks, 0);
-    uint32_t maxG = 0;
-    for (uint32_t q = 0; q < nd;) {
-      const uint32_t t = uint32_t(e->dtp[perm[q]].track);
-      uint32_t r = q;
-      while (r < nd && uint32_t(e->dtp[perm[r]].track) == t && r - q < 64) r++;
-      groups.push_back(make_uint4(t, q, r - q, tg[t]++));
-      maxG = std::max(maxG, tg[t]);
-      q = r;
-    }
-    if (groups.size() > e->pmGroupsCap) {
-      if (e->dPmGroups) HIPCHK(dfree(e->dPmGroups), "free layout groups");
-      e->pmGroupsCap = uint32_t(groups.size()) + 1024;
-      HIPCHK(dalloc(&e->dPmGroups, e->pmGroupsCap), "alloc layout groups");
-    }
-    if (maxG > e->pmMaxG) {
-      if (e->dPmAcc) HIPCHK(dfree(e->dPmAcc), "free layout accumulators");
-      e->pmMaxG = maxG;
-      HIPCHK(dalloc(&e->dPmAcc, size_t(maxG) * e->cfg.max_batch_pkts), "alloc layout accumulators");
-    }
-    e->nPmGroups = uint32_t(groups.size());
-    if (!groups.empty())
-      HIPCHK(hipMemcpy(e->dPmGroups, groups.data(), groups.size() * sizeof(uint4), hipMemcpyHostToDevice),
-             "layout groups copy");
-    HIPCHK(hipMemcpy(e->dTrackGroups, tg.data(), tg.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
-           "track groups copy");
   }
   if (nl) {
     HIPCHK(hipMemcpy(e->dSched, e->sched.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice), "sched copy");
@@ -1808,36 +1759,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   hipStream_t es = e->emitS;
   HIPCHK(hipStreamWaitEvent(es, x.decided, 0), "wait decided");
   HIPCHK(hipEventRecord(rg[3], es), "event");
-  {  // the packet-major layout of this batch's wire packets (emit stream, before emit)
-    PmLaunch pm;
-    pm.groups = e->dPmGroups;
-    pm.ngroups = e->nPmGroups;
-    pm.trackGroups = e->dTrackGroups;
-    pm.perm = e->dPerm;
-    pm.slotBase = x.dSlotBase;
-    pm.recBase = x.dRecBase;
-    pm.fwdCnt = x.dFwdCnt;
-    pm.tuples = x.dTuples;
-    pm.pkts = e->curPkts;
-    pm.tBegin = x.dTBegin;
-    pm.tEnd = x.dTEnd;
-    pm.ntracks = nt;
-    pm.npkts = e->curN;
-    pm.pktStride = e->cfg.max_batch_pkts;
-    pm.acc = e->dPmAcc;
-    pm.pktCnt = e->dPktCnt;
-    pm.pktBytes = e->dPktBytes;
-    pm.pktPos = e->dPktPos;
-    pm.pktByteBase = e->dPktByteBase;
-    pm.partA = e->dPmPartA;
-    pm.partB = e->dPmPartB;
-    pm.tot = e->dPmTot;
-    pm.pmMap = e->dPmMap;
-    pm.outCap = e->cfg.max_out_pkts;
-    if (nd) HIPCHK(launch_pm_layout(es, pm), "packet-major layout");
-  }
   EmitLaunch m;
-  m.pmMap = e->dPmMap;
   m.perm = e->dPerm;
   m.recBase = x.dRecBase;
   m.byteBase = x.dByteBase;
@@ -2139,7 +2061,7 @@ int lkf_protect(lkf_engine *e, int64_t send_time_ns) {
   if (rc) return rc;
   BatchCtx &x = e->ctx[e->lastCtx];
   if (!x.dProt)
-    HIPCHK(dalloc(&x.dProt, 2 * e->cfg.max_out_bytes + 64), "alloc protected arena");
+    HIPCHK(dalloc(&x.dProt, e->cfg.max_out_bytes + 16 * uint64_t(e->cfg.max_out_pkts)), "alloc protected arena");
   SrtpProtectArgs a;
   a.tab = e->dAesTab;
   a.totals = x.dTot + 2;
@@ -2175,7 +2097,7 @@ int lkf_output_protected_device(lkf_engine *e, const uint8_t **d_arena, uint64_t
   uint64_t tot[4];
   D2H(tot, x.dTot, sizeof(tot), "tot copy");
   if (d_arena) *d_arena = x.dProt;
-  if (arena_len) *arena_len = 2 * tot[3];  // record i's protected packet at 2 * out_off
+  if (arena_len) *arena_len = tot[3] + 16 * tot[2];
   return LKF_OK;
 }
 

@@ -3035,7 +3035,6 @@ constexpr int EMIT_U = 4;  // 16-B chunks per lane in flight per copy iteration 
 
 
 struct EmitArgs {
-  const uint4 *pmMap;   // packet-major position -> (tuple slot, record, DownTrack)
   const u32 *perm;      // output position -> DownTrack (track-major order)
   const u64 *recBase;   // [position] exclusive scan of forwarded counts
   const u64 *byteBase;  // [position] exclusive scan of output bytes
@@ -3125,19 +3124,31 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
     const u64 r0 = g * EMIT_G;
     const u32 nrec = u32(min(u64(EMIT_G), total - r0));
     // ---- prefix phase: lane = record
+    CHK(g + 1 < A.gCap, CK_EMIT_GROUP, g + 1, A.gCap);
+    const u32 pLo = A.gFirst[g];
+    const u32 pHi = (g + 1 < ngroups) ? A.gFirst[g + 1] + 1 : A.ndts;
     u64 outOff = 0;
     if (lane < nrec) {
-      // the record at packet-major position r0 + lane (k_pm_group<true>)
-      const uint4 pm = A.pmMap[r0 + lane];
-      const u64 slot = pm.x, r = pm.y;
-      const u32 d = pm.z;
+      const u64 r = r0 + lane;
+      // position owning record r: last p in [pLo, pHi) with recBase[p] <= r
+      u32 lo = pLo, hi = pHi;
+      while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (A.recBase[mid] <= r)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      CHK(lo < A.ndts, CK_EMIT_POS, lo, A.ndts);
+      const u32 d = A.perm[lo];
       CHK(d < A.maxDts, CK_EMIT_DT, d, A.maxDts);
-      CHK(slot < A.tupleCap, CK_EMIT_TUPLE, slot, A.tupleCap);
-      const Tuple t = A.tuples[slot];
+      CHK(A.slotBase[d] + (r - A.recBase[lo]) < A.tupleCap, CK_EMIT_TUPLE, A.slotBase[d] + (r - A.recBase[lo]),
+          A.tupleCap);
+      const Tuple t = A.tuples[A.slotBase[d] + (r - A.recBase[lo])];
       CHK(t.pkt < A.npkts, CK_EMIT_PKT, t.pkt, A.npkts);
       const PktV p = load_pkt(A.pkts + t.pkt);
       const DevDT dt = A.dts[d];
-      outOff = t.relOff;  // (absolute: the packet-major layout)
+      outOff = A.byteBase[lo] + t.relOff;
       CHK(r < A.outCap, CK_EMIT_OUT, r, A.outCap);
       CHK(outOff + t.outLen <= A.outByteCap, CK_EMIT_BYTES, outOff + t.outLen, A.outByteCap);
       CHK(u64(p.arenaOff) + p.poff + p.plen <= A.arenaLen, CK_EMIT_ARENA, u64(p.arenaOff) + p.poff + p.plen,
@@ -3163,7 +3174,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       // pion's TWCC HeaderExtensionInterceptor: the transport's next sequence
       // number in send order (this record's ordinal in its DownTrack's output
       // after the DownTrack's base)
-      const u16 tcc = dt.extTcc ? u16(A.twccBase[d] + u32(slot - A.slotBase[d])) : u16(0);
+      const u16 tcc = dt.extTcc ? u16(A.twccBase[d] + u32(r - A.recBase[lo])) : u16(0);
       w[0] = u8((p.hdr0 & 0xe0) | (hasExt ? 0x10 : 0) | cc);  // V, P copied; X per new extensions
       w[1] = u8(((t.flags & LKF_OUT_MARKER) ? 0x80 : 0) | (dt.pt & 0x7f));
       const u16 sn = u16(t.extSN);
@@ -4303,87 +4314,8 @@ hipError_t launch_twcc_stamp(hipStream_t s, const DevDT *dts, uint32_t *ctrD, ui
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// Packet-major output layout.  Output positions (DownTracks, track-major) are
-// cut into groups of up to 64 consecutive positions of one track; a wave per
-// group walks its DownTracks in position order over their decided tuples (a
-// DownTrack forwards a packet at most once, so the lanes of one DownTrack's
-// chunk touch distinct packets).
-//   k_pm_group<false>  per (group, packet): the aligned bytes and copies
-//   k_pm_scan          per packet: exclusive over its track's groups; totals
-//   scan               per packet: byte and position bases (batch order)
-//   k_pm_group<true>   per tuple: its offset (packet base + group prefix + the
-//                      DownTracks before it in the group) into Tuple.relOff,
-//                      and its packet-major position -> (tuple, record, DT)
-// ---------------------------------------------------------------------------
-template <bool ASSIGN>
-__global__ void __launch_bounds__(64) k_pm_group(PmLaunch A) {
-  const u32 k = blockIdx.x, lane = threadIdx.x;
-  if (k >= A.ngroups) return;
-  const uint4 g = A.groups[k];
-  const u32 T = g.x, q0 = g.y, nq = g.z, gl = g.w;
-  uint2 *const acc = A.acc + size_t(gl) * A.pktStride;
-  if (!ASSIGN) {
-    const u32 pb = A.tBegin[T], pe = A.tEnd[T];
-    for (u32 p = pb + lane; p < pe; p += 64) acc[p] = make_uint2(0, 0);
-    __threadfence_block();
-  }
-  for (u32 q = q0; q < q0 + nq; q++) {
-    const u32 d = A.perm[q];
-    const u32 n = A.fwdCnt[d];
-    const u64 base = A.slotBase[d];
-    const u64 rec0 = ASSIGN ? A.recBase[q] : 0;
-    for (u32 c = 0; c < n; c += 64) {
-      const u32 j = c + lane;
-      if (j < n) {
-        Tuple *const t = A.tuples + base + j;
-        const u32 p = t->pkt;
-        const u32 al = (u32(t->outLen) + 15u) & ~15u;
-        const uint2 v = acc[p];
-        if (ASSIGN) {
-          t->relOff = u32(A.pktByteBase[p] + v.x);
-          const u64 pos = A.pktPos[p] + v.y;
-          if (pos < A.outCap) A.pmMap[pos] = make_uint4(u32(base + j), u32(rec0 + j), d, 0u);
-        }
-        acc[p] = make_uint2(v.x + al, v.y + 1u);
-      }
-    }
-    __threadfence_block();  // (the next DownTrack's lanes may take the same packets)
-  }
-}
-__global__ void k_pm_scan(PmLaunch A) {
-  const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= A.npkts) return;
-  u32 cnt = 0;
-  u64 bytes = 0;
-  const u32 T = A.pkts[p].track;
-  if (T < A.ntracks && p >= A.tBegin[T] && p < A.tEnd[T]) {  // (entries past an ingest's count are stale)
-    const u32 ng = A.trackGroups[T];
-    for (u32 gl = 0; gl < ng; gl++) {
-      uint2 *const e = A.acc + size_t(gl) * A.pktStride + p;
-      const uint2 v = *e;
-      *e = make_uint2(u32(bytes), cnt);
-      bytes += v.x;
-      cnt += v.y;
-    }
-  }
-  A.pktCnt[p] = cnt;
-  A.pktBytes[p] = bytes;
-}
-hipError_t launch_pm_layout(hipStream_t s, const PmLaunch &a) {
-  if (a.ngroups == 0 || a.npkts == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pm_group<false>, dim3(a.ngroups), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(k_pm_scan, dim3((a.npkts + 255) / 256), dim3(256), 0, s, a);
-  hipError_t r = launch_scan(s, 1, nullptr, nullptr, nullptr, a.pktCnt, a.pktBytes, a.npkts, a.partA, a.partB, a.pktPos,
-                             a.pktByteBase, a.tot, a.tot + 1, nullptr);
-  if (r != hipSuccess) return r;
-  hipLaunchKernelGGL(k_pm_group<true>, dim3(a.ngroups), dim3(64), 0, s, a);
-  return hipGetLastError();
-}
-
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   EmitArgs A;
-  A.pmMap = a.pmMap;
   A.perm = a.perm;
   A.recBase = a.recBase;
   A.byteBase = a.byteBase;

@@ -49,31 +49,7 @@ struct DecideLaunch {
   uint32_t maxDts, maxTracks, npkts, nev;
 };
 
-// Packet-major output layout (k_pm_*): a batch's wire packets are laid out
-// by input packet (batch order), the copies of one packet for its DownTracks
-// contiguous in output-position order, so emit reads each payload once and
-// writes one contiguous sweep.  Groups of up to 64 consecutive output
-// positions of one track; acc holds [group index within the track][packet].
-struct PmLaunch {
-  const uint4 *groups;       // (track, first position, positions, group index within the track)
-  uint32_t ngroups;
-  const uint32_t *trackGroups;  // groups per track
-  const uint32_t *perm;
-  const uint64_t *slotBase, *recBase;
-  const uint32_t *fwdCnt;
-  Tuple *tuples;
-  const lkf_pkt *pkts;
-  const uint32_t *tBegin, *tEnd;
-  uint32_t ntracks, npkts, pktStride;  // npkts: the batch's launch bound; acc row stride
-  uint2 *acc;
-  uint32_t *pktCnt;
-  uint64_t *pktBytes, *pktPos, *pktByteBase, *partA, *partB, *tot;
-  uint4 *pmMap;  // [packet-major position] (tuple slot, record, DownTrack, 0)
-  uint64_t outCap;
-};
-hipError_t launch_pm_layout(hipStream_t s, const PmLaunch &a);
 struct EmitLaunch {
-  const uint4 *pmMap;    // packet-major position -> (tuple slot, record, DownTrack)
   const uint32_t *perm;  // output position -> DownTrack
   const uint64_t *recBase, *byteBase, *slotBase, *totals;  // recBase/byteBase by position
   const uint32_t *gFirst;  // [group] position owning record 64*group (k_scan_down mode 1)

@@ -435,7 +435,7 @@ __device__ bool protect_record(const SrtpProtectArgs &A, const AesLds &tb, u64 i
   const lkf_out r = A.out[i];
   const u32 len = r.out_len;
   const uint4 *src = reinterpret_cast<const uint4 *>(A.arena + r.out_off);
-  uint4 *dst = reinterpret_cast<uint4 *>(A.prot + 2 * r.out_off);  // (room for the tag: 2 x the 16-B aligned length)
+  uint4 *dst = reinterpret_cast<uint4 *>(A.prot + r.out_off + 16 * i);
   const u8 *sb = A.arena + r.out_off;
   const DevDT dt = A.dts[r.dt];
   const uint4 c0v = src[0];

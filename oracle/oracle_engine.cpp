@@ -536,34 +536,25 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
       e->dts[d]->packetsSent++;
       e->dts[d]->bytesSent += o.sent;
     }
-  // Output records: by track, then DownTrack handle, then packet (the send
-  // order).  Wire packets, 16-B aligned, are laid out packet-major: by input
-  // packet (batch order), a packet's copies in record order.  (An
-  // engine-defined batch layout: the reference hands each packet to its
-  // DownTrack's pacer directly.)
+  // Output order: by track, then DownTrack handle, then packet; wire packets
+  // 16-B aligned.  (An engine-defined batch layout: the reference hands each
+  // packet to its DownTrack's pacer directly.)
   e->outRecs.clear();
   e->outArena.clear();
-  std::vector<const std::vector<u8> *> bytes;
+  u64 off = 0;
   for (auto &tds : trackDts)
     for (u32 d : tds)
       for (auto &o : e->dts[d]->outs) {
         if (e->dts[d]->p.ext_transport_cc)  // send order = output order
           twcc_put(o.bytes.data(), o.bytes.size(), e->dts[d]->p.ext_transport_cc, twcc_next(e, *e->dts[d]));
-        e->outRecs.push_back(o.rec);
-        bytes.push_back(&o.bytes);
+        lkf_out r = o.rec;
+        r.out_off = off;
+        e->outRecs.push_back(r);
+        e->outArena.insert(e->outArena.end(), o.bytes.begin(), o.bytes.end());
+        u64 al = (o.bytes.size() + 15) & ~u64(15);
+        e->outArena.resize(off + al, 0);
+        off += al;
       }
-  std::vector<size_t> order(e->outRecs.size());
-  for (size_t i = 0; i < order.size(); i++) order[i] = i;
-  std::stable_sort(order.begin(), order.end(),
-                   [&](size_t a, size_t b) { return e->outRecs[a].pkt < e->outRecs[b].pkt; });
-  u64 off = 0;
-  for (size_t i : order) {
-    e->outRecs[i].out_off = off;
-    off += (bytes[i]->size() + 15) & ~u64(15);
-  }
-  e->outArena.assign(off, 0);
-  for (size_t i = 0; i < e->outRecs.size(); i++)
-    std::memcpy(e->outArena.data() + e->outRecs[i].out_off, bytes[i]->data(), bytes[i]->size());
   e->stats.arena_bytes = off;
   return LKF_OK;
 }
@@ -606,7 +597,7 @@ int orc_set_downtrack_transport(orc_engine *e, int32_t dt, int32_t t) {
 int orc_protect(orc_engine *e, int64_t send_time_ns) {
   const u32 abs = orc_srtp::abs_send_time(send_time_ns);
   const size_t n = e->outRecs.size();
-  e->protArena.assign(2 * e->outArena.size(), 0);  // record i's protected packet at 2 * out_off
+  e->protArena.assign(e->outArena.size() + 16 * n, 0);
   for (size_t i = 0; i < n; i++) {  // records in send order (a DownTrack's packets in order)
     const lkf_out &r = e->outRecs[i];
     ODT &d = *e->dts[r.dt];
@@ -616,7 +607,7 @@ int orc_protect(orc_engine *e, int64_t send_time_ns) {
       pkt = e->transportsGcm[size_t(d.transport)]
                 ? orc_srtp::protect_gcm(*e->transportsGcm[size_t(d.transport)], d.srtp, pkt)
                 : orc_srtp::protect(e->transports[size_t(d.transport)], d.srtp, pkt);
-    std::memcpy(e->protArena.data() + 2 * r.out_off, pkt.data(), pkt.size());
+    std::memcpy(e->protArena.data() + r.out_off + 16 * i, pkt.data(), pkt.size());
   }
   return LKF_OK;
 }

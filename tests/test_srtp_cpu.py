@@ -36,7 +36,7 @@ def _run(o, workload, tr, nb, check, gcm_every=0):
                 r = rec[i]
                 plain = bytes(arena[r["out_off"]:r["out_off"] + r["out_len"]])
                 exp = ck.expect(r, plain, send)
-                off = 2 * int(r["out_off"])
+                off = int(r["out_off"]) + 16 * i
                 got = bytes(prot[off:off + len(exp)])
                 assert got == exp, (b, i, int(r["dt"]), int(r["ext_sn"]))
                 if int(r["dt"]) in tmap:

@@ -30,7 +30,7 @@ def _compare(pkg, eng, o, oh, b, bound):
     n_prot = 0
     for i in range(len(orec)):
         r = orec[i]
-        off = 2 * int(r["out_off"])
+        off = int(r["out_off"]) + 16 * i
         d = int(r["dt"])
         ln = int(r["out_len"]) + ((16 if bound[d][3] == srtp_lib.GCM else 10) if d in bound else 0)
         if not np.array_equal(gp[off:off + ln], op[off:off + ln]):

@@ -87,7 +87,7 @@ def test_transport_cc_matches_oracle(pkg, workload, abi, cfg):
             gp, op = pkg.drain_protected(eng.api, eng.h), pkg.drain_protected(o.api, oh)
             assert len(gp) == len(op)
             for i in range(len(orec)):  # every protected packet (the gaps between them are unspecified)
-                off = 2 * int(orec["out_off"][i])
+                off = int(orec["out_off"][i]) + 16 * i
                 ln = int(orec["out_len"][i]) + (10 if int(orec["dt"][i]) in tg else 0)
                 assert np.array_equal(gp[off:off + ln], op[off:off + ln]), (b, i)
             tv = _tcc_values(tr, orec, oar)
