@@ -387,23 +387,36 @@ __global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__rest
                                                       u32 nstreams, IngParsed *__restrict__ out, u32 *__restrict__ twcc,
                                                       u32 *__restrict__ err) {
   __shared__ u32 sStage[kParseT * kStageW];
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const lkf_raw_pkt rp = raws[i];
-  // the datagram's first bytes into LDS: dword loads of the dword-aligned
-  // window (global loads need only dword alignment; a dword holding a byte of
-  // the datagram lies in that byte's page), all in flight together
-  u32 *const st = sStage + threadIdx.x * kStageW;
+  const u32 lane = threadIdx.x;
+  const u32 i = blockIdx.x * blockDim.x + lane;
+  lkf_raw_pkt rp = {};
+  if (i < n) rp = raws[i];
+  // the block's datagrams' first bytes into LDS, one datagram per load
+  // instruction (lane k loads dword k of its dword-aligned window: one or two
+  // cache lines per instruction, where a thread-per-datagram load touched 64),
+  // 16 datagrams' loads in flight.  Global loads need only dword alignment; a
+  // dword holding a byte of the datagram lies in that byte's page.
   const int sl = int(rp.len) < kParseStage ? int(rp.len) : kParseStage;
   {
-    const u32 *g = reinterpret_cast<const u32 *>(raw + (rp.off & ~u64(3)));
-    const int nw = (sl + int(rp.off & 3) + 3) >> 2;
-    u32 w[kStageW];
+    const u32 wbase = rp.off & ~3u;
+    const u32 nw = (u32(sl) + (rp.off & 3) + 3) >> 2;  // 0 for a lane past the batch
 #pragma unroll
-    for (int k = 0; k < kStageW; k++) w[k] = k < nw ? g[k] : 0u;
+    for (int j0 = 0; j0 < kParseT; j0 += 16) {
+      u32 w[16];
 #pragma unroll
-    for (int k = 0; k < kStageW; k++) st[k] = w[k];
+      for (int jj = 0; jj < 16; jj++) {
+        const u32 b = __builtin_amdgcn_readlane(wbase, j0 + jj);
+        const u32 c = __builtin_amdgcn_readlane(nw, j0 + jj);
+        w[jj] = lane < c ? reinterpret_cast<const u32 *>(raw + b)[lane] : 0u;
+      }
+#pragma unroll
+      for (int jj = 0; jj < 16; jj++)
+        if (lane < u32(kStageW)) sStage[(j0 + jj) * kStageW + lane] = w[jj];
+    }
   }
+  __syncthreads();
+  if (i >= n) return;
+  u32 *const st = sStage + lane * kStageW;
   IngParsed q = {};
   twcc[i] = 0;
   if (rp.stream >= nstreams) {
@@ -414,7 +427,7 @@ __global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__rest
   }
   const DevStream s = streams[rp.stream];
   q.track = s.track;
-  // (each thread reads only its own staged window: no barrier needed)
+  // (each thread reads its own datagram's staged window)
   const StagedBytes b{(LdsBytes)(reinterpret_cast<const u8 *>(st)) + (rp.off & 3), raw + rp.off, sl};
   int levelOff = -1, twOff = -1, twLen = 0;
   if (rtp_parse(b, int(rp.len), s.levelExt, s.ddExt, q, levelOff, s.twccExt, &twOff, &twLen)) {
@@ -2123,34 +2136,71 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
 // store per datagram; k_bkt_store then copies each stored datagram whose slot
 // no later datagram of the batch took, its SN field set to the adjusted SN.
 // ---------------------------------------------------------------------------
-// one wave per datagram at a time, grid-stride; 16-B copies when the source is
-// 16-B aligned (the ring slots are)
+// One wave per 64 datagrams (grid-stride): lane = datagram for the store word
+// and the descriptor (coalesced), then the wave copies the stored ones with
+// four datagrams' loads in flight — 16-B copies when the source is 16-B
+// aligned (the ring slots are), dword or byte copies otherwise.
+constexpr u32 kBktChunks = (kBktSlot - 16) / 16;  // 16-B chunks of the largest stored datagram (95)
+static_assert(kBktChunks <= 128, "k_bkt_store copies at most two chunks per lane");
 __global__ void __launch_bounds__(256) k_bkt_store(BucketLaunch A) {
   const u32 lane = threadIdx.x & 63;
   const u32 w0 = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-  for (u32 ic = w0; ic < A.n; ic += nw) {
-    const u64 st = A.store[ic];
-    if (!(st >> 63)) continue;
-    const u32 slot = u32(st);
-    const lkf_raw_pkt rp = A.raws[ic];
-    const u16 sn = u16(st >> 32);
-    u8 *dst = A.ring + size_t(slot) * kBktSlot + 16;
-    const u8 *src = A.raw + rp.off;
-    const u32 snw = (u32(sn >> 8) << 16) | (u32(sn & 255) << 24);  // SN field (bytes 2-3), little-endian word 0
-    if ((rp.off & 15) == 0) {
-      for (u32 c = lane; c < (rp.len + 15) / 16; c += 64) {
-        uint4 v = reinterpret_cast<const uint4 *>(src)[c];
-        if (c == 0) v.x = (v.x & 0x0000FFFFu) | snw;
-        reinterpret_cast<uint4 *>(dst)[c] = v;
+  for (u32 base = w0 * 64; base < A.n; base += nw * 64) {
+    const u32 ic = base + lane;
+    u64 stw = 0;
+    lkf_raw_pkt rp = {};
+    if (ic < A.n) {
+      stw = A.store[ic];
+      if (stw >> 63) rp = A.raws[ic];
+    }
+    const u32 slotL = u32(stw), snL = u32(stw >> 32) & 0xffffu;
+    u64 todo = __ballot(stw >> 63);
+    while (todo) {
+      u32 js[4];
+      u32 k = 0;
+      for (; k < 4 && todo; k++) {
+        js[k] = u32(__ffsll(static_cast<long long>(todo))) - 1;
+        todo &= todo - 1;
       }
-    } else if ((rp.off & 3) == 0) {
-      for (u32 w = lane; w < (rp.len + 3) / 4; w += 64) {
-        u32 v = reinterpret_cast<const u32 *>(src)[w];
-        if (w == 0) v = (v & 0x0000FFFFu) | snw;
-        reinterpret_cast<u32 *>(dst)[w] = v;
+      uint4 v[4][2];
+#pragma unroll
+      for (u32 x = 0; x < 4; x++) {  // the aligned datagrams' loads, all in flight
+        v[x][0] = v[x][1] = make_uint4(0, 0, 0, 0);
+        if (x < k) {
+          const u32 off = __builtin_amdgcn_readlane(rp.off, js[x]);
+          const u32 nc = (__builtin_amdgcn_readlane(rp.len, js[x]) + 15) / 16;
+          if ((off & 15) == 0) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.raw + off);
+            if (lane < nc) v[x][0] = src[lane];
+            if (lane + 64 < nc) v[x][1] = src[lane + 64];
+          }
+        }
       }
-    } else {
-      for (u32 j = lane; j < rp.len; j += 64) dst[j] = j == 2 ? u8(sn >> 8) : j == 3 ? u8(sn) : src[j];
+#pragma unroll
+      for (u32 x = 0; x < 4; x++) {
+        if (x >= k) break;
+        const u32 off = __builtin_amdgcn_readlane(rp.off, js[x]);
+        const u32 len = __builtin_amdgcn_readlane(rp.len, js[x]);
+        const u32 slot = __builtin_amdgcn_readlane(slotL, js[x]);
+        const u16 sn = u16(__builtin_amdgcn_readlane(snL, js[x]));
+        u8 *dst = A.ring + size_t(slot) * kBktSlot + 16;
+        const u8 *src = A.raw + off;
+        const u32 snw = (u32(sn >> 8) << 16) | (u32(sn & 255) << 24);  // SN field (bytes 2-3), little-endian word 0
+        if ((off & 15) == 0) {
+          const u32 nc = (len + 15) / 16;
+          if (lane == 0) v[x][0].x = (v[x][0].x & 0x0000FFFFu) | snw;
+          if (lane < nc) reinterpret_cast<uint4 *>(dst)[lane] = v[x][0];
+          if (lane + 64 < nc) reinterpret_cast<uint4 *>(dst)[lane + 64] = v[x][1];
+        } else if ((off & 3) == 0) {
+          for (u32 w = lane; w < (len + 3) / 4; w += 64) {
+            u32 d = reinterpret_cast<const u32 *>(src)[w];
+            if (w == 0) d = (d & 0x0000FFFFu) | snw;
+            reinterpret_cast<u32 *>(dst)[w] = d;
+          }
+        } else {
+          for (u32 j = lane; j < len; j += 64) dst[j] = j == 2 ? u8(sn >> 8) : j == 3 ? u8(sn) : src[j];
+        }
+      }
     }
   }
 }
