@@ -850,19 +850,17 @@ __device__ inline bool fc_integrity(const DDIngState &d, u64 fn) {
   return (d.feFlags[int((fn - d.fcBase) % u64(kFICFrames))] & 4) != 0;
 }
 
-// Parse: false -> the packet produces no ExtPacket (a parse error); *limit
-// when an engine limit (not the reference) refused it
-__device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u8 *buf, int len, u16 sn, IngDD &out, bool &limit) {
-  limit = false;
-  const u32 cur = (d.flags & DI_CUR) ? 1u : 0u;
-  DDPkt o = {};
-  bool att = false;
-  const int e = dd::dd_parse(buf, len, (d.flags & DI_HAS_STRUCT) ? structs + cur : nullptr, structs + (cur ^ 1u), o,
-                             att);
-  if (e) {
-    limit = e == dd::LIMIT;
-    return false;
-  }
+// The fields of a parsed descriptor the parser state needs
+struct DDLite {
+  u16 frameNumber;
+  u8 flags, sid, tid;  // flags: DP_*
+  u32 activeMask;
+};
+// The parser state's part of Parse (dependencydescriptorparser.go:100-162) for
+// a descriptor already read: sequence / frame-number unwrap, the frame
+// integrity checker, an attached structure, the active decode targets.
+// false -> no ExtPacket (out as far as it was filled, as Parse leaves it)
+__device__ bool dd_fold(DDIngState &d, u16 sn, const DDLite &o, bool att, IngDD &out) {
   const u64 extSeq = wa16_ext(d.seqCycles, d.seqExtHighest, d.seqStart, d.seqHighest, d.flags, DI_SEQ_INIT, sn);
   const u64 extFN = wa16_ext(d.fnCycles, d.fnExtHighest, d.fnStart, d.fnHighest, d.flags, DI_FN_INIT, o.frameNumber);
   if (extFN < d.structureExtFN) return false;  // ErrFrameEarlierThanKeyFrame
@@ -888,6 +886,47 @@ __device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u
   out.sid = o.sid;
   out.tid = o.tid;
   return true;
+}
+
+// DependencyDescriptorExtension.Unmarshal against the structure in force
+// (cur; nullptr before any) with no structure attached (the caller checked
+// the flag): -> (error, the descriptor's DDLite), out of line (one call per
+// lane of a run).
+__device__ __noinline__ int dd_parse_lite(const u8 *buf, int len, const DDStruct *cur, DDLite &out) {
+  DDPkt o = {};
+  bool att = false;
+  const int e = dd::dd_parse(buf, len, cur, nullptr, o, att);
+  out.frameNumber = o.frameNumber;
+  out.flags = o.flags;
+  out.sid = o.sid;
+  out.tid = o.tid;
+  out.activeMask = o.activeMask;
+  return e;
+}
+// a descriptor that attaches a structure (template_dependency_structure_present_flag)
+__device__ __forceinline__ bool dd_attaches(const u8 *buf, int len) { return len > 3 && (buf[3] & 0x80); }
+
+// Parse: false -> the packet produces no ExtPacket (a parse error); *limit
+// when an engine limit (not the reference) refused it
+__device__ __noinline__ bool dd_ingest(DDIngState &d, DDStruct *structs, const u8 *buf, int len, u16 sn, IngDD &out,
+                                       bool &limit) {
+  limit = false;
+  const u32 cur = (d.flags & DI_CUR) ? 1u : 0u;
+  DDPkt o = {};
+  bool att = false;
+  const int e = dd::dd_parse(buf, len, (d.flags & DI_HAS_STRUCT) ? structs + cur : nullptr, structs + (cur ^ 1u), o,
+                             att);
+  if (e) {
+    limit = e == dd::LIMIT;
+    return false;
+  }
+  DDLite l;
+  l.frameNumber = o.frameNumber;
+  l.flags = o.flags;
+  l.sid = o.sid;
+  l.tid = o.tid;
+  l.activeMask = o.activeMask;
+  return dd_fold(d, sn, l, att, out);
 }
 
 // The stream's RTX bucket inside the stream kernel (mediatransportutil
@@ -1245,9 +1284,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u32 prevTs = u32(__shfl_up(p.ts, 1, 64));
     const u16 gs = u16(p.sn - (lane == pos ? sh.snHighest : prevSn));
     const u32 gt = p.ts - (lane == pos ? sh.tsHighest : prevTs);
+    // (a descriptor that attaches a structure changes what the later ones are
+    // read against: it takes the serial step)
+    const bool ddLane = hasDD && p.ddLen;
     const bool ok = lane >= pos && stateOk && in && rp.stream == sid && (p.flags & IP_OK) && p.payloadLen > 0 &&
-                    !(p.flags & IP_VP8_BAD) && !(hasDD && p.ddLen) && gs >= 1 && gs <= 0x8000u &&
-                    gt <= 0x80000000u && (!bkOn || rp.len <= 1498u);
+                    !(p.flags & IP_VP8_BAD) && !(ddLane && dd_attaches(raw + rp.off + p.ddOff, p.ddLen)) &&
+                    gs >= 1 && gs <= 0x8000u && gt <= 0x80000000u && (!bkOn || rp.len <= 1498u);
     const u64 snScan = wave_incl_scan_u64(ok ? u64(gs) : 0, lane);  // only read below the run end
     u64 bad = ~__ballot(ok) & ~((1ull << pos) - 1);
     // the history update below is exact while the run spans < 4096 SNs
@@ -1292,6 +1334,58 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u64 newJ = __ballot(run && extTs != (lane == pos ? sh.lastJitterExtTs : prevExtTs));
     const u64 transit = rx_transit(sh, s.clockRate, extTs, rp.arrival_ns);
     if (run) rx_gap(gap, u64(gs));
+    // getExtPacket's dependency descriptor for the run's datagrams that carry
+    // one (buffer.go:599-620, after the bucket as Buffer.calc orders them):
+    // each lane reads its descriptor against the structure in force (none of
+    // them attaches one), then lane 0 folds them into the parser state in
+    // order; a descriptor the parser refuses leaves its datagram without an
+    // ExtPacket (failMask).
+    u64 ddFail = 0;
+    const u64 ddM = __ballot(run && ddLane);
+    if (ddM) {
+      DDIngState &dst = ddStates[s.ddIdx];
+      const u32 dfl = dst.flags;
+      const DDStruct *curS = (dfl & DI_HAS_STRUCT) ? ddStructs + size_t(s.ddIdx) * 2 + ((dfl & DI_CUR) ? 1 : 0) : nullptr;
+      DDLite dl = {};
+      int de = 0;
+      if (run && ddLane) de = dd_parse_lite(raw + rp.off + p.ddOff, p.ddLen, curS, dl);
+      const u32 dlw0 = u32(dl.frameNumber) | (u32(dl.flags) << 16) | (u32(dl.sid & 15) << 24) | (u32(dl.tid & 15) << 28);
+      const u16 snL = u16(ext - sh.rmOpenValue);
+      // (the loop and its readlanes run on the whole wave, so every lane's
+      // operands exist; only lane 0 folds and stores)
+      for (u64 w = ddM; w; w &= w - 1) {
+        const u32 x = u32(__ffsll(static_cast<long long>(w)) - 1);
+        const int ex = __builtin_amdgcn_readlane(de, x);
+        const u32 icx = u32(__builtin_amdgcn_readlane(int(ic), x));
+        const u32 w0 = u32(__builtin_amdgcn_readlane(int(dlw0), x));
+        const u32 amx = u32(__builtin_amdgcn_readlane(int(dl.activeMask), x));
+        const u16 snx = u16(__builtin_amdgcn_readlane(int(snL), x));
+        const u32 offx = u32(__builtin_amdgcn_readlane(int(p.ddOff), x));
+        const u32 lenx = u32(__builtin_amdgcn_readlane(int(p.ddLen), x));
+        if (lane == 0) {
+          IngDD dv = {};
+          bool okx = false;
+          if (ex) {
+            if (ex == dd::LIMIT) atomicOr(err, 4u);
+          } else {
+            DDLite o;
+            o.frameNumber = u16(w0);
+            o.flags = u8(w0 >> 16);
+            o.sid = u8((w0 >> 24) & 15);
+            o.tid = u8(w0 >> 28);
+            o.activeMask = amx;
+            okx = dd_fold(dst, snx, o, false, dv);
+            if (okx) {
+              dv.ddOff = u16(offx);
+              dv.ddLen = u8(lenx);
+            }
+          }
+          if (ingDD) ingDD[icx] = dv;
+          if (!okx) ddFail |= 1ull << x;
+        }
+      }
+      ddFail = rl_u64(ddFail, 0);
+    }
     if (run) {
       lkf_flow f = {};
       f.pkt = 0xffffffffu;
@@ -1303,9 +1397,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         f.loss_start = ext - gs + 1;
         f.loss_end = ext;
       }
+      const bool failed = (ddFail >> lane) & 1;
+      if (failed) f.flags = u8((f.flags & ~LKF_FLOW_FORWARD) | LKF_FLOW_BAD);
       flows[ic] = f;
-      fwd[ic] = 1;
-      if (ingDD) ingDD[ic] = IngDD{};
+      fwd[ic] = failed ? 0u : 1u;
+      if (ingDD && !ddLane) ingDD[ic] = IngDD{};
       if (bkOn) {  // the run's pushes: this lane's skipped slots invalidated, then its own
         const u32 dk = lane == pos ? d0 : u32(gs);
         const int step0 = int(sB.step);
