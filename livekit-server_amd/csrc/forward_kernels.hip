@@ -4009,68 +4009,121 @@ __device__ void dd_tracker_observe(DDTrkState &T, const DDStruct &S, const DDPkt
   }
 }
 
-__global__ void k_dd_decode(const RunDesc *__restrict__ desc, const u32 *__restrict__ tBegin,
-                            const u32 *__restrict__ tEnd, const DevTrack *__restrict__ tracks, u32 ntracks,
-                            DDStruct *structs, DDTrack *ddTracks, DDPkt *__restrict__ out, u32 *err,
-                            const u32 *__restrict__ trackDDTrk, DDTrkState *ddTrk) {
+// One wave per track, 64 packets at a time: the descriptors of a run of
+// packets that attach no structure are read lane-parallel against the
+// structure in force; a packet that attaches one is read alone (its structure
+// goes to the ring's next slot and is in force from then on).  The DD stream
+// tracker (order-dependent) folds the chunk's packets on lane 0 in order.
+__global__ void __launch_bounds__(64) k_dd_decode(const RunDesc *__restrict__ desc, const u32 *__restrict__ tBegin,
+                                                  const u32 *__restrict__ tEnd, const DevTrack *__restrict__ tracks,
+                                                  u32 ntracks, DDStruct *structs, DDTrack *ddTracks,
+                                                  DDPkt *__restrict__ out, u32 *err,
+                                                  const u32 *__restrict__ trackDDTrk, DDTrkState *ddTrk) {
   const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
   const lkf_pkt_dd *__restrict__ dds = reinterpret_cast<const lkf_pkt_dd *>(desc->dd);
   const u8 *__restrict__ arena = reinterpret_cast<const u8 *>(desc->arena);
-  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 t = blockIdx.x, lane = threadIdx.x;
   if (t >= ntracks) return;
   const u32 ddIdx = tracks[t].ddIdx;
   if (ddIdx == 0xffffffffu) return;
-  DDTrack st = ddTracks[ddIdx];
+  DDTrack st = ddTracks[ddIdx];  // (wave-uniform)
   DDStruct *ring = structs + size_t(ddIdx) * kDDSlots;
   u32 updates = 0;
-  bool bad = false;
-  for (u32 i = tBegin[t]; i < tEnd[t]; i++) {
-    if (!(pkts[i].flags & LKF_PKT_DD)) continue;
+  bool bad = false;  // per lane
+  const u32 pb = tBegin[t], pe = tEnd[t];
+  const u32 trk = trackDDTrk ? trackDDTrk[t] : 0xffffffffu;
+  for (u32 j = pb; j < pe; j += 64) {
+    const u32 i = j + lane;
+    bool isDD = false;
+    u32 aoff = 0, psize = 0, pay = 0;
+    if (i < pe) {
+      const lkf_pkt &pk = pkts[i];
+      isDD = pk.flags & LKF_PKT_DD;
+      aoff = pk.arena_off;
+      psize = u32(pk.payload_off) + pk.payload_len;
+      pay = pk.payload_len;
+    }
+    lkf_pkt_dd r = {};
+    if (isDD && dds) r = dds[i];
+    // template_dependency_structure_present_flag (the first extended-field bit)
+    const bool attL = isDD && dds && r.dd_len > 3 && (arena[u64(aoff) + r.dd_off + 3] & 0x80);
     DDPkt o = {};
-    if (!dds) {  // LKF_PKT_DD packets without their lkf_pkt_dd side array
-      bad = true;
-      out[i] = o;
-      continue;
-    }
-    const lkf_pkt_dd r = dds[i];
-    o.extFN = r.ext_frame_num;
-    o.extKFN = r.ext_key_frame_num;
-    o.extFlags = r.flags;
-    const u32 next = st.valid ? (st.cur + 1) % kDDSlots : 0u;
-    bool att = false;
-    const int e = r.dd_len ? dd::dd_parse(arena + pkts[i].arena_off + r.dd_off, r.dd_len,
-                                          st.valid ? ring + st.cur : nullptr, ring + next, o, att)
-                           : int(dd::INVALID);
-    if (e) {
-      bad = true;
-      o.flags = 0;
-    } else {
-      if (att) {
-        st.cur = next;
-        st.valid = 1;
-        updates++;
+    u64 pend = __ballot(isDD);
+    while (pend) {
+      const u64 attM = __ballot(attL) & pend;
+      const u32 a = attM ? u32(__ffsll(static_cast<long long>(attM)) - 1) : 64u;
+      const u64 runM = pend & (a < 64 ? ((1ull << a) - 1) : ~0ull);  // decoded together
+      const u32 cur = st.cur, next = st.valid ? (st.cur + 1) % kDDSlots : 0u;
+      const DDStruct *curS = st.valid ? ring + cur : nullptr;
+      bool attOK = false;
+      if (((runM >> lane) & 1) || lane == a) {
+        if (!dds) {  // LKF_PKT_DD packets without their lkf_pkt_dd side array
+          bad = true;
+        } else {
+          o.extFN = r.ext_frame_num;
+          o.extKFN = r.ext_key_frame_num;
+          o.extFlags = r.flags;
+          bool att = false;
+          const int e =
+              r.dd_len ? dd::dd_parse(arena + aoff + r.dd_off, r.dd_len, curS, ring + next, o, att) : int(dd::INVALID);
+          if (e) {
+            bad = true;
+            o.flags = 0;
+          } else {
+            attOK = att;
+            o.slot = u8(att ? next : cur);
+            o.flags |= DP_VALID;
+          }
+        }
       }
-      o.slot = u8(st.cur);
-      o.flags |= DP_VALID;
-      if (trackDDTrk && trackDDTrk[t] != 0xffffffffu)  // the track's DD stream tracker (receiver.go:686-695)
-        dd_tracker_observe(ddTrk[trackDDTrk[t]], ring[o.slot], o, r.flags,
-                           u32(pkts[i].payload_off) + pkts[i].payload_len, pkts[i].payload_len);
+      if (a < 64) {  // the attaching packet's structure is in force from here on
+        if (__builtin_amdgcn_readlane(int(attOK), a)) {
+          st.cur = next;
+          st.valid = 1;
+          updates++;
+        }
+        pend &= ~((2ull << a) - 1);
+      } else {
+        pend = 0;
+      }
     }
-    out[i] = o;
+    if (isDD) out[i] = o;
+    if (trk != 0xffffffffu) {  // StreamTrackerDependencyDescriptor.Observe in packet order
+      const u64 vM = __ballot(isDD && (o.flags & DP_VALID));
+      const u32 w0 = u32(o.flags) | (u32(o.slot) << 8) | (u32(o.ndti) << 16) | (u32(r.flags) << 24);
+      for (u64 w = vM; w; w &= w - 1) {  // (whole wave: every lane's operands exist)
+        const u32 x = u32(__ffsll(static_cast<long long>(w)) - 1);
+        const u32 fx = u32(__builtin_amdgcn_readlane(int(w0), x));
+        const u32 amx = u32(__builtin_amdgcn_readlane(int(o.activeMask), x));
+        const u64 dtx = (u64(u32(__builtin_amdgcn_readlane(int(u32(o.dtis >> 32)), x))) << 32) |
+                        u32(__builtin_amdgcn_readlane(int(u32(o.dtis)), x));
+        const u32 szx = u32(__builtin_amdgcn_readlane(int(psize), x));
+        const u32 pyx = u32(__builtin_amdgcn_readlane(int(pay), x));
+        if (lane == 0) {
+          DDPkt q = {};
+          q.flags = u8(fx);
+          q.slot = u8(fx >> 8);
+          q.ndti = u8(fx >> 16);
+          q.activeMask = amx;
+          q.dtis = dtx;
+          dd_tracker_observe(ddTrk[trk], ring[q.slot], q, fx >> 24, szx, pyx);
+        }
+      }
+    }
   }
   // batch n+1's decode may run while batch n decides: a ring slot is reused
   // only after kDDSlots structures, so at most half of them per batch
   if (updates > u32(kDDSlots / 2)) bad = true;
-  if (bad) atomicOr(err, 16u);
-  ddTracks[ddIdx] = st;
+  if (__ballot(bad) && lane == 0) atomicOr(err, 16u);
+  if (lane == 0) ddTracks[ddIdx] = st;
 }
 
 hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                             const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,
                             uint32_t *err, const uint32_t *trackDDTrk, DDTrkState *ddTrk) {
   if (!ntracks) return hipSuccess;
-  hipLaunchKernelGGL(k_dd_decode, dim3((ntracks + 63) / 64), dim3(64), 0, s, desc, tBegin, tEnd, tracks, ntracks,
-                     structs, ddTracks, out, err, trackDDTrk, ddTrk);
+  hipLaunchKernelGGL(k_dd_decode, dim3(ntracks), dim3(64), 0, s, desc, tBegin, tEnd, tracks, ntracks, structs,
+                     ddTracks, out, err, trackDDTrk, ddTrk);
   return hipGetLastError();
 }
 
