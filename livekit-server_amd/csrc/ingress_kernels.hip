@@ -1036,7 +1036,7 @@ __device__ __forceinline__ void rx_jitter(StreamHot &h, u32 clockRate, u64 ets, 
 template <int HS>
 __device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream &s,
                                          const IngParsed &p, const lkf_raw_pkt &rp, u32 ic, lkf_flow *flows,
-                                         u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *ddStates,
+                                         u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *dds,
                                          DDStruct *ddStructs, u32 *err, const BktCtx &bk, bool bkOn, u32 *gap) {
   const i64 arrival = rp.arrival_ns;
   lkf_flow f = {};
@@ -1137,7 +1137,7 @@ __device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, c
     // getExtPacket (buffer.go:599-671): the dependency descriptor first
     if (payloadSize > 0 && s.ddIdx != 0xffffffffu && p.ddLen) {
       bool limit = false;
-      if (!dd_ingest(ddStates[s.ddIdx], ddStructs + size_t(s.ddIdx) * 2, raw + rp.off + p.ddOff, p.ddLen,
+      if (!dd_ingest(*dds, ddStructs + size_t(s.ddIdx) * 2, raw + rp.off + p.ddOff, p.ddLen,
                      u16(f.ext_sn), dv, limit)) {
         if (limit) atomicOr(err, 4u);
         f.flags |= LKF_FLOW_BAD;
@@ -1209,6 +1209,12 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
   return v;
 }
 
+// Two instantiations: <false> for the streams without a dependency-descriptor
+// parser, <true> (launched only when DD streams exist) for those with one,
+// whose DependencyDescriptorParser + FrameIntegrityChecker state (3.3 KB) is
+// staged in LDS for the batch — lane 0's fold of the descriptors then updates
+// it there (the plain streams keep the smaller LDS footprint and occupancy).
+template <bool DDK>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_ing_stream_wave(
     const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q, const DevStream *__restrict__ streams,
     StreamHot *__restrict__ hot, u64 *__restrict__ hist, RangeEntry *__restrict__ rings,
@@ -1222,8 +1228,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   __shared__ StreamHot sh;
   __shared__ BucketState sB;
   __shared__ u32 sOwn[kBktLds];  // (LDS is otherwise small: 4 waves per SIMD either way)
+  __shared__ __attribute__((aligned(16))) u8 sDDIRaw[DDK ? sizeof(DDIngState) : 16];
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
+  if ((s.ddIdx != 0xffffffffu) != DDK) return;  // the other instantiation's stream
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;
   if (s.closed) {  // Buffer.Close: Write returns io.EOF, nothing is processed
@@ -1251,6 +1259,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     bk.lds = M <= kBktLds;
     if (bk.lds)
       for (int i = int(lane); i < M; i += 64) sOwn[i] = kNoOwner;
+  }
+  DDIngState *dds = nullptr;
+  if (DDK) {
+    dds = reinterpret_cast<DDIngState *>(sDDIRaw);
+    const uint4 *g = reinterpret_cast<const uint4 *>(ddStates + s.ddIdx);
+    uint4 *l = reinterpret_cast<uint4 *>(sDDIRaw);
+    for (u32 i = lane; i < sizeof(DDIngState) / 16; i += 64) l[i] = g[i];
   }
   __syncthreads();
   RangeEntry *ring = rings + size_t(sid) * kRangeCap;
@@ -1309,7 +1324,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u32 end = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;  // the run is [pos, end)
     if (end == pos) {  // the datagram at pos through the serial Buffer.calc step
       if (lane == pos && rp.stream == sid)
-        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, ddStates, ddStructs, err, bk, bkOn, gap);
+        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, dds, ddStructs, err, bk, bkOn, gap);
       __syncthreads();
       pos++;
       continue;
@@ -1343,7 +1358,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     u64 ddFail = 0;
     const u64 ddM = __ballot(run && ddLane);
     if (ddM) {
-      DDIngState &dst = ddStates[s.ddIdx];
+      DDIngState &dst = *dds;
       const u32 dfl = dst.flags;
       const DDStruct *curS = (dfl & DI_HAS_STRUCT) ? ddStructs + size_t(s.ddIdx) * 2 + ((dfl & DI_CUR) ? 1 : 0) : nullptr;
       DDLite dl = {};
@@ -1492,6 +1507,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   hg[lane] = sHist[lane];
   reinterpret_cast<u32 *>(hot + sid)[lane] = reinterpret_cast<const u32 *>(&sh)[lane];
   if (bkOn && lane < 4) reinterpret_cast<u32 *>(bka.state + sid)[lane] = reinterpret_cast<const u32 *>(&sB)[lane];
+  if (DDK) {
+    __syncthreads();
+    uint4 *g = reinterpret_cast<uint4 *>(ddStates + s.ddIdx);
+    const uint4 *l = reinterpret_cast<const uint4 *>(sDDIRaw);
+    for (u32 i = lane; i < sizeof(DDIngState) / 16; i += 64) g[i] = l[i];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2200,9 +2221,13 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
       bka.store = a.bucket->store;
       bka.epoch = a.bucket->epoch;
     }
-    hipLaunchKernelGGL(k_ing_stream_wave, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams, a.hot,
-                       a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs, a.ingDD,
-                       a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap);
+    hipLaunchKernelGGL(k_ing_stream_wave<false>, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams,
+                       a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs,
+                       a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap);
+    if (a.ddStates)  // DD streams exist
+      hipLaunchKernelGGL(k_ing_stream_wave<true>, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams,
+                         a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs,
+                         a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap);
   }
   if (a.nack && a.nstreams) {  // after the flows: the loss ranges it pushes
     hipError_t r = hipEventRecord(sideFork, st);
