@@ -3974,9 +3974,9 @@ hipError_t launch_err_fold(hipStream_t s, const u32 *err, u32 *sticky, u32 shift
 // its extension bytes with the track's current FrameDependencyStructure (as
 // the Go parser did at ingress, dependencydescriptorparser.go:86-97), into one
 // DDPkt per packet for k_decide_dt.  A structure attached to a packet goes to
-// the next slot of the track's ring and becomes current.  One thread per
-// track (packets of a track in order); runs on the prep stream, so batch n+1's
-// decode follows batch n's.
+// the next slot of the track's ring and becomes current.  One wave per track
+// (see the kernel); runs on the prep stream, so batch n+1's decode follows
+// batch n's.
 // ---------------------------------------------------------------------------
 // StreamTrackerDependencyDescriptor.Observe (streamtracker_dd.go:133-212) of one
 // packet, serial in the track's lane
