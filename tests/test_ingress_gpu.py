@@ -213,3 +213,23 @@ def test_ingress_config3_bench_size(pkg, workload, abi):
     the oracle's."""
     tr = workload.Trace(3, duration_s=2.0, batch_s=1.0, rooms=125)
     assert run_ingress_parity(pkg, workload, abi, tr) > 0
+
+
+def test_ingress_config5_dd_heavy_loss_small_batches(pkg, workload, abi):
+    """DD streams through the run path under heavy loss and deep reordering
+    with 50-ms ingests: runs cut by reorders, descriptors that attach a
+    structure (key frames) at any lane of a chunk, lost first / last packets
+    of frames (frame integrity), all against the oracle's serial parser."""
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.05, rooms=4, loss=0.2, reorder=0.1, seed=59)
+    assert tr.has_dd()
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
+
+
+def test_ingress_config5_bench_size(pkg, workload, abi):
+    """configs[4] at the per-GPU size bench.py runs (2,000 rooms x 5
+    participants, VP9/AV1 L3T3 with dependency descriptors): raw datagrams
+    through Buffer.calc with the DD parser in the stream wave's runs, then the
+    SVC / DD forwarding, identical to the oracle."""
+    tr = workload.Trace(5, duration_s=2.0, batch_s=1.0, rooms=2000)
+    assert tr.has_dd()
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
