@@ -178,8 +178,8 @@ def kernel_sources_sha():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
                     help="BASELINE.json configs[N-1] (2 = configs[1], the headline)")
     ap.add_argument("--rooms", type=int, default=0, help="rooms per GPU (0: the config's)")
