@@ -2262,6 +2262,12 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
 // four datagrams' loads in flight — 16-B copies when the source is 16-B
 // aligned (the ring slots are), dword or byte copies otherwise.
 constexpr u32 kBktChunks = (kBktSlot - 16) / 16;  // 16-B chunks of the largest stored datagram (95)
+__device__ __forceinline__ void bkt_store16(uint4 *p, uint4 v) {
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+  __builtin_nontemporal_store(v.z, &p->z);
+  __builtin_nontemporal_store(v.w, &p->w);
+}
 static_assert(kBktChunks <= 128, "k_bkt_store copies at most two chunks per lane");
 __global__ void __launch_bounds__(256) k_bkt_store(BucketLaunch A) {
   const u32 lane = threadIdx.x & 63;
@@ -2310,8 +2316,10 @@ __global__ void __launch_bounds__(256) k_bkt_store(BucketLaunch A) {
         if ((off & 15) == 0) {
           const u32 nc = (len + 15) / 16;
           if (lane == 0) v[x][0].x = (v[x][0].x & 0x0000FFFFu) | snw;
-          if (lane < nc) reinterpret_cast<uint4 *>(dst)[lane] = v[x][0];
-          if (lane + 64 < nc) reinterpret_cast<uint4 *>(dst)[lane + 64] = v[x][1];
+          // (non-temporal: the ring is read back only for a NACK, long after;
+          // the batch's payloads stay in the caches for emit)
+          if (lane < nc) bkt_store16(reinterpret_cast<uint4 *>(dst) + lane, v[x][0]);
+          if (lane + 64 < nc) bkt_store16(reinterpret_cast<uint4 *>(dst) + lane + 64, v[x][1]);
         } else if ((off & 3) == 0) {
           for (u32 w = lane; w < (len + 3) / 4; w += 64) {
             u32 d = reinterpret_cast<const u32 *>(src)[w];
