@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -423,8 +424,12 @@ struct lkf_engine {
   lkf_speaker *dSpkSlots = nullptr;
   uint32_t *dSpkCounts = nullptr;
   size_t spkCap = 0;
-  // 1: k_decide_dt (one wave per DownTrack, lanes = packets; default)
-  // 0: k_decide (one lane per DownTrack, one wave per track)
+  // device -> host copies refused by the range check (CHKRANGE) since the last
+  // lkf_debug_check of this engine (lkf_debug_check folds them in)
+  std::atomic<uint64_t> rangeViolations{0};
+  // the current batch's descriptors / DD side array are engine allocations
+  // (lkf_submit / lkf_ingest*) rather than the caller's (lkf_submit_device)
+  bool curOwned = false, curDDOwned = false;
 };
 
 static int fail(lkf_engine *e, const char *what, hipError_t r) {
@@ -534,13 +539,15 @@ static int drain_streams(lkf_engine *e) {
 // "an illegal memory access" from the copy call itself (the runtime's staging
 // copy reads the bad range) — round 2's recorded fault was exactly that
 // (a drain of tot[3] bytes past the output arena).
-static uint64_t gRangeViolations = 0;
+// every engine's refusals, for lkf_debug_check(NULL) (the whole device)
+static std::atomic<uint64_t> gRangeViolationsAll{0};
 static int range_fail(lkf_engine *e, const void *src, size_t n, const char *what) {
   char buf[256];
   snprintf(buf, sizeof(buf), "internal: %s: device range [%p, +%zu) outside every live engine allocation", what, src,
            n);
   e->err = buf;
-  gRangeViolations++;
+  e->rangeViolations.fetch_add(1, std::memory_order_relaxed);
+  gRangeViolationsAll.fetch_add(1, std::memory_order_relaxed);
   return LKF_EHIP;
 }
 #define CHKRANGE(src, n, what)                                                     \
@@ -1252,6 +1259,8 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
   e->curN = n;
   e->curNDev = nullptr;
   e->curDD = nullptr;
+  e->curOwned = true;
+  e->curDDOwned = true;
   e->ingestStarted = false;
   e->curArenaLen = arena_len;
   e->haveBatch = true;
@@ -1266,6 +1275,8 @@ int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const ui
   e->curN = n;
   e->curNDev = nullptr;
   e->curDD = nullptr;
+  e->curOwned = false;
+  e->curDDOwned = true;
   e->ingestStarted = false;
   e->curArenaLen = arena_len;
   e->haveBatch = true;
@@ -1284,6 +1295,7 @@ int lkf_submit_dd(lkf_engine *e, const lkf_pkt_dd *dd, uint32_t n) {
   if (n) HIPCHK(hipMemcpyAsync(x.dDDIn, dd, size_t(n) * sizeof(lkf_pkt_dd), hipMemcpyHostToDevice, e->own), "dd");
   HIPCHK(hipStreamSynchronize(e->own), "submit dd sync");
   e->curDD = x.dDDIn;
+  e->curDDOwned = true;
   return LKF_OK;
 }
 
@@ -1291,6 +1303,7 @@ int lkf_submit_dd_device(lkf_engine *e, const lkf_pkt_dd *d_dd, uint32_t n) {
   if (!e || (n && !d_dd)) return LKF_EINVAL;
   if (!e->haveBatch || n != e->curN) return LKF_EINVAL;
   e->curDD = d_dd;
+  e->curDDOwned = false;
   return LKF_OK;
 }
 
@@ -1462,6 +1475,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   if (!e->haveBatch) {  // control-only run: an empty batch applies queued ops
     e->curPkts = x.dPktsOwn;
     e->curArena = x.dArenaOwn;
+    e->curOwned = e->curDDOwned = true;
     e->curN = 0;
     e->curNDev = nullptr;
     e->curArenaLen = 0;
@@ -2387,6 +2401,10 @@ static int rtx_emit_common(lkf_engine *e, const lkf_rtx *rtx, uint32_t n, const 
 // for that point: the scratch buffers below are rewritten from the host.
 static int rtx_order(lkf_engine *e, uint32_t n) {
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (e->twccDirty) {  // a transport-cc DownTrack added / bound since the last run: its counters first
+    const int rt = rebuild_twcc(e);
+    if (rt) return rt;
+  }
   const int rc = sender_after_queued(e);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->sendS), "sync sender stream");
@@ -2667,6 +2685,10 @@ static int pad_common(lkf_engine *e, int blank, const lkf_pad_req *reqs, uint32_
   }
   int rc = flush_topology(e);
   if (rc) return rc;
+  if (e->twccDirty) {  // a transport-cc DownTrack added / bound since the last run: its counters first
+    rc = rebuild_twcc(e);
+    if (rc) return rc;
+  }
   // k_pad reads and writes the DownTracks' Forwarder / sequencer state, which
   // between runs only the decide stream touches: it runs there, behind the
   // queued decides (their emits keep running); its sendingPacket updates go to
@@ -3529,8 +3551,12 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   e->ingRaws = dRaws;
   e->curPkts = x.dPktsOwn;
   e->curN = n;  // launch bound; the count is e->dITotal
-  e->curNDev = e->dITotal;
+  // (an empty ingest launches nothing, so dITotal still holds the previous
+  // ingest's count: the batch is empty, with no device-side count)
+  e->curNDev = n ? e->dITotal : nullptr;
   e->curDD = a.outDD;  // the ExtPackets' descriptors (nullptr: no DD stream)
+  e->curOwned = true;
+  e->curDDOwned = true;
   e->curArena = dRaw;
   e->curArenaLen = rawLen;
   e->haveBatch = true;
@@ -3545,6 +3571,14 @@ int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
   if (x.used) HIPCHK(hipStreamWaitEvent(e->prepS, x.emitted, 0), "wait emit");  // batch n-2 reads these buffers
+  if (e->haveBatch && e->curPkts == x.dPktsOwn) {
+    // a second ingest into this context before lkf_run: the previous ingest's
+    // NACK queues (side stream) and bucket copies (sender stream) still read
+    // the datagrams these copies overwrite
+    const int lp = e->ingPar;
+    if (e->sidePending[lp]) HIPCHK(hipStreamWaitEvent(e->prepS, e->sideDone[lp], 0), "wait nack queues");
+    if (e->bktPending[lp]) HIPCHK(hipStreamWaitEvent(e->prepS, e->bktDone[lp], 0), "wait bucket copies");
+  }
   if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->prepS),
                 "raw pkts");
   if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->prepS), "raw arena");
@@ -3601,7 +3635,9 @@ int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
   }
   *n_out = n;
   if (cap < n) return LKF_ENOSPC;
-  if (n) D2H(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), "ingested copy");
+  if (n && e->curOwned) D2H(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), "ingested copy");
+  if (n && !e->curOwned)  // the caller's device buffer (lkf_submit_device): not an engine allocation
+    HIPCHK(hipMemcpy(out, e->curPkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyDeviceToHost), "ingested copy");
   return LKF_OK;
 }
 
@@ -3621,8 +3657,10 @@ int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_ou
   *n_out = n;
   if (cap < n) return LKF_ENOSPC;
   if (!n) return LKF_OK;
-  if (e->curDD)
+  if (e->curDD && e->curDDOwned)
     D2H(out, e->curDD, size_t(n) * sizeof(lkf_pkt_dd), "ingested dd copy");
+  else if (e->curDD)  // the caller's device buffer (lkf_submit_dd_device)
+    HIPCHK(hipMemcpy(out, e->curDD, size_t(n) * sizeof(lkf_pkt_dd), hipMemcpyDeviceToHost), "ingested dd copy");
   else
     std::memset(out, 0, size_t(n) * sizeof(lkf_pkt_dd));
   return LKF_OK;
@@ -3856,10 +3894,12 @@ int lkf_debug_check(lkf_engine *e, uint64_t out[4], int reset) {
   for (int i = 0; i < 4; i++) out[i] = v[i];
   // host-side device -> host range violations (CHKRANGE) count as well, in
   // every build; site 0xD2H marks one when the device recorded none
-  if (gRangeViolations) {
+  // an engine's own refusals; with no engine, every engine's
+  std::atomic<uint64_t> &ctr = e ? e->rangeViolations : gRangeViolationsAll;
+  const uint64_t rv = reset ? ctr.exchange(0) : ctr.load();
+  if (rv) {
     if (!out[0]) out[1] = 0xD2, out[2] = 0, out[3] = 0;
-    out[0] += gRangeViolations;
-    if (reset) gRangeViolations = 0;
+    out[0] += rv;
     return LKF_OK;
   }
   return r == hipSuccess ? LKF_OK : LKF_ENODEV;

@@ -233,3 +233,59 @@ def test_ingress_config5_bench_size(pkg, workload, abi):
     tr = workload.Trace(5, duration_s=2.0, batch_s=1.0, rooms=2000)
     assert tr.has_dd()
     assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
+
+
+def test_empty_ingest_after_ingest(pkg, workload, abi):
+    """an empty ingest after a full one produces an empty
+    ExtPacket batch (lkf_ingested returns 0 records), forwards nothing, and
+    the next full ingest continues as the oracle does; a second host ingest
+    into the same batch context before lkf_run (its datagram copies overwrite
+    what the first one's NACK queues and bucket copies read) leaves the
+    receivers' state equal to the oracle's."""
+    trace = workload.Trace(2, duration_s=3.0, batch_s=1.0, rooms=2, seed=23)
+    o = load_oracle()
+    eng = pkg.Engine.for_trace(trace)
+    oh = o.create(500)
+    try:
+        for api, h in ((eng.api, eng.h), (o.api, oh)):
+            workload.load_topology(api, h, trace)
+            workload.load_streams(api, h, trace)
+        for b in range(trace.nbatches):
+            workload.queue_events(eng.api, eng.h, trace, b)
+            workload.queue_events(o.api, oh, trace, b)
+            rp, n, ar, alen = trace.batch_raw(b)
+            if b == 1:  # a full ingest, then (same context, no run) another full ingest
+                eng.ingest(rp, n // 2, ar, alen)
+                assert o.api["ingest"](oh, rp, n // 2, ar, alen) == 0
+                eng.ingest(C.cast(C.cast(rp, C.c_void_p).value + (n // 2) * C.sizeof(abi.lkf_raw_pkt),
+                                  C.POINTER(abi.lkf_raw_pkt)), n - n // 2, ar, alen)
+                assert o.api["ingest"](oh, C.cast(C.cast(rp, C.c_void_p).value + (n // 2) *
+                                                  C.sizeof(abi.lkf_raw_pkt), C.POINTER(abi.lkf_raw_pkt)),
+                                       n - n // 2, ar, alen) == 0
+            else:
+                eng.ingest(rp, n, ar, alen)
+                assert o.api["ingest"](oh, rp, n, ar, alen) == 0
+            gp, op = _ingested(eng.api, eng.h, abi), _ingested(o.api, oh, abi)
+            assert gp == op and len(gp) > 0, b
+            if b == 0:  # an empty ingest replaces the batch: nothing to forward
+                eng.ingest(rp, 0, ar, 0)
+                assert o.api["ingest"](oh, rp, 0, ar, 0) == 0
+                assert _ingested(eng.api, eng.h, abi) == b"" == _ingested(o.api, oh, abi)
+                op = b""
+            eng.run()
+            eng.sync()
+            m = len(op) // 64
+            if m:
+                o.run(oh, C.cast(C.c_char_p(op), C.POINTER(abi.lkf_pkt)), m, ar, alen)
+            else:
+                o.run(oh, None, 0, ar, alen)
+            grec, gar = eng.drain()
+            orec, oar = pkg.drain_arrays(o.api, oh)
+            assert np.array_equal(grec, orec) and np.array_equal(gar, oar), b
+            if b == 0:
+                assert len(grec) == 0
+        for s in range(trace.nstreams):
+            assert eng.stream_stats(s) == pkg.stream_stats(o.api, oh, s), s
+    finally:
+        eng.close()
+        o.destroy(oh)

@@ -119,3 +119,61 @@ def test_transport_cc_matches_oracle(pkg, workload, abi, cfg):
     finally:
         o.destroy(oh)
         eng.close()
+
+
+def test_transport_bound_between_runs(pkg, workload, abi):
+    """transport-cc DownTracks forward on their own counters
+    (no transport at the first run, so no transport counters exist yet), then
+    are bound to transports and send padding, blank frames and RTX before the
+    next lkf_run: the transports' counters must exist by then (stamped packets
+    equal the oracle's) and the next batches continue from them."""
+    tr = workload.Trace(2, duration_s=3.0, batch_s=1.0, rooms=2, seed=18, twcc=1)
+    o = load_oracle()
+    eng = pkg.Engine.for_trace(tr)
+    oh = o.create(500)
+    try:
+        workload.load_topology(eng.api, eng.h, tr)
+        workload.load_topology(o.api, oh, tr)
+        stamped = 0
+        for b in range(tr.nbatches):
+            workload.queue_events(eng.api, eng.h, tr, b)
+            workload.queue_events(o.api, oh, tr, b)
+            pk, n, ar, alen = tr.batch(b)
+            eng.submit(pk, n, ar, alen)
+            eng.run()
+            eng.sync()
+            o.run(oh, pk, n, ar, alen)
+            grec, gar = eng.drain()
+            orec, oar = pkg.drain_arrays(o.api, oh)
+            assert np.array_equal(grec, orec) and np.array_equal(gar, oar), b
+            stamped += len(_tcc_values(tr, orec, oar))
+            if b == 0:  # bind, then padding, blank frames and RTX before the next run
+                tg = srtp_lib.bind_transports(pkg, eng.api, eng.h, tr, seed=4)
+                to = srtp_lib.bind_transports(pkg, o.api, oh, tr, seed=4)
+                assert sorted(tg) == sorted(to)
+                now = EPOCH + 10**9
+                reqs = pad_lib.make_reqs(tr.ndts, seed=41, frac=0.5)
+                g, r = pad_lib.pad(eng.api, eng.h, reqs, now), pad_lib.pad(o.api, oh, reqs, now)
+                assert np.array_equal(g[0], r[0]) and np.array_equal(g[1], r[1])
+                assert len(_tcc_values(tr, r[0], r[1])) > 0
+                reqs = pad_lib.make_reqs(tr.ndts, seed=42, frac=0.5)
+                g = pad_lib.pad(eng.api, eng.h, reqs, now, blank=True)
+                r = pad_lib.pad(o.api, oh, reqs, now, blank=True)
+                assert np.array_equal(g[0], r[0]) and np.array_equal(g[1], r[1])
+                nacks = rtx_lib.make_nacks(o.api, oh, tr, seed=43)
+                g = rtx_lib.rtx_lookup(eng.api, eng.h, nacks, now)
+                r = rtx_lib.rtx_lookup(o.api, oh, nacks, now)
+                assert len(g) == len(r) > 5
+                idx = rtx_lib.packet_index(tr, 1)
+                go, gw = rtx_lib.rtx_emit(eng.api, eng.h, tr, g, idx)
+                oo, ow = rtx_lib.rtx_emit(o.api, oh, tr, r, idx)
+                for f in oo.dtype.names:
+                    assert np.array_equal(go[f], oo[f]), f
+                assert np.array_equal(gw, ow)
+        assert stamped > 100
+        check_sender_stats(pkg, eng.api, eng.h, o.api, oh, range(tr.ndts))
+        rec = pkg.debug_check(reset=True)  # (a refused device -> host copy counts too)
+        assert rec is None or rec[0] == 0, rec
+    finally:
+        o.destroy(oh)
+        eng.close()
