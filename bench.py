@@ -109,6 +109,24 @@ class _BenchShard(C.Structure):  # oracle/cpu_bench.cpp orc_bench_shard
                 ("ntracks", C.c_uint32), ("ndts", C.c_uint32), ("nstreams", C.c_uint32), ("nbatches", C.c_uint32)]
 
 
+def _dt_subset_shard(tr, b_events, keep):
+    """A shard of one trace holding only DownTracks `keep` (all its tracks and
+    streams): the DownTrack parameters and each batch's control ops (dt
+    re-indexed, ops of other DownTracks dropped)."""
+    abi = importlib.import_module("livekit-server_amd.abi")
+    dts = (type(tr.downtracks[0]) * len(keep))(*[tr.downtracks[d] for d in keep])
+    where = {d: i for i, d in enumerate(keep)}
+    evs = []
+    for ev, nev in b_events:
+        sel = [ev[i] for i in range(nev) if ev[i].dt in where]
+        arr = (abi.lkfs_event * max(1, len(sel)))()
+        for i, x in enumerate(sel):
+            arr[i] = x
+            arr[i].dt = where[x.dt]
+        evs.append((arr, len(sel)))
+    return dts, evs
+
+
 def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2, ingress=False):
     """CPU oracle (C++ restatement of the Go path, -O3) on a bounded sample of
     the same workload: `sample_rooms` rooms of the config's shape,
@@ -116,22 +134,44 @@ def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2, ingress=
     engine each) that `threads` C++ threads pull from a shared counter
     (oracle/cpu_bench.cpp; no Python in the timed region).  With `ingress`
     each batch goes through Buffer.calc (orc_ingest) first, as the GPU step
-    does.  Returns (forwarded/s, wall s, rooms, batches, per-thread busy s)."""
+    does.  When the rooms are too few to keep the threads busy and their
+    tracks fan out to 20 or more DownTracks, each room's DownTracks are split
+    over several engines as well: the reference writes such a track's
+    DownTracks in parallel (DownTrackSpreader.Broadcast -> utils.ParallelExec
+    with the receiver's load-balance threshold 20, downtrackspreader.go:89-102,
+    rtc/mediatrack.go:257); every such engine also runs the room's Buffer.calc,
+    which the reference does once per packet (a small overstatement of the CPU
+    work: one publisher's datagrams against thousands of DownTracks).  Returns
+    (forwarded/s, wall s, rooms, batches, per-thread busy s, engines)."""
     from tests.oracle_lib import load as load_oracle
     wl = importlib.import_module("livekit-server_amd.workload")
     o = load_oracle()
-    threads = max(1, min(threads, sample_rooms))
+    threads = max(1, threads)
     per = max(1, sample_rooms // (threads * 8))  # about 8 shards per thread
-    nsh = max(1, sample_rooms // per)
-    traces, shards, keep = [], (_BenchShard * nsh)(), []
-    for t in range(nsh):
-        tr = wl.Trace(config, duration_s=float(sample_batches), batch_s=1.0, rooms=per, room_base=t * per)
-        traces.append(tr)
+    nrs = max(1, sample_rooms // per)
+    traces = []
+    for t in range(nrs):
+        traces.append(wl.Trace(config, duration_s=float(sample_batches), batch_s=1.0, rooms=per, room_base=t * per))
+    fan = max(int(np.bincount([traces[0].downtracks[d].track for d in range(traces[0].ndts)]).max()), 0)
+    split = 1
+    if nrs < threads * 4 and fan >= 20:  # DownTrackSpreader's parallel fan-out
+        split = -(-threads * 4 // nrs)
+    units = [(tr, k) for tr in traces for k in range(split)]
+    shards, keep = (_BenchShard * len(units))(), []
+    for i, (tr, k) in enumerate(units):
+        bevs = [wl.events_ptr(tr, b) for b in range(tr.nbatches)]
+        if split > 1:
+            sel = [d for d in range(tr.ndts) if d % split == k]
+            dts, bevs = _dt_subset_shard(tr, bevs, sel)
+            keep.append((dts, bevs))
+            ndts = len(sel)
+        else:
+            dts, ndts = tr.downtracks, tr.ndts
         bb = (_BenchBatch * tr.nbatches)()
         dd = tr.has_dd() and not ingress
         for b in range(tr.nbatches):
             pk, n, ar, alen = tr.batch(b)
-            ev, nev = wl.events_ptr(tr, b)
+            ev, nev = bevs[b]
             x = bb[b]
             x.pkts, x.n, x.arena, x.alen = C.cast(pk, C.c_void_p), n, C.cast(ar, C.c_void_p), alen
             x.ev, x.nev = C.cast(ev, C.c_void_p), nev
@@ -140,11 +180,13 @@ def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2, ingress=
                 rp, nraw, _, _ = tr.batch_raw(b)
                 x.raws, x.nraw = C.cast(rp, C.c_void_p), nraw
         keep.append(bb)
-        s = shards[t]
-        s.tracks, s.dts = C.cast(tr.tracks, C.c_void_p), C.cast(tr.downtracks, C.c_void_p)
-        s.streams = C.cast(tr.streams, C.c_void_p) if ingress else None
-        s.batches = C.cast(bb, C.c_void_p)
-        s.ntracks, s.ndts, s.nstreams, s.nbatches = tr.ntracks, tr.ndts, (tr.nstreams if ingress else 0), tr.nbatches
+        sh = shards[i]
+        sh.tracks, sh.dts = C.cast(tr.tracks, C.c_void_p), C.cast(dts, C.c_void_p)
+        sh.streams = C.cast(tr.streams, C.c_void_p) if ingress else None
+        sh.batches = C.cast(bb, C.c_void_p)
+        sh.ntracks, sh.ndts, sh.nstreams, sh.nbatches = tr.ntracks, ndts, (tr.nstreams if ingress else 0), tr.nbatches
+    nsh = len(units)
+    threads = min(threads, nsh)
     fwd = (C.c_uint64 * nsh)()
     busy = (C.c_double * threads)()
     wall = C.c_double()
@@ -157,7 +199,115 @@ def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2, ingress=
     nb = traces[0].nbatches
     for tr in traces:
         tr.close()
-    return sum(fwd) / wall.value, wall.value, per * nsh, nb, list(busy)
+    return sum(fwd) / wall.value, wall.value, per * nrs, nb, list(busy), nsh
+
+
+def parity_gate(eng, pkg, config, room_ids, nb, batch_s, ingress, trace, threads, warm_cum, timed_cum):
+    """The parity gate (timing is reported only for bit-exact
+    output), outside the timed region: the CPU oracle runs the same rooms and
+    the same `nb` batches as the GPU did (shards of rooms on `threads` C++
+    threads, oracle/cpu_bench.cpp orc_parity_run), then
+      - the cumulative counters over all nb batches (tuples, forwarded, bytes,
+        arena bytes, every drop reason),
+      - every DownTrack's exported Forwarder state and RTPStatsSender,
+      - every stream's RTPStatsReceiver (with the ingress step)
+    must be identical, DownTracks and streams keyed by SSRC (a room shard
+    keeps its rooms' SSRCs).  -> dict (parity: bool + what was compared)."""
+    from tests.oracle_lib import load as load_oracle
+    wl = importlib.import_module("livekit-server_amd.workload")
+    abi = pkg.abi
+    o = load_oracle()
+    t0 = time.perf_counter()
+    per = max(1, len(room_ids) // (threads * 4))
+    chunks = [room_ids[i:i + per] for i in range(0, len(room_ids), per)]
+    traces, keep, shards = [], [], (_BenchShard * len(chunks))()
+    for t, rids in enumerate(chunks):
+        tr = wl.Trace(config, duration_s=nb * batch_s, batch_s=batch_s, room_ids=rids)
+        traces.append(tr)
+        bb = (_BenchBatch * nb)()
+        dd = tr.has_dd() and not ingress
+        for b in range(nb):
+            pk, n, ar, alen = tr.batch(b)
+            ev, nev = wl.events_ptr(tr, b)
+            x = bb[b]
+            x.pkts, x.n, x.arena, x.alen = C.cast(pk, C.c_void_p), n, C.cast(ar, C.c_void_p), alen
+            x.ev, x.nev = C.cast(ev, C.c_void_p), nev
+            x.dd = C.cast(tr.batch_dd(b)[0], C.c_void_p) if dd else None
+            if ingress:
+                rp, nraw, _, _ = tr.batch_raw(b)
+                x.raws, x.nraw = C.cast(rp, C.c_void_p), nraw
+        keep.append(bb)
+        sh = shards[t]
+        sh.tracks, sh.dts = C.cast(tr.tracks, C.c_void_p), C.cast(tr.downtracks, C.c_void_p)
+        sh.streams = C.cast(tr.streams, C.c_void_p) if ingress else None
+        sh.batches = C.cast(bb, C.c_void_p)
+        sh.ntracks, sh.ndts, sh.nstreams, sh.nbatches = tr.ntracks, tr.ndts, (tr.nstreams if ingress else 0), nb
+    ndts = sum(tr.ndts for tr in traces)
+    nst = sum(tr.nstreams for tr in traces) if ingress else 0
+    fs_sz, ss_sz, st_sz = C.sizeof(abi.lkf_fwd_state), abi.SENDER_STATS_DTYPE.itemsize, C.sizeof(abi.lkf_stream_stats)
+    dstride = (8 + fs_sz + ss_sz + 7) & ~7
+    sstride = (8 + st_sz + 7) & ~7
+    drec = np.zeros(max(1, ndts) * dstride, dtype=np.uint8)
+    srec = np.zeros(max(1, nst) * sstride, dtype=np.uint8)
+    cum = (abi.lkf_stats * len(chunks))()
+    f = o.lib.orc_parity_run
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,
+                  C.c_void_p, C.c_uint64]
+    rc = f(C.cast(shards, C.c_void_p), len(chunks), threads, 1 if ingress else 0, 500, C.cast(cum, C.c_void_p),
+           drec.ctypes.data, dstride, srec.ctypes.data, sstride)
+    for tr in traces:
+        tr.close()
+    res = {"parity": False, "oracle_rc": rc}
+    if rc != 0:
+        return res
+    # cumulative counters
+    ocum = {"tuples": 0, "forwarded": 0, "out_bytes": 0, "arena_bytes": 0, "drops": [0] * abi.LKF_DROP_NREASONS}
+    for c in cum:
+        d = c.as_dict()
+        for k in ("tuples", "forwarded", "out_bytes", "arena_bytes"):
+            ocum[k] += d[k]
+        ocum["drops"] = [a + b for a, b in zip(ocum["drops"], d["drops"])]
+    gcum = {k: warm_cum[k] + timed_cum[k] for k in ("tuples", "forwarded", "out_bytes", "arena_bytes")}
+    gcum["drops"] = [a + b for a, b in zip(warm_cum["drops"], timed_cum["drops"])]
+    ok_cum = gcum == ocum
+    # per DownTrack (by SSRC): Forwarder state + RTPStatsSender
+    orc = {}
+    for i in range(ndts):
+        r = drec[i * dstride:(i + 1) * dstride]
+        orc[int(r[:4].view(np.uint32)[0])] = r
+    bad_dt = 0
+    st = abi.lkf_fwd_state()
+    ss = np.zeros(1, dtype=abi.SENDER_STATS_DTYPE)
+    for d in range(trace.ndts):
+        ssrc = int(trace.downtracks[d].ssrc)
+        r = orc.get(ssrc)
+        if r is None or eng.api["get_state"](eng.h, d, C.byref(st)) != 0 or \
+                eng.api["sender_stats_get"](eng.h, d, ss.ctypes.data) != 0:
+            bad_dt += 1
+            continue
+        ost = abi.lkf_fwd_state.from_buffer_copy(bytes(r[8:8 + fs_sz]))
+        oss = np.frombuffer(bytes(r[8 + fs_sz:8 + fs_sz + ss_sz]), dtype=abi.SENDER_STATS_DTYPE)
+        if st.as_tuple() != ost.as_tuple() or any(not np.array_equal(ss[k], oss[k]) for k in ss.dtype.names):
+            bad_dt += 1
+    # per stream (by SSRC): RTPStatsReceiver
+    bad_st = 0
+    if ingress:
+        ors = {}
+        for i in range(nst):
+            r = srec[i * sstride:(i + 1) * sstride]
+            ors[int(r[:4].view(np.uint32)[0])] = r
+        for s_ in range(trace.nstreams):
+            r = ors.get(int(trace.streams[s_].ssrc))
+            if r is None or pkg.stream_stats(eng.api, eng.h, s_) != \
+                    abi.lkf_stream_stats.from_buffer_copy(bytes(r[8:8 + st_sz])).as_tuple():
+                bad_st += 1
+    res.update({"parity": bool(ok_cum and bad_dt == 0 and bad_st == 0 and ndts == trace.ndts),
+                "counters_equal": ok_cum, "downtracks_checked": trace.ndts, "downtracks_differing": bad_dt,
+                "streams_checked": trace.nstreams if ingress else 0, "streams_differing": bad_st,
+                "batches": nb, "forwarded_total": gcum["forwarded"], "oracle_threads": threads,
+                "gate_s": round(time.perf_counter() - t0, 1)})
+    return res
 
 
 def kernel_sources_sha():
@@ -206,6 +356,9 @@ def main():
     ap.add_argument("--alloc-per-step", type=int, default=0,
                     help="deployment shape: the stream allocator's AllocateOptimal for this many video DownTracks "
                          "after every step's run (a control-rate call: it waits for the queued runs)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the parity gate (the CPU oracle over the same rooms and batches, compared after "
+                         "the timed region: counters, every Forwarder state, RTPStatsSender, RTPStatsReceiver)")
     ap.add_argument("--srtp-profile", choices=["aes_cm", "gcm"], default="aes_cm",
                     help="with --srtp: SRTP_AES128_CM_HMAC_SHA1_80 or SRTP_AEAD_AES_128_GCM transports")
     args = ap.parse_args()
@@ -353,7 +506,7 @@ def main():
         step(b)
     torch.cuda.synchronize(dev)
     eng.sync()
-    eng.cumulative(reset=True)
+    warm_cum = eng.cumulative(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -404,6 +557,16 @@ def main():
                 "subscribers_deficient": int((btab[:, :, :, 3] > 0).sum()),
                 "room_plan": "LPT bin packing by expected tuples (rooms.plan_room_shards)"}
 
+    parity = None
+    if not args.no_parity and not args.srtp and not args.alloc_per_step:
+        # (outside the timed region; every rank checks its own rooms)
+        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        parity = parity_gate(eng, pkg, args.config, plan[rank], nb, args.batch_s, args.ingress, trace, thr,
+                             warm_cum, cum)
+        if dist:
+            ok = torch.tensor([1.0 if parity["parity"] else 0.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            parity["parity_all_ranks"] = bool(ok.item() > 0)
     fwd = cum["forwarded"]
     steps_pkts = sum(meta[b][0] for b in range(args.warmup, nb))
     algo, b_in, b_ing = algorithmic_bytes(trace, range(args.warmup, nb), fwd, cum["out_bytes"], trace.ndts,
@@ -463,17 +626,18 @@ def main():
             # the GPU box gives one GPU a 16-CPU share (os.cpu_count() is the whole host)
             thr = args.cpu_threads or min(16, os.cpu_count() or 1)
             cc = CONFIGS[args.config]
-            v, secs, rooms, nbat, busy = cpu_baseline(thr, sample_rooms=cc["sample"], config=args.config,
+            v, secs, rooms, nbat, busy, neng = cpu_baseline(thr, sample_rooms=cc["sample"], config=args.config,
+                                                            ingress=args.ingress)
+            v1, secs1, rooms1, _, _, _ = cpu_baseline(1, sample_rooms=cc["sample1"], config=args.config,
                                                       ingress=args.ingress)
-            v1, secs1, rooms1, _, _ = cpu_baseline(1, sample_rooms=cc["sample1"], config=args.config,
-                                                   ingress=args.ingress)
-            used = max(1, min(thr, rooms))
+            used = max(1, min(thr, neng))
             cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": used, "kind": "port",
-                   "sample": "configs[%d] shape%s: %d rooms, 4 s of media (%d batches incl. the arrival tail), rooms "
-                             "sharded over %d C++ threads, one oracle engine each (oracle/cpu_bench.cpp; %.1f s "
+                   "sample": "configs[%d] shape%s: %d rooms, 4 s of media (%d batches incl. the arrival tail), %d "
+                             "oracle engines (rooms%s) pulled by %d C++ threads (oracle/cpu_bench.cpp; %.1f s "
                              "wall); single thread: %d rooms, %.1f s wall" % (
                                  args.config - 1, " through Buffer.calc (orc_ingest)" if args.ingress else "", rooms,
-                                 nbat, used, secs, rooms1, secs1),
+                                 nbat, neng, " and, as DownTrackSpreader's parallel fan-out, their DownTracks"
+                                 if neng > rooms else "", used, secs, rooms1, secs1),
                    "single_thread_value": round(v1, 1), "host_nproc": os.cpu_count(), "cpu_model": cpu_model(),
                    "thread_busy_s": {"min": round(min(busy), 3), "max": round(max(busy), 3)}}
             # one thread per core of the box's 16-CPU share per GPU; rooms shard
@@ -514,6 +678,9 @@ def main():
                                       "achieved": round(pipe_ach, 1),
                                       "frac": round(pipe_ach / PEAK_HBM_GBPS, 4)}},
             "cpu_baseline": cpu,
+            "parity": (parity["parity_all_ranks"] if parity and "parity_all_ranks" in parity
+                       else parity["parity"] if parity else None),
+            "parity_gate": parity,
             "host_enqueue_ms_per_step": round(t_host * 1e3 / args.steps, 4),
             "collective": coll,
             "tuples_per_step": cum["tuples"] // args.steps,

@@ -95,7 +95,8 @@ constexpr uint32_t kIdle = 0xffffffffu;
 struct BatchCtx {
   uint32_t *dTBegin = nullptr, *dTEnd = nullptr, *dTRuns = nullptr, *dErr = nullptr;
   uint64_t *dSlotBase = nullptr, *dPartA = nullptr, *dPartB = nullptr, *dTot = nullptr;
-  Tuple *dTuples = nullptr;
+  FwdRec *dRecs = nullptr;    // decide -> emit: forwarded records at slotBase[dt] + j
+  FwdBase *dFBase = nullptr;  // per DownTrack: the base of its records' 32-bit SN / TS
   uint32_t *dFwdCnt = nullptr;
   uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
   uint32_t *dGFirst = nullptr;  // emit group g -> output position owning record 64g
@@ -359,7 +360,6 @@ struct lkf_engine {
   uint32_t emitGrid = 2048;       // persistent grid-stride launch (LKF_EMIT_PERSISTENT=1)
   bool emitPersistent = false;
   uint32_t decideK = 0;  // DownTracks per decide wave (0: from the batch's packets per track)
-  uint32_t senderMode = 0;  // sender statistics kernel: 0 by batch shape, 1 thread per DownTrack, 2 wave
   // SRTP protect (tables allocated with the first transport or lkf_protect)
   std::vector<lkf_transport_params> transports;
   lkf_transport_params *dTransports = nullptr;
@@ -893,7 +893,8 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dPartA, nparts));
     A(dalloc(&x.dPartB, nparts));
     A(dalloc(&x.dTot, 4));
-    A(dalloc(&x.dTuples, c.max_batch_tuples));
+    A(dalloc(&x.dRecs, c.max_batch_tuples));
+    A(dalloc(&x.dFBase, c.max_downtracks));
     A(dalloc(&x.dFwdCnt, c.max_downtracks));
     A(dalloc(&x.dFwdBytes, c.max_downtracks));
     A(dalloc(&x.dRecBase, c.max_downtracks));
@@ -1001,7 +1002,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
   if (const char *v = getenv("LKF_EMIT_PERSISTENT")) e->emitPersistent = atoi(v) != 0;
   if (const char *v = getenv("LKF_DECIDE_K")) e->decideK = uint32_t(std::min(64, std::max(0, atoi(v))));
-  if (const char *v = getenv("LKF_SENDER_MODE")) e->senderMode = uint32_t(std::min(2, std::max(0, atoi(v))));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   if (const char *v = getenv("LKF_GRAPH")) e->useGraph = atoi(v) != 0;
@@ -1065,7 +1065,7 @@ void lkf_destroy(lkf_engine *e) {
                     static_cast<void *>(x.dDDUsed)})
       if (p) (void)dfree(p);
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
-                 x.dPartB,  x.dTot,      x.dTuples,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
+                 x.dPartB,  x.dTot,      x.dRecs,  x.dFBase,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
                  x.dRawPkts, x.dBktStore, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane, x.dTwccBase};
     for (void *p : q)
@@ -1426,7 +1426,7 @@ static int rebuild_twcc(lkf_engine *e) {
     flat.insert(flat.end(), lst[t].begin(), lst[t].end());
   }
   off[nt] = uint32_t(flat.size());
-  if (nt > e->twccTCap) {  // grow the transport counters, keeping the old ones
+  if (nt > e->twccTCap || !e->dTwccCtrT) {  // grow the transport counters (first: before any transport), keeping the old ones
     const uint32_t cap = std::max<uint32_t>(nt, 2 * e->twccTCap + 64);
     uint32_t *c = nullptr, *o = nullptr;
     HIPCHK(dalloc(&c, cap), "alloc twcc counters");
@@ -1700,7 +1700,11 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.tBegin = x.dTBegin;
   d.tEnd = x.dTEnd;
   d.slotBase = x.dSlotBase;
-  d.tuples = x.dTuples;
+  d.recs = x.dRecs;
+  d.fbase = x.dFBase;
+  d.ss = e->dSS;
+  d.ssRing = e->dSSRing;
+  d.ssGap = e->dSSGap;
   d.tupleCap = e->cfg.max_batch_tuples;
   d.err = x.dErr;
   d.events = x.dEvents;
@@ -1760,7 +1764,8 @@ int lkf_run(lkf_engine *e, void *stream) {
     q.srmCap = e->srmCap;
     q.ddIdx = e->dSeqDDIdx;
     q.seqDD = e->dSeqDD;
-    q.tuples = x.dTuples;
+    q.recs = x.dRecs;
+    q.fbase = x.dFBase;
     q.slotBase = x.dSlotBase;
     q.fwdCnt = x.dFwdCnt;
     q.pkts = e->curPkts;
@@ -1780,7 +1785,8 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.gFirst = x.dGFirst;
   m.slotBase = x.dSlotBase;
   m.totals = x.dTot + 2;
-  m.tuples = x.dTuples;
+  m.recs = x.dRecs;
+  m.fbase = x.dFBase;
   m.pkts = e->curPkts;
   m.arena = e->curArena;
   m.dts = e->dDTs;
@@ -1807,38 +1813,14 @@ int lkf_run(lkf_engine *e, void *stream) {
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum, x.dErr, e->dSticky), "accumulate");
-  {  // sendingPacket -> RTPStatsSender.Update per forwarded tuple: on its own
-     // stream from the decided tuples, beside this batch's emit and the next
-     // decide; the emit stream waits for it before the context counts as done.
-     // A short batch's thread-per-DownTrack kernel goes straight after emit on
-     // the emit stream instead (three fewer stream operations per run: a
-     // 10-ms tick at 100 rooms is bound by the host's enqueue).
-    SenderLaunch sl;
-    sl.tuples = x.dTuples;
-    sl.slotBase = x.dSlotBase;
-    sl.fwdCnt = x.dFwdCnt;
-    sl.pkts = e->curPkts;
-    sl.ss = e->dSS;
-    sl.ring = e->dSSRing;
-    sl.gap = e->dSSGap;
-    sl.ndts = nd;
-    // a few tuples per DownTrack (the same estimate as decide's DownTracks per wave)
-    sl.perThread = e->senderMode ? uint32_t(e->senderMode == 1)
-                                 : uint32_t(uint64_t(e->curN) / std::max<uint32_t>(1, nt) < 12);
-    if (sl.perThread) {
-      if (e->bktStorePending) {  // this batch's bucket copies (sender stream) finish before the context is reused
-        HIPCHK(hipEventRecord(x.sent, e->sendS), "event");
-        HIPCHK(hipStreamWaitEvent(e->emitS, x.sent, 0), "wait bucket store");
-      }
-      HIPCHK(launch_sender_stats(e->emitS, sl), "sender stats");
-    } else {
-      HIPCHK(hipStreamWaitEvent(e->sendS, x.decided, 0), "wait decided (sender)");
-      HIPCHK(launch_sender_stats(e->sendS, sl), "sender stats");
-      HIPCHK(hipEventRecord(x.sent, e->sendS), "event");
-      HIPCHK(hipStreamWaitEvent(e->emitS, x.sent, 0), "wait sender stats");
-    }
-    e->bktStorePending = false;
+  // (sendingPacket -> RTPStatsSender.Update of every forwarded tuple runs inside
+  // decide, ss_fold.)  This batch's bucket copies (sender stream) finish before
+  // its context counts as done.
+  if (e->bktStorePending) {
+    HIPCHK(hipEventRecord(x.sent, e->sendS), "event");
+    HIPCHK(hipStreamWaitEvent(e->emitS, x.sent, 0), "wait bucket store");
   }
+  e->bktStorePending = false;
   HIPCHK(hipEventRecord(x.emitted, e->emitS), "event");
   if (e->hostProf && e->nRuns >= 3) {  // steady state: skip the first runs (initial control ops, first touch)
     e->hp[0] += std::chrono::duration<double, std::milli>(tp1 - tp0).count();
@@ -1886,6 +1868,10 @@ int lkf_sync(lkf_engine *e) {
   if (acc & 32u) {
     e->err = "internal: a DownTrack with padding exclusions was decided by the plain kernel";
     return LKF_EINVAL;
+  }
+  if (acc & 64u) {
+    e->err = "a DownTrack's munged RTP sequence numbers or timestamps spread over 2^31 or more within one batch";
+    return LKF_ENOSPC;
   }
   if (acc & 16u) {
     e->err = "dependency descriptor unreadable, missing its lkf_pkt_dd entry, or beyond an engine limit";

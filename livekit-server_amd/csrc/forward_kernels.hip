@@ -9,7 +9,8 @@
 //                   (forwarder.go:1436-1765) + RTPMunger (rtpmunger.go) +
 //                   Simulcast/VP8-temporal selectors + VP8 munger
 //                   (codecmunger/vp8.go) + sequencer.push (sequencer.go:123)
-//                   -> compact per-DownTrack Tuple records
+//                   -> compact per-DownTrack FwdRec records (24 B), with
+//                   RTPStatsSender.Update folded in (ss_flush)
 //   scan (output)   per DownTrack record base + byte base (16-B aligned wire
 //                   packets; order: track, then DownTrack, then packet)
 //   k_emit          flat 16-B chunk sweep over the output arena: RTP header +
@@ -25,6 +26,7 @@
 #include "dd_device.h"
 #include "fwd_state.h"
 #include "kernels.h"
+#include "sender_device.h"
 
 namespace lkf {
 
@@ -1081,12 +1083,38 @@ __device__ int fw_translate(Lane &L, const PktV &p, u32 k, Fwd &o) {
 __device__ __forceinline__ u32 pack4(u8 a, u8 b, u8 c, u8 d) {
   return u32(a) | (u32(b) << 8) | (u32(c) << 16) | (u32(d) << 24);
 }
-__device__ __forceinline__ void store_rec(Tuple *dst, const Tuple &t) {  // 3 x dwordx4 (pad = 0)
-  uint4 *d = reinterpret_cast<uint4 *>(dst);
-  d[0] = make_uint4(u32(t.extSN), u32(t.extSN >> 32), u32(t.extTS), u32(t.extTS >> 32));
-  d[1] = make_uint4(t.pkt, t.relOff, u32(t.outLen) | (u32(t.flags) << 16) | (u32(u8(t.layer)) << 24),
-                    pack4(t.codecLen, t.codec[0], t.codec[1], t.codec[2]));
-  d[2] = make_uint4(pack4(t.codec[3], t.codec[4], t.codec[5], t.ddLen), u32(t.hdrLen), t.ddOff, 0u);
+struct __attribute__((aligned(8))) U4x8 {  // 16 B at an 8-B aligned address (one dwordx4 access)
+  u32 x, y, z, w;
+};
+// a forwarded record (FwdRec): one dwordx4 + one dwordx2 store
+__device__ __forceinline__ void store_fwd(FwdRec *dst, u64 sn, u64 ts, u32 pkt, u32 relOff, u32 outLen, u32 flags,
+                                          u32 ddLen, u32 aux) {
+  *reinterpret_cast<U4x8 *>(dst) = U4x8{u32(sn), u32(ts), pkt, relOff >> 4};
+  reinterpret_cast<uint2 *>(dst)[2] = make_uint2(outLen | (flags << 16) | (ddLen << 24), aux);
+}
+// FwdRec.aux of a munged VP8 descriptor: its picture id, TL0PICIDX and KEYIDX
+__device__ __forceinline__ u32 vp8_aux(u32 mpid, u32 mtl0, u32 mkey) {
+  return (mpid & 0xffffu) | ((mtl0 & 0xffu) << 16) | ((mkey & 0x1fu) << 24);
+}
+// ... read back from marshalled bytes (vp8_marshal's layout, byte i = bits 8i..8i+7)
+__device__ __forceinline__ u32 vp8_aux_of(u64 cb) {
+  if (!(cb & 0x80)) return 0;  // no extension byte: none of the fields
+  const u32 x = u32(cb >> 8) & 0xff;
+  int idx = 2;
+  u32 pid = 0, tl0 = 0, key = 0;
+  if (x & 0x80) {
+    const u32 b = u32(cb >> (8 * idx)) & 0xff;
+    if (b & 0x80) {
+      pid = ((b & 0x7f) << 8) | (u32(cb >> (8 * (idx + 1))) & 0xff);
+      idx += 2;
+    } else {
+      pid = b;
+      idx++;
+    }
+  }
+  if (x & 0x40) tl0 = u32(cb >> (8 * idx++)) & 0xff;
+  if (x & 0x30) key = u32(cb >> (8 * idx)) & 0x1f;
+  return vp8_aux(pid, tl0, key);
 }
 __device__ __forceinline__ void store_rec(SeqMeta *dst, const SeqMeta &m) {  // 2 x dwordx4 (pad = 0)
   uint4 *d = reinterpret_cast<uint4 *>(dst);
@@ -1540,9 +1568,12 @@ struct DecideArgs {
   const lkf_pkt *pkts;
   const u32 *tBegin, *tEnd;
   const u64 *slotBase;
-  Tuple *tuples;
+  FwdRec *recs;
+  FwdBase *fbase;  // per DownTrack: its first forwarded record's munged SN / TS (FwdRec widening)
   u64 tupleCap;
   u32 *err;
+  SenderStats *ss;  // RTPStatsSender per DownTrack (+ snInfo ring, gap histogram)
+  u32 *ssRing, *ssGap;
   const DevEvent *events;
   const u32 *evOff;  // per lane [evOff[l], evOff[l+1])
   u32 *fwdCnt;
@@ -1565,13 +1596,19 @@ struct DecideArgs {
   u32 maxDts, maxTracks, npkts, nev;
 };
 
+struct SsEnt;
 // One wave per (track, <=64 DownTracks): the packet loop is wave-uniform, so
 // packet descriptors come through the scalar cache and every branch on packet
 // fields is a scalar branch; lanes diverge only on per-DownTrack state.
 // Per (packet, DownTrack) body of DownTrack.WriteRTP (downtrack.go:680-760).
 struct LaneOut {
-  Tuple *outT;
+  FwdRec *outT;
   u64 nFwd, nBytes, nTuples;
+  u64 bSN, bTS;  // the batch's first forwarded munged SN / TS (FwdBase)
+  SenderStats *ss;  // the DownTrack's RTPStatsSender, staged in LDS
+  u32 *ssRing, *ssGap;
+  SsEnt *ssBuf;  // this chunk's forwarded tuples for ss_flush (LDS)
+  u32 ssN;
   i32 sentDiff;  // sendingPacket's bytesSent - sum of out_len: incoming minus outgoing header bytes
   u32 relOff;
   u32 drops[LKF_DROP_NREASONS];
@@ -1582,6 +1619,167 @@ struct LaneOut {
   u64 tupBase, tupCap;  // this DownTrack's first tuple slot, the batch's capacity
 #endif
 };
+
+__device__ __forceinline__ double rl_f64(double v, u32 k) {
+  return __builtin_bit_cast(double, rl64(__builtin_bit_cast(u64, v), k));
+}
+
+// DownTrack.sendingPacket -> RTPStatsSender.Update (downtrack.go:1930-1959,
+// rtpstats_sender.go:229-432) inside the decide wave.  Every forwarded tuple
+// appends one 24-B entry to the wave's LDS buffer (SsEnt: munged SN / TS low
+// bits against the batch base, arrival, incoming header size, forwarded
+// payload, marker / key frame) in send order; at the end of each chunk (at
+// most 64 packets, so at most 64 entries) ss_flush folds the buffer into the
+// DownTrack's RTPStatsSender (LDS copy, written back once per batch).  The
+// fold runs where the chunk's registers are dead, so the run body keeps its
+// register budget.
+struct SsEnt {
+  u32 sn, ts;   // low 32 bits of the munged extended SN / TS (widened against FwdBase)
+  i64 t;        // arrival (the virtual clock of sendingPacket)
+  u32 hp;       // incoming header size | forwarded payload << 16
+  u32 fl;       // 1 marker, 2 key frame
+};
+static_assert(sizeof(SsEnt) == 24, "SsEnt is 24 B");
+__device__ __forceinline__ void ss_put(SsEnt *e, u64 sn, u64 ts, i64 t, u32 hdr, u32 pay, bool marker, bool kf) {
+  *reinterpret_cast<uint2 *>(e) = make_uint2(u32(sn), u32(ts));
+  reinterpret_cast<uint2 *>(e)[1] = make_uint2(u32(u64(t)), u32(u64(t) >> 32));
+  reinterpret_cast<uint2 *>(e)[2] = make_uint2(hdr | (pay << 16), (marker ? 1u : 0u) | (kf ? 2u : 0u));
+}
+
+// The fold of m entries, lane = entry.  A segment of in-order entries — each
+// above the one before it by at most 64, with a payload, not moving the
+// timestamp backwards — only accumulates: per lane the gap histogram, the
+// cleared snInfo slots of the SNs it skips and its own slot (distinct: a
+// segment spans at most 4096 SNs); the counters as wave sums; the highest
+// timestamp and its time from the last lane that raised it; the jitter filter
+// (a float64 recurrence, rtpstats_base.go:775-813) stepped over the segment's
+// new frames on uniform values.  The entry that ends a segment (out of order,
+// duplicate, a larger gap, the first packet) takes the scalar Update,
+// wave-uniform.
+__device__ __forceinline__ void ss_flush(SenderStats &S, u32 *ring, u32 *gap, const SsEnt *buf, u32 m, u64 bSN,
+                                      u64 bTS) {
+  const u32 lane = lane_id();
+  const u64 lt = (1ull << lane) - 1;
+  const bool valid = lane < m;
+  u64 esn = 0, ets = 0;
+  i64 t = 0;
+  u32 hdr = 0, pay = 0;
+  bool marker = false, kf = false;
+  if (valid) {
+    const SsEnt &e = buf[lane];
+    esn = widen32(bSN, e.sn);
+    ets = widen32(bTS, e.ts);
+    t = e.t;
+    hdr = e.hp & 0xffffu;
+    pay = e.hp >> 16;
+    marker = e.fl & 1;
+    kf = e.fl & 2;
+  }
+  const u64 pEsn = sh64(esn, lane ? int(lane) - 1 : 0), pEts = sh64(ets, lane ? int(lane) - 1 : 0);
+  u32 pos = 0;
+  while (pos < m) {
+    const bool inSeg = valid && lane >= pos;
+    const u64 prev = lane > pos ? pEsn : S.extHighestSN;
+    const u64 g = esn - prev;
+    const bool ok = S.initialized && pay > 0 && i64(g) > 0 && g <= 64 && ets >= S.extStartTS &&
+                    (lane == pos || ets >= pEts);
+    const u64 badM = __ballot(inSeg && !ok);
+    const u32 end = badM ? u32(__ffsll((long long)badM) - 1) : m;
+    if (end > pos) {
+      const bool act = lane >= pos && lane < end;
+      if (act && g >= 2) {  // updateGapHistogram; clearSnInfos(prev + 1, esn)
+        atomicAdd(&gap[g - 1 > u64(kGapBins) ? kGapBins - 1 : u32(g - 2)], 1u);
+        for (u64 q = prev + 1; q != esn; q++) ring[q & ss::kSnMask] = 0;
+      }
+      if (act)  // setSnInfo
+        ring[esn & ss::kSnMask] =
+            u32(u16(hdr + pay)) | (u32(u8(hdr)) << 16) | ((marker ? ss::kFlagMarker : 0u) << 24);
+      // highest timestamp: the lanes above every earlier one (non-decreasing in the segment)
+      const u64 before = (lane > pos && pEts > S.extHighestTS) ? pEts : S.extHighestTS;
+      const u64 upM = __ballot(act && ets > before);
+      // the jitter's new frames: a timestamp other than the previous packet's
+      const bool isNew = act && ets != (lane > pos ? pEts : S.lastJitterExtTimestamp);
+      const u64 newM = __ballot(isNew);
+      const i64 since = i64(u64(t) - u64(S.firstTime));
+      const u64 rtp = u64(i64(u64(since) * u64(i64(S.clockRate))) / 1000000000LL);
+      const u64 transit = rtp - ets;
+      const int pn = prev_in(newM, lt);
+      const u64 pnT = sh64(transit, pn >= 0 ? pn : int(lane));
+      const u64 prevTransit = pn >= 0 ? pnT : S.lastTransit;
+      i64 dj = i64(transit - prevTransit);
+      if (dj < 0) dj = i64(0 - u64(dj));
+      const double dd = double(dj);
+      const u64 useM = __ballot(isNew && prevTransit != 0);
+      // the segment's totals (<= 64 packets: the sums fit 32 bits)
+      const u32 sumB = wave_sum_u32(act ? hdr + pay : 0u), sumH = wave_sum_u32(act ? hdr : 0u);
+      const u32 lost = wave_sum_u32((act && g >= 2) ? u32(g - 1) : 0u);
+      const u32 frames = u32(__popcll(__ballot(act && marker))), kfs = u32(__popcll(__ballot(act && kf)));
+      double j = S.jitter, mj = S.maxJitter;
+      for (u64 w = newM; w; w &= w - 1) {
+        const u32 k = u32(__ffsll((long long)w) - 1);
+        if ((useM >> k) & 1) {
+          j += (rl_f64(dd, k) - j) / 16;
+          if (j > mj) mj = j;
+        }
+      }
+      const u64 lastEsn = rl64(esn, end - 1);
+      u64 trL = 0, etsL = 0, tU = 0, etsU = 0;
+      if (newM) {
+        const u32 kl = 63 - __clzll(newM);
+        trL = rl64(transit, kl);
+        etsL = rl64(ets, kl);
+      }
+      if (upM) {
+        const u32 ku = 63 - __clzll(upM);
+        tU = rl64(u64(t), ku);
+        etsU = rl64(ets, ku);
+      }
+      wave_lds_sync();
+      if (lane == 0) {
+        S.jitter = j;
+        S.maxJitter = mj;
+        if (newM) {
+          S.lastTransit = trL;
+          S.lastJitterExtTimestamp = etsL;
+        }
+        if (upM) {
+          S.highestTime = i64(tU);
+          S.extHighestTS = etsU;
+        }
+        S.extHighestSN = lastEsn;
+        S.packetsLost += lost;
+        S.bytes += sumB;
+        S.headerBytes += sumH;
+        S.frames += frames;
+        S.keyFrames += kfs;
+      }
+      wave_lds_sync();
+    }
+    pos = end;
+    if (pos < m) {  // the entry that ends the segment: the scalar Update (every lane, uniform arguments)
+      ss::ss_update(S, ring, gap, i64(rl64(u64(t), pos)), rl64(esn, pos), rl64(ets, pos), rl32(u32(marker), pos) != 0,
+                    rl32(hdr, pos), rl32(pay, pos), 0);
+      if (rl32(u32(kf), pos)) S.keyFrames++;  // UpdateKeyFrame(1) rtpstats_base.go:429-439
+      wave_lds_sync();
+      pos++;
+    }
+  }
+}
+
+// FwdBase: a DownTrack's first forwarded record of the batch sets it; every
+// record's munged SN / TS must lie within 2^31 of it (FwdRec carries their low
+// 32 bits) — error bit 64 (LKF_ENOSPC at lkf_sync) otherwise
+__device__ __forceinline__ void fwd_base(LaneOut &o, u32 *err, u64 fwM, u64 osn, u64 ots) {
+  if (!fwM) return;
+  if (o.nFwd == 0) {
+    const u32 f0 = u32(__ffsll((long long)fwM) - 1);
+    o.bSN = rl64(osn, f0);
+    o.bTS = rl64(ots, f0);
+  }
+  const bool act = (fwM >> lane_id()) & 1;
+  const bool wide = act && ((((osn - o.bSN) + 0x80000000ull) >> 32) != 0 || (((ots - o.bTS) + 0x80000000ull) >> 32) != 0);
+  if (__ballot(wide) && lane_id() == 0) atomicOr(err, 64u);
+}
 
 template <bool DDK>
 __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneOut &o) {
@@ -1694,42 +1892,31 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
   const bool useCodec = f.cbLen > 0 && (p.flags & LKF_PKT_VP8);
   int payLen = useCodec ? (f.cbLen + int(p.plen) - int(p.vhs)) : int(p.plen);
   const bool marker = f.marker || (p.hdr1 & 0x80);
-  Tuple t;
-  t.extSN = f.osn;
-  t.extTS = f.ots;
-  t.pkt = k;
-  t.relOff = o.relOff;
-  t.outLen = u16(hdrLen + payLen);
-  t.flags = u8((f.switching ? LKF_OUT_SWITCHING : 0) | (f.resuming ? LKF_OUT_RESUMING : 0) |
-               ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
-               (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0) | (ddOn ? T_DD : 0));
-  t.layer = p.layer;
-  t.codecLen = u8(f.cbLen);
-#pragma unroll
-  for (int i = 0; i < 6; i++) t.codec[i] = u8(f.cb >> (8 * i));
-  t.hdrLen = u16(hdrLen);
-  t.pad0 = 0;
-  t.pad1 = 0;
-  t.ddLen = ddOn ? u8(f.ddLen) : 0;
-  t.ddOff = 0;
+  u32 flags = (f.switching ? LKF_OUT_SWITCHING : 0) | (f.resuming ? LKF_OUT_RESUMING : 0) |
+              ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
+              (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0) | (ddOn ? T_DD : 0);
+  u32 ddLen = ddOn ? u32(f.ddLen) : 0u;
+  u32 aux = useCodec ? vp8_aux_of(f.cb) : 0u;
   if (DDK && ddOn) {  // the marshalled DD bytes go to the batch's DD arena (read by k_emit)
     u64 off = 0;
     if (lane_id() == 0) off = atomicAdd((unsigned long long *)o.ddUsed, (unsigned long long)f.ddLen);
     off = rl64(off, 0);
     if (off + u64(f.ddLen) > o.ddCap) {
       if (lane_id() == 0) atomicOr(L.err, 8u);
-      t.flags &= u8(~T_DD);
-      t.ddLen = 0;
+      flags &= ~u32(T_DD);
+      ddLen = 0;
     } else {
       wave_lds_sync();
       for (int i = int(lane_id()); i < f.ddLen; i += 64) o.ddArena[off + u64(i)] = L.ddBuf[i];
-      t.ddOff = u32(off);
+      aux = u32(off);
     }
   }
 #if LKF_CHECKED
   CHK(o.tupBase + o.nFwd < o.tupCap, CK_DEC_TUPLE, o.tupBase + o.nFwd, o.tupCap);
 #endif
-  if (lane_id() == 0) store_rec(o.outT + o.nFwd, t);  // wave-uniform record: one lane stores it
+  fwd_base(o, L.err, 1ull, f.osn, f.ots);
+  if (lane_id() == 0)  // wave-uniform record: one lane stores it
+    store_fwd(o.outT + o.nFwd, f.osn, f.ots, k, o.relOff, u32(hdrLen + payLen), flags, ddLen, aux);
   // sequencer.push (downtrack.go:724-735)
   seq_push<DDK>(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
   // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
@@ -1738,6 +1925,12 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
     L.h.statsFirstTime = p.arr;
     L.h.statsExtStartTS = f.ots;
   }
+  // sendingPacket -> RTPStatsSender.Update (downtrack.go:1930-1959): the
+  // incoming header's size (getTranslatedRTPHeader keeps its extensions) and
+  // the forwarded payload, folded at the end of the chunk (ss_flush)
+  if (lane_id() == 0)
+    ss_put(o.ssBuf + o.ssN, f.osn, f.ots, p.arr, p.poff, u32(payLen), marker, (p.flags & LKF_PKT_KEYFRAME) != 0);
+  o.ssN++;
   o.nFwd++;
   o.nBytes += u64(hdrLen + payLen);
   o.sentDiff += i32(p.poff) - hdrLen;  // getTranslatedRTPHeader keeps the incoming extensions (downtrack.go:1714-1726)
@@ -2245,28 +2438,14 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   }
   const bool kf = p.flags & LKF_PKT_KEYFRAME;
   const u32 j = u32(__popcll(fwR & lt));
+  fwd_base(o, L.err, fwR, osn, ots);
   if (f) {
-    Tuple t;
-    t.extSN = osn;
-    t.extTS = ots;
-    t.pkt = pi;
-    t.relOff = o.relOff + relEx;
-    t.outLen = u16(outLen);
-    t.flags = u8((kf ? LKF_OUT_KEYFRAME : 0) | (mk ? LKF_OUT_MARKER : 0) | (playout ? T_PLAYOUT : 0) |
-                 (ddKeep ? T_DD : 0));
-    t.layer = p.layer;
-    t.codecLen = 0;
-#pragma unroll
-    for (int i = 0; i < 6; i++) t.codec[i] = 0;
-    t.hdrLen = u16(hdrLen);
-    t.ddLen = ddKeep ? u8(ddLen) : 0;
-    t.pad0 = 0;
-    t.ddOff = ddKeep ? ddOff : 0;
-    t.pad1 = 0;
 #if LKF_CHECKED
     CHK(o.tupBase + o.nFwd + j < o.tupCap, CK_DEC_TUPLE, o.tupBase + o.nFwd + j, o.tupCap);
 #endif
-    store_rec(o.outT + o.nFwd + j, t);
+    store_fwd(o.outT + o.nFwd + j, osn, ots, pi, o.relOff + relEx, outLen,
+              (kf ? LKF_OUT_KEYFRAME : 0) | (mk ? LKF_OUT_MARKER : 0) | (playout ? T_PLAYOUT : 0) | (ddKeep ? T_DD : 0),
+              ddKeep ? u32(ddLen) : 0u, ddKeep ? ddOff : 0u);
     u32 slot = u32(L.h.seqHighSlot) + u32(osn - L.h.seqExtHighestSN);  // sequencer.push, in order
     while (slot >= L.seqSize) slot -= L.seqSize;
     SeqMeta m = {};
@@ -2292,6 +2471,8 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       store_rec(L.seq + x2, SeqMeta{});
     }
   }
+  if (f) ss_put(o.ssBuf + o.ssN + j, osn, ots, p.arr, p.poff, p.plen, mk, kf);
+  o.ssN += u32(__popcll(fwR));
   const u32 sumLen = wave_sum_u32(outLen);
   sentAcc += f ? i32(p.poff) - hdrLen : 0;
   if (fwR) {
@@ -2439,10 +2620,20 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   o.sentDiff = 0;
   i32 sentAcc = 0;  // per lane: run-path forwarded packets' incoming minus outgoing header bytes
   o.relOff = 0;
+  o.bSN = o.bTS = 0;
   for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
   __shared__ __attribute__((aligned(16))) DTHot sHot;
+  __shared__ __attribute__((aligned(16))) SenderStats sSS;  // the DownTrack's RTPStatsSender (ss_flush)
   Lane L{sHot};
   reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
+  if (lane < sizeof(SenderStats) / 16)
+    reinterpret_cast<uint4 *>(&sSS)[lane] = reinterpret_cast<const uint4 *>(A.ss + d)[lane];
+  __shared__ __attribute__((aligned(16))) SsEnt sSsBuf[64];  // one chunk's forwarded tuples (ss_flush)
+  o.ss = &sSS;
+  o.ssBuf = sSsBuf;
+  o.ssN = 0;
+  o.ssRing = A.ssRing + size_t(d) * kSnInfoSize;
+  o.ssGap = A.ssGap + size_t(d) * kGapWords;
   __syncthreads();
   RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
   L.rm = sRm;
@@ -2522,7 +2713,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       __syncthreads();
     }
   }
-  o.outT = A.tuples + slot0;
+  o.outT = A.recs + slot0;
   // SVC DownTracks (one SSRC, every packet relevant to the selector): svc_run
   // (the host schedules them in k_decide_dt<true>)
   const bool svcDT = 0 != 5 && DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
@@ -2800,28 +2991,15 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const u32 relEx = excl_scan_u32(aligned, lane);
         const bool marker = pktMarker;  // tp.marker (= hdr.Marker for video, false for audio) || hdr.Marker
         const u32 j = u32(__popcll(fwR & lt));
+        fwd_base(o, L.err, fwR, osn, ots);
         if (fwd) {
-          Tuple t;
-          t.extSN = osn;
-          t.extTS = ots;
-          t.pkt = pi;
-          t.relOff = o.relOff + relEx;
-          t.outLen = u16(outLen);
-          t.flags = u8(((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
-                       (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0));
-          t.layer = p.layer;
-          t.codecLen = u8(video ? cbLen : 0);
-#pragma unroll
-          for (int i = 0; i < 6; i++) t.codec[i] = u8(cb >> (8 * i));
-          t.hdrLen = u16(hdrLen);
-          t.ddLen = 0;
-          t.pad0 = 0;
-          t.ddOff = 0;
-          t.pad1 = 0;
 #if LKF_CHECKED
           CHK(slot0 + o.nFwd + j < A.tupleCap, CK_DEC_TUPLE, slot0 + o.nFwd + j, A.tupleCap);
 #endif
-          store_rec(o.outT + o.nFwd + j, t);
+          store_fwd(o.outT + o.nFwd + j, osn, ots, pi, o.relOff + relEx, outLen,
+                    ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
+                        (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0),
+                    0u, useCodec ? vp8_aux(mpid, mtl0, mkey) : 0u);
           // sequencer.push (sequencer.go:123-209): in order, the slot the SN's
           // distance past the highest
           u32 slot = u32(L.h.seqHighSlot) + u32(osn - L.h.seqExtHighestSN);
@@ -2839,6 +3017,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           CHK(slot < L.seqSize, CK_DEC_SEQ, slot, L.seqSize);
           store_rec(L.seq + slot, m);
         }
+        if (fwd) ss_put(o.ssBuf + o.ssN + j, osn, ots, p.arr, p.poff, u32(payLen), marker, kf);
+        o.ssN += u32(__popcll(fwR));
         const u32 sumLen = wave_sum_u32(outLen);
         sentAcc += fwd ? i32(p.poff) - hdrLen : 0;  // (reduced once per DownTrack)
         // ---- advance the DownTrack state past the run (uniform)
@@ -2955,11 +3135,18 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       o.nTuples += skipped;
       o.drops[LKF_DROP_NOT_SELECTED] += skipped;
     }
+    if (o.ssN) {  // the chunk's forwarded tuples -> RTPStatsSender
+      wave_lds_sync();
+      ss_flush(sSS, o.ssRing, o.ssGap, sSsBuf, o.ssN, o.bSN, o.bTS);
+      o.ssN = 0;
+    }
     kpos = lim;
   }
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
   __syncthreads();
   reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
+  if (o.nFwd && lane < sizeof(SenderStats) / 16)  // (only a forwarded packet changes it)
+    reinterpret_cast<uint4 *>(A.ss + d)[lane] = reinterpret_cast<const uint4 *>(&sSS)[lane];
   if (L.rmDirty) {
     wave_lds_sync();
     for (u32 i = lane; i < L.h.rmCount; i += 64) {
@@ -2988,6 +3175,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   if (lane == 0) {
     A.fwdCnt[d] = u32(o.nFwd);
     A.fwdBytes[d] = o.relOff;
+    if (o.nFwd) A.fbase[d] = FwdBase{o.bSN, o.bTS};
     // DownTrack.sendingPacket: bytesSent += header + payload (downtrack.go:1934-1940)
     // (atomics without return: the wave does not wait for a read of the old totals)
     if (o.nFwd) atomicAdd((unsigned long long *)&A.dtCum[d].packets, (unsigned long long)o.nFwd);
@@ -3041,7 +3229,8 @@ struct EmitArgs {
   const u32 *gFirst;    // [group] position owning record group*EMIT_G
   const u64 *slotBase;
   const u64 *totals;    // [0] records, [1] bytes
-  const Tuple *tuples;
+  const FwdRec *recs;
+  const FwdBase *fbase;  // per DownTrack: the base its records' 32-bit SN / TS widen against
   const lkf_pkt *pkts;
   const u8 *arena;
   const DevDT *dts;
@@ -3144,41 +3333,46 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       CHK(d < A.maxDts, CK_EMIT_DT, d, A.maxDts);
       CHK(A.slotBase[d] + (r - A.recBase[lo]) < A.tupleCap, CK_EMIT_TUPLE, A.slotBase[d] + (r - A.recBase[lo]),
           A.tupleCap);
-      const Tuple t = A.tuples[A.slotBase[d] + (r - A.recBase[lo])];
-      CHK(t.pkt < A.npkts, CK_EMIT_PKT, t.pkt, A.npkts);
-      const PktV p = load_pkt(A.pkts + t.pkt);
+      const FwdRec *rp = A.recs + (A.slotBase[d] + (r - A.recBase[lo]));
+      const U4x8 ra = *reinterpret_cast<const U4x8 *>(rp);  // sn, ts, pkt, rel16
+      const uint2 rb = reinterpret_cast<const uint2 *>(rp)[2];  // outLen | flags | ddLen, aux
+      const u32 tPkt = ra.z, tLen = rb.x & 0xffffu, tFlags = (rb.x >> 16) & 0xffu, tDDLen = rb.x >> 24, tAux = rb.y;
+      CHK(tPkt < A.npkts, CK_EMIT_PKT, tPkt, A.npkts);
+      const PktV p = load_pkt(A.pkts + tPkt);
       const DevDT dt = A.dts[d];
-      outOff = A.byteBase[lo] + t.relOff;
+      const FwdBase fb = A.fbase[d];
+      outOff = A.byteBase[lo] + (u64(ra.w) << 4);
       CHK(r < A.outCap, CK_EMIT_OUT, r, A.outCap);
-      CHK(outOff + t.outLen <= A.outByteCap, CK_EMIT_BYTES, outOff + t.outLen, A.outByteCap);
+      CHK(outOff + tLen <= A.outByteCap, CK_EMIT_BYTES, outOff + tLen, A.outByteCap);
       CHK(u64(p.arenaOff) + p.poff + p.plen <= A.arenaLen, CK_EMIT_ARENA, u64(p.arenaOff) + p.poff + p.plen,
           A.arenaLen);
-      CHK(!(t.flags & T_DD) || u64(t.ddOff) + t.ddLen <= A.ddCap, CK_EMIT_DD, u64(t.ddOff) + t.ddLen, A.ddCap);
+      CHK(!(tFlags & T_DD) || u64(tAux) + tDDLen <= A.ddCap, CK_EMIT_DD, u64(tAux) + tDDLen, A.ddCap);
+      const u64 extSN = widen32(fb.sn, ra.x), extTS = widen32(fb.ts, ra.y);
       lkf_out o;
-      o.ext_sn = t.extSN;
-      o.ext_ts = t.extTS;
+      o.ext_sn = extSN;
+      o.ext_ts = extTS;
       o.out_off = outOff;
       o.dt = d;
-      o.pkt = t.pkt;
-      o.out_len = t.outLen;
-      o.flags = t.flags & 0x0f;
-      o.layer = t.layer;
+      o.pkt = tPkt;
+      o.out_len = u16(tLen);
+      o.flags = u8(tFlags & 0x0f);
+      o.layer = p.layer;
       o.reserved = 0;
       A.out[r] = o;
       // prefix: RTP header (getTranslatedRTPHeader downtrack.go:1714-1726)
       u8 *w = pre[lane];
       const int cc = p.hdr0 & 0xf;
-      const bool playout = t.flags & T_PLAYOUT;
-      const bool ddOn = (PRE == PRE_MAX_DD) && (t.flags & T_DD);
+      const bool playout = tFlags & T_PLAYOUT;
+      const bool ddOn = (PRE == PRE_MAX_DD) && (tFlags & T_DD);
       const bool hasExt = playout || dt.extAbs || ddOn || dt.extTcc;
       // pion's TWCC HeaderExtensionInterceptor: the transport's next sequence
       // number in send order (this record's ordinal in its DownTrack's output
       // after the DownTrack's base)
       const u16 tcc = dt.extTcc ? u16(A.twccBase[d] + u32(r - A.recBase[lo])) : u16(0);
       w[0] = u8((p.hdr0 & 0xe0) | (hasExt ? 0x10 : 0) | cc);  // V, P copied; X per new extensions
-      w[1] = u8(((t.flags & LKF_OUT_MARKER) ? 0x80 : 0) | (dt.pt & 0x7f));
-      const u16 sn = u16(t.extSN);
-      const u32 ts = u32(t.extTS);
+      w[1] = u8(((tFlags & LKF_OUT_MARKER) ? 0x80 : 0) | (dt.pt & 0x7f));
+      const u16 sn = u16(extSN);
+      const u32 ts = u32(extTS);
       w[2] = u8(sn >> 8);
       w[3] = u8(sn);
       w[4] = u8(ts >> 24);
@@ -3192,16 +3386,16 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       int n = 12;
       const u8 *raw = A.arena + p.arenaOff;
       for (int i = 0; i < 4 * cc; i++) w[n++] = raw[12 + i];
-      if (hasExt && !(ddOn && t.ddLen > 16)) {  // pion Header.MarshalTo one-byte profile (RFC 8285)
-        const int eb = (ddOn ? 1 + t.ddLen : 0) + (playout ? 4 : 0) + (dt.extAbs ? 4 : 0) + (dt.extTcc ? 3 : 0);
+      if (hasExt && !(ddOn && tDDLen > 16)) {  // pion Header.MarshalTo one-byte profile (RFC 8285)
+        const int eb = (ddOn ? 1 + tDDLen : 0) + (playout ? 4 : 0) + (dt.extAbs ? 4 : 0) + (dt.extTcc ? 3 : 0);
         const int words = (eb + 3) >> 2;
         w[n++] = 0xBE;
         w[n++] = 0xDE;
         w[n++] = u8(words >> 8);
         w[n++] = u8(words);
         if (ddOn) {  // the DD element first (pacer/base.go:77-83)
-          w[n++] = u8((dt.extDD << 4) | (t.ddLen - 1));
-          for (int i = 0; i < t.ddLen; i++) w[n++] = A.ddArena[t.ddOff + i];
+          w[n++] = u8((dt.extDD << 4) | (tDDLen - 1));
+          for (int i = 0; i < tDDLen; i++) w[n++] = A.ddArena[tAux + i];
         }
         if (playout) {
           w[n++] = u8((dt.extPlayout << 4) | 2);
@@ -3222,15 +3416,15 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         }
         for (int i = eb; i < 4 * words; i++) w[n++] = 0;
       } else if (hasExt) {  // two-byte profile 0x1000: a DD element above 16 B
-        const int eb = 2 + t.ddLen + (playout ? 5 : 0) + (dt.extAbs ? 5 : 0) + (dt.extTcc ? 4 : 0);
+        const int eb = 2 + tDDLen + (playout ? 5 : 0) + (dt.extAbs ? 5 : 0) + (dt.extTcc ? 4 : 0);
         const int words = (eb + 3) >> 2;
         w[n++] = 0x10;
         w[n++] = 0x00;
         w[n++] = u8(words >> 8);
         w[n++] = u8(words);
         w[n++] = dt.extDD;
-        w[n++] = t.ddLen;
-        for (int i = 0; i < t.ddLen; i++) w[n++] = A.ddArena[t.ddOff + i];
+        w[n++] = tDDLen;
+        for (int i = 0; i < tDDLen; i++) w[n++] = A.ddArena[tAux + i];
         if (playout) {
           w[n++] = dt.extPlayout;
           w[n++] = 3;
@@ -3254,11 +3448,19 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         for (int i = eb; i < 4 * words; i++) w[n++] = 0;
       }
       u64 src = u64(p.arenaOff) + p.poff;
-      if (t.flags & T_CODEC) {  // translateVP8PacketTo downtrack.go:1728-1736
+      if (tFlags & T_CODEC) {  // translateVP8PacketTo downtrack.go:1728-1736: the munged
+                               // descriptor, re-marshalled from its munged fields as decide did
+        const u16 mpid = u16(tAux & 0xffffu);
+        const bool mM = mpid > 127, M = p.vbits & LKF_VP8_M;
+        const int hs = int(p.vhs) + (mM == M ? 0 : (mM ? 1 : -1));
+        u64 cb = 0;
+        const int cl = vp8_marshal(p.vfirst, p.vbits & LKF_VP8_I, mM, mpid, p.vbits & LKF_VP8_L, u8(tAux >> 16),
+                                   p.vbits & LKF_VP8_T, p.tid, p.vbits & LKF_VP8_Y, p.vbits & LKF_VP8_K,
+                                   u8(tAux >> 24), hs, cb);
 #pragma unroll
         for (int i = 0; i < 6; i++)
-          if (i < t.codecLen) w[n + i] = t.codec[i];
-        n += t.codecLen;
+          if (i < cl) w[n + i] = u8(cb >> (8 * i));
+        n += cl > 0 ? cl : 0;
         src += p.vhs;
       }
       // LDS region = prefix rounded up to 16 B, its tail filled from the
@@ -3269,11 +3471,11 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
         const u32 vw[4] = {v.x, v.y, v.z, v.w};
         for (int i = n; i < R; i++) {
           const int b = i - n;
-          w[i] = (i < int(t.outLen)) ? u8(vw[b >> 2] >> (8 * (b & 3))) : 0;
+          w[i] = (i < int(tLen)) ? u8(vw[b >> 2] >> (8 * (b & 3))) : 0;
         }
       }
       sSrc[lane] = src;
-      sLen[lane] = t.outLen;
+      sLen[lane] = tLen;
       sPre[lane] = u32(n) | (u32(R) << 16);
     }
     // first chunk of each record relative to the group's first output byte
@@ -3426,7 +3628,8 @@ __global__ void k_seq_lookup(DTHot *hot, SeqMeta *seqBase, u32 seqSize, u8 *srmB
 __global__ void __launch_bounds__(64) k_seq_dd(const u32 *__restrict__ list, u32 n, const DTHot *__restrict__ hot,
                                                const SeqMeta *__restrict__ seqBase, u32 seqSize, u8 *srmBase,
                                                u64 srmStride, u32 srmCap, const u32 *__restrict__ ddIdx, u8 *seqDD,
-                                               const Tuple *__restrict__ tuples, const u64 *__restrict__ slotBase,
+                                               const FwdRec *__restrict__ recs, const FwdBase *__restrict__ fbase,
+                                               const u64 *__restrict__ slotBase,
                                                const u32 *__restrict__ fwdCnt, const lkf_pkt *__restrict__ pkts,
                                                const u8 *__restrict__ ddArena) {
   const u32 w = blockIdx.x, lane = threadIdx.x;
@@ -3439,19 +3642,21 @@ __global__ void __launch_bounds__(64) k_seq_dd(const u32 *__restrict__ list, u32
   const SeqMeta *seq = seqBase + size_t(d) * seqSize;
   SeqRM *srm = reinterpret_cast<SeqRM *>(srmBase + size_t(d) * srmStride);
   u8 *ring = seqDD + size_t(ddIdx[d]) * seqSize * kSeqDDBytes;
-  const Tuple *tp = tuples + slotBase[d];
+  const FwdRec *tp = recs + slotBase[d];
+  const u64 bSN = fbase[d].sn;
   for (u32 c0 = 0; c0 < cnt; c0 += 64) {
     const u32 k = c0 + lane;
     if (k < cnt) {
-      const Tuple t = tp[k];
+      const FwdRec t = tp[k];
+      const u64 extSN = widen32(bSN, t.sn);
       u64 ext = 0;
-      const int slot = seq_find(h, srm, srmCap, seqSize, u16(t.extSN), ext);
-      if (slot >= 0 && ext == t.extSN && seq[slot].targetSeqNo == u16(t.extSN) &&
+      const int slot = seq_find(h, srm, srmCap, seqSize, u16(extSN), ext);
+      if (slot >= 0 && ext == extSN && seq[slot].targetSeqNo == u16(extSN) &&
           seq[slot].sourceSeqNo == u16(pkts[t.pkt].ext_sn)) {
         u8 *e = ring + size_t(slot) * kSeqDDBytes;
         const u32 len = (t.flags & T_DD) ? t.ddLen : 0u;
         e[0] = u8(len);
-        for (u32 i = 0; i < len; i++) e[1 + i] = ddArena[t.ddOff + i];
+        for (u32 i = 0; i < len; i++) e[1 + i] = ddArena[t.aux + i];
       }
     }
   }
@@ -3460,7 +3665,7 @@ __global__ void __launch_bounds__(64) k_seq_dd(const u32 *__restrict__ list, u32
 hipError_t launch_seq_dd(hipStream_t s, const SeqDDLaunch &a) {
   if (!a.n) return hipSuccess;
   hipLaunchKernelGGL(k_seq_dd, dim3(a.n), dim3(64), 0, s, a.list, a.n, a.hot, a.seq, a.seqSize, a.srm, a.srmStride,
-                     a.srmCap, a.ddIdx, a.seqDD, a.tuples, a.slotBase, a.fwdCnt, a.pkts, a.ddArena);
+                     a.srmCap, a.ddIdx, a.seqDD, a.recs, a.fbase, a.slotBase, a.fwdCnt, a.pkts, a.ddArena);
   return hipGetLastError();
 }
 
@@ -4208,9 +4413,13 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.tBegin = a.tBegin;
   A.tEnd = a.tEnd;
   A.slotBase = a.slotBase;
-  A.tuples = a.tuples;
+  A.recs = a.recs;
+  A.fbase = a.fbase;
   A.tupleCap = a.tupleCap;
   A.err = a.err;
+  A.ss = a.ss;
+  A.ssRing = a.ssRing;
+  A.ssGap = a.ssGap;
   A.events = a.events;
   A.evOff = a.evOff;
   A.fwdCnt = a.fwdCnt;
@@ -4375,7 +4584,8 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   A.gFirst = a.gFirst;
   A.slotBase = a.slotBase;
   A.totals = a.totals;
-  A.tuples = a.tuples;
+  A.recs = a.recs;
+  A.fbase = a.fbase;
   A.pkts = a.pkts;
   A.arena = a.arena;
   A.dts = a.dts;

@@ -140,24 +140,35 @@ struct alignas(16) SeqMeta {  // packetMeta sequencer.go:44-73 (32 B)
 };
 static_assert(sizeof(SeqMeta) == 32, "SeqMeta must be 32 B");
 
-// Decide -> emit hand-off record, one per forwarded tuple (48 B), written at
-// slot_base[dt] + j (j = DownTrack's forwarded ordinal in the batch).
-struct alignas(16) Tuple {
-  uint64_t extSN, extTS;
+// Decide -> emit hand-off record, one per forwarded tuple (24 B), written at
+// slot_base[dt] + j (j = the DownTrack's forwarded ordinal in the batch).
+// Only what emit cannot rebuild travels:
+//   - the munged SN / TS as their low 32 bits: emit widens them against the
+//     DownTrack's FwdBase (its first forwarded record of the batch); decide
+//     checks that every record lies within 2^31 of it (error bit 64 otherwise);
+//   - the munged VP8 descriptor as its three munged fields (picture id,
+//     TL0PICIDX, KEYIDX): emit re-marshals it from them and the packet's own
+//     descriptor bits (VP8.MarshalTo helpers.go:170-227), as decide did;
+//   - the layer, the header length and the incoming header size are the
+//     packet's (lkf_pkt) or recomputed by emit.
+// RTPStatsSender.Update needs none of it: decide folds it in (ss_fold).
+struct alignas(8) FwdRec {
+  uint32_t sn, ts;    // low 32 bits of the munged extended SN / TS
   uint32_t pkt;
-  uint32_t relOff;    // byte offset in the DownTrack's output region
+  uint32_t rel16;     // byte offset in the DownTrack's output region / 16 (packets are 16-B aligned)
   uint16_t outLen;
   uint8_t flags;      // lkf_out flags | T_DD | T_PLAYOUT | T_CODEC
-  int8_t layer;
-  uint8_t codecLen;
-  uint8_t codec[6];
   uint8_t ddLen;      // dependency-descriptor extension bytes (T_DD)
-  uint16_t hdrLen;    // RTP header incl. extension block
-  uint16_t pad0;
-  uint32_t ddOff;     // offset of the DD bytes in the batch's DD arena
-  uint32_t pad1;
+  uint32_t aux;       // T_CODEC: munged picture id | TL0PICIDX << 16 | KEYIDX << 24; T_DD: DD arena offset
 };
-static_assert(sizeof(Tuple) == 48, "Tuple must be 48 B");
+static_assert(sizeof(FwdRec) == 24, "FwdRec must be 24 B");
+struct alignas(16) FwdBase {  // per DownTrack and batch: its first forwarded record's munged SN / TS
+  uint64_t sn, ts;
+};
+// a record's 64-bit value from its low 32 bits and the DownTrack's base
+__host__ __device__ inline uint64_t widen32(uint64_t base, uint32_t lo) {
+  return base + uint64_t(int64_t(int32_t(lo - uint32_t(base))));
+}
 enum : uint8_t { T_DD = 0x20, T_PLAYOUT = 0x40, T_CODEC = 0x80 };
 
 // ---- dependency descriptor (AV1 / VP9 SVC, §8(a) a9 + a16) -----------------

@@ -27,9 +27,12 @@ struct DecideLaunch {
   const lkf_pkt *pkts;
   const uint32_t *tBegin, *tEnd;
   const uint64_t *slotBase;
-  Tuple *tuples;
+  FwdRec *recs;     // forwarded records at slotBase[dt] + j
+  FwdBase *fbase;   // per DownTrack: the base of its records' 32-bit SN / TS
   uint64_t tupleCap;
   uint32_t *err;
+  SenderStats *ss;  // RTPStatsSender per DownTrack, updated by decide (snInfo ring, gap histogram)
+  uint32_t *ssRing, *ssGap;
   const DevEvent *events;
   const uint32_t *evOff;
   uint32_t *fwdCnt;
@@ -53,7 +56,8 @@ struct EmitLaunch {
   const uint32_t *perm;  // output position -> DownTrack
   const uint64_t *recBase, *byteBase, *slotBase, *totals;  // recBase/byteBase by position
   const uint32_t *gFirst;  // [group] position owning record 64*group (k_scan_down mode 1)
-  const Tuple *tuples;
+  const FwdRec *recs;
+  const FwdBase *fbase;
   const lkf_pkt *pkts;
   const uint8_t *arena;
   const DevDT *dts;
@@ -384,7 +388,8 @@ struct SeqDDLaunch {
   uint32_t srmCap;
   const uint32_t *ddIdx;  // DownTrack -> ring index
   uint8_t *seqDD;         // [ring index][slot] kSeqDDBytes
-  const Tuple *tuples;
+  const FwdRec *recs;
+  const FwdBase *fbase;
   const uint64_t *slotBase;
   const uint32_t *fwdCnt;
   const lkf_pkt *pkts;
@@ -397,17 +402,6 @@ hipError_t launch_rtx_dd(hipStream_t s, uint32_t n, const lkf_rtx *rtx, const De
                          uint32_t seqSize, const uint32_t *ddIdx, const uint8_t *seqDD, uint8_t *dd);
 
 // ---- DownTrack sender statistics (sender_kernels.hip) ------------------------
-struct SenderLaunch {  // the forwarded tuples of one batch
-  const Tuple *tuples;
-  const uint64_t *slotBase;
-  const uint32_t *fwdCnt;
-  const lkf_pkt *pkts;
-  SenderStats *ss;
-  uint32_t *ring;  // kSnInfoSize per DownTrack
-  uint32_t *gap;   // kGapWords per DownTrack
-  uint32_t ndts;
-  uint32_t perThread;  // 1: one thread per DownTrack (short batches), 0: one wave
-};
 struct SenderUpd {  // one host-listed sendingPacket (padding, blank frame, RTX)
   uint64_t esn, ets;
   int64_t t;
@@ -423,7 +417,6 @@ struct SenderListLaunch {
   uint32_t *ring;
   uint32_t *gap;
 };
-hipError_t launch_sender_stats(hipStream_t s, const SenderLaunch &a);
 hipError_t launch_sender_updates(hipStream_t s, const SenderListLaunch &a);
 
 }  // namespace lkf

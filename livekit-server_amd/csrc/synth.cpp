@@ -663,9 +663,11 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       sp.twcc_ext = 5;  // transport-cc (video datagrams carry it; audio ones do not)
       // publishers negotiate NACK feedback for Opus and every video codec
       // (pkg/rtc/config.go:92-101): each Buffer gets a NackQueue; RTTs vary
-      // (a quarter keep the queue's default)
+      // (a quarter keep the queue's default), keyed by the track's SSRC so a
+      // room draws the same RTTs in any shard of rooms
       sp.nack = 1;
-      sp.rtt_ms = (ti % 4 == 0) ? 0u : u32(20 + (ti * 37 + u32(l) * 11) % 130);
+      const u32 rk = tg[ti].ssrc[0];
+      sp.rtt_ms = (rk % 4 == 0) ? 0u : u32(20 + (rk * 37u + u32(l) * 11) % 130);
       tr->streams.push_back(sp);
     }
   }

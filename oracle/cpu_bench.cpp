@@ -13,6 +13,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -31,6 +32,9 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
 int orc_get_stats(orc_engine *e, lkf_stats *out);
 int orc_ingest(orc_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t *raw, uint64_t raw_len);
 int orc_ingested_ptr(orc_engine *e, const lkf_pkt **pkts, uint32_t *n);
+int orc_get_state(orc_engine *e, int32_t dt, lkf_fwd_state *o);
+int orc_sender_stats_get(orc_engine *e, int32_t dt, lkf_sender_stats *o);
+int orc_stream_stats_get(orc_engine *e, int32_t s, lkf_stream_stats *o);
 
 // one batch of a shard (pointers into the synthetic trace)
 typedef struct orc_bench_batch {
@@ -54,6 +58,77 @@ typedef struct orc_bench_shard {
   uint32_t ntracks, ndts, nstreams, nbatches;
 } orc_bench_shard;
 
+// per shard, after its last batch (the engine still alive): nullptr, or a
+// callback that reads its state out
+struct ShardDone {
+  virtual void done(uint32_t shard, orc_engine *e, const lkf_stats &cum) = 0;
+};
+static int drive(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthreads, int ingress, uint32_t seq_size,
+                 uint64_t *forwarded, double *busy_s, double *wall_s, ShardDone *after);
+
+int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthreads, int ingress,
+                  uint32_t seq_size, uint64_t *forwarded, double *busy_s, double *wall_s) {
+  return drive(shards, nshards, nthreads, ingress, seq_size, forwarded, busy_s, wall_s, nullptr);
+}
+
+// bench.py's parity gate (outside its timed region): the same shards run to
+// the end, then per shard its cumulative counters (cum[shard]) and, per
+// DownTrack, {ssrc, lkf_fwd_state, lkf_sender_stats} (dtRecs, shards' DownTracks
+// in order, stride dtStride bytes) and per stream {ssrc, lkf_stream_stats}
+// (stRecs, stride stStride; ingress only).  SSRCs key the records to the GPU
+// engine's DownTracks and streams (a room shard keeps its rooms' SSRCs).
+int orc_parity_run(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthreads, int ingress,
+                   uint32_t seq_size, lkf_stats *cum, uint8_t *dtRecs, uint64_t dtStride, uint8_t *stRecs,
+                   uint64_t stStride) {
+  struct Reader : ShardDone {
+    const orc_bench_shard *sh;
+    uint32_t n;
+    lkf_stats *cum;
+    uint8_t *dt, *st;
+    uint64_t dtStride, stStride;
+    int rc = 0;
+    void done(uint32_t i, orc_engine *e, const lkf_stats &c) override {
+      uint64_t d0 = 0, s0 = 0;
+      for (uint32_t k = 0; k < i; k++) {
+        d0 += sh[k].ndts;
+        s0 += sh[k].nstreams;
+      }
+      cum[i] = c;
+      for (uint32_t d = 0; d < sh[i].ndts; d++) {
+        uint8_t *r = dt + (d0 + d) * dtStride;
+        std::memcpy(r, &sh[i].dts[d].ssrc, 4);
+        lkf_fwd_state fs{};
+        lkf_sender_stats ss{};
+        if (orc_get_state(e, int32_t(d), &fs) || orc_sender_stats_get(e, int32_t(d), &ss)) rc = -1;
+        std::memcpy(r + 8, &fs, sizeof(fs));
+        std::memcpy(r + 8 + sizeof(fs), &ss, sizeof(ss));
+      }
+      if (st)
+        for (uint32_t k = 0; k < sh[i].nstreams; k++) {
+          uint8_t *r = st + (s0 + k) * stStride;
+          std::memcpy(r, &sh[i].streams[k].ssrc, 4);
+          lkf_stream_stats ts{};
+          if (orc_stream_stats_get(e, int32_t(k), &ts)) rc = -1;
+          std::memcpy(r + 8, &ts, sizeof(ts));
+        }
+    }
+  } rd;
+  rd.sh = shards;
+  rd.n = nshards;
+  rd.cum = cum;
+  rd.dt = dtRecs;
+  rd.st = ingress ? stRecs : nullptr;
+  rd.dtStride = dtStride;
+  rd.stStride = stStride;
+  if (dtStride < 8 + sizeof(lkf_fwd_state) + sizeof(lkf_sender_stats) ||
+      (rd.st && stStride < 8 + sizeof(lkf_stream_stats)))
+    return -22;
+  std::vector<uint64_t> fwd(nshards);
+  double wall = 0;
+  const int r = drive(shards, nshards, nthreads, ingress, seq_size, fwd.data(), nullptr, &wall, &rd);
+  return r ? r : rd.rc;
+}
+
 // Runs the shards on `nthreads` threads: every shard's engine is built
 // first (tracks, DownTracks, streams: untimed), then all threads start at one
 // barrier and pull shards from a shared counter, each shard's batches in
@@ -63,8 +138,8 @@ typedef struct orc_bench_shard {
 // seconds from the common start to the last thread's end, busy_s[t] = thread
 // t's own timed seconds (nullptr: not wanted).  0, or the first non-zero
 // return code of an oracle call.
-int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthreads, int ingress,
-                  uint32_t seq_size, uint64_t *forwarded, double *busy_s, double *wall_s) {
+static int drive(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthreads, int ingress, uint32_t seq_size,
+                 uint64_t *forwarded, double *busy_s, double *wall_s, ShardDone *after) {
   if (nthreads == 0) nthreads = 1;
   std::vector<orc_engine *> eng(nshards, nullptr);
   std::atomic<int> rc{0};
@@ -88,6 +163,7 @@ int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthr
     const orc_bench_shard &s = shards[i];
     orc_engine *e = eng[i];
     uint64_t fwd = 0;
+    lkf_stats cum{};
     int r = 0;
     for (uint32_t b = 0; b < s.nbatches && !r; b++) {
       const orc_bench_batch &x = s.batches[b];
@@ -106,8 +182,16 @@ int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthr
       lkf_stats st{};
       if (!r) r = orc_get_stats(e, &st);
       fwd += st.forwarded;
+      if (after) {
+        cum.tuples += st.tuples;
+        cum.forwarded += st.forwarded;
+        cum.out_bytes += st.out_bytes;
+        cum.arena_bytes += st.arena_bytes;
+        for (int k = 0; k < LKF_DROP_NREASONS; k++) cum.drops[k] += st.drops[k];
+      }
     }
     forwarded[i] = fwd;
+    if (after && !r) after->done(i, e, cum);
     if (r) rc = r;
   };
   for (uint32_t t = 0; t < nthreads; t++)
