@@ -371,7 +371,24 @@ int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p);
 int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p);
 /* DownTrack.Close / receiver.DeleteDownTrack. */
 int lkf_remove_downtrack(lkf_engine *e, int32_t dt);
-/* Replaces the streamtrackermanager layer offsets (SR data arrived). */
+/* Reference-layer timestamp offsets of a simulcast track
+ * (StreamTrackerManager.layerOffsets, read by GetReferenceLayerRTPTimestamp
+ * streamtrackermanager.go:660-679 on every source switch, forwarder.go:1512-1520).
+ * They change as RTCP sender reports arrive; each change is a control op of
+ * the track applied at a packet index of the next lkf_run's batch (every
+ * DownTrack of the track sees it from packet at_pkt on), with no pipeline
+ * drain.
+ *   lkf_sender_report: SetRTCPSenderReportData(layer, _, newest) (:603-627):
+ *     the newest sender report of `layer` (64-bit NTP timestamp, RTP
+ *     timestamp); the offsets it implies for (layer, i) and (i, layer)
+ *     (updateLayerOffsetLocked :561-601: reports at most 60 s apart, the other
+ *     layer's RTP timestamp carried to the reference's NTP time; 0 -> 1) apply
+ *     from packet at_pkt.  NTP times convert as mediatransportutil NtpTime.Time.
+ *   lkf_set_layer_offsets_at: the whole [ref][layer] table from packet at_pkt.
+ *   lkf_set_layer_offsets: the same from the next batch's first packet. */
+int lkf_sender_report(lkf_engine *e, int32_t track, int32_t layer, uint64_t ntp_timestamp, uint32_t rtp_timestamp,
+                      uint32_t at_pkt);
+int lkf_set_layer_offsets_at(lkf_engine *e, int32_t track, const uint32_t offsets[9], uint32_t at_pkt);
 int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9]);
 
 /* ---- control ------------------------------------------------------------ */

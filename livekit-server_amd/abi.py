@@ -418,6 +418,10 @@ def bind_engine_api(lib, prefix):
     api["remove_downtrack"] = _bind(lib, prefix + "remove_downtrack", C.c_int, [e, C.c_int32])
     api["remove_track"] = _bind(lib, prefix + "remove_track", C.c_int, [e, C.c_int32])
     api["set_layer_offsets"] = _bind(lib, prefix + "set_layer_offsets", C.c_int, [e, C.c_int32, P(C.c_uint32)])
+    api["set_layer_offsets_at"] = _bind(lib, prefix + "set_layer_offsets_at", C.c_int,
+                                        [e, C.c_int32, P(C.c_uint32), C.c_uint32])
+    api["sender_report"] = _bind(lib, prefix + "sender_report", C.c_int,
+                                 [e, C.c_int32, C.c_int32, C.c_uint64, C.c_uint32, C.c_uint32])
     api["ctl"] = _bind(lib, prefix + "ctl", C.c_int,
                        [e, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_uint32])
     api["ctl_batch"] = _bind(lib, prefix + "ctl_batch", C.c_int, [e, C.c_void_p, C.c_uint32])

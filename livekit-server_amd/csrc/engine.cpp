@@ -97,6 +97,7 @@ struct BatchCtx {
   uint64_t *dSlotBase = nullptr, *dPartA = nullptr, *dPartB = nullptr, *dTot = nullptr;
   FwdRec *dRecs = nullptr;    // decide -> emit: forwarded records at slotBase[dt] + j
   FwdBase *dFBase = nullptr;  // per DownTrack: the base of its records' 32-bit SN / TS
+  FwdBase *dWide = nullptr;   // per tuple slot: a T_WIDE record's full SN / TS
   uint32_t *dFwdCnt = nullptr;
   uint64_t *dFwdBytes = nullptr, *dRecBase = nullptr, *dByteBase = nullptr;
   uint32_t *dGFirst = nullptr;  // emit group g -> output position owning record 64g
@@ -124,6 +125,9 @@ struct BatchCtx {
   hipEvent_t decided = nullptr;  // decide stage done (decide stream)
   hipEvent_t sent = nullptr;     // sender statistics done (sender stream)
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
+  hipEvent_t ingested = nullptr;  // this context's ingest done (ingest stream)
+  bool fromIngest = false;        // the pending batch of this context is an ingest's output
+  uint64_t *dITotal = nullptr;    // that ingest's ExtPacket count (device; k_track_ranges reads it)
   bool used = false;
   // SRTP-protected copy of the output (lkf_protect; allocated on first use)
   uint8_t *dProt = nullptr;
@@ -152,6 +156,12 @@ struct lkf_engine {
   std::vector<std::pair<uint32_t, uint32_t>> sortA, sortB;  // control-op radix sort (lane, index)
   hipStream_t own = nullptr;    // copies, lookups
   hipStream_t prepS = nullptr;  // ingest + batch preparation (high priority)
+  // the ingests' stream (Buffer.calc): the prep stream.  A stream of its own
+  // (ingest n+1 beside batch n's preparation; a run's preparation waits for its
+  // ingest's event, which stays) measured 9 % slower on every step shape, even
+  // those without an ingest: one more high-priority stream than the runtime's
+  // hardware queues, so two of the engine's streams shared one (r5 A/B)
+  hipStream_t ingS = nullptr;
   hipStream_t decS = nullptr;   // decide stage (high priority)
   hipStream_t emitS = nullptr;  // emit stage (low priority)
   hipStream_t sendS = nullptr;  // sender statistics of a decided batch (low priority, beside its emit)
@@ -427,6 +437,25 @@ struct lkf_engine {
   // device -> host copies refused by the range check (CHKRANGE) since the last
   // lkf_debug_check of this engine (lkf_debug_check folds them in)
   std::atomic<uint64_t> rangeViolations{0};
+  // Sender-report-driven reference-layer offsets (StreamTrackerManager,
+  // streamtrackermanager.go:561-627): per track the newest sender report of
+  // each layer and the offsets table as of the last queued change.  Queued
+  // changes (track, at_pkt, table) expand into per-DownTrack ops of the next
+  // lkf_run (kOpLayerOffsets); tracks[t].layer_offsets is the table as of the
+  // last run (a DownTrack added now starts from it).
+  struct TrackSR {
+    uint64_t ntp[3] = {0, 0, 0};
+    uint32_t rtp[3] = {0, 0, 0};
+    uint8_t have[3] = {0, 0, 0};
+    uint32_t offs[9] = {};
+  };
+  std::vector<TrackSR> trkSR;
+  struct TrackOp {
+    uint32_t track, at;
+    uint32_t offs[9];
+  };
+  std::vector<TrackOp> trkOps;
+  uint32_t *dDTOffs = nullptr;  // per DownTrack kDTOffsWords: the offsets its Forwarder reads
   // the current batch's descriptors / DD side array are engine allocations
   // (lkf_submit / lkf_ingest*) rather than the caller's (lkf_submit_device)
   bool curOwned = false, curDDOwned = false;
@@ -524,6 +553,7 @@ static int drain_streams(lkf_engine *e) {
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   if (e->cur && e->cur != e->own) HIPCHK(hipStreamSynchronize(e->cur), "sync run stream");
   HIPCHK(hipStreamSynchronize(e->own), "sync own stream");
+  HIPCHK(hipStreamSynchronize(e->ingS), "sync ingest stream");
   HIPCHK(hipStreamSynchronize(e->prepS), "sync prep stream");
   HIPCHK(hipStreamSynchronize(e->decS), "sync decide stream");
   HIPCHK(hipStreamSynchronize(e->emitS), "sync emit stream");
@@ -670,6 +700,14 @@ static int flush_topology(lkf_engine *e) {
     HIPCHK(hipMemcpy(e->dDTs + first, e->pendDTs.data(), e->pendDTs.size() * sizeof(DevDT), hipMemcpyHostToDevice),
            "dt upload");
     HIPCHK(hipMemset(e->dDTCum + first, 0, e->pendDTs.size() * sizeof(DTCum)), "dt totals reset");
+    {  // the track's reference-layer offsets as of the last run (later changes arrive as ops)
+      std::vector<uint32_t> ro(e->pendDTs.size() * kDTOffsWords, 0u);
+      for (size_t i = 0; i < e->pendDTs.size(); i++)
+        std::memcpy(&ro[i * kDTOffsWords], e->tracks[e->pendDTs[i].track].layer_offsets, 9 * sizeof(uint32_t));
+      HIPCHK(hipMemcpy(e->dDTOffs + first * kDTOffsWords, ro.data(), ro.size() * sizeof(uint32_t),
+                       hipMemcpyHostToDevice),
+             "dt offsets upload");
+    }
     {  // NewRTPStatsSender (downtrack.go:315): zero statistics at the track's clock rate
       std::vector<SenderStats> ss(e->pendDTs.size());
       std::memset(ss.data(), 0, ss.size() * sizeof(SenderStats));
@@ -846,11 +884,13 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     for (int i = 0; i < ncu; i++) ((i % 32) < cuSplit ? mA : mB)[size_t(i / 32)] |= 1u << (i % 32);
     A(hipExtStreamCreateWithCUMask(&e->decS, words, mA.data()));
     A(hipExtStreamCreateWithCUMask(&e->prepS, words, mA.data()));
+    e->ingS = e->prepS;
     A(hipExtStreamCreateWithCUMask(&e->emitS, words, mB.data()));
     A(hipExtStreamCreateWithCUMask(&e->sendS, words, mB.data()));
   } else {
     A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
     A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
+    e->ingS = e->prepS;
     A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
     A(hipStreamCreateWithPriority(&e->sendS, hipStreamNonBlocking, leastPrio));
   }
@@ -883,6 +923,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dCum, kStatsWords));
   A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
+  A(dalloc(&e->dDTOffs, size_t(c.max_downtracks) * kDTOffsWords));
   const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
   for (auto &x : e->ctx) {
     A(dalloc(&x.dTBegin, c.max_tracks));
@@ -895,6 +936,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dTot, 4));
     A(dalloc(&x.dRecs, c.max_batch_tuples));
     A(dalloc(&x.dFBase, c.max_downtracks));
+    A(dalloc(&x.dWide, c.max_batch_tuples));
     A(dalloc(&x.dFwdCnt, c.max_downtracks));
     A(dalloc(&x.dFwdBytes, c.max_downtracks));
     A(dalloc(&x.dRecBase, c.max_downtracks));
@@ -919,6 +961,8 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(hipEventCreateWithFlags(&x.prepped, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.pulled, hipEventDisableTiming));
     A(hipEventCreateWithFlags(&x.emitted, hipEventDisableTiming));
+    A(hipEventCreateWithFlags(&x.ingested, hipEventDisableTiming));
+    A(dalloc(&x.dITotal, 2));
     A(hipEventCreateWithFlags(&x.sent, hipEventDisableTiming));
   }
   for (auto &r : e->ring)
@@ -1018,6 +1062,7 @@ void lkf_destroy(lkf_engine *e) {
   (void)hipSetDevice(e->dev);
   if (e->cur && e->cur != e->own) (void)hipStreamSynchronize(e->cur);
   if (e->own) (void)hipStreamSynchronize(e->own);
+  if (e->ingS) (void)hipStreamSynchronize(e->ingS);
   if (e->prepS) (void)hipStreamSynchronize(e->prepS);
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
@@ -1035,7 +1080,7 @@ void lkf_destroy(lkf_engine *e) {
                   static_cast<void *>(e->dAllocOut)})
     if (p) (void)dfree(p);
   void *ptrs[] = {e->dTracks,  e->dHot,  e->dDTCum, e->dDTs,    e->dRm,  e->dVc,  e->dSeq,    e->dSched,
-                  e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm,
+                  e->dWaveTrack, e->dCum, e->dSticky, e->dSns, e->dSeqOut, e->dSeqN, e->dPerm, e->dDTOffs,
                   e->dStreams, e->dStreamHot, e->dHist, e->dRxGap, e->dStreamRings,
                   e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktRing, e->dBktStream, e->dBktSn,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITRuns, e->dIErr,
@@ -1065,7 +1110,7 @@ void lkf_destroy(lkf_engine *e) {
                     static_cast<void *>(x.dDDUsed)})
       if (p) (void)dfree(p);
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
-                 x.dPartB,  x.dTot,      x.dRecs,  x.dFBase,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
+                 x.dPartB,  x.dTot,      x.dRecs,  x.dFBase,  x.dWide,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
                  x.dByteBase, x.dOut,    x.dOutArena, x.dStats,   x.dPktsOwn,  x.dArenaOwn,
                  x.dRawPkts, x.dBktStore, x.dGFirst, x.dLayerList, x.dLayerBefore, x.dLayerCnt, x.dEvents, x.dEvOff, x.dEvLane, x.dTwccBase};
     for (void *p : q)
@@ -1074,6 +1119,8 @@ void lkf_destroy(lkf_engine *e) {
     if (x.prepped) (void)hipEventDestroy(x.prepped);
     if (x.pulled) (void)hipEventDestroy(x.pulled);
     if (x.emitted) (void)hipEventDestroy(x.emitted);
+    if (x.ingested) (void)hipEventDestroy(x.ingested);
+    if (x.dITotal) (void)dfree(x.dITotal);
     if (x.sent) (void)hipEventDestroy(x.sent);
   }
   for (auto &r : e->ring)
@@ -1100,11 +1147,12 @@ void lkf_destroy(lkf_engine *e) {
                     static_cast<void *>(g.listCnt), static_cast<void *>(g.nackInfo), static_cast<void *>(g.nackPairOff),
                     static_cast<void *>(g.nackPairCnt), static_cast<void *>(g.nackPairs)})
       if (p) (void)dfree(p);
-  if (e->sideS) (void)hipStreamDestroy(e->sideS);
+  if (e->sideS && e->sideS != e->sendS) (void)hipStreamDestroy(e->sideS);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
   if (e->sendS) (void)hipStreamDestroy(e->sendS);
   if (e->decS) (void)hipStreamDestroy(e->decS);
   if (e->prepS) (void)hipStreamDestroy(e->prepS);
+  if (e->ingS && e->ingS != e->prepS) (void)hipStreamDestroy(e->ingS);
   if (e->own) (void)hipStreamDestroy(e->own);
   delete e;
 }
@@ -1118,21 +1166,76 @@ int32_t lkf_add_track(lkf_engine *e, const lkf_track_params *p) {
   if (track_has_dd(*p)) ddIdx = e->nDDTracks++;
   e->trackDD.push_back(ddIdx);
   e->trackActive.push_back(1);
+  e->trkSR.emplace_back();
+  std::memcpy(e->trkSR.back().offs, p->layer_offsets, 9 * sizeof(uint32_t));
   e->pendTracks.push_back(to_dev_track(*p, ddIdx));  // uploaded by flush_topology
   e->schedDirty = true;
   return h;
 }
 
+int lkf_set_layer_offsets_at(lkf_engine *e, int32_t track, const uint32_t offsets[9], uint32_t at_pkt) {
+  if (!e || !offsets || track < 0 || track >= int32_t(e->tracks.size())) return LKF_EINVAL;
+  lkf_engine::TrackOp op;
+  op.track = uint32_t(track);
+  op.at = at_pkt;
+  std::memcpy(op.offs, offsets, sizeof(op.offs));
+  std::memcpy(e->trkSR[size_t(track)].offs, offsets, sizeof(op.offs));
+  e->trkOps.push_back(op);
+  return LKF_OK;
+}
+
 int lkf_set_layer_offsets(lkf_engine *e, int32_t track, const uint32_t offsets[9]) {
+  return lkf_set_layer_offsets_at(e, track, offsets, 0);
+}
+
+// mediatransportutil v0.0.0-20231213075826-cccbf2b93d3f NtpTime.Duration (the
+// offset of NtpTime.Time from the NTP epoch): seconds, and the 32-bit fraction
+// in nanoseconds rounded half up
+static int64_t ntp_ns(uint64_t t) {
+  const uint64_t sec = (t >> 32) * 1000000000ull;
+  const uint64_t frac = (t & 0xffffffffull) * 1000000000ull;
+  uint64_t nsec = frac >> 32;
+  if (uint32_t(frac) >= 0x80000000u) nsec++;
+  return int64_t(sec + nsec);
+}
+
+// StreamTrackerManager.updateLayerOffsetLocked (streamtrackermanager.go:561-601)
+static bool sr_layer_offset(lkf_engine::TrackSR &s, uint32_t clockRate, int ref, int other) {
+  if (!s.have[ref] || s.ntp[ref] == 0 || !s.have[other] || s.ntp[other] == 0) return false;
+  const int64_t d = ntp_ns(s.ntp[ref]) - ntp_ns(s.ntp[other]);  // srRef.Time().Sub(srOther.Time())
+  const double secs = double(d / 1000000000) + double(d % 1000000000) / 1e9;  // Duration.Seconds
+  if (std::fabs(secs) > 60.0) return false;  // senderReportThresholdSeconds :36
+  const int64_t rtpDiff = d * int64_t(clockRate) / 1000000000;
+  const uint32_t norm = s.rtp[other] + uint32_t(rtpDiff);
+  uint32_t off = s.rtp[ref] - norm;
+  if (off == 0) off = 1;
+  const bool changed = s.offs[ref * 3 + other] != off;
+  s.offs[ref * 3 + other] = off;
+  return changed;
+}
+
+// SetRTCPSenderReportData (streamtrackermanager.go:603-627)
+int lkf_sender_report(lkf_engine *e, int32_t track, int32_t layer, uint64_t ntp_timestamp, uint32_t rtp_timestamp,
+                      uint32_t at_pkt) {
   if (!e || track < 0 || track >= int32_t(e->tracks.size())) return LKF_EINVAL;
-  int rc = flush_topology(e);
-  if (rc) return rc;
-  rc = drain_streams(e);
-  if (rc) return rc;
-  std::memcpy(e->tracks[track].layer_offsets, offsets, 9 * sizeof(uint32_t));
-  DevTrack t = to_dev_track(e->tracks[track], e->trackDD[track]);
-  HIPCHK(hipMemcpy(e->dTracks + track, &t, sizeof(t), hipMemcpyHostToDevice), "offsets copy");
-  return upload_done(e);
+  if (layer < 0 || layer > 2) return LKF_OK;  // (invalid layer: ignored, as the reference)
+  lkf_engine::TrackSR &s = e->trkSR[size_t(track)];
+  s.ntp[layer] = ntp_timestamp;
+  s.rtp[layer] = rtp_timestamp;
+  s.have[layer] = 1;
+  bool changed = false;
+  for (int i = 0; i < 3; i++) {
+    if (i == layer) continue;
+    changed |= sr_layer_offset(s, e->tracks[size_t(track)].clock_rate, layer, i);
+    changed |= sr_layer_offset(s, e->tracks[size_t(track)].clock_rate, i, layer);
+  }
+  if (!changed) return LKF_OK;
+  lkf_engine::TrackOp op;
+  op.track = uint32_t(track);
+  op.at = at_pkt;
+  std::memcpy(op.offs, s.offs, sizeof(op.offs));
+  e->trkOps.push_back(op);
+  return LKF_OK;
 }
 
 int32_t lkf_add_downtrack(lkf_engine *e, const lkf_downtrack_params *p) {
@@ -1500,6 +1603,8 @@ int lkf_run(lkf_engine *e, void *stream) {
   const uint32_t nl = uint32_t(e->sched.size());
   // this context's previous batch (run n-2) must have finished its emit stage
   if (x.used) HIPCHK(hipStreamWaitEvent(ps, x.emitted, 0), "wait emit");
+  if (x.fromIngest && e->haveBatch) HIPCHK(hipStreamWaitEvent(ps, x.ingested, 0), "wait ingest");
+  x.fromIngest = false;
 
   // Per-lane control-op CSR (stable: queue order within a lane, then by
   // at_pkt).  The host sorts only the ops: an LSD radix sort on the lane
@@ -1511,6 +1616,28 @@ int lkf_run(lkf_engine *e, void *stream) {
   const auto tp1 = clk::now();
   if (x.used) HIPCHK(hipEventSynchronize(x.pulled), "stage wait");  // run n-3's pull of this staging is done
   const auto tp2 = clk::now();
+  if (!e->trkOps.empty()) {  // a track's layer-offset changes: one op per active DownTrack of it
+    std::stable_sort(e->trkOps.begin(), e->trkOps.end(), [](const lkf_engine::TrackOp &a, const lkf_engine::TrackOp &b) {
+      return a.track != b.track ? a.track < b.track : a.at < b.at;
+    });
+    std::vector<std::vector<uint32_t>> byT(nt);
+    for (uint32_t d = 0; d < nd; d++)
+      if (e->active[d]) byT[e->dtp[d].track].push_back(d);
+    for (const auto &op : e->trkOps) {
+      lkf_engine::Pend q;
+      std::memset(&q.ev, 0, sizeof(q.ev));
+      q.ev.at = op.at;
+      q.ev.op = kOpLayerOffsets;
+      for (int k = 0; k < 4; k++) q.ev.a[k] = int64_t(uint64_t(op.offs[2 * k]) | (uint64_t(op.offs[2 * k + 1]) << 32));
+      q.ev.pad = int64_t(op.offs[8]);
+      for (uint32_t d : byT[op.track]) {
+        q.dt = d;
+        e->pending.push_back(q);
+      }
+      std::memcpy(e->tracks[op.track].layer_offsets, op.offs, sizeof(op.offs));  // as of the end of this run
+    }
+    e->trkOps.clear();
+  }
   auto &ka = e->sortA, &kb = e->sortB;  // (lane, pending index)
   ka.clear();
   for (uint32_t i = 0; i < uint32_t(e->pending.size()); i++) {
@@ -1702,9 +1829,11 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.slotBase = x.dSlotBase;
   d.recs = x.dRecs;
   d.fbase = x.dFBase;
+  d.wide = x.dWide;
   d.ss = e->dSS;
   d.ssRing = e->dSSRing;
   d.ssGap = e->dSSGap;
+  d.dtOffs = e->dDTOffs;
   d.tupleCap = e->cfg.max_batch_tuples;
   d.err = x.dErr;
   d.events = x.dEvents;
@@ -1766,6 +1895,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     q.seqDD = e->dSeqDD;
     q.recs = x.dRecs;
     q.fbase = x.dFBase;
+    q.wide = x.dWide;
     q.slotBase = x.dSlotBase;
     q.fwdCnt = x.dFwdCnt;
     q.pkts = e->curPkts;
@@ -1787,6 +1917,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   m.totals = x.dTot + 2;
   m.recs = x.dRecs;
   m.fbase = x.dFBase;
+  m.wide = x.dWide;
   m.pkts = e->curPkts;
   m.arena = e->curArena;
   m.dts = e->dDTs;
@@ -1868,10 +1999,6 @@ int lkf_sync(lkf_engine *e) {
   if (acc & 32u) {
     e->err = "internal: a DownTrack with padding exclusions was decided by the plain kernel";
     return LKF_EINVAL;
-  }
-  if (acc & 64u) {
-    e->err = "a DownTrack's munged RTP sequence numbers or timestamps spread over 2^31 or more within one batch";
-    return LKF_ENOSPC;
   }
   if (acc & 16u) {
     e->err = "dependency descriptor unreadable, missing its lkf_pkt_dd entry, or beyond an engine limit";
@@ -3441,7 +3568,7 @@ static void IngSetSelect(lkf_engine *e, int par) {
 static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, uint32_t n, const uint8_t *dRaw,
                          uint64_t rawLen) {
   const uint32_t nt = uint32_t(e->tracks.size());
-  hipStream_t s = e->prepS;
+  hipStream_t s = e->ingS;
   // the batch's GPU span (lkf_timing_window total) starts before its ingest
   HIPCHK(hipEventRecord(e->ring[e->nRuns % lkf_engine::kRing][0], s), "event");
   e->ingestStarted = true;
@@ -3475,7 +3602,7 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.pos = e->dPos;
   a.partA = e->dIPartA;
   a.partB = e->dIPartB;
-  a.total = e->dITotal;
+  a.total = x.dITotal;
   a.out = x.dPktsOwn;
   a.list = e->dIList;
   a.listCnt = e->dIListCnt;
@@ -3533,13 +3660,15 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
     e->bktStorePending = true;
   }
   HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 8), "ingest error fold");
+  HIPCHK(hipEventRecord(x.ingested, s), "event");  // the run's preparation (prep stream) waits for it
+  x.fromIngest = true;
   e->lastIngestN = n;
   e->ingRaws = dRaws;
   e->curPkts = x.dPktsOwn;
-  e->curN = n;  // launch bound; the count is e->dITotal
-  // (an empty ingest launches nothing, so dITotal still holds the previous
+  e->curN = n;  // launch bound; the count is x.dITotal
+  // (an empty ingest launches nothing, so dITotal still holds an older
   // ingest's count: the batch is empty, with no device-side count)
-  e->curNDev = n ? e->dITotal : nullptr;
+  e->curNDev = n ? x.dITotal : nullptr;
   e->curDD = a.outDD;  // the ExtPackets' descriptors (nullptr: no DD stream)
   e->curOwned = true;
   e->curDDOwned = true;
@@ -3556,20 +3685,20 @@ int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
   if (rc) return rc;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
-  if (x.used) HIPCHK(hipStreamWaitEvent(e->prepS, x.emitted, 0), "wait emit");  // batch n-2 reads these buffers
+  if (x.used) HIPCHK(hipStreamWaitEvent(e->ingS, x.emitted, 0), "wait emit");  // batch n-3 reads these buffers
   if (e->haveBatch && e->curPkts == x.dPktsOwn) {
     // a second ingest into this context before lkf_run: the previous ingest's
     // NACK queues (side stream) and bucket copies (sender stream) still read
     // the datagrams these copies overwrite
     const int lp = e->ingPar;
-    if (e->sidePending[lp]) HIPCHK(hipStreamWaitEvent(e->prepS, e->sideDone[lp], 0), "wait nack queues");
-    if (e->bktPending[lp]) HIPCHK(hipStreamWaitEvent(e->prepS, e->bktDone[lp], 0), "wait bucket copies");
+    if (e->sidePending[lp]) HIPCHK(hipStreamWaitEvent(e->ingS, e->sideDone[lp], 0), "wait nack queues");
+    if (e->bktPending[lp]) HIPCHK(hipStreamWaitEvent(e->ingS, e->bktDone[lp], 0), "wait bucket copies");
   }
-  if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->prepS),
+  if (n) HIPCHK(hipMemcpyAsync(x.dRawPkts, pkts, size_t(n) * sizeof(lkf_raw_pkt), hipMemcpyHostToDevice, e->ingS),
                 "raw pkts");
-  if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->prepS), "raw arena");
+  if (raw_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, raw, raw_len, hipMemcpyHostToDevice, e->ingS), "raw arena");
   // host buffers are reusable when lkf_ingest returns (the header's contract)
-  HIPCHK(hipStreamSynchronize(e->prepS), "ingest copy sync");
+  HIPCHK(hipStreamSynchronize(e->ingS), "ingest copy sync");
   return ingest_common(e, x, x.dRawPkts, n, x.dArenaOwn, raw_len);
 }
 
@@ -3580,7 +3709,7 @@ int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, cons
   if (rc) return rc;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
-  if (x.used) HIPCHK(hipStreamWaitEvent(e->prepS, x.emitted, 0), "wait emit");
+  if (x.used) HIPCHK(hipStreamWaitEvent(e->ingS, x.emitted, 0), "wait emit");
   return ingest_common(e, x, d_pkts, n, d_raw, raw_len);
 }
 
@@ -3589,7 +3718,7 @@ int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out
   *n_out = e->lastIngestN;
   if (cap < e->lastIngestN) return LKF_ENOSPC;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
+  HIPCHK(hipStreamSynchronize(e->ingS), "sync");
   if (e->lastIngestN)
     D2H(out, e->dFlows, size_t(e->lastIngestN) * sizeof(lkf_flow), "flows");
   return LKF_OK;
@@ -3600,7 +3729,7 @@ int lkf_ingest_twcc(lkf_engine *e, uint32_t *out, uint32_t cap, uint32_t *n_out)
   *n_out = e->lastIngestN;
   if (cap < e->lastIngestN) return LKF_ENOSPC;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
+  HIPCHK(hipStreamSynchronize(e->ingS), "sync");
   if (e->lastIngestN)
     D2H(out, e->dTwcc, size_t(e->lastIngestN) * sizeof(uint32_t), "twcc");
   return LKF_OK;
@@ -3609,7 +3738,7 @@ int lkf_ingest_twcc(lkf_engine *e, uint32_t *out, uint32_t cap, uint32_t *n_out)
 int lkf_ingested(lkf_engine *e, lkf_pkt *out, uint32_t cap, uint32_t *n_out) {
   if (!e || !n_out) return LKF_EINVAL;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
+  HIPCHK(hipStreamSynchronize(e->ingS), "sync");
   uint32_t n = 0;
   if (e->haveBatch) {
     n = e->curN;
@@ -3631,7 +3760,7 @@ int lkf_ingested_dd(lkf_engine *e, lkf_pkt_dd *out, uint32_t cap, uint32_t *n_ou
   if (!e || !n_out) return LKF_EINVAL;
   uint32_t n = 0;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
-  HIPCHK(hipStreamSynchronize(e->prepS), "sync");
+  HIPCHK(hipStreamSynchronize(e->ingS), "sync");
   if (e->haveBatch) {
     n = e->curN;
     if (e->curNDev) {
@@ -3813,7 +3942,7 @@ int lkf_speakers_enqueue(lkf_engine *e, int64_t now_ns) {
   a.nowNs = now_ns;
   a.slots = e->dSpkSlots;
   a.counts = e->dSpkCounts;
-  HIPCHK(launch_speakers(e->prepS, a), "speakers");
+  HIPCHK(launch_speakers(e->ingS, a), "speakers");
   return LKF_OK;
 }
 
@@ -3841,19 +3970,19 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
   a.nowNs = now_ns;
   a.slots = e->dSpkSlots;
   a.counts = e->dSpkCounts;
-  // decide stream: ordered after the ingest that updated the levels
-  HIPCHK(launch_speakers(e->prepS, a), "speakers");
+  // the ingest stream: ordered after the ingest that updated the levels
+  HIPCHK(launch_speakers(e->ingS, a), "speakers");
   std::vector<uint32_t> counts(e->nRooms);
   std::vector<lkf_speaker> slots(size_t(e->nRooms) * 64);
   CHKRANGE(e->dSpkCounts, counts.size() * sizeof(uint32_t), "async d2h");
   HIPCHK(hipMemcpyAsync(counts.data(), e->dSpkCounts, counts.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        e->prepS),
+                        e->ingS),
          "counts copy");
   CHKRANGE(e->dSpkSlots, slots.size() * sizeof(lkf_speaker), "async d2h");
   HIPCHK(hipMemcpyAsync(slots.data(), e->dSpkSlots, slots.size() * sizeof(lkf_speaker), hipMemcpyDeviceToHost,
-                        e->prepS),
+                        e->ingS),
          "slots copy");
-  HIPCHK(hipStreamSynchronize(e->prepS), "speakers sync");
+  HIPCHK(hipStreamSynchronize(e->ingS), "speakers sync");
   uint32_t k = 0;
   for (uint32_t r = 0; r < e->nRooms; r++) k += counts[r];
   *n_out = k;

@@ -200,8 +200,10 @@ __device__ __forceinline__ void wave_lds_sync() { __syncthreads(); }
 // ---------------------------------------------------------------------------
 struct Lane {
   DTHot &h;  // the wave's DownTrack state, staged in LDS (no SGPR pressure / spill traffic)
-  RangeEntry *rm;  // the closed-range ring, staged in LDS for the batch
-  bool rmDirty;    // a closed range was written (write the ring back)
+  RangeEntry *rm;  // the closed-range ring (decide: in LDS, filled on first lookup; padding: HBM)
+  RangeEntry *rmG; // the ring in HBM
+  u32 rmNew;       // closed ranges appended since the ring was staged (the newest ones; written back)
+  bool rmLoaded;   // the older live ranges are in L.rm (rm_load)
   bool vcDirty;    // a VP8 munger map changed (write the maps back)
   VP8Cold *vc;
   i32 *dropKey;  // LDS copy of vc->dropKey
@@ -214,7 +216,7 @@ struct Lane {
   u32 srmCap;
   // track
   u32 kind, codec, hasRefTS, clockRate;
-  const u32 *offs;
+  u32 *offs;  // the DownTrack's reference-layer offsets row (HBM; read on a source switch)
   // static DT
   u8 extPlayout, extAbs, extDD, extTcc;
   // dependency-descriptor selector (F_DD): state staged in LDS, the track's
@@ -241,10 +243,26 @@ __device__ __forceinline__ RangeEntry rm_at(const Lane &L, int i) {  // i-th clo
   int idx = (int(L.h.rmHead) + i) % kRangeCap;
   return L.rm[idx];
 }
+// The decide wave stages the ring lazily: the common path only appends
+// (rm_exclude) and never reads it, so the live ranges older than this batch's
+// appends come from HBM only when a lookup first needs them (wave-uniform).
+__device__ __forceinline__ void rm_load(Lane &L) {
+  if (L.rmLoaded) return;
+  L.rmLoaded = true;
+  const u32 nc = L.h.rmCount, old = nc - min(L.rmNew, nc);
+  if (!old) return;
+  wave_lds_sync();
+  for (u32 i = lane_id(); i < old; i += 64) {
+    const u32 idx = (u32(L.h.rmHead) + i) % kRangeCap;
+    L.rm[idx] = L.rmG[idx];
+  }
+  wave_lds_sync();
+}
 // ClearAndResetValue rangemap.go:66
 __device__ __forceinline__ void rm_reset(Lane &L, u64 start, u64 val) {
   L.h.rmHead = 0;
   L.h.rmCount = 0;
+  L.rmNew = 0;  // (no live range left to stage or write back)
   L.h.rmOpenStart = start;
   L.h.rmOpenValue = val;
 }
@@ -270,7 +288,7 @@ __device__ __forceinline__ bool rm_exclude(Lane &L, u64 s, u64 e) {
     L.rm[L.h.rmHead] = c;
     L.h.rmHead = u16((L.h.rmHead + 1) % kRangeCap);
   }
-  L.rmDirty = true;
+  L.rmNew++;
   L.h.rmOpenStart = e;
   L.h.rmOpenValue = nv;
   return true;
@@ -280,7 +298,7 @@ __device__ __forceinline__ bool rm_exclude(Lane &L, u64 s, u64 e) {
 // range i", then "key strictly between range i-1 and range i" (-> miss).  The
 // first hit of that walk is the hit with the largest index (inside before
 // between at equal index), so each lane tests one index and a ballot picks it.
-__device__ __forceinline__ bool rm_get(const Lane &L, u64 key, u64 &out) {
+__device__ __forceinline__ bool rm_get(Lane &L, u64 key, u64 &out) {
   out = 0;
   if (key >= L.h.rmOpenStart) {
     out = L.h.rmOpenValue;
@@ -288,6 +306,7 @@ __device__ __forceinline__ bool rm_get(const Lane &L, u64 key, u64 &out) {
   }
   const int nc = L.h.rmCount;
   if (nc == 0) return false;  // key < open start = first start
+  rm_load(L);
   if (key < rm_at(L, 0).start) return false;
   const u32 l = lane_id();
   int best = -1;
@@ -785,6 +804,11 @@ __device__ __forceinline__ void apply_ctl(Lane &L, const DevEvent &ev) {
     case LKF_CTL_PLAYOUT_ACKED:
       setf(L, F_PLAYOUT_ACKED, ev.a[0] != 0);
       break;
+    case kOpLayerOffsets: {  // the track's layerOffsets from this packet on (lkf_sender_report)
+      const u32 l = lane_id();
+      if (l < 9) L.offs[l] = l < 8 ? u32(u64(ev.a[l >> 1]) >> (32 * (l & 1))) : u32(u64(ev.pad));
+      break;
+    }
     default:
       break;
   }
@@ -1086,9 +1110,14 @@ __device__ __forceinline__ u32 pack4(u8 a, u8 b, u8 c, u8 d) {
 struct __attribute__((aligned(8))) U4x8 {  // 16 B at an 8-B aligned address (one dwordx4 access)
   u32 x, y, z, w;
 };
-// a forwarded record (FwdRec): one dwordx4 + one dwordx2 store
-__device__ __forceinline__ void store_fwd(FwdRec *dst, u64 sn, u64 ts, u32 pkt, u32 relOff, u32 outLen, u32 flags,
-                                          u32 ddLen, u32 aux) {
+// a forwarded record (FwdRec): one dwordx4 + one dwordx2 store; its full SN /
+// TS go to the wide side array too when they lie 2^31 or more from the base
+__device__ __forceinline__ void store_fwd(FwdRec *dst, FwdBase *wdst, u64 bSN, u64 bTS, u64 sn, u64 ts, u32 pkt,
+                                          u32 relOff, u32 outLen, u32 flags, u32 ddLen, u32 aux) {
+  if ((((sn - bSN) + 0x80000000ull) >> 32) != 0 || (((ts - bTS) + 0x80000000ull) >> 32) != 0) {
+    flags |= T_WIDE;
+    *wdst = FwdBase{sn, ts};
+  }
   *reinterpret_cast<U4x8 *>(dst) = U4x8{u32(sn), u32(ts), pkt, relOff >> 4};
   reinterpret_cast<uint2 *>(dst)[2] = make_uint2(outLen | (flags << 16) | (ddLen << 24), aux);
 }
@@ -1570,10 +1599,12 @@ struct DecideArgs {
   const u64 *slotBase;
   FwdRec *recs;
   FwdBase *fbase;  // per DownTrack: its first forwarded record's munged SN / TS (FwdRec widening)
+  FwdBase *wide;   // per tuple slot: the full SN / TS of a T_WIDE record
   u64 tupleCap;
   u32 *err;
   SenderStats *ss;  // RTPStatsSender per DownTrack (+ snInfo ring, gap histogram)
   u32 *ssRing, *ssGap;
+  u32 *dtOffs;      // per DownTrack reference-layer offsets (kDTOffsWords)
   const DevEvent *events;
   const u32 *evOff;  // per lane [evOff[l], evOff[l+1])
   u32 *fwdCnt;
@@ -1603,6 +1634,7 @@ struct SsEnt;
 // Per (packet, DownTrack) body of DownTrack.WriteRTP (downtrack.go:680-760).
 struct LaneOut {
   FwdRec *outT;
+  FwdBase *outW;  // the wide side array at this DownTrack's first slot (T_WIDE records)
   u64 nFwd, nBytes, nTuples;
   u64 bSN, bTS;  // the batch's first forwarded munged SN / TS (FwdBase)
   SenderStats *ss;  // the DownTrack's RTPStatsSender, staged in LDS
@@ -1766,19 +1798,12 @@ __device__ __forceinline__ void ss_flush(SenderStats &S, u32 *ring, u32 *gap, co
   }
 }
 
-// FwdBase: a DownTrack's first forwarded record of the batch sets it; every
-// record's munged SN / TS must lie within 2^31 of it (FwdRec carries their low
-// 32 bits) — error bit 64 (LKF_ENOSPC at lkf_sync) otherwise
-__device__ __forceinline__ void fwd_base(LaneOut &o, u32 *err, u64 fwM, u64 osn, u64 ots) {
-  if (!fwM) return;
-  if (o.nFwd == 0) {
-    const u32 f0 = u32(__ffsll((long long)fwM) - 1);
-    o.bSN = rl64(osn, f0);
-    o.bTS = rl64(ots, f0);
-  }
-  const bool act = (fwM >> lane_id()) & 1;
-  const bool wide = act && ((((osn - o.bSN) + 0x80000000ull) >> 32) != 0 || (((ots - o.bTS) + 0x80000000ull) >> 32) != 0);
-  if (__ballot(wide) && lane_id() == 0) atomicOr(err, 64u);
+// FwdBase: a DownTrack's first forwarded record of the batch sets it
+__device__ __forceinline__ void fwd_base(LaneOut &o, u64 fwM, u64 osn, u64 ots) {
+  if (!fwM || o.nFwd != 0) return;
+  const u32 f0 = u32(__ffsll((long long)fwM) - 1);
+  o.bSN = rl64(osn, f0);
+  o.bTS = rl64(ots, f0);
 }
 
 template <bool DDK>
@@ -1914,9 +1939,10 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 #if LKF_CHECKED
   CHK(o.tupBase + o.nFwd < o.tupCap, CK_DEC_TUPLE, o.tupBase + o.nFwd, o.tupCap);
 #endif
-  fwd_base(o, L.err, 1ull, f.osn, f.ots);
+  fwd_base(o, 1ull, f.osn, f.ots);
   if (lane_id() == 0)  // wave-uniform record: one lane stores it
-    store_fwd(o.outT + o.nFwd, f.osn, f.ots, k, o.relOff, u32(hdrLen + payLen), flags, ddLen, aux);
+    store_fwd(o.outT + o.nFwd, o.outW + o.nFwd, o.bSN, o.bTS, f.osn, f.ots, k, o.relOff, u32(hdrLen + payLen), flags,
+              ddLen, aux);
   // sequencer.push (downtrack.go:724-735)
   seq_push<DDK>(L, p.arr / 1000000LL, p.esn, f.osn, f.ots, marker, p.layer, f.cb, f.cbLen);
   // sendingPacket -> RTPStatsSender.Update start (rtpstats_sender.go:245-262)
@@ -1958,7 +1984,10 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 // the whole wave on the broadcast packet, and the run restarts after it.
 // ---------------------------------------------------------------------------
 
-#define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
+#ifndef LKF_DECIDE_WAVES  // occupancy floor (waves per SIMD); 4 and 6 measured slower (r3, r5)
+#define LKF_DECIDE_WAVES 5
+#endif
+#define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(LKF_DECIDE_WAVES, 8)))
 
 // Consume the chunk's descriptor registers here, once.  gfx9 counts stores in
 // vmcnt too: a first use sunk into the run loop would wait there for every
@@ -2438,12 +2467,12 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   }
   const bool kf = p.flags & LKF_PKT_KEYFRAME;
   const u32 j = u32(__popcll(fwR & lt));
-  fwd_base(o, L.err, fwR, osn, ots);
+  fwd_base(o, fwR, osn, ots);
   if (f) {
 #if LKF_CHECKED
     CHK(o.tupBase + o.nFwd + j < o.tupCap, CK_DEC_TUPLE, o.tupBase + o.nFwd + j, o.tupCap);
 #endif
-    store_fwd(o.outT + o.nFwd + j, osn, ots, pi, o.relOff + relEx, outLen,
+    store_fwd(o.outT + o.nFwd + j, o.outW + o.nFwd + j, o.bSN, o.bTS, osn, ots, pi, o.relOff + relEx, outLen,
               (kf ? LKF_OUT_KEYFRAME : 0) | (mk ? LKF_OUT_MARKER : 0) | (playout ? T_PLAYOUT : 0) | (ddKeep ? T_DD : 0),
               ddKeep ? u32(ddLen) : 0u, ddKeep ? ddOff : 0u);
     u32 slot = u32(L.h.seqHighSlot) + u32(osn - L.h.seqExtHighestSN);  // sequencer.push, in order
@@ -2637,7 +2666,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __syncthreads();
   RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
   L.rm = sRm;
-  L.rmDirty = false;
+  L.rmG = rmG;
+  L.rmNew = 0;
+  L.rmLoaded = false;
   L.vcDirty = false;
   L.vc = A.vc + d;
   L.dropKey = sDrop;
@@ -2656,10 +2687,6 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       sMissVal[idx] = L.vc->missVal[idx];
     }
   }
-  for (u32 i = lane; i < L.h.rmCount; i += 64) {  // live closed ranges of the RangeMap ring
-    const u32 idx = (L.h.rmHead + i) % kRangeCap;
-    sRm[idx] = rmG[idx];
-  }
   if (slot0 + (pe - pb) > A.tupleCap) {  // tuple slots exhausted: skip, flag
     if (lane == 0) atomicOr(A.err, 8u);
     pe = pb;
@@ -2674,7 +2701,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.codec = tk.codec;
   L.hasRefTS = tk.hasRefTS;
   L.clockRate = tk.clockRate;
-  L.offs = tk.layerOffsets;
+  L.offs = A.dtOffs + size_t(d) * kDTOffsWords;
   L.extPlayout = dt.extPlayout;
   L.extAbs = dt.extAbs;
   L.extDD = dt.extDD;
@@ -2714,6 +2741,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     }
   }
   o.outT = A.recs + slot0;
+  o.outW = A.wide + slot0;
   // SVC DownTracks (one SSRC, every packet relevant to the selector): svc_run
   // (the host schedules them in k_decide_dt<true>)
   const bool svcDT = 0 != 5 && DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
@@ -2991,12 +3019,12 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const u32 relEx = excl_scan_u32(aligned, lane);
         const bool marker = pktMarker;  // tp.marker (= hdr.Marker for video, false for audio) || hdr.Marker
         const u32 j = u32(__popcll(fwR & lt));
-        fwd_base(o, L.err, fwR, osn, ots);
+        fwd_base(o, fwR, osn, ots);
         if (fwd) {
 #if LKF_CHECKED
           CHK(slot0 + o.nFwd + j < A.tupleCap, CK_DEC_TUPLE, slot0 + o.nFwd + j, A.tupleCap);
 #endif
-          store_fwd(o.outT + o.nFwd + j, osn, ots, pi, o.relOff + relEx, outLen,
+          store_fwd(o.outT + o.nFwd + j, o.outW + o.nFwd + j, o.bSN, o.bTS, osn, ots, pi, o.relOff + relEx, outLen,
                     ((p.flags & LKF_PKT_KEYFRAME) ? LKF_OUT_KEYFRAME : 0) | (marker ? LKF_OUT_MARKER : 0) |
                         (playout ? T_PLAYOUT : 0) | (useCodec ? T_CODEC : 0),
                     0u, useCodec ? vp8_aux(mpid, mtl0, mkey) : 0u);
@@ -3147,10 +3175,11 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
   if (o.nFwd && lane < sizeof(SenderStats) / 16)  // (only a forwarded packet changes it)
     reinterpret_cast<uint4 *>(A.ss + d)[lane] = reinterpret_cast<const uint4 *>(&sSS)[lane];
-  if (L.rmDirty) {
+  if (L.rmNew) {  // the ranges appended this batch (the ring's newest): the older ones are unchanged in HBM
     wave_lds_sync();
-    for (u32 i = lane; i < L.h.rmCount; i += 64) {
-      const u32 idx = (L.h.rmHead + i) % kRangeCap;
+    const u32 nc = L.h.rmCount, nn = min(L.rmNew, nc);
+    for (u32 i = lane; i < nn; i += 64) {
+      const u32 idx = (u32(L.h.rmHead) + nc - nn + i) % kRangeCap;
       rmG[idx] = sRm[idx];
     }
   }
@@ -3231,6 +3260,7 @@ struct EmitArgs {
   const u64 *totals;    // [0] records, [1] bytes
   const FwdRec *recs;
   const FwdBase *fbase;  // per DownTrack: the base its records' 32-bit SN / TS widen against
+  const FwdBase *wide;   // per tuple slot: a T_WIDE record's full SN / TS
   const lkf_pkt *pkts;
   const u8 *arena;
   const DevDT *dts;
@@ -3347,7 +3377,12 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       CHK(u64(p.arenaOff) + p.poff + p.plen <= A.arenaLen, CK_EMIT_ARENA, u64(p.arenaOff) + p.poff + p.plen,
           A.arenaLen);
       CHK(!(tFlags & T_DD) || u64(tAux) + tDDLen <= A.ddCap, CK_EMIT_DD, u64(tAux) + tDDLen, A.ddCap);
-      const u64 extSN = widen32(fb.sn, ra.x), extTS = widen32(fb.ts, ra.y);
+      u64 extSN = widen32(fb.sn, ra.x), extTS = widen32(fb.ts, ra.y);
+      if (tFlags & T_WIDE) {
+        const FwdBase wv = A.wide[A.slotBase[d] + (r - A.recBase[lo])];
+        extSN = wv.sn;
+        extTS = wv.ts;
+      }
       lkf_out o;
       o.ext_sn = extSN;
       o.ext_ts = extTS;
@@ -3355,7 +3390,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
       o.dt = d;
       o.pkt = tPkt;
       o.out_len = u16(tLen);
-      o.flags = u8(tFlags & 0x0f);
+      o.flags = u8(tFlags & 0x0f);  // (the T_* bits stay internal)
       o.layer = p.layer;
       o.reserved = 0;
       A.out[r] = o;
@@ -3629,6 +3664,7 @@ __global__ void __launch_bounds__(64) k_seq_dd(const u32 *__restrict__ list, u32
                                                const SeqMeta *__restrict__ seqBase, u32 seqSize, u8 *srmBase,
                                                u64 srmStride, u32 srmCap, const u32 *__restrict__ ddIdx, u8 *seqDD,
                                                const FwdRec *__restrict__ recs, const FwdBase *__restrict__ fbase,
+                                               const FwdBase *__restrict__ wide,
                                                const u64 *__restrict__ slotBase,
                                                const u32 *__restrict__ fwdCnt, const lkf_pkt *__restrict__ pkts,
                                                const u8 *__restrict__ ddArena) {
@@ -3648,7 +3684,7 @@ __global__ void __launch_bounds__(64) k_seq_dd(const u32 *__restrict__ list, u32
     const u32 k = c0 + lane;
     if (k < cnt) {
       const FwdRec t = tp[k];
-      const u64 extSN = widen32(bSN, t.sn);
+      const u64 extSN = (t.flags & T_WIDE) ? wide[slotBase[d] + k].sn : widen32(bSN, t.sn);
       u64 ext = 0;
       const int slot = seq_find(h, srm, srmCap, seqSize, u16(extSN), ext);
       if (slot >= 0 && ext == extSN && seq[slot].targetSeqNo == u16(extSN) &&
@@ -3665,7 +3701,7 @@ __global__ void __launch_bounds__(64) k_seq_dd(const u32 *__restrict__ list, u32
 hipError_t launch_seq_dd(hipStream_t s, const SeqDDLaunch &a) {
   if (!a.n) return hipSuccess;
   hipLaunchKernelGGL(k_seq_dd, dim3(a.n), dim3(64), 0, s, a.list, a.n, a.hot, a.seq, a.seqSize, a.srm, a.srmStride,
-                     a.srmCap, a.ddIdx, a.seqDD, a.recs, a.fbase, a.slotBase, a.fwdCnt, a.pkts, a.ddArena);
+                     a.srmCap, a.ddIdx, a.seqDD, a.recs, a.fbase, a.wide, a.slotBase, a.fwdCnt, a.pkts, a.ddArena);
   return hipGetLastError();
 }
 
@@ -3986,8 +4022,10 @@ __global__ void __launch_bounds__(64) k_pad(PadArgs A) {
   reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];
   __syncthreads();
   Lane L{sHot};
-  L.rm = A.rm + size_t(d) * kRangeCap;
-  L.rmDirty = false;
+  L.rm = A.rm + size_t(d) * kRangeCap;  // (the ring in place: nothing to stage or write back)
+  L.rmG = L.rm;
+  L.rmNew = 0;
+  L.rmLoaded = true;
   L.vcDirty = false;
   L.seq = A.seq + size_t(d) * A.seqSize;
   L.seqSize = A.seqSize;
@@ -4415,11 +4453,13 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.slotBase = a.slotBase;
   A.recs = a.recs;
   A.fbase = a.fbase;
+  A.wide = a.wide;
   A.tupleCap = a.tupleCap;
   A.err = a.err;
   A.ss = a.ss;
   A.ssRing = a.ssRing;
   A.ssGap = a.ssGap;
+  A.dtOffs = a.dtOffs;
   A.events = a.events;
   A.evOff = a.evOff;
   A.fwdCnt = a.fwdCnt;
@@ -4586,6 +4626,7 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   A.totals = a.totals;
   A.recs = a.recs;
   A.fbase = a.fbase;
+  A.wide = a.wide;
   A.pkts = a.pkts;
   A.arena = a.arena;
   A.dts = a.dts;

@@ -144,8 +144,8 @@ static_assert(sizeof(SeqMeta) == 32, "SeqMeta must be 32 B");
 // slot_base[dt] + j (j = the DownTrack's forwarded ordinal in the batch).
 // Only what emit cannot rebuild travels:
 //   - the munged SN / TS as their low 32 bits: emit widens them against the
-//     DownTrack's FwdBase (its first forwarded record of the batch); decide
-//     checks that every record lies within 2^31 of it (error bit 64 otherwise);
+//     DownTrack's FwdBase (its first forwarded record of the batch); a record
+//     beyond 2^31 of it is flagged T_WIDE and its full values kept aside;
 //   - the munged VP8 descriptor as its three munged fields (picture id,
 //     TL0PICIDX, KEYIDX): emit re-marshals it from them and the packet's own
 //     descriptor bits (VP8.MarshalTo helpers.go:170-227), as decide did;
@@ -169,7 +169,11 @@ struct alignas(16) FwdBase {  // per DownTrack and batch: its first forwarded re
 __host__ __device__ inline uint64_t widen32(uint64_t base, uint32_t lo) {
   return base + uint64_t(int64_t(int32_t(lo - uint32_t(base))));
 }
-enum : uint8_t { T_DD = 0x20, T_PLAYOUT = 0x40, T_CODEC = 0x80 };
+// T_WIDE: the record's munged SN or TS lies 2^31 or more from its DownTrack's
+// FwdBase (a source switch can move the munged timestamp that far, e.g. after
+// a reference-layer offset change): its full values are in the batch's wide
+// side array at the record's slot (written and read only for such records)
+enum : uint8_t { T_WIDE = 0x10, T_DD = 0x20, T_PLAYOUT = 0x40, T_CODEC = 0x80 };
 
 // ---- dependency descriptor (AV1 / VP9 SVC, §8(a) a9 + a16) -----------------
 // Engine limits (the reference allows more; a packet beyond them is flagged
@@ -444,6 +448,12 @@ struct alignas(16) RunDesc {
   uint32_t pad[5];
 };
 static_assert(sizeof(RunDesc) == 64, "RunDesc is 64 B");
+
+// internal control op (not an lkf_ctl op): a track's reference-layer offsets
+// table from this packet on (lkf_sender_report / lkf_set_layer_offsets*):
+// offsets[0..7] packed two per a[] word, offsets[8] in pad
+constexpr int32_t kOpLayerOffsets = 100;
+constexpr uint32_t kDTOffsWords = 12;  // per DownTrack offsets row (9 used)
 
 struct DevEvent {  // one queued lkf_ctl op (48 B)
   uint32_t at;

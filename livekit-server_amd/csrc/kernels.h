@@ -29,10 +29,12 @@ struct DecideLaunch {
   const uint64_t *slotBase;
   FwdRec *recs;     // forwarded records at slotBase[dt] + j
   FwdBase *fbase;   // per DownTrack: the base of its records' 32-bit SN / TS
+  FwdBase *wide;    // per tuple slot: the full SN / TS of a T_WIDE record
   uint64_t tupleCap;
   uint32_t *err;
   SenderStats *ss;  // RTPStatsSender per DownTrack, updated by decide (snInfo ring, gap histogram)
   uint32_t *ssRing, *ssGap;
+  uint32_t *dtOffs;  // per DownTrack kDTOffsWords: the reference-layer offsets its Forwarder reads
   const DevEvent *events;
   const uint32_t *evOff;
   uint32_t *fwdCnt;
@@ -58,6 +60,7 @@ struct EmitLaunch {
   const uint32_t *gFirst;  // [group] position owning record 64*group (k_scan_down mode 1)
   const FwdRec *recs;
   const FwdBase *fbase;
+  const FwdBase *wide;
   const lkf_pkt *pkts;
   const uint8_t *arena;
   const DevDT *dts;
@@ -390,6 +393,7 @@ struct SeqDDLaunch {
   uint8_t *seqDD;         // [ring index][slot] kSeqDDBytes
   const FwdRec *recs;
   const FwdBase *fbase;
+  const FwdBase *wide;
   const uint64_t *slotBase;
   const uint32_t *fwdCnt;
   const lkf_pkt *pkts;

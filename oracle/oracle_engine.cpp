@@ -36,9 +36,17 @@ using namespace orc;
 
 namespace {
 
+// StreamTrackerManager.senderReports[layer].newest (streamtrackermanager.go:98-104)
+struct OSenderReport {
+  bool valid = false;
+  u64 ntp = 0;  // mediatransportutil.NtpTime
+  u32 rtp = 0;
+};
 struct OTrack {
-  lkf_track_params p;
+  lkf_track_params p;  // p.layer_offsets: StreamTrackerManager.layerOffsets as the batch reaches it
   bool removed = false;  // orc_remove_track
+  OSenderReport sr[3];
+  u32 queued[3][3] = {};  // layerOffsets after every change queued so far (lkf_sender_report)
   // the structure the DD extension bytes of this track's ExtPackets are read
   // with (the Go parser's r.structure at ingress; replaced by every packet
   // that attaches one) and its decode targets (ProcessFrameDependencyStructure)
@@ -98,9 +106,14 @@ struct OStream {
 
 }  // namespace
 
+struct OTrackOp {  // a track's layerOffsets from packet `at` of the next batch on
+  u32 track, at;
+  u32 offs[3][3];
+};
 struct orc_engine {
   u32 seqSize = 500;
   std::vector<OTrack> tracks;
+  std::vector<OTrackOp> trackOps;
   std::vector<std::unique_ptr<ODT>> dts;
   std::vector<OEv> pending;
   lkf_stats stats{};
@@ -383,6 +396,7 @@ void orc_destroy(orc_engine *e) { delete e; }
 int32_t orc_add_track(orc_engine *e, const lkf_track_params *p) {
   OTrack t;
   t.p = *p;
+  std::memcpy(t.queued, p->layer_offsets, sizeof(t.queued));
   e->tracks.push_back(t);
   return int32_t(e->tracks.size() - 1);
 }
@@ -449,10 +463,79 @@ int orc_remove_track(orc_engine *e, int32_t track) {
   return LKF_OK;
 }
 
-int orc_set_layer_offsets(orc_engine *e, int32_t track, const uint32_t *offs) {
-  if (track < 0 || track >= (int)e->tracks.size()) return LKF_EINVAL;
-  std::memcpy(e->tracks[track].p.layer_offsets, offs, sizeof(uint32_t) * 9);
+// The offsets change at a packet index of the next batch (the engine's
+// control-op semantics; the reference changes them from its RTCP goroutine).
+int orc_set_layer_offsets_at(orc_engine *e, int32_t track, const uint32_t *offs, uint32_t at) {
+  if (track < 0 || track >= (int)e->tracks.size() || !offs) return LKF_EINVAL;
+  OTrackOp op;
+  op.track = u32(track);
+  op.at = at;
+  std::memcpy(op.offs, offs, sizeof(op.offs));
+  std::memcpy(e->tracks[track].queued, offs, sizeof(op.offs));
+  e->trackOps.push_back(op);
   return LKF_OK;
+}
+int orc_set_layer_offsets(orc_engine *e, int32_t track, const uint32_t *offs) {
+  return orc_set_layer_offsets_at(e, track, offs, 0);
+}
+// test hook: a track's layerOffsets as the last queued change leaves them (queued = 1)
+// or as the last batch left them (queued = 0)
+int orc_debug_layer_offsets(orc_engine *e, int32_t track, int queued, uint32_t *out) {
+  if (track < 0 || track >= (int)e->tracks.size() || !out) return LKF_EINVAL;
+  std::memcpy(out, queued ? &e->tracks[track].queued[0][0] : &e->tracks[track].p.layer_offsets[0][0], 36);
+  return LKF_OK;
+}
+
+namespace {
+// mediatransportutil (v0.0.0-20231213075826-cccbf2b93d3f, ntp.go; not vendored
+// in /root/reference) NtpTime.Time() = ntpEpoch.Add(Duration()), Duration():
+//   sec := (t >> 32) * 1e9; frac := (t & 0xffffffff) * 1e9; nsec := frac >> 32;
+//   if uint32(frac) >= 0x80000000 { nsec++ }; return time.Duration(sec + nsec)
+// Two NtpTimes' Time().Sub is the difference of their Durations.
+i64 ntpDuration(u64 t) {
+  const u64 sec = (t >> 32) * 1000000000ull;
+  const u64 frac = (t & 0xFFFFFFFFull) * 1000000000ull;
+  u64 nsec = frac >> 32;
+  if (u32(frac) >= 0x80000000u) nsec++;
+  return i64(sec + nsec);
+}
+// time.Duration.Seconds
+double durSeconds(i64 d) {
+  const i64 sec = d / 1000000000LL, nsec = d % 1000000000LL;
+  return double(sec) + double(nsec) / 1e9;
+}
+// updateLayerOffsetLocked streamtrackermanager.go:561-601
+void updateLayerOffset(OTrack &t, int ref, int other) {
+  const OSenderReport &srRef = t.sr[ref], &srOther = t.sr[other];
+  if (!srRef.valid || srRef.ntp == 0 || !srOther.valid || srOther.ntp == 0) return;
+  const i64 ntpDiff = ntpDuration(srRef.ntp) - ntpDuration(srOther.ntp);
+  if (std::fabs(durSeconds(ntpDiff)) > 60.0) return;  // senderReportThresholdSeconds
+  const i64 rtpDiff = ntpDiff * i64(t.p.clock_rate) / 1000000000LL;  // / 1e9 (int64)
+  const u32 normalizedOtherTS = srOther.rtp + u32(rtpDiff);
+  u32 offset = srRef.rtp - normalizedOtherTS;
+  if (offset == 0) offset = 1;
+  t.queued[ref][other] = offset;
+}
+}  // namespace
+
+// SetRTCPSenderReportData streamtrackermanager.go:603-627 (the newest report;
+// srFirst only feeds GetCalculatedClockRate, outside the path)
+int orc_sender_report(orc_engine *e, int32_t track, int32_t layer, uint64_t ntp, uint32_t rtp, uint32_t at) {
+  if (track < 0 || track >= (int)e->tracks.size()) return LKF_EINVAL;
+  if (layer < 0 || layer > 2) return LKF_OK;
+  OTrack &t = e->tracks[track];
+  u32 before[3][3];
+  std::memcpy(before, t.queued, sizeof(before));
+  t.sr[layer].valid = true;
+  t.sr[layer].ntp = ntp;
+  t.sr[layer].rtp = rtp;
+  for (int i = 0; i < 3; i++) {
+    if (i == layer) continue;
+    updateLayerOffset(t, layer, i);
+    updateLayerOffset(t, i, layer);
+  }
+  if (std::memcmp(before, t.queued, sizeof(before)) == 0) return LKF_OK;
+  return orc_set_layer_offsets_at(e, track, &t.queued[0][0], at);
 }
 
 int orc_ctl(orc_engine *e, int32_t dt, int32_t op, int64_t a0, int64_t a1, int64_t a2, int64_t a3, uint32_t at) {
@@ -494,6 +577,13 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
     e->dts[d]->outs.clear();
     if (e->dts[d]->active) trackDts[e->dts[d]->p.track].push_back(d);
   }
+  // the tracks' layer-offset changes, per track in packet order
+  std::vector<std::vector<OTrackOp>> tq(e->tracks.size());
+  for (const auto &op : e->trackOps) tq[op.track].push_back(op);
+  e->trackOps.clear();
+  for (auto &q : tq)
+    std::stable_sort(q.begin(), q.end(), [](const OTrackOp &a, const OTrackOp &b) { return a.at < b.at; });
+  std::vector<size_t> tqc(e->tracks.size(), 0);
   for (u32 i = 0; i < n; i++) {
     const lkf_pkt &pd = pkts[i];
     if (pd.track >= e->tracks.size()) return LKF_EINVAL;
@@ -515,6 +605,11 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
                                                 x.ActiveDecodeTargetsUpdated, x.Descriptor->hasActiveMask,
                                                 x.Descriptor->ActiveDecodeTargetsBitmask, tg, nt, dtis, nd);
     }
+    {
+      auto &q = tq[pd.track];
+      size_t &c = tqc[pd.track];
+      for (; c < q.size() && q[c].at <= i; c++) std::memcpy(e->tracks[pd.track].p.layer_offsets, q[c].offs, 36);
+    }
     for (u32 d : trackDts[pd.track]) {
       ODT &dt = *e->dts[d];
       while (evc[d] < evq[d].size() && evq[d][evc[d]].at <= i) applyCtl(e, dt, evq[d][evc[d]++]);
@@ -523,6 +618,8 @@ int orc_run(orc_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *arena
   }
   for (u32 d = 0; d < ndt; d++)
     while (evc[d] < evq[d].size()) applyCtl(e, *e->dts[d], evq[d][evc[d]++]);
+  for (size_t t = 0; t < tq.size(); t++)  // changes after the batch's last packet
+    for (; tqc[t] < tq[t].size(); tqc[t]++) std::memcpy(e->tracks[t].p.layer_offsets, tq[t][tqc[t]].offs, 36);
   // spatialTracker.Observe after each packet's fan-out (receiver.go:686-695);
   // len(RawPacket) = header + payload (padding not counted, as the engine)
   if (!e->trk.empty())

@@ -2,7 +2,7 @@
 # Closing pass per bench shape (FINAL_SHAPES: '|'-separated "name:bench args"):
 #   1. PMC passes, one rocprofv3 run per counter (FETCH_SIZE, WRITE_SIZE),
 #      summarised per kernel (scripts/pmc_summary.py, tagged with the sources'
-#      sha and the shape) and copied to profiles/r4_pmc_<name>.json so that
+#      sha and the shape) and copied to profiles/${ROUND:-r5}_pmc_<name>.json so that
 #   2. the bench line (with its CPU baseline) quotes the measured traffic,
 #   3. rocprofv3 --kernel-trace --stats of the same command (kernel CSV).
 # Outputs under gpurun_out/$OUT_NAME; every GPU step has its own limit and the
@@ -10,7 +10,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/${OUT_NAME:-r4_final}
+O=gpurun_out/${OUT_NAME:-${ROUND:-r5}_final}
 mkdir -p $O profiles
 SHAPES="${FINAL_SHAPES:-c2:|c2ext:--extpackets}"
 IFS='|' read -ra LIST <<< "$SHAPES"
@@ -21,21 +21,23 @@ for item in "${LIST[@]}"; do
     i=0
     for ctr in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $O/pmc_$name/p$i -o run -- \
-        python3 bench.py $args --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_${name}_p$i.log 2>&1
+        python3 bench.py $args --steps 3 --warmup 1 --no-cpu-baseline --no-parity > $O/pmc_${name}_p$i.log 2>&1
       rc=$?; echo "$name pmc $ctr rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/pmc_${name}_p$i.log; exit $rc; }
       i=$((i+1))
     done
     BENCH_ARGS="$args" python3 scripts/pmc_summary.py $O/pmc_$name --delete-raw > $O/pmc_${name}_summary.log 2>&1 || exit 5
-    cp $O/pmc_$name/summary.json profiles/r4_pmc_$name.json
-    cp $O/pmc_$name/summary.json $O/r4_pmc_$name.json
-    python3 -c "import json,sys; d=json.load(open('$O/r4_pmc_$name.json')); print('$name hbm_bytes_per_step', d.get('hbm_bytes_per_step'))"
+    cp $O/pmc_$name/summary.json profiles/${ROUND:-r5}_pmc_$name.json
+    cp $O/pmc_$name/summary.json $O/${ROUND:-r5}_pmc_$name.json
+    python3 -c "import json,sys; d=json.load(open('$O/${ROUND:-r5}_pmc_$name.json')); print('$name hbm_bytes_per_step', d.get('hbm_bytes_per_step'))"
   fi
-  timeout -k 10 600 python3 bench.py $args --steps ${STEPS:-20} --warmup 5 ${BENCH_EXTRA:-} > $O/bench_$name.log 2>&1
-  rc=$?; echo "$name bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/bench_$name.log; exit $rc; }
-  grep '^{' $O/bench_$name.log | tail -1 > $O/bench_$name.json; cut -c1-300 $O/bench_$name.json
+  if [ "${BENCH:-1}" = "1" ]; then
+    timeout -k 10 600 python3 bench.py $args --steps ${STEPS:-20} --warmup 5 ${BENCH_EXTRA:-} > $O/bench_$name.log 2>&1
+    rc=$?; echo "$name bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/bench_$name.log; exit $rc; }
+    grep '^{' $O/bench_$name.log | tail -1 > $O/bench_$name.json; cut -c1-300 $O/bench_$name.json
+  fi
   if [ "${PROF:-1}" = "1" ]; then
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$name -o run -- \
-      python3 bench.py $args --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline > $O/prof_$name.log 2>&1
+      python3 bench.py $args --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --no-parity > $O/prof_$name.log 2>&1
     rc=$?; echo "$name prof rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/prof_$name.log; exit $rc; }
     f=$(find $O/prof_$name -name '*kernel_stats.csv' | head -1)
     [ -n "$f" ] && cp "$f" $O/kernel_stats_$name.csv
