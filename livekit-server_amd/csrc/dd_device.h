@@ -145,6 +145,7 @@ __device__ inline int read_structure(BitR &b, DDStruct &s) {
   s.numDT = u8(v + 1);
   s.numTmpl = 0;
   s.numRes = 0;
+  s.nfdPool = 0;
   int tid = 0, sid = 0;
   for (;;) {
     if (s.numTmpl == 64) return TOO_MANY;
@@ -152,7 +153,8 @@ __device__ inline int read_structure(BitR &b, DDStruct &s) {
     t.sid = u8(sid);
     t.tid = u8(tid);
     t.nfd = 0;
-    t.chains = 0;
+    t.fdOff = 0;
+    t.chains[0] = t.chains[1] = t.chains[2] = t.chains[3] = 0;
     t.dtis = 0;
     if ((e = b.bits(2, v))) return e;
     const int idc = int(v);
@@ -170,18 +172,21 @@ __device__ inline int read_structure(BitR &b, DDStruct &s) {
       if ((e = b.bits(2, v))) return e;
       s.t[k].dtis |= v << (2 * i);
     }
-  for (int k = 0; k < s.numTmpl; k++)
+  for (int k = 0; k < s.numTmpl; k++) {  // the templates' frame diffs, one pool in template order
+    s.t[k].fdOff = s.nfdPool;
     for (;;) {
       bool follow;
       if ((e = b.flag(follow))) return e;
       if (!follow) break;
       if ((e = b.bits(4, v))) return e;
-      if (s.t[k].nfd >= kDDTmplFdiffs) return LIMIT;
-      s.t[k].fd[s.t[k].nfd++] = u8(v + 1);
+      if (s.nfdPool >= kDDFdPool) return LIMIT;  // (more than 255 bytes hold)
+      s.fdPool[s.nfdPool++] = u8(v + 1);
+      s.t[k].nfd++;
     }
+  }
   u32 nc;
   if ((e = b.nonSymmetric(u32(s.numDT) + 1, nc))) return e;
-  if (nc > u32(kDDChains)) return LIMIT;
+  if (nc > u32(kDDChains)) return LIMIT;  // (nc <= NumDecodeTargets <= 32: never)
   s.numChains = u8(nc);
   if (nc) {
     for (int i = 0; i < s.numDT; i++) {
@@ -192,7 +197,7 @@ __device__ inline int read_structure(BitR &b, DDStruct &s) {
     for (int k = 0; k < s.numTmpl; k++)
       for (u32 c = 0; c < nc; c++) {
         if ((e = b.bits(4, v))) return e;
-        s.t[k].chains |= u32(v) << (4 * c);
+        s.t[k].chains[c >> 3] |= u32(v) << (4 * (c & 7));
       }
   }
   bool hasRes;
@@ -215,9 +220,12 @@ __device__ inline int read_structure(BitR &b, DDStruct &s) {
 // Parse: buf/len = the DD extension payload; cur = the track's current
 // structure (nullptr before any); att = the ring slot an attached structure is
 // written to.  On success o holds the descriptor and *usedAttached tells
-// whether att became the structure.
+// whether att became the structure.  A frame's custom frame diffs beyond
+// kDDFdInline go to spill (bump-allocated at *spillUsed, spillCap entries);
+// spill == nullptr keeps only their count (FD_NONE).
 __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDStruct *att, DDPkt &o,
-                               bool &usedAttached) {
+                               bool &usedAttached, u16 *spill = nullptr, u32 *spillUsed = nullptr,
+                               u32 spillCap = 0) {
   usedAttached = false;
   BitR b(buf, len);
   u64 v;
@@ -256,12 +264,17 @@ __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDSt
   o.tid = t.tid;
   o.dtis = t.dtis;
   o.ndti = s->numDT;
-  if (t.nfd > kDDFdiffs) return LIMIT;
   o.nfd = t.nfd;
-  for (int i = 0; i < t.nfd; i++) o.fd[i] = t.fd[i];
+  if (t.nfd <= kDDFdInline) {
+    o.fdKind = FD_INLINE;
+    for (int i = 0; i < t.nfd; i++) o.fd[i] = s->fdPool[t.fdOff + i];
+  } else {  // a long template list stays in the structure's pool
+    o.fdKind = FD_POOL;
+    o.fdRef = t.fdOff;
+  }
   o.nchain = s->numChains;
-  o.chainDiffs = 0;
-  for (int c = 0; c < s->numChains; c++) o.chainDiffs |= u64((t.chains >> (4 * c)) & 0xf) << (8 * c);
+  for (int w = 0; w < kDDChains / 8; w++) o.chainDiffs[w] = 0;
+  for (int c = 0; c < s->numChains; c++) o.chainDiffs[c >> 3] |= u64(dd_tmpl_chain(t, c)) << (8 * (c & 7));
   if (customDtis) {
     o.dtis = 0;
     for (int i = 0; i < s->numDT; i++) {
@@ -270,21 +283,41 @@ __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDSt
     }
   }
   if (customFdiffs) {
-    o.nfd = 0;
+    const BitR at = b;  // (a list longer than kDDFdInline is read again into the spill)
+    u32 n = 0;
     for (;;) {
       if ((e = b.bits(2, v))) return e;
       if (v == 0) break;
       u64 f;
       if ((e = b.bits(int(v) * 4, f))) return e;
-      if (o.nfd >= kDDFdiffs) return LIMIT;
-      o.fd[o.nfd++] = u16(f + 1);
+      if (n < u32(kDDFdInline)) o.fd[n] = u16(f + 1);
+      n++;
+    }
+    o.nfd = u16(n);
+    o.fdKind = FD_INLINE;
+    if (n > u32(kDDFdInline)) {
+      if (!spill) {
+        o.fdKind = FD_NONE;
+      } else {
+        const u32 off = atomicAdd(spillUsed, n);
+        if (off + n > spillCap) return LIMIT;  // (the batch's spill capacity)
+        BitR r = at;
+        for (u32 k = 0; k < n; k++) {
+          r.bits(2, v);
+          u64 f;
+          r.bits(int(v) * 4, f);
+          spill[off + k] = u16(f + 1);
+        }
+        o.fdKind = FD_SPILL;
+        o.fdRef = off;
+      }
     }
   }
   if (customChains) {
-    o.chainDiffs = 0;
+    for (int w = 0; w < kDDChains / 8; w++) o.chainDiffs[w] = 0;
     for (int c = 0; c < s->numChains; c++) {
       if ((e = b.bits(8, v))) return e;
-      o.chainDiffs |= v << (8 * c);
+      o.chainDiffs[c >> 3] |= v << (8 * (c & 7));
     }
   }
   if (s->numRes && o.sid >= s->numRes) return INVALID;
@@ -330,6 +363,14 @@ __device__ __forceinline__ int ns_bits(u32 val, u32 numValues) {
   return val < numMin ? w - 1 : w;
 }
 
+// FrameDependencies.FrameDiffs[i] of a parsed packet: in the DDPkt, in the
+// parse-time structure's pool (pool = its fdPool), or in the batch's spill
+__device__ __forceinline__ u32 fd_at(const DDPkt &p, const u8 *pool, const u16 *spill, int i) {
+  if (p.fdKind == FD_INLINE) return p.fd[i];
+  if (p.fdKind == FD_POOL) return pool[p.fdRef + u32(i)];
+  return spill[p.fdRef + u32(i)];
+}
+
 struct Match {
   int idx;
   bool cDtis, cFdiffs, cChains;
@@ -338,25 +379,28 @@ struct Match {
 
 // calculateMatch: frame DTIs / FrameDiffs are never nil after a parse (Clone);
 // a template's FrameDiffs is nil iff it has none (reflect.DeepEqual(nil, []) = false)
-__device__ inline Match dd_match(const DDStruct &s, int idx, const DDPkt &p) {
+__device__ inline Match dd_match(const DDStruct &s, int idx, const DDPkt &p, const u8 *ppool, const u16 *spill) {
   const DDTmpl &t = s.t[idx];
   Match m;
   m.idx = idx;
   bool fdEq = t.nfd != 0 && t.nfd == p.nfd;
-  for (int i = 0; fdEq && i < p.nfd; i++) fdEq = p.fd[i] == t.fd[i];
+  for (int i = 0; fdEq && i < p.nfd; i++) fdEq = fd_at(p, ppool, spill, i) == s.fdPool[t.fdOff + i];
   m.cFdiffs = !fdEq;
   const u64 dm = p.ndti >= 32 ? ~u64(0) : ((u64(1) << (2 * p.ndti)) - 1);
   m.cDtis = !(p.ndti == s.numDT && (p.dtis & dm) == (t.dtis & dm));
   m.cChains = false;
   for (int i = 0; i < s.numChains; i++)
-    if (p.nchain <= i || u32((p.chainDiffs >> (8 * i)) & 0xff) != ((t.chains >> (4 * i)) & 0xf)) {
+    if (p.nchain <= i || dd_chain_diff(p, i) != dd_tmpl_chain(t, i)) {
       m.cChains = true;
       break;
     }
   m.extra = 0;
   if (m.cFdiffs) {
     m.extra = 2 * (1 + p.nfd);
-    for (int i = 0; i < p.nfd; i++) m.extra += p.fd[i] <= 16 ? 4 : p.fd[i] <= 256 ? 8 : 12;
+    for (int i = 0; i < p.nfd; i++) {
+      const u32 f = fd_at(p, ppool, spill, i);
+      m.extra += f <= 16 ? 4 : f <= 256 ? 8 : 12;
+    }
   }
   if (m.cDtis) m.extra += 2 * p.ndti;
   if (m.cChains) m.extra += 8 * s.numChains;
@@ -379,8 +423,9 @@ __device__ inline int structure_bits(const DDStruct &s) {
 
 // Marshal (activeChains = all): writes the descriptor to out (zeroed here),
 // returns its length in bytes, or -1 (error: the selector drops the frame).
+// (ppool/spill: where p's frame diffs are, see fd_at)
 __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
-                                              u32 active, u8 *out, int cap) {
+                                              u32 active, u8 *out, int cap, const u8 *ppool, const u16 *spill) {
   // findBestTemplate
   int first = -1;
   for (int i = 0; i < s.numTmpl; i++)
@@ -392,9 +437,9 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
   int lastIdx = 0;  // as written: the last index whose layer differs
   for (int i = first; i < s.numTmpl; i++)
     if (s.t[i].sid != p.sid || s.t[i].tid != p.tid) lastIdx = i;
-  Match best = dd_match(s, first, p);
+  Match best = dd_match(s, first, p, ppool, spill);
   for (int i = first + 1; i <= lastIdx; i++) {
-    const Match m = dd_match(s, i, p);
+    const Match m = dd_match(s, i, p, ppool, spill);
     if (m.extra < best.extra) best = m;
   }
   const bool attached = p.flags & DP_ATTACHED;
@@ -444,14 +489,14 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
       for (int k = 0; k < s.numTmpl; k++)
         for (int i = 0; i < s.numDT; i++) e |= w.write(dti_at(s.t[k].dtis, i), 2);
       for (int k = 0; k < s.numTmpl; k++) {
-        for (int i = 0; i < s.t[k].nfd; i++) e |= w.write((u64(1) << 4) | u64(s.t[k].fd[i] - 1), 5);
+        for (int i = 0; i < s.t[k].nfd; i++) e |= w.write((u64(1) << 4) | u64(s.fdPool[s.t[k].fdOff + i] - 1), 5);
         e |= w.write(0, 1);
       }
       e |= w.nonSymmetric(s.numChains, u32(s.numDT) + 1);
       if (s.numChains) {
         for (int i = 0; i < s.numDT; i++) e |= w.nonSymmetric(s.protectedBy[i], s.numChains);
         for (int k = 0; k < s.numTmpl; k++)
-          for (int c = 0; c < s.numChains; c++) e |= w.write((s.t[k].chains >> (4 * c)) & 0xf, 4);
+          for (int c = 0; c < s.numChains; c++) e |= w.write(dd_tmpl_chain(s.t[k], c), 4);
       }
       e |= w.write(s.numRes ? 1 : 0, 1);
       for (int i = 0; i < s.numRes; i++) {
@@ -464,7 +509,7 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
       for (int i = 0; i < p.ndti; i++) e |= w.write(dti_at(p.dtis, i), 2);
     if (best.cFdiffs) {
       for (int i = 0; i < p.nfd; i++) {
-        const u64 f = p.fd[i];
+        const u64 f = fd_at(p, ppool, spill, i);
         if (f <= 16)
           e |= w.write((u64(1) << 4) | (f - 1), 6);
         else if (f <= 256)
@@ -479,15 +524,15 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
       // with fewer chain diffs than chains would index out of range (a
       // recovered panic in the reference): the frame is dropped
       if (p.nchain < s.numChains) return -1;
-      for (int c = 0; c < s.numChains; c++) e |= w.write((p.chainDiffs >> (8 * c)) & 0xff, 8);
+      for (int c = 0; c < s.numChains; c++) e |= w.write(dd_chain_diff(p, c), 8);
     }
   }
   w.finish();
   return e ? -1 : nbytes;
 }
 __device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
-                                                   u32 active, u8 *out) {
-  return dd_marshal_inl(s, p, frameNumber, hasActive, active, out, kDDMaxBytes);
+                                                   u32 active, u8 *out, const u8 *ppool, const u16 *spill) {
+  return dd_marshal_inl(s, p, frameNumber, hasActive, active, out, kDDMaxBytes, ppool, spill);
 }
 
 // ---- selector ------------------------------------------------------------------
@@ -519,7 +564,7 @@ __device__ inline void c_fire(DDState &d, u64 e, u32 sd) {
       }
     }
     d.expCount[c] = u8(n);
-    if (hit && sd != SD_FORWARDED) d.chBroken |= u8(1u << c);
+    if (hit && sd != SD_FORWARDED) d.chBroken |= 1u << c;
   }
 }
 __device__ __forceinline__ void c_set(DDState &d, u64 e, u32 sd) {
@@ -599,9 +644,9 @@ __device__ inline bool c_expect(DDState &d, int c, u64 e, bool &overflow) {
 __device__ inline void chain_on_frame(DDState &d, int c, u64 efn, const DDPkt &p, bool &overflow) {
   if (!((d.chActive >> c) & 1)) return;
   if (p.nchain <= c) return;
-  const u32 diff = u32(p.chainDiffs >> (8 * c)) & 0xff;
+  const u32 diff = dd_chain_diff(p, c);
   if (diff == 0) {
-    d.chBroken &= u8(~(1u << c));
+    d.chBroken &= ~(1u << c);
     d.expCount[c] = 0;
     return;
   }
@@ -614,7 +659,7 @@ __device__ inline void chain_on_frame(DDState &d, int c, u64 efn, const DDPkt &p
     intact = true;
   else if (sd == SD_UNKNOWN)
     intact = c_expect(d, c, prev, overflow);
-  if (!intact) d.chBroken |= u8(1u << c);
+  if (!intact) d.chBroken |= 1u << c;
 }
 
 // updateDependencyStructure :363-392 (chains recreated: inactive, broken)
@@ -623,7 +668,7 @@ __device__ inline void update_structure(DDState &d, const DDStruct &s, u8 slot, 
   d.extKeyFrameNum = efn;
   d.flags |= DS_KF_VALID;
   d.numChains = s.numChains;
-  d.chBroken = u8((1u << s.numChains) - 1);
+  d.chBroken = s.numChains >= 32 ? ~0u : (1u << s.numChains) - 1;
   d.chActive = 0;
   d.chUpdating = 0;
   for (int c = 0; c < kDDChains; c++) d.expCount[c] = 0;
@@ -637,13 +682,13 @@ __device__ inline void update_active(DDState &d, const DDStruct &s, u32 mask) {
   for (int i = 0; i < d.numTargets; i++) {
     const bool a = (mask >> s.dtTarget[i]) & 1;
     if (a) d.dtActive |= 1u << i;
-    if (d.numChains > 0 && a) d.chUpdating |= u8(1u << s.protectedBy[s.dtTarget[i]]);
+    if (d.numChains > 0 && a) d.chUpdating |= 1u << s.protectedBy[s.dtTarget[i]];
   }
   for (int c = 0; c < d.numChains; c++) {
     const bool a = (d.chUpdating >> c) & 1, was = (d.chActive >> c) & 1;
     if (a == was) continue;
-    if (!was) d.chBroken |= u8(1u << c);
-    d.chActive = a ? u8(d.chActive | (1u << c)) : u8(d.chActive & ~(1u << c));
+    if (!was) d.chBroken |= 1u << c;
+    d.chActive = a ? d.chActive | (1u << c) : d.chActive & ~(1u << c);
   }
   d.chUpdating = 0;
 }
@@ -682,7 +727,7 @@ struct SelResult {
 // track's ring in HBM for that slot)
 __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStruct *structs, const DDPkt *pp, bool pktMarker,
                                       i32 &curS, i32 &curT, i32 &prevS, i32 &prevT, i32 tgtS, i32 tgtT, u8 *out,
-                                      const DDStruct *staged, u32 stagedSlot) {
+                                      const DDStruct *staged, u32 stagedSlot, const u16 *spill) {
   auto pick = [&](u32 slot) -> const DDStruct & { return slot == stagedSlot ? *staged : structs[slot]; };
   SelResult r = {false, false, false, false, false, 0, false};
   if (curS != -1 && curT != -1) r.relevant = true;
@@ -727,10 +772,12 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
     c_add(d, efn, SD_DROPPED);
     return r;
   }
+  const u8 *const ppool = pick(p.slot).fdPool;
   for (int i = 0; i < p.nfd; i++) {
-    if (p.fd[i] == 0) continue;
+    const u32 f = fd_at(p, ppool, spill, i);
+    if (f == 0) continue;
     bool old;
-    if (c_decision(d, efn - p.fd[i], old) == SD_DROPPED) {
+    if (c_decision(d, efn - f, old) == SD_DROPPED) {
       c_add(d, efn, SD_DROPPED);
       return r;
     }
@@ -763,7 +810,7 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
     hasActive = true;
     active = d.mask;
   }
-  const int n = dd_marshal(s, p, fn, hasActive, active, out);
+  const int n = dd_marshal(s, p, fn, hasActive, active, out, ppool, spill);
   if (n < 0) {
     c_add(d, efn, SD_DROPPED);
     return r;

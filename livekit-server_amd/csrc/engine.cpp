@@ -115,7 +115,8 @@ struct BatchCtx {
   lkf_pkt_dd *dDDIn = nullptr;
   DDPkt *dDDPkt = nullptr;
   uint8_t *dDDArena = nullptr;
-  uint64_t *dDDUsed = nullptr;
+  uint64_t *dDDUsed = nullptr;  // [0] the arena's bump cursor, [1] the spill's (u32)
+  uint16_t *dDDSpill = nullptr;  // custom frame-diff lists longer than kDDFdInline (k_dd_decode)
   DevEvent *dEvents = nullptr;   // this batch's control ops (per-wave CSR)
   uint32_t *dEvOff = nullptr;
   uint32_t *dEvLane = nullptr;   // lane of each op (sorted), for k_ev_offsets
@@ -127,6 +128,12 @@ struct BatchCtx {
   hipEvent_t emitted = nullptr;  // emit stage done (emit stream)
   hipEvent_t ingested = nullptr;  // this context's ingest done (ingest stream)
   bool fromIngest = false;        // the pending batch of this context is an ingest's output
+  // that ingest also prepared the batch (k_ing_out: track ranges, zeroed
+  // counters) for this topology (tracks, DownTracks); lkf_run then skips
+  // k_batch_init and k_track_ranges
+  bool prepByIngest = false;
+  bool gPrepFused = false;  // gPrep was captured without k_batch_init / k_track_ranges
+  uint32_t prepNT = 0, prepND = 0;
   uint64_t *dITotal = nullptr;    // that ingest's ExtPacket count (device; k_track_ranges reads it)
   bool used = false;
   // SRTP-protected copy of the output (lkf_protect; allocated on first use)
@@ -275,6 +282,7 @@ struct lkf_engine {
   uint32_t nDDTracks = 0;
   bool ddAlloc = false;
   uint64_t ddArenaCap = 0;
+  uint32_t ddSpillCap = 0;
   DDStruct *dDDStruct = nullptr;  // [ddIdx * kDDSlots + slot]
   DDTrack *dDDTrack = nullptr;
   DDState *dDDState = nullptr;    // per DownTrack
@@ -664,10 +672,12 @@ static int ensure_dd(lkf_engine *e) {
   HIPCHK(hipMemset(e->dDDTrack, 0, size_t(c.max_tracks) * sizeof(DDTrack)), "dd tracks reset");
   HIPCHK(hipMemset(e->dDDStruct, 0, size_t(c.max_tracks) * kDDSlots * sizeof(DDStruct)), "dd structures reset");
   e->ddArenaCap = c.max_out_bytes / 4 + (1u << 20);
+  e->ddSpillCap = uint32_t(std::min<uint64_t>(uint64_t(c.max_batch_pkts) * kDDFdInline + 4096, 0x7fffffffu));
   for (auto &x : e->ctx) {
     HIPCHK(dalloc(&x.dDDPkt, c.max_batch_pkts), "alloc dd pkts");
     HIPCHK(dalloc(&x.dDDArena, e->ddArenaCap), "alloc dd arena");
-    HIPCHK(dalloc(&x.dDDUsed, 1), "alloc dd cursor");
+    HIPCHK(dalloc(&x.dDDUsed, 2), "alloc dd cursor");
+    HIPCHK(dalloc(&x.dDDSpill, e->ddSpillCap), "alloc dd spill");
   }
   e->ddAlloc = true;
   return LKF_OK;
@@ -815,9 +825,9 @@ static int flush_topology(lkf_engine *e) {
       HIPCHK(dalloc(&e->dNackRecPos, c.max_batch_pkts), "alloc nack positions");
       HIPCHK(dalloc(&e->dNackPairPos, c.max_batch_pkts), "alloc nack pair positions");
       HIPCHK(dalloc(&e->dNackTot, 2), "alloc nack totals");
-      const size_t npart = (size_t(c.max_batch_pkts) + 1023) / 1024 + 1;  // (as the ingest's scan partials)
-      HIPCHK(dalloc(&e->dNackPartA, npart), "alloc nack scan partials");
-      HIPCHK(dalloc(&e->dNackPartB, npart), "alloc nack scan partials");
+      const size_t npart = scan_state_words(c.max_batch_pkts);  // (the compaction's scan state)
+      HIPCHK(dalloc(&e->dNackPartA, npart), "alloc nack scan state");
+      HIPCHK(hipMemset(e->dNackPartA, 0, npart * sizeof(uint64_t)), "nack scan state reset");
       HIPCHK(dalloc(&e->dNackOut, c.max_batch_pkts), "alloc nack records");
       HIPCHK(dalloc(&e->dNackPairsOut, e->nackPairCap), "alloc nack pairs out");
     }
@@ -887,6 +897,24 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     e->ingS = e->prepS;
     A(hipExtStreamCreateWithCUMask(&e->emitS, words, mB.data()));
     A(hipExtStreamCreateWithCUMask(&e->sendS, words, mB.data()));
+  } else if (const char *rv = getenv("LKF_PREP_RESERVE"); rv && atoi(rv) > 0 && atoi(rv) < 32) {
+    // LKF_PREP_RESERVE=K (A/B): of every 32 CUs, K are left to the prep
+    // stream alone (the ingest + batch-prep chain, the pipelined step's
+    // critical path); prep keeps every CU, the other streams the rest
+    const int k = atoi(rv);
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device);
+    const uint32_t words = uint32_t((ncu + 31) / 32);
+    std::vector<uint32_t> mAll(words, 0), mRest(words, 0);
+    for (int i = 0; i < ncu; i++) {
+      mAll[size_t(i / 32)] |= 1u << (i % 32);
+      if ((i % 32) >= k) mRest[size_t(i / 32)] |= 1u << (i % 32);
+    }
+    A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
+    e->ingS = e->prepS;
+    A(hipExtStreamCreateWithCUMask(&e->decS, words, mRest.data()));
+    A(hipExtStreamCreateWithCUMask(&e->emitS, words, mRest.data()));
+    A(hipExtStreamCreateWithCUMask(&e->sendS, words, mRest.data()));
   } else {
     A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
     A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
@@ -924,7 +952,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dSticky, 4));
   A(dalloc(&e->dPerm, c.max_downtracks));
   A(dalloc(&e->dDTOffs, size_t(c.max_downtracks) * kDTOffsWords));
-  const size_t nparts = (c.max_downtracks + 1023) / 1024 + 1;
+  const size_t nparts = scan_state_words(c.max_downtracks);  // the slot and output scans' state
   for (auto &x : e->ctx) {
     A(dalloc(&x.dTBegin, c.max_tracks));
     A(dalloc(&x.dTEnd, c.max_tracks));
@@ -932,7 +960,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(dalloc(&x.dErr, 4));
     A(dalloc(&x.dSlotBase, c.max_downtracks));
     A(dalloc(&x.dPartA, nparts));
-    A(dalloc(&x.dPartB, nparts));
+    A(hipMemset(x.dPartA, 0, nparts * sizeof(uint64_t)));
     A(dalloc(&x.dTot, 4));
     A(dalloc(&x.dRecs, c.max_batch_tuples));
     A(dalloc(&x.dFBase, c.max_downtracks));
@@ -987,9 +1015,9 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   A(dalloc(&e->dTwcc, c.max_batch_pkts));
   e->dFwdFlag = e->ing[0].fwd;
   A(dalloc(&e->dPos, c.max_batch_pkts));
-  const size_t ipart = (size_t(c.max_batch_pkts) + 1023) / 1024 + 1;
+  const size_t ipart = scan_state_words(c.max_batch_pkts);  // the ingest scan's state
   A(dalloc(&e->dIPartA, ipart));
-  A(dalloc(&e->dIPartB, ipart));
+  A(hipMemset(e->dIPartA, 0, ipart * sizeof(uint64_t)));
   A(dalloc(&e->dITotal, 2));
   e->dITBegin = e->ing[0].tBegin;
   e->dITEnd = e->ing[0].tEnd;
@@ -1107,7 +1135,7 @@ void lkf_destroy(lkf_engine *e) {
   for (auto &x : e->ctx) {
     if (x.dProt) (void)dfree(x.dProt);
     for (void *p : {static_cast<void *>(x.dDDIn), static_cast<void *>(x.dDDPkt), static_cast<void *>(x.dDDArena),
-                    static_cast<void *>(x.dDDUsed)})
+                    static_cast<void *>(x.dDDUsed), static_cast<void *>(x.dDDSpill)})
       if (p) (void)dfree(p);
     void *q[] = {x.dTBegin, x.dTEnd,     x.dTRuns,   x.dErr,      x.dSlotBase, x.dPartA,
                  x.dPartB,  x.dTot,      x.dRecs,  x.dFBase,  x.dWide,  x.dFwdCnt,   x.dFwdBytes, x.dRecBase,
@@ -1357,6 +1385,7 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
   if (n) HIPCHK(hipMemcpyAsync(x.dPktsOwn, pkts, size_t(n) * sizeof(lkf_pkt), hipMemcpyHostToDevice, e->own), "pkts");
   if (arena_len) HIPCHK(hipMemcpyAsync(x.dArenaOwn, arena, arena_len, hipMemcpyHostToDevice, e->own), "arena");
   HIPCHK(hipStreamSynchronize(e->own), "submit sync");
+  x.prepByIngest = false;
   e->curPkts = x.dPktsOwn;
   e->curArena = x.dArenaOwn;
   e->curN = n;
@@ -1373,6 +1402,7 @@ int lkf_submit(lkf_engine *e, const lkf_pkt *pkts, uint32_t n, const uint8_t *ar
 int lkf_submit_device(lkf_engine *e, const lkf_pkt *d_pkts, uint32_t n, const uint8_t *d_arena, uint64_t arena_len) {
   if (!e || (n && !d_pkts)) return LKF_EINVAL;
   if (n > e->cfg.max_batch_pkts) return LKF_ENOSPC;
+  e->ctx[e->nRuns % lkf_engine::kCtx].prepByIngest = false;
   e->curPkts = d_pkts;
   e->curArena = d_arena;
   e->curN = n;
@@ -1604,7 +1634,10 @@ int lkf_run(lkf_engine *e, void *stream) {
   // this context's previous batch (run n-2) must have finished its emit stage
   if (x.used) HIPCHK(hipStreamWaitEvent(ps, x.emitted, 0), "wait emit");
   if (x.fromIngest && e->haveBatch) HIPCHK(hipStreamWaitEvent(ps, x.ingested, 0), "wait ingest");
+  const bool prepDone = x.fromIngest && e->haveBatch && x.prepByIngest && x.prepNT == nt && x.prepND == nd &&
+                        e->curPkts == x.dPktsOwn;
   x.fromIngest = false;
+  x.prepByIngest = false;
 
   // Per-lane control-op CSR (stable: queue order within a lane, then by
   // at_pkt).  The host sorts only the ops: an LSD radix sort on the lane
@@ -1732,11 +1765,13 @@ int lkf_run(lkf_engine *e, void *stream) {
     return LKF_OK;
   };
   auto prep = [&]() -> int {
-    HIPCHK(launch_batch_init(ps, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr,
-                             x.dStats, x.dFwdCnt, x.dFwdBytes),
-           "batch init");
-    HIPCHK(launch_track_ranges(ps, x.dDesc, e->cfg.max_batch_pkts, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
-           "track_ranges");
+    if (!prepDone) {  // (an ingest's k_ing_out did both)
+      HIPCHK(launch_batch_init(ps, nt, nd, kStatsWords * (1 + kStatCopies), x.dTBegin, x.dTEnd, x.dTRuns, x.dErr,
+                               x.dStats, x.dFwdCnt, x.dFwdBytes),
+             "batch init");
+      HIPCHK(launch_track_ranges(ps, x.dDesc, e->cfg.max_batch_pkts, nt, x.dTBegin, x.dTEnd, x.dTRuns, x.dErr),
+             "track_ranges");
+    }
     HIPCHK(launch_scan(ps, 0, e->dDTs, x.dTBegin, x.dTEnd, nullptr, nullptr, nd, x.dPartA, x.dPartB, x.dSlotBase,
                        nullptr, x.dTot + 0, nullptr, nullptr),
            "slot scan");
@@ -1746,9 +1781,10 @@ int lkf_run(lkf_engine *e, void *stream) {
     if (e->nTrk)  // StreamTracker.Observe of every (track, spatial layer) tracker (receiver.go:686-695)
       HIPCHK(launch_tracker_observe(ps, e->dTrk, e->nTrk, x.dDesc, x.dTBegin, x.dTEnd), "tracker observe");
     if (e->ddAlloc) {  // dependency descriptors of this batch (track structure rings advance in order)
-      HIPCHK(hipMemsetAsync(x.dDDUsed, 0, sizeof(uint64_t), ps), "dd cursor reset");
+      HIPCHK(hipMemsetAsync(x.dDDUsed, 0, 2 * sizeof(uint64_t), ps), "dd cursor reset");
       HIPCHK(launch_dd_decode(ps, x.dDesc, x.dTBegin, x.dTEnd, e->dTracks, nt, e->dDDStruct, e->dDDTrack, x.dDDPkt,
-                              x.dErr, e->nDDTrk ? e->dTrackDDTrk : nullptr, e->dDDTrk),
+                              x.dErr, e->nDDTrk ? e->dTrackDDTrk : nullptr, e->dDDTrk, x.dDDSpill,
+                              reinterpret_cast<uint32_t *>(x.dDDUsed + 1), e->ddSpillCap),
              "dd decode");
     }
     return LKF_OK;
@@ -1793,10 +1829,11 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipEventRecord(x.pulled, cs), "event");
   HIPCHK(hipStreamWaitEvent(ps, x.pulled, 0), "wait pull");
   if (e->useGraph) {
-    if (x.gPrepEpoch != e->epoch || !x.gPrep) {
+    if (x.gPrepEpoch != e->epoch || !x.gPrep || x.gPrepFused != prepDone) {
       const int rc = capture(ps, x.gPrep, prep);
       if (rc) return rc;
       x.gPrepEpoch = e->epoch;
+      x.gPrepFused = prepDone;
     }
     HIPCHK(hipGraphLaunch(x.gPrep, ps), "prep graph");
   } else {
@@ -1857,6 +1894,7 @@ int lkf_run(lkf_engine *e, void *stream) {
   d.ddState = e->ddAlloc ? e->dDDState : nullptr;
   d.ddArena = x.dDDArena;
   d.ddUsed = x.dDDUsed;
+  d.ddSpill = e->ddAlloc ? x.dDDSpill : nullptr;
   d.ddCap = e->ddArenaCap;
   d.maxDts = e->cfg.max_downtracks;
   d.maxTracks = e->cfg.max_tracks;
@@ -2009,7 +2047,8 @@ int lkf_sync(lkf_engine *e) {
     return LKF_EORDER;
   }
   if (acc & 12u) {
-    e->err = "output or tuple capacity exceeded";
+    e->err = (acc & 8u) ? "output or tuple capacity exceeded (decide: tuple slots or DD arena)"
+                        : "output or tuple capacity exceeded (emit: output records or bytes)";
     return LKF_ENOSPC;
   }
   return LKF_OK;
@@ -3640,6 +3679,15 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
     bl.epoch = ++e->bktEpoch;
     a.bucket = &bl;
   }
+  // the forwarding context's preparation for lkf_run (k_ing_out)
+  a.fwdPrep.tBegin = x.dTBegin;
+  a.fwdPrep.tEnd = x.dTEnd;
+  a.fwdPrep.err = x.dErr;
+  a.fwdPrep.fwdCnt = x.dFwdCnt;
+  a.fwdPrep.stats = x.dStats;
+  a.fwdPrep.fwdBytes = x.dFwdBytes;
+  a.fwdPrep.nstats = kStatsWords * (1 + kStatCopies);
+  a.fwdPrep.ndts = uint32_t(e->dtp.size());
   const bool dd = e->nDDStreams != 0;
   a.ddStates = dd ? e->dDDIng : nullptr;
   a.ddStructs = dd ? e->dDDIngStruct : nullptr;
@@ -3662,6 +3710,9 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   HIPCHK(launch_err_fold(s, e->dIErr, e->dSticky, 8), "ingest error fold");
   HIPCHK(hipEventRecord(x.ingested, s), "event");  // the run's preparation (prep stream) waits for it
   x.fromIngest = true;
+  x.prepByIngest = n != 0;
+  x.prepNT = nt;
+  x.prepND = uint32_t(e->dtp.size());
   e->lastIngestN = n;
   e->ingRaws = dRaws;
   e->curPkts = x.dPktsOwn;
@@ -3996,6 +4047,18 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
 // Not part of include/lkfwd.h: the bounds-check record of a checked build
 // (-DLKF_CHECKED=1, liblkfwd_checked.so): {violations, first site, index,
 // capacity}; LKF_ENODEV from a product build.
+// Not part of include/lkfwd.h: the SVC-run stop counters of a diagnostic
+// build (-DLKF_SVC_STATS=1; forward_kernels.hip g_svc), after a drain.
+int lkf_debug_svc_stats(lkf_engine *e, uint64_t out[32], int reset) {
+  if (!e || !out) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  unsigned long long v[32];
+  const hipError_t r = read_svc_stats(v, reset);
+  for (int i = 0; i < 32; i++) out[i] = v[i];
+  return r == hipSuccess ? LKF_OK : LKF_ENODEV;
+}
+
 int lkf_debug_check(lkf_engine *e, uint64_t out[4], int reset) {
   if (!out) return LKF_EINVAL;
   if (e) {
@@ -4036,8 +4099,9 @@ int lkf_debug_dd_state(lkf_engine *e, int32_t dt, uint64_t out[16]) {
   out[1] = d.cBase;
   out[2] = d.cLast;
   for (int i = 0; i < 8; i++) out[3 + i] = d.masks[i];
-  out[11] = d.chBroken & ((1u << d.numChains) - 1);
-  out[12] = d.chActive & ((1u << d.numChains) - 1);
+  const uint32_t cm = d.numChains >= 32 ? ~0u : (1u << d.numChains) - 1;
+  out[11] = d.chBroken & cm;
+  out[12] = d.chActive & cm;
   uint64_t ex = 0;
   for (int c = 0; c < d.numChains; c++) ex += d.expCount[c];
   out[13] = ex;

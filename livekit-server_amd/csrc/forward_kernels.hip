@@ -226,6 +226,7 @@ struct Lane {
   const DDStruct *ddS;  // LDS copy of ring slot ddSSlot (the current structure when the batch started)
   u32 ddSSlot;
   const DDPkt *ddPkts;
+  const u16 *ddSpill;
   u8 *ddBuf;
   u32 *err;
 };
@@ -1033,7 +1034,7 @@ __device__ int fw_translate(Lane &L, const PktV &p, u32 k, Fwd &o) {
     const bool hasDD = (p.flags & LKF_PKT_DD) && L.ddPkts && (L.ddPkts[k].flags & DP_VALID);
     // (the descriptor is read where k_dd_decode left it: no private copy)
     const dd::SelResult r = dd::dd_select(*L.dd, L.ddRing, hasDD ? L.ddPkts + k : nullptr, pktMarker, L.h.curS, L.h.curT, L.h.prevS,
-                                          L.h.prevT, L.h.tgtS, L.h.tgtT, L.ddBuf, L.ddS, L.ddSSlot);
+                                          L.h.prevT, L.h.tgtS, L.h.tgtT, L.ddBuf, L.ddS, L.ddSSlot, L.ddSpill);
     if (r.limit && lane_id() == 0) atomicOr(L.err, 16u);
     if (!r.selected) {
       if (r.relevant && hasf(L, F_STARTED)) {  // forwarder.go:1694-1702 (RTPMarker false)
@@ -1424,7 +1425,7 @@ __global__ void k_track_ranges(const RunDesc *__restrict__ desc, u32 ntracks, u3
 }
 
 // ---------------------------------------------------------------------------
-// Scans (3-phase: block reduce -> top scan -> block rescan with offsets).
+// Scans (one launch: k_scan_1p).
 // Value = (a, b) u64 pairs; mode selects how the input is formed.
 // ---------------------------------------------------------------------------
 constexpr int SCAN_T = 256;
@@ -1497,83 +1498,128 @@ __device__ __forceinline__ void block_scan_excl(u64 &a, u64 &b, u64 &ta, u64 &tb
   b = pb + ib - b;
 }
 
-__global__ void __launch_bounds__(SCAN_T) k_scan_reduce(ScanIn in, u32 n, u64 *__restrict__ partA,
-                                                        u64 *__restrict__ partB) {
-  u64 sa = 0, sb = 0;
-  u32 base = blockIdx.x * SCAN_TILE;
-  for (int k = 0; k < SCAN_ITEMS; k++) {
-    u32 d = base + k * SCAN_T + threadIdx.x;
-    if (d < n) {
-      u64 a, b;
-      scan_load(in, d, a, b);
-      sa += a;
-      sb += b;
-    }
-  }
-  sa = wave_sum(sa);
-  sb = wave_sum(sb);
-  __shared__ u64 ra[SCAN_T / 64], rb[SCAN_T / 64];
-  if ((threadIdx.x & 63) == 0) {
-    ra[threadIdx.x >> 6] = sa;
-    rb[threadIdx.x >> 6] = sb;
+// Single-pass scan (decoupled look-back): one launch instead of reduce / top
+// / down — each is a dispatch on the prep or decide stream, and pipelined
+// the stream's kernels wait for free CU slots one after another.  Tiles take
+// ordered tickets; a tile publishes its aggregate at once, then looks back
+// over its predecessors (aggregates, up to the first inclusive prefix) and
+// publishes its own inclusive prefix.  A tile only waits on tiles that took
+// their tickets earlier, so no co-residency is needed.  The hand-off is the
+// guide's R2 form: each published value is 32-bit halves in 8-B {tag, value}
+// granules stored and polled with agent-scope relaxed atomics (write-through
+// sc1 stores, L1-bypassing loads), the tag the flag.  The last tile to arrive
+// clears the granules and counters for the next launch on this state (the
+// allocation is zeroed for the first); launches on one state are
+// stream-ordered.
+//   state: [0] tickets, [1] arrivals (u32 each in a u64 word), [2..15] pad,
+//          then per tile 8 granules: aggregate (a lo, a hi, b lo, b hi),
+//          inclusive prefix (a lo, a hi, b lo, b hi)
+constexpr u32 kScanStHead = 16;
+constexpr u32 kScanSpin = 1u << 22;  // polls before a look-back gives up (totals -> ~0: capacity errors)
+
+__device__ __forceinline__ void gr_put(u64 *g, u32 v) {
+  __hip_atomic_store(g, (1ull << 32) | u64(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(SCAN_T) k_scan_1p(ScanIn in, u32 n, u32 nb, u64 *__restrict__ st,
+                                                    u64 *__restrict__ outA, u64 *__restrict__ outB,
+                                                    u64 *__restrict__ totA, u64 *__restrict__ totB) {
+  __shared__ u32 sTile, sLast;
+  __shared__ u64 sPre[2];
+  __shared__ u32 sBad;
+  u32 *const ctr = reinterpret_cast<u32 *>(st);
+  u64 *const gr = st + kScanStHead;
+  const u32 tid = threadIdx.x, lane = tid & 63;
+  if (tid == 0) {
+    sTile = atomicAdd(&ctr[0], 1u);
+    sBad = 0;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    u64 ta = 0, tb = 0;
-    for (int w = 0; w < SCAN_T / 64; w++) {
-      ta += ra[w];
-      tb += rb[w];
-    }
-    partA[blockIdx.x] = ta;
-    partB[blockIdx.x] = tb;
-  }
-}
-
-// single block: exclusive scan of nparts partial sums (in place), totals
-__global__ void __launch_bounds__(SCAN_T) k_scan_top(u64 *__restrict__ partA, u64 *__restrict__ partB, u32 nparts,
-                                                     u64 *__restrict__ totA, u64 *__restrict__ totB) {
-  u64 carryA = 0, carryB = 0;
-  for (u32 base = 0; base < nparts; base += SCAN_T) {
-    u32 i = base + threadIdx.x;
-    u64 a = i < nparts ? partA[i] : 0, b = i < nparts ? partB[i] : 0;
-    u64 ta, tb;
-    block_scan_excl(a, b, ta, tb);
-    if (i < nparts) {
-      partA[i] = a + carryA;
-      partB[i] = b + carryB;
-    }
-    carryA += ta;
-    carryB += tb;
-  }
-  if (threadIdx.x == 0) {
-    *totA = carryA;
-    if (totB) *totB = carryB;
-  }
-}
-
-__global__ void __launch_bounds__(SCAN_T) k_scan_down(ScanIn in, u32 n, const u64 *__restrict__ partA,
-                                                      const u64 *__restrict__ partB, u64 *__restrict__ outA,
-                                                      u64 *__restrict__ outB) {
-  u32 base = blockIdx.x * SCAN_TILE;
-  u64 carryA = partA[blockIdx.x], carryB = partB[blockIdx.x];
+  const u32 tile = sTile;
+  const u32 i0 = tile * SCAN_TILE + tid * SCAN_ITEMS;  // blocked: a thread's items are consecutive
+  u64 va[SCAN_ITEMS], vb[SCAN_ITEMS], ta = 0, tb = 0;
+#pragma unroll
   for (int k = 0; k < SCAN_ITEMS; k++) {
-    u32 d = base + k * SCAN_T + threadIdx.x;
-    u64 a = 0, b = 0;
-    if (d < n) scan_load(in, d, a, b);
-    const u64 cnt = a;
-    u64 ta, tb;
-    block_scan_excl(a, b, ta, tb);
+    va[k] = vb[k] = 0;
+    if (i0 + k < n) scan_load(in, i0 + k, va[k], vb[k]);
+    ta += va[k];
+    tb += vb[k];
+  }
+  u64 ea = ta, eb = tb, TA, TB;
+  block_scan_excl(ea, eb, TA, TB);
+  u64 *const g = gr + 8 * size_t(tile);
+  if (tid == 0) {
+    if (tile == 0) {
+      gr_put(g + 4, u32(TA)), gr_put(g + 5, u32(TA >> 32)), gr_put(g + 6, u32(TB)), gr_put(g + 7, u32(TB >> 32));
+      sPre[0] = sPre[1] = 0;
+    } else {
+      gr_put(g + 0, u32(TA)), gr_put(g + 1, u32(TA >> 32)), gr_put(g + 2, u32(TB)), gr_put(g + 3, u32(TB >> 32));
+    }
+  }
+  if (tile > 0 && tid < 64) {  // look-back: lanes 0-7 read one predecessor's granules per poll
+    u64 pa = 0, pb = 0;
+    int j = int(tile) - 1;
+    for (u32 spins = 0;;) {
+      const u64 x = lane < 8 ? __hip_atomic_load(gr + 8 * size_t(j) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0ull;
+      const u64 rdy = __ballot(lane < 8 && (x >> 32) == 1);
+      const u32 v = u32(x);
+      if ((rdy & 0xF0) == 0xF0 || (rdy & 0x0F) == 0x0F) {
+        const int o = (rdy & 0xF0) == 0xF0 ? 4 : 0;
+        const u64 a = (u64(u32(__shfl(int(v), o + 1, 64))) << 32) | u32(__shfl(int(v), o, 64));
+        const u64 b = (u64(u32(__shfl(int(v), o + 3, 64))) << 32) | u32(__shfl(int(v), o + 2, 64));
+        pa += a;
+        pb += b;
+        if (o == 4) break;  // an inclusive prefix ends the walk (tile 0 always has one)
+        j--;
+        spins = 0;
+        continue;
+      }
+      if (++spins > kScanSpin) {
+        if (lane == 0) sBad = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) {
+      const u64 ia = pa + TA, ib = pb + TB;
+      gr_put(g + 4, u32(ia)), gr_put(g + 5, u32(ia >> 32)), gr_put(g + 6, u32(ib)), gr_put(g + 7, u32(ib >> 32));
+      sPre[0] = pa;
+      sPre[1] = pb;
+    }
+  }
+  __syncthreads();
+  u64 ca = sPre[0] + ea, cb = sPre[1] + eb;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    const u32 d = i0 + k;
     if (d < n) {
-      outA[d] = a + carryA;
-      if (outB) outB[d] = b + carryB;
+      outA[d] = ca;
+      if (outB) outB[d] = cb;
       // emit groups of 64 records whose first record belongs to position d
-      if (in.gFirst && cnt) {
-        const u64 r0 = a + carryA, r1 = min(r0 + cnt, in.gCap);
-        for (u64 g = (r0 + 63) >> 6; (g << 6) < r1; g++) in.gFirst[g] = d;
+      if (in.gFirst && va[k]) {
+        const u64 r0 = ca, r1 = min(r0 + va[k], in.gCap);
+        for (u64 gg = (r0 + 63) >> 6; (gg << 6) < r1; gg++) in.gFirst[gg] = d;
       }
     }
-    carryA += ta;
-    carryB += tb;
+    ca += va[k];
+    cb += vb[k];
+  }
+  if (tile == nb - 1 && tid == 0) {
+    *totA = sBad ? ~0ull : sPre[0] + TA;
+    if (totB) *totB = sBad ? ~0ull : sPre[1] + TB;
+  }
+  // the last tile to arrive clears the state for the next launch
+  __syncthreads();
+  if (tid == 0) sLast = atomicAdd(&ctr[2], 1u) == nb - 1 ? 1u : 0u;
+  __syncthreads();
+  if (sLast) {
+    for (u32 k = tid; k < 8 * nb; k += SCAN_T)
+      __hip_atomic_store(gr + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctr[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1623,6 +1669,7 @@ struct DecideArgs {
   u8 *ddArena;
   u64 *ddUsed;
   u64 ddCap;
+  const u16 *ddSpill;
   // capacities (checked builds test device-computed indices against them)
   u32 maxDts, maxTracks, npkts, nev;
 };
@@ -1987,7 +2034,12 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 #ifndef LKF_DECIDE_WAVES  // occupancy floor (waves per SIMD); 4 and 6 measured slower (r3, r5)
 #define LKF_DECIDE_WAVES 5
 #endif
-#define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(LKF_DECIDE_WAVES, 8)))
+// (the DD selector's instantiation cannot reach that floor: it asks for 2, so
+// the compiler keeps VGPRs + AGPRs within 256 rather than drop to 1 wave)
+#ifndef LKF_DECIDE_DD_WAVES
+#define LKF_DECIDE_DD_WAVES 2
+#endif
+#define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(DDK ? LKF_DECIDE_DD_WAVES : LKF_DECIDE_WAVES, 8)))
 
 // Consume the chunk's descriptor registers here, once.  gfx9 counts stores in
 // vmcnt too: a first use sunk into the run loop would wait there for every
@@ -2082,7 +2134,17 @@ constexpr int kSvcDDBytes = 48;  // per-lane marshal buffer (a descriptor withou
 constexpr int kSvcFrames = 72;   // frame decisions of one run: frame cLast + up to 64 later frames
 enum : u32 { SK_BAD = 0, SK_FWD = 1, SK_MDROP = 2, SK_NDROP = 3 };  // lane kinds of an SVC run
 
+// LKF_SVC_STATS=1 (diagnostic builds): where SVC runs stop.  g_svc[0] runs,
+// [1] packets decided in runs, [2] full steps after a run, [3] runs refused
+// at the start (no keyframe / cache yet), [16 + c] the stopping lane's first
+// failed condition c (the SVC_WHY codes below; 15: the window ended).
+#if LKF_SVC_STATS
+__device__ unsigned long long g_svc[32];
+#define SVC_WHY(c) \
+  if (why == 0 && inWin && !good) why = (c)
+#else
 #define SVC_WHY(c)
+#endif
 
 template <bool DDK>
 __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 pi, u32 n, u32 pos, u32 nextAt,
@@ -2134,6 +2196,10 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     }
     swAll = hiPos >= 0 && (i32(s->dtS[hiPos]) != L.h.curS || i32(s->dtT[hiPos]) != L.h.curT);
   }
+#if LKF_SVC_STATS
+  if (!uni && lane == 0) atomicAdd(&g_svc[3], 1ull);
+  u32 why = 0;
+#endif
   if (!uni) return pos;
   bool good = inWin;
   u32 kind = SK_BAD;
@@ -2187,10 +2253,15 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     }
   } else if (DDK) {  // ---- DependencyDescriptor.Select
     DDState &d = *L.dd;
-    DDPkt dp = {};  // (scalar fields only: the frame diffs and the marshal read dpg)
+    DDPkt dp;  // (the scalar fields only: the frame diffs, chain diffs and the marshal read dpg)
     const bool hasDD = inWin && (p.flags & LKF_PKT_DD) && L.ddPkts;
     const DDPkt *const dpg = L.ddPkts + (hasDD ? pi : 0u);
-    if (hasDD) dp = *dpg;
+    {
+      const uint4 *src = reinterpret_cast<const uint4 *>(dpg);
+      uint4 *dst = reinterpret_cast<uint4 *>(&dp);
+#pragma unroll
+      for (int k = 0; k < int(kDDPktScalar / 16); k++) dst[k] = hasDD ? src[k] : make_uint4(0, 0, 0, 0);
+    }
     const bool ddLane = hasDD && (dp.flags & DP_VALID);  // (no descriptor: not selected, no DD state change)
     const u64 cl0 = d.cLast;
     const u64 efn = dp.extFN;
@@ -2267,7 +2338,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     if (eval && good) {  // FrameChain.OnFrame (framechain.go:43-92): every active chain stays intact
       for (int c = 0; c < int(d.numChains); c++) {
         if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c) continue;
-        const u32 diff = u32(dp.chainDiffs >> (8 * c)) & 0xff;
+        const u32 diff = dd_chain_diff(*dpg, c);
         const bool broken = (d.chBroken >> c) & 1;
         if (diff == 0) {
           good = good && !broken;  // (a broken chain restarting: full step)
@@ -2277,8 +2348,9 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       }
     }
     SVC_WHY(8);
+    if (ddFwdSel) good = good && dp.fdKind == FD_INLINE;  // (a pooled or spilled list: full step)
     if (ddFwdSel && good)  // a referenced frame that was dropped drops this one (:192-201): full step
-      for (int j = 0; j < int(dp.nfd) && j < kDDFdiffs; j++)
+      for (int j = 0; j < int(dp.nfd) && j < kDDFdInline; j++)
         if (dpg->fd[j] != 0 && dec(efn - dpg->fd[j]) == dd::SD_DROPPED) good = false;
     SVC_WHY(9);
     if (ddFwdSel && good) {
@@ -2288,7 +2360,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       const bool hasActive = (dp.flags & DP_ACTIVE) || hasMask;
       const u32 active = hasMask ? d.mask : dp.activeMask;
       ddLen = dd::dd_marshal_inl(*s, *dpg, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
-                                 kSvcDDBytes);
+                                 kSvcDDBytes, nullptr, nullptr);
       if (ddLen < 0) good = false;
       mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
     }
@@ -2329,6 +2401,16 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   SVC_WHY(13);
   const u64 stopM = __ballot(inWin ? !good : (valid && lane >= pos));
   const u32 x = stopM ? u32(__ffsll((long long)stopM) - 1) : n;
+#if LKF_SVC_STATS
+  {
+    const u32 wx = x < 64 ? rl32(why, x) : 0u;
+    if (lane == 0) {
+      atomicAdd(&g_svc[0], 1ull);
+      atomicAdd(&g_svc[1], (unsigned long long)(x > pos ? x - pos : 0));
+      if (x < n) atomicAdd(&g_svc[16 + (wx ? wx : 15)], 1ull);
+    }
+  }
+#endif
   if (x <= pos) return pos;
   const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
   const bool inRun = (runM >> lane) & 1;
@@ -2708,6 +2790,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.extTcc = dt.extTcc;
   L.err = A.err;
   L.ddPkts = A.ddPkts;
+  L.ddSpill = A.ddSpill;
   L.ddRing = nullptr;
   L.ddS = reinterpret_cast<const DDStruct *>(sDDSRaw);
   L.ddSSlot = 0xffffffffu;
@@ -2726,7 +2809,11 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     L.ddRing = A.ddStructs + size_t(tk.ddIdx) * kDDSlots;
     const uint4 *g = reinterpret_cast<const uint4 *>(A.ddState + d);
     uint4 *l = reinterpret_cast<uint4 *>(sDD);
-    for (u32 i = lane; i < sizeof(DDState) / 16; i += 64) l[i] = g[i];
+    // the head and the expectFrames rows of the chains in use (a structure
+    // update zeroes every row's count, so rows past them are never read first)
+    const u32 nc0 = __builtin_amdgcn_readfirstlane(u32(A.ddState[d].numChains));
+    const u32 nDD = (kDDStateHead + nc0 * kDDExpect * 8) / 16;
+    for (u32 i = lane; i < nDD; i += 64) l[i] = g[i];
     __syncthreads();
     // the structure in force: its decode targets, chains and templates are
     // read on every descriptor (selection, marshalling); the ring entries are
@@ -2735,7 +2822,15 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     if (sDD->flags & DS_KF_VALID) {
       const uint4 *gs = reinterpret_cast<const uint4 *>(L.ddRing + slot);
       uint4 *ls = reinterpret_cast<uint4 *>(sDDSRaw);
-      for (u32 i = lane; i < sizeof(DDStruct) / 16; i += 64) ls[i] = gs[i];
+      // the header and the templates in use, then the used part of the pool
+      const u32 nT = __builtin_amdgcn_readfirstlane(u32(L.ddRing[slot].numTmpl));
+      const u32 nP = __builtin_amdgcn_readfirstlane(u32(L.ddRing[slot].nfdPool));
+      constexpr u32 kTOff = __builtin_offsetof(DDStruct, t) / 16, kPOff = __builtin_offsetof(DDStruct, fdPool) / 16;
+      const u32 nHead = kTOff + nT * (sizeof(DDTmpl) / 16), nPool = (nP + 15) / 16;
+      for (u32 i = lane; i < nHead + nPool; i += 64) {
+        const u32 k = i < nHead ? i : kPOff + (i - nHead);
+        ls[k] = gs[k];
+      }
       L.ddSSlot = slot;
       __syncthreads();
     }
@@ -2816,6 +2911,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           const u32 px = rl32(pi, x);
           decide_step<DDK>(L, load_pkt(pkts + px), px, o);
           vm_drain();
+#if LKF_SVC_STATS
+          if (lane == 0) atomicAdd(&g_svc[2], 1ull);
+#endif
           pos = x + 1;
         }
         continue;
@@ -3187,7 +3285,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     wave_lds_sync();
     uint4 *g = reinterpret_cast<uint4 *>(A.ddState + d);
     const uint4 *l = reinterpret_cast<const uint4 *>(sDD);
-    for (u32 i = lane; i < sizeof(DDState) / 16; i += 64) g[i] = l[i];
+    const u32 nDD = (kDDStateHead + u32(sDD->numChains) * kDDExpect * 8) / 16;
+    for (u32 i = lane; i < nDD; i += 64) g[i] = l[i];
   }
   if ((L.h.flags & F_VP8) && L.vcDirty) {  // the maps go back only when a batch changed them
     if (lane < u32(kSetCap)) {
@@ -4261,7 +4360,8 @@ __global__ void __launch_bounds__(64) k_dd_decode(const RunDesc *__restrict__ de
                                                   const u32 *__restrict__ tEnd, const DevTrack *__restrict__ tracks,
                                                   u32 ntracks, DDStruct *structs, DDTrack *ddTracks,
                                                   DDPkt *__restrict__ out, u32 *err,
-                                                  const u32 *__restrict__ trackDDTrk, DDTrkState *ddTrk) {
+                                                  const u32 *__restrict__ trackDDTrk, DDTrkState *ddTrk, u16 *spill,
+                                                  u32 *spillUsed, u32 spillCap) {
   const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
   const lkf_pkt_dd *__restrict__ dds = reinterpret_cast<const lkf_pkt_dd *>(desc->dd);
   const u8 *__restrict__ arena = reinterpret_cast<const u8 *>(desc->arena);
@@ -4308,7 +4408,9 @@ __global__ void __launch_bounds__(64) k_dd_decode(const RunDesc *__restrict__ de
           o.extFlags = r.flags;
           bool att = false;
           const int e =
-              r.dd_len ? dd::dd_parse(arena + aoff + r.dd_off, r.dd_len, curS, ring + next, o, att) : int(dd::INVALID);
+              r.dd_len ? dd::dd_parse(arena + aoff + r.dd_off, r.dd_len, curS, ring + next, o, att, spill, spillUsed,
+                                      spillCap)
+                       : int(dd::INVALID);
           if (e) {
             bad = true;
             o.flags = 0;
@@ -4363,10 +4465,11 @@ __global__ void __launch_bounds__(64) k_dd_decode(const RunDesc *__restrict__ de
 
 hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                             const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,
-                            uint32_t *err, const uint32_t *trackDDTrk, DDTrkState *ddTrk) {
+                            uint32_t *err, const uint32_t *trackDDTrk, DDTrkState *ddTrk, uint16_t *spill,
+                            uint32_t *spillUsed, uint32_t spillCap) {
   if (!ntracks) return hipSuccess;
   hipLaunchKernelGGL(k_dd_decode, dim3(ntracks), dim3(64), 0, s, desc, tBegin, tEnd, tracks, ntracks, structs,
-                     ddTracks, out, err, trackDDTrk, ddTrk);
+                     ddTracks, out, err, trackDDTrk, ddTrk, spill, spillUsed, spillCap);
   return hipGetLastError();
 }
 
@@ -4374,6 +4477,21 @@ hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *
 // launch wrappers (kernels.h)
 // ---------------------------------------------------------------------------
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
+
+hipError_t read_svc_stats(unsigned long long out[32], int reset) {
+#if LKF_SVC_STATS
+  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_svc), sizeof(unsigned long long) * 32);
+  if (r == hipSuccess && reset) {
+    unsigned long long z[32] = {};
+    r = hipMemcpyToSymbol(HIP_SYMBOL(g_svc), z, sizeof(z));
+  }
+  return r;
+#else
+  for (int i = 0; i < 32; i++) out[i] = 0;
+  (void)reset;
+  return hipErrorNotSupported;
+#endif
+}
 
 hipError_t read_check(unsigned long long out[4], int reset) {
 #if LKF_CHECKED
@@ -4414,6 +4532,7 @@ hipError_t launch_track_ranges(hipStream_t s, const RunDesc *desc, u32 maxPkts, 
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const u32 *tBegin, const u32 *tEnd, const u32 *cnt,
                        const u64 *bytes, u32 n, u64 *partA, u64 *partB, u64 *outA, u64 *outB, u64 *totA, u64 *totB,
                        const u32 *perm, u32 *gFirst, u64 gCap) {
+  (void)partB;
   ScanIn in;
   in.gFirst = gFirst;
   in.gCap = gCap;
@@ -4424,12 +4543,12 @@ hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const u32 *tBe
   in.tEnd = tEnd;
   in.cnt = cnt;
   in.bytes = bytes;
-  u32 nb = nblk(n ? n : 1, SCAN_TILE);
-  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_T), 0, s, in, n, partA, partB);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, partA, partB, nb, totA, totB);
-  hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(SCAN_T), 0, s, in, n, partA, partB, outA, outB);
+  const u32 nb = nblk(n ? n : 1, SCAN_TILE);
+  hipLaunchKernelGGL(k_scan_1p, dim3(nb), dim3(SCAN_T), 0, s, in, n, nb, partA, outA, outB, totA, totB);
   return hipGetLastError();
 }
+
+size_t scan_state_words(uint32_t maxN) { return kScanStHead + 8 * size_t(nblk(maxN ? maxN : 1, SCAN_TILE)); }
 
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   if (a.nlanes == 0) return hipSuccess;
@@ -4475,6 +4594,7 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   A.ddState = a.ddState;
   A.ddArena = a.ddArena;
   A.ddUsed = a.ddUsed;
+  A.ddSpill = a.ddSpill;
   A.ddCap = a.ddCap;
   A.maxDts = a.maxDts;
   A.maxTracks = a.maxTracks;

@@ -176,49 +176,80 @@ __host__ __device__ inline uint64_t widen32(uint64_t base, uint32_t lo) {
 enum : uint8_t { T_WIDE = 0x10, T_DD = 0x20, T_PLAYOUT = 0x40, T_CODEC = 0x80 };
 
 // ---- dependency descriptor (AV1 / VP9 SVC, §8(a) a9 + a16) -----------------
-// Engine limits (the reference allows more; a packet beyond them is flagged
-// with error bit 16 -> LKF_EINVAL at lkf_sync, never decided silently):
-constexpr int kDDChains = 8;       // NumChains (L3T3 uses 3)
-constexpr int kDDTmplFdiffs = 16;  // frame diffs of one template
-constexpr int kDDFdiffs = 8;       // frame diffs of one frame (custom fdiffs)
+// Sizes at the reference's maxima (dependencydescriptorextension.go:65-68,
+// dependencydescriptorreader.go:217-303): 32 decode targets and so up to 32
+// chains, 64 templates; frame diffs are unbounded there except by the
+// extension's length (a two-byte element carries at most 255 bytes), so:
+//   - a structure's template frame diffs share one pool (5 bits each: at most
+//     408 fit in 255 bytes);
+//   - a frame keeps up to kDDFdInline frame diffs in its DDPkt; a longer list
+//     (custom frame diffs, 6+ bits each: at most 340) goes to the batch's
+//     spill array (k_dd_decode), a template's longer list stays in the pool.
+// Engine limits that remain: FrameChain.expectFrames holds kDDExpect frames
+// per chain, the structure ring kDDSlots structures per track, the spill array
+// its capacity; beyond them a packet is flagged (error bit 16 -> LKF_EINVAL /
+// LKF_ENOSPC at lkf_sync), never decided silently.
+constexpr int kDDChains = 32;      // MaxDecodeTargets (NumChains <= NumDecodeTargets)
+constexpr int kDDFdPool = 416;     // template frame diffs of one structure (408 fit in 255 bytes)
+constexpr int kDDFdInline = 8;     // frame diffs kept in a DDPkt
 constexpr int kDDExpect = 16;      // frames one chain may wait on (FrameChain.expectFrames)
 constexpr int kDDSlots = 8;        // structure ring per track
 constexpr int kDDMaxBytes = 255;   // marshalled DD (pion two-byte extension element)
 constexpr int kSeqDDBytes = 256;   // a sequencer slot's ddBytes entry: length byte + kDDMaxBytes
 
 struct DDTmpl {  // dependencydescriptor.FrameDependencyTemplate of a structure (32 B)
-  uint8_t sid, tid, nfd, pad;
-  uint32_t chains;   // 4-bit frame_chain_fdiff per chain
-  uint64_t dtis;     // 2-bit DecodeTargetIndication per decode target
-  uint8_t fd[kDDTmplFdiffs];  // frame diffs (1..16)
+  uint8_t sid, tid;
+  uint16_t nfd;        // frame diffs (1..16 each), at fdPool[fdOff ..) of the structure
+  uint16_t fdOff;
+  uint16_t pad;
+  uint64_t dtis;       // 2-bit DecodeTargetIndication per decode target
+  uint32_t chains[4];  // 4-bit frame_chain_fdiff per chain (chain c: word c / 8, nibble c % 8)
 };
 static_assert(sizeof(DDTmpl) == 32, "DDTmpl must be 32 B");
 
 struct alignas(16) DDStruct {  // FrameDependencyStructure + ProcessFrameDependencyStructure
   uint8_t structureId, numDT, numChains, numTmpl;
-  uint8_t numRes, pad[3];
+  uint8_t numRes, pad;
+  uint16_t nfdPool;            // template frame diffs in fdPool
   uint8_t protectedBy[32];     // DecodeTargetProtectedByChain
   uint16_t resW[4], resH[4];   // Resolutions (width, height)
   uint8_t dtTarget[32], dtS[32], dtT[32];  // decode targets sorted high -> low layer
   uint8_t pad2[8];
   DDTmpl t[64];
+  uint8_t fdPool[kDDFdPool];
 };
 static_assert(sizeof(DDStruct) % 16 == 0, "DDStruct must be 16-B granular");
+static_assert(__builtin_offsetof(DDStruct, t) % 16 == 0 && __builtin_offsetof(DDStruct, fdPool) % 16 == 0,
+              "DDStruct staging granules");
+__host__ __device__ inline uint32_t dd_tmpl_chain(const DDTmpl &t, int c) { return (t.chains[c >> 3] >> (4 * (c & 7))) & 0xfu; }
+struct DDPkt;
+__host__ __device__ inline uint32_t dd_chain_diff(const DDPkt &p, int c);
 
 enum : uint8_t { DP_FIRST = 1, DP_LAST = 2, DP_ATTACHED = 4, DP_ACTIVE = 8, DP_VALID = 16 };
-struct alignas(16) DDPkt {  // one packet's parsed descriptor (k_dd_decode -> k_decide_dt), 64 B
+// where a frame's frame diffs are (DDPkt.fdKind): in fd[], in the parse-time
+// structure's pool (fdRef = offset), in the batch's spill array (fdRef =
+// offset), or not kept (the ingress parser, which needs only their count)
+enum : uint8_t { FD_INLINE = 0, FD_POOL = 1, FD_SPILL = 2, FD_NONE = 3 };
+struct alignas(16) DDPkt {  // one packet's parsed descriptor (k_dd_decode -> k_decide_dt), 96 B
   uint64_t extFN, extKFN;
-  uint64_t dtis;        // FrameDependencies.DecodeTargetIndications (2 bits each)
-  uint64_t chainDiffs;  // FrameDependencies.ChainDiffs (8 bits each)
-  uint16_t fd[kDDFdiffs];  // FrameDependencies.FrameDiffs
-  uint32_t activeMask;  // ActiveDecodeTargetsBitmask (valid with DP_ACTIVE)
+  uint64_t dtis;         // FrameDependencies.DecodeTargetIndications (2 bits each)
+  uint32_t activeMask;   // ActiveDecodeTargetsBitmask (valid with DP_ACTIVE)
   uint16_t frameNumber;
-  uint8_t sid, tid, nfd, ndti, nchain, flags;  // flags: DP_*
-  uint8_t extFlags;     // LKF_DD_*
-  uint8_t slot;         // structure ring slot the descriptor was read with (attached: written to)
-  uint8_t pad[2];
+  uint16_t nfd;          // FrameDependencies.FrameDiffs: count (where: fdKind)
+  uint8_t sid, tid, ndti, nchain, flags;  // flags: DP_*
+  uint8_t extFlags;      // LKF_DD_*
+  uint8_t slot;          // structure ring slot the descriptor was read with (attached: written to)
+  uint8_t fdKind;        // FD_*
+  uint32_t fdRef;
+  uint16_t fd[kDDFdInline];
+  uint8_t pad[4];
+  uint64_t chainDiffs[kDDChains / 8];  // FrameDependencies.ChainDiffs (8 bits each: chain c in word c / 8)
 };
-static_assert(sizeof(DDPkt) == 64, "DDPkt must be 64 B");
+constexpr uint32_t kDDPktScalar = 48;  // the bytes of DDPkt before fd[2] (the selector's fast path copies these)
+static_assert(sizeof(DDPkt) == 96, "DDPkt must be 96 B");
+__host__ __device__ inline uint32_t dd_chain_diff(const DDPkt &p, int c) {
+  return uint32_t(p.chainDiffs[c >> 3] >> (8 * (c & 7))) & 0xffu;
+}
 
 struct DDTrack {  // per-track structure-ring cursor (forwarding side)
   uint32_t cur;    // slot of the current structure
@@ -238,14 +269,17 @@ struct alignas(16) DDState {
   uint32_t flags;               // DS_*
   uint32_t mask, prevMask;      // activeDecodeTargetsBitmask / previous
   uint32_t dtActive;            // DecodeTarget.active, by position in the sorted list
+  uint32_t chBroken, chActive, chUpdating;  // per chain
   uint8_t slot;                 // structure ring slot of d.structure
   uint8_t numChains, numTargets;  // len(d.chains), len(d.decodeTargets)
-  uint8_t chBroken, chActive, chUpdating;
+  uint8_t pad;
   uint8_t expCount[kDDChains];
-  uint8_t pad[2];
-  uint64_t exp[kDDChains][kDDExpect];  // FrameChain.expectFrames (a set: see dd_device.h)
+  uint64_t pad2;                // (exp rows 16-B aligned)
+  uint64_t exp[kDDChains][kDDExpect];  // FrameChain.expectFrames (a set: see dd_device.h); rows < numChains staged
 };
+constexpr uint32_t kDDStateHead = 176;  // the bytes of DDState before exp[][] (always staged)
 static_assert(sizeof(DDState) % 16 == 0, "DDState must be 16-B granular");
+static_assert(__builtin_offsetof(DDState, exp) == kDDStateHead, "DDState head");
 
 struct DevTrack {  // track table (24 x 4 B)
   uint32_t kind, codec, hasRefTS, clockRate;

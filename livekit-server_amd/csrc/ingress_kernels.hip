@@ -855,6 +855,7 @@ struct DDLite {
   u16 frameNumber;
   u8 flags, sid, tid;  // flags: DP_*
   u32 activeMask;
+  int err;  // dd_parse_lite's result
 };
 // The parser state's part of Parse (dependencydescriptorparser.go:100-162) for
 // a descriptor already read: sequence / frame-number unwrap, the frame
@@ -892,16 +893,19 @@ __device__ bool dd_fold(DDIngState &d, u16 sn, const DDLite &o, bool att, IngDD 
 // (cur; nullptr before any) with no structure attached (the caller checked
 // the flag): -> (error, the descriptor's DDLite), out of line (one call per
 // lane of a run).
-__device__ __noinline__ int dd_parse_lite(const u8 *buf, int len, const DDStruct *cur, DDLite &out) {
+// (returned by value: a reference to the caller's copy would put it on every
+// lane's private stack)
+__device__ __noinline__ DDLite dd_parse_lite(const u8 *buf, int len, const DDStruct *cur) {
   DDPkt o = {};
   bool att = false;
-  const int e = dd::dd_parse(buf, len, cur, nullptr, o, att);
+  DDLite out;
+  out.err = dd::dd_parse(buf, len, cur, nullptr, o, att);
   out.frameNumber = o.frameNumber;
   out.flags = o.flags;
   out.sid = o.sid;
   out.tid = o.tid;
   out.activeMask = o.activeMask;
-  return e;
+  return out;
 }
 // a descriptor that attaches a structure (template_dependency_structure_present_flag)
 __device__ __forceinline__ bool dd_attaches(const u8 *buf, int len) { return len > 3 && (buf[3] & 0x80); }
@@ -1033,11 +1037,19 @@ __device__ __forceinline__ void rx_jitter(StreamHot &h, u32 clockRate, u64 ets, 
 // One datagram through Buffer.calc (buffer.go:407-489): processHeaderExtensions,
 // RTPStatsReceiver.Update (rtpstats_receiver.go:76-241), the padding
 // RangeMap, the dependency descriptor; its flow, forward flag and DD record.
+// (the datagram, its descriptor and the stream come as pointers into the
+// batch's arrays and the bucket context from LDS: references to the caller's
+// per-lane copies put them on every lane's private stack — 400 B of scratch a
+// lane, written by every wave of the stream kernel, r4's tick WRITE_SIZE)
 template <int HS>
-__device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream &s,
-                                         const IngParsed &p, const lkf_raw_pkt &rp, u32 ic, lkf_flow *flows,
+__device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream *sg,
+                                         const IngParsed *pg, const lkf_raw_pkt *rg, u32 ic, lkf_flow *flows,
                                          u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *dds,
-                                         DDStruct *ddStructs, u32 *err, const BktCtx &bk, bool bkOn, u32 *gap) {
+                                         DDStruct *ddStructs, u32 *err, const BktCtx *bkg, bool bkOn, u32 *gap) {
+  const DevStream s = *sg;
+  const IngParsed p = *pg;
+  const lkf_raw_pkt rp = *rg;
+  const BktCtx bk = *bkg;
   const i64 arrival = rp.arrival_ns;
   lkf_flow f = {};
   f.pkt = 0xffffffffu;
@@ -1214,8 +1226,11 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
 // whose DependencyDescriptorParser + FrameIntegrityChecker state (3.3 KB) is
 // staged in LDS for the batch — lane 0's fold of the descriptors then updates
 // it there (the plain streams keep the smaller LDS footprint and occupancy).
+#ifndef LKF_ING_WAVES  // occupancy floor of the stream wave (waves per SIMD)
+#define LKF_ING_WAVES 4
+#endif
 template <bool DDK>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_ing_stream_wave(
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING_WAVES))) k_ing_stream_wave(
     const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q, const DevStream *__restrict__ streams,
     StreamHot *__restrict__ hot, u64 *__restrict__ hist, RangeEntry *__restrict__ rings,
     const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows,
@@ -1229,6 +1244,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
   __shared__ BucketState sB;
   __shared__ u32 sOwn[kBktLds];  // (LDS is otherwise small: 4 waves per SIMD either way)
   __shared__ __attribute__((aligned(16))) u8 sDDIRaw[DDK ? sizeof(DDIngState) : 16];
+  __shared__ BktCtx sBk;  // (ing_step's copy of bk)
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
   if ((s.ddIdx != 0xffffffffu) != DDK) return;  // the other instantiation's stream
@@ -1260,6 +1276,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     if (bk.lds)
       for (int i = int(lane); i < M; i += 64) sOwn[i] = kNoOwner;
   }
+  if (lane == 0) sBk = bk;
   DDIngState *dds = nullptr;
   if (DDK) {
     dds = reinterpret_cast<DDIngState *>(sDDIRaw);
@@ -1324,7 +1341,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const u32 end = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;  // the run is [pos, end)
     if (end == pos) {  // the datagram at pos through the serial Buffer.calc step
       if (lane == pos && rp.stream == sid)
-        ing_step<1>(sh, sHist, ring, s, p, rp, ic, flows, fwd, ingDD, raw, dds, ddStructs, err, bk, bkOn, gap);
+        ing_step<1>(sh, sHist, ring, streams + sid, q + ic, raws + ic, ic, flows, fwd, ingDD, raw, dds, ddStructs, err,
+                    &sBk, bkOn, gap);
       __syncthreads();
       pos++;
       continue;
@@ -1362,8 +1380,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
       const u32 dfl = dst.flags;
       const DDStruct *curS = (dfl & DI_HAS_STRUCT) ? ddStructs + size_t(s.ddIdx) * 2 + ((dfl & DI_CUR) ? 1 : 0) : nullptr;
       DDLite dl = {};
-      int de = 0;
-      if (run && ddLane) de = dd_parse_lite(raw + rp.off + p.ddOff, p.ddLen, curS, dl);
+      if (run && ddLane) dl = dd_parse_lite(raw + rp.off + p.ddOff, p.ddLen, curS);
+      const int de = dl.err;
       const u32 dlw0 = u32(dl.frameNumber) | (u32(dl.flags) << 16) | (u32(dl.sid & 15) << 24) | (u32(dl.tid & 15) << 28);
       const u16 snL = u16(ext - sh.rmOpenValue);
       // (the loop and its readlanes run on the whole wave, so every lane's
@@ -1862,11 +1880,45 @@ __global__ void k_nack_compact(u32 n, const lkf_raw_pkt *__restrict__ raws, cons
 // ---------------------------------------------------------------------------
 // k_ing_out: the ExtPacket of every forwarded datagram at its batch position
 // ---------------------------------------------------------------------------
+// FwdPrep: the forwarding context's per-batch preparation folded in (one
+// dispatch instead of k_batch_init + k_track_ranges on the prep chain).
+struct FwdPrep {
+  u32 *tBegin, *tEnd, *err, *fwdCnt;
+  u64 *stats, *fwdBytes;
+  u32 nstats, ndts, ntracks;
+  const u32 *rawBegin, *rawEnd;  // the ingest's per-track datagram ranges (grouped by track)
+  const u64 *total;              // ExtPackets of the ingest
+};
 __global__ void k_ing_out(const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
                           const DevStream *__restrict__ streams, const u32 *__restrict__ fwd,
                           const u64 *__restrict__ pos, u32 n, lkf_flow *__restrict__ flows,
-                          lkf_pkt *__restrict__ out, const IngDD *__restrict__ ingDD, lkf_pkt_dd *__restrict__ outDD) {
+                          lkf_pkt *__restrict__ out, const IngDD *__restrict__ ingDD, lkf_pkt_dd *__restrict__ outDD,
+                          FwdPrep fp) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (fp.tBegin) {
+    // track t's ExtPackets are [pos[rawBegin], pos[rawEnd]) (the ingest writes
+    // them in datagram order, datagrams grouped by track); an empty track
+    // [0, 0) as k_track_ranges leaves it.  The counters start at zero.
+    const u32 stride = gridDim.x * blockDim.x;
+    for (u32 j = i; j < fp.ntracks || j < fp.ndts || j < fp.nstats || j < 4; j += stride) {
+      if (j < fp.ntracks) {
+        const u32 rb = fp.rawBegin[j], re = fp.rawEnd[j];
+        u32 b = 0, e = 0;
+        if (re > rb) {
+          b = u32(pos[rb]);
+          e = re < n ? u32(pos[re]) : u32(*fp.total);
+        }
+        fp.tBegin[j] = b < e ? b : 0u;
+        fp.tEnd[j] = b < e ? e : 0u;
+      }
+      if (j < fp.ndts) {
+        fp.fwdCnt[j] = 0;
+        fp.fwdBytes[j] = 0;
+      }
+      if (j < fp.nstats) fp.stats[j] = 0;
+      if (j < 4) fp.err[j] = 0;
+    }
+  }
   if (i >= n || !fwd[i]) return;
   const u32 k = u32(pos[i]);
   const IngParsed p = q[i];
@@ -2245,8 +2297,28 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
   if (r != hipSuccess) return r;
-  hipLaunchKernelGGL(k_ing_out, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.raws, a.parsed, a.streams, a.fwd, a.pos,
-                     a.n, a.flows, a.out, a.ingDD, a.outDD);
+  FwdPrep fp = {};
+  if (a.fwdPrep.tBegin) {
+    fp.tBegin = a.fwdPrep.tBegin;
+    fp.tEnd = a.fwdPrep.tEnd;
+    fp.err = a.fwdPrep.err;
+    fp.fwdCnt = a.fwdPrep.fwdCnt;
+    fp.stats = a.fwdPrep.stats;
+    fp.fwdBytes = a.fwdPrep.fwdBytes;
+    fp.nstats = a.fwdPrep.nstats;
+    fp.ndts = a.fwdPrep.ndts;
+    fp.ntracks = a.ntracks;
+    fp.rawBegin = a.tBegin;
+    fp.rawEnd = a.tEnd;
+    fp.total = a.total;
+  }
+  u32 go = nblk(a.n, 256);
+  if (fp.tBegin) {  // (enough threads for the per-track / per-DownTrack part too, grid-stride beyond)
+    const u32 m = std::max(std::max(a.ntracks, fp.ndts), fp.nstats);
+    go = std::max(go, std::min<u32>(nblk(m, 256), 1024));
+  }
+  hipLaunchKernelGGL(k_ing_out, dim3(go), dim3(256), 0, st, a.raws, a.parsed, a.streams, a.fwd, a.pos, a.n, a.flows,
+                     a.out, a.ingDD, a.outDD, fp);
   return hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ struct DecideLaunch {
   uint8_t *ddArena;
   uint64_t *ddUsed;
   uint64_t ddCap;
+  const uint16_t *ddSpill;  // k_dd_decode's spilled frame-diff lists
   // capacities (tested in -DLKF_CHECKED=1 builds)
   uint32_t maxDts, maxTracks, npkts, nev;
 };
@@ -87,12 +88,16 @@ hipError_t launch_twcc_stamp(hipStream_t s, const DevDT *dts, uint32_t *ctrD, ui
                              const uint64_t *off, const uint32_t *len, uint8_t *arena);
 // -DLKF_CHECKED=1 builds: {violations, first site, its index, its capacity}
 hipError_t read_check(unsigned long long out[4], int reset);
+hipError_t read_svc_stats(unsigned long long out[32], int reset);  // LKF_SVC_STATS builds
 
 hipError_t launch_batch_init(hipStream_t s, uint32_t ntracks, uint32_t ndts, uint32_t nstats, uint32_t *tBegin,
                              uint32_t *tEnd, uint32_t *tRuns, uint32_t *err, uint64_t *stats, uint32_t *fwdCnt,
                              uint64_t *fwdBytes);
 hipError_t launch_track_ranges(hipStream_t s, const RunDesc *desc, uint32_t maxPkts, uint32_t ntracks,
                                uint32_t *tBegin, uint32_t *tEnd, uint32_t *tRuns, uint32_t *err);
+// the scan's state (partA): scan_state_words(maxN) u64 words, zeroed at allocation
+// (each launch leaves it zeroed); partB is unused
+size_t scan_state_words(uint32_t maxN);
 hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t *tBegin, const uint32_t *tEnd,
                        const uint32_t *cnt, const uint64_t *bytes, uint32_t n, uint64_t *partA, uint64_t *partB,
                        uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB,
@@ -131,6 +136,15 @@ struct IngestLaunch {
   lkf_nack_pair *nackPairs;
   uint32_t nackPairCap;
   const BucketLaunch *bucket = nullptr;  // the RTX buckets (nullptr: none)
+  // the forwarding batch context's preparation, done by k_ing_out (tBegin
+  // nullptr: not done): per-track ExtPacket ranges from the ingest's datagram
+  // ranges and positions, and the zeroing k_batch_init would do (lkf_run then
+  // skips k_batch_init and k_track_ranges)
+  struct {
+    uint32_t *tBegin = nullptr, *tEnd = nullptr, *err = nullptr, *fwdCnt = nullptr;
+    uint64_t *stats = nullptr, *fwdBytes = nullptr;
+    uint32_t nstats = 0, ndts = 0;
+  } fwdPrep;
 };
 // The receivers' RTX buckets (mediatransportutil bucket, buffer.go:471; oracle
 // bucket_oracle.h): per stream a ring of maxSteps slots of kBktSlot bytes (the
@@ -210,7 +224,8 @@ hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const uint32_t
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
 hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                             const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,
-                            uint32_t *err, const uint32_t *trackDDTrk = nullptr, DDTrkState *ddTrk = nullptr);
+                            uint32_t *err, const uint32_t *trackDDTrk, DDTrkState *ddTrk, uint16_t *spill,
+                            uint32_t *spillUsed, uint32_t spillCap);
 // the DD stream trackers' bitrate report (tracker_kernels.hip)
 hipError_t launch_dd_tracker_tick(hipStream_t s, DDTrkState *st, const int32_t *ids, uint32_t n, int64_t elapsedNs,
                                   lkf_dd_tracker_status *out);

@@ -128,11 +128,14 @@ static void fill_payload(u8 *dst, int n, u64 key) {
 // T0 frames of spatial layer c), resolutions 320x180 / 640x360 / 1280x720.
 // Frames that deviate from their template (chain diffs after a skipped layer,
 // the second reference of odd T2 frames) carry custom fields.
+// The wide form (svc_dd = 2) takes the reader to the reference's maxima: one
+// chain per decode target (chain c follows spatial layer c / 3, so 9 chains),
+// T2 templates with 17 frame diffs, custom frame-diff lists of 9 and 18.
 struct DDTmplGen {
   int sid, tid;
   std::vector<int> fd, chains, dtis;
 };
-static std::vector<DDTmplGen> dd_templates() {
+static std::vector<DDTmplGen> dd_templates(bool wide) {
   static const int ch[3][4][3] = {{{0, 0, 0}, {12, 11, 10}, {6, 5, 4}, {3, 2, 1}},
                                   {{1, 0, 0}, {1, 12, 11}, {7, 6, 5}, {4, 3, 2}},
                                   {{2, 1, 0}, {2, 1, 12}, {8, 7, 6}, {5, 4, 3}}};
@@ -145,7 +148,13 @@ static std::vector<DDTmplGen> dd_templates() {
       static const int base[4] = {0, 12, 6, 3};
       if (k > 0) t.fd.push_back(base[k]);
       if (sp > 0) t.fd.push_back(1);
-      t.chains.assign(ch[sp][k], ch[sp][k] + 3);
+      static const int more[4] = {6, 12, 9, 3};
+      if (wide && k == 3)
+        for (int j = 0; t.fd.size() < 17; j++) t.fd.push_back(more[j % 4]);
+      if (wide)
+        for (int c = 0; c < 9; c++) t.chains.push_back(ch[sp][k][c / 3]);
+      else
+        t.chains.assign(ch[sp][k], ch[sp][k] + 3);
       for (int tg = 0; tg < 9; tg++) {
         const int s2 = tg / 3, t2 = tg % 3;
         int x = 0;
@@ -207,8 +216,9 @@ static std::vector<u8> dd_encode(const std::vector<DDTmplGen> &T, int structureI
         for (int f : x.fd) o.put((1u << 4) | u32(f - 1), 5);
         o.put(0, 1);
       }
-      o.ns(3, 9 + 1);
-      for (int tg = 0; tg < 9; tg++) o.ns(u32(tg / 3), 3);
+      const u32 nch = u32(T[0].chains.size());
+      o.ns(nch, 9 + 1);
+      for (int tg = 0; tg < 9; tg++) o.ns(nch == 9 ? u32(tg) : u32(tg / 3), nch);
       for (auto &x : T)
         for (int c : x.chains) o.put(u64(c), 4);
       o.put(1, 1);
@@ -255,6 +265,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   const bool withEvents = cfg->with_events != 0;
   const bool cb = cfg->has_callbacks != 0;
   const bool svcDD = cfg->svc_dd != 0;
+  const bool ddWide = cfg->svc_dd == 2;
   const bool h264 = cfg->h264 > 0;
 
   u32 rooms = cfg->rooms, parts = cfg->participants;
@@ -453,7 +464,8 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       u8 tl00 = u8(rng.next());
       u16 twcc = u16(rng.next());
       // dependency descriptor (DD tracks only: the RNG stream of VP9 tracks is unchanged)
-      static const std::vector<DDTmplGen> ddT = dd_templates();
+      static const std::vector<DDTmplGen> ddT3 = dd_templates(false), ddT9 = dd_templates(true);
+      const std::vector<DDTmplGen> &ddT = ddWide ? ddT9 : ddT3;
       int structureId = 0;
       u64 fn0 = 0;
       bool reducedTrack = false;
@@ -494,10 +506,13 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
             tmpl = sl * 4 + kk;
             fdv = ddT[size_t(tmpl)].fd;
             if (!kf && tid == 2 && f % 4 == 3) fdv.push_back(9);
+            if (ddWide && !kf && tid == 1 && f % 8 == 2)  // a custom list of 9-10
+              for (int j = 0; j < 8; j++) fdv.push_back(j % 2 ? 6 : 12);
+            const int nch = int(ddT[size_t(tmpl)].chains.size());
             if (kf) {
               chv = ddT[size_t(tmpl)].chains;
             } else {
-              for (int c = 0; c < 3; c++) chv.push_back(int(std::min<u64>(255, efn - lastChain[c])));
+              for (int c = 0; c < nch; c++) chv.push_back(int(std::min<u64>(255, efn - lastChain[nch == 9 ? c / 3 : c])));
             }
             if (kf || tid == 0) lastChain[sl] = efn;
           }

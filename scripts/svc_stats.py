@@ -1,0 +1,47 @@
+"""Diagnostic: where the SVC runs of k_decide_dt<true> stop on configs[4]
+(needs the LKF_SVC_STATS build: make -C livekit-server_amd/csrc ab
+ABNAME=svcst ABFLAGS=-DLKF_SVC_STATS=1, run with LKF_LIB=liblkfwd_svcst.so).
+Prints the counters per batch (forwarding path, ExtPackets)."""
+import ctypes as C
+import importlib
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+pkg = importlib.import_module("livekit-server_amd")
+workload = importlib.import_module("livekit-server_amd.workload")
+
+WHY = {1: "start/seq", 2: "vp9 switch", 3: "frame order", 4: "ndti", 5: "frame head", 6: "struct/active/kfn/nchain",
+       7: "switch/fn init", 8: "chain", 9: "fdiff dropped/long", 10: "marshal", 11: "reorder/pad", 12: "excl",
+       13: "osn/ots", 14: "expect", 15: "window end"}
+
+
+def main():
+    rooms = int(sys.argv[1]) if len(sys.argv) > 1 else 500
+    svc_dd = int(sys.argv[2]) if len(sys.argv) > 2 else -1
+    tr = workload.Trace(5, duration_s=3.0, batch_s=1.0, rooms=rooms, svc_dd=svc_dd)
+    eng = pkg.Engine.for_trace(tr)
+    workload.load_topology(eng.api, eng.h, tr)
+    fn = eng.lib.lkf_debug_svc_stats
+    out = (C.c_uint64 * 32)()
+    fn(eng.h, out, 1)
+    for b in range(tr.nbatches):
+        workload.queue_events(eng.api, eng.h, tr, b)
+        pk, n, ar, alen = tr.batch(b)
+        dd = tr.batch_dd(b)[0] if tr.has_dd() else None
+        t0 = time.time()
+        eng.submit(pk, n, ar, alen, dd)
+        eng.run()
+        eng.sync()
+        dt = time.time() - t0
+        assert fn(eng.h, out, 1) == 0
+        v = list(out)
+        print(f"batch {b}: n={n} {dt*1e3:.1f} ms  runs={v[0]} run_pkts={v[1]} full_steps={v[2]} refused={v[3]}",
+              flush=True)
+        print("   stops: " + ", ".join(f"{WHY.get(i, i)}={v[16 + i]}" for i in range(16) if v[16 + i]), flush=True)
+    tr.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -165,6 +165,14 @@ def test_ingress_config5_dd_loss_reorder(pkg, workload, abi):
     assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
 
 
+def test_ingress_config5_dd_wide(pkg, workload, abi):
+    """The wide descriptor (9 chains, 17-18 frame diffs) through the stream
+    parser and then the selector (tests/test_dd_wide_cpu.py)."""
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.5, rooms=4, loss=0.04, reorder=0.03, seed=63, svc_dd=2)
+    assert tr.has_dd()
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
+
+
 def test_ingress_h264_keyframes(pkg, workload, abi):
     """H.264 simulcast publishers: IsH264KeyFrame over single NALU / STAP-A /
     STAP-B / FU-A SPS packets (and truncated aggregates) on the GPU."""

@@ -206,6 +206,22 @@ def test_config5_dd_heavy_loss(pkg, workload, abi):
     run_parity(pkg, workload, abi, tr)
 
 
+def test_config5_dd_wide(pkg, workload, abi):
+    """The descriptor at the reference reader's maxima (synth svc_dd=2,
+    tests/test_dd_wide_cpu.py): 9 chains, templates with 17 frame diffs (the
+    structure's pool), custom lists of 9-18 (the batch's spill array), all
+    decided and re-marshalled bit-exactly, no engine-limit error."""
+    tr = workload.Trace(5, duration_s=4.0, batch_s=0.5, rooms=8, svc_dd=2, seed=61)
+    assert tr.has_dd()
+    t = run_parity(pkg, workload, abi, tr)
+    assert t["forwarded"] > 0
+
+
+def test_config5_dd_wide_heavy_loss(pkg, workload, abi):
+    tr = workload.Trace(5, duration_s=3.0, batch_s=0.25, rooms=4, loss=0.2, reorder=0.15, seed=62, svc_dd=2)
+    run_parity(pkg, workload, abi, tr)
+
+
 def test_empty_and_control_only_batches(pkg, workload, abi):
     """An empty batch and a control-only run are no-ops that still apply ops."""
     tr = workload.Trace(1, duration_s=1.0, batch_s=1.0)
