@@ -264,17 +264,36 @@ __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDSt
   o.tid = t.tid;
   o.dtis = t.dtis;
   o.ndti = s->numDT;
+  // the inline frame diffs gather in four words by name (a run-time index
+  // into o.fd put the whole descriptor on the private stack)
+  u32 fw0 = 0, fw1 = 0, fw2 = 0, fw3 = 0;
+  auto put_fd = [&](u32 k, u32 f) {
+    const u32 x = f << (16 * (k & 1));
+    fw0 |= (k >> 1) == 0 ? x : 0u;
+    fw1 |= (k >> 1) == 1 ? x : 0u;
+    fw2 |= (k >> 1) == 2 ? x : 0u;
+    fw3 |= (k >> 1) == 3 ? x : 0u;
+  };
   o.nfd = t.nfd;
   if (t.nfd <= kDDFdInline) {
     o.fdKind = FD_INLINE;
-    for (int i = 0; i < t.nfd; i++) o.fd[i] = s->fdPool[t.fdOff + i];
+    for (int i = 0; i < t.nfd; i++) put_fd(u32(i), s->fdPool[t.fdOff + i]);
   } else {  // a long template list stays in the structure's pool
     o.fdKind = FD_POOL;
     o.fdRef = t.fdOff;
   }
   o.nchain = s->numChains;
-  for (int w = 0; w < kDDChains / 8; w++) o.chainDiffs[w] = 0;
-  for (int c = 0; c < s->numChains; c++) o.chainDiffs[c >> 3] |= u64(dd_tmpl_chain(t, c)) << (8 * (c & 7));
+  {  // (four words by name, not by a run-time index: that put o on the private stack)
+    u64 w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    for (int c = 0; c < s->numChains; c++) {
+      const u64 v = u64(dd_tmpl_chain(t, c)) << (8 * (c & 7));
+      w0 |= (c >> 3) == 0 ? v : 0;
+      w1 |= (c >> 3) == 1 ? v : 0;
+      w2 |= (c >> 3) == 2 ? v : 0;
+      w3 |= (c >> 3) == 3 ? v : 0;
+    }
+    o.chainDiffs[0] = w0, o.chainDiffs[1] = w1, o.chainDiffs[2] = w2, o.chainDiffs[3] = w3;
+  }
   if (customDtis) {
     o.dtis = 0;
     for (int i = 0; i < s->numDT; i++) {
@@ -285,12 +304,13 @@ __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDSt
   if (customFdiffs) {
     const BitR at = b;  // (a list longer than kDDFdInline is read again into the spill)
     u32 n = 0;
+    fw0 = fw1 = fw2 = fw3 = 0;
     for (;;) {
       if ((e = b.bits(2, v))) return e;
       if (v == 0) break;
       u64 f;
       if ((e = b.bits(int(v) * 4, f))) return e;
-      if (n < u32(kDDFdInline)) o.fd[n] = u16(f + 1);
+      if (n < u32(kDDFdInline)) put_fd(n, u32(u16(f + 1)));
       n++;
     }
     o.nfd = u16(n);
@@ -314,12 +334,19 @@ __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDSt
     }
   }
   if (customChains) {
-    for (int w = 0; w < kDDChains / 8; w++) o.chainDiffs[w] = 0;
+    u64 w0 = 0, w1 = 0, w2 = 0, w3 = 0;
     for (int c = 0; c < s->numChains; c++) {
       if ((e = b.bits(8, v))) return e;
-      o.chainDiffs[c >> 3] |= v << (8 * (c & 7));
+      const u64 x = v << (8 * (c & 7));
+      w0 |= (c >> 3) == 0 ? x : 0;
+      w1 |= (c >> 3) == 1 ? x : 0;
+      w2 |= (c >> 3) == 2 ? x : 0;
+      w3 |= (c >> 3) == 3 ? x : 0;
     }
+    o.chainDiffs[0] = w0, o.chainDiffs[1] = w1, o.chainDiffs[2] = w2, o.chainDiffs[3] = w3;
   }
+  o.fd[0] = u16(fw0), o.fd[1] = u16(fw0 >> 16), o.fd[2] = u16(fw1), o.fd[3] = u16(fw1 >> 16);
+  o.fd[4] = u16(fw2), o.fd[5] = u16(fw2 >> 16), o.fd[6] = u16(fw3), o.fd[7] = u16(fw3 >> 16);
   if (s->numRes && o.sid >= s->numRes) return INVALID;
   return OK;
 }

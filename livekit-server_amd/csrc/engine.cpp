@@ -2046,8 +2046,12 @@ int lkf_sync(lkf_engine *e) {
     e->err = "batch not grouped by track / bad track handle";
     return LKF_EORDER;
   }
+  if (acc & 64u) {
+    e->err = "output or tuple capacity exceeded (decide: the batch's DD arena)";
+    return LKF_ENOSPC;
+  }
   if (acc & 12u) {
-    e->err = (acc & 8u) ? "output or tuple capacity exceeded (decide: tuple slots or DD arena)"
+    e->err = (acc & 8u) ? "output or tuple capacity exceeded (decide: tuple slots)"
                         : "output or tuple capacity exceeded (emit: output records or bytes)";
     return LKF_ENOSPC;
   }

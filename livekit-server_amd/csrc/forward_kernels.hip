@@ -1974,7 +1974,7 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
     if (lane_id() == 0) off = atomicAdd((unsigned long long *)o.ddUsed, (unsigned long long)f.ddLen);
     off = rl64(off, 0);
     if (off + u64(f.ddLen) > o.ddCap) {
-      if (lane_id() == 0) atomicOr(L.err, 8u);
+      if (lane_id() == 0) atomicOr(L.err, 64u);  // (the DD arena)
       flags &= ~u32(T_DD);
       ddLen = 0;
     } else {
@@ -2130,6 +2130,9 @@ __global__ void __launch_bounds__(64) k_layer_index(const RunDesc *__restrict__ 
 // update, a reorder, padding) goes through decide_step, as in the simulcast
 // runs.
 // ---------------------------------------------------------------------------
+#ifndef LKF_SVC_CHAINS  // chain breaks / restarts decided in SVC runs (0: they end the run; A/B)
+#define LKF_SVC_CHAINS 1
+#endif
 constexpr int kSvcDDBytes = 48;  // per-lane marshal buffer (a descriptor without a structure fits)
 constexpr int kSvcFrames = 72;   // frame decisions of one run: frame cLast + up to 64 later frames
 enum : u32 { SK_BAD = 0, SK_FWD = 1, SK_MDROP = 2, SK_NDROP = 3 };  // lane kinds of an SVC run
@@ -2180,6 +2183,10 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   int hiPos = -1, maxTgt = -1;
   u32 hiTarget = 0;
   bool swAll = false;  // a selected packet would switch layers
+  // chains whose restart would change the selection: those of the eligible
+  // decode targets above the selected one (all broken, or one would have been
+  // picked); the selected target's own chain (hiChain) may not break in a run
+  u32 aboveM = 0, hiChain = 0xffffffffu;
   if (DDK && dd) {
     const DDState &d = *L.dd;
     uni = (d.flags & DS_KF_VALID) && (d.flags & DS_CACHE_INIT);
@@ -2191,8 +2198,10 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       if (d.numChains == 0 || !((d.chBroken >> s->protectedBy[target]) & 1)) {
         hiPos = i;
         hiTarget = u32(target);
+        if (d.numChains) hiChain = s->protectedBy[target];
         break;
       }
+      aboveM |= 1u << s->protectedBy[target];
     }
     swAll = hiPos >= 0 && (i32(s->dtS[hiPos]) != L.h.curS || i32(s->dtT[hiPos]) != L.h.curT);
   }
@@ -2208,6 +2217,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   int ddLen = 0;
   u64 ddEfn = 0;
   bool ddPut = false, ddFwdSel = false;
+  u32 chBrk = 0, chRst = 0;  // chains this lane breaks / restarts (FrameChain.OnFrame)
   if (!dd) {  // ---- VP9.Select
     const bool isV = p.flags & LKF_PKT_VP9;
     const bool U = p.vp9 & LKF_VP9_U, B = p.vp9 & LKF_VP9_B, E = p.vp9 & LKF_VP9_E, P = p.vp9 & LKF_VP9_P;
@@ -2335,18 +2345,41 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       bool old;
       return dd::c_decision(d, e, old);
     };
-    if (eval && good) {  // FrameChain.OnFrame (framechain.go:43-92): every active chain stays intact
+    // FrameChain.OnFrame (framechain.go:43-92) of every active chain, before
+    // the selection: a restart (diff 0) clears the chain's broken bit and its
+    // expected frames; an intact chain whose previous frame is not forwarded
+    // breaks.  In a run: breaks of chains that do not protect the selected
+    // target, and restarts of chains that protect no eligible target above it
+    // and wait on no frame, leave every lane's selection as the run start has
+    // it; they are recorded per lane (chBrk / chRst) and the chain's state
+    // after the run is its last event's.  A lane sees a chain broken by an
+    // earlier lane of the run as broken (the reference skips it) and so
+    // records nothing it would not; restarts and breaks of the selected
+    // target's chain, and frames still undecided (an expectation), take the
+    // full step.
+    if (eval && good)  // restarts
+      for (int c = 0; c < int(d.numChains); c++) {
+        if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c || dd_chain_diff(*dpg, c) != 0) continue;
+        if (((aboveM >> c) & 1) || d.expCount[c] != 0 || (!LKF_SVC_CHAINS && ((d.chBroken >> c) & 1)))
+          good = false;
+        else if (LKF_SVC_CHAINS)
+          chRst |= 1u << c;
+      }
+    u32 rstSeen = 0;  // chains an earlier lane of the window restarted (intact from there)
+    for (int c = 0; c < int(d.numChains); c++)
+      if (__ballot(inWin && ((chRst >> c) & 1)) & lt) rstSeen |= 1u << c;
+    if (eval && good)  // breaks
       for (int c = 0; c < int(d.numChains); c++) {
         if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c) continue;
         const u32 diff = dd_chain_diff(*dpg, c);
-        const bool broken = (d.chBroken >> c) & 1;
-        if (diff == 0) {
-          good = good && !broken;  // (a broken chain restarting: full step)
-          continue;
-        }
-        if (!broken && dec(efn - diff) != dd::SD_FORWARDED) good = false;
+        if (diff == 0 || (((d.chBroken & ~rstSeen) >> c) & 1)) continue;  // (a restart; a chain broken before this lane)
+        const u32 sd = dec(efn - diff);
+        if (sd == dd::SD_FORWARDED) continue;
+        if (sd == dd::SD_UNKNOWN || u32(c) == hiChain || !LKF_SVC_CHAINS)  // (expectFrames / the selection)
+          good = false;
+        else
+          chBrk |= 1u << c;
       }
-    }
     SVC_WHY(8);
     if (ddFwdSel) good = good && dp.fdKind == FD_INLINE;  // (a pooled or spilled list: full step)
     if (ddFwdSel && good)  // a referenced frame that was dropped drops this one (:192-201): full step
@@ -2415,6 +2448,19 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   const u64 runM = (x >= 64 ? ~0ull : ((1ull << x) - 1)) & ~((1ull << pos) - 1);
   const bool inRun = (runM >> lane) & 1;
   if (DDK && dd) {
+    // ---- frame chains: each chain ends in the state of its run's last event
+    // (a break sets its bit, a restart clears it; restarts here wait on no
+    // frame, so its expected frames stay empty)
+    {
+      DDState &d = *L.dd;
+      for (int c = 0; c < int(d.numChains); c++) {
+        const u64 bm = __ballot(inRun && ((chBrk >> c) & 1)), rm = __ballot(inRun && ((chRst >> c) & 1));
+        if (!(bm | rm)) continue;
+        const int lb = bm ? 63 - __clzll(bm) : -1, lr = rm ? 63 - __clzll(rm) : -1;
+        if (lane == 0) d.chBroken = lb > lr ? (d.chBroken | (1u << c)) : (d.chBroken & ~(1u << c));
+      }
+      wave_lds_sync();
+    }
     // ---- decision cache (selectordecisioncache.go:112-165) for the frames the
     // run added, in lane order: a new frame fills the entries it skipped with
     // unknown, marks the entries kNack behind the previous last frame missing
@@ -2529,7 +2575,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       if (lane == 0) base = atomicAdd(reinterpret_cast<unsigned long long *>(o.ddUsed), (unsigned long long)dTot);
       base = rl64(base, 0);
       if (base + dTot > o.ddCap) {
-        if (lane == 0) atomicOr(L.err, 8u);
+        if (lane == 0) atomicOr(L.err, 64u);  // (the DD arena)
         ddKeep = false;
       } else if (ddOn) {
         // (a fixed-trip copy: a loop bounded by the per-lane length made the
@@ -2839,7 +2885,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   o.outW = A.wide + slot0;
   // SVC DownTracks (one SSRC, every packet relevant to the selector): svc_run
   // (the host schedules them in k_decide_dt<true>)
-  const bool svcDT = 0 != 5 && DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
+  const bool svcDT = DDK && (L.h.flags & F_VIDEO) && !(L.h.flags & F_SIMULCAST) &&
                      ((L.h.flags & F_VP9) || ((L.h.flags & F_DD) && ddDT));
   u32 nextAt = ev < evEnd ? A.events[ev].at : 0xffffffffu;
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);

@@ -5,8 +5,8 @@
 //   k_ing_parse    thread per datagram: rtp.Packet.Unmarshal (pion/rtp
 //                  v1.8.3, restated), the ssrc-audio-level extension
 //                  (RFC 6464) and the VP8 payload descriptor
-//                  (buffer/helpers.go:76-162)
-//   k_ing_ranges   datagrams grouped by track -> [begin, end) per track
+//                  (buffer/helpers.go:76-162); datagrams grouped by track
+//                  -> [begin, end) per track
 //   k_ing_stream_wave  one wave per received stream (buffer.Buffer), its
 //                  datagrams in order: processHeaderExtensions ->
 //                  AudioLevel.Observe (buffer.go:573-596, audiolevel.go:70-102),
@@ -382,10 +382,18 @@ __device__ __forceinline__ bool vp9_parse(BP p, int len, IngParsed &q) {
 constexpr int kParseT = 64;       // k_ing_parse block (8 KB of LDS: fits beside the decide waves)
 constexpr int kParseStage = 128;  // bytes of each datagram staged in LDS
 constexpr int kStageW = kParseStage / 4 + 1;  // dwords per thread: a dword-aligned window (odd stride: no bank conflicts)
+// (with the per-track datagram ranges: a datagram's track is its stream's,
+// so the boundaries need no parse — k_ing_ranges' work, one dispatch fewer
+// on the ingest chain)
+__device__ __forceinline__ u32 raw_track(const lkf_raw_pkt *raws, const DevStream *streams, u32 nstreams, u32 i) {
+  const u32 sid = raws[i].stream;
+  return sid < nstreams ? streams[sid].track : 0xffffffffu;
+}
 __global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__restrict__ raws, u32 n,
                                                       const u8 *__restrict__ raw, const DevStream *__restrict__ streams,
                                                       u32 nstreams, IngParsed *__restrict__ out, u32 *__restrict__ twcc,
-                                                      u32 *__restrict__ err) {
+                                                      u32 *__restrict__ err, u32 ntracks, u32 *__restrict__ tBegin,
+                                                      u32 *__restrict__ tEnd, u32 *__restrict__ tRuns) {
   __shared__ u32 sStage[kParseT * kStageW];
   const u32 lane = threadIdx.x;
   const u32 i = blockIdx.x * blockDim.x + lane;
@@ -416,6 +424,20 @@ __global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__rest
   }
   __syncthreads();
   if (i >= n) return;
+  {  // per-track ranges (k_ing_init zeroed them)
+    const u32 t = raw_track(raws, streams, nstreams, i);
+    if (t < ntracks) {
+      const u32 tp = i > 0 ? raw_track(raws, streams, nstreams, i - 1) : 0xffffffffu;
+      const u32 tn = i + 1 < n ? raw_track(raws, streams, nstreams, i + 1) : 0xffffffffu;
+      if (tp != t) {
+        tBegin[t] = i;
+        if (atomicAdd(&tRuns[t], 1u) != 0) atomicOr(err, 2u);
+      }
+      if (tn != t) tEnd[t] = i + 1;
+    } else {
+      atomicOr(err, 1u);
+    }
+  }
   u32 *const st = sStage + lane * kStageW;
   IngParsed q = {};
   twcc[i] = 0;
@@ -457,24 +479,6 @@ __global__ void __launch_bounds__(kParseT) k_ing_parse(const lkf_raw_pkt *__rest
     }
   }
   out[i] = q;
-}
-
-__global__ void k_ing_ranges(const IngParsed *__restrict__ q, u32 n, u32 ntracks, u32 *__restrict__ tBegin,
-                             u32 *__restrict__ tEnd, u32 *__restrict__ tRuns, u32 *__restrict__ err) {
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const u32 t = q[i].track;
-  if (t >= ntracks) {
-    atomicOr(err, 1u);
-    return;
-  }
-  const u32 tp = i > 0 ? q[i - 1].track : 0xffffffffu;
-  const u32 tn = i + 1 < n ? q[i + 1].track : 0xffffffffu;
-  if (tp != t) {
-    tBegin[t] = i;
-    if (atomicAdd(&tRuns[t], 1u) != 0) atomicOr(err, 2u);
-  }
-  if (tn != t) tEnd[t] = i + 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -2259,9 +2263,7 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
                        a.total, a.bucket ? a.bucket->store : nullptr);
   }
   hipLaunchKernelGGL(k_ing_parse, dim3(nblk(a.n, kParseT)), dim3(kParseT), 0, st, a.raws, a.n, a.raw, a.streams, a.nstreams,
-                     a.parsed, a.twcc, a.err);
-  hipLaunchKernelGGL(k_ing_ranges, dim3(nblk(a.n, 256)), dim3(256), 0, st, a.parsed, a.n, a.ntracks, a.tBegin, a.tEnd,
-                     a.tRuns, a.err);
+                     a.parsed, a.twcc, a.err, a.ntracks, a.tBegin, a.tEnd, a.tRuns);
   hipLaunchKernelGGL(k_ing_lists, dim3(a.ntracks), dim3(64), 0, st, a.raws, a.streams, a.nstreams, a.tBegin,
                      a.tEnd, a.listStride, a.list, a.listCnt);
   if (a.nstreams) {

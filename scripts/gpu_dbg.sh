@@ -7,14 +7,16 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${OUT_NAME:-dbg1}; mkdir -p $O
-timeout -k 10 ${PYTEST_TIMEOUT:-480} python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread \
-  ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_gpu.log | tail -15
-[ $rc -le 1 ] || exit $rc
-K="test_provisional_pass_matches_oracle or dd_wide or test_config5_av1_vp9_dd"
-for lib in ${DBG_LIBS:-liblkfwd_w5.so}; do
-  LKF_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_alloc_gpu.py tests/test_parity_gpu.py tests/test_ingress_gpu.py -m gpu -v --timeout 200 --timeout-method thread -k "$K" > $O/$lib.log 2>&1
-  rc=$?; echo "$lib rc=$rc"; grep -E "PASS|FAIL|Error:" $O/$lib.log | head -20
+if [ "${FULL:-0}" = "1" ]; then
+  timeout -k 10 ${PYTEST_TIMEOUT:-480} python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread \
+    ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_gpu.log | tail -15
+  [ $rc -le 1 ] || exit $rc
+fi
+K="${DBG_K:-provisional_pass_matches_oracle or dd_tracker_matches_oracle}"
+for lib in ${DBG_LIBS:-liblkfwd.so liblkfwd_checked.so}; do
+  LKF_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_alloc_gpu.py tests/test_tracker_gpu.py -m gpu -v --timeout 200 --timeout-method thread -k "$K" > $O/$lib.log 2>&1
+  rc=$?; echo "$lib rc=$rc"; grep -E "PASS|FAIL|Error:|CK_|check" $O/$lib.log | head -20
   [ $rc -le 1 ] || exit $rc
 done
 if [ "${SVC:-1}" = "1" ]; then
@@ -22,9 +24,11 @@ if [ "${SVC:-1}" = "1" ]; then
   rc=$?; echo "svc rc=$rc"; tail -12 $O/svc_stats.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "${AB:-1}" = "1" ]; then
-  AB_LIBS="liblkfwd.so liblkfwd_iw3.so" AB_REPS=2 \
+  AB_LIBS="liblkfwd.so liblkfwd_iw3.so liblkfwd_dw4.so" AB_REPS=2 \
   AB_SHAPES="--steps 20 --warmup 5 --no-cpu-baseline --no-parity|--batch-s 0.01 --rooms 1000 --steps 100 --warmup 20 --no-cpu-baseline --no-parity" \
   OUT_NAME=${OUT_NAME:-dbg1}/ab bash scripts/gpu_ab.sh || exit $?
+  AB_LIBS="liblkfwd.so liblkfwd_w3.so" AB_REPS=2 AB_SHAPES="--config 5 --steps 5 --warmup 2 --no-cpu-baseline --no-parity" \
+  OUT_NAME=${OUT_NAME:-dbg1}/ab5 bash scripts/gpu_ab.sh || exit $?
   AB_ENVS="-|LKF_PREP_RESERVE=2|LKF_PREP_RESERVE=4|LKF_PREP_RESERVE=8" AB_REPS=1 \
   OUT_NAME=${OUT_NAME:-dbg1}/env bash scripts/gpu_env_ab.sh || exit $?
 fi

@@ -24,6 +24,8 @@ def main():
     eng = pkg.Engine.for_trace(tr)
     workload.load_topology(eng.api, eng.h, tr)
     fn = eng.lib.lkf_debug_svc_stats
+    fn.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
+    fn.restype = C.c_int
     out = (C.c_uint64 * 32)()
     fn(eng.h, out, 1)
     for b in range(tr.nbatches):
