@@ -224,6 +224,7 @@ struct lkf_engine {
   // its graphs when its epoch is older
   uint64_t epoch = 1;
   bool useGraph = true;  // LKF_GRAPH=0: the stages as direct launches (A/B)
+  bool debugDD = false;  // LKF_DEBUG_DD=1: report the DD cursors (diagnostic)
 
   // device: persistent state
   DevTrack *dTracks = nullptr;
@@ -897,24 +898,6 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     e->ingS = e->prepS;
     A(hipExtStreamCreateWithCUMask(&e->emitS, words, mB.data()));
     A(hipExtStreamCreateWithCUMask(&e->sendS, words, mB.data()));
-  } else if (const char *rv = getenv("LKF_PREP_RESERVE"); rv && atoi(rv) > 0 && atoi(rv) < 32) {
-    // LKF_PREP_RESERVE=K (A/B): of every 32 CUs, K are left to the prep
-    // stream alone (the ingest + batch-prep chain, the pipelined step's
-    // critical path); prep keeps every CU, the other streams the rest
-    const int k = atoi(rv);
-    int ncu = 256;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device);
-    const uint32_t words = uint32_t((ncu + 31) / 32);
-    std::vector<uint32_t> mAll(words, 0), mRest(words, 0);
-    for (int i = 0; i < ncu; i++) {
-      mAll[size_t(i / 32)] |= 1u << (i % 32);
-      if ((i % 32) >= k) mRest[size_t(i / 32)] |= 1u << (i % 32);
-    }
-    A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
-    e->ingS = e->prepS;
-    A(hipExtStreamCreateWithCUMask(&e->decS, words, mRest.data()));
-    A(hipExtStreamCreateWithCUMask(&e->emitS, words, mRest.data()));
-    A(hipExtStreamCreateWithCUMask(&e->sendS, words, mRest.data()));
   } else {
     A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
     A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
@@ -1077,6 +1060,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   if (const char *v = getenv("LKF_GRAPH")) e->useGraph = atoi(v) != 0;
+  if (const char *v = getenv("LKF_DEBUG_DD")) e->debugDD = atoi(v) != 0;
   return e;
 }
 
@@ -1094,6 +1078,9 @@ void lkf_destroy(lkf_engine *e) {
   if (e->prepS) (void)hipStreamSynchronize(e->prepS);
   if (e->decS) (void)hipStreamSynchronize(e->decS);
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
+  if (e->sendS) (void)hipStreamSynchronize(e->sendS);  // (bucket copies, sender updates)
+  if (e->sideS) (void)hipStreamSynchronize(e->sideS);  // (NACK queues)
+  (void)hipDeviceSynchronize();                        // (anything else queued before the buffers go)
   for (void *p : {static_cast<void *>(e->dNacks), static_cast<void *>(e->dNackG), static_cast<void *>(e->dNackValid),
                   static_cast<void *>(e->dRtx), static_cast<void *>(e->dRtxSrc), static_cast<void *>(e->dRtxLen),
                   static_cast<void *>(e->dRtxOff), static_cast<void *>(e->dRtxIn), static_cast<void *>(e->dRtxOut),
@@ -1687,6 +1674,11 @@ int lkf_run(lkf_engine *e, void *stream) {
     ka.swap(kb);
   }
   if (nev > x.stageCap || !x.stage) {  // (graphs captured with the old staging are re-captured)
+    // the queued pull of this context's previous run may still read the old
+    // staging, and its graphs are destroyed when re-captured: drain first
+    if (x.stage) {
+      if (int rc = drain_streams(e)) return rc;
+    }
     stage_free(&x.stage, &x.stageDev);
     x.stageCap = uint32_t(std::max<size_t>(2 * nev, 4096));
     HIPCHK(stage_alloc(&x.stage, &x.stageDev, sizeof(RunDesc) + size_t(x.stageCap) * (sizeof(DevEvent) + 4)),
@@ -1727,7 +1719,9 @@ int lkf_run(lkf_engine *e, void *stream) {
     // ps waits on that run's "emitted" event above, so draining ps covers its
     // prep, decide and emit stages (the lane list is read by k_ev_offsets on ps,
     // the ops and offsets by the decide stage).
-    HIPCHK(hipStreamSynchronize(ps), "sync before events realloc");
+    // (every stream: the pull graph on the engine's own stream reads them too,
+    // and the graphs captured with them are destroyed below)
+    if (int rc = drain_streams(e)) return rc;
     if (nev > x.evCap) {
       if (x.dEvents) HIPCHK(dfree(x.dEvents), "free events");
       x.evCap = std::max<uint64_t>(2 * nev, 4096);
@@ -1776,12 +1770,11 @@ int lkf_run(lkf_engine *e, void *stream) {
                        nullptr, x.dTot + 0, nullptr, nullptr),
            "slot scan");
     HIPCHK(launch_layer_index(ps, x.dDesc, x.dTBegin, x.dTEnd, nt, e->cfg.max_batch_pkts, x.dLayerList,
-                              x.dLayerBefore, x.dLayerCnt),
+                              x.dLayerBefore, x.dLayerCnt, e->ddAlloc ? x.dDDUsed : nullptr),
            "layer index");
     if (e->nTrk)  // StreamTracker.Observe of every (track, spatial layer) tracker (receiver.go:686-695)
       HIPCHK(launch_tracker_observe(ps, e->dTrk, e->nTrk, x.dDesc, x.dTBegin, x.dTEnd), "tracker observe");
     if (e->ddAlloc) {  // dependency descriptors of this batch (track structure rings advance in order)
-      HIPCHK(hipMemsetAsync(x.dDDUsed, 0, 2 * sizeof(uint64_t), ps), "dd cursor reset");
       HIPCHK(launch_dd_decode(ps, x.dDesc, x.dTBegin, x.dTEnd, e->dTracks, nt, e->dDDStruct, e->dDDTrack, x.dDDPkt,
                               x.dErr, e->nDDTrk ? e->dTrackDDTrk : nullptr, e->dDDTrk, x.dDDSpill,
                               reinterpret_cast<uint32_t *>(x.dDDUsed + 1), e->ddSpillCap),
@@ -1802,7 +1795,12 @@ int lkf_run(lkf_engine *e, void *stream) {
   // (re)captures a stage as a graph on stream st: the captured launches are the
   // same as the direct ones
   auto capture = [&](hipStream_t st, hipGraphExec_t &g, auto body) -> int {
-    if (g) HIPCHK(hipGraphExecDestroy(g), "graph destroy");
+    // an exec is destroyed only once its last launch (on st, this context's
+    // previous run) has finished: HIP may release its kernel arguments at once
+    if (g) {
+      HIPCHK(hipStreamSynchronize(st), "graph idle");
+      HIPCHK(hipGraphExecDestroy(g), "graph destroy");
+    }
     g = nullptr;
     HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "begin capture");
     const int rc = body();
@@ -1841,6 +1839,14 @@ int lkf_run(lkf_engine *e, void *stream) {
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(x.prepped, ps), "event");
+  if (e->debugDD && e->ddAlloc) {  // LKF_DEBUG_DD=1 (diagnostic): the context's DD cursor after its prep
+    HIPCHK(hipStreamSynchronize(ps), "debug sync");
+    uint64_t u[2] = {0, 0};
+    HIPCHK(hipMemcpy(u, x.dDDUsed, sizeof(u), hipMemcpyDeviceToHost), "debug copy");
+    fprintf(stderr, "[lkf dd] run %llu ctx %d after prep: cursor %llu spill %llu graph %d epoch %llu/%llu\n",
+            (unsigned long long)e->nRuns, ci, (unsigned long long)u[0], (unsigned long long)u[1], int(e->useGraph),
+            (unsigned long long)x.gPrepEpoch, (unsigned long long)e->epoch);
+  }
   HIPCHK(hipStreamWaitEvent(s, x.prepped, 0), "wait prep");
   DecideLaunch d;
   d.layerList = x.dLayerList;
@@ -2019,6 +2025,14 @@ int lkf_sync(lkf_engine *e) {
   if (rc) return rc;
   uint32_t acc = 0;
   D2H(&acc, e->dSticky, sizeof(acc), "err copy");
+  if (e->debugDD && e->ddAlloc) {
+    for (int c = 0; c < lkf_engine::kCtx; c++) {
+      uint64_t u[2] = {0, 0};
+      if (hipMemcpy(u, e->ctx[c].dDDUsed, sizeof(u), hipMemcpyDeviceToHost) == hipSuccess)
+        fprintf(stderr, "[lkf dd] sync after run %llu: ctx %d cursor %llu (%p)\n", (unsigned long long)e->nRuns, c,
+                (unsigned long long)u[0], static_cast<void *>(e->ctx[c].dDDUsed));
+    }
+  }
   if (!acc) return LKF_OK;
   HIPCHK(hipMemset(e->dSticky, 0, sizeof(uint32_t)), "err reset");
   HIPCHK(hipDeviceSynchronize(), "err reset sync");  // null-stream memset vs the engine's streams
@@ -2048,6 +2062,45 @@ int lkf_sync(lkf_engine *e) {
   }
   if (acc & 64u) {
     e->err = "output or tuple capacity exceeded (decide: the batch's DD arena)";
+    if (e->ddAlloc) {  // (the contexts' cursors, for the report)
+      char buf[192];
+      size_t o = 0;
+      for (auto &x : e->ctx) {
+        uint64_t u[2] = {0, 0};
+        if (x.dDDUsed && hipMemcpy(u, x.dDDUsed, sizeof(u), hipMemcpyDeviceToHost) == hipSuccess && o < sizeof(buf))
+          o += size_t(snprintf(buf + o, sizeof(buf) - o, " %llu/%llu", (unsigned long long)u[0],
+                               (unsigned long long)e->ddArenaCap));
+      }
+      e->err += " used/cap:";
+      e->err += buf;
+      // (diagnostic) the live allocations around context 0's cursor, and the
+      // contexts' small buffers by name
+      const uintptr_t c0 = reinterpret_cast<uintptr_t>(e->ctx[0].dDDUsed);
+      {
+        std::lock_guard<std::mutex> g(dreg().m);
+        for (auto it = dreg().a.lower_bound(c0 > (1u << 20) ? c0 - (1u << 20) : 0);
+             it != dreg().a.end() && it->first < c0 + (1u << 20); ++it) {
+          char t[64];
+          snprintf(t, sizeof(t), " [%+lld:%zu]", (long long)(intptr_t(it->first) - intptr_t(c0)), it->second);
+          e->err += t;
+        }
+      }
+      for (int c = 0; c < lkf_engine::kCtx; c++) {
+        const BatchCtx &x = e->ctx[c];
+        const void *ps[] = {x.dTBegin, x.dTEnd, x.dTRuns, x.dErr, x.dTot, x.dDesc, x.dEvents, x.dEvOff, x.dEvLane,
+                            x.dDDUsed, x.dStats, x.dPartA, x.dFBase, x.dLayerCnt, x.dTwccBase};
+        const char *nm[] = {"tB", "tE", "tR", "err", "tot", "desc", "ev", "evoff", "evlane", "ddu", "stats",
+                            "partA", "fbase", "lcnt", "twcc"};
+        for (size_t k = 0; k < sizeof(ps) / sizeof(ps[0]); k++) {
+          const intptr_t dlt = intptr_t(reinterpret_cast<uintptr_t>(ps[k])) - intptr_t(c0);
+          if (ps[k] && dlt > -(1 << 20) && dlt < (1 << 20)) {
+            char t[48];
+            snprintf(t, sizeof(t), " %d.%s%+lld", c, nm[k], (long long)dlt);
+            e->err += t;
+          }
+        }
+      }
+    }
     return LKF_ENOSPC;
   }
   if (acc & 12u) {

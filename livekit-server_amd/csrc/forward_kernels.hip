@@ -2034,10 +2034,11 @@ __device__ __forceinline__ void decide_step(Lane &L, const PktV &p, u32 k, LaneO
 #ifndef LKF_DECIDE_WAVES  // occupancy floor (waves per SIMD); 4 and 6 measured slower (r3, r5)
 #define LKF_DECIDE_WAVES 5
 #endif
-// (the DD selector's instantiation cannot reach that floor: it asks for 2, so
-// the compiler keeps VGPRs + AGPRs within 256 rather than drop to 1 wave)
+// (the DD selector's instantiation cannot reach that floor: at 3 waves per
+// SIMD it fits 168 VGPRs with 176 B of spills, 2 % faster on configs[4] than 2
+// waves at 254 VGPRs; asked for 5 the compiler gives up and drops to 1 wave)
 #ifndef LKF_DECIDE_DD_WAVES
-#define LKF_DECIDE_DD_WAVES 2
+#define LKF_DECIDE_DD_WAVES 3
 #endif
 #define DECIDE_ATTR __attribute__((amdgpu_waves_per_eu(DDK ? LKF_DECIDE_DD_WAVES : LKF_DECIDE_WAVES, 8)))
 
@@ -2073,9 +2074,13 @@ __device__ __forceinline__ bool steady_state(const Lane &L) {
 // before packet i.
 __global__ void __launch_bounds__(64) k_layer_index(const RunDesc *__restrict__ desc, const u32 *__restrict__ tBegin,
                                                     const u32 *__restrict__ tEnd, u32 stride, u32 *__restrict__ list,
-                                                    u32 *__restrict__ before, u32 *__restrict__ cnt) {
+                                                    u32 *__restrict__ before, u32 *__restrict__ cnt,
+                                                    u64 *__restrict__ zero2) {
   const lkf_pkt *__restrict__ pkts = reinterpret_cast<const lkf_pkt *>(desc->pkts);
   const u32 t = blockIdx.x, lane = threadIdx.x;
+  // (the batch's DD bump cursors start at zero: a kernel store on the prep
+  // chain rather than a memset node in the captured prep graph)
+  if (zero2 && t == 0 && lane < 2) zero2[lane] = 0;
   const u64 lt = (1ull << lane) - 1;
   const u32 b = tBegin[t], e = tEnd[t];
   u32 c0 = 0, c1 = 0, c2 = 0;
@@ -2210,6 +2215,10 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   u32 why = 0;
 #endif
   if (!uni) return pos;
+#if LKF_SVC_STATS
+  const u64 tA = __builtin_amdgcn_s_memtime();
+  u64 tB = tA, tC = tA;
+#endif
   bool good = inWin;
   u32 kind = SK_BAD;
   int nsr = LKF_DROP_NOT_SELECTED;  // reason of an SK_NDROP lane
@@ -2386,6 +2395,9 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       for (int j = 0; j < int(dp.nfd) && j < kDDFdInline; j++)
         if (dpg->fd[j] != 0 && dec(efn - dpg->fd[j]) == dd::SD_DROPPED) good = false;
     SVC_WHY(9);
+#if LKF_SVC_STATS
+    tB = __builtin_amdgcn_s_memtime();
+#endif
     if (ddFwdSel && good) {
       // frame number (FrameNumberWrapper without a structure update) and the
       // descriptor marshalled with the active mask in force (:223-262)
@@ -2398,6 +2410,9 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
     }
     SVC_WHY(10);
+#if LKF_SVC_STATS
+    tC = __builtin_amdgcn_s_memtime();
+#endif
     kind = ddFwdSel ? SK_FWD : (relevantDrop ? SK_MDROP : SK_NDROP);  // (RTPMarker false for the drops)
     ddEfn = efn;
     ddPut = firstAdd;
@@ -2442,6 +2457,14 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       atomicAdd(&g_svc[1], (unsigned long long)(x > pos ? x - pos : 0));
       if (x < n) atomicAdd(&g_svc[16 + (wx ? wx : 15)], 1ull);
     }
+  }
+#endif
+#if LKF_SVC_STATS
+  const u64 tD = __builtin_amdgcn_s_memtime();
+  if (lane == 0 && dd) {
+    atomicAdd(&g_svc[10], (unsigned long long)(tB - tA));
+    atomicAdd(&g_svc[11], (unsigned long long)(tC - tB));
+    atomicAdd(&g_svc[12], (unsigned long long)(tD - tC));
   }
 #endif
   if (x <= pos) return pos;
@@ -2749,6 +2772,12 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   while (todo) {
   const u32 jw = u32(__ffsll(static_cast<long long>(todo))) - 1;
   todo &= todo - 1;
+#if LKF_SVC_STATS
+  // per-phase cycles of the SVC DownTracks (g_svc[4..9]: prologue, runs,
+  // full steps after runs, chunk tails, epilogue, DownTracks)
+  const u64 tP0 = __builtin_amdgcn_s_memtime();
+  u64 tRun = 0, tStep = 0;
+#endif
   // The lane index again, opaque to the compiler, so lane-derived values are
   // recomputed per DownTrack rather than hoisted out of the loop and held in
   // registers across the whole body.
@@ -2891,6 +2920,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const uint4 *src = reinterpret_cast<const uint4 *>(pkts);
 
   u32 kpos = pb;  // first packet of the track not yet decided
+#if LKF_SVC_STATS
+  const u64 tP1 = __builtin_amdgcn_s_memtime();
+#endif
   while (kpos < pe) {
     if (nextAt <= kpos) {
       while (nextAt <= kpos) {
@@ -2951,12 +2983,22 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         // SVC DownTrack: a run, then the stopping packet's full step (its
         // descriptor reloaded wave-uniform, so the chunk's raw registers are
         // dead on this path)
+#if LKF_SVC_STATS
+        const u64 tr0 = __builtin_amdgcn_s_memtime();
+#endif
         x = svc_run<DDK>(L, o, p, pi, n, pos, nextAt, valid, sentAcc, sSvcScr, sSvcFD);
         pos = x;
+#if LKF_SVC_STATS
+        const u64 tr1 = __builtin_amdgcn_s_memtime();
+        tRun += tr1 - tr0;
+#endif
         if (x < n && rl32(pi, x) < nextAt) {
           const u32 px = rl32(pi, x);
           decide_step<DDK>(L, load_pkt(pkts + px), px, o);
           vm_drain();
+#if LKF_SVC_STATS
+          tStep += __builtin_amdgcn_s_memtime() - tr1;
+#endif
 #if LKF_SVC_STATS
           if (lane == 0) atomicAdd(&g_svc[2], 1ull);
 #endif
@@ -3314,6 +3356,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     }
     kpos = lim;
   }
+#if LKF_SVC_STATS
+  const u64 tP2 = __builtin_amdgcn_s_memtime();
+#endif
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
   __syncthreads();
   reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
@@ -3367,6 +3412,17 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     for (int i = 0; i < LKF_DROP_NREASONS; i++)
       if (o.drops[i]) atomicAdd((unsigned long long *)&st[4 + i], (unsigned long long)o.drops[i]);
   }
+#if LKF_SVC_STATS
+  if (DDK && lane == 0 && (L.h.flags & (F_DD | F_VP9))) {
+    const u64 tP3 = __builtin_amdgcn_s_memtime();
+    atomicAdd(&g_svc[4], (unsigned long long)(tP1 - tP0));
+    atomicAdd(&g_svc[5], (unsigned long long)tRun);
+    atomicAdd(&g_svc[6], (unsigned long long)tStep);
+    atomicAdd(&g_svc[7], (unsigned long long)(tP2 - tP1 - tRun - tStep));
+    atomicAdd(&g_svc[8], (unsigned long long)(tP3 - tP2));
+    atomicAdd(&g_svc[9], 1ull);
+  }
+#endif
   }  // next DownTrack of this wave
 }
 
@@ -4664,9 +4720,10 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
 }
 
 hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const u32 *tBegin, const u32 *tEnd, u32 ntracks,
-                              u32 stride, u32 *list, u32 *before, u32 *cnt) {
+                              u32 stride, u32 *list, u32 *before, u32 *cnt, u64 *zero2) {
   if (!ntracks) return hipSuccess;
-  hipLaunchKernelGGL(k_layer_index, dim3(ntracks), dim3(64), 0, s, desc, tBegin, tEnd, stride, list, before, cnt);
+  hipLaunchKernelGGL(k_layer_index, dim3(ntracks), dim3(64), 0, s, desc, tBegin, tEnd, stride, list, before, cnt,
+                     zero2);
   return hipGetLastError();
 }
 

@@ -220,7 +220,8 @@ hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a, hipStream_t side,
 hipError_t launch_speakers(hipStream_t s, const SpeakersLaunch &a);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
-                              uint32_t ntracks, uint32_t stride, uint32_t *list, uint32_t *before, uint32_t *cnt);
+                              uint32_t ntracks, uint32_t stride, uint32_t *list, uint32_t *before, uint32_t *cnt,
+                              uint64_t *zero2 = nullptr);
 hipError_t launch_emit(hipStream_t s, const EmitLaunch &a);
 hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                             const DevTrack *tracks, uint32_t ntracks, DDStruct *structs, DDTrack *ddTracks, DDPkt *out,

@@ -42,6 +42,11 @@ def main():
         print(f"batch {b}: n={n} {dt*1e3:.1f} ms  runs={v[0]} run_pkts={v[1]} full_steps={v[2]} refused={v[3]}",
               flush=True)
         print("   stops: " + ", ".join(f"{WHY.get(i, i)}={v[16 + i]}" for i in range(16) if v[16 + i]), flush=True)
+        if v[9]:  # per SVC DownTrack, s_memtime (shader clock) cycles, thousands
+            print("   per DT (kcycles): prologue %.1f runs %.1f full steps %.1f rest of loop %.1f epilogue %.1f (n=%d)" %
+                  tuple([v[k] / v[9] / 1000.0 for k in (4, 5, 6, 7, 8)] + [v[9]]), flush=True)
+            print("   in DD runs (kcycles per DT): decision %.1f marshal %.1f munger/seq decision %.1f" %
+                  tuple(v[k] / v[9] / 1000.0 for k in (10, 11, 12)), flush=True)
     tr.close()
 
 
