@@ -109,6 +109,60 @@ __device__ __forceinline__ u32 dti_at(u64 dtis, int i) { return u32(dtis >> (2 *
 // ProcessFrameDependencyStructure: decode-target layers = max (S, T) over the
 // templates that are present in the target; sorted high -> low by
 // VideoLayer.GreaterThan (insertion sort: Go's pdqsort below 12 elements)
+struct Match {
+  int idx;
+  bool cDtis, cFdiffs, cChains;
+  int extra;
+};
+
+// calculateMatch of template j for a packet that uses template k without
+// custom fields (its frame diffs, DTIs and chain diffs are template k's)
+#ifndef LKF_DD_FASTBEST
+#define LKF_DD_FASTBEST 1  // marshal: the structure's precomputed best template (tmpl_best)
+#endif
+
+__device__ inline Match tmpl_match(const DDStruct &s, int j, int k) {
+  const DDTmpl &t = s.t[j], &q = s.t[k];
+  Match m;
+  m.idx = j;
+  bool fdEq = t.nfd != 0 && t.nfd == q.nfd;
+  for (int i = 0; fdEq && i < q.nfd; i++) fdEq = s.fdPool[q.fdOff + i] == s.fdPool[t.fdOff + i];
+  m.cFdiffs = !fdEq;
+  const u64 dm = s.numDT >= 32 ? ~u64(0) : ((u64(1) << (2 * s.numDT)) - 1);
+  m.cDtis = (q.dtis & dm) != (t.dtis & dm);
+  m.cChains = false;
+  for (int i = 0; i < s.numChains; i++)
+    if (dd_tmpl_chain(q, i) != dd_tmpl_chain(t, i)) {
+      m.cChains = true;
+      break;
+    }
+  m.extra = 0;
+  if (m.cFdiffs) m.extra = 2 * (1 + q.nfd) + 4 * q.nfd;  // (template frame diffs are 1-16: 4 bits each)
+  if (m.cDtis) m.extra += 2 * s.numDT;
+  if (m.cChains) m.extra += 8 * s.numChains;
+  return m;
+}
+
+// findBestTemplate (dependencydescriptorwriter.go) for every template's
+// custom-field-free packets, as dd_marshal_inl runs it
+__device__ inline void tmpl_best(DDStruct &s) {
+  for (int k = 0; k < s.numTmpl; k++) {
+    const DDTmpl &q = s.t[k];
+    int first = 0;
+    while (first < s.numTmpl && !(s.t[first].sid == q.sid && s.t[first].tid == q.tid)) first++;
+    int lastIdx = 0;  // as written: the last index whose layer differs
+    for (int i = first; i < s.numTmpl; i++)
+      if (s.t[i].sid != q.sid || s.t[i].tid != q.tid) lastIdx = i;
+    Match best = tmpl_match(s, first, k);
+    for (int i = first + 1; i <= lastIdx; i++) {
+      const Match m = tmpl_match(s, i, k);
+      if (m.extra < best.extra) best = m;
+    }
+    s.t[k].best = u8(best.idx);
+    s.t[k].bestC = u8((best.cDtis ? 1 : 0) | (best.cFdiffs ? 2 : 0) | (best.cChains ? 4 : 0));
+  }
+}
+
 __device__ inline void process_structure(DDStruct &s) {
   for (int t = 0; t < s.numDT; t++) {
     int ls = 0, lt = 0;
@@ -154,6 +208,7 @@ __device__ inline int read_structure(BitR &b, DDStruct &s) {
     t.tid = u8(tid);
     t.nfd = 0;
     t.fdOff = 0;
+    t.best = t.bestC = 0;
     t.chains[0] = t.chains[1] = t.chains[2] = t.chains[3] = 0;
     t.dtis = 0;
     if ((e = b.bits(2, v))) return e;
@@ -214,6 +269,7 @@ __device__ inline int read_structure(BitR &b, DDStruct &s) {
     s.numRes = u8(layers);
   }
   process_structure(s);
+  tmpl_best(s);
   return OK;
 }
 
@@ -260,6 +316,8 @@ __device__ inline int dd_parse(const u8 *buf, int len, const DDStruct *cur, DDSt
   const int idx = (templateId + 64 - s->structureId) % 64;
   if (idx >= s->numTmpl) return INVALID;
   const DDTmpl &t = s->t[idx];
+  o.tmplIdx = u8(idx);
+  o.custom = u8((customDtis ? 1 : 0) | (customFdiffs ? 2 : 0) | (customChains ? 4 : 0));
   o.sid = t.sid;
   o.tid = t.tid;
   o.dtis = t.dtis;
@@ -398,11 +456,7 @@ __device__ __forceinline__ u32 fd_at(const DDPkt &p, const u8 *pool, const u16 *
   return spill[p.fdRef + u32(i)];
 }
 
-struct Match {
-  int idx;
-  bool cDtis, cFdiffs, cChains;
-  int extra;
-};
+
 
 // calculateMatch: frame DTIs / FrameDiffs are never nil after a parse (Clone);
 // a template's FrameDiffs is nil iff it has none (reflect.DeepEqual(nil, []) = false)
@@ -452,22 +506,44 @@ __device__ inline int structure_bits(const DDStruct &s) {
 // returns its length in bytes, or -1 (error: the selector drops the frame).
 // (ppool/spill: where p's frame diffs are, see fd_at)
 __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
-                                              u32 active, u8 *out, int cap, const u8 *ppool, const u16 *spill) {
-  // findBestTemplate
-  int first = -1;
-  for (int i = 0; i < s.numTmpl; i++)
-    if (s.t[i].sid == p.sid && s.t[i].tid == p.tid) {
-      first = i;
-      break;
+                                              u32 active, u8 *out, int cap, const u8 *ppool, const u16 *spill,
+                                              bool sameStruct) {
+  // findBestTemplate.  A packet read with this structure, with no custom
+  // field and no structure attached, carries exactly its template's fields:
+  // the search's result was computed with the structure (tmpl_best)
+  Match best;
+  if (LKF_DD_FASTBEST && sameStruct && !(p.flags & DP_ATTACHED) && p.custom == 0 && p.tmplIdx < s.numTmpl) {
+    const DDTmpl &q = s.t[p.tmplIdx];
+    best.idx = q.best;
+    best.cDtis = q.bestC & 1;
+    best.cFdiffs = (q.bestC >> 1) & 1;
+    best.cChains = (q.bestC >> 2) & 1;
+    best.extra = 0;
+    if (best.cFdiffs) {
+      best.extra = 2 * (1 + p.nfd);
+      for (int i = 0; i < p.nfd; i++) {
+        const u32 f = fd_at(p, ppool, spill, i);
+        best.extra += f <= 16 ? 4 : f <= 256 ? 8 : 12;
+      }
     }
-  if (first < 0) return -1;
-  int lastIdx = 0;  // as written: the last index whose layer differs
-  for (int i = first; i < s.numTmpl; i++)
-    if (s.t[i].sid != p.sid || s.t[i].tid != p.tid) lastIdx = i;
-  Match best = dd_match(s, first, p, ppool, spill);
-  for (int i = first + 1; i <= lastIdx; i++) {
-    const Match m = dd_match(s, i, p, ppool, spill);
-    if (m.extra < best.extra) best = m;
+    if (best.cDtis) best.extra += 2 * p.ndti;
+    if (best.cChains) best.extra += 8 * s.numChains;
+  } else {
+    int first = -1;
+    for (int i = 0; i < s.numTmpl; i++)
+      if (s.t[i].sid == p.sid && s.t[i].tid == p.tid) {
+        first = i;
+        break;
+      }
+    if (first < 0) return -1;
+    int lastIdx = 0;  // as written: the last index whose layer differs
+    for (int i = first; i < s.numTmpl; i++)
+      if (s.t[i].sid != p.sid || s.t[i].tid != p.tid) lastIdx = i;
+    best = dd_match(s, first, p, ppool, spill);
+    for (int i = first + 1; i <= lastIdx; i++) {
+      const Match m = dd_match(s, i, p, ppool, spill);
+      if (m.extra < best.extra) best = m;
+    }
   }
   const bool attached = p.flags & DP_ATTACHED;
   const u64 all = (u64(1) << s.numDT) - 1;
@@ -558,8 +634,9 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
   return e ? -1 : nbytes;
 }
 __device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
-                                                   u32 active, u8 *out, const u8 *ppool, const u16 *spill) {
-  return dd_marshal_inl(s, p, frameNumber, hasActive, active, out, kDDMaxBytes, ppool, spill);
+                                                   u32 active, u8 *out, const u8 *ppool, const u16 *spill,
+                                                   bool sameStruct) {
+  return dd_marshal_inl(s, p, frameNumber, hasActive, active, out, kDDMaxBytes, ppool, spill, sameStruct);
 }
 
 // ---- selector ------------------------------------------------------------------
@@ -837,7 +914,7 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
     hasActive = true;
     active = d.mask;
   }
-  const int n = dd_marshal(s, p, fn, hasActive, active, out, ppool, spill);
+  const int n = dd_marshal(s, p, fn, hasActive, active, out, ppool, spill, p.slot == d.slot);
   if (n < 0) {
     c_add(d, efn, SD_DROPPED);
     return r;

@@ -4106,13 +4106,13 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
 // capacity}; LKF_ENODEV from a product build.
 // Not part of include/lkfwd.h: the SVC-run stop counters of a diagnostic
 // build (-DLKF_SVC_STATS=1; forward_kernels.hip g_svc), after a drain.
-int lkf_debug_svc_stats(lkf_engine *e, uint64_t out[32], int reset) {
+int lkf_debug_svc_stats(lkf_engine *e, uint64_t out[48], int reset) {
   if (!e || !out) return LKF_EINVAL;
   int rc = drain_streams(e);
   if (rc) return rc;
-  unsigned long long v[32];
+  unsigned long long v[48];
   const hipError_t r = read_svc_stats(v, reset);
-  for (int i = 0; i < 32; i++) out[i] = v[i];
+  for (int i = 0; i < 48; i++) out[i] = v[i];
   return r == hipSuccess ? LKF_OK : LKF_ENODEV;
 }
 

@@ -2147,7 +2147,7 @@ enum : u32 { SK_BAD = 0, SK_FWD = 1, SK_MDROP = 2, SK_NDROP = 3 };  // lane kind
 // at the start (no keyframe / cache yet), [16 + c] the stopping lane's first
 // failed condition c (the SVC_WHY codes below; 15: the window ended).
 #if LKF_SVC_STATS
-__device__ unsigned long long g_svc[32];
+__device__ unsigned long long g_svc[48];
 #define SVC_WHY(c) \
   if (why == 0 && inWin && !good) why = (c)
 #else
@@ -2405,7 +2405,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       const bool hasActive = (dp.flags & DP_ACTIVE) || hasMask;
       const u32 active = hasMask ? d.mask : dp.activeMask;
       ddLen = dd::dd_marshal_inl(*s, *dpg, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
-                                 kSvcDDBytes, nullptr, nullptr);
+                                 kSvcDDBytes, nullptr, nullptr, u32(dp.slot) == u32(d.slot));
       if (ddLen < 0) good = false;
       mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
     }
@@ -2810,8 +2810,13 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   for (int i = 0; i < LKF_DROP_NREASONS; i++) o.drops[i] = 0;
   __shared__ __attribute__((aligned(16))) DTHot sHot;
   __shared__ __attribute__((aligned(16))) SenderStats sSS;  // the DownTrack's RTPStatsSender (ss_flush)
+  __shared__ u32 sHot0[64];  // the state as loaded: only the dwords the batch changes go back
   Lane L{sHot};
-  reinterpret_cast<u32 *>(&sHot)[lane] = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
+  {
+    const u32 h0 = reinterpret_cast<const u32 *>(A.hot + d)[lane];  // 64 dwords
+    reinterpret_cast<u32 *>(&sHot)[lane] = h0;
+    sHot0[lane] = h0;
+  }
   if (lane < sizeof(SenderStats) / 16)
     reinterpret_cast<uint4 *>(&sSS)[lane] = reinterpret_cast<const uint4 *>(A.ss + d)[lane];
   __shared__ __attribute__((aligned(16))) SsEnt sSsBuf[64];  // one chunk's forwarded tuples (ss_flush)
@@ -2821,6 +2826,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   o.ssRing = A.ssRing + size_t(d) * kSnInfoSize;
   o.ssGap = A.ssGap + size_t(d) * kGapWords;
   __syncthreads();
+#if LKF_SVC_STATS
+  const u64 tPa = __builtin_amdgcn_s_memtime();
+#endif
   RangeEntry *const rmG = A.rm + size_t(d) * kRangeCap;
   L.rm = sRm;
   L.rmG = rmG;
@@ -3361,7 +3369,10 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #endif
   while (ev < evEnd) apply_ctl(L, A.events[ev++]);
   __syncthreads();
-  reinterpret_cast<u32 *>(A.hot + d)[lane] = reinterpret_cast<const u32 *>(&sHot)[lane];
+  {
+    const u32 h1 = reinterpret_cast<const u32 *>(&sHot)[lane];
+    if (h1 != sHot0[lane]) reinterpret_cast<u32 *>(A.hot + d)[lane] = h1;
+  }
   if (o.nFwd && lane < sizeof(SenderStats) / 16)  // (only a forwarded packet changes it)
     reinterpret_cast<uint4 *>(A.ss + d)[lane] = reinterpret_cast<const uint4 *>(&sSS)[lane];
   if (L.rmNew) {  // the ranges appended this batch (the ring's newest): the older ones are unchanged in HBM
@@ -3421,6 +3432,15 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     atomicAdd(&g_svc[7], (unsigned long long)(tP2 - tP1 - tRun - tStep));
     atomicAdd(&g_svc[8], (unsigned long long)(tP3 - tP2));
     atomicAdd(&g_svc[9], 1ull);
+  }
+  if (!DDK && lane == 0) {  // the plain DownTracks (g_svc[32..37]): hot-state load, rest of the
+    const u64 tP3 = __builtin_amdgcn_s_memtime();  // prologue, body, epilogue, DownTracks, packets
+    atomicAdd(&g_svc[32], (unsigned long long)(tPa - tP0));
+    atomicAdd(&g_svc[33], (unsigned long long)(tP1 - tPa));
+    atomicAdd(&g_svc[34], (unsigned long long)(tP2 - tP1));
+    atomicAdd(&g_svc[35], (unsigned long long)(tP3 - tP2));
+    atomicAdd(&g_svc[36], 1ull);
+    atomicAdd(&g_svc[37], (unsigned long long)(pe - pb));
   }
 #endif
   }  // next DownTrack of this wave
@@ -4580,16 +4600,16 @@ hipError_t launch_dd_decode(hipStream_t s, const RunDesc *desc, const uint32_t *
 // ---------------------------------------------------------------------------
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 
-hipError_t read_svc_stats(unsigned long long out[32], int reset) {
+hipError_t read_svc_stats(unsigned long long out[48], int reset) {
 #if LKF_SVC_STATS
-  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_svc), sizeof(unsigned long long) * 32);
+  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_svc), sizeof(unsigned long long) * 48);
   if (r == hipSuccess && reset) {
-    unsigned long long z[32] = {};
+    unsigned long long z[48] = {};
     r = hipMemcpyToSymbol(HIP_SYMBOL(g_svc), z, sizeof(z));
   }
   return r;
 #else
-  for (int i = 0; i < 32; i++) out[i] = 0;
+  for (int i = 0; i < 48; i++) out[i] = 0;
   (void)reset;
   return hipErrorNotSupported;
 #endif

@@ -201,7 +201,10 @@ struct DDTmpl {  // dependencydescriptor.FrameDependencyTemplate of a structure 
   uint8_t sid, tid;
   uint16_t nfd;        // frame diffs (1..16 each), at fdPool[fdOff ..) of the structure
   uint16_t fdOff;
-  uint16_t pad;
+  // marshalling a packet of this template without custom fields: the template
+  // findBestTemplate picks (best) and the fields it must write custom (bestC:
+  // 1 DTIs, 2 frame diffs, 4 chain diffs); set when the structure is read
+  uint8_t best, bestC;
   uint64_t dtis;       // 2-bit DecodeTargetIndication per decode target
   uint32_t chains[4];  // 4-bit frame_chain_fdiff per chain (chain c: word c / 8, nibble c % 8)
 };
@@ -242,7 +245,9 @@ struct alignas(16) DDPkt {  // one packet's parsed descriptor (k_dd_decode -> k_
   uint8_t fdKind;        // FD_*
   uint32_t fdRef;
   uint16_t fd[kDDFdInline];
-  uint8_t pad[4];
+  uint8_t tmplIdx;       // the template the descriptor names (structure slot's index)
+  uint8_t custom;        // custom fields present: 1 DTIs, 2 frame diffs, 4 chain diffs
+  uint8_t pad[2];
   uint64_t chainDiffs[kDDChains / 8];  // FrameDependencies.ChainDiffs (8 bits each: chain c in word c / 8)
 };
 constexpr uint32_t kDDPktScalar = 48;  // the bytes of DDPkt before fd[2] (the selector's fast path copies these)

@@ -1260,8 +1260,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
   }
   u64 *const hg = hist + size_t(sid) * kHistWords;
   u32 *const gap = rxGap + size_t(sid) * kGapWords;
-  sHist[lane] = hg[lane];
-  reinterpret_cast<u32 *>(&sh)[lane] = reinterpret_cast<const u32 *>(hot + sid)[lane];
+  // (the loaded words are kept: only the ones the batch changes go back)
+  const u64 hist0 = hg[lane];
+  const u32 hot0 = reinterpret_cast<const u32 *>(hot + sid)[lane];
+  sHist[lane] = hist0;
+  reinterpret_cast<u32 *>(&sh)[lane] = hot0;
   // the stream's RTX bucket (bka.state nullptr: no buckets)
   const bool bkOn = bka.state != nullptr;
   BktCtx bk = {};
@@ -1526,8 +1529,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
     pos = end;
     }
   }
-  hg[lane] = sHist[lane];
-  reinterpret_cast<u32 *>(hot + sid)[lane] = reinterpret_cast<const u32 *>(&sh)[lane];
+  if (sHist[lane] != hist0) hg[lane] = sHist[lane];
+  const u32 hot1 = reinterpret_cast<const u32 *>(&sh)[lane];
+  if (hot1 != hot0) reinterpret_cast<u32 *>(hot + sid)[lane] = hot1;
   if (bkOn && lane < 4) reinterpret_cast<u32 *>(bka.state + sid)[lane] = reinterpret_cast<const u32 *>(&sB)[lane];
   if (DDK) {
     __syncthreads();
@@ -1576,13 +1580,15 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;  // no datagram of its track: no calc, no doNACKs
   NackState *const g = states + sid;
-  for (u32 i = lane; i < u32(kNackSlots); i += 64) {
+  // only the live entries are staged (every read below is of an index < count)
+  u32 count = g->count;
+  const u32 rtt = g->rtt;
+  for (u32 i = lane; i < count; i += 64) {
     sLast[i] = g->last[i];
     sSn[i] = g->sn[i];
     sTries[i] = g->tries[i];
   }
-  u32 count = g->count;
-  const u32 rtt = g->rtt;
+  bool dirty = false;  // wave-uniform: an entry moved, was pushed or was nacked
   __syncthreads();
   // getNack's required interval per tries value (tries < MaxTries):
   // tries 0: MinInterval; else min(MaxInterval, floor(rtt * 1.25^(tries-1)) ms),
@@ -1622,6 +1628,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
     }
     __syncthreads();
     count--;
+    dirty = true;
   };
   auto removeSn = [&](u32 sn16) {  // the first entry with that SN
     const u64 m0 = __ballot(lane < count && sSn[lane] == sn16);
@@ -1766,6 +1773,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
           }
           __syncthreads();
           count = newCount;
+          dirty = true;
           nextDue = now + req0 < nextDue ? now + req0 : nextDue;  // the new entries (tries 0, lastNackedAt now)
         }
       }
@@ -1806,6 +1814,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
         }
       __syncthreads();
       const u32 numNacked = u32(__popcll(s0m) + __popcll(s1m));
+      dirty = true;
       if (numNacked && (stageN + u32(kNackCap) > kPairStage || recN == kRecStage)) flush();
       lkf_nack_pair *const sPairs = sStage + stageN;
       u32 np = 0;
@@ -1849,15 +1858,15 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
     }
   }
   flush();
-  for (u32 i = lane; i < u32(kNackSlots); i += 64) {
-    g->last[i] = sLast[i];
-    g->sn[i] = u16(sSn[i]);
-    g->tries[i] = u8(sTries[i]);
+  if (dirty) {  // (entries past count are never read: only the live ones go back)
+    for (u32 i = lane; i < count; i += 64) {
+      g->last[i] = sLast[i];
+      g->sn[i] = u16(sSn[i]);
+      g->tries[i] = u8(sTries[i]);
+    }
+    if (lane == 0) g->count = count;
   }
-  if (lane == 0) {
-    g->count = count;
-    if (nacked) g->nacks += nacked;
-  }
+  if (lane == 0 && nacked) g->nacks += nacked;
 }
 
 // lkf_ingest_nacks: records at their compacted positions, pairs gathered in

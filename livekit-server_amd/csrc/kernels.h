@@ -88,7 +88,7 @@ hipError_t launch_twcc_stamp(hipStream_t s, const DevDT *dts, uint32_t *ctrD, ui
                              const uint64_t *off, const uint32_t *len, uint8_t *arena);
 // -DLKF_CHECKED=1 builds: {violations, first site, its index, its capacity}
 hipError_t read_check(unsigned long long out[4], int reset);
-hipError_t read_svc_stats(unsigned long long out[32], int reset);  // LKF_SVC_STATS builds
+hipError_t read_svc_stats(unsigned long long out[48], int reset);  // LKF_SVC_STATS builds
 
 hipError_t launch_batch_init(hipStream_t s, uint32_t ntracks, uint32_t ndts, uint32_t nstats, uint32_t *tBegin,
                              uint32_t *tEnd, uint32_t *tRuns, uint32_t *err, uint64_t *stats, uint32_t *fwdCnt,

@@ -20,13 +20,17 @@ WHY = {1: "start/seq", 2: "vp9 switch", 3: "frame order", 4: "ndti", 5: "frame h
 def main():
     rooms = int(sys.argv[1]) if len(sys.argv) > 1 else 500
     svc_dd = int(sys.argv[2]) if len(sys.argv) > 2 else -1
-    tr = workload.Trace(5, duration_s=3.0, batch_s=1.0, rooms=rooms, svc_dd=svc_dd)
+    cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 5  # (2 with batch 0.01: the 10-ms tick)
+    batch_s = float(sys.argv[4]) if len(sys.argv) > 4 else 1.0
+    dur = float(sys.argv[5]) if len(sys.argv) > 5 else 3.0
+    kw = dict(svc_dd=svc_dd) if cfg == 5 else {}
+    tr = workload.Trace(cfg, duration_s=dur, batch_s=batch_s, rooms=rooms, **kw)
     eng = pkg.Engine.for_trace(tr)
     workload.load_topology(eng.api, eng.h, tr)
     fn = eng.lib.lkf_debug_svc_stats
     fn.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     fn.restype = C.c_int
-    out = (C.c_uint64 * 32)()
+    out = (C.c_uint64 * 48)()
     fn(eng.h, out, 1)
     for b in range(tr.nbatches):
         workload.queue_events(eng.api, eng.h, tr, b)
@@ -47,6 +51,10 @@ def main():
                   tuple([v[k] / v[9] / 1000.0 for k in (4, 5, 6, 7, 8)] + [v[9]]), flush=True)
             print("   in DD runs (kcycles per DT): decision %.1f marshal %.1f munger/seq decision %.1f" %
                   tuple(v[k] / v[9] / 1000.0 for k in (10, 11, 12)), flush=True)
+        if v[36]:  # the plain DownTracks (k_decide_dt<false>)
+            print("   plain DTs (kcycles per DT): hot load %.2f rest of prologue %.2f body %.2f epilogue %.2f "
+                  "(n=%d, %.2f pkts/DT)" % tuple([v[k] / v[36] / 1000.0 for k in (32, 33, 34, 35)] +
+                                                 [v[36], v[37] / v[36]]), flush=True)
     tr.close()
 
 
