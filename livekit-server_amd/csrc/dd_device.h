@@ -633,6 +633,44 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
   w.finish();
   return e ? -1 : nbytes;
 }
+// dd_marshal_inl for a packet read with s, with no custom field and no
+// structure attached: its fields are template k's, so the descriptor is
+// written from the structure alone (svc_run: no read of the packet's lists)
+__device__ __forceinline__ int dd_marshal_tmpl(const DDStruct &s, int k, u8 pflags, u16 frameNumber, bool hasActive,
+                                               u32 active, u8 *out, int cap) {
+  const DDTmpl &q = s.t[k];
+  const bool cDtis = q.bestC & 1, cFdiffs = q.bestC & 2, cChains = q.bestC & 4;
+  int extra = 0;
+  if (cFdiffs) extra = 2 * (1 + q.nfd) + 4 * q.nfd;  // (template frame diffs are 1-16)
+  if (cDtis) extra += 2 * s.numDT;
+  if (cChains) extra += 8 * s.numChains;
+  const bool extended = extra > 0 || hasActive;
+  int vbits = 1 + 1 + 6 + 16 + extra;
+  if (extended) vbits += 5 + (hasActive ? s.numDT : 0);
+  const int nbytes = (vbits + 7) / 8;
+  if (nbytes > kDDMaxBytes || nbytes > cap) return -1;
+  BitW w(out, nbytes);
+  int e = 0;
+  e |= w.write(pflags & DP_FIRST ? 1 : 0, 1);
+  e |= w.write(pflags & DP_LAST ? 1 : 0, 1);
+  e |= w.write(u64((q.best + s.structureId) % 64), 6);
+  e |= w.write(frameNumber, 16);
+  if (extended) {
+    e |= w.write((u64(hasActive) << 3) | (u64(cDtis) << 2) | (u64(cFdiffs) << 1) | u64(cChains), 5);
+    if (hasActive) e |= w.write(active, s.numDT);
+    if (cDtis)
+      for (int i = 0; i < s.numDT; i++) e |= w.write(dti_at(q.dtis, i), 2);
+    if (cFdiffs) {
+      for (int i = 0; i < q.nfd; i++) e |= w.write((u64(1) << 4) | u64(s.fdPool[q.fdOff + i] - 1), 6);
+      e |= w.write(0, 2);
+    }
+    if (cChains)
+      for (int c = 0; c < s.numChains; c++) e |= w.write(dd_tmpl_chain(q, c), 8);
+  }
+  w.finish();
+  return e ? -1 : nbytes;
+}
+
 __device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
                                                    u32 active, u8 *out, const u8 *ppool, const u16 *spill,
                                                    bool sameStruct) {

@@ -2147,7 +2147,8 @@ enum : u32 { SK_BAD = 0, SK_FWD = 1, SK_MDROP = 2, SK_NDROP = 3 };  // lane kind
 // at the start (no keyframe / cache yet), [16 + c] the stopping lane's first
 // failed condition c (the SVC_WHY codes below; 15: the window ended).
 #if LKF_SVC_STATS
-__device__ unsigned long long g_svc[48];
+__device__ unsigned long long g_svc[64 * 48];  // 64 copies (by workgroup) of 48 counters
+#define SVC_ADD(k, v) atomicAdd(&g_svc[(blockIdx.x & 63) * 48 + (k)], (unsigned long long)(v))
 #define SVC_WHY(c) \
   if (why == 0 && inWin && !good) why = (c)
 #else
@@ -2211,7 +2212,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     swAll = hiPos >= 0 && (i32(s->dtS[hiPos]) != L.h.curS || i32(s->dtT[hiPos]) != L.h.curT);
   }
 #if LKF_SVC_STATS
-  if (!uni && lane == 0) atomicAdd(&g_svc[3], 1ull);
+  if (!uni && lane == 0) SVC_ADD(3, 1ull);
   u32 why = 0;
 #endif
   if (!uni) return pos;
@@ -2282,6 +2283,12 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       for (int k = 0; k < int(kDDPktScalar / 16); k++) dst[k] = hasDD ? src[k] : make_uint4(0, 0, 0, 0);
     }
     const bool ddLane = hasDD && (dp.flags & DP_VALID);  // (no descriptor: not selected, no DD state change)
+    // a descriptor read with the structure in force and without custom fields
+    // carries its template's lists: they are read from the structure in LDS
+    const bool tmplSrc = LKF_DD_FASTBEST && u32(dp.slot) == u32(d.slot) && dp.custom == 0 &&
+                         !(dp.flags & DP_ATTACHED) && dp.tmplIdx < s->numTmpl;
+    const DDTmpl &tq = s->t[tmplSrc ? dp.tmplIdx : 0];
+    auto chainDiff = [&](int c) -> u32 { return tmplSrc ? dd_tmpl_chain(tq, c) : dd_chain_diff(*dpg, c); };
     const u64 cl0 = d.cLast;
     const u64 efn = dp.extFN;
     const u64 ddM = __ballot(ddLane);
@@ -2368,7 +2375,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     // full step.
     if (eval && good)  // restarts
       for (int c = 0; c < int(d.numChains); c++) {
-        if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c || dd_chain_diff(*dpg, c) != 0) continue;
+        if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c || chainDiff(c) != 0) continue;
         if (((aboveM >> c) & 1) || d.expCount[c] != 0 || (!LKF_SVC_CHAINS && ((d.chBroken >> c) & 1)))
           good = false;
         else if (LKF_SVC_CHAINS)
@@ -2380,7 +2387,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     if (eval && good)  // breaks
       for (int c = 0; c < int(d.numChains); c++) {
         if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c) continue;
-        const u32 diff = dd_chain_diff(*dpg, c);
+        const u32 diff = chainDiff(c);
         if (diff == 0 || (((d.chBroken & ~rstSeen) >> c) & 1)) continue;  // (a restart; a chain broken before this lane)
         const u32 sd = dec(efn - diff);
         if (sd == dd::SD_FORWARDED) continue;
@@ -2390,10 +2397,12 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
           chBrk |= 1u << c;
       }
     SVC_WHY(8);
-    if (ddFwdSel) good = good && dp.fdKind == FD_INLINE;  // (a pooled or spilled list: full step)
+    if (ddFwdSel) good = good && (tmplSrc || dp.fdKind == FD_INLINE);  // (a custom pooled or spilled list: full step)
     if (ddFwdSel && good)  // a referenced frame that was dropped drops this one (:192-201): full step
-      for (int j = 0; j < int(dp.nfd) && j < kDDFdInline; j++)
-        if (dpg->fd[j] != 0 && dec(efn - dpg->fd[j]) == dd::SD_DROPPED) good = false;
+      for (int j = 0; j < int(dp.nfd) && (tmplSrc || j < kDDFdInline); j++) {
+        const u32 f = tmplSrc ? u32(s->fdPool[tq.fdOff + j]) : u32(dpg->fd[j]);
+        if (f != 0 && dec(efn - f) == dd::SD_DROPPED) good = false;
+      }
     SVC_WHY(9);
 #if LKF_SVC_STATS
     tB = __builtin_amdgcn_s_memtime();
@@ -2404,8 +2413,10 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
       const bool hasMask = d.flags & DS_HAS_MASK;
       const bool hasActive = (dp.flags & DP_ACTIVE) || hasMask;
       const u32 active = hasMask ? d.mask : dp.activeMask;
-      ddLen = dd::dd_marshal_inl(*s, *dpg, u16(efn + d.fnOffset), hasActive, active, sScr + lane * kSvcDDBytes,
-                                 kSvcDDBytes, nullptr, nullptr, u32(dp.slot) == u32(d.slot));
+      ddLen = tmplSrc ? dd::dd_marshal_tmpl(*s, dp.tmplIdx, dp.flags, u16(efn + d.fnOffset), hasActive, active,
+                                            sScr + lane * kSvcDDBytes, kSvcDDBytes)
+                      : dd::dd_marshal_inl(*s, *dpg, u16(efn + d.fnOffset), hasActive, active,
+                                           sScr + lane * kSvcDDBytes, kSvcDDBytes, nullptr, nullptr, false);
       if (ddLen < 0) good = false;
       mk = (p.hdr1 & 0x80) || ((dp.flags & DP_LAST) && L.h.curS == i32(dp.sid));
     }
@@ -2453,18 +2464,18 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   {
     const u32 wx = x < 64 ? rl32(why, x) : 0u;
     if (lane == 0) {
-      atomicAdd(&g_svc[0], 1ull);
-      atomicAdd(&g_svc[1], (unsigned long long)(x > pos ? x - pos : 0));
-      if (x < n) atomicAdd(&g_svc[16 + (wx ? wx : 15)], 1ull);
+      SVC_ADD(0, 1ull);
+      SVC_ADD(1, (unsigned long long)(x > pos ? x - pos : 0));
+      if (x < n) SVC_ADD(16 + (wx ? wx : 15), 1ull);
     }
   }
 #endif
 #if LKF_SVC_STATS
   const u64 tD = __builtin_amdgcn_s_memtime();
   if (lane == 0 && dd) {
-    atomicAdd(&g_svc[10], (unsigned long long)(tB - tA));
-    atomicAdd(&g_svc[11], (unsigned long long)(tC - tB));
-    atomicAdd(&g_svc[12], (unsigned long long)(tD - tC));
+    SVC_ADD(10, (unsigned long long)(tB - tA));
+    SVC_ADD(11, (unsigned long long)(tC - tB));
+    SVC_ADD(12, (unsigned long long)(tD - tC));
   }
 #endif
   if (x <= pos) return pos;
@@ -3008,7 +3019,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           tStep += __builtin_amdgcn_s_memtime() - tr1;
 #endif
 #if LKF_SVC_STATS
-          if (lane == 0) atomicAdd(&g_svc[2], 1ull);
+          if (lane == 0) SVC_ADD(2, 1ull);
 #endif
           pos = x + 1;
         }
@@ -3426,21 +3437,21 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
 #if LKF_SVC_STATS
   if (DDK && lane == 0 && (L.h.flags & (F_DD | F_VP9))) {
     const u64 tP3 = __builtin_amdgcn_s_memtime();
-    atomicAdd(&g_svc[4], (unsigned long long)(tP1 - tP0));
-    atomicAdd(&g_svc[5], (unsigned long long)tRun);
-    atomicAdd(&g_svc[6], (unsigned long long)tStep);
-    atomicAdd(&g_svc[7], (unsigned long long)(tP2 - tP1 - tRun - tStep));
-    atomicAdd(&g_svc[8], (unsigned long long)(tP3 - tP2));
-    atomicAdd(&g_svc[9], 1ull);
+    SVC_ADD(4, (unsigned long long)(tP1 - tP0));
+    SVC_ADD(5, (unsigned long long)tRun);
+    SVC_ADD(6, (unsigned long long)tStep);
+    SVC_ADD(7, (unsigned long long)(tP2 - tP1 - tRun - tStep));
+    SVC_ADD(8, (unsigned long long)(tP3 - tP2));
+    SVC_ADD(9, 1ull);
   }
   if (!DDK && lane == 0) {  // the plain DownTracks (g_svc[32..37]): hot-state load, rest of the
     const u64 tP3 = __builtin_amdgcn_s_memtime();  // prologue, body, epilogue, DownTracks, packets
-    atomicAdd(&g_svc[32], (unsigned long long)(tPa - tP0));
-    atomicAdd(&g_svc[33], (unsigned long long)(tP1 - tPa));
-    atomicAdd(&g_svc[34], (unsigned long long)(tP2 - tP1));
-    atomicAdd(&g_svc[35], (unsigned long long)(tP3 - tP2));
-    atomicAdd(&g_svc[36], 1ull);
-    atomicAdd(&g_svc[37], (unsigned long long)(pe - pb));
+    SVC_ADD(32, (unsigned long long)(tPa - tP0));
+    SVC_ADD(33, (unsigned long long)(tP1 - tPa));
+    SVC_ADD(34, (unsigned long long)(tP2 - tP1));
+    SVC_ADD(35, (unsigned long long)(tP3 - tP2));
+    SVC_ADD(36, 1ull);
+    SVC_ADD(37, (unsigned long long)(pe - pb));
   }
 #endif
   }  // next DownTrack of this wave
@@ -4602,10 +4613,15 @@ static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
 
 hipError_t read_svc_stats(unsigned long long out[48], int reset) {
 #if LKF_SVC_STATS
-  hipError_t r = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_svc), sizeof(unsigned long long) * 48);
+  static unsigned long long v[64 * 48];
+  hipError_t r = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_svc), sizeof(v));
+  for (int k = 0; k < 48; k++) {
+    out[k] = 0;
+    for (int c = 0; c < 64; c++) out[k] += v[c * 48 + k];
+  }
   if (r == hipSuccess && reset) {
-    unsigned long long z[48] = {};
-    r = hipMemcpyToSymbol(HIP_SYMBOL(g_svc), z, sizeof(z));
+    for (auto &x : v) x = 0;
+    r = hipMemcpyToSymbol(HIP_SYMBOL(g_svc), v, sizeof(v));
   }
   return r;
 #else

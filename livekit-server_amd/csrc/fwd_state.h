@@ -243,14 +243,15 @@ struct alignas(16) DDPkt {  // one packet's parsed descriptor (k_dd_decode -> k_
   uint8_t extFlags;      // LKF_DD_*
   uint8_t slot;          // structure ring slot the descriptor was read with (attached: written to)
   uint8_t fdKind;        // FD_*
-  uint32_t fdRef;
-  uint16_t fd[kDDFdInline];
   uint8_t tmplIdx;       // the template the descriptor names (structure slot's index)
   uint8_t custom;        // custom fields present: 1 DTIs, 2 frame diffs, 4 chain diffs
   uint8_t pad[2];
+  uint32_t fdRef;
+  uint16_t fd[kDDFdInline];
   uint64_t chainDiffs[kDDChains / 8];  // FrameDependencies.ChainDiffs (8 bits each: chain c in word c / 8)
 };
-constexpr uint32_t kDDPktScalar = 48;  // the bytes of DDPkt before fd[2] (the selector's fast path copies these)
+constexpr uint32_t kDDPktScalar = 48;  // the bytes of DDPkt before fd[] (the selector's fast path copies these)
+static_assert(__builtin_offsetof(DDPkt, fd) == kDDPktScalar, "the scalar part ends where fd[] starts");
 static_assert(sizeof(DDPkt) == 96, "DDPkt must be 96 B");
 __host__ __device__ inline uint32_t dd_chain_diff(const DDPkt &p, int c) {
   return uint32_t(p.chainDiffs[c >> 3] >> (8 * (c & 7))) & 0xffu;
