@@ -893,7 +893,13 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
     c_add(d, efn, SD_DROPPED);
     return r;
   }
+#if defined(LKF_SVC_STATS) && LKF_SVC_STATS
+  const u64 tq0 = __builtin_amdgcn_s_memtime();
+#endif
   for (int c = 0; c < d.numChains; c++) chain_on_frame(d, c, efn, p, r.limit);
+#if defined(LKF_SVC_STATS) && LKF_SVC_STATS
+  const u64 tq1 = __builtin_amdgcn_s_memtime();
+#endif
   int hiPos = -1;
   u32 dti = 0;
   for (int i = 0; i < d.numTargets; i++) {
@@ -952,7 +958,18 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
     hasActive = true;
     active = d.mask;
   }
+#if defined(LKF_SVC_STATS) && LKF_SVC_STATS
+  const u64 tq2 = __builtin_amdgcn_s_memtime();
+#endif
   const int n = dd_marshal(s, p, fn, hasActive, active, out, ppool, spill, p.slot == d.slot);
+#if defined(LKF_SVC_STATS) && LKF_SVC_STATS
+  if ((threadIdx.x & 63) == 0) {  // g_svc[40..43]: chains, selection, marshal cycles, marshals
+    SVC_ADD(40, tq1 - tq0);
+    SVC_ADD(41, tq2 - tq1);
+    SVC_ADD(42, __builtin_amdgcn_s_memtime() - tq2);
+    SVC_ADD(43, 1ull);
+  }
+#endif
   if (n < 0) {
     c_add(d, efn, SD_DROPPED);
     return r;

@@ -23,6 +23,13 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/lkfwd.h"
+#ifndef LKF_SVC_STATS
+#define LKF_SVC_STATS 0
+#endif
+#if LKF_SVC_STATS  // (diagnostic builds: the counters, below at svc_run)
+__device__ unsigned long long g_svc[64 * 48];  // 64 copies (by workgroup) of 48 counters
+#define SVC_ADD(k, v) atomicAdd(&g_svc[(blockIdx.x & 63) * 48 + (k)], (unsigned long long)(v))
+#endif
 #include "dd_device.h"
 #include "fwd_state.h"
 #include "kernels.h"
@@ -228,6 +235,7 @@ struct Lane {
   const DDPkt *ddPkts;
   const u16 *ddSpill;
   u8 *ddBuf;
+  DDPkt *ddPktL;  // LDS: the full step's descriptor (dd_select reads it there, not from HBM)
   u32 *err;
 };
 
@@ -1031,10 +1039,28 @@ __device__ int fw_translate(Lane &L, const PktV &p, u32 k, Fwd &o) {
     }
   }
   if (DDK && hasf(L, F_DD)) {  // DependencyDescriptor.Select videolayerselector/dependencydescriptor.go:65-355
-    const bool hasDD = (p.flags & LKF_PKT_DD) && L.ddPkts && (L.ddPkts[k].flags & DP_VALID);
-    // (the descriptor is read where k_dd_decode left it: no private copy)
-    const dd::SelResult r = dd::dd_select(*L.dd, L.ddRing, hasDD ? L.ddPkts + k : nullptr, pktMarker, L.h.curS, L.h.curT, L.h.prevS,
+    // (the descriptor is staged in LDS: dd_select's state writes and its
+    // reads of the descriptor go through generic pointers, so every read
+    // after a write is a reload — from LDS, not from HBM)
+    const bool inDD = (p.flags & LKF_PKT_DD) && L.ddPkts;
+    if (inDD) {
+      const u32 ln = lane_id();
+      if (ln < sizeof(DDPkt) / 16)
+        reinterpret_cast<uint4 *>(L.ddPktL)[ln] = reinterpret_cast<const uint4 *>(L.ddPkts + k)[ln];
+      wave_lds_sync();
+    }
+    const bool hasDD = inDD && (L.ddPktL->flags & DP_VALID);
+#if LKF_SVC_STATS
+    const u64 tS0 = __builtin_amdgcn_s_memtime();
+#endif
+    const dd::SelResult r = dd::dd_select(*L.dd, L.ddRing, hasDD ? L.ddPktL : nullptr, pktMarker, L.h.curS, L.h.curT, L.h.prevS,
                                           L.h.prevT, L.h.tgtS, L.h.tgtT, L.ddBuf, L.ddS, L.ddSSlot, L.ddSpill);
+#if LKF_SVC_STATS
+    if (lane_id() == 0) {  // g_svc[13..14]: dd_select cycles, calls
+      SVC_ADD(13, __builtin_amdgcn_s_memtime() - tS0);
+      SVC_ADD(14, 1ull);
+    }
+#endif
     if (r.limit && lane_id() == 0) atomicOr(L.err, 16u);
     if (!r.selected) {
       if (r.relevant && hasf(L, F_STARTED)) {  // forwarder.go:1694-1702 (RTPMarker false)
@@ -1735,8 +1761,21 @@ __device__ __forceinline__ void ss_put(SsEnt *e, u64 sn, u64 ts, i64 t, u32 hdr,
 // new frames on uniform values.  The entry that ends a segment (out of order,
 // duplicate, a larger gap, the first packet) takes the scalar Update,
 // wave-uniform.
+#ifndef LKF_SS_SCALAR  // chunks of at most this many forwarded tuples fold entry by entry
+#define LKF_SS_SCALAR 3
+#endif
 __device__ __forceinline__ void ss_flush(SenderStats &S, u32 *ring, u32 *gap, const SsEnt *buf, u32 m, u64 bSN,
                                       u64 bTS) {
+  if (m <= u32(LKF_SS_SCALAR)) {  // a short chunk (the short ticks): the scalar Update per entry,
+    for (u32 i = 0; i < m; i++) {  // cheaper than the segment's cross-lane reductions
+      const SsEnt &e = buf[i];
+      ss::ss_update(S, ring, gap, e.t, widen32(bSN, e.sn), widen32(bTS, e.ts), (e.fl & 1) != 0, e.hp & 0xffffu,
+                    e.hp >> 16, 0);
+      if (e.fl & 2) S.keyFrames++;  // UpdateKeyFrame(1) rtpstats_base.go:429-439
+      wave_lds_sync();
+    }
+    return;
+  }
   const u32 lane = lane_id();
   const u64 lt = (1ull << lane) - 1;
   const bool valid = lane < m;
@@ -2147,8 +2186,6 @@ enum : u32 { SK_BAD = 0, SK_FWD = 1, SK_MDROP = 2, SK_NDROP = 3 };  // lane kind
 // at the start (no keyframe / cache yet), [16 + c] the stopping lane's first
 // failed condition c (the SVC_WHY codes below; 15: the window ended).
 #if LKF_SVC_STATS
-__device__ unsigned long long g_svc[64 * 48];  // 64 copies (by workgroup) of 48 counters
-#define SVC_ADD(k, v) atomicAdd(&g_svc[(blockIdx.x & 63) * 48 + (k)], (unsigned long long)(v))
 #define SVC_WHY(c) \
   if (why == 0 && inWin && !good) why = (c)
 #else
@@ -2734,6 +2771,9 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
 #undef SVC_WHY
 
 template <bool DDK>
+#ifndef LKF_DEC_PREFETCH  // a single-chunk track's packets loaded with the DownTrack's state
+#define LKF_DEC_PREFETCH 0  // (measured: the headline 1.3 % slower with it, the tick flat; r5 A/B)
+#endif
 __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
   __shared__ i32 sDrop[kSetCap];
   __shared__ i32 sEx[kSetCap];
@@ -2762,7 +2802,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   {
     const u32 K = A.perWave, lane = threadIdx.x;
     const u32 wj = A.waveBase + ((blockIdx.x >> 3) * K + lane) * 8 + (blockIdx.x & 7);
-    u32 dj = 0xffffffffu, tj = 0, ej = 0, eej = 0, pbj = 0, pej = 0;
+    u32 dj = 0xffffffffu, tj = 0, ej = 0, eej = 0, pbj = 0, pej = 0, cj = 0;
     if (lane < K && wj < A.waveEnd) {
       dj = A.sched[wj];
       tj = A.waveTrack[wj];
@@ -2772,11 +2812,12 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     if (dj != 0xffffffffu) {  // (0xffffffff: padding slot of the per-XCD schedule)
       pbj = A.tBegin[tj];
       pej = A.tEnd[tj];
+      cj = A.tracks[tj].codec;  // (the VP8 maps are then loaded with the hot state)
     }
     todo = __ballot(dj != 0xffffffffu && (pbj < pej || ej < eej));
     if (lane < K) {
       sSlot[2 * lane] = make_uint4(wj, dj, tj, ej);
-      sSlot[2 * lane + 1] = make_uint4(eej, pbj, pej, 0);
+      sSlot[2 * lane + 1] = make_uint4(eej, pbj, pej, cj);
     }
     wave_lds_sync();
   }
@@ -2787,7 +2828,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   // per-phase cycles of the SVC DownTracks (g_svc[4..9]: prologue, runs,
   // full steps after runs, chunk tails, epilogue, DownTracks)
   const u64 tP0 = __builtin_amdgcn_s_memtime();
-  u64 tRun = 0, tStep = 0;
+  u64 tRun = 0, tStep = 0, tLoad = 0, tSs = 0;
 #endif
   // The lane index again, opaque to the compiler, so lane-derived values are
   // recomputed per DownTrack rather than hoisted out of the loop and held in
@@ -2812,6 +2853,18 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const u32 pb = __builtin_amdgcn_readfirstlane(sb.y);
   u32 pe = __builtin_amdgcn_readfirstlane(sb.z);
   const u64 slot0 = A.slotBase[d];
+  // A track with at most 64 packets in the batch is one chunk: its packets
+  // are loaded together with the DownTrack's state (one round trip fewer)
+  bool pre = LKF_DEC_PREFETCH && pe - pb <= 64u;  // (cleared once the chunk takes them)
+  uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
+  if (pre && lane < pe - pb) {
+    CHK(pb + lane < A.npkts, CK_DEC_PKT, pb + lane, A.npkts);
+    const uint4 *ps = reinterpret_cast<const uint4 *>(pkts) + u64(pb + lane) * 4;
+    r0 = ps[0];
+    r1 = ps[1];
+    r2 = ps[2];
+    r3 = ps[3];
+  }
   LaneOut o;
   o.nFwd = o.nBytes = o.nTuples = 0;
   o.sentDiff = 0;
@@ -2830,6 +2883,13 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   }
   if (lane < sizeof(SenderStats) / 16)
     reinterpret_cast<uint4 *>(&sSS)[lane] = reinterpret_cast<const uint4 *>(A.ss + d)[lane];
+  // VP8 munger maps live in LDS for the batch: the picture-id sets here, the
+  // live entries of the missing-picture ring once the hot state is in
+  const bool vp8Track = __builtin_amdgcn_readfirstlane(sb.w) == LKF_CODEC_VP8;
+  if (vp8Track && lane < u32(kSetCap)) {
+    sDrop[lane] = A.vc[d].dropKey[lane];
+    sEx[lane] = A.vc[d].exKey[lane];
+  }
   __shared__ __attribute__((aligned(16))) SsEnt sSsBuf[64];  // one chunk's forwarded tuples (ss_flush)
   o.ss = &sSS;
   o.ssBuf = sSsBuf;
@@ -2851,12 +2911,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.exKey = sEx;
   L.missKey = sMissKey;
   L.missVal = sMissVal;
-  const bool vp8Track = A.tracks[track].codec == LKF_CODEC_VP8;
-  if (vp8Track) {  // VP8 munger maps live in LDS for the batch
-    if (lane < u32(kSetCap)) {
-      sDrop[lane] = L.vc->dropKey[lane];
-      sEx[lane] = L.vc->exKey[lane];
-    }
+  if (vp8Track) {
     for (u32 i = lane; i < L.h.missCount; i += 64) {  // the live entries of the missing-picture ring
       const u32 idx = (L.h.missHead + i) % kMissCap;
       sMissKey[idx] = L.vc->missKey[idx];
@@ -2884,6 +2939,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.extTcc = dt.extTcc;
   L.err = A.err;
   L.ddPkts = A.ddPkts;
+  __shared__ __attribute__((aligned(16))) DDPkt sDDPkt;
+  L.ddPktL = &sDDPkt;
   L.ddSpill = A.ddSpill;
   L.ddRing = nullptr;
   L.ddS = reinterpret_cast<const DDStruct *>(sDDSRaw);
@@ -2943,6 +3000,9 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   const u64 tP1 = __builtin_amdgcn_s_memtime();
 #endif
   while (kpos < pe) {
+#if LKF_SVC_STATS
+    const u64 tc0 = __builtin_amdgcn_s_memtime();
+#endif
     if (nextAt <= kpos) {
       while (nextAt <= kpos) {
         apply_ctl(L, A.events[ev++]);
@@ -2975,16 +3035,27 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
       lim = kpos + n;
     }
     const bool valid = lane < n;
-    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
-    if (valid) {
-      CHK(pi < A.npkts, CK_DEC_PKT, pi, A.npkts);
-      const u64 q = u64(pi) * 4;
-      r0 = src[q];
-      r1 = src[q + 1];
-      r2 = src[q + 2];
-      r3 = src[q + 3];
+    if (!pre) {  // (pre: the prefetched chunk, pi = pb + lane)
+      r0 = r1 = r2 = r3 = make_uint4(0, 0, 0, 0);
+      if (valid) {
+        CHK(pi < A.npkts, CK_DEC_PKT, pi, A.npkts);
+        const u64 q = u64(pi) * 4;
+        r0 = src[q];
+        r1 = src[q + 1];
+        r2 = src[q + 2];
+        r3 = src[q + 3];
+      }
     }
+    pre = false;
     pin_loaded(r0, r1, r2, r3);
+#if LKF_SVC_STATS
+    {
+      u64 tl0;  // (the loads' wait: the chunk's first use of the registers)
+      const u32 dep = __builtin_amdgcn_readfirstlane(r0.x ^ r3.w);  // (waits for the loads)
+      asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(tl0) : "s"(dep));
+      tLoad += tl0 - tc0;
+    }
+#endif
     const PktV p = decode_pkt(r0, r1, r2, r3);
     u32 pos = 0;
     u32 own = n;  // packets of the chunk decided (steady: the rest of the range is skipped drops)
@@ -3370,7 +3441,13 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     }
     if (o.ssN) {  // the chunk's forwarded tuples -> RTPStatsSender
       wave_lds_sync();
+#if LKF_SVC_STATS
+      const u64 ts0 = __builtin_amdgcn_s_memtime();
+#endif
       ss_flush(sSS, o.ssRing, o.ssGap, sSsBuf, o.ssN, o.bSN, o.bTS);
+#if LKF_SVC_STATS
+      tSs += __builtin_amdgcn_s_memtime() - ts0;
+#endif
       o.ssN = 0;
     }
     kpos = lim;
@@ -3452,6 +3529,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     SVC_ADD(35, (unsigned long long)(tP3 - tP2));
     SVC_ADD(36, 1ull);
     SVC_ADD(37, (unsigned long long)(pe - pb));
+    SVC_ADD(38, tLoad);
+    SVC_ADD(39, tSs);
   }
 #endif
   }  // next DownTrack of this wave

@@ -51,10 +51,17 @@ def main():
                   tuple([v[k] / v[9] / 1000.0 for k in (4, 5, 6, 7, 8)] + [v[9]]), flush=True)
             print("   in DD runs (kcycles per DT): decision %.1f marshal %.1f munger/seq decision %.1f" %
                   tuple(v[k] / v[9] / 1000.0 for k in (10, 11, 12)), flush=True)
+            if v[14]:
+                print("   dd_select: %d calls, %.1f kcycles per call" % (v[14], v[13] / v[14] / 1000.0), flush=True)
+                if v[43]:
+                    print("      reaching the marshal (%d): chains %.1f, selection %.1f, marshal %.1f kcycles each" %
+                          (v[43], v[40] / v[43] / 1e3, v[41] / v[43] / 1e3, v[42] / v[43] / 1e3), flush=True)
         if v[36]:  # the plain DownTracks (k_decide_dt<false>)
             print("   plain DTs (kcycles per DT): hot load %.2f rest of prologue %.2f body %.2f epilogue %.2f "
                   "(n=%d, %.2f pkts/DT)" % tuple([v[k] / v[36] / 1000.0 for k in (32, 33, 34, 35)] +
                                                  [v[36], v[37] / v[36]]), flush=True)
+            print("      body: to the first chunk's packets %.2f, RTPStatsSender folds %.2f" %
+                  (v[38] / v[36] / 1000.0, v[39] / v[36] / 1000.0), flush=True)
     tr.close()
 
 
