@@ -117,6 +117,9 @@ struct Match {
 
 // calculateMatch of template j for a packet that uses template k without
 // custom fields (its frame diffs, DTIs and chain diffs are template k's)
+#ifndef LKF_DD_SER
+#define LKF_DD_SER 1  // marshal: an attached structure copied from its serialization (ser_structure)
+#endif
 #ifndef LKF_DD_FASTBEST
 #define LKF_DD_FASTBEST 1  // marshal: the structure's precomputed best template (tmpl_best)
 #endif
@@ -507,7 +510,7 @@ __device__ inline int structure_bits(const DDStruct &s) {
 // (ppool/spill: where p's frame diffs are, see fd_at)
 __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
                                               u32 active, u8 *out, int cap, const u8 *ppool, const u16 *spill,
-                                              bool sameStruct) {
+                                              bool sameStruct, const DDStruct *serS = nullptr) {
   // findBestTemplate.  A packet read with this structure, with no custom
   // field and no structure attached, carries exactly its template's fields:
   // the search's result was computed with the structure (tmpl_best)
@@ -550,9 +553,12 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
   const bool writeActive = hasActive && !(attached && u64(active) == all);
   const bool extended = best.extra > 0 || attached || hasActive;
   int vbits = 1 + 1 + 6 + 16 + best.extra;
+  // an attached structure: its serialization (ser_structure) when given
+  const u32 serBits = (attached && serS) ? u32(serS->serBits) : 0u;
+  if (attached && serS && serBits == 0xffffu) return -1;
   if (extended) {
     vbits += 5;
-    if (attached) vbits += structure_bits(s);
+    if (attached) vbits += serS ? int(serBits) : structure_bits(s);
     if (writeActive) vbits += s.numDT;
   }
   const int nbytes = (vbits + 7) / 8;
@@ -570,7 +576,18 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
     e |= w.write(best.cDtis ? 1 : 0, 1);
     e |= w.write(best.cFdiffs ? 1 : 0, 1);
     e |= w.write(best.cChains ? 1 : 0, 1);
-    if (attached) {
+    if (attached && serS) {  // 32 bits at a time from the serialized structure
+      const u8 *q = serS->ser;
+      u32 k = 0;
+      for (; k + 32 <= serBits; k += 32) {
+        const u32 j = k >> 3;
+        e |= w.write((u32(q[j]) << 24) | (u32(q[j + 1]) << 16) | (u32(q[j + 2]) << 8) | u32(q[j + 3]), 32);
+      }
+      for (; k < serBits; k += 8) {
+        const u32 r = serBits - k < 8 ? serBits - k : 8u;
+        e |= w.write(u32(q[k >> 3]) >> (8 - r), int(r));
+      }
+    } else if (attached) {
       if (!(s.structureId < 64 && s.numDT > 0 && s.numDT <= 32)) return -1;
       e |= w.write(s.structureId, 6);
       e |= w.write(u64(s.numDT - 1), 5);
@@ -673,8 +690,56 @@ __device__ __forceinline__ int dd_marshal_tmpl(const DDStruct &s, int k, u8 pfla
 
 __device__ __attribute__((noinline)) int dd_marshal(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
                                                    u32 active, u8 *out, const u8 *ppool, const u16 *spill,
-                                                   bool sameStruct) {
-  return dd_marshal_inl(s, p, frameNumber, hasActive, active, out, kDDMaxBytes, ppool, spill, sameStruct);
+                                                   bool sameStruct, const DDStruct *serS) {
+  return dd_marshal_inl(s, p, frameNumber, hasActive, active, out, kDDMaxBytes, ppool, spill, sameStruct, serS);
+}
+
+// The structure's part of an attaching descriptor (Marshal's
+// writeTemplateDependencyStructure .. resolutions), as dd_marshal_inl writes
+// it, into s.ser: every DownTrack that forwards the attaching packet copies it
+__device__ inline void ser_structure(DDStruct &s) {
+  for (int i = 0; i < kDDSerBytes; i++) s.ser[i] = 0;
+  BitW w(s.ser, kDDSerBytes);
+  int e = 0;
+  s.serBits = 0xffffu;
+  if (!(s.structureId < 64 && s.numDT > 0 && s.numDT <= 32)) return;
+  e |= w.write(s.structureId, 6);
+  e |= w.write(u64(s.numDT - 1), 5);
+  if (!(s.numTmpl > 0 && s.t[0].sid == 0 && s.t[0].tid == 0)) return;
+  for (int i = 1; i < s.numTmpl; i++) {
+    const DDTmpl &a = s.t[i - 1], &n = s.t[i];
+    int idc;
+    if (n.sid == a.sid && n.tid == a.tid)
+      idc = 0;
+    else if (n.sid == a.sid && n.tid == a.tid + 1)
+      idc = 1;
+    else if (n.sid == a.sid + 1 && n.tid == 0)
+      idc = 2;
+    else
+      return;
+    e |= w.write(u64(idc), 2);
+  }
+  e |= w.write(3, 2);
+  for (int k = 0; k < s.numTmpl; k++)
+    for (int i = 0; i < s.numDT; i++) e |= w.write(dti_at(s.t[k].dtis, i), 2);
+  for (int k = 0; k < s.numTmpl; k++) {
+    for (int i = 0; i < s.t[k].nfd; i++) e |= w.write((u64(1) << 4) | u64(s.fdPool[s.t[k].fdOff + i] - 1), 5);
+    e |= w.write(0, 1);
+  }
+  e |= w.nonSymmetric(s.numChains, u32(s.numDT) + 1);
+  if (s.numChains) {
+    for (int i = 0; i < s.numDT; i++) e |= w.nonSymmetric(s.protectedBy[i], s.numChains);
+    for (int k = 0; k < s.numTmpl; k++)
+      for (int c = 0; c < s.numChains; c++) e |= w.write(dd_tmpl_chain(s.t[k], c), 4);
+  }
+  e |= w.write(s.numRes ? 1 : 0, 1);
+  for (int i = 0; i < s.numRes; i++) {
+    e |= w.write(u64(s.resW[i]) - 1, 16);
+    e |= w.write(u64(s.resH[i]) - 1, 16);
+  }
+  const int bits = w.bitPos;
+  w.finish();
+  if (!e) s.serBits = u16(bits);
 }
 
 // ---- selector ------------------------------------------------------------------
@@ -961,13 +1026,18 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
 #if defined(LKF_SVC_STATS) && LKF_SVC_STATS
   const u64 tq2 = __builtin_amdgcn_s_memtime();
 #endif
-  const int n = dd_marshal(s, p, fn, hasActive, active, out, ppool, spill, p.slot == d.slot);
+  const int n = dd_marshal(s, p, fn, hasActive, active, out, ppool, spill, p.slot == d.slot,
+                           LKF_DD_SER && attached ? structs + p.slot : nullptr);
 #if defined(LKF_SVC_STATS) && LKF_SVC_STATS
   if ((threadIdx.x & 63) == 0) {  // g_svc[40..43]: chains, selection, marshal cycles, marshals
     SVC_ADD(40, tq1 - tq0);
     SVC_ADD(41, tq2 - tq1);
     SVC_ADD(42, __builtin_amdgcn_s_memtime() - tq2);
     SVC_ADD(43, 1ull);
+    if (p.flags & DP_ATTACHED) {  // g_svc[44..45]: the marshals that write a structure
+      SVC_ADD(44, __builtin_amdgcn_s_memtime() - tq2);
+      SVC_ADD(45, 1ull);
+    }
   }
 #endif
   if (n < 0) {

@@ -1056,7 +1056,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   int perCU = 24;
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
   if (const char *v = getenv("LKF_EMIT_PERSISTENT")) e->emitPersistent = atoi(v) != 0;
-  if (const char *v = getenv("LKF_DECIDE_K")) e->decideK = uint32_t(std::min(64, std::max(0, atoi(v))));
+  if (const char *v = getenv("LKF_DECIDE_K")) e->decideK = uint32_t(std::min(8, std::max(0, atoi(v))));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
   if (const char *v = getenv("LKF_GRAPH")) e->useGraph = atoi(v) != 0;

@@ -1762,7 +1762,7 @@ __device__ __forceinline__ void ss_put(SsEnt *e, u64 sn, u64 ts, i64 t, u32 hdr,
 // duplicate, a larger gap, the first packet) takes the scalar Update,
 // wave-uniform.
 #ifndef LKF_SS_SCALAR  // chunks of at most this many forwarded tuples fold entry by entry
-#define LKF_SS_SCALAR 3
+#define LKF_SS_SCALAR 0  // (3 measured slower: headline +1.5 %, tick +1.2 %; r5 A/B)
 #endif
 __device__ __forceinline__ void ss_flush(SenderStats &S, u32 *ring, u32 *gap, const SsEnt *buf, u32 m, u64 bSN,
                                       u64 bTS) {
@@ -2770,10 +2770,11 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
 }
 #undef SVC_WHY
 
-template <bool DDK>
+constexpr u32 kDecideMaxK = 8;  // schedule slots per decide wave (LKF_DECIDE_K is clamped to it; 8 and 16 measured slower than 4)
 #ifndef LKF_DEC_PREFETCH  // a single-chunk track's packets loaded with the DownTrack's state
 #define LKF_DEC_PREFETCH 0  // (measured: the headline 1.3 % slower with it, the tick flat; r5 A/B)
 #endif
+template <bool DDK>
 __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, const lkf_pkt *__restrict__ pkts) {
   __shared__ i32 sDrop[kSetCap];
   __shared__ i32 sEx[kSetCap];
@@ -2783,7 +2784,8 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   // (the plain instantiation keeps a 16-B stub: LDS is allocated per instantiation)
   __shared__ __attribute__((aligned(16))) u8 sDDRaw[DDK ? sizeof(DDState) + kDDMaxBytes + 1 : 16];
   __shared__ u8 sSvcScr[DDK ? 64 * kSvcDDBytes : 16];  // svc_run: per-lane marshalled descriptors
-  __shared__ __attribute__((aligned(16))) u8 sDDSRaw[DDK ? sizeof(DDStruct) : 16];  // the structure in force
+  // the structure in force (the staged part: not its serialization)
+  __shared__ __attribute__((aligned(16))) u8 sDDSRaw[DDK ? __builtin_offsetof(DDStruct, serBits) : 16];
   __shared__ u8 sSvcFD[kSvcFrames];                    // svc_run: decisions of the run's frames
   DDState *const sDD = reinterpret_cast<DDState *>(sDDRaw);
   u8 *const sDDBuf = sDDRaw + (DDK ? sizeof(DDState) : 0);
@@ -2797,7 +2799,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   // batch is skipped: its state does not change and k_batch_init zeroed its
   // counters.
   // The list is kept in LDS (not registers) across the DownTrack loop.
-  __shared__ uint4 sSlot[2 * 64];
+  __shared__ uint4 sSlot[2 * kDecideMaxK];
   u64 todo;
   {
     const u32 K = A.perWave, lane = threadIdx.x;
@@ -4628,6 +4630,7 @@ __global__ void __launch_bounds__(64) k_dd_decode(const RunDesc *__restrict__ de
             o.flags = 0;
           } else {
             attOK = att;
+            if (att && LKF_DD_SER) dd::ser_structure(ring[next]);  // (the attaching packet's lane only)
             o.slot = u8(att ? next : cur);
             o.flags |= DP_VALID;
           }
@@ -4822,7 +4825,7 @@ hipError_t launch_decide(hipStream_t s, const DecideLaunch &a) {
   // Each part is a multiple of 8 slots (per-XCD lists of equal length);
   // a workgroup takes perWave consecutive slots of one XCD's list.
   const u32 nPlain = a.nlanes - a.ddLanes;
-  const u32 K = a.perWave ? a.perWave : 1;
+  const u32 K = a.perWave ? (a.perWave < kDecideMaxK ? a.perWave : kDecideMaxK) : 1;
   A.perWave = K;
   auto blocks = [K](u32 lanes) { return (lanes / 8 + K - 1) / K * 8; };
   A.waveBase = 0;

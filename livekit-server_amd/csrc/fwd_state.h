@@ -210,6 +210,7 @@ struct DDTmpl {  // dependencydescriptor.FrameDependencyTemplate of a structure 
 };
 static_assert(sizeof(DDTmpl) == 32, "DDTmpl must be 32 B");
 
+constexpr int kDDSerBytes = 256;  // a serialized structure (an attaching descriptor is at most 255 B)
 struct alignas(16) DDStruct {  // FrameDependencyStructure + ProcessFrameDependencyStructure
   uint8_t structureId, numDT, numChains, numTmpl;
   uint8_t numRes, pad;
@@ -220,6 +221,13 @@ struct alignas(16) DDStruct {  // FrameDependencyStructure + ProcessFrameDepende
   uint8_t pad2[8];
   DDTmpl t[64];
   uint8_t fdPool[kDDFdPool];
+  // the structure as a descriptor that attaches it writes it (structureId
+  // through the resolutions), serialized once when the forwarding side reads
+  // it (k_dd_decode); serBits 0xffff: not writable (the marshal fails).
+  // After the pool: decide never stages it (read from the ring in HBM)
+  uint16_t serBits;
+  uint8_t pad3[14];
+  uint8_t ser[kDDSerBytes];
 };
 static_assert(sizeof(DDStruct) % 16 == 0, "DDStruct must be 16-B granular");
 static_assert(__builtin_offsetof(DDStruct, t) % 16 == 0 && __builtin_offsetof(DDStruct, fdPool) % 16 == 0,

@@ -56,6 +56,9 @@ def main():
                 if v[43]:
                     print("      reaching the marshal (%d): chains %.1f, selection %.1f, marshal %.1f kcycles each" %
                           (v[43], v[40] / v[43] / 1e3, v[41] / v[43] / 1e3, v[42] / v[43] / 1e3), flush=True)
+                if v[45]:
+                    print("      of which with a structure attached: %d, marshal %.1f kcycles each" %
+                          (v[45], v[44] / v[45] / 1e3), flush=True)
         if v[36]:  # the plain DownTracks (k_decide_dt<false>)
             print("   plain DTs (kcycles per DT): hot load %.2f rest of prologue %.2f body %.2f epilogue %.2f "
                   "(n=%d, %.2f pkts/DT)" % tuple([v[k] / v[36] / 1000.0 for k in (32, 33, 34, 35)] +
