@@ -511,11 +511,12 @@ __device__ inline int structure_bits(const DDStruct &s) {
 __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p, u16 frameNumber, bool hasActive,
                                               u32 active, u8 *out, int cap, const u8 *ppool, const u16 *spill,
                                               bool sameStruct, const DDStruct *serS = nullptr) {
-  // findBestTemplate.  A packet read with this structure, with no custom
-  // field and no structure attached, carries exactly its template's fields:
-  // the search's result was computed with the structure (tmpl_best)
+  // findBestTemplate.  A packet read with this structure (the one it
+  // attaches, or the one in force) and with no custom field carries exactly
+  // its template's fields: the search's result was computed with the
+  // structure (tmpl_best)
   Match best;
-  if (LKF_DD_FASTBEST && sameStruct && !(p.flags & DP_ATTACHED) && p.custom == 0 && p.tmplIdx < s.numTmpl) {
+  if (LKF_DD_FASTBEST && sameStruct && p.custom == 0 && p.tmplIdx < s.numTmpl) {
     const DDTmpl &q = s.t[p.tmplIdx];
     best.idx = q.best;
     best.cDtis = q.bestC & 1;

@@ -2770,6 +2770,36 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
 }
 #undef SVC_WHY
 
+#ifndef LKF_DD_RESTAGE
+#define LKF_DD_RESTAGE 1
+#endif
+// The structure in force staged in LDS: its decode targets, chains and
+// templates are read on every descriptor (selection, marshalling).  The ring
+// entries are fixed while the batch decides (k_dd_decode filled them); a
+// descriptor that attaches a new structure moves the DownTrack to another
+// slot, which is then staged in turn (dd_restage).
+__device__ __forceinline__ void dd_stage_struct(Lane &L, const DDState *sDD, u8 *sDDSRaw, u32 lane) {
+  const u32 slot = __builtin_amdgcn_readfirstlane(u32(sDD->slot));
+  const uint4 *gs = reinterpret_cast<const uint4 *>(L.ddRing + slot);
+  uint4 *ls = reinterpret_cast<uint4 *>(sDDSRaw);
+  // the header and the templates in use, then the used part of the pool
+  const u32 nT = __builtin_amdgcn_readfirstlane(u32(L.ddRing[slot].numTmpl));
+  const u32 nP = __builtin_amdgcn_readfirstlane(u32(L.ddRing[slot].nfdPool));
+  constexpr u32 kTOff = __builtin_offsetof(DDStruct, t) / 16, kPOff = __builtin_offsetof(DDStruct, fdPool) / 16;
+  const u32 nHead = kTOff + nT * (sizeof(DDTmpl) / 16), nPool = (nP + 15) / 16;
+  for (u32 i = lane; i < nHead + nPool; i += 64) {
+    const u32 k = i < nHead ? i : kPOff + (i - nHead);
+    ls[k] = gs[k];
+  }
+  L.ddSSlot = slot;
+  __syncthreads();
+}
+__device__ __forceinline__ void dd_restage(Lane &L, const DDState *sDD, u8 *sDDSRaw, u32 lane) {
+  wave_lds_sync();
+  const bool moved = __builtin_amdgcn_readfirstlane(int((sDD->flags & DS_KF_VALID) && u32(sDD->slot) != L.ddSSlot));
+  if (LKF_DD_RESTAGE && moved) dd_stage_struct(L, sDD, sDDSRaw, lane);
+}
+
 constexpr u32 kDecideMaxK = 8;  // schedule slots per decide wave (LKF_DECIDE_K is clamped to it; 8 and 16 measured slower than 4)
 #ifndef LKF_DEC_PREFETCH  // a single-chunk track's packets loaded with the DownTrack's state
 #define LKF_DEC_PREFETCH 0  // (measured: the headline 1.3 % slower with it, the tick flat; r5 A/B)
@@ -2968,25 +2998,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     const u32 nDD = (kDDStateHead + nc0 * kDDExpect * 8) / 16;
     for (u32 i = lane; i < nDD; i += 64) l[i] = g[i];
     __syncthreads();
-    // the structure in force: its decode targets, chains and templates are
-    // read on every descriptor (selection, marshalling); the ring entries are
-    // fixed while the batch decides (k_dd_decode filled them)
-    const u32 slot = __builtin_amdgcn_readfirstlane(u32(sDD->slot));
-    if (sDD->flags & DS_KF_VALID) {
-      const uint4 *gs = reinterpret_cast<const uint4 *>(L.ddRing + slot);
-      uint4 *ls = reinterpret_cast<uint4 *>(sDDSRaw);
-      // the header and the templates in use, then the used part of the pool
-      const u32 nT = __builtin_amdgcn_readfirstlane(u32(L.ddRing[slot].numTmpl));
-      const u32 nP = __builtin_amdgcn_readfirstlane(u32(L.ddRing[slot].nfdPool));
-      constexpr u32 kTOff = __builtin_offsetof(DDStruct, t) / 16, kPOff = __builtin_offsetof(DDStruct, fdPool) / 16;
-      const u32 nHead = kTOff + nT * (sizeof(DDTmpl) / 16), nPool = (nP + 15) / 16;
-      for (u32 i = lane; i < nHead + nPool; i += 64) {
-        const u32 k = i < nHead ? i : kPOff + (i - nHead);
-        ls[k] = gs[k];
-      }
-      L.ddSSlot = slot;
-      __syncthreads();
-    }
+    if (sDD->flags & DS_KF_VALID) dd_stage_struct(L, sDD, sDDSRaw, lane);
   }
   o.outT = A.recs + slot0;
   o.outW = A.wide + slot0;
@@ -3088,6 +3100,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
           const u32 px = rl32(pi, x);
           decide_step<DDK>(L, load_pkt(pkts + px), px, o);
           vm_drain();
+          if (ddDT) dd_restage(L, sDD, sDDSRaw, lane);
 #if LKF_SVC_STATS
           tStep += __builtin_amdgcn_s_memtime() - tr1;
 #endif
@@ -3428,6 +3441,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
         const u32 px = rl32(pi, x);
         decide_step<DDK>(L, decode_pkt(a0, a1, a2, a3), px, o);
         vm_drain();
+        if (DDK && ddDT) dd_restage(L, sDD, sDDSRaw, lane);
         pos = x + 1;
         if (steady && !steady_state(L)) {  // left the steady state: the chunk ends after this packet
           own = x + 1;
