@@ -927,6 +927,7 @@ struct SelResult {
   bool selected, relevant, switching, resuming, marker;
   int ddLen;  // marshalled bytes in the output buffer (selected only)
   bool limit;  // an engine limit was hit (kDDExpect)
+  u32 stagedSlot;  // the ring slot the LDS copy holds on return
 };
 
 // Select :65-355.  Layers are the DownTrack's Base layers (DTHot); structs is
@@ -935,9 +936,9 @@ struct SelResult {
 // track's ring in HBM for that slot)
 __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStruct *structs, const DDPkt *pp, bool pktMarker,
                                       i32 &curS, i32 &curT, i32 &prevS, i32 &prevT, i32 tgtS, i32 tgtT, u8 *out,
-                                      const DDStruct *staged, u32 stagedSlot, const u16 *spill) {
+                                      DDStruct *staged, u32 stagedSlot, const u16 *spill) {
   auto pick = [&](u32 slot) -> const DDStruct & { return slot == stagedSlot ? *staged : structs[slot]; };
-  SelResult r = {false, false, false, false, false, 0, false};
+  SelResult r = {false, false, false, false, false, 0, false, stagedSlot};
   if (curS != -1 && curT != -1) r.relevant = true;
   if (!pp) return r;  // (no descriptor)
   const DDPkt &p = *pp;
@@ -953,7 +954,24 @@ __device__ __attribute__((noinline)) SelResult dd_select(DDState &d, const DDStr
     invalidate_keyframe(d);
     return r;
   }
-  const DDStruct &s = pick(d.slot);
+  // the structure in force, in LDS: staged again when this descriptor moved
+  // the DownTrack to another slot (so the selection and the marshal read LDS)
+  if (u32(d.slot) != stagedSlot) {
+    const u32 slot = d.slot, ln = threadIdx.x & 63u;
+    const uint4 *gs = reinterpret_cast<const uint4 *>(structs + slot);
+    uint4 *ls = reinterpret_cast<uint4 *>(staged);
+    const u32 nT = structs[slot].numTmpl, nP = structs[slot].nfdPool;
+    constexpr u32 kTOff = __builtin_offsetof(DDStruct, t) / 16, kPOff = __builtin_offsetof(DDStruct, fdPool) / 16;
+    const u32 nHead = kTOff + nT * (sizeof(DDTmpl) / 16), nPool = (nP + 15) / 16;
+    for (u32 i = ln; i < nHead + nPool; i += 64) {
+      const u32 k = i < nHead ? i : kPOff + (i - nHead);
+      ls[k] = gs[k];
+    }
+    stagedSlot = slot;
+    r.stagedSlot = slot;
+    __syncthreads();
+  }
+  const DDStruct &s = *staged;
   if (p.extFlags & LKF_DD_ACTIVE_UPDATED) update_active(d, s, p.activeMask);
   if (p.nchain != d.numChains) {
     c_add(d, efn, SD_DROPPED);

@@ -230,7 +230,7 @@ struct Lane {
   // structure ring, this batch's decoded descriptors, the marshal buffer
   DDState *dd;
   const DDStruct *ddRing;
-  const DDStruct *ddS;  // LDS copy of ring slot ddSSlot (the current structure when the batch started)
+  DDStruct *ddS;  // LDS copy of ring slot ddSSlot (the structure in force: staged again when it changes)
   u32 ddSSlot;
   const DDPkt *ddPkts;
   const u16 *ddSpill;
@@ -1062,6 +1062,7 @@ __device__ int fw_translate(Lane &L, const PktV &p, u32 k, Fwd &o) {
     }
 #endif
     if (r.limit && lane_id() == 0) atomicOr(L.err, 16u);
+    L.ddSSlot = r.stagedSlot;
     if (!r.selected) {
       if (r.relevant && hasf(L, F_STARTED)) {  // forwarder.go:1694-1702 (RTPMarker false)
         int ord;
@@ -2233,7 +2234,8 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
   if (DDK && dd) {
     const DDState &d = *L.dd;
     uni = (d.flags & DS_KF_VALID) && (d.flags & DS_CACHE_INIT);
-    s = u32(d.slot) == L.ddSSlot ? L.ddS : L.ddRing + d.slot;
+    uni = uni && u32(d.slot) == L.ddSSlot;  // (the structure in force is the staged one)
+    s = L.ddS;
     for (int i = 0; uni && i < int(d.numTargets); i++) {  // the decode target Select picks (:133-176)
       if (!((d.dtActive >> i) & 1) || i32(s->dtS[i]) > L.h.tgtS || i32(s->dtT[i]) > L.h.tgtT) continue;
       const int target = s->dtTarget[i];
@@ -2975,7 +2977,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   L.ddPktL = &sDDPkt;
   L.ddSpill = A.ddSpill;
   L.ddRing = nullptr;
-  L.ddS = reinterpret_cast<const DDStruct *>(sDDSRaw);
+  L.ddS = reinterpret_cast<DDStruct *>(sDDSRaw);
   L.ddSSlot = 0xffffffffu;
   L.dd = sDD;
   L.ddBuf = sDDBuf;
