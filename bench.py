@@ -152,6 +152,8 @@ def cpu_baseline(threads, sample_rooms=256, sample_batches=4, config=2, ingress=
     traces = []
     for t in range(nrs):
         traces.append(wl.Trace(config, duration_s=float(sample_batches), batch_s=1.0, rooms=per, room_base=t * per))
+        if ingress:
+            wl.events_at_batch_start(traces[-1])
     fan = max(int(np.bincount([traces[0].downtracks[d].track for d in range(traces[0].ndts)]).max()), 0)
     split = 1
     if nrs < threads * 4 and fan >= 20:  # DownTrackSpreader's parallel fan-out
@@ -223,6 +225,8 @@ def parity_gate(eng, pkg, config, room_ids, nb, batch_s, ingress, trace, threads
     traces, keep, shards = [], [], (_BenchShard * len(chunks))()
     for t, rids in enumerate(chunks):
         tr = wl.Trace(config, duration_s=nb * batch_s, batch_s=batch_s, room_ids=rids)
+        if ingress:
+            wl.events_at_batch_start(tr)  # (as the GPU's trace)
         traces.append(tr)
         bb = (_BenchBatch * nb)()
         dd = tr.has_dd() and not ingress
@@ -273,23 +277,40 @@ def parity_gate(eng, pkg, config, room_ids, nb, batch_s, ingress, trace, threads
     ok_cum = gcum == ocum
     # per DownTrack (by SSRC): Forwarder state + RTPStatsSender
     orc = {}
-    for i in range(ndts):
+    for i in range(ndts):  # keyed by (SSRC, subscriber): random SSRCs of different rooms collide
         r = drec[i * dstride:(i + 1) * dstride]
-        orc[int(r[:4].view(np.uint32)[0])] = r
+        k = tuple(int(x) for x in r[:8].view(np.uint32))
+        orc.setdefault(k, []).append(r)
     bad_dt = 0
+    dup_keys = 0  # DownTracks whose (SSRC, subscriber) is not unique (matched against any of them)
+    examples = []
     st = abi.lkf_fwd_state()
     ss = np.zeros(1, dtype=abi.SENDER_STATS_DTYPE)
     for d in range(trace.ndts):
-        ssrc = int(trace.downtracks[d].ssrc)
-        r = orc.get(ssrc)
-        if r is None or eng.api["get_state"](eng.h, d, C.byref(st)) != 0 or \
+        key = (int(trace.downtracks[d].ssrc), int(trace.downtracks[d].subscriber))
+        rs = orc.get(key)
+        if rs is None or eng.api["get_state"](eng.h, d, C.byref(st)) != 0 or \
                 eng.api["sender_stats_get"](eng.h, d, ss.ctypes.data) != 0:
             bad_dt += 1
             continue
+
+        def same(r):
+            ost_ = abi.lkf_fwd_state.from_buffer_copy(bytes(r[8:8 + fs_sz]))
+            oss_ = np.frombuffer(bytes(r[8 + fs_sz:8 + fs_sz + ss_sz]), dtype=abi.SENDER_STATS_DTYPE)
+            return st.as_tuple() == ost_.as_tuple() and all(np.array_equal(ss[k], oss_[k]) for k in ss.dtype.names)
+        if len(rs) > 1:
+            dup_keys += 1
+        r = rs[0]
         ost = abi.lkf_fwd_state.from_buffer_copy(bytes(r[8:8 + fs_sz]))
         oss = np.frombuffer(bytes(r[8 + fs_sz:8 + fs_sz + ss_sz]), dtype=abi.SENDER_STATS_DTYPE)
-        if st.as_tuple() != ost.as_tuple() or any(not np.array_equal(ss[k], oss[k]) for k in ss.dtype.names):
+        if not any(same(x) for x in rs):
             bad_dt += 1
+            if len(examples) < 4:  # what differs (GPU, oracle), for the record
+                fd = {n: (getattr(st, n), getattr(ost, n)) for n, *_ in abi.lkf_fwd_state._fields_
+                      if not isinstance(getattr(st, n), C.Array) and getattr(st, n) != getattr(ost, n)}
+                sd = {k: (ss[k].tolist(), oss[k].tolist()) for k in ss.dtype.names if not np.array_equal(ss[k], oss[k])}
+                examples.append({"dt": d, "track": int(trace.downtracks[d].track), "fwd_state": fd,
+                                 "sender_stats": {k: v for k, v in list(sd.items())[:6]}})
     # per stream (by SSRC): RTPStatsReceiver
     bad_st = 0
     if ingress:
@@ -306,7 +327,12 @@ def parity_gate(eng, pkg, config, room_ids, nb, batch_s, ingress, trace, threads
                 "counters_equal": ok_cum, "downtracks_checked": trace.ndts, "downtracks_differing": bad_dt,
                 "streams_checked": trace.nstreams if ingress else 0, "streams_differing": bad_st,
                 "batches": nb, "forwarded_total": gcum["forwarded"], "oracle_threads": threads,
+                "dt_keys_not_unique": dup_keys,
                 "gate_s": round(time.perf_counter() - t0, 1)})
+    if not ok_cum:
+        res["counters_gpu_oracle"] = {k: (gcum[k], ocum[k]) for k in gcum if gcum[k] != ocum[k]}
+    if examples:
+        res["differing_examples"] = examples
     return res
 
 
@@ -396,6 +422,8 @@ def main():
     rooms_mod = importlib.import_module("livekit-server_amd.rooms")
     plan = rooms_mod.plan_room_shards([1.0] * (world * args.rooms), world)
     trace = wl.Trace(args.config, duration_s=nb * args.batch_s, batch_s=args.batch_s, room_ids=plan[rank])
+    if args.ingress:
+        wl.events_at_batch_start(trace)
     has_dd = trace.has_dd() and not args.ingress  # (ingest produces the DD side array on the GPU)
     lib = os.environ.get("LKF_LIB") or None
     if lib and os.sep not in lib:  # a name: one of the in-tree builds

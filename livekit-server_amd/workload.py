@@ -119,6 +119,22 @@ def events_ptr(trace, b):
     return ev, n.value
 
 
+def events_at_batch_start(trace):
+    """The ingress steps: every scripted control op applies at the start of
+    its batch (at_pkt 0).  The workload computes at_pkt as an index into its
+    own ExtPacket batch, which in an ingress step exists only after
+    Buffer.calc, with other per-track counts (late datagrams, padding):
+    there the index would land on another track's packet, and where it lands
+    would depend on which rooms share the engine, so engines holding
+    different room sets (bench.py's sharded parity gate and CPU baseline)
+    would not apply the op at the same point."""
+    for b in range(trace.nbatches):
+        ev, n = events_ptr(trace, b)
+        if n:
+            for e in (abi.lkfs_event * n).from_address(C.cast(ev, C.c_void_p).value):
+                e.at_pkt = 0
+
+
 def queue_events(api, eng, trace, b):
     """Queues batch b's scripted control ops (lkfs_event == lkf_ctl_event layout)."""
     ev, n = events_ptr(trace, b)

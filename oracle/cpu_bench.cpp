@@ -73,7 +73,7 @@ int orc_cpu_bench(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthr
 
 // bench.py's parity gate (outside its timed region): the same shards run to
 // the end, then per shard its cumulative counters (cum[shard]) and, per
-// DownTrack, {ssrc, lkf_fwd_state, lkf_sender_stats} (dtRecs, shards' DownTracks
+// DownTrack, {ssrc, subscriber, lkf_fwd_state, lkf_sender_stats} (dtRecs, shards' DownTracks
 // in order, stride dtStride bytes) and per stream {ssrc, lkf_stream_stats}
 // (stRecs, stride stStride; ingress only).  SSRCs key the records to the GPU
 // engine's DownTracks and streams (a room shard keeps its rooms' SSRCs).
@@ -97,6 +97,7 @@ int orc_parity_run(const orc_bench_shard *shards, uint32_t nshards, uint32_t nth
       for (uint32_t d = 0; d < sh[i].ndts; d++) {
         uint8_t *r = dt + (d0 + d) * dtStride;
         std::memcpy(r, &sh[i].dts[d].ssrc, 4);
+        std::memcpy(r + 4, &sh[i].dts[d].subscriber, 4);  // (SSRCs of different rooms can collide)
         lkf_fwd_state fs{};
         lkf_sender_stats ss{};
         if (orc_get_state(e, int32_t(d), &fs) || orc_sender_stats_get(e, int32_t(d), &ss)) rc = -1;

@@ -55,6 +55,8 @@ def test_parity_gate_oracle_vs_oracle(config, ingress):
     room_ids = rooms.plan_room_shards([1.0] * 12, 2)[1]  # rank 1's rooms of a 2-rank plan
     nb = 3
     tr = wl.Trace(config, duration_s=float(nb), batch_s=1.0, room_ids=room_ids)
+    if ingress:  # (bench.py's ingress step: control ops at the batch start)
+        wl.events_at_batch_start(tr)
     o = load_oracle()
     h, tot = _run_whole(o, wl, abi, tr, nb, ingress)
     zero = {"tuples": 0, "forwarded": 0, "out_bytes": 0, "arena_bytes": 0, "drops": [0] * abi.LKF_DROP_NREASONS}
