@@ -117,6 +117,9 @@ struct Match {
 
 // calculateMatch of template j for a packet that uses template k without
 // custom fields (its frame diffs, DTIs and chain diffs are template k's)
+#ifndef LKF_DD_PACK
+#define LKF_DD_PACK 1  // SVC runs: a custom-field-free descriptor packed in a register (dd_marshal_tmpl)
+#endif
 #ifndef LKF_DD_SER
 #define LKF_DD_SER 1  // marshal: an attached structure copied from its serialization (ser_structure)
 #endif
@@ -657,6 +660,24 @@ __device__ __forceinline__ int dd_marshal_inl(const DDStruct &s, const DDPkt &p,
 __device__ __forceinline__ int dd_marshal_tmpl(const DDStruct &s, int k, u8 pflags, u16 frameNumber, bool hasActive,
                                                u32 active, u8 *out, int cap) {
   const DDTmpl &q = s.t[k];
+  if (LKF_DD_PACK && q.bestC == 0) {
+    // no custom field: the mandatory fields (+ the extended flags and the
+    // active mask) are at most 61 bits, packed MSB first in one register and
+    // stored as two big-endian dwords (out is dword-aligned, cap >= 8)
+    const u32 nd = s.numDT;
+    u64 v = (u64((pflags & DP_FIRST) ? 1 : 0) << 63) | (u64((pflags & DP_LAST) ? 1 : 0) << 62) |
+            (u64((q.best + s.structureId) % 64) << 56) | (u64(frameNumber) << 40);
+    int bits = 24;
+    if (hasActive) {  // extended: attached 0, active 1, custom DTIs / frame diffs / chains 0
+      v |= u64(0x08) << 35;
+      v |= (u64(active) & (nd >= 32 ? 0xffffffffull : ((1ull << nd) - 1))) << (35 - nd);
+      bits = 29 + int(nd);
+    }
+    u32 *o = reinterpret_cast<u32 *>(out);
+    o[0] = __builtin_bswap32(u32(v >> 32));
+    o[1] = __builtin_bswap32(u32(v));
+    return (bits + 7) / 8;
+  }
   const bool cDtis = q.bestC & 1, cFdiffs = q.bestC & 2, cChains = q.bestC & 4;
   int extra = 0;
   if (cFdiffs) extra = 2 * (1 + q.nfd) + 4 * q.nfd;  // (template frame diffs are 1-16)

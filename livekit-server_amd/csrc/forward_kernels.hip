@@ -2815,7 +2815,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
   __shared__ RangeEntry sRm[kRangeCap];
   // (the plain instantiation keeps a 16-B stub: LDS is allocated per instantiation)
   __shared__ __attribute__((aligned(16))) u8 sDDRaw[DDK ? sizeof(DDState) + kDDMaxBytes + 1 : 16];
-  __shared__ u8 sSvcScr[DDK ? 64 * kSvcDDBytes : 16];  // svc_run: per-lane marshalled descriptors
+  __shared__ __attribute__((aligned(16))) u8 sSvcScr[DDK ? 64 * kSvcDDBytes : 16];  // svc_run: per-lane marshalled descriptors
   // the structure in force (the staged part: not its serialization)
   __shared__ __attribute__((aligned(16))) u8 sDDSRaw[DDK ? __builtin_offsetof(DDStruct, serBits) : 16];
   __shared__ u8 sSvcFD[kSvcFrames];                    // svc_run: decisions of the run's frames
