@@ -1556,6 +1556,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
 // RTCP NACK) and the offset of its pairs in the batch's pair buffer.
 // ---------------------------------------------------------------------------
 
+#ifndef LKF_NACK_LIVE  // stage only the live entries (1), or all slots with the count (0, round 4)
+#define LKF_NACK_LIVE 1
+#endif
 __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__ raws,
                                                  const IngParsed *__restrict__ q, const lkf_flow *__restrict__ flows,
                                                  const DevStream *__restrict__ streams, NackState *__restrict__ states,
@@ -1583,7 +1586,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   // only the live entries are staged (every read below is of an index < count)
   u32 count = g->count;
   const u32 rtt = g->rtt;
-  for (u32 i = lane; i < count; i += 64) {
+  for (u32 i = lane; i < (LKF_NACK_LIVE ? count : u32(kNackSlots)); i += 64) {
     sLast[i] = g->last[i];
     sSn[i] = g->sn[i];
     sTries[i] = g->tries[i];
