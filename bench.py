@@ -336,6 +336,61 @@ def parity_gate(eng, pkg, config, room_ids, nb, batch_s, ingress, trace, threads
     return res
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` without a torch.distributed launcher: start N fresh
+    child processes of this script, one per GPU, with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (the same environment
+    `torch.distributed.run --nproc-per-node N` gives them).  The parent never
+    touches the GPU: it only waits.  Rank 0 prints the JSON line.  A failing
+    rank ends the others (they would block in a collective).  -> exit code."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:  # the exact process groups this launcher started
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
+
+
+def tick_times(b, batch_s, update_ms):
+    """Room.audioUpdateWorker ticks (every UpdateInterval of media time,
+    room.go:1278-1316, config.go:380-384) that fall in batch b's media window
+    (b * batch_s, (b + 1) * batch_s], in seconds.  A tick runs after the batch
+    that contains it has been enqueued (levels and totals as of that batch)."""
+    if update_ms <= 0:
+        return []
+    u = update_ms / 1e3
+    k0 = int(np.floor(b * batch_s / u + 1e-9)) + 1
+    out = []
+    k = k0
+    while k * u <= (b + 1) * batch_s + 1e-9:
+        out.append(k * u)
+        k += 1
+    return out
+
+
 def kernel_sources_sha():
     """Digest of the engine sources: a PMC traffic summary is only quoted for
     the build it was measured on."""
@@ -387,7 +442,19 @@ def main():
                          "the timed region: counters, every Forwarder state, RTPStatsSender, RTPStatsReceiver)")
     ap.add_argument("--srtp-profile", choices=["aes_cm", "gcm"], default="aes_cm",
                     help="with --srtp: SRTP_AES128_CM_HMAC_SHA1_80 or SRTP_AEAD_AES_128_GCM transports")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--update-ms", type=float, default=400.0,
+                    help="N > 1: the room manager's summary all-gather every this many ms of media "
+                         "(Room.audioUpdateWorker, UpdateInterval 400 ms); 0 = only once after the run")
+    ap.add_argument("--ticks-n1", action="store_true",
+                    help="run the --update-ms summary ticks at N = 1 too (packing only: no peer to gather from)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher rehearsal without a GPU: the CPU oracle (tests/dryrun_engine.py) stands in for "
+                         "the engine and the backend is gloo; the line is marked dry_run and is not a measurement")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))  # (before anything touches the GPU)
     if not args.rooms:
         args.rooms = CONFIGS[args.config]["rooms"]
     speakers = args.config == 3
@@ -403,14 +470,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dry = args.dry_run
+    backend = "gloo" if dry else args.dist_backend
+    if dry:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+
+    def csync():
+        if not dry:
+            torch.cuda.synchronize(dev)
+
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group(backend)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
 
     pkg = importlib.import_module("livekit-server_amd")
     wl = importlib.import_module("livekit-server_amd.workload")
@@ -428,7 +504,10 @@ def main():
     lib = os.environ.get("LKF_LIB") or None
     if lib and os.sep not in lib:  # a name: one of the in-tree builds
         lib = os.path.join(ROOT, "livekit-server_amd", "lib", lib)
-    eng = pkg.Engine.for_trace(trace, device=local, lib_path=lib)
+    if dry:  # (test infrastructure: the oracle behind Engine's bench-facing methods)
+        eng = importlib.import_module("tests.dryrun_engine").DryRunEngine.for_trace(trace)
+    else:
+        eng = pkg.Engine.for_trace(trace, device=local, lib_path=lib)
     wl.load_topology(eng.api, eng.h, trace)
 
     if args.ingress:
@@ -449,7 +528,7 @@ def main():
 
     # inputs resident in HBM before the timed region (--host-io: in pinned host memory)
     dpk, dar, meta, ddd = [], [], [], []
-    hdev = torch.device("cpu") if args.host_io else dev
+    hdev = torch.device("cpu") if args.host_io or dry else dev
     for b in range(nb):
         if args.ingress:
             pk, n, ar, alen = trace.batch_raw(b)  # raw datagrams: Buffer.calc runs inside the step
@@ -470,8 +549,76 @@ def main():
             dptr, dn = trace.batch_dd(b)
             dsz = C.sizeof(pkg.abi.lkf_pkt_dd)
             ddd.append(torch.frombuffer(bytearray(C.string_at(dptr, max(1, dn) * dsz)), dtype=torch.uint8).to(hdev))
-    stream = torch.cuda.current_stream(dev)
-    sp = C.c_void_p(stream.cuda_stream)
+    sp = None if dry else C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+    # N > 1: the room manager's summaries (speaker ranking + per-subscriber
+    # bandwidth records) all-gathered every --update-ms of media inside the
+    # loop.  On the GPU path the engine packs them in HBM on a stream of their
+    # own (lkf_room_summaries_enqueue: no host wait, the forwarding pipeline
+    # keeps running) and RCCL gathers them there; the gather's own time is
+    # measured with events on that stream and reported apart from the metric.
+    # Without a GPU (--dry-run) or over gloo they go through host memory.
+    width = max(len(p) for p in plan)
+    my_rooms = np.asarray(plan[rank], dtype=np.int64)
+    tick_on = args.update_ms > 0 and (world > 1 or args.ticks_n1)
+    dev_ticks = tick_on and not dry and backend == "nccl"
+    tick_log = []  # per tick: (media s, gather events or host ms)
+    if dev_ticks:
+        K, S = rooms_mod.K_MAX, rooms_mod.S_MAX
+        mgr = torch.cuda.Stream(dev)
+        ring = []
+        for _ in range(8):
+            spk = torch.full((width, K, 3), -1, dtype=torch.int32, device=dev)
+            spk[:, :, 1:] = 0
+            bwe = torch.zeros((width, S, 5), dtype=torch.int64, device=dev)
+            bwe[:, :, 0] = -1
+            spk_all, bwe_all = (torch.empty((world,) + tuple(spk.shape), dtype=spk.dtype, device=dev),
+                                torch.empty((world,) + tuple(bwe.shape), dtype=bwe.dtype, device=dev)) \
+                if world > 1 else (spk[None], bwe[None])  # (N = 1: the records are the table)
+            ring.append((spk, bwe, spk_all, bwe_all, torch.cuda.Event(enable_timing=True),
+                         torch.cuda.Event(enable_timing=True)))
+        torch.cuda.synchronize(dev)
+        rs_call = eng.api["room_summaries_enqueue"]
+        rs_ids = np.ascontiguousarray(my_rooms.astype(np.uint32))
+        mgr_p = mgr.cuda_stream
+
+    def gather_tables(spk_np, bwe_np):
+        """host path: one all-gather of each record table -> numpy [world, ...]"""
+        if not dist:
+            return spk_np[None], bwe_np[None]
+        return (rooms_mod.all_gather_records(dist, cdev, spk_np), rooms_mod.all_gather_records(dist, cdev, bwe_np))
+
+    def host_records(now):
+        spk = rooms_mod.pack_speakers(pkg.speakers_array(eng.api, eng.h, now), my_rooms)
+        if width > len(spk):  # a short bin-packed shard: padding rows
+            pad = np.full((width - len(spk),) + spk.shape[1:], -1, dtype=np.int32)
+            pad[:, :, 1:] = 0
+            spk = np.concatenate([spk, pad])
+        return spk, rooms_mod.fold_summaries(pkg.downtrack_summaries(eng.api, eng.h), my_rooms, rows=width)
+
+    def summary_tick(t_s):
+        now = 1700000000 * 10**9 + int(round(t_s * 1e9))
+        if dev_ticks:
+            i = len(tick_log) % len(ring)
+            spk, bwe, spk_all, bwe_all, e0, e1 = ring[i]
+            if len(tick_log) >= len(ring):  # the engine writes these buffers: their last gather must be done
+                e1.synchronize()
+                j = len(tick_log) - len(ring)
+                tick_log[j] = (tick_log[j][0], e0.elapsed_time(e1), None)
+            rc = rs_call(eng.h, now, rs_ids.ctypes.data, len(rs_ids), spk.data_ptr(), K, bwe.data_ptr(), S, mgr_p)
+            assert rc == 0, rc
+            e0.record(mgr)
+            if dist:
+                with torch.cuda.stream(mgr):
+                    dist.all_gather_into_tensor(spk_all, spk)
+                    dist.all_gather_into_tensor(bwe_all, bwe)
+            e1.record(mgr)
+            tick_log.append((t_s, (e0, e1), i))
+        else:
+            spk, bwe = host_records(now)
+            t0_ = time.perf_counter()
+            tabs = gather_tables(spk, bwe)
+            tick_log.append((t_s, (time.perf_counter() - t0_) * 1e3, tabs))
 
     hprof = [0.0, 0.0, 0.0] if os.environ.get("LKF_HOST_PROF") else None
     if args.host_io:  # pinned host output buffers for lkf_drain_run
@@ -511,7 +658,7 @@ def main():
                 assert eng.api["submit_dd_device"](eng.h, C.c_void_p(ddd[b].data_ptr()), n) == 0
         tc = time.perf_counter()
         eng.run(sp)
-        if speakers:  # Room.audioUpdateWorker's tick (ranking stays in HBM for the all-gather)
+        if speakers and not tick_on and not dry:  # Room.audioUpdateWorker's tick (ranking stays in HBM; N > 1: summary_tick)
             assert eng.api["speakers_enqueue"](eng.h, 1700000000 * 10**9 + int((b + 1) * args.batch_s * 1e9)) == 0
         if args.srtp:
             assert eng.api["protect"](eng.h, 1700000000 * 10**9 + int(b * args.batch_s * 1e9)) == 0
@@ -524,6 +671,9 @@ def main():
             drain_prev(1)
         if args.sync_each:
             eng.sync()
+        if tick_on:
+            for t_s in tick_times(b, args.batch_s, args.update_ms):
+                summary_tick(t_s)
         if hprof is not None:
             td = time.perf_counter()
             hprof[0] += tb - ta
@@ -532,12 +682,12 @@ def main():
 
     for b in range(args.warmup):
         step(b)
-    torch.cuda.synchronize(dev)
+    csync()
     eng.sync()
     warm_cum = eng.cumulative(reset=True)
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    csync()
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
@@ -547,7 +697,7 @@ def main():
     if hprof is not None:
         print("host ms/step (incl. warmup): queue_events %.4f submit %.4f run %.4f" %
               tuple(1e3 * x / nb for x in hprof), file=sys.stderr)
-    torch.cuda.synchronize(dev)
+    csync()
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
@@ -564,26 +714,87 @@ def main():
         assert eng.lib.lkf_protect_timing_window(C.c_void_p(eng.h), win, C.byref(pm)) == 0
         prot_ms = pm.value * args.steps / win
     coll = None
-    if dist:
-        # the one collective — per-room speaker summaries
-        # (Room.GetActiveSpeakers) all-gathered over RCCL every 400 ms of media;
-        # outside the timed forwarding region (not part of the throughput metric)
-        now = 1700000000 * 10**9 + int(nb * args.batch_s * 1e9)
-        sp = pkg.speakers_array(eng.api, eng.h, now)
-        width = max(len(p) for p in plan)
-        bwe = rooms_mod.fold_summaries(pkg.downtrack_summaries(eng.api, eng.h), plan[rank], rows=width)
-        torch.cuda.synchronize(dev)
-        tc0 = time.perf_counter()
-        table = rooms_mod.all_gather_speakers(dist, dev, sp, plan[rank])
-        btab = rooms_mod.all_gather_records(dist, dev, bwe)
-        tc1 = time.perf_counter()
-        coll = {"op": "all_gather (RCCL) of per-room speaker records + per-subscriber bandwidth records",
+    if dist or tick_on:
+        # the per-room speaker and per-subscriber bandwidth
+        # records, gathered every --update-ms of media inside the loop (above)
+        if not tick_log:  # (--update-ms 0: once, after the run)
+            summary_tick(nb * args.batch_s)
+        csync()
+        t_last, _, last = tick_log[-1]
+        timed = [x for x in tick_log if x[0] > args.warmup * args.batch_s + 1e-9]
+        match = None
+        if dev_ticks:
+            def ms_of(x):
+                return x[1] if x[2] is None else x[1][0].elapsed_time(x[1][1])
+            gms = [ms_of(x) for x in tick_log]
+            gms_timed = [ms_of(x) for x in timed]
+            table, btab = ring[last][2].cpu().numpy(), ring[last][3].cpu().numpy()
+            if t_last > (nb - 1) * args.batch_s:  # the last tick saw the final state: pack it on the host too
+                hs, hb = host_records(1700000000 * 10**9 + int(round(t_last * 1e9)))
+                match = bool(np.array_equal(table[rank], hs) and np.array_equal(btab[rank], hb))
+        else:
+            gms = [x[1] for x in tick_log]
+            gms_timed = [x[1] for x in timed]
+            table, btab = last
+        coll = {"op": "all_gather of per-room speaker records + per-subscriber bandwidth records (%s)" % (
+                    "RCCL" if backend == "nccl" else backend),
+                "path": ("device: lkf_room_summaries_enqueue packs the records in HBM on a side stream, RCCL "
+                         "all_gather_into_tensor there (no host wait in the loop)" if dev_ticks else
+                         "host: lkf_speakers + lkf_downtrack_summaries, packed and gathered from host memory"),
+                "update_ms": args.update_ms, "ticks": len(tick_log), "ticks_in_timed_region": len(timed),
+                "gather_ms_mean": round(float(np.mean(gms)), 4) if gms else None,
+                "gather_ms_per_step": round(float(np.sum(gms_timed)) / args.steps, 4),
                 "bytes_per_rank": int(table[0].nbytes + btab[0].nbytes),
-                "ms": round((tc1 - tc0) * 1e3, 3), "rooms_gathered": int(table.shape[0] * table.shape[1]),
+                "rooms_gathered": int(table.shape[0] * table.shape[1]),
                 "rooms_with_speakers": int((table[:, :, 0, 0] >= 0).sum()),
                 "subscribers_gathered": int((btab[:, :, :, 0] >= 0).sum()),
                 "subscribers_deficient": int((btab[:, :, :, 3] > 0).sum()),
-                "room_plan": "LPT bin packing by expected tuples (rooms.plan_room_shards)"}
+                "device_records_match_host": match,
+                "room_plan": "LPT bin packing by expected tuples (rooms.plan_room_shards)",
+                "note": "the gathers' time is reported here, apart from the metric; the timed loop includes "
+                        "their enqueue"}
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        # the GPU box gives one GPU a 16-CPU share (os.cpu_count() is the whole
+        # host); at N > 1 every rank runs its share at once (N x 16 threads on
+        # the node, the memory system shared as the GPUs' hosts would share it)
+        # and the rates add up; the single-thread sample runs on rank 0 alone
+        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cc = CONFIGS[args.config]
+        if dist:
+            dist.barrier()
+        v, secs, rooms, nbat, busy, neng = cpu_baseline(thr, sample_rooms=cc["sample"], config=args.config,
+                                                        ingress=args.ingress)
+        v_all, busy_min, busy_max = v, min(busy), max(busy)
+        if dist:
+            t = torch.tensor([v, -min(busy), max(busy)], dtype=torch.float64, device=cdev)
+            tsum = t.clone()
+            dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            v_all, busy_min, busy_max = float(tsum[0]), -float(t[1]), float(t[2])
+        v1 = secs1 = rooms1 = 0
+        if rank == 0:
+            v1, secs1, rooms1, _, _, _ = cpu_baseline(1, sample_rooms=cc["sample1"], config=args.config,
+                                                      ingress=args.ingress)
+        if dist:
+            dist.barrier()
+        used = max(1, min(thr, neng))
+        cpu = {"value": round(v_all, 1), "unit": "forwarded RTP pkts/s", "cores": used * world, "kind": "port",
+               "sample": "configs[%d] shape%s: %d rooms, 4 s of media (%d batches incl. the arrival tail), %d "
+                         "oracle engines (rooms%s) pulled by %d C++ threads (oracle/cpu_bench.cpp; %.1f s "
+                         "wall)%s; single thread: %d rooms, %.1f s wall" % (
+                             args.config - 1, " through Buffer.calc (orc_ingest)" if args.ingress else "", rooms,
+                             nbat, neng, " and, as DownTrackSpreader's parallel fan-out, their DownTracks"
+                             if neng > rooms else "", used, secs,
+                             (" on each of %d ranks at once (one 16-CPU share per GPU), rates summed" % world)
+                             if world > 1 else "", rooms1, secs1),
+               "single_thread_value": round(v1, 1), "host_nproc": os.cpu_count(), "cpu_model": cpu_model(),
+               "thread_busy_s": {"min": round(busy_min, 3), "max": round(busy_max, 3)}}
+        if world > 1:
+            cpu["per_rank_value"] = round(v, 1)
+        # thread_scaling_eff = the threads' rate over (threads x the single-thread rate), both measured
+        cpu["thread_scaling_eff"] = round(v_all / (v1 * used * world), 3) if v1 else None
 
     parity = None
     if not args.no_parity and not args.srtp and not args.alloc_per_step:
@@ -592,7 +803,7 @@ def main():
         parity = parity_gate(eng, pkg, args.config, plan[rank], nb, args.batch_s, args.ingress, trace, thr,
                              warm_cum, cum)
         if dist:
-            ok = torch.tensor([1.0 if parity["parity"] else 0.0], dtype=torch.float64, device=dev)
+            ok = torch.tensor([1.0 if parity["parity"] else 0.0], dtype=torch.float64, device=cdev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             parity["parity_all_ranks"] = bool(ok.item() > 0)
     fwd = cum["forwarded"]
@@ -606,7 +817,7 @@ def main():
     decide_bytes = 64 * steps_pkts + 32 * fwd + 256 * trace.ndts * args.steps
     emit_bytes = payload_in + cum["out_bytes"] + 40 * fwd
     if dist:
-        t = torch.tensor([elapsed, float(fwd), float(algo), tot_ms, emit_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, float(fwd), float(algo), tot_ms, emit_ms], dtype=torch.float64, device=cdev)
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -649,30 +860,6 @@ def main():
                 traffic_src = os.path.relpath(path, ROOT)
                 break
         pipe_ach = algo / (tot_ms / 1e3) / 1e9 if tot_ms else 0.0
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            # the GPU box gives one GPU a 16-CPU share (os.cpu_count() is the whole host)
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cc = CONFIGS[args.config]
-            v, secs, rooms, nbat, busy, neng = cpu_baseline(thr, sample_rooms=cc["sample"], config=args.config,
-                                                            ingress=args.ingress)
-            v1, secs1, rooms1, _, _, _ = cpu_baseline(1, sample_rooms=cc["sample1"], config=args.config,
-                                                      ingress=args.ingress)
-            used = max(1, min(thr, neng))
-            cpu = {"value": round(v, 1), "unit": "forwarded RTP pkts/s", "cores": used, "kind": "port",
-                   "sample": "configs[%d] shape%s: %d rooms, 4 s of media (%d batches incl. the arrival tail), %d "
-                             "oracle engines (rooms%s) pulled by %d C++ threads (oracle/cpu_bench.cpp; %.1f s "
-                             "wall); single thread: %d rooms, %.1f s wall" % (
-                                 args.config - 1, " through Buffer.calc (orc_ingest)" if args.ingress else "", rooms,
-                                 nbat, neng, " and, as DownTrackSpreader's parallel fan-out, their DownTracks"
-                                 if neng > rooms else "", used, secs, rooms1, secs1),
-                   "single_thread_value": round(v1, 1), "host_nproc": os.cpu_count(), "cpu_model": cpu_model(),
-                   "thread_busy_s": {"min": round(min(busy), 3), "max": round(max(busy), 3)}}
-            # one thread per core of the box's 16-CPU share per GPU; rooms shard
-            # with no shared state, so the rate scales with threads up to the
-            # memory system (thread_scaling_eff = the 16-thread rate over 16 x
-            # the single-thread rate, both measured)
-            cpu["thread_scaling_eff"] = round(v / (v1 * used), 3) if v1 else None
         line = {
             "metric": "forwarded RTP pkts/sec per GPU & node (bit-exact) + % HBM roofline",
             "value": round(fwd_all / elapsed, 1),
@@ -713,7 +900,12 @@ def main():
             "collective": coll,
             "tuples_per_step": cum["tuples"] // args.steps,
             "forwarded_per_step": fwd // args.steps,
+            "forwarded_total": int(fwd_all),
         }
+        if dry:
+            line["dry_run"] = True
+            line["note"] = ("launcher rehearsal: the CPU oracle stood in for the engine (tests/dryrun_engine.py); "
+                            "not a measurement")
         if args.host_io:  # PCIe-inclusive deployment shape (never the headline value)
             h2d = sum(meta[b][0] * 64 + meta[b][1] for b in range(args.warmup, nb))
             line["host_io"] = {"h2d_bytes_per_step": h2d // args.steps,

@@ -912,6 +912,23 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
  * tick inside a pipelined loop): it runs after the last enqueued ingest and
  * stays in HBM for the summary all-gather. */
 int lkf_speakers_enqueue(lkf_engine *e, int64_t now_ns);
+/* The room manager's periodic summary (Room.audioUpdateWorker's tick every
+ * UpdateInterval, room.go:1278-1316) without a host wait:
+ * the ranking at now_ns and every active DownTrack's sendingPacket totals
+ * (bytesSent / packets, downtrack.go:1930-1959) with lastAllocation.IsDeficient,
+ * packed into the fixed-shape records a cross-GPU all-gather moves, in
+ * caller device memory:
+ *   spk int32 [rows][k][3]: (participant, float32 bits of the quantised level,
+ *       active) ranked as lkf_speakers; participant -1 pads (k <= 64);
+ *   bwe int64 [rows][s][5]: (subscriber, packets, bytes, deficient DownTracks,
+ *       DownTracks) per subscriber of the room, subscribers ascending (the
+ *       first s); subscriber -1 pads;
+ * row r is room room_ids[r] (ascending; every room of the engine's tracks
+ * must be listed).  Enqueued after the last enqueued ingest and decide; the
+ * writes run on `stream` (a hipStream_t), which then orders the caller's
+ * collective; the engine's next ranking and decide wait for them. */
+int lkf_room_summaries_enqueue(lkf_engine *e, int64_t now_ns, const uint32_t *room_ids, uint32_t rows, int32_t *spk,
+                               uint32_t k, int64_t *bwe, uint32_t s, void *stream);
 
 /* ---- introspection ------------------------------------------------------ */
 /* Duration of the last batch's decide kernel, emit kernel and whole batch, ms. */

@@ -177,6 +177,17 @@ def speakers_array(api, h, now_ns):
         cap = n.value
 
 
+def room_summaries_enqueue(api, h, now_ns, room_ids, spk_ptr, k, bwe_ptr, s, stream_ptr):
+    """lkf_room_summaries_enqueue: the speaker and bandwidth records of the
+    rooms `room_ids` (ascending) packed into device buffers spk int32
+    [rows, k, 3] / bwe int64 [rows, s, 5] on the caller stream `stream_ptr`,
+    without a host wait (rooms.pack_speakers / rooms.fold_summaries layout)."""
+    ids = np.ascontiguousarray(np.asarray(room_ids, dtype=np.uint32))
+    rc = api["room_summaries_enqueue"](h, now_ns, ids.ctypes.data, len(ids), spk_ptr, k, bwe_ptr, s, stream_ptr)
+    if rc != 0:
+        raise EngineError("room_summaries_enqueue rc=%d" % rc)
+
+
 def downtrack_summaries(api, h):
     """lkf_downtrack_summaries: one DT_SUMMARY_DTYPE row per DownTrack handle."""
     n = C.c_uint32()

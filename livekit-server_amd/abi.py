@@ -448,6 +448,10 @@ def bind_engine_api(lib, prefix):
         api["submit_dd_device"] = _bind(lib, prefix + "submit_dd_device", C.c_int, [e, C.c_void_p, C.c_uint32])
     if hasattr(lib, prefix + "speakers_enqueue"):
         api["speakers_enqueue"] = _bind(lib, prefix + "speakers_enqueue", C.c_int, [e, C.c_int64])
+    if hasattr(lib, prefix + "room_summaries_enqueue"):  # engine only (device records)
+        api["room_summaries_enqueue"] = _bind(lib, prefix + "room_summaries_enqueue", C.c_int,
+                                              [e, C.c_int64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                               C.c_void_p, C.c_uint32, C.c_void_p])
     api["stream_stats_get"] = _bind(lib, prefix + "stream_stats_get", C.c_int, [e, C.c_int32, P(lkf_stream_stats)])
     api["ingest_nacks"] = _bind(lib, prefix + "ingest_nacks", C.c_int,
                                 [e, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32)])

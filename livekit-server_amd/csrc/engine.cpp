@@ -26,6 +26,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/lkfwd.h"
@@ -223,6 +224,7 @@ struct lkf_engine {
   // on (tables, schedule, DD / tracker allocations); a context re-captures
   // its graphs when its epoch is older
   uint64_t epoch = 1;
+  uint64_t topoGen = 0;  // bumped by every topology change (tracks, DownTracks, streams, removals, rooms)
   bool useGraph = true;  // LKF_GRAPH=0: the stages as direct launches (A/B)
   bool debugDD = false;  // LKF_DEBUG_DD=1: report the DD cursors (diagnostic)
 
@@ -443,6 +445,17 @@ struct lkf_engine {
   lkf_speaker *dSpkSlots = nullptr;
   uint32_t *dSpkCounts = nullptr;
   size_t spkCap = 0;
+  std::vector<uint32_t> spkRoomIds;  // host copy of dRoomId
+  // lkf_room_summaries_enqueue: the records' layout for (rows, k, s) and the
+  // topology it was built for; two events order the caller's stream after the
+  // packs (ingest and decide streams)
+  std::vector<uint32_t> rsRooms;
+  uint32_t rsK = 0, rsS = 0;
+  uint64_t rsGen = ~0ull;
+  int32_t *dRsRowEng = nullptr;
+  uint32_t *dRsSlotOff = nullptr, *dRsSlotDts = nullptr;
+  int64_t *dRsSlotSub = nullptr;
+  hipEvent_t rsSpk = nullptr, rsDec = nullptr;
   // device -> host copies refused by the range check (CHKRANGE) since the last
   // lkf_debug_check of this engine (lkf_debug_check folds them in)
   std::atomic<uint64_t> rangeViolations{0};
@@ -678,6 +691,9 @@ static int ensure_dd(lkf_engine *e) {
     HIPCHK(dalloc(&x.dDDPkt, c.max_batch_pkts), "alloc dd pkts");
     HIPCHK(dalloc(&x.dDDArena, e->ddArenaCap), "alloc dd arena");
     HIPCHK(dalloc(&x.dDDUsed, 2), "alloc dd cursor");
+    // (zeroed here too: k_layer_index zeroes it per batch, but recycled memory
+    // must never be read as a cursor; DESIGN.md §6 round-5 cursor report)
+    HIPCHK(hipMemset(x.dDDUsed, 0, 2 * sizeof(uint64_t)), "dd cursor reset");
     HIPCHK(dalloc(&x.dDDSpill, e->ddSpillCap), "alloc dd spill");
   }
   e->ddAlloc = true;
@@ -688,6 +704,7 @@ static int ensure_dd(lkf_engine *e) {
 static int flush_topology(lkf_engine *e) {
   if (e->pendTracks.empty() && e->pendDTs.empty() && e->pendStreams.empty()) return LKF_OK;
   e->epoch++;  // the stage graphs read the topology's sizes
+  e->topoGen++;
   int rc = drain_streams(e);
   if (rc) return rc;
   rc = ensure_dd(e);
@@ -1100,7 +1117,7 @@ void lkf_destroy(lkf_engine *e) {
                   e->dTwcc, e->dBkt, e->dBktTag, e->dBktOwner, e->dBktRing, e->dBktStream, e->dBktSn,
                   e->dPos, e->dIPartA, e->dIPartB, e->dITotal, e->dITRuns, e->dIErr,
                   e->dRoomPartOff, e->dPartId, e->dPartMicOff, e->dMics, e->dRoomId, e->dSpkSlots,
-                  e->dSpkCounts, e->dNack,
+                  e->dSpkCounts, e->dNack, e->dRsRowEng, e->dRsSlotOff, e->dRsSlotDts, e->dRsSlotSub,
                   e->dNackRecPos, e->dNackPairPos, e->dNackTot, e->dNackOut, e->dNackPairsOut, e->dNackPartA,
                   e->dNackPartB,
                   e->dSS, e->dSSGap, e->dSSRing, e->dSSList, e->dSSGroups, e->dSeqDD, e->dSeqDDIdx,
@@ -1151,6 +1168,8 @@ void lkf_destroy(lkf_engine *e) {
   if (e->bounce) (void)hipHostFree(e->bounce);
   if (e->inEv) (void)hipEventDestroy(e->inEv);
   if (e->bktEv) (void)hipEventDestroy(e->bktEv);
+  for (hipEvent_t ev : {e->rsSpk, e->rsDec})
+    if (ev) (void)hipEventDestroy(ev);
   if (e->sideFork) (void)hipEventDestroy(e->sideFork);
   for (int i = 0; i < 2; i++) {
     if (e->sideDone[i]) (void)hipEventDestroy(e->sideDone[i]);
@@ -1294,6 +1313,7 @@ int lkf_remove_downtrack(lkf_engine *e, int32_t dt) {
   rc = drain_streams(e);
   if (rc) return rc;
   e->active[dt] = 0;
+  e->topoGen++;
   uint8_t zero = 0;
   HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(e->dDTs + dt) + offsetof(DevDT, active), &zero, 1,
                    hipMemcpyHostToDevice),
@@ -1314,6 +1334,7 @@ int lkf_remove_track(lkf_engine *e, int32_t track) {
   for (size_t d = 0; d < e->dtp.size(); d++)  // closeTracks: every DownTrack of the receiver
     if (e->dtp[d].track == track && e->active[d]) {
       e->active[d] = 0;
+      e->topoGen++;
       HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(e->dDTs + d) + offsetof(DevDT, active), &zero, 1,
                        hipMemcpyHostToDevice),
              "remove copy");
@@ -4003,6 +4024,8 @@ static int rebuild_speakers(lkf_engine *e) {
   roomOff.push_back(uint32_t(partId.size()));
   partMicOff.push_back(uint32_t(mics.size()));
   e->nRooms = uint32_t(roomId.size());
+  e->spkRoomIds = roomId;
+  e->topoGen++;
   uint32_t **bufs[] = {&e->dRoomPartOff, &e->dPartId, &e->dPartMicOff, &e->dMics, &e->dRoomId};
   const std::vector<uint32_t> *src[] = {&roomOff, &partId, &partMicOff, &mics, &roomId};
   for (int i = 0; i < 5; i++) {
@@ -4101,6 +4124,157 @@ int lkf_speakers(lkf_engine *e, int64_t now_ns, lkf_speaker *out, uint32_t cap, 
   return LKF_OK;
 }
 
+// The room manager's periodic summary without a host wait (see lkfwd.h).
+// The ranking and its pack run on the ingest stream after the last enqueued
+// ingest; the totals' pack on the decide stream after the last enqueued
+// decide (the DownTracks' sendingPacket totals); the caller's stream waits
+// for both.  The engine never waits for the caller: the caller keeps `spk` /
+// `bwe` unread by earlier work of its own until this tick's writes land
+// (bench.py: a ring of buffers, each reused after its gather's event).
+int lkf_room_summaries_enqueue(lkf_engine *e, int64_t now_ns, const uint32_t *room_ids, uint32_t rows, int32_t *spk,
+                               uint32_t k, int64_t *bwe, uint32_t s, void *stream) {
+  if (!e || (rows && !room_ids) || !spk || !bwe || k == 0 || k > 64 || s == 0) return LKF_EINVAL;
+  for (uint32_t r = 1; r < rows; r++)
+    if (room_ids[r] <= room_ids[r - 1]) return LKF_EINVAL;  // ascending, distinct
+  int rc = flush_topology(e);
+  if (rc) return rc;
+  if (e->spkDirty) {
+    rc = drain_streams(e);
+    if (rc) return rc;
+    rc = rebuild_speakers(e);
+    if (rc) return rc;
+  }
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (!e->rsSpk) {
+    HIPCHK(hipEventCreateWithFlags(&e->rsSpk, hipEventDisableTiming), "event");
+    HIPCHK(hipEventCreateWithFlags(&e->rsDec, hipEventDisableTiming), "event");
+  }
+  const uint32_t nd = uint32_t(e->dtp.size());
+  if (rows != e->rsRooms.size() || !std::equal(room_ids, room_ids + rows, e->rsRooms.begin()) || k != e->rsK ||
+      s != e->rsS || e->topoGen != e->rsGen) {
+    std::vector<uint32_t> rooms(room_ids, room_ids + rows);
+    auto rowOf = [&](uint32_t room) -> int32_t {
+      auto it = std::lower_bound(rooms.begin(), rooms.end(), room);
+      return it != rooms.end() && *it == room ? int32_t(it - rooms.begin()) : -1;
+    };
+    std::vector<int32_t> rowEng(std::max<uint32_t>(rows, 1), -1);
+    for (uint32_t r = 0; r < e->nRooms; r++) {
+      const int32_t row = rowOf(e->spkRoomIds[r]);
+      if (row < 0) {
+        e->err = "room_summaries: a room with microphones is not among room_ids";
+        return LKF_EINVAL;
+      }
+      rowEng[row] = int32_t(r);
+    }
+    // active DownTracks by (row, subscriber, handle); a room's first s subscribers get slots
+    std::vector<std::tuple<int32_t, uint32_t, uint32_t>> by;
+    for (uint32_t d = 0; d < nd; d++) {
+      if (!e->active[d]) continue;
+      const int32_t row = rowOf(e->tracks[e->dtp[d].track].room);
+      if (row < 0) {
+        e->err = "room_summaries: a DownTrack's room is not among room_ids";
+        return LKF_EINVAL;
+      }
+      by.emplace_back(row, e->dtp[d].subscriber, d);
+    }
+    std::sort(by.begin(), by.end());
+    const size_t nslots = size_t(std::max<uint32_t>(rows, 1)) * s;
+    std::vector<uint32_t> off(nslots + 1, 0), dts;
+    std::vector<int64_t> sub(nslots, -1);
+    std::vector<uint32_t> cnt(nslots, 0);
+    for (size_t i = 0; i < by.size();) {
+      const int32_t row = std::get<0>(by[i]);
+      uint32_t pos = 0;
+      while (i < by.size() && std::get<0>(by[i]) == row) {
+        const uint32_t su = std::get<1>(by[i]);
+        size_t j = i;
+        while (j < by.size() && std::get<0>(by[j]) == row && std::get<1>(by[j]) == su) j++;
+        if (pos < s) {
+          const size_t slot = size_t(row) * s + pos;
+          sub[slot] = su;
+          cnt[slot] = uint32_t(j - i);
+        }
+        pos++;
+        i = j;
+      }
+    }
+    for (size_t q = 0; q < nslots; q++) off[q + 1] = off[q] + cnt[q];
+    dts.resize(std::max<uint32_t>(off[nslots], 1));
+    {
+      std::vector<uint32_t> fillp(off.begin(), off.end() - 1);
+      size_t i = 0;
+      while (i < by.size()) {
+        const int32_t row = std::get<0>(by[i]);
+        uint32_t pos = 0;
+        while (i < by.size() && std::get<0>(by[i]) == row) {
+          const uint32_t su = std::get<1>(by[i]);
+          while (i < by.size() && std::get<0>(by[i]) == row && std::get<1>(by[i]) == su) {
+            if (pos < s) dts[fillp[size_t(row) * s + pos]++] = std::get<2>(by[i]);
+            i++;
+          }
+          pos++;
+        }
+      }
+    }
+    HIPCHK(hipStreamSynchronize(e->ingS), "sync ingest stream");  // (a queued pack may read the old layout)
+    HIPCHK(hipStreamSynchronize(e->decS), "sync decide stream");
+    for (void *p : {static_cast<void *>(e->dRsRowEng), static_cast<void *>(e->dRsSlotOff),
+                    static_cast<void *>(e->dRsSlotDts), static_cast<void *>(e->dRsSlotSub)})
+      if (p) HIPCHK(dfree(p), "free");
+    HIPCHK(dalloc(&e->dRsRowEng, rowEng.size()), "alloc");
+    HIPCHK(dalloc(&e->dRsSlotOff, off.size()), "alloc");
+    HIPCHK(dalloc(&e->dRsSlotDts, dts.size()), "alloc");
+    HIPCHK(dalloc(&e->dRsSlotSub, sub.size()), "alloc");
+    HIPCHK(hipMemcpy(e->dRsRowEng, rowEng.data(), rowEng.size() * 4, hipMemcpyHostToDevice), "copy");
+    HIPCHK(hipMemcpy(e->dRsSlotOff, off.data(), off.size() * 4, hipMemcpyHostToDevice), "copy");
+    HIPCHK(hipMemcpy(e->dRsSlotDts, dts.data(), dts.size() * 4, hipMemcpyHostToDevice), "copy");
+    HIPCHK(hipMemcpy(e->dRsSlotSub, sub.data(), sub.size() * 8, hipMemcpyHostToDevice), "copy");
+    e->rsRooms = rooms;
+    e->rsK = k;
+    e->rsS = s;
+    e->rsGen = e->topoGen;
+  }
+  hipStream_t cs = reinterpret_cast<hipStream_t>(stream);
+  if (e->nRooms) {
+    SpeakersLaunch a;
+    a.nrooms = e->nRooms;
+    a.roomPartOff = e->dRoomPartOff;
+    a.partId = e->dPartId;
+    a.partMicOff = e->dPartMicOff;
+    a.mics = e->dMics;
+    a.roomId = e->dRoomId;
+    a.streams = e->dStreams;
+    a.hot = e->dStreamHot;
+    a.nowNs = now_ns;
+    a.slots = e->dSpkSlots;
+    a.counts = e->dSpkCounts;
+    HIPCHK(launch_speakers(e->ingS, a), "speakers");
+  }
+  RoomPackLaunch p;
+  p.rows = rows;
+  p.k = k;
+  p.s = s;
+  p.rowEng = e->dRsRowEng;
+  p.slots = e->dSpkSlots;
+  p.counts = e->dSpkCounts;
+  p.slotOff = e->dRsSlotOff;
+  p.slotDts = e->dRsSlotDts;
+  p.slotSub = e->dRsSlotSub;
+  p.cum = e->dDTCum;
+  p.spk = spk;
+  p.bwe = bwe;
+  // the ranking's pack right behind the ranking (ingest stream), the totals'
+  // right behind the last enqueued decide: each reads its source before the
+  // next ingest / decide on its stream can change it, and nothing of the
+  // engine waits for the caller
+  HIPCHK(launch_room_pack(e->ingS, e->decS, p), "room pack");
+  HIPCHK(hipEventRecord(e->rsSpk, e->ingS), "event");
+  HIPCHK(hipEventRecord(e->rsDec, e->decS), "event");
+  HIPCHK(hipStreamWaitEvent(cs, e->rsSpk, 0), "wait");
+  HIPCHK(hipStreamWaitEvent(cs, e->rsDec, 0), "wait");
+  return LKF_OK;
+}
+
 // Not part of include/lkfwd.h: the bounds-check record of a checked build
 // (-DLKF_CHECKED=1, liblkfwd_checked.so): {violations, first site, index,
 // capacity}; LKF_ENODEV from a product build.
@@ -4138,6 +4312,24 @@ int lkf_debug_check(lkf_engine *e, uint64_t out[4], int reset) {
     return LKF_OK;
   }
   return r == hipSuccess ? LKF_OK : LKF_ENODEV;
+}
+
+// Not part of include/lkfwd.h: every batch context's DD arena and spill bump
+// cursors (out[2c], out[2c+1]) after a drain, and the arena's capacity
+// (out[6]); LKF_EINVAL before the DD tables exist.  tests/test_dd_recapture_gpu.py
+// checks them after graph re-captures forced under queued runs.
+int lkf_debug_dd_cursors(lkf_engine *e, uint64_t out[7]) {
+  if (!e || !out || !e->ddAlloc) return LKF_EINVAL;
+  int rc = drain_streams(e);
+  if (rc) return rc;
+  for (int c = 0; c < lkf_engine::kCtx; c++) {
+    uint64_t u[2] = {0, 0};
+    D2H(u, e->ctx[c].dDDUsed, sizeof(u), "dd cursor copy");
+    out[2 * c] = u[0];
+    out[2 * c + 1] = u[1] & 0xffffffffu;
+  }
+  out[6] = e->ddArenaCap;
+  return LKF_OK;
 }
 
 // Not part of include/lkfwd.h: a DD DownTrack's selector state for debugging

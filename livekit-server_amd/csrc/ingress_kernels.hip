@@ -2228,6 +2228,52 @@ __global__ void __launch_bounds__(64) k_speakers(const u32 *__restrict__ roomPar
 }
 
 // ---------------------------------------------------------------------------
+// k_spk_pack / k_bwe_pack: the summary records the room manager all-gathers every
+// UpdateInterval (Room.audioUpdateWorker room.go:1278-1316),
+// packed in place from the ranking slots and the DownTracks' sendingPacket
+// totals: spk row entries (participant, float bits of the level, active) and
+// bwe slots (subscriber, packets, bytes, deficient DownTracks, DownTracks),
+// one thread per entry.  A slot's DownTracks are a host-built list (ascending
+// subscribers within a room, as rooms.fold_summaries orders them), so the sums
+// are plain loops: no atomics, the same bits every tick.
+// ---------------------------------------------------------------------------
+__global__ void k_spk_pack(RoomPackLaunch a) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.rows * a.k) return;
+  const u32 row = i / a.k, j = i % a.k;
+  const i32 r = a.rowEng[row];
+  i32 v0 = -1, v1 = 0, v2 = 0;
+  if (r >= 0 && j < a.counts[r]) {
+    const lkf_speaker sp = a.slots[size_t(r) * 64 + j];
+    v0 = i32(sp.participant);
+    v1 = __float_as_int(sp.level);
+    v2 = i32(sp.active);
+  }
+  a.spk[size_t(i) * 3] = v0;
+  a.spk[size_t(i) * 3 + 1] = v1;
+  a.spk[size_t(i) * 3 + 2] = v2;
+}
+
+__global__ void k_bwe_pack(RoomPackLaunch a) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.rows * a.s) return;
+  const u32 b = a.slotOff[i], e = a.slotOff[i + 1];
+  u64 pk = 0, by = 0, def = 0;
+  for (u32 q = b; q < e; q++) {
+    const DTCum c = a.cum[a.slotDts[q]];
+    pk += c.packets;
+    by += c.bytes;
+    def += (c.flags & F_DEFICIENT) ? 1u : 0u;
+  }
+  i64 *o = a.bwe + size_t(i) * 5;
+  o[0] = b == e ? -1 : a.slotSub[i];
+  o[1] = i64(pk);
+  o[2] = i64(by);
+  o[3] = i64(def);
+  o[4] = i64(e - b);
+}
+
+// ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
 static u32 nblk(u64 n, u32 t) { return u32((n + t - 1) / t); }
@@ -2486,6 +2532,12 @@ hipError_t launch_nack_compact(hipStream_t st, u32 n, const lkf_raw_pkt *raws, c
   if (r != hipSuccess) return r;
   hipLaunchKernelGGL(k_nack_compact, dim3(nblk(n, 256)), dim3(256), 0, st, n, raws, streams, info, pairOff, pairs,
                      recPos, pairPos, outRecs, outPairs);
+  return hipGetLastError();
+}
+
+hipError_t launch_room_pack(hipStream_t spkStream, hipStream_t bweStream, const RoomPackLaunch &a) {
+  if (a.rows * a.k) hipLaunchKernelGGL(k_spk_pack, dim3(nblk(u64(a.rows) * a.k, 256)), dim3(256), 0, spkStream, a);
+  if (a.rows * a.s) hipLaunchKernelGGL(k_bwe_pack, dim3(nblk(u64(a.rows) * a.s, 256)), dim3(256), 0, bweStream, a);
   return hipGetLastError();
 }
 

@@ -218,6 +218,22 @@ struct SpeakersLaunch {
 hipError_t launch_ingest(hipStream_t s, const IngestLaunch &a, hipStream_t side, hipEvent_t sideFork,
                          hipEvent_t sideDone, bool *sideUsed);
 hipError_t launch_speakers(hipStream_t s, const SpeakersLaunch &a);
+// The room manager's fixed-shape summary records (lkf_room_summaries_enqueue):
+// row r of spk [rows, k, 3] = the ranking slots of engine room rowEng[r];
+// slot i of bwe [rows, s, 5] = the DownTracks slotDts[slotOff[i] .. slotOff[i+1]).
+struct RoomPackLaunch {
+  uint32_t rows, k, s;
+  const int32_t *rowEng;  // row -> engine speaker room (-1: no microphones)
+  const lkf_speaker *slots;
+  const uint32_t *counts;
+  const uint32_t *slotOff, *slotDts;
+  const int64_t *slotSub;  // subscriber of a slot (-1 padding)
+  const DTCum *cum;
+  int32_t *spk;
+  int64_t *bwe;
+};
+// (the ranking's pack on spkStream, the totals' pack on bweStream)
+hipError_t launch_room_pack(hipStream_t spkStream, hipStream_t bweStream, const RoomPackLaunch &a);
 hipError_t launch_decide(hipStream_t s, const DecideLaunch &a);
 hipError_t launch_layer_index(hipStream_t s, const RunDesc *desc, const uint32_t *tBegin, const uint32_t *tEnd,
                               uint32_t ntracks, uint32_t stride, uint32_t *list, uint32_t *before, uint32_t *cnt,
