@@ -777,23 +777,70 @@ __device__ __forceinline__ void c_put(DDState &d, u64 e, u32 sd) {
   const int bp = int(off & 31) * 2;
   d.masks[off >> 5] = (d.masks[off >> 5] & ~(u64(3) << bp)) | (u64(sd & 3) << bp);
 }
+// ---- FrameChain.expectFrames as a set (round 6) ---------------------------------
+// A chain waits only on frames ExpectDecision accepted: not older than
+// cLast - 255 when registered, and gone (missing: the chain breaks) once older
+// than cLast - 256; below cLast + 256 in every case but one: a packet whose
+// frame number jumped ahead of cLast may register one frame beyond, and its own
+// add then moves cLast past it.  So each chain keeps a ring of 512 bits, bit
+// e % 512 for frame e in [cLast - 256, cLast + 256), and one frame beyond
+// (exp[c][8], expFar[c]).  A broken chain's set is never read again (the
+// reference skips its callbacks and clears it with the chain-intact frame that
+// un-breaks it), so it is cleared when the chain breaks.
+constexpr u64 kExpHalf = 256;
+__device__ __forceinline__ bool x_in_win(const DDState &d, u64 e) {
+  return e + kExpHalf >= d.cLast && e < d.cLast + kExpHalf;
+}
+__device__ __forceinline__ bool x_has(const DDState &d, int c, u64 e) {
+  if (x_in_win(d, e)) return (d.exp[c][(e >> 6) & 7] >> (e & 63)) & 1u;
+  return d.expFar[c] && d.exp[c][8] == e;
+}
+__device__ __forceinline__ void x_del(DDState &d, int c, u64 e) {
+  if (x_in_win(d, e))
+    d.exp[c][(e >> 6) & 7] &= ~(u64(1) << (e & 63));
+  else if (d.expFar[c] && d.exp[c][8] == e)
+    d.expFar[c] = 0;
+}
+__device__ __forceinline__ void x_clear(DDState &d, int c) {
+  for (int w = 0; w < kDDExpWords; w++) d.exp[c][w] = 0;
+  d.expFar[c] = 0;
+}
+__device__ __forceinline__ bool x_any(const DDState &d, int c) {
+  u64 o = 0;
+  for (int w = 0; w < kDDExpWords; w++) o |= d.exp[c][w];
+  return o != 0 || d.expFar[c];
+}
+// any waited-on frame in [a, b) (frames outside the ring's window are not in it)
+__device__ inline bool x_any_frames(const DDState &d, int c, u64 a, u64 b) {
+  bool hit = d.expFar[c] && d.exp[c][8] >= a && d.exp[c][8] < b;
+  const u64 lo = d.cLast >= kExpHalf ? d.cLast - kExpHalf : 0, hi = d.cLast + kExpHalf;
+  a = a > lo ? a : lo;
+  b = b < hi ? b : hi;
+  while (!hit && a < b) {
+    const u32 bit = u32(a & 63);
+    const u64 n = (b - a) < u64(64 - bit) ? (b - a) : u64(64 - bit);
+    const u64 m = (n >= 64 ? ~u64(0) : ((u64(1) << n) - 1)) << bit;
+    hit = (d.exp[c][(a >> 6) & 7] & m) != 0;
+    a += n;
+  }
+  return hit;
+}
+__device__ __forceinline__ u32 x_count(const DDState &d, int c) {
+  u32 n = d.expFar[c] ? 1u : 0u;
+  for (int w = 0; w < kDDExpWords; w++) n += u32(__popcll(d.exp[c][w]));
+  return n;
+}
+
 // callbacks of frame e firing with decision sd (see the header comment)
 __device__ inline void c_fire(DDState &d, u64 e, u32 sd) {
   for (int c = 0; c < d.numChains; c++) {
     if ((d.chBroken >> c) & 1) continue;
-    bool hit = false;
-    int n = d.expCount[c];
-    for (int i = 0; i < n;) {
-      if (d.exp[c][i] == e) {
-        hit = true;
-        d.exp[c][i] = d.exp[c][n - 1];
-        n--;
-      } else {
-        i++;
-      }
+    if (!x_has(d, c, e)) continue;
+    x_del(d, c, e);
+    if (sd != SD_FORWARDED) {
+      d.chBroken |= 1u << c;
+      x_clear(d, c);
     }
-    d.expCount[c] = u8(n);
-    if (hit && sd != SD_FORWARDED) d.chBroken |= 1u << c;
   }
 }
 __device__ __forceinline__ void c_set(DDState &d, u64 e, u32 sd) {
@@ -842,30 +889,57 @@ __device__ inline void c_add(DDState &d, u64 entity, u32 sd) {
       if (c_get(d, ms + k) == SD_UNKNOWN) c_set(d, ms + k, SD_MISSING);
   }
   c_set(d, entity, sd);
-  d.cLast = entity;
-  // frames waited on that aged out of the window: missing
-  for (int c = 0; c < d.numChains; c++)
-    for (int i = 0; i < d.expCount[c];) {
-      const u64 e = d.exp[c][i];
-      if (e + kEntries < d.cLast) {
-        c_fire(d, e, SD_MISSING);
-        if (i < d.expCount[c] && d.exp[c][i] == e) i++;  // broken chain keeps its set
+  const u64 l0 = d.cLast;
+  // frames waited on that aged out of the window (e + 256 < cLast, i.e. the
+  // frames [l0 - 256, entity - 256)): missing, which breaks the chain; then
+  // the ring follows cLast and takes the frame registered beyond it
+  const u64 a = l0 >= kExpHalf ? l0 - kExpHalf : 0, b = entity >= kExpHalf ? entity - kExpHalf : 0;
+  for (int c = 0; c < d.numChains; c++) {
+    if ((d.chBroken >> c) & 1) continue;
+    bool hit = false;
+    if (b > a) {
+      if (b - a >= 2 * kExpHalf) {
+        for (int w = 0; w < kDDExpWords; w++) hit = hit || d.exp[c][w] != 0;
       } else {
-        i++;
+        u64 x = a;
+        while (!hit && x < b) {
+          const u32 bit = u32(x & 63);
+          const u64 n = (b - x) < u64(64 - bit) ? (b - x) : u64(64 - bit);
+          const u64 m = (n >= 64 ? ~u64(0) : ((u64(1) << n) - 1)) << bit;
+          hit = (d.exp[c][(x >> 6) & 7] & m) != 0;
+          x += n;
+        }
       }
+    }
+    if (hit) {
+      d.chBroken |= 1u << c;
+      x_clear(d, c);
+    }
+  }
+  d.cLast = entity;
+  for (int c = 0; c < d.numChains; c++)
+    if (d.expFar[c] && x_in_win(d, d.exp[c][8])) {
+      const u64 e = d.exp[c][8];
+      d.exp[c][(e >> 6) & 7] |= u64(1) << (e & 63);
+      d.expFar[c] = 0;
     }
 }
 // ExpectDecision :96-110 + the chain's append
 __device__ inline bool c_expect(DDState &d, int c, u64 e, bool &overflow) {
   if (!(d.flags & DS_CACHE_INIT) || e < d.cBase) return false;
   if (e < d.cLast && d.cLast - e >= kEntries) return false;
-  for (int i = 0; i < d.expCount[c]; i++)
-    if (d.exp[c][i] == e) return true;
-  if (d.expCount[c] >= kDDExpect) {
+  if (x_in_win(d, e)) {
+    d.exp[c][(e >> 6) & 7] |= u64(1) << (e & 63);
+    return true;
+  }
+  // beyond the ring (this packet's frame number jumped ahead): one such frame
+  // per chain until the packet's add moves cLast past it
+  if (d.expFar[c] && d.exp[c][8] != e) {
     overflow = true;
     return true;
   }
-  d.exp[c][d.expCount[c]++] = e;
+  d.exp[c][8] = e;
+  d.expFar[c] = 1;
   return true;
 }
 
@@ -876,7 +950,7 @@ __device__ inline void chain_on_frame(DDState &d, int c, u64 efn, const DDPkt &p
   const u32 diff = dd_chain_diff(p, c);
   if (diff == 0) {
     d.chBroken &= ~(1u << c);
-    d.expCount[c] = 0;
+    x_clear(d, c);
     return;
   }
   if ((d.chBroken >> c) & 1) return;
@@ -900,7 +974,7 @@ __device__ inline void update_structure(DDState &d, const DDStruct &s, u8 slot, 
   d.chBroken = s.numChains >= 32 ? ~0u : (1u << s.numChains) - 1;
   d.chActive = 0;
   d.chUpdating = 0;
-  for (int c = 0; c < kDDChains; c++) d.expCount[c] = 0;
+  for (int c = 0; c < kDDChains; c++) x_clear(d, c);
   d.numTargets = s.numDT;
   d.dtActive = 0;
 }
@@ -947,7 +1021,7 @@ __device__ inline u64 fn_update(DDState &d, u64 nw, bool updateOffset) {
 struct SelResult {
   bool selected, relevant, switching, resuming, marker;
   int ddLen;  // marshalled bytes in the output buffer (selected only)
-  bool limit;  // an engine limit was hit (kDDExpect)
+  bool limit;  // an engine limit was hit (a second frame beyond the expectation ring)
   u32 stagedSlot;  // the ring slot the LDS copy holds on return
 };
 

@@ -4352,7 +4352,10 @@ int lkf_debug_dd_state(lkf_engine *e, int32_t dt, uint64_t out[16]) {
   out[11] = d.chBroken & cm;
   out[12] = d.chActive & cm;
   uint64_t ex = 0;
-  for (int c = 0; c < d.numChains; c++) ex += d.expCount[c];
+  for (int c = 0; c < d.numChains; c++) {  // (the set's size: the ring's bits and the frame beyond it)
+    ex += d.expFar[c] ? 1 : 0;
+    for (int w = 0; w < kDDExpWords; w++) ex += uint64_t(__builtin_popcountll(d.exp[c][w]));
+  }
   out[13] = ex;
   out[14] = (d.flags & DS_FN_INIT) ? d.fnLast : ~0ull;
   out[15] = uint64_t(uint8_t(h.curS + 128)) | (uint64_t(uint8_t(h.curT + 128)) << 8);

@@ -2379,13 +2379,16 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     // fires its callback, and so would marking it missing or aging it out of
     // the window; a lane whose add could do any of these takes the full step
     // (bounds: the missing marks of an add lie in [cLast - kNack, efn - kNack))
+    // (the missing marks [cl0 - kNack, efn - kNack), the aged-out [cl0 - 256, efn - 256))
     for (int c = 0; c < int(d.numChains); c++) {
-      if ((d.chBroken >> c) & 1) continue;
-      for (int i = 0; i < int(d.expCount[c]); i++) {
-        const u64 e = d.exp[c][i];
-        if (adds && (e == efn || (efn > cl0 && ((e + dd::kNack >= cl0 && e + dd::kNack < efn) || e + dd::kEntries < efn))))
-          good = false;
+      if (((d.chBroken >> c) & 1) || !adds) continue;
+      bool hit = dd::x_has(d, c, efn);
+      if (efn > cl0) {
+        const u64 k0 = cl0 >= dd::kNack ? cl0 - dd::kNack : 0, k1 = efn >= dd::kNack ? efn - dd::kNack : 0;
+        const u64 a0 = cl0 >= dd::kEntries ? cl0 - dd::kEntries : 0, a1 = efn >= dd::kEntries ? efn - dd::kEntries : 0;
+        hit = hit || dd::x_any_frames(d, c, k0, k1) || dd::x_any_frames(d, c, a0, a1);
       }
+      if (hit) good = false;
     }
     SVC_WHY(14);
     const u64 addM = __ballot(adds);
@@ -2415,7 +2418,7 @@ __device__ __forceinline__ u32 svc_run(Lane &L, LaneOut &o, const PktV &p, u32 p
     if (eval && good)  // restarts
       for (int c = 0; c < int(d.numChains); c++) {
         if (!((d.chActive >> c) & 1) || int(dp.nchain) <= c || chainDiff(c) != 0) continue;
-        if (((aboveM >> c) & 1) || d.expCount[c] != 0 || (!LKF_SVC_CHAINS && ((d.chBroken >> c) & 1)))
+        if (((aboveM >> c) & 1) || dd::x_any(d, c) || (!LKF_SVC_CHAINS && ((d.chBroken >> c) & 1)))
           good = false;
         else if (LKF_SVC_CHAINS)
           chRst |= 1u << c;
@@ -2997,7 +3000,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     // the head and the expectFrames rows of the chains in use (a structure
     // update zeroes every row's count, so rows past them are never read first)
     const u32 nc0 = __builtin_amdgcn_readfirstlane(u32(A.ddState[d].numChains));
-    const u32 nDD = (kDDStateHead + nc0 * kDDExpect * 8) / 16;
+    const u32 nDD = (kDDStateHead + nc0 * kDDExpRow * 8) / 16;
     for (u32 i = lane; i < nDD; i += 64) l[i] = g[i];
     __syncthreads();
     if (sDD->flags & DS_KF_VALID) dd_stage_struct(L, sDD, sDDSRaw, lane);
@@ -3493,7 +3496,7 @@ __global__ void __launch_bounds__(64) DECIDE_ATTR k_decide_dt(DecideArgs A, cons
     wave_lds_sync();
     uint4 *g = reinterpret_cast<uint4 *>(A.ddState + d);
     const uint4 *l = reinterpret_cast<const uint4 *>(sDD);
-    const u32 nDD = (kDDStateHead + u32(sDD->numChains) * kDDExpect * 8) / 16;
+    const u32 nDD = (kDDStateHead + u32(sDD->numChains) * kDDExpRow * 8) / 16;
     for (u32 i = lane; i < nDD; i += 64) g[i] = l[i];
   }
   if ((L.h.flags & F_VP8) && L.vcDirty) {  // the maps go back only when a batch changed them
@@ -3577,7 +3580,10 @@ constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 desc
 // (two-byte extension profile) = 343
 constexpr int PRE_MAX_DD = 352;
 
-constexpr int EMIT_U = 4;  // 16-B chunks per lane in flight per copy iteration (6 and 8 measured no faster, r4_ab_runs.txt)
+#ifndef LKF_EMIT_U  // 16-B chunks per lane in flight per copy iteration (6 and 8 measured no faster at full occupancy, r4_ab_runs.txt)
+#define LKF_EMIT_U 4
+#endif
+constexpr int EMIT_U = LKF_EMIT_U;
 
 
 struct EmitArgs {
@@ -3644,8 +3650,18 @@ __device__ __forceinline__ void store16(u8 *p, uint4 v) {
   __builtin_nontemporal_store(v.w, reinterpret_cast<u32 *>(p) + 3);
 }
 
+#ifndef LKF_EMIT_XCD  // (A/B) the XCD-aware group partition (1) or a plain grid-stride (0)
+#define LKF_EMIT_XCD 1
+#endif
+#ifndef LKF_EMIT_LDS  // (A/B) LDS per emit workgroup raised to this many bytes (0: as needed) -> fewer resident
+#define LKF_EMIT_LDS 0
+#endif
 template <int PRE>
 __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
+#if LKF_EMIT_LDS
+  __shared__ u32 sPad[LKF_EMIT_LDS / 4];
+  if (threadIdx.x == 1023) sPad[blockIdx.x % (LKF_EMIT_LDS / 4)] = 0;  // (never: keeps the allocation)
+#endif
   __shared__ __attribute__((aligned(16))) u8 pre[EMIT_G][PRE];
   __shared__ u64 sSrc[EMIT_G];  // arena offset of the record's first payload byte after the prefix
   __shared__ u32 sCs[EMIT_G];   // first chunk of the record, relative to the group
@@ -3664,7 +3680,7 @@ __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
   // track's payloads (one per subscribing DownTrack) are adjacent, so the
   // re-reads hit that XCD's 4 MiB L2 instead of going to HBM.  (Falls back to
   // a plain grid-stride when the grid is not a multiple of 8.)
-  const u32 nx = (gridDim.x % 8 == 0) ? 8u : 1u;
+  const u32 nx = (LKF_EMIT_XCD && gridDim.x % 8 == 0) ? 8u : 1u;
   const u32 xcd = blockIdx.x % nx, slotInX = blockIdx.x / nx, perX = gridDim.x / nx;
   const u64 gpx = (ngroups + nx - 1) / nx;
   const u64 gBeg = u64(xcd) * gpx, gEnd = min(ngroups, gBeg + gpx);

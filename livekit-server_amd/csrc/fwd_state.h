@@ -185,14 +185,18 @@ enum : uint8_t { T_WIDE = 0x10, T_DD = 0x20, T_PLAYOUT = 0x40, T_CODEC = 0x80 };
 //   - a frame keeps up to kDDFdInline frame diffs in its DDPkt; a longer list
 //     (custom frame diffs, 6+ bits each: at most 340) goes to the batch's
 //     spill array (k_dd_decode), a template's longer list stays in the pool.
-// Engine limits that remain: FrameChain.expectFrames holds kDDExpect frames
-// per chain, the structure ring kDDSlots structures per track, the spill array
-// its capacity; beyond them a packet is flagged (error bit 16 -> LKF_EINVAL /
-// LKF_ENOSPC at lkf_sync), never decided silently.
+// FrameChain.expectFrames (round 6: no longer capped at 16): every frame a
+// chain can wait on lies in the decision cache's window around cLast, so the
+// set is a 512-bit ring over [cLast - 256, cLast + 256) (dd_device.h) plus one
+// frame beyond it for the packet whose frame number jumped ahead of cLast.
+// Engine limits that remain: the structure ring kDDSlots structures per track,
+// the spill array its capacity; beyond them a packet is flagged (error bit 16
+// -> LKF_EINVAL / LKF_ENOSPC at lkf_sync), never decided silently.
 constexpr int kDDChains = 32;      // MaxDecodeTargets (NumChains <= NumDecodeTargets)
 constexpr int kDDFdPool = 416;     // template frame diffs of one structure (408 fit in 255 bytes)
 constexpr int kDDFdInline = 8;     // frame diffs kept in a DDPkt
-constexpr int kDDExpect = 16;      // frames one chain may wait on (FrameChain.expectFrames)
+constexpr int kDDExpWords = 8;     // FrameChain.expectFrames: a 512-bit ring over [cLast - 256, cLast + 256)
+constexpr int kDDExpRow = 10;      // u64 per chain row: the ring, the frame beyond it, padding (80 B)
 constexpr int kDDSlots = 8;        // structure ring per track
 constexpr int kDDMaxBytes = 255;   // marshalled DD (pion two-byte extension element)
 constexpr int kSeqDDBytes = 256;   // a sequencer slot's ddBytes entry: length byte + kDDMaxBytes
@@ -287,9 +291,9 @@ struct alignas(16) DDState {
   uint8_t slot;                 // structure ring slot of d.structure
   uint8_t numChains, numTargets;  // len(d.chains), len(d.decodeTargets)
   uint8_t pad;
-  uint8_t expCount[kDDChains];
+  uint8_t expFar[kDDChains];    // exp[c][8] holds a waited-on frame beyond the ring
   uint64_t pad2;                // (exp rows 16-B aligned)
-  uint64_t exp[kDDChains][kDDExpect];  // FrameChain.expectFrames (a set: see dd_device.h); rows < numChains staged
+  uint64_t exp[kDDChains][kDDExpRow];  // FrameChain.expectFrames (a set: see dd_device.h); rows < numChains staged
 };
 constexpr uint32_t kDDStateHead = 176;  // the bytes of DDState before exp[][] (always staged)
 static_assert(sizeof(DDState) % 16 == 0, "DDState must be 16-B granular");

@@ -1556,6 +1556,349 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
 // RTCP NACK) and the offset of its pairs in the batch's pair buffer.
 // ---------------------------------------------------------------------------
 
+// ---- the lane-parallel form (round 6) -----------------------------------
+// Pairs() runs at every datagram of the stream, Remove() before it, Push()
+// in between; so an entry's life depends only on the stream's arrival times
+// and its own SN: it is nacked at the first datagram whose arrival is at
+// least its lastNackedAt plus the interval its tries require, again from
+// there, and it leaves at the datagram that carries its SN (Remove, before
+// that datagram's Pairs) or at the first Pairs after its MaxTries-th nack
+// (purge).  Entries interact only through the queue's capacity (the newest
+// CacheSize kept on Push), through Remove's "first entry with that SN", and
+// through the pair packing of one Pairs call (the entries nacked together, in
+// queue order, against the queue's first entry).  When the capacity cannot be
+// reached in this ingest (entries at the start plus every SN pushed <=
+// CacheSize), the SNs are distinct and the arrivals do not go back in time,
+// each entry's life is computed on its own lane (binary searches over the
+// arrival times), the nacks of one datagram are gathered by a sort of
+// (datagram, entry) events, and each such datagram's pairs are packed on a
+// lane of their own.  Otherwise the serial form below runs.
+constexpr u32 kNackFastN = 1024;  // datagrams of a stream the lane-parallel form stages
+constexpr u32 kNackFastEv = 512;  // nack events: at most MaxTries per entry (5 x 100)
+constexpr u32 kNackNone = 0xffffffffu;
+struct NackFastLds {
+  i64 arr[kNackFastN];
+  u16 sn[kNackFastN];
+  u16 nextMine[kNackFastN + 1];
+  u8 fl[kNackFastN];  // 1 mine, 2 updateStreamState ran, 4 a loss range
+  // entries (queue order: the queue at the start, then every pushed SN in push order)
+  i64 eLast[kNackSlots];
+  u32 eRem[kNackSlots], eDeath[kNackSlots];
+  i32 eBirth[kNackSlots];
+  u16 eSn[kNackSlots];
+  u8 eTries[kNackSlots];
+  u32 pushK[kNackCap], pushOff[kNackCap + 1];
+  u16 pushS0[kNackCap];
+  u32 key[kNackFastEv];  // nack events: datagram << 7 | entry
+  u32 gStart[kNackFastEv + 1];
+  u32 gNp[kNackFastEv], gOff[kNackFastEv];
+  lkf_nack_pair stage[kNackFastEv];
+  u32 nEv;
+};
+static_assert(kNackSlots <= 128 && kNackFastN <= 1024, "event keys hold 7 bits of entry, 10 of datagram");
+
+__device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 count0, u32 rtt, u32 nIdx,
+                          const u32 *lst, bool useList, u32 pb, const lkf_raw_pkt *__restrict__ raws,
+                          const IngParsed *__restrict__ q, const lkf_flow *__restrict__ flows, u32 *__restrict__ info,
+                          u32 *__restrict__ pairOff, u32 *pairCnt, lkf_nack_pair *__restrict__ pairs, u32 pairCap,
+                          u32 *err) {
+  if (nIdx > kNackFastN || count0 > u32(kNackCap)) return false;
+  // ---- the stream's datagrams, and its pushes
+  u64 lossTot = 0;
+  u32 nPush = 0;
+  bool mono = true;
+  i64 prevArr = INT64_MIN;
+  for (u32 base = 0; base < nIdx; base += 64) {
+    const u32 k = base + lane;
+    const bool v = k < nIdx;
+    u32 ic = 0, flg = 0;
+    u16 sn = 0;
+    i64 arr = prevArr;
+    u64 L = 0, s0 = 0;
+    if (v) {
+      ic = useList ? lst[k] : pb + k;
+      const lkf_raw_pkt rp = raws[ic];
+      arr = rp.arrival_ns;
+      if (rp.stream == sid) {
+        flg = 1;
+        if (q[ic].flags & IP_OK) {
+          flg |= 2;
+          sn = q[ic].sn;
+          const lkf_flow f = flows[ic];
+          if (f.flags & LKF_FLOW_HAS_LOSS) {
+            flg |= 4;
+            s0 = f.loss_start;
+            L = f.loss_end - f.loss_start;
+          }
+        }
+      }
+      F.arr[k] = arr;
+      F.sn[k] = sn;
+      F.fl[k] = u8(flg);
+    }
+    const u64 prevLane = u64(__shfl_up(u64(arr), 1, 64));
+    if (__ballot(v && arr < (lane ? i64(prevLane) : prevArr))) mono = false;
+    prevArr = i64(rl_u64(u64(arr), 63));
+    if (__ballot(L > u64(kNackCap) || ((flg & 4) && L == 0))) return false;
+    const u64 lm = __ballot(flg & 4);
+    const u32 before4 = u32(__popcll(lm & ((1ull << lane) - 1)));
+    if ((flg & 4) && nPush + before4 < u32(kNackCap)) {
+      F.pushK[nPush + before4] = k;
+      F.pushS0[nPush + before4] = u16(s0);
+    }
+    // the loss lengths in push order (a prefix over the chunk's loss datagrams)
+    u64 Ls = wave_incl_scan_u64(L, lane);
+    if ((flg & 4) && nPush + before4 < u32(kNackCap)) F.pushOff[nPush + before4 + 1] = u32(lossTot + Ls);
+    lossTot += rl_u64(Ls, 63);
+    nPush += u32(__popcll(lm));
+    if (u64(count0) + lossTot > u64(kNackCap)) return false;  // the capacity could be reached
+  }
+  if (!mono) return false;
+  const u32 M = count0 + u32(lossTot);
+  if (lane == 0) F.pushOff[0] = 0;
+  __syncthreads();
+  // ---- the entries
+  for (u32 e = lane; e < count0; e += 64) {
+    F.eSn[e] = g->sn[e];
+    F.eTries[e] = g->tries[e];
+    F.eLast[e] = g->last[e];
+    F.eBirth[e] = -1;
+  }
+  for (u32 p = 0; p < nPush; p++) {
+    const u32 o = F.pushOff[p], L = F.pushOff[p + 1] - o, k = F.pushK[p];
+    const u16 s0 = F.pushS0[p];
+    for (u32 i = lane; i < L; i += 64) {
+      const u32 e = count0 + o + i;
+      F.eSn[e] = u16(s0 + i);
+      F.eTries[e] = 0;
+      F.eLast[e] = F.arr[k];
+      F.eBirth[e] = i32(k);
+    }
+  }
+  for (u32 e = lane; e < M; e += 64) F.eRem[e] = kNackNone;
+  // next datagram of the stream at or after k (Pairs runs there)
+  if (lane == 0) F.nextMine[nIdx] = 0xffffu;
+  for (i32 base = i32((nIdx - 1) & ~63u); base >= 0; base -= 64) {
+    const u32 k = u32(base) + lane;
+    const bool mine = k < nIdx && (F.fl[k] & 1);
+    const u64 mm = __ballot(mine);
+    const u64 ge = mm & ~((1ull << lane) - 1);
+    const u32 after = (u32(base) + 64 < nIdx) ? u32(F.nextMine[u32(base) + 64]) : 0xffffu;
+    __syncthreads();
+    if (k < nIdx) F.nextMine[k] = ge ? u16(u32(base) + u32(__ffsll((long long)ge) - 1)) : u16(after);
+    __syncthreads();
+  }
+  __syncthreads();
+  // distinct SNs (Remove takes the first entry with an SN: equal SNs need the serial form)
+  bool dup = false;
+  for (u32 e = lane; e < M; e += 64)
+    for (u32 f = 0; f < e; f++) dup = dup || F.eSn[f] == F.eSn[e];
+  if (__ballot(dup)) return false;
+  // Remove: the first datagram (from the entry's birth on) that carries its SN
+  for (u32 base = 0; base < nIdx; base += 64) {
+    const u32 k = base + lane;
+    const bool upd = k < nIdx && (F.fl[k] & 2);
+    const u16 sn = upd ? F.sn[k] : 0;
+    for (u32 e = 0; e < M; e++) {
+      const u32 st = u32(F.eBirth[e] + 1);
+      const u64 m = __ballot(upd && sn == F.eSn[e] && k >= st);
+      if (m && F.eRem[e] == kNackNone) {
+        __syncthreads();
+        if (lane == 0) F.eRem[e] = base + u32(__ffsll((long long)m) - 1);
+        __syncthreads();
+      }
+    }
+  }
+  if (lane == 0) F.nEv = 0;
+  __syncthreads();
+  // ---- each entry's life
+  auto backoff = [&](u64 num, u64 den) {
+    i64 r = i64(num / den) * 1000000;
+    if (r > 400000000) r = 400000000;
+    return r < 20000000 ? i64(20000000) : r;
+  };
+  const i64 req0 = 20000000, req1 = backoff(rtt, 1), req2 = backoff(u64(rtt) * 5, 4),
+            req3 = backoff(u64(rtt) * 25, 16), req4 = backoff(u64(rtt) * 125, 64);
+  for (u32 e = lane; e < M; e += 64) {
+    u32 t = F.eTries[e];
+    i64 l = F.eLast[e];
+    u32 k = u32(F.eBirth[e] + 1);
+    const u32 rm = F.eRem[e];
+    u32 death = kNackNone;
+    for (;;) {
+      u32 j;
+      if (t >= kNackMaxTries) {
+        j = k < nIdx ? u32(F.nextMine[k]) : 0xffffu;
+        if (j == 0xffffu) j = kNackNone;
+        if (rm != kNackNone && rm <= j) death = rm;
+        else if (j != kNackNone) death = j + 1;  // purged by the Pairs there (still the queue's at it)
+        break;
+      }
+      const i64 need = l + (t == 0 ? req0 : t == 1 ? req1 : t == 2 ? req2 : t == 3 ? req3 : req4);
+      u32 lo = k, hi = nIdx;  // first datagram at or after k arriving at or after need
+      while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (F.arr[mid] >= need) hi = mid;
+        else lo = mid + 1;
+      }
+      j = lo < nIdx ? u32(F.nextMine[lo]) : 0xffffu;
+      if (j == 0xffffu) j = kNackNone;
+      if (rm != kNackNone && rm <= j) {
+        death = rm;
+        break;
+      }
+      if (j == kNackNone) break;
+      const u32 slot = atomicAdd(&F.nEv, 1u);
+      if (slot < kNackFastEv) F.key[slot] = (j << 7) | e;
+      t++;
+      l = F.arr[j];
+      k = j + 1;
+    }
+    F.eTries[e] = u8(t);
+    F.eLast[e] = l;
+    F.eDeath[e] = death;
+  }
+  __syncthreads();
+  const u32 E = F.nEv;
+  if (E > kNackFastEv) {  // (cannot happen: at most MaxTries nacks per entry)
+    if (lane == 0) atomicOr(err, 8u);
+    return true;
+  }
+  // ---- the events in (datagram, queue) order: a bitonic sort in LDS
+  u32 P = 1;
+  while (P < E) P <<= 1;
+  for (u32 i = E + lane; i < P; i += 64) F.key[i] = 0xffffffffu;
+  __syncthreads();
+  for (u32 size = 2; size <= P; size <<= 1)
+    for (u32 stride = size >> 1; stride > 0; stride >>= 1) {
+      for (u32 i = lane; i < P; i += 64) {
+        const u32 jx = i ^ stride;
+        if (jx > i) {
+          const u32 a = F.key[i], b = F.key[jx];
+          const bool up = (i & size) == 0;
+          if ((a > b) == up) {
+            F.key[i] = b;
+            F.key[jx] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  // ---- one group per nacking datagram: its pairs (NackQueue.Pairs), packed on a lane
+  u32 G = 0;
+  for (u32 base = 0; base < E; base += 64) {
+    const u32 i = base + lane;
+    const bool st = i < E && (i == 0 || (F.key[i] >> 7) != (F.key[i - 1] >> 7));
+    const u64 m = __ballot(st);
+    if (st) F.gStart[G + u32(__popcll(m & ((1ull << lane) - 1)))] = i;
+    G += u32(__popcll(m));
+  }
+  if (lane == 0) F.gStart[G] = E;
+  __syncthreads();
+  u64 nacked = 0;
+  for (u32 gi = lane; gi < G; gi += 64) {
+    const u32 b = F.gStart[gi], en = F.gStart[gi + 1];
+    const u32 j = F.key[b] >> 7;
+    u32 first = 0;  // the queue's first entry at the Pairs of datagram j
+    for (u32 e = 0; e < M; e++)
+      if (F.eBirth[e] <= i32(j) && j < F.eDeath[e]) {
+        first = F.eSn[e];
+        break;
+      }
+    u32 baseSN = u32(u16(first - 17u));
+    bool active = false;
+    lkf_nack_pair cur = {0, 0};
+    u32 np = 0;
+    for (u32 i = b; i < en; i++) {
+      const u32 sn16 = F.eSn[F.key[i] & 127u];
+      const u32 d = u32(u16(sn16 - baseSN));
+      if (d > 16) {
+        if (active) F.stage[b + np++] = cur;
+        baseSN = sn16;
+        cur.packet_id = u16(sn16);
+        cur.lost_packets = 0;
+        active = true;
+      } else {
+        const u32 sh = u32(u16(d - 1));
+        if (sh < 16) cur.lost_packets = u16(cur.lost_packets | (1u << sh));
+      }
+    }
+    if (active) F.stage[b + np++] = cur;
+    F.gNp[gi] = np;
+    nacked += np ? u64(en - b) : 0ull;  // (UpdateNack only with a packet)
+  }
+  nacked = wave_sum_u64(nacked);
+  __syncthreads();
+  // pair offsets (a prefix over the groups), one reservation for the stream
+  u32 tot = 0;
+  for (u32 base = 0; base < G; base += 64) {
+    const u32 gi = base + lane;
+    const u64 np = gi < G ? F.gNp[gi] : 0;
+    const u64 inc = wave_incl_scan_u64(np, lane);
+    if (gi < G) F.gOff[gi] = tot + u32(inc - np);
+    tot += u32(rl_u64(inc, 63));
+  }
+  __syncthreads();
+  if (tot) {
+    u32 off = 0;
+    if (lane == 0) off = atomicAdd(pairCnt, tot);
+    off = __builtin_amdgcn_readfirstlane(off);
+    if (off + tot > pairCap) {
+      if (lane == 0) atomicOr(err, 8u);  // pair buffer capacity: these RTCP NACKs are not recorded
+    } else {
+      for (u32 gi = lane; gi < G; gi += 64) {
+        const u32 b = F.gStart[gi], np = F.gNp[gi], o = off + F.gOff[gi];
+        for (u32 i = 0; i < np; i++) pairs[o + i] = F.stage[b + i];
+        if (np) {
+          const u32 kk = F.key[b] >> 7;
+          const u32 icx = useList ? lst[kk] : pb + kk;
+          info[icx] = np | ((F.gStart[gi + 1] - b) << 16);
+          pairOff[icx] = o;
+        }
+      }
+    }
+  }
+  // ---- the queue after the ingest: the entries still in it, in order
+  bool changed = M != count0 || E > 0;
+  u32 kept = 0;
+  for (u32 base = 0; base < M; base += 64) {
+    const u32 e = base + lane;
+    const bool live = e < M && F.eDeath[e] == kNackNone;
+    changed = changed || (e < M && !live);
+    const u64 m = __ballot(live);
+    const u32 at = kept + u32(__popcll(m & ((1ull << lane) - 1)));
+    i64 l = 0;
+    u16 sn = 0;
+    u8 t = 0;
+    if (live) {
+      l = F.eLast[e];
+      sn = F.eSn[e];
+      t = F.eTries[e];
+    }
+    __syncthreads();
+    if (live) {  // (entries move only toward the front: e >= at)
+      F.eLast[at] = l;
+      F.eSn[at] = sn;
+      F.eTries[at] = t;
+    }
+    __syncthreads();
+    kept += u32(__popcll(m));
+  }
+  if (__ballot(changed)) {
+    for (u32 i = lane; i < kept; i += 64) {
+      g->last[i] = F.eLast[i];
+      g->sn[i] = F.eSn[i];
+      g->tries[i] = F.eTries[i];
+    }
+    if (lane == 0) g->count = kept;
+  }
+  if (lane == 0 && nacked) g->nacks += nacked;
+  return true;
+}
+
+#ifndef LKF_NACK_FAST  // the lane-parallel form where it is exact (1), or always the serial one (0)
+#define LKF_NACK_FAST 1
+#endif
 #ifndef LKF_NACK_LIVE  // stage only the live entries (1), or all slots with the count (0, round 4)
 #define LKF_NACK_LIVE 1
 #endif
@@ -1567,16 +1910,28 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
                                                  const u32 *__restrict__ cnt, u32 stride, u32 *__restrict__ info,
                                                  u32 *__restrict__ pairOff, u32 *pairCnt,
                                                  lkf_nack_pair *__restrict__ pairs, u32 pairCap, u32 *err) {
-  __shared__ i64 sLast[kNackSlots];
-  __shared__ u32 sSn[kNackSlots];
-  __shared__ u32 sTries[kNackSlots];
-  __shared__ u32 sPurge[kNackSlots];
   // the stream's RTCP NACKs of this ingest, staged and written in blocks: one
   // reservation in the batch's pair buffer per block instead of one atomic per
   // NACK (every stream's NACKs on one counter serialised the kernel)
   constexpr u32 kPairStage = 512, kRecStage = 64;
-  __shared__ lkf_nack_pair sStage[kPairStage];
-  __shared__ u32 sRecIc[kRecStage], sRecInfo[kRecStage], sRecOff[kRecStage];
+  struct Serial {
+    i64 last[kNackSlots];
+    u32 sn[kNackSlots], tries[kNackSlots], purge[kNackSlots];
+    lkf_nack_pair stage[kPairStage];
+    u32 recIc[kRecStage], recInfo[kRecStage], recOff[kRecStage];
+  };
+  // (the lane-parallel form and the serial one share the LDS: the serial form
+  // runs only when the other declined, before it wrote anything but LDS)
+  __shared__ union U {
+    NackFastLds f;
+    Serial s;
+  } sU;
+  i64 *const sLast = sU.s.last;
+  u32 *const sSn = sU.s.sn;
+  u32 *const sTries = sU.s.tries;
+  u32 *const sPurge = sU.s.purge;
+  lkf_nack_pair *const sStage = sU.s.stage;
+  u32 *const sRecIc = sU.s.recIc, *const sRecInfo = sU.s.recInfo, *const sRecOff = sU.s.recOff;
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
   if (!s.nack || s.closed) return;
@@ -1586,6 +1941,13 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   // only the live entries are staged (every read below is of an index < count)
   u32 count = g->count;
   const u32 rtt = g->rtt;
+  const bool useList = s.layer < 3;
+  const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
+  const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
+  if (LKF_NACK_FAST && nack_fast(sU.f, lane, sid, g, count, rtt, nIdx, lst, useList, pb, raws, q, flows, info,
+                                 pairOff, pairCnt, pairs, pairCap, err))
+    return;
+  __syncthreads();
   for (u32 i = lane; i < (LKF_NACK_LIVE ? count : u32(kNackSlots)); i += 64) {
     sLast[i] = g->last[i];
     sSn[i] = g->sn[i];
@@ -1638,9 +2000,6 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
     const u64 m1 = __ballot(lane + 64 < count && sSn[lane + 64] == sn16);
     if (m0 | m1) removeAt(m0 ? u32(__ffsll((long long)m0) - 1) : 64u + u32(__ffsll((long long)m1) - 1));
   };
-  const bool useList = s.layer < 3;
-  const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
-  const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
   u64 nacked = 0;
   // The earliest arrival time at which Pairs() can do anything: min over the
   // entries of lastNackedAt + the interval its tries require (an entry at

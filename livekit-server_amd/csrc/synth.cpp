@@ -63,6 +63,7 @@ struct Plan {
   u8 level;
   u8 pt;
   u8 vp9;  // LKF_VP9_* flags (config 5 SVC packets)
+  u8 lost; // (svc_dd = 3) lost by the scripted burst, whatever the random loss draws
 };
 
 struct TrackGen {
@@ -266,6 +267,12 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
   const bool cb = cfg->has_callbacks != 0;
   const bool svcDD = cfg->svc_dd != 0;
   const bool ddWide = cfg->svc_dd == 2;
+  // svc_dd = 3: as 1, with chain 0 following every frame (custom chain diffs:
+  // the previous frame number) and, for 2 s of every 3, every other frame
+  // number lost: each arriving frame then waits on the lost one before it, so
+  // a chain holds dozens of expected frames (FrameChain.expectFrames) until
+  // the oldest ages out of the decision cache's NACK window and breaks it
+  const bool ddBurst = cfg->svc_dd == 3;
   const bool h264 = cfg->h264 > 0;
 
   u32 rooms = cfg->rooms, parts = cfg->participants;
@@ -475,6 +482,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
         reducedTrack = (ti % 2) == 0;  // publisher drops S2 (active targets 0x3F) for 1 s
       }
       u64 lastChain[3] = {0, 0, 0};
+      u64 lastAny = 0;  // (svc_dd = 3) the previous frame number
       bool wasReduced = false;
       std::vector<i64> reqs;
       for (int l = 0; l < 3; l++) reqs.insert(reqs.end(), kfReq[ti][l].begin(), kfReq[ti][l].end());
@@ -513,8 +521,10 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
               chv = ddT[size_t(tmpl)].chains;
             } else {
               for (int c = 0; c < nch; c++) chv.push_back(int(std::min<u64>(255, efn - lastChain[nch == 9 ? c / 3 : c])));
+              if (ddBurst && efn > lastAny && lastAny) chv[0] = int(std::min<u64>(255, efn - lastAny));
             }
             if (kf || tid == 0) lastChain[sl] = efn;
+            lastAny = efn;
           }
           for (int q = 0; q < kSvcPkts[sl]; q++, k++) {
             Plan pl{};
@@ -535,6 +545,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
             pl.vp9 = u8(LKF_VP9_I | LKF_VP9_L | (kf ? 0 : LKF_VP9_P) | (q == 0 ? LKF_VP9_B : 0) |
                         (q == kSvcPkts[sl] - 1 ? LKF_VP9_E : 0) | (tid > 0 ? LKF_VP9_U : 0));
             pl.pt = g.p.codec == LKF_CODEC_AV1 ? 35 : 98;
+            pl.lost = u8(ddBurst && g.dd && !kf && (f % 90) >= 15 && (f % 90) < 75 && (efn & 1));
             if (g.dd) {
               const bool attach = kf && sl == 0 && q == 0;
               pl.tid = u8(ddT[size_t(tmpl)].tid);  // the descriptor's TemporalId (key superframes: T0)
@@ -652,7 +663,7 @@ extern "C" lkfs_trace *lkfs_generate(const lkfs_cfg *cfg) {
       std::vector<Plan> kept;
       kept.reserve(st.size());
       for (auto &pl : st)
-        if (!(loss > 0 && rng.uni() < loss)) kept.push_back(pl);
+        if (!(loss > 0 && rng.uni() < loss) && !pl.lost) kept.push_back(pl);
       st.swap(kept);
       std::stable_sort(st.begin(), st.end(), [](const Plan &a, const Plan &b) { return a.arrival < b.arrival; });
     }

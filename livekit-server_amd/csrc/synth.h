@@ -32,7 +32,9 @@ typedef struct lkfs_cfg {
   int32_t has_callbacks; /* -1 -> default (1): has_ref_ts / has_expected_ts */
   int32_t svc_dd;        /* config 5: -1 -> default (1): AV1 + VP9 publishers with the dependency
                             descriptor beside VP9-descriptor ones; 0: VP9 descriptor only; 2: as 1
-                            with the wide descriptor (9 chains, 17-18 frame diffs) */
+                            with the wide descriptor (9 chains, 17-18 frame diffs); 3: as 1 with
+                            chain 0 over every frame and bursts of every other frame lost (chains
+                            waiting on dozens of frames) */
   int32_t h264;          /* configs 1-3: 1 -> H.264 simulcast publishers (config 1: the publisher;
                             else every third) with SPS key frames as single NALU / STAP-A / STAP-B /
                             FU-A; <= 0 -> VP8 only */

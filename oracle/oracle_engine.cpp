@@ -749,7 +749,13 @@ int orc_debug_dd_state(orc_engine *e, int32_t dt, uint64_t out[16]) {
   for (size_t c = 0; c < d.chains.size(); c++) {
     if (d.chains[c]->broken) out[11] |= 1ull << c;
     if (d.chains[c]->active) out[12] |= 1ull << c;
-    ex += d.chains[c]->expectFrames.size();
+    // distinct frames waited on by the unbroken chains (a frame registered by
+    // several packets is one callback target; a broken chain's list is inert)
+    if (!d.chains[c]->broken) {
+      std::vector<u64> f = d.chains[c]->expectFrames;
+      std::sort(f.begin(), f.end());
+      ex += uint64_t(std::unique(f.begin(), f.end()) - f.begin());
+    }
   }
   out[13] = ex;
   out[14] = d.fnWrapper.inited ? d.fnWrapper.last : ~0ull;

@@ -19,8 +19,11 @@ for item in "${LIST[@]}"; do
   args=${item#*:}
   if [ "${PMC:-1}" = "1" ]; then
     i=0
-    for ctr in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $O/pmc_$name/p$i -o run -- \
+    CTRS="FETCH_SIZE WRITE_SIZE"
+    # EXACT=1: the request counters by size as well (scripts/pmc_summary.py exact_bytes)
+    [ "${EXACT:-1}" = "1" ] && CTRS="$CTRS TCC_EA0_RDREQ_sum,TCC_EA0_RDREQ_32B_sum,TCC_EA0_RDREQ_64B_sum,TCC_EA0_RDREQ_128B_sum TCC_EA0_WRREQ_sum,TCC_EA0_WRREQ_64B_sum"
+    for ctr in $CTRS; do
+      timeout -k 10 300 rocprofv3 --pmc ${ctr//,/ } --kernel-trace --output-format csv -d $O/pmc_$name/p$i -o run -- \
         python3 bench.py $args --steps 3 --warmup 1 --no-cpu-baseline --no-parity > $O/pmc_${name}_p$i.log 2>&1
       rc=$?; echo "$name pmc $ctr rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/pmc_${name}_p$i.log; exit $rc; }
       i=$((i+1))

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${OUT_NAME:-r6}
 mkdir -p $O
 if [ -n "${R6_TESTS:-}" ]; then
-  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest -x -v --timeout 300 --timeout-method thread $R6_TESTS > $O/pytest.log 2>&1
+  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest -x -v --timeout 300 --timeout-method thread $R6_TESTS ${R6_K:+-k "$R6_K"} > $O/pytest.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log
   [ $rc -eq 0 ] || exit $rc
 fi

@@ -19,12 +19,36 @@ def short_name(name):
     return n[5:] if n.startswith("void ") else n
 
 
+RD = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+WR = ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum")
+
+
+def exact_bytes(c):
+    """Read and write bytes from the L2's memory-side request counters by
+    request size (the passes EXACT=1 of scripts/gpu_final.sh collects):
+    32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B, and 64 x WRREQ_64B +
+    32 x (WRREQ - WRREQ_64B).  FETCH_SIZE's rocprofv3 expression counts a
+    128-B request (not in TCC_BUBBLE on gfx950) as 64 B, which is why the
+    guide doubles it; the by-size sum needs no correction.  -> (read, write)
+    or None."""
+    if not all(k in c for k in RD + WR):
+        return None
+    rd = 32 * c[RD[0]] + 64 * c[RD[1]] + 128 * c[RD[2]]
+    wr = 64 * c[WR[1]] + 32 * (c[WR[0]] - c[WR[1]])
+    return rd, wr
+
+
 def totals(out):
     """per-launch HBM bytes per kernel and the whole step's (per k_decide_dt<false> dispatch = per batch)"""
     for k in list(out.keys()):
         c = out[k]
         if isinstance(c, dict) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             out[short_name(k).split("::")[-1] + "_hbm_bytes_per_launch"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+        if isinstance(c, dict) and exact_bytes(c):
+            rd, wr = exact_bytes(c)
+            out[short_name(k).split("::")[-1] + "_hbm_exact_rd_wr_per_launch"] = [int(rd), int(wr)]
+            if "TCC_EA0_RDREQ_sum" in c:  # the by-size counts should add up to all read requests
+                c["_rdreq_by_size_over_all"] = (c[RD[0]] + c[RD[1]] + c[RD[2]]) / max(1.0, c["TCC_EA0_RDREQ_sum"])
     dec = [c for k, c in out.items() if isinstance(c, dict) and short_name(k).startswith("lkf::k_decide_dt")]
     nsteps = max((c.get("_dispatch_samples", 0) for c in dec), default=0)
     if nsteps:
@@ -33,6 +57,12 @@ def totals(out):
             if isinstance(c, dict) and short_name(k).startswith("lkf::") and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
                 tot += (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 * c["_dispatch_samples"]
         out["hbm_bytes_per_step"] = int(tot / nsteps)
+        ex = [(exact_bytes(c), c["_dispatch_samples"]) for k, c in out.items()
+              if isinstance(c, dict) and short_name(k).startswith("lkf::")]
+        if ex and all(e for e, _ in ex):
+            out["hbm_exact_read_per_step"] = int(sum(e[0] * n for e, n in ex) / nsteps)
+            out["hbm_exact_write_per_step"] = int(sum(e[1] * n for e, n in ex) / nsteps)
+            out["hbm_exact_bytes_per_step"] = out["hbm_exact_read_per_step"] + out["hbm_exact_write_per_step"]
     return out
 
 

@@ -173,6 +173,13 @@ def test_ingress_config5_dd_wide(pkg, workload, abi):
     assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
 
 
+def test_ingress_config5_dd_burst(pkg, workload, abi):
+    """The burst workload (svc_dd = 3: chains waiting on dozens of frames)
+    through the stream parser and then the selector."""
+    tr = workload.Trace(5, duration_s=4.0, batch_s=0.5, rooms=4, seed=94, svc_dd=3)
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
+
+
 def test_ingress_h264_keyframes(pkg, workload, abi):
     """H.264 simulcast publishers: IsH264KeyFrame over single NALU / STAP-A /
     STAP-B / FU-A SPS packets (and truncated aggregates) on the GPU."""
@@ -210,6 +217,24 @@ def test_ingress_nack_heavy_loss(pkg, workload, abi):
     tr = workload.Trace(2, duration_s=3.0, batch_s=0.05, rooms=4, loss=0.25, reorder=0.1, seed=77)
     assert run_ingress_parity(pkg, workload, abi, tr, speakers=False) > 0
     assert run_ingress_parity.nack_pkts > 100
+
+
+@pytest.mark.parametrize("loss,reorder,batch_s,seed", [(0.02, 0.01, 1.0, 5), (0.06, 0.04, 1.0, 6), (0.3, 0.1, 1.0, 7),
+                                                       (0.05, 0.03, 0.01, 8)])
+def test_ingress_nack_lane_parallel(pkg, workload, abi, loss, reorder, batch_s, seed):
+    """Round 6: k_ing_nack decides each queue entry's nacks on a lane of its
+    own where that is exact (no capacity eviction possible, distinct SNs,
+    arrivals in order) and falls back to the serial form per stream
+    otherwise.  1-s ingests as the bench runs them (the lane-parallel form on
+    nearly every stream), heavy loss (queues reach CacheSize: the serial form
+    on many streams, both forms in one launch), and 10-ms ticks; every RTCP
+    NACK, its pairs and the per-stream receiver statistics (nacks included)
+    equal the oracle's."""
+    tr = workload.Trace(2, duration_s=4.0 if batch_s >= 1.0 else 0.6, batch_s=batch_s, rooms=12, loss=loss,
+                        reorder=reorder, seed=seed)
+    rtt = {1: [(s, 30 + (11 * s) % 300) for s in range(0, tr.nstreams, 2)]}
+    assert run_ingress_parity(pkg, workload, abi, tr, speakers=False, rtt_changes=rtt) > 0
+    assert run_ingress_parity.nack_pkts > 10
 
 
 def test_ingress_config3_bench_size(pkg, workload, abi):
