@@ -43,7 +43,14 @@ enum lkf_codec {
 
 /* Control ops, applied to one DownTrack immediately before the first packet
  * of its track whose batch index >= at_pkt (or at batch end).  Each op is the
- * Forwarder/DownTrack method named beside it (pkg/sfu/forwarder.go). */
+ * Forwarder/DownTrack method named beside it (pkg/sfu/forwarder.go).
+ * at_pkt indexes the ExtPacket batch the next lkf_run forwards.  When that
+ * batch comes from lkf_ingest* (Buffer.calc on the GPU), its ExtPackets exist
+ * only after the ingest, so a caller cannot in general name a position inside
+ * it: such callers queue their ops at 0 (the batch start) or beyond the batch
+ * (its end), which is what bench.py's ingress steps do
+ * (workload.events_at_batch_start); an ExtPacket batch the caller submits
+ * itself (lkf_submit*) takes any index. */
 enum lkf_ctl_op {
   LKF_CTL_MUTE = 1,              /* Mute(a0 muted, a1 isSubscribeMutable)  :377  */
   LKF_CTL_PUBMUTE = 2,           /* PubMute(a0)                            :422  */

@@ -133,7 +133,6 @@ struct BatchCtx {
   // counters) for this topology (tracks, DownTracks); lkf_run then skips
   // k_batch_init and k_track_ranges
   bool prepByIngest = false;
-  bool gPrepFused = false;  // gPrep was captured without k_batch_init / k_track_ranges
   uint32_t prepNT = 0, prepND = 0;
   uint64_t *dITotal = nullptr;    // that ingest's ExtPacket count (device; k_track_ranges reads it)
   bool used = false;
@@ -149,8 +148,11 @@ struct BatchCtx {
   // the prep stage (k_h2d ... layer index) and the decide stage's tail
   // (counters, output scan) as HIP graphs, captured for the engine's topology
   // epoch; replayed every run (one launch each instead of ~11)
-  hipGraphExec_t gPrep = nullptr, gScan = nullptr, gCtl = nullptr;
-  uint64_t gPrepEpoch = 0, gScanEpoch = 0, gCtlEpoch = 0;
+  // (two prep graphs: [1] with the ingest's prep fused in — k_batch_init /
+  // k_track_ranges left out — [0] without; a context alternating between an
+  // ingest-prepared batch and another replays both instead of re-capturing)
+  hipGraphExec_t gPrep[2] = {nullptr, nullptr}, gScan = nullptr, gCtl = nullptr;
+  uint64_t gPrepEpoch[2] = {0, 0}, gScanEpoch = 0, gCtlEpoch = 0;
 };
 
 }  // namespace
@@ -1160,7 +1162,8 @@ void lkf_destroy(lkf_engine *e) {
       if (ev) (void)hipEventDestroy(ev);
   for (auto &x : e->ctx) {
     stage_free(&x.stage, &x.stageDev);
-    if (x.gPrep) (void)hipGraphExecDestroy(x.gPrep);
+    for (auto &g : x.gPrep)
+      if (g) (void)hipGraphExecDestroy(g);
     if (x.gCtl) (void)hipGraphExecDestroy(x.gCtl);
     if (x.gScan) (void)hipGraphExecDestroy(x.gScan);
     if (x.dDesc) (void)dfree(x.dDesc);
@@ -1704,7 +1707,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     x.stageCap = uint32_t(std::max<size_t>(2 * nev, 4096));
     HIPCHK(stage_alloc(&x.stage, &x.stageDev, sizeof(RunDesc) + size_t(x.stageCap) * (sizeof(DevEvent) + 4)),
            "alloc stage");
-    x.gPrepEpoch = 0;
+    x.gPrepEpoch[0] = x.gPrepEpoch[1] = 0;
     x.gCtlEpoch = 0;
   }
   DevEvent *evs = reinterpret_cast<DevEvent *>(x.stage + sizeof(RunDesc));
@@ -1758,7 +1761,7 @@ int lkf_run(lkf_engine *e, void *stream) {
       x.evLaneCap = std::max<uint64_t>(2 * nev, 4096);
       HIPCHK(dalloc(&x.dEvLane, x.evLaneCap), "alloc evlane");
     }
-    x.gPrepEpoch = 0;
+    x.gPrepEpoch[0] = x.gPrepEpoch[1] = 0;
     x.gCtlEpoch = 0;
   }
   const auto tp3 = clk::now();
@@ -1848,13 +1851,13 @@ int lkf_run(lkf_engine *e, void *stream) {
   HIPCHK(hipEventRecord(x.pulled, cs), "event");
   HIPCHK(hipStreamWaitEvent(ps, x.pulled, 0), "wait pull");
   if (e->useGraph) {
-    if (x.gPrepEpoch != e->epoch || !x.gPrep || x.gPrepFused != prepDone) {
-      const int rc = capture(ps, x.gPrep, prep);
+    const int fi = prepDone ? 1 : 0;
+    if (x.gPrepEpoch[fi] != e->epoch || !x.gPrep[fi]) {
+      const int rc = capture(ps, x.gPrep[fi], prep);
       if (rc) return rc;
-      x.gPrepEpoch = e->epoch;
-      x.gPrepFused = prepDone;
+      x.gPrepEpoch[fi] = e->epoch;
     }
-    HIPCHK(hipGraphLaunch(x.gPrep, ps), "prep graph");
+    HIPCHK(hipGraphLaunch(x.gPrep[fi], ps), "prep graph");
   } else {
     const int rc = prep();
     if (rc) return rc;
@@ -1866,7 +1869,7 @@ int lkf_run(lkf_engine *e, void *stream) {
     HIPCHK(hipMemcpy(u, x.dDDUsed, sizeof(u), hipMemcpyDeviceToHost), "debug copy");
     fprintf(stderr, "[lkf dd] run %llu ctx %d after prep: cursor %llu spill %llu graph %d epoch %llu/%llu\n",
             (unsigned long long)e->nRuns, ci, (unsigned long long)u[0], (unsigned long long)u[1], int(e->useGraph),
-            (unsigned long long)x.gPrepEpoch, (unsigned long long)e->epoch);
+            (unsigned long long)x.gPrepEpoch[prepDone ? 1 : 0], (unsigned long long)e->epoch);
   }
   HIPCHK(hipStreamWaitEvent(s, x.prepped, 0), "wait prep");
   DecideLaunch d;
@@ -4334,7 +4337,7 @@ int lkf_debug_dd_cursors(lkf_engine *e, uint64_t out[7]) {
 
 // Not part of include/lkfwd.h: a DD DownTrack's selector state for debugging
 // (out[16]: cache init, base, last, masks[8], chain broken bits, chain active
-// bits, sum of chain expectations, frame-number wrapper last, current layers
+// bits, frames the unbroken chains wait on, frame-number wrapper last, current layers
 // spatial | temporal << 8 (+128 each)).
 int lkf_debug_dd_state(lkf_engine *e, int32_t dt, uint64_t out[16]) {
   if (!e || !out || dt < 0 || size_t(dt) >= e->dtp.size() || !e->dDDState) return LKF_EINVAL;
@@ -4353,6 +4356,7 @@ int lkf_debug_dd_state(lkf_engine *e, int32_t dt, uint64_t out[16]) {
   out[12] = d.chActive & cm;
   uint64_t ex = 0;
   for (int c = 0; c < d.numChains; c++) {  // (the set's size: the ring's bits and the frame beyond it)
+    if ((d.chBroken >> c) & 1) continue;    // (a broken chain's set is inert until it is cleared)
     ex += d.expFar[c] ? 1 : 0;
     for (int w = 0; w < kDDExpWords; w++) ex += uint64_t(__builtin_popcountll(d.exp[c][w]));
   }

@@ -1544,8 +1544,11 @@ __device__ __forceinline__ void block_scan_excl(u64 &a, u64 &b, u64 &ta, u64 &tb
 constexpr u32 kScanStHead = 16;
 constexpr u32 kScanSpin = 1u << 22;  // polls before a look-back gives up (totals -> ~0: capacity errors)
 
-__device__ __forceinline__ void gr_put(u64 *g, u32 v) {
-  __hip_atomic_store(g, (1ull << 32) | u64(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// tag 1: the value; tag 2: poisoned (a look-back behind it gave up, so every
+// prefix built on it is wrong: tiles that read it publish poison in turn and
+// the last tile reports ~0 totals, a capacity error for the caller)
+__device__ __forceinline__ void gr_put(u64 *g, u32 v, u32 tag = 1) {
+  __hip_atomic_store(g, (u64(tag) << 32) | u64(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(SCAN_T) k_scan_1p(ScanIn in, u32 n, u32 nb, u64 *__restrict__ st,
@@ -1589,10 +1592,15 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_1p(ScanIn in, u32 n, u32 nb, u6
     for (u32 spins = 0;;) {
       const u64 x = lane < 8 ? __hip_atomic_load(gr + 8 * size_t(j) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                              : 0ull;
-      const u64 rdy = __ballot(lane < 8 && (x >> 32) == 1);
+      const u64 rdy = __ballot(lane < 8 && (x >> 32) != 0);
+      const u64 poison = __ballot(lane < 8 && (x >> 32) == 2);
       const u32 v = u32(x);
       if ((rdy & 0xF0) == 0xF0 || (rdy & 0x0F) == 0x0F) {
         const int o = (rdy & 0xF0) == 0xF0 ? 4 : 0;
+        if (poison & (0x0Full << o)) {  // built on a look-back that gave up
+          if (lane == 0) sBad = 1;
+          break;
+        }
         const u64 a = (u64(u32(__shfl(int(v), o + 1, 64))) << 32) | u32(__shfl(int(v), o, 64));
         const u64 b = (u64(u32(__shfl(int(v), o + 3, 64))) << 32) | u32(__shfl(int(v), o + 2, 64));
         pa += a;
@@ -1610,7 +1618,9 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_1p(ScanIn in, u32 n, u32 nb, u6
     }
     if (lane == 0) {
       const u64 ia = pa + TA, ib = pb + TB;
-      gr_put(g + 4, u32(ia)), gr_put(g + 5, u32(ia >> 32)), gr_put(g + 6, u32(ib)), gr_put(g + 7, u32(ib >> 32));
+      const u32 tag = sBad ? 2u : 1u;
+      gr_put(g + 4, u32(ia), tag), gr_put(g + 5, u32(ia >> 32), tag), gr_put(g + 6, u32(ib), tag),
+          gr_put(g + 7, u32(ib >> 32), tag);
       sPre[0] = pa;
       sPre[1] = pb;
     }
@@ -3580,8 +3590,8 @@ constexpr int PRE_MAX = 96;  // 12 + 4*15 CSRC + 12 extension block + 6 VP8 desc
 // (two-byte extension profile) = 343
 constexpr int PRE_MAX_DD = 352;
 
-#ifndef LKF_EMIT_U  // 16-B chunks per lane in flight per copy iteration (6 and 8 measured no faster at full occupancy, r4_ab_runs.txt)
-#define LKF_EMIT_U 4
+#ifndef LKF_EMIT_U  // 16-B chunks per lane in flight per copy iteration (6 with the round-6 residency cap;
+#define LKF_EMIT_U 6  // 4, 6 and 8 measured alike at full occupancy, r4_ab_runs.txt)
 #endif
 constexpr int EMIT_U = LKF_EMIT_U;
 
@@ -3653,14 +3663,23 @@ __device__ __forceinline__ void store16(u8 *p, uint4 v) {
 #ifndef LKF_EMIT_XCD  // (A/B) the XCD-aware group partition (1) or a plain grid-stride (0)
 #define LKF_EMIT_XCD 1
 #endif
-#ifndef LKF_EMIT_LDS  // (A/B) LDS per emit workgroup raised to this many bytes (0: as needed) -> fewer resident
-#define LKF_EMIT_LDS 0
+// Round 6: emit's resident workgroups capped through LDS.  With the
+// compiler's 6 waves per SIMD (24 one-wave workgroups per CU, 768 per XCD) the
+// payload lines that the DownTracks of one track re-read are evicted from the
+// XCD's 4 MiB L2 between their readers: exact read bytes (request counters by
+// size) 651 MB per configs[1] batch for 319 MB of payload.  Extra LDS per
+// workgroup bounds residency (A/B in one GPU call, profiles/r6_ab_runs.txt):
+// 12 per CU -> 524 MB at the same step time, 8 -> 449 MB but 3-5 % slower,
+// 4 -> 339 MB and 25 % slower.  (The DD instantiation is LDS-bound already.)
+#ifndef LKF_EMIT_LDS  // LDS per <96> workgroup raised by this many bytes (0: as needed)
+#define LKF_EMIT_LDS 5900
 #endif
 template <int PRE>
 __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
 #if LKF_EMIT_LDS
-  __shared__ u32 sPad[LKF_EMIT_LDS / 4];
-  if (threadIdx.x == 1023) sPad[blockIdx.x % (LKF_EMIT_LDS / 4)] = 0;  // (never: keeps the allocation)
+  constexpr u32 kPad = PRE == PRE_MAX ? LKF_EMIT_LDS / 4 : 1;
+  __shared__ u32 sPad[kPad];
+  if (threadIdx.x == 1023) sPad[blockIdx.x % kPad] = 0;  // (never: keeps the allocation)
 #endif
   __shared__ __attribute__((aligned(16))) u8 pre[EMIT_G][PRE];
   __shared__ u64 sSrc[EMIT_G];  // arena offset of the record's first payload byte after the prefix

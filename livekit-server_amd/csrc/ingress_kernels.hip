@@ -1573,8 +1573,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
 // arrival times), the nacks of one datagram are gathered by a sort of
 // (datagram, entry) events, and each such datagram's pairs are packed on a
 // lane of their own.  Otherwise the serial form below runs.
-constexpr u32 kNackFastN = 1024;  // datagrams of a stream the lane-parallel form stages
-constexpr u32 kNackFastEv = 512;  // nack events: at most MaxTries per entry (5 x 100)
+constexpr u32 kNackFastN = 512;  // datagrams of a stream the lane-parallel form stages (a 1-s video layer: ~300)
+constexpr u32 kNackFastEv = 256;  // nack events: at most MaxTries per entry (the form takes <= 51 entries)
 constexpr u32 kNackNone = 0xffffffffu;
 struct NackFastLds {
   i64 arr[kNackFastN];
@@ -1608,22 +1608,43 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
   u32 nPush = 0;
   bool mono = true;
   i64 prevArr = INT64_MIN;
-  for (u32 base = 0; base < nIdx; base += 64) {
+  // the datagrams' indices, then their descriptors, every chunk's loads in
+  // flight together (a chunk at a time waited two round trips per chunk)
+  constexpr u32 kCh = kNackFastN / 64;
+  u32 icv[kCh], stv[kCh], qfv[kCh];
+  i64 arv[kCh];
+#pragma unroll
+  for (u32 c = 0; c < kCh; c++) {
+    const u32 k = c * 64 + lane;
+    icv[c] = k < nIdx ? (useList ? lst[k] : pb + k) : 0u;
+  }
+#pragma unroll
+  for (u32 c = 0; c < kCh; c++) {
+    stv[c] = 0xffffffffu;
+    arv[c] = 0;
+    qfv[c] = 0;
+    if (c * 64 + lane < nIdx) {
+      stv[c] = raws[icv[c]].stream;
+      arv[c] = raws[icv[c]].arrival_ns;
+      qfv[c] = u32(q[icv[c]].flags) | (u32(q[icv[c]].sn) << 16);
+    }
+  }
+#pragma unroll
+  for (u32 c = 0; c < kCh; c++) {
+    const u32 base = c * 64;
+    if (base >= nIdx) break;
     const u32 k = base + lane;
     const bool v = k < nIdx;
-    u32 ic = 0, flg = 0;
+    u32 ic = icv[c], flg = 0;
     u16 sn = 0;
-    i64 arr = prevArr;
+    i64 arr = v ? arv[c] : prevArr;
     u64 L = 0, s0 = 0;
     if (v) {
-      ic = useList ? lst[k] : pb + k;
-      const lkf_raw_pkt rp = raws[ic];
-      arr = rp.arrival_ns;
-      if (rp.stream == sid) {
+      if (stv[c] == sid) {
         flg = 1;
-        if (q[ic].flags & IP_OK) {
+        if (qfv[c] & IP_OK) {
           flg |= 2;
-          sn = q[ic].sn;
+          sn = u16(qfv[c] >> 16);
           const lkf_flow f = flows[ic];
           if (f.flags & LKF_FLOW_HAS_LOSS) {
             flg |= 4;
@@ -1655,6 +1676,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
   }
   if (!mono) return false;
   const u32 M = count0 + u32(lossTot);
+  if (M * kNackMaxTries > kNackFastEv) return false;  // (more entries than the event list holds nacks of)
   if (lane == 0) F.pushOff[0] = 0;
   __syncthreads();
   // ---- the entries
@@ -1760,7 +1782,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
   }
   __syncthreads();
   const u32 E = F.nEv;
-  if (E > kNackFastEv) {  // (cannot happen: at most MaxTries nacks per entry)
+  if (E > kNackFastEv) {  // (cannot happen: at most MaxTries nacks per entry, M * MaxTries <= kNackFastEv)
     if (lane == 0) atomicOr(err, 8u);
     return true;
   }

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <thread>
+#include <map>
 #include <vector>
 
 #include "../include/lkfwd.h"
@@ -94,10 +95,16 @@ int orc_parity_run(const orc_bench_shard *shards, uint32_t nshards, uint32_t nth
         s0 += sh[k].nstreams;
       }
       cum[i] = c;
+      // key: (room, the DownTrack's ordinal among its room's DownTracks) — one
+      // per DownTrack (random SSRCs of different rooms can collide), the same
+      // ordinal a single trace of those rooms gives it (rooms generate alike)
+      std::map<uint32_t, uint32_t> ordOf;
       for (uint32_t d = 0; d < sh[i].ndts; d++) {
         uint8_t *r = dt + (d0 + d) * dtStride;
-        std::memcpy(r, &sh[i].dts[d].ssrc, 4);
-        std::memcpy(r + 4, &sh[i].dts[d].subscriber, 4);  // (SSRCs of different rooms can collide)
+        const uint32_t room = sh[i].tracks[sh[i].dts[d].track].room;
+        const uint32_t ord = ordOf[room]++;
+        std::memcpy(r, &room, 4);
+        std::memcpy(r + 4, &ord, 4);
         lkf_fwd_state fs{};
         lkf_sender_stats ss{};
         if (orc_get_state(e, int32_t(d), &fs) || orc_sender_stats_get(e, int32_t(d), &ss)) rc = -1;
@@ -108,6 +115,7 @@ int orc_parity_run(const orc_bench_shard *shards, uint32_t nshards, uint32_t nth
         for (uint32_t k = 0; k < sh[i].nstreams; k++) {
           uint8_t *r = st + (s0 + k) * stStride;
           std::memcpy(r, &sh[i].streams[k].ssrc, 4);
+          std::memcpy(r + 4, &sh[i].tracks[sh[i].streams[k].track].room, 4);  // (keyed by room and SSRC)
           lkf_stream_stats ts{};
           if (orc_stream_stats_get(e, int32_t(k), &ts)) rc = -1;
           std::memcpy(r + 8, &ts, sizeof(ts));
@@ -156,7 +164,7 @@ static int drive(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthre
     int r = 0;
     for (uint32_t t = 0; t < s.ntracks && !r; t++) r = orc_add_track(e, &s.tracks[t]) == int32_t(t) ? 0 : -1;
     for (uint32_t d = 0; d < s.ndts && !r; d++) r = orc_add_downtrack(e, &s.dts[d]) == int32_t(d) ? 0 : -1;
-    if (ingress)
+    if (ingress && s.streams)
       for (uint32_t k = 0; k < s.nstreams && !r; k++) r = orc_add_stream(e, &s.streams[k]) == int32_t(k) ? 0 : -1;
     if (r) rc = r;
   };
@@ -170,7 +178,7 @@ static int drive(const orc_bench_shard *shards, uint32_t nshards, uint32_t nthre
       const orc_bench_batch &x = s.batches[b];
       if (x.nev) r = orc_ctl_batch(e, x.ev, x.nev);
       if (r) break;
-      if (ingress) {
+      if (ingress && x.raws) {
         r = orc_ingest(e, x.raws, x.nraw, x.arena, x.alen);
         const lkf_pkt *p = nullptr;
         uint32_t n = 0;

@@ -5,6 +5,12 @@ import sys
 
 import pytest
 
+# torch before any engine library: the process then has one HIP runtime
+# (liblkfwd.so binds to the libamdhip64 torch loaded, as in bench.py, which
+# imports torch first).  A test process that loaded liblkfwd first left torch
+# on a second runtime that reported no GPU to the tests that use torch.
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
