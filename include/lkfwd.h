@@ -454,6 +454,16 @@ int lkf_drain(lkf_engine *e, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_
  * sticky error word (lkf_sync does).  LKF_EINVAL if that run does not exist. */
 int lkf_drain_run(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap,
                   uint64_t *n_out, uint64_t *arena_len);
+/* The same without waiting for the copies: the record count and byte length
+ * are read (after that run's emit stage), then the two device -> host copies
+ * are enqueued on the engine's copy stream and the call returns, so a caller's
+ * next lkf_submit (host -> device) crosses PCIe while they run — both
+ * directions at once.  `out` and `arena` must be page-locked and must not be
+ * read or reused before lkf_drain_wait returns. */
+int lkf_drain_run_async(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap,
+                        uint64_t *n_out, uint64_t *arena_len);
+/* Waits for every copy lkf_drain_run_async enqueued. */
+int lkf_drain_wait(lkf_engine *e);
 /* Device pointers of the output (zero-copy consumer, e.g. an SRTP stage). */
 int lkf_output_device(lkf_engine *e, const lkf_out **d_out, uint64_t *n_out, const uint8_t **d_arena,
                       uint64_t *arena_len);

@@ -305,6 +305,23 @@ class Engine:
         self._chk(f(self.h, age, out_ptr, cap, arena_ptr, arena_cap, C.byref(n), C.byref(alen)), "drain_run")
         return n.value, alen.value
 
+    def drain_run_async(self, age, out_ptr, cap, arena_ptr, arena_cap):
+        """lkf_drain_run_async into page-locked buffers: returns (records, bytes)
+        once the copies are enqueued; drain_wait() before reading them."""
+        n = C.c_uint64()
+        alen = C.c_uint64()
+        f = self.lib.lkf_drain_run_async
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        self._chk(f(self.h, age, out_ptr, cap, arena_ptr, arena_cap, C.byref(n), C.byref(alen)), "drain_run_async")
+        return n.value, alen.value
+
+    def drain_wait(self):
+        self.lib.lkf_drain_wait.restype = C.c_int
+        self.lib.lkf_drain_wait.argtypes = [C.c_void_p]
+        self._chk(self.lib.lkf_drain_wait(self.h), "drain_wait")
+
     def output_device(self):
         d_out = C.c_void_p()
         d_ar = C.c_void_p()

@@ -161,10 +161,11 @@ struct lkf_engine {
   int dev = 0;
   // LKF_HOST_PROF=1: wall time of lkf_run's host sections (printed by lkf_destroy)
   bool hostProf = false;
-  double hp[7] = {};  // pre, stage wait, csr build, launches, total, runs, staging copies
+  double hp[9] = {};  // pre, stage wait, csr build, launches, total, runs, staging copies; ingest total, ingests
   std::vector<uint32_t> fill;  // event CSR fill cursors
   std::vector<std::pair<uint32_t, uint32_t>> sortA, sortB;  // control-op radix sort (lane, index)
   hipStream_t own = nullptr;    // copies, lookups
+  hipStream_t d2hS = nullptr;   // lkf_drain_run_async's device -> host copies (created on first use)
   hipStream_t prepS = nullptr;  // ingest + batch preparation (high priority)
   // the ingests' stream (Buffer.calc): the prep stream.  A stream of its own
   // (ingest n+1 beside batch n's preparation; a run's preparation waits for its
@@ -313,7 +314,10 @@ struct lkf_engine {
 
   // three batch contexts: batch n+1 is ingested/prepared while batch n decides
   // and batch n-1 emits (its buffers are not reused until n+2)
-  static constexpr int kCtx = 3;
+#ifndef LKF_CTX  // batch contexts in flight (A/B)
+#define LKF_CTX 3
+#endif
+  static constexpr int kCtx = LKF_CTX;
   BatchCtx ctx[kCtx];
   uint64_t nRuns = 0;
   int lastCtx = -1;
@@ -918,13 +922,33 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
     A(hipExtStreamCreateWithCUMask(&e->emitS, words, mB.data()));
     A(hipExtStreamCreateWithCUMask(&e->sendS, words, mB.data()));
   } else {
-    A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, greatestPrio));
-    A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, greatestPrio));
+    // LKF_PRIO=<decide><prep><emit><sender> (A/B): h(igh) or l(ow) each;
+    // default "hhll" (the decide and prep chain ahead of emit for free CU slots)
+    const char *pr = getenv("LKF_PRIO");
+    auto prio = [&](int i, bool hi) { return (pr && int(strlen(pr)) > i) ? (pr[i] == 'h' ? greatestPrio : leastPrio)
+                                                                         : (hi ? greatestPrio : leastPrio); };
+    A(hipStreamCreateWithPriority(&e->decS, hipStreamNonBlocking, prio(0, true)));
+    A(hipStreamCreateWithPriority(&e->prepS, hipStreamNonBlocking, prio(1, true)));
     e->ingS = e->prepS;
-    A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, leastPrio));
-    A(hipStreamCreateWithPriority(&e->sendS, hipStreamNonBlocking, leastPrio));
+    A(hipStreamCreateWithPriority(&e->emitS, hipStreamNonBlocking, prio(2, false)));
+    A(hipStreamCreateWithPriority(&e->sendS, hipStreamNonBlocking, prio(3, false)));
   }
-  A(hipStreamCreateWithFlags(&e->sideS, hipStreamNonBlocking));
+  // LKF_SIDE_CUS=N (A/B): the NACK queues' side stream on N of every 32 CUs
+  // (the last N of each XCD's), so its long latency-bound waves leave the
+  // other CUs to emit; 0 (default): every CU
+  int sideCus = 0;
+  if (const char *v = getenv("LKF_SIDE_CUS")) sideCus = atoi(v);
+  if (sideCus > 0 && sideCus < 32) {
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device);
+    const uint32_t words = uint32_t((ncu + 31) / 32);
+    std::vector<uint32_t> m(words, 0);
+    for (int i = 0; i < ncu; i++)
+      if ((i % 32) >= 32 - sideCus) m[size_t(i / 32)] |= 1u << (i % 32);
+    A(hipExtStreamCreateWithCUMask(&e->sideS, words, m.data()));
+  } else {
+    A(hipStreamCreateWithFlags(&e->sideS, hipStreamNonBlocking));
+  }
   A(hipEventCreateWithFlags(&e->inEv, hipEventDisableTiming));
   A(hipEventCreateWithFlags(&e->bktEv, hipEventDisableTiming));
   A(hipEventCreateWithFlags(&e->sideFork, hipEventDisableTiming));
@@ -1090,6 +1114,9 @@ void lkf_destroy(lkf_engine *e) {
             "lkf host ms/run: pre %.4f stage-wait %.4f csr %.4f copies %.4f launches %.4f total %.4f (%d runs)\n",
             e->hp[0] / e->hp[5], e->hp[1] / e->hp[5], e->hp[2] / e->hp[5], e->hp[6] / e->hp[5],
             e->hp[3] / e->hp[5], e->hp[4] / e->hp[5], int(e->hp[5]));
+  if (e->hostProf && e->hp[8] > 0)
+    fprintf(stderr, "lkf host ms/ingest: %.4f (%d ingests: the launches of the Buffer.calc chain, no host wait)\n",
+            e->hp[7] / e->hp[8], int(e->hp[8]));
   (void)hipSetDevice(e->dev);
   if (e->cur && e->cur != e->own) (void)hipStreamSynchronize(e->cur);
   if (e->own) (void)hipStreamSynchronize(e->own);
@@ -1099,6 +1126,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->emitS) (void)hipStreamSynchronize(e->emitS);
   if (e->sendS) (void)hipStreamSynchronize(e->sendS);  // (bucket copies, sender updates)
   if (e->sideS) (void)hipStreamSynchronize(e->sideS);  // (NACK queues)
+  if (e->d2hS) (void)hipStreamSynchronize(e->d2hS);    // (asynchronous drains)
   (void)hipDeviceSynchronize();                        // (anything else queued before the buffers go)
   for (void *p : {static_cast<void *>(e->dNacks), static_cast<void *>(e->dNackG), static_cast<void *>(e->dNackValid),
                   static_cast<void *>(e->dRtx), static_cast<void *>(e->dRtxSrc), static_cast<void *>(e->dRtxLen),
@@ -1191,6 +1219,7 @@ void lkf_destroy(lkf_engine *e) {
   if (e->prepS) (void)hipStreamDestroy(e->prepS);
   if (e->ingS && e->ingS != e->prepS) (void)hipStreamDestroy(e->ingS);
   if (e->own) (void)hipStreamDestroy(e->own);
+  if (e->d2hS) (void)hipStreamDestroy(e->d2hS);
   delete e;
 }
 
@@ -2223,6 +2252,41 @@ int lkf_drain_run(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8
     const int r = copy_to_host(e, arena, x.dOutArena, tot[3], "drain bytes");
     if (r) return r;
   }
+  return LKF_OK;
+}
+
+int lkf_drain_run_async(lkf_engine *e, uint32_t age, lkf_out *out, uint64_t cap, uint8_t *arena, uint64_t arena_cap,
+                        uint64_t *n_out, uint64_t *arena_len) {
+  if (!e || age >= uint32_t(lkf_engine::kCtx) || uint64_t(age) >= e->nRuns) return LKF_EINVAL;
+  HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
+  if (!e->d2hS) HIPCHK(hipStreamCreateWithFlags(&e->d2hS, hipStreamNonBlocking), "copy stream");
+  BatchCtx &x = e->ctx[(e->nRuns - 1 - age) % lkf_engine::kCtx];
+  HIPCHK(hipEventSynchronize(x.emitted), "wait emitted");
+  uint64_t tot[4];
+  D2H(tot, x.dTot, sizeof(tot), "tot copy");
+  if (n_out) *n_out = tot[2];
+  if (arena_len) *arena_len = tot[3];
+  if (tot[2] > e->cfg.max_out_pkts || tot[3] > e->cfg.max_out_bytes) {  // (see lkf_output_device)
+    e->err = "output or tuple capacity exceeded";
+    return LKF_ENOSPC;
+  }
+  if (tot[2] > cap || tot[3] > arena_cap) return LKF_ENOSPC;
+  // (the context is reused only after run n + 3 is enqueued, which the caller
+  // does after lkf_drain_wait: the source stays valid while the copies run)
+  if (out && tot[2]) {
+    CHKRANGE(x.dOut, tot[2] * sizeof(lkf_out), "async d2h");
+    HIPCHK(hipMemcpyAsync(out, x.dOut, tot[2] * sizeof(lkf_out), hipMemcpyDeviceToHost, e->d2hS), "drain recs");
+  }
+  if (arena && tot[3]) {
+    CHKRANGE(x.dOutArena, tot[3], "async d2h");
+    HIPCHK(hipMemcpyAsync(arena, x.dOutArena, tot[3], hipMemcpyDeviceToHost, e->d2hS), "drain bytes");
+  }
+  return LKF_OK;
+}
+
+int lkf_drain_wait(lkf_engine *e) {
+  if (!e) return LKF_EINVAL;
+  if (e->d2hS) HIPCHK(hipStreamSynchronize(e->d2hS), "copy stream sync");
   return LKF_OK;
 }
 
@@ -3837,12 +3901,18 @@ int lkf_ingest(lkf_engine *e, const lkf_raw_pkt *pkts, uint32_t n, const uint8_t
 int lkf_ingest_device(lkf_engine *e, const lkf_raw_pkt *d_pkts, uint32_t n, const uint8_t *d_raw, uint64_t raw_len) {
   if (!e || (n && (!d_pkts || !d_raw))) return LKF_EINVAL;
   if (n > e->cfg.max_batch_pkts) return LKF_ENOSPC;
+  const auto t0 = std::chrono::steady_clock::now();
   int rc = flush_topology(e);
   if (rc) return rc;
   HIPCHK(hipSetDevice(e->dev), "hipSetDevice");
   BatchCtx &x = e->ctx[e->nRuns % lkf_engine::kCtx];
   if (x.used) HIPCHK(hipStreamWaitEvent(e->ingS, x.emitted, 0), "wait emit");
-  return ingest_common(e, x, d_pkts, n, d_raw, raw_len);
+  rc = ingest_common(e, x, d_pkts, n, d_raw, raw_len);
+  if (e->hostProf) {
+    e->hp[7] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    e->hp[8] += 1;
+  }
+  return rc;
 }
 
 int lkf_ingest_flows(lkf_engine *e, lkf_flow *out, uint32_t cap, uint32_t *n_out) {

@@ -1456,7 +1456,10 @@ __global__ void k_track_ranges(const RunDesc *__restrict__ desc, u32 ntracks, u3
 // Value = (a, b) u64 pairs; mode selects how the input is formed.
 // ---------------------------------------------------------------------------
 constexpr int SCAN_T = 256;
-constexpr int SCAN_ITEMS = 4;
+#ifndef LKF_SCAN_ITEMS  // items per thread (tile = 256 x this): fewer tiles, a shorter look-back chain
+#define LKF_SCAN_ITEMS 4
+#endif
+constexpr int SCAN_ITEMS = LKF_SCAN_ITEMS;
 constexpr int SCAN_TILE = SCAN_T * SCAN_ITEMS;
 
 struct ScanIn {

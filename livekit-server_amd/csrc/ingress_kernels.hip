@@ -1576,6 +1576,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
 constexpr u32 kNackFastN = 512;  // datagrams of a stream the lane-parallel form stages (a 1-s video layer: ~300)
 constexpr u32 kNackFastEv = 256;  // nack events: at most MaxTries per entry (the form takes <= 51 entries)
 constexpr u32 kNackNone = 0xffffffffu;
+constexpr u32 kNackHash = 256;
 struct NackFastLds {
   i64 arr[kNackFastN];
   u16 sn[kNackFastN];
@@ -1590,6 +1591,7 @@ struct NackFastLds {
   u32 pushK[kNackCap], pushOff[kNackCap + 1];
   u16 pushS0[kNackCap];
   u32 key[kNackFastEv];  // nack events: datagram << 7 | entry
+  u8 hash[256];          // entry by SN (kNackHash slots)
   u32 gStart[kNackFastEv + 1];
   u32 gNp[kNackFastEv], gOff[kNackFastEv];
   lkf_nack_pair stage[kNackFastEv];
@@ -1611,8 +1613,9 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
   // the datagrams' indices, then their descriptors, every chunk's loads in
   // flight together (a chunk at a time waited two round trips per chunk)
   constexpr u32 kCh = kNackFastN / 64;
-  u32 icv[kCh], stv[kCh], qfv[kCh];
+  u32 icv[kCh], stv[kCh], qfv[kCh], ffv[kCh];
   i64 arv[kCh];
+  u64 lsv[kCh], lev[kCh];
 #pragma unroll
   for (u32 c = 0; c < kCh; c++) {
     const u32 k = c * 64 + lane;
@@ -1623,10 +1626,20 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     stv[c] = 0xffffffffu;
     arv[c] = 0;
     qfv[c] = 0;
+    ffv[c] = 0;
     if (c * 64 + lane < nIdx) {
       stv[c] = raws[icv[c]].stream;
       arv[c] = raws[icv[c]].arrival_ns;
       qfv[c] = u32(q[icv[c]].flags) | (u32(q[icv[c]].sn) << 16);
+      ffv[c] = flows[icv[c]].flags;
+    }
+  }
+#pragma unroll
+  for (u32 c = 0; c < kCh; c++) {  // the loss ranges (a loss datagram's flow), all chunks in flight
+    lsv[c] = lev[c] = 0;
+    if (c * 64 + lane < nIdx && stv[c] == sid && (qfv[c] & IP_OK) && (ffv[c] & LKF_FLOW_HAS_LOSS)) {
+      lsv[c] = flows[icv[c]].loss_start;
+      lev[c] = flows[icv[c]].loss_end;
     }
   }
 #pragma unroll
@@ -1635,7 +1648,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     if (base >= nIdx) break;
     const u32 k = base + lane;
     const bool v = k < nIdx;
-    u32 ic = icv[c], flg = 0;
+    u32 flg = 0;
     u16 sn = 0;
     i64 arr = v ? arv[c] : prevArr;
     u64 L = 0, s0 = 0;
@@ -1645,11 +1658,10 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
         if (qfv[c] & IP_OK) {
           flg |= 2;
           sn = u16(qfv[c] >> 16);
-          const lkf_flow f = flows[ic];
-          if (f.flags & LKF_FLOW_HAS_LOSS) {
+          if (ffv[c] & LKF_FLOW_HAS_LOSS) {
             flg |= 4;
-            s0 = f.loss_start;
-            L = f.loss_end - f.loss_start;
+            s0 = lsv[c];
+            L = lev[c] - lsv[c];
           }
         }
       }
@@ -1711,26 +1723,39 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     __syncthreads();
   }
   __syncthreads();
-  // distinct SNs (Remove takes the first entry with an SN: equal SNs need the serial form)
+  // the entries by SN in an LDS hash (256 slots, linear probing: at most 51
+  // entries); an SN already there means equal SNs, which Remove's "first
+  // entry with that SN" leaves to the serial form
+  for (u32 i = lane; i < kNackHash; i += 64) F.hash[i] = 0xffu;
+  __syncthreads();
   bool dup = false;
-  for (u32 e = lane; e < M; e += 64)
-    for (u32 f = 0; f < e; f++) dup = dup || F.eSn[f] == F.eSn[e];
+  if (lane == 0)
+    for (u32 e = 0; e < M && !dup; e++) {
+      u32 h = (u32(F.eSn[e]) * 0x9E37u >> 8) & (kNackHash - 1);
+      while (F.hash[h] != 0xffu && !dup) {
+        dup = F.eSn[F.hash[h]] == F.eSn[e];
+        h = (h + 1) & (kNackHash - 1);
+      }
+      F.hash[h] = u8(e);
+    }
   if (__ballot(dup)) return false;
-  // Remove: the first datagram (from the entry's birth on) that carries its SN
+  __syncthreads();
+  // Remove: the first datagram (from the entry's birth on) that carries its SN,
+  // a probe of the hash per datagram and an LDS minimum per entry
   for (u32 base = 0; base < nIdx; base += 64) {
     const u32 k = base + lane;
-    const bool upd = k < nIdx && (F.fl[k] & 2);
-    const u16 sn = upd ? F.sn[k] : 0;
-    for (u32 e = 0; e < M; e++) {
-      const u32 st = u32(F.eBirth[e] + 1);
-      const u64 m = __ballot(upd && sn == F.eSn[e] && k >= st);
-      if (m && F.eRem[e] == kNackNone) {
-        __syncthreads();
-        if (lane == 0) F.eRem[e] = base + u32(__ffsll((long long)m) - 1);
-        __syncthreads();
+    if (k < nIdx && (F.fl[k] & 2)) {
+      const u16 sn = F.sn[k];
+      for (u32 h = (u32(sn) * 0x9E37u >> 8) & (kNackHash - 1); F.hash[h] != 0xffu; h = (h + 1) & (kNackHash - 1)) {
+        const u32 e = F.hash[h];
+        if (F.eSn[e] == sn) {
+          if (k >= u32(F.eBirth[e] + 1)) atomicMin(&F.eRem[e], k);
+          break;
+        }
       }
     }
   }
+  __syncthreads();
   if (lane == 0) F.nEv = 0;
   __syncthreads();
   // ---- each entry's life
