@@ -431,6 +431,7 @@ struct lkf_engine {
     uint32_t *fwd = nullptr, *tBegin = nullptr, *tEnd = nullptr, *list = nullptr, *listCnt = nullptr;
     uint32_t *nackInfo = nullptr, *nackPairOff = nullptr, *nackPairCnt = nullptr;
     lkf_nack_pair *nackPairs = nullptr;
+    NackIn *nackIn = nullptr;  // the NACK kernel's per-datagram input, in list order
   } ing[2];
   int ingPar = 0;
   // NACK queues (allocated with the first stream that has one) and the last
@@ -834,11 +835,18 @@ static int flush_topology(lkf_engine *e) {
       HIPCHK(dalloc(&e->dNack, e->maxStreams), "alloc nack queues");
       HIPCHK(hipMemset(e->dNack, 0, size_t(e->maxStreams) * sizeof(NackState)), "nack queues reset");
       e->nackPairCap = uint32_t(std::min<uint64_t>(uint64_t(c.max_batch_pkts) * 8 + 4096, 1u << 30));
+      // + every stream's block for the lane-parallel form (kernels.h kNackFastPairs)
+      const uint64_t pairsAll = uint64_t(e->nackPairCap) + uint64_t(e->maxStreams) * kNackFastPairs;
+      if (pairsAll >= (1ull << 32)) {
+        e->err = "too many streams for the NACK pair buffer";
+        return LKF_ENOSPC;
+      }
       for (auto &g : e->ing) {
         HIPCHK(dalloc(&g.nackInfo, c.max_batch_pkts), "alloc nack info");
         HIPCHK(dalloc(&g.nackPairOff, c.max_batch_pkts), "alloc nack pair offsets");
         HIPCHK(dalloc(&g.nackPairCnt, 1), "alloc nack pair count");
-        HIPCHK(dalloc(&g.nackPairs, e->nackPairCap), "alloc nack pairs");
+        HIPCHK(dalloc(&g.nackPairs, pairsAll), "alloc nack pairs");
+        HIPCHK(dalloc(&g.nackIn, 3 * size_t(c.max_batch_pkts) + 64), "alloc nack inputs");
         HIPCHK(hipMemset(g.nackInfo, 0, size_t(c.max_batch_pkts) * sizeof(uint32_t)), "nack info reset");
         HIPCHK(hipMemset(g.nackPairCnt, 0, sizeof(uint32_t)), "nack count reset");
       }
@@ -853,7 +861,7 @@ static int flush_topology(lkf_engine *e) {
       HIPCHK(dalloc(&e->dNackPartA, npart), "alloc nack scan state");
       HIPCHK(hipMemset(e->dNackPartA, 0, npart * sizeof(uint64_t)), "nack scan state reset");
       HIPCHK(dalloc(&e->dNackOut, c.max_batch_pkts), "alloc nack records");
-      HIPCHK(dalloc(&e->dNackPairsOut, e->nackPairCap), "alloc nack pairs out");
+      HIPCHK(dalloc(&e->dNackPairsOut, pairsAll), "alloc nack pairs out");
     }
     if (e->dNack) {  // each new queue: empty, the stream's initial RTT (0: defaultRtt)
       for (size_t i = 0; i < k; i++) {
@@ -1210,7 +1218,8 @@ void lkf_destroy(lkf_engine *e) {
     for (void *p : {static_cast<void *>(g.parsed), static_cast<void *>(g.flows), static_cast<void *>(g.fwd),
                     static_cast<void *>(g.tBegin), static_cast<void *>(g.tEnd), static_cast<void *>(g.list),
                     static_cast<void *>(g.listCnt), static_cast<void *>(g.nackInfo), static_cast<void *>(g.nackPairOff),
-                    static_cast<void *>(g.nackPairCnt), static_cast<void *>(g.nackPairs)})
+                    static_cast<void *>(g.nackPairCnt), static_cast<void *>(g.nackPairs),
+                    static_cast<void *>(g.nackIn)})
       if (p) (void)dfree(p);
   if (e->sideS && e->sideS != e->sendS) (void)hipStreamDestroy(e->sideS);
   if (e->emitS) (void)hipStreamDestroy(e->emitS);
@@ -3797,6 +3806,7 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
   a.nackPairCnt = e->dNackPairCnt;
   a.nackPairs = e->dNackPairs;
   a.nackPairCap = e->nackPairCap;
+  a.nackIn = e->ing[e->ingPar].nackIn;
   BucketLaunch bl;
   if (e->bktSlots && e->bktStorePending) {  // a second ingest before lkf_run: the first one's copies read this
                                             // context's store list first

@@ -24,6 +24,9 @@
 //   k_speakers     one wave per room, lane per participant: loudest active
 //                  microphone (AudioLevel.GetLevel audiolevel.go:105-112,
 //                  uptrackmanager.go:422-436), rank, quantise (room.go:254-279)
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include "../../include/lkfwd.h"
@@ -1046,7 +1049,7 @@ __device__ __forceinline__ void rx_jitter(StreamHot &h, u32 clockRate, u64 ets, 
 // per-lane copies put them on every lane's private stack — 400 B of scratch a
 // lane, written by every wave of the stream kernel, r4's tick WRITE_SIZE)
 template <int HS>
-__device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream *sg,
+__device__ __noinline__ lkf_flow ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, const DevStream *sg,
                                          const IngParsed *pg, const lkf_raw_pkt *rg, u32 ic, lkf_flow *flows,
                                          u32 *fwd, IngDD *ingDD, const u8 *raw, DDIngState *dds,
                                          DDStruct *ddStructs, u32 *err, const BktCtx *bkg, bool bkOn, u32 *gap) {
@@ -1173,13 +1176,14 @@ __device__ __noinline__ void ing_step(StreamHot &h, u64 *hs, RangeEntry *ring, c
   flows[ic] = f;
   fwd[ic] = forward;
   if (ingDD) ingDD[ic] = dv;
+  return f;
 }
 
 // The datagrams of a closed stream (lkf_remove_track): not handled, no state
 // change, no ExtPacket (lanes first, first + step, ...)
 __device__ void closed_flows(const DevStream &s, u32 sid, u32 pb, u32 pe, const lkf_raw_pkt *raws, lkf_flow *flows,
                              u32 *fwd, IngDD *ingDD, const u32 *list, const u32 *cnt, u32 stride, u32 first,
-                             u32 step) {
+                             u32 step, NackIn *nackIn) {
   const bool useList = s.layer < 3;
   const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
   const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
@@ -1192,6 +1196,7 @@ __device__ void closed_flows(const DevStream &s, u32 sid, u32 pb, u32 pe, const 
     flows[ic] = f;
     fwd[ic] = 0;
     if (ingDD) ingDD[ic] = IngDD{};
+    if (nackIn && useList) nackIn[size_t(lst - list) + k] = NackIn{raws[ic].arrival_ns, sid, 0u, 0u, 0u};
   }
 }
 
@@ -1225,6 +1230,13 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
   return v;
 }
 
+// a datagram's NackIn word: its SN, whether updateStreamState ran, whether it
+// pushes a loss range
+__device__ __forceinline__ u32 nk_snfl(const IngParsed &p, const lkf_flow &f) {
+  const bool ok = (p.flags & IP_OK) != 0;
+  return u32(p.sn) | ((ok ? 2u : 0u) | (ok && (f.flags & LKF_FLOW_HAS_LOSS) ? 4u : 0u)) << 16;
+}
+
 // Two instantiations: <false> for the streams without a dependency-descriptor
 // parser, <true> (launched only when DD streams exist) for those with one,
 // whose DependencyDescriptorParser + FrameIntegrityChecker state (3.3 KB) is
@@ -1240,7 +1252,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
     const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows,
     u32 *__restrict__ fwd, const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
     IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list, const u32 *__restrict__ cnt, u32 stride,
-    BktArgs bka, u32 *__restrict__ rxGap) {
+    BktArgs bka, u32 *__restrict__ rxGap, NackIn *__restrict__ nackIn) {
   static_assert(kHistWords == 64, "one history word per lane");
   static_assert(sizeof(StreamHot) == 64 * sizeof(u32), "one StreamHot dword per lane");
   __shared__ u64 sHist[kHistWords];
@@ -1255,7 +1267,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
   if (pb >= pe) return;
   if (s.closed) {  // Buffer.Close: Write returns io.EOF, nothing is processed
-    closed_flows(s, sid, pb, pe, raws, flows, fwd, ingDD, list, cnt, stride, lane, 64);
+    closed_flows(s, sid, pb, pe, raws, flows, fwd, ingDD, list, cnt, stride, lane, 64, nackIn);
     return;
   }
   u64 *const hg = hist + size_t(sid) * kHistWords;
@@ -1316,6 +1328,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
       rp = raws[ic];
     }
     const u32 m = min(64u, nIdx - j);
+    u32 nkSnFl = 0, nkS0 = 0, nkLen = 0;  // this lane's NackIn (its datagram's flow)
     for (u32 pos = 0; pos < m;) {
     const u32 need = S_INIT | S_SN_INIT | S_TS_INIT;
     const bool stateOk = runStream && (sh.flags & need) == need && sh.rmOpenStart <= sh.snExtHighest + 1;
@@ -1347,9 +1360,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
     }
     const u32 end = bad ? u32(__ffsll(static_cast<long long>(bad)) - 1) : 64u;  // the run is [pos, end)
     if (end == pos) {  // the datagram at pos through the serial Buffer.calc step
-      if (lane == pos && rp.stream == sid)
-        ing_step<1>(sh, sHist, ring, streams + sid, q + ic, raws + ic, ic, flows, fwd, ingDD, raw, dds, ddStructs, err,
-                    &sBk, bkOn, gap);
+      if (lane == pos && rp.stream == sid) {
+        const lkf_flow fo = ing_step<1>(sh, sHist, ring, streams + sid, q + ic, raws + ic, ic, flows, fwd, ingDD, raw,
+                                        dds, ddStructs, err, &sBk, bkOn, gap);
+        nkSnFl = nk_snfl(p, fo);
+        nkS0 = u32(u16(fo.loss_start));
+        nkLen = u32(min<u64>(fo.loss_end - fo.loss_start, 0xffffffffull));
+      }
       __syncthreads();
       pos++;
       continue;
@@ -1440,6 +1457,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
       const bool failed = (ddFail >> lane) & 1;
       if (failed) f.flags = u8((f.flags & ~LKF_FLOW_FORWARD) | LKF_FLOW_BAD);
       flows[ic] = f;
+      nkSnFl = nk_snfl(p, f);
+      nkS0 = u32(u16(f.loss_start));
+      nkLen = u32(min<u64>(f.loss_end - f.loss_start, 0xffffffffull));
       fwd[ic] = failed ? 0u : 1u;
       if (ingDD && !ddLane) ingDD[ic] = IngDD{};
       if (bkOn) {  // the run's pushes: this lane's skipped slots invalidated, then its own
@@ -1528,6 +1548,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
     __syncthreads();
     pos = end;
     }
+    // (every stream writes its own, NACK queue or not: a list may hold another
+    // stream's datagrams, which only that stream's wave writes)
+    if (nackIn && useList && in && rp.stream == sid)
+      nackIn[size_t(lst - list) + k] = NackIn{rp.arrival_ns, sid, nkSnFl, nkS0, nkLen};
   }
   if (sHist[lane] != hist0) hg[lane] = sHist[lane];
   const u32 hot1 = reinterpret_cast<const u32 *>(&sh)[lane];
@@ -1573,8 +1597,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
 // arrival times), the nacks of one datagram are gathered by a sort of
 // (datagram, entry) events, and each such datagram's pairs are packed on a
 // lane of their own.  Otherwise the serial form below runs.
-constexpr u32 kNackFastN = 512;  // datagrams of a stream the lane-parallel form stages (a 1-s video layer: ~300)
-constexpr u32 kNackFastEv = 256;  // nack events: at most MaxTries per entry (the form takes <= 51 entries)
+#ifndef LKF_NACK_N
+#define LKF_NACK_N 512
+#endif
+constexpr u32 kNackFastN = LKF_NACK_N;  // datagrams of a stream the lane-parallel form stages (a 1-s video layer: ~300)
+constexpr u32 kNackFastEv = kNackFastPairs;  // nack events: at most MaxTries per entry (the form takes <= 51 entries)
 constexpr u32 kNackNone = 0xffffffffu;
 constexpr u32 kNackHash = 256;
 struct NackFastLds {
@@ -1584,62 +1611,126 @@ struct NackFastLds {
   u8 fl[kNackFastN];  // 1 mine, 2 updateStreamState ran, 4 a loss range
   // entries (queue order: the queue at the start, then every pushed SN in push order)
   i64 eLast[kNackSlots];
-  u32 eRem[kNackSlots], eDeath[kNackSlots];
-  i32 eBirth[kNackSlots];
+  u32 eRem[kNackSlots];
+  u16 eDeath[kNackSlots];  // 0xffff: still queued
+  int16_t eBirth[kNackSlots];  // the pushing datagram, -1: queued before the ingest
   u16 eSn[kNackSlots];
   u8 eTries[kNackSlots];
-  u32 pushK[kNackCap], pushOff[kNackCap + 1];
+  u16 pushK[kNackCap], pushOff[kNackCap + 1];
   u16 pushS0[kNackCap];
-  u32 key[kNackFastEv];  // nack events: datagram << 7 | entry
+  u16 key[kNackFastEv];  // nack events: datagram << 7 | entry (0xffff: none)
   u8 hash[256];          // entry by SN (kNackHash slots)
-  u32 gStart[kNackFastEv + 1];
-  u32 gNp[kNackFastEv], gOff[kNackFastEv];
+  u16 gStart[kNackFastEv + 1];
+  u16 gNp[kNackFastEv], gOff[kNackFastEv];
   lkf_nack_pair stage[kNackFastEv];
   u32 nEv;
 };
-static_assert(kNackSlots <= 128 && kNackFastN <= 1024, "event keys hold 7 bits of entry, 10 of datagram");
+static_assert(kNackSlots <= 128 && kNackFastN <= 512 && kNackFastEv / kNackMaxTries < 127,
+              "16-bit event keys: 9 bits of datagram, 7 of entry, below the 0xffff pad");
 
+#ifndef LKF_NACK_DBG  // (diagnosis builds: print why a stream takes the serial form)
+#define LKF_NACK_DBG 0
+#endif
+#define NF_DECLINE(code)                                                                                 \
+  do {                                                                                                   \
+    if (LKF_NACK_DBG == 1 && lane == 0) printf("nack serial sid=%u why=%d nIdx=%u count0=%u\n", sid, code, nIdx, count0); \
+    return false;                                                                                        \
+  } while (0)
+#if LKF_NACK_DBG == 2  // per-wave phase stamps (wall clock, 100 MHz), read by lkf_debug_nack_stamps
+constexpr u32 kNackStampCap = 1u << 16;
+__device__ u64 gNackStamp[size_t(kNackStampCap) * 7];
+#else
+constexpr u32 kNackStampCap = 0;
+__device__ u64 *const gNackStamp = nullptr;
+#endif
+// a wave's stamp record (lane 0; nullptr in production builds), its entry time stored
+__device__ __forceinline__ u64 *nack_stamp(u32 lane, u32 sid, u64 tEntry) {
+  if (LKF_NACK_DBG != 2 || sid >= kNackStampCap) return nullptr;
+  u64 *r = gNackStamp + size_t(sid) * 7;  // (by stream: no shared counter to perturb the timing)
+  if (lane == 0) r[1] = tEntry;
+  return r;
+}
 __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 count0, u32 rtt, u32 nIdx,
-                          const u32 *lst, bool useList, u32 pb, const lkf_raw_pkt *__restrict__ raws,
-                          const IngParsed *__restrict__ q, const lkf_flow *__restrict__ flows, u32 *__restrict__ info,
+                          const u32 *lst, bool useList, u32 pb, const NackIn *__restrict__ nk,
+                          const lkf_raw_pkt *__restrict__ raws, const IngParsed *__restrict__ q,
+                          const lkf_flow *__restrict__ flows, u32 *__restrict__ info,
                           u32 *__restrict__ pairOff, u32 *pairCnt, lkf_nack_pair *__restrict__ pairs, u32 pairCap,
-                          u32 *err) {
-  if (nIdx > kNackFastN || count0 > u32(kNackCap)) return false;
+                          u32 *err, u64 *stamp) {
+  // (LKF_NACK_DBG 2: the wave's phase stamps, stored as they are taken)
+#define NF_STAMP(w)                                                    \
+  do {                                                                 \
+    if (LKF_NACK_DBG == 2 && lane == 0 && stamp) stamp[w] = wall_clock64(); \
+  } while (0)
+  if (nIdx > kNackFastN || count0 * kNackMaxTries > kNackFastEv) NF_DECLINE(1);
+  // the queue's entries (at most 51: one per lane), loaded beside the datagrams
+  static_assert(kNackFastEv / kNackMaxTries <= 64, "one queued entry per lane");
+  u32 q0sn = 0, q0tries = 0;
+  i64 q0last = 0;
+  if (lane < count0) {
+    q0sn = g->sn[lane];
+    q0tries = g->tries[lane];
+    q0last = g->last[lane];
+  }
   // ---- the stream's datagrams, and its pushes
   u64 lossTot = 0;
   u32 nPush = 0;
   bool mono = true;
   i64 prevArr = INT64_MIN;
-  // the datagrams' indices, then their descriptors, every chunk's loads in
-  // flight together (a chunk at a time waited two round trips per chunk)
+  // every chunk's loads in flight together (a chunk at a time waited a round
+  // trip per chunk): the stream kernel's NackIn records, contiguous in list
+  // order, or (no records: a stream without a list) the datagram's index, then
+  // its raw, parsed and flow entries
   constexpr u32 kCh = kNackFastN / 64;
-  u32 icv[kCh], stv[kCh], qfv[kCh], ffv[kCh];
+  u32 stv[kCh], sfv[kCh];  // stream; SN | (2 parsed, 4 loss) << 16
   i64 arv[kCh];
-  u64 lsv[kCh], lev[kCh];
+  u64 s0v[kCh], lnv[kCh];
+  if (nk) {
 #pragma unroll
-  for (u32 c = 0; c < kCh; c++) {
-    const u32 k = c * 64 + lane;
-    icv[c] = k < nIdx ? (useList ? lst[k] : pb + k) : 0u;
-  }
-#pragma unroll
-  for (u32 c = 0; c < kCh; c++) {
-    stv[c] = 0xffffffffu;
-    arv[c] = 0;
-    qfv[c] = 0;
-    ffv[c] = 0;
-    if (c * 64 + lane < nIdx) {
-      stv[c] = raws[icv[c]].stream;
-      arv[c] = raws[icv[c]].arrival_ns;
-      qfv[c] = u32(q[icv[c]].flags) | (u32(q[icv[c]].sn) << 16);
-      ffv[c] = flows[icv[c]].flags;
+    for (u32 c = 0; c < kCh; c++) {
+      const u32 k = c * 64 + lane;
+      stv[c] = 0xffffffffu;
+      arv[c] = 0;
+      sfv[c] = 0;
+      s0v[c] = lnv[c] = 0;
+      if (k < nIdx) {
+        const NackIn r = nk[k];
+        stv[c] = r.stream;
+        arv[c] = r.arrival;
+        sfv[c] = r.snFl;
+        s0v[c] = r.s0;
+        lnv[c] = r.len;
+      }
     }
-  }
+  } else {
+    u32 icv[kCh], ffv[kCh];
 #pragma unroll
-  for (u32 c = 0; c < kCh; c++) {  // the loss ranges (a loss datagram's flow), all chunks in flight
-    lsv[c] = lev[c] = 0;
-    if (c * 64 + lane < nIdx && stv[c] == sid && (qfv[c] & IP_OK) && (ffv[c] & LKF_FLOW_HAS_LOSS)) {
-      lsv[c] = flows[icv[c]].loss_start;
-      lev[c] = flows[icv[c]].loss_end;
+    for (u32 c = 0; c < kCh; c++) {
+      const u32 k = c * 64 + lane;
+      icv[c] = k < nIdx ? (useList ? lst[k] : pb + k) : 0u;
+    }
+#pragma unroll
+    for (u32 c = 0; c < kCh; c++) {
+      stv[c] = 0xffffffffu;
+      arv[c] = 0;
+      sfv[c] = 0;
+      ffv[c] = 0;
+      if (c * 64 + lane < nIdx) {
+        stv[c] = raws[icv[c]].stream;
+        arv[c] = raws[icv[c]].arrival_ns;
+        const IngParsed &pq = q[icv[c]];
+        sfv[c] = u32(pq.sn) | ((pq.flags & IP_OK) ? 2u << 16 : 0u);
+        ffv[c] = flows[icv[c]].flags;
+      }
+    }
+#pragma unroll
+    for (u32 c = 0; c < kCh; c++) {  // the loss ranges (a loss datagram's flow), all chunks in flight
+      s0v[c] = lnv[c] = 0;
+      if (c * 64 + lane < nIdx && stv[c] == sid && (sfv[c] & (2u << 16)) && (ffv[c] & LKF_FLOW_HAS_LOSS)) {
+        sfv[c] |= 4u << 16;
+        const u64 ls = flows[icv[c]].loss_start;
+        s0v[c] = u16(ls);
+        lnv[c] = flows[icv[c]].loss_end - ls;
+      }
     }
   }
 #pragma unroll
@@ -1655,13 +1746,13 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     if (v) {
       if (stv[c] == sid) {
         flg = 1;
-        if (qfv[c] & IP_OK) {
+        if (sfv[c] & (2u << 16)) {
           flg |= 2;
-          sn = u16(qfv[c] >> 16);
-          if (ffv[c] & LKF_FLOW_HAS_LOSS) {
+          sn = u16(sfv[c]);
+          if (sfv[c] & (4u << 16)) {
             flg |= 4;
-            s0 = lsv[c];
-            L = lev[c] - lsv[c];
+            s0 = s0v[c];
+            L = lnv[c];
           }
         }
       }
@@ -1672,31 +1763,32 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     const u64 prevLane = u64(__shfl_up(u64(arr), 1, 64));
     if (__ballot(v && arr < (lane ? i64(prevLane) : prevArr))) mono = false;
     prevArr = i64(rl_u64(u64(arr), 63));
-    if (__ballot(L > u64(kNackCap) || ((flg & 4) && L == 0))) return false;
+    if (__ballot(L > u64(kNackCap) || ((flg & 4) && L == 0))) NF_DECLINE(2);
     const u64 lm = __ballot(flg & 4);
     const u32 before4 = u32(__popcll(lm & ((1ull << lane) - 1)));
     if ((flg & 4) && nPush + before4 < u32(kNackCap)) {
-      F.pushK[nPush + before4] = k;
+      F.pushK[nPush + before4] = u16(k);
       F.pushS0[nPush + before4] = u16(s0);
     }
     // the loss lengths in push order (a prefix over the chunk's loss datagrams)
     u64 Ls = wave_incl_scan_u64(L, lane);
-    if ((flg & 4) && nPush + before4 < u32(kNackCap)) F.pushOff[nPush + before4 + 1] = u32(lossTot + Ls);
+    if ((flg & 4) && nPush + before4 < u32(kNackCap)) F.pushOff[nPush + before4 + 1] = u16(lossTot + Ls);
     lossTot += rl_u64(Ls, 63);
     nPush += u32(__popcll(lm));
-    if (u64(count0) + lossTot > u64(kNackCap)) return false;  // the capacity could be reached
+    if (u64(count0) + lossTot > u64(kNackCap)) NF_DECLINE(3);  // the capacity could be reached
   }
-  if (!mono) return false;
+  NF_STAMP(2);
+  if (!mono) NF_DECLINE(4);
   const u32 M = count0 + u32(lossTot);
-  if (M * kNackMaxTries > kNackFastEv) return false;  // (more entries than the event list holds nacks of)
+  if (M * kNackMaxTries > kNackFastEv) NF_DECLINE(5);  // (more entries than the event list holds nacks of)
   if (lane == 0) F.pushOff[0] = 0;
   __syncthreads();
   // ---- the entries
-  for (u32 e = lane; e < count0; e += 64) {
-    F.eSn[e] = g->sn[e];
-    F.eTries[e] = g->tries[e];
-    F.eLast[e] = g->last[e];
-    F.eBirth[e] = -1;
+  if (lane < count0) {
+    F.eSn[lane] = u16(q0sn);
+    F.eTries[lane] = u8(q0tries);
+    F.eLast[lane] = q0last;
+    F.eBirth[lane] = -1;
   }
   for (u32 p = 0; p < nPush; p++) {
     const u32 o = F.pushOff[p], L = F.pushOff[p + 1] - o, k = F.pushK[p];
@@ -1706,7 +1798,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
       F.eSn[e] = u16(s0 + i);
       F.eTries[e] = 0;
       F.eLast[e] = F.arr[k];
-      F.eBirth[e] = i32(k);
+      F.eBirth[e] = int16_t(k);
     }
   }
   for (u32 e = lane; e < M; e += 64) F.eRem[e] = kNackNone;
@@ -1738,7 +1830,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
       }
       F.hash[h] = u8(e);
     }
-  if (__ballot(dup)) return false;
+  if (__ballot(dup)) NF_DECLINE(6);
   __syncthreads();
   // Remove: the first datagram (from the entry's birth on) that carries its SN,
   // a probe of the hash per datagram and an LDS minimum per entry
@@ -1756,6 +1848,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     }
   }
   __syncthreads();
+  NF_STAMP(3);
   if (lane == 0) F.nEv = 0;
   __syncthreads();
   // ---- each entry's life
@@ -1796,14 +1889,14 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
       }
       if (j == kNackNone) break;
       const u32 slot = atomicAdd(&F.nEv, 1u);
-      if (slot < kNackFastEv) F.key[slot] = (j << 7) | e;
+      if (slot < kNackFastEv) F.key[slot] = u16((j << 7) | e);
       t++;
       l = F.arr[j];
       k = j + 1;
     }
     F.eTries[e] = u8(t);
     F.eLast[e] = l;
-    F.eDeath[e] = death;
+    F.eDeath[e] = u16(death == kNackNone ? 0xffffu : death);
   }
   __syncthreads();
   const u32 E = F.nEv;
@@ -1814,7 +1907,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
   // ---- the events in (datagram, queue) order: a bitonic sort in LDS
   u32 P = 1;
   while (P < E) P <<= 1;
-  for (u32 i = E + lane; i < P; i += 64) F.key[i] = 0xffffffffu;
+  for (u32 i = E + lane; i < P; i += 64) F.key[i] = 0xffffu;
   __syncthreads();
   for (u32 size = 2; size <= P; size <<= 1)
     for (u32 stride = size >> 1; stride > 0; stride >>= 1) {
@@ -1824,23 +1917,24 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
           const u32 a = F.key[i], b = F.key[jx];
           const bool up = (i & size) == 0;
           if ((a > b) == up) {
-            F.key[i] = b;
-            F.key[jx] = a;
+            F.key[i] = u16(b);
+            F.key[jx] = u16(a);
           }
         }
       }
       __syncthreads();
     }
+  NF_STAMP(4);
   // ---- one group per nacking datagram: its pairs (NackQueue.Pairs), packed on a lane
   u32 G = 0;
   for (u32 base = 0; base < E; base += 64) {
     const u32 i = base + lane;
     const bool st = i < E && (i == 0 || (F.key[i] >> 7) != (F.key[i - 1] >> 7));
     const u64 m = __ballot(st);
-    if (st) F.gStart[G + u32(__popcll(m & ((1ull << lane) - 1)))] = i;
+    if (st) F.gStart[G + u32(__popcll(m & ((1ull << lane) - 1)))] = u16(i);
     G += u32(__popcll(m));
   }
-  if (lane == 0) F.gStart[G] = E;
+  if (lane == 0) F.gStart[G] = u16(E);
   __syncthreads();
   u64 nacked = 0;
   for (u32 gi = lane; gi < G; gi += 64) {
@@ -1848,7 +1942,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     const u32 j = F.key[b] >> 7;
     u32 first = 0;  // the queue's first entry at the Pairs of datagram j
     for (u32 e = 0; e < M; e++)
-      if (F.eBirth[e] <= i32(j) && j < F.eDeath[e]) {
+      if (F.eBirth[e] <= i32(j) && j < u32(F.eDeath[e])) {
         first = F.eSn[e];
         break;
       }
@@ -1871,7 +1965,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
       }
     }
     if (active) F.stage[b + np++] = cur;
-    F.gNp[gi] = np;
+    F.gNp[gi] = u16(np);
     nacked += np ? u64(en - b) : 0ull;  // (UpdateNack only with a packet)
   }
   nacked = wave_sum_u64(nacked);
@@ -1882,26 +1976,23 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     const u32 gi = base + lane;
     const u64 np = gi < G ? F.gNp[gi] : 0;
     const u64 inc = wave_incl_scan_u64(np, lane);
-    if (gi < G) F.gOff[gi] = tot + u32(inc - np);
+    if (gi < G) F.gOff[gi] = u16(tot + u32(inc - np));
     tot += u32(rl_u64(inc, 63));
   }
   __syncthreads();
+  // (the stream's own block of kNackFastPairs past the shared buffer: a pair
+  // covers at least one event, so tot <= E <= kNackFastEv.  One counter
+  // reserved by every stream serialised ~4000 returning atomics on one address)
   if (tot) {
-    u32 off = 0;
-    if (lane == 0) off = atomicAdd(pairCnt, tot);
-    off = __builtin_amdgcn_readfirstlane(off);
-    if (off + tot > pairCap) {
-      if (lane == 0) atomicOr(err, 8u);  // pair buffer capacity: these RTCP NACKs are not recorded
-    } else {
-      for (u32 gi = lane; gi < G; gi += 64) {
-        const u32 b = F.gStart[gi], np = F.gNp[gi], o = off + F.gOff[gi];
-        for (u32 i = 0; i < np; i++) pairs[o + i] = F.stage[b + i];
-        if (np) {
-          const u32 kk = F.key[b] >> 7;
-          const u32 icx = useList ? lst[kk] : pb + kk;
-          info[icx] = np | ((F.gStart[gi + 1] - b) << 16);
-          pairOff[icx] = o;
-        }
+    const u32 off = pairCap + sid * kNackFastPairs;
+    for (u32 gi = lane; gi < G; gi += 64) {
+      const u32 b = F.gStart[gi], np = F.gNp[gi], o = off + F.gOff[gi];
+      for (u32 i = 0; i < np; i++) pairs[o + i] = F.stage[b + i];
+      if (np) {
+        const u32 kk = F.key[b] >> 7;
+        const u32 icx = useList ? lst[kk] : pb + kk;
+        info[icx] = np | ((F.gStart[gi + 1] - b) << 16);
+        pairOff[icx] = o;
       }
     }
   }
@@ -1910,7 +2001,7 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
   u32 kept = 0;
   for (u32 base = 0; base < M; base += 64) {
     const u32 e = base + lane;
-    const bool live = e < M && F.eDeath[e] == kNackNone;
+    const bool live = e < M && F.eDeath[e] == 0xffffu;
     changed = changed || (e < M && !live);
     const u64 m = __ballot(live);
     const u32 at = kept + u32(__popcll(m & ((1ull << lane) - 1)));
@@ -1940,6 +2031,11 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     if (lane == 0) g->count = kept;
   }
   if (lane == 0 && nacked) g->nacks += nacked;
+  NF_STAMP(5);
+  if (LKF_NACK_DBG == 2 && lane == 0 && stamp) {
+    stamp[0] = u64(sid) | (u64(nIdx) << 32);
+    stamp[6] = u64(M) | (u64(E) << 32);
+  }
   return true;
 }
 
@@ -1956,7 +2052,8 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
                                                  const u32 *__restrict__ tEnd, const u32 *__restrict__ list,
                                                  const u32 *__restrict__ cnt, u32 stride, u32 *__restrict__ info,
                                                  u32 *__restrict__ pairOff, u32 *pairCnt,
-                                                 lkf_nack_pair *__restrict__ pairs, u32 pairCap, u32 *err) {
+                                                 lkf_nack_pair *__restrict__ pairs, u32 pairCap, u32 *err,
+                                                 const NackIn *__restrict__ nackIn) {
   // the stream's RTCP NACKs of this ingest, staged and written in blocks: one
   // reservation in the batch's pair buffer per block instead of one atomic per
   // NACK (every stream's NACKs on one counter serialised the kernel)
@@ -1979,6 +2076,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   u32 *const sPurge = sU.s.purge;
   lkf_nack_pair *const sStage = sU.s.stage;
   u32 *const sRecIc = sU.s.recIc, *const sRecInfo = sU.s.recInfo, *const sRecOff = sU.s.recOff;
+  const u64 tEntry = LKF_NACK_DBG == 2 ? wall_clock64() : 0;  // (diagnosis builds)
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
   if (!s.nack || s.closed) return;
@@ -1991,8 +2089,9 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   const bool useList = s.layer < 3;
   const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
   const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
-  if (LKF_NACK_FAST && nack_fast(sU.f, lane, sid, g, count, rtt, nIdx, lst, useList, pb, raws, q, flows, info,
-                                 pairOff, pairCnt, pairs, pairCap, err))
+  const NackIn *nk = useList && nackIn ? nackIn + size_t(s.layer) * stride + pb : nullptr;
+  if (LKF_NACK_FAST && nack_fast(sU.f, lane, sid, g, count, rtt, nIdx, lst, useList, pb, nk, raws, q, flows, info,
+                                 pairOff, pairCnt, pairs, pairCap, err, nack_stamp(lane, sid, tEntry)))
     return;
   __syncthreads();
   for (u32 i = lane; i < (LKF_NACK_LIVE ? count : u32(kNackSlots)); i += 64) {
@@ -2741,11 +2840,11 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
     }
     hipLaunchKernelGGL(k_ing_stream_wave<false>, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams,
                        a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs,
-                       a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap);
+                       a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap, a.nack ? a.nackIn : nullptr);
     if (a.ddStates)  // DD streams exist
       hipLaunchKernelGGL(k_ing_stream_wave<true>, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams,
                          a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs,
-                         a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap);
+                         a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap, a.nack ? a.nackIn : nullptr);
   }
   if (a.nack && a.nstreams) {  // after the flows: the loss ranges it pushes
     hipError_t r = hipEventRecord(sideFork, st);
@@ -2755,10 +2854,17 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
                        a.nackPairCnt);
     hipLaunchKernelGGL(k_ing_nack, dim3(a.nstreams), dim3(64), 0, side, a.raws, a.parsed, a.flows, a.streams, a.nack,
                        a.hot, a.tBegin, a.tEnd, a.list, a.listCnt, a.listStride, a.nackInfo, a.nackPairOff,
-                       a.nackPairCnt, a.nackPairs, a.nackPairCap, a.err);
+                       a.nackPairCnt, a.nackPairs, a.nackPairCap, a.err, a.nackIn);
     r = hipEventRecord(sideDone, side);
     if (r != hipSuccess) return r;
     *sideUsed = true;
+    // (measurement: LKF_NACK_ALONE=1 orders the rest of the ingest after the
+    // NACK queues, so a kernel trace times k_ing_nack with the GPU to itself)
+    static const bool alone = [] {
+      const char *v = getenv("LKF_NACK_ALONE");
+      return v && atoi(v) != 0;
+    }();
+    if (alone && (r = hipStreamWaitEvent(st, sideDone, 0)) != hipSuccess) return r;
   }
   hipError_t r = launch_scan(st, 2, nullptr, nullptr, nullptr, a.fwd, nullptr, a.n, a.partA, a.partB, a.pos, nullptr,
                              a.total, nullptr, nullptr);
@@ -2955,3 +3061,29 @@ hipError_t launch_speakers(hipStream_t st, const SpeakersLaunch &a) {
 }
 
 }  // namespace lkf
+
+// (diagnosis builds, LKF_NACK_DBG=2) the NACK kernel's per-wave phase stamps
+// since the last call: 7 words per wave; returns the count (then reset)
+extern "C" int lkf_debug_nack_stamps(unsigned long long *out, unsigned int cap) {
+#if LKF_NACK_DBG == 2
+  static std::vector<unsigned long long> all;
+  all.assign(size_t(lkf::kNackStampCap) * 7, 0);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(lkf::gNackStamp), all.size() * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  unsigned int n = 0;
+  for (size_t i = 0; i < lkf::kNackStampCap && n < cap; i++)
+    if (all[i * 7 + 5]) {  // (a wave that finished the lane-parallel form)
+      for (int w = 0; w < 7; w++) out[size_t(n) * 7 + w] = all[i * 7 + w];
+      n++;
+    }
+  std::fill(all.begin(), all.end(), 0ull);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(lkf::gNackStamp), all.data(), all.size() * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  return int(n);
+#else
+  (void)out;
+  (void)cap;
+  return -1;
+#endif
+}

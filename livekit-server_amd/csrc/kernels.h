@@ -103,6 +103,22 @@ hipError_t launch_scan(hipStream_t s, int mode, const DevDT *dts, const uint32_t
                        uint64_t *outA, uint64_t *outB, uint64_t *totA, uint64_t *totB,
                        const uint32_t *perm, uint32_t *gFirst = nullptr, uint64_t gCap = 0);
 struct BucketLaunch;
+// What a NACK queue reads of one datagram of its stream's list, written by the
+// stream kernel in list order ([layer slot * listStride + tBegin + j], like the
+// list): the NACK kernel's loads are then contiguous instead of one scattered
+// line per datagram in each of the raw, parsed and flow arrays.
+struct NackIn {
+  int64_t arrival;  // lkf_raw_pkt.arrival_ns
+  uint32_t stream;  // lkf_raw_pkt.stream (a list may hold another stream's datagrams)
+  uint32_t snFl;    // RTP SN | (2: parsed (updateStreamState ran), 4: a loss range) << 16
+  uint32_t s0, len; // the loss range's first SN and length (flow loss_start, loss_end - loss_start)
+};
+static_assert(sizeof(NackIn) == 24, "24 B per datagram");
+// The NACK kernel's lane-parallel form: at most this many nack events per
+// stream and ingest, so at most this many RTCP NACK pairs; each stream writes
+// them to its own block past the shared pair buffer (nackPairCap + stream *
+// kNackFastPairs), the serial form bump-allocates in the shared part.
+constexpr uint32_t kNackFastPairs = 256;
 struct IngestLaunch {
   const lkf_raw_pkt *raws;
   uint32_t n;
@@ -135,6 +151,7 @@ struct IngestLaunch {
   uint32_t *nackInfo, *nackPairOff, *nackPairCnt;
   lkf_nack_pair *nackPairs;
   uint32_t nackPairCap;
+  NackIn *nackIn;  // 3 * listStride records (nullptr: the NACK kernel reads the raw arrays)
   const BucketLaunch *bucket = nullptr;  // the RTX buckets (nullptr: none)
   // the forwarding batch context's preparation, done by k_ing_out (tBegin
   // nullptr: not done): per-track ExtPacket ranges from the ingest's datagram
