@@ -3672,18 +3672,11 @@ __device__ __forceinline__ void store16(u8 *p, uint4 v) {
 // XCD's 4 MiB L2 between their readers: exact read bytes (request counters by
 // size) 651 MB per configs[1] batch for 319 MB of payload.  Extra LDS per
 // workgroup bounds residency (A/B in one GPU call, profiles/r6_ab_runs.txt):
-// 12 per CU -> 524 MB at the same step time, 8 -> 449 MB but 3-5 % slower,
-// 4 -> 339 MB and 25 % slower.  (The DD instantiation is LDS-bound already.)
-#ifndef LKF_EMIT_LDS  // LDS per <96> workgroup raised by this many bytes (0: as needed)
-#define LKF_EMIT_LDS 5900
-#endif
+// 12 per CU -> 524 MB, 8 -> 449 MB, 4 -> 339 MB.  The cap is reserved at
+// launch as dynamic LDS (EmitLaunch.ldsPad): it pays where emit shares the GPU
+// with an ingest chain, and costs where emit has it to itself (§4 DESIGN.md).
 template <int PRE>
 __global__ void __launch_bounds__(EMIT_T) k_emit(EmitArgs A) {
-#if LKF_EMIT_LDS
-  constexpr u32 kPad = PRE == PRE_MAX ? LKF_EMIT_LDS / 4 : 1;
-  __shared__ u32 sPad[kPad];
-  if (threadIdx.x == 1023) sPad[blockIdx.x % kPad] = 0;  // (never: keeps the allocation)
-#endif
   __shared__ __attribute__((aligned(16))) u8 pre[EMIT_G][PRE];
   __shared__ u64 sSrc[EMIT_G];  // arena offset of the record's first payload byte after the prefix
   __shared__ u32 sCs[EMIT_G];   // first chunk of the record, relative to the group
@@ -5042,7 +5035,7 @@ hipError_t launch_emit(hipStream_t s, const EmitLaunch &a) {
   if (a.ddArena)
     hipLaunchKernelGGL(k_emit<PRE_MAX_DD>, dim3(a.grid), dim3(EMIT_T), 0, s, A);
   else
-    hipLaunchKernelGGL(k_emit<PRE_MAX>, dim3(a.grid), dim3(EMIT_T), 0, s, A);
+    hipLaunchKernelGGL(k_emit<PRE_MAX>, dim3(a.grid), dim3(EMIT_T), a.ldsPad, s, A);
   return hipGetLastError();
 }
 

@@ -73,6 +73,7 @@ struct EmitLaunch {
   uint32_t grid;
   const uint8_t *ddArena;  // non-null: batches with DD tracks (k_emit<PRE_MAX_DD>)
   const uint32_t *twccBase = nullptr;  // per DownTrack transport-cc base of the batch (DownTracks with extTcc)
+  uint32_t ldsPad = 0;  // dynamic LDS reserved per workgroup (caps residency; the plain instantiation)
   // capacities (tested in -DLKF_CHECKED=1 builds)
   uint32_t maxDts, npkts;
   uint64_t tupleCap, arenaLen, ddCap, gCap;
