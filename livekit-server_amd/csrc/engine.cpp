@@ -387,6 +387,7 @@ struct lkf_engine {
   uint32_t emitGrid = 2048;       // persistent grid-stride launch (LKF_EMIT_PERSISTENT=1)
   bool emitPersistent = false;
   uint32_t emitLdsPad = 5900;  // bytes of LDS reserved per emit workgroup of an ingest-fed batch (12 per CU)
+  uint32_t emitCapFanout = 16;  // ... when the batch has fewer DownTracks per track than this
   uint32_t decideK = 0;  // DownTracks per decide wave (0: from the batch's packets per track)
   // SRTP protect (tables allocated with the first transport or lkf_protect)
   std::vector<lkf_transport_params> transports;
@@ -1109,6 +1110,7 @@ lkf_engine *lkf_create(int hip_device, const lkf_cfg *cfg) {
   if (const char *v = getenv("LKF_EMIT_WG_PER_CU")) perCU = std::max(1, atoi(v));
   if (const char *v = getenv("LKF_EMIT_PERSISTENT")) e->emitPersistent = atoi(v) != 0;
   if (const char *v = getenv("LKF_EMIT_LDS")) e->emitLdsPad = uint32_t(std::max(0, atoi(v)));  // (A/B)
+  if (const char *v = getenv("LKF_EMIT_CAP_FANOUT")) e->emitCapFanout = uint32_t(std::max(0, atoi(v)));
   if (const char *v = getenv("LKF_DECIDE_K")) e->decideK = uint32_t(std::min(8, std::max(0, atoi(v))));
   e->emitGrid = uint32_t(cus) * uint32_t(perCU);
   if (const char *v = getenv("LKF_HOST_PROF")) e->hostProf = atoi(v) != 0;
@@ -2050,12 +2052,15 @@ int lkf_run(lkf_engine *e, void *stream) {
   // stream) interleaves with this emit instead of waiting for a persistent grid.
   m.grid = e->emitPersistent ? e->emitGrid
                              : uint32_t(((e->cfg.max_out_pkts + 63) / 64 + 7) / 8 * 8);
-  // An ingest-fed batch's emit runs beside the next ingest chain: its
-  // workgroups are capped at 12 per CU (LDS reserved at launch), which keeps the
-  // payload lines its DownTracks re-read in L2 and leaves CUs to the ingest
-  // (configs[1]: 0.78 -> 0.74 ms per step).  A submitted batch's emit has the
-  // GPU mostly to itself and runs uncapped (the cap: 0.455 -> 0.54 ms).
-  m.ldsPad = ingestFed ? e->emitLdsPad : 0;
+  // An ingest-fed batch's emit runs beside the next ingest chain: at a low
+  // fan-out (fewer than emitCapFanout DownTracks per track) its workgroups are
+  // capped at 12 per CU (LDS reserved at launch), which keeps the payload lines
+  // its DownTracks re-read in L2 and leaves CUs to the ingest (configs[1], 9 per
+  // track: 0.78 -> 0.74 ms per step).  A submitted batch's emit, or one with a
+  // high fan-out, is most of the step and runs uncapped (the cap: ExtPacket
+  // configs[1] 0.455 -> 0.54 ms, configs[2] 2.51 -> 2.83 ms, configs[3] 3.35 ->
+  // 3.47 ms; profiles/r6_ab_runs.txt).
+  m.ldsPad = (ingestFed && uint64_t(nd) < uint64_t(e->emitCapFanout) * std::max<uint32_t>(1, nt)) ? e->emitLdsPad : 0;
   if (nd) HIPCHK(launch_emit(e->emitS, m), "emit");
   HIPCHK(hipEventRecord(rg[4], e->emitS), "event");
   HIPCHK(launch_accumulate(e->emitS, x.dStats, x.dTot, e->dCum, x.dErr, e->dSticky), "accumulate");
