@@ -1597,6 +1597,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
 // arrival times), the nacks of one datagram are gathered by a sort of
 // (datagram, entry) events, and each such datagram's pairs are packed on a
 // lane of their own.  Otherwise the serial form below runs.
+#ifndef LKF_NACK_FAST_MIN  // fewest datagrams of a stream for the lane-parallel form
+#define LKF_NACK_FAST_MIN 16
+#endif
 #ifndef LKF_NACK_N
 #define LKF_NACK_N 512
 #endif
@@ -1661,7 +1664,10 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
   do {                                                                 \
     if (LKF_NACK_DBG == 2 && lane == 0 && stamp) stamp[w] = wall_clock64(); \
   } while (0)
-  if (nIdx > kNackFastN || count0 * kNackMaxTries > kNackFastEv) NF_DECLINE(1);
+  // (a stream with a few datagrams: the serial form's per-datagram steps cost
+  // less than this form's fixed phases — 10-ms ticks, 1-2 per stream: 92 vs
+  // 203 us per ingest)
+  if (nIdx < LKF_NACK_FAST_MIN || nIdx > kNackFastN || count0 * kNackMaxTries > kNackFastEv) NF_DECLINE(1);
   // the queue's entries (at most 51: one per lane), loaded beside the datagrams
   static_assert(kNackFastEv / kNackMaxTries <= 64, "one queued entry per lane");
   u32 q0sn = 0, q0tries = 0;
