@@ -3871,7 +3871,11 @@ static int ingest_common(lkf_engine *e, BatchCtx &x, const lkf_raw_pkt *dRaws, u
                         // batch context counts as done only after it, like the sender statistics)
     HIPCHK(hipEventRecord(e->bktEv, s), "event");
     HIPCHK(hipStreamWaitEvent(e->sendS, e->bktEv, 0), "wait ingest (bucket store)");
-    HIPCHK(launch_bucket_store(e->sendS, bl), "bucket store");
+    static const bool skipStore = [] {  // (measurement only: LKF_SKIP_BKT_STORE=1 leaves the rings stale)
+      const char *v = getenv("LKF_SKIP_BKT_STORE");
+      return v && atoi(v) != 0;
+    }();
+    if (!skipStore) HIPCHK(launch_bucket_store(e->sendS, bl), "bucket store");
     HIPCHK(hipEventRecord(e->bktDone[par], e->sendS), "event");
     e->bktPending[par] = true;
     e->bktStorePending = true;
