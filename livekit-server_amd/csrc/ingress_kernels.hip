@@ -1784,6 +1784,9 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
     if (u64(count0) + lossTot > u64(kNackCap)) NF_DECLINE(3);  // the capacity could be reached
   }
   NF_STAMP(2);
+  // no queued entry and no loss: the queue stays empty and nothing is nacked
+  // (configs[2] has no loss: the rest of this form is fixed cost)
+  if (count0 == 0 && lossTot == 0) return true;
   if (!mono) NF_DECLINE(4);
   const u32 M = count0 + u32(lossTot);
   if (M * kNackMaxTries > kNackFastEv) NF_DECLINE(5);  // (more entries than the event list holds nacks of)
@@ -2051,6 +2054,11 @@ __device__ bool nack_fast(NackFastLds &F, u32 lane, u32 sid, NackState *g, u32 c
 #ifndef LKF_NACK_LIVE  // stage only the live entries (1), or all slots with the count (0, round 4)
 #define LKF_NACK_LIVE 1
 #endif
+// FAST: the lane-parallel form first (its 13 KB of LDS hold 12 workgroups per
+// CU); the serial-only instantiation (5 KB) is launched for short ingests,
+// where every stream takes the serial form anyway (LKF_NACK_FAST_MIN) and
+// occupancy is what counts (10-ms ticks at 1,000 rooms: 40,000 streams).
+template <bool FAST>
 __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__ raws,
                                                  const IngParsed *__restrict__ q, const lkf_flow *__restrict__ flows,
                                                  const DevStream *__restrict__ streams, NackState *__restrict__ states,
@@ -2072,16 +2080,18 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   };
   // (the lane-parallel form and the serial one share the LDS: the serial form
   // runs only when the other declined, before it wrote anything but LDS)
-  __shared__ union U {
+  union U {
     NackFastLds f;
     Serial s;
-  } sU;
-  i64 *const sLast = sU.s.last;
-  u32 *const sSn = sU.s.sn;
-  u32 *const sTries = sU.s.tries;
-  u32 *const sPurge = sU.s.purge;
-  lkf_nack_pair *const sStage = sU.s.stage;
-  u32 *const sRecIc = sU.s.recIc, *const sRecInfo = sU.s.recInfo, *const sRecOff = sU.s.recOff;
+  };
+  __shared__ __attribute__((aligned(16))) u8 sRaw[FAST ? sizeof(U) : sizeof(Serial)];
+  Serial &sS = *reinterpret_cast<Serial *>(sRaw);
+  i64 *const sLast = sS.last;
+  u32 *const sSn = sS.sn;
+  u32 *const sTries = sS.tries;
+  u32 *const sPurge = sS.purge;
+  lkf_nack_pair *const sStage = sS.stage;
+  u32 *const sRecIc = sS.recIc, *const sRecInfo = sS.recInfo, *const sRecOff = sS.recOff;
   const u64 tEntry = LKF_NACK_DBG == 2 ? wall_clock64() : 0;  // (diagnosis builds)
   const u32 sid = blockIdx.x, lane = threadIdx.x;
   const DevStream s = streams[sid];
@@ -2096,7 +2106,7 @@ __global__ void __launch_bounds__(64) k_ing_nack(const lkf_raw_pkt *__restrict__
   const u32 nIdx = useList ? cnt[s.track * 3 + s.layer] : pe - pb;
   const u32 *lst = list + size_t(useList ? s.layer : 0) * stride + pb;
   const NackIn *nk = useList && nackIn ? nackIn + size_t(s.layer) * stride + pb : nullptr;
-  if (LKF_NACK_FAST && nack_fast(sU.f, lane, sid, g, count, rtt, nIdx, lst, useList, pb, nk, raws, q, flows, info,
+  if (FAST && LKF_NACK_FAST && nack_fast(*reinterpret_cast<NackFastLds *>(sRaw), lane, sid, g, count, rtt, nIdx, lst, useList, pb, nk, raws, q, flows, info,
                                  pairOff, pairCnt, pairs, pairCap, err, nack_stamp(lane, sid, tEntry)))
     return;
   __syncthreads();
@@ -2858,9 +2868,15 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
     if (r != hipSuccess) return r;
     hipLaunchKernelGGL(k_nack_init, dim3(std::min<u32>(nblk(a.n, 256), 1024)), dim3(256), 0, side, a.n, a.nackInfo,
                        a.nackPairCnt);
-    hipLaunchKernelGGL(k_ing_nack, dim3(a.nstreams), dim3(64), 0, side, a.raws, a.parsed, a.flows, a.streams, a.nack,
-                       a.hot, a.tBegin, a.tEnd, a.list, a.listCnt, a.listStride, a.nackInfo, a.nackPairOff,
-                       a.nackPairCnt, a.nackPairs, a.nackPairCap, a.err, a.nackIn);
+    // (the lane-parallel form needs >= LKF_NACK_FAST_MIN datagrams in a stream)
+#define NACK_ARGS                                                                                              \
+  a.raws, a.parsed, a.flows, a.streams, a.nack, a.hot, a.tBegin, a.tEnd, a.list, a.listCnt, a.listStride, a.nackInfo, \
+      a.nackPairOff, a.nackPairCnt, a.nackPairs, a.nackPairCap, a.err, a.nackIn
+    if (u64(a.n) >= u64(LKF_NACK_FAST_MIN) * a.nstreams)
+      hipLaunchKernelGGL(k_ing_nack<true>, dim3(a.nstreams), dim3(64), 0, side, NACK_ARGS);
+    else
+      hipLaunchKernelGGL(k_ing_nack<false>, dim3(a.nstreams), dim3(64), 0, side, NACK_ARGS);
+#undef NACK_ARGS
     r = hipEventRecord(sideDone, side);
     if (r != hipSuccess) return r;
     *sideUsed = true;
@@ -2911,6 +2927,9 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
 // and the descriptor (coalesced), then the wave copies the stored ones with
 // four datagrams' loads in flight — 16-B copies when the source is 16-B
 // aligned (the ring slots are), dword or byte copies otherwise.
+#ifndef LKF_BKT_NOREAD  // (measurement builds: the ring copies written without reading the arena)
+#define LKF_BKT_NOREAD 0
+#endif
 constexpr u32 kBktChunks = (kBktSlot - 16) / 16;  // 16-B chunks of the largest stored datagram (95)
 __device__ __forceinline__ void bkt_store16(uint4 *p, uint4 v) {
   __builtin_nontemporal_store(v.x, &p->x);
@@ -2946,7 +2965,7 @@ __global__ void __launch_bounds__(256) k_bkt_store(BucketLaunch A) {
         if (x < k) {
           const u32 off = __builtin_amdgcn_readlane(rp.off, js[x]);
           const u32 nc = (__builtin_amdgcn_readlane(rp.len, js[x]) + 15) / 16;
-          if ((off & 15) == 0) {
+          if ((off & 15) == 0 && !LKF_BKT_NOREAD) {
             const uint4 *src = reinterpret_cast<const uint4 *>(A.raw + off);
             if (lane < nc) v[x][0] = src[lane];
             if (lane + 64 < nc) v[x][1] = src[lane + 64];
