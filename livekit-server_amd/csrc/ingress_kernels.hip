@@ -1242,8 +1242,13 @@ __device__ __forceinline__ u32 nk_snfl(const IngParsed &p, const lkf_flow &f) {
 // whose DependencyDescriptorParser + FrameIntegrityChecker state (3.3 KB) is
 // staged in LDS for the batch — lane 0's fold of the descriptors then updates
 // it there (the plain streams keep the smaller LDS footprint and occupancy).
-#ifndef LKF_ING_WAVES  // occupancy floor of the stream wave (waves per SIMD)
-#define LKF_ING_WAVES 4
+// Occupancy floor of the stream wave (waves per SIMD).  3 (round 6) over 4:
+// the registers it frees take the spills out of the serial step, and a batch's
+// 4,000 streams still fit the GPU in one round (configs[1] 0.745 -> 0.727 ms,
+// 10-ms tick 0.575 -> 0.553 ms, configs[4] 13.46 -> 13.21 ms; 2: the tick alike,
+// configs[4] 14.7 ms; profiles/r6_ab_runs.txt)
+#ifndef LKF_ING_WAVES
+#define LKF_ING_WAVES 3
 #endif
 template <bool DDK>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING_WAVES))) k_ing_stream_wave(
