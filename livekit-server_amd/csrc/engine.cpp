@@ -1959,8 +1959,12 @@ int lkf_run(lkf_engine *e, void *stream) {
   if (e->decideK) {
     d.perWave = e->decideK;
   } else {
+    // (round 6: 2 below 48 packets per track — 4 at the shortest ticks measured
+    // slower since the stream wave and the NACK queues changed: 10-ms ticks at
+    // 1,000 rooms 0.555 -> 0.533 ms ingress, 0.338 -> 0.331 ms ExtPacket, at 100
+    // rooms 0.130 -> 0.106 ms; 1: 0.557 / 0.346 ms; profiles/r6_ab_runs.txt)
     const uint64_t per = uint64_t(e->curN) / std::max<uint32_t>(1, nt);  // (ingest: the datagram count bound)
-    d.perWave = per >= 48 ? 1 : per >= 12 ? 2 : 4;
+    d.perWave = per >= 48 ? 1 : 2;
   }
   d.ddPkts = e->ddAlloc ? x.dDDPkt : nullptr;
   d.ddStructs = e->dDDStruct;
