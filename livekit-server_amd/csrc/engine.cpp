@@ -1963,8 +1963,14 @@ int lkf_run(lkf_engine *e, void *stream) {
     // slower since the stream wave and the NACK queues changed: 10-ms ticks at
     // 1,000 rooms 0.555 -> 0.533 ms ingress, 0.338 -> 0.331 ms ExtPacket, at 100
     // rooms 0.130 -> 0.106 ms; 1: 0.557 / 0.346 ms; profiles/r6_ab_runs.txt)
+    // Many DownTracks: one wave each is bound by the dispatch rate (≈240 waves
+    // per µs over the 8 XCDs: configs[2]'s 337 k DownTracks ≈ 1.4 ms), so a
+    // wave serves one more DownTrack per 100 k (configs[2] 2.74 -> 2.54 ms at
+    // 4; configs[1]'s 18 k stay at one: 2 costs 0.74 -> 0.87 ms there;
+    // configs[3]'s 100 k measured alike at 1 and 2)
     const uint64_t per = uint64_t(e->curN) / std::max<uint32_t>(1, nt);  // (ingest: the datagram count bound)
-    d.perWave = per >= 48 ? 1 : 2;
+    const uint32_t byCount = uint32_t(std::min<uint64_t>(8, (uint64_t(nd) + 99999) / 100000));
+    d.perWave = std::max<uint32_t>(per >= 48 ? 1 : 2, byCount);
   }
   d.ddPkts = e->ddAlloc ? x.dDDPkt : nullptr;
   d.ddStructs = e->dDDStruct;
