@@ -1247,6 +1247,9 @@ __device__ __forceinline__ u32 nk_snfl(const IngParsed &p, const lkf_flow &f) {
 // 4,000 streams still fit the GPU in one round (configs[1] 0.745 -> 0.727 ms,
 // 10-ms tick 0.575 -> 0.553 ms, configs[4] 13.46 -> 13.21 ms; 2: the tick alike,
 // configs[4] 14.7 ms; profiles/r6_ab_runs.txt)
+#ifndef LKF_ING_PER_WAVE  // (A/B) streams per stream-wave workgroup; 0: from the ingest's length
+#define LKF_ING_PER_WAVE 0
+#endif
 #ifndef LKF_ING_WAVES
 #define LKF_ING_WAVES 3
 #endif
@@ -1257,7 +1260,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
     const u32 *__restrict__ tBegin, const u32 *__restrict__ tEnd, lkf_flow *__restrict__ flows,
     u32 *__restrict__ fwd, const u8 *__restrict__ raw, DDIngState *ddStates, DDStruct *ddStructs,
     IngDD *__restrict__ ingDD, u32 *err, const u32 *__restrict__ list, const u32 *__restrict__ cnt, u32 stride,
-    BktArgs bka, u32 *__restrict__ rxGap, NackIn *__restrict__ nackIn) {
+    BktArgs bka, u32 *__restrict__ rxGap, NackIn *__restrict__ nackIn, u32 nstreams, u32 perWave) {
   static_assert(kHistWords == 64, "one history word per lane");
   static_assert(sizeof(StreamHot) == 64 * sizeof(u32), "one StreamHot dword per lane");
   __shared__ u64 sHist[kHistWords];
@@ -1266,14 +1269,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
   __shared__ u32 sOwn[kBktLds];  // (LDS is otherwise small: 4 waves per SIMD either way)
   __shared__ __attribute__((aligned(16))) u8 sDDIRaw[DDK ? sizeof(DDIngState) : 16];
   __shared__ BktCtx sBk;  // (ing_step's copy of bk)
-  const u32 sid = blockIdx.x, lane = threadIdx.x;
+  // A wave serves perWave consecutive streams, one after the other: a short
+  // ingest (10-ms ticks: one or two datagrams per stream) with one workgroup
+  // per stream is bound by the workgroup dispatch rate (≈240 per µs).
+  const u32 lane = threadIdx.x;
+  for (u32 jw = 0; jw < perWave; jw++) {
+  const u32 sid = blockIdx.x * perWave + jw;
+  if (sid >= nstreams) break;
+  if (jw) __syncthreads();  // (the previous stream's LDS is read out)
   const DevStream s = streams[sid];
-  if ((s.ddIdx != 0xffffffffu) != DDK) return;  // the other instantiation's stream
+  if ((s.ddIdx != 0xffffffffu) != DDK) continue;  // the other instantiation's stream
   const u32 pb = tBegin[s.track], pe = tEnd[s.track];
-  if (pb >= pe) return;
+  if (pb >= pe) continue;
   if (s.closed) {  // Buffer.Close: Write returns io.EOF, nothing is processed
     closed_flows(s, sid, pb, pe, raws, flows, fwd, ingDD, list, cnt, stride, lane, 64, nackIn);
-    return;
+    continue;
   }
   u64 *const hg = hist + size_t(sid) * kHistWords;
   u32 *const gap = rxGap + size_t(sid) * kGapWords;
@@ -1568,6 +1578,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKF_ING
     const uint4 *l = reinterpret_cast<const uint4 *>(sDDIRaw);
     for (u32 i = lane; i < sizeof(DDIngState) / 16; i += 64) g[i] = l[i];
   }
+  }  // next stream of this wave
 }
 
 // ---------------------------------------------------------------------------
@@ -2859,13 +2870,16 @@ hipError_t launch_ingest(hipStream_t st, const IngestLaunch &a, hipStream_t side
       bka.store = a.bucket->store;
       bka.epoch = a.bucket->epoch;
     }
-    hipLaunchKernelGGL(k_ing_stream_wave<false>, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams,
+    // streams per wave: 4 when the ingest has fewer than 8 datagrams per stream
+    const u32 sper = LKF_ING_PER_WAVE ? u32(LKF_ING_PER_WAVE) : u64(a.n) < u64(8) * a.nstreams ? 4u : 1u;
+    const u32 sgrid = (a.nstreams + sper - 1) / sper;
+    hipLaunchKernelGGL(k_ing_stream_wave<false>, dim3(sgrid), dim3(64), 0, st, a.raws, a.parsed, a.streams,
                        a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs,
-                       a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap, a.nack ? a.nackIn : nullptr);
+                       a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap, a.nack ? a.nackIn : nullptr, a.nstreams, sper);
     if (a.ddStates)  // DD streams exist
-      hipLaunchKernelGGL(k_ing_stream_wave<true>, dim3(a.nstreams), dim3(64), 0, st, a.raws, a.parsed, a.streams,
+      hipLaunchKernelGGL(k_ing_stream_wave<true>, dim3(sgrid), dim3(64), 0, st, a.raws, a.parsed, a.streams,
                          a.hot, a.hist, a.rings, a.tBegin, a.tEnd, a.flows, a.fwd, a.raw, a.ddStates, a.ddStructs,
-                         a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap, a.nack ? a.nackIn : nullptr);
+                         a.ingDD, a.err, a.list, a.listCnt, a.listStride, bka, a.rxGap, a.nack ? a.nackIn : nullptr, a.nstreams, sper);
   }
   if (a.nack && a.nstreams) {  // after the flows: the loss ranges it pushes
     hipError_t r = hipEventRecord(sideFork, st);
